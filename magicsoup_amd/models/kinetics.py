@@ -1,0 +1,498 @@
+"""Protein kinetics: token -> parameter maps, cell parameter tensors and the signal integrator.
+
+Public surface and numerics follow the reference ``python/magicsoup/kinetics.py``:
+
+* token maps (``kinetics.py:16-289``): Hill numbers, log-normal Km / Vmax weights, signs and the
+  reaction / transporter / effector stoichiometry vectors, each with an ``inverse()`` used by the
+  genome factories;
+* dense per-cell parameters ``N, Nf, Nb, A`` (int32, (c, p, s)), ``Kmr`` (f32, (c, p, s)) and
+  ``Kmf, Kmb, Vmax, Ke`` (f32, (c, p)) that users and tests may read and assign;
+* ``integrate_signals`` = 3 parts with Vmax trimmed by 0.7 / 0.2 / 0.1, each with the
+  negative-concentration guard and up to 4 equilibrium-damping iterations with a global early exit.
+
+The hot paths are native: ``integrate_signals`` runs the fused kernel of ``csrc/hip/kinetics.hip`` on
+GPU (``csrc/host/kinetics_host.cpp`` on CPU) and ``set_cell_params`` / ``set_cell_params_tokens``
+run the fused parameter builder. The private ``_get_*`` / ``_multiply_signals`` helpers are kept as
+plain-PyTorch specifications of each stage; they are the oracle the native kernels are tested
+against, and they run when a subclass overrides them (e.g. to switch stages off in a test).
+"""
+from __future__ import annotations
+
+import math
+import random
+from typing import Any
+
+import numpy as np
+import torch
+
+from magicsoup_amd.constants import GAS_CONSTANT, ProteinSpecType, EPS as _EPS, MAX as _MAX, MIN as _MIN
+from magicsoup_amd.models.containers import Chemistry, Molecule, Protein
+from magicsoup_amd.ops import kinetics_ops
+
+__all__ = ["Kinetics", "_EPS", "_MAX", "_MIN"]
+
+_TRIMS = (0.7, 0.2, 0.1)
+_INCREMENTS = (0.5, 0.25, 0.125, 0.0625)
+
+
+class _HillMapFact:
+    """Token -> Hill coefficient 1..5 with chances 16/31, 8/31, 4/31, 2/31, 1/31."""
+
+    def __init__(self, max_token: int, device: str = "cpu", zero_value: int = 0):
+        pool = [1] * 16 + [2] * 8 + [3] * 4 + [4] * 2 + [5]
+        vals = [zero_value] + random.choices(pool, k=max_token)
+        self.numbers = torch.tensor(vals, dtype=torch.int32, device=device)
+
+    def __call__(self, t: torch.Tensor) -> torch.Tensor:
+        return self.numbers[t]
+
+    def inverse(self) -> dict[int, list[int]]:
+        nums = self.numbers.cpu().tolist()
+        return {h: [i for i, v in enumerate(nums) if v == h] for h in (1, 3, 5)}
+
+
+class _LogNormWeightMapFact:
+    """Token -> float drawn from a log-normal truncated to ``weight_range`` (token 0 -> NaN).
+
+    mu is the mean of the log bounds and sigma the log range (reference kinetics.py:53-64).
+    """
+
+    def __init__(
+        self,
+        max_token: int,
+        weight_range: tuple[float, float],
+        device: str = "cpu",
+        zero_value: float = math.nan,
+    ):
+        lo, hi = min(weight_range), max(weight_range)
+        llo, lhi = math.log(lo), math.log(hi)
+        mu, sig = (llo + lhi) / 2, lhi - llo
+        vals = []
+        for _ in range(max_token):
+            v = math.exp(random.gauss(mu, sig))
+            while not lo <= v <= hi:
+                v = math.exp(random.gauss(mu, sig))
+            vals.append(v)
+        self.weights = torch.tensor([zero_value] + vals, dtype=torch.float32, device=device)
+
+    def __call__(self, t: torch.Tensor) -> torch.Tensor:
+        return self.weights[t]
+
+    def inverse(self) -> dict[float, list[int]]:
+        out: dict[float, list[int]] = {}
+        for i, v in enumerate(self.weights.cpu().tolist()):
+            if i > 0:
+                out.setdefault(v, []).append(i)
+        return out
+
+
+class _SignMapFact:
+    """Token -> +1 / -1 with equal chance (token 0 -> 0)."""
+
+    def __init__(self, max_token: int, device: str = "cpu", zero_value: int = 0):
+        vals = [zero_value] + random.choices([1, -1], k=max_token)
+        self.signs = torch.tensor(vals, dtype=torch.int32, device=device)
+
+    def __call__(self, t: torch.Tensor) -> torch.Tensor:
+        return self.signs[t]
+
+    def inverse(self) -> dict[bool, list[int]]:
+        s = self.signs.cpu().tolist()
+        return {True: [i for i, v in enumerate(s) if v == 1], False: [i for i, v in enumerate(s) if v == -1]}
+
+
+class _VectorMapFact:
+    """Token -> one of ``vectors`` (uniformly assigned); token 0 -> the zero vector."""
+
+    def __init__(
+        self,
+        max_token: int,
+        n_signals: int,
+        vectors: list[list[int]],
+        device: str = "cpu",
+        zero_value: int = 0,
+    ):
+        M = torch.full((max_token + 1, n_signals), fill_value=zero_value, dtype=torch.int32)
+        if len(vectors) > 0:
+            if any(len(v) != n_signals for v in vectors):
+                raise ValueError(f"Not all vectors have length of signal_size={n_signals}")
+            if len(vectors) > max_token:
+                raise ValueError(
+                    f"There are max_token={max_token} and {len(vectors)} vectors."
+                    " It is not possible to map all vectors"
+                )
+            if any(all(d == 0 for d in v) for v in vectors):
+                raise ValueError(
+                    "At least one vector includes only zeros."
+                    " Each vector should contain at least one non-zero value."
+                )
+            picks = random.choices(range(len(vectors)), k=max_token)
+            M[1:] = torch.tensor([vectors[i] for i in picks], dtype=torch.int32)
+        self.M = M.to(device)
+
+    def __call__(self, t: torch.Tensor) -> torch.Tensor:
+        return self.M[t]
+
+
+class _ReactionMapFact(_VectorMapFact):
+    """Token -> stoichiometry vector (length 2m) of a chemistry reaction (intracellular half only)."""
+
+    def __init__(
+        self,
+        molmap: dict[Molecule, int],
+        reactions: list[tuple[list[Molecule], list[Molecule]]],
+        max_token: int,
+        device: str = "cpu",
+        zero_value: int = 0,
+    ):
+        n_signals = 2 * len(molmap)
+        vecs = [_stoich(molmap, subs, prods, n_signals) for subs, prods in reactions]
+        super().__init__(max_token=max_token, n_signals=n_signals, vectors=vecs, device=device, zero_value=zero_value)
+
+    def inverse(
+        self,
+        molmap: dict[Molecule, int],
+        reactions: list[tuple[list[Molecule], list[Molecule]]],
+        n_signals: int,
+    ) -> dict[tuple[tuple[Molecule, ...], tuple[Molecule, ...]], list[int]]:
+        M = self.M.cpu()
+        out = {}
+        for subs, prods in reactions:
+            v = torch.tensor(_stoich(molmap, subs, prods, n_signals), dtype=M.dtype)
+            out[(tuple(subs), tuple(prods))] = torch.argwhere((M == v).all(dim=1)).flatten().tolist()
+        return out
+
+
+def _stoich(molmap, subs, prods, n_signals) -> list[int]:
+    v = [0] * n_signals
+    for mol in subs:
+        v[molmap[mol]] -= 1
+    for mol in prods:
+        v[molmap[mol]] += 1
+    return v
+
+
+class _TransporterMapFact(_VectorMapFact):
+    """Token -> transport vector: -1 for the intracellular, +1 for the extracellular signal."""
+
+    def __init__(self, n_molecules: int, max_token: int, device: str = "cpu", zero_value: int = 0):
+        n = n_molecules
+        vecs = [[-1 if j == i else (1 if j == i + n else 0) for j in range(2 * n)] for i in range(n)]
+        super().__init__(max_token=max_token, n_signals=2 * n, vectors=vecs, device=device, zero_value=zero_value)
+
+    def inverse(self, molecules: list[Molecule]) -> dict[Molecule, list[int]]:
+        M = self.M.cpu()
+        return {mol: torch.argwhere(M[:, i] != 0).flatten().tolist() for i, mol in enumerate(molecules)}
+
+
+class _RegulatoryMapFact(_VectorMapFact):
+    """Token -> one-hot effector signal (index >= m means extracellular / transmembrane)."""
+
+    def __init__(self, n_molecules: int, max_token: int, device: str = "cpu", zero_value: int = 0):
+        s = 2 * n_molecules
+        vecs = [[1 if j == i else 0 for j in range(s)] for i in range(s)]
+        super().__init__(max_token=max_token, n_signals=s, vectors=vecs, device=device, zero_value=zero_value)
+
+    def inverse(self, molecules: list[Molecule]) -> dict[tuple[Molecule, bool], list[int]]:
+        n = len(molecules)
+        M = self.M.cpu()
+        out = {}
+        for i, mol in enumerate(molecules):
+            out[(mol, False)] = torch.argwhere(M[:, i] != 0).flatten().tolist()
+            out[(mol, True)] = torch.argwhere(M[:, i + n] != 0).flatten().tolist()
+        return out
+
+
+_PARAMS = ("Ke", "Kmf", "Kmb", "Kmr", "Vmax", "N", "Nf", "Nb", "A")
+
+
+class Kinetics:
+    """Protein work of all cells.
+
+    Parameters:
+        chemistry: Simulation chemistry.
+        abs_temp: Absolute temperature (K); scales the equilibrium constants.
+        km_range / vmax_range: Ranges of the log-normal Km (mM) / Vmax (mM/s) token weights.
+        device: Device of all tensors (must match the world's).
+        scalar_enc_size: Number of 1-codon tokens (``max(genetics.one_codon_map.values())``).
+        vector_enc_size: Number of 2-codon tokens (``max(genetics.two_codon_map.values())``).
+
+    Signals are the m intracellular molecules followed by the m extracellular ones (s = 2m).
+    Cell parameters: ``Kmf, Kmb, Vmax, Ke`` (c, p); ``Kmr`` (c, p, s), already raised to the Hill
+    exponent; ``N, Nf, Nb`` stoichiometry (net / forward / backward) and ``A`` allosteric Hill
+    exponents (c, p, s, int32).
+    """
+
+    def __init__(
+        self,
+        chemistry: Chemistry,
+        abs_temp: float = 310.0,
+        km_range: tuple[float, float] = (1e-2, 100.0),
+        vmax_range: tuple[float, float] = (1e-3, 100.0),
+        device: str = "cpu",
+        scalar_enc_size: int = 64 - 3,
+        vector_enc_size: int = 4096 - 3 * 64,
+    ):
+        self.abs_temp = abs_temp
+        self.device = device
+        self.mol_names = [d.name for d in chemistry.molecules]
+        self.mol_energies = torch.tensor(
+            [d.energy for d in chemistry.molecules] * 2, dtype=torch.float32, device=device
+        )
+        s = 2 * len(chemistry.molecules)
+        self.n_signals = s
+        for name in _PARAMS:
+            shape = (0, 0, s) if name in ("Kmr", "N", "Nf", "Nb", "A") else (0, 0)
+            dt = torch.int32 if name in ("N", "Nf", "Nb", "A") else torch.float32
+            setattr(self, name, torch.zeros(*shape, dtype=dt, device=device))
+
+        mol_2_mi = {d: i for i, d in enumerate(chemistry.molecules)}
+        self.km_map = _LogNormWeightMapFact(max_token=scalar_enc_size, weight_range=km_range, device=device)
+        self.vmax_map = _LogNormWeightMapFact(max_token=scalar_enc_size, weight_range=vmax_range, device=device)
+        self.sign_map = _SignMapFact(max_token=scalar_enc_size, device=device)
+        self.hill_map = _HillMapFact(max_token=scalar_enc_size, device=device)
+        self.reaction_map = _ReactionMapFact(
+            molmap=mol_2_mi, reactions=chemistry.reactions, max_token=vector_enc_size, device=device
+        )
+        self.transport_map = _TransporterMapFact(
+            n_molecules=len(chemistry.molecules), max_token=vector_enc_size, device=device
+        )
+        self.effector_map = _RegulatoryMapFact(
+            n_molecules=len(chemistry.molecules), max_token=vector_enc_size, device=device
+        )
+
+        self.km_2_idxs = self.km_map.inverse()
+        self.vmax_2_idxs = self.vmax_map.inverse()
+        self.sign_2_idxs = self.sign_map.inverse()
+        self.hill_2_idxs = self.hill_map.inverse()
+        self.trnsp_2_idxs = self.transport_map.inverse(molecules=chemistry.molecules)
+        self.regul_2_idxs = self.effector_map.inverse(molecules=chemistry.molecules)
+        self.catal_2_idxs = self.reaction_map.inverse(
+            molmap=mol_2_mi, reactions=chemistry.reactions, n_signals=s
+        )
+        self.last_masks: list[int] = []
+
+    # ------------------------------------------------------------------ proteome views
+    def get_proteome(self, proteome: list[ProteinSpecType]) -> list[Protein]:
+        """Human-readable :class:`Protein` views of one translated proteome."""
+        from magicsoup_amd.models.containers import CatalyticDomain, RegulatoryDomain, TransporterDomain
+
+        mols = [Molecule.from_name(n) for n in self.mol_names]
+        m = len(mols)
+        vmax = self.vmax_map.weights.cpu().tolist()
+        km = self.km_map.weights.cpu().tolist()
+        signs = self.sign_map.signs.cpu().tolist()
+        hills = self.hill_map.numbers.cpu().tolist()
+        RM, TM, EM = (self.reaction_map.M.cpu(), self.transport_map.M.cpu(), self.effector_map.M.cpu())
+        out = []
+        for doms, cds_start, cds_end, is_fwd in proteome:
+            views = []
+            for (t, i0, i1, i2, i3), start, end in doms:
+                sign = signs[i2]
+                if t == 1:
+                    vec = RM[i3].tolist()
+                    lft, rgt = [], []
+                    for mi, nv in enumerate(vec):
+                        sn = nv * sign
+                        (rgt if sn > 0 else lft).extend([mols[mi % m]] * abs(nv) if sn != 0 else [])
+                    views.append(CatalyticDomain((lft, rgt), km=km[i1], vmax=vmax[i0], start=start, end=end))
+                elif t == 2:
+                    vec = TM[i3].tolist()
+                    mi = next(i for i, d in enumerate(vec) if d != 0)
+                    views.append(
+                        TransporterDomain(
+                            mols[mi % m], km=km[i1], vmax=vmax[i0], is_exporter=vec[mi] * sign < 0, start=start, end=end
+                        )
+                    )
+                elif t == 3:
+                    vec = EM[i3].tolist()
+                    mi = next(i for i, d in enumerate(vec) if d != 0)
+                    views.append(
+                        RegulatoryDomain(
+                            mols[mi % m],
+                            hill=hills[i0],
+                            km=km[i1],
+                            is_inhibiting=vec[mi] * sign < 0,
+                            is_transmembrane=mi >= m,
+                            start=start,
+                            end=end,
+                        )
+                    )
+            out.append(Protein(domains=views, cds_start=cds_start, cds_end=cds_end, is_fwd=is_fwd))
+        return out
+
+    # ------------------------------------------------------------------ parameter building
+    def set_cell_params(self, cell_idxs: list[int], proteomes: list[list[ProteinSpecType]]):
+        """Derive and write the parameters of cells ``cell_idxs`` from translated proteomes.
+
+        Rows are written in place into the current parameter tensors; proteins beyond a proteome's
+        length get the padding values of the reference (Ke 1, Kmf = Kmb = EPS, Kmr 1, rest 0).
+        """
+        if len(cell_idxs) == 0:
+            return
+        tokens = self._collect_proteome_idxs(proteomes)
+        self.set_cell_params_tokens(cell_idxs, tokens)
+
+    def set_cell_params_tokens(self, cell_idxs, tokens: torch.Tensor):
+        """Fused parameter build from dense tokens (n, P, D, 5) int32 for rows ``cell_idxs``."""
+        rows = torch.as_tensor(cell_idxs, dtype=torch.int32)
+        if tokens.size(1) > self.N.size(1):
+            self.increase_max_proteins(int(tokens.size(1)))
+        kinetics_ops.build_params(self, rows, tokens)
+
+    def unset_cell_params(self, cell_idxs):
+        """Zero all parameters of the given cells."""
+        if isinstance(cell_idxs, list) and len(cell_idxs) == 0:
+            return
+        for name in _PARAMS:
+            getattr(self, name)[cell_idxs] = 0
+
+    def copy_cell_params(self, from_idxs, to_idxs):
+        """Copy the parameter rows ``from_idxs`` to rows ``to_idxs``."""
+        for name in _PARAMS:
+            t = getattr(self, name)
+            t[to_idxs] = t[from_idxs]
+
+    def remove_cell_params(self, keep: torch.Tensor):
+        """Keep only the rows where the bool mask ``keep`` (c,) is true."""
+        for name in _PARAMS:
+            setattr(self, name, getattr(self, name)[keep])
+
+    def increase_max_cells(self, by_n: int):
+        """Append ``by_n`` zero rows to every parameter tensor."""
+        for name in _PARAMS:
+            t = getattr(self, name)
+            z = torch.zeros(by_n, *t.shape[1:], dtype=t.dtype, device=t.device)
+            setattr(self, name, torch.cat([t, z], dim=0))
+
+    def increase_max_proteins(self, max_n: int):
+        """Grow the protein dimension of every parameter tensor to ``max_n`` (zero-filled)."""
+        have = int(self.N.size(1))
+        if max_n <= have:
+            return
+        for name in _PARAMS:
+            t = getattr(self, name)
+            z = torch.zeros(t.size(0), max_n - have, *t.shape[2:], dtype=t.dtype, device=t.device)
+            setattr(self, name, torch.cat([t, z], dim=1))
+
+    # ------------------------------------------------------------------ integration
+    def integrate_signals(self, X: torch.Tensor) -> torch.Tensor:
+        """Let all proteins work for one time step.
+
+        Parameters:
+            X: Signals (c, s): intracellular molecules then the extracellular molecules of each
+                cell's pixel. Must be >= 0.
+
+        Returns:
+            Updated signals (c, s) as a new tensor.
+        """
+        if self._stages_overridden():
+            for trim in _TRIMS:
+                X = self._integrate_signals_part(adj_vmax=(self.Vmax * trim).clamp(0.0), X0=X)
+            return X
+        out = X.to(torch.float32).contiguous().clone()
+        self.last_masks = kinetics_ops.integrate(self, out, trims=_TRIMS, n_iters=len(_INCREMENTS))
+        return out
+
+    def _stages_overridden(self) -> bool:
+        cls = type(self)
+        return any(
+            getattr(cls, name) is not getattr(Kinetics, name)
+            for name in (
+                "_integrate_signals_part",
+                "_get_velocities",
+                "_get_equilibrium_adjusted_x",
+                "_get_negative_adjusted_nv",
+                "_get_quotient",
+                "_multiply_signals",
+            )
+        )
+
+    # ---- PyTorch specifications of each stage (oracle for the native kernels) ----
+    def _integrate_signals_part(self, adj_vmax: torch.Tensor, X0: torch.Tensor) -> torch.Tensor:
+        V = self._get_velocities(X=X0, Vmax=adj_vmax)
+        NV = self.N.float() * V.unsqueeze(2)
+        NV_adj = self._get_negative_adjusted_nv(NV=NV, X=X0)
+        X1 = (X0 + NV_adj.sum(1)).clamp(min=0.0)
+        return self._get_equilibrium_adjusted_x(X0=X0, X1=X1, NV=NV_adj, V=V)
+
+    def _get_velocities(self, X: torch.Tensor, Vmax: torch.Tensor) -> torch.Tensor:
+        kf, f_on = self._multiply_signals(X=X, N=self.Nf)
+        kf = torch.where(f_on, kf / self.Kmf, 0.0)
+        kf = torch.where(kf.isinf(), _MAX, kf)
+        kb, b_on = self._multiply_signals(X=X, N=self.Nb)
+        kb = torch.where(b_on, kb / self.Kmb, 0.0)
+        kb = torch.where(kb.isinf(), _MAX, kb)
+        a_cat = (kf - kb) / (1 + kf + kb)
+
+        is_reg = self.A != 0
+        x_reg = is_reg.float() * X.unsqueeze(1)
+        a = torch.pow(x_reg, self.A)
+        a = a / (a + self.Kmr)
+        a = torch.where(a.isnan() | ~is_reg, 1.0, a)
+        a_reg = torch.prod(a, 2)
+        a_reg = torch.where(a_reg.isinf(), _MAX, a_reg)
+        return (a_cat * Vmax * a_reg).clamp(_MIN, _MAX)
+
+    def _get_equilibrium_adjusted_x(
+        self, X0: torch.Tensor, X1: torch.Tensor, NV: torch.Tensor, V: torch.Tensor
+    ) -> torch.Tensor:
+        has_impact = V.abs() > 0.1
+        is_fwd = V > 0.0
+        F = torch.ones_like(V)
+        hi_t, lo_t = 1.5, 1 / 1.5
+        for inc in _INCREMENTS:
+            QKe = self._get_quotient(X=X1) / self.Ke
+            low = torch.where(is_fwd, QKe < lo_t, QKe > hi_t) & ~(is_fwd & (F == 1.0))
+            high = torch.where(is_fwd, QKe > hi_t, QKe < lo_t) & ~(~is_fwd & (F == 0.0))
+            if not torch.any((low | high) & has_impact):
+                return X1
+            F = (F - inc * high.float() + inc * low.float()).clamp(0.0, 1.0)
+            X1 = (X0 + torch.einsum("cps,cp->cs", NV, F)).clamp(min=0.0)
+        return X1
+
+    def _get_negative_adjusted_nv(self, NV: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
+        F = X / (-NV).clamp(min=0.0).sum(1)
+        F = torch.where(F > 1.0, 1.0, F)
+        removing = NV < 0.0
+        F_prot = torch.where(removing, F.unsqueeze(1), 1.0)
+        return NV * F_prot.min(dim=2).values.unsqueeze(2)
+
+    def _get_quotient(self, X: torch.Tensor) -> torch.Tensor:
+        prods, p_on = self._multiply_signals(X=X, N=self.Nb)
+        subs, s_on = self._multiply_signals(X=X, N=self.Nf)
+        prods = torch.where(p_on, prods, 0.0)
+        subs = torch.where(s_on, subs, 0.0)
+        return (prods / subs).clamp(min=_EPS, max=_MAX).nan_to_num(1.0)
+
+    def _multiply_signals(self, X: torch.Tensor, N: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        on = N > 0
+        x = on.float() * X.unsqueeze(1)
+        xx = torch.prod(torch.pow(x, N), 2)
+        xx = torch.where(xx.isnan() | (xx < 0.0), 0.0, xx)
+        xx = torch.where(xx.isinf(), _MAX, xx)
+        return xx, on.any(dim=2)
+
+    # ------------------------------------------------------------------ helpers
+    def _collect_proteome_idxs(self, proteomes: list[list[ProteinSpecType]]) -> torch.Tensor:
+        """Dense int32 tokens (n, P, D, 5) of proteome specs (P >= 1, D >= 1)."""
+        n = len(proteomes)
+        P = max([len(p) for p in proteomes] + [1])
+        D = max([len(doms) for p in proteomes for doms, *_ in p] + [1])
+        arr = np.zeros((n, P, D, 5), dtype=np.int32)
+        for ci, prots in enumerate(proteomes):
+            for pi, (doms, *_) in enumerate(prots):
+                for di, (spec, *_) in enumerate(doms):
+                    arr[ci, pi, di] = spec
+        return torch.from_numpy(arr)
+
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        state["last_masks"] = []
+        return state
+
+    def _i32_tensor(self, d: Any) -> torch.Tensor:
+        return torch.tensor(d, device=self.device, dtype=torch.int32)
+
+    def _f32_tensor(self, d: Any) -> torch.Tensor:
+        return torch.tensor(d, device=self.device, dtype=torch.float32)

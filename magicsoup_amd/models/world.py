@@ -1,0 +1,633 @@
+"""The simulation world: cells on a toroidal map, molecules on a per-species map.
+
+Public API and semantics follow the reference ``python/magicsoup/world.py`` (class ``World``,
+``world.py:36-1004``): the same constructor arguments, methods, return values and public state
+(``cell_genomes``, ``cell_labels``, ``cell_map``, ``cell_positions``, ``cell_lifetimes``,
+``cell_divisions``, ``cell_molecules``, ``molecule_map``, ``n_cells``, ``genetics``, ``kinetics``,
+``chemistry``) and the same ``save_state`` / ``load_state`` file format.
+
+MI355X-first design:
+
+* every per-cell array lives in a capacity-managed device buffer; the public tensors are views,
+  so spawning / dividing appends without re-copying the population (reference ``_expand_c`` +
+  ``torch.cat`` on every call, ``world.py:986-989``);
+* genomes and labels live in device byte arenas (:mod:`magicsoup_amd.models.strings`); the public
+  ``cell_genomes`` / ``cell_labels`` are lazy list views;
+* translation, parameter build, the kinetics integrator, diffusion / permeation / degradation,
+  placement, neighbour search, mutation and recombination run as gfx950 HIP kernels
+  (:mod:`magicsoup_amd.ops.hip_ops`) for GPU worlds and in the OpenMP host core for CPU worlds;
+* API calls accept index lists (reference) or device index tensors (no host round trip), and
+  ``*_t`` variants return tensors instead of Python lists.
+"""
+from __future__ import annotations
+
+import math
+import pickle
+import random
+from pathlib import Path
+from typing import Any, Sequence
+
+import numpy as np
+import torch
+
+from magicsoup_amd.models.containers import Cell, Chemistry
+from magicsoup_amd.models.genetics import Genetics
+from magicsoup_amd.models.kinetics import Kinetics
+from magicsoup_amd.models.strings import StringArena, StringColumn, pack_strings
+from magicsoup_amd.ops import world_ops
+from magicsoup_amd.utils.util import randstr
+from magicsoup_amd.utils.profiling import range_push, range_pop
+
+_LABEL_LEN = 12
+
+
+def _diffusion_weights(rate: float) -> tuple[float, float]:
+    """Stencil weights (neighbour a, centre b) for a diffusivity (reference world.py:948-971)."""
+    rate = min(abs(rate), 1.0)
+    if rate == 0.0:
+        return 0.0, 1.0
+    d = 1 / rate
+    a = 1 / (d + 8)
+    b = d * a
+    b = b + 1.0 - (8 * a + b)
+    return a, b
+
+
+def _permeation_factor(rate: float) -> float:
+    """Per-step exchange fraction for a permeability (reference world.py:935-946)."""
+    rate = min(abs(rate), 1.0)
+    if rate == 0.0:
+        return 0.0
+    return 1 / (1 / rate + 1)
+
+
+class _Column:
+    """A capacity-managed per-cell buffer exposed as a cached view of its first ``n`` rows."""
+
+    __slots__ = ("buf", "_view", "_n")
+
+    def __init__(self, buf: torch.Tensor):
+        self.buf = buf
+        self._view: torch.Tensor | None = None
+        self._n = -1
+
+    def view(self, n: int) -> torch.Tensor:
+        if self._view is None or self._n != n:
+            self._view = self.buf if self.buf.size(0) == n else self.buf[:n]
+            self._n = n
+        return self._view
+
+    def adopt(self, t: torch.Tensor, n: int) -> None:
+        if t is self._view:
+            return
+        self.buf = t
+        self._view = t
+        self._n = n
+
+    def reserve(self, n_old: int, n_new: int) -> None:
+        if n_new <= self.buf.size(0):
+            return
+        cap = max(n_new, int(self.buf.size(0) * 1.5) + 64)
+        nb = torch.zeros(cap, *self.buf.shape[1:], dtype=self.buf.dtype, device=self.buf.device)
+        if n_old:
+            nb[:n_old] = self.view(n_old)
+        self.buf = nb
+        self._view = None
+
+
+class World:
+    """State of a simulation and the operations that advance it.
+
+    Parameters:
+        chemistry: Molecules and reactions of the simulation.
+        map_size: Pixels per side of the square, toroidal map.
+        abs_temp: Absolute temperature in K (scales reaction equilibria).
+        mol_map_init: ``"randn"`` (|N(10, 1)|) or ``"zeros"`` initial molecule map.
+        start_codons / stop_codons: CDS delimiters for the genetics.
+        device: Torch device of all state (``"cuda"`` = the MI355X via ROCm). Falls back to CPU when
+            no GPU is present, like the reference.
+        batch_size: Accepted for API compatibility (the reference ignores it as well).
+        seed: Optional seed of all native RNG streams (placement, mutation, recombination).
+    """
+
+    def __init__(
+        self,
+        chemistry: Chemistry,
+        map_size: int = 128,
+        abs_temp: float = 310.0,
+        mol_map_init: str = "randn",
+        start_codons: tuple[str, ...] = ("TTG", "GTG", "ATG"),
+        stop_codons: tuple[str, ...] = ("TGA", "TAG", "TAA"),
+        device: str = "cpu",
+        batch_size: int | None = None,
+        seed: int | None = None,
+    ):
+        if not torch.cuda.is_available():
+            device = "cpu"
+        self.device = device
+        self.batch_size = batch_size
+        self.map_size = map_size
+        self.abs_temp = abs_temp
+        self.chemistry = chemistry
+        if seed is not None:
+            world_ops.set_seed(seed, device)
+
+        self.genetics = Genetics(start_codons=start_codons, stop_codons=stop_codons)
+        self.kinetics = Kinetics(
+            chemistry=chemistry,
+            abs_temp=abs_temp,
+            device=device,
+            scalar_enc_size=max(self.genetics.one_codon_map.values()),
+            vector_enc_size=max(self.genetics.two_codon_map.values()),
+        )
+
+        self.n_molecules = len(chemistry.molecules)
+        self._int_mol_idxs = list(range(self.n_molecules))
+        self._ext_mol_idxs = list(range(self.n_molecules, 2 * self.n_molecules))
+        self._mol_degrads = [math.exp(-math.log(2) / m.half_life) for m in chemistry.molecules]
+        self._diffusion = [_diffusion_weights(m.diffusivity) for m in chemistry.molecules]
+        self._permeation = [_permeation_factor(m.permeability) for m in chemistry.molecules]
+
+        dev = torch.device(device)
+        m = self.n_molecules
+        self.n_cells = 0
+        self._genomes = StringArena(dev, width=64)
+        self._labels = StringArena(dev, width=16)
+        self._genome_col = StringColumn(self._genomes)
+        self._label_col = StringColumn(self._labels)
+        self._cols = {
+            "cell_molecules": _Column(torch.zeros(0, m, dtype=torch.float32, device=dev)),
+            "cell_positions": _Column(torch.zeros(0, 2, dtype=torch.int32, device=dev)),
+            "cell_lifetimes": _Column(torch.zeros(0, dtype=torch.int32, device=dev)),
+            "cell_divisions": _Column(torch.zeros(0, dtype=torch.int32, device=dev)),
+        }
+        self.cell_map = torch.zeros(map_size, map_size, dtype=torch.bool, device=dev)
+        self.molecule_map = self._get_molecule_map(n=m, size=map_size, init=mol_map_init)
+
+    # ------------------------------------------------------------------ public state
+    def __getattr__(self, name):  # only reached for attributes not found normally
+        cols = self.__dict__.get("_cols")
+        if cols is not None and name in cols:
+            return cols[name].view(self.__dict__["n_cells"])
+        raise AttributeError(name)
+
+    def __setattr__(self, name, value):
+        cols = self.__dict__.get("_cols")
+        if cols is not None and name in cols:
+            t = torch.as_tensor(value, device=self.device)
+            want = torch.float32 if name == "cell_molecules" else torch.int32
+            t = t.to(want).contiguous() if (t.dtype != want or not t.is_contiguous()) else t
+            cols[name].adopt(t, int(t.size(0)))
+            return
+        if name == "cell_genomes":
+            self._set_strings(self._genomes, list(value))
+            return
+        if name == "cell_labels":
+            self._set_strings(self._labels, list(value))
+            return
+        super().__setattr__(name, value)
+
+    @property
+    def cell_genomes(self) -> StringColumn:
+        """Genomes ordered by cell index (a lazy ``list[str]`` view of the device arena)."""
+        return self._genome_col
+
+    @property
+    def cell_labels(self) -> StringColumn:
+        """Labels ordered by cell index (a lazy ``list[str]`` view)."""
+        return self._label_col
+
+    def _set_strings(self, arena: StringArena, strs: list[str]) -> None:
+        arena.clear()
+        arena.append_strings(strs)
+
+    # ------------------------------------------------------------------ capacity helpers
+    def _reserve(self, n_new: int) -> None:
+        for col in self._cols.values():
+            col.reserve(self.n_cells, n_new)
+
+    def _grow(self, k: int) -> None:
+        """Append k zero-initialised cell rows to every per-cell array (world + kinetics)."""
+        n = self.n_cells
+        self._reserve(n + k)
+        for col in self._cols.values():
+            col.buf[n : n + k] = 0
+        self.n_cells = n + k
+        self.kinetics.increase_max_cells(by_n=k)
+
+    def _idx_tensor(self, idxs, unique: bool = True) -> torch.Tensor:
+        if isinstance(idxs, torch.Tensor):
+            t = idxs.to(self.device)
+            if t.dtype == torch.bool:
+                t = torch.nonzero(t).flatten()
+            t = t.to(torch.long).flatten()
+        else:
+            t = torch.tensor(list(idxs), dtype=torch.long, device=self.device)
+        if unique and t.numel() > 1:
+            t = torch.unique(t)
+        return t
+
+    # ------------------------------------------------------------------ queries
+    def get_cell(self, by_idx: int | None = None, by_position: tuple[int, int] | None = None) -> Cell:
+        """A :class:`Cell` view of the cell at index ``by_idx`` or at pixel ``by_position``.
+
+        Raises ``ValueError`` if no cell lives at ``by_position``.
+        """
+        idx = -1
+        if by_idx is not None:
+            idx = by_idx
+        if by_position is not None:
+            pos = torch.tensor(by_position, dtype=torch.int32, device=self.device)
+            hits = torch.argwhere((self.cell_positions == pos).all(dim=1)).flatten().tolist()
+            if len(hits) == 0:
+                raise ValueError(f"Cell at {by_position} not found")
+            idx = hits[0]
+        return Cell(
+            world=self,
+            idx=idx,
+            genome=self.cell_genomes[idx],
+            position=tuple(self.cell_positions[idx].tolist()),  # type: ignore[arg-type]
+            label=self.cell_labels[idx],
+            n_steps_alive=int(self.cell_lifetimes[idx].item()),
+            n_divisions=int(self.cell_divisions[idx].item()),
+        )
+
+    def get_neighbors(self, cell_idxs: list[int], nghbr_idxs: list[int] | None = None) -> list[tuple[int, int]]:
+        """Unique pairs ``(a, b)``, ``a < b``, of cells in each other's Moore neighbourhood.
+
+        Each cell of ``cell_idxs`` pairs with neighbouring cells of ``nghbr_idxs`` (default:
+        ``cell_idxs`` itself).
+        """
+        pairs = self.get_neighbors_t(cell_idxs, nghbr_idxs)
+        return [tuple(d) for d in pairs.tolist()]
+
+    def get_neighbors_t(self, cell_idxs, nghbr_idxs=None) -> torch.Tensor:
+        """Tensor form of :meth:`get_neighbors`: int32 (k, 2) on the world's device."""
+        frm = self._idx_tensor(cell_idxs)
+        if frm.numel() == 0:
+            return torch.zeros(0, 2, dtype=torch.int32, device=self.device)
+        to = frm if nghbr_idxs is None else self._idx_tensor(nghbr_idxs)
+        if to.numel() == 0:
+            return torch.zeros(0, 2, dtype=torch.int32, device=self.device)
+        return world_ops.neighbors(self, frm, to)
+
+    # ------------------------------------------------------------------ cell lifecycle
+    def spawn_cells(self, genomes) -> list[int]:
+        """Place new cells with ``genomes`` on random free pixels.
+
+        Each new cell takes half of its pixel's molecules, gets a random label, lifetime 0 and
+        0 divisions. If there are fewer free pixels than genomes, a random subset is spawned.
+        ``genomes`` is a ``list[str]`` or a packed ``(bytes (k, L) uint8, lengths (k,))`` tuple.
+
+        Returns the indices of the new cells.
+        """
+        range_push("spawn_cells")
+        try:
+            rows, lens = self._as_packed(genomes)
+            k = int(rows.size(0))
+            if k == 0:
+                return []
+            pos = world_ops.free_positions(self, k)
+            kp = int(pos.size(0))
+            if kp == 0:
+                return []
+            if kp < k:
+                keep = torch.randperm(k, device=rows.device)[:kp]
+                rows, lens = rows[keep], lens[keep]
+                k = kp
+            n0 = self.n_cells
+            self._grow(k)
+            self._genomes.append_packed(rows, lens)
+            self._labels.append_packed(*self._random_labels(k))
+            new = torch.arange(n0, n0 + k, device=self.device)
+            self._place(new, pos)
+            world_ops.pickup_molecules(self, new, pos)
+            self._update_params_rows(new)
+            return list(range(n0, n0 + k))
+        finally:
+            range_pop()
+
+    def add_cells(self, cells: list[Cell]) -> list[int]:
+        """Place :class:`Cell` objects on random free pixels, keeping their genome, label,
+        intracellular molecules, lifetime and divisions (no molecule pickup)."""
+        k = len(cells)
+        if k == 0:
+            return []
+        pos = world_ops.free_positions(self, k)
+        kp = int(pos.size(0))
+        if kp == 0:
+            return []
+        if kp < k:
+            cells = list(cells)
+            random.shuffle(cells)
+            cells = cells[:kp]
+            k = kp
+        n0 = self.n_cells
+        self._grow(k)
+        self._genomes.append_strings([c.genome for c in cells])
+        self._labels.append_strings([c.label for c in cells])
+        new = torch.arange(n0, n0 + k, device=self.device)
+        self._place(new, pos)
+        mols = torch.stack([torch.as_tensor(c.int_molecules) for c in cells]).to(self.device, torch.float32)
+        self.cell_molecules[n0:] = mols
+        self.cell_lifetimes[n0:] = torch.tensor([c.n_steps_alive for c in cells], dtype=torch.int32)
+        self.cell_divisions[n0:] = torch.tensor([c.n_divisions for c in cells], dtype=torch.int32)
+        self._update_params_rows(new)
+        return list(range(n0, n0 + k))
+
+    def divide_cells(self, cell_idxs) -> list[tuple[int, int]]:
+        """Let cells divide into a random free pixel of their Moore neighbourhood.
+
+        Children are appended at the end, inherit genome, proteome and label; molecules are split
+        evenly; both descendants get ``divisions + 1`` and lifetime 0. Cells without a free
+        neighbour do not divide. Returns ``(parent_idx, child_idx)`` pairs.
+        """
+        parents, children = self.divide_cells_t(cell_idxs)
+        return list(zip(parents.tolist(), children.tolist()))
+
+    def divide_cells_t(self, cell_idxs) -> tuple[torch.Tensor, torch.Tensor]:
+        """Tensor form of :meth:`divide_cells`: (parents, children) long tensors."""
+        range_push("divide_cells")
+        try:
+            idxs = self._idx_tensor(cell_idxs)
+            empty = torch.zeros(0, dtype=torch.long, device=self.device)
+            if idxs.numel() == 0:
+                return empty, empty
+            parents, child_pos = world_ops.divide_placement(self, idxs)
+            k = int(parents.numel())
+            if k == 0:
+                return empty, empty
+            n0 = self.n_cells
+            self._grow(k)
+            children = torch.arange(n0, n0 + k, device=self.device)
+            self._genomes.append_rows_from(parents)
+            self._labels.append_rows_from(parents)
+            self.kinetics.copy_cell_params(from_idxs=parents, to_idxs=children)
+            self._place(children, child_pos)
+            world_ops.split_cells(self, parents, children)
+            return parents, children
+        finally:
+            range_pop()
+
+    def update_cells(self, genome_idx_pairs: list[tuple[str, int]]):
+        """Replace the genomes of existing cells and re-derive their proteomes."""
+        if len(genome_idx_pairs) == 0:
+            return
+        genomes, idxs = zip(*genome_idx_pairs)
+        self._genomes.set_strings(list(idxs), list(genomes))
+        self._update_params_rows(torch.tensor(list(idxs), dtype=torch.long, device=self.device))
+
+    def kill_cells(self, cell_idxs=None):
+        """Remove cells; their molecules spill onto their pixel. Remaining cells keep their order
+        (indices after a removed cell shift down)."""
+        range_push("kill_cells")
+        try:
+            if cell_idxs is None:
+                cell_idxs = torch.arange(self.n_cells, device=self.device)
+            idxs = self._idx_tensor(cell_idxs)
+            k = int(idxs.numel())
+            if k == 0:
+                return
+            world_ops.spill_and_free(self, idxs)
+            keep = torch.ones(self.n_cells, dtype=torch.bool, device=self.device)
+            keep[idxs] = False
+            keep_idx = torch.nonzero(keep).flatten()
+            self._compact(keep_idx, keep)
+        finally:
+            range_pop()
+
+    def _compact(self, keep_idx: torch.Tensor, keep: torch.Tensor) -> None:
+        n_new = int(keep_idx.numel())
+        for col in self._cols.values():
+            v = col.view(self.n_cells)
+            col.buf[:n_new] = v[keep_idx]
+            col._view = None
+        self.kinetics.remove_cell_params(keep=keep)
+        self._genomes.keep(keep_idx)
+        self._labels.keep(keep_idx)
+        self.n_cells = n_new
+
+    def move_cells(self, cell_idxs=None):
+        """Move cells to a random free pixel of their Moore neighbourhood (if there is one)."""
+        if cell_idxs is None:
+            cell_idxs = torch.arange(self.n_cells, device=self.device)
+        idxs = self._idx_tensor(cell_idxs)
+        if idxs.numel() == 0:
+            return
+        moved, new_pos = world_ops.move_placement(self, idxs)
+        if moved.numel() == 0:
+            return
+        old = self.cell_positions[moved].long()
+        self.cell_map[old[:, 0], old[:, 1]] = False
+        self._place(moved, new_pos)
+
+    def reposition_cells(self, cell_idxs=None):
+        """Move cells to random free pixels anywhere on the map."""
+        if cell_idxs is None:
+            cell_idxs = torch.arange(self.n_cells, device=self.device)
+        idxs = self._idx_tensor(cell_idxs)
+        if idxs.numel() == 0:
+            return
+        old = self.cell_positions[idxs].long()
+        self.cell_map[old[:, 0], old[:, 1]] = False
+        pos = world_ops.free_positions(self, int(idxs.numel()))
+        self._place(idxs[: pos.size(0)], pos)
+
+    def _place(self, idxs: torch.Tensor, pos: torch.Tensor) -> None:
+        pos = pos.to(self.device, torch.int32)
+        self.cell_positions[idxs] = pos
+        p = pos.long()
+        self.cell_map[p[:, 0], p[:, 1]] = True
+
+    # ------------------------------------------------------------------ physics
+    def enzymatic_activity(self):
+        """Let all proteins of all cells work for one time step (updates ``cell_molecules`` and
+        the molecule map pixels under the cells)."""
+        if self.n_cells == 0:
+            return
+        range_push("enzymatic_activity")
+        try:
+            world_ops.enzymatic_activity(self)
+        finally:
+            range_pop()
+
+    @torch.no_grad()
+    def diffuse_molecules(self):
+        """One step of diffusion over the molecule map, then membrane permeation."""
+        range_push("diffuse_molecules")
+        try:
+            world_ops.diffuse(self)
+            if self.n_cells > 0:
+                world_ops.permeate(self)
+        finally:
+            range_pop()
+
+    def degrade_molecules(self):
+        """Decay molecules in the map and in cells by one time step (per-species half life)."""
+        world_ops.degrade(self)
+
+    def increment_cell_lifetimes(self):
+        """Add 1 to every cell's lifetime."""
+        self.cell_lifetimes += 1
+
+    # ------------------------------------------------------------------ evolution
+    def mutate_cells(self, cell_idxs: list[int] | None = None, p: float = 1e-6, p_indel: float = 0.4, p_del: float = 0.66):
+        """Point mutations (substitutions and indels) with per-bp rate ``p``; proteomes of mutated
+        cells are re-derived."""
+        range_push("mutate_cells")
+        try:
+            if self.n_cells == 0:
+                return
+            rows = None if cell_idxs is None else self._idx_tensor(cell_idxs, unique=False)
+            changed = world_ops.point_mutations(self, rows, p, p_indel, p_del)
+            if changed.numel() > 0:
+                self._update_params_rows(changed)
+        finally:
+            range_pop()
+
+    def recombinate_cells(self, cell_idxs: list[int] | None = None, p: float = 1e-7):
+        """Recombine the genomes of neighbouring cells (strand breaks with per-bp rate ``p`` and
+        random re-joining); both genomes of every recombined pair are replaced."""
+        range_push("recombinate_cells")
+        try:
+            if self.n_cells < 2:
+                return
+            idxs = torch.arange(self.n_cells, device=self.device) if cell_idxs is None else cell_idxs
+            pairs = self.get_neighbors_t(idxs)
+            if pairs.size(0) == 0:
+                return
+            changed = world_ops.recombinations(self, pairs, p)
+            if changed.numel() > 0:
+                self._update_params_rows(changed)
+        finally:
+            range_pop()
+
+    # ------------------------------------------------------------------ params
+    def _update_params_rows(self, rows: torch.Tensor) -> None:
+        """Translate the genomes of ``rows`` and rebuild their kinetic parameters."""
+        rows = rows.to(self.device, torch.long)
+        if rows.numel() == 0:
+            return
+        data, lens = self._genomes.view()
+        tokens, nprots = world_ops.translate(self, data, lens, rows)
+        self.kinetics.increase_max_proteins(int(tokens.size(1)))
+        empty = nprots == 0
+        if bool(empty.any()):
+            self.kinetics.unset_cell_params(rows[empty])
+        full = ~empty
+        if bool(full.any()):
+            self.kinetics.set_cell_params_tokens(rows[full], tokens[full])
+
+    # ------------------------------------------------------------------ persistence
+    def save(self, rundir: Path, name: str = "world.pkl"):
+        """Pickle the whole world (chemistry, genetics, kinetics maps and state)."""
+        rundir = Path(rundir)
+        rundir.mkdir(parents=True, exist_ok=True)
+        with open(rundir / name, "wb") as fh:
+            pickle.dump(self, fh)
+
+    @classmethod
+    def from_file(cls, rundir: Path, name: str = "world.pkl", device: str | None = None) -> "World":
+        """Restore a world written by :meth:`save` (optionally onto another device)."""
+        from magicsoup_amd.utils.checkpoint import load_world_pickle
+
+        return load_world_pickle(Path(rundir) / name, device=device)
+
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        n = self.n_cells
+        for k in ("_genome_col", "_label_col"):
+            state.pop(k, None)
+        state["_cols"] = {k: c.view(n).cpu().clone() for k, c in self._cols.items()}
+        state["_genomes"] = self._genomes.to_strings()
+        state["_labels"] = self._labels.to_strings()
+        state["cell_map"] = self.cell_map.cpu()
+        state["molecule_map"] = self.molecule_map.cpu()
+        return state
+
+    def __setstate__(self, state):
+        dev = torch.device(state["device"] if torch.cuda.is_available() else "cpu")
+        if dev.type == "cpu":
+            state["device"] = "cpu"
+        cols = state.pop("_cols")
+        genomes = state.pop("_genomes")
+        labels = state.pop("_labels")
+        self.__dict__.update(state)
+        self.__dict__["_cols"] = {k: _Column(v.to(dev)) for k, v in cols.items()}
+        for c in self._cols.values():
+            c.view(int(c.buf.size(0)))
+        self.__dict__["_genomes"] = StringArena(dev, width=64)
+        self.__dict__["_labels"] = StringArena(dev, width=16)
+        self._genomes.append_strings(genomes)
+        self._labels.append_strings(labels)
+        self.__dict__["_genome_col"] = StringColumn(self._genomes)
+        self.__dict__["_label_col"] = StringColumn(self._labels)
+        self.__dict__["cell_map"] = state["cell_map"].to(dev)
+        self.__dict__["molecule_map"] = state["molecule_map"].to(dev)
+
+    def to(self, device: str) -> "World":
+        """Move all state of this world to ``device`` (returns ``self``)."""
+        dev = torch.device(device)
+        st = self.__getstate__()
+        st["device"] = device
+        self.__setstate__(st)
+        kin = self.kinetics
+        kin.device = device
+        for name, val in list(vars(kin).items()):
+            if isinstance(val, torch.Tensor):
+                setattr(kin, name, val.to(dev))
+        for mp in (kin.km_map, kin.vmax_map, kin.sign_map, kin.hill_map, kin.reaction_map, kin.transport_map, kin.effector_map):
+            for name, val in list(vars(mp).items()):
+                if isinstance(val, torch.Tensor):
+                    setattr(mp, name, val.to(dev))
+        return self
+
+    def save_state(self, statedir: Path):
+        """Write the current state (tensors + ``cells.fasta``) in the reference's format."""
+        from magicsoup_amd.utils.checkpoint import save_state
+
+        save_state(self, Path(statedir))
+
+    def load_state(self, statedir: Path, ignore_cell_params: bool = False):
+        """Load a state written by :meth:`save_state` (re-translating genomes unless
+        ``ignore_cell_params``)."""
+        from magicsoup_amd.utils.checkpoint import load_state
+
+        load_state(self, Path(statedir), ignore_cell_params=ignore_cell_params)
+
+    # ------------------------------------------------------------------ internals
+    def _as_packed(self, genomes) -> tuple[torch.Tensor, torch.Tensor]:
+        if isinstance(genomes, tuple) and len(genomes) == 2 and isinstance(genomes[0], torch.Tensor):
+            rows, lens = genomes
+            return rows.to(self.device, torch.uint8), lens.to(self.device, torch.int32)
+        genomes = list(genomes)
+        arr, lens = pack_strings(genomes)
+        return torch.from_numpy(arr).to(self.device), torch.from_numpy(lens).to(self.device)
+
+    def _random_labels(self, k: int) -> tuple[torch.Tensor, torch.Tensor]:
+        return world_ops.random_labels(self, k, _LABEL_LEN)
+
+    def _find_free_random_positions(self, n_cells: int) -> torch.Tensor:
+        return world_ops.free_positions(self, n_cells)
+
+    def _get_molecule_map(self, n: int, size: int, init: str) -> torch.Tensor:
+        if init == "zeros":
+            return torch.zeros(n, size, size, dtype=torch.float32, device=self.device)
+        if init == "randn":
+            return (torch.randn(n, size, size, dtype=torch.float32, device=self.device) + 10.0).abs()
+        raise ValueError(f"Didnt recognize mol_map_init={init}. Should be one of: 'zeros', 'randn'.")
+
+    def _get_permeate(self, mol_perm_rate: float) -> float:
+        return _permeation_factor(mol_perm_rate)
+
+    def _get_diffuse(self, mol_diff_rate: float) -> tuple[float, float]:
+        return _diffusion_weights(mol_diff_rate)
+
+    def _i32_tensor(self, d: Any) -> torch.Tensor:
+        return torch.tensor(d, device=self.device, dtype=torch.int32)
+
+    def _f32_tensor(self, d: Any) -> torch.Tensor:
+        return torch.tensor(d, device=self.device, dtype=torch.float32)
+
+    def __repr__(self) -> str:
+        return f"World(map_size:{self.map_size!r},abs_temp:{self.abs_temp!r},device:{self.device!r})"

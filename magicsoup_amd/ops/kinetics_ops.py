@@ -1,0 +1,101 @@
+"""Dispatch of the kinetics hot paths to the native cores.
+
+CPU tensors go to the OpenMP host module, HIP tensors to the gfx950 kernels (no fallback between
+the two). Tensors cross into C++ as contiguous buffers; HIP launches run on the current stream.
+"""
+from __future__ import annotations
+
+import torch
+
+from magicsoup_amd.constants import GAS_CONSTANT
+from magicsoup_amd.ops import native
+
+_I32 = ("N", "Nf", "Nb", "A")
+_F32 = ("Kmr", "Kmf", "Kmb", "Vmax", "Ke")
+
+
+def _canonical_params(kin) -> dict[str, torch.Tensor]:
+    """Parameter tensors as contiguous int32 / float32, re-assigned on the object if converted."""
+    out = {}
+    for name in _I32 + _F32:
+        t = getattr(kin, name)
+        want = torch.int32 if name in _I32 else torch.float32
+        if t.dtype != want or not t.is_contiguous():
+            t = t.to(want).contiguous()
+            setattr(kin, name, t)
+        out[name] = t
+    return out
+
+
+def _np(t: torch.Tensor):
+    return t.detach().numpy()
+
+
+def integrate(kin, X: torch.Tensor, trims, n_iters: int) -> list[int]:
+    """Fused integrate_signals on X (c, s) in place; returns the per-part iteration masks."""
+    p = _canonical_params(kin)
+    c = X.size(0)
+    if c == 0:
+        return []
+    if p["N"].size(0) < c:
+        raise ValueError(f"kinetics has {p['N'].size(0)} cell rows but X has {c}")
+    if X.is_cuda:
+        from magicsoup_amd.ops import hip_ops
+
+        return hip_ops.integrate(X, p, list(trims), n_iters)
+    masks = native.host().integrate_signals(
+        _np(X),
+        *(_np(p[k]) for k in ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke")),
+        None,
+        [float(t) for t in trims],
+        int(n_iters),
+    )
+    return list(masks)
+
+
+def _luts(kin, device) -> dict[str, torch.Tensor]:
+    return {
+        "vmax": kin.vmax_map.weights.to(device=device, dtype=torch.float32).contiguous(),
+        "km": kin.km_map.weights.to(device=device, dtype=torch.float32).contiguous(),
+        "signs": kin.sign_map.signs.to(device=device, dtype=torch.int32).contiguous(),
+        "hills": kin.hill_map.numbers.to(device=device, dtype=torch.int32).contiguous(),
+        "react": kin.reaction_map.M.to(device=device, dtype=torch.int32).contiguous(),
+        "trnsp": kin.transport_map.M.to(device=device, dtype=torch.int32).contiguous(),
+        "eff": kin.effector_map.M.to(device=device, dtype=torch.int32).contiguous(),
+        "energies": kin.mol_energies.to(device=device, dtype=torch.float32).contiguous(),
+    }
+
+
+def build_params(kin, rows: torch.Tensor, tokens: torch.Tensor) -> None:
+    """Write parameter rows ``rows`` from dense tokens (n, P, D, 5)."""
+    p = _canonical_params(kin)
+    dev = p["N"].device
+    if rows.numel() == 0:
+        return
+    tokens = tokens.to(device=dev, dtype=torch.int32).contiguous()
+    rows = rows.to(device=dev, dtype=torch.int32).contiguous()
+    luts = _luts(kin, dev)
+    # vector maps may be narrower than the token alphabet if a user swapped them (tests do)
+    n_vec = min(luts["react"].size(0), luts["trnsp"].size(0), luts["eff"].size(0))
+    for k in ("react", "trnsp", "eff"):
+        luts[k] = luts[k][:n_vec].contiguous()
+    if dev.type == "cuda":
+        from magicsoup_amd.ops import hip_ops
+
+        hip_ops.build_params(tokens, rows, luts, p, float(kin.abs_temp), GAS_CONSTANT)
+        return
+    native.host().build_params(
+        _np(tokens),
+        _np(rows),
+        _np(luts["vmax"]),
+        _np(luts["km"]),
+        _np(luts["signs"]),
+        _np(luts["hills"]),
+        _np(luts["react"]),
+        _np(luts["trnsp"]),
+        _np(luts["eff"]),
+        _np(luts["energies"]),
+        float(kin.abs_temp),
+        float(GAS_CONSTANT),
+        *(_np(p[k]) for k in ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke")),
+    )

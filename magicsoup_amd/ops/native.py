@@ -1,0 +1,57 @@
+"""Loader for the native modules.
+
+``host()`` returns the OpenMP host core, ``hip()`` the gfx950 device core. Both are built in-tree on
+first use if missing (see :mod:`magicsoup_amd.ops.build`). A missing or broken device module on a
+machine with a GPU is a hard error: there is no silent fallback from a CUDA/HIP tensor to a CPU or
+eager-PyTorch implementation.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import threading
+
+_lock = threading.Lock()
+_mods: dict[str, object] = {}
+
+
+def _load(name: str, builder) -> object:
+    with _lock:
+        if name in _mods:
+            return _mods[name]
+        try:
+            mod = importlib.import_module(f"magicsoup_amd.{name}")
+        except ImportError:
+            if os.environ.get("MS_NO_AUTOBUILD"):
+                raise
+            builder()
+            mod = importlib.import_module(f"magicsoup_amd.{name}")
+        _mods[name] = mod
+        return mod
+
+
+def host():
+    """The OpenMP host module ``magicsoup_amd._host`` (built on demand)."""
+    from magicsoup_amd.ops import build
+
+    return _load("_host", build.build_host)
+
+
+def hip():
+    """The gfx950 device module ``magicsoup_amd._hip`` (built on demand; raises if unavailable)."""
+    from magicsoup_amd.ops import build
+
+    try:
+        return _load("_hip", build.build_hip)
+    except Exception as err:  # pragma: no cover - exercised on GPU boxes only
+        raise RuntimeError(
+            "magicsoup_amd: the gfx950 HIP extension (_hip) could not be loaded; GPU execution"
+            " requires it (no fallback). Build it with `python -m magicsoup_amd.ops.build`."
+        ) from err
+
+
+def set_seed(seed: int) -> None:
+    """Seed every native RNG stream (host and device) for reproducible runs."""
+    host().set_seed(int(seed) & 0xFFFFFFFFFFFFFFFF)
+    if "_hip" in _mods:
+        _mods["_hip"].set_seed(int(seed) & 0xFFFFFFFFFFFFFFFF)  # type: ignore[attr-defined]
