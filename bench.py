@@ -1,0 +1,185 @@
+"""Flagship benchmark: whole simulation steps per second.
+
+Workload = the reference's macro benchmark loop (``performance/run_simulation.py:57-100``) at the
+BASELINE.json config: Wood-Ljungdahl chemistry, 4096x4096 map, random-normal molecule map, 500 bp
+random genomes, population topped up to >= 50,000 cells every step. One step:
+
+    top up to N cells -> enzymatic_activity -> kill (ATP < 1) -> replicate (ATP > 5: ATP -= 4,
+    divide) -> recombinate_cells -> mutate_cells -> degrade -> diffuse -> increment lifetimes
+
+Single GPU: one ``World`` on ``cuda:0``. N GPUs (``torchrun --nproc-per-node N``): one world,
+domain-decomposed over the ranks (``magicsoup_amd.parallel``; strong scaling of the fixed config).
+Rank 0 prints one JSON line; ``value`` is steps/s of the whole job (max time over ranks).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--map-size S] [--cells C]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+BASELINE_STEPS_PER_S = 3.3  # reference, 40k cells, latest published
+METRIC = "simulation steps/sec (whole node), 4096×4096 map / 50k cells, 1/2/4/8 MI355X"
+
+
+def _args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--map-size", type=int, default=4096)
+    ap.add_argument("--cells", type=int, default=50_000)
+    ap.add_argument("--genome-size", type=int, default=500)
+    ap.add_argument("--chemistry", default="wood_ljungdahl", help="wood_ljungdahl | synthetic:M:R")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--profile-phases", action="store_true", help="print per-phase times to stderr")
+    return ap.parse_args()
+
+
+def _chemistry(spec: str):
+    if spec.startswith("synthetic"):
+        from magicsoup_amd.examples.synthetic import make_chemistry
+
+        _, m, r = spec.split(":")
+        return make_chemistry(int(m), int(r), seed=0)
+    from magicsoup_amd.examples.wood_ljungdahl import CHEMISTRY
+
+    return CHEMISTRY
+
+
+def random_genomes(k: int, size: int, device) -> tuple[torch.Tensor, torch.Tensor]:
+    """k uniformly random genomes of ``size`` nt as a packed (bytes, lengths) batch (on device)."""
+    lut = torch.tensor(list(b"TCGA"), dtype=torch.uint8, device=device)
+    rows = lut[torch.randint(0, 4, (k, size), device=device)]
+    return rows, torch.full((k,), size, dtype=torch.int32, device=device)
+
+
+def step(world, n_target: int, genome_size: int, atp: int, timer=None):
+    def ph(name):
+        import contextlib
+
+        return timer.phase(name) if timer is not None else contextlib.nullcontext()
+
+    with ph("top_up"):
+        n = world.n_cells
+        if n < n_target:
+            world.spawn_cells(random_genomes(n_target - n, genome_size, world.cell_molecules.device))
+    with ph("activity"):
+        world.enzymatic_activity()
+    with ph("kill"):
+        kill = torch.nonzero(world.cell_molecules[:, atp] < 1.0).flatten()
+        world.kill_cells(kill)
+    with ph("replicate"):
+        repl = torch.nonzero(world.cell_molecules[:, atp] > 5.0).flatten()
+        world.cell_molecules[repl, atp] -= 4.0
+        world.divide_cells_t(repl)
+    with ph("recombinate"):
+        world.recombinate_cells()
+    with ph("mutate"):
+        world.mutate_cells()
+    with ph("wrap_up"):
+        world.degrade_molecules()
+        world.diffuse_molecules()
+        world.increment_cell_lifetimes()
+
+
+def main():
+    a = _args()
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world_size > 1
+    if distributed:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = f"cuda:{local_rank}" if torch.cuda.is_available() else "cpu"
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_rank)
+
+    import magicsoup_amd as ms
+    from magicsoup_amd.utils.profiling import PhaseTimer
+
+    chem = _chemistry(a.chemistry)
+    atp = chem.molname_2_idx.get("ATP", 0)
+    ms.set_seed(a.seed + rank)
+    torch.manual_seed(a.seed + rank)
+
+    if distributed:
+        from magicsoup_amd.parallel import DistributedWorld
+
+        world = DistributedWorld(chemistry=chem, map_size=a.map_size, device=device, seed=a.seed)
+    else:
+        world = ms.World(chemistry=chem, map_size=a.map_size, device=device, seed=a.seed)
+
+    t0 = time.time()
+    world.spawn_cells(random_genomes(a.cells // max(1, world_size if distributed else 1), a.genome_size, device))
+    setup_s = time.time() - t0
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if distributed:
+            torch.distributed.barrier()
+            torch.cuda.synchronize()
+
+    n_target = a.cells // world_size if distributed else a.cells
+    for _ in range(a.warmup):
+        step(world, n_target, a.genome_size, atp)
+    sync()
+    timer = PhaseTimer(device) if a.profile_phases else None
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(world, n_target, a.genome_size, atp, timer)
+    sync()
+    dt = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+        nc = torch.tensor([world.n_cells], dtype=torch.int64, device=device)
+        torch.distributed.all_reduce(nc)
+        n_cells = int(nc.item())
+    else:
+        n_cells = world.n_cells
+    ms_per_step = dt / a.steps * 1e3
+    value = a.steps / dt
+    if rank == 0:
+        if timer is not None:
+            print(json.dumps({"phases_ms": timer.summary(), "setup_s": setup_s, "n_cells": n_cells}), file=sys.stderr)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "steps/s",
+            "n_gpus": world_size if distributed else a.gpus,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(value / BASELINE_STEPS_PER_S, 2),
+            "dtype": "fp32",
+            "data": "synthetic (random 500 bp genomes, |N(10,1)| molecule map, random-init kinetics maps)",
+            "config": {
+                "model": f"magicsoup World, {a.chemistry} chemistry ({len(chem.molecules)} molecules /"
+                f" {len(chem.reactions)} reactions)",
+                "global_batch": a.cells,
+                "seq_len": a.genome_size,
+                "map_size": a.map_size,
+                "cells_at_end": n_cells,
+                "parallelism": f"spatial{world_size}" if distributed else "single",
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if distributed:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

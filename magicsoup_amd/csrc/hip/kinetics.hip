@@ -1,0 +1,484 @@
+// gfx950 kinetics kernels: fused signal integrator (World.enzymatic_activity) and the fused
+// parameter builder (Kinetics.set_cell_params).
+//
+// Integrator mapping (see ms_kinetics.h for the exact-global-exit scheme):
+//   * G lanes (32 or 64) of a wavefront own one cell; a 256-thread workgroup holds 256/G cells.
+//   * The cell's active proteins (Vmax' != 0) are compacted with a ballot prefix; their
+//     stoichiometry rows are staged once per part into LDS as packed int8x4 words (N, Nf, Nb, A),
+//     row stride padded to an odd word count so both access patterns are bank-conflict free:
+//       - protein phase: lane = protein, loops over signals (products, quotients, flags);
+//       - signal phase:  lane = signal, loops over proteins (consumption sums, X updates).
+//   * All 4 equilibrium iterations run unconditionally; the 5 candidate states go to a snapshot
+//     buffer and every cell ORs its "still correcting" bits into one word per part. The next part
+//     (or the final scatter) picks the state where the reference's global `torch.any` loop stops.
+//   3 part launches + 1 scatter launch per enzymatic_activity; no grid barriers, no host syncs.
+#include "hip_common.h"
+#include "ms_kinetics.h"
+
+namespace msd {
+
+constexpr int kBlock = 256;
+
+struct IntegrateArgs {
+  int c, P, s, m, S;
+  const int32_t *N, *Nf, *Nb, *A;
+  const float *Kmr, *Kmf, *Kmb, *Vmax, *Ke;
+  const float* cell_mols;     // (c, m)       part 0 source
+  const float* molmap;        // (m, S, S)    part 0 source
+  const int32_t* positions;   // (c, 2)       part 0 source
+  const float* snap_prev;     // (c, kSnap, s) previous part's candidates (part > 0)
+  const unsigned* mask_prev;  // previous part's iteration mask
+  int n_iters_prev;
+  float* snap_out;            // (c, kSnap, s)
+  unsigned* mask_out;
+  float trim;
+  int n_iters;
+  int* overflow;              // set if a stoichiometry does not fit in int8
+  int slot_words;             // LDS words per cell slot
+  int sp;                     // padded LDS row stride (odd)
+};
+
+__device__ __forceinline__ int stop_iter(unsigned mask, int n_iters) {
+  for (int it = 0; it < n_iters; ++it)
+    if (!(mask & (1u << it))) return it;
+  return n_iters;
+}
+
+__device__ __forceinline__ int w_n(int w) { return (int)(int8_t)(w & 0xFF); }
+__device__ __forceinline__ int w_nf(int w) { return (w >> 8) & 0xFF; }
+__device__ __forceinline__ int w_nb(int w) { return (w >> 16) & 0xFF; }
+__device__ __forceinline__ int w_a(int w) { return (int)(int8_t)((w >> 24) & 0xFF); }
+
+template <int G>
+__global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  const int slot = threadIdx.x / G, lane = threadIdx.x % G;
+  const int cps = blockDim.x / G;
+  unsigned& block_bits = *reinterpret_cast<unsigned*>(smem + cps * a.slot_words);
+  const int cell = blockIdx.x * cps + slot;
+  const bool valid = cell < a.c;
+  const int P = a.P, s = a.s, SP = a.sp;
+
+  int* words = smem + slot * a.slot_words;
+  int* act = words + P * SP;
+  float* V = reinterpret_cast<float*>(act + P);
+  float* Va = V + P;
+  float* F = Va + P;
+  float* kmf = F + P;
+  float* kmb = kmf + P;
+  float* ke = kmb + P;
+  int* flg = reinterpret_cast<int*>(ke + P);
+  float* X0 = reinterpret_cast<float*>(flg + P);
+  float* Xc = X0 + s;
+  float* fs = Xc + s;
+  int* na_p = reinterpret_cast<int*>(fs + s);
+
+  if (threadIdx.x == 0) block_bits = 0u;
+
+  // ---- 1. load X0 (part 0: gather cell + pixel molecules; else: selected previous candidate)
+  if (valid) {
+    if (a.snap_prev == nullptr) {
+      const int px = a.positions[2 * cell], py = a.positions[2 * cell + 1];
+      const size_t pix = (size_t)px * a.S + py, plane = (size_t)a.S * a.S;
+      for (int j = lane; j < s; j += G)
+        X0[j] = j < a.m ? a.cell_mols[(size_t)cell * a.m + j] : a.molmap[(size_t)(j - a.m) * plane + pix];
+    } else {
+      const int k = stop_iter(*a.mask_prev, a.n_iters_prev);
+      const float* src = a.snap_prev + ((size_t)cell * ms::kSnap + k) * s;
+      for (int j = lane; j < s; j += G) X0[j] = src[j];
+    }
+  }
+
+  // ---- 2. compact active proteins (Vmax' != 0) in ascending order with a ballot prefix
+  {
+    const int gbase = (threadIdx.x & 63) - lane;  // first lane of this group inside the wave
+    int na = 0;
+    for (int p0 = 0; p0 < P; p0 += G) {
+      const int p = p0 + lane;
+      float vm = 0.0f;
+      bool on = false;
+      if (valid && p < P) {
+        vm = a.Vmax[(size_t)cell * P + p] * a.trim;
+        on = !(vm <= 0.0f);  // NaN stays active (propagates like the reference)
+      }
+      const unsigned long long bal = __ballot(on);
+      unsigned long long gm;
+      if constexpr (G == 64) gm = bal;
+      else gm = (bal >> gbase) & ((1ull << G) - 1ull);
+      const int rank = __popcll(gm & ((1ull << lane) - 1ull));
+      if (on) {
+        const int k = na + rank;
+        act[k] = p;
+        const size_t o = (size_t)cell * P + p;
+        kmf[k] = a.Kmf[o];
+        kmb[k] = a.Kmb[o];
+        ke[k] = a.Ke[o];
+        V[k] = vm > 0.0f || vm != vm ? vm : 0.0f;  // temporarily holds Vmax'
+      }
+      na += __popcll(gm);
+    }
+    if (lane == 0) *na_p = na;
+  }
+  __syncthreads();
+  const int na = valid ? *na_p : 0;
+
+  // ---- 3. stage packed stoichiometry rows of the active proteins
+  for (int idx = lane; idx < na * s; idx += G) {
+    const int k = idx / s, j = idx - k * s;
+    const size_t o = ((size_t)cell * P + act[k]) * s + j;
+    const int n = a.N[o], nf = a.Nf[o], nb = a.Nb[o], aa = a.A[o];
+    if (n < -128 || n > 127 || nf > 255 || nb > 255 || nf < 0 || nb < 0 || aa < -128 || aa > 127) atomicOr(a.overflow, 1);
+    words[k * SP + j] = (n & 0xFF) | ((nf & 0xFF) << 8) | ((nb & 0xFF) << 16) | ((aa & 0xFF) << 24);
+  }
+  __syncthreads();
+
+  // ---- 4. velocities (protein phase)
+  for (int k = lane; k < na; k += G) {
+    const int* wr = words + k * SP;
+    const float* kmr = a.Kmr + ((size_t)cell * P + act[k]) * s;
+    float xf = 1.0f, xb = 1.0f, ar = 1.0f;
+    bool anyf = false, anyb = false;
+    for (int j = 0; j < s; ++j) {
+      const int w = wr[j];
+      if (w == 0) continue;
+      const int nf = w_nf(w), nb = w_nb(w), av = w_a(w);
+      const float x = X0[j];
+      if (nf > 0) {
+        xf *= ms::ipow(x, nf);
+        anyf = true;
+      }
+      if (nb > 0) {
+        xb *= ms::ipow(x, nb);
+        anyb = true;
+      }
+      if (av != 0) {
+        float r = ms::ipow(x, av);
+        r = r / (r + kmr[j]);
+        if (ms::f_isnan(r)) r = 1.0f;
+        ar *= r;
+      }
+    }
+    float kf = ms::clean_prod(xf) / kmf[k];
+    if (!anyf) kf = 0.0f;
+    if (ms::f_isinf(kf)) kf = ms::kMax;
+    float kb = ms::clean_prod(xb) / kmb[k];
+    if (!anyb) kb = 0.0f;
+    if (ms::f_isinf(kb)) kb = ms::kMax;
+    if (ms::f_isinf(ar)) ar = ms::kMax;
+    const float acat = (kf - kb) / (1.0f + kf + kb);
+    float v = acat * V[k] * ar;
+    v = v < ms::kMin ? ms::kMin : (v > ms::kMax ? ms::kMax : v);
+    V[k] = v;
+  }
+  __syncthreads();
+
+  // ---- 5. consumption per signal and the negative-concentration factors (signal phase)
+  for (int j = lane; j < s; j += G) {
+    float cons = 0.0f;
+    for (int k = 0; k < na; ++k) {
+      const float nv = (float)w_n(words[k * SP + j]) * V[k];
+      if (nv < 0.0f) cons += -nv;
+    }
+    const float f = X0[j] / cons;
+    fs[j] = f > 1.0f ? 1.0f : f;
+  }
+  __syncthreads();
+
+  // ---- 6. per-protein limiting factor (protein phase)
+  for (int k = lane; k < na; k += G) {
+    const int* wr = words + k * SP;
+    const float v = V[k];
+    float fmin = 1.0f;
+    bool nan = false;
+    for (int j = 0; j < s; ++j) {
+      const int n = w_n(wr[j]);
+      if ((float)n * v < 0.0f) {
+        const float f = fs[j];
+        if (ms::f_isnan(f)) nan = true;
+        else if (f < fmin) fmin = f;
+      }
+    }
+    Va[k] = v * (nan ? NAN : fmin);
+    F[k] = 1.0f;
+    flg[k] = (v > 0.0f ? 1 : 0) | (fabsf(v) > 0.1f ? 2 : 0);
+  }
+  __syncthreads();
+
+  // ---- 7. X1 (signal phase), candidate 0
+  float* snap = a.snap_out + (size_t)(valid ? cell : 0) * ms::kSnap * s;
+  for (int j = lane; j < s; j += G) {
+    float x = X0[j];
+    for (int k = 0; k < na; ++k) {
+      const int n = w_n(words[k * SP + j]);
+      if (n != 0) x += (float)n * Va[k];
+    }
+    x = x < 0.0f ? 0.0f : x;
+    Xc[j] = x;
+    if (valid) snap[j] = x;
+  }
+  __syncthreads();
+
+  // ---- 8. equilibrium damping trajectory
+  unsigned bits = 0u;
+  float inc = 0.5f;
+  for (int it = 0; it < a.n_iters; ++it, inc *= 0.5f) {
+    for (int k = lane; k < na; k += G) {
+      const int* wr = words + k * SP;
+      float pf = 1.0f, pb = 1.0f;
+      bool anyf = false, anyb = false;
+      for (int j = 0; j < s; ++j) {
+        const int w = wr[j];
+        if (w == 0) continue;
+        const int nf = w_nf(w), nb = w_nb(w);
+        if (nf > 0) {
+          pf *= ms::ipow(Xc[j], nf);
+          anyf = true;
+        }
+        if (nb > 0) {
+          pb *= ms::ipow(Xc[j], nb);
+          anyb = true;
+        }
+      }
+      pf = anyf ? ms::clean_prod(pf) : 0.0f;
+      pb = anyb ? ms::clean_prod(pb) : 0.0f;
+      float Q = pb / pf;
+      if (ms::f_isnan(Q)) Q = 1.0f;
+      else Q = Q < ms::kEps ? ms::kEps : (Q > ms::kMax ? ms::kMax : Q);
+      const float qke = Q / ke[k];
+      const bool fwd = flg[k] & 1, imp = flg[k] & 2;
+      const float f0 = F[k];
+      bool low = fwd ? (qke < ms::kLower) : (qke > ms::kUpper);
+      if (fwd && f0 == 1.0f) low = false;
+      bool high = fwd ? (qke > ms::kUpper) : (qke < ms::kLower);
+      if (!fwd && f0 == 0.0f) high = false;
+      if ((low || high) && imp) bits |= 1u << it;
+      float f = f0;
+      if (high) f -= inc;
+      if (low) f += inc;
+      F[k] = f > 1.0f ? 1.0f : (f < 0.0f ? 0.0f : f);
+    }
+    __syncthreads();
+    float* sn = snap + (size_t)(it + 1) * s;
+    for (int j = lane; j < s; j += G) {
+      float x = X0[j];
+      for (int k = 0; k < na; ++k) {
+        const int n = w_n(words[k * SP + j]);
+        if (n != 0) x += (float)n * (Va[k] * F[k]);
+      }
+      x = x < 0.0f ? 0.0f : x;
+      Xc[j] = x;
+      if (valid) sn[j] = x;
+    }
+    __syncthreads();
+  }
+
+  // ---- 9. one mask OR per workgroup
+  if (bits) atomicOr(&block_bits, bits);
+  __syncthreads();
+  if (threadIdx.x == 0 && block_bits) atomicOr(a.mask_out, block_bits);
+}
+
+// Final state -> cell_molecules and the molecule-map pixels under the cells.
+__global__ void __launch_bounds__(kBlock) integrate_scatter_kernel(int c, int s, int m, int S, const float* snap,
+                                                                   const unsigned* mask, int n_iters,
+                                                                   const int32_t* positions, float* cell_mols,
+                                                                   float* molmap, float* X_out) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)c * s) return;
+  const int cell = (int)(t / s), j = (int)(t - (long long)cell * s);
+  const int k = stop_iter(*mask, n_iters);
+  const float x = snap[((size_t)cell * ms::kSnap + k) * s + j];
+  if (X_out) {
+    X_out[(size_t)cell * s + j] = x;
+    return;
+  }
+  if (j < m) {
+    cell_mols[(size_t)cell * m + j] = x;
+  } else {
+    const size_t pix = (size_t)positions[2 * cell] * S + positions[2 * cell + 1];
+    molmap[(size_t)(j - m) * S * S + pix] = x;
+  }
+}
+
+// X (c, s) -> snapshot slot 0 with an all-zero mask, so a part kernel can start from an explicit X.
+__global__ void load_x_kernel(int c, int s, const float* X, float* snap) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)c * s) return;
+  const int cell = (int)(t / s), j = (int)(t - (long long)cell * s);
+  snap[(size_t)cell * ms::kSnap * s + j] = X[t];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Parameter build: one thread per (row, protein slot). Semantics in kinetics_host.cpp.
+struct BuildArgs {
+  int n, P, D, Pt, s;
+  const int32_t* tokens;  // (n, P, D, 5)
+  const int32_t* rows;    // (n,)
+  const float *vmax_w, *km_w;
+  const int32_t *signs, *hills, *RM, *TM, *EM;
+  int nw, nk, nsg, nh, nv;
+  const float* energies;
+  float abs_temp, gas;
+  int32_t *N, *Nf, *Nb, *A;
+  float *Kmr, *Kmf, *Kmb, *Vmax, *Ke;
+};
+
+__device__ __forceinline__ int lut(int t, int lim) { return (t >= 0 && t < lim) ? t : 0; }
+
+__global__ void __launch_bounds__(kBlock) build_params_kernel(BuildArgs b) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)b.n * b.Pt) return;
+  const int ci = (int)(t / b.Pt), p = (int)(t - (long long)ci * b.Pt);
+  const size_t row = (size_t)b.rows[ci];
+  const size_t o2 = row * b.Pt + p, o3 = o2 * b.s;
+  const int32_t* pt = b.tokens + ((size_t)ci * b.P + (p < b.P ? p : 0)) * b.D * 5;
+  const int nd = p < b.P ? b.D : 0;
+
+  ms::NanMean vm, km;
+  for (int d = 0; d < nd; ++d) {
+    const int32_t* dm = pt + d * 5;
+    if (dm[0] == 0 || dm[0] == 3) continue;
+    vm.add(b.vmax_w[lut(dm[1], b.nw)]);
+    km.add(b.km_w[lut(dm[2], b.nk)]);
+  }
+  float E = 0.0f;
+  for (int j = 0; j < b.s; ++j) {
+    int n = 0, nf = 0, nb = 0, av = 0, kc = 0;
+    float ks = 0.0f;
+    for (int d = 0; d < nd; ++d) {
+      const int32_t* dm = pt + d * 5;
+      const int ty = dm[0];
+      if (ty == 0) continue;
+      const int sgn = b.signs[lut(dm[3], b.nsg)];
+      const int vi = lut(dm[4], b.nv);
+      if (ty == 3) {
+        const int e = b.EM[(size_t)vi * b.s + j];
+        if (e == 0) continue;
+        av += e * sgn * b.hills[lut(dm[1], b.nh)];
+        const float kv = (float)e * b.km_w[lut(dm[2], b.nk)];
+        if (!ms::f_isnan(kv) && kv != 0.0f) {
+          ks += kv;
+          ++kc;
+        }
+      } else {
+        const int v = (ty == 1 ? b.RM : b.TM)[(size_t)vi * b.s + j];
+        const int ndv = v * sgn;
+        n += ndv;
+        if (ndv < 0) nf += -ndv;
+        if (ndv > 0) nb += ndv;
+      }
+    }
+    b.N[o3 + j] = n;
+    b.Nf[o3 + j] = nf;
+    b.Nb[o3 + j] = nb;
+    b.A[o3 + j] = av;
+    b.Kmr[o3 + j] = powf(kc > 0 ? ks / (float)kc : 0.0f, (float)av);
+    E += (float)n * b.energies[j];
+  }
+  float kev = expf(-E / b.abs_temp / b.gas);
+  kev = kev < ms::kEps ? ms::kEps : (kev > ms::kMax ? ms::kMax : kev);
+  const float kmn = km.value0();
+  float kmfv = kev >= 1.0f ? kmn : kmn / kev;
+  float kmbv = kev >= 1.0f ? kmn * kev : kmn;
+  b.Ke[o2] = kev;
+  b.Kmf[o2] = kmfv < ms::kEps ? ms::kEps : (kmfv > ms::kMax ? ms::kMax : kmfv);
+  b.Kmb[o2] = kmbv < ms::kEps ? ms::kEps : (kmbv > ms::kMax ? ms::kMax : kmbv);
+  b.Vmax[o2] = vm.value0();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host launchers
+
+static int slot_words_for(int P, int s, int sp) {
+  int w = P * sp + P * 8 + 3 * s + 1;
+  return (w + 3) & ~3;  // keep every slot 16-byte aligned
+}
+
+// X_src: if nonzero, integrate explicit signals X (c, s) and write the result back there
+// (Kinetics.integrate_signals); otherwise gather from / scatter to the world state.
+void integrate(int c, int P, int s, int m, int S, uintptr_t N, uintptr_t Nf, uintptr_t Nb, uintptr_t A,
+               uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb, uintptr_t Vmax, uintptr_t Ke, uintptr_t cell_mols,
+               uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
+               uintptr_t masks, uintptr_t overflow, const std::vector<float>& trims, int n_iters, uintptr_t stream) {
+  if (c <= 0) return;
+  if (n_iters < 0 || n_iters > ms::kEqIters) throw std::invalid_argument("n_iters must be in 0..4");
+  const int nparts = (int)trims.size();
+  hipStream_t st = S_(stream);
+  MS_HIP_CHECK(hipMemsetAsync(P_<unsigned>(masks), 0, sizeof(unsigned) * (nparts + 1), st));
+  const int G = s <= 32 ? 32 : 64;
+  const int sp = (s % 2 == 0) ? s + 1 : s;
+  const int slot_words = slot_words_for(P, s, sp);
+  const size_t slot_bytes = (size_t)slot_words * 4;
+  const size_t budget = 64 * 1024;
+  int cps = kBlock / G;
+  while (cps > 1 && cps * slot_bytes > budget) --cps;
+  const size_t lds = cps * slot_bytes + 16;
+  if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
+  const int threads = cps * G;
+  const unsigned grid = cdiv(c, cps);
+
+  float* snaps[2] = {P_<float>(snap_a), P_<float>(snap_b)};
+  unsigned* mk = P_<unsigned>(masks);
+  if (X_io) {
+    // explicit X: stage it as candidate 0 of snap_b with the zero mask slot nparts
+    load_x_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(c, s, P_<float>(X_io), snaps[1]);
+    MS_LAUNCH_CHECK();
+  }
+  for (int part = 0; part < nparts; ++part) {
+    IntegrateArgs a{};
+    a.c = c; a.P = P; a.s = s; a.m = m; a.S = S;
+    a.N = P_<int32_t>(N); a.Nf = P_<int32_t>(Nf); a.Nb = P_<int32_t>(Nb); a.A = P_<int32_t>(A);
+    a.Kmr = P_<float>(Kmr); a.Kmf = P_<float>(Kmf); a.Kmb = P_<float>(Kmb); a.Vmax = P_<float>(Vmax); a.Ke = P_<float>(Ke);
+    a.cell_mols = P_<float>(cell_mols); a.molmap = P_<float>(molmap); a.positions = P_<int32_t>(positions);
+    if (part == 0 && !X_io) {
+      a.snap_prev = nullptr;
+    } else if (part == 0) {
+      a.snap_prev = snaps[1];
+      a.mask_prev = mk + nparts;  // zero word -> candidate 0
+      a.n_iters_prev = n_iters;
+    } else {
+      a.snap_prev = snaps[(part - 1) & 1];
+      a.mask_prev = mk + part - 1;
+      a.n_iters_prev = n_iters;
+    }
+    a.snap_out = snaps[part & 1];
+    a.mask_out = mk + part;
+    a.trim = trims[part];
+    a.n_iters = n_iters;
+    a.overflow = P_<int>(overflow);
+    a.slot_words = slot_words;
+    a.sp = sp;
+    if (G == 32) integrate_part_kernel<32><<<grid, threads, lds, st>>>(a);
+    else integrate_part_kernel<64><<<grid, threads, lds, st>>>(a);
+    MS_LAUNCH_CHECK();
+  }
+  const int last = nparts - 1;
+  if (nparts == 0) return;
+  integrate_scatter_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(
+      c, s, m, S, snaps[last & 1], mk + last, n_iters, P_<int32_t>(positions), P_<float>(cell_mols),
+      P_<float>(molmap), X_io ? P_<float>(X_io) : nullptr);
+  MS_LAUNCH_CHECK();
+}
+
+void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_t rows, uintptr_t vmax_w, int nw,
+                  uintptr_t km_w, int nk, uintptr_t signs, int nsg, uintptr_t hills, int nh, uintptr_t RM,
+                  uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
+                  uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
+                  uintptr_t Vmax, uintptr_t Ke, uintptr_t stream) {
+  if (n <= 0 || Pt <= 0) return;
+  if (P > Pt) throw std::invalid_argument("build_params: token proteins exceed parameter capacity");
+  BuildArgs b{};
+  b.n = n; b.P = P; b.D = D; b.Pt = Pt; b.s = s;
+  b.tokens = P_<int32_t>(tokens); b.rows = P_<int32_t>(rows);
+  b.vmax_w = P_<float>(vmax_w); b.km_w = P_<float>(km_w);
+  b.signs = P_<int32_t>(signs); b.hills = P_<int32_t>(hills);
+  b.RM = P_<int32_t>(RM); b.TM = P_<int32_t>(TM); b.EM = P_<int32_t>(EM);
+  b.nw = nw; b.nk = nk; b.nsg = nsg; b.nh = nh; b.nv = nv;
+  b.energies = P_<float>(energies); b.abs_temp = abs_temp; b.gas = gas;
+  b.N = P_<int32_t>(N); b.Nf = P_<int32_t>(Nf); b.Nb = P_<int32_t>(Nb); b.A = P_<int32_t>(A);
+  b.Kmr = P_<float>(Kmr); b.Kmf = P_<float>(Kmf); b.Kmb = P_<float>(Kmb); b.Vmax = P_<float>(Vmax); b.Ke = P_<float>(Ke);
+  build_params_kernel<<<cdiv((long long)n * Pt, kBlock), kBlock, 0, S_(stream)>>>(b);
+  MS_LAUNCH_CHECK();
+}
+
+}  // namespace msd

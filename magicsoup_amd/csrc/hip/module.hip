@@ -1,0 +1,96 @@
+// pybind11 entry point of the gfx950 device module magicsoup_amd._hip.
+//
+// Tensors cross as raw device pointers (uintptr_t) together with the caller's current HIP stream,
+// so launches are ordered with PyTorch's work on that stream and can be captured into hipGraphs.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <atomic>
+
+#include "hip_common.h"
+
+namespace py = pybind11;
+
+namespace msd {
+// kinetics.hip
+void integrate(int c, int P, int s, int m, int S, uintptr_t N, uintptr_t Nf, uintptr_t Nb, uintptr_t A,
+               uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb, uintptr_t Vmax, uintptr_t Ke, uintptr_t cell_mols,
+               uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
+               uintptr_t masks, uintptr_t overflow, const std::vector<float>& trims, int n_iters, uintptr_t stream);
+void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_t rows, uintptr_t vmax_w, int nw,
+                  uintptr_t km_w, int nk, uintptr_t signs, int nsg, uintptr_t hills, int nh, uintptr_t RM,
+                  uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
+                  uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
+                  uintptr_t Vmax, uintptr_t Ke, uintptr_t stream);
+// world.hip
+void diffuse(int m, int S, uintptr_t map, uintptr_t tmp, uintptr_t wa, uintptr_t wb, uintptr_t scale,
+             uintptr_t partials, uintptr_t corr, uintptr_t totals, uintptr_t stream);
+size_t diffuse_partials_len(int m, int S);
+void scale_planes(int m, long long plane, uintptr_t map, uintptr_t f, uintptr_t stream);
+void permeate(int c, int m, int S, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map, uintptr_t stream);
+void claim_free(int k, long long n_pix, uintptr_t cell_map, uint64_t seed, uint64_t call, int attempts, uintptr_t out,
+                uintptr_t stream);
+void pick_neighbour(int k, uintptr_t cells, uintptr_t pos, int S, uintptr_t cell_map, uintptr_t pending, uint64_t seed,
+                    uint64_t call, uintptr_t cand, uintptr_t stream);
+void index_map(int c, uintptr_t pos, int S, uintptr_t idx_map, bool clear, uintptr_t stream);
+void neighbor_pairs(int nf, uintptr_t from, uintptr_t pos, int S, uintptr_t idx_map, uintptr_t in_from, uintptr_t in_to,
+                    uintptr_t counter, int cap, uintptr_t pairs, uintptr_t stream);
+// genetics.hip
+void translate_count(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, const std::vector<uint8_t>& st,
+                     const std::vector<uint8_t>& sp, const std::vector<uint8_t>& oc, uintptr_t dom_type,
+                     uintptr_t two_codon, int dom_size, int dom_type_size, uintptr_t nprot, uintptr_t ndom,
+                     uintptr_t stream);
+void translate_write(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, const std::vector<uint8_t>& st,
+                     const std::vector<uint8_t>& sp, const std::vector<uint8_t>& oc, uintptr_t dom_type,
+                     uintptr_t two_codon, int dom_size, int dom_type_size, uintptr_t nprot, int P, int D,
+                     uintptr_t tokens, uintptr_t stream);
+// mutations.hip
+void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
+               uintptr_t stream);
+void mut_apply(int nsel, uintptr_t sel, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t k,
+               double p_indel, double p_del, uint64_t seed, uint64_t call, uintptr_t out, int out_width,
+               uintptr_t out_len, uintptr_t stream);
+void rec_count(int n, uintptr_t pairs, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
+               uintptr_t stream);
+void rec_apply(int nsel, uintptr_t sel, uintptr_t pairs, uintptr_t arena, int width, uintptr_t lens, uintptr_t k,
+               uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out, int out_width,
+               uintptr_t out_len, uintptr_t stream);
+}  // namespace msd
+
+namespace {
+std::atomic<uint64_t> g_seed{0xC0FFEE1234ull};
+std::atomic<uint64_t> g_call{0};
+}  // namespace
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "magicsoup_amd gfx950 (MI355X) device kernels";
+  m.def("set_seed", [](uint64_t s) {
+    g_seed.store(s);
+    g_call.store(0);
+  });
+  m.def("next_call", []() { return py::make_tuple(g_seed.load(), g_call.fetch_add(1) + 1); },
+        "(seed, call) for a fresh Philox stream family");
+  m.def("device_arch", []() {
+    hipDeviceProp_t p;
+    int dev = 0;
+    MS_HIP_CHECK(hipGetDevice(&dev));
+    MS_HIP_CHECK(hipGetDeviceProperties(&p, dev));
+    return std::string(p.gcnArchName);
+  });
+  m.def("integrate", &msd::integrate);
+  m.def("build_params", &msd::build_params);
+  m.def("diffuse", &msd::diffuse);
+  m.def("diffuse_partials_len", &msd::diffuse_partials_len);
+  m.def("scale_planes", &msd::scale_planes);
+  m.def("permeate", &msd::permeate);
+  m.def("claim_free", &msd::claim_free);
+  m.def("pick_neighbour", &msd::pick_neighbour);
+  m.def("index_map", &msd::index_map);
+  m.def("neighbor_pairs", &msd::neighbor_pairs);
+  m.def("translate_count", &msd::translate_count);
+  m.def("translate_write", &msd::translate_write);
+  m.def("mut_count", &msd::mut_count);
+  m.def("mut_apply", &msd::mut_apply);
+  m.def("rec_count", &msd::rec_count);
+  m.def("rec_apply", &msd::rec_apply);
+}

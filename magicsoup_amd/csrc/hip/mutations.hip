@@ -1,0 +1,185 @@
+// gfx950 point mutations and recombinations on the device genome arena
+// (semantics of rust/mutations.rs:11-154).
+//
+// Both are two-phase: a cheap per-item Poisson draw over all genomes / neighbour pairs, then an
+// apply kernel for the (usually few) items that drew at least one event. Apply kernels draw the
+// event positions by sequential selection sampling (k distinct sorted positions in one O(L) pass)
+// and stream the new sequences into scratch rows; the host side copies them back into the arena.
+#include "hip_common.h"
+
+namespace msd {
+
+constexpr uint64_t kApplyStream = 0x6A09E667F3BCC909ull;
+
+__device__ __forceinline__ uint8_t rand_nt(Philox& rng) {
+  const char nts[4] = {'A', 'C', 'T', 'G'};
+  return (uint8_t)nts[rng.below(4)];
+}
+
+// k[i] ~ Poisson(p * len(row_i))
+__global__ void __launch_bounds__(256) mut_count_kernel(int n, const int64_t* rows, const int32_t* lens, double p,
+                                                        uint64_t seed, uint64_t call, int32_t* k) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = rows ? rows[i] : i;
+  const int L = lens[r];
+  if (L < 1) {
+    k[i] = 0;
+    return;
+  }
+  Philox rng(seed, call, (uint32_t)i);
+  long long kk = poisson(rng, p * (double)L);
+  k[i] = (int32_t)(kk > L ? L : kk);
+}
+
+// Mutated copy of genome `rows[sel[j]]` into scratch row j.
+__global__ void __launch_bounds__(64) mut_apply_kernel(int nsel, const int64_t* sel, const int64_t* rows,
+                                                       const uint8_t* arena, int width, const int32_t* lens,
+                                                       const int32_t* k, double p_indel, double p_del, uint64_t seed,
+                                                       uint64_t call, uint8_t* out, int out_width, int32_t* out_len) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nsel) return;
+  const int64_t i = sel[j];
+  const int64_t r = rows ? rows[i] : i;
+  const uint8_t* s = arena + (size_t)r * width;
+  const int L = lens[r];
+  int need = k[i];
+  Philox rng(seed, call ^ kApplyStream, (uint32_t)i);
+  uint8_t* o = out + (size_t)j * out_width;
+  int w = 0;
+  for (int t = 0; t < L; ++t) {
+    const uint8_t ch = s[t];
+    // selection sampling: position t is chosen with chance need / (L - t)
+    if (need > 0 && rng.below((uint32_t)(L - t)) < (uint32_t)need) {
+      --need;
+      if (rng.uniform_d() < p_indel) {
+        if (rng.uniform_d() < p_del) continue;  // deletion
+        if (w < out_width) o[w++] = rand_nt(rng);  // insertion before the current nucleotide
+        if (w < out_width) o[w++] = ch;
+      } else {
+        if (w < out_width) o[w++] = rand_nt(rng);  // substitution (may repeat the old nucleotide)
+      }
+    } else {
+      if (w < out_width) o[w++] = ch;
+    }
+  }
+  out_len[j] = w;
+}
+
+// k[i] ~ Poisson(p * (len(a) + len(b))) for neighbour pair i
+__global__ void __launch_bounds__(256) rec_count_kernel(int n, const int32_t* pairs, const int32_t* lens, double p,
+                                                        uint64_t seed, uint64_t call, int32_t* k) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int nb = lens[pairs[2 * i]] + lens[pairs[2 * i + 1]];
+  if (nb < 1) {
+    k[i] = 0;
+    return;
+  }
+  Philox rng(seed, call, (uint32_t)i);
+  long long kk = poisson(rng, p * (double)nb);
+  k[i] = (int32_t)(kk > nb ? nb : kk);
+}
+
+// Recombine pair sel[j]: cut both strands at k[.] sorted positions, shuffle the k+2 parts and split
+// them at a random index into two new genomes (scratch rows 2j and 2j+1). `parts` holds 3 ints per
+// part and up to (len(a) + len(b) + 2) parts per selected pair.
+__global__ void __launch_bounds__(64) rec_apply_kernel(int nsel, const int64_t* sel, const int32_t* pairs,
+                                                       const uint8_t* arena, int width, const int32_t* lens,
+                                                       const int32_t* k, uint64_t seed, uint64_t call, int32_t* parts,
+                                                       int parts_cap, uint8_t* out, int out_width, int32_t* out_len) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nsel) return;
+  const int64_t i = sel[j];
+  const int ca = pairs[2 * i], cb = pairs[2 * i + 1];
+  const int n0 = lens[ca], n1 = lens[cb], nb = n0 + n1;
+  int need = k[i];
+  Philox rng(seed, call ^ kApplyStream, (uint32_t)i);
+  int32_t* pt = parts + (size_t)j * parts_cap * 3;
+  int np = 0, start = 0, src = 0;
+  for (int t = 0; t < nb; ++t) {
+    if (t == n0) {  // close the last part of strand a
+      pt[3 * np] = 0; pt[3 * np + 1] = start; pt[3 * np + 2] = n0; ++np;
+      start = 0;
+      src = 1;
+    }
+    if (need > 0 && rng.below((uint32_t)(nb - t)) < (uint32_t)need) {
+      --need;
+      const int pos = src == 0 ? t : t - n0;
+      pt[3 * np] = src; pt[3 * np + 1] = start; pt[3 * np + 2] = pos; ++np;
+      start = pos;
+    }
+  }
+  if (n0 == nb) {  // strand b empty: close strand a here
+    pt[3 * np] = 0; pt[3 * np + 1] = start; pt[3 * np + 2] = n0; ++np;
+    start = 0;
+  }
+  pt[3 * np] = 1; pt[3 * np + 1] = start; pt[3 * np + 2] = n1; ++np;
+  // Fisher-Yates shuffle of the parts
+  for (int q = np - 1; q > 0; --q) {
+    const int r = (int)rng.below((uint32_t)(q + 1));
+    for (int f = 0; f < 3; ++f) {
+      const int32_t tmp = pt[3 * q + f];
+      pt[3 * q + f] = pt[3 * r + f];
+      pt[3 * r + f] = tmp;
+    }
+  }
+  const int split = (int)rng.below((uint32_t)np);
+  const uint8_t* sa = arena + (size_t)ca * width;
+  const uint8_t* sb = arena + (size_t)cb * width;
+  uint8_t* o0 = out + (size_t)(2 * j) * out_width;
+  uint8_t* o1 = out + (size_t)(2 * j + 1) * out_width;
+  int w0 = 0, w1 = 0;
+  for (int q = 0; q < np; ++q) {
+    const uint8_t* s = pt[3 * q] == 0 ? sa : sb;
+    for (int t = pt[3 * q + 1]; t < pt[3 * q + 2]; ++t) {
+      if (q < split) {
+        if (w0 < out_width) o0[w0++] = s[t];
+      } else {
+        if (w1 < out_width) o1[w1++] = s[t];
+      }
+    }
+  }
+  out_len[2 * j] = w0;
+  out_len[2 * j + 1] = w1;
+}
+
+void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
+               uintptr_t stream) {
+  if (n <= 0) return;
+  mut_count_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, rows ? P_<int64_t>(rows) : nullptr, P_<int32_t>(lens), p,
+                                                         seed, call, P_<int32_t>(k));
+  MS_LAUNCH_CHECK();
+}
+
+void mut_apply(int nsel, uintptr_t sel, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t k,
+               double p_indel, double p_del, uint64_t seed, uint64_t call, uintptr_t out, int out_width,
+               uintptr_t out_len, uintptr_t stream) {
+  if (nsel <= 0) return;
+  mut_apply_kernel<<<cdiv(nsel, 64), 64, 0, S_(stream)>>>(nsel, P_<int64_t>(sel), rows ? P_<int64_t>(rows) : nullptr,
+                                                          P_<uint8_t>(arena), width, P_<int32_t>(lens), P_<int32_t>(k),
+                                                          p_indel, p_del, seed, call, P_<uint8_t>(out), out_width,
+                                                          P_<int32_t>(out_len));
+  MS_LAUNCH_CHECK();
+}
+
+void rec_count(int n, uintptr_t pairs, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
+               uintptr_t stream) {
+  if (n <= 0) return;
+  rec_count_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, P_<int32_t>(pairs), P_<int32_t>(lens), p, seed, call,
+                                                         P_<int32_t>(k));
+  MS_LAUNCH_CHECK();
+}
+
+void rec_apply(int nsel, uintptr_t sel, uintptr_t pairs, uintptr_t arena, int width, uintptr_t lens, uintptr_t k,
+               uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out, int out_width,
+               uintptr_t out_len, uintptr_t stream) {
+  if (nsel <= 0) return;
+  rec_apply_kernel<<<cdiv(nsel, 64), 64, 0, S_(stream)>>>(nsel, P_<int64_t>(sel), P_<int32_t>(pairs),
+                                                          P_<uint8_t>(arena), width, P_<int32_t>(lens), P_<int32_t>(k),
+                                                          seed, call, P_<int32_t>(parts), parts_cap, P_<uint8_t>(out),
+                                                          out_width, P_<int32_t>(out_len));
+  MS_LAUNCH_CHECK();
+}
+
+}  // namespace msd

@@ -1,0 +1,337 @@
+// gfx950 kernels for the world map and cell geometry:
+//   * diffusion: LDS-tiled 3x3 circular stencil per molecule plane with an optional fused
+//     pre-scale (a pending degrade_molecules), per-tile double partial sums of the mass before and
+//     after, a per-molecule reduction and a correction + clamp pass writing back in place
+//     (reference world.py:627-649 semantics);
+//   * permeation and degradation (world.py:651-678);
+//   * placement: random free-pixel claims (spawn / add / reposition) and neighbour candidate picks
+//     for division / movement (conflicts resolved by list priority on the host side);
+//   * neighbour pairs via a pixel -> cell index map (O(n) instead of the reference's O(n^2)).
+#include "hip_common.h"
+
+namespace msd {
+
+constexpr int kTW = 64;   // tile width  (y, contiguous)
+constexpr int kTH = 32;   // tile height (x)
+constexpr int kRows = 4;  // thread rows per block (block = kTW x kRows = 256 threads)
+
+__device__ __forceinline__ int wrap(int v, int S) { return v < 0 ? v + S : (v >= S ? v - S : v); }
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// grid: (ceil(S/kTW), ceil(S/kTH), m); out = b*x + a*sum(neighbours) on pre-scaled inputs.
+__global__ void __launch_bounds__(kTW* kRows) diffuse_stencil_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                                     const float* __restrict__ wa, const float* __restrict__ wb,
+                                                                     const float* __restrict__ scale, int S,
+                                                                     double* __restrict__ partials) {
+  __shared__ float tile[kTH + 2][kTW + 2 + 1];
+  __shared__ double red[2][kRows * kTW / 64];
+  const int mol = blockIdx.z;
+  const int y0 = blockIdx.x * kTW, x0 = blockIdx.y * kTH;
+  const size_t plane = (size_t)S * S;
+  const float* src = in + (size_t)mol * plane;
+  const float sc = scale ? scale[mol] : 1.0f;
+  const int tid = threadIdx.y * kTW + threadIdx.x;
+
+  for (int i = tid; i < (kTH + 2) * (kTW + 2); i += kTW * kRows) {
+    const int r = i / (kTW + 2), cc = i - r * (kTW + 2);
+    const int gx = wrap(x0 + r - 1, S), gy = wrap(y0 + cc - 1, S);
+    float v = 0.0f;
+    if (x0 + r - 1 < S + 1 && y0 + cc - 1 < S + 1) v = src[(size_t)gx * S + gy] * sc;
+    tile[r][cc] = v;
+  }
+  __syncthreads();
+
+  const float a = wa[mol], b = wb[mol];
+  double before = 0.0, after = 0.0;
+  const int ty = threadIdx.x, gy = y0 + ty;
+  float* dst = out + (size_t)mol * plane;
+  if (gy < S) {
+    for (int r = threadIdx.y; r < kTH; r += kRows) {
+      const int gx = x0 + r;
+      if (gx >= S) break;
+      const int lr = r + 1, lc = ty + 1;
+      const float c0 = tile[lr][lc];
+      const float ns = tile[lr - 1][lc - 1] + tile[lr - 1][lc] + tile[lr - 1][lc + 1] + tile[lr][lc - 1] +
+                       tile[lr][lc + 1] + tile[lr + 1][lc - 1] + tile[lr + 1][lc] + tile[lr + 1][lc + 1];
+      const float v = b * c0 + a * ns;
+      dst[(size_t)gx * S + gy] = v;
+      before += c0;
+      after += v;
+    }
+  }
+  before = wave_sum(before);
+  after = wave_sum(after);
+  const int wid = tid >> 6;
+  if ((tid & 63) == 0) {
+    red[0][wid] = before;
+    red[1][wid] = after;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double sb = 0.0, sa = 0.0;
+    for (int w = 0; w < kRows * kTW / 64; ++w) {
+      sb += red[0][w];
+      sa += red[1][w];
+    }
+    const size_t tiles = (size_t)gridDim.x * gridDim.y;
+    const size_t t = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    partials[((size_t)mol * tiles + t) * 2] = sb;
+    partials[((size_t)mol * tiles + t) * 2 + 1] = sa;
+  }
+}
+
+// one block per molecule: corr[mol] = (before - after) / S^2
+__global__ void __launch_bounds__(256) diffuse_reduce_kernel(const double* partials, int tiles, int S, float* corr,
+                                                             double* totals) {
+  __shared__ double sb[4], sa[4];
+  const int mol = blockIdx.x;
+  double b = 0.0, a = 0.0;
+  for (int t = threadIdx.x; t < tiles; t += blockDim.x) {
+    b += partials[((size_t)mol * tiles + t) * 2];
+    a += partials[((size_t)mol * tiles + t) * 2 + 1];
+  }
+  b = wave_sum(b);
+  a = wave_sum(a);
+  if ((threadIdx.x & 63) == 0) {
+    sb[threadIdx.x >> 6] = b;
+    sa[threadIdx.x >> 6] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tb = sb[0] + sb[1] + sb[2] + sb[3], ta = sa[0] + sa[1] + sa[2] + sa[3];
+    corr[mol] = (float)((tb - ta) / ((double)S * (double)S));
+    if (totals) {
+      totals[2 * mol] = tb;
+      totals[2 * mol + 1] = ta;
+    }
+  }
+}
+
+// map = max(tmp + corr[mol], 0), float4-vectorised over the (m, S*S) planes
+__global__ void __launch_bounds__(256) diffuse_correct_kernel(const float* __restrict__ tmp, float* __restrict__ map,
+                                                              const float* __restrict__ corr, long long plane, int m) {
+  const long long n4 = plane / 4;
+  const long long total = n4 * m;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int mol = (int)(i / n4);
+    const float c = corr[mol];
+    float4 v = reinterpret_cast<const float4*>(tmp)[i];
+    v.x = fmaxf(v.x + c, 0.0f);
+    v.y = fmaxf(v.y + c, 0.0f);
+    v.z = fmaxf(v.z + c, 0.0f);
+    v.w = fmaxf(v.w + c, 0.0f);
+    reinterpret_cast<float4*>(map)[i] = v;
+  }
+  // scalar tail when S*S is not a multiple of 4
+  const long long tail = plane - n4 * 4;
+  if (tail) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < tail * m; i += (long long)gridDim.x * blockDim.x) {
+      const int mol = (int)(i / tail);
+      const long long o = (long long)mol * plane + n4 * 4 + (i - (long long)mol * tail);
+      map[o] = fmaxf(tmp[o] + corr[mol], 0.0f);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) correct_scalar_kernel(const float* tmp, float* map, const float* corr, long long plane, int m) {
+  const long long total = plane * m;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    map[i] = fmaxf(tmp[i] + corr[i / plane], 0.0f);
+  }
+}
+
+// map *= f[mol] (standalone degradation of the map)
+__global__ void __launch_bounds__(256) scale_planes_kernel(float* map, const float* f, long long plane, int m) {
+  const long long total = plane * m;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
+    map[i] *= f[i / plane];
+}
+
+// exchange between cells and their pixels, one thread per (cell, molecule)
+__global__ void __launch_bounds__(256) permeate_kernel(int c, int m, int S, const int32_t* pos, const float* perm,
+                                                       float* cell_mols, float* map) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)c * m) return;
+  const int cell = (int)(t / m), i = (int)(t - (long long)cell * m);
+  const float p = perm[i];
+  if (p == 0.0f) return;
+  const size_t o = (size_t)i * S * S + (size_t)pos[2 * cell] * S + pos[2 * cell + 1];
+  const float xi = cell_mols[t], xe = map[o];
+  const float di = xi * p, de = xe * p;
+  cell_mols[t] = xi + (de - di);
+  map[o] = xe + (di - de);
+}
+
+// ---------------------------------------------------------------- placement
+// Claim k uniformly random free pixels by rejection: atomically set the pixel's byte in the
+// (4-byte padded) bool occupancy map; out[i] = pixel or -1 after `attempts` misses.
+__global__ void __launch_bounds__(256) claim_free_kernel(int k, long long n_pix, uint8_t* cell_map, uint64_t seed,
+                                                         uint64_t call, int attempts, long long* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k) return;
+  Philox rng(seed, call, (uint32_t)i);
+  long long got = -1;
+  for (int t = 0; t < attempts; ++t) {
+    const long long pix = (long long)rng.below64((uint64_t)n_pix);
+    if (cell_map[pix]) continue;
+    unsigned* word = reinterpret_cast<unsigned*>(cell_map + (pix & ~3ll));
+    const unsigned bit = 1u << (8 * (pix & 3));
+    const unsigned old = atomicOr(word, bit);
+    if (!(old & (0xFFu << (8 * (pix & 3))))) {
+      got = pix;
+      break;
+    }
+  }
+  out[i] = got;
+}
+
+// reference neighbour order: (w,n),(w,y),(w,s),(x,n),(x,s),(e,n),(e,y),(e,s); duplicates (tiny
+// maps) removed. Returns the count.
+__device__ __forceinline__ int moore(int x, int y, int S, long long* nb) {
+  const int e = x + 1 == S ? 0 : x + 1, w = x == 0 ? S - 1 : x - 1;
+  const int s = y + 1 == S ? 0 : y + 1, n = y == 0 ? S - 1 : y - 1;
+  const int xs[8] = {w, w, w, x, x, e, e, e}, ys[8] = {n, y, s, n, s, n, y, s};
+  int cnt = 0;
+  for (int k = 0; k < 8; ++k) {
+    const long long p = (long long)xs[k] * S + ys[k];
+    bool dup = false;
+    for (int q = 0; q < cnt; ++q) dup |= nb[q] == p;
+    if (!dup) nb[cnt++] = p;
+  }
+  return cnt;
+}
+
+// For each pending cell pick a uniformly random free Moore neighbour (cand = pixel) or report
+// that none is free (cand = -1).
+__global__ void __launch_bounds__(256) pick_neighbour_kernel(int k, const int64_t* cells, const int32_t* pos, int S,
+                                                             const uint8_t* cell_map, const uint8_t* pending,
+                                                             uint64_t seed, uint64_t call, long long* cand) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k) return;
+  if (!pending[i]) {
+    cand[i] = -1;
+    return;
+  }
+  const int c = (int)cells[i];
+  long long nb[8], fr[8];
+  const int cnt = moore(pos[2 * c], pos[2 * c + 1], S, nb);
+  int nf = 0;
+  for (int q = 0; q < cnt; ++q)
+    if (!cell_map[nb[q]]) fr[nf++] = nb[q];
+  if (nf == 0) {
+    cand[i] = -1;
+    return;
+  }
+  Philox rng(seed, call, (uint32_t)i);
+  cand[i] = fr[rng.below((uint32_t)nf)];
+}
+
+// ---------------------------------------------------------------- neighbours
+__global__ void __launch_bounds__(256) scatter_index_kernel(int c, const int32_t* pos, int S, int32_t* idx_map) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c) return;
+  idx_map[(size_t)pos[2 * i] * S + pos[2 * i + 1]] = i;
+}
+
+__global__ void __launch_bounds__(256) clear_index_kernel(int c, const int32_t* pos, int S, int32_t* idx_map) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c) return;
+  idx_map[(size_t)pos[2 * i] * S + pos[2 * i + 1]] = -1;
+}
+
+__global__ void __launch_bounds__(256) neighbor_pairs_kernel(int nf, const int64_t* from, const int32_t* pos, int S,
+                                                             const int32_t* idx_map, const uint8_t* in_from,
+                                                             const uint8_t* in_to, int* counter, int cap,
+                                                             int64_t* pairs) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nf) return;
+  const int c = (int)from[i];
+  long long nb[8];
+  const int cnt = moore(pos[2 * c], pos[2 * c + 1], S, nb);
+  for (int q = 0; q < cnt; ++q) {
+    const int o = idx_map[nb[q]];
+    if (o < 0 || o == c || !in_to[o]) continue;
+    if (in_from[o] && in_to[c] && o < c) continue;  // found from the other side
+    const int slot = atomicAdd(counter, 1);
+    if (slot < cap) pairs[slot] = c < o ? ((int64_t)c << 32) | o : ((int64_t)o << 32) | c;
+  }
+}
+
+// ---------------------------------------------------------------- host launchers
+void diffuse(int m, int S, uintptr_t map, uintptr_t tmp, uintptr_t wa, uintptr_t wb, uintptr_t scale,
+             uintptr_t partials, uintptr_t corr, uintptr_t totals, uintptr_t stream) {
+  if (m <= 0 || S <= 0) return;
+  hipStream_t st = S_(stream);
+  const dim3 grid(cdiv(S, kTW), cdiv(S, kTH), m), block(kTW, kRows);
+  diffuse_stencil_kernel<<<grid, block, 0, st>>>(P_<float>(map), P_<float>(tmp), P_<float>(wa), P_<float>(wb),
+                                                 scale ? P_<float>(scale) : nullptr, S, P_<double>(partials));
+  MS_LAUNCH_CHECK();
+  const int tiles = (int)(grid.x * grid.y);
+  diffuse_reduce_kernel<<<m, 256, 0, st>>>(P_<double>(partials), tiles, S, P_<float>(corr),
+                                           totals ? P_<double>(totals) : nullptr);
+  MS_LAUNCH_CHECK();
+  const long long plane = (long long)S * S;
+  const unsigned g = std::min<long long>(cdiv(plane * m / 4 + 1, 256), 4096);
+  if (plane % 4 == 0) diffuse_correct_kernel<<<g, 256, 0, st>>>(P_<float>(tmp), P_<float>(map), P_<float>(corr), plane, m);
+  else correct_scalar_kernel<<<g, 256, 0, st>>>(P_<float>(tmp), P_<float>(map), P_<float>(corr), plane, m);
+  MS_LAUNCH_CHECK();
+}
+
+size_t diffuse_partials_len(int m, int S) { return (size_t)cdiv(S, kTW) * cdiv(S, kTH) * m * 2; }
+
+void scale_planes(int m, long long plane, uintptr_t map, uintptr_t f, uintptr_t stream) {
+  if (m <= 0 || plane <= 0) return;
+  const unsigned g = std::min<long long>(cdiv(plane * m, 256), 4096);
+  scale_planes_kernel<<<g, 256, 0, S_(stream)>>>(P_<float>(map), P_<float>(f), plane, m);
+  MS_LAUNCH_CHECK();
+}
+
+void permeate(int c, int m, int S, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map, uintptr_t stream) {
+  if (c <= 0 || m <= 0) return;
+  permeate_kernel<<<cdiv((long long)c * m, 256), 256, 0, S_(stream)>>>(c, m, S, P_<int32_t>(pos), P_<float>(perm),
+                                                                       P_<float>(cell_mols), P_<float>(map));
+  MS_LAUNCH_CHECK();
+}
+
+void claim_free(int k, long long n_pix, uintptr_t cell_map, uint64_t seed, uint64_t call, int attempts, uintptr_t out,
+                uintptr_t stream) {
+  if (k <= 0) return;
+  claim_free_kernel<<<cdiv(k, 256), 256, 0, S_(stream)>>>(k, n_pix, P_<uint8_t>(cell_map), seed, call, attempts,
+                                                           P_<long long>(out));
+  MS_LAUNCH_CHECK();
+}
+
+void pick_neighbour(int k, uintptr_t cells, uintptr_t pos, int S, uintptr_t cell_map, uintptr_t pending, uint64_t seed,
+                    uint64_t call, uintptr_t cand, uintptr_t stream) {
+  if (k <= 0) return;
+  pick_neighbour_kernel<<<cdiv(k, 256), 256, 0, S_(stream)>>>(k, P_<int64_t>(cells), P_<int32_t>(pos), S,
+                                                               P_<uint8_t>(cell_map), P_<uint8_t>(pending), seed, call,
+                                                               P_<long long>(cand));
+  MS_LAUNCH_CHECK();
+}
+
+void index_map(int c, uintptr_t pos, int S, uintptr_t idx_map, bool clear, uintptr_t stream) {
+  if (c <= 0) return;
+  if (clear)
+    clear_index_kernel<<<cdiv(c, 256), 256, 0, S_(stream)>>>(c, P_<int32_t>(pos), S, P_<int32_t>(idx_map));
+  else
+    scatter_index_kernel<<<cdiv(c, 256), 256, 0, S_(stream)>>>(c, P_<int32_t>(pos), S, P_<int32_t>(idx_map));
+  MS_LAUNCH_CHECK();
+}
+
+void neighbor_pairs(int nf, uintptr_t from, uintptr_t pos, int S, uintptr_t idx_map, uintptr_t in_from, uintptr_t in_to,
+                    uintptr_t counter, int cap, uintptr_t pairs, uintptr_t stream) {
+  if (nf <= 0) return;
+  neighbor_pairs_kernel<<<cdiv(nf, 256), 256, 0, S_(stream)>>>(nf, P_<int64_t>(from), P_<int32_t>(pos), S,
+                                                               P_<int32_t>(idx_map), P_<uint8_t>(in_from),
+                                                               P_<uint8_t>(in_to), P_<int>(counter), cap,
+                                                               P_<int64_t>(pairs));
+  MS_LAUNCH_CHECK();
+}
+
+}  // namespace msd

@@ -161,14 +161,24 @@ class World:
             "cell_lifetimes": _Column(torch.zeros(0, dtype=torch.int32, device=dev)),
             "cell_divisions": _Column(torch.zeros(0, dtype=torch.int32, device=dev)),
         }
+        self.__dict__["_pending_scale"] = None
         self.cell_map = torch.zeros(map_size, map_size, dtype=torch.bool, device=dev)
         self.molecule_map = self._get_molecule_map(n=m, size=map_size, init=mol_map_init)
 
     # ------------------------------------------------------------------ public state
     def __getattr__(self, name):  # only reached for attributes not found normally
-        cols = self.__dict__.get("_cols")
+        d = self.__dict__
+        cols = d.get("_cols")
         if cols is not None and name in cols:
-            return cols[name].view(self.__dict__["n_cells"])
+            return cols[name].view(d["n_cells"])
+        if name == "molecule_map" and "_molmap" in d:
+            if d.get("_pending_scale") is not None:
+                from magicsoup_amd.ops import hip_ops
+
+                hip_ops.apply_pending_scale(self)
+            return d["_molmap"]
+        if name == "cell_map" and "_cell_map" in d:
+            return d["_cell_map"]
         raise AttributeError(name)
 
     def __setattr__(self, name, value):
@@ -179,6 +189,16 @@ class World:
             t = t.to(want).contiguous() if (t.dtype != want or not t.is_contiguous()) else t
             cols[name].adopt(t, int(t.size(0)))
             return
+        if name == "molecule_map":
+            t = torch.as_tensor(value, device=self.device)
+            if t.dtype != torch.float32 or not t.is_contiguous():
+                t = t.to(torch.float32).contiguous()
+            self.__dict__["_molmap"] = t
+            self.__dict__["_pending_scale"] = None
+            return
+        if name == "cell_map":
+            self._set_cell_map(value)
+            return
         if name == "cell_genomes":
             self._set_strings(self._genomes, list(value))
             return
@@ -186,6 +206,21 @@ class World:
             self._set_strings(self._labels, list(value))
             return
         super().__setattr__(name, value)
+
+    def _set_cell_map(self, value) -> None:
+        """Keep the occupancy map in a 4-byte aligned, 4-byte padded buffer (the placement kernels
+        claim pixels with 32-bit atomics); assigning copies into the existing buffer."""
+        t = torch.as_tensor(value, device=self.device).to(torch.bool)
+        cur = self.__dict__.get("_cell_map")
+        if cur is not None and cur.shape == t.shape:
+            if t.data_ptr() != cur.data_ptr():
+                cur.copy_(t)
+            return
+        n = t.numel()
+        buf = torch.zeros((n + 3) // 4 * 4 + 4, dtype=torch.bool, device=self.device)
+        view = buf[:n].view(t.shape)
+        view.copy_(t)
+        self.__dict__["_cell_map"] = view
 
     @property
     def cell_genomes(self) -> StringColumn:
@@ -541,8 +576,11 @@ class World:
         state["_cols"] = {k: c.view(n).cpu().clone() for k, c in self._cols.items()}
         state["_genomes"] = self._genomes.to_strings()
         state["_labels"] = self._labels.to_strings()
-        state["cell_map"] = self.cell_map.cpu()
-        state["molecule_map"] = self.molecule_map.cpu()
+        state["_molmap"] = self.molecule_map.cpu()
+        state["_cell_map"] = self.cell_map.cpu()
+        state["_pending_scale"] = None
+        for k in ("_hip_scratch", "_idx_map", "_diff_w", "_perm_t", "_degrade_t"):
+            state.pop(k, None)
         return state
 
     def __setstate__(self, state):
@@ -562,8 +600,9 @@ class World:
         self._labels.append_strings(labels)
         self.__dict__["_genome_col"] = StringColumn(self._genomes)
         self.__dict__["_label_col"] = StringColumn(self._labels)
-        self.__dict__["cell_map"] = state["cell_map"].to(dev)
-        self.__dict__["molecule_map"] = state["molecule_map"].to(dev)
+        cmap = self.__dict__.pop("_cell_map")
+        self.__dict__["_molmap"] = self.__dict__["_molmap"].to(dev)
+        self._set_cell_map(cmap.to(dev))
 
     def to(self, device: str) -> "World":
         """Move all state of this world to ``device`` (returns ``self``)."""

@@ -1,0 +1,420 @@
+"""Python side of the gfx950 kernels: buffer management and launches on the current HIP stream.
+
+Every function here requires the ``_hip`` extension (no eager-PyTorch fallback on a GPU); a few
+bookkeeping steps between kernels (sorting conflict candidates, index compaction) use stock tensor
+ops on the same stream.
+"""
+from __future__ import annotations
+
+import torch
+
+from magicsoup_amd.ops import native
+
+_SNAP = 5  # candidate states per cell per integration part (kinetics.py:819 has 4 increments)
+
+
+def _m():
+    return native.hip()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t: torch.Tensor | None) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+class Scratch:
+    """Grow-only named device buffers (one set per world / kinetics object)."""
+
+    def __init__(self):
+        self.bufs: dict[str, torch.Tensor] = {}
+
+    def get(self, name: str, numel: int, dtype, device, zero: bool = False) -> torch.Tensor:
+        t = self.bufs.get(name)
+        if t is None or t.numel() < numel or t.dtype != dtype or t.device != device:
+            t = torch.empty(max(numel, 1), dtype=dtype, device=device)
+            self.bufs[name] = t
+        v = t[:numel]
+        if zero:
+            v.zero_()
+        return v
+
+
+def _scratch(obj) -> Scratch:
+    sc = obj.__dict__.get("_hip_scratch")
+    if sc is None:
+        sc = Scratch()
+        obj.__dict__["_hip_scratch"] = sc
+    return sc
+
+
+def set_seed(seed: int) -> None:
+    _m().set_seed(int(seed) & 0xFFFFFFFFFFFFFFFF)
+
+
+def _rng() -> tuple[int, int]:
+    return _m().next_call()
+
+
+# ---------------------------------------------------------------------------- kinetics
+def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n_iters=4):
+    N = p["N"]
+    P, s = int(N.size(1)), int(N.size(2))
+    dev = N.device
+    sc = _scratch(kin)
+    snap_a = sc.get("snap_a", c * _SNAP * s, torch.float32, dev)
+    snap_b = sc.get("snap_b", c * _SNAP * s, torch.float32, dev)
+    masks = sc.get("masks", len(trims) + 1, torch.int32, dev)
+    overflow = sc.get("overflow", 1, torch.int32, dev)
+    if world is not None:
+        m = world.n_molecules
+        S = int(world.map_size)
+        cm, mm, pos = world.cell_molecules, world._molmap, world.cell_positions
+    else:
+        m, S, cm, mm, pos = 0, 0, None, None, None
+    _m().integrate(
+        c, P, s, m, S,
+        _p(N), _p(p["Nf"]), _p(p["Nb"]), _p(p["A"]),
+        _p(p["Kmr"]), _p(p["Kmf"]), _p(p["Kmb"]), _p(p["Vmax"]), _p(p["Ke"]),
+        _p(cm), _p(mm), _p(pos), _p(X_io),
+        _p(snap_a), _p(snap_b), _p(masks), _p(overflow),
+        [float(t) for t in trims], int(n_iters), _stream(),
+    )
+    return masks
+
+
+def integrate(X: torch.Tensor, p: dict, trims, n_iters: int) -> list[int]:
+    """Kinetics.integrate_signals on an explicit X (c, s) (in place)."""
+    c = int(X.size(0))
+    kin = _KinProxy(p)
+    masks = _launch_integrate(kin, p, c, X_io=X, trims=trims, n_iters=n_iters)
+    return [int(v) for v in masks[: len(trims)].tolist()]
+
+
+class _KinProxy:
+    """Scratch holder keyed on the parameter tensors' owner when only a dict is at hand."""
+
+    _cache: dict[int, Scratch] = {}
+
+    def __init__(self, p):
+        key = p["N"].device.index or 0
+        sc = self._cache.get(key)
+        if sc is None:
+            sc = self._cache[key] = Scratch()
+        self.__dict__["_hip_scratch"] = sc
+
+
+def enzymatic_activity(world) -> None:
+    """Fused gather -> 3-part integrate -> scatter over the world state (5 launches, no syncs)."""
+    from magicsoup_amd.ops.kinetics_ops import _canonical_params
+
+    kin = world.kinetics
+    p = _canonical_params(kin)
+    c = world.n_cells
+    if p["N"].size(0) < c:
+        raise ValueError("kinetics has fewer cell rows than the world")
+    _ensure_world_layout(world)
+    _launch_integrate(kin, p, c, world=world)
+
+
+def build_params(tokens, rows, luts, p, abs_temp: float, gas: float) -> None:
+    n, P, D = int(tokens.size(0)), int(tokens.size(1)), int(tokens.size(2))
+    Pt, s = int(p["N"].size(1)), int(p["N"].size(2))
+    _m().build_params(
+        n, P, D, Pt, s, _p(tokens), _p(rows),
+        _p(luts["vmax"]), luts["vmax"].numel(), _p(luts["km"]), luts["km"].numel(),
+        _p(luts["signs"]), luts["signs"].numel(), _p(luts["hills"]), luts["hills"].numel(),
+        _p(luts["react"]), _p(luts["trnsp"]), _p(luts["eff"]), int(luts["react"].size(0)),
+        _p(luts["energies"]), float(abs_temp), float(gas),
+        *(_p(p[k]) for k in ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke")),
+        _stream(),
+    )
+
+
+# ---------------------------------------------------------------------------- map physics
+def _ensure_world_layout(world) -> None:
+    """Canonical dtypes / contiguity of the tensors the kernels touch."""
+    cm = world.cell_molecules
+    if cm.dtype != torch.float32 or not cm.is_contiguous():
+        world.cell_molecules = cm.to(torch.float32).contiguous()
+    pos = world.cell_positions
+    if pos.dtype != torch.int32 or not pos.is_contiguous():
+        world.cell_positions = pos.to(torch.int32).contiguous()
+
+
+def diffuse(world) -> None:
+    mm = world._molmap
+    m, S = int(mm.size(0)), int(mm.size(1))
+    sc = _scratch(world)
+    dev = mm.device
+    tmp = sc.get("diff_tmp", mm.numel(), torch.float32, dev)
+    partials = sc.get("diff_partials", int(_m().diffuse_partials_len(m, S)), torch.float64, dev)
+    corr = sc.get("diff_corr", m, torch.float32, dev)
+    w = world.__dict__.get("_diff_w")
+    if w is None or w[0] != world._diffusion:
+        wa = torch.tensor([float(a) for a, _ in world._diffusion], dtype=torch.float32, device=dev)
+        wb = torch.tensor([float(b) for _, b in world._diffusion], dtype=torch.float32, device=dev)
+        w = (list(world._diffusion), wa, wb)
+        world.__dict__["_diff_w"] = w
+    scale = world.__dict__.get("_pending_scale")
+    _m().diffuse(m, S, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale), _p(partials), _p(corr), 0, _stream())
+    world.__dict__["_pending_scale"] = None
+
+
+def permeate(world) -> None:
+    mm = world.molecule_map
+    _ensure_world_layout(world)
+    dev = mm.device
+    perm = world.__dict__.get("_perm_t")
+    if perm is None or perm[0] != world._permeation:
+        perm = (list(world._permeation), torch.tensor(world._permeation, dtype=torch.float32, device=dev))
+        world.__dict__["_perm_t"] = perm
+    if not any(x != 0.0 for x in perm[0]):
+        return
+    _m().permeate(world.n_cells, world.n_molecules, int(world.map_size), _p(world.cell_positions), _p(perm[1]),
+                  _p(world.cell_molecules), _p(mm), _stream())
+
+
+def _degrade_factors(world) -> torch.Tensor:
+    dev = world._molmap.device
+    f = world.__dict__.get("_degrade_t")
+    if f is None or f[0] != world._mol_degrads:
+        f = (list(world._mol_degrads), torch.tensor(world._mol_degrads, dtype=torch.float32, device=dev))
+        world.__dict__["_degrade_t"] = f
+    return f[1]
+
+
+def degrade(world) -> None:
+    """Cells decay now; the map decay is deferred and fused into the next diffusion stencil
+    (or applied by :func:`apply_pending_scale` on any other access to ``molecule_map``)."""
+    f = _degrade_factors(world)
+    if world.n_cells > 0:
+        cm = world.cell_molecules
+        cm.mul_(f)
+    pend = world.__dict__.get("_pending_scale")
+    world.__dict__["_pending_scale"] = f.clone() if pend is None else pend * f
+
+
+def apply_pending_scale(world) -> None:
+    f = world.__dict__.get("_pending_scale")
+    if f is None:
+        return
+    mm = world.__dict__["_molmap"]
+    world.__dict__["_pending_scale"] = None
+    _m().scale_planes(int(mm.size(0)), int(mm.size(1)) * int(mm.size(2)), _p(mm), _p(f), _stream())
+
+
+# ---------------------------------------------------------------------------- placement
+def _cell_map_bytes(world) -> torch.Tensor:
+    cmap = world.cell_map
+    return cmap.view(torch.uint8).reshape(-1)
+
+
+def free_positions(world, k: int) -> torch.Tensor:
+    S = int(world.map_size)
+    n_pix = S * S
+    dev = world.cell_map.device
+    cmap = _cell_map_bytes(world)
+    out = torch.empty(k, dtype=torch.int64, device=dev)
+    seed, call = _rng()
+    _m().claim_free(k, n_pix, _p(cmap), seed, call, 64, _p(out), _stream())
+    got = out[out >= 0]
+    if got.numel() < k:
+        # crowded map: exact sampling of the remainder over the remaining free pixels
+        free = torch.nonzero(cmap[:n_pix] == 0).flatten()
+        need = min(k - int(got.numel()), int(free.numel()))
+        if need > 0:
+            extra = free[torch.randperm(free.numel(), device=dev)[:need]]
+            cmap[extra] = 1
+            got = torch.cat([got, extra])
+    return torch.stack([got // S, got % S], dim=1).to(torch.int32)
+
+
+def _place_rounds(world, cells: torch.Tensor, vacate: bool, max_rounds: int = 16):
+    """Priority-ordered parallel neighbour claims. Returns (winner cells, new pixels)."""
+    S = int(world.map_size)
+    dev = cells.device
+    k = int(cells.numel())
+    pos = world.cell_positions
+    _ensure_world_layout(world)
+    pos = world.cell_positions
+    cmap = _cell_map_bytes(world)
+    pending = torch.ones(k, dtype=torch.uint8, device=dev)
+    cand = torch.empty(k, dtype=torch.int64, device=dev)
+    win_cells, win_pix = [], []
+    order = torch.arange(k, device=dev)
+    for _ in range(max_rounds):
+        seed, call = _rng()
+        _m().pick_neighbour(k, _p(cells), _p(pos), S, _p(cmap), _p(pending), seed, call, _p(cand), _stream())
+        has = cand >= 0
+        # cells without any free neighbour give up (reference: they do not divide / move)
+        pending &= has.to(torch.uint8)
+        idx = torch.nonzero(has).flatten()
+        if idx.numel() == 0:
+            break
+        px = cand[idx]
+        # lowest list position wins each contested pixel
+        key = px * k + order[idx]
+        srt = torch.sort(key).values
+        first = torch.ones_like(srt, dtype=torch.bool)
+        first[1:] = (srt[1:] // k) != (srt[:-1] // k)
+        wins = srt[first] % k
+        wpix = cand[wins]
+        cmap[wpix] = 1
+        if vacate:
+            old = pos[cells[wins]].long()
+            cmap[old[:, 0] * S + old[:, 1]] = 0
+        pending[wins] = 0
+        win_cells.append(wins)
+        win_pix.append(wpix)
+        if not bool(pending.any()):
+            break
+    if not win_cells:
+        e = torch.zeros(0, dtype=torch.long, device=dev)
+        return e, torch.zeros(0, 2, dtype=torch.int32, device=dev)
+    wins = torch.cat(win_cells)
+    wpix = torch.cat(win_pix)
+    o = torch.argsort(wins)
+    wins, wpix = wins[o], wpix[o]
+    return cells[wins], torch.stack([wpix // S, wpix % S], dim=1).to(torch.int32)
+
+
+def divide_placement(world, idxs: torch.Tensor):
+    parents, cpos = _place_rounds(world, idxs.to(torch.int64).contiguous(), vacate=False)
+    return parents, cpos
+
+
+def move_placement(world, idxs: torch.Tensor):
+    return _place_rounds(world, idxs.to(torch.int64).contiguous(), vacate=True)
+
+
+def split_cells(world, parents: torch.Tensor, children: torch.Tensor) -> None:
+    cm = world.cell_molecules
+    half = cm[parents] * 0.5
+    cm[parents] = half
+    cm[children] = half
+    dv = world.cell_divisions
+    d = dv[parents] + 1
+    dv[parents] = d
+    dv[children] = d
+    lt = world.cell_lifetimes
+    lt[parents] = 0
+    lt[children] = 0
+
+
+def neighbors(world, frm: torch.Tensor, to: torch.Tensor) -> torch.Tensor:
+    S = int(world.map_size)
+    dev = world.cell_map.device
+    _ensure_world_layout(world)
+    n = world.n_cells
+    pos = world.cell_positions
+    sc = _scratch(world)
+    idx_map = world.__dict__.get("_idx_map")
+    if idx_map is None or idx_map.numel() != S * S:
+        idx_map = torch.full((S * S,), -1, dtype=torch.int32, device=dev)
+        world.__dict__["_idx_map"] = idx_map
+    _m().index_map(n, _p(pos), S, _p(idx_map), False, _stream())
+    in_from = sc.get("nb_from", n, torch.uint8, dev, zero=True)
+    in_to = sc.get("nb_to", n, torch.uint8, dev, zero=True)
+    in_from[frm] = 1
+    in_to[to] = 1
+    frm64 = frm.to(torch.int64).contiguous()
+    cap = 8 * int(frm64.numel())
+    pairs = sc.get("nb_pairs", cap, torch.int64, dev)
+    counter = sc.get("nb_count", 1, torch.int32, dev, zero=True)
+    _m().neighbor_pairs(int(frm64.numel()), _p(frm64), _p(pos), S, _p(idx_map), _p(in_from), _p(in_to),
+                        _p(counter), cap, _p(pairs), _stream())
+    cnt = int(counter.item())
+    _m().index_map(n, _p(pos), S, _p(idx_map), True, _stream())  # leave the map all -1
+    keys = torch.sort(pairs[:cnt]).values
+    if keys.numel() > 1:
+        keys = torch.unique_consecutive(keys)
+    return torch.stack([keys >> 32, keys & 0xFFFFFFFF], dim=1).to(torch.int32)
+
+
+# ---------------------------------------------------------------------------- genomes
+def translate(genetics, data: torch.Tensor, lens: torch.Tensor, rows: torch.Tensor):
+    dev = data.device
+    n = int(rows.numel())
+    luts = genetics.device_luts(dev)
+    st = genetics.__dict__.get("_lut_lists")
+    tables = genetics.tables
+    if st is None or st[0] is not tables:
+        a, b, c, _, _ = tables.luts()
+        st = (tables, list(bytes(a)), list(bytes(b)), list(bytes(c)))
+        genetics.__dict__["_lut_lists"] = st
+    rows64 = rows.to(torch.int64).contiguous()
+    width = int(data.size(1))
+    counts = torch.empty(2 * n, dtype=torch.int32, device=dev)
+    ndom = torch.empty(2 * n, dtype=torch.int32, device=dev)
+    args = (_p(luts["dom_type"]), _p(luts["two_codon"]), tables.dom_size, tables.dom_type_size)
+    _m().translate_count(n, _p(rows64), _p(data), width, _p(lens), st[1], st[2], st[3], *args,
+                         _p(counts), _p(ndom), _stream())
+    per = counts.view(n, 2).sum(1)
+    PD = torch.stack([per.max(), ndom.max()]).tolist() if n else [0, 0]
+    P, D = max(int(PD[0]), 1), max(int(PD[1]), 1)
+    tokens = torch.zeros(n, P, D, 5, dtype=torch.int32, device=dev)
+    _m().translate_write(n, _p(rows64), _p(data), width, _p(lens), st[1], st[2], st[3], *args,
+                         _p(counts), P, D, _p(tokens), _stream())
+    return tokens, per
+
+
+def point_mutations(world, rows, p: float, p_indel: float, p_del: float) -> torch.Tensor:
+    arena = world._genomes
+    dev = arena.data.device
+    n = arena.n if rows is None else int(rows.numel())
+    if n == 0:
+        return torch.zeros(0, dtype=torch.long, device=dev)
+    rows64 = None if rows is None else rows.to(torch.int64).contiguous()
+    k = torch.empty(n, dtype=torch.int32, device=dev)
+    seed, call = _rng()
+    _m().mut_count(n, _p(rows64), _p(arena.lens), float(p), seed, call, _p(k), _stream())
+    sel = torch.nonzero(k > 0).flatten()
+    nsel = int(sel.numel())
+    if nsel == 0:
+        return torch.zeros(0, dtype=torch.long, device=dev)
+    tgt = sel if rows64 is None else rows64[sel]
+    bound = int((arena.lens[tgt] + k[sel]).max().item())
+    out_w = max(bound, 1)
+    out = torch.zeros(nsel, out_w, dtype=torch.uint8, device=dev)
+    out_len = torch.empty(nsel, dtype=torch.int32, device=dev)
+    _m().mut_apply(nsel, _p(sel), _p(rows64), _p(arena.data), int(arena.data.size(1)), _p(arena.lens), _p(k),
+                   float(p_indel), float(p_del), seed, call, _p(out), out_w, _p(out_len), _stream())
+    arena.set_rows(tgt, out, out_len)
+    return tgt
+
+
+def recombinations(world, pairs: torch.Tensor, p: float) -> torch.Tensor:
+    arena = world._genomes
+    dev = arena.data.device
+    pairs = pairs.to(torch.int32).contiguous()
+    n = int(pairs.size(0))
+    k = torch.empty(n, dtype=torch.int32, device=dev)
+    seed, call = _rng()
+    _m().rec_count(n, _p(pairs), _p(arena.lens), float(p), seed, call, _p(k), _stream())
+    sel = torch.nonzero(k > 0).flatten()
+    nsel = int(sel.numel())
+    if nsel == 0:
+        return torch.zeros(0, dtype=torch.long, device=dev)
+    sp = pairs[sel].long()
+    tot = arena.lens[sp[:, 0]] + arena.lens[sp[:, 1]]
+    mx = torch.stack([tot.max(), k[sel].max()]).tolist()
+    out_w, parts_cap = max(int(mx[0]), 1), int(mx[1]) + 2
+    out = torch.zeros(2 * nsel, out_w, dtype=torch.uint8, device=dev)
+    out_len = torch.empty(2 * nsel, dtype=torch.int32, device=dev)
+    parts = torch.empty(nsel * parts_cap * 3, dtype=torch.int32, device=dev)
+    _m().rec_apply(nsel, _p(sel), _p(pairs), _p(arena.data), int(arena.data.size(1)), _p(arena.lens), _p(k),
+                   seed, call, _p(parts), parts_cap, _p(out), out_w, _p(out_len), _stream())
+    cells = sp.reshape(-1)  # (a0, b0, a1, b1, ...) matches the scratch row order
+    # the last recombination that touched a cell wins (reference update order)
+    order = torch.arange(cells.numel(), device=dev)
+    key = cells * cells.numel() + order
+    srt = torch.sort(key).values
+    last = torch.ones_like(srt, dtype=torch.bool)
+    last[:-1] = (srt[:-1] // cells.numel()) != (srt[1:] // cells.numel())
+    pick = srt[last] % cells.numel()
+    tgt = cells[pick]
+    arena.set_rows(tgt, out[pick], out_len[pick])
+    return tgt

@@ -1,0 +1,29 @@
+#!/bin/bash
+# GPU-box check: tests, smoke, benches. Each GPU step has its own time limit; a crash, abort or
+# timeout (exit 124/134/137/139) ends the script without starting further GPU work.
+# usage: scripts/gpu_check.sh [tests|bench|all] [extra bench args...]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export PYTHONPATH="$PWD:${PYTHONPATH:-}"
+what="${1:-all}"; shift || true
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+run() {  # run <name> <seconds> <cmd...>
+  local name="$1" secs="$2"; shift 2
+  echo "== $name" | tee -a gpurun_out/summary.log
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc" | tee -a gpurun_out/summary.log
+  tail -5 "gpurun_out/$name.log" | tee -a gpurun_out/summary.log
+  if fatal $rc; then echo "fatal rc=$rc in $name, stopping" | tee -a gpurun_out/summary.log; exit $rc; fi
+  return 0
+}
+python -c "import __graft_entry__ as g; g.build()" || exit 1
+if [[ "$what" == tests || "$what" == all ]]; then
+  run pytest_gpu 900 python -m pytest tests -m gpu -q -x
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [[ "$what" == bench || "$what" == all ]]; then
+  run bench_256_40k 600 python bench.py --map-size 256 --cells 40000 --steps 20 --warmup 5 --profile-phases "$@"
+  run bench_4096_50k 600 python bench.py --steps 20 --warmup 5 --profile-phases "$@"
+fi

@@ -1,0 +1,222 @@
+"""Numerics of the gfx950 kernels against fp32 PyTorch / host references (GPU only)."""
+import copy
+
+import pytest
+import torch
+
+import magicsoup_amd as ms
+from magicsoup_amd.examples.wood_ljungdahl import CHEMISTRY
+from magicsoup_amd.ops import native
+from tests.conftest import gen_genomes
+
+pytestmark = pytest.mark.gpu
+
+
+def _world(device, map_size=64, n=300, s=500, seed=1):
+    ms.set_seed(seed)
+    torch.manual_seed(seed)
+    w = ms.World(chemistry=CHEMISTRY, map_size=map_size, device=device, seed=seed)
+    if n:
+        w.spawn_cells(gen_genomes(n, s))
+    return w
+
+
+def test_extension_is_gfx950():
+    assert native.hip().device_arch().startswith("gfx950")
+
+
+def test_translation_matches_host():
+    genetics = ms.Genetics()
+    genomes = gen_genomes(500, 800) + ["", "ATG", ms.random_genome(30)]
+    from magicsoup_amd.models.strings import pack_strings
+
+    arr, lens = pack_strings(genomes)
+    tok_h, np_h = genetics.tables.translate_tokens(arr, lens)
+    from magicsoup_amd.ops import hip_ops
+
+    data = torch.from_numpy(arr).cuda()
+    ln = torch.from_numpy(lens).cuda()
+    rows = torch.arange(len(genomes), device="cuda")
+    tok_d, np_d = hip_ops.translate(genetics, data, ln, rows)
+    assert torch.equal(np_d.cpu(), torch.as_tensor(np_h))
+    assert torch.equal(tok_d.cpu(), torch.as_tensor(tok_h))
+
+
+def _copy_world_cpu_to_gpu(wc):
+    wg = copy.deepcopy(wc)
+    return wg.to("cuda")
+
+
+def test_param_build_matches_host():
+    wc = _world("cpu", n=200)
+    rows = torch.arange(wc.n_cells)
+    data, lens = wc._genomes.view()
+    from magicsoup_amd.ops import world_ops, hip_ops, kinetics_ops
+
+    tokens, nprot = world_ops.translate(wc, data, lens, rows)
+    wg = _copy_world_cpu_to_gpu(wc)
+    kg = wg.kinetics
+    for name in ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke"):
+        getattr(kg, name).zero_()
+    full = nprot > 0
+    kinetics_ops.build_params(kg, rows[full].int(), tokens[full].cuda())
+    kc = wc.kinetics
+    for name in ("N", "Nf", "Nb", "A"):
+        assert torch.equal(getattr(kg, name).cpu()[full], getattr(kc, name)[full]), name
+    for name in ("Kmr", "Kmf", "Kmb", "Vmax", "Ke"):
+        a, b = getattr(kg, name).cpu()[full], getattr(kc, name)[full]
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-30, equal_nan=True), name
+
+
+@pytest.mark.parametrize("n_iters", [0, 4])
+def test_integrator_matches_torch_oracle(n_iters):
+    w = _world("cuda", n=400)
+    kin = w.kinetics
+    pos = w.cell_positions.long()
+    X = torch.cat([w.cell_molecules, w.molecule_map[:, pos[:, 0], pos[:, 1]].T], dim=1).contiguous()
+
+    from magicsoup_amd.ops import kinetics_ops
+
+    # torch oracle (stage-by-stage reference semantics)
+    Xr = X.clone()
+    for trim in (0.7, 0.2, 0.1):
+        V = kin._get_velocities(X=Xr, Vmax=(kin.Vmax * trim).clamp(0.0))
+        NV = kin.N.float() * V.unsqueeze(2)
+        NVa = kin._get_negative_adjusted_nv(NV=NV, X=Xr)
+        X1 = (Xr + NVa.sum(1)).clamp(min=0.0)
+        Xr = kin._get_equilibrium_adjusted_x(X0=Xr, X1=X1, NV=NVa, V=V) if n_iters else X1
+    Xk = X.clone()
+    kinetics_ops.integrate(kin, Xk, trims=(0.7, 0.2, 0.1), n_iters=n_iters)
+    assert torch.isfinite(Xk).all()
+    assert (Xk >= 0).all()
+    assert torch.allclose(Xk, Xr, rtol=1e-3, atol=1e-3)
+
+
+def test_integrator_matches_host_core():
+    wc = _world("cpu", n=300)
+    wg = _copy_world_cpu_to_gpu(wc)
+    pos = wc.cell_positions.long()
+    X = torch.cat([wc.cell_molecules, wc.molecule_map[:, pos[:, 0], pos[:, 1]].T], dim=1).contiguous()
+    Xc = wc.kinetics.integrate_signals(X)
+    Xg = wg.kinetics.integrate_signals(X.cuda()).cpu()
+    assert torch.allclose(Xg, Xc, rtol=1e-4, atol=1e-4)
+    assert wg.kinetics.last_masks == wc.kinetics.last_masks
+
+
+def test_enzymatic_activity_matches_host():
+    wc = _world("cpu", n=300)
+    wg = _copy_world_cpu_to_gpu(wc)
+    wc.enzymatic_activity()
+    wg.enzymatic_activity()
+    assert torch.allclose(wg.cell_molecules.cpu(), wc.cell_molecules, rtol=1e-4, atol=1e-4)
+    assert torch.allclose(wg.molecule_map.cpu(), wc.molecule_map, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("size", [5, 67, 256])
+def test_diffusion_matches_host(size):
+    wc = _world("cpu", map_size=size, n=0)
+    wg = _copy_world_cpu_to_gpu(wc)
+    wc.degrade_molecules()
+    wc.diffuse_molecules()
+    wg.degrade_molecules()
+    wg.diffuse_molecules()
+    assert torch.allclose(wg.molecule_map.cpu(), wc.molecule_map, rtol=1e-5, atol=1e-5)
+
+
+def test_diffusion_conserves_mass():
+    w = _world("cuda", map_size=512, n=0)
+    before = w.molecule_map.double().sum(dim=[1, 2])
+    for _ in range(10):
+        w.diffuse_molecules()
+    after = w.molecule_map.double().sum(dim=[1, 2])
+    assert torch.all((after - before).abs() / before < 1e-5)
+
+
+def test_permeation_matches_host():
+    wc = _world("cpu", n=300)
+    wg = _copy_world_cpu_to_gpu(wc)
+    from magicsoup_amd.ops import world_ops
+
+    world_ops.permeate(wc)
+    world_ops.permeate(wg)
+    assert torch.allclose(wg.cell_molecules.cpu(), wc.cell_molecules, rtol=1e-6, atol=1e-6)
+    assert torch.allclose(wg.molecule_map.cpu(), wc.molecule_map, rtol=1e-6, atol=1e-6)
+
+
+def test_neighbors_match_host():
+    wc = _world("cpu", map_size=32, n=600)
+    wg = _copy_world_cpu_to_gpu(wc)
+    idx = list(range(0, wc.n_cells, 2))
+    a = set(wc.get_neighbors(idx))
+    b = set(wg.get_neighbors(idx))
+    assert a == b
+    a = set(wc.get_neighbors(idx, nghbr_idxs=list(range(wc.n_cells))))
+    b = set(wg.get_neighbors(idx, nghbr_idxs=list(range(wc.n_cells))))
+    assert a == b
+
+
+def _check_invariants(w):
+    n = w.n_cells
+    assert int(w.cell_map.sum().item()) == n
+    pos = w.cell_positions.long()
+    keys = pos[:, 0] * w.map_size + pos[:, 1]
+    assert keys.unique().numel() == n
+    assert bool(w.cell_map[pos[:, 0], pos[:, 1]].all())
+    assert len(w.cell_genomes) == n and len(w.cell_labels) == n
+    assert w.kinetics.N.size(0) == n
+
+
+def test_world_lifecycle_on_gpu():
+    w = _world("cuda", map_size=64, n=1000)
+    _check_invariants(w)
+    total0 = w.molecule_map.double().sum(dim=[1, 2]) + w.cell_molecules.double().sum(0)
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    for _ in range(5):
+        w.enzymatic_activity()
+        kill = torch.argwhere(w.cell_molecules[:, atp] < 1.0).flatten()
+        w.kill_cells(kill)
+        _check_invariants(w)
+        repl = torch.argwhere(w.cell_molecules[:, atp] > 5.0).flatten()
+        w.cell_molecules[repl, atp] -= 4.0
+        w.divide_cells(repl)
+        _check_invariants(w)
+        w.recombinate_cells(p=1e-4)
+        w.mutate_cells(p=1e-4)
+        w.degrade_molecules()
+        w.diffuse_molecules()
+        w.increment_cell_lifetimes()
+        w.move_cells()
+        _check_invariants(w)
+    assert torch.isfinite(w.molecule_map).all() and torch.isfinite(w.cell_molecules).all()
+    # re-translating every genome from scratch reproduces the incrementally maintained params
+    N = w.kinetics.N.clone()
+    w.update_cells([(g, i) for i, g in enumerate(w.cell_genomes)])
+    P = min(N.size(1), w.kinetics.N.size(1))
+    assert torch.equal(N[:, :P], w.kinetics.N[:, :P])
+    del total0
+
+
+def test_spawn_divide_kill_conserve_mass_on_gpu():
+    w = ms.World(chemistry=CHEMISTRY, map_size=128, device="cuda")
+    exp = w.molecule_map.double().sum(dim=[1, 2])
+    idxs = w.spawn_cells(gen_genomes(1000, 500))
+    got = w.molecule_map.double().sum(dim=[1, 2]) + w.cell_molecules.double().sum(0)
+    assert torch.all((got - exp).abs() < 1e-1)
+    pc = w.divide_cells(idxs)
+    got = w.molecule_map.double().sum(dim=[1, 2]) + w.cell_molecules.double().sum(0)
+    assert torch.all((got - exp).abs() < 1e-1)
+    w.kill_cells(idxs + [c for _, c in pc])
+    got = w.molecule_map.double().sum(dim=[1, 2]) + w.cell_molecules.double().sum(0)
+    assert torch.all((got - exp).abs() < 1e-1)
+    assert w.n_cells == 0
+
+
+def test_mutations_on_gpu_change_genomes():
+    w = _world("cuda", n=500, s=200)
+    before = list(w.cell_genomes)
+    w.mutate_cells(p=0.01)
+    after = list(w.cell_genomes)
+    changed = sum(a != b for a, b in zip(before, after))
+    assert changed > 300
+    w.mutate_cells(p=0.05, p_indel=1.0, p_del=1.0)
+    assert all(len(g) <= len(b) for g, b in zip(w.cell_genomes, after))
