@@ -5,7 +5,8 @@ BASELINE.json config: Wood-Ljungdahl chemistry, 4096x4096 map, random-normal mol
 random genomes, population topped up to >= 50,000 cells every step. One step:
 
     top up to N cells -> enzymatic_activity -> kill (ATP < 1) -> replicate (ATP > 5: ATP -= 4,
-    divide) -> recombinate_cells -> mutate_cells -> degrade -> diffuse -> increment lifetimes
+    divide) -> dilute back to N cells (random kills) -> recombinate_cells -> mutate_cells ->
+    degrade -> diffuse -> increment lifetimes
 
 Single GPU: one ``World`` on ``cuda:0``. N GPUs (``torchrun --nproc-per-node N``): one world,
 domain-decomposed over the ranks (``magicsoup_amd.parallel``; strong scaling of the fixed config).
@@ -78,6 +79,12 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None):
         repl = torch.nonzero(world.cell_molecules[:, atp] > 5.0).flatten()
         world.cell_molecules[repl, atp] -= 4.0
         world.divide_cells_t(repl)
+    with ph("dilute"):
+        # chemostat-style dilution keeps the population at the configured size (the reference loop
+        # only tops up; on a 4096^2 map the population would otherwise grow ~6x within 25 steps)
+        excess = world.n_cells - n_target
+        if excess > 0:
+            world.kill_cells(torch.randperm(world.n_cells, device=world.cell_molecules.device)[:excess])
     with ph("recombinate"):
         world.recombinate_cells()
     with ph("mutate"):

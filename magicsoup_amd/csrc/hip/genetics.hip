@@ -1,98 +1,259 @@
-// gfx950 genome translation over the device genome arena.
+// gfx950 genome translation over the device genome arena: one wavefront per genome.
 //
-// One thread per (genome, strand) runs the single-source scan of ms_common.h (the same code the
-// OpenMP host path runs): pass 1 counts proteins and domains, pass 2 writes dense tokens
-// (n, P, D, 5); reverse-strand proteins are placed after the forward-strand ones of their genome,
-// which reproduces the reference's protein order (rust/genetics.rs:151-175).
+// The sequential reference scan (rust/genetics.rs:13-123; single-source host version in
+// ms_common.h) is reformulated so that all 64 lanes work at once:
+//   1. lanes over positions: codon index of every position on both strands -> LDS;
+//   2. lanes over start codons: walk to the first in-frame stop; every CDS long enough goes into a
+//      per-strand list (LDS atomic append, order restored next);
+//   3. rank every CDS by (stop ascending, start descending) -- exactly the reference's emission
+//      order (a stop closes its frame's pending starts latest-first);
+//   4. lanes over CDSs in that order: domain extraction (count pass: #domains + "has a catalytic or
+//      transporter domain"; write pass: tokens at the protein's slot, from a wave prefix sum).
+// Forward-strand proteins precede reverse-strand ones (rust/genetics.rs:151-175).
 #include "hip_common.h"
 
 namespace msd {
 
-struct DevTables {
-  ms::TransTables t;
+constexpr int kGBlock = 256;  // 4 waves -> up to 4 genomes per workgroup
+constexpr int kLutBytes = 64 * 3 + 16 + 4096 * 2;
+
+struct TransArgs {
+  int n, width, gpb, cap, dt_entries;
+  bool stage_dt;
+  const int64_t* rows;
+  const uint8_t* arena;
+  const int32_t* lens;
+  const uint8_t *is_start, *is_stop, *one_codon, *dom_type;
+  const uint16_t* two_codon;
+  int dom_size, dom_type_size;
+  int32_t* nprot;   // (2n,) proteins per strand
+  int32_t* ndom;    // (2n,) max domains per strand (count pass)
+  int32_t* tokens;  // (n, P, D, 5) (write pass)
+  int P, D;
 };
 
-__global__ void __launch_bounds__(256) translate_count_kernel(int n, const int64_t* rows, const uint8_t* arena, int width,
-                                                              const int32_t* lens, DevTables T, int32_t* nprot,
-                                                              int32_t* ndom) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 2 * n) return;
-  const int g = t >> 1, strand = t & 1;
-  const int64_t r = rows[g];
-  const uint8_t* s = arena + (size_t)r * width;
-  const int L = lens[r];
-  ms::CountVisitor v;
-  if (strand == 0) {
-    ms::FwdSeq q{s};
-    ms::scan_strand(q, L, T.t, true, v);
-  } else {
-    ms::RevSeq q{s, L};
-    ms::scan_strand(q, L, T.t, false, v);
-  }
-  nprot[t] = v.n_prots;
-  ndom[t] = v.max_doms;
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-__global__ void __launch_bounds__(256) translate_write_kernel(int n, const int64_t* rows, const uint8_t* arena, int width,
-                                                              const int32_t* lens, DevTables T, const int32_t* nprot,
-                                                              int P, int D, int32_t* tokens) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 2 * n) return;
-  const int g = t >> 1, strand = t & 1;
-  const int64_t r = rows[g];
-  const uint8_t* s = arena + (size_t)r * width;
-  const int L = lens[r];
-  const int off = strand == 0 ? 0 : nprot[2 * g];
-  ms::TokenVisitor v{tokens + ((size_t)g * P + off) * D * 5, P - off, D};
-  if (strand == 0) {
-    ms::FwdSeq q{s};
-    ms::scan_strand(q, L, T.t, true, v);
-  } else {
-    ms::RevSeq q{s, L};
-    ms::scan_strand(q, L, T.t, false, v);
+template <bool kWrite>
+__global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint8_t* l_start = sm;
+  uint8_t* l_stop = sm + 64;
+  uint8_t* l_one = sm + 128;
+  const uint16_t* l_two = reinterpret_cast<const uint16_t*>(sm + 64 * 3 + 16);
+  uint8_t* l_dt = sm + kLutBytes;
+  const int dt_bytes = a.stage_dt ? ((a.dt_entries + 15) & ~15) : 0;
+  // per-wave slot: codons [2][width] bytes, CDS lists [2][cap] u32, emission order [2][cap] u16
+  const size_t slot_bytes = ((size_t)2 * a.width + (size_t)2 * a.cap * 6 + 16 + 15) & ~(size_t)15;
+  uint8_t* slot = sm + kLutBytes + dt_bytes + (size_t)wid * slot_bytes;
+  uint8_t* cod = slot;
+  uint32_t* cds = reinterpret_cast<uint32_t*>(slot + 2 * a.width);  // (q << 16) | p
+  uint16_t* order = reinterpret_cast<uint16_t*>(cds + 2 * a.cap);
+  int* counters = reinterpret_cast<int*>(order + 2 * a.cap);
+
+  for (int i = threadIdx.x; i < 64; i += blockDim.x) {
+    l_start[i] = a.is_start[i];
+    l_stop[i] = a.is_stop[i];
+    l_one[i] = a.one_codon[i];
+  }
+  for (int i = threadIdx.x; i < 4096 * 2 / 16; i += blockDim.x)
+    reinterpret_cast<uint4*>(sm + 64 * 3 + 16)[i] = reinterpret_cast<const uint4*>(a.two_codon)[i];
+  if (a.stage_dt)
+    for (int i = threadIdx.x; i < dt_bytes / 16; i += blockDim.x)
+      reinterpret_cast<uint4*>(l_dt)[i] = reinterpret_cast<const uint4*>(a.dom_type)[i];
+  const uint8_t* DT = a.stage_dt ? l_dt : a.dom_type;
+
+  const int g = blockIdx.x * a.gpb + wid;
+  const bool active = wid < a.gpb && g < a.n;
+  int L = 0;
+  const uint8_t* s = nullptr;
+  if (active) {
+    const int64_t r = a.rows[g];
+    L = a.lens[r];
+    s = a.arena + (size_t)r * a.width;
+    if (lane < 2) counters[lane] = 0;
+  }
+  __syncthreads();
+  if (!active) return;  // whole waves only; no block-wide barrier below
+
+  // ---- 1. codon index per position, both strands (0xFF past the end)
+  const int ncod = L - 2;
+  for (int i = lane; i < L; i += 64) {
+    uint8_t cf = 0xFF, cr = 0xFF;
+    if (i < ncod) {
+      cf = (uint8_t)((ms::nt_code(s[i]) << 4) | (ms::nt_code(s[i + 1]) << 2) | ms::nt_code(s[i + 2]));
+      // reverse-complement position i covers forward bases L-1-i, L-2-i, L-3-i
+      cr = (uint8_t)((ms::nt_comp(ms::nt_code(s[L - 1 - i])) << 4) |
+                     (ms::nt_comp(ms::nt_code(s[L - 2 - i])) << 2) | ms::nt_comp(ms::nt_code(s[L - 3 - i])));
+    }
+    cod[i] = cf;
+    cod[a.width + i] = cr;
+  }
+  wave_sync();
+
+  // ---- 2. CDS candidates: start codon -> first in-frame stop (too short / unstopped: dropped)
+  if (L >= a.dom_size && L >= 3) {
+    for (int st = 0; st < 2; ++st) {
+      const uint8_t* c = cod + st * a.width;
+      for (int p = lane; p < ncod; p += 64) {
+        if (!l_start[c[p]]) continue;
+        int q = p + 3;
+        while (q < ncod && !l_stop[c[q]]) q += 3;
+        if (q >= ncod || q + 3 - p < a.dom_size) continue;
+        const int k = atomicAdd(&counters[st], 1);
+        cds[st * a.cap + k] = ((uint32_t)q << 16) | (uint32_t)p;  // k < ncod <= cap
+      }
+    }
+  }
+  wave_sync();
+
+  // ---- 3. emission order: stop ascending, start descending
+  int ncds[2];
+  for (int st = 0; st < 2; ++st) {
+    ncds[st] = counters[st];
+    const uint32_t* lst = cds + st * a.cap;
+    for (int e = lane; e < ncds[st]; e += 64) {
+      const uint32_t ve = lst[e];
+      const uint32_t ke = (ve & 0xFFFF0000u) | (0xFFFFu - (ve & 0xFFFFu));
+      int rank = 0;
+      for (int f = 0; f < ncds[st]; ++f) {
+        const uint32_t vf = lst[f];
+        rank += ((vf & 0xFFFF0000u) | (0xFFFFu - (vf & 0xFFFFu))) < ke;
+      }
+      order[st * a.cap + rank] = (uint16_t)e;
+    }
+  }
+  wave_sync();
+
+  // ---- 4. domain extraction in emission order
+  const int ds = a.dom_size, dts = a.dom_type_size, ntc = dts / 3;
+  int prot_base = 0;  // forward-strand proteins come first
+  for (int st = 0; st < 2; ++st) {
+    const uint8_t* c = cod + st * a.width;
+    int n_prot = 0, max_dom = 0;
+    for (int e0 = 0; e0 < ncds[st]; e0 += 64) {
+      const int e = e0 + lane;
+      const bool have = e < ncds[st];
+      int p = 0, n = 0;
+      if (have) {
+        const uint32_t v = cds[st * a.cap + order[st * a.cap + e]];
+        p = (int)(v & 0xFFFFu);
+        n = (int)(v >> 16) + 3 - p;
+      }
+      int nd = 0;
+      bool useful = false;
+      for (int i = 0; i + ds <= n;) {
+        int idx = 0;
+        for (int t = 0; t < ntc; ++t) idx = (idx << 6) | c[p + i + 3 * t];
+        const int ty = DT[idx];
+        if (ty) {
+          useful |= ty != 3;
+          ++nd;
+          i += ds;
+        } else {
+          i += 3;
+        }
+      }
+      const unsigned long long bal = __ballot(useful);
+      const int rank = __popcll(bal & ((1ull << lane) - 1ull));
+      if constexpr (kWrite) {
+        const int slot_p = prot_base + n_prot + rank;
+        if (useful && slot_p < a.P) {
+          int32_t* tk = a.tokens + ((size_t)g * a.P + slot_p) * a.D * 5;
+          int d = 0;
+          for (int i = 0; i + ds <= n && d < a.D;) {
+            int idx = 0;
+            for (int t = 0; t < ntc; ++t) idx = (idx << 6) | c[p + i + 3 * t];
+            const int ty = DT[idx];
+            if (ty) {
+              const int o = p + i + dts;
+              int32_t* dm = tk + d * 5;
+              dm[0] = ty;
+              dm[1] = l_one[c[o]];
+              dm[2] = l_one[c[o + 3]];
+              dm[3] = l_one[c[o + 6]];
+              dm[4] = l_two[((int)c[o + 9] << 6) | c[o + 12]];
+              ++d;
+              i += ds;
+            } else {
+              i += 3;
+            }
+          }
+        }
+      } else {
+        if (useful && nd > max_dom) max_dom = nd;
+      }
+      n_prot += __popcll(bal);
+    }
+    if constexpr (!kWrite) {
+      for (int o = 32; o > 0; o >>= 1) max_dom = max(max_dom, __shfl_xor(max_dom, o));
+      if (lane == 0) {
+        a.nprot[2 * g + st] = n_prot;
+        a.ndom[2 * g + st] = max_dom;
+      }
+    }
+    prot_base += n_prot;
   }
 }
 
-static DevTables make_tables(const std::vector<uint8_t>& is_start, const std::vector<uint8_t>& is_stop,
-                             const std::vector<uint8_t>& one_codon, uintptr_t dom_type, uintptr_t two_codon,
-                             int dom_size, int dom_type_size) {
-  if (is_start.size() != 64 || is_stop.size() != 64 || one_codon.size() != 64)
-    throw std::invalid_argument("codon LUTs must have 64 entries");
-  DevTables T{};
-  for (int i = 0; i < 64; ++i) {
-    T.t.is_start[i] = is_start[i];
-    T.t.is_stop[i] = is_stop[i];
-    T.t.one_codon[i] = one_codon[i];
-  }
-  T.t.dom_type = P_<uint8_t>(dom_type);
-  T.t.two_codon = P_<uint16_t>(two_codon);
-  T.t.dom_size = dom_size;
-  T.t.dom_type_size = dom_type_size;
-  return T;
-}
-
-void translate_count(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, const std::vector<uint8_t>& st,
-                     const std::vector<uint8_t>& sp, const std::vector<uint8_t>& oc, uintptr_t dom_type,
-                     uintptr_t two_codon, int dom_size, int dom_type_size, uintptr_t nprot, uintptr_t ndom,
-                     uintptr_t stream) {
+static void launch(bool write, int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+                   uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
+                   uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t stream) {
   if (n <= 0) return;
-  DevTables T = make_tables(st, sp, oc, dom_type, two_codon, dom_size, dom_type_size);
-  translate_count_kernel<<<cdiv(2ll * n, 256), 256, 0, S_(stream)>>>(n, P_<int64_t>(rows), P_<uint8_t>(arena), width,
-                                                                     P_<int32_t>(lens), T, P_<int32_t>(nprot),
-                                                                     P_<int32_t>(ndom));
+  if (width % 16 != 0) throw std::invalid_argument("genome arena width must be a multiple of 16");
+  if (width > 65535) throw std::invalid_argument("genomes longer than 65535 nt are not supported on the GPU");
+  TransArgs a{};
+  a.n = n;
+  a.width = width;
+  a.dt_entries = dt_entries;
+  a.rows = P_<int64_t>(rows);
+  a.arena = P_<uint8_t>(arena);
+  a.lens = P_<int32_t>(lens);
+  const uint8_t* l = P_<uint8_t>(luts);  // is_start | is_stop | one_codon (64 bytes each)
+  a.is_start = l;
+  a.is_stop = l + 64;
+  a.one_codon = l + 128;
+  a.dom_type = P_<uint8_t>(dom_type);
+  a.two_codon = P_<uint16_t>(two_codon);
+  a.dom_size = dom_size;
+  a.dom_type_size = dom_type_size;
+  a.nprot = P_<int32_t>(nprot);
+  a.ndom = P_<int32_t>(ndom);
+  a.tokens = P_<int32_t>(tokens);
+  a.P = P;
+  a.D = D;
+  a.stage_dt = dt_entries <= 4096;
+  a.cap = width;  // a strand has at most one CDS per codon position (< width)
+  const size_t fixed = kLutBytes + (a.stage_dt ? ((dt_entries + 15) & ~15) : 0);
+  const size_t slot = ((size_t)2 * width + (size_t)2 * a.cap * 6 + 16 + 15) & ~(size_t)15;
+  if (fixed + slot > 160 * 1024) throw std::invalid_argument("genome too long for the LDS-resident translation");
+  int gpb = kGBlock / 64;
+  while (gpb > 1 && fixed + gpb * slot > 64 * 1024) --gpb;
+  a.gpb = gpb;
+  const size_t lds = fixed + gpb * slot;
+  const unsigned grid = cdiv(n, gpb);
+  if (write) translate_kernel<true><<<grid, gpb * 64, lds, S_(stream)>>>(a);
+  else translate_kernel<false><<<grid, gpb * 64, lds, S_(stream)>>>(a);
   MS_LAUNCH_CHECK();
 }
 
-void translate_write(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, const std::vector<uint8_t>& st,
-                     const std::vector<uint8_t>& sp, const std::vector<uint8_t>& oc, uintptr_t dom_type,
-                     uintptr_t two_codon, int dom_size, int dom_type_size, uintptr_t nprot, int P, int D,
-                     uintptr_t tokens, uintptr_t stream) {
-  if (n <= 0) return;
-  DevTables T = make_tables(st, sp, oc, dom_type, two_codon, dom_size, dom_type_size);
-  translate_write_kernel<<<cdiv(2ll * n, 256), 256, 0, S_(stream)>>>(n, P_<int64_t>(rows), P_<uint8_t>(arena), width,
-                                                                     P_<int32_t>(lens), T, P_<int32_t>(nprot), P, D,
-                                                                     P_<int32_t>(tokens));
-  MS_LAUNCH_CHECK();
+void translate_count(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+                     uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
+                     uintptr_t nprot, uintptr_t ndom, uintptr_t stream) {
+  launch(false, n, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot,
+         ndom, 0, 0, 0, stream);
+}
+
+void translate_write(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+                     uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
+                     uintptr_t nprot, int P, int D, uintptr_t tokens, uintptr_t stream) {
+  launch(true, n, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot, 0,
+         P, D, tokens, stream);
 }
 
 }  // namespace msd

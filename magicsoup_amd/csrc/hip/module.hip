@@ -36,14 +36,12 @@ void index_map(int c, uintptr_t pos, int S, uintptr_t idx_map, bool clear, uintp
 void neighbor_pairs(int nf, uintptr_t from, uintptr_t pos, int S, uintptr_t idx_map, uintptr_t in_from, uintptr_t in_to,
                     uintptr_t counter, int cap, uintptr_t pairs, uintptr_t stream);
 // genetics.hip
-void translate_count(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, const std::vector<uint8_t>& st,
-                     const std::vector<uint8_t>& sp, const std::vector<uint8_t>& oc, uintptr_t dom_type,
-                     uintptr_t two_codon, int dom_size, int dom_type_size, uintptr_t nprot, uintptr_t ndom,
-                     uintptr_t stream);
-void translate_write(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, const std::vector<uint8_t>& st,
-                     const std::vector<uint8_t>& sp, const std::vector<uint8_t>& oc, uintptr_t dom_type,
-                     uintptr_t two_codon, int dom_size, int dom_type_size, uintptr_t nprot, int P, int D,
-                     uintptr_t tokens, uintptr_t stream);
+void translate_count(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+                     uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
+                     uintptr_t nprot, uintptr_t ndom, uintptr_t stream);
+void translate_write(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+                     uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
+                     uintptr_t nprot, int P, int D, uintptr_t tokens, uintptr_t stream);
 // mutations.hip
 void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
                uintptr_t stream);

@@ -11,6 +11,31 @@ namespace msd {
 
 constexpr uint64_t kApplyStream = 0x6A09E667F3BCC909ull;
 
+constexpr int kFloydMax = 32;
+
+// k distinct sorted positions in [0, n): Floyd's algorithm + insertion sort (k <= kFloydMax).
+__device__ __forceinline__ void floyd_sorted(Philox& rng, int n, int k, int* pos) {
+  int cnt = 0;
+  for (int j = n - k; j < n; ++j) {
+    int t = (int)rng.below((uint32_t)(j + 1));
+    for (int q = 0; q < cnt; ++q)
+      if (pos[q] == t) {
+        t = j;
+        break;
+      }
+    pos[cnt++] = t;
+  }
+  for (int a = 1; a < cnt; ++a) {
+    const int v = pos[a];
+    int b = a - 1;
+    while (b >= 0 && pos[b] > v) {
+      pos[b + 1] = pos[b];
+      --b;
+    }
+    pos[b + 1] = v;
+  }
+}
+
 __device__ __forceinline__ uint8_t rand_nt(Philox& rng) {
   const char nts[4] = {'A', 'C', 'T', 'G'};
   return (uint8_t)nts[rng.below(4)];
@@ -33,6 +58,17 @@ __global__ void __launch_bounds__(256) mut_count_kernel(int n, const int64_t* ro
 }
 
 // Mutated copy of genome `rows[sel[j]]` into scratch row j.
+__device__ __forceinline__ void mutate_at(Philox& rng, uint8_t ch, double p_indel, double p_del, uint8_t* o, int& w,
+                                          int cap) {
+  if (rng.uniform_d() < p_indel) {
+    if (rng.uniform_d() < p_del) return;         // deletion
+    if (w < cap) o[w++] = rand_nt(rng);         // insertion before the current nucleotide
+    if (w < cap) o[w++] = ch;
+  } else if (w < cap) {
+    o[w++] = rand_nt(rng);                      // substitution (may repeat the old nucleotide)
+  }
+}
+
 __global__ void __launch_bounds__(64) mut_apply_kernel(int nsel, const int64_t* sel, const int64_t* rows,
                                                        const uint8_t* arena, int width, const int32_t* lens,
                                                        const int32_t* k, double p_indel, double p_del, uint64_t seed,
@@ -43,24 +79,30 @@ __global__ void __launch_bounds__(64) mut_apply_kernel(int nsel, const int64_t* 
   const int64_t r = rows ? rows[i] : i;
   const uint8_t* s = arena + (size_t)r * width;
   const int L = lens[r];
-  int need = k[i];
+  const int kk = k[i];
   Philox rng(seed, call ^ kApplyStream, (uint32_t)i);
   uint8_t* o = out + (size_t)j * out_width;
   int w = 0;
-  for (int t = 0; t < L; ++t) {
-    const uint8_t ch = s[t];
-    // selection sampling: position t is chosen with chance need / (L - t)
-    if (need > 0 && rng.below((uint32_t)(L - t)) < (uint32_t)need) {
-      --need;
-      if (rng.uniform_d() < p_indel) {
-        if (rng.uniform_d() < p_del) continue;  // deletion
-        if (w < out_width) o[w++] = rand_nt(rng);  // insertion before the current nucleotide
-        if (w < out_width) o[w++] = ch;
-      } else {
-        if (w < out_width) o[w++] = rand_nt(rng);  // substitution (may repeat the old nucleotide)
+  if (kk <= kFloydMax) {
+    int pos[kFloydMax];
+    floyd_sorted(rng, L, kk, pos);
+    int prev = 0;
+    for (int q = 0; q < kk; ++q) {
+      for (int t = prev; t < pos[q] && w < out_width; ++t) o[w++] = s[t];
+      mutate_at(rng, s[pos[q]], p_indel, p_del, o, w, out_width);
+      prev = pos[q] + 1;
+    }
+    for (int t = prev; t < L && w < out_width; ++t) o[w++] = s[t];
+  } else {
+    int need = kk;
+    for (int t = 0; t < L; ++t) {
+      // selection sampling: position t is chosen with chance need / (L - t)
+      if (need > 0 && rng.below((uint32_t)(L - t)) < (uint32_t)need) {
+        --need;
+        mutate_at(rng, s[t], p_indel, p_del, o, w, out_width);
+      } else if (w < out_width) {
+        o[w++] = s[t];
       }
-    } else {
-      if (w < out_width) o[w++] = ch;
     }
   }
   out_len[j] = w;
@@ -96,25 +138,46 @@ __global__ void __launch_bounds__(64) rec_apply_kernel(int nsel, const int64_t* 
   int need = k[i];
   Philox rng(seed, call ^ kApplyStream, (uint32_t)i);
   int32_t* pt = parts + (size_t)j * parts_cap * 3;
-  int np = 0, start = 0, src = 0;
-  for (int t = 0; t < nb; ++t) {
-    if (t == n0) {  // close the last part of strand a
-      pt[3 * np] = 0; pt[3 * np + 1] = start; pt[3 * np + 2] = n0; ++np;
-      start = 0;
-      src = 1;
+  int np = 0;
+  auto push = [&](int src, int a0, int a1) {
+    pt[3 * np] = src; pt[3 * np + 1] = a0; pt[3 * np + 2] = a1; ++np;
+  };
+  if (need <= kFloydMax) {
+    int cuts[kFloydMax];
+    floyd_sorted(rng, nb, need, cuts);
+    int start = 0, q = 0;
+    for (; q < need && cuts[q] < n0; ++q) {
+      push(0, start, cuts[q]);
+      start = cuts[q];
     }
-    if (need > 0 && rng.below((uint32_t)(nb - t)) < (uint32_t)need) {
-      --need;
-      const int pos = src == 0 ? t : t - n0;
-      pt[3 * np] = src; pt[3 * np + 1] = start; pt[3 * np + 2] = pos; ++np;
-      start = pos;
-    }
-  }
-  if (n0 == nb) {  // strand b empty: close strand a here
-    pt[3 * np] = 0; pt[3 * np + 1] = start; pt[3 * np + 2] = n0; ++np;
+    push(0, start, n0);
     start = 0;
+    for (; q < need; ++q) {
+      push(1, start, cuts[q] - n0);
+      start = cuts[q] - n0;
+    }
+    push(1, start, n1);
+  } else {
+    int start = 0, src = 0;
+    for (int t = 0; t < nb; ++t) {
+      if (t == n0) {  // close the last part of strand a
+        push(0, start, n0);
+        start = 0;
+        src = 1;
+      }
+      if (need > 0 && rng.below((uint32_t)(nb - t)) < (uint32_t)need) {
+        --need;
+        const int pos = src == 0 ? t : t - n0;
+        push(src, start, pos);
+        start = pos;
+      }
+    }
+    if (n0 == nb) {  // strand b empty: close strand a here
+      push(0, start, n0);
+      start = 0;
+    }
+    push(1, start, n1);
   }
-  pt[3 * np] = 1; pt[3 * np + 1] = start; pt[3 * np + 2] = n1; ++np;
   // Fisher-Yates shuffle of the parts
   for (int q = np - 1; q > 0; --q) {
     const int r = (int)rng.below((uint32_t)(q + 1));

@@ -36,19 +36,22 @@ HostTables::HostTables(const std::vector<std::string>& start_codons,
     throw std::invalid_argument("dom_type_size must be in 1..9 nucleotides");
   dom_type.assign(size_t(1) << (2 * dom_type_size), 0);
   two_codon.assign(4096, 0);
-  for (int i = 0; i < 64; ++i) t.is_start[i] = t.is_stop[i] = t.one_codon[i] = 0;
+  for (int i = 0; i < 64; ++i) is_start[i] = is_stop[i] = one_codon[i] = 0;
+  t.is_start = is_start;
+  t.is_stop = is_stop;
+  t.one_codon = one_codon;
   for (auto& c : start_codons) {
     if (c.size() != 3) throw std::invalid_argument("start codons must have 3 nucleotides");
-    t.is_start[seq_index(c)] = 1;
+    is_start[seq_index(c)] = 1;
   }
   for (auto& c : stop_codons) {
     if (c.size() != 3) throw std::invalid_argument("stop codons must have 3 nucleotides");
-    t.is_stop[seq_index(c)] = 1;
+    is_stop[seq_index(c)] = 1;
   }
   for (auto& kv : domain_map)
     if ((int)kv.first.size() == dom_type_size) dom_type[seq_index(kv.first)] = (uint8_t)kv.second;
   for (auto& kv : one_codon_map)
-    if (kv.first.size() == 3) t.one_codon[seq_index(kv.first)] = (uint8_t)kv.second;
+    if (kv.first.size() == 3) one_codon[seq_index(kv.first)] = (uint8_t)kv.second;
   for (auto& kv : two_codon_map)
     if (kv.first.size() == 6) two_codon[seq_index(kv.first)] = (uint16_t)kv.second;
   t.dom_type = dom_type.data();

@@ -36,10 +36,13 @@ inline std::mt19937_64 item_engine(uint64_t call_seed, uint64_t item) {
 
 // Owning translation tables built from the dictionaries of a Genetics object.
 struct HostTables {
+  uint8_t is_start[64], is_stop[64], one_codon[64];
   std::vector<uint8_t> dom_type;
   std::vector<uint16_t> two_codon;
   ms::TransTables t{};
 
+  HostTables(const HostTables&) = delete;  // `t` points into this object's own arrays
+  HostTables& operator=(const HostTables&) = delete;
   HostTables(const std::vector<std::string>& start_codons, const std::vector<std::string>& stop_codons,
              const std::unordered_map<std::string, int>& domain_map,
              const std::unordered_map<std::string, int>& one_codon_map,

@@ -24,9 +24,9 @@ constexpr int kMaxDomTypeNts = 9;  // n_dom_type_codons <= 3 -> LUT of 4^9 entri
 
 // Translation lookup tables (see models/genetics.py for how they are derived from a Genetics object).
 struct TransTables {
-  uint8_t is_start[64];
-  uint8_t is_stop[64];
-  uint8_t one_codon[64];        // 1-codon token (1..61), 0 for stop codons
+  const uint8_t* is_start;      // 64 entries
+  const uint8_t* is_stop;       // 64 entries
+  const uint8_t* one_codon;     // 64 entries: 1-codon token (1..61), 0 for stop codons
   const uint8_t* dom_type;      // 4^dom_type_size entries: 0 none, 1 catalytic, 2 transporter, 3 regulatory
   const uint16_t* two_codon;    // 4096 entries: 2-codon token (1..3904), 0 if the first codon is a stop
   int dom_size;                 // nts per domain

@@ -141,6 +141,7 @@ class Genetics:
         if key not in cache:
             st, sp, oc, dt, tc = tables.luts()
             cache[key] = {
+                "small": torch.from_numpy(np.concatenate([np.asarray(st), np.asarray(sp), np.asarray(oc)])).to(device),
                 "is_start": torch.from_numpy(np.asarray(st)).to(device),
                 "is_stop": torch.from_numpy(np.asarray(sp)).to(device),
                 "one_codon": torch.from_numpy(np.asarray(oc)).to(device),

@@ -84,6 +84,8 @@ def build_hip(force: bool = False, jobs: int = 8) -> Path:
         "-fPIC",
         "-fvisibility=hidden",
         "-munsafe-fp-atomics",
+        # no FMA contraction: device results match the OpenMP host core operation for operation
+        "-ffp-contract=off",
         f"-I{CSRC / 'include'}",
         *_py_includes(),
     ]

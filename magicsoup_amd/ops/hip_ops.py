@@ -336,28 +336,23 @@ def neighbors(world, frm: torch.Tensor, to: torch.Tensor) -> torch.Tensor:
 
 # ---------------------------------------------------------------------------- genomes
 def translate(genetics, data: torch.Tensor, lens: torch.Tensor, rows: torch.Tensor):
+    """Two-pass device translation of arena rows ``rows`` -> (tokens (k, P, D, 5), n_prots (k,))."""
     dev = data.device
     n = int(rows.numel())
-    luts = genetics.device_luts(dev)
-    st = genetics.__dict__.get("_lut_lists")
     tables = genetics.tables
-    if st is None or st[0] is not tables:
-        a, b, c, _, _ = tables.luts()
-        st = (tables, list(bytes(a)), list(bytes(b)), list(bytes(c)))
-        genetics.__dict__["_lut_lists"] = st
+    luts = genetics.device_luts(dev)
     rows64 = rows.to(torch.int64).contiguous()
     width = int(data.size(1))
     counts = torch.empty(2 * n, dtype=torch.int32, device=dev)
     ndom = torch.empty(2 * n, dtype=torch.int32, device=dev)
-    args = (_p(luts["dom_type"]), _p(luts["two_codon"]), tables.dom_size, tables.dom_type_size)
-    _m().translate_count(n, _p(rows64), _p(data), width, _p(lens), st[1], st[2], st[3], *args,
-                         _p(counts), _p(ndom), _stream())
+    common = (_p(luts["small"]), _p(luts["dom_type"]), int(luts["dom_type"].numel()), _p(luts["two_codon"]),
+              tables.dom_size, tables.dom_type_size)
+    _m().translate_count(n, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), _p(ndom), _stream())
     per = counts.view(n, 2).sum(1)
     PD = torch.stack([per.max(), ndom.max()]).tolist() if n else [0, 0]
     P, D = max(int(PD[0]), 1), max(int(PD[1]), 1)
     tokens = torch.zeros(n, P, D, 5, dtype=torch.int32, device=dev)
-    _m().translate_write(n, _p(rows64), _p(data), width, _p(lens), st[1], st[2], st[3], *args,
-                         _p(counts), P, D, _p(tokens), _stream())
+    _m().translate_write(n, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), P, D, _p(tokens), _stream())
     return tokens, per
 
 
