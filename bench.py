@@ -104,8 +104,11 @@ def main():
     if distributed:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:  # CPU rehearsal of the multi-rank path
+            dist.init_process_group("gloo")
     device = f"cuda:{local_rank}" if torch.cuda.is_available() else "cpu"
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
@@ -134,7 +137,8 @@ def main():
             torch.cuda.synchronize()
         if distributed:
             torch.distributed.barrier()
-            torch.cuda.synchronize()
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
 
     n_target = a.cells // world_size if distributed else a.cells
     for _ in range(a.warmup):

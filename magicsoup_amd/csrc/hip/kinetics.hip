@@ -20,17 +20,17 @@ namespace msd {
 constexpr int kBlock = 256;
 
 struct IntegrateArgs {
-  int c, P, s, m, S;
+  int c, P, s, m, R, C;
   const int32_t *N, *Nf, *Nb, *A;
   const float *Kmr, *Kmf, *Kmb, *Vmax, *Ke;
   const float* cell_mols;     // (c, m)       part 0 source
-  const float* molmap;        // (m, S, S)    part 0 source
+  const float* molmap;        // (m, R, C)    part 0 source
   const int32_t* positions;   // (c, 2)       part 0 source
   const float* snap_prev;     // (c, kSnap, s) previous part's candidates (part > 0)
-  const unsigned* mask_prev;  // previous part's iteration mask
+  const unsigned* mask_prev;  // previous part's 4 iteration flags
   int n_iters_prev;
   float* snap_out;            // (c, kSnap, s)
-  unsigned* mask_out;
+  unsigned* mask_out;         // this part's 4 iteration flags (0/1, MAX-reducible across ranks)
   float trim;
   int n_iters;
   int* overflow;              // set if a stoichiometry does not fit in int8
@@ -38,9 +38,9 @@ struct IntegrateArgs {
   int sp;                     // padded LDS row stride (odd)
 };
 
-__device__ __forceinline__ int stop_iter(unsigned mask, int n_iters) {
+__device__ __forceinline__ int stop_iter(const unsigned* flags, int n_iters) {
   for (int it = 0; it < n_iters; ++it)
-    if (!(mask & (1u << it))) return it;
+    if (!flags[it]) return it;
   return n_iters;
 }
 
@@ -79,11 +79,11 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
   if (valid) {
     if (a.snap_prev == nullptr) {
       const int px = a.positions[2 * cell], py = a.positions[2 * cell + 1];
-      const size_t pix = (size_t)px * a.S + py, plane = (size_t)a.S * a.S;
+      const size_t pix = (size_t)px * a.C + py, plane = (size_t)a.R * a.C;
       for (int j = lane; j < s; j += G)
         X0[j] = j < a.m ? a.cell_mols[(size_t)cell * a.m + j] : a.molmap[(size_t)(j - a.m) * plane + pix];
     } else {
-      const int k = stop_iter(*a.mask_prev, a.n_iters_prev);
+      const int k = stop_iter(a.mask_prev, a.n_iters_prev);
       const float* src = a.snap_prev + ((size_t)cell * ms::kSnap + k) * s;
       for (int j = lane; j < s; j += G) X0[j] = src[j];
     }
@@ -275,18 +275,20 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
   // ---- 9. one mask OR per workgroup
   if (bits) atomicOr(&block_bits, bits);
   __syncthreads();
-  if (threadIdx.x == 0 && block_bits) atomicOr(a.mask_out, block_bits);
+  if (threadIdx.x == 0 && block_bits)
+    for (int it = 0; it < ms::kEqIters; ++it)
+      if (block_bits & (1u << it)) atomicOr(a.mask_out + it, 1u);
 }
 
 // Final state -> cell_molecules and the molecule-map pixels under the cells.
-__global__ void __launch_bounds__(kBlock) integrate_scatter_kernel(int c, int s, int m, int S, const float* snap,
+__global__ void __launch_bounds__(kBlock) integrate_scatter_kernel(int c, int s, int m, int R, int C, const float* snap,
                                                                    const unsigned* mask, int n_iters,
                                                                    const int32_t* positions, float* cell_mols,
                                                                    float* molmap, float* X_out) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long long)c * s) return;
   const int cell = (int)(t / s), j = (int)(t - (long long)cell * s);
-  const int k = stop_iter(*mask, n_iters);
+  const int k = stop_iter(mask, n_iters);
   const float x = snap[((size_t)cell * ms::kSnap + k) * s + j];
   if (X_out) {
     X_out[(size_t)cell * s + j] = x;
@@ -295,8 +297,8 @@ __global__ void __launch_bounds__(kBlock) integrate_scatter_kernel(int c, int s,
   if (j < m) {
     cell_mols[(size_t)cell * m + j] = x;
   } else {
-    const size_t pix = (size_t)positions[2 * cell] * S + positions[2 * cell + 1];
-    molmap[(size_t)(j - m) * S * S + pix] = x;
+    const size_t pix = (size_t)positions[2 * cell] * C + positions[2 * cell + 1];
+    molmap[(size_t)(j - m) * R * C + pix] = x;
   }
 }
 
@@ -394,39 +396,44 @@ static int slot_words_for(int P, int s, int sp) {
   return (w + 3) & ~3;  // keep every slot 16-byte aligned
 }
 
-// X_src: if nonzero, integrate explicit signals X (c, s) and write the result back there
-// (Kinetics.integrate_signals); otherwise gather from / scatter to the world state.
-void integrate(int c, int P, int s, int m, int S, uintptr_t N, uintptr_t Nf, uintptr_t Nb, uintptr_t A,
+// Launch integration parts [part_begin, part_end) of trims.size() parts. X_io: if nonzero,
+// integrate explicit signals X (c, s) and write the result back there (Kinetics.integrate_signals);
+// otherwise gather from / scatter to the world state (cell_mols, molmap, positions). `masks` holds
+// 4 flags per part plus a zero block; the caller may all-reduce (MAX) a part's flags across ranks
+// between launches for the reference's global early exit over a domain-decomposed population.
+void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t Nf, uintptr_t Nb, uintptr_t A,
                uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb, uintptr_t Vmax, uintptr_t Ke, uintptr_t cell_mols,
                uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
-               uintptr_t masks, uintptr_t overflow, const std::vector<float>& trims, int n_iters, uintptr_t stream) {
+               uintptr_t masks, uintptr_t overflow, const std::vector<float>& trims, int n_iters, int part_begin,
+               int part_end, uintptr_t stream) {
   if (c <= 0) return;
   if (n_iters < 0 || n_iters > ms::kEqIters) throw std::invalid_argument("n_iters must be in 0..4");
   const int nparts = (int)trims.size();
+  if (part_begin < 0 || part_end > nparts || part_begin > part_end) throw std::invalid_argument("bad part range");
   hipStream_t st = S_(stream);
-  MS_HIP_CHECK(hipMemsetAsync(P_<unsigned>(masks), 0, sizeof(unsigned) * (nparts + 1), st));
+  unsigned* mk = P_<unsigned>(masks);
+  unsigned* zero_flags = mk + ms::kEqIters * nparts;
+  float* snaps[2] = {P_<float>(snap_a), P_<float>(snap_b)};
+  if (part_begin == 0) {
+    MS_HIP_CHECK(hipMemsetAsync(mk, 0, sizeof(unsigned) * ms::kEqIters * (nparts + 1), st));
+    if (X_io) {  // explicit X: stage it as candidate 0 of snap_b, selected through the zero flags
+      load_x_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(c, s, P_<float>(X_io), snaps[1]);
+      MS_LAUNCH_CHECK();
+    }
+  }
   const int G = s <= 32 ? 32 : 64;
   const int sp = (s % 2 == 0) ? s + 1 : s;
   const int slot_words = slot_words_for(P, s, sp);
   const size_t slot_bytes = (size_t)slot_words * 4;
-  const size_t budget = 64 * 1024;
   int cps = kBlock / G;
-  while (cps > 1 && cps * slot_bytes > budget) --cps;
+  while (cps > 1 && cps * slot_bytes > 64 * 1024) --cps;
   const size_t lds = cps * slot_bytes + 16;
   if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
   const int threads = cps * G;
   const unsigned grid = cdiv(c, cps);
-
-  float* snaps[2] = {P_<float>(snap_a), P_<float>(snap_b)};
-  unsigned* mk = P_<unsigned>(masks);
-  if (X_io) {
-    // explicit X: stage it as candidate 0 of snap_b with the zero mask slot nparts
-    load_x_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(c, s, P_<float>(X_io), snaps[1]);
-    MS_LAUNCH_CHECK();
-  }
-  for (int part = 0; part < nparts; ++part) {
+  for (int part = part_begin; part < part_end; ++part) {
     IntegrateArgs a{};
-    a.c = c; a.P = P; a.s = s; a.m = m; a.S = S;
+    a.c = c; a.P = P; a.s = s; a.m = m; a.R = R; a.C = C;
     a.N = P_<int32_t>(N); a.Nf = P_<int32_t>(Nf); a.Nb = P_<int32_t>(Nb); a.A = P_<int32_t>(A);
     a.Kmr = P_<float>(Kmr); a.Kmf = P_<float>(Kmf); a.Kmb = P_<float>(Kmb); a.Vmax = P_<float>(Vmax); a.Ke = P_<float>(Ke);
     a.cell_mols = P_<float>(cell_mols); a.molmap = P_<float>(molmap); a.positions = P_<int32_t>(positions);
@@ -434,15 +441,15 @@ void integrate(int c, int P, int s, int m, int S, uintptr_t N, uintptr_t Nf, uin
       a.snap_prev = nullptr;
     } else if (part == 0) {
       a.snap_prev = snaps[1];
-      a.mask_prev = mk + nparts;  // zero word -> candidate 0
+      a.mask_prev = zero_flags;
       a.n_iters_prev = n_iters;
     } else {
       a.snap_prev = snaps[(part - 1) & 1];
-      a.mask_prev = mk + part - 1;
+      a.mask_prev = mk + ms::kEqIters * (part - 1);
       a.n_iters_prev = n_iters;
     }
     a.snap_out = snaps[part & 1];
-    a.mask_out = mk + part;
+    a.mask_out = mk + ms::kEqIters * part;
     a.trim = trims[part];
     a.n_iters = n_iters;
     a.overflow = P_<int>(overflow);
@@ -452,12 +459,13 @@ void integrate(int c, int P, int s, int m, int S, uintptr_t N, uintptr_t Nf, uin
     else integrate_part_kernel<64><<<grid, threads, lds, st>>>(a);
     MS_LAUNCH_CHECK();
   }
-  const int last = nparts - 1;
-  if (nparts == 0) return;
-  integrate_scatter_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(
-      c, s, m, S, snaps[last & 1], mk + last, n_iters, P_<int32_t>(positions), P_<float>(cell_mols),
-      P_<float>(molmap), X_io ? P_<float>(X_io) : nullptr);
-  MS_LAUNCH_CHECK();
+  if (part_end == nparts && nparts > 0 && part_begin < part_end) {
+    const int last = nparts - 1;
+    integrate_scatter_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(
+        c, s, m, R, C, snaps[last & 1], mk + ms::kEqIters * last, n_iters, P_<int32_t>(positions),
+        P_<float>(cell_mols), P_<float>(molmap), X_io ? P_<float>(X_io) : nullptr);
+    MS_LAUNCH_CHECK();
+  }
 }
 
 void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_t rows, uintptr_t vmax_w, int nw,

@@ -13,28 +13,33 @@ namespace py = pybind11;
 
 namespace msd {
 // kinetics.hip
-void integrate(int c, int P, int s, int m, int S, uintptr_t N, uintptr_t Nf, uintptr_t Nb, uintptr_t A,
+void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t Nf, uintptr_t Nb, uintptr_t A,
                uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb, uintptr_t Vmax, uintptr_t Ke, uintptr_t cell_mols,
                uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
-               uintptr_t masks, uintptr_t overflow, const std::vector<float>& trims, int n_iters, uintptr_t stream);
+               uintptr_t masks, uintptr_t overflow, const std::vector<float>& trims, int n_iters, int part_begin,
+               int part_end, uintptr_t stream);
 void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_t rows, uintptr_t vmax_w, int nw,
                   uintptr_t km_w, int nk, uintptr_t signs, int nsg, uintptr_t hills, int nh, uintptr_t RM,
                   uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
                   uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
                   uintptr_t Vmax, uintptr_t Ke, uintptr_t stream);
 // world.hip
-void diffuse(int m, int S, uintptr_t map, uintptr_t tmp, uintptr_t wa, uintptr_t wb, uintptr_t scale,
-             uintptr_t partials, uintptr_t corr, uintptr_t totals, uintptr_t stream);
-size_t diffuse_partials_len(int m, int S);
+void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
+                     uintptr_t wb, uintptr_t scale, uintptr_t partials, uintptr_t totals, uintptr_t stream);
+void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t totals,
+                     double n_pix, uintptr_t stream);
+size_t diffuse_partials_len(int m, int C, int H);
 void scale_planes(int m, long long plane, uintptr_t map, uintptr_t f, uintptr_t stream);
-void permeate(int c, int m, int S, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map, uintptr_t stream);
-void claim_free(int k, long long n_pix, uintptr_t cell_map, uint64_t seed, uint64_t call, int attempts, uintptr_t out,
-                uintptr_t stream);
-void pick_neighbour(int k, uintptr_t cells, uintptr_t pos, int S, uintptr_t cell_map, uintptr_t pending, uint64_t seed,
-                    uint64_t call, uintptr_t cand, uintptr_t stream);
-void index_map(int c, uintptr_t pos, int S, uintptr_t idx_map, bool clear, uintptr_t stream);
-void neighbor_pairs(int nf, uintptr_t from, uintptr_t pos, int S, uintptr_t idx_map, uintptr_t in_from, uintptr_t in_to,
-                    uintptr_t counter, int cap, uintptr_t pairs, uintptr_t stream);
+void permeate(int c, int m, int R, int C, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map,
+              uintptr_t stream);
+void claim_free(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uint64_t seed, uint64_t call,
+                int attempts, uintptr_t out, uintptr_t stream);
+void pick_neighbour(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap,
+                    uintptr_t cell_map, uintptr_t pending, uint64_t seed, uint64_t call, uintptr_t cand,
+                    uintptr_t stream);
+void index_map(int c, uintptr_t pos, int C, uintptr_t idx_map, bool clear, uintptr_t stream);
+void neighbor_pairs(int nf, uintptr_t from, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map,
+                    uintptr_t in_from, uintptr_t in_to, uintptr_t counter, int cap, uintptr_t pairs, uintptr_t stream);
 // genetics.hip
 void translate_count(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
@@ -77,7 +82,8 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("integrate", &msd::integrate);
   m.def("build_params", &msd::build_params);
-  m.def("diffuse", &msd::diffuse);
+  m.def("diffuse_stencil", &msd::diffuse_stencil);
+  m.def("diffuse_correct", &msd::diffuse_correct);
   m.def("diffuse_partials_len", &msd::diffuse_partials_len);
   m.def("scale_planes", &msd::scale_planes);
   m.def("permeate", &msd::permeate);

@@ -165,9 +165,12 @@ unsigned cell_part(const CellParams& q, int np, int s, const float* X0, float tr
 
 // Fused integrate_signals on host. X (c, s) is updated in place. trims: velocity trim factors
 // (reference (0.7, 0.2, 0.1)); n_iters: equilibrium iterations (4, or 0 to disable them).
-// Returns the list of per-part global iteration masks (for diagnostics / tests).
+// Returns the list of per-part global iteration masks (for diagnostics / tests). `reduce_mask`
+// (optional callable int -> int) turns a part's local mask into the global one (a domain-decomposed
+// world ORs the masks of all ranks, reproducing the reference's `torch.any` over the population).
 py::list integrate_signals(farr X, iarr N, iarr Nf, iarr Nb, iarr A, farr Kmr, farr Kmf, farr Kmb, farr Vmax,
-                           farr Ke, py::object nprot_obj, std::vector<float> trims, int n_iters) {
+                           farr Ke, py::object nprot_obj, std::vector<float> trims, int n_iters,
+                           py::object reduce_mask) {
   if (X.ndim() != 2 || N.ndim() != 3) throw std::invalid_argument("X must be (c,s) and N (c,p,s)");
   const int c = (int)X.shape(0), s = (int)X.shape(1), P = (int)N.shape(1);
   if (N.shape(0) < c || N.shape(2) != s) throw std::invalid_argument("param/signal shape mismatch");
@@ -200,6 +203,10 @@ py::list integrate_signals(farr X, iarr N, iarr Nf, iarr Nb, iarr A, farr Kmr, f
                             V.data(), Va.data(), F.data(), fwd.data(), imp.data(), cons.data(), fs.data());
         }
       }
+    }
+    if (!reduce_mask.is_none()) mask = reduce_mask(mask).cast<unsigned>();
+    {
+      py::gil_scoped_release nogil;
       int stop = n_iters;
       for (int it = 0; it < n_iters; ++it)
         if (!(mask & (1u << it))) {
@@ -316,7 +323,7 @@ void build_params(iarr tokens, iarr rows, farr vmax_w, farr km_w, iarr signs, ia
 void bind_kinetics(py::module_& m) {
   m.def("integrate_signals", &integrate_signals, py::arg("X"), py::arg("N"), py::arg("Nf"), py::arg("Nb"),
         py::arg("A"), py::arg("Kmr"), py::arg("Kmf"), py::arg("Kmb"), py::arg("Vmax"), py::arg("Ke"),
-        py::arg("nprot"), py::arg("trims"), py::arg("n_iters"));
+        py::arg("nprot"), py::arg("trims"), py::arg("n_iters"), py::arg("reduce_mask") = py::none());
   m.def("build_params", &build_params);
 }
 

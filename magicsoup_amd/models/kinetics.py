@@ -353,17 +353,52 @@ class Kinetics:
             t = getattr(self, name)
             t[to_idxs] = t[from_idxs]
 
+    # The parameter tensors are views of capacity-managed row buffers: appending rows (spawn,
+    # divide) reuses spare capacity instead of re-copying every row like the reference's
+    # torch.cat (kinetics.py:688-703), and removing rows gathers the survivors into a second
+    # buffer in one pass. A tensor assigned from outside is adopted as the new buffer.
+    def _buffer(self, name: str) -> torch.Tensor:
+        t = getattr(self, name)
+        bufs = self.__dict__.setdefault("_bufs", {})
+        buf = bufs.get(name)
+        if buf is None or t.data_ptr() != buf.data_ptr() or t.shape[1:] != buf.shape[1:] or not t.is_contiguous():
+            buf = t.contiguous()
+            bufs[name] = buf
+        return buf
+
     def remove_cell_params(self, keep: torch.Tensor):
-        """Keep only the rows where the bool mask ``keep`` (c,) is true."""
+        """Keep only the rows where ``keep`` is true (bool mask (c,)) or listed (ascending index
+        tensor), preserving their order."""
+        idx = torch.nonzero(keep).flatten() if keep.dtype == torch.bool else keep.to(torch.long)
+        k = int(idx.numel())
+        spares = self.__dict__.setdefault("_spares", {})
         for name in _PARAMS:
-            setattr(self, name, getattr(self, name)[keep])
+            t = getattr(self, name)
+            buf = self._buffer(name)
+            spare = spares.get(name)
+            if spare is None or spare.size(0) < k or spare.shape[1:] != buf.shape[1:] or spare.dtype != buf.dtype:
+                spare = torch.empty(max(k, buf.size(0)), *buf.shape[1:], dtype=buf.dtype, device=buf.device)
+            torch.index_select(t, 0, idx, out=spare[:k])
+            spares[name] = buf
+            self._bufs[name] = spare
+            setattr(self, name, spare[:k])
 
     def increase_max_cells(self, by_n: int):
         """Append ``by_n`` zero rows to every parameter tensor."""
+        if by_n <= 0:
+            return
         for name in _PARAMS:
             t = getattr(self, name)
-            z = torch.zeros(by_n, *t.shape[1:], dtype=t.dtype, device=t.device)
-            setattr(self, name, torch.cat([t, z], dim=0))
+            n = int(t.size(0))
+            buf = self._buffer(name)
+            if n + by_n > buf.size(0):
+                cap = max(n + by_n, int(buf.size(0) * 1.5) + 64)
+                nb = torch.empty(cap, *buf.shape[1:], dtype=buf.dtype, device=buf.device)
+                nb[:n] = t
+                buf = self._bufs[name] = nb
+            view = buf[: n + by_n]
+            view[n:].zero_()
+            setattr(self, name, view)
 
     def increase_max_proteins(self, max_n: int):
         """Grow the protein dimension of every parameter tensor to ``max_n`` (zero-filled)."""
@@ -376,7 +411,7 @@ class Kinetics:
             setattr(self, name, torch.cat([t, z], dim=1))
 
     # ------------------------------------------------------------------ integration
-    def integrate_signals(self, X: torch.Tensor) -> torch.Tensor:
+    def integrate_signals(self, X: torch.Tensor, _reduce_mask=None) -> torch.Tensor:
         """Let all proteins work for one time step.
 
         Parameters:
@@ -391,7 +426,9 @@ class Kinetics:
                 X = self._integrate_signals_part(adj_vmax=(self.Vmax * trim).clamp(0.0), X0=X)
             return X
         out = X.to(torch.float32).contiguous().clone()
-        self.last_masks = kinetics_ops.integrate(self, out, trims=_TRIMS, n_iters=len(_INCREMENTS))
+        self.last_masks = kinetics_ops.integrate(
+            self, out, trims=_TRIMS, n_iters=len(_INCREMENTS), reduce_mask=_reduce_mask
+        )
         return out
 
     def _stages_overridden(self) -> bool:
@@ -489,6 +526,10 @@ class Kinetics:
     def __getstate__(self):
         state = self.__dict__.copy()
         state["last_masks"] = []
+        for k in ("_bufs", "_spares", "_hip_scratch"):
+            state.pop(k, None)
+        for name in _PARAMS:
+            state[name] = getattr(self, name).clone()
         return state
 
     def _i32_tensor(self, d: Any) -> torch.Tensor:

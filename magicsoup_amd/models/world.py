@@ -110,6 +110,11 @@ class World:
         seed: Optional seed of all native RNG streams (placement, mutation, recombination).
     """
 
+    # domain-decomposition hooks of the op layer (set by magicsoup_amd.parallel.DistributedWorld)
+    _exchange_map_halo = None
+    _allreduce_flags = None
+    _allreduce_totals = None
+
     def __init__(
         self,
         chemistry: Chemistry,
@@ -162,8 +167,12 @@ class World:
             "cell_divisions": _Column(torch.zeros(0, dtype=torch.int32, device=dev)),
         }
         self.__dict__["_pending_scale"] = None
-        self.cell_map = torch.zeros(map_size, map_size, dtype=torch.bool, device=dev)
+        self.cell_map = torch.zeros(*self._map_shape(), dtype=torch.bool, device=dev)
         self.molecule_map = self._get_molecule_map(n=m, size=map_size, init=mol_map_init)
+
+    def _map_shape(self) -> tuple[int, int]:
+        """(rows, cols) of this process's map (a strip with halo rows in magicsoup_amd.parallel)."""
+        return self.map_size, self.map_size
 
     # ------------------------------------------------------------------ public state
     def __getattr__(self, name):  # only reached for attributes not found normally
@@ -437,7 +446,7 @@ class World:
             v = col.view(self.n_cells)
             col.buf[:n_new] = v[keep_idx]
             col._view = None
-        self.kinetics.remove_cell_params(keep=keep)
+        self.kinetics.remove_cell_params(keep=keep_idx)
         self._genomes.keep(keep_idx)
         self._labels.keep(keep_idx)
         self.n_cells = n_new
@@ -612,6 +621,8 @@ class World:
         self.__setstate__(st)
         kin = self.kinetics
         kin.device = device
+        for k in ("_bufs", "_spares", "_hip_scratch"):
+            kin.__dict__.pop(k, None)
         for name, val in list(vars(kin).items()):
             if isinstance(val, torch.Tensor):
                 setattr(kin, name, val.to(dev))
@@ -650,10 +661,11 @@ class World:
         return world_ops.free_positions(self, n_cells)
 
     def _get_molecule_map(self, n: int, size: int, init: str) -> torch.Tensor:
+        shape = (n, size, size) if self._map_shape() == (size, size) else (n, *self._map_shape())
         if init == "zeros":
-            return torch.zeros(n, size, size, dtype=torch.float32, device=self.device)
+            return torch.zeros(*shape, dtype=torch.float32, device=self.device)
         if init == "randn":
-            return (torch.randn(n, size, size, dtype=torch.float32, device=self.device) + 10.0).abs()
+            return (torch.randn(*shape, dtype=torch.float32, device=self.device) + 10.0).abs()
         raise ValueError(f"Didnt recognize mol_map_init={init}. Should be one of: 'zeros', 'randn'.")
 
     def _get_permeate(self, mol_perm_rate: float) -> float:

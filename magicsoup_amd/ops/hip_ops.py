@@ -9,6 +9,7 @@ from __future__ import annotations
 import torch
 
 from magicsoup_amd.ops import native
+from magicsoup_amd.ops.world_ops import geom
 
 _SNAP = 5  # candidate states per cell per integration part (kinetics.py:819 has 4 increments)
 
@@ -58,31 +59,51 @@ def _rng() -> tuple[int, int]:
     return _m().next_call()
 
 
+# ---------------------------------------------------------------------------- geometry
 # ---------------------------------------------------------------------------- kinetics
-def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n_iters=4):
+_EQ = 4  # equilibrium-damping iterations per part
+
+
+def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n_iters=4, flags_hook=None):
     N = p["N"]
     P, s = int(N.size(1)), int(N.size(2))
     dev = N.device
     sc = _scratch(kin)
     snap_a = sc.get("snap_a", c * _SNAP * s, torch.float32, dev)
     snap_b = sc.get("snap_b", c * _SNAP * s, torch.float32, dev)
-    masks = sc.get("masks", len(trims) + 1, torch.int32, dev)
+    masks = sc.get("masks", _EQ * (len(trims) + 1), torch.int32, dev)
     overflow = sc.get("overflow", 1, torch.int32, dev)
     if world is not None:
         m = world.n_molecules
-        S = int(world.map_size)
+        R, C = geom(world)[:2]
         cm, mm, pos = world.cell_molecules, world._molmap, world.cell_positions
     else:
-        m, S, cm, mm, pos = 0, 0, None, None, None
-    _m().integrate(
-        c, P, s, m, S,
+        m, R, C, cm, mm, pos = 0, 0, 0, None, None, None
+    args = [
+        c, P, s, m, R, C,
         _p(N), _p(p["Nf"]), _p(p["Nb"]), _p(p["A"]),
         _p(p["Kmr"]), _p(p["Kmf"]), _p(p["Kmb"]), _p(p["Vmax"]), _p(p["Ke"]),
         _p(cm), _p(mm), _p(pos), _p(X_io),
         _p(snap_a), _p(snap_b), _p(masks), _p(overflow),
-        [float(t) for t in trims], int(n_iters), _stream(),
-    )
+        [float(t) for t in trims], int(n_iters),
+    ]
+    nparts = len(trims)
+    if flags_hook is None:
+        _m().integrate(*args, 0, nparts, _stream())
+    else:
+        # domain-decomposed world: all-reduce each part's iteration flags before the next part reads
+        # them, reproducing the reference's `torch.any` over the whole population
+        for part in range(nparts):
+            _m().integrate(*args, part, part + 1, _stream())
+            flags_hook(masks[_EQ * part : _EQ * (part + 1)])
+        if nparts:
+            _m().integrate(*args, nparts, nparts, _stream())
     return masks
+
+
+def _flags_to_bits(masks: torch.Tensor, nparts: int) -> list[int]:
+    f = masks[: _EQ * nparts].view(nparts, _EQ).tolist()
+    return [sum(1 << i for i, v in enumerate(row) if v) for row in f]
 
 
 def integrate(X: torch.Tensor, p: dict, trims, n_iters: int) -> list[int]:
@@ -90,11 +111,11 @@ def integrate(X: torch.Tensor, p: dict, trims, n_iters: int) -> list[int]:
     c = int(X.size(0))
     kin = _KinProxy(p)
     masks = _launch_integrate(kin, p, c, X_io=X, trims=trims, n_iters=n_iters)
-    return [int(v) for v in masks[: len(trims)].tolist()]
+    return _flags_to_bits(masks, len(trims))
 
 
 class _KinProxy:
-    """Scratch holder keyed on the parameter tensors' owner when only a dict is at hand."""
+    """Scratch holder keyed on the device when only a parameter dict is at hand."""
 
     _cache: dict[int, Scratch] = {}
 
@@ -107,7 +128,7 @@ class _KinProxy:
 
 
 def enzymatic_activity(world) -> None:
-    """Fused gather -> 3-part integrate -> scatter over the world state (5 launches, no syncs)."""
+    """Fused gather -> 3-part integrate -> scatter over the world state (no host syncs)."""
     from magicsoup_amd.ops.kinetics_ops import _canonical_params
 
     kin = world.kinetics
@@ -116,7 +137,8 @@ def enzymatic_activity(world) -> None:
     if p["N"].size(0) < c:
         raise ValueError("kinetics has fewer cell rows than the world")
     _ensure_world_layout(world)
-    _launch_integrate(kin, p, c, world=world)
+    hook = getattr(world, "_allreduce_flags", None)
+    _launch_integrate(kin, p, c, world=world, flags_hook=hook)
 
 
 def build_params(tokens, rows, luts, p, abs_temp: float, gas: float) -> None:
@@ -145,22 +167,37 @@ def _ensure_world_layout(world) -> None:
 
 
 def diffuse(world) -> None:
+    """Stencil over the owned rows (+ fused pending degradation) -> (global) mass totals ->
+    correction + clamp. A domain-decomposed world refreshes its halo rows first and all-reduces the
+    totals (see magicsoup_amd.parallel)."""
+    R, C, r_lo, r_hi, wrap = geom(world)
+    halo = getattr(world, "_exchange_map_halo", None)
+    if halo is not None:
+        halo()
     mm = world._molmap
-    m, S = int(mm.size(0)), int(mm.size(1))
+    m = int(mm.size(0))
     sc = _scratch(world)
     dev = mm.device
     tmp = sc.get("diff_tmp", mm.numel(), torch.float32, dev)
-    partials = sc.get("diff_partials", int(_m().diffuse_partials_len(m, S)), torch.float64, dev)
-    corr = sc.get("diff_corr", m, torch.float32, dev)
+    partials = sc.get("diff_partials", int(_m().diffuse_partials_len(m, C, r_hi - r_lo)), torch.float64, dev)
+    totals = sc.get("diff_totals", 2 * m, torch.float64, dev)
     w = world.__dict__.get("_diff_w")
     if w is None or w[0] != world._diffusion:
         wa = torch.tensor([float(a) for a, _ in world._diffusion], dtype=torch.float32, device=dev)
         wb = torch.tensor([float(b) for _, b in world._diffusion], dtype=torch.float32, device=dev)
         w = (list(world._diffusion), wa, wb)
         world.__dict__["_diff_w"] = w
+    # a pending degradation scales the halo rows as well: every rank degrades identically, so the
+    # neighbours' unscaled boundary rows carry the same pending factor
     scale = world.__dict__.get("_pending_scale")
-    _m().diffuse(m, S, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale), _p(partials), _p(corr), 0, _stream())
+    _m().diffuse_stencil(m, R, C, r_lo, r_hi, wrap, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale), _p(partials),
+                         _p(totals), _stream())
     world.__dict__["_pending_scale"] = None
+    reduce = getattr(world, "_allreduce_totals", None)
+    if reduce is not None:
+        reduce(totals)
+    n_pix = float(getattr(world, "_n_pix_global", R * C if wrap else (r_hi - r_lo) * C))
+    _m().diffuse_correct(m, R, C, r_lo, r_hi, _p(mm), _p(tmp), _p(totals), n_pix, _stream())
 
 
 def permeate(world) -> None:
@@ -173,7 +210,8 @@ def permeate(world) -> None:
         world.__dict__["_perm_t"] = perm
     if not any(x != 0.0 for x in perm[0]):
         return
-    _m().permeate(world.n_cells, world.n_molecules, int(world.map_size), _p(world.cell_positions), _p(perm[1]),
+    R, C = geom(world)[:2]
+    _m().permeate(world.n_cells, world.n_molecules, R, C, _p(world.cell_positions), _p(perm[1]),
                   _p(world.cell_molecules), _p(mm), _stream())
 
 
@@ -213,31 +251,30 @@ def _cell_map_bytes(world) -> torch.Tensor:
 
 
 def free_positions(world, k: int) -> torch.Tensor:
-    S = int(world.map_size)
-    n_pix = S * S
+    """Up to k distinct uniformly random free pixels of the owned rows, int32 (k', 2) (local x)."""
+    R, C, r_lo, r_hi, _ = geom(world)
     dev = world.cell_map.device
     cmap = _cell_map_bytes(world)
     out = torch.empty(k, dtype=torch.int64, device=dev)
     seed, call = _rng()
-    _m().claim_free(k, n_pix, _p(cmap), seed, call, 64, _p(out), _stream())
+    _m().claim_free(k, R, C, r_lo, r_hi, _p(cmap), seed, call, 64, _p(out), _stream())
     got = out[out >= 0]
     if got.numel() < k:
-        # crowded map: exact sampling of the remainder over the remaining free pixels
-        free = torch.nonzero(cmap[:n_pix] == 0).flatten()
+        # crowded map: exact sampling of the remainder over the remaining free owned pixels
+        free = torch.nonzero(cmap[r_lo * C : r_hi * C] == 0).flatten() + r_lo * C
         need = min(k - int(got.numel()), int(free.numel()))
         if need > 0:
             extra = free[torch.randperm(free.numel(), device=dev)[:need]]
             cmap[extra] = 1
             got = torch.cat([got, extra])
-    return torch.stack([got // S, got % S], dim=1).to(torch.int32)
+    return torch.stack([got // C, got % C], dim=1).to(torch.int32)
 
 
 def _place_rounds(world, cells: torch.Tensor, vacate: bool, max_rounds: int = 16):
     """Priority-ordered parallel neighbour claims. Returns (winner cells, new pixels)."""
-    S = int(world.map_size)
+    R, C, r_lo, r_hi, wrap = geom(world)
     dev = cells.device
     k = int(cells.numel())
-    pos = world.cell_positions
     _ensure_world_layout(world)
     pos = world.cell_positions
     cmap = _cell_map_bytes(world)
@@ -247,7 +284,8 @@ def _place_rounds(world, cells: torch.Tensor, vacate: bool, max_rounds: int = 16
     order = torch.arange(k, device=dev)
     for _ in range(max_rounds):
         seed, call = _rng()
-        _m().pick_neighbour(k, _p(cells), _p(pos), S, _p(cmap), _p(pending), seed, call, _p(cand), _stream())
+        _m().pick_neighbour(k, _p(cells), _p(pos), R, C, r_lo, r_hi, wrap, _p(cmap), _p(pending), seed, call,
+                            _p(cand), _stream())
         has = cand >= 0
         # cells without any free neighbour give up (reference: they do not divide / move)
         pending &= has.to(torch.uint8)
@@ -264,8 +302,11 @@ def _place_rounds(world, cells: torch.Tensor, vacate: bool, max_rounds: int = 16
         wpix = cand[wins]
         cmap[wpix] = 1
         if vacate:
-            old = pos[cells[wins]].long()
-            cmap[old[:, 0] * S + old[:, 1]] = 0
+            # a move into a halo row is only committed once the owning rank accepts it, so the
+            # mover keeps its pixel until then (magicsoup_amd.parallel)
+            mv = wins if wrap else wins[(wpix >= r_lo * C) & (wpix < r_hi * C)]
+            old = pos[cells[mv]].long()
+            cmap[old[:, 0] * C + old[:, 1]] = 0
         pending[wins] = 0
         win_cells.append(wins)
         win_pix.append(wpix)
@@ -278,7 +319,7 @@ def _place_rounds(world, cells: torch.Tensor, vacate: bool, max_rounds: int = 16
     wpix = torch.cat(win_pix)
     o = torch.argsort(wins)
     wins, wpix = wins[o], wpix[o]
-    return cells[wins], torch.stack([wpix // S, wpix % S], dim=1).to(torch.int32)
+    return cells[wins], torch.stack([wpix // C, wpix % C], dim=1).to(torch.int32)
 
 
 def divide_placement(world, idxs: torch.Tensor):
@@ -304,18 +345,20 @@ def split_cells(world, parents: torch.Tensor, children: torch.Tensor) -> None:
     lt[children] = 0
 
 
-def neighbors(world, frm: torch.Tensor, to: torch.Tensor) -> torch.Tensor:
-    S = int(world.map_size)
+def neighbors(world, frm: torch.Tensor, to: torch.Tensor, pos: torch.Tensor | None = None, n: int | None = None) -> torch.Tensor:
+    """Unique (a < b) Moore-neighbour pairs between cells ``frm`` and ``to`` as int32 (k, 2).
+    ``pos`` / ``n`` default to the world's cells (a caller may append ghost cells)."""
+    R, C, r_lo, r_hi, wrap = geom(world)
     dev = world.cell_map.device
     _ensure_world_layout(world)
-    n = world.n_cells
-    pos = world.cell_positions
+    if pos is None:
+        pos, n = world.cell_positions, world.n_cells
     sc = _scratch(world)
     idx_map = world.__dict__.get("_idx_map")
-    if idx_map is None or idx_map.numel() != S * S:
-        idx_map = torch.full((S * S,), -1, dtype=torch.int32, device=dev)
+    if idx_map is None or idx_map.numel() != R * C:
+        idx_map = torch.full((R * C,), -1, dtype=torch.int32, device=dev)
         world.__dict__["_idx_map"] = idx_map
-    _m().index_map(n, _p(pos), S, _p(idx_map), False, _stream())
+    _m().index_map(n, _p(pos), C, _p(idx_map), False, _stream())
     in_from = sc.get("nb_from", n, torch.uint8, dev, zero=True)
     in_to = sc.get("nb_to", n, torch.uint8, dev, zero=True)
     in_from[frm] = 1
@@ -324,10 +367,10 @@ def neighbors(world, frm: torch.Tensor, to: torch.Tensor) -> torch.Tensor:
     cap = 8 * int(frm64.numel())
     pairs = sc.get("nb_pairs", cap, torch.int64, dev)
     counter = sc.get("nb_count", 1, torch.int32, dev, zero=True)
-    _m().neighbor_pairs(int(frm64.numel()), _p(frm64), _p(pos), S, _p(idx_map), _p(in_from), _p(in_to),
-                        _p(counter), cap, _p(pairs), _stream())
+    _m().neighbor_pairs(int(frm64.numel()), _p(frm64), _p(pos), R, C, r_lo, r_hi, wrap, _p(idx_map), _p(in_from),
+                        _p(in_to), _p(counter), cap, _p(pairs), _stream())
     cnt = int(counter.item())
-    _m().index_map(n, _p(pos), S, _p(idx_map), True, _stream())  # leave the map all -1
+    _m().index_map(n, _p(pos), C, _p(idx_map), True, _stream())  # leave the map all -1
     keys = torch.sort(pairs[:cnt]).values
     if keys.numel() > 1:
         keys = torch.unique_consecutive(keys)

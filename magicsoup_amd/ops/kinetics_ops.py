@@ -31,8 +31,9 @@ def _np(t: torch.Tensor):
     return t.detach().numpy()
 
 
-def integrate(kin, X: torch.Tensor, trims, n_iters: int) -> list[int]:
-    """Fused integrate_signals on X (c, s) in place; returns the per-part iteration masks."""
+def integrate(kin, X: torch.Tensor, trims, n_iters: int, reduce_mask=None) -> list[int]:
+    """Fused integrate_signals on X (c, s) in place; returns the per-part iteration masks.
+    ``reduce_mask`` (host path) maps a part's local iteration mask to the global one."""
     p = _canonical_params(kin)
     c = X.size(0)
     if c == 0:
@@ -49,6 +50,7 @@ def integrate(kin, X: torch.Tensor, trims, n_iters: int) -> list[int]:
         None,
         [float(t) for t in trims],
         int(n_iters),
+        reduce_mask,
     )
     return list(masks)
 

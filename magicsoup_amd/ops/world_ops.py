@@ -42,6 +42,21 @@ def _np(t: torch.Tensor):
     return t.detach().cpu().numpy()
 
 
+def geom(world) -> tuple[int, int, int, int, int]:
+    """(rows, cols, first owned row, end of owned rows, x wraps) of a world's local map. A whole
+    map wraps in x; a strip of a domain-decomposed world (magicsoup_amd.parallel) has one halo row
+    on each side and does not."""
+    g = getattr(world, "_geom", None)
+    if g is not None:
+        return g()
+    S = int(world.map_size)
+    return S, S, 0, S, 1
+
+
+def _halo_occ(world, wrap: int):
+    return None if wrap else _np(world.cell_map.view(torch.uint8))
+
+
 def _molmap(world) -> torch.Tensor:
     mm = world.molecule_map
     if mm.dtype != torch.float32 or not mm.is_contiguous():
@@ -54,7 +69,9 @@ def free_positions(world, k: int) -> torch.Tensor:
     """Up to k distinct uniformly random free pixels (int32 (k', 2)), in random order."""
     if _is_gpu(world):
         return _hip().free_positions(world, k)
-    free = torch.nonzero(~world.cell_map.to(torch.bool)).to(torch.int32)
+    _, _, r_lo, r_hi, _ = geom(world)
+    free = torch.nonzero(~world.cell_map[r_lo:r_hi].to(torch.bool)).to(torch.int32)
+    free[:, 0] += r_lo
     n = free.size(0)
     if n == 0:
         return torch.zeros(0, 2, dtype=torch.int32)
@@ -67,7 +84,10 @@ def divide_placement(world, idxs: torch.Tensor):
     if _is_gpu(world):
         return _hip().divide_placement(world, idxs)
     pos = world.cell_positions.to(torch.int32).contiguous()
-    parents, cpos = native.host().divide_cells(_np(idxs.to(torch.int32)), _np(pos), int(world.map_size))
+    R, C, r_lo, r_hi, wrap = geom(world)
+    parents, cpos = native.host().divide_cells(
+        _np(idxs.to(torch.int32)), _np(pos), R, C, r_lo, r_hi, bool(wrap), _halo_occ(world, wrap)
+    )
     return torch.from_numpy(np.asarray(parents)).long(), torch.from_numpy(np.asarray(cpos))
 
 
@@ -76,16 +96,24 @@ def move_placement(world, idxs: torch.Tensor):
     if _is_gpu(world):
         return _hip().move_placement(world, idxs)
     pos = world.cell_positions.to(torch.int32).contiguous()
-    moved, npos = native.host().move_cells(_np(idxs.to(torch.int32)), _np(pos), int(world.map_size))
+    R, C, r_lo, r_hi, wrap = geom(world)
+    moved, npos = native.host().move_cells(
+        _np(idxs.to(torch.int32)), _np(pos), R, C, r_lo, r_hi, bool(wrap), _halo_occ(world, wrap)
+    )
     return torch.from_numpy(np.asarray(moved)).long(), torch.from_numpy(np.asarray(npos))
 
 
-def neighbors(world, frm: torch.Tensor, to: torch.Tensor) -> torch.Tensor:
-    """Unique (a < b) neighbour pairs, int32 (k, 2)."""
+def neighbors(world, frm: torch.Tensor, to: torch.Tensor, pos: torch.Tensor | None = None) -> torch.Tensor:
+    """Unique (a < b) neighbour pairs, int32 (k, 2). ``pos`` defaults to the world's cell
+    positions (a domain-decomposed world appends ghost cells of its neighbours)."""
     if _is_gpu(world):
-        return _hip().neighbors(world, frm, to)
-    pos = world.cell_positions.to(torch.int32).contiguous()
-    out = native.host().get_neighbors(_np(frm.to(torch.int32)), _np(to.to(torch.int32)), _np(pos), int(world.map_size))
+        n = None if pos is None else int(pos.size(0))
+        return _hip().neighbors(world, frm, to, pos=pos, n=n)
+    if pos is None:
+        pos = world.cell_positions
+    pos = pos.to(torch.int32).contiguous()
+    R, C, _, _, wrap = geom(world)
+    out = native.host().get_neighbors(_np(frm.to(torch.int32)), _np(to.to(torch.int32)), _np(pos), R, C, bool(wrap))
     return torch.from_numpy(np.asarray(out))
 
 
@@ -143,19 +171,47 @@ def enzymatic_activity(world) -> None:
     pos = world.cell_positions.long()
     xs, ys = pos[:, 0], pos[:, 1]
     X0 = torch.cat([world.cell_molecules, mm[:, xs, ys].T], dim=1)
-    X1 = kin.integrate_signals(X0)
+    red = _mask_reducer(world)
+    X1 = kin.integrate_signals(X0) if red is None else kin.integrate_signals(X0, _reduce_mask=red)
     m = world.n_molecules
     mm[:, xs, ys] = X1[:, m:].T
     world.cell_molecules[:] = X1[:, :m]
 
 
+def _mask_reducer(world):
+    """Host-path hook: OR a part's iteration mask over all ranks of a domain-decomposed world."""
+    hook = getattr(world, "_allreduce_flags", None)
+    if hook is None:
+        return None
+
+    def reduce(mask: int) -> int:
+        flags = torch.tensor([(mask >> i) & 1 for i in range(4)], dtype=torch.int32)
+        hook(flags)
+        return sum(1 << i for i, v in enumerate(flags.tolist()) if v)
+
+    return reduce
+
+
 def diffuse(world) -> None:
+    """Stencil over the owned rows -> (global) per-molecule mass totals -> correction + clamp.
+    A domain-decomposed world refreshes its halo rows first and all-reduces the totals."""
     mm = _molmap(world)
     if mm.is_cuda:
         return _hip().diffuse(world)
+    R, C, r_lo, r_hi, wrap = geom(world)
+    halo = getattr(world, "_exchange_map_halo", None)
+    if halo is not None:
+        halo()
     a = [float(w[0]) for w in world._diffusion]
     b = [float(w[1]) for w in world._diffusion]
-    native.host().diffuse(mm.numpy(), a, b)
+    out = torch.empty_like(mm)
+    totals = native.host().diffuse_stencil(mm.numpy(), out.numpy(), a, b, [1.0] * len(a), r_lo, r_hi, bool(wrap))
+    tot = torch.from_numpy(np.asarray(totals))
+    reduce = getattr(world, "_allreduce_totals", None)
+    if reduce is not None:
+        reduce(tot)
+    n_pix = float(getattr(world, "_n_pix_global", (r_hi - r_lo) * C))
+    native.host().diffuse_correct(mm.numpy(), out.numpy(), tot.numpy(), n_pix, r_lo, r_hi)
 
 
 def permeate(world) -> None:

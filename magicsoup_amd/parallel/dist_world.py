@@ -1,0 +1,617 @@
+"""A World domain-decomposed over the ranks of a torch.distributed group.
+
+The reference simulates one map in one process (``python/magicsoup/world.py``); it has no multi-GPU
+path. Here the map's x axis is cut into ``world_size`` strips of ``H = map_size / world_size`` rows,
+one per rank (one process per MI355X, RCCL over xGMI; ``gloo`` for CPU runs). Each rank holds
+
+* the molecule map of its strip plus one halo row on each side: ``(m, H + 2, map_size)``,
+* the occupancy map in the same shape, and
+* the cells whose pixels lie in its strip (local x in ``1..H``).
+
+The global map is still a torus: rank 0's upper halo is rank ``N - 1``'s last row. Everything that
+only touches a cell and its own pixel (integration, permeation, degradation, mutation, kill, spawn)
+runs locally. What couples ranks:
+
+* diffusion: the halo rows are refreshed before the stencil (two row exchanges per step) and the
+  per-molecule mass totals of the correction are all-reduced so the global map conserves mass;
+* integration: the equilibrium-damping early exit is the reference's ``torch.any`` over all cells
+  (kinetics.py:837), so the four per-part iteration flags are MAX-all-reduced between parts;
+* division / movement into a neighbour's boundary row: a claim protocol. Each rank places its
+  cells as usual, treating the halo rows (refreshed occupancy) as candidates. Claims into a halo row
+  are sent with the full cell record to the owner, which accepts a claim if the pixel is still free
+  after its own placements and appends the cell; the claimer then commits (splits the parent /
+  drops the emigrant). A rejected cell does not divide / move this step.
+* recombination across a strip boundary: each rank receives its lower neighbour's boundary-row
+  cells as ghosts, recombines pairs that include them, and sends the ghosts' new genomes back.
+
+Per-cell RNG streams differ per rank, so a run is reproducible for a fixed rank count but not
+bit-identical to a single-process run.
+"""
+from __future__ import annotations
+
+import copy
+import random
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+
+from magicsoup_amd.models.world import World
+from magicsoup_amd.ops import world_ops
+
+_U8 = torch.uint8
+
+
+def _pack(cols: list[torch.Tensor], k: int) -> torch.Tensor:
+    """Byte-concatenate per-row columns into a (k, B) uint8 record block."""
+    parts = [c.contiguous().view(_U8).reshape(k, -1) for c in cols]
+    return torch.cat(parts, dim=1) if parts else torch.zeros(k, 0, dtype=_U8)
+
+
+def _unpack(buf: torch.Tensor, specs: list[tuple[torch.dtype, int]]) -> list[torch.Tensor]:
+    """Inverse of :func:`_pack` for columns of (dtype, elements per row)."""
+    k = int(buf.size(0))
+    out, o = [], 0
+    for dt, n in specs:
+        nb = n * torch.empty(0, dtype=dt).element_size()
+        col = buf[:, o : o + nb].contiguous().view(dt)
+        out.append(col.reshape(k) if n == 1 and dt != _U8 else col.reshape(k, n))
+        o += nb
+    return out
+
+
+def _copy_maps(dst: World, src: World) -> None:
+    """Give ``dst`` the genetics and kinetics parameter maps of ``src`` (on dst's device)."""
+    dst.genetics = copy.deepcopy(src.genetics)
+    kin, dev = dst.kinetics, torch.device(dst.device)
+    for name in ("km_map", "vmax_map", "sign_map", "hill_map", "reaction_map", "transport_map", "effector_map"):
+        mp = copy.deepcopy(getattr(src.kinetics, name))
+        for attr, val in list(vars(mp).items()):
+            if isinstance(val, torch.Tensor):
+                setattr(mp, attr, val.to(dev))
+        setattr(kin, name, mp)
+
+
+class DistributedWorld(World):
+    """:class:`~magicsoup_amd.World` over the ranks of ``group`` (default: the whole job).
+
+    Constructor arguments are those of ``World`` (``map_size`` is the global map size and must be a
+    multiple of the number of ranks with at least 2 rows per rank). Every rank must call every
+    method collectively (same order, same arguments apart from local cell indices).
+
+    Local state (``cell_positions`` in local rows ``1..H``, ``molecule_map`` / ``cell_map`` with
+    halo rows) is what the kernels work on; :meth:`global_positions`, :meth:`owned_molecule_map`,
+    :meth:`gather` and :meth:`scatter_from` convert to and from the global picture.
+    """
+
+    def __init__(self, *args, group=None, **kwargs):
+        if not dist.is_initialized():
+            raise RuntimeError("DistributedWorld needs an initialised torch.distributed process group")
+        g = self.__dict__
+        g["group"] = group
+        g["rank"] = dist.get_rank(group)
+        g["world_size"] = dist.get_world_size(group)
+        map_size = kwargs.get("map_size", args[1] if len(args) > 1 else 128)
+        n = self.world_size
+        if map_size % n != 0 or map_size // n < 2:
+            raise ValueError(f"map_size={map_size} must be a multiple of {n} ranks with >= 2 rows per rank")
+        g["H"] = map_size // n
+        g["row0"] = self.rank * self.H
+        g["_up"] = dist.get_global_rank(group, (self.rank - 1) % n) if group is not None else (self.rank - 1) % n
+        g["_down"] = dist.get_global_rank(group, (self.rank + 1) % n) if group is not None else (self.rank + 1) % n
+        seed = kwargs.pop("seed", None)
+        if seed is not None:
+            kwargs["seed"] = int(seed) + 1_000_003 * self.rank  # independent streams per rank
+        # Genetics (codon maps) and Kinetics (parameter maps) are random draws from Python's
+        # `random`: every rank must hold the same ones, so build them from rank 0's stream
+        shared = [random.getrandbits(63) if self.rank == 0 else 0]
+        dist.broadcast_object_list(shared, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        own = random.getstate()
+        random.seed(shared[0])
+        try:
+            super().__init__(*args, **kwargs)
+        finally:
+            random.setstate(own)
+        g["_n_pix_global"] = map_size * map_size
+        g["_stage"] = dist.get_backend(group) == "gloo" and torch.device(self.device).type == "cuda"
+        g["migrated"] = {"divided_out": 0, "divided_in": 0, "moved_out": 0, "moved_in": 0, "rejected": 0}
+        if n > 1:
+            # hooks the op layer calls (World has them as None): halo refresh before the diffusion
+            # stencil, MAX of the integrator's iteration flags, SUM of the diffusion mass totals
+            g["_exchange_map_halo"] = self._do_exchange_map_halo
+            g["_allreduce_flags"] = self._do_allreduce_flags
+            g["_allreduce_totals"] = self._do_allreduce_totals
+            self._exchange_occupancy()  # first p2p call is collective on every rank
+            self._do_exchange_map_halo()
+
+    # ------------------------------------------------------------------ geometry
+    def _map_shape(self) -> tuple[int, int]:
+        if self.world_size == 1:
+            return self.map_size, self.map_size
+        return self.H + 2, self.map_size
+
+    def _geom(self) -> tuple[int, int, int, int, int]:
+        S = self.map_size
+        if self.world_size == 1:
+            return S, S, 0, S, 1
+        return self.H + 2, S, 1, self.H + 1, 0
+
+    @property
+    def _lo(self) -> int:
+        return 0 if self.world_size == 1 else 1
+
+    def global_positions(self) -> torch.Tensor:
+        """Cell positions in global map coordinates (int32 (n, 2))."""
+        pos = self.cell_positions.clone()
+        pos[:, 0] += self.row0 - self._lo
+        return pos
+
+    def owned_molecule_map(self) -> torch.Tensor:
+        """View (m, H, map_size) of the molecule map rows this rank owns."""
+        mm = self.molecule_map
+        return mm[:, self._lo : self._lo + self.H]
+
+    def owned_cell_map(self) -> torch.Tensor:
+        return self.cell_map[self._lo : self._lo + self.H]
+
+    # ------------------------------------------------------------------ communication
+    def _tensor_device(self) -> torch.device:
+        return self._molmap.device
+
+    def _exchange(self, to_up, to_down, from_down, from_up) -> None:
+        """One neighbour exchange: ``to_up`` arrives at the upper neighbour as its ``from_down``,
+        ``to_down`` at the lower one as its ``from_up``. ``None`` skips an op (the peer must skip
+        the matching one). Ops to the same peer are matched in issue order (RCCL) and by tag (gloo)."""
+        if self._stage:
+            return self._exchange_staged(to_up, to_down, from_down, from_up)
+        ops = []
+        if to_up is not None:
+            ops.append(dist.P2POp(dist.isend, to_up, self._up, self.group, 0))
+        if to_down is not None:
+            ops.append(dist.P2POp(dist.isend, to_down, self._down, self.group, 1))
+        if from_down is not None:
+            ops.append(dist.P2POp(dist.irecv, from_down, self._down, self.group, 0))
+        if from_up is not None:
+            ops.append(dist.P2POp(dist.irecv, from_up, self._up, self.group, 1))
+        if not ops:
+            return
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+
+    def _exchange_staged(self, to_up, to_down, from_down, from_up) -> None:
+        """gloo with device tensors (e.g. several ranks sharing one GPU in tests): via host copies."""
+        h = [None if t is None else t.cpu() for t in (to_up, to_down)]
+        r = [None if t is None else torch.empty(t.shape, dtype=t.dtype) for t in (from_down, from_up)]
+        self.__dict__["_stage"] = False
+        try:
+            self._exchange(h[0], h[1], r[0], r[1])
+        finally:
+            self.__dict__["_stage"] = True
+        for dst, src in zip((from_down, from_up), r):
+            if dst is not None:
+                dst.copy_(src)
+
+    def _all_reduce(self, t: torch.Tensor, op) -> None:
+        if self._stage:
+            h = t.cpu()
+            dist.all_reduce(h, op=op, group=self.group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op, group=self.group)
+
+    def _exchange_var(self, up: torch.Tensor | None, down: torch.Tensor | None, meta_up=(), meta_down=()):
+        """Exchange variable-size uint8 record blocks (k, B) with both neighbours. ``meta_*`` are
+        extra header ints (e.g. column widths). Returns ((block, meta) from down, (block, meta) from up)."""
+        dev = self._tensor_device()
+        nm = max(len(meta_up), len(meta_down))
+
+        def hdr(block, meta):
+            k, b = (0, 0) if block is None else (int(block.size(0)), int(block.size(1)))
+            return torch.tensor([k, b, *meta, *([0] * (nm - len(meta)))], dtype=torch.int64, device=dev)
+
+        h_up, h_dn = hdr(up, meta_up), hdr(down, meta_down)
+        r_dn, r_up = torch.empty_like(h_up), torch.empty_like(h_up)
+        self._exchange(h_up, h_dn, r_dn, r_up)
+        hd, hu = r_dn.tolist(), r_up.tolist()
+        s_up = up.reshape(-1) if up is not None and up.numel() else None
+        s_dn = down.reshape(-1) if down is not None and down.numel() else None
+        b_dn = torch.empty(hd[0] * hd[1], dtype=_U8, device=dev) if hd[0] * hd[1] else None
+        b_up = torch.empty(hu[0] * hu[1], dtype=_U8, device=dev) if hu[0] * hu[1] else None
+        self._exchange(s_up, s_dn, b_dn, b_up)
+
+        def block(b, h):
+            return torch.zeros(h[0], h[1], dtype=_U8, device=dev) if b is None else b.view(h[0], h[1])
+
+        return (block(b_dn, hd), hd[2:]), (block(b_up, hu), hu[2:])
+
+    def _do_exchange_map_halo(self) -> None:
+        """Refresh the molecule-map halo rows from the neighbours' boundary rows (raw buffer: a
+        pending degradation factor is identical on every rank and applied by the stencil)."""
+        if self.world_size == 1:
+            return
+        mm = self.__dict__["_molmap"]
+        H = self.H
+        sb = self.__dict__.get("_halo_bufs")
+        if sb is None or sb[0].shape != mm[:, 1].shape or sb[0].device != mm.device:
+            sb = tuple(torch.empty_like(mm[:, 1]) for _ in range(4))
+            self.__dict__["_halo_bufs"] = sb
+        s_up, s_dn, r_dn, r_up = sb
+        s_up.copy_(mm[:, 1])
+        s_dn.copy_(mm[:, H])
+        self._exchange(s_up, s_dn, r_dn, r_up)
+        mm[:, H + 1].copy_(r_dn)
+        mm[:, 0].copy_(r_up)
+
+    def _exchange_occupancy(self) -> None:
+        if self.world_size == 1:
+            return
+        cm = self.cell_map.view(_U8)
+        H = self.H
+        s_up, s_dn = cm[1].contiguous(), cm[H].contiguous()
+        r_dn, r_up = torch.empty_like(s_up), torch.empty_like(s_up)
+        self._exchange(s_up, s_dn, r_dn, r_up)
+        cm[H + 1].copy_(r_dn)
+        cm[0].copy_(r_up)
+
+    def _do_allreduce_flags(self, flags: torch.Tensor) -> None:
+        self._all_reduce(flags, dist.ReduceOp.MAX)
+
+    def _do_allreduce_totals(self, totals: torch.Tensor) -> None:
+        self._all_reduce(totals, dist.ReduceOp.SUM)
+
+    # ------------------------------------------------------------------ cell records
+    def _records(self, cells: torch.Tensor, ys: torch.Tensor, child: bool) -> tuple[torch.Tensor, tuple[int, int]]:
+        """Full records of ``cells`` landing on columns ``ys`` of a neighbour's boundary row: the
+        child of a division (half the molecules, divisions + 1, lifetime 0) or the cell itself."""
+        k = int(cells.numel())
+        gw, lw = int(self._genomes.width), int(self._labels.width)
+        if k == 0:
+            return None, (gw, lw)
+        mol = self.cell_molecules[cells]
+        div = self.cell_divisions[cells]
+        life = self.cell_lifetimes[cells]
+        if child:
+            mol = mol * 0.5
+            div = div + 1
+            life = torch.zeros_like(life)
+        cols = [
+            ys.to(torch.int32),
+            self._genomes.lens[cells],
+            self._labels.lens[cells],
+            div.to(torch.int32),
+            life.to(torch.int32),
+            mol.to(torch.float32),
+            self._labels.data[cells],
+            self._genomes.data[cells],
+        ]
+        return _pack(cols, k), (gw, lw)
+
+    def _unpack_records(self, buf: torch.Tensor, meta) -> dict:
+        gw, lw = int(meta[0]), int(meta[1])
+        m = self.n_molecules
+        i32 = torch.int32
+        ys, glen, llen, div, life, mol, lab, gen = _unpack(
+            buf, [(i32, 1), (i32, 1), (i32, 1), (i32, 1), (i32, 1), (torch.float32, m), (_U8, lw), (_U8, gw)]
+        )
+        return dict(ys=ys, glen=glen, llen=llen, div=div, life=life, mol=mol, lab=lab, gen=gen)
+
+    def _append_records(self, r: dict, row: int, keep: torch.Tensor) -> int:
+        """Append the accepted records (bool mask ``keep``) as new cells on local row ``row``."""
+        idx = torch.nonzero(keep).flatten()
+        k = int(idx.numel())
+        if k == 0:
+            return 0
+        n0 = self.n_cells
+        self._grow(k)
+        self._genomes.append_packed(r["gen"][idx], r["glen"][idx])
+        self._labels.append_packed(r["lab"][idx], r["llen"][idx])
+        new = torch.arange(n0, n0 + k, device=self.device)
+        ys = r["ys"][idx]
+        pos = torch.stack([torch.full_like(ys, row), ys], dim=1)
+        self._place(new, pos)
+        self.cell_molecules[new] = r["mol"][idx]
+        self.cell_divisions[new] = r["div"][idx]
+        self.cell_lifetimes[new] = r["life"][idx]
+        self._update_params_rows(new)
+        return k
+
+    def _migrate(self, rec_up, rec_dn) -> tuple[torch.Tensor, torch.Tensor, int]:
+        """Send claim records to the neighbours, accept / append incoming ones, and return the
+        accept flags of our own claims (to up, to down) and the number of cells received."""
+        (b_dn, m_dn), (b_up, m_up) = self._exchange_var(rec_up[0], rec_dn[0], rec_up[1], rec_dn[1])
+        cmap = self.cell_map
+        got = 0
+        flags = {}
+        # records from the upper neighbour land on our first row, from the lower one on our last
+        for key, buf, meta, row in (("up", b_up, m_up, 1), ("dn", b_dn, m_dn, self.H)):
+            if buf.size(0) == 0:
+                flags[key] = None
+                continue
+            r = self._unpack_records(buf, meta)
+            ys = r["ys"].long()
+            ok = ~cmap[row, ys]
+            got += self._append_records(r, row, ok)
+            flags[key] = ok.to(_U8)
+        k_up = 0 if rec_up[0] is None else int(rec_up[0].size(0))
+        k_dn = 0 if rec_dn[0] is None else int(rec_dn[0].size(0))
+        dev = self._tensor_device()
+        f_up = torch.empty(k_up, dtype=_U8, device=dev) if k_up else None
+        f_dn = torch.empty(k_dn, dtype=_U8, device=dev) if k_dn else None
+        # verdicts on records from up go back up (they arrive there as from-down), and vice versa
+        self._exchange(flags["up"], flags["dn"], f_dn, f_up)
+        acc_up = f_up.bool() if k_up else torch.zeros(0, dtype=torch.bool, device=dev)
+        acc_dn = f_dn.bool() if k_dn else torch.zeros(0, dtype=torch.bool, device=dev)
+        return acc_up, acc_dn, got
+
+    # ------------------------------------------------------------------ lifecycle overrides
+    def divide_cells_t(self, cell_idxs) -> tuple[torch.Tensor, torch.Tensor]:
+        """Division (collective). Children landing in a neighbour's boundary row are created on
+        that rank; the returned pairs cover local children only (counts in ``self.migrated``)."""
+        if self.world_size == 1:
+            return super().divide_cells_t(cell_idxs)
+        idxs = self._idx_tensor(cell_idxs)
+        dev = self.device
+        empty = torch.zeros(0, dtype=torch.long, device=dev)
+        self._exchange_occupancy()
+        if idxs.numel():
+            parents, cpos = world_ops.divide_placement(self, idxs)
+            parents = parents.to(dev)
+            cpos = cpos.to(dev)
+        else:
+            parents, cpos = empty, torch.zeros(0, 2, dtype=torch.int32, device=dev)
+        row = cpos[:, 0]
+        up, dn = row == 0, row == self.H + 1
+        loc = ~(up | dn)
+        p_up, p_dn = parents[up], parents[dn]
+        lp = cpos[loc].long()
+        self.cell_map[lp[:, 0], lp[:, 1]] = True  # own children first when arbitrating claims
+        rec_up = self._records(p_up, cpos[up, 1], child=True)
+        rec_dn = self._records(p_dn, cpos[dn, 1], child=True)
+        acc_up, acc_dn, got = self._migrate(rec_up, rec_dn)
+        # halo claims are scratch: the halo rows are refreshed before their next use
+        self.cell_map[0] = False
+        self.cell_map[self.H + 1] = False
+        # exported children: the parent keeps half, both get divisions + 1 and lifetime 0
+        out = torch.cat([p_up[acc_up], p_dn[acc_dn]])
+        if out.numel():
+            self.cell_molecules[out] *= 0.5
+            self.cell_divisions[out] += 1
+            self.cell_lifetimes[out] = 0
+        mig = self.migrated
+        mig["divided_out"] += int(out.numel())
+        mig["divided_in"] += got
+        mig["rejected"] += int(acc_up.numel() + acc_dn.numel() - out.numel())
+        parents, cpos = parents[loc], cpos[loc]
+        k = int(parents.numel())
+        if k == 0:
+            return empty, empty
+        n0 = self.n_cells
+        self._grow(k)
+        children = torch.arange(n0, n0 + k, device=dev)
+        self._genomes.append_rows_from(parents)
+        self._labels.append_rows_from(parents)
+        self.kinetics.copy_cell_params(from_idxs=parents, to_idxs=children)
+        self._place(children, cpos)
+        world_ops.split_cells(self, parents, children)
+        return parents, children
+
+    def move_cells(self, cell_idxs=None):
+        """Movement (collective). Cells moving into a neighbour's boundary row migrate to it."""
+        if self.world_size == 1:
+            return super().move_cells(cell_idxs)
+        if cell_idxs is None:
+            cell_idxs = torch.arange(self.n_cells, device=self.device)
+        idxs = self._idx_tensor(cell_idxs)
+        dev = self.device
+        self._exchange_occupancy()
+        if idxs.numel():
+            moved, npos = world_ops.move_placement(self, idxs)
+            moved, npos = moved.to(dev), npos.to(dev)
+        else:
+            moved, npos = torch.zeros(0, dtype=torch.long, device=dev), torch.zeros(0, 2, dtype=torch.int32, device=dev)
+        row = npos[:, 0]
+        up, dn = row == 0, row == self.H + 1
+        loc = ~(up | dn)
+        m_up, m_dn = moved[up], moved[dn]
+        # local moves first, so the owner's arbitration sees its final occupancy
+        if bool(loc.any()):
+            mv = moved[loc]
+            old = self.cell_positions[mv].long()
+            self.cell_map[old[:, 0], old[:, 1]] = False
+            self._place(mv, npos[loc])
+        rec_up = self._records(m_up, npos[up, 1], False)
+        rec_dn = self._records(m_dn, npos[dn, 1], False)
+        acc_up, acc_dn, got = self._migrate(rec_up, rec_dn)
+        self.cell_map[0] = False
+        self.cell_map[self.H + 1] = False
+        gone = torch.cat([m_up[acc_up], m_dn[acc_dn]])
+        mig = self.migrated
+        mig["moved_in"] += got
+        mig["moved_out"] += int(gone.numel())
+        mig["rejected"] += int(acc_up.numel() + acc_dn.numel() - gone.numel())
+        if gone.numel():
+            self._remove(gone)
+
+    def _remove(self, idxs: torch.Tensor) -> None:
+        """Drop cells that emigrated (free their pixels, no molecule spill)."""
+        pos = self.cell_positions[idxs].long()
+        self.cell_map[pos[:, 0], pos[:, 1]] = False
+        keep = torch.ones(self.n_cells, dtype=torch.bool, device=self.device)
+        keep[idxs] = False
+        self._compact(torch.nonzero(keep).flatten(), keep)
+
+    def reposition_cells(self, cell_idxs=None):
+        """Move cells to random free pixels of this rank's strip (cells do not change rank)."""
+        return super().reposition_cells(cell_idxs)
+
+    # ------------------------------------------------------------------ recombination
+    def recombinate_cells(self, cell_idxs: list[int] | None = None, p: float = 1e-7):
+        """Recombination between neighbouring cells (collective), including pairs across strip
+        boundaries: a rank recombines its last-row cells with ghosts of the lower neighbour's first
+        row and returns the ghosts' new genomes to their owner."""
+        if self.world_size == 1:
+            return super().recombinate_cells(cell_idxs, p)
+        dev = self.device
+        n = self.n_cells
+        pos = self.cell_positions
+        # ghosts for the upper neighbour: our first-row cells
+        first = torch.nonzero(pos[:, 0] == 1).flatten() if n else torch.zeros(0, dtype=torch.long, device=dev)
+        if cell_idxs is not None:
+            allowed = torch.zeros(n, dtype=torch.bool, device=dev)
+            allowed[self._idx_tensor(cell_idxs)] = True
+            first = first[allowed[first]]
+        k = int(first.numel())
+        send = None
+        if k:
+            send = _pack([first.to(torch.int32), pos[first, 1], self._genomes.lens[first], self._genomes.data[first]], k)
+        (g_buf, g_meta), _ = self._exchange_var(send, None, (int(self._genomes.width),), (0,))
+        ng = int(g_buf.size(0))
+        changed_local = torch.zeros(0, dtype=torch.long, device=dev)
+        upd = None
+        if n + ng >= 2:
+            idxs = torch.arange(n, device=dev) if cell_idxs is None else self._idx_tensor(cell_idxs)
+            if ng:
+                gi, gy, gl, gd = _unpack(g_buf, [(torch.int32, 1), (torch.int32, 1), (torch.int32, 1), (_U8, int(g_meta[0]))])
+                gpos = torch.stack([torch.full_like(gy, self.H + 1), gy], dim=1)
+                all_pos = torch.cat([pos, gpos]).contiguous()
+                to = torch.cat([idxs, torch.arange(n, n + ng, device=dev)])
+                pairs = world_ops.neighbors(self, idxs, to, pos=all_pos) if idxs.numel() else None
+                self._genomes.append_packed(gd, gl)  # ghost rows n .. n+ng-1 (temporary)
+            else:
+                pairs = self.get_neighbors_t(idxs) if idxs.numel() else None
+            try:
+                if pairs is not None and pairs.size(0):
+                    changed = world_ops.recombinations(self, pairs.to(dev), p).to(dev)
+                    changed_local = changed[changed < n]
+                    cg = changed[changed >= n] - n
+                    if cg.numel():
+                        rows = cg + n
+                        upd = _pack([gi[cg], self._genomes.lens[rows], self._genomes.data[rows]], int(cg.numel()))
+            finally:
+                if ng:
+                    self._genomes.n = n
+                    self._genomes.version += 1
+        # ghost updates go back down to their owners
+        _, (u_buf, u_meta) = self._exchange_var(None, upd, (0,), (int(self._genomes.width),))
+        if u_buf.size(0):
+            ui, ul, ud = _unpack(u_buf, [(torch.int32, 1), (torch.int32, 1), (_U8, int(u_meta[0]))])
+            rows = ui.long()
+            self._genomes.set_rows(rows, ud, ul)
+            changed_local = torch.cat([changed_local, rows])
+        if changed_local.numel():
+            self._update_params_rows(torch.unique(changed_local))
+
+    # ------------------------------------------------------------------ global views / persistence
+    def gather(self, dst: int = 0) -> World | None:
+        """Assemble the global state as a single-process CPU :class:`World` on rank ``dst``
+        (``None`` elsewhere). Proteomes are re-derived from the genomes."""
+        mm = self.owned_molecule_map().cpu()
+        part = {
+            "genomes": self.cell_genomes.tolist(),
+            "labels": self.cell_labels.tolist(),
+            "pos": self.global_positions().cpu(),
+            "mol": self.cell_molecules.cpu(),
+            "life": self.cell_lifetimes.cpu(),
+            "div": self.cell_divisions.cpu(),
+            "mm": mm,
+        }
+        parts = [None] * self.world_size if self.rank == dst else None
+        dist.gather_object(part, parts, dst=dist.get_global_rank(self.group, dst) if self.group else dst, group=self.group)
+        if self.rank != dst:
+            return None
+        w = World(
+            chemistry=self.chemistry,
+            map_size=self.map_size,
+            abs_temp=self.abs_temp,
+            mol_map_init="zeros",
+            start_codons=self.genetics.start_codons,
+            stop_codons=self.genetics.stop_codons,
+            device="cpu",
+        )
+        _copy_maps(w, self)
+        w.molecule_map = torch.cat([q["mm"] for q in parts], dim=1)
+        genomes = [g for q in parts for g in q["genomes"]]
+        n = len(genomes)
+        if n:
+            w._grow(n)
+            w._genomes.append_strings(genomes)
+            w._labels.append_strings([lab for q in parts for lab in q["labels"]])
+            pos = torch.cat([q["pos"] for q in parts])
+            w._place(torch.arange(n), pos)
+            w.cell_molecules[:] = torch.cat([q["mol"] for q in parts])
+            w.cell_lifetimes[:] = torch.cat([q["life"] for q in parts])
+            w.cell_divisions[:] = torch.cat([q["div"] for q in parts])
+            w._update_params_rows(torch.arange(n))
+        return w
+
+    def adopt_maps(self, world: World) -> None:
+        """Use the genetics (codon maps) and kinetics parameter maps of ``world``."""
+        _copy_maps(self, world)
+
+    def scatter_from(self, world: World, maps: bool = True, params: bool = True) -> None:
+        """Replace this rank's state by its strip of a global ``world`` (same on every rank);
+        with ``maps`` also adopt its genetics / kinetics maps."""
+        S, H, lo = self.map_size, self.H, self._lo
+        if world.map_size != S:
+            raise ValueError("map sizes differ")
+        if maps:
+            self.adopt_maps(world)
+        self.kill_cells_local_all()
+        mm = self.__dict__["_molmap"]
+        mm.zero_()
+        mm[:, lo : lo + H] = world.molecule_map[:, self.row0 : self.row0 + H].to(mm.device)
+        self.__dict__["_pending_scale"] = None
+        gpos = world.cell_positions.long().cpu()
+        mine = torch.nonzero((gpos[:, 0] >= self.row0) & (gpos[:, 0] < self.row0 + H)).flatten()
+        k = int(mine.numel())
+        if k:
+            sel = mine.tolist()
+            self._grow(k)
+            self._genomes.append_strings(world._genomes.to_strings(sel))
+            self._labels.append_strings(world._labels.to_strings(sel))
+            lpos = gpos[mine].clone()
+            lpos[:, 0] += lo - self.row0
+            new = torch.arange(k, device=self.device)
+            self._place(new, lpos.to(torch.int32))
+            self.cell_molecules[:] = world.cell_molecules[mine.to(world.cell_molecules.device)].to(self.device)
+            self.cell_lifetimes[:] = world.cell_lifetimes[mine.to(world.cell_lifetimes.device)].to(self.device)
+            self.cell_divisions[:] = world.cell_divisions[mine.to(world.cell_divisions.device)].to(self.device)
+            if params:
+                self._update_params_rows(new)
+        if self.world_size > 1:
+            self._do_exchange_map_halo()
+
+    def kill_cells_local_all(self) -> None:
+        """Remove every local cell without spilling molecules (state reset)."""
+        if self.n_cells:
+            self._remove(torch.arange(self.n_cells, device=self.device))
+
+    def save_state(self, statedir: Path):
+        """Collective: rank 0 writes the global state in the reference's format."""
+        w = self.gather()
+        if w is not None:
+            w.save_state(Path(statedir))
+        dist.barrier(group=self.group)
+
+    def load_state(self, statedir: Path, ignore_cell_params: bool = False):
+        """Collective: every rank reads the global state and keeps its strip."""
+        w = World(
+            chemistry=self.chemistry,
+            map_size=self.map_size,
+            abs_temp=self.abs_temp,
+            mol_map_init="zeros",
+            start_codons=self.genetics.start_codons,
+            stop_codons=self.genetics.stop_codons,
+            device="cpu",
+        )
+        w.load_state(Path(statedir), ignore_cell_params=True)
+        self.scatter_from(w, maps=False, params=not ignore_cell_params)
+
+    def __getstate__(self):
+        raise TypeError("a DistributedWorld is bound to its process group; use gather() or save_state()")
+
+    def __repr__(self) -> str:
+        return (
+            f"DistributedWorld(map_size:{self.map_size!r},rank:{self.rank}/{self.world_size},"
+            f"rows:{self.row0}..{self.row0 + self.H - 1},device:{self.device!r})"
+        )
