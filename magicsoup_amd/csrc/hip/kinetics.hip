@@ -405,7 +405,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t 
                uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb, uintptr_t Vmax, uintptr_t Ke, uintptr_t cell_mols,
                uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
                uintptr_t masks, uintptr_t overflow, const std::vector<float>& trims, int n_iters, int part_begin,
-               int part_end, uintptr_t stream) {
+               int part_end, bool scatter, uintptr_t stream) {
   if (c <= 0) return;
   if (n_iters < 0 || n_iters > ms::kEqIters) throw std::invalid_argument("n_iters must be in 0..4");
   const int nparts = (int)trims.size();
@@ -459,7 +459,9 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t 
     else integrate_part_kernel<64><<<grid, threads, lds, st>>>(a);
     MS_LAUNCH_CHECK();
   }
-  if (part_end == nparts && nparts > 0 && part_begin < part_end) {
+  // the write-back selects the last part's snapshot by its (possibly all-reduced) flags, so a
+  // domain-decomposed caller runs it as a separate call once those flags are global
+  if (scatter && part_end == nparts && nparts > 0) {
     const int last = nparts - 1;
     integrate_scatter_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(
         c, s, m, R, C, snaps[last & 1], mk + ms::kEqIters * last, n_iters, P_<int32_t>(positions),

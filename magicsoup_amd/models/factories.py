@@ -219,10 +219,10 @@ class RegulatoryDomainFact:
         spec = dct["spec"]
         return cls(
             effector=Molecule.from_name(spec["effector"]),
-            km=spec["km"],
+            km=spec.get("km"),
             hill=spec.get("hill"),
             is_inhibiting=spec.get("is_inhibiting"),
-            is_transmembrane=spec["is_transmembrane"],
+            is_transmembrane=bool(spec.get("is_transmembrane", False)),
         )
 
     def __repr__(self) -> str:

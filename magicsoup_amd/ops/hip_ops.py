@@ -89,15 +89,16 @@ def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n
     ]
     nparts = len(trims)
     if flags_hook is None:
-        _m().integrate(*args, 0, nparts, _stream())
+        _m().integrate(*args, 0, nparts, True, _stream())
     else:
-        # domain-decomposed world: all-reduce each part's iteration flags before the next part reads
-        # them, reproducing the reference's `torch.any` over the whole population
+        # domain-decomposed world: all-reduce each part's iteration flags before the next part (or
+        # the final write-back) reads them, reproducing the reference's `torch.any` over the whole
+        # population
         for part in range(nparts):
-            _m().integrate(*args, part, part + 1, _stream())
+            _m().integrate(*args, part, part + 1, False, _stream())
             flags_hook(masks[_EQ * part : _EQ * (part + 1)])
         if nparts:
-            _m().integrate(*args, nparts, nparts, _stream())
+            _m().integrate(*args, nparts, nparts, True, _stream())
     return masks
 
 

@@ -228,3 +228,17 @@ def test_mutations_on_gpu_change_genomes():
     assert changed > 300
     w.mutate_cells(p=0.05, p_indel=1.0, p_del=1.0)
     assert all(len(g) <= len(b) for g, b in zip(w.cell_genomes, after))
+
+
+def test_integrator_split_parts_match_fused():
+    """The per-part launches a domain-decomposed world uses (flags all-reduced between parts)
+    reproduce the fused single launch exactly."""
+    wa = _world("cuda", n=500)
+    wa2 = _world("cuda", n=500)
+    calls = []
+    wa2.__dict__["_allreduce_flags"] = lambda flags: calls.append(int(flags.numel()))
+    wa.enzymatic_activity()
+    wa2.enzymatic_activity()
+    assert calls == [4, 4, 4]
+    assert torch.equal(wa.cell_molecules, wa2.cell_molecules)
+    assert torch.equal(wa.molecule_map, wa2.molecule_map)

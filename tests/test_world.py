@@ -1,0 +1,414 @@
+"""World behaviours on the CPU path (reference tests/fast/test_world.py). The GPU path is checked
+against this one in tests/test_gpu_kernels.py."""
+import tempfile
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+import magicsoup_amd as ms
+from magicsoup_amd.examples.wood_ljungdahl import MOLECULES
+
+
+def _chem(mols=None, reactions=()):
+    return ms.Chemistry(molecules=list(mols or MOLECULES), reactions=list(reactions))
+
+
+def _diffuse_oracle(x: np.ndarray, rate: float) -> np.ndarray:
+    """3x3 toroidal stencil with the reference's weights (world.py:948-971), mass-corrected, >= 0."""
+    rate = min(abs(rate), 1.0)
+    if rate == 0:
+        return x.copy()
+    d = 1 / rate
+    a = 1 / (d + 8)
+    b = d * a
+    b = b + 1.0 - (8 * a + b)
+    nb = sum(np.roll(np.roll(x, i, 0), j, 1) for i in (-1, 0, 1) for j in (-1, 0, 1) if (i, j) != (0, 0))
+    y = b * x + a * nb
+    y += (x.sum() - y.sum()) / x.size
+    return np.maximum(y, 0.0)
+
+
+# --------------------------------------------------------------------------------------------- physics
+def test_diffusion_point_sources():
+    m0 = ms.Molecule("WTdiffA", 10, diffusivity=0.0)
+    m1 = ms.Molecule("WTdiffB", 10, diffusivity=0.5)
+    w = ms.World(chemistry=_chem([m0, m1]), map_size=5)
+    mm = torch.zeros(2, 5, 5)
+    mm[0, 1, 3] = 2.0
+    mm[1, 0, 0] = 1.0
+    mm[1, 4, 2] = 1.0
+    w.molecule_map = mm
+    w.diffuse_molecules()
+    out = w.molecule_map
+    assert out.shape == (2, 5, 5)
+    assert torch.equal(out[0], mm[0])  # diffusivity 0: unchanged
+    # rate 0.5: a = 0.1 to each neighbour, b = 0.2 stays
+    exp = torch.zeros(5, 5)
+    for x, y in ((0, 0), (4, 2)):
+        for dx in (-1, 0, 1):
+            for dy in (-1, 0, 1):
+                exp[(x + dx) % 5, (y + dy) % 5] += 0.2 if dx == dy == 0 else 0.1
+    assert torch.allclose(out[1], exp, atol=1e-7)
+
+
+@pytest.mark.parametrize("size", [3, 8, 33])
+@pytest.mark.parametrize("rate", [0.01, 0.3, 1.0])
+def test_diffusion_matches_numpy_oracle(size, rate):
+    mol = ms.Molecule(f"WTdiff{size}_{int(rate * 100)}", 10, diffusivity=rate)
+    w = ms.World(chemistry=_chem([mol]), map_size=size)
+    x = w.molecule_map[0].double().numpy().copy()
+    for _ in range(3):
+        w.diffuse_molecules()
+        x = _diffuse_oracle(x, rate)
+    assert np.allclose(w.molecule_map[0].numpy(), x, rtol=1e-5, atol=1e-5)
+    assert abs(w.molecule_map[0].double().sum().item() - x.sum()) / x.sum() < 1e-6
+
+
+def test_degradation_scales_map_and_cells():
+    w = ms.World(chemistry=_chem(MOLECULES[:2]), map_size=5)
+    w.spawn_cells([ms.random_genome(100)])
+    w._mol_degrads = [0.8, 0.5]
+    mm = w.molecule_map.clone()
+    cm = w.cell_molecules.clone()
+    w.degrade_molecules()
+    assert torch.allclose(w.molecule_map[0], mm[0] * 0.8)
+    assert torch.allclose(w.molecule_map[1], mm[1] * 0.5)
+    assert torch.allclose(w.cell_molecules, cm * torch.tensor([0.8, 0.5]))
+
+
+def test_degradation_rate_from_half_life():
+    mol = ms.Molecule("WThalf", 10, half_life=4)
+    w = ms.World(chemistry=_chem([mol]), map_size=4)
+    before = w.molecule_map.clone()
+    for _ in range(4):
+        w.degrade_molecules()
+    assert torch.allclose(w.molecule_map, before * 0.5, rtol=1e-5)
+
+
+def test_permeation_exchanges_towards_equilibrium():
+    mol = ms.Molecule("WTperm", 10, permeability=1.0)
+    w = ms.World(chemistry=_chem([mol]), map_size=4, mol_map_init="zeros")
+    w.spawn_cells([ms.random_genome(50)])
+    x, y = w.cell_positions[0].tolist()
+    w.cell_molecules[0, 0] = 6.0
+    w.molecule_map[0, x, y] = 0.0
+    from magicsoup_amd.ops import world_ops
+
+    world_ops.permeate(w)
+    # p = 1 / (1/1 + 1) = 0.5 of the difference moves
+    assert torch.isclose(w.cell_molecules[0, 0], torch.tensor(3.0))
+    assert torch.isclose(w.molecule_map[0, x, y], torch.tensor(3.0))
+
+
+# --------------------------------------------------------------------------------------------- lifecycle
+def test_spawn_cells_take_half_of_their_pixel():
+    w = ms.World(chemistry=_chem(MOLECULES[:2]), map_size=5)
+    mm0 = w.molecule_map.clone()
+    for batch in ([ms.random_genome(400) for _ in range(3)], ["", ""], [ms.random_genome(90), "", ms.random_genome(90)]):
+        w.spawn_cells(genomes=batch)
+        xs, ys = w.cell_positions[:, 0].long(), w.cell_positions[:, 1].long()
+        assert torch.allclose(w.molecule_map[:, xs, ys], mm0[:, xs, ys] / 2)
+        assert torch.allclose(w.cell_molecules.T, mm0[:, xs, ys] / 2)
+    assert w.n_cells == 8
+    assert int(w.cell_map.sum()) == 8
+    assert len(set(w.cell_labels)) == 8
+    assert (w.cell_lifetimes == 0).all() and (w.cell_divisions == 0).all()
+
+
+def test_spawn_more_cells_than_pixels():
+    w = ms.World(chemistry=_chem(MOLECULES[:2]), map_size=3)
+    idxs = w.spawn_cells([ms.random_genome(50) for _ in range(20)])
+    assert len(idxs) == 9 and w.n_cells == 9
+    assert bool(w.cell_map.all())
+    assert w.spawn_cells([ms.random_genome(50)]) == []
+
+
+def test_add_cells_keeps_their_state():
+    w = ms.World(chemistry=_chem(MOLECULES[:2]), map_size=6)
+    mm0 = w.molecule_map.clone()
+    genomes = [ms.random_genome(s) for s in (400, 200, 100)]
+    cells = [
+        ms.Cell(world=w, label="L0", genome=genomes[0], int_molecules=torch.tensor([1.5, 0.5])),
+        ms.Cell(world=w, label="L1", genome=genomes[1], int_molecules=torch.tensor([0.25, 2.0])),
+        ms.Cell(world=w, label="L2", genome=genomes[2], int_molecules=torch.tensor([3.0, 0.0]), n_steps_alive=7,
+                n_divisions=2),
+    ]
+    assert w.add_cells(cells[:2]) == [0, 1]
+    assert w.add_cells(cells[2:]) == [2]
+    xs, ys = w.cell_positions[:, 0].long(), w.cell_positions[:, 1].long()
+    assert torch.equal(w.molecule_map[:, xs, ys], mm0[:, xs, ys])  # no pickup
+    assert torch.equal(w.cell_molecules, torch.tensor([[1.5, 0.5], [0.25, 2.0], [3.0, 0.0]]))
+    assert w.cell_lifetimes.tolist() == [0, 0, 7]
+    assert w.cell_divisions.tolist() == [0, 0, 2]
+    assert list(w.cell_genomes) == genomes
+    assert list(w.cell_labels) == ["L0", "L1", "L2"]
+
+
+def test_divide_cells_split_and_inherit():
+    w = ms.World(chemistry=_chem(MOLECULES[:2]), map_size=6)
+    idxs = w.spawn_cells([ms.random_genome(500) for _ in range(3)])
+    before = w.cell_molecules.clone()
+    pairs = w.divide_cells(idxs)
+    assert sorted(p for p, _ in pairs) == [0, 1, 2]
+    assert sorted(c for _, c in pairs) == [3, 4, 5]
+    assert int(w.cell_map.sum()) == 6
+    for p, c in pairs:
+        assert torch.allclose(w.cell_molecules[p], before[p] / 2)
+        assert torch.equal(w.cell_molecules[c], w.cell_molecules[p])
+        assert w.cell_genomes[p] == w.cell_genomes[c]
+        assert w.cell_labels[p] == w.cell_labels[c]
+        assert torch.equal(w.kinetics.N[p], w.kinetics.N[c])
+        px, py = w.cell_positions[p].tolist()
+        cx, cy = w.cell_positions[c].tolist()
+        assert ms.dist_1d(px, cx, 6) <= 1 and ms.dist_1d(py, cy, 6) <= 1
+
+
+def test_divide_on_full_maps():
+    w = ms.World(chemistry=_chem(MOLECULES[:2]), map_size=2)
+    idxs = w.spawn_cells([ms.random_genome(300) for _ in range(2)])
+    assert len(w.divide_cells(idxs)) == 2
+    assert int(w.cell_map.sum()) == 4
+    assert w.divide_cells(idxs) == []
+    w = ms.World(chemistry=_chem(MOLECULES[:2]), map_size=3)
+    w.spawn_cells([ms.random_genome(300) for _ in range(9)])
+    assert w.divide_cells(list(range(9))) == []
+
+
+def test_divisions_and_lifetimes_after_division():
+    w = ms.World(chemistry=_chem(), map_size=16)
+    w.spawn_cells([ms.random_genome(300) for _ in range(2)])
+    w.cell_divisions[0] = 3
+    w.cell_divisions[1] = 8
+    w.cell_lifetimes[0] = 4
+    w.cell_lifetimes[1] = 9
+    w.divide_cells([1])
+    assert w.cell_divisions.tolist() == [3, 9, 9]
+    assert w.cell_lifetimes.tolist() == [4, 0, 0]
+    w.increment_cell_lifetimes()
+    assert w.cell_lifetimes.tolist() == [5, 1, 1]
+
+
+def test_move_cells_keep_state():
+    w = ms.World(chemistry=_chem(MOLECULES[:2]), map_size=32)
+    idxs = w.spawn_cells([ms.random_genome(300) for _ in range(4)])
+    mols, labels, genomes = w.cell_molecules.clone(), list(w.cell_labels), list(w.cell_genomes)
+    for _ in range(4):
+        old = w.cell_positions.clone()
+        w.move_cells(idxs)
+        assert int(w.cell_map.sum()) == 4
+        assert torch.equal(w.cell_molecules, mols)
+        assert list(w.cell_labels) == labels and list(w.cell_genomes) == genomes
+        for i in idxs:
+            (ox, oy), (nx, ny) = old[i].tolist(), w.cell_positions[i].tolist()
+            assert (ox, oy) != (nx, ny)
+            assert ms.dist_1d(ox, nx, 32) <= 1 and ms.dist_1d(oy, ny, 32) <= 1
+            assert bool(w.cell_map[nx, ny])
+
+
+def test_reposition_cells():
+    w = ms.World(chemistry=_chem(), map_size=64)
+    w.spawn_cells([ms.random_genome(300) for _ in range(3)])
+    c0 = [w.get_cell(by_idx=i) for i in range(3)]
+    w.reposition_cells([0, 2])
+    c1 = [w.get_cell(by_idx=i) for i in range(3)]
+    assert c1[0].position != c0[0].position and c1[2].position != c0[2].position
+    assert c1[1].position == c0[1].position
+    for a, b in zip(c0, c1):
+        assert torch.equal(a.int_molecules, b.int_molecules)
+        assert (a.genome, a.label) == (b.genome, b.label)
+    assert int(w.cell_map.sum()) == 3
+
+
+def test_molecules_are_conserved_by_spawn_divide_kill():
+    w = ms.World(chemistry=_chem(), map_size=64)
+    total = lambda: w.molecule_map.double().sum(dim=[1, 2]) + w.cell_molecules.double().sum(dim=0)  # noqa: E731
+    exp = total()
+    idxs = w.spawn_cells([ms.random_genome(500) for _ in range(500)])
+    assert torch.allclose(total(), exp, rtol=1e-6)
+    pairs = w.divide_cells(idxs)
+    assert torch.allclose(total(), exp, rtol=1e-6)
+    w.kill_cells(idxs + [c for _, c in pairs])
+    assert torch.allclose(total(), exp, rtol=1e-6)
+    assert w.n_cells == 0 and int(w.cell_map.sum()) == 0
+
+
+def test_indices_stay_consistent():
+    w = ms.World(chemistry=_chem(), map_size=64)
+    idxs = w.spawn_cells([ms.random_genome(1000) for _ in range(600)])
+    n0 = w.n_cells
+    assert n0 == 600 and len(w.cell_genomes) == n0 and len(set(w.cell_labels)) == n0
+    pairs = w.divide_cells(idxs)
+    n1 = w.n_cells
+    assert n1 == n0 + len(pairs)
+    assert {p for p, _ in pairs} <= set(idxs) and not {c for _, c in pairs} & set(idxs)
+    assert len(set(w.cell_labels)) == n0
+    # kill parents: children shift down to the front, keeping their order and genomes
+    child_genomes = [w.cell_genomes[c] for _, c in pairs]
+    w.kill_cells(idxs)
+    assert w.n_cells == len(pairs)
+    assert list(w.cell_genomes) == child_genomes
+    assert int(w.cell_map.sum()) == w.n_cells
+    assert w.kinetics.N.size(0) == w.n_cells
+    w.kill_cells(list(range(w.n_cells)))
+    assert w.n_cells == 0 and int(w.cell_map.sum()) == 0
+
+
+def test_kill_removes_params_rows():
+    w = ms.World(chemistry=_chem(), map_size=16)
+    w.spawn_cells([ms.random_genome(800) for _ in range(10)])
+    N = w.kinetics.N.clone()
+    w.kill_cells([1, 4, 5])
+    keep = [0, 2, 3, 6, 7, 8, 9]
+    assert torch.equal(w.kinetics.N, N[keep])
+
+
+def test_get_cell_by_index_and_position():
+    w = ms.World(chemistry=_chem(MOLECULES[:2]), map_size=5)
+    w.spawn_cells([ms.random_genome(300) for _ in range(3)])
+    pos = tuple(w.cell_positions[2].tolist())
+    c = w.get_cell(by_position=pos)
+    assert c.idx == 2 and c.position == pos
+    assert c.genome == w.cell_genomes[2] and c.label == w.cell_labels[2]
+    free = [(x, y) for x in range(5) for y in range(5) if not w.cell_map[x, y]][0]
+    with pytest.raises(ValueError):
+        w.get_cell(by_position=free)
+
+
+def test_update_cells_and_empty_genomes():
+    w = ms.World(chemistry=_chem(), map_size=16)
+    g0, g1, g2 = ms.random_genome(500), ms.random_genome(1000), ms.random_genome(600)
+    w.spawn_cells([g0, g0])
+    assert torch.equal(w.kinetics.N[0], w.kinetics.N[1])
+    w.spawn_cells([g1])
+    w.update_cells([(g2, 1)])
+    assert list(w.cell_genomes) == [g0, g2, g1]
+    w.kill_cells([0])
+    assert list(w.cell_genomes) == [g2, g1]
+    w.update_cells([(g0, 0), ("", 1)])
+    assert list(w.cell_genomes) == [g0, ""]
+    assert (w.kinetics.N[1] == 0).all() and (w.kinetics.Vmax[1] == 0).all()
+    w.update_cells([("", 0)])
+    assert (w.kinetics.N == 0).all()
+
+
+def test_empty_proteome_cells():
+    w = ms.World(chemistry=_chem(), map_size=9)
+    genomes = [ms.random_genome(10), "", ms.random_genome(12)]
+    w.spawn_cells(genomes)
+    assert all(len(w.get_cell(by_idx=i).proteome) == 0 for i in range(3))
+    w.enzymatic_activity()  # nothing to do, nothing breaks
+    assert torch.isfinite(w.cell_molecules).all()
+
+
+def test_neighbors_fixture():
+    w = ms.World(chemistry=_chem(), map_size=7)
+    pos = [(0, 0), (0, 1), (6, 6), (3, 3), (4, 4), (3, 5), (0, 6), (5, 0)]
+    w.n_cells = len(pos)
+    w.cell_positions = torch.tensor(pos, dtype=torch.int32)
+    cm = torch.zeros(7, 7, dtype=torch.bool)
+    for x, y in pos:
+        cm[x, y] = True
+    w.cell_map = cm
+
+    def brute(frm, to):
+        out = set()
+        for a in frm:
+            for b in to:
+                if a == b:
+                    continue
+                (ax, ay), (bx, by) = pos[a], pos[b]
+                if ms.dist_1d(ax, bx, 7) <= 1 and ms.dist_1d(ay, by, 7) <= 1:
+                    out.add((min(a, b), max(a, b)))
+        return out
+
+    everyone = list(range(len(pos)))
+    for i in everyone:
+        assert set(w.get_neighbors([i], everyone)) == brute([i], everyone)
+    assert set(w.get_neighbors(everyone)) == brute(everyone, everyone)
+    # toroidal wrap: (0,0)-(6,6), (0,0)-(0,6), (0,6)-(6,6), (5,0)-(6,6)
+    assert {(0, 2), (0, 6), (2, 6), (2, 7)} <= set(w.get_neighbors(everyone))
+    assert set(w.get_neighbors([3, 4], [5])) == brute([3, 4], [5]) == {(4, 5)}
+    res = w.get_neighbors([0, 3])
+    assert res == sorted(res)
+
+
+def test_public_tensors_are_stable_references():
+    w = ms.World(chemistry=_chem(), map_size=4, mol_map_init="zeros")
+    w.spawn_cells([ms.random_genome(400) for _ in range(2)])
+    refs = (w.molecule_map, w.cell_molecules, w.cell_map)
+    w.diffuse_molecules()
+    w.enzymatic_activity()
+    w.degrade_molecules()
+    assert w.molecule_map is refs[0] and w.cell_molecules is refs[1] and w.cell_map is refs[2]
+    w.molecule_map = torch.full_like(w.molecule_map, 2.0)
+    w.cell_molecules = torch.full_like(w.cell_molecules, 2.0)
+    assert float(w.molecule_map.mean()) == 2.0 and float(w.cell_molecules.mean()) == 2.0
+    refs = (w.molecule_map, w.cell_molecules)
+    w.diffuse_molecules()
+    w.enzymatic_activity()
+    assert w.molecule_map is refs[0] and w.cell_molecules is refs[1]
+
+
+# --------------------------------------------------------------------------------------------- persistence
+def test_save_and_load_state_roundtrip():
+    mi, mj = ms.Molecule("WTsaveI", 10e3), ms.Molecule("WTsaveJ", 20e3)
+    chem = ms.Chemistry(molecules=[mi, mj], reactions=[([mi], [mj])])
+    w = ms.World(chemistry=chem, map_size=7)
+    w.spawn_cells([ms.random_genome(500) for _ in range(3)] + [""])
+    w.cell_lifetimes[1] = 5
+    w.cell_divisions[2] = 2
+    with tempfile.TemporaryDirectory() as d:
+        w.save_state(Path(d))
+        assert {p.name for p in Path(d).iterdir()} >= {"cells.fasta"}
+        w2 = ms.World(chemistry=chem, map_size=7)
+        w2.load_state(Path(d))
+    assert torch.equal(w2.cell_map, w.cell_map)
+    assert torch.equal(w2.molecule_map, w.molecule_map)
+    assert torch.equal(w2.cell_molecules, w.cell_molecules)
+    assert torch.equal(w2.cell_positions, w.cell_positions)
+    assert w2.cell_lifetimes.tolist() == w.cell_lifetimes.tolist()
+    assert w2.cell_divisions.tolist() == w.cell_divisions.tolist()
+    assert list(w2.cell_genomes) == list(w.cell_genomes)
+    assert list(w2.cell_labels) == list(w.cell_labels)
+
+
+def test_loading_several_states_replaces_cells():
+    mi, mj = ms.Molecule("WTsaveI", 10e3), ms.Molecule("WTsaveJ", 20e3)
+    chem = ms.Chemistry(molecules=[mi, mj], reactions=[([mi], [mj])])
+    with tempfile.TemporaryDirectory() as d:
+        w = ms.World(chemistry=chem, map_size=7)
+        counts = []
+        for k, action in enumerate(("spawn", "spawn", "kill")):
+            if action == "spawn":
+                w.spawn_cells([ms.random_genome(500) for _ in range(3)])
+            else:
+                w.kill_cells(list(range(4)))
+            w.save_state(Path(d) / f"s{k}")
+            counts.append(w.n_cells)
+        assert counts == [3, 6, 2]
+        w = ms.World(chemistry=chem, map_size=7)
+        for k in (0, 1, 2, 0):
+            w.load_state(Path(d) / f"s{k}", ignore_cell_params=(k == 1))
+            assert w.n_cells == counts[k] == len(w.cell_genomes) == int(w.cell_map.sum())
+            assert w.kinetics.N.size(0) == counts[k]
+
+
+def test_save_and_from_file_world_object():
+    mi, mj = ms.Molecule("WTsaveI", 10e3), ms.Molecule("WTsaveJ", 20e3)
+    chem = ms.Chemistry(molecules=[mi, mj], reactions=[([mi], [mj])])
+    for size, temp in ((7, 310.0), (9, 300.0)):
+        w = ms.World(chemistry=chem, map_size=size, abs_temp=temp)
+        w.spawn_cells([ms.random_genome(400) for _ in range(4)])
+        with tempfile.TemporaryDirectory() as d:
+            w.save(rundir=Path(d))
+            w2 = ms.World.from_file(rundir=Path(d))
+        assert (w2.abs_temp, w2.map_size, w2.device) == (temp, size, "cpu")
+        assert w2.chemistry.molecules[0] is mi and w2.chemistry.molecules[1] is mj
+        assert w2.chemistry.reactions == [([mi], [mj])]
+        assert w2.chemistry.mol_2_idx == {mi: 0, mj: 1}
+        assert list(w2.cell_genomes) == list(w.cell_genomes)
+        assert torch.equal(w2.kinetics.N, w.kinetics.N)
+        assert torch.equal(w2.kinetics.Vmax, w.kinetics.Vmax)
+        w2.enzymatic_activity()  # usable after restore
