@@ -89,7 +89,8 @@ def test_factories_from_container_dicts():
     ]
     facts = [ms.CatalyticDomainFact.from_dict(doms[0]), ms.TransporterDomainFact.from_dict(doms[1]),
              ms.RegulatoryDomainFact.from_dict(doms[2])]
-    assert facts[0].reaction == ([_X], [_Y]) and facts[1].molecule is _Z and facts[2].hill == 2
+    assert (facts[0].substrates, facts[0].products) == ([_X], [_Y])
+    assert facts[1].molecule is _Z and facts[2].hill == 2
     assert len(ms.GenomeFact(world=w, proteome=[facts]).generate()) == 2 * CODON_SIZE + 3 * w.genetics.dom_size
     # whole proteins as written by Protein.to_dict()
     fact = ms.GenomeFact.from_dicts([{"cds_start": 0, "cds_end": 0, "is_fwd": True, "domains": doms}], world=w)
