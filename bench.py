@@ -39,6 +39,8 @@ def _args():
     ap.add_argument("--chemistry", default="wood_ljungdahl", help="wood_ljungdahl | synthetic:M:R")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--profile-phases", action="store_true", help="print per-phase times to stderr")
+    ap.add_argument("--phase-sync", action="store_true", help="with --profile-phases: drain the GPU at phase "
+                    "boundaries (for attributing a kernel trace to phases; slows the step)")
     return ap.parse_args()
 
 
@@ -60,31 +62,41 @@ def random_genomes(k: int, size: int, device) -> tuple[torch.Tensor, torch.Tenso
     return rows, torch.full((k,), size, dtype=torch.int32, device=device)
 
 
-def step(world, n_target: int, genome_size: int, atp: int, timer=None):
+def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=None):
     def ph(name):
         import contextlib
 
         return timer.phase(name) if timer is not None else contextlib.nullcontext()
 
+    def note(key, val):
+        if stats is not None:
+            stats[key] = stats.get(key, 0) + int(val)
+
     with ph("top_up"):
         n = world.n_cells
         if n < n_target:
             world.spawn_cells(random_genomes(n_target - n, genome_size, world.cell_molecules.device))
+            note("spawned", n_target - n)
     with ph("activity"):
         world.enzymatic_activity()
     with ph("kill"):
         kill = torch.nonzero(world.cell_molecules[:, atp] < 1.0).flatten()
         world.kill_cells(kill)
+        if stats is not None:
+            note("killed", kill.numel())
     with ph("replicate"):
         repl = torch.nonzero(world.cell_molecules[:, atp] > 5.0).flatten()
         world.cell_molecules[repl, atp] -= 4.0
         world.divide_cells_t(repl)
+        if stats is not None:
+            note("divided", repl.numel())
     with ph("dilute"):
         # chemostat-style dilution keeps the population at the configured size (the reference loop
         # only tops up; on a 4096^2 map the population would otherwise grow ~6x within 25 steps)
         excess = world.n_cells - n_target
         if excess > 0:
             world.kill_cells(torch.randperm(world.n_cells, device=world.cell_molecules.device)[:excess])
+            note("diluted", excess)
     with ph("recombinate"):
         world.recombinate_cells()
     with ph("mutate"):
@@ -144,10 +156,11 @@ def main():
     for _ in range(a.warmup):
         step(world, n_target, a.genome_size, atp)
     sync()
-    timer = PhaseTimer(device) if a.profile_phases else None
+    timer = PhaseTimer(device, sync=a.phase_sync) if a.profile_phases else None
     t0 = time.perf_counter()
+    stats = {} if a.profile_phases else None
     for _ in range(a.steps):
-        step(world, n_target, a.genome_size, atp, timer)
+        step(world, n_target, a.genome_size, atp, timer, stats)
     sync()
     dt = time.perf_counter() - t0
     if distributed:
@@ -163,7 +176,9 @@ def main():
     value = a.steps / dt
     if rank == 0:
         if timer is not None:
-            print(json.dumps({"phases_ms": timer.summary(), "setup_s": setup_s, "n_cells": n_cells}), file=sys.stderr)
+            per_step = {k: v / a.steps for k, v in (stats or {}).items()}
+            print(json.dumps({"phases_ms": timer.summary(), "events_per_step": per_step, "setup_s": setup_s,
+                              "n_cells": n_cells}), file=sys.stderr)
         out = {
             "metric": METRIC,
             "value": round(value, 3),

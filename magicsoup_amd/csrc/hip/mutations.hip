@@ -2,9 +2,10 @@
 // (semantics of rust/mutations.rs:11-154).
 //
 // Both are two-phase: a cheap per-item Poisson draw over all genomes / neighbour pairs, then an
-// apply kernel for the (usually few) items that drew at least one event. Apply kernels draw the
-// event positions by sequential selection sampling (k distinct sorted positions in one O(L) pass)
-// and stream the new sequences into scratch rows; the host side copies them back into the arena.
+// apply kernel for the (usually few) items that drew at least one event. An apply kernel runs one
+// wavefront per item: one lane draws the k event positions (Floyd's sorted sampling) into an LDS
+// plan, then all 64 lanes stream the new sequence into a scratch row; the host side copies the
+// rows back into the arena.
 #include "hip_common.h"
 
 namespace msd {
@@ -57,55 +58,83 @@ __global__ void __launch_bounds__(256) mut_count_kernel(int n, const int64_t* ro
   k[i] = (int32_t)(kk > L ? L : kk);
 }
 
-// Mutated copy of genome `rows[sel[j]]` into scratch row j.
-__device__ __forceinline__ void mutate_at(Philox& rng, uint8_t ch, double p_indel, double p_del, uint8_t* o, int& w,
-                                          int cap) {
+// One mutation event at nucleotide `ch`: the 0..2 nucleotides it emits (reference
+// rust/mutations.rs:30-60: indel with p_indel, then deletion with p_del, else insertion before ch;
+// otherwise a substitution that may repeat the old nucleotide).
+__device__ __forceinline__ int mutate_at(Philox& rng, uint8_t ch, double p_indel, double p_del, uint8_t* lit) {
   if (rng.uniform_d() < p_indel) {
-    if (rng.uniform_d() < p_del) return;         // deletion
-    if (w < cap) o[w++] = rand_nt(rng);         // insertion before the current nucleotide
-    if (w < cap) o[w++] = ch;
-  } else if (w < cap) {
-    o[w++] = rand_nt(rng);                      // substitution (may repeat the old nucleotide)
+    if (rng.uniform_d() < p_del) return 0;  // deletion
+    lit[0] = rand_nt(rng);                  // insertion before the current nucleotide
+    lit[1] = ch;
+    return 2;
+  }
+  lit[0] = rand_nt(rng);  // substitution
+  return 1;
+}
+
+// Cooperative copy of src[a, b) to dst[w, ...) by the 64 lanes of a wave (clipped at cap).
+__device__ __forceinline__ void wave_copy(const uint8_t* src, int a, int b, uint8_t* dst, int w, int cap, int lane) {
+  for (int t = a + lane; t < b; t += 64) {
+    const int o = w + (t - a);
+    if (o < cap) dst[o] = src[t];
   }
 }
 
+// One wavefront per selected genome: lane 0 draws the event positions and the emitted literals into
+// an LDS plan (copy segment, literal, copy segment, ...); all lanes then stream the segments.
+// Genomes with more than kFloydMax events (very high rates) take a serial selection-sampling path.
 __global__ void __launch_bounds__(64) mut_apply_kernel(int nsel, const int64_t* sel, const int64_t* rows,
                                                        const uint8_t* arena, int width, const int32_t* lens,
                                                        const int32_t* k, double p_indel, double p_del, uint64_t seed,
                                                        uint64_t call, uint8_t* out, int out_width, int32_t* out_len) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ int pos[kFloydMax];
+  __shared__ uint8_t lit[kFloydMax][2];
+  __shared__ int nlit[kFloydMax];
+  const int j = blockIdx.x, lane = threadIdx.x;
   if (j >= nsel) return;
   const int64_t i = sel[j];
   const int64_t r = rows ? rows[i] : i;
   const uint8_t* s = arena + (size_t)r * width;
   const int L = lens[r];
   const int kk = k[i];
-  Philox rng(seed, call ^ kApplyStream, (uint32_t)i);
   uint8_t* o = out + (size_t)j * out_width;
-  int w = 0;
-  if (kk <= kFloydMax) {
-    int pos[kFloydMax];
-    floyd_sorted(rng, L, kk, pos);
-    int prev = 0;
-    for (int q = 0; q < kk; ++q) {
-      for (int t = prev; t < pos[q] && w < out_width; ++t) o[w++] = s[t];
-      mutate_at(rng, s[pos[q]], p_indel, p_del, o, w, out_width);
-      prev = pos[q] + 1;
-    }
-    for (int t = prev; t < L && w < out_width; ++t) o[w++] = s[t];
-  } else {
-    int need = kk;
-    for (int t = 0; t < L; ++t) {
-      // selection sampling: position t is chosen with chance need / (L - t)
-      if (need > 0 && rng.below((uint32_t)(L - t)) < (uint32_t)need) {
-        --need;
-        mutate_at(rng, s[t], p_indel, p_del, o, w, out_width);
-      } else if (w < out_width) {
-        o[w++] = s[t];
+  if (kk > kFloydMax) {
+    if (lane == 0) {
+      Philox rng(seed, call ^ kApplyStream, (uint32_t)i);
+      int need = kk, w = 0;
+      uint8_t l2[2];
+      for (int t = 0; t < L; ++t) {
+        // selection sampling: position t is chosen with chance need / (L - t)
+        if (need > 0 && rng.below((uint32_t)(L - t)) < (uint32_t)need) {
+          --need;
+          const int nl = mutate_at(rng, s[t], p_indel, p_del, l2);
+          for (int q = 0; q < nl; ++q)
+            if (w < out_width) o[w++] = l2[q];
+        } else if (w < out_width) {
+          o[w++] = s[t];
+        }
       }
+      out_len[j] = w;
     }
+    return;
   }
-  out_len[j] = w;
+  if (lane == 0) {
+    Philox rng(seed, call ^ kApplyStream, (uint32_t)i);
+    floyd_sorted(rng, L, kk, pos);
+    for (int q = 0; q < kk; ++q) nlit[q] = mutate_at(rng, s[pos[q]], p_indel, p_del, lit[q]);
+  }
+  __syncthreads();
+  int prev = 0, w = 0;
+  for (int q = 0; q < kk; ++q) {
+    wave_copy(s, prev, pos[q], o, w, out_width, lane);
+    w += pos[q] - prev;
+    if (lane < nlit[q] && w + lane < out_width) o[w + lane] = lit[q][lane];
+    w += nlit[q];
+    prev = pos[q] + 1;
+  }
+  wave_copy(s, prev, L, o, w, out_width, lane);
+  w += L - prev;
+  if (lane == 0) out_len[j] = w < out_width ? w : out_width;
 }
 
 // k[i] ~ Poisson(p * (len(a) + len(b))) for neighbour pair i
@@ -124,87 +153,99 @@ __global__ void __launch_bounds__(256) rec_count_kernel(int n, const int32_t* pa
 }
 
 // Recombine pair sel[j]: cut both strands at k[.] sorted positions, shuffle the k+2 parts and split
-// them at a random index into two new genomes (scratch rows 2j and 2j+1). `parts` holds 3 ints per
-// part and up to (len(a) + len(b) + 2) parts per selected pair.
+// them at a random index into two new genomes (scratch rows 2j and 2j+1). One wavefront per pair:
+// lane 0 plans the parts (LDS for up to kFloydMax cuts, else the global `parts` scratch with
+// parts_cap entries of 3 ints), then all lanes copy them.
 __global__ void __launch_bounds__(64) rec_apply_kernel(int nsel, const int64_t* sel, const int32_t* pairs,
                                                        const uint8_t* arena, int width, const int32_t* lens,
                                                        const int32_t* k, uint64_t seed, uint64_t call, int32_t* parts,
                                                        int parts_cap, uint8_t* out, int out_width, int32_t* out_len) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ int32_t lparts[(kFloydMax + 2) * 3];
+  __shared__ int meta[2];  // number of parts, split index
+  const int j = blockIdx.x, lane = threadIdx.x;
   if (j >= nsel) return;
   const int64_t i = sel[j];
   const int ca = pairs[2 * i], cb = pairs[2 * i + 1];
   const int n0 = lens[ca], n1 = lens[cb], nb = n0 + n1;
-  int need = k[i];
-  Philox rng(seed, call ^ kApplyStream, (uint32_t)i);
-  int32_t* pt = parts + (size_t)j * parts_cap * 3;
-  int np = 0;
-  auto push = [&](int src, int a0, int a1) {
-    pt[3 * np] = src; pt[3 * np + 1] = a0; pt[3 * np + 2] = a1; ++np;
-  };
-  if (need <= kFloydMax) {
-    int cuts[kFloydMax];
-    floyd_sorted(rng, nb, need, cuts);
-    int start = 0, q = 0;
-    for (; q < need && cuts[q] < n0; ++q) {
-      push(0, start, cuts[q]);
-      start = cuts[q];
-    }
-    push(0, start, n0);
-    start = 0;
-    for (; q < need; ++q) {
-      push(1, start, cuts[q] - n0);
-      start = cuts[q] - n0;
-    }
-    push(1, start, n1);
-  } else {
-    int start = 0, src = 0;
-    for (int t = 0; t < nb; ++t) {
-      if (t == n0) {  // close the last part of strand a
-        push(0, start, n0);
-        start = 0;
-        src = 1;
+  const int kk = k[i];
+  int32_t* pt = kk <= kFloydMax ? lparts : parts + (size_t)j * parts_cap * 3;
+  if (lane == 0) {
+    int need = kk;
+    Philox rng(seed, call ^ kApplyStream, (uint32_t)i);
+    int np = 0;
+    auto push = [&](int src, int a0, int a1) {
+      pt[3 * np] = src; pt[3 * np + 1] = a0; pt[3 * np + 2] = a1; ++np;
+    };
+    if (need <= kFloydMax) {
+      int cuts[kFloydMax];
+      floyd_sorted(rng, nb, need, cuts);
+      int start = 0, q = 0;
+      for (; q < need && cuts[q] < n0; ++q) {
+        push(0, start, cuts[q]);
+        start = cuts[q];
       }
-      if (need > 0 && rng.below((uint32_t)(nb - t)) < (uint32_t)need) {
-        --need;
-        const int pos = src == 0 ? t : t - n0;
-        push(src, start, pos);
-        start = pos;
-      }
-    }
-    if (n0 == nb) {  // strand b empty: close strand a here
       push(0, start, n0);
       start = 0;
+      for (; q < need; ++q) {
+        push(1, start, cuts[q] - n0);
+        start = cuts[q] - n0;
+      }
+      push(1, start, n1);
+    } else {
+      int start = 0, src = 0;
+      for (int t = 0; t < nb; ++t) {
+        if (t == n0) {  // close the last part of strand a
+          push(0, start, n0);
+          start = 0;
+          src = 1;
+        }
+        if (need > 0 && rng.below((uint32_t)(nb - t)) < (uint32_t)need) {
+          --need;
+          const int pos = src == 0 ? t : t - n0;
+          push(src, start, pos);
+          start = pos;
+        }
+      }
+      if (n0 == nb) {  // strand b empty: close strand a here
+        push(0, start, n0);
+        start = 0;
+      }
+      push(1, start, n1);
     }
-    push(1, start, n1);
-  }
-  // Fisher-Yates shuffle of the parts
-  for (int q = np - 1; q > 0; --q) {
-    const int r = (int)rng.below((uint32_t)(q + 1));
-    for (int f = 0; f < 3; ++f) {
-      const int32_t tmp = pt[3 * q + f];
-      pt[3 * q + f] = pt[3 * r + f];
-      pt[3 * r + f] = tmp;
+    // Fisher-Yates shuffle of the parts
+    for (int q = np - 1; q > 0; --q) {
+      const int r = (int)rng.below((uint32_t)(q + 1));
+      for (int f = 0; f < 3; ++f) {
+        const int32_t tmp = pt[3 * q + f];
+        pt[3 * q + f] = pt[3 * r + f];
+        pt[3 * r + f] = tmp;
+      }
     }
+    meta[0] = np;
+    meta[1] = (int)rng.below((uint32_t)np);
   }
-  const int split = (int)rng.below((uint32_t)np);
+  __syncthreads();
+  const int np = meta[0], split = meta[1];
   const uint8_t* sa = arena + (size_t)ca * width;
   const uint8_t* sb = arena + (size_t)cb * width;
   uint8_t* o0 = out + (size_t)(2 * j) * out_width;
   uint8_t* o1 = out + (size_t)(2 * j + 1) * out_width;
   int w0 = 0, w1 = 0;
   for (int q = 0; q < np; ++q) {
-    const uint8_t* s = pt[3 * q] == 0 ? sa : sb;
-    for (int t = pt[3 * q + 1]; t < pt[3 * q + 2]; ++t) {
-      if (q < split) {
-        if (w0 < out_width) o0[w0++] = s[t];
-      } else {
-        if (w1 < out_width) o1[w1++] = s[t];
-      }
+    const uint8_t* src = pt[3 * q] == 0 ? sa : sb;
+    const int a0 = pt[3 * q + 1], a1 = pt[3 * q + 2];
+    if (q < split) {
+      wave_copy(src, a0, a1, o0, w0, out_width, lane);
+      w0 += a1 - a0;
+    } else {
+      wave_copy(src, a0, a1, o1, w1, out_width, lane);
+      w1 += a1 - a0;
     }
   }
-  out_len[2 * j] = w0;
-  out_len[2 * j + 1] = w1;
+  if (lane == 0) {
+    out_len[2 * j] = w0 < out_width ? w0 : out_width;
+    out_len[2 * j + 1] = w1 < out_width ? w1 : out_width;
+  }
 }
 
 void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
@@ -219,7 +260,7 @@ void mut_apply(int nsel, uintptr_t sel, uintptr_t rows, uintptr_t arena, int wid
                double p_indel, double p_del, uint64_t seed, uint64_t call, uintptr_t out, int out_width,
                uintptr_t out_len, uintptr_t stream) {
   if (nsel <= 0) return;
-  mut_apply_kernel<<<cdiv(nsel, 64), 64, 0, S_(stream)>>>(nsel, P_<int64_t>(sel), rows ? P_<int64_t>(rows) : nullptr,
+  mut_apply_kernel<<<nsel, 64, 0, S_(stream)>>>(nsel, P_<int64_t>(sel), rows ? P_<int64_t>(rows) : nullptr,
                                                           P_<uint8_t>(arena), width, P_<int32_t>(lens), P_<int32_t>(k),
                                                           p_indel, p_del, seed, call, P_<uint8_t>(out), out_width,
                                                           P_<int32_t>(out_len));
@@ -238,7 +279,7 @@ void rec_apply(int nsel, uintptr_t sel, uintptr_t pairs, uintptr_t arena, int wi
                uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out, int out_width,
                uintptr_t out_len, uintptr_t stream) {
   if (nsel <= 0) return;
-  rec_apply_kernel<<<cdiv(nsel, 64), 64, 0, S_(stream)>>>(nsel, P_<int64_t>(sel), P_<int32_t>(pairs),
+  rec_apply_kernel<<<nsel, 64, 0, S_(stream)>>>(nsel, P_<int64_t>(sel), P_<int32_t>(pairs),
                                                           P_<uint8_t>(arena), width, P_<int32_t>(lens), P_<int32_t>(k),
                                                           seed, call, P_<int32_t>(parts), parts_cap, P_<uint8_t>(out),
                                                           out_width, P_<int32_t>(out_len));

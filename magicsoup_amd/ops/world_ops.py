@@ -195,9 +195,11 @@ def _mask_reducer(world):
 def diffuse(world) -> None:
     """Stencil over the owned rows -> (global) per-molecule mass totals -> correction + clamp.
     A domain-decomposed world refreshes its halo rows first and all-reduces the totals."""
-    mm = _molmap(world)
-    if mm.is_cuda:
+    if world.__dict__["_molmap"].is_cuda:
+        # the raw buffer: a pending degradation is fused into the stencil (reading
+        # `molecule_map` here would apply it in a separate pass)
         return _hip().diffuse(world)
+    mm = _molmap(world)
     R, C, r_lo, r_hi, wrap = geom(world)
     halo = getattr(world, "_exchange_map_halo", None)
     if halo is not None:

@@ -49,14 +49,19 @@ class PhaseTimer:
     """Accumulate per-phase times. On GPU, phases are bracketed with HIP events and resolved
     lazily (no synchronisation inside the timed loop)."""
 
-    def __init__(self, device: str | torch.device = "cpu"):
+    def __init__(self, device: str | torch.device = "cpu", sync: bool = False):
         self.gpu = torch.device(device).type == "cuda"
+        # sync=True drains the device at phase boundaries, so a kernel trace can be attributed to
+        # phases by timestamps (profiling only: it serialises host and device)
+        self.sync = sync and self.gpu
         self._pending: list[tuple[str, object, object]] = []
         self.totals: dict[str, float] = defaultdict(float)
         self.counts: dict[str, int] = defaultdict(int)
 
     @contextlib.contextmanager
     def phase(self, name: str):
+        if self.sync:
+            torch.cuda.synchronize()
         range_push(name)
         if self.gpu:
             a = torch.cuda.Event(enable_timing=True)
@@ -67,6 +72,8 @@ class PhaseTimer:
             finally:
                 b.record()
                 self._pending.append((name, a, b))
+                if self.sync:
+                    torch.cuda.synchronize()
                 range_pop()
         else:
             t0 = time.perf_counter()

@@ -1,6 +1,8 @@
 """DistributedWorld on the GPU: 2 ranks sharing one MI355X (gloo, host-staged exchanges), so the
 strip-geometry HIP kernels (halo rows, no x wrap, claims into halo rows) run for real. The RCCL
 transport itself is exercised by the multi-GPU bench."""
+import copy
+
 import pytest
 import torch
 
@@ -23,11 +25,13 @@ def _body_physics(rank, ws):
     def world():
         ms.set_seed(3)
         torch.manual_seed(3)
-        w = ms.World(chemistry=_chem(), map_size=64, seed=3, device="cuda")
+        w = ms.World(chemistry=_chem(), map_size=64, seed=3, device="cpu")
         w.spawn_cells(gen_genomes(600, 300))
         return w
 
-    g, ref = world(), world()
+    # built on the CPU (deterministic placement) so both ranks scatter the same global world
+    g = world()
+    ref = copy.deepcopy(g).to("cuda")
     dw = DistributedWorld(chemistry=_chem(), map_size=64, seed=5, device="cuda")
     dw.scatter_from(g)
     for _ in range(3):

@@ -234,7 +234,7 @@ def test_integrator_split_parts_match_fused():
     """The per-part launches a domain-decomposed world uses (flags all-reduced between parts)
     reproduce the fused single launch exactly."""
     wa = _world("cuda", n=500)
-    wa2 = _world("cuda", n=500)
+    wa2 = copy.deepcopy(wa)  # (GPU placement is race-resolved: clone rather than rebuild)
     calls = []
     wa2.__dict__["_allreduce_flags"] = lambda flags: calls.append(int(flags.numel()))
     wa.enzymatic_activity()
