@@ -1,14 +1,17 @@
 // gfx950 genome translation over the device genome arena: one wavefront per genome.
 //
 // The sequential reference scan (rust/genetics.rs:13-123; single-source host version in
-// ms_common.h) is reformulated so that all 64 lanes work at once:
+// ms_common.h) is reformulated so that all 64 lanes work at once and no lane walks the genome:
 //   1. lanes over positions: codon index of every position on both strands -> LDS;
-//   2. lanes over start codons: walk to the first in-frame stop; every CDS long enough goes into a
-//      per-strand list (LDS atomic append, order restored next);
-//   3. rank every CDS by (stop ascending, start descending) -- exactly the reference's emission
+//   2. per strand and frame, a wave suffix-min scan gives the next in-frame stop of every position,
+//      and lanes over positions tabulate the domain type starting at each position;
+//   3. lanes over start codons: the CDS end is one lookup; CDSs long enough go into a per-strand
+//      list (LDS atomic append, order restored next);
+//   4. rank every CDS by (stop ascending, start descending) -- exactly the reference's emission
 //      order (a stop closes its frame's pending starts latest-first);
-//   4. lanes over CDSs in that order: domain extraction (count pass: #domains + "has a catalytic or
-//      transporter domain"; write pass: tokens at the protein's slot, from a wave prefix sum).
+//   5. lanes over CDSs in that order: domain extraction from the domain-type table (count pass:
+//      #domains + "has a catalytic or transporter domain"; write pass: tokens at the protein's slot,
+//      from a wave prefix sum).
 // Forward-strand proteins precede reverse-strand ones (rust/genetics.rs:151-175).
 #include "hip_common.h"
 
@@ -32,6 +35,11 @@ struct TransArgs {
   int P, D;
 };
 
+__host__ __device__ inline size_t slot_bytes_for(int width, int cap) {
+  return ((size_t)2 * cap * 4 + (size_t)2 * width * 2 + (size_t)2 * cap * 2 + (size_t)2 * width * 2 + 16 + 15) &
+         ~(size_t)15;
+}
+
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
@@ -48,13 +56,16 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   const uint16_t* l_two = reinterpret_cast<const uint16_t*>(sm + 64 * 3 + 16);
   uint8_t* l_dt = sm + kLutBytes;
   const int dt_bytes = a.stage_dt ? ((a.dt_entries + 15) & ~15) : 0;
-  // per-wave slot: codons [2][width] bytes, CDS lists [2][cap] u32, emission order [2][cap] u16
-  const size_t slot_bytes = ((size_t)2 * a.width + (size_t)2 * a.cap * 6 + 16 + 15) & ~(size_t)15;
+  // per-wave slot: CDS lists [2][cap] u32, next stop [2][width] u16, emission order [2][cap] u16,
+  // codons [2][width] u8, domain type at position [2][width] u8, counters
+  const size_t slot_bytes = slot_bytes_for(a.width, a.cap);
   uint8_t* slot = sm + kLutBytes + dt_bytes + (size_t)wid * slot_bytes;
-  uint8_t* cod = slot;
-  uint32_t* cds = reinterpret_cast<uint32_t*>(slot + 2 * a.width);  // (q << 16) | p
-  uint16_t* order = reinterpret_cast<uint16_t*>(cds + 2 * a.cap);
-  int* counters = reinterpret_cast<int*>(order + 2 * a.cap);
+  uint32_t* cds = reinterpret_cast<uint32_t*>(slot);  // (q << 16) | p
+  uint16_t* nstop = reinterpret_cast<uint16_t*>(cds + 2 * a.cap);
+  uint16_t* order = nstop + 2 * a.width;
+  uint8_t* cod = reinterpret_cast<uint8_t*>(order + 2 * a.cap);
+  uint8_t* dtp = cod + 2 * a.width;
+  int* counters = reinterpret_cast<int*>(dtp + 2 * a.width);
 
   for (int i = threadIdx.x; i < 64; i += blockDim.x) {
     l_start[i] = a.is_start[i];
@@ -96,15 +107,50 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   }
   wave_sync();
 
-  // ---- 2. CDS candidates: start codon -> first in-frame stop (too short / unstopped: dropped)
+  // ---- 2. next in-frame stop at or after every position (suffix-min scan per strand and frame),
+  //         domain type starting at every position
+  const int ds = a.dom_size, dts = a.dom_type_size, ntc = dts / 3;
+  for (int st = 0; st < 2; ++st) {
+    const uint8_t* c = cod + st * a.width;
+    uint16_t* ns = nstop + st * a.width;
+    for (int f = 0; f < 3; ++f) {
+      const int nf = ncod > f ? (ncod - f + 2) / 3 : 0;  // positions f, f+3, ... < ncod
+      int carry = 0xFFFF;
+      for (int hi = nf; hi > 0; hi -= 64) {
+        const int e = hi - 64 + lane;
+        const int pe = f + 3 * e;
+        int v = (e >= 0 && l_stop[c[pe]]) ? pe : 0xFFFF;
+        for (int off = 1; off < 64; off <<= 1) {
+          const int u = __shfl_down(v, off);
+          if (lane + off < 64) v = min(v, u);
+        }
+        v = min(v, carry);
+        if (e >= 0) ns[pe] = (uint16_t)v;
+        carry = __shfl(v, 0);
+      }
+    }
+    uint8_t* dt = dtp + st * a.width;
+    for (int p = lane; p < L; p += 64) {
+      uint8_t ty = 0;
+      if (p + dts <= L) {
+        int idx = 0;
+        for (int t = 0; t < ntc; ++t) idx = (idx << 6) | c[p + 3 * t];
+        ty = DT[idx];
+      }
+      dt[p] = ty;
+    }
+  }
+  wave_sync();
+
+  // ---- 3. CDS candidates: start codon -> first in-frame stop (too short / unstopped: dropped)
   if (L >= a.dom_size && L >= 3) {
     for (int st = 0; st < 2; ++st) {
       const uint8_t* c = cod + st * a.width;
+      const uint16_t* ns = nstop + st * a.width;
       for (int p = lane; p < ncod; p += 64) {
         if (!l_start[c[p]]) continue;
-        int q = p + 3;
-        while (q < ncod && !l_stop[c[q]]) q += 3;
-        if (q >= ncod || q + 3 - p < a.dom_size) continue;
+        const int q = p + 3 < ncod ? (int)ns[p + 3] : 0xFFFF;
+        if (q == 0xFFFF || q + 3 - p < a.dom_size) continue;
         const int k = atomicAdd(&counters[st], 1);
         cds[st * a.cap + k] = ((uint32_t)q << 16) | (uint32_t)p;  // k < ncod <= cap
       }
@@ -112,7 +158,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   }
   wave_sync();
 
-  // ---- 3. emission order: stop ascending, start descending
+  // ---- 4. emission order: stop ascending, start descending
   int ncds[2];
   for (int st = 0; st < 2; ++st) {
     ncds[st] = counters[st];
@@ -130,11 +176,11 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   }
   wave_sync();
 
-  // ---- 4. domain extraction in emission order
-  const int ds = a.dom_size, dts = a.dom_type_size, ntc = dts / 3;
+  // ---- 5. domain extraction in emission order
   int prot_base = 0;  // forward-strand proteins come first
   for (int st = 0; st < 2; ++st) {
     const uint8_t* c = cod + st * a.width;
+    const uint8_t* dt = dtp + st * a.width;
     int n_prot = 0, max_dom = 0;
     for (int e0 = 0; e0 < ncds[st]; e0 += 64) {
       const int e = e0 + lane;
@@ -148,9 +194,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
       int nd = 0;
       bool useful = false;
       for (int i = 0; i + ds <= n;) {
-        int idx = 0;
-        for (int t = 0; t < ntc; ++t) idx = (idx << 6) | c[p + i + 3 * t];
-        const int ty = DT[idx];
+        const int ty = dt[p + i];
         if (ty) {
           useful |= ty != 3;
           ++nd;
@@ -167,9 +211,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
           int32_t* tk = a.tokens + ((size_t)g * a.P + slot_p) * a.D * 5;
           int d = 0;
           for (int i = 0; i + ds <= n && d < a.D;) {
-            int idx = 0;
-            for (int t = 0; t < ntc; ++t) idx = (idx << 6) | c[p + i + 3 * t];
-            const int ty = DT[idx];
+            const int ty = dt[p + i];
             if (ty) {
               const int o = p + i + dts;
               int32_t* dm = tk + d * 5;
@@ -230,7 +272,7 @@ static void launch(bool write, int n, uintptr_t rows, uintptr_t arena, int width
   a.stage_dt = dt_entries <= 4096;
   a.cap = width;  // a strand has at most one CDS per codon position (< width)
   const size_t fixed = kLutBytes + (a.stage_dt ? ((dt_entries + 15) & ~15) : 0);
-  const size_t slot = ((size_t)2 * width + (size_t)2 * a.cap * 6 + 16 + 15) & ~(size_t)15;
+  const size_t slot = slot_bytes_for(width, a.cap);
   if (fixed + slot > 160 * 1024) throw std::invalid_argument("genome too long for the LDS-resident translation");
   int gpb = kGBlock / 64;
   while (gpb > 1 && fixed + gpb * slot > 64 * 1024) --gpb;

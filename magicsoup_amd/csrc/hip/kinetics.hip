@@ -327,24 +327,25 @@ struct BuildArgs {
 
 __device__ __forceinline__ int lut(int t, int lim) { return (t >= 0 && t < lim) ? t : 0; }
 
+// One G-lane group per (row, protein slot); lanes over signals j. Each lane folds the protein's
+// domains for its signals (stoichiometry, effector Hill sums, Kmr means), the group reduces the
+// energy change for Ke, and lane 0 writes the per-protein scalars. The energy sum is accumulated in
+// double (integer N times float energies: exact, hence order-independent) so host and device agree
+// bit for bit.
+template <int G>
 __global__ void __launch_bounds__(kBlock) build_params_kernel(BuildArgs b) {
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (long long)b.n * b.Pt) return;
-  const int ci = (int)(t / b.Pt), p = (int)(t - (long long)ci * b.Pt);
+  const long long grp = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / G;
+  const int lane = threadIdx.x % G;
+  if (grp >= (long long)b.n * b.Pt) return;  // whole groups exit together
+  const int ci = (int)(grp / b.Pt), p = (int)(grp - (long long)ci * b.Pt);
   const size_t row = (size_t)b.rows[ci];
   const size_t o2 = row * b.Pt + p, o3 = o2 * b.s;
   const int32_t* pt = b.tokens + ((size_t)ci * b.P + (p < b.P ? p : 0)) * b.D * 5;
-  const int nd = p < b.P ? b.D : 0;
+  int nd = p < b.P ? b.D : 0;
+  while (nd > 0 && pt[(nd - 1) * 5] == 0) --nd;  // trailing empty domain slots
 
-  ms::NanMean vm, km;
-  for (int d = 0; d < nd; ++d) {
-    const int32_t* dm = pt + d * 5;
-    if (dm[0] == 0 || dm[0] == 3) continue;
-    vm.add(b.vmax_w[lut(dm[1], b.nw)]);
-    km.add(b.km_w[lut(dm[2], b.nk)]);
-  }
-  float E = 0.0f;
-  for (int j = 0; j < b.s; ++j) {
+  double E = 0.0;
+  for (int j = lane; j < b.s; j += G) {
     int n = 0, nf = 0, nb = 0, av = 0, kc = 0;
     float ks = 0.0f;
     for (int d = 0; d < nd; ++d) {
@@ -375,9 +376,18 @@ __global__ void __launch_bounds__(kBlock) build_params_kernel(BuildArgs b) {
     b.Nb[o3 + j] = nb;
     b.A[o3 + j] = av;
     b.Kmr[o3 + j] = powf(kc > 0 ? ks / (float)kc : 0.0f, (float)av);
-    E += (float)n * b.energies[j];
+    E += (double)n * (double)b.energies[j];
   }
-  float kev = expf(-E / b.abs_temp / b.gas);
+  for (int o = G / 2; o > 0; o >>= 1) E += __shfl_xor(E, o, G);
+  if (lane != 0) return;
+  ms::NanMean vm, km;
+  for (int d = 0; d < nd; ++d) {
+    const int32_t* dm = pt + d * 5;
+    if (dm[0] == 0 || dm[0] == 3) continue;
+    vm.add(b.vmax_w[lut(dm[1], b.nw)]);
+    km.add(b.km_w[lut(dm[2], b.nk)]);
+  }
+  float kev = expf(-(float)E / b.abs_temp / b.gas);
   kev = kev < ms::kEps ? ms::kEps : (kev > ms::kMax ? ms::kMax : kev);
   const float kmn = km.value0();
   float kmfv = kev >= 1.0f ? kmn : kmn / kev;
@@ -487,7 +497,9 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
   b.energies = P_<float>(energies); b.abs_temp = abs_temp; b.gas = gas;
   b.N = P_<int32_t>(N); b.Nf = P_<int32_t>(Nf); b.Nb = P_<int32_t>(Nb); b.A = P_<int32_t>(A);
   b.Kmr = P_<float>(Kmr); b.Kmf = P_<float>(Kmf); b.Kmb = P_<float>(Kmb); b.Vmax = P_<float>(Vmax); b.Ke = P_<float>(Ke);
-  build_params_kernel<<<cdiv((long long)n * Pt, kBlock), kBlock, 0, S_(stream)>>>(b);
+  const long long groups = (long long)n * Pt;
+  if (s <= 32) build_params_kernel<32><<<cdiv(groups * 32, kBlock), kBlock, 0, S_(stream)>>>(b);
+  else build_params_kernel<64><<<cdiv(groups * 64, kBlock), kBlock, 0, S_(stream)>>>(b);
   MS_LAUNCH_CHECK();
 }
 

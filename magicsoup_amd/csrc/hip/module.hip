@@ -6,12 +6,26 @@
 #include <pybind11/stl.h>
 
 #include <atomic>
+#include <tuple>
+#include <vector>
 
 #include "hip_common.h"
 
 namespace py = pybind11;
 
 namespace msd {
+void split_cells(int k, int m, uintptr_t parents, uintptr_t children, uintptr_t cell_mols, uintptr_t divisions,
+                 uintptr_t lifetimes, uintptr_t stream);
+void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, bool vacate,
+                  uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result, int rounds,
+                  uint64_t seed, uint64_t call, uintptr_t stream);
+void spill_free(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
+                uintptr_t cell_map, uintptr_t stream);
+void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
+            uintptr_t stream);
+void gather_rows(int n, uintptr_t src_rows, uintptr_t dst_rows,
+                 const std::vector<std::tuple<uintptr_t, uintptr_t, long long, long long, long long>>& descs,
+                 uintptr_t stream);
 // kinetics.hip
 void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t Nf, uintptr_t Nb, uintptr_t A,
                uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb, uintptr_t Vmax, uintptr_t Ke, uintptr_t cell_mols,
@@ -86,6 +100,11 @@ PYBIND11_MODULE(_hip, m) {
   m.def("diffuse_correct", &msd::diffuse_correct);
   m.def("diffuse_partials_len", &msd::diffuse_partials_len);
   m.def("scale_planes", &msd::scale_planes);
+  m.def("gather_rows", &msd::gather_rows);
+  m.def("spill_free", &msd::spill_free);
+  m.def("pickup", &msd::pickup);
+  m.def("place_rounds", &msd::place_rounds);
+  m.def("split_cells", &msd::split_cells);
   m.def("permeate", &msd::permeate);
   m.def("claim_free", &msd::claim_free);
   m.def("pick_neighbour", &msd::pick_neighbour);

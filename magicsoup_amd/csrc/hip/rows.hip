@@ -1,0 +1,95 @@
+// Multi-tensor row movement: one launch copies rows of up to kMaxDescs row-major tensors.
+//
+// A world operation touches every per-cell array at once -- cell molecules, positions, lifetimes,
+// divisions, the genome and label arenas and the nine kinetics parameter tensors -- with the same
+// row mapping (order-preserving compaction on kill_cells, parent -> child cloning on divide_cells).
+// Instead of one gather launch per tensor (plus a copy back), all of them go through one kernel:
+// the work is flattened over (descriptor, row, 16-byte chunk) with a prefix over descriptors, so
+// large rows (kinetics (P, s) slices of a few KiB) and 4-byte rows share one grid.
+#include <tuple>
+#include <vector>
+
+#include "hip_common.h"
+
+namespace msd {
+
+constexpr int kMaxDescs = 24;
+
+struct RowDesc {
+  const uint8_t* src;
+  uint8_t* dst;
+  long long src_stride, dst_stride;  // bytes between rows
+  int units;                         // row size in units
+  int unit;                          // 16 or 4 bytes
+};
+
+struct RowArgs {
+  RowDesc d[kMaxDescs];
+  long long first[kMaxDescs + 1];  // prefix of n * units over descriptors
+  int nd, n;
+  const int64_t* src_rows;  // nullptr: identity
+  const int64_t* dst_rows;  // nullptr: identity
+};
+
+__global__ void __launch_bounds__(256) gather_rows_kernel(RowArgs a) {
+  const long long total = a.first[a.nd];
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    int k = 0;
+    while (k + 1 < a.nd && a.first[k + 1] <= t) ++k;
+    const RowDesc& d = a.d[k];
+    const long long u = t - a.first[k];
+    const int i = (int)(u / d.units), c = (int)(u - (long long)i * d.units);
+    const long long sr = a.src_rows ? a.src_rows[i] : i;
+    const long long dr = a.dst_rows ? a.dst_rows[i] : i;
+    if (d.unit == 16) {
+      const uint4* s = reinterpret_cast<const uint4*>(d.src + sr * d.src_stride) + c;
+      reinterpret_cast<uint4*>(d.dst + dr * d.dst_stride)[c] = *s;
+    } else {
+      const uint32_t* s = reinterpret_cast<const uint32_t*>(d.src + sr * d.src_stride) + c;
+      reinterpret_cast<uint32_t*>(d.dst + dr * d.dst_stride)[c] = *s;
+    }
+  }
+}
+
+// descs: (src_ptr, dst_ptr, src_stride_bytes, dst_stride_bytes, row_bytes) per tensor. Row bytes and
+// strides must be multiples of 4 (of 16 for the vector path, chosen per tensor).
+void gather_rows(int n, uintptr_t src_rows, uintptr_t dst_rows,
+                 const std::vector<std::tuple<uintptr_t, uintptr_t, long long, long long, long long>>& descs,
+                 uintptr_t stream) {
+  if (n <= 0 || descs.empty()) return;
+  for (size_t b = 0; b < descs.size(); b += kMaxDescs) {
+    RowArgs a{};
+    a.n = n;
+    a.src_rows = src_rows ? P_<int64_t>(src_rows) : nullptr;
+    a.dst_rows = dst_rows ? P_<int64_t>(dst_rows) : nullptr;
+    int nd = 0;
+    long long acc = 0;
+    for (size_t q = b; q < descs.size() && nd < kMaxDescs; ++q) {
+      const auto& [sp, dp, ss, ds, rb] = descs[q];
+      if (rb <= 0) continue;
+      if (rb % 4 || ss % 4 || ds % 4 || sp % 4 || dp % 4)
+        throw std::invalid_argument("gather_rows: rows, strides and pointers must be 4-byte aligned");
+      const bool vec = rb % 16 == 0 && ss % 16 == 0 && ds % 16 == 0 && sp % 16 == 0 && dp % 16 == 0;
+      RowDesc& d = a.d[nd];
+      d.src = P_<uint8_t>(sp);
+      d.dst = P_<uint8_t>(dp);
+      d.src_stride = ss;
+      d.dst_stride = ds;
+      d.unit = vec ? 16 : 4;
+      d.units = (int)(rb / d.unit);
+      a.first[nd] = acc;
+      acc += (long long)n * d.units;
+      ++nd;
+    }
+    a.first[nd] = acc;
+    a.nd = nd;
+    if (nd == 0 || acc == 0) continue;
+    const long long blocks = (acc + 255) / 256;
+    const unsigned grid = (unsigned)(blocks < 65536 ? blocks : 65536);
+    gather_rows_kernel<<<grid, 256, 0, S_(stream)>>>(a);
+    MS_LAUNCH_CHECK();
+  }
+}
+
+}  // namespace msd

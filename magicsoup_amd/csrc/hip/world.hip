@@ -165,6 +165,54 @@ __global__ void __launch_bounds__(256) scale_planes_kernel(float* map, const flo
     map[i] *= f[i / plane];
 }
 
+// Division bookkeeping after the rows were cloned (reference world.py:446-473): parent and child
+// share the parent's molecules half-half, both get divisions + 1 and lifetime 0. One thread per
+// (pair, molecule); molecule 0 threads also do the scalar fields.
+__global__ void __launch_bounds__(256) split_cells_kernel(int k, int m, const int64_t* parents, const int64_t* children,
+                                                          float* cell_mols, int32_t* divisions, int32_t* lifetimes) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)k * m) return;
+  const int i = (int)(t / m), j = (int)(t - (long long)i * m);
+  const long long p = parents[i], c = children[i];
+  const float h = cell_mols[p * m + j] * 0.5f;
+  cell_mols[p * m + j] = h;
+  cell_mols[c * m + j] = h;
+  if (j == 0) {
+    const int32_t d = divisions[p] + 1;
+    divisions[p] = d;
+    divisions[c] = d;
+    lifetimes[p] = 0;
+    lifetimes[c] = 0;
+  }
+}
+
+// Killed cells spill their molecules onto their pixel and free it (reference world.py:520-530);
+// new cells take half of their pixel's molecules (world.py:326-331). One thread per
+// (cell, molecule); pixels are distinct, so no atomics.
+__global__ void __launch_bounds__(256) spill_free_kernel(int k, int m, const int64_t* idxs, const int32_t* pos, int C,
+                                                         long long plane, const float* cell_mols, float* map,
+                                                         uint8_t* cell_map) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)k * m) return;
+  const int i = (int)(t / m), j = (int)(t - (long long)i * m);
+  const long long c = idxs[i];
+  const long long pix = (long long)pos[2 * c] * C + pos[2 * c + 1];
+  map[j * plane + pix] += cell_mols[c * m + j];
+  if (j == 0) cell_map[pix] = 0;
+}
+
+__global__ void __launch_bounds__(256) pickup_kernel(int k, int m, const int64_t* idxs, const int32_t* pos, int C,
+                                                     long long plane, float* cell_mols, float* map) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)k * m) return;
+  const int i = (int)(t / m), j = (int)(t - (long long)i * m);
+  const long long c = idxs[i];
+  const long long pix = (long long)pos[2 * c] * C + pos[2 * c + 1];
+  const float half = map[j * plane + pix] * 0.5f;
+  cell_mols[c * m + j] += half;
+  map[j * plane + pix] -= half;
+}
+
 // exchange between cells and their pixels, one thread per (cell, molecule)
 __global__ void __launch_bounds__(256) permeate_kernel(int c, int m, Geom g, const int32_t* pos, const float* perm,
                                                        float* cell_mols, float* map) {
@@ -245,6 +293,55 @@ __global__ void __launch_bounds__(256) pick_neighbour_kernel(int k, const int64_
   cand[i] = fr[rng.below((uint32_t)nf)];
 }
 
+// Device-resolved placement rounds (divide / move): in a round every pending cell bids for a
+// random free Moore neighbour with atomicMin(claim[pixel], list position); the lowest list position
+// wins each pixel (the reference places cells in list order, rust/world.rs:59-146), losers retry
+// next round against the updated occupancy. `claim` is an int32 per pixel kept at INT_MAX between
+// rounds: the winner resets its pixel (a loser reading the reset value still sees "not mine").
+// Cells without any free neighbour drop out. No host synchronisation between rounds.
+constexpr int kNoClaim = 0x7FFFFFFF;
+
+__global__ void __launch_bounds__(256) place_bid_kernel(int k, const int64_t* cells, const int32_t* pos, Geom g,
+                                                        const uint8_t* cell_map, uint8_t* pending, uint64_t seed,
+                                                        uint64_t call, long long* cand, int* claim) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k || !pending[i]) return;
+  const int c = (int)cells[i];
+  long long nb[8], fr[8];
+  const int cnt = moore(pos[2 * c], pos[2 * c + 1], g, nb);
+  int nf = 0;
+  for (int q = 0; q < cnt; ++q)
+    if (!cell_map[nb[q]]) fr[nf++] = nb[q];
+  if (nf == 0) {
+    pending[i] = 0;
+    cand[i] = -1;
+    return;
+  }
+  Philox rng(seed, call, (uint32_t)i);
+  const long long px = fr[rng.below((uint32_t)nf)];
+  cand[i] = px;
+  atomicMin(claim + px, i);
+}
+
+__global__ void __launch_bounds__(256) place_resolve_kernel(int k, const int64_t* cells, const int32_t* pos, Geom g,
+                                                            bool vacate, uint8_t* cell_map, uint8_t* pending,
+                                                            const long long* cand, int* claim, long long* result) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k || !pending[i]) return;
+  const long long px = cand[i];
+  if (px < 0 || claim[px] != i) return;
+  claim[px] = kNoClaim;
+  cell_map[px] = 1;
+  result[i] = px;
+  pending[i] = 0;
+  // a move into a halo row is committed only after the owning rank accepts it: keep the pixel
+  const int x = (int)(px / g.C);
+  if (vacate && (g.wrap || (x >= g.r_lo && x < g.r_hi))) {
+    const int c = (int)cells[i];
+    cell_map[(size_t)pos[2 * c] * g.C + pos[2 * c + 1]] = 0;
+  }
+}
+
 // ---------------------------------------------------------------- neighbours
 __global__ void __launch_bounds__(256) index_map_kernel(int c, const int32_t* pos, int C, int32_t* idx_map, bool clear) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -311,6 +408,33 @@ void scale_planes(int m, long long plane, uintptr_t map, uintptr_t f, uintptr_t 
   MS_LAUNCH_CHECK();
 }
 
+void spill_free(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
+                uintptr_t cell_map, uintptr_t stream) {
+  if (k <= 0 || m <= 0) return;
+  spill_free_kernel<<<cdiv((long long)k * m, 256), 256, 0, S_(stream)>>>(
+      k, m, P_<int64_t>(idxs), P_<int32_t>(pos), C, (long long)R * C, P_<float>(cell_mols), P_<float>(map),
+      P_<uint8_t>(cell_map));
+  MS_LAUNCH_CHECK();
+}
+
+void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
+            uintptr_t stream) {
+  if (k <= 0 || m <= 0) return;
+  pickup_kernel<<<cdiv((long long)k * m, 256), 256, 0, S_(stream)>>>(k, m, P_<int64_t>(idxs), P_<int32_t>(pos), C,
+                                                                     (long long)R * C, P_<float>(cell_mols),
+                                                                     P_<float>(map));
+  MS_LAUNCH_CHECK();
+}
+
+void split_cells(int k, int m, uintptr_t parents, uintptr_t children, uintptr_t cell_mols, uintptr_t divisions,
+                 uintptr_t lifetimes, uintptr_t stream) {
+  if (k <= 0 || m <= 0) return;
+  split_cells_kernel<<<cdiv((long long)k * m, 256), 256, 0, S_(stream)>>>(
+      k, m, P_<int64_t>(parents), P_<int64_t>(children), P_<float>(cell_mols), P_<int32_t>(divisions),
+      P_<int32_t>(lifetimes));
+  MS_LAUNCH_CHECK();
+}
+
 void permeate(int c, int m, int R, int C, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map,
               uintptr_t stream) {
   if (c <= 0 || m <= 0) return;
@@ -338,6 +462,24 @@ void pick_neighbour(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_l
                                                                P_<uint8_t>(cell_map), P_<uint8_t>(pending), seed, call,
                                                                P_<long long>(cand));
   MS_LAUNCH_CHECK();
+}
+
+void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, bool vacate,
+                  uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result, int rounds,
+                  uint64_t seed, uint64_t call, uintptr_t stream) {
+  if (k <= 0) return;
+  const Geom g = geom(R, C, r_lo, r_hi, wrap);
+  const unsigned grid = cdiv(k, 256);
+  for (int r = 0; r < rounds; ++r) {
+    place_bid_kernel<<<grid, 256, 0, S_(stream)>>>(k, P_<int64_t>(cells), P_<int32_t>(pos), g, P_<uint8_t>(cell_map),
+                                                   P_<uint8_t>(pending), seed, call + ((uint64_t)r << 48), P_<long long>(cand),
+                                                   P_<int>(claim));
+    MS_LAUNCH_CHECK();
+    place_resolve_kernel<<<grid, 256, 0, S_(stream)>>>(k, P_<int64_t>(cells), P_<int32_t>(pos), g, vacate,
+                                                       P_<uint8_t>(cell_map), P_<uint8_t>(pending),
+                                                       P_<long long>(cand), P_<int>(claim), P_<long long>(result));
+    MS_LAUNCH_CHECK();
+  }
 }
 
 void index_map(int c, uintptr_t pos, int C, uintptr_t idx_map, bool clear, uintptr_t stream) {

@@ -298,13 +298,15 @@ void build_params(iarr tokens, iarr rows, farr vmax_w, farr km_w, iarr signs, ia
           }
         }
       }
-      float E = 0.0f;
+      // integer N times float energies, summed in double: exact, so independent of the order
+      // (the device reduces it across lanes)
+      double E = 0.0;
       for (int j = 0; j < s; ++j) {
         const float km_mean = kmr_cnt[j] > 0 ? kmr_sum[j] / (float)kmr_cnt[j] : 0.0f;
         kmr_[j] = powf(km_mean, (float)a_[j]);
-        E += (float)n_[j] * en[j];
+        E += (double)n_[j] * (double)en[j];
       }
-      float ke = expf(-E / abs_temp / gas_const);
+      float ke = expf(-(float)E / abs_temp / gas_const);
       ke = ke < ms::kEps ? ms::kEps : (ke > ms::kMax ? ms::kMax : ke);
       const float kmn = km.value0();
       float kmf = ke >= 1.0f ? kmn : kmn / ke;

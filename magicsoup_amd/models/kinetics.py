@@ -383,8 +383,35 @@ class Kinetics:
             self._bufs[name] = spare
             setattr(self, name, spare[:k])
 
-    def increase_max_cells(self, by_n: int):
-        """Append ``by_n`` zero rows to every parameter tensor."""
+    def _param_tensors(self) -> list[torch.Tensor]:
+        return [getattr(self, name) for name in _PARAMS]
+
+    def _compact_pairs(self, k: int) -> list[tuple[torch.Tensor, torch.Tensor]]:
+        """(current, spare target) row tensors for an order-preserving compaction to ``k`` rows;
+        the caller gathers, then :meth:`_commit_compact` swaps the buffers."""
+        spares = self.__dict__.setdefault("_spares", {})
+        pairs = []
+        for name in _PARAMS:
+            t = getattr(self, name)
+            buf = self._buffer(name)
+            spare = spares.get(name)
+            if spare is None or spare.size(0) < k or spare.shape[1:] != buf.shape[1:] or spare.dtype != buf.dtype:
+                spare = spares[name] = torch.empty(max(k, buf.size(0)), *buf.shape[1:], dtype=buf.dtype,
+                                                   device=buf.device)
+            pairs.append((t, spare[:k]))
+        return pairs
+
+    def _commit_compact(self, k: int) -> None:
+        spares = self.__dict__["_spares"]
+        for name in _PARAMS:
+            buf, spare = self._bufs[name], spares[name]
+            spares[name] = buf
+            self._bufs[name] = spare
+            setattr(self, name, spare[:k])
+
+    def increase_max_cells(self, by_n: int, zero: bool = True):
+        """Append ``by_n`` rows (zero-filled unless the caller writes them all) to every parameter
+        tensor."""
         if by_n <= 0:
             return
         for name in _PARAMS:
@@ -397,7 +424,8 @@ class Kinetics:
                 nb[:n] = t
                 buf = self._bufs[name] = nb
             view = buf[: n + by_n]
-            view[n:].zero_()
+            if zero:
+                view[n:].zero_()
             setattr(self, name, view)
 
     def increase_max_proteins(self, max_n: int):

@@ -128,6 +128,33 @@ class StringArena:
         self.n = 0
         self.version += 1
 
+    # ---------------------------------------------------------------- fused row movement (device)
+    def compact_pairs(self, k: int) -> list[tuple[torch.Tensor, torch.Tensor]]:
+        """(source, target) row tensors for an order-preserving compaction to ``k`` rows into the
+        spare buffers (see :meth:`commit_compact`)."""
+        sp = self.__dict__.get("_spare")
+        cap = max(k, self.capacity)
+        if sp is None or sp[0].size(0) < cap or sp[0].size(1) != self.width or sp[0].device != self.data.device:
+            sp = (torch.empty(cap, self.width, dtype=torch.uint8, device=self.device),
+                  torch.empty(cap, dtype=torch.int32, device=self.device))
+            self.__dict__["_spare"] = sp
+        return [(self.data[: self.n], sp[0][:k]), (self.lens[: self.n], sp[1][:k])]
+
+    def commit_compact(self, k: int) -> None:
+        sd, sl = self.__dict__.pop("_spare")
+        self.__dict__["_spare"] = (self.data, self.lens)
+        self.data, self.lens = sd, sl
+        self.n = k
+        self.version += 1
+
+    def clone_pairs(self, k: int) -> list[tuple[torch.Tensor, torch.Tensor]]:
+        """Append ``k`` rows and return in-place (source, target) row tensors covering old and new
+        rows, for copying existing rows into the new ones."""
+        self.reserve(self.n + k)
+        self.n += k
+        self.version += 1
+        return [(self.data[: self.n], self.data[: self.n]), (self.lens[: self.n], self.lens[: self.n])]
+
     def view(self) -> tuple[torch.Tensor, torch.Tensor]:
         return self.data[: self.n], self.lens[: self.n]
 

@@ -62,14 +62,18 @@ def _permeation_factor(rate: float) -> float:
 
 
 class _Column:
-    """A capacity-managed per-cell buffer exposed as a cached view of its first ``n`` rows."""
+    """A capacity-managed per-cell buffer exposed as a cached view of its first ``n`` rows.
 
-    __slots__ = ("buf", "_view", "_n")
+    ``spare`` is a second buffer of the same capacity: an order-preserving compaction gathers the
+    surviving rows into it and the two are swapped (no copy back)."""
+
+    __slots__ = ("buf", "_view", "_n", "spare")
 
     def __init__(self, buf: torch.Tensor):
         self.buf = buf
         self._view: torch.Tensor | None = None
         self._n = -1
+        self.spare: torch.Tensor | None = None
 
     def view(self, n: int) -> torch.Tensor:
         if self._view is None or self._n != n:
@@ -92,6 +96,17 @@ class _Column:
         if n_old:
             nb[:n_old] = self.view(n_old)
         self.buf = nb
+        self._view = None
+
+    def spare_rows(self, k: int) -> torch.Tensor:
+        sp = self.spare
+        b = self.buf
+        if sp is None or sp.size(0) < max(k, b.size(0)) or sp.shape[1:] != b.shape[1:] or sp.dtype != b.dtype:
+            sp = self.spare = torch.empty(max(k, b.size(0)), *b.shape[1:], dtype=b.dtype, device=b.device)
+        return sp[:k]
+
+    def swap(self) -> None:
+        self.buf, self.spare = self.spare, self.buf
         self._view = None
 
 
@@ -250,14 +265,39 @@ class World:
         for col in self._cols.values():
             col.reserve(self.n_cells, n_new)
 
-    def _grow(self, k: int) -> None:
-        """Append k zero-initialised cell rows to every per-cell array (world + kinetics)."""
+    def _grow(self, k: int, zero: bool = True) -> None:
+        """Append k cell rows to every per-cell array (world + kinetics); zero-initialised unless
+        the caller overwrites them all."""
         n = self.n_cells
         self._reserve(n + k)
-        for col in self._cols.values():
-            col.buf[n : n + k] = 0
+        if zero:
+            for col in self._cols.values():
+                col.buf[n : n + k] = 0
         self.n_cells = n + k
-        self.kinetics.increase_max_cells(by_n=k)
+        self.kinetics.increase_max_cells(by_n=k, zero=zero)
+
+    def _clone_rows(self, src: torch.Tensor, dst: torch.Tensor) -> None:
+        """Append copies of cells ``src`` as the new rows ``dst`` (= n_cells, n_cells + 1, ...):
+        columns, genome / label arena rows and kinetics parameters."""
+        k = int(src.numel())
+        n0 = self.n_cells
+        if not src.is_cuda:
+            self._grow(k)
+            self._genomes.append_rows_from(src)
+            self._labels.append_rows_from(src)
+            for name, col in self._cols.items():
+                if name != "cell_positions":
+                    col.buf[n0 : n0 + k] = col.buf[src]
+            self.kinetics.copy_cell_params(from_idxs=src, to_idxs=dst)
+            return
+        from magicsoup_amd.ops import hip_ops
+
+        self._grow(k, zero=False)
+        n = self.n_cells
+        pairs = [(col.view(n), col.view(n)) for name, col in self._cols.items() if name != "cell_positions"]
+        pairs += self._genomes.clone_pairs(k) + self._labels.clone_pairs(k)
+        pairs += [(t, t) for t in self.kinetics._param_tensors()]
+        hip_ops.gather_rows(pairs, k, src_rows=src, dst_rows=dst)
 
     def _idx_tensor(self, idxs, unique: bool = True) -> torch.Tensor:
         if isinstance(idxs, torch.Tensor):
@@ -402,11 +442,8 @@ class World:
             if k == 0:
                 return empty, empty
             n0 = self.n_cells
-            self._grow(k)
             children = torch.arange(n0, n0 + k, device=self.device)
-            self._genomes.append_rows_from(parents)
-            self._labels.append_rows_from(parents)
-            self.kinetics.copy_cell_params(from_idxs=parents, to_idxs=children)
+            self._clone_rows(parents, children)
             self._place(children, child_pos)
             world_ops.split_cells(self, parents, children)
             return parents, children
@@ -442,6 +479,23 @@ class World:
 
     def _compact(self, keep_idx: torch.Tensor, keep: torch.Tensor) -> None:
         n_new = int(keep_idx.numel())
+        if keep_idx.is_cuda:
+            # every per-cell array (columns, arenas, kinetics parameters) in one gather launch
+            # into spare buffers, then swap
+            from magicsoup_amd.ops import hip_ops
+
+            n = self.n_cells
+            pairs = [(col.view(n), col.spare_rows(n_new)) for col in self._cols.values()]
+            pairs += self._genomes.compact_pairs(n_new) + self._labels.compact_pairs(n_new)
+            pairs += self.kinetics._compact_pairs(n_new)
+            hip_ops.gather_rows(pairs, n_new, src_rows=keep_idx)
+            for col in self._cols.values():
+                col.swap()
+            self._genomes.commit_compact(n_new)
+            self._labels.commit_compact(n_new)
+            self.kinetics._commit_compact(n_new)
+            self.n_cells = n_new
+            return
         for col in self._cols.values():
             v = col.view(self.n_cells)
             col.buf[:n_new] = v[keep_idx]

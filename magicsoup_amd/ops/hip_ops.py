@@ -271,55 +271,33 @@ def free_positions(world, k: int) -> torch.Tensor:
     return torch.stack([got // C, got % C], dim=1).to(torch.int32)
 
 
-def _place_rounds(world, cells: torch.Tensor, vacate: bool, max_rounds: int = 16):
-    """Priority-ordered parallel neighbour claims. Returns (winner cells, new pixels)."""
+_PLACE_ROUNDS = 8
+
+
+def _place_rounds(world, cells: torch.Tensor, vacate: bool, rounds: int = _PLACE_ROUNDS):
+    """Priority-ordered parallel neighbour claims resolved on the device (atomicMin per pixel, see
+    world.hip place_rounds). Returns (winner cells in list order, new pixels int32 (k', 2))."""
     R, C, r_lo, r_hi, wrap = geom(world)
     dev = cells.device
     k = int(cells.numel())
     _ensure_world_layout(world)
     pos = world.cell_positions
     cmap = _cell_map_bytes(world)
-    pending = torch.ones(k, dtype=torch.uint8, device=dev)
-    cand = torch.empty(k, dtype=torch.int64, device=dev)
-    win_cells, win_pix = [], []
-    order = torch.arange(k, device=dev)
-    for _ in range(max_rounds):
-        seed, call = _rng()
-        _m().pick_neighbour(k, _p(cells), _p(pos), R, C, r_lo, r_hi, wrap, _p(cmap), _p(pending), seed, call,
-                            _p(cand), _stream())
-        has = cand >= 0
-        # cells without any free neighbour give up (reference: they do not divide / move)
-        pending &= has.to(torch.uint8)
-        idx = torch.nonzero(has).flatten()
-        if idx.numel() == 0:
-            break
-        px = cand[idx]
-        # lowest list position wins each contested pixel
-        key = px * k + order[idx]
-        srt = torch.sort(key).values
-        first = torch.ones_like(srt, dtype=torch.bool)
-        first[1:] = (srt[1:] // k) != (srt[:-1] // k)
-        wins = srt[first] % k
-        wpix = cand[wins]
-        cmap[wpix] = 1
-        if vacate:
-            # a move into a halo row is only committed once the owning rank accepts it, so the
-            # mover keeps its pixel until then (magicsoup_amd.parallel)
-            mv = wins if wrap else wins[(wpix >= r_lo * C) & (wpix < r_hi * C)]
-            old = pos[cells[mv]].long()
-            cmap[old[:, 0] * C + old[:, 1]] = 0
-        pending[wins] = 0
-        win_cells.append(wins)
-        win_pix.append(wpix)
-        if not bool(pending.any()):
-            break
-    if not win_cells:
-        e = torch.zeros(0, dtype=torch.long, device=dev)
-        return e, torch.zeros(0, 2, dtype=torch.int32, device=dev)
-    wins = torch.cat(win_cells)
-    wpix = torch.cat(win_pix)
-    o = torch.argsort(wins)
-    wins, wpix = wins[o], wpix[o]
+    sc = _scratch(world)
+    claim = world.__dict__.get("_claim_map")
+    if claim is None or claim.numel() != R * C or claim.device != dev:
+        claim = torch.full((R * C,), 0x7FFFFFFF, dtype=torch.int32, device=dev)
+        world.__dict__["_claim_map"] = claim
+    pending = sc.get("pl_pending", k, torch.uint8, dev)
+    pending.fill_(1)
+    cand = sc.get("pl_cand", k, torch.int64, dev)
+    result = sc.get("pl_result", k, torch.int64, dev)
+    result.fill_(-1)
+    seed, call = _rng()
+    _m().place_rounds(k, _p(cells), _p(pos), R, C, r_lo, r_hi, wrap, bool(vacate), _p(cmap), _p(pending), _p(cand),
+                      _p(claim), _p(result), int(rounds), seed, call, _stream())
+    wins = torch.nonzero(result >= 0).flatten()
+    wpix = result[wins]
     return cells[wins], torch.stack([wpix // C, wpix % C], dim=1).to(torch.int32)
 
 
@@ -332,18 +310,55 @@ def move_placement(world, idxs: torch.Tensor):
     return _place_rounds(world, idxs.to(torch.int64).contiguous(), vacate=True)
 
 
+def spill_and_free(world, idxs: torch.Tensor) -> None:
+    """Killed cells spill their molecules onto their pixel and release it (one launch)."""
+    _ensure_world_layout(world)
+    R, C = geom(world)[:2]
+    ix = idxs.to(torch.int64).contiguous()
+    _m().spill_free(int(ix.numel()), world.n_molecules, _p(ix), _p(world.cell_positions), R, C,
+                    _p(world.cell_molecules), _p(world._molmap), _p(_cell_map_bytes(world)), _stream())
+
+
+def pickup_molecules(world, new: torch.Tensor) -> None:
+    """New cells take half of their pixel's molecules (one launch; positions already set)."""
+    _ensure_world_layout(world)
+    R, C = geom(world)[:2]
+    ix = new.to(torch.int64).contiguous()
+    _m().pickup(int(ix.numel()), world.n_molecules, _p(ix), _p(world.cell_positions), R, C,
+                _p(world.cell_molecules), _p(world._molmap), _stream())
+
+
 def split_cells(world, parents: torch.Tensor, children: torch.Tensor) -> None:
-    cm = world.cell_molecules
-    half = cm[parents] * 0.5
-    cm[parents] = half
-    cm[children] = half
-    dv = world.cell_divisions
-    d = dv[parents] + 1
-    dv[parents] = d
-    dv[children] = d
-    lt = world.cell_lifetimes
-    lt[parents] = 0
-    lt[children] = 0
+    """Halve the parents' molecules into both descendants; divisions + 1, lifetime 0 (one launch)."""
+    _ensure_world_layout(world)
+    k = int(parents.numel())
+    par = parents.to(torch.int64).contiguous()
+    chi = children.to(torch.int64).contiguous()
+    _m().split_cells(k, world.n_molecules, _p(par), _p(chi), _p(world.cell_molecules), _p(world.cell_divisions),
+                     _p(world.cell_lifetimes), _stream())
+
+
+def gather_rows(pairs, n: int, src_rows: torch.Tensor | None = None, dst_rows: torch.Tensor | None = None) -> None:
+    """dst[dst_rows[i]] = src[src_rows[i]] for i < n, for every (src, dst) tensor pair, in one launch
+    (rows are dim 0; each row contiguous; identity where an index tensor is None)."""
+    descs = []
+    for src, dst in pairs:
+        if src.dim() == 0:
+            continue
+        es = src.element_size()
+        row = 1
+        for d in src.shape[1:]:
+            row *= int(d)
+        if row == 0:
+            continue
+        assert dst.dtype == src.dtype and tuple(dst.shape[1:]) == tuple(src.shape[1:]), "gather_rows: shape mismatch"
+        assert src.dim() == 1 or (src.stride(-1) == 1 and src[0].is_contiguous()), "gather_rows: rows must be contiguous"
+        descs.append((src.data_ptr(), dst.data_ptr(), src.stride(0) * es, dst.stride(0) * es, row * es))
+    if n <= 0 or not descs:
+        return
+    sr = None if src_rows is None else src_rows.to(torch.int64).contiguous()
+    dr = None if dst_rows is None else dst_rows.to(torch.int64).contiguous()
+    _m().gather_rows(int(n), _p(sr), _p(dr), descs, _stream())
 
 
 def neighbors(world, frm: torch.Tensor, to: torch.Tensor, pos: torch.Tensor | None = None, n: int | None = None) -> torch.Tensor:

@@ -21,7 +21,8 @@ _gen_cpu.manual_seed(torch.initial_seed() & 0xFFFFFFFF)
 
 
 def _is_gpu(world) -> bool:
-    return world.molecule_map.is_cuda
+    # the raw buffer: reading `molecule_map` would apply a pending (fused) degradation
+    return world.__dict__["_molmap"].is_cuda
 
 
 def _hip():
@@ -131,6 +132,10 @@ def random_labels(world, k: int, length: int):
 # ---------------------------------------------------------------------------- cell <-> map exchange
 def pickup_molecules(world, new: torch.Tensor, pos: torch.Tensor) -> None:
     """New cells take half of their pixel's molecules."""
+    if world.__dict__["_molmap"].is_cuda:
+        # a pending degradation must be applied before pixels change
+        _molmap(world)
+        return _hip().pickup_molecules(world, new)
     mm = _molmap(world)
     xs, ys = pos[:, 0].long(), pos[:, 1].long()
     half = mm[:, xs, ys] * 0.5
@@ -140,6 +145,9 @@ def pickup_molecules(world, new: torch.Tensor, pos: torch.Tensor) -> None:
 
 def spill_and_free(world, idxs: torch.Tensor) -> None:
     """Killed cells release their pixel and spill their molecules onto it."""
+    if world.__dict__["_molmap"].is_cuda:
+        _molmap(world)
+        return _hip().spill_and_free(world, idxs)
     mm = _molmap(world)
     pos = world.cell_positions[idxs].long()
     xs, ys = pos[:, 0], pos[:, 1]

@@ -386,11 +386,8 @@ class DistributedWorld(World):
         if k == 0:
             return empty, empty
         n0 = self.n_cells
-        self._grow(k)
         children = torch.arange(n0, n0 + k, device=dev)
-        self._genomes.append_rows_from(parents)
-        self._labels.append_rows_from(parents)
-        self.kinetics.copy_cell_params(from_idxs=parents, to_idxs=children)
+        self._clone_rows(parents, children)
         self._place(children, cpos)
         world_ops.split_cells(self, parents, children)
         return parents, children
