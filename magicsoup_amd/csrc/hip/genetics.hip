@@ -22,6 +22,10 @@ constexpr int kLutBytes = 64 * 3 + 16 + 4096 * 2;
 
 struct TransArgs {
   int n, width, gpb, cap, dt_entries;
+  int lmax;                    // slot capacity (positions); longer genomes take the global-slot pass
+  uint8_t* gslot;              // global slots (long-genome pass) or nullptr (LDS slots)
+  const int32_t* list;         // item -> genome index (long-genome pass) or nullptr (identity)
+  int32_t *long_list, *long_count;  // LDS count pass: genomes longer than lmax
   bool stage_dt;
   const int64_t* rows;
   const uint8_t* arena;
@@ -56,16 +60,19 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   const uint16_t* l_two = reinterpret_cast<const uint16_t*>(sm + 64 * 3 + 16);
   uint8_t* l_dt = sm + kLutBytes;
   const int dt_bytes = a.stage_dt ? ((a.dt_entries + 15) & ~15) : 0;
-  // per-wave slot: CDS lists [2][cap] u32, next stop [2][width] u16, emission order [2][cap] u16,
-  // codons [2][width] u8, domain type at position [2][width] u8, counters
-  const size_t slot_bytes = slot_bytes_for(a.width, a.cap);
-  uint8_t* slot = sm + kLutBytes + dt_bytes + (size_t)wid * slot_bytes;
+  // per-wave slot: CDS lists [2][cap] u32, next stop [2][lmax] u16, emission order [2][cap] u16,
+  // codons [2][lmax] u8, domain type at position [2][lmax] u8, counters
+  const size_t slot_bytes = slot_bytes_for(a.lmax, a.cap);
+  const int item = blockIdx.x * a.gpb + wid;
+  uint8_t* slot = a.gslot ? a.gslot + (size_t)item * slot_bytes
+                          : sm + kLutBytes + dt_bytes + (size_t)wid * slot_bytes;
+  const int LW = a.lmax;
   uint32_t* cds = reinterpret_cast<uint32_t*>(slot);  // (q << 16) | p
   uint16_t* nstop = reinterpret_cast<uint16_t*>(cds + 2 * a.cap);
-  uint16_t* order = nstop + 2 * a.width;
+  uint16_t* order = nstop + 2 * LW;
   uint8_t* cod = reinterpret_cast<uint8_t*>(order + 2 * a.cap);
-  uint8_t* dtp = cod + 2 * a.width;
-  int* counters = reinterpret_cast<int*>(dtp + 2 * a.width);
+  uint8_t* dtp = cod + 2 * LW;
+  int* counters = reinterpret_cast<int*>(dtp + 2 * LW);
 
   for (int i = threadIdx.x; i < 64; i += blockDim.x) {
     l_start[i] = a.is_start[i];
@@ -79,8 +86,8 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
       reinterpret_cast<uint4*>(l_dt)[i] = reinterpret_cast<const uint4*>(a.dom_type)[i];
   const uint8_t* DT = a.stage_dt ? l_dt : a.dom_type;
 
-  const int g = blockIdx.x * a.gpb + wid;
-  const bool active = wid < a.gpb && g < a.n;
+  const bool active = wid < a.gpb && item < a.n;
+  const int g = active ? (a.list ? a.list[item] : item) : 0;
   int L = 0;
   const uint8_t* s = nullptr;
   if (active) {
@@ -91,6 +98,11 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   }
   __syncthreads();
   if (!active) return;  // whole waves only; no block-wide barrier below
+  if (L > LW) {         // LDS pass: too long for a slot -> queued for the global-slot pass
+    if (!kWrite && lane == 0) a.long_list[atomicAdd(a.long_count, 1)] = g;
+    return;
+  }
+  wave_sync();
 
   // ---- 1. codon index per position, both strands (0xFF past the end)
   const int ncod = L - 2;
@@ -103,7 +115,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
                      (ms::nt_comp(ms::nt_code(s[L - 2 - i])) << 2) | ms::nt_comp(ms::nt_code(s[L - 3 - i])));
     }
     cod[i] = cf;
-    cod[a.width + i] = cr;
+    cod[LW + i] = cr;
   }
   wave_sync();
 
@@ -111,8 +123,8 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   //         domain type starting at every position
   const int ds = a.dom_size, dts = a.dom_type_size, ntc = dts / 3;
   for (int st = 0; st < 2; ++st) {
-    const uint8_t* c = cod + st * a.width;
-    uint16_t* ns = nstop + st * a.width;
+    const uint8_t* c = cod + st * LW;
+    uint16_t* ns = nstop + st * LW;
     for (int f = 0; f < 3; ++f) {
       const int nf = ncod > f ? (ncod - f + 2) / 3 : 0;  // positions f, f+3, ... < ncod
       int carry = 0xFFFF;
@@ -129,7 +141,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
         carry = __shfl(v, 0);
       }
     }
-    uint8_t* dt = dtp + st * a.width;
+    uint8_t* dt = dtp + st * LW;
     for (int p = lane; p < L; p += 64) {
       uint8_t ty = 0;
       if (p + dts <= L) {
@@ -145,8 +157,8 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   // ---- 3. CDS candidates: start codon -> first in-frame stop (too short / unstopped: dropped)
   if (L >= a.dom_size && L >= 3) {
     for (int st = 0; st < 2; ++st) {
-      const uint8_t* c = cod + st * a.width;
-      const uint16_t* ns = nstop + st * a.width;
+      const uint8_t* c = cod + st * LW;
+      const uint16_t* ns = nstop + st * LW;
       for (int p = lane; p < ncod; p += 64) {
         if (!l_start[c[p]]) continue;
         const int q = p + 3 < ncod ? (int)ns[p + 3] : 0xFFFF;
@@ -179,8 +191,8 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   // ---- 5. domain extraction in emission order
   int prot_base = 0;  // forward-strand proteins come first
   for (int st = 0; st < 2; ++st) {
-    const uint8_t* c = cod + st * a.width;
-    const uint8_t* dt = dtp + st * a.width;
+    const uint8_t* c = cod + st * LW;
+    const uint8_t* dt = dtp + st * LW;
     int n_prot = 0, max_dom = 0;
     for (int e0 = 0; e0 < ncds[st]; e0 += 64) {
       const int e = e0 + lane;
@@ -243,9 +255,12 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   }
 }
 
+constexpr int kLdsMaxLen = 1024;  // genomes up to this length use LDS slots
+
 static void launch(bool write, int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
                    uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
-                   uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t stream) {
+                   uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t list, uintptr_t gslot,
+                   uintptr_t long_list, uintptr_t long_count, uintptr_t stream) {
   if (n <= 0) return;
   if (width % 16 != 0) throw std::invalid_argument("genome arena width must be a multiple of 16");
   if (width > 65535) throw std::invalid_argument("genomes longer than 65535 nt are not supported on the GPU");
@@ -270,32 +285,47 @@ static void launch(bool write, int n, uintptr_t rows, uintptr_t arena, int width
   a.P = P;
   a.D = D;
   a.stage_dt = dt_entries <= 4096;
-  a.cap = width;  // a strand has at most one CDS per codon position (< width)
+  a.list = list ? P_<int32_t>(list) : nullptr;
+  a.gslot = gslot ? P_<uint8_t>(gslot) : nullptr;
+  a.long_list = P_<int32_t>(long_list);
+  a.long_count = P_<int32_t>(long_count);
+  // LDS pass: slots for genomes up to kLdsMaxLen (longer ones are queued); global pass: whole width
+  a.lmax = a.gslot ? width : (width < kLdsMaxLen ? width : kLdsMaxLen);
+  a.cap = a.lmax;  // a strand has at most one CDS per codon position
   const size_t fixed = kLutBytes + (a.stage_dt ? ((dt_entries + 15) & ~15) : 0);
-  const size_t slot = slot_bytes_for(width, a.cap);
-  if (fixed + slot > 160 * 1024) throw std::invalid_argument("genome too long for the LDS-resident translation");
+  const size_t slot = slot_bytes_for(a.lmax, a.cap);
   int gpb = kGBlock / 64;
-  while (gpb > 1 && fixed + gpb * slot > 64 * 1024) --gpb;
+  if (!a.gslot) {
+    while (gpb > 1 && fixed + gpb * slot > 64 * 1024) --gpb;
+    if (fixed + gpb * slot > 160 * 1024) throw std::invalid_argument("translation slot does not fit in LDS");
+  }
   a.gpb = gpb;
-  const size_t lds = fixed + gpb * slot;
+  const size_t lds = fixed + (a.gslot ? 0 : gpb * slot);
   const unsigned grid = cdiv(n, gpb);
   if (write) translate_kernel<true><<<grid, gpb * 64, lds, S_(stream)>>>(a);
   else translate_kernel<false><<<grid, gpb * 64, lds, S_(stream)>>>(a);
   MS_LAUNCH_CHECK();
 }
 
+size_t translate_slot_bytes(int width) { return slot_bytes_for(width, width); }
+
+// n items; list: item -> genome index into rows (0 = identity); gslot: global slots for the
+// long-genome pass (n * translate_slot_bytes(width) bytes) or 0 for the LDS pass, which queues
+// genomes longer than its slots in long_list / long_count.
 void translate_count(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
-                     uintptr_t nprot, uintptr_t ndom, uintptr_t stream) {
+                     uintptr_t nprot, uintptr_t ndom, uintptr_t list, uintptr_t gslot, uintptr_t long_list,
+                     uintptr_t long_count, uintptr_t stream) {
   launch(false, n, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot,
-         ndom, 0, 0, 0, stream);
+         ndom, 0, 0, 0, list, gslot, long_list, long_count, stream);
 }
 
 void translate_write(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
-                     uintptr_t nprot, int P, int D, uintptr_t tokens, uintptr_t stream) {
+                     uintptr_t nprot, int P, int D, uintptr_t tokens, uintptr_t list, uintptr_t gslot,
+                     uintptr_t stream) {
   launch(true, n, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot, 0,
-         P, D, tokens, stream);
+         P, D, tokens, list, gslot, 0, 0, stream);
 }
 
 }  // namespace msd

@@ -57,10 +57,13 @@ void neighbor_pairs(int nf, uintptr_t from, uintptr_t pos, int R, int C, int r_l
 // genetics.hip
 void translate_count(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
-                     uintptr_t nprot, uintptr_t ndom, uintptr_t stream);
+                     uintptr_t nprot, uintptr_t ndom, uintptr_t list, uintptr_t gslot, uintptr_t long_list,
+                     uintptr_t long_count, uintptr_t stream);
 void translate_write(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
-                     uintptr_t nprot, int P, int D, uintptr_t tokens, uintptr_t stream);
+                     uintptr_t nprot, int P, int D, uintptr_t tokens, uintptr_t list, uintptr_t gslot,
+                     uintptr_t stream);
+size_t translate_slot_bytes(int width);
 // mutations.hip
 void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
                uintptr_t stream);
@@ -112,6 +115,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("neighbor_pairs", &msd::neighbor_pairs);
   m.def("translate_count", &msd::translate_count);
   m.def("translate_write", &msd::translate_write);
+  m.def("translate_slot_bytes", &msd::translate_slot_bytes);
   m.def("mut_count", &msd::mut_count);
   m.def("mut_apply", &msd::mut_apply);
   m.def("rec_count", &msd::rec_count);

@@ -395,7 +395,10 @@ def neighbors(world, frm: torch.Tensor, to: torch.Tensor, pos: torch.Tensor | No
 
 # ---------------------------------------------------------------------------- genomes
 def translate(genetics, data: torch.Tensor, lens: torch.Tensor, rows: torch.Tensor):
-    """Two-pass device translation of arena rows ``rows`` -> (tokens (k, P, D, 5), n_prots (k,))."""
+    """Two-pass device translation of arena rows ``rows`` -> (tokens (k, P, D, 5), n_prots (k,)).
+
+    Genomes up to 1024 nt are translated from LDS slots; longer ones are queued by the count pass
+    and translated in a second launch with global-memory slots (only when there are any)."""
     dev = data.device
     n = int(rows.numel())
     tables = genetics.tables
@@ -404,14 +407,29 @@ def translate(genetics, data: torch.Tensor, lens: torch.Tensor, rows: torch.Tens
     width = int(data.size(1))
     counts = torch.empty(2 * n, dtype=torch.int32, device=dev)
     ndom = torch.empty(2 * n, dtype=torch.int32, device=dev)
+    long_list = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    long_count = torch.zeros(1, dtype=torch.int32, device=dev)
     common = (_p(luts["small"]), _p(luts["dom_type"]), int(luts["dom_type"].numel()), _p(luts["two_codon"]),
               tables.dom_size, tables.dom_type_size)
-    _m().translate_count(n, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), _p(ndom), _stream())
+    _m().translate_count(n, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), _p(ndom), 0, 0,
+                         _p(long_list), _p(long_count), _stream())
     per = counts.view(n, 2).sum(1)
-    PD = torch.stack([per.max(), ndom.max()]).tolist() if n else [0, 0]
-    P, D = max(int(PD[0]), 1), max(int(PD[1]), 1)
+    stats = torch.stack([per.max(), ndom.max(), long_count[0]]).tolist() if n else [0, 0, 0]
+    n_long = int(stats[2])
+    gslot = None
+    if n_long:
+        gslot = torch.empty(n_long * int(_m().translate_slot_bytes(width)), dtype=torch.uint8, device=dev)
+        _m().translate_count(n_long, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), _p(ndom),
+                             _p(long_list), _p(gslot), _p(long_list), _p(long_count), _stream())
+        per = counts.view(n, 2).sum(1)
+        stats = torch.stack([per.max(), ndom.max()]).tolist()
+    P, D = max(int(stats[0]), 1), max(int(stats[1]), 1)
     tokens = torch.zeros(n, P, D, 5, dtype=torch.int32, device=dev)
-    _m().translate_write(n, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), P, D, _p(tokens), _stream())
+    _m().translate_write(n, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), P, D, _p(tokens), 0, 0,
+                         _stream())
+    if n_long:
+        _m().translate_write(n_long, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), P, D, _p(tokens),
+                             _p(long_list), _p(gslot), _stream())
     return tokens, per
 
 
