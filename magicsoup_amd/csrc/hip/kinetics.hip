@@ -316,6 +316,7 @@ struct BuildArgs {
   int n, P, D, Pt, s;
   const int32_t* tokens;  // (n, P, D, 5)
   const int32_t* rows;    // (n,)
+  const int32_t* nprot;   // (n,) proteins per row (0: the row is unset, all params 0) or nullptr
   const float *vmax_w, *km_w;
   const int32_t *signs, *hills, *RM, *TM, *EM;
   int nw, nk, nsg, nh, nv;
@@ -341,6 +342,22 @@ __global__ void __launch_bounds__(kBlock) build_params_kernel(BuildArgs b) {
   const size_t row = (size_t)b.rows[ci];
   const size_t o2 = row * b.Pt + p, o3 = o2 * b.s;
   const int32_t* pt = b.tokens + ((size_t)ci * b.P + (p < b.P ? p : 0)) * b.D * 5;
+  if (b.nprot && b.nprot[ci] == 0) {  // empty proteome: unset_cell_params semantics (all zero)
+    for (int j = lane; j < b.s; j += G) {
+      b.N[o3 + j] = 0;
+      b.Nf[o3 + j] = 0;
+      b.Nb[o3 + j] = 0;
+      b.A[o3 + j] = 0;
+      b.Kmr[o3 + j] = 0.0f;
+    }
+    if (lane == 0) {
+      b.Ke[o2] = 0.0f;
+      b.Kmf[o2] = 0.0f;
+      b.Kmb[o2] = 0.0f;
+      b.Vmax[o2] = 0.0f;
+    }
+    return;
+  }
   int nd = p < b.P ? b.D : 0;
   while (nd > 0 && pt[(nd - 1) * 5] == 0) --nd;  // trailing empty domain slots
 
@@ -484,12 +501,13 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
                   uintptr_t km_w, int nk, uintptr_t signs, int nsg, uintptr_t hills, int nh, uintptr_t RM,
                   uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
                   uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
-                  uintptr_t Vmax, uintptr_t Ke, uintptr_t stream) {
+                  uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t stream) {
   if (n <= 0 || Pt <= 0) return;
   if (P > Pt) throw std::invalid_argument("build_params: token proteins exceed parameter capacity");
   BuildArgs b{};
   b.n = n; b.P = P; b.D = D; b.Pt = Pt; b.s = s;
   b.tokens = P_<int32_t>(tokens); b.rows = P_<int32_t>(rows);
+  b.nprot = nprot ? P_<int32_t>(nprot) : nullptr;
   b.vmax_w = P_<float>(vmax_w); b.km_w = P_<float>(km_w);
   b.signs = P_<int32_t>(signs); b.hills = P_<int32_t>(hills);
   b.RM = P_<int32_t>(RM); b.TM = P_<int32_t>(TM); b.EM = P_<int32_t>(EM);

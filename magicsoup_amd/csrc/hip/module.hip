@@ -21,6 +21,8 @@ void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo,
                   uint64_t seed, uint64_t call, uintptr_t stream);
 void spill_free(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
                 uintptr_t cell_map, uintptr_t stream);
+void spill_free_mask(int n, int m, uintptr_t dead, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
+                     uintptr_t cell_map, uintptr_t stream);
 void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
             uintptr_t stream);
 void gather_rows(int n, uintptr_t src_rows, uintptr_t dst_rows,
@@ -36,7 +38,7 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
                   uintptr_t km_w, int nk, uintptr_t signs, int nsg, uintptr_t hills, int nh, uintptr_t RM,
                   uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
                   uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
-                  uintptr_t Vmax, uintptr_t Ke, uintptr_t stream);
+                  uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t stream);
 // world.hip
 void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
                      uintptr_t wb, uintptr_t scale, uintptr_t partials, uintptr_t totals, uintptr_t stream);
@@ -106,6 +108,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gather_rows", &msd::gather_rows);
   m.def("spill_free", &msd::spill_free);
   m.def("pickup", &msd::pickup);
+  m.def("spill_free_mask", &msd::spill_free_mask);
   m.def("place_rounds", &msd::place_rounds);
   m.def("split_cells", &msd::split_cells);
   m.def("permeate", &msd::permeate);

@@ -201,6 +201,18 @@ __global__ void __launch_bounds__(256) spill_free_kernel(int k, int m, const int
   if (j == 0) cell_map[pix] = 0;
 }
 
+__global__ void __launch_bounds__(256) spill_free_mask_kernel(int n, int m, const uint8_t* dead, const int32_t* pos,
+                                                              int C, long long plane, const float* cell_mols,
+                                                              float* map, uint8_t* cell_map) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)n * m) return;
+  const int c = (int)(t / m), j = (int)(t - (long long)c * m);
+  if (!dead[c]) return;
+  const long long pix = (long long)pos[2 * c] * C + pos[2 * c + 1];
+  map[j * plane + pix] += cell_mols[(long long)c * m + j];
+  if (j == 0) cell_map[pix] = 0;
+}
+
 __global__ void __launch_bounds__(256) pickup_kernel(int k, int m, const int64_t* idxs, const int32_t* pos, int C,
                                                      long long plane, float* cell_mols, float* map) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -413,6 +425,15 @@ void spill_free(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintp
   if (k <= 0 || m <= 0) return;
   spill_free_kernel<<<cdiv((long long)k * m, 256), 256, 0, S_(stream)>>>(
       k, m, P_<int64_t>(idxs), P_<int32_t>(pos), C, (long long)R * C, P_<float>(cell_mols), P_<float>(map),
+      P_<uint8_t>(cell_map));
+  MS_LAUNCH_CHECK();
+}
+
+void spill_free_mask(int n, int m, uintptr_t dead, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
+                     uintptr_t cell_map, uintptr_t stream) {
+  if (n <= 0 || m <= 0) return;
+  spill_free_mask_kernel<<<cdiv((long long)n * m, 256), 256, 0, S_(stream)>>>(
+      n, m, P_<uint8_t>(dead), P_<int32_t>(pos), C, (long long)R * C, P_<float>(cell_mols), P_<float>(map),
       P_<uint8_t>(cell_map));
   MS_LAUNCH_CHECK();
 }

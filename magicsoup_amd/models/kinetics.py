@@ -333,12 +333,13 @@ class Kinetics:
         tokens = self._collect_proteome_idxs(proteomes)
         self.set_cell_params_tokens(cell_idxs, tokens)
 
-    def set_cell_params_tokens(self, cell_idxs, tokens: torch.Tensor):
-        """Fused parameter build from dense tokens (n, P, D, 5) int32 for rows ``cell_idxs``."""
+    def set_cell_params_tokens(self, cell_idxs, tokens: torch.Tensor, nprot: torch.Tensor | None = None):
+        """Fused parameter build from dense tokens (n, P, D, 5) int32 for rows ``cell_idxs``;
+        rows with ``nprot == 0`` (if given) are unset."""
         rows = torch.as_tensor(cell_idxs, dtype=torch.int32)
         if tokens.size(1) > self.N.size(1):
             self.increase_max_proteins(int(tokens.size(1)))
-        kinetics_ops.build_params(self, rows, tokens)
+        kinetics_ops.build_params(self, rows, tokens, nprot=nprot)
 
     def unset_cell_params(self, cell_idxs):
         """Zero all parameters of the given cells."""

@@ -300,16 +300,22 @@ class World:
         hip_ops.gather_rows(pairs, k, src_rows=src, dst_rows=dst)
 
     def _idx_tensor(self, idxs, unique: bool = True) -> torch.Tensor:
+        """Cell indices as a long tensor on the world's device (ascending and duplicate-free when
+        ``unique``; lists are deduplicated on the host, tensors with a membership mask)."""
         if isinstance(idxs, torch.Tensor):
             t = idxs.to(self.device)
             if t.dtype == torch.bool:
-                t = torch.nonzero(t).flatten()
+                return torch.nonzero(t).flatten()
             t = t.to(torch.long).flatten()
-        else:
-            t = torch.tensor(list(idxs), dtype=torch.long, device=self.device)
-        if unique and t.numel() > 1:
-            t = torch.unique(t)
-        return t
+            if unique and t.numel() > 1:
+                mask = torch.zeros(self.n_cells, dtype=torch.bool, device=self.device)
+                mask[t] = True
+                t = torch.nonzero(mask).flatten()
+            return t
+        lst = list(idxs)
+        if unique:
+            lst = sorted(set(lst))
+        return torch.tensor(lst, dtype=torch.long, device=self.device)
 
     # ------------------------------------------------------------------ queries
     def get_cell(self, by_idx: int | None = None, by_position: tuple[int, int] | None = None) -> Cell:
@@ -463,16 +469,24 @@ class World:
         (indices after a removed cell shift down)."""
         range_push("kill_cells")
         try:
-            if cell_idxs is None:
-                cell_idxs = torch.arange(self.n_cells, device=self.device)
-            idxs = self._idx_tensor(cell_idxs)
-            k = int(idxs.numel())
-            if k == 0:
+            n = self.n_cells
+            if n == 0:
                 return
-            world_ops.spill_and_free(self, idxs)
-            keep = torch.ones(self.n_cells, dtype=torch.bool, device=self.device)
-            keep[idxs] = False
+            if cell_idxs is None:
+                dead = torch.ones(n, dtype=torch.bool, device=self.device)
+            elif isinstance(cell_idxs, torch.Tensor) and cell_idxs.dtype == torch.bool:
+                dead = cell_idxs.to(self.device)
+            else:
+                t = cell_idxs if isinstance(cell_idxs, torch.Tensor) else torch.tensor(list(cell_idxs), dtype=torch.long)
+                dead = torch.zeros(n, dtype=torch.bool, device=self.device)
+                if t.numel() == 0:
+                    return
+                dead[t.to(self.device, torch.long)] = True  # duplicates are harmless
+            world_ops.spill_and_free_mask(self, dead)
+            keep = ~dead
             keep_idx = torch.nonzero(keep).flatten()
+            if int(keep_idx.numel()) == n:
+                return
             self._compact(keep_idx, keep)
         finally:
             range_pop()
@@ -590,8 +604,11 @@ class World:
         try:
             if self.n_cells < 2:
                 return
-            idxs = torch.arange(self.n_cells, device=self.device) if cell_idxs is None else cell_idxs
-            pairs = self.get_neighbors_t(idxs)
+            if cell_idxs is None:
+                idxs = torch.arange(self.n_cells, device=self.device)
+                pairs = world_ops.neighbors(self, idxs, idxs)
+            else:
+                pairs = self.get_neighbors_t(cell_idxs)
             if pairs.size(0) == 0:
                 return
             changed = world_ops.recombinations(self, pairs, p)
@@ -609,12 +626,8 @@ class World:
         data, lens = self._genomes.view()
         tokens, nprots = world_ops.translate(self, data, lens, rows)
         self.kinetics.increase_max_proteins(int(tokens.size(1)))
-        empty = nprots == 0
-        if bool(empty.any()):
-            self.kinetics.unset_cell_params(rows[empty])
-        full = ~empty
-        if bool(full.any()):
-            self.kinetics.set_cell_params_tokens(rows[full], tokens[full])
+        # one build launch: rows without proteins are unset in the same pass
+        self.kinetics.set_cell_params_tokens(rows, tokens, nprot=nprots)
 
     # ------------------------------------------------------------------ persistence
     def save(self, rundir: Path, name: str = "world.pkl"):

@@ -142,7 +142,7 @@ def enzymatic_activity(world) -> None:
     _launch_integrate(kin, p, c, world=world, flags_hook=hook)
 
 
-def build_params(tokens, rows, luts, p, abs_temp: float, gas: float) -> None:
+def build_params(tokens, rows, luts, p, abs_temp: float, gas: float, nprot=None) -> None:
     n, P, D = int(tokens.size(0)), int(tokens.size(1)), int(tokens.size(2))
     Pt, s = int(p["N"].size(1)), int(p["N"].size(2))
     _m().build_params(
@@ -152,6 +152,7 @@ def build_params(tokens, rows, luts, p, abs_temp: float, gas: float) -> None:
         _p(luts["react"]), _p(luts["trnsp"]), _p(luts["eff"]), int(luts["react"].size(0)),
         _p(luts["energies"]), float(abs_temp), float(gas),
         *(_p(p[k]) for k in ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke")),
+        _p(nprot),
         _stream(),
     )
 
@@ -317,6 +318,15 @@ def spill_and_free(world, idxs: torch.Tensor) -> None:
     ix = idxs.to(torch.int64).contiguous()
     _m().spill_free(int(ix.numel()), world.n_molecules, _p(ix), _p(world.cell_positions), R, C,
                     _p(world.cell_molecules), _p(world._molmap), _p(_cell_map_bytes(world)), _stream())
+
+
+def spill_and_free_mask(world, dead: torch.Tensor) -> None:
+    """Mask form of :func:`spill_and_free` (no index list, duplicates impossible)."""
+    _ensure_world_layout(world)
+    R, C = geom(world)[:2]
+    d = dead.to(torch.uint8).contiguous() if dead.dtype != torch.bool else dead.contiguous().view(torch.uint8)
+    _m().spill_free_mask(world.n_cells, world.n_molecules, _p(d), _p(world.cell_positions), R, C,
+                         _p(world.cell_molecules), _p(world._molmap), _p(_cell_map_bytes(world)), _stream())
 
 
 def pickup_molecules(world, new: torch.Tensor) -> None:

@@ -68,8 +68,9 @@ def _luts(kin, device) -> dict[str, torch.Tensor]:
     }
 
 
-def build_params(kin, rows: torch.Tensor, tokens: torch.Tensor) -> None:
-    """Write parameter rows ``rows`` from dense tokens (n, P, D, 5)."""
+def build_params(kin, rows: torch.Tensor, tokens: torch.Tensor, nprot: torch.Tensor | None = None) -> None:
+    """Write parameter rows ``rows`` from dense tokens (n, P, D, 5). With ``nprot`` (GPU), rows
+    whose proteome is empty are unset (all zero) in the same launch."""
     p = _canonical_params(kin)
     dev = p["N"].device
     if rows.numel() == 0:
@@ -84,8 +85,18 @@ def build_params(kin, rows: torch.Tensor, tokens: torch.Tensor) -> None:
     if dev.type == "cuda":
         from magicsoup_amd.ops import hip_ops
 
-        hip_ops.build_params(tokens, rows, luts, p, float(kin.abs_temp), GAS_CONSTANT)
+        np_ = None if nprot is None else nprot.to(device=dev, dtype=torch.int32).contiguous()
+        hip_ops.build_params(tokens, rows, luts, p, float(kin.abs_temp), GAS_CONSTANT, nprot=np_)
         return
+    if nprot is not None:
+        nprot = nprot.cpu()
+        empty = nprot == 0
+        if bool(empty.any()):
+            kin.unset_cell_params(rows.cpu()[empty].long())
+        full = ~empty
+        if not bool(full.any()):
+            return
+        rows, tokens = rows[full], tokens[full]
     native.host().build_params(
         _np(tokens),
         _np(rows),

@@ -155,6 +155,14 @@ def spill_and_free(world, idxs: torch.Tensor) -> None:
     mm[:, xs, ys] += world.cell_molecules[idxs].T
 
 
+def spill_and_free_mask(world, dead: torch.Tensor) -> None:
+    """Cells flagged in ``dead`` (bool (n,)) spill their molecules and release their pixels."""
+    if world.__dict__["_molmap"].is_cuda:
+        _molmap(world)
+        return _hip().spill_and_free_mask(world, dead)
+    spill_and_free(world, torch.nonzero(dead).flatten())
+
+
 def split_cells(world, parents: torch.Tensor, children: torch.Tensor) -> None:
     """Molecules split evenly, divisions + 1 and lifetime 0 for both descendants."""
     if _is_gpu(world):

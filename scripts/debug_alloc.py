@@ -1,9 +1,10 @@
 """Log every capacity reallocation of the per-cell stores during bench steps (debug aid)."""
+import os
 import sys
 
 import torch
 
-sys.argv = [sys.argv[0]] + sys.argv[1:]
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 from magicsoup_amd.models import kinetics as K  # noqa: E402
 from magicsoup_amd.models import strings as S  # noqa: E402
@@ -27,8 +28,13 @@ def wrap(cls, name, tag, probe):
 
 
 wrap(S.StringArena, "reserve", "arena.reserve", lambda s: (s.data.data_ptr(), tuple(s.data.shape)))
-wrap(K.Kinetics, "increase_max_cells", "kin.grow_cells", lambda s: (s.N.data_ptr() if "_bufs" not in s.__dict__ else
-                                                                     s._bufs.get("N", s.N).data_ptr(), tuple(s.N.shape)))
+def _kcap(s):
+    b = s.__dict__.get("_bufs", {}).get("N")
+    return (0, 0) if b is None else (b.data_ptr(), b.size(0))
+
+
+wrap(K.Kinetics, "increase_max_cells", "kin.grow_cells", _kcap)
+wrap(K.Kinetics, "_commit_compact", "kin.compact", _kcap)
 wrap(K.Kinetics, "increase_max_proteins", "kin.grow_prot", lambda s: tuple(s.N.shape))
 wrap(W._Column, "reserve", "col.reserve", lambda s: (s.buf.data_ptr(), tuple(s.buf.shape)))
 
