@@ -3,10 +3,13 @@
 //
 // Integrator mapping (see ms_kinetics.h for the exact-global-exit scheme):
 //   * G lanes (32 or 64) of a wavefront own one cell; a 256-thread workgroup holds 256/G cells.
+//     A cell never spans waves, so phases are separated by wave-level LDS fences, not workgroup
+//     barriers: the waves of a block progress independently.
 //   * The cell's active proteins (Vmax' != 0) are compacted with a ballot prefix; their
 //     stoichiometry rows are staged once per part into LDS as packed int8x4 words (N, Nf, Nb, A),
 //     row stride padded to an odd word count so both access patterns are bank-conflict free:
-//       - protein phase: lane = protein, loops over signals (products, quotients, flags);
+//       - protein phase: lane = protein, loops over that protein's non-zero signals (a sparse
+//         index list built once per part: proteins touch a handful of the s signals);
 //       - signal phase:  lane = signal, loops over proteins (consumption sums, X updates).
 //   * All 4 equilibrium iterations run unconditionally; the 5 candidate states go to a snapshot
 //     buffer and every cell ORs its "still correcting" bits into one word per part. The next part
@@ -49,12 +52,17 @@ __device__ __forceinline__ int w_nf(int w) { return (w >> 8) & 0xFF; }
 __device__ __forceinline__ int w_nb(int w) { return (w >> 16) & 0xFF; }
 __device__ __forceinline__ int w_a(int w) { return (int)(int8_t)((w >> 24) & 0xFF); }
 
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 template <int G>
 __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
   const int slot = threadIdx.x / G, lane = threadIdx.x % G;
   const int cps = blockDim.x / G;
-  unsigned& block_bits = *reinterpret_cast<unsigned*>(smem + cps * a.slot_words);
   const int cell = blockIdx.x * cps + slot;
   const bool valid = cell < a.c;
   const int P = a.P, s = a.s, SP = a.sp;
@@ -72,8 +80,8 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
   float* Xc = X0 + s;
   float* fs = Xc + s;
   int* na_p = reinterpret_cast<int*>(fs + s);
-
-  if (threadIdx.x == 0) block_bits = 0u;
+  int* nnz = na_p + 1;                                       // (P,) non-zero signals per protein
+  uint8_t* nzj = reinterpret_cast<uint8_t*>(nnz + P);         // (P, s) their indices
 
   // ---- 1. load X0 (part 0: gather cell + pixel molecules; else: selected previous candidate)
   if (valid) {
@@ -119,7 +127,7 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
     }
     if (lane == 0) *na_p = na;
   }
-  __syncthreads();
+  wave_lds_sync();
   const int na = valid ? *na_p : 0;
 
   // ---- 3. stage packed stoichiometry rows of the active proteins
@@ -130,17 +138,28 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
     if (n < -128 || n > 127 || nf > 255 || nb > 255 || nf < 0 || nb < 0 || aa < -128 || aa > 127) atomicOr(a.overflow, 1);
     words[k * SP + j] = (n & 0xFF) | ((nf & 0xFF) << 8) | ((nb & 0xFF) << 16) | ((aa & 0xFF) << 24);
   }
-  __syncthreads();
+  wave_lds_sync();
+  for (int k = lane; k < na; k += G) {
+    const int* wr = words + k * SP;
+    uint8_t* nz = nzj + k * s;
+    int cnt = 0;
+    for (int j = 0; j < s; ++j)
+      if (wr[j] != 0) nz[cnt++] = (uint8_t)j;
+    nnz[k] = cnt;
+  }
+  wave_lds_sync();
 
   // ---- 4. velocities (protein phase)
   for (int k = lane; k < na; k += G) {
     const int* wr = words + k * SP;
     const float* kmr = a.Kmr + ((size_t)cell * P + act[k]) * s;
+    const uint8_t* nz = nzj + k * s;
+    const int cnt = nnz[k];
     float xf = 1.0f, xb = 1.0f, ar = 1.0f;
     bool anyf = false, anyb = false;
-    for (int j = 0; j < s; ++j) {
+    for (int q = 0; q < cnt; ++q) {
+      const int j = nz[q];
       const int w = wr[j];
-      if (w == 0) continue;
       const int nf = w_nf(w), nb = w_nb(w), av = w_a(w);
       const float x = X0[j];
       if (nf > 0) {
@@ -170,7 +189,7 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
     v = v < ms::kMin ? ms::kMin : (v > ms::kMax ? ms::kMax : v);
     V[k] = v;
   }
-  __syncthreads();
+  wave_lds_sync();
 
   // ---- 5. consumption per signal and the negative-concentration factors (signal phase)
   for (int j = lane; j < s; j += G) {
@@ -182,15 +201,18 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
     const float f = X0[j] / cons;
     fs[j] = f > 1.0f ? 1.0f : f;
   }
-  __syncthreads();
+  wave_lds_sync();
 
   // ---- 6. per-protein limiting factor (protein phase)
   for (int k = lane; k < na; k += G) {
     const int* wr = words + k * SP;
     const float v = V[k];
+    const uint8_t* nz = nzj + k * s;
+    const int cnt = nnz[k];
     float fmin = 1.0f;
     bool nan = false;
-    for (int j = 0; j < s; ++j) {
+    for (int q = 0; q < cnt; ++q) {
+      const int j = nz[q];
       const int n = w_n(wr[j]);
       if ((float)n * v < 0.0f) {
         const float f = fs[j];
@@ -202,7 +224,7 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
     F[k] = 1.0f;
     flg[k] = (v > 0.0f ? 1 : 0) | (fabsf(v) > 0.1f ? 2 : 0);
   }
-  __syncthreads();
+  wave_lds_sync();
 
   // ---- 7. X1 (signal phase), candidate 0
   float* snap = a.snap_out + (size_t)(valid ? cell : 0) * ms::kSnap * s;
@@ -216,7 +238,7 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
     Xc[j] = x;
     if (valid) snap[j] = x;
   }
-  __syncthreads();
+  wave_lds_sync();
 
   // ---- 8. equilibrium damping trajectory
   unsigned bits = 0u;
@@ -224,11 +246,13 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
   for (int it = 0; it < a.n_iters; ++it, inc *= 0.5f) {
     for (int k = lane; k < na; k += G) {
       const int* wr = words + k * SP;
+      const uint8_t* nz = nzj + k * s;
+      const int cnt = nnz[k];
       float pf = 1.0f, pb = 1.0f;
       bool anyf = false, anyb = false;
-      for (int j = 0; j < s; ++j) {
+      for (int q = 0; q < cnt; ++q) {
+        const int j = nz[q];
         const int w = wr[j];
-        if (w == 0) continue;
         const int nf = w_nf(w), nb = w_nb(w);
         if (nf > 0) {
           pf *= ms::ipow(Xc[j], nf);
@@ -257,7 +281,7 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
       if (low) f += inc;
       F[k] = f > 1.0f ? 1.0f : (f < 0.0f ? 0.0f : f);
     }
-    __syncthreads();
+    wave_lds_sync();
     float* sn = snap + (size_t)(it + 1) * s;
     for (int j = lane; j < s; j += G) {
       float x = X0[j];
@@ -269,15 +293,14 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
       Xc[j] = x;
       if (valid) sn[j] = x;
     }
-    __syncthreads();
+    wave_lds_sync();
   }
 
-  // ---- 9. one mask OR per workgroup
-  if (bits) atomicOr(&block_bits, bits);
-  __syncthreads();
-  if (threadIdx.x == 0 && block_bits)
+  // ---- 9. one mask OR per wavefront
+  for (int o = 32; o > 0; o >>= 1) bits |= __shfl_xor(bits, o);
+  if ((threadIdx.x & 63) == 0 && bits)
     for (int it = 0; it < ms::kEqIters; ++it)
-      if (block_bits & (1u << it)) atomicOr(a.mask_out + it, 1u);
+      if (bits & (1u << it)) atomicOr(a.mask_out + it, 1u);
 }
 
 // Final state -> cell_molecules and the molecule-map pixels under the cells.
@@ -419,7 +442,7 @@ __global__ void __launch_bounds__(kBlock) build_params_kernel(BuildArgs b) {
 // Host launchers
 
 static int slot_words_for(int P, int s, int sp) {
-  int w = P * sp + P * 8 + 3 * s + 1;
+  int w = P * sp + P * 8 + 3 * s + 1 + P + (P * s + 3) / 4;
   return (w + 3) & ~3;  // keep every slot 16-byte aligned
 }
 
@@ -454,7 +477,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t 
   const size_t slot_bytes = (size_t)slot_words * 4;
   int cps = kBlock / G;
   while (cps > 1 && cps * slot_bytes > 64 * 1024) --cps;
-  const size_t lds = cps * slot_bytes + 16;
+  const size_t lds = cps * slot_bytes;
   if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
   const int threads = cps * G;
   const unsigned grid = cdiv(c, cps);
