@@ -80,16 +80,16 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
     with ph("activity"):
         world.enzymatic_activity()
     with ph("kill"):
-        kill = torch.nonzero(world.cell_molecules[:, atp] < 1.0).flatten()
+        kill = world.cell_molecules[:, atp] < 1.0  # boolean masks: no index read-back
         world.kill_cells(kill)
         if stats is not None:
-            note("killed", kill.numel())
+            note("killed", kill.sum())
     with ph("replicate"):
-        repl = torch.nonzero(world.cell_molecules[:, atp] > 5.0).flatten()
-        world.cell_molecules[repl, atp] -= 4.0
+        repl = world.cell_molecules[:, atp] > 5.0
+        world.cell_molecules[:, atp] -= 4.0 * repl
         world.divide_cells_t(repl)
         if stats is not None:
-            note("divided", repl.numel())
+            note("divided", repl.sum())
     with ph("dilute"):
         # chemostat-style dilution keeps the population at the configured size (the reference loop
         # only tops up; on a 4096^2 map the population would otherwise grow ~6x within 25 steps)

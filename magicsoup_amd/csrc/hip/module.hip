@@ -25,6 +25,10 @@ void spill_free_mask(int n, int m, uintptr_t dead, uintptr_t pos, int R, int C, 
                      uintptr_t cell_map, uintptr_t stream);
 void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
             uintptr_t stream);
+void neighbor_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map, uintptr_t keys,
+                    uintptr_t stream);
+void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
+                    uintptr_t stream);
 void gather_rows(int n, uintptr_t src_rows, uintptr_t dst_rows,
                  const std::vector<std::tuple<uintptr_t, uintptr_t, long long, long long, long long>>& descs,
                  uintptr_t stream);
@@ -106,6 +110,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("diffuse_partials_len", &msd::diffuse_partials_len);
   m.def("scale_planes", &msd::scale_planes);
   m.def("gather_rows", &msd::gather_rows);
+  m.def("neighbor_slots", &msd::neighbor_slots);
+  m.def("rec_count_keys", &msd::rec_count_keys);
   m.def("spill_free", &msd::spill_free);
   m.def("pickup", &msd::pickup);
   m.def("spill_free_mask", &msd::spill_free_mask);

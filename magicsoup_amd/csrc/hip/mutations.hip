@@ -152,6 +152,26 @@ __global__ void __launch_bounds__(256) rec_count_kernel(int n, const int32_t* pa
   k[i] = (int32_t)(kk > nb ? nb : kk);
 }
 
+// Same draw over fixed neighbour slots (int64 keys (a << 32) | b, -1 = empty slot).
+__global__ void __launch_bounds__(256) rec_count_keys_kernel(int n, const int64_t* keys, const int32_t* lens, double p,
+                                                             uint64_t seed, uint64_t call, int32_t* k) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t key = keys[i];
+  if (key < 0) {
+    k[i] = 0;
+    return;
+  }
+  const int nb = lens[key >> 32] + lens[key & 0xFFFFFFFF];
+  if (nb < 1) {
+    k[i] = 0;
+    return;
+  }
+  Philox rng(seed, call, (uint32_t)i);
+  long long kk = poisson(rng, p * (double)nb);
+  k[i] = (int32_t)(kk > nb ? nb : kk);
+}
+
 // Recombine pair sel[j]: cut both strands at k[.] sorted positions, shuffle the k+2 parts and split
 // them at a random index into two new genomes (scratch rows 2j and 2j+1). One wavefront per pair:
 // lane 0 plans the parts (LDS for up to kFloydMax cuts, else the global `parts` scratch with
@@ -272,6 +292,14 @@ void rec_count(int n, uintptr_t pairs, uintptr_t lens, double p, uint64_t seed, 
   if (n <= 0) return;
   rec_count_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, P_<int32_t>(pairs), P_<int32_t>(lens), p, seed, call,
                                                          P_<int32_t>(k));
+  MS_LAUNCH_CHECK();
+}
+
+void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
+                    uintptr_t stream) {
+  if (n <= 0) return;
+  rec_count_keys_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, P_<int64_t>(keys), P_<int32_t>(lens), p, seed, call,
+                                                              P_<int32_t>(k));
   MS_LAUNCH_CHECK();
 }
 

@@ -379,6 +379,25 @@ __global__ void __launch_bounds__(256) neighbor_pairs_kernel(int nf, const int64
   }
 }
 
+// All neighbour pairs of all cells in fixed slots: slot c*8 + q holds (c << 32) | o for the q-th
+// Moore neighbour o > c of cell c, else -1. Deterministic order (cell-major, reference neighbour
+// order), no atomics, no counter read-back.
+__global__ void __launch_bounds__(256) neighbor_slots_kernel(int n, const int32_t* pos, Geom g, const int32_t* idx_map,
+                                                             int64_t* keys) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  long long nb[8];
+  const int cnt = moore(pos[2 * c], pos[2 * c + 1], g, nb);
+  for (int q = 0; q < 8; ++q) {
+    int64_t key = -1;
+    if (q < cnt) {
+      const int o = idx_map[nb[q]];
+      if (o > c) key = ((int64_t)c << 32) | o;
+    }
+    keys[(size_t)c * 8 + q] = key;
+  }
+}
+
 // ---------------------------------------------------------------- host launchers
 static Geom geom(int R, int C, int r_lo, int r_hi, int wrap) {
   if (R <= 0 || C <= 0 || r_lo < 0 || r_hi > R || r_lo >= r_hi) throw std::invalid_argument("bad map geometry");
@@ -506,6 +525,15 @@ void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo,
 void index_map(int c, uintptr_t pos, int C, uintptr_t idx_map, bool clear, uintptr_t stream) {
   if (c <= 0) return;
   index_map_kernel<<<cdiv(c, 256), 256, 0, S_(stream)>>>(c, P_<int32_t>(pos), C, P_<int32_t>(idx_map), clear);
+  MS_LAUNCH_CHECK();
+}
+
+void neighbor_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map, uintptr_t keys,
+                    uintptr_t stream) {
+  if (n <= 0) return;
+  const Geom g = geom(R, C, r_lo, r_hi, wrap);
+  neighbor_slots_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, P_<int32_t>(pos), g, P_<int32_t>(idx_map),
+                                                               P_<int64_t>(keys));
   MS_LAUNCH_CHECK();
 }
 

@@ -604,14 +604,19 @@ class World:
         try:
             if self.n_cells < 2:
                 return
-            if cell_idxs is None:
-                idxs = torch.arange(self.n_cells, device=self.device)
-                pairs = world_ops.neighbors(self, idxs, idxs)
+            if cell_idxs is None and self._genomes.data.is_cuda:
+                from magicsoup_amd.ops import hip_ops
+
+                changed = hip_ops.recombinate_all(self, p)
             else:
-                pairs = self.get_neighbors_t(cell_idxs)
-            if pairs.size(0) == 0:
-                return
-            changed = world_ops.recombinations(self, pairs, p)
+                if cell_idxs is None:
+                    idxs = torch.arange(self.n_cells, device=self.device)
+                    pairs = world_ops.neighbors(self, idxs, idxs)
+                else:
+                    pairs = self.get_neighbors_t(cell_idxs)
+                if pairs.size(0) == 0:
+                    return
+                changed = world_ops.recombinations(self, pairs, p)
             if changed.numel() > 0:
                 self._update_params_rows(changed)
         finally:

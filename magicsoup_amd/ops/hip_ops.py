@@ -371,6 +371,15 @@ def gather_rows(pairs, n: int, src_rows: torch.Tensor | None = None, dst_rows: t
     _m().gather_rows(int(n), _p(sr), _p(dr), descs, _stream())
 
 
+def _index_map(world, npix: int, dev) -> torch.Tensor:
+    """Pixel -> cell index map (int32, -1 = empty), kept all -1 between uses."""
+    idx_map = world.__dict__.get("_idx_map")
+    if idx_map is None or idx_map.numel() != npix or idx_map.device != dev:
+        idx_map = torch.full((npix,), -1, dtype=torch.int32, device=dev)
+        world.__dict__["_idx_map"] = idx_map
+    return idx_map
+
+
 def neighbors(world, frm: torch.Tensor, to: torch.Tensor, pos: torch.Tensor | None = None, n: int | None = None) -> torch.Tensor:
     """Unique (a < b) Moore-neighbour pairs between cells ``frm`` and ``to`` as int32 (k, 2).
     ``pos`` / ``n`` default to the world's cells (a caller may append ghost cells)."""
@@ -380,10 +389,7 @@ def neighbors(world, frm: torch.Tensor, to: torch.Tensor, pos: torch.Tensor | No
     if pos is None:
         pos, n = world.cell_positions, world.n_cells
     sc = _scratch(world)
-    idx_map = world.__dict__.get("_idx_map")
-    if idx_map is None or idx_map.numel() != R * C:
-        idx_map = torch.full((R * C,), -1, dtype=torch.int32, device=dev)
-        world.__dict__["_idx_map"] = idx_map
+    idx_map = _index_map(world, R * C, dev)
     _m().index_map(n, _p(pos), C, _p(idx_map), False, _stream())
     in_from = sc.get("nb_from", n, torch.uint8, dev, zero=True)
     in_to = sc.get("nb_to", n, torch.uint8, dev, zero=True)
@@ -476,6 +482,42 @@ def recombinations(world, pairs: torch.Tensor, p: float) -> torch.Tensor:
     k = torch.empty(n, dtype=torch.int32, device=dev)
     seed, call = _rng()
     _m().rec_count(n, _p(pairs), _p(arena.lens), float(p), seed, call, _p(k), _stream())
+    return _rec_apply(world, pairs, k, seed, call)
+
+
+def recombinate_all(world, p: float) -> torch.Tensor:
+    """recombinate_cells() over all cells: neighbour pairs in fixed per-cell slots (no pair list
+    read-back), Poisson draws per slot, one sync for the selected pairs."""
+    arena = world._genomes
+    dev = arena.data.device
+    n = world.n_cells
+    keys = neighbor_slot_keys(world)
+    k = _scratch(world).get("nb_k", 8 * n, torch.int32, dev)
+    seed, call = _rng()
+    _m().rec_count_keys(8 * n, _p(keys), _p(arena.lens), float(p), seed, call, _p(k), _stream())
+    pairs = torch.stack([keys >> 32, keys & 0xFFFFFFFF], dim=1).to(torch.int32)
+    return _rec_apply(world, pairs, k, seed, call)
+
+
+def neighbor_slot_keys(world) -> torch.Tensor:
+    """All neighbour pairs of all cells as int64 keys (a << 32) | b (a < b) in fixed slots c*8 + q
+    (-1 = empty), without a read-back."""
+    R, C, r_lo, r_hi, wrap = geom(world)
+    dev = world._genomes.data.device
+    n = world.n_cells
+    _ensure_world_layout(world)
+    pos = world.cell_positions
+    idx_map = _index_map(world, R * C, dev)
+    _m().index_map(n, _p(pos), C, _p(idx_map), False, _stream())
+    keys = _scratch(world).get("nb_keys", 8 * n, torch.int64, dev)
+    _m().neighbor_slots(n, _p(pos), R, C, r_lo, r_hi, wrap, _p(idx_map), _p(keys), _stream())
+    _m().index_map(n, _p(pos), C, _p(idx_map), True, _stream())
+    return keys
+
+
+def _rec_apply(world, pairs: torch.Tensor, k: torch.Tensor, seed: int, call: int) -> torch.Tensor:
+    arena = world._genomes
+    dev = arena.data.device
     sel = torch.nonzero(k > 0).flatten()
     nsel = int(sel.numel())
     if nsel == 0:

@@ -1,0 +1,19 @@
+#!/bin/bash
+# PMC counters for the hot kernels (one rocprofv3 pass per counter group; no tracing domains).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/pmc
+export PYTHONPATH="$PWD:${PYTHONPATH:-}"
+REPO="$PWD"
+cd /tmp && export TMPDIR=/tmp
+KR="${KR:-integrate_part|diffuse_stencil|diffuse_correct|gather_rows}"
+i=0
+for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM" \
+           "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH" \
+           "FETCH_SIZE WRITE_SIZE" "OccupancyPercent MeanOccupancyPerActiveCU" "LDSBankConflict"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "$KR" -d "$REPO/gpurun_out/pmc/g$i" -o run \
+    --output-format csv -- python3 "$REPO/scripts/kernel_bench.py" 4096 50000 3 > "$REPO/gpurun_out/pmc/g$i.log" 2>&1
+  rc=$?; echo "group $i rc=$rc"
+  case $rc in 124|134|137|139) exit $rc;; esac
+done

@@ -244,3 +244,14 @@ def test_integrator_split_parts_match_fused():
     assert calls == [4, 4, 4]
     assert torch.equal(wa.cell_molecules, wa2.cell_molecules)
     assert torch.equal(wa.molecule_map, wa2.molecule_map)
+
+
+def test_neighbor_slots_match_pair_list():
+    w = _world("cuda", map_size=32, n=700)
+    from magicsoup_amd.ops import hip_ops
+
+    keys = hip_ops.neighbor_slot_keys(w)
+    keys = keys[keys >= 0]
+    got = {(int(k) >> 32, int(k) & 0xFFFFFFFF) for k in keys.tolist()}
+    assert len(got) == int(keys.numel())  # each pair once
+    assert got == set(w.get_neighbors(list(range(w.n_cells))))
