@@ -43,7 +43,7 @@ def test_generated_genomes_encode_the_proteome():
     p1 = [ms.TransporterDomainFact(molecule=_X), ms.RegulatoryDomainFact(effector=_Z, is_transmembrane=True, hill=3)]
     fact = ms.GenomeFact(world=w, proteome=[p0, p1], target_size=150)
     hits = 0
-    for _ in range(12):  # token codons may randomly contain a stop codon: retry a few times
+    for _ in range(40):  # token codons may randomly contain a stop codon: retry a few times
         g = fact.generate()
         assert len(g) == 150
         w.kill_cells()
