@@ -39,6 +39,7 @@ struct IntegrateArgs {
   int* overflow;              // set if a stoichiometry does not fit in int8
   int slot_words;             // LDS words per cell slot
   int sp;                     // padded LDS row stride (odd)
+  const int64_t* prow;        // cell -> parameter storage row (nullptr: identity)
 };
 
 __device__ __forceinline__ int stop_iter(const unsigned* flags, int n_iters) {
@@ -66,6 +67,7 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
   const int cell = blockIdx.x * cps + slot;
   const bool valid = cell < a.c;
   const int P = a.P, s = a.s, SP = a.sp;
+  const size_t prow = valid ? (a.prow ? (size_t)a.prow[cell] : (size_t)cell) : 0;  // parameter row
 
   int* words = smem + slot * a.slot_words;
   int* act = words + P * SP;
@@ -106,7 +108,7 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
       float vm = 0.0f;
       bool on = false;
       if (valid && p < P) {
-        vm = a.Vmax[(size_t)cell * P + p] * a.trim;
+        vm = a.Vmax[prow * P + p] * a.trim;
         on = !(vm <= 0.0f);  // NaN stays active (propagates like the reference)
       }
       const unsigned long long bal = __ballot(on);
@@ -117,7 +119,7 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
       if (on) {
         const int k = na + rank;
         act[k] = p;
-        const size_t o = (size_t)cell * P + p;
+        const size_t o = prow * P + p;
         kmf[k] = a.Kmf[o];
         kmb[k] = a.Kmb[o];
         ke[k] = a.Ke[o];
@@ -133,7 +135,7 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
   // ---- 3. stage packed stoichiometry rows of the active proteins
   for (int idx = lane; idx < na * s; idx += G) {
     const int k = idx / s, j = idx - k * s;
-    const size_t o = ((size_t)cell * P + act[k]) * s + j;
+    const size_t o = (prow * P + act[k]) * s + j;
     const int n = a.N[o], nf = a.Nf[o], nb = a.Nb[o], aa = a.A[o];
     if (n < -128 || n > 127 || nf > 255 || nb > 255 || nf < 0 || nb < 0 || aa < -128 || aa > 127) atomicOr(a.overflow, 1);
     words[k * SP + j] = (n & 0xFF) | ((nf & 0xFF) << 8) | ((nb & 0xFF) << 16) | ((aa & 0xFF) << 24);
@@ -152,7 +154,7 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
   // ---- 4. velocities (protein phase)
   for (int k = lane; k < na; k += G) {
     const int* wr = words + k * SP;
-    const float* kmr = a.Kmr + ((size_t)cell * P + act[k]) * s;
+    const float* kmr = a.Kmr + (prow * P + act[k]) * s;
     const uint8_t* nz = nzj + k * s;
     const int cnt = nnz[k];
     float xf = 1.0f, xb = 1.0f, ar = 1.0f;
@@ -455,7 +457,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t 
                uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb, uintptr_t Vmax, uintptr_t Ke, uintptr_t cell_mols,
                uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
                uintptr_t masks, uintptr_t overflow, const std::vector<float>& trims, int n_iters, int part_begin,
-               int part_end, bool scatter, uintptr_t stream) {
+               int part_end, bool scatter, uintptr_t prow, uintptr_t stream) {
   if (c <= 0) return;
   if (n_iters < 0 || n_iters > ms::kEqIters) throw std::invalid_argument("n_iters must be in 0..4");
   const int nparts = (int)trims.size();
@@ -505,6 +507,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t 
     a.overflow = P_<int>(overflow);
     a.slot_words = slot_words;
     a.sp = sp;
+    a.prow = prow ? P_<int64_t>(prow) : nullptr;
     if (G == 32) integrate_part_kernel<32><<<grid, threads, lds, st>>>(a);
     else integrate_part_kernel<64><<<grid, threads, lds, st>>>(a);
     MS_LAUNCH_CHECK();

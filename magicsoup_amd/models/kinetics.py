@@ -204,6 +204,7 @@ class _RegulatoryMapFact(_VectorMapFact):
 
 
 _PARAMS = ("Ke", "Kmf", "Kmb", "Kmr", "Vmax", "N", "Nf", "Nb", "A")
+_I32_PARAMS = ("N", "Nf", "Nb", "A")
 
 
 class Kinetics:
@@ -241,6 +242,7 @@ class Kinetics:
         )
         s = 2 * len(chemistry.molecules)
         self.n_signals = s
+        self.__dict__.update(_store_d={}, _slot=None, _ncells=0, _nrows=0)
         for name in _PARAMS:
             shape = (0, 0, s) if name in ("Kmr", "N", "Nf", "Nb", "A") else (0, 0)
             dt = torch.int32 if name in ("N", "Nf", "Nb", "A") else torch.float32
@@ -336,108 +338,192 @@ class Kinetics:
     def set_cell_params_tokens(self, cell_idxs, tokens: torch.Tensor, nprot: torch.Tensor | None = None):
         """Fused parameter build from dense tokens (n, P, D, 5) int32 for rows ``cell_idxs``;
         rows with ``nprot == 0`` (if given) are unset."""
-        rows = torch.as_tensor(cell_idxs, dtype=torch.int32)
-        if tokens.size(1) > self.N.size(1):
+        if tokens.size(1) > self._P():
             self.increase_max_proteins(int(tokens.size(1)))
+        slot = self._slot_tensor()
+        if slot is None:
+            rows = torch.as_tensor(cell_idxs, dtype=torch.int32)
+        else:
+            rows = self._rows(torch.as_tensor(cell_idxs, device=slot.device).long()).to(torch.int32)
         kinetics_ops.build_params(self, rows, tokens, nprot=nprot)
 
     def unset_cell_params(self, cell_idxs):
         """Zero all parameters of the given cells."""
         if isinstance(cell_idxs, list) and len(cell_idxs) == 0:
             return
-        for name in _PARAMS:
-            getattr(self, name)[cell_idxs] = 0
+        rows = self._rows(cell_idxs)
+        for t in self._store.values():
+            t[rows] = 0
 
     def copy_cell_params(self, from_idxs, to_idxs):
-        """Copy the parameter rows ``from_idxs`` to rows ``to_idxs``."""
-        for name in _PARAMS:
-            t = getattr(self, name)
-            t[to_idxs] = t[from_idxs]
+        """Copy the parameters of cells ``from_idxs`` to cells ``to_idxs``."""
+        store = self._store
+        dev = store["N"].device
+        if dev.type == "cuda":
+            from magicsoup_amd.ops import hip_ops
 
-    # The parameter tensors are views of capacity-managed row buffers: appending rows (spawn,
-    # divide) reuses spare capacity instead of re-copying every row like the reference's
-    # torch.cat (kinetics.py:688-703), and removing rows gathers the survivors into a second
-    # buffer in one pass. A tensor assigned from outside is adopted as the new buffer.
-    def _buffer(self, name: str) -> torch.Tensor:
-        t = getattr(self, name)
-        bufs = self.__dict__.setdefault("_bufs", {})
-        buf = bufs.get(name)
-        if buf is None or t.data_ptr() != buf.data_ptr() or t.shape[1:] != buf.shape[1:] or not t.is_contiguous():
-            buf = t.contiguous()
-            bufs[name] = buf
-        return buf
+            fr = self._rows(torch.as_tensor(from_idxs, device=dev).long())
+            to = self._rows(torch.as_tensor(to_idxs, device=dev).long())
+            hip_ops.gather_rows([(t, t) for t in store.values()], int(fr.numel()), src_rows=fr, dst_rows=to)
+            return
+        fr, to = self._rows(from_idxs), self._rows(to_idxs)
+        for t in store.values():
+            t[to] = t[fr]
+
+    # ---- parameter storage ----
+    # The parameters live in row-storage tensors with spare capacity; cell i's row is _slot[i]
+    # (None: row i). On the GPU, removing cells only compacts the small slot vector and new cells
+    # take fresh rows at the end, so the (c, p, s) rows are not moved on every kill_cells (the
+    # reference copies all parameter tensors there, kinetics.py:667-686). The storage is gathered
+    # back into cell order when it runs out of rows, when p grows, or when a parameter tensor is
+    # read through the public attributes -- users always see dense, cell-ordered tensors they
+    # can modify in place.
+    @property
+    def _store(self) -> dict[str, torch.Tensor]:
+        return self.__dict__["_store_d"]
+
+    def _P(self) -> int:
+        return int(self._store["N"].size(1))
+
+    def _get_param(self, name: str) -> torch.Tensor:
+        self._materialize()
+        t = self._store[name]
+        n = self.__dict__["_ncells"]
+        return t if t.size(0) == n else t[:n]
+
+    def _set_param(self, name: str, value) -> None:
+        d = self.__dict__
+        if "_store_d" not in d:
+            d["_store_d"], d["_slot"], d["_ncells"], d["_nrows"] = {}, None, 0, 0
+        self._materialize()
+        t = torch.as_tensor(value)
+        if not t.is_contiguous():
+            t = t.contiguous()
+        self._store[name] = t
+        d["_ncells"] = d["_nrows"] = int(t.size(0))
+        d.get("_spare", {}).pop(name, None)
+
+    def _rows(self, cells):
+        """Storage rows of cells (identity unless cells were removed on the GPU)."""
+        slot = self.__dict__["_slot"]
+        if slot is None:
+            return cells
+        return slot[torch.as_tensor(cells, device=slot.device)]
+
+    def _slot_tensor(self) -> torch.Tensor | None:
+        return self.__dict__["_slot"]
+
+    def _kernel_params(self) -> dict[str, torch.Tensor]:
+        """Storage tensors in kernel layout (contiguous int32 / float32), rows = capacity."""
+        store = self._store
+        for name, t in list(store.items()):
+            want = torch.int32 if name in _I32_PARAMS else torch.float32
+            if t.dtype != want or not t.is_contiguous():
+                self._materialize()
+                store[name] = store[name].to(want).contiguous()
+        return store
+
+    def _materialize(self) -> None:
+        d = self.__dict__
+        slot = d.get("_slot")
+        if slot is None:
+            return
+        n = d["_ncells"]
+        store = self._store
+        spare = d.setdefault("_spare", {})
+        target = {}
+        for name, t in store.items():
+            sp = spare.get(name)
+            if sp is None or sp.size(0) < max(n, 1) or sp.shape[1:] != t.shape[1:] or sp.dtype != t.dtype or sp.device != t.device:
+                sp = torch.empty(max(n, t.size(0)), *t.shape[1:], dtype=t.dtype, device=t.device)
+            target[name] = sp
+        if slot.is_cuda:
+            from magicsoup_amd.ops import hip_ops
+
+            hip_ops.gather_rows([(store[k], target[k][:n]) for k in store], n, src_rows=slot)
+        else:
+            for k in store:
+                torch.index_select(store[k], 0, slot, out=target[k][:n])
+        for k in list(store):
+            spare[k], store[k] = store[k], target[k]
+        d["_slot"] = None
+        d["_nrows"] = n
 
     def remove_cell_params(self, keep: torch.Tensor):
-        """Keep only the rows where ``keep`` is true (bool mask (c,)) or listed (ascending index
+        """Keep only the cells where ``keep`` is true (bool mask (c,)) or listed (ascending index
         tensor), preserving their order."""
         idx = torch.nonzero(keep).flatten() if keep.dtype == torch.bool else keep.to(torch.long)
+        d = self.__dict__
         k = int(idx.numel())
-        spares = self.__dict__.setdefault("_spares", {})
-        for name in _PARAMS:
-            t = getattr(self, name)
-            buf = self._buffer(name)
-            spare = spares.get(name)
-            if spare is None or spare.size(0) < k or spare.shape[1:] != buf.shape[1:] or spare.dtype != buf.dtype:
-                spare = torch.empty(max(k, buf.size(0)), *buf.shape[1:], dtype=buf.dtype, device=buf.device)
-            torch.index_select(t, 0, idx, out=spare[:k])
-            spares[name] = buf
-            self._bufs[name] = spare
-            setattr(self, name, spare[:k])
-
-    def _param_tensors(self) -> list[torch.Tensor]:
-        return [getattr(self, name) for name in _PARAMS]
-
-    def _compact_pairs(self, k: int) -> list[tuple[torch.Tensor, torch.Tensor]]:
-        """(current, spare target) row tensors for an order-preserving compaction to ``k`` rows;
-        the caller gathers, then :meth:`_commit_compact` swaps the buffers."""
-        spares = self.__dict__.setdefault("_spares", {})
-        pairs = []
-        for name in _PARAMS:
-            t = getattr(self, name)
-            buf = self._buffer(name)
-            spare = spares.get(name)
-            if spare is None or spare.size(0) < k or spare.shape[1:] != buf.shape[1:] or spare.dtype != buf.dtype:
-                spare = spares[name] = torch.empty(max(k, buf.size(0)), *buf.shape[1:], dtype=buf.dtype,
-                                                   device=buf.device)
-            pairs.append((t, spare[:k]))
-        return pairs
-
-    def _commit_compact(self, k: int) -> None:
-        spares = self.__dict__["_spares"]
-        for name in _PARAMS:
-            buf, spare = self._bufs[name], spares[name]
-            spares[name] = buf
-            self._bufs[name] = spare
-            setattr(self, name, spare[:k])
+        if idx.is_cuda:
+            slot = d["_slot"]
+            if slot is None:
+                slot = torch.arange(d["_ncells"], device=idx.device)
+            d["_slot"] = slot[idx]
+            d["_ncells"] = k
+            return
+        self._materialize()
+        spare = d.setdefault("_spare", {})
+        store = self._store
+        n = d["_ncells"]
+        for name, t in list(store.items()):
+            sp = spare.get(name)
+            if sp is None or sp.size(0) < max(k, 1) or sp.shape[1:] != t.shape[1:] or sp.dtype != t.dtype:
+                sp = torch.empty(max(k, t.size(0)), *t.shape[1:], dtype=t.dtype, device=t.device)
+            torch.index_select(t[:n], 0, idx, out=sp[:k])
+            spare[name], store[name] = t, sp
+        d["_ncells"] = d["_nrows"] = k
 
     def increase_max_cells(self, by_n: int, zero: bool = True):
-        """Append ``by_n`` rows (zero-filled unless the caller writes them all) to every parameter
-        tensor."""
+        """Append ``by_n`` cells (parameters zero-filled unless the caller writes them all)."""
         if by_n <= 0:
             return
-        for name in _PARAMS:
-            t = getattr(self, name)
-            n = int(t.size(0))
-            buf = self._buffer(name)
-            if n + by_n > buf.size(0):
-                cap = max(n + by_n, int(buf.size(0) * 1.5) + 64)
-                nb = torch.empty(cap, *buf.shape[1:], dtype=buf.dtype, device=buf.device)
-                nb[:n] = t
-                buf = self._bufs[name] = nb
-            view = buf[: n + by_n]
-            if zero:
-                view[n:].zero_()
-            setattr(self, name, view)
+        d = self.__dict__
+        store = self._store
+        cap = min(int(t.size(0)) for t in store.values())
+        if d["_slot"] is not None and d["_nrows"] + by_n > cap:
+            self._materialize()
+        n = d["_ncells"]
+        if d["_slot"] is None:
+            r0 = n
+            if n + by_n > cap:
+                new_cap = max(n + by_n, int(cap * 1.5) + 64)
+                for name, t in list(store.items()):
+                    nb = torch.empty(new_cap, *t.shape[1:], dtype=t.dtype, device=t.device)
+                    nb[:n] = t[:n]
+                    store[name] = nb
+                d.pop("_spare", None)
+        else:
+            r0 = d["_nrows"]
+            slot = d["_slot"]
+            d["_slot"] = torch.cat([slot, torch.arange(r0, r0 + by_n, device=slot.device, dtype=slot.dtype)])
+        d["_nrows"] = r0 + by_n
+        d["_ncells"] = n + by_n
+        if zero:
+            for t in store.values():
+                t[r0 : r0 + by_n].zero_()
 
     def increase_max_proteins(self, max_n: int):
         """Grow the protein dimension of every parameter tensor to ``max_n`` (zero-filled)."""
-        have = int(self.N.size(1))
-        if max_n <= have:
+        if max_n <= self._P():
             return
-        for name in _PARAMS:
-            t = getattr(self, name)
-            z = torch.zeros(t.size(0), max_n - have, *t.shape[2:], dtype=t.dtype, device=t.device)
-            setattr(self, name, torch.cat([t, z], dim=1))
+        self._materialize()
+        store = self._store
+        n = self.__dict__["_ncells"]
+        for name, t in list(store.items()):
+            t = t[:n]
+            z = torch.zeros(n, max_n - t.size(1), *t.shape[2:], dtype=t.dtype, device=t.device)
+            store[name] = torch.cat([t, z], dim=1)
+        self.__dict__["_nrows"] = n
+        self.__dict__.pop("_spare", None)
+
+    def _to_device(self, dev: torch.device) -> None:
+        self._materialize()
+        n = self.__dict__["_ncells"]
+        for name, t in list(self._store.items()):
+            self._store[name] = t[:n].to(dev)
+        self.__dict__["_nrows"] = n
+        self.__dict__.pop("_spare", None)
 
     # ------------------------------------------------------------------ integration
     def integrate_signals(self, X: torch.Tensor, _reduce_mask=None) -> torch.Tensor:
@@ -553,12 +639,14 @@ class Kinetics:
         return torch.from_numpy(arr)
 
     def __getstate__(self):
+        self._materialize()
         state = self.__dict__.copy()
         state["last_masks"] = []
-        for k in ("_bufs", "_spares", "_hip_scratch"):
+        for k in ("_spare", "_hip_scratch"):
             state.pop(k, None)
-        for name in _PARAMS:
-            state[name] = getattr(self, name).clone()
+        n = state["_ncells"]
+        state["_store_d"] = {k: v[:n].clone() for k, v in self._store.items()}
+        state["_nrows"] = n
         return state
 
     def _i32_tensor(self, d: Any) -> torch.Tensor:
@@ -566,3 +654,17 @@ class Kinetics:
 
     def _f32_tensor(self, d: Any) -> torch.Tensor:
         return torch.tensor(d, device=self.device, dtype=torch.float32)
+
+
+def _param_property(name: str) -> property:
+    def get(self):
+        return self._get_param(name)
+
+    def set(self, value):
+        self._set_param(name, value)
+
+    return property(get, set, doc=f"Cell parameter tensor ``{name}`` (dense, in cell order).")
+
+
+for _name in _PARAMS:
+    setattr(Kinetics, _name, _param_property(_name))

@@ -296,8 +296,8 @@ class World:
         n = self.n_cells
         pairs = [(col.view(n), col.view(n)) for name, col in self._cols.items() if name != "cell_positions"]
         pairs += self._genomes.clone_pairs(k) + self._labels.clone_pairs(k)
-        pairs += [(t, t) for t in self.kinetics._param_tensors()]
         hip_ops.gather_rows(pairs, k, src_rows=src, dst_rows=dst)
+        self.kinetics.copy_cell_params(from_idxs=src, to_idxs=dst)
 
     def _idx_tensor(self, idxs, unique: bool = True) -> torch.Tensor:
         """Cell indices as a long tensor on the world's device (ascending and duplicate-free when
@@ -501,13 +501,13 @@ class World:
             n = self.n_cells
             pairs = [(col.view(n), col.spare_rows(n_new)) for col in self._cols.values()]
             pairs += self._genomes.compact_pairs(n_new) + self._labels.compact_pairs(n_new)
-            pairs += self.kinetics._compact_pairs(n_new)
             hip_ops.gather_rows(pairs, n_new, src_rows=keep_idx)
+            # kinetics parameters stay where they are; only the cell -> row map is compacted
+            self.kinetics.remove_cell_params(keep=keep_idx)
             for col in self._cols.values():
                 col.swap()
             self._genomes.commit_compact(n_new)
             self._labels.commit_compact(n_new)
-            self.kinetics._commit_compact(n_new)
             self.n_cells = n_new
             return
         for col in self._cols.values():
@@ -693,11 +693,11 @@ class World:
         self.__setstate__(st)
         kin = self.kinetics
         kin.device = device
-        for k in ("_bufs", "_spares", "_hip_scratch"):
-            kin.__dict__.pop(k, None)
+        kin.__dict__.pop("_hip_scratch", None)
+        kin._to_device(dev)
         for name, val in list(vars(kin).items()):
             if isinstance(val, torch.Tensor):
-                setattr(kin, name, val.to(dev))
+                kin.__dict__[name] = val.to(dev)
         for mp in (kin.km_map, kin.vmax_map, kin.sign_map, kin.hill_map, kin.reaction_map, kin.transport_map, kin.effector_map):
             for name, val in list(vars(mp).items()):
                 if isinstance(val, torch.Tensor):

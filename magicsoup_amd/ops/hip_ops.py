@@ -64,7 +64,8 @@ def _rng() -> tuple[int, int]:
 _EQ = 4  # equilibrium-damping iterations per part
 
 
-def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n_iters=4, flags_hook=None):
+def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n_iters=4, flags_hook=None,
+                      slot=None):
     N = p["N"]
     P, s = int(N.size(1)), int(N.size(2))
     dev = N.device
@@ -87,18 +88,19 @@ def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n
         _p(snap_a), _p(snap_b), _p(masks), _p(overflow),
         [float(t) for t in trims], int(n_iters),
     ]
+    slot_p = _p(None if slot is None else slot.to(torch.int64).contiguous())
     nparts = len(trims)
     if flags_hook is None:
-        _m().integrate(*args, 0, nparts, True, _stream())
+        _m().integrate(*args, 0, nparts, True, slot_p, _stream())
     else:
         # domain-decomposed world: all-reduce each part's iteration flags before the next part (or
         # the final write-back) reads them, reproducing the reference's `torch.any` over the whole
         # population
         for part in range(nparts):
-            _m().integrate(*args, part, part + 1, False, _stream())
+            _m().integrate(*args, part, part + 1, False, slot_p, _stream())
             flags_hook(masks[_EQ * part : _EQ * (part + 1)])
         if nparts:
-            _m().integrate(*args, nparts, nparts, True, _stream())
+            _m().integrate(*args, nparts, nparts, True, slot_p, _stream())
     return masks
 
 
@@ -107,11 +109,11 @@ def _flags_to_bits(masks: torch.Tensor, nparts: int) -> list[int]:
     return [sum(1 << i for i, v in enumerate(row) if v) for row in f]
 
 
-def integrate(X: torch.Tensor, p: dict, trims, n_iters: int) -> list[int]:
+def integrate(X: torch.Tensor, p: dict, trims, n_iters: int, slot=None) -> list[int]:
     """Kinetics.integrate_signals on an explicit X (c, s) (in place)."""
     c = int(X.size(0))
     kin = _KinProxy(p)
-    masks = _launch_integrate(kin, p, c, X_io=X, trims=trims, n_iters=n_iters)
+    masks = _launch_integrate(kin, p, c, X_io=X, trims=trims, n_iters=n_iters, slot=slot)
     return _flags_to_bits(masks, len(trims))
 
 
@@ -135,11 +137,11 @@ def enzymatic_activity(world) -> None:
     kin = world.kinetics
     p = _canonical_params(kin)
     c = world.n_cells
-    if p["N"].size(0) < c:
-        raise ValueError("kinetics has fewer cell rows than the world")
+    if kin.__dict__["_ncells"] < c:
+        raise ValueError("kinetics has fewer cells than the world")
     _ensure_world_layout(world)
     hook = getattr(world, "_allreduce_flags", None)
-    _launch_integrate(kin, p, c, world=world, flags_hook=hook)
+    _launch_integrate(kin, p, c, world=world, flags_hook=hook, slot=kin._slot_tensor())
 
 
 def build_params(tokens, rows, luts, p, abs_temp: float, gas: float, nprot=None) -> None:

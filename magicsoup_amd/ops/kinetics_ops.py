@@ -15,16 +15,9 @@ _F32 = ("Kmr", "Kmf", "Kmb", "Vmax", "Ke")
 
 
 def _canonical_params(kin) -> dict[str, torch.Tensor]:
-    """Parameter tensors as contiguous int32 / float32, re-assigned on the object if converted."""
-    out = {}
-    for name in _I32 + _F32:
-        t = getattr(kin, name)
-        want = torch.int32 if name in _I32 else torch.float32
-        if t.dtype != want or not t.is_contiguous():
-            t = t.to(want).contiguous()
-            setattr(kin, name, t)
-        out[name] = t
-    return out
+    """Parameter storage in kernel layout (contiguous int32 / float32). Rows are storage rows: on
+    a GPU, cell i's parameters are at row ``kin._slot_tensor()[i]`` when that is not None."""
+    return kin._kernel_params()
 
 
 def _np(t: torch.Tensor):
@@ -34,16 +27,20 @@ def _np(t: torch.Tensor):
 def integrate(kin, X: torch.Tensor, trims, n_iters: int, reduce_mask=None) -> list[int]:
     """Fused integrate_signals on X (c, s) in place; returns the per-part iteration masks.
     ``reduce_mask`` (host path) maps a part's local iteration mask to the global one."""
-    p = _canonical_params(kin)
     c = X.size(0)
     if c == 0:
         return []
-    if p["N"].size(0) < c:
-        raise ValueError(f"kinetics has {p['N'].size(0)} cell rows but X has {c}")
     if X.is_cuda:
         from magicsoup_amd.ops import hip_ops
 
-        return hip_ops.integrate(X, p, list(trims), n_iters)
+        p = _canonical_params(kin)
+        if kin.__dict__["_ncells"] < c:
+            raise ValueError(f"kinetics has {kin.__dict__['_ncells']} cells but X has {c}")
+        return hip_ops.integrate(X, p, list(trims), n_iters, slot=kin._slot_tensor())
+    kin._materialize()
+    p = _canonical_params(kin)
+    if p["N"].size(0) < c:
+        raise ValueError(f"kinetics has {p['N'].size(0)} cell rows but X has {c}")
     masks = native.host().integrate_signals(
         _np(X),
         *(_np(p[k]) for k in ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke")),

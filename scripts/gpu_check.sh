@@ -24,6 +24,8 @@ if [[ "$what" == tests || "$what" == all ]]; then
   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [[ "$what" == bench || "$what" == all ]]; then
-  run bench_256_40k 600 python bench.py --map-size 256 --cells 40000 --steps 20 --warmup 5 --profile-phases "$@"
-  run bench_4096_50k 600 python bench.py --steps 20 --warmup 5 --profile-phases "$@"
+  # clean runs (the driver's measurement), then a phase breakdown (timers + event counts add syncs)
+  run bench_256_40k 600 python bench.py --map-size 256 --cells 40000 --steps 30 --warmup 5 "$@"
+  run bench_4096_50k 600 python bench.py --steps 30 --warmup 5 "$@"
+  run bench_4096_50k_phases 600 python bench.py --steps 20 --warmup 5 --profile-phases "$@"
 fi
