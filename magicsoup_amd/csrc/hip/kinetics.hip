@@ -21,6 +21,7 @@
 namespace msd {
 
 constexpr int kBlock = 256;
+constexpr int kNarrowP = 12;  // LDS protein slots of the narrow integrator launch
 
 struct IntegrateArgs {
   int c, P, s, m, R, C;
@@ -40,6 +41,9 @@ struct IntegrateArgs {
   int slot_words;             // LDS words per cell slot
   int sp;                     // padded LDS row stride (odd)
   const int64_t* prow;        // cell -> parameter storage row (nullptr: identity)
+  const int32_t* list;        // item -> cell (nullptr: identity)
+  const int32_t* count;       // number of items in `list` (device)
+  int Ps;                     // LDS protein capacity of a slot (>= active proteins of listed cells)
 };
 
 __device__ __forceinline__ int stop_iter(const unsigned* flags, int n_iters) {
@@ -64,26 +68,27 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
   extern __shared__ __attribute__((aligned(16))) int smem[];
   const int slot = threadIdx.x / G, lane = threadIdx.x % G;
   const int cps = blockDim.x / G;
-  const int cell = blockIdx.x * cps + slot;
-  const bool valid = cell < a.c;
-  const int P = a.P, s = a.s, SP = a.sp;
+  const int item = blockIdx.x * cps + slot;
+  const bool valid = a.list ? item < *a.count : item < a.c;
+  const int cell = valid ? (a.list ? a.list[item] : item) : 0;
+  const int P = a.P, s = a.s, SP = a.sp, Ps = a.Ps;
   const size_t prow = valid ? (a.prow ? (size_t)a.prow[cell] : (size_t)cell) : 0;  // parameter row
 
   int* words = smem + slot * a.slot_words;
-  int* act = words + P * SP;
-  float* V = reinterpret_cast<float*>(act + P);
-  float* Va = V + P;
-  float* F = Va + P;
-  float* kmf = F + P;
-  float* kmb = kmf + P;
-  float* ke = kmb + P;
-  int* flg = reinterpret_cast<int*>(ke + P);
-  float* X0 = reinterpret_cast<float*>(flg + P);
+  int* act = words + Ps * SP;
+  float* V = reinterpret_cast<float*>(act + Ps);
+  float* Va = V + Ps;
+  float* F = Va + Ps;
+  float* kmf = F + Ps;
+  float* kmb = kmf + Ps;
+  float* ke = kmb + Ps;
+  int* flg = reinterpret_cast<int*>(ke + Ps);
+  float* X0 = reinterpret_cast<float*>(flg + Ps);
   float* Xc = X0 + s;
   float* fs = Xc + s;
   int* na_p = reinterpret_cast<int*>(fs + s);
-  int* nnz = na_p + 1;                                       // (P,) non-zero signals per protein
-  uint8_t* nzj = reinterpret_cast<uint8_t*>(nnz + P);         // (P, s) their indices
+  int* nnz = na_p + 1;                                       // (Ps,) non-zero signals per protein
+  uint8_t* nzj = reinterpret_cast<uint8_t*>(nnz + Ps);        // (Ps, s) their indices
 
   // ---- 1. load X0 (part 0: gather cell + pixel molecules; else: selected previous candidate)
   if (valid) {
@@ -116,7 +121,7 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
       if constexpr (G == 64) gm = bal;
       else gm = (bal >> gbase) & ((1ull << G) - 1ull);
       const int rank = __popcll(gm & ((1ull << lane) - 1ull));
-      if (on) {
+      if (on && na + rank < Ps) {
         const int k = na + rank;
         act[k] = p;
         const size_t o = prow * P + p;
@@ -127,7 +132,7 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
       }
       na += __popcll(gm);
     }
-    if (lane == 0) *na_p = na;
+    if (lane == 0) *na_p = na < Ps ? na : Ps;
   }
   wave_lds_sync();
   const int na = valid ? *na_p : 0;
@@ -305,6 +310,21 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
       if (bits & (1u << it)) atomicOr(a.mask_out + it, 1u);
 }
 
+// Split the cells by their number of active proteins (Vmax > 0 or NaN; the same set for every part
+// since all trims are positive): cells with at most `pn` go to the narrow list (small LDS slots,
+// high occupancy), the others to the wide list (slots for all P proteins). List order does not
+// matter: cells are independent and the iteration flags are OR-reduced.
+__global__ void __launch_bounds__(256) bin_cells_kernel(int c, int P, int pn, const float* Vmax, const int64_t* prow,
+                                                        int32_t* lists, int32_t* counts) {
+  const int cell = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cell >= c) return;
+  const size_t r = prow ? (size_t)prow[cell] : (size_t)cell;
+  int na = 0;
+  for (int p = 0; p < P; ++p) na += !(Vmax[r * P + p] <= 0.0f);
+  if (na <= pn) lists[atomicAdd(counts, 1)] = cell;
+  else lists[c + atomicAdd(counts + 1, 1)] = cell;
+}
+
 // Final state -> cell_molecules and the molecule-map pixels under the cells.
 __global__ void __launch_bounds__(kBlock) integrate_scatter_kernel(int c, int s, int m, int R, int C, const float* snap,
                                                                    const unsigned* mask, int n_iters,
@@ -457,7 +477,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t 
                uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb, uintptr_t Vmax, uintptr_t Ke, uintptr_t cell_mols,
                uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
                uintptr_t masks, uintptr_t overflow, const std::vector<float>& trims, int n_iters, int part_begin,
-               int part_end, bool scatter, uintptr_t prow, uintptr_t stream) {
+               int part_end, bool scatter, uintptr_t prow, uintptr_t lists, uintptr_t stream) {
   if (c <= 0) return;
   if (n_iters < 0 || n_iters > ms::kEqIters) throw std::invalid_argument("n_iters must be in 0..4");
   const int nparts = (int)trims.size();
@@ -475,42 +495,72 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t 
   }
   const int G = s <= 32 ? 32 : 64;
   const int sp = (s % 2 == 0) ? s + 1 : s;
-  const int slot_words = slot_words_for(P, s, sp);
-  const size_t slot_bytes = (size_t)slot_words * 4;
-  int cps = kBlock / G;
-  while (cps > 1 && cps * slot_bytes > 64 * 1024) --cps;
-  const size_t lds = cps * slot_bytes;
-  if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
-  const int threads = cps * G;
-  const unsigned grid = cdiv(c, cps);
-  for (int part = part_begin; part < part_end; ++part) {
-    IntegrateArgs a{};
-    a.c = c; a.P = P; a.s = s; a.m = m; a.R = R; a.C = C;
-    a.N = P_<int32_t>(N); a.Nf = P_<int32_t>(Nf); a.Nb = P_<int32_t>(Nb); a.A = P_<int32_t>(A);
-    a.Kmr = P_<float>(Kmr); a.Kmf = P_<float>(Kmf); a.Kmb = P_<float>(Kmb); a.Vmax = P_<float>(Vmax); a.Ke = P_<float>(Ke);
-    a.cell_mols = P_<float>(cell_mols); a.molmap = P_<float>(molmap); a.positions = P_<int32_t>(positions);
-    if (part == 0 && !X_io) {
-      a.snap_prev = nullptr;
-    } else if (part == 0) {
-      a.snap_prev = snaps[1];
-      a.mask_prev = zero_flags;
-      a.n_iters_prev = n_iters;
-    } else {
-      a.snap_prev = snaps[(part - 1) & 1];
-      a.mask_prev = mk + ms::kEqIters * (part - 1);
-      a.n_iters_prev = n_iters;
-    }
-    a.snap_out = snaps[part & 1];
-    a.mask_out = mk + ms::kEqIters * part;
-    a.trim = trims[part];
-    a.n_iters = n_iters;
-    a.overflow = P_<int>(overflow);
-    a.slot_words = slot_words;
-    a.sp = sp;
-    a.prow = prow ? P_<int64_t>(prow) : nullptr;
-    if (G == 32) integrate_part_kernel<32><<<grid, threads, lds, st>>>(a);
-    else integrate_part_kernel<64><<<grid, threads, lds, st>>>(a);
+  // narrow / wide binning (only worth it when P is well above the typical active count)
+  const bool binned = lists != 0 && P > kNarrowP;
+  int32_t* lst = P_<int32_t>(lists);
+  int32_t* cnt = lst ? lst + 2 * (size_t)c : nullptr;
+  if (binned && part_begin == 0) {
+    MS_HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), st));
+    bin_cells_kernel<<<cdiv(c, 256), 256, 0, st>>>(c, P, kNarrowP, P_<float>(Vmax), prow ? P_<int64_t>(prow) : nullptr,
+                                                   lst, cnt);
     MS_LAUNCH_CHECK();
+  }
+  struct Launch {
+    int Ps;
+    const int32_t* list;
+    const int32_t* count;
+  };
+  Launch launches[2];
+  int nl = 0;
+  if (binned) {
+    launches[nl++] = Launch{kNarrowP, lst, cnt};
+    launches[nl++] = Launch{P, lst + c, cnt + 1};
+  } else {
+    launches[nl++] = Launch{P, nullptr, nullptr};
+  }
+  for (int part = part_begin; part < part_end; ++part) {
+    for (int li = 0; li < nl; ++li) {
+      const Launch& L = launches[li];
+      const int slot_words = slot_words_for(L.Ps, s, sp);
+      const size_t slot_bytes = (size_t)slot_words * 4;
+      int cps = kBlock / G;
+      while (cps > 1 && cps * slot_bytes > 64 * 1024) --cps;
+      const size_t lds = cps * slot_bytes;
+      if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
+      const int threads = cps * G;
+      const unsigned grid = cdiv(c, cps);
+      IntegrateArgs a{};
+      a.c = c; a.P = P; a.s = s; a.m = m; a.R = R; a.C = C;
+      a.N = P_<int32_t>(N); a.Nf = P_<int32_t>(Nf); a.Nb = P_<int32_t>(Nb); a.A = P_<int32_t>(A);
+      a.Kmr = P_<float>(Kmr); a.Kmf = P_<float>(Kmf); a.Kmb = P_<float>(Kmb); a.Vmax = P_<float>(Vmax);
+      a.Ke = P_<float>(Ke);
+      a.cell_mols = P_<float>(cell_mols); a.molmap = P_<float>(molmap); a.positions = P_<int32_t>(positions);
+      if (part == 0 && !X_io) {
+        a.snap_prev = nullptr;
+      } else if (part == 0) {
+        a.snap_prev = snaps[1];
+        a.mask_prev = zero_flags;
+        a.n_iters_prev = n_iters;
+      } else {
+        a.snap_prev = snaps[(part - 1) & 1];
+        a.mask_prev = mk + ms::kEqIters * (part - 1);
+        a.n_iters_prev = n_iters;
+      }
+      a.snap_out = snaps[part & 1];
+      a.mask_out = mk + ms::kEqIters * part;
+      a.trim = trims[part];
+      a.n_iters = n_iters;
+      a.overflow = P_<int>(overflow);
+      a.slot_words = slot_words;
+      a.sp = sp;
+      a.prow = prow ? P_<int64_t>(prow) : nullptr;
+      a.list = L.list;
+      a.count = L.count;
+      a.Ps = L.Ps;
+      if (G == 32) integrate_part_kernel<32><<<grid, threads, lds, st>>>(a);
+      else integrate_part_kernel<64><<<grid, threads, lds, st>>>(a);
+      MS_LAUNCH_CHECK();
+    }
   }
   // the write-back selects the last part's snapshot by its (possibly all-reduced) flags, so a
   // domain-decomposed caller runs it as a separate call once those flags are global

@@ -89,18 +89,19 @@ def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n
         [float(t) for t in trims], int(n_iters),
     ]
     slot_p = _p(None if slot is None else slot.to(torch.int64).contiguous())
+    lists = sc.get("bin_lists", 2 * c + 2, torch.int32, dev)  # narrow / wide cell lists + counts
     nparts = len(trims)
     if flags_hook is None:
-        _m().integrate(*args, 0, nparts, True, slot_p, _stream())
+        _m().integrate(*args, 0, nparts, True, slot_p, _p(lists), _stream())
     else:
         # domain-decomposed world: all-reduce each part's iteration flags before the next part (or
         # the final write-back) reads them, reproducing the reference's `torch.any` over the whole
         # population
         for part in range(nparts):
-            _m().integrate(*args, part, part + 1, False, slot_p, _stream())
+            _m().integrate(*args, part, part + 1, False, slot_p, _p(lists), _stream())
             flags_hook(masks[_EQ * part : _EQ * (part + 1)])
         if nparts:
-            _m().integrate(*args, nparts, nparts, True, slot_p, _stream())
+            _m().integrate(*args, nparts, nparts, True, slot_p, _p(lists), _stream())
     return masks
 
 
