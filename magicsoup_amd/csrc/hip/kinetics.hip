@@ -16,6 +16,7 @@
 //     (or the final scatter) picks the state where the reference's global `torch.any` loop stops.
 //   3 part launches + 1 scatter launch per enzymatic_activity; no grid barriers, no host syncs.
 #include "hip_common.h"
+#include "map_types.h"
 #include "ms_kinetics.h"
 
 namespace msd {
@@ -28,7 +29,8 @@ struct IntegrateArgs {
   const int32_t *N, *Nf, *Nb, *A;
   const float *Kmr, *Kmf, *Kmb, *Vmax, *Ke;
   const float* cell_mols;     // (c, m)       part 0 source
-  const float* molmap;        // (m, R, C)    part 0 source
+  const void* molmap;         // (m, R, C)    part 0 source (storage type map_dtype)
+  int map_dtype;
   const int32_t* positions;   // (c, 2)       part 0 source
   const float* snap_prev;     // (c, kSnap, s) previous part's candidates (part > 0)
   const unsigned* mask_prev;  // previous part's 4 iteration flags
@@ -96,7 +98,8 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
       const int px = a.positions[2 * cell], py = a.positions[2 * cell + 1];
       const size_t pix = (size_t)px * a.C + py, plane = (size_t)a.R * a.C;
       for (int j = lane; j < s; j += G)
-        X0[j] = j < a.m ? a.cell_mols[(size_t)cell * a.m + j] : a.molmap[(size_t)(j - a.m) * plane + pix];
+        X0[j] = j < a.m ? a.cell_mols[(size_t)cell * a.m + j]
+                        : ld_map(a.molmap, (size_t)(j - a.m) * plane + pix, a.map_dtype);
     } else {
       const int k = stop_iter(a.mask_prev, a.n_iters_prev);
       const float* src = a.snap_prev + ((size_t)cell * ms::kSnap + k) * s;
@@ -329,7 +332,7 @@ __global__ void __launch_bounds__(256) bin_cells_kernel(int c, int P, int pn, co
 __global__ void __launch_bounds__(kBlock) integrate_scatter_kernel(int c, int s, int m, int R, int C, const float* snap,
                                                                    const unsigned* mask, int n_iters,
                                                                    const int32_t* positions, float* cell_mols,
-                                                                   float* molmap, float* X_out) {
+                                                                   void* molmap, int map_dtype, float* X_out) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long long)c * s) return;
   const int cell = (int)(t / s), j = (int)(t - (long long)cell * s);
@@ -343,7 +346,7 @@ __global__ void __launch_bounds__(kBlock) integrate_scatter_kernel(int c, int s,
     cell_mols[(size_t)cell * m + j] = x;
   } else {
     const size_t pix = (size_t)positions[2 * cell] * C + positions[2 * cell + 1];
-    molmap[(size_t)(j - m) * R * C + pix] = x;
+    st_map(molmap, (size_t)(j - m) * R * C + pix, x, map_dtype);
   }
 }
 
@@ -477,7 +480,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t 
                uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb, uintptr_t Vmax, uintptr_t Ke, uintptr_t cell_mols,
                uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
                uintptr_t masks, uintptr_t overflow, const std::vector<float>& trims, int n_iters, int part_begin,
-               int part_end, bool scatter, uintptr_t prow, uintptr_t lists, uintptr_t stream) {
+               int part_end, bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t stream) {
   if (c <= 0) return;
   if (n_iters < 0 || n_iters > ms::kEqIters) throw std::invalid_argument("n_iters must be in 0..4");
   const int nparts = (int)trims.size();
@@ -534,7 +537,8 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t 
       a.N = P_<int32_t>(N); a.Nf = P_<int32_t>(Nf); a.Nb = P_<int32_t>(Nb); a.A = P_<int32_t>(A);
       a.Kmr = P_<float>(Kmr); a.Kmf = P_<float>(Kmf); a.Kmb = P_<float>(Kmb); a.Vmax = P_<float>(Vmax);
       a.Ke = P_<float>(Ke);
-      a.cell_mols = P_<float>(cell_mols); a.molmap = P_<float>(molmap); a.positions = P_<int32_t>(positions);
+      a.cell_mols = P_<float>(cell_mols); a.molmap = P_<void>(molmap); a.positions = P_<int32_t>(positions);
+      a.map_dtype = map_dtype;
       if (part == 0 && !X_io) {
         a.snap_prev = nullptr;
       } else if (part == 0) {
@@ -568,7 +572,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t 
     const int last = nparts - 1;
     integrate_scatter_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(
         c, s, m, R, C, snaps[last & 1], mk + ms::kEqIters * last, n_iters, P_<int32_t>(positions),
-        P_<float>(cell_mols), P_<float>(molmap), X_io ? P_<float>(X_io) : nullptr);
+        P_<float>(cell_mols), P_<void>(molmap), map_dtype, X_io ? P_<float>(X_io) : nullptr);
     MS_LAUNCH_CHECK();
   }
 }

@@ -1,0 +1,110 @@
+// Molecule-map storage types: fp32 (default), bf16, fp16; kernels compute in fp32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace msd {
+
+enum MapType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
+
+struct bf16_t {
+  uint16_t u;
+};
+
+template <class T>
+__device__ __forceinline__ float ld(const T* p);
+template <>
+__device__ __forceinline__ float ld<float>(const float* p) {
+  return *p;
+}
+template <>
+__device__ __forceinline__ float ld<bf16_t>(const bf16_t* p) {
+  return __uint_as_float((uint32_t)p->u << 16);
+}
+template <>
+__device__ __forceinline__ float ld<_Float16>(const _Float16* p) {
+  return (float)*p;
+}
+
+template <class T>
+__device__ __forceinline__ void st(T* p, float v);
+template <>
+__device__ __forceinline__ void st<float>(float* p, float v) {
+  *p = v;
+}
+template <>
+__device__ __forceinline__ void st<bf16_t>(bf16_t* p, float v) {
+  uint32_t u = __float_as_uint(v);
+  if ((u & 0x7F800000u) == 0x7F800000u) {  // inf / nan: truncate, keep a quiet nan
+    p->u = (uint16_t)((u >> 16) | ((u & 0xFFFFu) ? 0x40u : 0u));
+    return;
+  }
+  u += 0x7FFFu + ((u >> 16) & 1u);  // round to nearest even
+  p->u = (uint16_t)(u >> 16);
+}
+template <>
+__device__ __forceinline__ void st<_Float16>(_Float16* p, float v) {
+  *p = (_Float16)v;
+}
+
+// 4 consecutive, 4-element-aligned values (one 16 B / 8 B vector access)
+template <class T>
+__device__ __forceinline__ void ld4(const T* p, float v[4]);
+template <>
+__device__ __forceinline__ void ld4<float>(const float* p, float v[4]) {
+  const float4 q = *reinterpret_cast<const float4*>(p);
+  v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+}
+template <>
+__device__ __forceinline__ void ld4<bf16_t>(const bf16_t* p, float v[4]) {
+  const uint2 q = *reinterpret_cast<const uint2*>(p);
+  v[0] = __uint_as_float(q.x << 16), v[1] = __uint_as_float(q.x & 0xFFFF0000u);
+  v[2] = __uint_as_float(q.y << 16), v[3] = __uint_as_float(q.y & 0xFFFF0000u);
+}
+template <>
+__device__ __forceinline__ void ld4<_Float16>(const _Float16* p, float v[4]) {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  const h4 q = *reinterpret_cast<const h4*>(p);
+  v[0] = (float)q[0], v[1] = (float)q[1], v[2] = (float)q[2], v[3] = (float)q[3];
+}
+
+template <class T>
+__device__ __forceinline__ void st4(T* p, const float v[4]);
+template <>
+__device__ __forceinline__ void st4<float>(float* p, const float v[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+template <>
+__device__ __forceinline__ void st4<bf16_t>(bf16_t* p, const float v[4]) {
+  bf16_t h[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) st(h + j, v[j]);
+  *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)h[0].u | ((uint32_t)h[1].u << 16),
+                                            (uint32_t)h[2].u | ((uint32_t)h[3].u << 16));
+}
+template <>
+__device__ __forceinline__ void st4<_Float16>(_Float16* p, const float v[4]) {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  h4 q;
+  q[0] = (_Float16)v[0], q[1] = (_Float16)v[1], q[2] = (_Float16)v[2], q[3] = (_Float16)v[3];
+  *reinterpret_cast<h4*>(p) = q;
+}
+
+// runtime-typed access (cold paths: a few pixels per cell)
+__device__ __forceinline__ float ld_map(const void* base, size_t i, int dtype) {
+  switch (dtype) {
+    case kBF16: return ld(reinterpret_cast<const bf16_t*>(base) + i);
+    case kF16: return ld(reinterpret_cast<const _Float16*>(base) + i);
+    default: return ld(reinterpret_cast<const float*>(base) + i);
+  }
+}
+
+__device__ __forceinline__ void st_map(void* base, size_t i, float v, int dtype) {
+  switch (dtype) {
+    case kBF16: st(reinterpret_cast<bf16_t*>(base) + i, v); break;
+    case kF16: st(reinterpret_cast<_Float16*>(base) + i, v); break;
+    default: st(reinterpret_cast<float*>(base) + i, v); break;
+  }
+}
+
+}  // namespace msd

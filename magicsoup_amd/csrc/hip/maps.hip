@@ -1,0 +1,424 @@
+// gfx950 molecule-map physics: diffusion stencil + mass correction, degradation, permeation and the
+// cell <-> pixel exchanges of spawn / kill (reference world.py:326-331, 520-530, 627-678).
+//
+// The map may be stored as fp32 (default), bf16 or fp16 (opt-in, BASELINE's large-map configs);
+// every kernel computes in fp32 and the diffusion mass totals in fp64.
+//
+// Diffusion stencil: one wavefront owns 64 columns and a band of rows and slides down the band
+// with the 3x3 window in registers -- every map value is loaded once per band (plus one halo row
+// above and below), left/right neighbours come from lane shuffles, only the two edge lanes load
+// their outer column. No LDS, no workgroup barriers; the per-wave before/after sums are reduced
+// per block into fp64 partials.
+#include "hip_common.h"
+#include "map_types.h"
+
+namespace msd {
+
+struct MGeom {
+  int R, C, r_lo, r_hi, wrap;
+};
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// ---------------------------------------------------------------- diffusion
+constexpr int kBand = 32;  // rows per wavefront band
+constexpr int kWaves = 4;  // wavefronts per block (adjacent 64-column strips)
+
+// grid: (ceil(C / (64 kWaves)), ceil(H / kBand), m). out = b*x + a*sum(8 neighbours) of the
+// pre-scaled input over the owned rows of the band; fp64 before/after partial sums per block.
+template <class T>
+__global__ void __launch_bounds__(64 * kWaves) diffuse_stencil_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                                      const float* __restrict__ wa,
+                                                                      const float* __restrict__ wb,
+                                                                      const float* __restrict__ scale, MGeom g,
+                                                                      double* __restrict__ partials) {
+  __shared__ double red[2][kWaves];
+  const int mol = blockIdx.z;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int H = g.r_hi - g.r_lo;
+  const int y = (blockIdx.x * kWaves + wv) * 64 + lane;
+  const bool col = y < g.C;
+  const int yl = y == 0 ? g.C - 1 : y - 1, yr = y + 1 >= g.C ? y + 1 - g.C : y + 1;
+  // a neighbour comes from the adjacent lane unless it is outside this wave's valid columns
+  const bool own_l = lane > 0 && y - 1 >= 0, own_r = lane < 63 && y + 1 < g.C;
+  const size_t plane = (size_t)g.R * g.C;
+  const T* src = in + (size_t)mol * plane;
+  T* dst = out + (size_t)mol * plane;
+  const float sc = scale ? scale[mol] : 1.0f;
+  const float a = wa[mol], b = wb[mol];
+  const int o0 = blockIdx.y * kBand, o1 = min(H, o0 + kBand);
+
+  auto row_of = [&](int o) {  // owned-row offset -> map row (halo / wrap)
+    int x = g.r_lo + o;
+    if (x < 0) x += g.R;
+    if (x >= g.R) x -= g.R;
+    return x;
+  };
+  // v: centre, l/r: horizontal neighbours, h = l + v + r, for rows o-1 (p), o (c), o+1 (n)
+  auto load = [&](int o, float& v, float& l, float& r) {
+    const size_t base = (size_t)row_of(o) * g.C;
+    v = col ? ld(src + base + y) * sc : 0.0f;
+    const float vl = __shfl_up(v, 1), vr = __shfl_down(v, 1);
+    l = own_l ? vl : (col ? ld(src + base + yl) * sc : 0.0f);
+    r = own_r ? vr : (col ? ld(src + base + yr) * sc : 0.0f);
+  };
+  float vp, lp, rp, vc, lc, rc;
+  load(o0 - 1, vp, lp, rp);
+  load(o0, vc, lc, rc);
+  float hp = lp + vp + rp, hc = lc + vc + rc;
+  double before = 0.0, after = 0.0;
+  for (int o = o0; o < o1; ++o) {
+    float vn, ln, rn;
+    load(o + 1, vn, ln, rn);
+    const float hn = ln + vn + rn;
+    const float ns = hp + hn + lc + rc;
+    const float v = b * vc + a * ns;
+    if (col) {
+      st(dst + (size_t)row_of(o) * g.C + y, v);
+      before += vc;
+      after += v;
+    }
+    hp = hc;
+    vc = vn;
+    lc = ln;
+    rc = rn;
+    hc = hn;
+  }
+  before = wave_sum_d(before);
+  after = wave_sum_d(after);
+  if (lane == 0) {
+    red[0][wv] = before;
+    red[1][wv] = after;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double sb = 0.0, sa = 0.0;
+    for (int w = 0; w < kWaves; ++w) {
+      sb += red[0][w];
+      sa += red[1][w];
+    }
+    const size_t tiles = (size_t)gridDim.x * gridDim.y;
+    const size_t t = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    partials[((size_t)mol * tiles + t) * 2] = sb;
+    partials[((size_t)mol * tiles + t) * 2 + 1] = sa;
+  }
+}
+
+// Vector variant for C % 4 == 0 (every practical map): a lane owns 4 adjacent columns (one
+// 16 B / 8 B access per row), a wave 256 columns; the 4 waves of a block take 4 consecutive bands
+// of the same column strip. Rows are fetched two ahead so two loads per wave are in flight.
+// grid: (ceil(C / 256), ceil(ceil(H / kBand) / 4), m).
+constexpr int kVBand = 32;
+template <class T>
+__global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                               const float* __restrict__ wa,
+                                                               const float* __restrict__ wb,
+                                                               const float* __restrict__ scale, MGeom g,
+                                                               double* __restrict__ partials) {
+  __shared__ double red[2][4];
+  const int mol = blockIdx.z;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int H = g.r_hi - g.r_lo;
+  const int y0 = blockIdx.x * 256 + lane * 4;
+  const bool col = y0 < g.C;
+  const bool need_l = lane == 0 && col, need_r = col && (lane == 63 || y0 + 4 >= g.C);
+  const int yl = y0 == 0 ? g.C - 1 : y0 - 1, yr = y0 + 4 >= g.C ? 0 : y0 + 4;
+  const size_t plane = (size_t)g.R * g.C;
+  const T* src = in + (size_t)mol * plane;
+  T* dst = out + (size_t)mol * plane;
+  const float sc = scale ? scale[mol] : 1.0f;
+  const float a = wa[mol], b = wb[mol];
+  const int o0 = (blockIdx.y * 4 + wv) * kVBand, o1 = min(H, o0 + kVBand);
+
+  auto row_of = [&](int o) {
+    int x = g.r_lo + o;
+    if (x < 0) x += g.R;
+    if (x >= g.R) x -= g.R;
+    return x;
+  };
+  struct Raw {
+    float v[4], el, er;
+  };
+  auto fetch = [&](int o, Raw& r) {
+    const size_t base = (size_t)row_of(o) * g.C;
+    if (col) ld4(src + base + y0, r.v);
+    else r.v[0] = r.v[1] = r.v[2] = r.v[3] = 0.0f;
+    r.el = need_l ? ld(src + base + yl) : 0.0f;
+    r.er = need_r ? ld(src + base + yr) : 0.0f;
+  };
+  // scaled values of the row plus the left neighbour of column y0 and the right one of y0 + 3
+  auto finish = [&](const Raw& r, float v[4], float& L, float& Rn) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = r.v[j] * sc;
+    const float up = __shfl_up(v[3], 1), dn = __shfl_down(v[0], 1);
+    L = need_l ? r.el * sc : up;
+    Rn = need_r ? r.er * sc : dn;
+  };
+  auto hsum = [](const float v[4], float L, float Rn, float h[4]) {
+    h[0] = L + v[0] + v[1];
+    h[1] = v[0] + v[1] + v[2];
+    h[2] = v[1] + v[2] + v[3];
+    h[3] = v[2] + v[3] + Rn;
+  };
+
+  double before = 0.0, after = 0.0;
+  if (o0 < H) {
+    Raw rp, rc, rn, rn2;
+    fetch(o0 - 1, rp);
+    fetch(o0, rc);
+    fetch(o0 + 1, rn);
+    float vp[4], Lp, Rp, vc[4], Lc, Rc, hp[4], hc[4];
+    finish(rp, vp, Lp, Rp);
+    finish(rc, vc, Lc, Rc);
+    hsum(vp, Lp, Rp, hp);
+    hsum(vc, Lc, Rc, hc);
+    for (int o = o0; o < o1; ++o) {
+      if (o + 2 <= o1) fetch(o + 2, rn2);  // row o + 2 (at most the halo row below the band)
+      float vn[4], Ln, Rn, hn[4];
+      finish(rn, vn, Ln, Rn);
+      hsum(vn, Ln, Rn, hn);
+      float res[4];
+      const float lft[4] = {Lc, vc[0], vc[1], vc[2]}, rgt[4] = {vc[1], vc[2], vc[3], Rc};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) res[j] = b * vc[j] + a * (hp[j] + hn[j] + lft[j] + rgt[j]);
+      if (col) {
+        st4(dst + (size_t)row_of(o) * g.C + y0, res);
+        before += (double)((vc[0] + vc[1]) + (vc[2] + vc[3]));
+        after += (double)((res[0] + res[1]) + (res[2] + res[3]));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        hp[j] = hc[j];
+        hc[j] = hn[j];
+        vc[j] = vn[j];
+      }
+      Lc = Ln;
+      Rc = Rn;
+      rn = rn2;
+    }
+  }
+  before = wave_sum_d(before);
+  after = wave_sum_d(after);
+  if (lane == 0) {
+    red[0][wv] = before;
+    red[1][wv] = after;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const size_t tiles = (size_t)gridDim.x * gridDim.y;
+    const size_t t = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    partials[((size_t)mol * tiles + t) * 2] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    partials[((size_t)mol * tiles + t) * 2 + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  }
+}
+
+// one block per molecule: totals[mol] = (sum before, sum after) over the owned rows
+__global__ void __launch_bounds__(256) diffuse_reduce_kernel(const double* partials, int tiles, double* totals) {
+  __shared__ double sb[4], sa[4];
+  const int mol = blockIdx.x;
+  double b = 0.0, a = 0.0;
+  for (int t = threadIdx.x; t < tiles; t += blockDim.x) {
+    b += partials[((size_t)mol * tiles + t) * 2];
+    a += partials[((size_t)mol * tiles + t) * 2 + 1];
+  }
+  b = wave_sum_d(b);
+  a = wave_sum_d(a);
+  if ((threadIdx.x & 63) == 0) {
+    sb[threadIdx.x >> 6] = b;
+    sa[threadIdx.x >> 6] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    totals[2 * mol] = sb[0] + sb[1] + sb[2] + sb[3];
+    totals[2 * mol + 1] = sa[0] + sa[1] + sa[2] + sa[3];
+  }
+}
+
+// map[owned rows] = max(tmp + (before - after) / n_pix, 0); a plane's owned rows are one
+// contiguous range of `span` values starting at r_lo * C. 4 values per thread and iteration.
+template <class T>
+__global__ void __launch_bounds__(256) diffuse_correct_kernel(const T* __restrict__ tmp, T* __restrict__ map,
+                                                              const double* __restrict__ totals, double n_pix,
+                                                              long long plane, long long start, long long span, int m) {
+  const long long s4 = (span + 3) / 4;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < s4 * m;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int mol = (int)(i / s4);
+    const float c = (float)((totals[2 * mol] - totals[2 * mol + 1]) / n_pix);
+    const long long q = (i - (long long)mol * s4) * 4;
+    const long long o = (long long)mol * plane + start + q;
+    if (q + 4 <= span && (o % 4) == 0) {
+      float v[4];
+      ld4(tmp + o, v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j] + c, 0.0f);
+      st4(map + o, v);
+    } else {
+      for (long long e = 0; e < 4 && q + e < span; ++e) st(map + o + e, fmaxf(ld(tmp + o + e) + c, 0.0f));
+    }
+  }
+}
+
+// map *= f[mol] (standalone degradation of the map)
+template <class T>
+__global__ void __launch_bounds__(256) scale_planes_kernel(T* map, const float* f, long long plane, int m) {
+  const long long total = plane * m;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
+    st(map + i, ld(map + i) * f[i / plane]);
+}
+
+// ---------------------------------------------------------------- cell <-> pixel exchanges
+// Killed cells spill their molecules onto their pixel and free it; new cells take half of their
+// pixel's molecules. One thread per (cell, molecule); pixels are distinct, so no atomics.
+template <class T>
+__global__ void __launch_bounds__(256) spill_free_kernel(int k, int m, const int64_t* idxs, const uint8_t* dead,
+                                                         const int32_t* pos, int C, long long plane,
+                                                         const float* cell_mols, T* map, uint8_t* cell_map) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)k * m) return;
+  const int i = (int)(t / m), j = (int)(t - (long long)i * m);
+  long long c = i;
+  if (idxs) c = idxs[i];
+  else if (!dead[c]) return;
+  const long long pix = (long long)pos[2 * c] * C + pos[2 * c + 1];
+  T* p = map + j * plane + pix;
+  st(p, ld(p) + cell_mols[c * m + j]);
+  if (j == 0) cell_map[pix] = 0;
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) pickup_kernel(int k, int m, const int64_t* idxs, const int32_t* pos, int C,
+                                                     long long plane, float* cell_mols, T* map) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)k * m) return;
+  const int i = (int)(t / m), j = (int)(t - (long long)i * m);
+  const long long c = idxs[i];
+  const long long pix = (long long)pos[2 * c] * C + pos[2 * c + 1];
+  T* p = map + j * plane + pix;
+  const float x = ld(p);
+  const float half = x * 0.5f;
+  cell_mols[c * m + j] += half;
+  st(p, x - half);
+}
+
+// exchange between cells and their pixels (reference world.py:651-665), one thread per
+// (cell, molecule)
+template <class T>
+__global__ void __launch_bounds__(256) permeate_kernel(int c, int m, long long plane, int C, const int32_t* pos,
+                                                       const float* perm, float* cell_mols, T* map) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)c * m) return;
+  const int cell = (int)(t / m), i = (int)(t - (long long)cell * m);
+  const float p = perm[i];
+  if (p == 0.0f) return;
+  T* q = map + (size_t)i * plane + (size_t)pos[2 * cell] * C + pos[2 * cell + 1];
+  const float xi = cell_mols[t], xe = ld(q);
+  const float di = xi * p, de = xe * p;
+  cell_mols[t] = xi + (de - di);
+  st(q, xe + (di - de));
+}
+
+// ---------------------------------------------------------------- host launchers
+static MGeom mgeom(int R, int C, int r_lo, int r_hi, int wrap) {
+  if (R <= 0 || C <= 0 || r_lo < 0 || r_hi > R || r_lo >= r_hi) throw std::invalid_argument("bad map geometry");
+  if (!wrap && (r_lo < 1 || r_hi > R - 1)) throw std::invalid_argument("a non-wrapping strip needs halo rows");
+  return MGeom{R, C, r_lo, r_hi, wrap};
+}
+
+// dispatch a templated launch on the map storage type
+#define MS_MAP_DISPATCH(dtype, LAUNCH)                                   \
+  switch (dtype) {                                                       \
+    case kF32: { using T = float; LAUNCH; } break;                       \
+    case kBF16: { using T = bf16_t; LAUNCH; } break;                     \
+    case kF16: { using T = _Float16; LAUNCH; } break;                    \
+    default: throw std::invalid_argument("unknown molecule map dtype");  \
+  }
+
+static bool use_vec4(int C) { return C % 4 == 0; }
+
+size_t diffuse_partials_len(int m, int C, int H) {
+  if (use_vec4(C)) return (size_t)cdiv(C, 256) * cdiv(cdiv(H, kVBand), 4) * m * 2;
+  return (size_t)cdiv(C, 64 * kWaves) * cdiv(H, kBand) * m * 2;
+}
+
+void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
+                     uintptr_t wb, uintptr_t scale, uintptr_t partials, uintptr_t totals, int dtype, uintptr_t stream) {
+  if (m <= 0) return;
+  const MGeom g = mgeom(R, C, r_lo, r_hi, wrap);
+  hipStream_t st_ = S_(stream);
+  const int H = r_hi - r_lo;
+  const bool v4 = use_vec4(C);
+  const dim3 grid = v4 ? dim3(cdiv(C, 256), cdiv(cdiv(H, kVBand), 4), m) : dim3(cdiv(C, 64 * kWaves), cdiv(H, kBand), m);
+  if (v4) {
+    MS_MAP_DISPATCH(dtype, (diffuse_stencil4_kernel<T><<<grid, 256, 0, st_>>>(
+                               P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
+                               g, P_<double>(partials))));
+  } else {
+    MS_MAP_DISPATCH(dtype, (diffuse_stencil_kernel<T><<<grid, 64 * kWaves, 0, st_>>>(
+                               P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
+                               g, P_<double>(partials))));
+  }
+  MS_LAUNCH_CHECK();
+  diffuse_reduce_kernel<<<m, 256, 0, st_>>>(P_<double>(partials), (int)(grid.x * grid.y), P_<double>(totals));
+  MS_LAUNCH_CHECK();
+}
+
+void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t totals,
+                     double n_pix, int dtype, uintptr_t stream) {
+  if (m <= 0) return;
+  const long long plane = (long long)R * C, start = (long long)r_lo * C, span = (long long)(r_hi - r_lo) * C;
+  const unsigned g = std::min<long long>(cdiv((span + 3) / 4 * m, 256), 8192);
+  MS_MAP_DISPATCH(dtype, (diffuse_correct_kernel<T><<<g, 256, 0, S_(stream)>>>(P_<T>(tmp), P_<T>(map),
+                                                                               P_<double>(totals), n_pix, plane,
+                                                                               start, span, m)));
+  MS_LAUNCH_CHECK();
+}
+
+void scale_planes(int m, long long plane, uintptr_t map, uintptr_t f, int dtype, uintptr_t stream) {
+  if (m <= 0 || plane <= 0) return;
+  const unsigned g = std::min<long long>(cdiv(plane * m, 256), 8192);
+  MS_MAP_DISPATCH(dtype, (scale_planes_kernel<T><<<g, 256, 0, S_(stream)>>>(P_<T>(map), P_<float>(f), plane, m)));
+  MS_LAUNCH_CHECK();
+}
+
+void spill_free(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
+                uintptr_t cell_map, int dtype, uintptr_t stream) {
+  if (k <= 0 || m <= 0) return;
+  MS_MAP_DISPATCH(dtype, (spill_free_kernel<T><<<cdiv((long long)k * m, 256), 256, 0, S_(stream)>>>(
+                             k, m, P_<int64_t>(idxs), nullptr, P_<int32_t>(pos), C, (long long)R * C,
+                             P_<float>(cell_mols), P_<T>(map), P_<uint8_t>(cell_map))));
+  MS_LAUNCH_CHECK();
+}
+
+void spill_free_mask(int n, int m, uintptr_t dead, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
+                     uintptr_t cell_map, int dtype, uintptr_t stream) {
+  if (n <= 0 || m <= 0) return;
+  MS_MAP_DISPATCH(dtype, (spill_free_kernel<T><<<cdiv((long long)n * m, 256), 256, 0, S_(stream)>>>(
+                             n, m, nullptr, P_<uint8_t>(dead), P_<int32_t>(pos), C, (long long)R * C,
+                             P_<float>(cell_mols), P_<T>(map), P_<uint8_t>(cell_map))));
+  MS_LAUNCH_CHECK();
+}
+
+void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map, int dtype,
+            uintptr_t stream) {
+  if (k <= 0 || m <= 0) return;
+  MS_MAP_DISPATCH(dtype, (pickup_kernel<T><<<cdiv((long long)k * m, 256), 256, 0, S_(stream)>>>(
+                             k, m, P_<int64_t>(idxs), P_<int32_t>(pos), C, (long long)R * C, P_<float>(cell_mols),
+                             P_<T>(map))));
+  MS_LAUNCH_CHECK();
+}
+
+void permeate(int c, int m, int R, int C, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map, int dtype,
+              uintptr_t stream) {
+  if (c <= 0 || m <= 0) return;
+  MS_MAP_DISPATCH(dtype, (permeate_kernel<T><<<cdiv((long long)c * m, 256), 256, 0, S_(stream)>>>(
+                             c, m, (long long)R * C, C, P_<int32_t>(pos), P_<float>(perm), P_<float>(cell_mols),
+                             P_<T>(map))));
+  MS_LAUNCH_CHECK();
+}
+
+}  // namespace msd

@@ -19,16 +19,25 @@ void split_cells(int k, int m, uintptr_t parents, uintptr_t children, uintptr_t 
 void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, bool vacate,
                   uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result, int rounds,
                   uint64_t seed, uint64_t call, uintptr_t stream);
-void spill_free(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
-                uintptr_t cell_map, uintptr_t stream);
-void spill_free_mask(int n, int m, uintptr_t dead, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
-                     uintptr_t cell_map, uintptr_t stream);
-void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
-            uintptr_t stream);
 void neighbor_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map, uintptr_t keys,
                     uintptr_t stream);
 void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
                     uintptr_t stream);
+// maps.hip
+size_t diffuse_partials_len(int m, int C, int H);
+void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
+                     uintptr_t wb, uintptr_t scale, uintptr_t partials, uintptr_t totals, int dtype, uintptr_t stream);
+void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t totals,
+                     double n_pix, int dtype, uintptr_t stream);
+void scale_planes(int m, long long plane, uintptr_t map, uintptr_t f, int dtype, uintptr_t stream);
+void spill_free(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
+                uintptr_t cell_map, int dtype, uintptr_t stream);
+void spill_free_mask(int n, int m, uintptr_t dead, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
+                     uintptr_t cell_map, int dtype, uintptr_t stream);
+void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map, int dtype,
+            uintptr_t stream);
+void permeate(int c, int m, int R, int C, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map, int dtype,
+              uintptr_t stream);
 void gather_rows(int n, uintptr_t src_rows, uintptr_t dst_rows,
                  const std::vector<std::tuple<uintptr_t, uintptr_t, long long, long long, long long>>& descs,
                  uintptr_t stream);
@@ -37,26 +46,15 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t 
                uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb, uintptr_t Vmax, uintptr_t Ke, uintptr_t cell_mols,
                uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
                uintptr_t masks, uintptr_t overflow, const std::vector<float>& trims, int n_iters, int part_begin,
-               int part_end, bool scatter, uintptr_t prow, uintptr_t lists, uintptr_t stream);
+               int part_end, bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t stream);
 void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_t rows, uintptr_t vmax_w, int nw,
                   uintptr_t km_w, int nk, uintptr_t signs, int nsg, uintptr_t hills, int nh, uintptr_t RM,
                   uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
                   uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
                   uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t stream);
 // world.hip
-void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
-                     uintptr_t wb, uintptr_t scale, uintptr_t partials, uintptr_t totals, uintptr_t stream);
-void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t totals,
-                     double n_pix, uintptr_t stream);
-size_t diffuse_partials_len(int m, int C, int H);
-void scale_planes(int m, long long plane, uintptr_t map, uintptr_t f, uintptr_t stream);
-void permeate(int c, int m, int R, int C, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map,
-              uintptr_t stream);
 void claim_free(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uint64_t seed, uint64_t call,
                 int attempts, uintptr_t out, uintptr_t stream);
-void pick_neighbour(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap,
-                    uintptr_t cell_map, uintptr_t pending, uint64_t seed, uint64_t call, uintptr_t cand,
-                    uintptr_t stream);
 void index_map(int c, uintptr_t pos, int C, uintptr_t idx_map, bool clear, uintptr_t stream);
 void neighbor_pairs(int nf, uintptr_t from, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map,
                     uintptr_t in_from, uintptr_t in_to, uintptr_t counter, int cap, uintptr_t pairs, uintptr_t stream);
@@ -119,7 +117,6 @@ PYBIND11_MODULE(_hip, m) {
   m.def("split_cells", &msd::split_cells);
   m.def("permeate", &msd::permeate);
   m.def("claim_free", &msd::claim_free);
-  m.def("pick_neighbour", &msd::pick_neighbour);
   m.def("index_map", &msd::index_map);
   m.def("neighbor_pairs", &msd::neighbor_pairs);
   m.def("translate_count", &msd::translate_count);

@@ -141,10 +141,15 @@ class World:
         device: str = "cpu",
         batch_size: int | None = None,
         seed: int | None = None,
+        map_dtype: torch.dtype = torch.float32,
     ):
         if not torch.cuda.is_available():
             device = "cpu"
         self.device = device
+        if map_dtype not in (torch.float32, torch.bfloat16, torch.float16):
+            raise ValueError(f"map_dtype must be float32, bfloat16 or float16, got {map_dtype}")
+        # reduced-precision map storage is a GPU-kernel feature; host kernels are fp32-only
+        self.map_dtype = map_dtype if torch.device(device).type == "cuda" else torch.float32
         self.batch_size = batch_size
         self.map_size = map_size
         self.abs_temp = abs_temp
@@ -215,8 +220,9 @@ class World:
             return
         if name == "molecule_map":
             t = torch.as_tensor(value, device=self.device)
-            if t.dtype != torch.float32 or not t.is_contiguous():
-                t = t.to(torch.float32).contiguous()
+            want = self.__dict__.get("map_dtype", torch.float32)
+            if t.dtype != want or not t.is_contiguous():
+                t = t.to(want).contiguous()
             self.__dict__["_molmap"] = t
             self.__dict__["_pending_scale"] = None
             return
@@ -682,7 +688,9 @@ class World:
         self.__dict__["_genome_col"] = StringColumn(self._genomes)
         self.__dict__["_label_col"] = StringColumn(self._labels)
         cmap = self.__dict__.pop("_cell_map")
-        self.__dict__["_molmap"] = self.__dict__["_molmap"].to(dev)
+        mdt = self.__dict__.get("map_dtype", torch.float32) if dev.type == "cuda" else torch.float32
+        self.__dict__["map_dtype"] = mdt
+        self.__dict__["_molmap"] = self.__dict__["_molmap"].to(dev, mdt).contiguous()
         self._set_cell_map(cmap.to(dev))
 
     def to(self, device: str) -> "World":
@@ -735,9 +743,9 @@ class World:
     def _get_molecule_map(self, n: int, size: int, init: str) -> torch.Tensor:
         shape = (n, size, size) if self._map_shape() == (size, size) else (n, *self._map_shape())
         if init == "zeros":
-            return torch.zeros(*shape, dtype=torch.float32, device=self.device)
+            return torch.zeros(*shape, dtype=self.map_dtype, device=self.device)
         if init == "randn":
-            return (torch.randn(*shape, dtype=torch.float32, device=self.device) + 10.0).abs()
+            return (torch.randn(*shape, dtype=torch.float32, device=self.device) + 10.0).abs().to(self.map_dtype)
         raise ValueError(f"Didnt recognize mol_map_init={init}. Should be one of: 'zeros', 'randn'.")
 
     def _get_permeate(self, mol_perm_rate: float) -> float:

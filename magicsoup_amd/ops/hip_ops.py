@@ -26,6 +26,17 @@ def _p(t: torch.Tensor | None) -> int:
     return 0 if t is None else t.data_ptr()
 
 
+_MAP_DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def _mdt(t: torch.Tensor) -> int:
+    """Storage-type code of a molecule map for the kernels (maps.hip MapType)."""
+    try:
+        return _MAP_DTYPES[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported molecule map dtype {t.dtype}") from None
+
+
 class Scratch:
     """Grow-only named device buffers (one set per world / kinetics object)."""
 
@@ -78,8 +89,9 @@ def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n
         m = world.n_molecules
         R, C = geom(world)[:2]
         cm, mm, pos = world.cell_molecules, world._molmap, world.cell_positions
+        mdt = _mdt(mm)
     else:
-        m, R, C, cm, mm, pos = 0, 0, 0, None, None, None
+        m, R, C, cm, mm, pos, mdt = 0, 0, 0, None, None, None, 0
     args = [
         c, P, s, m, R, C,
         _p(N), _p(p["Nf"]), _p(p["Nb"]), _p(p["A"]),
@@ -92,16 +104,16 @@ def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n
     lists = sc.get("bin_lists", 2 * c + 2, torch.int32, dev)  # narrow / wide cell lists + counts
     nparts = len(trims)
     if flags_hook is None:
-        _m().integrate(*args, 0, nparts, True, slot_p, _p(lists), _stream())
+        _m().integrate(*args, 0, nparts, True, slot_p, _p(lists), mdt, _stream())
     else:
         # domain-decomposed world: all-reduce each part's iteration flags before the next part (or
         # the final write-back) reads them, reproducing the reference's `torch.any` over the whole
         # population
         for part in range(nparts):
-            _m().integrate(*args, part, part + 1, False, slot_p, _p(lists), _stream())
+            _m().integrate(*args, part, part + 1, False, slot_p, _p(lists), mdt, _stream())
             flags_hook(masks[_EQ * part : _EQ * (part + 1)])
         if nparts:
-            _m().integrate(*args, nparts, nparts, True, slot_p, _p(lists), _stream())
+            _m().integrate(*args, nparts, nparts, True, slot_p, _p(lists), mdt, _stream())
     return masks
 
 
@@ -183,7 +195,7 @@ def diffuse(world) -> None:
     m = int(mm.size(0))
     sc = _scratch(world)
     dev = mm.device
-    tmp = sc.get("diff_tmp", mm.numel(), torch.float32, dev)
+    tmp = sc.get("diff_tmp", mm.numel(), mm.dtype, dev)
     partials = sc.get("diff_partials", int(_m().diffuse_partials_len(m, C, r_hi - r_lo)), torch.float64, dev)
     totals = sc.get("diff_totals", 2 * m, torch.float64, dev)
     w = world.__dict__.get("_diff_w")
@@ -196,13 +208,13 @@ def diffuse(world) -> None:
     # neighbours' unscaled boundary rows carry the same pending factor
     scale = world.__dict__.get("_pending_scale")
     _m().diffuse_stencil(m, R, C, r_lo, r_hi, wrap, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale), _p(partials),
-                         _p(totals), _stream())
+                         _p(totals), _mdt(mm), _stream())
     world.__dict__["_pending_scale"] = None
     reduce = getattr(world, "_allreduce_totals", None)
     if reduce is not None:
         reduce(totals)
     n_pix = float(getattr(world, "_n_pix_global", R * C if wrap else (r_hi - r_lo) * C))
-    _m().diffuse_correct(m, R, C, r_lo, r_hi, _p(mm), _p(tmp), _p(totals), n_pix, _stream())
+    _m().diffuse_correct(m, R, C, r_lo, r_hi, _p(mm), _p(tmp), _p(totals), n_pix, _mdt(mm), _stream())
 
 
 def permeate(world) -> None:
@@ -217,7 +229,7 @@ def permeate(world) -> None:
         return
     R, C = geom(world)[:2]
     _m().permeate(world.n_cells, world.n_molecules, R, C, _p(world.cell_positions), _p(perm[1]),
-                  _p(world.cell_molecules), _p(mm), _stream())
+                  _p(world.cell_molecules), _p(mm), _mdt(mm), _stream())
 
 
 def _degrade_factors(world) -> torch.Tensor:
@@ -246,7 +258,7 @@ def apply_pending_scale(world) -> None:
         return
     mm = world.__dict__["_molmap"]
     world.__dict__["_pending_scale"] = None
-    _m().scale_planes(int(mm.size(0)), int(mm.size(1)) * int(mm.size(2)), _p(mm), _p(f), _stream())
+    _m().scale_planes(int(mm.size(0)), int(mm.size(1)) * int(mm.size(2)), _p(mm), _p(f), _mdt(mm), _stream())
 
 
 # ---------------------------------------------------------------------------- placement
@@ -320,7 +332,8 @@ def spill_and_free(world, idxs: torch.Tensor) -> None:
     R, C = geom(world)[:2]
     ix = idxs.to(torch.int64).contiguous()
     _m().spill_free(int(ix.numel()), world.n_molecules, _p(ix), _p(world.cell_positions), R, C,
-                    _p(world.cell_molecules), _p(world._molmap), _p(_cell_map_bytes(world)), _stream())
+                    _p(world.cell_molecules), _p(world._molmap), _p(_cell_map_bytes(world)), _mdt(world._molmap),
+                    _stream())
 
 
 def spill_and_free_mask(world, dead: torch.Tensor) -> None:
@@ -329,7 +342,8 @@ def spill_and_free_mask(world, dead: torch.Tensor) -> None:
     R, C = geom(world)[:2]
     d = dead.to(torch.uint8).contiguous() if dead.dtype != torch.bool else dead.contiguous().view(torch.uint8)
     _m().spill_free_mask(world.n_cells, world.n_molecules, _p(d), _p(world.cell_positions), R, C,
-                         _p(world.cell_molecules), _p(world._molmap), _p(_cell_map_bytes(world)), _stream())
+                         _p(world.cell_molecules), _p(world._molmap), _p(_cell_map_bytes(world)), _mdt(world._molmap),
+                    _stream())
 
 
 def pickup_molecules(world, new: torch.Tensor) -> None:
@@ -338,7 +352,7 @@ def pickup_molecules(world, new: torch.Tensor) -> None:
     R, C = geom(world)[:2]
     ix = new.to(torch.int64).contiguous()
     _m().pickup(int(ix.numel()), world.n_molecules, _p(ix), _p(world.cell_positions), R, C,
-                _p(world.cell_molecules), _p(world._molmap), _stream())
+                _p(world.cell_molecules), _p(world._molmap), _mdt(world._molmap), _stream())
 
 
 def split_cells(world, parents: torch.Tensor, children: torch.Tensor) -> None:

@@ -60,8 +60,9 @@ def _halo_occ(world, wrap: int):
 
 def _molmap(world) -> torch.Tensor:
     mm = world.molecule_map
-    if mm.dtype != torch.float32 or not mm.is_contiguous():
-        world.molecule_map = mm = mm.to(torch.float32).contiguous()
+    want = getattr(world, "map_dtype", torch.float32)
+    if mm.dtype != want or not mm.is_contiguous():
+        world.molecule_map = mm = mm.to(want).contiguous()
     return mm
 
 

@@ -23,7 +23,10 @@ _FILES = ("cell_molecules", "cell_map", "molecule_map", "cell_lifetimes", "cell_
 def save_state(world, statedir: Path) -> None:
     statedir.mkdir(parents=True, exist_ok=True)
     for name in _FILES:
-        torch.save(getattr(world, name).detach().cpu().clone(), statedir / f"{name}.pt")
+        t = getattr(world, name).detach().cpu()
+        if name == "molecule_map":
+            t = t.to(torch.float32)  # checkpoints always hold fp32 maps, whatever the storage dtype
+        torch.save(t.clone(), statedir / f"{name}.pt")
     genomes = world.cell_genomes.tolist()
     labels = world.cell_labels.tolist()
     text = "\n".join(f">{i} {lab}\n{g}" for i, (g, lab) in enumerate(zip(genomes, labels)))

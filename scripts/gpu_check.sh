@@ -29,3 +29,9 @@ if [[ "$what" == bench || "$what" == all ]]; then
   run bench_4096_50k 600 python bench.py --steps 30 --warmup 5 "$@"
   run bench_4096_50k_phases 600 python bench.py --steps 20 --warmup 5 --profile-phases "$@"
 fi
+if [[ "$what" == lowp ]]; then
+  run pytest_maps 600 python -m pytest tests/test_gpu_kernels.py -m gpu -q -k "diffusion or reduced or bf16 or permeation"
+  run bench_4096_50k 600 python bench.py --steps 30 --warmup 5 "$@"
+  run bench_4096_50k_bf16 600 python bench.py --steps 30 --warmup 5 --map-dtype bf16 "$@"
+  run bench_4096_50k_phases 600 python bench.py --steps 20 --warmup 5 --profile-phases "$@"
+fi
