@@ -1,0 +1,231 @@
+"""Long-run invariants (reference tests/slow/*.py behaviours), on the host core and on the GPU.
+
+Marked ``slow``; sized so the CPU set still finishes in well under a minute with the native host core.
+"""
+import random
+
+import pytest
+import torch
+
+import magicsoup_amd as ms
+from magicsoup_amd.examples.wood_ljungdahl import CHEMISTRY as WL
+from magicsoup_amd.models import mutations as muts
+from tests.conftest import Retry, gen_genomes
+
+pytestmark = pytest.mark.slow
+
+DEVICES = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+
+_SX = ms.Molecule("SLx", 10e3)
+_SY = ms.Molecule("SLy", 20e3)
+_SZ = ms.Molecule("SLz", 30e3)
+
+
+# ----------------------------------------------------------------------------- world
+@pytest.mark.parametrize("device", DEVICES)
+def test_molecule_amount_integrity_during_diffusion(device):
+    world = ms.World(chemistry=ms.Chemistry(molecules=WL.molecules, reactions=[]), map_size=128, device=device)
+    exp = world.molecule_map.double().sum(dim=[1, 2])
+    for step in range(100):
+        world.diffuse_molecules()
+        res = world.molecule_map.double().sum(dim=[1, 2])
+        assert (res.sum() - exp.sum()).abs() < 10.0, step
+        assert torch.all((res - exp).abs() < 1.0), step
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_molecule_amount_integrity_during_reactions(device):
+    # x <-> y and x + y <-> z: counting z twice, the total is invariant under enzymatic activity
+    chem = ms.Chemistry(molecules=[_SX, _SY, _SZ], reactions=[([_SX], [_SY]), ([_SX, _SY], [_SZ])])
+    world = ms.World(chemistry=chem, map_size=128, device=device)
+    world.spawn_cells(genomes=[ms.random_genome(s=500) for _ in range(1000)])
+
+    def count() -> float:
+        mm, cm = world.molecule_map.double(), world.cell_molecules.double()
+        return float(mm[[0, 1]].sum() + 2 * mm[2].sum() + cm[:, [0, 1]].sum() + 2 * cm[:, 2].sum())
+
+    n0 = count()
+    for step in range(100):
+        world.enzymatic_activity()
+        assert count() == pytest.approx(n0, abs=1.0), step
+
+
+def test_run_world_without_reactions():
+    world = ms.World(chemistry=ms.Chemistry(molecules=WL.molecules[:2], reactions=[]))
+    world.spawn_cells(genomes=[ms.random_genome(s=500) for _ in range(1000)])
+    for _ in range(100):
+        world.enzymatic_activity()
+    assert world.n_cells > 0 and torch.isfinite(world.cell_molecules).all()
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_exploding_molecules(device):
+    # an unfair reaction step (one side slowed, the other not) would create molecules from nothing
+    world = ms.World(chemistry=WL, map_size=128, device=device)
+    world.spawn_cells(genomes=[ms.random_genome(s=500) for _ in range(1000)])
+    for i in range(100):
+        world.degrade_molecules()
+        world.diffuse_molecules()
+        world.enzymatic_activity()
+        for t in (world.molecule_map, world.cell_molecules):
+            assert t.min() >= 0.0, i
+            assert 0.0 < t.float().mean() < 50.0, i
+            assert t.max() < 500.0, i
+    assert world.molecule_map.dtype is torch.float32
+    assert world.cell_molecules.dtype is torch.float32
+    assert world.cell_divisions.dtype is torch.int32
+    assert world.cell_positions.dtype is torch.int32
+    assert world.cell_lifetimes.dtype is torch.int32
+    assert world.cell_map.dtype is torch.bool
+
+
+# ----------------------------------------------------------------------------- kinetics
+def _wl_kinetics(device="cpu") -> ms.Kinetics:
+    return ms.Kinetics(chemistry=WL, abs_temp=310, scalar_enc_size=61, vector_enc_size=3904, device=device)
+
+
+def test_cell_params_are_always_set_reproduceably():
+    n_cells = 100
+    for i in range(10):
+        proteomes = []
+        for _ in range(n_cells):
+            prots = []
+            for _ in range(random.randrange(20)):
+                doms = [((random.choice([1, 2, 3]), random.randrange(61), random.randrange(61), random.randrange(61),
+                          random.randrange(3904)), 1, 2) for _ in range(random.choice([1, 1, 2]))]
+                prots.append((doms, 0, 0, True))
+            proteomes.append(prots)
+        n_max = max(len(p) for p in proteomes)
+        kin = _wl_kinetics()
+        kin.increase_max_cells(by_n=n_cells)
+        kin.increase_max_proteins(max_n=n_max)
+        kin.set_cell_params(cell_idxs=list(range(n_cells)), proteomes=proteomes)
+        orig = {k: getattr(kin, k).clone() for k in ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke")}
+        kin.remove_cell_params(keep=torch.full((n_cells,), False))
+        kin.increase_max_cells(by_n=n_cells)
+        kin.increase_max_proteins(max_n=n_max)
+        kin.set_cell_params(cell_idxs=list(range(n_cells)), proteomes=proteomes)
+        for k, t in orig.items():
+            got = getattr(kin, k)
+            assert got.dtype is t.dtype, (i, k)
+            assert torch.equal(got, t), (i, k)
+
+
+def _random_kinetics(X_scale: float, device: str, clamp: bool) -> tuple[ms.Kinetics, torch.Tensor]:
+    n_cells, n_prots, s = 100, 100, 2 * len(WL.molecules)
+    kin = _wl_kinetics(device)
+    N = torch.randint(-8, 9, (n_cells, n_prots, s)).int()
+    kin.N = N
+    kin.Nf = torch.where(N < 0, -N, 0)
+    kin.Nb = torch.where(N > 0, N, 0)
+    v = torch.randn(n_cells, n_prots).abs()
+    kin.Vmax = (v.clamp(max=1.0) if clamp else v) * 100
+    kin.A = torch.randint(-5, 5, (n_cells, n_prots, s)).int()
+    Ke = torch.randn(n_cells, n_prots) * 100
+    lo = 0.001 if clamp else 0.0
+    kmf = torch.randn(n_cells, n_prots).abs().clamp(lo)
+    kin.Kmf = kmf
+    kin.Kmb = (kmf * Ke).clamp(lo) if clamp else kmf * Ke
+    kin.Kmr = torch.randn(n_cells, n_prots, s).abs().clamp(lo)
+    kin.Ke = kin.Kmb / kin.Kmf
+    if device != "cpu":
+        kin._to_device(torch.device(device))
+    X = (torch.randn(n_cells, s).abs().clamp(max=1.0) * X_scale).to(device)
+    return kin, X
+
+
+def _steps(device: str) -> int:
+    # the reference runs 1000 steps; the dense random (100 x 100 x 28) problem costs ~60 ms per step
+    # on the host core, so the CPU run is shortened
+    return 1000 if device != "cpu" else 200
+
+
+def _assert_dtypes(kin):
+    for k in ("N", "Nf", "Nb", "A"):
+        assert getattr(kin, k).dtype is torch.int32, k
+    for k in ("Ke", "Kmf", "Kmb", "Kmr", "Vmax"):
+        assert getattr(kin, k).dtype is torch.float32, k
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_random_kinetics_stay_zero(device):
+    # 0^0 = 1 or exp(log(0)) slips would create signals from nothing
+    kin, X = _random_kinetics(0.0, device, clamp=False)
+    for _ in range(_steps(device)):
+        X = kin.integrate_signals(X=X)
+        assert X.min() == 0.0 and X.max() == 0.0
+    _assert_dtypes(kin)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_random_kinetics_dont_explode(device):
+    # large exponents with many substrates overflow fp32: must clamp instead of producing inf / nan
+    kin, X = _random_kinetics(100.0, device, clamp=True)
+    for _ in range(_steps(device)):
+        X = kin.integrate_signals(X=X)
+        assert not torch.any(X < 0.0)
+        assert not torch.any(X.isnan())
+        assert torch.all(X.isfinite())
+        assert torch.all(X < 10_000)
+    _assert_dtypes(kin)
+
+
+# ----------------------------------------------------------------------------- genetics / mutations
+def test_genomes_are_always_translated_reproduceably():
+    genetics = ms.Genetics()
+    for i in range(100):
+        g = ms.random_genome(s=500)
+        first, *_ = genetics.translate_genomes(genomes=[g])
+        for prot in genetics.translate_genomes(genomes=[g] * 100):
+            assert prot == first, i
+
+
+def test_point_mutations_at_scale():
+    for _ in range(3):
+        # ~1 mutation per genome: a substitution can draw the same nt, so a few stay unchanged
+        genomes = gen_genomes(n=1000, s=10_000)
+        res = muts.point_mutations(seqs=genomes, p=1e-4)
+        assert 0 < len(res) <= len(genomes)
+        assert sum(genomes[i] != d for d, i in res) / len(res) > 0.9
+
+
+def test_recombinations_at_scale():
+    for _ in range(3):
+        genomes = gen_genomes(n=2000, s=5000)
+        pairs = list(zip(genomes, reversed(genomes)))
+        res = muts.recombinations(seq_pairs=pairs, p=1e-6)
+        assert len(res) <= len(genomes)
+        assert all(len(a) + len(b) == len(pairs[i][0]) + len(pairs[i][1]) for a, b, i in res)
+
+
+def test_genome_generation_consistency():
+    mi, mj, mk = ms.Molecule("SLi", 10e3), ms.Molecule("SLj", 10e3), ms.Molecule("SLk", 10e3)
+    world = ms.World(chemistry=ms.Chemistry(molecules=[mi, mj, mk], reactions=[([mi], [mj]), ([mi, mj], [mk])]))
+    retry = Retry(n_allowed_fails=3)
+    fact = ms.GenomeFact(world=world, proteome=[[ms.TransporterDomainFact(molecule=mi, is_exporter=False,
+                                                                          km=1.0, vmax=1.0)]])
+    for i in range(6):
+        with retry.catch_assert(i):
+            (ci,) = world.spawn_cells(genomes=[fact.generate()])
+            cell = world.get_cell(by_idx=ci)
+            # another protein may appear on the reverse complement by chance (hence Retry)
+            assert len(cell.proteome) == 1 and len(cell.proteome[0].domains) == 1
+            d0 = cell.proteome[0].domains[0]
+            assert isinstance(d0, ms.TransporterDomain) and d0.molecule is mi and not d0.is_exporter
+            assert abs(d0.vmax - 1.0) < 1.0 and abs(d0.km - 1.0) < 5.0
+            assert world.kinetics.N[ci][0][0] == 1 and world.kinetics.N[ci][0][3] == -1
+    world.kill_cells(cell_idxs=list(range(world.n_cells)))
+    retry.reset()
+    fact = ms.GenomeFact(world=world, proteome=[[ms.CatalyticDomainFact(reaction=([mj], [mi]), km=1.0, vmax=1.0)]])
+    for i in range(6):
+        with retry.catch_assert(i):
+            (ci,) = world.spawn_cells(genomes=[fact.generate()])
+            prots = world.get_cell(by_idx=ci).proteome
+            assert len(prots) == 1
+            doms = prots[0].domains
+            assert len(doms) == 1 and isinstance(doms[0], ms.CatalyticDomain)
+            d0 = doms[0]
+            # reaction orientation may come out either way; check as a set of sides
+            sides = {tuple(m.name for m in d0.substrates), tuple(m.name for m in d0.products)}
+            assert sides == {("SLj",), ("SLi",)}
+            assert abs(d0.vmax - 1.0) < 1.0 and abs(d0.km - 1.0) < 5.0
