@@ -322,6 +322,30 @@ __global__ void __launch_bounds__(256) permeate_kernel(int c, int m, long long p
   st(q, xe + (di - de));
 }
 
+// ---------------------------------------------------------------- health scan
+// flags |= 1 << shift for a non-finite value, 2 << shift for a negative one, over `planes` planes
+// of `span` values each (plane stride `stride`). One wave ballot per 64 values, one atomic per block.
+template <class T>
+__global__ void __launch_bounds__(256) health_kernel(const T* __restrict__ x, int planes, long long span,
+                                                     long long stride, int shift, int* flags) {
+  __shared__ int blk;
+  if (threadIdx.x == 0) blk = 0;
+  __syncthreads();
+  int f = 0;
+  const long long total = (long long)planes * span;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long pl = i / span;
+    const float v = ld(x + pl * stride + (i - pl * span));
+    f |= (isfinite(v) ? 0 : 1) | (v < 0.0f ? 2 : 0);
+  }
+  if (__ballot(f & 1)) f |= 1;
+  if (__ballot(f & 2)) f |= 2;
+  if ((threadIdx.x & 63) == 0 && f) atomicOr(&blk, f);
+  __syncthreads();
+  if (threadIdx.x == 0 && blk) atomicOr(flags, blk << shift);
+}
+
 // ---------------------------------------------------------------- host launchers
 static MGeom mgeom(int R, int C, int r_lo, int r_hi, int wrap) {
   if (R <= 0 || C <= 0 || r_lo < 0 || r_hi > R || r_lo >= r_hi) throw std::invalid_argument("bad map geometry");
@@ -375,6 +399,15 @@ void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uin
   MS_MAP_DISPATCH(dtype, (diffuse_correct_kernel<T><<<g, 256, 0, S_(stream)>>>(P_<T>(tmp), P_<T>(map),
                                                                                P_<double>(totals), n_pix, plane,
                                                                                start, span, m)));
+  MS_LAUNCH_CHECK();
+}
+
+void health_scan(int planes, long long span, long long stride, uintptr_t x, int dtype, int shift, uintptr_t flags,
+                 uintptr_t stream) {
+  if (planes <= 0 || span <= 0) return;
+  const unsigned g = std::min<long long>(cdiv((long long)planes * span, 256), 4096);
+  MS_MAP_DISPATCH(dtype, (health_kernel<T><<<g, 256, 0, S_(stream)>>>(P_<T>(x), planes, span, stride, shift,
+                                                                        P_<int>(flags))));
   MS_LAUNCH_CHECK();
 }
 

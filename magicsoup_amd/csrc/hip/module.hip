@@ -30,6 +30,8 @@ void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_
 void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t totals,
                      double n_pix, int dtype, uintptr_t stream);
 void scale_planes(int m, long long plane, uintptr_t map, uintptr_t f, int dtype, uintptr_t stream);
+void health_scan(int planes, long long span, long long stride, uintptr_t x, int dtype, int shift, uintptr_t flags,
+                 uintptr_t stream);
 void spill_free(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
                 uintptr_t cell_map, int dtype, uintptr_t stream);
 void spill_free_mask(int n, int m, uintptr_t dead, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
@@ -107,6 +109,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("diffuse_correct", &msd::diffuse_correct);
   m.def("diffuse_partials_len", &msd::diffuse_partials_len);
   m.def("scale_planes", &msd::scale_planes);
+  m.def("health_scan", &msd::health_scan);
   m.def("gather_rows", &msd::gather_rows);
   m.def("neighbor_slots", &msd::neighbor_slots);
   m.def("rec_count_keys", &msd::rec_count_keys);

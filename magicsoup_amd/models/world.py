@@ -21,7 +21,9 @@ MI355X-first design:
 """
 from __future__ import annotations
 
+import functools
 import math
+import os
 import pickle
 import random
 from pathlib import Path
@@ -36,9 +38,45 @@ from magicsoup_amd.models.kinetics import Kinetics
 from magicsoup_amd.models.strings import StringArena, StringColumn, pack_strings
 from magicsoup_amd.ops import world_ops
 from magicsoup_amd.utils.util import randstr
-from magicsoup_amd.utils.profiling import range_push, range_pop
+from magicsoup_amd.utils import profiling
+from magicsoup_amd.utils.profiling import range_pop, range_push
 
 _LABEL_LEN = 12
+_CHECK_ENV = os.environ.get("MS_CHECK_INVARIANTS") == "1"
+
+
+def _op(name: str):
+    """Instrument a public World operation: roctx range (``MS_ROCTX=1``), per-op HIP-event timing
+    (:meth:`World.enable_timings`) and invariant checks after the op (:meth:`World.set_debug_checks`
+    or ``MS_CHECK_INVARIANTS=1``). Only the outermost op of a nested call is timed / checked; with
+    nothing enabled the wrapper is one dict lookup."""
+
+    def deco(fn):
+        @functools.wraps(fn)
+        def wrapper(self, *args, **kwargs):
+            d = self.__dict__
+            timer, check = d.get("_timer"), d.get("_debug_checks", _CHECK_ENV)
+            if timer is None and not check and not profiling.roctx_enabled():
+                return fn(self, *args, **kwargs)
+            depth = d.get("_op_depth", 0)
+            d["_op_depth"] = depth + 1
+            range_push(name)
+            try:
+                if timer is not None and depth == 0:
+                    with timer.phase(name):
+                        out = fn(self, *args, **kwargs)
+                else:
+                    out = fn(self, *args, **kwargs)
+                if check and depth == 0:
+                    self.check_invariants(where=name)
+                return out
+            finally:
+                range_pop()
+                d["_op_depth"] = depth
+
+        return wrapper
+
+    return deco
 
 
 def _diffusion_weights(rate: float) -> tuple[float, float]:
@@ -357,6 +395,7 @@ class World:
         pairs = self.get_neighbors_t(cell_idxs, nghbr_idxs)
         return [tuple(d) for d in pairs.tolist()]
 
+    @_op("get_neighbors")
     def get_neighbors_t(self, cell_idxs, nghbr_idxs=None) -> torch.Tensor:
         """Tensor form of :meth:`get_neighbors`: int32 (k, 2) on the world's device."""
         frm = self._idx_tensor(cell_idxs)
@@ -368,6 +407,7 @@ class World:
         return world_ops.neighbors(self, frm, to)
 
     # ------------------------------------------------------------------ cell lifecycle
+    @_op("spawn_cells")
     def spawn_cells(self, genomes) -> list[int]:
         """Place new cells with ``genomes`` on random free pixels.
 
@@ -377,32 +417,29 @@ class World:
 
         Returns the indices of the new cells.
         """
-        range_push("spawn_cells")
-        try:
-            rows, lens = self._as_packed(genomes)
-            k = int(rows.size(0))
-            if k == 0:
-                return []
-            pos = world_ops.free_positions(self, k)
-            kp = int(pos.size(0))
-            if kp == 0:
-                return []
-            if kp < k:
-                keep = torch.randperm(k, device=rows.device)[:kp]
-                rows, lens = rows[keep], lens[keep]
-                k = kp
-            n0 = self.n_cells
-            self._grow(k)
-            self._genomes.append_packed(rows, lens)
-            self._labels.append_packed(*self._random_labels(k))
-            new = torch.arange(n0, n0 + k, device=self.device)
-            self._place(new, pos)
-            world_ops.pickup_molecules(self, new, pos)
-            self._update_params_rows(new)
-            return list(range(n0, n0 + k))
-        finally:
-            range_pop()
+        rows, lens = self._as_packed(genomes)
+        k = int(rows.size(0))
+        if k == 0:
+            return []
+        pos = world_ops.free_positions(self, k)
+        kp = int(pos.size(0))
+        if kp == 0:
+            return []
+        if kp < k:
+            keep = torch.randperm(k, device=rows.device)[:kp]
+            rows, lens = rows[keep], lens[keep]
+            k = kp
+        n0 = self.n_cells
+        self._grow(k)
+        self._genomes.append_packed(rows, lens)
+        self._labels.append_packed(*self._random_labels(k))
+        new = torch.arange(n0, n0 + k, device=self.device)
+        self._place(new, pos)
+        world_ops.pickup_molecules(self, new, pos)
+        self._update_params_rows(new)
+        return list(range(n0, n0 + k))
 
+    @_op("add_cells")
     def add_cells(self, cells: list[Cell]) -> list[int]:
         """Place :class:`Cell` objects on random free pixels, keeping their genome, label,
         intracellular molecules, lifetime and divisions (no molecule pickup)."""
@@ -441,27 +478,25 @@ class World:
         parents, children = self.divide_cells_t(cell_idxs)
         return list(zip(parents.tolist(), children.tolist()))
 
+    @_op("divide_cells")
     def divide_cells_t(self, cell_idxs) -> tuple[torch.Tensor, torch.Tensor]:
         """Tensor form of :meth:`divide_cells`: (parents, children) long tensors."""
-        range_push("divide_cells")
-        try:
-            idxs = self._idx_tensor(cell_idxs)
-            empty = torch.zeros(0, dtype=torch.long, device=self.device)
-            if idxs.numel() == 0:
-                return empty, empty
-            parents, child_pos = world_ops.divide_placement(self, idxs)
-            k = int(parents.numel())
-            if k == 0:
-                return empty, empty
-            n0 = self.n_cells
-            children = torch.arange(n0, n0 + k, device=self.device)
-            self._clone_rows(parents, children)
-            self._place(children, child_pos)
-            world_ops.split_cells(self, parents, children)
-            return parents, children
-        finally:
-            range_pop()
+        idxs = self._idx_tensor(cell_idxs)
+        empty = torch.zeros(0, dtype=torch.long, device=self.device)
+        if idxs.numel() == 0:
+            return empty, empty
+        parents, child_pos = world_ops.divide_placement(self, idxs)
+        k = int(parents.numel())
+        if k == 0:
+            return empty, empty
+        n0 = self.n_cells
+        children = torch.arange(n0, n0 + k, device=self.device)
+        self._clone_rows(parents, children)
+        self._place(children, child_pos)
+        world_ops.split_cells(self, parents, children)
+        return parents, children
 
+    @_op("update_cells")
     def update_cells(self, genome_idx_pairs: list[tuple[str, int]]):
         """Replace the genomes of existing cells and re-derive their proteomes."""
         if len(genome_idx_pairs) == 0:
@@ -470,32 +505,29 @@ class World:
         self._genomes.set_strings(list(idxs), list(genomes))
         self._update_params_rows(torch.tensor(list(idxs), dtype=torch.long, device=self.device))
 
+    @_op("kill_cells")
     def kill_cells(self, cell_idxs=None):
         """Remove cells; their molecules spill onto their pixel. Remaining cells keep their order
         (indices after a removed cell shift down)."""
-        range_push("kill_cells")
-        try:
-            n = self.n_cells
-            if n == 0:
+        n = self.n_cells
+        if n == 0:
+            return
+        if cell_idxs is None:
+            dead = torch.ones(n, dtype=torch.bool, device=self.device)
+        elif isinstance(cell_idxs, torch.Tensor) and cell_idxs.dtype == torch.bool:
+            dead = cell_idxs.to(self.device)
+        else:
+            t = cell_idxs if isinstance(cell_idxs, torch.Tensor) else torch.tensor(list(cell_idxs), dtype=torch.long)
+            dead = torch.zeros(n, dtype=torch.bool, device=self.device)
+            if t.numel() == 0:
                 return
-            if cell_idxs is None:
-                dead = torch.ones(n, dtype=torch.bool, device=self.device)
-            elif isinstance(cell_idxs, torch.Tensor) and cell_idxs.dtype == torch.bool:
-                dead = cell_idxs.to(self.device)
-            else:
-                t = cell_idxs if isinstance(cell_idxs, torch.Tensor) else torch.tensor(list(cell_idxs), dtype=torch.long)
-                dead = torch.zeros(n, dtype=torch.bool, device=self.device)
-                if t.numel() == 0:
-                    return
-                dead[t.to(self.device, torch.long)] = True  # duplicates are harmless
-            world_ops.spill_and_free_mask(self, dead)
-            keep = ~dead
-            keep_idx = torch.nonzero(keep).flatten()
-            if int(keep_idx.numel()) == n:
-                return
-            self._compact(keep_idx, keep)
-        finally:
-            range_pop()
+            dead[t.to(self.device, torch.long)] = True  # duplicates are harmless
+        world_ops.spill_and_free_mask(self, dead)
+        keep = ~dead
+        keep_idx = torch.nonzero(keep).flatten()
+        if int(keep_idx.numel()) == n:
+            return
+        self._compact(keep_idx, keep)
 
     def _compact(self, keep_idx: torch.Tensor, keep: torch.Tensor) -> None:
         n_new = int(keep_idx.numel())
@@ -525,6 +557,7 @@ class World:
         self._labels.keep(keep_idx)
         self.n_cells = n_new
 
+    @_op("move_cells")
     def move_cells(self, cell_idxs=None):
         """Move cells to a random free pixel of their Moore neighbourhood (if there is one)."""
         if cell_idxs is None:
@@ -539,6 +572,7 @@ class World:
         self.cell_map[old[:, 0], old[:, 1]] = False
         self._place(moved, new_pos)
 
+    @_op("reposition_cells")
     def reposition_cells(self, cell_idxs=None):
         """Move cells to random free pixels anywhere on the map."""
         if cell_idxs is None:
@@ -558,75 +592,65 @@ class World:
         self.cell_map[p[:, 0], p[:, 1]] = True
 
     # ------------------------------------------------------------------ physics
+    @_op("enzymatic_activity")
     def enzymatic_activity(self):
         """Let all proteins of all cells work for one time step (updates ``cell_molecules`` and
         the molecule map pixels under the cells)."""
         if self.n_cells == 0:
             return
-        range_push("enzymatic_activity")
-        try:
-            world_ops.enzymatic_activity(self)
-        finally:
-            range_pop()
+        world_ops.enzymatic_activity(self)
 
+    @_op("diffuse_molecules")
     @torch.no_grad()
     def diffuse_molecules(self):
         """One step of diffusion over the molecule map, then membrane permeation."""
-        range_push("diffuse_molecules")
-        try:
-            world_ops.diffuse(self)
-            if self.n_cells > 0:
-                world_ops.permeate(self)
-        finally:
-            range_pop()
+        world_ops.diffuse(self)
+        if self.n_cells > 0:
+            world_ops.permeate(self)
 
+    @_op("degrade_molecules")
     def degrade_molecules(self):
         """Decay molecules in the map and in cells by one time step (per-species half life)."""
         world_ops.degrade(self)
 
+    @_op("increment_cell_lifetimes")
     def increment_cell_lifetimes(self):
         """Add 1 to every cell's lifetime."""
         self.cell_lifetimes += 1
 
     # ------------------------------------------------------------------ evolution
+    @_op("mutate_cells")
     def mutate_cells(self, cell_idxs: list[int] | None = None, p: float = 1e-6, p_indel: float = 0.4, p_del: float = 0.66):
         """Point mutations (substitutions and indels) with per-bp rate ``p``; proteomes of mutated
         cells are re-derived."""
-        range_push("mutate_cells")
-        try:
-            if self.n_cells == 0:
-                return
-            rows = None if cell_idxs is None else self._idx_tensor(cell_idxs, unique=False)
-            changed = world_ops.point_mutations(self, rows, p, p_indel, p_del)
-            if changed.numel() > 0:
-                self._update_params_rows(changed)
-        finally:
-            range_pop()
+        if self.n_cells == 0:
+            return
+        rows = None if cell_idxs is None else self._idx_tensor(cell_idxs, unique=False)
+        changed = world_ops.point_mutations(self, rows, p, p_indel, p_del)
+        if changed.numel() > 0:
+            self._update_params_rows(changed)
 
+    @_op("recombinate_cells")
     def recombinate_cells(self, cell_idxs: list[int] | None = None, p: float = 1e-7):
         """Recombine the genomes of neighbouring cells (strand breaks with per-bp rate ``p`` and
         random re-joining); both genomes of every recombined pair are replaced."""
-        range_push("recombinate_cells")
-        try:
-            if self.n_cells < 2:
-                return
-            if cell_idxs is None and self._genomes.data.is_cuda:
-                from magicsoup_amd.ops import hip_ops
+        if self.n_cells < 2:
+            return
+        if cell_idxs is None and self._genomes.data.is_cuda:
+            from magicsoup_amd.ops import hip_ops
 
-                changed = hip_ops.recombinate_all(self, p)
+            changed = hip_ops.recombinate_all(self, p)
+        else:
+            if cell_idxs is None:
+                idxs = torch.arange(self.n_cells, device=self.device)
+                pairs = world_ops.neighbors(self, idxs, idxs)
             else:
-                if cell_idxs is None:
-                    idxs = torch.arange(self.n_cells, device=self.device)
-                    pairs = world_ops.neighbors(self, idxs, idxs)
-                else:
-                    pairs = self.get_neighbors_t(cell_idxs)
-                if pairs.size(0) == 0:
-                    return
-                changed = world_ops.recombinations(self, pairs, p)
-            if changed.numel() > 0:
-                self._update_params_rows(changed)
-        finally:
-            range_pop()
+                pairs = self.get_neighbors_t(cell_idxs)
+            if pairs.size(0) == 0:
+                return
+            changed = world_ops.recombinations(self, pairs, p)
+        if changed.numel() > 0:
+            self._update_params_rows(changed)
 
     # ------------------------------------------------------------------ params
     def _update_params_rows(self, rows: torch.Tensor) -> None:
@@ -712,12 +736,14 @@ class World:
                     setattr(mp, name, val.to(dev))
         return self
 
+    @_op("save_state")
     def save_state(self, statedir: Path):
         """Write the current state (tensors + ``cells.fasta``) in the reference's format."""
         from magicsoup_amd.utils.checkpoint import save_state
 
         save_state(self, Path(statedir))
 
+    @_op("load_state")
     def load_state(self, statedir: Path, ignore_cell_params: bool = False):
         """Load a state written by :meth:`save_state` (re-translating genomes unless
         ``ignore_cell_params``)."""
@@ -759,6 +785,76 @@ class World:
 
     def _f32_tensor(self, d: Any) -> torch.Tensor:
         return torch.tensor(d, device=self.device, dtype=torch.float32)
+
+    # ------------------------------------------------------------------ observability
+    def enable_timings(self, sync: bool = False) -> None:
+        """Time every public operation with HIP events (wall clock on CPU); read with
+        :meth:`step_timings`. ``sync=True`` drains the device around each op (exact attribution of
+        a kernel trace, at the cost of serialising host and device)."""
+        from magicsoup_amd.utils.profiling import PhaseTimer
+
+        self.__dict__["_timer"] = PhaseTimer(self.device, sync=sync)
+
+    def disable_timings(self) -> None:
+        self.__dict__.pop("_timer", None)
+
+    def step_timings(self, reset: bool = True) -> dict[str, dict[str, float]]:
+        """``{op: {"ms_total", "ms_mean", "n"}}`` since the last reset (resolves pending events)."""
+        timer = self.__dict__.get("_timer")
+        if timer is None:
+            return {}
+        out = timer.summary()
+        if reset:
+            self.enable_timings(sync=timer.sync)
+        return out
+
+    def set_debug_checks(self, on: bool = True) -> None:
+        """Run :meth:`check_invariants` after every public operation (debug mode; syncs)."""
+        self.__dict__["_debug_checks"] = bool(on)
+
+    def check_invariants(self, where: str = "") -> None:
+        """Raise ``RuntimeError`` if the population state is inconsistent: one cell per occupied
+        pixel, ``cell_map`` matching ``cell_positions``, every per-cell column / string arena /
+        kinetics row count equal to ``n_cells``."""
+        n = self.n_cells
+        R, C, r_lo, r_hi, _ = world_ops.geom(self)
+        problems = []
+        for name in self._cols:
+            if getattr(self, name).size(0) != n:
+                problems.append(f"{name} has {getattr(self, name).size(0)} rows")
+        if len(self.cell_genomes) != n or len(self.cell_labels) != n:
+            problems.append(f"{len(self.cell_genomes)} genomes / {len(self.cell_labels)} labels")
+        if self.kinetics.__dict__.get("_ncells", 0) != n:
+            problems.append(f"kinetics holds {self.kinetics.__dict__.get('_ncells', 0)} cells")
+        pos = self.cell_positions.long()
+        if n:
+            inside = (pos[:, 0] >= r_lo) & (pos[:, 0] < r_hi) & (pos[:, 1] >= 0) & (pos[:, 1] < C)
+            if not bool(inside.all()):
+                problems.append(f"{int((~inside).sum())} positions outside the owned rows")
+            else:
+                if (pos[:, 0] * C + pos[:, 1]).unique().numel() != n:
+                    problems.append("two cells share a pixel")
+                if not bool(self.cell_map[pos[:, 0], pos[:, 1]].all()):
+                    problems.append("cell_map is empty under a cell")
+        occupied = int(self.cell_map[r_lo:r_hi].sum())
+        if occupied != n:
+            problems.append(f"cell_map has {occupied} occupied pixels for {n} cells")
+        if problems:
+            raise RuntimeError(f"World invariants violated{' after ' + where if where else ''}: " + "; ".join(problems))
+
+    def health_flags(self) -> torch.Tensor:
+        """Device int32 flags (no host sync): bit 0 = a non-finite value, bit 1 = a negative value,
+        in the molecule map (bits 0/1) or in ``cell_molecules`` (bits 2/3)."""
+        return world_ops.health_flags(self)
+
+    def check_health(self) -> None:
+        """Raise ``FloatingPointError`` if the molecule map or the cells hold NaN / Inf / negative
+        amounts (one fused pass over the state, one sync)."""
+        f = int(self.health_flags().item())
+        if f:
+            what = [txt for bit, txt in ((1, "non-finite map values"), (2, "negative map values"),
+                                         (4, "non-finite cell molecules"), (8, "negative cell molecules")) if f & bit]
+            raise FloatingPointError("unhealthy world state: " + ", ".join(what))
 
     def __repr__(self) -> str:
         return f"World(map_size:{self.map_size!r},abs_temp:{self.abs_temp!r},device:{self.device!r})"

@@ -217,6 +217,19 @@ def diffuse(world) -> None:
     _m().diffuse_correct(m, R, C, r_lo, r_hi, _p(mm), _p(tmp), _p(totals), n_pix, _mdt(mm), _stream())
 
 
+def health_flags(world) -> torch.Tensor:
+    mm = world.molecule_map
+    R, C, r_lo, r_hi, _ = geom(world)
+    flags = torch.zeros(1, dtype=torch.int32, device=mm.device)
+    m = int(mm.size(0))
+    _m().health_scan(m, (r_hi - r_lo) * C, R * C, _p(mm) + r_lo * C * mm.element_size(), _mdt(mm), 0, _p(flags),
+                     _stream())
+    cm = world.cell_molecules
+    if cm.numel():
+        _m().health_scan(1, cm.numel(), cm.numel(), _p(cm), 0, 2, _p(flags), _stream())
+    return flags[0]
+
+
 def permeate(world) -> None:
     mm = world.molecule_map
     _ensure_world_layout(world)

@@ -260,6 +260,22 @@ def degrade(world) -> None:
         world.cell_molecules[:] = world.cell_molecules * f
 
 
+def health_flags(world) -> torch.Tensor:
+    """int32 flags: 1 non-finite / 2 negative map value (owned rows), 4 / 8 the same for cells."""
+    mm = _molmap(world)
+    if mm.is_cuda:
+        return _hip().health_flags(world)
+    _, _, r_lo, r_hi, _ = geom(world)
+    own = mm[:, r_lo:r_hi]
+    cm = world.cell_molecules
+    f = 0
+    f |= 1 if not bool(torch.isfinite(own).all()) else 0
+    f |= 2 if bool((own < 0).any()) else 0
+    f |= 4 if not bool(torch.isfinite(cm).all()) else 0
+    f |= 8 if bool((cm < 0).any()) else 0
+    return torch.tensor(f, dtype=torch.int32)
+
+
 # ---------------------------------------------------------------------------- genomes
 def translate(world, data: torch.Tensor, lens: torch.Tensor, rows: torch.Tensor):
     """Dense tokens (k, P, D, 5) int32 and protein counts (k,) for arena rows ``rows``."""

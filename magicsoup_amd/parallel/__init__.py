@@ -1,4 +1,10 @@
-"""Multi-GPU execution: a domain-decomposed World over torch.distributed (RCCL over xGMI)."""
-from magicsoup_amd.parallel.dist_world import DistributedWorld
+"""Multi-GPU execution over torch.distributed (RCCL over xGMI).
 
-__all__ = ["DistributedWorld"]
+* :class:`DistributedWorld` -- one world domain-decomposed into row strips, one strip per rank
+  (halo exchange, cell migration, global reductions).
+* :class:`Ensemble` -- independent replicate worlds, one per rank (no communication in the step).
+"""
+from magicsoup_amd.parallel.dist_world import DistributedWorld
+from magicsoup_amd.parallel.ensemble import Ensemble
+
+__all__ = ["DistributedWorld", "Ensemble"]

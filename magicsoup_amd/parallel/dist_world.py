@@ -33,6 +33,7 @@ import copy
 import random
 from pathlib import Path
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -79,12 +80,18 @@ class DistributedWorld(World):
     multiple of the number of ranks with at least 2 rows per rank). Every rank must call every
     method collectively (same order, same arguments apart from local cell indices).
 
+    ``exact_global_exit`` (default True) keeps the reference's integrator semantics exactly: the
+    equilibrium-damping early exit is decided over ALL cells of the job (kinetics.py:846), which costs
+    one tiny MAX all-reduce per damping iteration (up to 12 per step). ``False`` lets every rank decide
+    for its own cells (one fused integrator launch, no collectives; results then differ from a
+    single-process world only where one rank would stop iterating while another continues).
+
     Local state (``cell_positions`` in local rows ``1..H``, ``molecule_map`` / ``cell_map`` with
     halo rows) is what the kernels work on; :meth:`global_positions`, :meth:`owned_molecule_map`,
     :meth:`gather` and :meth:`scatter_from` convert to and from the global picture.
     """
 
-    def __init__(self, *args, group=None, **kwargs):
+    def __init__(self, *args, group=None, exact_global_exit: bool = True, **kwargs):
         if not dist.is_initialized():
             raise RuntimeError("DistributedWorld needs an initialised torch.distributed process group")
         g = self.__dict__
@@ -119,7 +126,8 @@ class DistributedWorld(World):
             # hooks the op layer calls (World has them as None): halo refresh before the diffusion
             # stencil, MAX of the integrator's iteration flags, SUM of the diffusion mass totals
             g["_exchange_map_halo"] = self._do_exchange_map_halo
-            g["_allreduce_flags"] = self._do_allreduce_flags
+            if exact_global_exit:
+                g["_allreduce_flags"] = self._do_allreduce_flags
             g["_allreduce_totals"] = self._do_allreduce_totals
             self._exchange_occupancy()  # first p2p call is collective on every rank
             self._do_exchange_map_halo()
@@ -577,6 +585,41 @@ class DistributedWorld(World):
                 self._update_params_rows(new)
         if self.world_size > 1:
             self._do_exchange_map_halo()
+
+    # ------------------------------------------------------------------ global index space
+    def _gather_ints(self, v: int) -> list[int]:
+        t = torch.zeros(self.world_size, dtype=torch.int64)
+        t[self.rank] = int(v)
+        t = t.to(self._tensor_device()) if not self._stage else t
+        self._all_reduce(t, dist.ReduceOp.SUM)
+        return [int(x) for x in t.cpu().tolist()]
+
+    def n_cells_global(self) -> int:
+        """Collective: number of cells over all ranks."""
+        return sum(self._gather_ints(self.n_cells))
+
+    def global_index_offset(self) -> int:
+        """Collective: global index of this rank's local cell 0 (cells are numbered rank by rank)."""
+        return sum(self._gather_ints(self.n_cells)[: self.rank])
+
+    def spawn_cells_global(self, genomes: list[str]) -> list[int]:
+        """Collective; every rank passes the same ``genomes``. Places them uniformly over the free
+        pixels of the WHOLE map (reference world.py:287-341 semantics on the global torus): the
+        number landing on each rank is a multivariate-hypergeometric draw over the ranks' free pixel
+        counts (shared seed, identical on every rank), each rank then spawns its share uniformly in
+        its strip. More genomes than free pixels: a random subset is kept. Returns the local
+        indices of the cells this rank received."""
+        free = self._gather_ints(self.H * self.map_size - self.n_cells)
+        seed = [random.getrandbits(63) if self.rank == 0 else 0]
+        dist.broadcast_object_list(seed, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0,
+                                   group=self.group)
+        rng = np.random.default_rng(seed[0])
+        n = min(len(genomes), sum(free))
+        order = rng.permutation(len(genomes))[:n]
+        counts = rng.multivariate_hypergeometric(np.asarray(free, dtype=np.int64), n) if n else [0] * len(free)
+        lo = int(np.sum(counts[: self.rank]))
+        mine = [genomes[int(i)] for i in order[lo : lo + int(counts[self.rank])]]
+        return self.spawn_cells(mine) if mine else []
 
     def kill_cells_local_all(self) -> None:
         """Remove every local cell without spilling molecules (state reset)."""

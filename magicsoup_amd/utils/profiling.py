@@ -26,6 +26,10 @@ if os.environ.get("MS_ROCTX") == "1":
             _roctx = None
 
 
+def roctx_enabled() -> bool:
+    return _roctx is not None
+
+
 def range_push(name: str) -> None:
     if _roctx is not None:
         _roctx.roctxRangePushA(name.encode())

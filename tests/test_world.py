@@ -412,3 +412,25 @@ def test_save_and_from_file_world_object():
         assert torch.equal(w2.kinetics.N, w.kinetics.N)
         assert torch.equal(w2.kinetics.Vmax, w.kinetics.Vmax)
         w2.enzymatic_activity()  # usable after restore
+
+
+def test_load_without_then_with_cell_params(tmp_path):
+    # reference quirk 8: a load with ignore_cell_params must still leave kinetics with
+    # exactly one row per cell so that a later full load replaces cleanly
+    mi, mj = ms.Molecule("LWi", 10e3), ms.Molecule("LWj", 20e3)
+    chem = ms.Chemistry(molecules=[mi, mj], reactions=[([mi], [mj])])
+    world = ms.World(chemistry=chem, map_size=7)
+    world.spawn_cells(genomes=[ms.random_genome(s=500) for _ in range(3)])
+    world.save_state(statedir=tmp_path / "s0")
+    world.spawn_cells(genomes=[ms.random_genome(s=500) for _ in range(3)])
+    world.save_state(statedir=tmp_path / "s1")
+    assert world.n_cells == 6 and world.kinetics.N.size(0) == 6
+
+    world = ms.World(chemistry=chem, map_size=7)
+    world.load_state(statedir=tmp_path / "s0", ignore_cell_params=True)
+    assert world.n_cells == 3 and len(world.cell_genomes) == 3
+    assert world.kinetics.N.size(0) == 3
+    world.load_state(statedir=tmp_path / "s1")
+    assert world.n_cells == 6 and len(world.cell_genomes) == 6
+    assert world.kinetics.N.size(0) == 6
+    assert int(world.cell_map.sum()) == 6
