@@ -25,21 +25,17 @@ constexpr int kBlock = 256;
 constexpr int kNarrowP = 12;  // LDS protein slots of the narrow integrator launch
 
 struct IntegrateArgs {
-  int c, P, s, m, R, C;
-  const int32_t *N, *Nf, *Nb, *A;
-  const float *Kmr, *Kmf, *Kmb, *Vmax, *Ke;
-  const float* cell_mols;     // (c, m)       part 0 source
-  const void* molmap;         // (m, R, C)    part 0 source (storage type map_dtype)
-  int map_dtype;
-  const int32_t* positions;   // (c, 2)       part 0 source
-  const float* snap_prev;     // (c, kSnap, s) previous part's candidates (part > 0)
+  int c, P, s;
+  const int32_t* W;           // (rows, P, s) packed int8x4 stoichiometry words (N, Nf, Nb, A)
+  const float4* Q;            // (rows, P)    (Vmax, Kmf, Kmb, Ke)
+  const float* Kmr;           // (rows, P, s)
+  const float* snap_prev;     // (c, kSnap, s) previous part's candidates (part 0: the gathered X)
   const unsigned* mask_prev;  // previous part's 4 iteration flags
   int n_iters_prev;
   float* snap_out;            // (c, kSnap, s)
   unsigned* mask_out;         // this part's 4 iteration flags (0/1, MAX-reducible across ranks)
   float trim;
   int n_iters;
-  int* overflow;              // set if a stoichiometry does not fit in int8
   int slot_words;             // LDS words per cell slot
   int sp;                     // padded LDS row stride (odd)
   const int64_t* prow;        // cell -> parameter storage row (nullptr: identity)
@@ -92,19 +88,11 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
   int* nnz = na_p + 1;                                       // (Ps,) non-zero signals per protein
   uint8_t* nzj = reinterpret_cast<uint8_t*>(nnz + Ps);        // (Ps, s) their indices
 
-  // ---- 1. load X0 (part 0: gather cell + pixel molecules; else: selected previous candidate)
+  // ---- 1. load X0: the selected candidate of the previous part (part 0: the gathered X)
   if (valid) {
-    if (a.snap_prev == nullptr) {
-      const int px = a.positions[2 * cell], py = a.positions[2 * cell + 1];
-      const size_t pix = (size_t)px * a.C + py, plane = (size_t)a.R * a.C;
-      for (int j = lane; j < s; j += G)
-        X0[j] = j < a.m ? a.cell_mols[(size_t)cell * a.m + j]
-                        : ld_map(a.molmap, (size_t)(j - a.m) * plane + pix, a.map_dtype);
-    } else {
-      const int k = stop_iter(a.mask_prev, a.n_iters_prev);
-      const float* src = a.snap_prev + ((size_t)cell * ms::kSnap + k) * s;
-      for (int j = lane; j < s; j += G) X0[j] = src[j];
-    }
+    const int k = stop_iter(a.mask_prev, a.n_iters_prev);
+    const float* src = a.snap_prev + ((size_t)cell * ms::kSnap + k) * s;
+    for (int j = lane; j < s; j += G) X0[j] = src[j];
   }
 
   // ---- 2. compact active proteins (Vmax' != 0) in ascending order with a ballot prefix
@@ -113,12 +101,10 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
     int na = 0;
     for (int p0 = 0; p0 < P; p0 += G) {
       const int p = p0 + lane;
-      float vm = 0.0f;
-      bool on = false;
-      if (valid && p < P) {
-        vm = a.Vmax[prow * P + p] * a.trim;
-        on = !(vm <= 0.0f);  // NaN stays active (propagates like the reference)
-      }
+      float4 q = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (valid && p < P) q = a.Q[prow * P + p];
+      const float vm = q.x * a.trim;
+      const bool on = valid && p < P && !(vm <= 0.0f);  // NaN stays active (propagates like the reference)
       const unsigned long long bal = __ballot(on);
       unsigned long long gm;
       if constexpr (G == 64) gm = bal;
@@ -127,10 +113,9 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
       if (on && na + rank < Ps) {
         const int k = na + rank;
         act[k] = p;
-        const size_t o = prow * P + p;
-        kmf[k] = a.Kmf[o];
-        kmb[k] = a.Kmb[o];
-        ke[k] = a.Ke[o];
+        kmf[k] = q.y;
+        kmb[k] = q.z;
+        ke[k] = q.w;
         V[k] = vm > 0.0f || vm != vm ? vm : 0.0f;  // temporarily holds Vmax'
       }
       na += __popcll(gm);
@@ -140,13 +125,27 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
   wave_lds_sync();
   const int na = valid ? *na_p : 0;
 
-  // ---- 3. stage packed stoichiometry rows of the active proteins
-  for (int idx = lane; idx < na * s; idx += G) {
-    const int k = idx / s, j = idx - k * s;
-    const size_t o = (prow * P + act[k]) * s + j;
-    const int n = a.N[o], nf = a.Nf[o], nb = a.Nb[o], aa = a.A[o];
-    if (n < -128 || n > 127 || nf > 255 || nb > 255 || nf < 0 || nb < 0 || aa < -128 || aa > 127) atomicOr(a.overflow, 1);
-    words[k * SP + j] = (n & 0xFF) | ((nf & 0xFF) << 8) | ((nb & 0xFF) << 16) | ((aa & 0xFF) << 24);
+  // ---- 3. stage the packed stoichiometry rows of the active proteins: 8 independent loads per
+  //         lane in flight per batch (one batch covers na * s <= 8 G words, i.e. most cells)
+  for (int base = 0; base < na * s; base += 8 * G) {
+    int w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int idx = base + u * G + lane;
+      w[u] = 0;
+      if (idx < na * s) {
+        const int k = idx / s, j = idx - k * s;
+        w[u] = a.W[(prow * P + act[k]) * s + j];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int idx = base + u * G + lane;
+      if (idx < na * s) {
+        const int k = idx / s, j = idx - k * s;
+        words[k * SP + j] = w[u];
+      }
+    }
   }
   wave_lds_sync();
   for (int k = lane; k < na; k += G) {
@@ -306,24 +305,33 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
     wave_lds_sync();
   }
 
-  // ---- 9. one mask OR per wavefront
+  // ---- 9. OR the "still correcting" bits: wave -> block -> at most one atomic per block and bit,
+  //         skipped once the flag is set (tens of thousands of same-address atomics would serialise
+  //         in one L2 channel)
+  __shared__ unsigned wave_bits[kBlock / 64];
   for (int o = 32; o > 0; o >>= 1) bits |= __shfl_xor(bits, o);
-  if ((threadIdx.x & 63) == 0 && bits)
+  if ((threadIdx.x & 63) == 0) wave_bits[threadIdx.x >> 6] = bits;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned b = 0u;
+    for (int w = 0; w < (int)(blockDim.x + 63) / 64; ++w) b |= wave_bits[w];
     for (int it = 0; it < ms::kEqIters; ++it)
-      if (bits & (1u << it)) atomicOr(a.mask_out + it, 1u);
+      if ((b & (1u << it)) && __hip_atomic_load(a.mask_out + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+        atomicOr(a.mask_out + it, 1u);
+  }
 }
 
 // Split the cells by their number of active proteins (Vmax > 0 or NaN; the same set for every part
 // since all trims are positive): cells with at most `pn` go to the narrow list (small LDS slots,
 // high occupancy), the others to the wide list (slots for all P proteins). List order does not
 // matter: cells are independent and the iteration flags are OR-reduced.
-__global__ void __launch_bounds__(256) bin_cells_kernel(int c, int P, int pn, const float* Vmax, const int64_t* prow,
+__global__ void __launch_bounds__(256) bin_cells_kernel(int c, int P, int pn, const float4* Q, const int64_t* prow,
                                                         int32_t* lists, int32_t* counts) {
   const int cell = blockIdx.x * blockDim.x + threadIdx.x;
   if (cell >= c) return;
   const size_t r = prow ? (size_t)prow[cell] : (size_t)cell;
   int na = 0;
-  for (int p = 0; p < P; ++p) na += !(Vmax[r * P + p] <= 0.0f);
+  for (int p = 0; p < P; ++p) na += !(Q[r * P + p].x <= 0.0f);
   if (na <= pn) lists[atomicAdd(counts, 1)] = cell;
   else lists[c + atomicAdd(counts + 1, 1)] = cell;
 }
@@ -358,6 +366,46 @@ __global__ void load_x_kernel(int c, int s, const float* X, float* snap) {
   snap[(size_t)cell * ms::kSnap * s + j] = X[t];
 }
 
+// Part 0 input: X = (cell molecules | molecules of the cell's pixel) -> candidate 0 of `snap`.
+// A flat, full-occupancy gather, so the random pixel reads (one per species plane) are not on the
+// LDS-limited integrator's critical path.
+__global__ void __launch_bounds__(kBlock) gather_x_kernel(int c, int s, int m, int R, int C, const float* cell_mols,
+                                                          const void* molmap, int map_dtype, const int32_t* positions,
+                                                          float* snap) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)c * s) return;
+  const int cell = (int)(t / s), j = (int)(t - (long long)cell * s);
+  float x;
+  if (j < m) {
+    x = cell_mols[(size_t)cell * m + j];
+  } else {
+    const size_t pix = (size_t)positions[2 * cell] * C + positions[2 * cell + 1];
+    x = ld_map(molmap, (size_t)(j - m) * R * C + pix, map_dtype);
+  }
+  snap[(size_t)cell * ms::kSnap * s + j] = x;
+}
+
+__device__ __forceinline__ int pack_word(int n, int nf, int nb, int av, int* overflow) {
+  if (n < -128 || n > 127 || nf < 0 || nf > 255 || nb < 0 || nb > 255 || av < -128 || av > 127) atomicOr(overflow, 1);
+  return (n & 0xFF) | ((nf & 0xFF) << 8) | ((nb & 0xFF) << 16) | ((av & 0xFF) << 24);
+}
+
+// Integrator layout of the parameters: W (rows, P, s) int8x4 words, Q (rows, P) float4. Rebuilt
+// from the API tensors after they were written from the host side; the fused parameter build
+// writes both layouts directly.
+__global__ void __launch_bounds__(kBlock) pack_params_kernel(long long items, int s, const int32_t* N,
+                                                             const int32_t* Nf, const int32_t* Nb, const int32_t* A,
+                                                             const float* Vmax, const float* Kmf, const float* Kmb,
+                                                             const float* Ke, int32_t* W, float4* Q, int* overflow) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= items * s) return;
+  W[t] = pack_word(N[t], Nf[t], Nb[t], A[t], overflow);
+  if (t % s == 0) {
+    const long long o = t / s;
+    Q[o] = make_float4(Vmax[o], Kmf[o], Kmb[o], Ke[o]);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Parameter build: one thread per (row, protein slot). Semantics in kinetics_host.cpp.
 struct BuildArgs {
@@ -372,6 +420,9 @@ struct BuildArgs {
   float abs_temp, gas;
   int32_t *N, *Nf, *Nb, *A;
   float *Kmr, *Kmf, *Kmb, *Vmax, *Ke;
+  int32_t* W;  // integrator layout (optional: nullptr skips it)
+  float4* Q;
+  int* overflow;
 };
 
 __device__ __forceinline__ int lut(int t, int lim) { return (t >= 0 && t < lim) ? t : 0; }
@@ -397,12 +448,14 @@ __global__ void __launch_bounds__(kBlock) build_params_kernel(BuildArgs b) {
       b.Nb[o3 + j] = 0;
       b.A[o3 + j] = 0;
       b.Kmr[o3 + j] = 0.0f;
+      if (b.W) b.W[o3 + j] = 0;
     }
     if (lane == 0) {
       b.Ke[o2] = 0.0f;
       b.Kmf[o2] = 0.0f;
       b.Kmb[o2] = 0.0f;
       b.Vmax[o2] = 0.0f;
+      if (b.Q) b.Q[o2] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     return;
   }
@@ -440,6 +493,7 @@ __global__ void __launch_bounds__(kBlock) build_params_kernel(BuildArgs b) {
     b.Nf[o3 + j] = nf;
     b.Nb[o3 + j] = nb;
     b.A[o3 + j] = av;
+    if (b.W) b.W[o3 + j] = pack_word(n, nf, nb, av, b.overflow);
     b.Kmr[o3 + j] = powf(kc > 0 ? ks / (float)kc : 0.0f, (float)av);
     E += (double)n * (double)b.energies[j];
   }
@@ -457,10 +511,14 @@ __global__ void __launch_bounds__(kBlock) build_params_kernel(BuildArgs b) {
   const float kmn = km.value0();
   float kmfv = kev >= 1.0f ? kmn : kmn / kev;
   float kmbv = kev >= 1.0f ? kmn * kev : kmn;
+  kmfv = kmfv < ms::kEps ? ms::kEps : (kmfv > ms::kMax ? ms::kMax : kmfv);
+  kmbv = kmbv < ms::kEps ? ms::kEps : (kmbv > ms::kMax ? ms::kMax : kmbv);
+  const float vmv = vm.value0();
   b.Ke[o2] = kev;
-  b.Kmf[o2] = kmfv < ms::kEps ? ms::kEps : (kmfv > ms::kMax ? ms::kMax : kmfv);
-  b.Kmb[o2] = kmbv < ms::kEps ? ms::kEps : (kmbv > ms::kMax ? ms::kMax : kmbv);
-  b.Vmax[o2] = vm.value0();
+  b.Kmf[o2] = kmfv;
+  b.Kmb[o2] = kmbv;
+  b.Vmax[o2] = vmv;
+  if (b.Q) b.Q[o2] = make_float4(vmv, kmfv, kmbv, kev);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -476,11 +534,10 @@ static int slot_words_for(int P, int s, int sp) {
 // otherwise gather from / scatter to the world state (cell_mols, molmap, positions). `masks` holds
 // 4 flags per part plus a zero block; the caller may all-reduce (MAX) a part's flags across ranks
 // between launches for the reference's global early exit over a domain-decomposed population.
-void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t Nf, uintptr_t Nb, uintptr_t A,
-               uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb, uintptr_t Vmax, uintptr_t Ke, uintptr_t cell_mols,
+void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q, uintptr_t Kmr, uintptr_t cell_mols,
                uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
-               uintptr_t masks, uintptr_t overflow, const std::vector<float>& trims, int n_iters, int part_begin,
-               int part_end, bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t stream) {
+               uintptr_t masks, const std::vector<float>& trims, int n_iters, int part_begin, int part_end,
+               bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t stream) {
   if (c <= 0) return;
   if (n_iters < 0 || n_iters > ms::kEqIters) throw std::invalid_argument("n_iters must be in 0..4");
   const int nparts = (int)trims.size();
@@ -491,10 +548,15 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t 
   float* snaps[2] = {P_<float>(snap_a), P_<float>(snap_b)};
   if (part_begin == 0) {
     MS_HIP_CHECK(hipMemsetAsync(mk, 0, sizeof(unsigned) * ms::kEqIters * (nparts + 1), st));
-    if (X_io) {  // explicit X: stage it as candidate 0 of snap_b, selected through the zero flags
+    // part 0 input -> candidate 0 of snap_b, selected through the zero flags
+    if (X_io) {
       load_x_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(c, s, P_<float>(X_io), snaps[1]);
-      MS_LAUNCH_CHECK();
+    } else {
+      gather_x_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(c, s, m, R, C, P_<float>(cell_mols),
+                                                                          P_<void>(molmap), map_dtype,
+                                                                          P_<int32_t>(positions), snaps[1]);
     }
+    MS_LAUNCH_CHECK();
   }
   const int G = s <= 32 ? 32 : 64;
   const int sp = (s % 2 == 0) ? s + 1 : s;
@@ -504,7 +566,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t 
   int32_t* cnt = lst ? lst + 2 * (size_t)c : nullptr;
   if (binned && part_begin == 0) {
     MS_HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), st));
-    bin_cells_kernel<<<cdiv(c, 256), 256, 0, st>>>(c, P, kNarrowP, P_<float>(Vmax), prow ? P_<int64_t>(prow) : nullptr,
+    bin_cells_kernel<<<cdiv(c, 256), 256, 0, st>>>(c, P, kNarrowP, P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr,
                                                    lst, cnt);
     MS_LAUNCH_CHECK();
   }
@@ -533,28 +595,20 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t 
       const int threads = cps * G;
       const unsigned grid = cdiv(c, cps);
       IntegrateArgs a{};
-      a.c = c; a.P = P; a.s = s; a.m = m; a.R = R; a.C = C;
-      a.N = P_<int32_t>(N); a.Nf = P_<int32_t>(Nf); a.Nb = P_<int32_t>(Nb); a.A = P_<int32_t>(A);
-      a.Kmr = P_<float>(Kmr); a.Kmf = P_<float>(Kmf); a.Kmb = P_<float>(Kmb); a.Vmax = P_<float>(Vmax);
-      a.Ke = P_<float>(Ke);
-      a.cell_mols = P_<float>(cell_mols); a.molmap = P_<void>(molmap); a.positions = P_<int32_t>(positions);
-      a.map_dtype = map_dtype;
-      if (part == 0 && !X_io) {
-        a.snap_prev = nullptr;
-      } else if (part == 0) {
+      a.c = c; a.P = P; a.s = s;
+      a.W = P_<int32_t>(W); a.Q = P_<float4>(Q); a.Kmr = P_<float>(Kmr);
+      if (part == 0) {
         a.snap_prev = snaps[1];
         a.mask_prev = zero_flags;
-        a.n_iters_prev = n_iters;
       } else {
         a.snap_prev = snaps[(part - 1) & 1];
         a.mask_prev = mk + ms::kEqIters * (part - 1);
-        a.n_iters_prev = n_iters;
       }
+      a.n_iters_prev = n_iters;
       a.snap_out = snaps[part & 1];
       a.mask_out = mk + ms::kEqIters * part;
       a.trim = trims[part];
       a.n_iters = n_iters;
-      a.overflow = P_<int>(overflow);
       a.slot_words = slot_words;
       a.sp = sp;
       a.prow = prow ? P_<int64_t>(prow) : nullptr;
@@ -577,12 +631,24 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t 
   }
 }
 
+void pack_params(long long items, int s, uintptr_t N, uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Vmax,
+                 uintptr_t Kmf, uintptr_t Kmb, uintptr_t Ke, uintptr_t W, uintptr_t Q, uintptr_t overflow,
+                 uintptr_t stream) {
+  if (items <= 0 || s <= 0) return;
+  pack_params_kernel<<<cdiv(items * s, kBlock), kBlock, 0, S_(stream)>>>(
+      items, s, P_<int32_t>(N), P_<int32_t>(Nf), P_<int32_t>(Nb), P_<int32_t>(A), P_<float>(Vmax), P_<float>(Kmf),
+      P_<float>(Kmb), P_<float>(Ke), P_<int32_t>(W), P_<float4>(Q), P_<int>(overflow));
+  MS_LAUNCH_CHECK();
+}
+
 void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_t rows, uintptr_t vmax_w, int nw,
                   uintptr_t km_w, int nk, uintptr_t signs, int nsg, uintptr_t hills, int nh, uintptr_t RM,
                   uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
                   uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
-                  uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t stream) {
+                  uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t W, uintptr_t Q, uintptr_t overflow,
+                  uintptr_t stream) {
   if (n <= 0 || Pt <= 0) return;
+  if ((W == 0) != (Q == 0) || (W != 0 && overflow == 0)) throw std::invalid_argument("build_params: W, Q, overflow");
   if (P > Pt) throw std::invalid_argument("build_params: token proteins exceed parameter capacity");
   BuildArgs b{};
   b.n = n; b.P = P; b.D = D; b.Pt = Pt; b.s = s;
@@ -595,6 +661,7 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
   b.energies = P_<float>(energies); b.abs_temp = abs_temp; b.gas = gas;
   b.N = P_<int32_t>(N); b.Nf = P_<int32_t>(Nf); b.Nb = P_<int32_t>(Nb); b.A = P_<int32_t>(A);
   b.Kmr = P_<float>(Kmr); b.Kmf = P_<float>(Kmf); b.Kmb = P_<float>(Kmb); b.Vmax = P_<float>(Vmax); b.Ke = P_<float>(Ke);
+  b.W = W ? P_<int32_t>(W) : nullptr; b.Q = Q ? P_<float4>(Q) : nullptr; b.overflow = P_<int>(overflow);
   const long long groups = (long long)n * Pt;
   if (s <= 32) build_params_kernel<32><<<cdiv(groups * 32, kBlock), kBlock, 0, S_(stream)>>>(b);
   else build_params_kernel<64><<<cdiv(groups * 64, kBlock), kBlock, 0, S_(stream)>>>(b);

@@ -44,16 +44,18 @@ void gather_rows(int n, uintptr_t src_rows, uintptr_t dst_rows,
                  const std::vector<std::tuple<uintptr_t, uintptr_t, long long, long long, long long>>& descs,
                  uintptr_t stream);
 // kinetics.hip
-void integrate(int c, int P, int s, int m, int R, int C, uintptr_t N, uintptr_t Nf, uintptr_t Nb, uintptr_t A,
-               uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb, uintptr_t Vmax, uintptr_t Ke, uintptr_t cell_mols,
+void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q, uintptr_t Kmr, uintptr_t cell_mols,
                uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
-               uintptr_t masks, uintptr_t overflow, const std::vector<float>& trims, int n_iters, int part_begin,
-               int part_end, bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t stream);
+               uintptr_t masks, const std::vector<float>& trims, int n_iters, int part_begin, int part_end,
+               bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t stream);
 void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_t rows, uintptr_t vmax_w, int nw,
                   uintptr_t km_w, int nk, uintptr_t signs, int nsg, uintptr_t hills, int nh, uintptr_t RM,
                   uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
                   uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
-                  uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t stream);
+                  uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t W, uintptr_t Q, uintptr_t overflow, uintptr_t stream);
+void pack_params(long long items, int s, uintptr_t N, uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Vmax,
+                 uintptr_t Kmf, uintptr_t Kmb, uintptr_t Ke, uintptr_t W, uintptr_t Q, uintptr_t overflow,
+                 uintptr_t stream);
 // world.hip
 void claim_free(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uint64_t seed, uint64_t call,
                 int attempts, uintptr_t out, uintptr_t stream);
@@ -105,6 +107,7 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("integrate", &msd::integrate);
   m.def("build_params", &msd::build_params);
+  m.def("pack_params", &msd::pack_params);
   m.def("diffuse_stencil", &msd::diffuse_stencil);
   m.def("diffuse_correct", &msd::diffuse_correct);
   m.def("diffuse_partials_len", &msd::diffuse_partials_len);

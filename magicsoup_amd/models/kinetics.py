@@ -19,6 +19,7 @@ against, and they run when a subclass overrides them (e.g. to switch stages off 
 from __future__ import annotations
 
 import math
+import weakref
 import random
 from typing import Any
 
@@ -205,6 +206,10 @@ class _RegulatoryMapFact(_VectorMapFact):
 
 _PARAMS = ("Ke", "Kmf", "Kmb", "Kmr", "Vmax", "N", "Nf", "Nb", "A")
 _I32_PARAMS = ("N", "Nf", "Nb", "A")
+# integrator layout (GPU): "_W" (rows, P, s) packed int8x4 (N, Nf, Nb, A) words, "_Q" (rows, P, 4)
+# (Vmax, Kmf, Kmb, Ke); derived from these API tensors, kept in the same row storage
+_PACK_SRC = ("N", "Nf", "Nb", "A", "Vmax", "Kmf", "Kmb", "Ke")
+_PACKED = ("_W", "_Q")
 
 
 class Kinetics:
@@ -352,8 +357,10 @@ class Kinetics:
         if isinstance(cell_idxs, list) and len(cell_idxs) == 0:
             return
         rows = self._rows(cell_idxs)
+        ok = self._pack_ok()
         for t in self._store.values():
-            t[rows] = 0
+            t[rows] = 0  # packed words 0 and Q = 0 match all-zero parameters
+        self._restamp(ok)
 
     def copy_cell_params(self, from_idxs, to_idxs):
         """Copy the parameters of cells ``from_idxs`` to cells ``to_idxs``."""
@@ -367,8 +374,10 @@ class Kinetics:
             hip_ops.gather_rows([(t, t) for t in store.values()], int(fr.numel()), src_rows=fr, dst_rows=to)
             return
         fr, to = self._rows(from_idxs), self._rows(to_idxs)
+        ok = self._pack_ok()
         for t in store.values():
             t[to] = t[fr]
+        self._restamp(ok)
 
     # ---- parameter storage ----
     # The parameters live in row-storage tensors with spare capacity; cell i's row is _slot[i]
@@ -396,6 +405,7 @@ class Kinetics:
         if "_store_d" not in d:
             d["_store_d"], d["_slot"], d["_ncells"], d["_nrows"] = {}, None, 0, 0
         self._materialize()
+        self._drop_packed()
         t = torch.as_tensor(value)
         if not t.is_contiguous():
             t = t.contiguous()
@@ -417,10 +427,54 @@ class Kinetics:
         """Storage tensors in kernel layout (contiguous int32 / float32), rows = capacity."""
         store = self._store
         for name, t in list(store.items()):
-            want = torch.int32 if name in _I32_PARAMS else torch.float32
+            want = torch.int32 if (name in _I32_PARAMS or name == "_W") else torch.float32
             if t.dtype != want or not t.is_contiguous():
                 self._materialize()
                 store[name] = store[name].to(want).contiguous()
+        return store
+
+    # ---- integrator layout (GPU) ----
+    # "_W" / "_Q" are rebuilt from the API tensors whenever those were replaced or modified from
+    # Python (detected through tensor identity + version counter); the GPU parameter build writes
+    # both layouts, and every row operation below moves them together with the API tensors.
+    def _pack_stamp(self):
+        store = self.__dict__.get("_store_d", {})
+        return tuple((weakref.ref(store[k]), store[k]._version) for k in _PACK_SRC if k in store)
+
+    def _pack_ok(self) -> bool:
+        d = self.__dict__
+        st = d.get("_packed_stamp")
+        store = d.get("_store_d", {})
+        if st is None or any(k not in store for k in _PACKED) or len(st) != len(_PACK_SRC):
+            return False
+        return all(ref() is store[k] and ver == store[k]._version for (ref, ver), k in zip(st, _PACK_SRC))
+
+    def _restamp(self, ok: bool) -> None:
+        """Mark the packed layout current after an op that moved it together with the sources."""
+        if ok:
+            self.__dict__["_packed_stamp"] = self._pack_stamp()
+
+    def _drop_packed(self) -> None:
+        store = self.__dict__.get("_store_d", {})
+        for k in _PACKED:
+            store.pop(k, None)
+            self.__dict__.get("_spare", {}).pop(k, None)
+        self.__dict__.pop("_packed_stamp", None)
+
+    def _packed_params(self) -> dict[str, torch.Tensor]:
+        """Storage tensors including the integrator layout (GPU only); repacks if stale."""
+        store = self._kernel_params()
+        if self._pack_ok():
+            return store
+        from magicsoup_amd.ops import hip_ops
+
+        self._drop_packed()
+        N = store["N"]
+        rows, P, s = int(N.size(0)), int(N.size(1)), int(N.size(2))
+        store["_W"] = torch.empty(rows, P, s, dtype=torch.int32, device=N.device)
+        store["_Q"] = torch.empty(rows, P, 4, dtype=torch.float32, device=N.device)
+        hip_ops.pack_params(self, store)
+        self._restamp(True)
         return store
 
     def _materialize(self) -> None:
@@ -428,6 +482,7 @@ class Kinetics:
         slot = d.get("_slot")
         if slot is None:
             return
+        ok = self._pack_ok()
         n = d["_ncells"]
         store = self._store
         spare = d.setdefault("_spare", {})
@@ -448,6 +503,7 @@ class Kinetics:
             spare[k], store[k] = store[k], target[k]
         d["_slot"] = None
         d["_nrows"] = n
+        self._restamp(ok)
 
     def remove_cell_params(self, keep: torch.Tensor):
         """Keep only the cells where ``keep`` is true (bool mask (c,)) or listed (ascending index
@@ -463,6 +519,7 @@ class Kinetics:
             d["_ncells"] = k
             return
         self._materialize()
+        ok = self._pack_ok()
         spare = d.setdefault("_spare", {})
         store = self._store
         n = d["_ncells"]
@@ -473,6 +530,7 @@ class Kinetics:
             torch.index_select(t[:n], 0, idx, out=sp[:k])
             spare[name], store[name] = t, sp
         d["_ncells"] = d["_nrows"] = k
+        self._restamp(ok)
 
     def increase_max_cells(self, by_n: int, zero: bool = True):
         """Append ``by_n`` cells (parameters zero-filled unless the caller writes them all)."""
@@ -483,6 +541,7 @@ class Kinetics:
         cap = min(int(t.size(0)) for t in store.values())
         if d["_slot"] is not None and d["_nrows"] + by_n > cap:
             self._materialize()
+        ok = self._pack_ok()
         n = d["_ncells"]
         if d["_slot"] is None:
             r0 = n
@@ -502,12 +561,16 @@ class Kinetics:
         if zero:
             for t in store.values():
                 t[r0 : r0 + by_n].zero_()
+        # zero=False: the caller fills the new rows with a GPU build or row copy, both of which
+        # write the packed layout too
+        self._restamp(ok)
 
     def increase_max_proteins(self, max_n: int):
         """Grow the protein dimension of every parameter tensor to ``max_n`` (zero-filled)."""
         if max_n <= self._P():
             return
         self._materialize()
+        ok = self._pack_ok()
         store = self._store
         n = self.__dict__["_ncells"]
         for name, t in list(store.items()):
@@ -516,9 +579,11 @@ class Kinetics:
             store[name] = torch.cat([t, z], dim=1)
         self.__dict__["_nrows"] = n
         self.__dict__.pop("_spare", None)
+        self._restamp(ok)
 
     def _to_device(self, dev: torch.device) -> None:
         self._materialize()
+        self._drop_packed()
         n = self.__dict__["_ncells"]
         for name, t in list(self._store.items()):
             self._store[name] = t[:n].to(dev)
@@ -645,7 +710,8 @@ class Kinetics:
         for k in ("_spare", "_hip_scratch"):
             state.pop(k, None)
         n = state["_ncells"]
-        state["_store_d"] = {k: v[:n].clone() for k, v in self._store.items()}
+        state["_store_d"] = {k: v[:n].clone() for k, v in self._store.items() if k not in _PACKED}
+        state.pop("_packed_stamp", None)
         state["_nrows"] = n
         return state
 

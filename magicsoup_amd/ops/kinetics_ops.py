@@ -33,10 +33,10 @@ def integrate(kin, X: torch.Tensor, trims, n_iters: int, reduce_mask=None) -> li
     if X.is_cuda:
         from magicsoup_amd.ops import hip_ops
 
-        p = _canonical_params(kin)
+        p = kin._packed_params()
         if kin.__dict__["_ncells"] < c:
             raise ValueError(f"kinetics has {kin.__dict__['_ncells']} cells but X has {c}")
-        return hip_ops.integrate(X, p, list(trims), n_iters, slot=kin._slot_tensor())
+        return hip_ops.integrate(kin, X, p, list(trims), n_iters, slot=kin._slot_tensor())
     kin._materialize()
     p = _canonical_params(kin)
     if p["N"].size(0) < c:
@@ -83,7 +83,7 @@ def build_params(kin, rows: torch.Tensor, tokens: torch.Tensor, nprot: torch.Ten
         from magicsoup_amd.ops import hip_ops
 
         np_ = None if nprot is None else nprot.to(device=dev, dtype=torch.int32).contiguous()
-        hip_ops.build_params(tokens, rows, luts, p, float(kin.abs_temp), GAS_CONSTANT, nprot=np_)
+        hip_ops.build_params(kin, tokens, rows, luts, p, float(kin.abs_temp), GAS_CONSTANT, nprot=np_)
         return
     if nprot is not None:
         nprot = nprot.cpu()
