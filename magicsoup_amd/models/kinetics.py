@@ -363,7 +363,13 @@ class Kinetics:
         self._restamp(ok)
 
     def copy_cell_params(self, from_idxs, to_idxs):
-        """Copy the parameters of cells ``from_idxs`` to cells ``to_idxs``."""
+        """Copy the parameters of cells ``from_idxs`` to cells ``to_idxs`` (sources are read before
+        any destination is written, as with ``t[to] = t[fr]``)."""
+        self._copy_rows(from_idxs, to_idxs, disjoint=False)
+
+    def _copy_rows(self, from_idxs, to_idxs, disjoint: bool) -> None:
+        """``disjoint``: the caller guarantees no destination is also a source (e.g. new cells),
+        so the GPU copies rows directly instead of staging them."""
         store = self._store
         dev = store["N"].device
         if dev.type == "cuda":
@@ -371,7 +377,13 @@ class Kinetics:
 
             fr = self._rows(torch.as_tensor(from_idxs, device=dev).long())
             to = self._rows(torch.as_tensor(to_idxs, device=dev).long())
-            hip_ops.gather_rows([(t, t) for t in store.values()], int(fr.numel()), src_rows=fr, dst_rows=to)
+            k = int(fr.numel())
+            if disjoint:
+                hip_ops.gather_rows([(t, t) for t in store.values()], k, src_rows=fr, dst_rows=to)
+                return
+            tmp = {name: torch.empty(k, *t.shape[1:], dtype=t.dtype, device=dev) for name, t in store.items()}
+            hip_ops.gather_rows([(store[nm], tmp[nm]) for nm in store], k, src_rows=fr)
+            hip_ops.gather_rows([(tmp[nm], store[nm]) for nm in store], k, dst_rows=to)
             return
         fr, to = self._rows(from_idxs), self._rows(to_idxs)
         ok = self._pack_ok()
@@ -503,6 +515,7 @@ class Kinetics:
             spare[k], store[k] = store[k], target[k]
         d["_slot"] = None
         d["_nrows"] = n
+        d["_free"], d["_nfree"] = None, 0
         self._restamp(ok)
 
     def remove_cell_params(self, keep: torch.Tensor):
@@ -513,8 +526,16 @@ class Kinetics:
         k = int(idx.numel())
         if idx.is_cuda:
             slot = d["_slot"]
+            n = d["_ncells"]
             if slot is None:
-                slot = torch.arange(d["_ncells"], device=idx.device)
+                slot = torch.arange(n, device=idx.device)
+            if k < n:  # rows of the removed cells become reusable by later growth
+                gone = torch.ones(n, dtype=torch.bool, device=idx.device)
+                gone[idx] = False
+                freed = slot[gone]
+                free = d.get("_free")
+                d["_free"] = freed if free is None or d.get("_nfree", 0) == 0 else torch.cat([free[: d["_nfree"]], freed])
+                d["_nfree"] = d.get("_nfree", 0) + (n - k)
             d["_slot"] = slot[idx]
             d["_ncells"] = k
             return
@@ -539,8 +560,11 @@ class Kinetics:
         d = self.__dict__
         store = self._store
         cap = min(int(t.size(0)) for t in store.values())
-        if d["_slot"] is not None and d["_nrows"] + by_n > cap:
+        nfree = d.get("_nfree", 0) if d["_slot"] is not None else 0
+        reuse = min(nfree, by_n)
+        if d["_slot"] is not None and d["_nrows"] + (by_n - reuse) > cap:
             self._materialize()
+            reuse = 0
         ok = self._pack_ok()
         n = d["_ncells"]
         if d["_slot"] is None:
@@ -552,15 +576,27 @@ class Kinetics:
                     nb[:n] = t[:n]
                     store[name] = nb
                 d.pop("_spare", None)
+            new_rows = slice(r0, r0 + by_n)
+            d["_nrows"] = r0 + by_n
         else:
-            r0 = d["_nrows"]
-            slot = d["_slot"]
-            d["_slot"] = torch.cat([slot, torch.arange(r0, r0 + by_n, device=slot.device, dtype=slot.dtype)])
-        d["_nrows"] = r0 + by_n
+            # reuse rows freed by removed cells first (most recently freed last), then append
+            slot, r0 = d["_slot"], d["_nrows"]
+            parts = []
+            if reuse:
+                parts.append(d["_free"][nfree - reuse : nfree].to(slot.dtype))
+                d["_nfree"] = nfree - reuse
+            if by_n > reuse:
+                parts.append(torch.arange(r0, r0 + by_n - reuse, device=slot.device, dtype=slot.dtype))
+                d["_nrows"] = r0 + by_n - reuse
+            new_rows = parts[0] if len(parts) == 1 else torch.cat(parts)
+            d["_slot"] = torch.cat([slot, new_rows])
         d["_ncells"] = n + by_n
         if zero:
             for t in store.values():
-                t[r0 : r0 + by_n].zero_()
+                if isinstance(new_rows, slice):
+                    t[new_rows].zero_()
+                else:
+                    t.index_fill_(0, new_rows, 0)
         # zero=False: the caller fills the new rows with a GPU build or row copy, both of which
         # write the packed layout too
         self._restamp(ok)

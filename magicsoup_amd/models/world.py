@@ -341,7 +341,7 @@ class World:
         pairs = [(col.view(n), col.view(n)) for name, col in self._cols.items() if name != "cell_positions"]
         pairs += self._genomes.clone_pairs(k) + self._labels.clone_pairs(k)
         hip_ops.gather_rows(pairs, k, src_rows=src, dst_rows=dst)
-        self.kinetics.copy_cell_params(from_idxs=src, to_idxs=dst)
+        self.kinetics._copy_rows(src, dst, disjoint=True)  # children are new rows
 
     def _idx_tensor(self, idxs, unique: bool = True) -> torch.Tensor:
         """Cell indices as a long tensor on the world's device (ascending and duplicate-free when

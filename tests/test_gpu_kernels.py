@@ -5,6 +5,7 @@ import pytest
 import torch
 
 import magicsoup_amd as ms
+from magicsoup_amd.models.kinetics import Kinetics
 from magicsoup_amd.examples.wood_ljungdahl import CHEMISTRY
 from magicsoup_amd.ops import native
 from tests.conftest import gen_genomes
@@ -290,3 +291,54 @@ def test_neighbor_slots_match_pair_list():
     got = {(int(k) >> 32, int(k) & 0xFFFFFFFF) for k in keys.tolist()}
     assert len(got) == int(keys.numel())  # each pair once
     assert got == set(w.get_neighbors(list(range(w.n_cells))))
+
+
+def test_param_row_storage_fuzz_matches_dense_model():
+    """Random kill / grow / copy / build sequences on GPU row storage (slot map, freed-row reuse,
+    packed integrator layout) against a dense cell-ordered model of the same operations."""
+    import random as _r
+
+    from magicsoup_amd.ops import kinetics_ops
+
+    rng = _r.Random(5)
+    w = _world("cuda", map_size=64, n=120)
+    kin = w.kinetics
+    names = ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke")
+    model = {k: getattr(kin, k).clone() for k in names}
+    X = torch.rand(kin.N.size(0), kin.N.size(2), device="cuda") * 5
+    for step in range(60):
+        n = kin.__dict__["_ncells"]
+        op = rng.choice(["kill", "grow", "copy", "integrate"])
+        if op == "kill" and n > 10:
+            keep = torch.rand(n, device="cuda") > 0.3
+            kin.remove_cell_params(keep)
+            for k in names:
+                model[k] = model[k][keep]
+            X = X[keep]
+        elif op == "grow":
+            k_new = rng.randint(1, 40)
+            kin.increase_max_cells(k_new)
+            for k in names:
+                z = torch.zeros(k_new, *model[k].shape[1:], dtype=model[k].dtype, device="cuda")
+                model[k] = torch.cat([model[k], z])
+            X = torch.cat([X, torch.rand(k_new, X.size(1), device="cuda") * 5])
+        elif op == "copy" and n > 4:
+            src = torch.randperm(n, device="cuda")[: n // 4]
+            dst = torch.randperm(n, device="cuda")[: n // 4]
+            kin.copy_cell_params(src, dst)
+            for k in names:
+                model[k][dst] = model[k][src]
+        else:
+            # integrate through the slot map + packed layout; compare with a dense copy
+            dense = Kinetics.__new__(Kinetics)
+            dense.__dict__.update(kin.__dict__)
+            dense.__dict__.update(_store_d={k: model[k].clone() for k in names}, _slot=None, _hip_scratch=None,
+                                  _ncells=model["N"].size(0), _nrows=model["N"].size(0), _packed_stamp=None,
+                                  _spare={})
+            dense.__dict__.pop("_hip_scratch")
+            Xa, Xb = X.clone(), X.clone()
+            kinetics_ops.integrate(kin, Xa, (0.7, 0.2, 0.1), 4)
+            kinetics_ops.integrate(dense, Xb, (0.7, 0.2, 0.1), 4)
+            assert torch.equal(Xa, Xb), step
+    for k in names:
+        assert torch.equal(getattr(kin, k), model[k]), k
