@@ -114,13 +114,20 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        # one rank per GPU; more ranks than GPUs (a rehearsal on a small box) share them round-robin
+        local_rank %= max(1, torch.cuda.device_count())
     distributed = world_size > 1
     if distributed:
         import torch.distributed as dist
 
-        if torch.cuda.is_available():
+        backend = os.environ.get("MS_DIST_BACKEND", "nccl")  # gloo: rehearsal with ranks sharing a GPU
+        if torch.cuda.is_available() and backend == "nccl":
             torch.cuda.set_device(local_rank)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        elif torch.cuda.is_available():
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group(backend)
         else:  # CPU rehearsal of the multi-rank path
             dist.init_process_group("gloo")
     device = f"cuda:{local_rank}" if torch.cuda.is_available() else "cpu"

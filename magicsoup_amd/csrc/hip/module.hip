@@ -83,6 +83,11 @@ void rec_count(int n, uintptr_t pairs, uintptr_t lens, double p, uint64_t seed, 
 void rec_apply(int nsel, uintptr_t sel, uintptr_t pairs, uintptr_t arena, int width, uintptr_t lens, uintptr_t k,
                uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out, int out_width,
                uintptr_t out_len, uintptr_t stream);
+void place_collect(int k, uintptr_t wins, uintptr_t cells, uintptr_t result, int C, uintptr_t par, uintptr_t npos,
+                   uintptr_t stream);
+// select.hip
+std::pair<long long, int> select_indices(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel,
+                                         uintptr_t rest, uintptr_t stream);
 }  // namespace msd
 
 namespace {
@@ -132,4 +137,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("mut_apply", &msd::mut_apply);
   m.def("rec_count", &msd::rec_count);
   m.def("rec_apply", &msd::rec_apply);
+  m.def("place_collect", &msd::place_collect);
+  m.def("select_indices", &msd::select_indices,
+        "(count, max) of an order-preserving compaction; synchronises the stream");
 }

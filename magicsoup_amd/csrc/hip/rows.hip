@@ -6,6 +6,7 @@
 // Instead of one gather launch per tensor (plus a copy back), all of them go through one kernel:
 // the work is flattened over (descriptor, row, 16-byte chunk) with a prefix over descriptors, so
 // large rows (kinetics (P, s) slices of a few KiB) and 4-byte rows share one grid.
+#include <algorithm>
 #include <tuple>
 #include <vector>
 
@@ -31,25 +32,29 @@ struct RowArgs {
   const int64_t* dst_rows;  // nullptr: identity
 };
 
-__global__ void __launch_bounds__(256) gather_rows_kernel(RowArgs a) {
-  const long long total = a.first[a.nd];
-  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (long long)gridDim.x * blockDim.x) {
-    int k = 0;
-    while (k + 1 < a.nd && a.first[k + 1] <= t) ++k;
-    const RowDesc& d = a.d[k];
-    const long long u = t - a.first[k];
-    const int i = (int)(u / d.units), c = (int)(u - (long long)i * d.units);
-    const long long sr = a.src_rows ? a.src_rows[i] : i;
-    const long long dr = a.dst_rows ? a.dst_rows[i] : i;
-    if (d.unit == 16) {
-      const uint4* s = reinterpret_cast<const uint4*>(d.src + sr * d.src_stride) + c;
-      reinterpret_cast<uint4*>(d.dst + dr * d.dst_stride)[c] = *s;
-    } else {
-      const uint32_t* s = reinterpret_cast<const uint32_t*>(d.src + sr * d.src_stride) + c;
-      reinterpret_cast<uint32_t*>(d.dst + dr * d.dst_stride)[c] = *s;
-    }
+// grid.y = descriptor: no per-element descriptor search; 32-bit index math within a descriptor
+// (n * units < 2^31 is checked on the host).
+template <class U>
+__device__ __forceinline__ void copy_units(const RowDesc& d, unsigned total, const int64_t* src_rows,
+                                           const int64_t* dst_rows) {
+  const unsigned units = (unsigned)d.units;
+  for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const unsigned i = t / units, c = t - i * units;
+    const long long sr = src_rows ? src_rows[i] : (long long)i;
+    const long long dr = dst_rows ? dst_rows[i] : (long long)i;
+    const U v = reinterpret_cast<const U*>(d.src + sr * d.src_stride)[c];
+    reinterpret_cast<U*>(d.dst + dr * d.dst_stride)[c] = v;
   }
+}
+
+__global__ void __launch_bounds__(256) gather_rows_kernel(RowArgs a) {
+  const RowDesc& d = a.d[blockIdx.y];
+  const unsigned total = (unsigned)(a.first[blockIdx.y + 1] - a.first[blockIdx.y]);
+  if (blockIdx.x * blockDim.x >= total) return;
+  if (d.unit == 16)
+    copy_units<uint4>(d, total, a.src_rows, a.dst_rows);
+  else
+    copy_units<uint32_t>(d, total, a.src_rows, a.dst_rows);
 }
 
 // descs: (src_ptr, dst_ptr, src_stride_bytes, dst_stride_bytes, row_bytes) per tensor. Row bytes and
@@ -85,9 +90,13 @@ void gather_rows(int n, uintptr_t src_rows, uintptr_t dst_rows,
     a.first[nd] = acc;
     a.nd = nd;
     if (nd == 0 || acc == 0) continue;
-    const long long blocks = (acc + 255) / 256;
-    const unsigned grid = (unsigned)(blocks < 65536 ? blocks : 65536);
-    gather_rows_kernel<<<grid, 256, 0, S_(stream)>>>(a);
+    long long widest = 0;
+    for (int q = 0; q < nd; ++q) widest = std::max(widest, a.first[q + 1] - a.first[q]);
+    if (widest >= (1ll << 31)) throw std::invalid_argument("gather_rows: too many units per tensor");
+    // enough blocks for the widest descriptor, capped (grid-stride beyond); ~2k blocks fill the chip
+    const long long blocks = (widest + 255) / 256;
+    const unsigned gx = (unsigned)(blocks < 2048 ? blocks : 2048);
+    gather_rows_kernel<<<dim3(gx, nd), 256, 0, S_(stream)>>>(a);
     MS_LAUNCH_CHECK();
   }
 }

@@ -1,0 +1,178 @@
+// Order-preserving stream compaction with the count delivered to pinned host memory.
+//
+// Every population change of the API (kill_cells, divide_cells, the mutated / recombined subset of
+// mutate_cells / recombinate_cells) needs "the ascending indices i with pred(i)" and, because the
+// reference API returns Python-sized results, their count on the host. torch.nonzero does this with
+// ~5 launches and a separate read-back; here it is two launches plus one stream synchronisation:
+//
+//   select_count_kernel   per 4096-item tile: selected count and max(vals) of selected items
+//   select_write_kernel   per tile: exclusive offset from the preceding tiles' counts, wave-ballot
+//                         prefix within the tile, write selected (and optionally the rejected)
+//                         indices; the last tile writes {count, max} straight into pinned host memory
+//
+// Predicates: u8 mask != 0, u8 mask == 0, int32 > 0, int64 >= 0.
+#include <algorithm>
+
+#include "hip_common.h"
+
+namespace msd {
+
+constexpr int kSelThreads = 256;
+constexpr int kSelItems = 16;
+constexpr int kSelTile = kSelThreads * kSelItems;  // 4096
+
+enum SelKind { kMaskSet = 0, kMaskClear = 1, kI32Pos = 2, kI64NonNeg = 3 };
+
+template <int K>
+__device__ __forceinline__ bool sel_pred(const void* src, long long i) {
+  if constexpr (K == kMaskSet) return reinterpret_cast<const uint8_t*>(src)[i] != 0;
+  if constexpr (K == kMaskClear) return reinterpret_cast<const uint8_t*>(src)[i] == 0;
+  if constexpr (K == kI32Pos) return reinterpret_cast<const int32_t*>(src)[i] > 0;
+  return reinterpret_cast<const int64_t*>(src)[i] >= 0;
+}
+
+template <int K>
+__global__ void __launch_bounds__(kSelThreads) select_count_kernel(long long n, const void* src, const int32_t* vals,
+                                                                   int32_t* tile_count, int32_t* tile_max) {
+  __shared__ int s_cnt[kSelThreads / 64], s_max[kSelThreads / 64];
+  const long long base = (long long)blockIdx.x * kSelTile;
+  int cnt = 0, mx = 0;
+#pragma unroll
+  for (int j = 0; j < kSelItems; ++j) {
+    const long long i = base + j * kSelThreads + threadIdx.x;
+    if (i < n && sel_pred<K>(src, i)) {
+      ++cnt;
+      if (vals) mx = max(mx, vals[i]);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o);
+    mx = max(mx, __shfl_xor(mx, o));
+  }
+  const int w = threadIdx.x >> 6;
+  if (lane_id() == 0) {
+    s_cnt[w] = cnt;
+    s_max[w] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int c = 0, m = 0;
+    for (int q = 0; q < kSelThreads / 64; ++q) {
+      c += s_cnt[q];
+      m = max(m, s_max[q]);
+    }
+    tile_count[blockIdx.x] = c;
+    tile_max[blockIdx.x] = m;
+  }
+}
+
+template <int K>
+__global__ void __launch_bounds__(kSelThreads) select_write_kernel(long long n, const void* src, const int32_t* tile_count,
+                                                                   const int32_t* tile_max, int64_t* sel,
+                                                                   int64_t* rest, int32_t* host_out) {
+  constexpr int W = kSelThreads / 64;
+  __shared__ long long s_red[W];
+  __shared__ int s_wc[kSelItems][W];
+  __shared__ int s_pre[kSelItems][W];
+  const int w = threadIdx.x >> 6, lane = lane_id();
+  const int b = blockIdx.x;
+  // exclusive offset of this tile: sum of the preceding tiles' counts
+  long long off = 0;
+  for (int q = threadIdx.x; q < b; q += kSelThreads) off += tile_count[q];
+  for (int o = 32; o > 0; o >>= 1) off += __shfl_xor(off, o);
+  if (lane == 0) s_red[w] = off;
+  const long long base = (long long)b * kSelTile;
+  uint64_t ballots[kSelItems];
+#pragma unroll
+  for (int j = 0; j < kSelItems; ++j) {
+    const long long i = base + j * kSelThreads + threadIdx.x;
+    const bool p = i < n && sel_pred<K>(src, i);
+    ballots[j] = __ballot(p);
+    if (lane == 0) s_wc[j][w] = __popcll(ballots[j]);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long t = 0;
+    for (int q = 0; q < W; ++q) t += s_red[q];
+    s_red[0] = t;
+    int acc = 0;
+    for (int j = 0; j < kSelItems; ++j)
+      for (int q = 0; q < W; ++q) {
+        s_pre[j][q] = acc;
+        acc += s_wc[j][q];
+      }
+  }
+  __syncthreads();
+  const long long tile_off = s_red[0];
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+  for (int j = 0; j < kSelItems; ++j) {
+    const long long i = base + j * kSelThreads + threadIdx.x;
+    if (i >= n) break;
+    const long long k = s_pre[j][w] + __popcll(ballots[j] & lt);  // selected before i within the tile
+    if ((ballots[j] >> lane) & 1ull) {
+      sel[tile_off + k] = i;
+    } else if (rest) {
+      rest[(base - tile_off) + (i - base - k)] = i;
+    }
+  }
+  if (b == (int)gridDim.x - 1 && threadIdx.x == 0) {
+    int total = (int)tile_off, m = 0;
+    for (int j = 0; j < kSelItems; ++j)
+      for (int q = 0; q < W; ++q) total += s_wc[j][q];
+    for (int q = 0; q < (int)gridDim.x; ++q) m = max(m, tile_max[q]);
+    host_out[0] = total;
+    host_out[1] = m;
+  }
+}
+
+namespace {
+int32_t* g_host = nullptr;  // pinned, coherent {count, max}
+int32_t* g_host_dev = nullptr;
+int32_t* g_tiles = nullptr;  // device {count[tiles], max[tiles]}
+long long g_tiles_cap = 0;
+}  // namespace
+
+// Returns {count, max(vals over selected)}; synchronises `stream`. sel must hold n entries (rest too,
+// when given). Writes nothing and returns {0, 0} for n == 0.
+std::pair<long long, int> select_indices(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel,
+                                         uintptr_t rest, uintptr_t stream) {
+  if (n <= 0) return {0, 0};
+  if (n >= (1ll << 40)) throw std::invalid_argument("select_indices: n too large");
+  if (!g_host) {
+    MS_HIP_CHECK(hipHostMalloc((void**)&g_host, 2 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
+    MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_host_dev, g_host, 0));
+  }
+  const long long tiles = (n + kSelTile - 1) / kSelTile;
+  if (tiles > g_tiles_cap) {
+    if (g_tiles) MS_HIP_CHECK(hipFree(g_tiles));
+    g_tiles_cap = std::max(tiles, 256ll);
+    MS_HIP_CHECK(hipMalloc((void**)&g_tiles, 2 * g_tiles_cap * sizeof(int32_t)));
+  }
+  g_host[0] = -1;
+  hipStream_t s = S_(stream);
+  const void* sp = reinterpret_cast<const void*>(src);
+  const int32_t* vp = vals ? P_<int32_t>(vals) : nullptr;
+  int32_t* tc = g_tiles;
+  int32_t* tm = g_tiles + g_tiles_cap;
+#define MS_SEL(K)                                                                                               \
+  select_count_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, vp, tc, tm);                          \
+  MS_LAUNCH_CHECK();                                                                                            \
+  select_write_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, tc, tm, P_<int64_t>(sel),             \
+                                                                 rest ? P_<int64_t>(rest) : nullptr, g_host_dev); \
+  MS_LAUNCH_CHECK();
+  switch (kind) {
+    case kMaskSet: MS_SEL(kMaskSet) break;
+    case kMaskClear: MS_SEL(kMaskClear) break;
+    case kI32Pos: MS_SEL(kI32Pos) break;
+    case kI64NonNeg: MS_SEL(kI64NonNeg) break;
+    default: throw std::invalid_argument("select_indices: unknown predicate");
+  }
+#undef MS_SEL
+  MS_HIP_CHECK(hipStreamSynchronize(s));
+  const long long cnt = g_host[0];
+  if (cnt < 0 || cnt > n) throw std::runtime_error("select_indices: bad count read-back");
+  return {cnt, g_host[1]};
+}
+
+}  // namespace msd

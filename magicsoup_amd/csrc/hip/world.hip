@@ -130,6 +130,20 @@ __global__ void __launch_bounds__(256) place_resolve_kernel(int k, const int64_t
   }
 }
 
+// Winners of the placement rounds (wins = ascending list positions with result >= 0): the cell and
+// its new pixel as (x, y).
+__global__ void __launch_bounds__(256) place_collect_kernel(int k, const int64_t* wins, const int64_t* cells,
+                                                            const long long* result, int C, int64_t* par,
+                                                            int32_t* npos) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k) return;
+  const long long w = wins[i];
+  const long long px = result[w];
+  par[i] = cells[w];
+  npos[2 * i] = (int32_t)(px / C);
+  npos[2 * i + 1] = (int32_t)(px - (px / C) * C);
+}
+
 // ---------------------------------------------------------------- neighbours
 __global__ void __launch_bounds__(256) index_map_kernel(int c, const int32_t* pos, int C, int32_t* idx_map, bool clear) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -215,6 +229,15 @@ void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo,
                                                        P_<long long>(cand), P_<int>(claim), P_<long long>(result));
     MS_LAUNCH_CHECK();
   }
+}
+
+void place_collect(int k, uintptr_t wins, uintptr_t cells, uintptr_t result, int C, uintptr_t par, uintptr_t npos,
+                   uintptr_t stream) {
+  if (k <= 0) return;
+  place_collect_kernel<<<cdiv(k, 256), 256, 0, S_(stream)>>>(k, P_<int64_t>(wins), P_<int64_t>(cells),
+                                                              P_<long long>(result), C, P_<int64_t>(par),
+                                                              P_<int32_t>(npos));
+  MS_LAUNCH_CHECK();
 }
 
 void index_map(int c, uintptr_t pos, int C, uintptr_t idx_map, bool clear, uintptr_t stream) {

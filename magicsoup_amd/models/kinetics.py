@@ -518,9 +518,9 @@ class Kinetics:
         d["_free"], d["_nfree"] = None, 0
         self._restamp(ok)
 
-    def remove_cell_params(self, keep: torch.Tensor):
+    def remove_cell_params(self, keep: torch.Tensor, removed: torch.Tensor | None = None):
         """Keep only the cells where ``keep`` is true (bool mask (c,)) or listed (ascending index
-        tensor), preserving their order."""
+        tensor), preserving their order. ``removed`` (optional) lists the other cells."""
         idx = torch.nonzero(keep).flatten() if keep.dtype == torch.bool else keep.to(torch.long)
         d = self.__dict__
         k = int(idx.numel())
@@ -530,12 +530,21 @@ class Kinetics:
             if slot is None:
                 slot = torch.arange(n, device=idx.device)
             if k < n:  # rows of the removed cells become reusable by later growth
-                gone = torch.ones(n, dtype=torch.bool, device=idx.device)
-                gone[idx] = False
-                freed = slot[gone]
+                if removed is None:
+                    gone = torch.ones(n, dtype=torch.bool, device=idx.device)
+                    gone[idx] = False
+                    freed = slot[gone]
+                else:
+                    freed = slot[removed.to(torch.long)]
+                nfree = d.get("_nfree", 0) if d.get("_free") is not None else 0
                 free = d.get("_free")
-                d["_free"] = freed if free is None or d.get("_nfree", 0) == 0 else torch.cat([free[: d["_nfree"]], freed])
-                d["_nfree"] = d.get("_nfree", 0) + (n - k)
+                if free is None or free.numel() < nfree + (n - k):
+                    nb = torch.empty(max(nfree + (n - k), 2 * nfree + 64), dtype=slot.dtype, device=slot.device)
+                    if nfree:
+                        nb[:nfree] = free[:nfree]
+                    free = d["_free"] = nb
+                free[nfree : nfree + (n - k)] = freed
+                d["_nfree"] = nfree + (n - k)
             d["_slot"] = slot[idx]
             d["_ncells"] = k
             return

@@ -349,6 +349,10 @@ class World:
         if isinstance(idxs, torch.Tensor):
             t = idxs.to(self.device)
             if t.dtype == torch.bool:
+                if t.is_cuda:
+                    from magicsoup_amd.ops import hip_ops
+
+                    return hip_ops.select(t, "set")[0]
                 return torch.nonzero(t).flatten()
             t = t.to(torch.long).flatten()
             if unique and t.numel() > 1:
@@ -523,13 +527,22 @@ class World:
                 return
             dead[t.to(self.device, torch.long)] = True  # duplicates are harmless
         world_ops.spill_and_free_mask(self, dead)
+        if dead.is_cuda:
+            from magicsoup_amd.ops import hip_ops
+
+            # survivors and the dead in one compaction pass (one stream sync for the count)
+            keep_idx, dead_idx, _ = hip_ops.select(dead, "clear", rest=True)
+            if int(keep_idx.numel()) == n:
+                return
+            self._compact(keep_idx, None, removed=dead_idx)
+            return
         keep = ~dead
         keep_idx = torch.nonzero(keep).flatten()
         if int(keep_idx.numel()) == n:
             return
         self._compact(keep_idx, keep)
 
-    def _compact(self, keep_idx: torch.Tensor, keep: torch.Tensor) -> None:
+    def _compact(self, keep_idx: torch.Tensor, keep: torch.Tensor | None, removed: torch.Tensor | None = None) -> None:
         n_new = int(keep_idx.numel())
         if keep_idx.is_cuda:
             # every per-cell array (columns, arenas, kinetics parameters) in one gather launch
@@ -541,7 +554,7 @@ class World:
             pairs += self._genomes.compact_pairs(n_new) + self._labels.compact_pairs(n_new)
             hip_ops.gather_rows(pairs, n_new, src_rows=keep_idx)
             # kinetics parameters stay where they are; only the cell -> row map is compacted
-            self.kinetics.remove_cell_params(keep=keep_idx)
+            self.kinetics.remove_cell_params(keep=keep_idx, removed=removed)
             for col in self._cols.values():
                 col.swap()
             self._genomes.commit_compact(n_new)

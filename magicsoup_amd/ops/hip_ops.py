@@ -70,6 +70,28 @@ def _rng() -> tuple[int, int]:
     return _m().next_call()
 
 
+_SEL = {"set": 0, "clear": 1, "i32pos": 2, "i64nonneg": 3}
+
+
+def select(src: torch.Tensor, kind: str, vals: torch.Tensor | None = None, rest: bool = False):
+    """Order-preserving compaction (select.hip): ascending int64 indices i with pred(src[i]) --
+    ``set`` / ``clear`` for bool / uint8 masks, ``i32pos`` (> 0), ``i64nonneg`` (>= 0) -- plus the
+    rejected indices when ``rest`` and max(vals[i]) over the selected i (0 without ``vals``).
+    Two launches and one stream synchronisation (the count lands in pinned host memory)."""
+    n = int(src.numel())
+    dev = src.device
+    if src.dtype == torch.bool:
+        src = src.view(torch.uint8)
+    src = src.contiguous()
+    sel = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    rst = torch.empty(max(n, 1), dtype=torch.int64, device=dev) if rest else None
+    if vals is not None:
+        assert vals.dtype == torch.int32 and vals.numel() >= n
+        vals = vals.contiguous()
+    cnt, mx = _m().select_indices(n, _SEL[kind], _p(src), _p(vals), _p(sel), _p(rst), _stream())
+    return sel[:cnt], (rst[: n - cnt] if rest else None), int(mx)
+
+
 # ---------------------------------------------------------------------------- geometry
 # ---------------------------------------------------------------------------- kinetics
 _EQ = 4  # equilibrium-damping iterations per part
@@ -304,7 +326,8 @@ def free_positions(world, k: int) -> torch.Tensor:
     out = torch.empty(k, dtype=torch.int64, device=dev)
     seed, call = _rng()
     _m().claim_free(k, R, C, r_lo, r_hi, _p(cmap), seed, call, 64, _p(out), _stream())
-    got = out[out >= 0]
+    ok = select(out, "i64nonneg")[0]
+    got = out if ok.numel() == k else out[ok]
     if got.numel() < k:
         # crowded map: exact sampling of the remainder over the remaining free owned pixels
         free = torch.nonzero(cmap[r_lo * C : r_hi * C] == 0).flatten() + r_lo * C
@@ -341,9 +364,12 @@ def _place_rounds(world, cells: torch.Tensor, vacate: bool, rounds: int = _PLACE
     seed, call = _rng()
     _m().place_rounds(k, _p(cells), _p(pos), R, C, r_lo, r_hi, wrap, bool(vacate), _p(cmap), _p(pending), _p(cand),
                       _p(claim), _p(result), int(rounds), seed, call, _stream())
-    wins = torch.nonzero(result >= 0).flatten()
-    wpix = result[wins]
-    return cells[wins], torch.stack([wpix // C, wpix % C], dim=1).to(torch.int32)
+    wins = select(result, "i64nonneg")[0]
+    k2 = int(wins.numel())
+    par = torch.empty(k2, dtype=torch.int64, device=dev)
+    npos = torch.empty(k2, 2, dtype=torch.int32, device=dev)
+    _m().place_collect(k2, _p(wins), _p(cells), _p(result), C, _p(par), _p(npos), _stream())
+    return par, npos
 
 
 def divide_placement(world, idxs: torch.Tensor):
@@ -505,12 +531,13 @@ def point_mutations(world, rows, p: float, p_indel: float, p_del: float) -> torc
     k = torch.empty(n, dtype=torch.int32, device=dev)
     seed, call = _rng()
     _m().mut_count(n, _p(rows64), _p(arena.lens), float(p), seed, call, _p(k), _stream())
-    sel = torch.nonzero(k > 0).flatten()
+    # bound of a mutated genome's length: its length + k (every mutation an insertion)
+    lens_k = (arena.lens[:n] if rows64 is None else arena.lens[rows64]) + k
+    sel, _, bound = select(k, "i32pos", vals=lens_k)
     nsel = int(sel.numel())
     if nsel == 0:
         return torch.zeros(0, dtype=torch.long, device=dev)
     tgt = sel if rows64 is None else rows64[sel]
-    bound = int((arena.lens[tgt] + k[sel]).max().item())
     out_w = max(bound, 1)
     out = torch.zeros(nsel, out_w, dtype=torch.uint8, device=dev)
     out_len = torch.empty(nsel, dtype=torch.int32, device=dev)
@@ -564,19 +591,20 @@ def neighbor_slot_keys(world) -> torch.Tensor:
 def _rec_apply(world, pairs: torch.Tensor, k: torch.Tensor, seed: int, call: int) -> torch.Tensor:
     arena = world._genomes
     dev = arena.data.device
-    sel = torch.nonzero(k > 0).flatten()
+    sel, _, kmax = select(k, "i32pos", vals=k)
     nsel = int(sel.numel())
     if nsel == 0:
         return torch.zeros(0, dtype=torch.long, device=dev)
     sp = pairs[sel].long()
-    tot = arena.lens[sp[:, 0]] + arena.lens[sp[:, 1]]
-    mx = torch.stack([tot.max(), k[sel].max()]).tolist()
-    out_w, parts_cap = max(int(mx[0]), 1), int(mx[1]) + 2
+    out_w, parts_cap = 2 * int(arena.width), kmax + 2  # a recombined genome is at most both parents
     out = torch.zeros(2 * nsel, out_w, dtype=torch.uint8, device=dev)
     out_len = torch.empty(2 * nsel, dtype=torch.int32, device=dev)
     parts = torch.empty(nsel * parts_cap * 3, dtype=torch.int32, device=dev)
     _m().rec_apply(nsel, _p(sel), _p(pairs), _p(arena.data), int(arena.data.size(1)), _p(arena.lens), _p(k),
                    seed, call, _p(parts), parts_cap, _p(out), out_w, _p(out_len), _stream())
+    # rare path (p = 1e-7 per bp): trim the scratch width to the longest result so the arena only
+    # widens when a genome actually outgrows it
+    out = out[:, : max(int(out_len.max().item()), 1)]
     cells = sp.reshape(-1)  # (a0, b0, a1, b1, ...) matches the scratch row order
     # the last recombination that touched a cell wins (reference update order)
     order = torch.arange(cells.numel(), device=dev)

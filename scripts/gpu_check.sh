@@ -20,7 +20,7 @@ run() {  # run <name> <seconds> <cmd...>
 }
 python -c "import __graft_entry__ as g; g.build()" || exit 1
 if [[ "$what" == tests || "$what" == all ]]; then
-  run pytest_gpu 900 python -m pytest tests -m gpu -q
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [[ "$what" == bench || "$what" == all ]]; then

@@ -342,3 +342,25 @@ def test_param_row_storage_fuzz_matches_dense_model():
             assert torch.equal(Xa, Xb), step
     for k in names:
         assert torch.equal(getattr(kin, k), model[k]), k
+
+
+@pytest.mark.parametrize("n", [1, 63, 4096, 4097, 50_000, 1_000_003])
+def test_select_matches_nonzero(n):
+    """select.hip compaction (both lists, count and max via pinned memory) against torch.nonzero."""
+    from magicsoup_amd.ops import hip_ops
+
+    g = torch.Generator(device="cuda").manual_seed(n)
+    mask = torch.rand(n, device="cuda", generator=g) < 0.3
+    sel, rest, _ = hip_ops.select(mask, "set", rest=True)
+    assert torch.equal(sel, torch.nonzero(mask).flatten())
+    assert torch.equal(rest, torch.nonzero(~mask).flatten())
+    sel2, _, _ = hip_ops.select(mask, "clear")
+    assert torch.equal(sel2, rest)
+    v = torch.randint(-5, 6, (n,), dtype=torch.int32, device="cuda", generator=g)
+    vals = torch.randint(0, 1000, (n,), dtype=torch.int32, device="cuda", generator=g)
+    sel3, _, mx = hip_ops.select(v, "i32pos", vals=vals)
+    ref = torch.nonzero(v > 0).flatten()
+    assert torch.equal(sel3, ref)
+    assert mx == (int(vals[ref].max()) if ref.numel() else 0)
+    r = torch.randint(-3, 3, (n,), dtype=torch.int64, device="cuda", generator=g)
+    assert torch.equal(hip_ops.select(r, "i64nonneg")[0], torch.nonzero(r >= 0).flatten())
