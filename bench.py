@@ -57,9 +57,14 @@ def _chemistry(spec: str):
     return CHEMISTRY
 
 
+_LUT: dict = {}
+
+
 def random_genomes(k: int, size: int, device) -> tuple[torch.Tensor, torch.Tensor]:
     """k uniformly random genomes of ``size`` nt as a packed (bytes, lengths) batch (on device)."""
-    lut = torch.tensor(list(b"TCGA"), dtype=torch.uint8, device=device)
+    lut = _LUT.get(str(device))
+    if lut is None:
+        lut = _LUT[str(device)] = torch.tensor(list(b"TCGA"), dtype=torch.uint8, device=device)
     rows = lut[torch.randint(0, 4, (k, size), device=device)]
     return rows, torch.full((k,), size, dtype=torch.int32, device=device)
 

@@ -22,7 +22,7 @@ void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo,
 void neighbor_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map, uintptr_t keys,
                     uintptr_t stream);
 void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
-                    uintptr_t stream);
+                    uintptr_t tot, uintptr_t stream);
 // maps.hip
 size_t diffuse_partials_len(int m, int C, int H);
 void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
@@ -60,7 +60,7 @@ void pack_params(long long items, int s, uintptr_t N, uintptr_t Nf, uintptr_t Nb
 void claim_free(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uint64_t seed, uint64_t call,
                 int attempts, uintptr_t out, uintptr_t stream);
 void index_map(int c, uintptr_t pos, int C, uintptr_t idx_map, bool clear, uintptr_t stream);
-void neighbor_pairs(int nf, uintptr_t from, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map,
+void neighbor_pairs(int nf, int n, uintptr_t from, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map,
                     uintptr_t in_from, uintptr_t in_to, uintptr_t counter, int cap, uintptr_t pairs, uintptr_t stream);
 // genetics.hip
 void translate_count(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
@@ -80,12 +80,16 @@ void mut_apply(int nsel, uintptr_t sel, uintptr_t rows, uintptr_t arena, int wid
                uintptr_t out_len, uintptr_t stream);
 void rec_count(int n, uintptr_t pairs, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
                uintptr_t stream);
-void rec_apply(int nsel, uintptr_t sel, uintptr_t pairs, uintptr_t arena, int width, uintptr_t lens, uintptr_t k,
-               uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out, int out_width,
-               uintptr_t out_len, uintptr_t stream);
+void rec_apply(int nsel, uintptr_t sel, uintptr_t pairs, uintptr_t keys, uintptr_t arena, int width, uintptr_t lens,
+               uintptr_t k, uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out, int out_width,
+               uintptr_t out_len, uintptr_t out_rows, uintptr_t stream);
+void arena_scatter(int k, uintptr_t rows, uintptr_t src, int src_width, uintptr_t src_len, uintptr_t arena, int width,
+                   uintptr_t lens, uintptr_t mark, uint64_t gen, uintptr_t flags, uintptr_t stream);
 void place_collect(int k, uintptr_t wins, uintptr_t cells, uintptr_t result, int C, uintptr_t par, uintptr_t npos,
                    uintptr_t stream);
 // select.hip
+std::tuple<int, int, int> translate_stats(int n, uintptr_t counts, uintptr_t ndom, uintptr_t long_count, uintptr_t per,
+                                          uintptr_t stream);
 std::pair<long long, int> select_indices(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel,
                                          uintptr_t rest, uintptr_t stream);
 }  // namespace msd
@@ -137,7 +141,10 @@ PYBIND11_MODULE(_hip, m) {
   m.def("mut_apply", &msd::mut_apply);
   m.def("rec_count", &msd::rec_count);
   m.def("rec_apply", &msd::rec_apply);
+  m.def("arena_scatter", &msd::arena_scatter);
   m.def("place_collect", &msd::place_collect);
+  m.def("translate_stats", &msd::translate_stats,
+        "(max proteins, max domains, long genomes) of a translate count pass; synchronises the stream");
   m.def("select_indices", &msd::select_indices,
         "(count, max) of an order-preserving compaction; synchronises the stream");
 }

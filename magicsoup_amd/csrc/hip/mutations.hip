@@ -154,15 +154,17 @@ __global__ void __launch_bounds__(256) rec_count_kernel(int n, const int32_t* pa
 
 // Same draw over fixed neighbour slots (int64 keys (a << 32) | b, -1 = empty slot).
 __global__ void __launch_bounds__(256) rec_count_keys_kernel(int n, const int64_t* keys, const int32_t* lens, double p,
-                                                             uint64_t seed, uint64_t call, int32_t* k) {
+                                                             uint64_t seed, uint64_t call, int32_t* k, int32_t* tot) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t key = keys[i];
   if (key < 0) {
     k[i] = 0;
+    if (tot) tot[i] = 0;
     return;
   }
   const int nb = lens[key >> 32] + lens[key & 0xFFFFFFFF];
+  if (tot) tot[i] = nb;
   if (nb < 1) {
     k[i] = 0;
     return;
@@ -177,15 +179,18 @@ __global__ void __launch_bounds__(256) rec_count_keys_kernel(int n, const int64_
 // lane 0 plans the parts (LDS for up to kFloydMax cuts, else the global `parts` scratch with
 // parts_cap entries of 3 ints), then all lanes copy them.
 __global__ void __launch_bounds__(64) rec_apply_kernel(int nsel, const int64_t* sel, const int32_t* pairs,
-                                                       const uint8_t* arena, int width, const int32_t* lens,
-                                                       const int32_t* k, uint64_t seed, uint64_t call, int32_t* parts,
-                                                       int parts_cap, uint8_t* out, int out_width, int32_t* out_len) {
+                                                       const int64_t* keys, const uint8_t* arena, int width,
+                                                       const int32_t* lens, const int32_t* k, uint64_t seed,
+                                                       uint64_t call, int32_t* parts, int parts_cap, uint8_t* out,
+                                                       int out_width, int32_t* out_len, int64_t* out_rows) {
   __shared__ int32_t lparts[(kFloydMax + 2) * 3];
   __shared__ int meta[2];  // number of parts, split index
   const int j = blockIdx.x, lane = threadIdx.x;
   if (j >= nsel) return;
   const int64_t i = sel[j];
-  const int ca = pairs[2 * i], cb = pairs[2 * i + 1];
+  // pairs: int32 (a, b) rows, or int64 slot keys (a << 32) | b
+  const int ca = keys ? (int)(keys[i] >> 32) : pairs[2 * i];
+  const int cb = keys ? (int)(keys[i] & 0xFFFFFFFF) : pairs[2 * i + 1];
   const int n0 = lens[ca], n1 = lens[cb], nb = n0 + n1;
   const int kk = k[i];
   int32_t* pt = kk <= kFloydMax ? lparts : parts + (size_t)j * parts_cap * 3;
@@ -265,7 +270,41 @@ __global__ void __launch_bounds__(64) rec_apply_kernel(int nsel, const int64_t* 
   if (lane == 0) {
     out_len[2 * j] = w0 < out_width ? w0 : out_width;
     out_len[2 * j + 1] = w1 < out_width ? w1 : out_width;
+    if (out_rows) {
+      out_rows[2 * j] = ca;
+      out_rows[2 * j + 1] = cb;
+    }
   }
+}
+
+// ---------------------------------------------------------------- arena commit
+// Last writer wins among duplicate target rows (a cell in several recombined pairs keeps the
+// result of the last pair, as the reference's sequential update does): generation-tagged 64-bit
+// marks, so the mark array never needs clearing.
+__global__ void __launch_bounds__(256) arena_mark_kernel(int k, const int64_t* rows, unsigned long long* mark,
+                                                         unsigned long long gen) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= k) return;
+  atomicMax(mark + rows[q], (gen << 32) | (unsigned long long)q);
+}
+
+// One wavefront per result row: copy it over its arena row (zero-padding the rest of the row) and
+// its length, if it won; flags[q] = won.
+__global__ void __launch_bounds__(64) arena_scatter_kernel(int k, const int64_t* rows, const uint8_t* src, int src_width,
+                                                           const int32_t* src_len, uint8_t* arena, int width,
+                                                           int32_t* lens, const unsigned long long* mark,
+                                                           unsigned long long gen, uint8_t* flags) {
+  const int q = blockIdx.x, lane = threadIdx.x;
+  if (q >= k) return;
+  const int64_t r = rows[q];
+  const bool won = !mark || mark[r] == ((gen << 32) | (unsigned long long)q);
+  if (lane == 0 && flags) flags[q] = won;
+  if (!won) return;
+  const int L = min(src_len[q], width);
+  const uint8_t* s = src + (size_t)q * src_width;
+  uint8_t* d = arena + (size_t)r * width;
+  for (int t = lane; t < width; t += 64) d[t] = t < L ? s[t] : 0;
+  if (lane == 0) lens[r] = L;
 }
 
 void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
@@ -296,21 +335,37 @@ void rec_count(int n, uintptr_t pairs, uintptr_t lens, double p, uint64_t seed, 
 }
 
 void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
-                    uintptr_t stream) {
+                    uintptr_t tot, uintptr_t stream) {
   if (n <= 0) return;
   rec_count_keys_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, P_<int64_t>(keys), P_<int32_t>(lens), p, seed, call,
-                                                              P_<int32_t>(k));
+                                                              P_<int32_t>(k), tot ? P_<int32_t>(tot) : nullptr);
   MS_LAUNCH_CHECK();
 }
 
-void rec_apply(int nsel, uintptr_t sel, uintptr_t pairs, uintptr_t arena, int width, uintptr_t lens, uintptr_t k,
-               uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out, int out_width,
-               uintptr_t out_len, uintptr_t stream) {
+void rec_apply(int nsel, uintptr_t sel, uintptr_t pairs, uintptr_t keys, uintptr_t arena, int width, uintptr_t lens,
+               uintptr_t k, uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out, int out_width,
+               uintptr_t out_len, uintptr_t out_rows, uintptr_t stream) {
   if (nsel <= 0) return;
-  rec_apply_kernel<<<nsel, 64, 0, S_(stream)>>>(nsel, P_<int64_t>(sel), P_<int32_t>(pairs),
-                                                          P_<uint8_t>(arena), width, P_<int32_t>(lens), P_<int32_t>(k),
-                                                          seed, call, P_<int32_t>(parts), parts_cap, P_<uint8_t>(out),
-                                                          out_width, P_<int32_t>(out_len));
+  if ((pairs == 0) == (keys == 0)) throw std::invalid_argument("rec_apply: give exactly one of pairs / keys");
+  rec_apply_kernel<<<nsel, 64, 0, S_(stream)>>>(nsel, P_<int64_t>(sel), pairs ? P_<int32_t>(pairs) : nullptr,
+                                                keys ? P_<int64_t>(keys) : nullptr, P_<uint8_t>(arena), width,
+                                                P_<int32_t>(lens), P_<int32_t>(k), seed, call, P_<int32_t>(parts),
+                                                parts_cap, P_<uint8_t>(out), out_width, P_<int32_t>(out_len),
+                                                out_rows ? P_<int64_t>(out_rows) : nullptr);
+  MS_LAUNCH_CHECK();
+}
+
+void arena_scatter(int k, uintptr_t rows, uintptr_t src, int src_width, uintptr_t src_len, uintptr_t arena, int width,
+                   uintptr_t lens, uintptr_t mark, uint64_t gen, uintptr_t flags, uintptr_t stream) {
+  if (k <= 0) return;
+  if (mark) {
+    arena_mark_kernel<<<cdiv(k, 256), 256, 0, S_(stream)>>>(k, P_<int64_t>(rows), P_<unsigned long long>(mark), gen);
+    MS_LAUNCH_CHECK();
+  }
+  arena_scatter_kernel<<<k, 64, 0, S_(stream)>>>(k, P_<int64_t>(rows), P_<uint8_t>(src), src_width,
+                                                 P_<int32_t>(src_len), P_<uint8_t>(arena), width, P_<int32_t>(lens),
+                                                 mark ? P_<unsigned long long>(mark) : nullptr, gen,
+                                                 flags ? P_<uint8_t>(flags) : nullptr);
   MS_LAUNCH_CHECK();
 }
 

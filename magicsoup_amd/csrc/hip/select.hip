@@ -12,6 +12,7 @@
 //
 // Predicates: u8 mask != 0, u8 mask == 0, int32 > 0, int64 >= 0.
 #include <algorithm>
+#include <tuple>
 
 #include "hip_common.h"
 
@@ -126,12 +127,74 @@ __global__ void __launch_bounds__(kSelThreads) select_write_kernel(long long n, 
   }
 }
 
+// Per-genome protein totals (fwd + rev) and the maxima a translate count pass needs on the host.
+// Block maxima are combined with atomicMax in a device accumulator; the last block to finish
+// (done counter) publishes {max proteins, max domains, long genomes} to pinned host memory and
+// resets the accumulator for the next call.
+__global__ void __launch_bounds__(256) translate_stats_kernel(int n, const int32_t* counts, const int32_t* ndom,
+                                                              const int32_t* long_count, int32_t* per, int32_t* acc,
+                                                              int32_t* host_out) {
+  int mp = 0, md = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int p = counts[2 * i] + counts[2 * i + 1];
+    per[i] = p;
+    mp = max(mp, p);
+    md = max(md, max(ndom[2 * i], ndom[2 * i + 1]));
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mp = max(mp, __shfl_xor(mp, o));
+    md = max(md, __shfl_xor(md, o));
+  }
+  if (lane_id() == 0) {
+    atomicMax(acc, mp);
+    atomicMax(acc + 1, md);
+  }
+  __threadfence();
+  __syncthreads();
+  __shared__ bool last;
+  if (threadIdx.x == 0) last = atomicAdd(acc + 2, 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    __threadfence();
+    host_out[0] = atomicExch(acc, 0);
+    host_out[1] = atomicExch(acc + 1, 0);
+    host_out[2] = *long_count;
+    acc[2] = 0;
+  }
+}
+
 namespace {
 int32_t* g_host = nullptr;  // pinned, coherent {count, max}
 int32_t* g_host_dev = nullptr;
 int32_t* g_tiles = nullptr;  // device {count[tiles], max[tiles]}
 long long g_tiles_cap = 0;
+int32_t* g_tacc = nullptr;  // device {max proteins, max domains, done blocks}, zero between calls
+
+void ensure_host() {
+  if (!g_host) {
+    MS_HIP_CHECK(hipHostMalloc((void**)&g_host, 4 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
+    MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_host_dev, g_host, 0));
+  }
+}
 }  // namespace
+
+std::tuple<int, int, int> translate_stats(int n, uintptr_t counts, uintptr_t ndom, uintptr_t long_count, uintptr_t per,
+                                          uintptr_t stream) {
+  if (n <= 0) return {0, 0, 0};
+  ensure_host();
+  if (!g_tacc) {
+    MS_HIP_CHECK(hipMalloc((void**)&g_tacc, 4 * sizeof(int32_t)));
+    MS_HIP_CHECK(hipMemset(g_tacc, 0, 4 * sizeof(int32_t)));
+  }
+  g_host[0] = -1;
+  const unsigned grid = std::min(cdiv(n, 256), 1024u);
+  translate_stats_kernel<<<grid, 256, 0, S_(stream)>>>(n, P_<int32_t>(counts), P_<int32_t>(ndom),
+                                                      P_<int32_t>(long_count), P_<int32_t>(per), g_tacc, g_host_dev);
+  MS_LAUNCH_CHECK();
+  MS_HIP_CHECK(hipStreamSynchronize(S_(stream)));
+  if (g_host[0] < 0) throw std::runtime_error("translate_stats: bad read-back");
+  return {g_host[0], g_host[1], g_host[2]};
+}
 
 // Returns {count, max(vals over selected)}; synchronises `stream`. sel must hold n entries (rest too,
 // when given). Writes nothing and returns {0, 0} for n == 0.
@@ -139,10 +202,7 @@ std::pair<long long, int> select_indices(long long n, int kind, uintptr_t src, u
                                          uintptr_t rest, uintptr_t stream) {
   if (n <= 0) return {0, 0};
   if (n >= (1ll << 40)) throw std::invalid_argument("select_indices: n too large");
-  if (!g_host) {
-    MS_HIP_CHECK(hipHostMalloc((void**)&g_host, 2 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
-    MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_host_dev, g_host, 0));
-  }
+  ensure_host();
   const long long tiles = (n + kSelTile - 1) / kSelTile;
   if (tiles > g_tiles_cap) {
     if (g_tiles) MS_HIP_CHECK(hipFree(g_tiles));

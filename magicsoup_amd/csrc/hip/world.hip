@@ -144,14 +144,78 @@ __global__ void __launch_bounds__(256) place_collect_kernel(int k, const int64_t
   npos[2 * i + 1] = (int32_t)(px - (px / C) * C);
 }
 
+// Small placement batches: all rounds in one workgroup (rounds separated by __syncthreads instead
+// of kernel boundaries), same bids / priorities / RNG streams as the multi-launch path.
+__global__ void __launch_bounds__(1024) place_rounds_wg_kernel(int k, const int64_t* cells, const int32_t* pos, Geom g,
+                                                               bool vacate, uint8_t* cell_map, uint8_t* pending,
+                                                               uint64_t seed, uint64_t call, long long* cand,
+                                                               int* claim, long long* result, int rounds) {
+  for (int r = 0; r < rounds; ++r) {
+    const uint64_t rc = call + ((uint64_t)r << 48);
+    for (int i = threadIdx.x; i < k; i += blockDim.x) {
+      if (!pending[i]) continue;
+      const int c = (int)cells[i];
+      long long nb[8], fr[8];
+      const int cnt = moore(pos[2 * c], pos[2 * c + 1], g, nb);
+      int nf = 0;
+      for (int q = 0; q < cnt; ++q)
+        if (!cell_map[nb[q]]) fr[nf++] = nb[q];
+      if (nf == 0) {
+        pending[i] = 0;
+        cand[i] = -1;
+        continue;
+      }
+      Philox rng(seed, rc, (uint32_t)i);
+      const long long px = fr[rng.below((uint32_t)nf)];
+      cand[i] = px;
+      atomicMin(claim + px, i);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < k; i += blockDim.x) {
+      if (!pending[i]) continue;
+      const long long px = cand[i];
+      if (px < 0 || claim[px] != i) continue;
+      result[i] = px;
+      pending[i] = 0;
+      cell_map[px] = 1;
+      const int x = (int)(px / g.C);
+      if (vacate && (g.wrap || (x >= g.r_lo && x < g.r_hi))) {
+        const int c = (int)cells[i];
+        cell_map[(size_t)pos[2 * c] * g.C + pos[2 * c + 1]] = 0;
+      }
+    }
+    __syncthreads();
+    // winners reset their pixel's claim only after every loser has compared against it
+    for (int i = threadIdx.x; i < k; i += blockDim.x) {
+      const long long px = cand[i];
+      if (px >= 0 && result[i] == px) claim[px] = kNoClaim;
+    }
+    __syncthreads();
+  }
+  // losers of the last round may still hold claims
+  for (int i = threadIdx.x; i < k; i += blockDim.x) {
+    const long long px = cand[i];
+    if (px >= 0) atomicCAS(claim + px, i, kNoClaim);
+  }
+}
+
 // ---------------------------------------------------------------- neighbours
+// The pixel -> cell index map is never cleared: index_map() writes every current cell's index, and a
+// reader accepts an entry only if that cell still sits on the pixel (stale entries of dead or moved
+// cells fail the check). Saves a clearing launch per neighbour query.
+__device__ __forceinline__ int cell_at(const int32_t* idx_map, const int32_t* pos, int n, int C, long long px) {
+  const int o = idx_map[px];
+  if (o < 0 || o >= n) return -1;
+  return ((long long)pos[2 * o] * C + pos[2 * o + 1]) == px ? o : -1;
+}
+
 __global__ void __launch_bounds__(256) index_map_kernel(int c, const int32_t* pos, int C, int32_t* idx_map, bool clear) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= c) return;
   idx_map[(size_t)pos[2 * i] * C + pos[2 * i + 1]] = clear ? -1 : i;
 }
 
-__global__ void __launch_bounds__(256) neighbor_pairs_kernel(int nf, const int64_t* from, const int32_t* pos, Geom g,
+__global__ void __launch_bounds__(256) neighbor_pairs_kernel(int nf, int n, const int64_t* from, const int32_t* pos, Geom g,
                                                              const int32_t* idx_map, const uint8_t* in_from,
                                                              const uint8_t* in_to, int* counter, int cap,
                                                              int64_t* pairs) {
@@ -161,7 +225,7 @@ __global__ void __launch_bounds__(256) neighbor_pairs_kernel(int nf, const int64
   long long nb[8];
   const int cnt = moore(pos[2 * c], pos[2 * c + 1], g, nb);
   for (int q = 0; q < cnt; ++q) {
-    const int o = idx_map[nb[q]];
+    const int o = cell_at(idx_map, pos, n, g.C, nb[q]);
     if (o < 0 || o == c || !in_to[o]) continue;
     if (in_from[o] && in_to[c] && o < c) continue;  // found from the other side
     const int slot = atomicAdd(counter, 1);
@@ -181,7 +245,7 @@ __global__ void __launch_bounds__(256) neighbor_slots_kernel(int n, const int32_
   for (int q = 0; q < 8; ++q) {
     int64_t key = -1;
     if (q < cnt) {
-      const int o = idx_map[nb[q]];
+      const int o = cell_at(idx_map, pos, n, g.C, nb[q]);
       if (o > c) key = ((int64_t)c << 32) | o;
     }
     keys[(size_t)c * 8 + q] = key;
@@ -213,11 +277,21 @@ void claim_free(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uin
   MS_LAUNCH_CHECK();
 }
 
+constexpr int kPlaceWgMax = 2048;  // single-workgroup rounds up to this many cells (one CU: ~2 cells per thread)
+
 void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, bool vacate,
                   uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result, int rounds,
                   uint64_t seed, uint64_t call, uintptr_t stream) {
   if (k <= 0) return;
   const Geom g = geom(R, C, r_lo, r_hi, wrap);
+  if (k <= kPlaceWgMax) {
+    place_rounds_wg_kernel<<<1, 1024, 0, S_(stream)>>>(k, P_<int64_t>(cells), P_<int32_t>(pos), g, vacate,
+                                                       P_<uint8_t>(cell_map), P_<uint8_t>(pending), seed, call,
+                                                       P_<long long>(cand), P_<int>(claim), P_<long long>(result),
+                                                       rounds);
+    MS_LAUNCH_CHECK();
+    return;
+  }
   const unsigned grid = cdiv(k, 256);
   for (int r = 0; r < rounds; ++r) {
     place_bid_kernel<<<grid, 256, 0, S_(stream)>>>(k, P_<int64_t>(cells), P_<int32_t>(pos), g, P_<uint8_t>(cell_map),
@@ -255,11 +329,11 @@ void neighbor_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int 
   MS_LAUNCH_CHECK();
 }
 
-void neighbor_pairs(int nf, uintptr_t from, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map,
+void neighbor_pairs(int nf, int n, uintptr_t from, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map,
                     uintptr_t in_from, uintptr_t in_to, uintptr_t counter, int cap, uintptr_t pairs, uintptr_t stream) {
   if (nf <= 0) return;
   const Geom g = geom(R, C, r_lo, r_hi, wrap);
-  neighbor_pairs_kernel<<<cdiv(nf, 256), 256, 0, S_(stream)>>>(nf, P_<int64_t>(from), P_<int32_t>(pos), g,
+  neighbor_pairs_kernel<<<cdiv(nf, 256), 256, 0, S_(stream)>>>(nf, n, P_<int64_t>(from), P_<int32_t>(pos), g,
                                                                P_<int32_t>(idx_map), P_<uint8_t>(in_from),
                                                                P_<uint8_t>(in_to), P_<int>(counter), cap,
                                                                P_<int64_t>(pairs));

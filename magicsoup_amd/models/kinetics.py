@@ -614,9 +614,27 @@ class Kinetics:
         """Grow the protein dimension of every parameter tensor to ``max_n`` (zero-filled)."""
         if max_n <= self._P():
             return
+        store = self._store
+        dev = store["N"].device
+        if dev.type == "cuda":
+            # widen in place of the row storage: every storage row (cell rows, free rows) keeps its
+            # index, so the cell -> row map stays valid and nothing is gathered back to cell order
+            from magicsoup_amd.ops import hip_ops
+
+            d = self.__dict__
+            nrows = d["_nrows"] if d["_slot"] is not None else d["_ncells"]
+            ok = self._pack_ok()
+            moves = []
+            for name, t in list(store.items()):
+                nb = torch.zeros(t.size(0), max_n, *t.shape[2:], dtype=t.dtype, device=dev)
+                moves.append((t, nb))
+                store[name] = nb
+            hip_ops.copy_row_prefixes(moves, nrows)
+            d.pop("_spare", None)
+            self._restamp(ok)
+            return
         self._materialize()
         ok = self._pack_ok()
-        store = self._store
         n = self.__dict__["_ncells"]
         for name, t in list(store.items()):
             t = t[:n]

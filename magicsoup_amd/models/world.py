@@ -496,7 +496,11 @@ class World:
         n0 = self.n_cells
         children = torch.arange(n0, n0 + k, device=self.device)
         self._clone_rows(parents, children)
-        self._place(children, child_pos)
+        if child_pos.is_cuda:
+            # the placement kernels already claimed the pixels in cell_map
+            self.cell_positions[n0 : n0 + k] = child_pos
+        else:
+            self._place(children, child_pos)
         world_ops.split_cells(self, parents, children)
         return parents, children
 
@@ -673,7 +677,12 @@ class World:
             return
         data, lens = self._genomes.view()
         tokens, nprots = world_ops.translate(self, data, lens, rows)
-        self.kinetics.increase_max_proteins(int(tokens.size(1)))
+        P = int(tokens.size(1))
+        if P > self.kinetics._P():
+            # a new longest proteome: grow with headroom on the GPU so that mutations creeping the
+            # maximum up do not re-layout all parameter tensors every few steps (padding proteins are
+            # inert: Vmax 0)
+            self.kinetics.increase_max_proteins(P + max(4, P // 4) if data.is_cuda else P)
         # one build launch: rows without proteins are unset in the same pass
         self.kinetics.set_cell_params_tokens(rows, tokens, nprot=nprots)
 

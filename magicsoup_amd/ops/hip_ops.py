@@ -443,8 +443,24 @@ def gather_rows(pairs, n: int, src_rows: torch.Tensor | None = None, dst_rows: t
     _m().gather_rows(int(n), _p(sr), _p(dr), descs, _stream())
 
 
+def copy_row_prefixes(moves, n: int) -> None:
+    """dst[i, :P_src] = src[i] for rows i < n of every (src (rows, P_src, ...), dst (rows, P_dst, ...))
+    pair with P_dst >= P_src (a wider protein dimension), in one launch: a source row is the
+    contiguous prefix of the destination row."""
+    descs = []
+    for src, dst in moves:
+        es = src.element_size()
+        rb = src[0].numel() * es if src.size(0) else 0
+        assert src.is_contiguous() and dst.is_contiguous() and dst.dtype == src.dtype
+        if rb:
+            descs.append((src.data_ptr(), dst.data_ptr(), src.stride(0) * es, dst.stride(0) * es, rb))
+    if n > 0 and descs:
+        _m().gather_rows(int(n), 0, 0, descs, _stream())
+
+
 def _index_map(world, npix: int, dev) -> torch.Tensor:
-    """Pixel -> cell index map (int32, -1 = empty), kept all -1 between uses."""
+    """Pixel -> cell index map (int32). Never cleared: an entry counts only if the cell it names still
+    sits on that pixel (world.hip cell_at), so stale entries of dead / moved cells are harmless."""
     idx_map = world.__dict__.get("_idx_map")
     if idx_map is None or idx_map.numel() != npix or idx_map.device != dev:
         idx_map = torch.full((npix,), -1, dtype=torch.int32, device=dev)
@@ -462,7 +478,7 @@ def neighbors(world, frm: torch.Tensor, to: torch.Tensor, pos: torch.Tensor | No
         pos, n = world.cell_positions, world.n_cells
     sc = _scratch(world)
     idx_map = _index_map(world, R * C, dev)
-    _m().index_map(n, _p(pos), C, _p(idx_map), False, _stream())
+    _m().index_map(n, _p(pos), C, _p(idx_map), False, _stream())  # readers skip stale entries
     in_from = sc.get("nb_from", n, torch.uint8, dev, zero=True)
     in_to = sc.get("nb_to", n, torch.uint8, dev, zero=True)
     in_from[frm] = 1
@@ -471,10 +487,9 @@ def neighbors(world, frm: torch.Tensor, to: torch.Tensor, pos: torch.Tensor | No
     cap = 8 * int(frm64.numel())
     pairs = sc.get("nb_pairs", cap, torch.int64, dev)
     counter = sc.get("nb_count", 1, torch.int32, dev, zero=True)
-    _m().neighbor_pairs(int(frm64.numel()), _p(frm64), _p(pos), R, C, r_lo, r_hi, wrap, _p(idx_map), _p(in_from),
+    _m().neighbor_pairs(int(frm64.numel()), int(n), _p(frm64), _p(pos), R, C, r_lo, r_hi, wrap, _p(idx_map), _p(in_from),
                         _p(in_to), _p(counter), cap, _p(pairs), _stream())
     cnt = int(counter.item())
-    _m().index_map(n, _p(pos), C, _p(idx_map), True, _stream())  # leave the map all -1
     keys = torch.sort(pairs[:cnt]).values
     if keys.numel() > 1:
         keys = torch.unique_consecutive(keys)
@@ -501,16 +516,15 @@ def translate(genetics, data: torch.Tensor, lens: torch.Tensor, rows: torch.Tens
               tables.dom_size, tables.dom_type_size)
     _m().translate_count(n, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), _p(ndom), 0, 0,
                          _p(long_list), _p(long_count), _stream())
-    per = counts.view(n, 2).sum(1)
-    stats = torch.stack([per.max(), ndom.max(), long_count[0]]).tolist() if n else [0, 0, 0]
+    per = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
+    stats = _m().translate_stats(n, _p(counts), _p(ndom), _p(long_count), _p(per), _stream())
     n_long = int(stats[2])
     gslot = None
     if n_long:
         gslot = torch.empty(n_long * int(_m().translate_slot_bytes(width)), dtype=torch.uint8, device=dev)
         _m().translate_count(n_long, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), _p(ndom),
                              _p(long_list), _p(gslot), _p(long_list), _p(long_count), _stream())
-        per = counts.view(n, 2).sum(1)
-        stats = torch.stack([per.max(), ndom.max()]).tolist()
+        stats = _m().translate_stats(n, _p(counts), _p(ndom), _p(long_count), _p(per), _stream())
     P, D = max(int(stats[0]), 1), max(int(stats[1]), 1)
     tokens = torch.zeros(n, P, D, 5, dtype=torch.int32, device=dev)
     _m().translate_write(n, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), P, D, _p(tokens), 0, 0,
@@ -519,6 +533,32 @@ def translate(genetics, data: torch.Tensor, lens: torch.Tensor, rows: torch.Tens
         _m().translate_write(n_long, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), P, D, _p(tokens),
                              _p(long_list), _p(gslot), _stream())
     return tokens, per
+
+
+def _arena_commit(arena, rows: torch.Tensor, out: torch.Tensor, out_len: torch.Tensor, need_width: int,
+                  dedupe: bool = False, owner=None) -> torch.Tensor:
+    """Write result rows ``out`` (k, w) / ``out_len`` over the arena rows ``rows`` in one launch
+    (arena_scatter); widens the arena first if a result may not fit. With ``dedupe`` the last result
+    per row wins and the winning rows are returned (one more select)."""
+    k = int(rows.numel())
+    if need_width > arena.width:
+        arena.reserve(arena.n, need_width)
+    mark, gen, flags = None, 0, None
+    if dedupe:
+        sc = _scratch(owner)
+        mark = sc.bufs.get("arena_mark")
+        if mark is None or mark.numel() < arena.n:
+            mark = sc.bufs["arena_mark"] = torch.zeros(max(arena.n, 1024) * 2, dtype=torch.int64, device=rows.device)
+            sc.bufs["arena_gen"] = 0
+        gen = sc.bufs["arena_gen"] = sc.bufs.get("arena_gen", 0) + 1
+        flags = torch.empty(k, dtype=torch.uint8, device=rows.device)
+    _m().arena_scatter(k, _p(rows), _p(out), int(out.stride(0)), _p(out_len), _p(arena.data), int(arena.width),
+                       _p(arena.lens), _p(mark), int(gen), _p(flags), _stream())
+    arena.version += 1
+    if not dedupe:
+        return rows
+    won = select(flags, "set")[0]
+    return rows[won]
 
 
 def point_mutations(world, rows, p: float, p_indel: float, p_del: float) -> torch.Tensor:
@@ -539,12 +579,14 @@ def point_mutations(world, rows, p: float, p_indel: float, p_del: float) -> torc
         return torch.zeros(0, dtype=torch.long, device=dev)
     tgt = sel if rows64 is None else rows64[sel]
     out_w = max(bound, 1)
-    out = torch.zeros(nsel, out_w, dtype=torch.uint8, device=dev)
+    out = torch.empty(nsel, out_w, dtype=torch.uint8, device=dev)
     out_len = torch.empty(nsel, dtype=torch.int32, device=dev)
     _m().mut_apply(nsel, _p(sel), _p(rows64), _p(arena.data), int(arena.data.size(1)), _p(arena.lens), _p(k),
                    float(p_indel), float(p_del), seed, call, _p(out), out_w, _p(out_len), _stream())
-    arena.set_rows(tgt, out, out_len)
-    return tgt
+    if rows64 is not None and nsel > 1:
+        # explicit rows may repeat (mutate_cells([i, i])): the last mutated copy wins
+        return _arena_commit(arena, tgt, out, out_len, bound, dedupe=True, owner=world)
+    return _arena_commit(arena, tgt, out, out_len, bound)
 
 
 def recombinations(world, pairs: torch.Tensor, p: float) -> torch.Tensor:
@@ -555,7 +597,8 @@ def recombinations(world, pairs: torch.Tensor, p: float) -> torch.Tensor:
     k = torch.empty(n, dtype=torch.int32, device=dev)
     seed, call = _rng()
     _m().rec_count(n, _p(pairs), _p(arena.lens), float(p), seed, call, _p(k), _stream())
-    return _rec_apply(world, pairs, k, seed, call)
+    tot = arena.lens[pairs[:, 0].long()] + arena.lens[pairs[:, 1].long()] if n else k
+    return _rec_apply(world, pairs, None, k, tot, seed, call)
 
 
 def recombinate_all(world, p: float) -> torch.Tensor:
@@ -565,11 +608,12 @@ def recombinate_all(world, p: float) -> torch.Tensor:
     dev = arena.data.device
     n = world.n_cells
     keys = neighbor_slot_keys(world)
-    k = _scratch(world).get("nb_k", 8 * n, torch.int32, dev)
+    sc = _scratch(world)
+    k = sc.get("nb_k", 8 * n, torch.int32, dev)
+    tot = sc.get("nb_tot", 8 * n, torch.int32, dev)
     seed, call = _rng()
-    _m().rec_count_keys(8 * n, _p(keys), _p(arena.lens), float(p), seed, call, _p(k), _stream())
-    pairs = torch.stack([keys >> 32, keys & 0xFFFFFFFF], dim=1).to(torch.int32)
-    return _rec_apply(world, pairs, k, seed, call)
+    _m().rec_count_keys(8 * n, _p(keys), _p(arena.lens), float(p), seed, call, _p(k), _p(tot), _stream())
+    return _rec_apply(world, None, keys, k, tot, seed, call)
 
 
 def neighbor_slot_keys(world) -> torch.Tensor:
@@ -584,35 +628,26 @@ def neighbor_slot_keys(world) -> torch.Tensor:
     _m().index_map(n, _p(pos), C, _p(idx_map), False, _stream())
     keys = _scratch(world).get("nb_keys", 8 * n, torch.int64, dev)
     _m().neighbor_slots(n, _p(pos), R, C, r_lo, r_hi, wrap, _p(idx_map), _p(keys), _stream())
-    _m().index_map(n, _p(pos), C, _p(idx_map), True, _stream())
     return keys
 
 
-def _rec_apply(world, pairs: torch.Tensor, k: torch.Tensor, seed: int, call: int) -> torch.Tensor:
+def _rec_apply(world, pairs, keys, k: torch.Tensor, tot: torch.Tensor, seed: int, call: int) -> torch.Tensor:
+    """Recombine the selected pairs (``pairs`` int32 (n, 2) or slot ``keys`` int64 (a << 32) | b)
+    and commit both results of every pair; a cell in several pairs keeps its last pair's result.
+    One sync selects the pairs (with the longest possible result), one more the committed cells."""
     arena = world._genomes
     dev = arena.data.device
-    sel, _, kmax = select(k, "i32pos", vals=k)
+    sel, _, bound = select(k, "i32pos", vals=tot)
     nsel = int(sel.numel())
     if nsel == 0:
         return torch.zeros(0, dtype=torch.long, device=dev)
-    sp = pairs[sel].long()
-    out_w, parts_cap = 2 * int(arena.width), kmax + 2  # a recombined genome is at most both parents
-    out = torch.zeros(2 * nsel, out_w, dtype=torch.uint8, device=dev)
+    # a recombined genome is at most both parents; k <= that length bounds the parts workspace
+    out_w, parts_cap = max(bound, 1), max(bound, 1) + 2
+    out = torch.empty(2 * nsel, out_w, dtype=torch.uint8, device=dev)
     out_len = torch.empty(2 * nsel, dtype=torch.int32, device=dev)
+    out_rows = torch.empty(2 * nsel, dtype=torch.int64, device=dev)
     parts = torch.empty(nsel * parts_cap * 3, dtype=torch.int32, device=dev)
-    _m().rec_apply(nsel, _p(sel), _p(pairs), _p(arena.data), int(arena.data.size(1)), _p(arena.lens), _p(k),
-                   seed, call, _p(parts), parts_cap, _p(out), out_w, _p(out_len), _stream())
-    # rare path (p = 1e-7 per bp): trim the scratch width to the longest result so the arena only
-    # widens when a genome actually outgrows it
-    out = out[:, : max(int(out_len.max().item()), 1)]
-    cells = sp.reshape(-1)  # (a0, b0, a1, b1, ...) matches the scratch row order
-    # the last recombination that touched a cell wins (reference update order)
-    order = torch.arange(cells.numel(), device=dev)
-    key = cells * cells.numel() + order
-    srt = torch.sort(key).values
-    last = torch.ones_like(srt, dtype=torch.bool)
-    last[:-1] = (srt[:-1] // cells.numel()) != (srt[1:] // cells.numel())
-    pick = srt[last] % cells.numel()
-    tgt = cells[pick]
-    arena.set_rows(tgt, out[pick], out_len[pick])
-    return tgt
+    _m().rec_apply(nsel, _p(sel), _p(pairs), _p(keys), _p(arena.data), int(arena.data.size(1)), _p(arena.lens), _p(k),
+                   seed, call, _p(parts), parts_cap, _p(out), out_w, _p(out_len), _p(out_rows), _stream())
+    # (a0, b0, a1, b1, ...) in pair order: the last write per cell wins (reference update order)
+    return _arena_commit(arena, out_rows, out, out_len, bound, dedupe=True, owner=world)

@@ -308,7 +308,7 @@ def test_param_row_storage_fuzz_matches_dense_model():
     X = torch.rand(kin.N.size(0), kin.N.size(2), device="cuda") * 5
     for step in range(60):
         n = kin.__dict__["_ncells"]
-        op = rng.choice(["kill", "grow", "copy", "integrate"])
+        op = rng.choice(["kill", "grow", "copy", "integrate", "widen"])
         if op == "kill" and n > 10:
             keep = torch.rand(n, device="cuda") > 0.3
             kin.remove_cell_params(keep)
@@ -322,6 +322,15 @@ def test_param_row_storage_fuzz_matches_dense_model():
                 z = torch.zeros(k_new, *model[k].shape[1:], dtype=model[k].dtype, device="cuda")
                 model[k] = torch.cat([model[k], z])
             X = torch.cat([X, torch.rand(k_new, X.size(1), device="cuda") * 5])
+        elif op == "widen":
+            # protein dimension grows in place of the row storage (slot map kept)
+            p_new = kin.N.size(1) + rng.randint(1, 3) if kin.__dict__["_slot"] is None else kin._P() + rng.randint(1, 3)
+            kin.increase_max_proteins(p_new)
+            for k in names:
+                t = model[k]
+                if t.dim() >= 2 and t.size(1) < p_new:
+                    z = torch.zeros(t.size(0), p_new - t.size(1), *t.shape[2:], dtype=t.dtype, device="cuda")
+                    model[k] = torch.cat([t, z], dim=1)
         elif op == "copy" and n > 4:
             src = torch.randperm(n, device="cuda")[: n // 4]
             dst = torch.randperm(n, device="cuda")[: n // 4]
@@ -364,3 +373,47 @@ def test_select_matches_nonzero(n):
     assert mx == (int(vals[ref].max()) if ref.numel() else 0)
     r = torch.randint(-3, 3, (n,), dtype=torch.int64, device="cuda", generator=g)
     assert torch.equal(hip_ops.select(r, "i64nonneg")[0], torch.nonzero(r >= 0).flatten())
+
+
+@pytest.mark.parametrize("n", [500, 6_000])
+def test_divide_placement_both_paths_keep_occupancy_consistent(n):
+    """Single-workgroup placement rounds (k <= 2048) and the multi-launch path (larger k) both
+    leave one cell per pixel, children in a parent's Moore neighbourhood and cell_map in sync."""
+    w = _world("cuda", map_size=256, n=n, s=200)
+    par, chi = w.divide_cells_t(torch.arange(w.n_cells, device="cuda"))
+    assert par.numel() > 0.5 * n
+    pos = w.cell_positions.long()
+    key = pos[:, 0] * 256 + pos[:, 1]
+    assert torch.unique(key).numel() == w.n_cells
+    assert int(w.cell_map.sum()) == w.n_cells
+    d = (pos[par] - pos[chi]).abs()
+    d = torch.minimum(d, 256 - d)
+    assert bool((d.max(dim=1).values == 1).all())
+
+
+def test_recombination_commit_on_gpu():
+    """Fused recombination commit: disjoint pairs conserve their total length; a cell in several
+    pairs keeps one of its results; arena lengths match the materialised strings."""
+    from magicsoup_amd.ops import hip_ops
+
+    w = _world("cuda", map_size=64, n=200, s=300)
+    before = list(w.cell_genomes)
+    pairs = torch.tensor([[2 * i, 2 * i + 1] for i in range(50)], dtype=torch.int32, device="cuda")
+    changed = hip_ops.recombinations(w, pairs, 1e-2)
+    assert changed.numel() > 0
+    after = list(w.cell_genomes)
+    for a, b in pairs.tolist():
+        assert len(after[a]) + len(after[b]) == len(before[a]) + len(before[b])
+    assert sorted(set(changed.tolist())) == sorted(changed.tolist())
+    # overlapping pairs (cell 0 in many): committed rows are unique, strings well-formed
+    pairs2 = torch.tensor([[0, j] for j in range(1, 40)], dtype=torch.int32, device="cuda")
+    ch2 = hip_ops.recombinations(w, pairs2, 1e-2)
+    assert torch.unique(ch2).numel() == ch2.numel()
+    g = list(w.cell_genomes)
+    assert all(set(x) <= set("TCGA") for x in g)
+    lens = w._genomes.lens[: w.n_cells].tolist()
+    assert lens == [len(x) for x in g]
+    w.recombinate_cells(p=1e-3)
+    w.mutate_cells(p=1e-3)
+    g = list(w.cell_genomes)
+    assert w._genomes.lens[: w.n_cells].tolist() == [len(x) for x in g]
