@@ -41,6 +41,8 @@ def _args():
     ap.add_argument("--map-dtype", default="fp32", choices=["fp32", "bf16", "fp16"],
                     help="molecule-map storage dtype (kernels compute in fp32; default matches the reference)")
     ap.add_argument("--profile-phases", action="store_true", help="print per-phase times to stderr")
+    ap.add_argument("--step-times", action="store_true", help="print each timed step's wall time to stderr "
+                    "(synchronises after every step)")
     ap.add_argument("--phase-sync", action="store_true", help="with --profile-phases: drain the GPU at phase "
                     "boundaries (for attributing a kernel trace to phases; slows the step)")
     return ap.parse_args()
@@ -174,9 +176,16 @@ def main():
     timer = PhaseTimer(device, sync=a.phase_sync) if a.profile_phases else None
     t0 = time.perf_counter()
     stats = {} if a.profile_phases else None
+    per_step = []
     for _ in range(a.steps):
+        t1 = time.perf_counter()
         step(world, n_target, a.genome_size, atp, timer, stats)
+        if a.step_times:
+            sync()
+            per_step.append(round((time.perf_counter() - t1) * 1e3, 3))
     sync()
+    if per_step and rank == 0:
+        print(json.dumps({"step_ms": per_step}), file=sys.stderr)
     dt = time.perf_counter() - t0
     if distributed:
         t = torch.tensor([dt], dtype=torch.float64, device=device)

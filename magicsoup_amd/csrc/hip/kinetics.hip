@@ -340,7 +340,8 @@ __global__ void __launch_bounds__(256) bin_cells_kernel(int c, int P, int pn, co
 __global__ void __launch_bounds__(kBlock) integrate_scatter_kernel(int c, int s, int m, int R, int C, const float* snap,
                                                                    const unsigned* mask, int n_iters,
                                                                    const int32_t* positions, float* cell_mols,
-                                                                   void* molmap, int map_dtype, float* X_out) {
+                                                                   void* molmap, int map_dtype, const float* corr,
+                                                                   float* X_out) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long long)c * s) return;
   const int cell = (int)(t / s), j = (int)(t - (long long)cell * s);
@@ -354,7 +355,7 @@ __global__ void __launch_bounds__(kBlock) integrate_scatter_kernel(int c, int s,
     cell_mols[(size_t)cell * m + j] = x;
   } else {
     const size_t pix = (size_t)positions[2 * cell] * C + positions[2 * cell + 1];
-    st_map(molmap, (size_t)(j - m) * R * C + pix, x, map_dtype);
+    st_map(molmap, (size_t)(j - m) * R * C + pix, corr_out(x, corr, j - m), map_dtype);
   }
 }
 
@@ -370,8 +371,8 @@ __global__ void load_x_kernel(int c, int s, const float* X, float* snap) {
 // A flat, full-occupancy gather, so the random pixel reads (one per species plane) are not on the
 // LDS-limited integrator's critical path.
 __global__ void __launch_bounds__(kBlock) gather_x_kernel(int c, int s, int m, int R, int C, const float* cell_mols,
-                                                          const void* molmap, int map_dtype, const int32_t* positions,
-                                                          float* snap) {
+                                                          const void* molmap, int map_dtype, const float* corr,
+                                                          const int32_t* positions, float* snap) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long long)c * s) return;
   const int cell = (int)(t / s), j = (int)(t - (long long)cell * s);
@@ -380,7 +381,7 @@ __global__ void __launch_bounds__(kBlock) gather_x_kernel(int c, int s, int m, i
     x = cell_mols[(size_t)cell * m + j];
   } else {
     const size_t pix = (size_t)positions[2 * cell] * C + positions[2 * cell + 1];
-    x = ld_map(molmap, (size_t)(j - m) * R * C + pix, map_dtype);
+    x = corr_in(ld_map(molmap, (size_t)(j - m) * R * C + pix, map_dtype), corr, j - m);
   }
   snap[(size_t)cell * ms::kSnap * s + j] = x;
 }
@@ -537,8 +538,9 @@ static int slot_words_for(int P, int s, int sp) {
 void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q, uintptr_t Kmr, uintptr_t cell_mols,
                uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
                uintptr_t masks, const std::vector<float>& trims, int n_iters, int part_begin, int part_end,
-               bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t stream) {
+               bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t map_corr, uintptr_t stream) {
   if (c <= 0) return;
+  const float* corr = map_corr ? P_<float>(map_corr) : nullptr;
   if (n_iters < 0 || n_iters > ms::kEqIters) throw std::invalid_argument("n_iters must be in 0..4");
   const int nparts = (int)trims.size();
   if (part_begin < 0 || part_end > nparts || part_begin > part_end) throw std::invalid_argument("bad part range");
@@ -553,7 +555,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
       load_x_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(c, s, P_<float>(X_io), snaps[1]);
     } else {
       gather_x_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(c, s, m, R, C, P_<float>(cell_mols),
-                                                                          P_<void>(molmap), map_dtype,
+                                                                          P_<void>(molmap), map_dtype, corr,
                                                                           P_<int32_t>(positions), snaps[1]);
     }
     MS_LAUNCH_CHECK();
@@ -626,7 +628,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     const int last = nparts - 1;
     integrate_scatter_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(
         c, s, m, R, C, snaps[last & 1], mk + ms::kEqIters * last, n_iters, P_<int32_t>(positions),
-        P_<float>(cell_mols), P_<void>(molmap), map_dtype, X_io ? P_<float>(X_io) : nullptr);
+        P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr, X_io ? P_<float>(X_io) : nullptr);
     MS_LAUNCH_CHECK();
   }
 }

@@ -108,3 +108,13 @@ __device__ __forceinline__ void st_map(void* base, size_t i, float v, int dtype)
 }
 
 }  // namespace msd
+
+namespace msd {
+// Deferred diffusion mass correction (see maps.hip): a map plane may hold raw values whose true
+// value is max(raw + corr[mol], 0). corr == nullptr: raw values are true values.
+__device__ __forceinline__ float corr_in(float raw, const float* corr, int mol) {
+  return corr ? fmaxf(raw + corr[mol], 0.0f) : raw;
+}
+__device__ __forceinline__ float corr_out(float v, const float* corr, int mol) { return corr ? v - corr[mol] : v; }
+}  // namespace msd
+

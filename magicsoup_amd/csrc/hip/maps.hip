@@ -34,7 +34,8 @@ template <class T>
 __global__ void __launch_bounds__(64 * kWaves) diffuse_stencil_kernel(const T* __restrict__ in, T* __restrict__ out,
                                                                       const float* __restrict__ wa,
                                                                       const float* __restrict__ wb,
-                                                                      const float* __restrict__ scale, MGeom g,
+                                                                      const float* __restrict__ scale,
+                                                                      const float* __restrict__ corr, MGeom g,
                                                                       double* __restrict__ partials) {
   __shared__ double red[2][kWaves];
   const int mol = blockIdx.z;
@@ -61,10 +62,10 @@ __global__ void __launch_bounds__(64 * kWaves) diffuse_stencil_kernel(const T* _
   // v: centre, l/r: horizontal neighbours, h = l + v + r, for rows o-1 (p), o (c), o+1 (n)
   auto load = [&](int o, float& v, float& l, float& r) {
     const size_t base = (size_t)row_of(o) * g.C;
-    v = col ? ld(src + base + y) * sc : 0.0f;
+    v = col ? corr_in(ld(src + base + y), corr, mol) * sc : 0.0f;
     const float vl = __shfl_up(v, 1), vr = __shfl_down(v, 1);
-    l = own_l ? vl : (col ? ld(src + base + yl) * sc : 0.0f);
-    r = own_r ? vr : (col ? ld(src + base + yr) * sc : 0.0f);
+    l = own_l ? vl : (col ? corr_in(ld(src + base + yl), corr, mol) * sc : 0.0f);
+    r = own_r ? vr : (col ? corr_in(ld(src + base + yr), corr, mol) * sc : 0.0f);
   };
   float vp, lp, rp, vc, lc, rc;
   load(o0 - 1, vp, lp, rp);
@@ -117,7 +118,8 @@ template <class T>
 __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restrict__ in, T* __restrict__ out,
                                                                const float* __restrict__ wa,
                                                                const float* __restrict__ wb,
-                                                               const float* __restrict__ scale, MGeom g,
+                                                               const float* __restrict__ scale,
+                                                               const float* __restrict__ corr, MGeom g,
                                                                double* __restrict__ partials) {
   __shared__ double red[2][4];
   const int mol = blockIdx.z;
@@ -153,10 +155,10 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
   // scaled values of the row plus the left neighbour of column y0 and the right one of y0 + 3
   auto finish = [&](const Raw& r, float v[4], float& L, float& Rn) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = r.v[j] * sc;
+    for (int j = 0; j < 4; ++j) v[j] = corr_in(r.v[j], corr, mol) * sc;
     const float up = __shfl_up(v[3], 1), dn = __shfl_down(v[0], 1);
-    L = need_l ? r.el * sc : up;
-    Rn = need_r ? r.er * sc : dn;
+    L = need_l ? corr_in(r.el, corr, mol) * sc : up;
+    Rn = need_r ? corr_in(r.er, corr, mol) * sc : dn;
   };
   auto hsum = [](const float v[4], float L, float Rn, float h[4]) {
     h[0] = L + v[0] + v[1];
@@ -238,6 +240,29 @@ __global__ void __launch_bounds__(256) diffuse_reduce_kernel(const double* parti
   }
 }
 
+// Deferred correction: instead of a second full pass map = max(tmp + (before - after) / n_pix, 0),
+// only the per-species constant is computed; the stencil output becomes the map (buffer swap) with
+// the constant pending, and every later reader applies max(raw + corr, 0) (corr_in) -- the next
+// stencil, the pixel gathers of the integrator / permeation / pickup / spill, or one full apply
+// when the map is accessed from Python. Saves a read + write of the whole map per step.
+__global__ void diffuse_corr_kernel(const double* __restrict__ totals, int m, double n_pix, float* __restrict__ corr) {
+  const int mol = blockIdx.x * blockDim.x + threadIdx.x;
+  if (mol < m) corr[mol] = (float)((totals[2 * mol] - totals[2 * mol + 1]) / n_pix);
+}
+
+// map = max(map + corr, 0) * f (pending correction and / or degradation; either may be null)
+template <class T>
+__global__ void __launch_bounds__(256) apply_pending_kernel(T* map, const float* corr, const float* f, long long plane,
+                                                            int m) {
+  const long long total = plane * m;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int mol = (int)(i / plane);
+    float v = corr_in(ld(map + i), corr, mol);
+    if (f) v *= f[mol];
+    st(map + i, v);
+  }
+}
+
 // map[owned rows] = max(tmp + (before - after) / n_pix, 0); a plane's owned rows are one
 // contiguous range of `span` values starting at r_lo * C. 4 values per thread and iteration.
 template <class T>
@@ -277,7 +302,8 @@ __global__ void __launch_bounds__(256) scale_planes_kernel(T* map, const float* 
 template <class T>
 __global__ void __launch_bounds__(256) spill_free_kernel(int k, int m, const int64_t* idxs, const uint8_t* dead,
                                                          const int32_t* pos, int C, long long plane,
-                                                         const float* cell_mols, T* map, uint8_t* cell_map) {
+                                                         const float* cell_mols, T* map, uint8_t* cell_map,
+                                                         const float* corr) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long long)k * m) return;
   const int i = (int)(t / m), j = (int)(t - (long long)i * m);
@@ -286,40 +312,40 @@ __global__ void __launch_bounds__(256) spill_free_kernel(int k, int m, const int
   else if (!dead[c]) return;
   const long long pix = (long long)pos[2 * c] * C + pos[2 * c + 1];
   T* p = map + j * plane + pix;
-  st(p, ld(p) + cell_mols[c * m + j]);
+  st(p, corr_out(corr_in(ld(p), corr, j) + cell_mols[c * m + j], corr, j));
   if (j == 0) cell_map[pix] = 0;
 }
 
 template <class T>
 __global__ void __launch_bounds__(256) pickup_kernel(int k, int m, const int64_t* idxs, const int32_t* pos, int C,
-                                                     long long plane, float* cell_mols, T* map) {
+                                                     long long plane, float* cell_mols, T* map, const float* corr) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long long)k * m) return;
   const int i = (int)(t / m), j = (int)(t - (long long)i * m);
   const long long c = idxs[i];
   const long long pix = (long long)pos[2 * c] * C + pos[2 * c + 1];
   T* p = map + j * plane + pix;
-  const float x = ld(p);
+  const float x = corr_in(ld(p), corr, j);
   const float half = x * 0.5f;
   cell_mols[c * m + j] += half;
-  st(p, x - half);
+  st(p, corr_out(x - half, corr, j));
 }
 
 // exchange between cells and their pixels (reference world.py:651-665), one thread per
 // (cell, molecule)
 template <class T>
 __global__ void __launch_bounds__(256) permeate_kernel(int c, int m, long long plane, int C, const int32_t* pos,
-                                                       const float* perm, float* cell_mols, T* map) {
+                                                       const float* perm, float* cell_mols, T* map, const float* corr) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long long)c * m) return;
   const int cell = (int)(t / m), i = (int)(t - (long long)cell * m);
   const float p = perm[i];
   if (p == 0.0f) return;
   T* q = map + (size_t)i * plane + (size_t)pos[2 * cell] * C + pos[2 * cell + 1];
-  const float xi = cell_mols[t], xe = ld(q);
+  const float xi = cell_mols[t], xe = corr_in(ld(q), corr, i);
   const float di = xi * p, de = xe * p;
   cell_mols[t] = xi + (de - di);
-  st(q, xe + (di - de));
+  st(q, corr_out(xe + (di - de), corr, i));
 }
 
 // ---------------------------------------------------------------- health scan
@@ -370,7 +396,8 @@ size_t diffuse_partials_len(int m, int C, int H) {
 }
 
 void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
-                     uintptr_t wb, uintptr_t scale, uintptr_t partials, uintptr_t totals, int dtype, uintptr_t stream) {
+                     uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t totals, int dtype,
+                     uintptr_t stream) {
   if (m <= 0) return;
   const MGeom g = mgeom(R, C, r_lo, r_hi, wrap);
   hipStream_t st_ = S_(stream);
@@ -380,11 +407,11 @@ void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_
   if (v4) {
     MS_MAP_DISPATCH(dtype, (diffuse_stencil4_kernel<T><<<grid, 256, 0, st_>>>(
                                P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
-                               g, P_<double>(partials))));
+                               corr ? P_<float>(corr) : nullptr, g, P_<double>(partials))));
   } else {
     MS_MAP_DISPATCH(dtype, (diffuse_stencil_kernel<T><<<grid, 64 * kWaves, 0, st_>>>(
                                P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
-                               g, P_<double>(partials))));
+                               corr ? P_<float>(corr) : nullptr, g, P_<double>(partials))));
   }
   MS_LAUNCH_CHECK();
   diffuse_reduce_kernel<<<m, 256, 0, st_>>>(P_<double>(partials), (int)(grid.x * grid.y), P_<double>(totals));
@@ -399,6 +426,20 @@ void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uin
   MS_MAP_DISPATCH(dtype, (diffuse_correct_kernel<T><<<g, 256, 0, S_(stream)>>>(P_<T>(tmp), P_<T>(map),
                                                                                P_<double>(totals), n_pix, plane,
                                                                                start, span, m)));
+  MS_LAUNCH_CHECK();
+}
+
+void diffuse_corr(int m, uintptr_t totals, double n_pix, uintptr_t corr, uintptr_t stream) {
+  if (m <= 0) return;
+  diffuse_corr_kernel<<<cdiv(m, 64), 64, 0, S_(stream)>>>(P_<double>(totals), m, n_pix, P_<float>(corr));
+  MS_LAUNCH_CHECK();
+}
+
+void apply_pending(int m, long long plane, uintptr_t map, uintptr_t corr, uintptr_t f, int dtype, uintptr_t stream) {
+  if (m <= 0 || plane <= 0 || (!corr && !f)) return;
+  const unsigned g = std::min<long long>(cdiv(plane * m, 256), 8192);
+  MS_MAP_DISPATCH(dtype, (apply_pending_kernel<T><<<g, 256, 0, S_(stream)>>>(
+                             P_<T>(map), corr ? P_<float>(corr) : nullptr, f ? P_<float>(f) : nullptr, plane, m)));
   MS_LAUNCH_CHECK();
 }
 
@@ -419,38 +460,38 @@ void scale_planes(int m, long long plane, uintptr_t map, uintptr_t f, int dtype,
 }
 
 void spill_free(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
-                uintptr_t cell_map, int dtype, uintptr_t stream) {
+                uintptr_t cell_map, int dtype, uintptr_t corr, uintptr_t stream) {
   if (k <= 0 || m <= 0) return;
   MS_MAP_DISPATCH(dtype, (spill_free_kernel<T><<<cdiv((long long)k * m, 256), 256, 0, S_(stream)>>>(
                              k, m, P_<int64_t>(idxs), nullptr, P_<int32_t>(pos), C, (long long)R * C,
-                             P_<float>(cell_mols), P_<T>(map), P_<uint8_t>(cell_map))));
+                             P_<float>(cell_mols), P_<T>(map), P_<uint8_t>(cell_map), P_<float>(corr))));
   MS_LAUNCH_CHECK();
 }
 
 void spill_free_mask(int n, int m, uintptr_t dead, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
-                     uintptr_t cell_map, int dtype, uintptr_t stream) {
+                     uintptr_t cell_map, int dtype, uintptr_t corr, uintptr_t stream) {
   if (n <= 0 || m <= 0) return;
   MS_MAP_DISPATCH(dtype, (spill_free_kernel<T><<<cdiv((long long)n * m, 256), 256, 0, S_(stream)>>>(
                              n, m, nullptr, P_<uint8_t>(dead), P_<int32_t>(pos), C, (long long)R * C,
-                             P_<float>(cell_mols), P_<T>(map), P_<uint8_t>(cell_map))));
+                             P_<float>(cell_mols), P_<T>(map), P_<uint8_t>(cell_map), P_<float>(corr))));
   MS_LAUNCH_CHECK();
 }
 
 void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map, int dtype,
-            uintptr_t stream) {
+            uintptr_t corr, uintptr_t stream) {
   if (k <= 0 || m <= 0) return;
   MS_MAP_DISPATCH(dtype, (pickup_kernel<T><<<cdiv((long long)k * m, 256), 256, 0, S_(stream)>>>(
                              k, m, P_<int64_t>(idxs), P_<int32_t>(pos), C, (long long)R * C, P_<float>(cell_mols),
-                             P_<T>(map))));
+                             P_<T>(map), P_<float>(corr))));
   MS_LAUNCH_CHECK();
 }
 
 void permeate(int c, int m, int R, int C, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map, int dtype,
-              uintptr_t stream) {
+              uintptr_t corr, uintptr_t stream) {
   if (c <= 0 || m <= 0) return;
   MS_MAP_DISPATCH(dtype, (permeate_kernel<T><<<cdiv((long long)c * m, 256), 256, 0, S_(stream)>>>(
                              c, m, (long long)R * C, C, P_<int32_t>(pos), P_<float>(perm), P_<float>(cell_mols),
-                             P_<T>(map))));
+                             P_<T>(map), P_<float>(corr))));
   MS_LAUNCH_CHECK();
 }
 

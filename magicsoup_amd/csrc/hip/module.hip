@@ -26,20 +26,23 @@ void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t se
 // maps.hip
 size_t diffuse_partials_len(int m, int C, int H);
 void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
-                     uintptr_t wb, uintptr_t scale, uintptr_t partials, uintptr_t totals, int dtype, uintptr_t stream);
+                     uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t totals, int dtype,
+                     uintptr_t stream);
+void diffuse_corr(int m, uintptr_t totals, double n_pix, uintptr_t corr, uintptr_t stream);
+void apply_pending(int m, long long plane, uintptr_t map, uintptr_t corr, uintptr_t f, int dtype, uintptr_t stream);
 void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t totals,
                      double n_pix, int dtype, uintptr_t stream);
 void scale_planes(int m, long long plane, uintptr_t map, uintptr_t f, int dtype, uintptr_t stream);
 void health_scan(int planes, long long span, long long stride, uintptr_t x, int dtype, int shift, uintptr_t flags,
                  uintptr_t stream);
 void spill_free(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
-                uintptr_t cell_map, int dtype, uintptr_t stream);
+                uintptr_t cell_map, int dtype, uintptr_t corr, uintptr_t stream);
 void spill_free_mask(int n, int m, uintptr_t dead, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
-                     uintptr_t cell_map, int dtype, uintptr_t stream);
+                     uintptr_t cell_map, int dtype, uintptr_t corr, uintptr_t stream);
 void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map, int dtype,
-            uintptr_t stream);
+            uintptr_t corr, uintptr_t stream);
 void permeate(int c, int m, int R, int C, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map, int dtype,
-              uintptr_t stream);
+              uintptr_t corr, uintptr_t stream);
 void gather_rows(int n, uintptr_t src_rows, uintptr_t dst_rows,
                  const std::vector<std::tuple<uintptr_t, uintptr_t, long long, long long, long long>>& descs,
                  uintptr_t stream);
@@ -47,7 +50,7 @@ void gather_rows(int n, uintptr_t src_rows, uintptr_t dst_rows,
 void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q, uintptr_t Kmr, uintptr_t cell_mols,
                uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
                uintptr_t masks, const std::vector<float>& trims, int n_iters, int part_begin, int part_end,
-               bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t stream);
+               bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t map_corr, uintptr_t stream);
 void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_t rows, uintptr_t vmax_w, int nw,
                   uintptr_t km_w, int nk, uintptr_t signs, int nsg, uintptr_t hills, int nh, uintptr_t RM,
                   uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
@@ -119,6 +122,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("pack_params", &msd::pack_params);
   m.def("diffuse_stencil", &msd::diffuse_stencil);
   m.def("diffuse_correct", &msd::diffuse_correct);
+  m.def("diffuse_corr", &msd::diffuse_corr);
+  m.def("apply_pending", &msd::apply_pending);
   m.def("diffuse_partials_len", &msd::diffuse_partials_len);
   m.def("scale_planes", &msd::scale_planes);
   m.def("health_scan", &msd::health_scan);

@@ -225,6 +225,7 @@ class World:
             "cell_divisions": _Column(torch.zeros(0, dtype=torch.int32, device=dev)),
         }
         self.__dict__["_pending_scale"] = None
+        self.__dict__["_pending_corr"] = None
         self.cell_map = torch.zeros(*self._map_shape(), dtype=torch.bool, device=dev)
         self.molecule_map = self._get_molecule_map(n=m, size=map_size, init=mol_map_init)
 
@@ -239,10 +240,10 @@ class World:
         if cols is not None and name in cols:
             return cols[name].view(d["n_cells"])
         if name == "molecule_map" and "_molmap" in d:
-            if d.get("_pending_scale") is not None:
+            if d.get("_pending_scale") is not None or d.get("_pending_corr") is not None:
                 from magicsoup_amd.ops import hip_ops
 
-                hip_ops.apply_pending_scale(self)
+                hip_ops.apply_pending(self)
             return d["_molmap"]
         if name == "cell_map" and "_cell_map" in d:
             return d["_cell_map"]
@@ -263,6 +264,7 @@ class World:
                 t = t.to(want).contiguous()
             self.__dict__["_molmap"] = t
             self.__dict__["_pending_scale"] = None
+            self.__dict__["_pending_corr"] = None
             return
         if name == "cell_map":
             self._set_cell_map(value)
@@ -712,6 +714,7 @@ class World:
         state["_molmap"] = self.molecule_map.cpu()
         state["_cell_map"] = self.cell_map.cpu()
         state["_pending_scale"] = None
+        state["_pending_corr"] = None
         for k in ("_hip_scratch", "_idx_map", "_diff_w", "_perm_t", "_degrade_t"):
             state.pop(k, None)
         return state

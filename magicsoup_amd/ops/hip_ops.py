@@ -18,8 +18,14 @@ def _m():
     return native.hip()
 
 
+_raw_stream = torch._C._cuda_getCurrentRawStream
+_cur_device = torch._C._cuda_getDevice
+
+
 def _stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    """Raw handle of the current HIP stream (the C accessors; torch.cuda.current_stream() spends
+    ~10 us per call resolving the device in Python)."""
+    return _raw_stream(_cur_device())
 
 
 def _p(t: torch.Tensor | None) -> int:
@@ -138,10 +144,11 @@ def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n
     if world is not None:
         m = world.n_molecules
         R, C = geom(world)[:2]
-        cm, mm, pos = world.cell_molecules, world._molmap, world.cell_positions
+        mm, corr = map_for_pixels(world)
+        cm, pos = world.cell_molecules, world.cell_positions
         mdt = _mdt(mm)
     else:
-        m, R, C, cm, mm, pos, mdt = 0, 0, 0, None, None, None, 0
+        m, R, C, cm, mm, pos, mdt, corr = 0, 0, 0, None, None, None, 0, None
     args = [
         c, P, s, m, R, C,
         _p(W), _p(p["_Q"]), _p(p["Kmr"]),
@@ -153,16 +160,16 @@ def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n
     lists = sc.get("bin_lists", 2 * c + 2, torch.int32, dev)  # narrow / wide cell lists + counts
     nparts = len(trims)
     if flags_hook is None:
-        _m().integrate(*args, 0, nparts, True, slot_p, _p(lists), mdt, _stream())
+        _m().integrate(*args, 0, nparts, True, slot_p, _p(lists), mdt, _p(corr), _stream())
     else:
         # domain-decomposed world: all-reduce each part's iteration flags before the next part (or
         # the final write-back) reads them, reproducing the reference's `torch.any` over the whole
         # population
         for part in range(nparts):
-            _m().integrate(*args, part, part + 1, False, slot_p, _p(lists), mdt, _stream())
+            _m().integrate(*args, part, part + 1, False, slot_p, _p(lists), mdt, _p(corr), _stream())
             flags_hook(masks[_EQ * part : _EQ * (part + 1)])
         if nparts:
-            _m().integrate(*args, nparts, nparts, True, slot_p, _p(lists), mdt, _stream())
+            _m().integrate(*args, nparts, nparts, True, slot_p, _p(lists), mdt, _p(corr), _stream())
     sc.bufs["pack_overflow_host"].copy_(_overflow_flag(kin), non_blocking=True)
     return masks
 
@@ -221,38 +228,56 @@ def _ensure_world_layout(world) -> None:
         world.cell_positions = pos.to(torch.int32).contiguous()
 
 
+def map_for_pixels(world):
+    """(raw map, pending correction or None) for kernels that touch the pixels under cells. A
+    pending degradation is applied first (together with any correction, one full pass); a pending
+    correction alone is handed to the kernel (maps.hip corr_in / corr_out)."""
+    d = world.__dict__
+    if d.get("_pending_scale") is not None:
+        apply_pending(world)
+    return d["_molmap"], d.get("_pending_corr")
+
+
 def diffuse(world) -> None:
-    """Stencil over the owned rows (+ fused pending degradation) -> (global) mass totals ->
-    correction + clamp. A domain-decomposed world refreshes its halo rows first and all-reduces the
-    totals (see magicsoup_amd.parallel)."""
+    """Stencil over the owned rows (+ fused pending degradation and correction) -> (global) mass
+    totals -> the new per-species correction, left pending: the stencil output becomes the map
+    (buffer swap) and readers apply max(raw + corr, 0) (maps.hip). A domain-decomposed world
+    refreshes its halo rows first and all-reduces the totals (see magicsoup_amd.parallel)."""
     R, C, r_lo, r_hi, wrap = geom(world)
     halo = getattr(world, "_exchange_map_halo", None)
     if halo is not None:
         halo()
-    mm = world._molmap
+    d = world.__dict__
+    mm = d["_molmap"]
     m = int(mm.size(0))
     sc = _scratch(world)
     dev = mm.device
     tmp = sc.get("diff_tmp", mm.numel(), mm.dtype, dev)
     partials = sc.get("diff_partials", int(_m().diffuse_partials_len(m, C, r_hi - r_lo)), torch.float64, dev)
     totals = sc.get("diff_totals", 2 * m, torch.float64, dev)
-    w = world.__dict__.get("_diff_w")
+    w = d.get("_diff_w")
     if w is None or w[0] != world._diffusion:
         wa = torch.tensor([float(a) for a, _ in world._diffusion], dtype=torch.float32, device=dev)
         wb = torch.tensor([float(b) for _, b in world._diffusion], dtype=torch.float32, device=dev)
         w = (list(world._diffusion), wa, wb)
-        world.__dict__["_diff_w"] = w
+        d["_diff_w"] = w
     # a pending degradation scales the halo rows as well: every rank degrades identically, so the
-    # neighbours' unscaled boundary rows carry the same pending factor
-    scale = world.__dict__.get("_pending_scale")
-    _m().diffuse_stencil(m, R, C, r_lo, r_hi, wrap, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale), _p(partials),
-                         _p(totals), _mdt(mm), _stream())
-    world.__dict__["_pending_scale"] = None
+    # neighbours' unscaled boundary rows carry the same pending factor (and the same correction:
+    # it is computed from all-reduced totals)
+    scale, corr = d.get("_pending_scale"), d.get("_pending_corr")
+    _m().diffuse_stencil(m, R, C, r_lo, r_hi, wrap, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale), _p(corr),
+                         _p(partials), _p(totals), _mdt(mm), _stream())
     reduce = getattr(world, "_allreduce_totals", None)
     if reduce is not None:
         reduce(totals)
     n_pix = float(getattr(world, "_n_pix_global", R * C if wrap else (r_hi - r_lo) * C))
-    _m().diffuse_correct(m, R, C, r_lo, r_hi, _p(mm), _p(tmp), _p(totals), n_pix, _mdt(mm), _stream())
+    new_corr = sc.get("diff_corr", m, torch.float32, dev)
+    _m().diffuse_corr(m, _p(totals), n_pix, _p(new_corr), _stream())
+    # swap: the stencil output is the map now; the old map buffer is the next scratch
+    d["_molmap"] = tmp.view(mm.shape)
+    sc.bufs["diff_tmp"] = mm.view(-1)
+    d["_pending_scale"] = None
+    d["_pending_corr"] = new_corr
 
 
 def health_flags(world) -> torch.Tensor:
@@ -269,7 +294,7 @@ def health_flags(world) -> torch.Tensor:
 
 
 def permeate(world) -> None:
-    mm = world.molecule_map
+    mm, corr = map_for_pixels(world)
     _ensure_world_layout(world)
     dev = mm.device
     perm = world.__dict__.get("_perm_t")
@@ -280,7 +305,7 @@ def permeate(world) -> None:
         return
     R, C = geom(world)[:2]
     _m().permeate(world.n_cells, world.n_molecules, R, C, _p(world.cell_positions), _p(perm[1]),
-                  _p(world.cell_molecules), _p(mm), _mdt(mm), _stream())
+                  _p(world.cell_molecules), _p(mm), _mdt(mm), _p(corr), _stream())
 
 
 def _degrade_factors(world) -> torch.Tensor:
@@ -303,13 +328,20 @@ def degrade(world) -> None:
     world.__dict__["_pending_scale"] = f.clone() if pend is None else pend * f
 
 
-def apply_pending_scale(world) -> None:
-    f = world.__dict__.get("_pending_scale")
-    if f is None:
+def apply_pending(world) -> None:
+    """Materialise a pending correction and / or degradation of the map (one full pass)."""
+    d = world.__dict__
+    f, corr = d.get("_pending_scale"), d.get("_pending_corr")
+    if f is None and corr is None:
         return
-    mm = world.__dict__["_molmap"]
-    world.__dict__["_pending_scale"] = None
-    _m().scale_planes(int(mm.size(0)), int(mm.size(1)) * int(mm.size(2)), _p(mm), _p(f), _mdt(mm), _stream())
+    mm = d["_molmap"]
+    d["_pending_scale"] = None
+    d["_pending_corr"] = None
+    _m().apply_pending(int(mm.size(0)), int(mm.size(1)) * int(mm.size(2)), _p(mm), _p(corr), _p(f), _mdt(mm),
+                       _stream())
+
+
+apply_pending_scale = apply_pending
 
 
 # ---------------------------------------------------------------------------- placement
@@ -386,9 +418,9 @@ def spill_and_free(world, idxs: torch.Tensor) -> None:
     _ensure_world_layout(world)
     R, C = geom(world)[:2]
     ix = idxs.to(torch.int64).contiguous()
+    mm, corr = map_for_pixels(world)
     _m().spill_free(int(ix.numel()), world.n_molecules, _p(ix), _p(world.cell_positions), R, C,
-                    _p(world.cell_molecules), _p(world._molmap), _p(_cell_map_bytes(world)), _mdt(world._molmap),
-                    _stream())
+                    _p(world.cell_molecules), _p(mm), _p(_cell_map_bytes(world)), _mdt(mm), _p(corr), _stream())
 
 
 def spill_and_free_mask(world, dead: torch.Tensor) -> None:
@@ -396,9 +428,9 @@ def spill_and_free_mask(world, dead: torch.Tensor) -> None:
     _ensure_world_layout(world)
     R, C = geom(world)[:2]
     d = dead.to(torch.uint8).contiguous() if dead.dtype != torch.bool else dead.contiguous().view(torch.uint8)
+    mm, corr = map_for_pixels(world)
     _m().spill_free_mask(world.n_cells, world.n_molecules, _p(d), _p(world.cell_positions), R, C,
-                         _p(world.cell_molecules), _p(world._molmap), _p(_cell_map_bytes(world)), _mdt(world._molmap),
-                    _stream())
+                         _p(world.cell_molecules), _p(mm), _p(_cell_map_bytes(world)), _mdt(mm), _p(corr), _stream())
 
 
 def pickup_molecules(world, new: torch.Tensor) -> None:
@@ -406,8 +438,9 @@ def pickup_molecules(world, new: torch.Tensor) -> None:
     _ensure_world_layout(world)
     R, C = geom(world)[:2]
     ix = new.to(torch.int64).contiguous()
+    mm, corr = map_for_pixels(world)
     _m().pickup(int(ix.numel()), world.n_molecules, _p(ix), _p(world.cell_positions), R, C,
-                _p(world.cell_molecules), _p(world._molmap), _mdt(world._molmap), _stream())
+                _p(world.cell_molecules), _p(mm), _mdt(mm), _p(corr), _stream())
 
 
 def split_cells(world, parents: torch.Tensor, children: torch.Tensor) -> None:
@@ -423,23 +456,28 @@ def split_cells(world, parents: torch.Tensor, children: torch.Tensor) -> None:
 def gather_rows(pairs, n: int, src_rows: torch.Tensor | None = None, dst_rows: torch.Tensor | None = None) -> None:
     """dst[dst_rows[i]] = src[src_rows[i]] for i < n, for every (src, dst) tensor pair, in one launch
     (rows are dim 0; each row contiguous; identity where an index tensor is None)."""
+    if n <= 0:
+        return
     descs = []
     for src, dst in pairs:
-        if src.dim() == 0:
-            continue
         es = src.element_size()
-        row = 1
-        for d in src.shape[1:]:
-            row *= int(d)
-        if row == 0:
+        st = src.stride()
+        if not st:
             continue
-        assert dst.dtype == src.dtype and tuple(dst.shape[1:]) == tuple(src.shape[1:]), "gather_rows: shape mismatch"
-        assert src.dim() == 1 or (src.stride(-1) == 1 and src[0].is_contiguous()), "gather_rows: rows must be contiguous"
-        descs.append((src.data_ptr(), dst.data_ptr(), src.stride(0) * es, dst.stride(0) * es, row * es))
-    if n <= 0 or not descs:
+        rb = (src.numel() // src.size(0) if src.size(0) else 0) * es
+        if rb == 0:
+            continue
+        if dst.dtype != src.dtype or dst.shape[1:] != src.shape[1:]:
+            raise ValueError("gather_rows: shape mismatch")
+        if len(st) > 1 and not (st[-1] == 1 and src.is_contiguous() or src[:1].is_contiguous()):
+            raise ValueError("gather_rows: rows must be contiguous")
+        descs.append((src.data_ptr(), dst.data_ptr(), st[0] * es, dst.stride(0) * es, rb))
+    if not descs:
         return
-    sr = None if src_rows is None else src_rows.to(torch.int64).contiguous()
-    dr = None if dst_rows is None else dst_rows.to(torch.int64).contiguous()
+    sr = None if src_rows is None else (src_rows if src_rows.dtype == torch.int64 and src_rows.is_contiguous()
+                                        else src_rows.to(torch.int64).contiguous())
+    dr = None if dst_rows is None else (dst_rows if dst_rows.dtype == torch.int64 and dst_rows.is_contiguous()
+                                        else dst_rows.to(torch.int64).contiguous())
     _m().gather_rows(int(n), _p(sr), _p(dr), descs, _stream())
 
 

@@ -121,7 +121,7 @@ def neighbors(world, frm: torch.Tensor, to: torch.Tensor, pos: torch.Tensor | No
 
 def random_labels(world, k: int, length: int):
     """k random labels over [A-Za-z0-9] as packed (bytes (k, length), lengths)."""
-    dev = world.molecule_map.device
+    dev = world.__dict__["_molmap"].device
     if dev.type == "cuda":
         idx = torch.randint(0, 62, (k, length), device=dev)
     else:
@@ -134,8 +134,7 @@ def random_labels(world, k: int, length: int):
 def pickup_molecules(world, new: torch.Tensor, pos: torch.Tensor) -> None:
     """New cells take half of their pixel's molecules."""
     if world.__dict__["_molmap"].is_cuda:
-        # a pending degradation must be applied before pixels change
-        _molmap(world)
+        # pending degradation / correction: handled by the kernel path (hip_ops.map_for_pixels)
         return _hip().pickup_molecules(world, new)
     mm = _molmap(world)
     xs, ys = pos[:, 0].long(), pos[:, 1].long()
@@ -147,7 +146,6 @@ def pickup_molecules(world, new: torch.Tensor, pos: torch.Tensor) -> None:
 def spill_and_free(world, idxs: torch.Tensor) -> None:
     """Killed cells release their pixel and spill their molecules onto it."""
     if world.__dict__["_molmap"].is_cuda:
-        _molmap(world)
         return _hip().spill_and_free(world, idxs)
     mm = _molmap(world)
     pos = world.cell_positions[idxs].long()
@@ -159,7 +157,6 @@ def spill_and_free(world, idxs: torch.Tensor) -> None:
 def spill_and_free_mask(world, dead: torch.Tensor) -> None:
     """Cells flagged in ``dead`` (bool (n,)) spill their molecules and release their pixels."""
     if world.__dict__["_molmap"].is_cuda:
-        _molmap(world)
         return _hip().spill_and_free_mask(world, dead)
     spill_and_free(world, torch.nonzero(dead).flatten())
 
@@ -182,7 +179,6 @@ def split_cells(world, parents: torch.Tensor, children: torch.Tensor) -> None:
 def enzymatic_activity(world) -> None:
     kin = world.kinetics
     if _is_gpu(world) and not kin._stages_overridden():
-        _molmap(world)
         return _hip().enzymatic_activity(world)
     mm = _molmap(world)
     pos = world.cell_positions.long()
@@ -234,9 +230,9 @@ def diffuse(world) -> None:
 
 
 def permeate(world) -> None:
-    mm = _molmap(world)
-    if mm.is_cuda:
+    if _is_gpu(world):
         return _hip().permeate(world)
+    mm = _molmap(world)
     p = torch.tensor(world._permeation, dtype=torch.float32)
     if not bool((p != 0).any()):
         return
@@ -251,9 +247,9 @@ def permeate(world) -> None:
 
 
 def degrade(world) -> None:
-    mm = _molmap(world)
-    if mm.is_cuda:
+    if _is_gpu(world):
         return _hip().degrade(world)
+    mm = _molmap(world)
     f = torch.tensor(world._mol_degrads, dtype=torch.float32)
     mm *= f[:, None, None]
     if world.n_cells > 0:

@@ -566,6 +566,7 @@ class DistributedWorld(World):
         mm.zero_()
         mm[:, lo : lo + H] = world.molecule_map[:, self.row0 : self.row0 + H].to(mm.device)
         self.__dict__["_pending_scale"] = None
+        self.__dict__["_pending_corr"] = None
         gpos = world.cell_positions.long().cpu()
         mine = torch.nonzero((gpos[:, 0] >= self.row0) & (gpos[:, 0] < self.row0 + H)).flatten()
         k = int(mine.numel())

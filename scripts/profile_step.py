@@ -28,4 +28,4 @@ torch.cuda.synchronize() if dev == "cuda" else None
 pr.disable()
 st = pstats.Stats(pr)
 st.sort_stats("cumulative").print_stats(45)
-st.sort_stats("tottime").print_stats(25)
+st.sort_stats("tottime").print_stats(45)

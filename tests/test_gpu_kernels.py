@@ -417,3 +417,29 @@ def test_recombination_commit_on_gpu():
     w.mutate_cells(p=1e-3)
     g = list(w.cell_genomes)
     assert w._genomes.lens[: w.n_cells].tolist() == [len(x) for x in g]
+
+
+def test_deferred_diffusion_correction_matches_materialised():
+    """The diffusion correction left pending (read through by the pixel kernels) gives the same
+    trajectory as applying it right after every diffusion."""
+    import copy as _copy
+
+    a = _world("cuda", map_size=96, n=400, s=400)
+    a.molecule_map = a.molecule_map * 0.01  # near-zero pixels so that the clamp also matters
+    b = _copy.deepcopy(a)
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    for step in range(6):
+        for w, eager in ((a, False), (b, True)):
+            ms.set_seed(100 + step)
+            w.enzymatic_activity()
+            w.kill_cells(w.cell_molecules[:, atp] < 0.5)
+            w.spawn_cells([ms.random_genome(300) for _ in range(5)])
+            w.degrade_molecules()
+            w.diffuse_molecules()
+            if eager:
+                _ = w.molecule_map  # materialise now
+        assert a.__dict__["_pending_corr"] is not None
+    assert a.n_cells == b.n_cells
+    assert torch.allclose(a.molecule_map, b.molecule_map, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(a.cell_molecules, b.cell_molecules, rtol=1e-5, atol=1e-6)
+    assert float(a.molecule_map.min()) >= 0.0
