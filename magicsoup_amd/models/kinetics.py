@@ -349,17 +349,34 @@ class Kinetics:
         if slot is None:
             rows = torch.as_tensor(cell_idxs, dtype=torch.int32)
         else:
-            rows = self._rows(torch.as_tensor(cell_idxs, device=slot.device).long()).to(torch.int32)
+            # rows may be shared (children of a division point at their parent's row): the new
+            # parameters go to fresh rows
+            cells = torch.as_tensor(cell_idxs, device=slot.device).long()
+            fresh = self._alloc_rows(int(cells.numel()))
+            self.__dict__["_slot"][cells] = fresh
+            rows = fresh.to(torch.int32)
         kinetics_ops.build_params(self, rows, tokens, nprot=nprot)
 
     def unset_cell_params(self, cell_idxs):
         """Zero all parameters of the given cells."""
         if isinstance(cell_idxs, list) and len(cell_idxs) == 0:
             return
+        if self._slot_tensor() is not None:
+            # shared rows: point the cells at one fresh all-zero row
+            cells = torch.as_tensor(cell_idxs, device=self._slot_tensor().device).long()
+            if cells.numel() == 0:
+                return
+            row = self._alloc_rows(1)
+            ok = self._pack_ok()
+            for t in self._store.values():
+                t[row] = 0  # packed words 0 and Q = 0 match all-zero parameters
+            self.__dict__["_slot"][cells] = row
+            self._restamp(ok)
+            return
         rows = self._rows(cell_idxs)
         ok = self._pack_ok()
         for t in self._store.values():
-            t[rows] = 0  # packed words 0 and Q = 0 match all-zero parameters
+            t[rows] = 0
         self._restamp(ok)
 
     def copy_cell_params(self, from_idxs, to_idxs):
@@ -368,28 +385,35 @@ class Kinetics:
         self._copy_rows(from_idxs, to_idxs, disjoint=False)
 
     def _copy_rows(self, from_idxs, to_idxs, disjoint: bool) -> None:
-        """``disjoint``: the caller guarantees no destination is also a source (e.g. new cells),
-        so the GPU copies rows directly instead of staging them."""
+        """On the GPU the destination cells share the source cells' storage rows (no parameter
+        copy; rows are never written in place while in row-storage mode). ``disjoint`` is kept for
+        callers that know no destination is also a source."""
         store = self._store
         dev = store["N"].device
         if dev.type == "cuda":
-            from magicsoup_amd.ops import hip_ops
-
-            fr = self._rows(torch.as_tensor(from_idxs, device=dev).long())
-            to = self._rows(torch.as_tensor(to_idxs, device=dev).long())
-            k = int(fr.numel())
-            if disjoint:
-                hip_ops.gather_rows([(t, t) for t in store.values()], k, src_rows=fr, dst_rows=to)
-                return
-            tmp = {name: torch.empty(k, *t.shape[1:], dtype=t.dtype, device=dev) for name, t in store.items()}
-            hip_ops.gather_rows([(store[nm], tmp[nm]) for nm in store], k, src_rows=fr)
-            hip_ops.gather_rows([(tmp[nm], store[nm]) for nm in store], k, dst_rows=to)
+            self._enter_slot_mode()
+            slot = self.__dict__["_slot"]
+            fr = torch.as_tensor(from_idxs, device=dev).long()
+            to = torch.as_tensor(to_idxs, device=dev).long()
+            slot[to] = slot[fr]
             return
         fr, to = self._rows(from_idxs), self._rows(to_idxs)
         ok = self._pack_ok()
         for t in store.values():
             t[to] = t[fr]
         self._restamp(ok)
+
+    def append_shared(self, from_idxs: torch.Tensor) -> None:
+        """Append cells that share the parameter rows of cells ``from_idxs`` (children of a
+        division inherit the parent's proteome; reference kinetics.py:646-665 copies the rows).
+        GPU row storage only."""
+        if int(from_idxs.numel()) == 0:
+            return
+        self._enter_slot_mode()
+        d = self.__dict__
+        slot = d["_slot"]
+        d["_slot"] = torch.cat([slot, slot[from_idxs.long()]])
+        d["_ncells"] += int(from_idxs.numel())
 
     # ---- parameter storage ----
     # The parameters live in row-storage tensors with spare capacity; cell i's row is _slot[i]
@@ -434,6 +458,39 @@ class Kinetics:
 
     def _slot_tensor(self) -> torch.Tensor | None:
         return self.__dict__["_slot"]
+
+    def _enter_slot_mode(self) -> None:
+        """GPU: switch from dense cell-ordered rows to the cell -> row map (identity to start)."""
+        d = self.__dict__
+        if d["_slot"] is None:
+            n = d["_ncells"]
+            d["_slot"] = torch.arange(n, device=self._store["N"].device)
+            d["_nrows"] = n
+
+    def _alloc_rows(self, k: int) -> torch.Tensor:
+        """k unused storage rows (int64, device) for cells whose parameters are about to be written.
+        Rows of removed cells are not tracked (a row may be shared); when the storage is exhausted
+        the live rows are gathered back to cell order (one pass) or the capacity grows."""
+        d = self.__dict__
+        self._enter_slot_mode()
+        store = self._store
+        cap = min(int(t.size(0)) for t in store.values())
+        if d["_nrows"] + k > cap:
+            self._materialize()  # dense again: rows 0..n-1 live
+            self._enter_slot_mode()
+            n = d["_ncells"]
+            if n + k > cap:
+                new_cap = max(n + k, int(cap * 1.5) + 64)
+                ok = self._pack_ok()
+                for name, t in list(store.items()):
+                    nb = torch.empty(new_cap, *t.shape[1:], dtype=t.dtype, device=t.device)
+                    nb[:n] = t[:n]
+                    store[name] = nb
+                d.pop("_spare", None)
+                self._restamp(ok)
+        r0 = d["_nrows"]
+        d["_nrows"] = r0 + k
+        return torch.arange(r0, r0 + k, device=store["N"].device)
 
     def _kernel_params(self) -> dict[str, torch.Tensor]:
         """Storage tensors in kernel layout (contiguous int32 / float32), rows = capacity."""
@@ -515,7 +572,6 @@ class Kinetics:
             spare[k], store[k] = store[k], target[k]
         d["_slot"] = None
         d["_nrows"] = n
-        d["_free"], d["_nfree"] = None, 0
         self._restamp(ok)
 
     def remove_cell_params(self, keep: torch.Tensor, removed: torch.Tensor | None = None):
@@ -525,27 +581,10 @@ class Kinetics:
         d = self.__dict__
         k = int(idx.numel())
         if idx.is_cuda:
-            slot = d["_slot"]
-            n = d["_ncells"]
-            if slot is None:
-                slot = torch.arange(n, device=idx.device)
-            if k < n:  # rows of the removed cells become reusable by later growth
-                if removed is None:
-                    gone = torch.ones(n, dtype=torch.bool, device=idx.device)
-                    gone[idx] = False
-                    freed = slot[gone]
-                else:
-                    freed = slot[removed.to(torch.long)]
-                nfree = d.get("_nfree", 0) if d.get("_free") is not None else 0
-                free = d.get("_free")
-                if free is None or free.numel() < nfree + (n - k):
-                    nb = torch.empty(max(nfree + (n - k), 2 * nfree + 64), dtype=slot.dtype, device=slot.device)
-                    if nfree:
-                        nb[:nfree] = free[:nfree]
-                    free = d["_free"] = nb
-                free[nfree : nfree + (n - k)] = freed
-                d["_nfree"] = nfree + (n - k)
-            d["_slot"] = slot[idx]
+            # only the cell -> row map is compacted; rows of removed cells (possibly shared with
+            # survivors) stay until the next re-gather (_alloc_rows)
+            self._enter_slot_mode()
+            d["_slot"] = d["_slot"][idx]
             d["_ncells"] = k
             return
         self._materialize()
@@ -568,44 +607,33 @@ class Kinetics:
             return
         d = self.__dict__
         store = self._store
+        if d["_slot"] is not None:
+            # GPU row storage: the new cells share one fresh all-zero row (a later build gives them
+            # rows of their own)
+            row = self._alloc_rows(1)
+            ok = self._pack_ok()
+            for t in store.values():
+                t[row] = 0
+            slot = d["_slot"]
+            d["_slot"] = torch.cat([slot, row.expand(by_n)])
+            d["_ncells"] += by_n
+            self._restamp(ok)
+            return
         cap = min(int(t.size(0)) for t in store.values())
-        nfree = d.get("_nfree", 0) if d["_slot"] is not None else 0
-        reuse = min(nfree, by_n)
-        if d["_slot"] is not None and d["_nrows"] + (by_n - reuse) > cap:
-            self._materialize()
-            reuse = 0
         ok = self._pack_ok()
         n = d["_ncells"]
-        if d["_slot"] is None:
-            r0 = n
-            if n + by_n > cap:
-                new_cap = max(n + by_n, int(cap * 1.5) + 64)
-                for name, t in list(store.items()):
-                    nb = torch.empty(new_cap, *t.shape[1:], dtype=t.dtype, device=t.device)
-                    nb[:n] = t[:n]
-                    store[name] = nb
-                d.pop("_spare", None)
-            new_rows = slice(r0, r0 + by_n)
-            d["_nrows"] = r0 + by_n
-        else:
-            # reuse rows freed by removed cells first (most recently freed last), then append
-            slot, r0 = d["_slot"], d["_nrows"]
-            parts = []
-            if reuse:
-                parts.append(d["_free"][nfree - reuse : nfree].to(slot.dtype))
-                d["_nfree"] = nfree - reuse
-            if by_n > reuse:
-                parts.append(torch.arange(r0, r0 + by_n - reuse, device=slot.device, dtype=slot.dtype))
-                d["_nrows"] = r0 + by_n - reuse
-            new_rows = parts[0] if len(parts) == 1 else torch.cat(parts)
-            d["_slot"] = torch.cat([slot, new_rows])
+        if n + by_n > cap:
+            new_cap = max(n + by_n, int(cap * 1.5) + 64)
+            for name, t in list(store.items()):
+                nb = torch.empty(new_cap, *t.shape[1:], dtype=t.dtype, device=t.device)
+                nb[:n] = t[:n]
+                store[name] = nb
+            d.pop("_spare", None)
+        d["_nrows"] = n + by_n
         d["_ncells"] = n + by_n
         if zero:
             for t in store.values():
-                if isinstance(new_rows, slice):
-                    t[new_rows].zero_()
-                else:
-                    t.index_fill_(0, new_rows, 0)
+                t[n : n + by_n].zero_()
         # zero=False: the caller fills the new rows with a GPU build or row copy, both of which
         # write the packed layout too
         self._restamp(ok)

@@ -311,16 +311,17 @@ class World:
         for col in self._cols.values():
             col.reserve(self.n_cells, n_new)
 
-    def _grow(self, k: int, zero: bool = True) -> None:
-        """Append k cell rows to every per-cell array (world + kinetics); zero-initialised unless
-        the caller overwrites them all."""
+    def _grow(self, k: int, zero: bool = True, params: bool = True) -> None:
+        """Append k cell rows to every per-cell array (world + kinetics unless ``params``);
+        zero-initialised unless the caller overwrites them all."""
         n = self.n_cells
         self._reserve(n + k)
         if zero:
             for col in self._cols.values():
                 col.buf[n : n + k] = 0
         self.n_cells = n + k
-        self.kinetics.increase_max_cells(by_n=k, zero=zero)
+        if params:
+            self.kinetics.increase_max_cells(by_n=k, zero=zero)
 
     def _clone_rows(self, src: torch.Tensor, dst: torch.Tensor) -> None:
         """Append copies of cells ``src`` as the new rows ``dst`` (= n_cells, n_cells + 1, ...):
@@ -338,12 +339,13 @@ class World:
             return
         from magicsoup_amd.ops import hip_ops
 
-        self._grow(k, zero=False)
+        self._grow(k, zero=False, params=False)
         n = self.n_cells
         pairs = [(col.view(n), col.view(n)) for name, col in self._cols.items() if name != "cell_positions"]
         pairs += self._genomes.clone_pairs(k) + self._labels.clone_pairs(k)
         hip_ops.gather_rows(pairs, k, src_rows=src, dst_rows=dst)
-        self.kinetics._copy_rows(src, dst, disjoint=True)  # children are new rows
+        # children share their parent's parameter rows until either is re-translated
+        self.kinetics.append_shared(src)
 
     def _idx_tensor(self, idxs, unique: bool = True) -> torch.Tensor:
         """Cell indices as a long tensor on the world's device (ascending and duplicate-free when

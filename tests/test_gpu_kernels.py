@@ -308,7 +308,7 @@ def test_param_row_storage_fuzz_matches_dense_model():
     X = torch.rand(kin.N.size(0), kin.N.size(2), device="cuda") * 5
     for step in range(60):
         n = kin.__dict__["_ncells"]
-        op = rng.choice(["kill", "grow", "copy", "integrate", "widen"])
+        op = rng.choice(["kill", "grow", "copy", "integrate", "widen", "unset"])
         if op == "kill" and n > 10:
             keep = torch.rand(n, device="cuda") > 0.3
             kin.remove_cell_params(keep)
@@ -322,6 +322,12 @@ def test_param_row_storage_fuzz_matches_dense_model():
                 z = torch.zeros(k_new, *model[k].shape[1:], dtype=model[k].dtype, device="cuda")
                 model[k] = torch.cat([model[k], z])
             X = torch.cat([X, torch.rand(k_new, X.size(1), device="cuda") * 5])
+        elif op == "unset" and n > 4:
+            # cells sharing a row with others (after "copy") must not clear their sharers
+            cells = torch.randperm(n, device="cuda")[: n // 5]
+            kin.unset_cell_params(cells)
+            for k in names:
+                model[k][cells] = 0
         elif op == "widen":
             # protein dimension grows in place of the row storage (slot map kept)
             p_new = kin.N.size(1) + rng.randint(1, 3) if kin.__dict__["_slot"] is None else kin._P() + rng.randint(1, 3)
