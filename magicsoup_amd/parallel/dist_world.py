@@ -367,38 +367,61 @@ class DistributedWorld(World):
             cpos = cpos.to(dev)
         else:
             parents, cpos = empty, torch.zeros(0, 2, dtype=torch.int32, device=dev)
-        row = cpos[:, 0]
-        up, dn = row == 0, row == self.H + 1
-        loc = ~(up | dn)
-        p_up, p_dn = parents[up], parents[dn]
-        lp = cpos[loc].long()
-        self.cell_map[lp[:, 0], lp[:, 1]] = True  # own children first when arbitrating claims
-        rec_up = self._records(p_up, cpos[up, 1], child=True)
-        rec_dn = self._records(p_dn, cpos[dn, 1], child=True)
+        # split the winners by destination row (local / upper halo / lower halo) with one stable
+        # sort and one read-back instead of a boolean compaction per class
+        i_loc, i_up, i_dn = self._split_by_row(cpos[:, 0])
+        p_up, p_dn = parents[i_up], parents[i_dn]
+        if not cpos.is_cuda:
+            # own children first when arbitrating claims (the GPU placement kernels already
+            # marked every claimed pixel, halo rows too)
+            lp = cpos[i_loc].long()
+            self.cell_map[lp[:, 0], lp[:, 1]] = True
+        rec_up = self._records(p_up, cpos[i_up, 1], child=True)
+        rec_dn = self._records(p_dn, cpos[i_dn, 1], child=True)
         acc_up, acc_dn, got = self._migrate(rec_up, rec_dn)
         # halo claims are scratch: the halo rows are refreshed before their next use
         self.cell_map[0] = False
         self.cell_map[self.H + 1] = False
-        # exported children: the parent keeps half, both get divisions + 1 and lifetime 0
-        out = torch.cat([p_up[acc_up], p_dn[acc_dn]])
-        if out.numel():
-            self.cell_molecules[out] *= 0.5
-            self.cell_divisions[out] += 1
-            self.cell_lifetimes[out] = 0
+        # exported children: the parent keeps half, both get divisions + 1 and lifetime 0 (masked
+        # updates of all exporters, no compaction of the accepted ones)
+        p_out = torch.cat([p_up, p_dn])
+        if p_out.numel():
+            acc = torch.cat([acc_up, acc_dn])
+            f = 1.0 - 0.5 * acc.to(torch.float32)
+            self.cell_molecules[p_out] = self.cell_molecules[p_out] * f[:, None]
+            self.cell_divisions[p_out] = self.cell_divisions[p_out] + acc.to(torch.int32)
+            self.cell_lifetimes[p_out] = torch.where(acc, 0, self.cell_lifetimes[p_out])
+            n_out = int(acc.sum())
+        else:
+            n_out = 0
         mig = self.migrated
-        mig["divided_out"] += int(out.numel())
+        mig["divided_out"] += n_out
         mig["divided_in"] += got
-        mig["rejected"] += int(acc_up.numel() + acc_dn.numel() - out.numel())
-        parents, cpos = parents[loc], cpos[loc]
+        mig["rejected"] += int(p_out.numel()) - n_out
+        parents, cpos = parents[i_loc], cpos[i_loc]
         k = int(parents.numel())
         if k == 0:
             return empty, empty
         n0 = self.n_cells
         children = torch.arange(n0, n0 + k, device=dev)
         self._clone_rows(parents, children)
-        self._place(children, cpos)
+        if cpos.is_cuda:
+            self.cell_positions[n0 : n0 + k] = cpos
+        else:
+            self._place(children, cpos)
         world_ops.split_cells(self, parents, children)
         return parents, children
+
+    def _split_by_row(self, rows: torch.Tensor):
+        """Indices (in order) of entries whose local row is owned / the upper halo (0) / the lower
+        halo (H + 1): one stable sort and one read-back."""
+        if rows.numel() == 0:
+            e = torch.zeros(0, dtype=torch.long, device=rows.device)
+            return e, e, e
+        cls = (rows == 0).to(torch.int8) + 2 * (rows == self.H + 1).to(torch.int8)
+        order = torch.sort(cls, stable=True).indices
+        c = torch.bincount(cls.to(torch.int64), minlength=3).tolist()
+        return order[: c[0]], order[c[0] : c[0] + c[1]], order[c[0] + c[1] :]
 
     def move_cells(self, cell_idxs=None):
         """Movement (collective). Cells moving into a neighbour's boundary row migrate to it."""
@@ -414,18 +437,20 @@ class DistributedWorld(World):
             moved, npos = moved.to(dev), npos.to(dev)
         else:
             moved, npos = torch.zeros(0, dtype=torch.long, device=dev), torch.zeros(0, 2, dtype=torch.int32, device=dev)
-        row = npos[:, 0]
-        up, dn = row == 0, row == self.H + 1
-        loc = ~(up | dn)
-        m_up, m_dn = moved[up], moved[dn]
-        # local moves first, so the owner's arbitration sees its final occupancy
-        if bool(loc.any()):
-            mv = moved[loc]
-            old = self.cell_positions[mv].long()
-            self.cell_map[old[:, 0], old[:, 1]] = False
-            self._place(mv, npos[loc])
-        rec_up = self._records(m_up, npos[up, 1], False)
-        rec_dn = self._records(m_dn, npos[dn, 1], False)
+        i_loc, i_up, i_dn = self._split_by_row(npos[:, 0])
+        m_up, m_dn = moved[i_up], moved[i_dn]
+        # local moves first, so the owner's arbitration sees its final occupancy (the placement
+        # kernels already vacated their old pixels and marked the new ones)
+        if i_loc.numel():
+            mv = moved[i_loc]
+            if npos.is_cuda:
+                self.cell_positions[mv] = npos[i_loc]
+            else:
+                old = self.cell_positions[mv].long()
+                self.cell_map[old[:, 0], old[:, 1]] = False
+                self._place(mv, npos[i_loc])
+        rec_up = self._records(m_up, npos[i_up, 1], False)
+        rec_dn = self._records(m_dn, npos[i_dn, 1], False)
         acc_up, acc_dn, got = self._migrate(rec_up, rec_dn)
         self.cell_map[0] = False
         self.cell_map[self.H + 1] = False
@@ -443,7 +468,13 @@ class DistributedWorld(World):
         self.cell_map[pos[:, 0], pos[:, 1]] = False
         keep = torch.ones(self.n_cells, dtype=torch.bool, device=self.device)
         keep[idxs] = False
-        self._compact(torch.nonzero(keep).flatten(), keep)
+        if keep.is_cuda:
+            from magicsoup_amd.ops import hip_ops
+
+            keep_idx, gone, _ = hip_ops.select(keep, "set", rest=True)
+            self._compact(keep_idx, None, removed=gone)
+        else:
+            self._compact(torch.nonzero(keep).flatten(), keep)
 
     def reposition_cells(self, cell_idxs=None):
         """Move cells to random free pixels of this rank's strip (cells do not change rank)."""
