@@ -67,3 +67,45 @@ def test_synthetic_wide_chemistry():
     assert w.kinetics.N.size(2) == 128
     w.enzymatic_activity()
     assert torch.isfinite(w.cell_molecules).all()
+
+
+def test_figure_sanity_checks_quick():
+    """docs/figures.py: every supporting figure's sanity property holds (quick sizes, no plots)."""
+    import importlib.util
+    from pathlib import Path
+
+    spec = importlib.util.spec_from_file_location("figures", Path(__file__).resolve().parents[1] / "docs" / "figures.py")
+    fig = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(fig)
+    check = fig.run(quick=True, plot=False)
+    bad = [(n, d) for n, ok, d in check.results if not ok]
+    assert not bad, bad
+
+
+def test_demo_run_and_gif(tmp_path):
+    """docs/run.py writes scalars, frames, checkpoints and the pickled world; docs/create_gif.py
+    renders them; a checkpoint reloads into World.from_file."""
+    import importlib.util
+    import json
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1] / "docs"
+
+    def load(name):
+        spec = importlib.util.spec_from_file_location(name, root / f"{name}.py")
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        return mod
+
+    run, gif = load("run"), load("create_gif")
+    rundir = run.main(run._args(["--rundir", str(tmp_path / "r"), "--n-steps", "6", "--map-size", "32",
+                                 "--init-n-cells", "60", "--check-every", "2", "--save-state", "--device", "cpu",
+                                 "--seed", "1"]))
+    lines = [json.loads(x) for x in open(rundir / "scalars.jsonl")]
+    assert [x["step"] for x in lines] == [0, 2, 4] and "ATP" in lines[0]
+    assert gif.create_gif([rundir, rundir], tmp_path / "c.gif") == 3
+    import magicsoup_amd as ms
+
+    w = ms.World.from_file(rundir=rundir)
+    w.load_state(statedir=rundir / "step=4")
+    assert w.n_cells == lines[-1]["n_cells"]
