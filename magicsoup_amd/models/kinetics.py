@@ -362,16 +362,11 @@ class Kinetics:
         if isinstance(cell_idxs, list) and len(cell_idxs) == 0:
             return
         if self._slot_tensor() is not None:
-            # shared rows: point the cells at one fresh all-zero row
+            # shared rows: point the cells at the all-zero row
             cells = torch.as_tensor(cell_idxs, device=self._slot_tensor().device).long()
             if cells.numel() == 0:
                 return
-            row = self._alloc_rows(1)
-            ok = self._pack_ok()
-            for t in self._store.values():
-                t[row] = 0  # packed words 0 and Q = 0 match all-zero parameters
-            self.__dict__["_slot"][cells] = row
-            self._restamp(ok)
+            self.__dict__["_slot"][cells] = self._zero_row()
             return
         rows = self._rows(cell_idxs)
         ok = self._pack_ok()
@@ -442,6 +437,7 @@ class Kinetics:
             d["_store_d"], d["_slot"], d["_ncells"], d["_nrows"] = {}, None, 0, 0
         self._materialize()
         self._drop_packed()
+        d.pop("_zero_row_t", None)
         t = torch.as_tensor(value)
         if not t.is_contiguous():
             t = t.contiguous()
@@ -467,6 +463,23 @@ class Kinetics:
             d["_slot"] = torch.arange(n, device=self._store["N"].device)
             d["_nrows"] = n
 
+    def _zero_row(self) -> torch.Tensor:
+        """Index (int64 (1,), device) of a storage row holding all-zero parameters, shared by cells
+        without a proteome. Created once per storage layout; never written afterwards (builds
+        always take fresh rows)."""
+        d = self.__dict__
+        z = d.get("_zero_row_t")
+        if z is not None:
+            return z
+        z = self._alloc_rows(1)
+        r = int(d["_nrows"]) - 1
+        ok = self._pack_ok()
+        for t in self._store.values():
+            t[r : r + 1].zero_()  # packed words 0 and Q = 0 match all-zero parameters
+        self._restamp(ok)
+        d["_zero_row_t"] = z
+        return z
+
     def _alloc_rows(self, k: int) -> torch.Tensor:
         """k unused storage rows (int64, device) for cells whose parameters are about to be written.
         Rows of removed cells are not tracked (a row may be shared); when the storage is exhausted
@@ -479,8 +492,9 @@ class Kinetics:
             self._materialize()  # dense again: rows 0..n-1 live
             self._enter_slot_mode()
             n = d["_ncells"]
-            if n + k > cap:
-                new_cap = max(n + k, int(cap * 1.5) + 64)
+            if n + k + n // 2 > cap:
+                # keep >= n/2 spare rows after a re-gather so that re-gathers stay rare (amortised)
+                new_cap = max(n + k + n // 2, int(cap * 1.5) + 64)
                 ok = self._pack_ok()
                 for name, t in list(store.items()):
                     nb = torch.empty(new_cap, *t.shape[1:], dtype=t.dtype, device=t.device)
@@ -572,6 +586,7 @@ class Kinetics:
             spare[k], store[k] = store[k], target[k]
         d["_slot"] = None
         d["_nrows"] = n
+        d.pop("_zero_row_t", None)
         self._restamp(ok)
 
     def remove_cell_params(self, keep: torch.Tensor, removed: torch.Tensor | None = None):
@@ -608,16 +623,11 @@ class Kinetics:
         d = self.__dict__
         store = self._store
         if d["_slot"] is not None:
-            # GPU row storage: the new cells share one fresh all-zero row (a later build gives them
+            # GPU row storage: the new cells share the all-zero row (a later build gives them
             # rows of their own)
-            row = self._alloc_rows(1)
-            ok = self._pack_ok()
-            for t in store.values():
-                t[row] = 0
-            slot = d["_slot"]
-            d["_slot"] = torch.cat([slot, row.expand(by_n)])
+            row = self._zero_row()
+            d["_slot"] = torch.cat([d["_slot"], row.expand(by_n)])
             d["_ncells"] += by_n
-            self._restamp(ok)
             return
         cap = min(int(t.size(0)) for t in store.values())
         ok = self._pack_ok()

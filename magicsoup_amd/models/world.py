@@ -442,7 +442,7 @@ class World:
         self._genomes.append_packed(rows, lens)
         self._labels.append_packed(*self._random_labels(k))
         new = torch.arange(n0, n0 + k, device=self.device)
-        self._place(new, pos)
+        self._place_new(n0, pos)
         world_ops.pickup_molecules(self, new, pos)
         self._update_params_rows(new)
         return list(range(n0, n0 + k))
@@ -468,7 +468,7 @@ class World:
         self._genomes.append_strings([c.genome for c in cells])
         self._labels.append_strings([c.label for c in cells])
         new = torch.arange(n0, n0 + k, device=self.device)
-        self._place(new, pos)
+        self._place_new(n0, pos)
         mols = torch.stack([torch.as_tensor(c.int_molecules) for c in cells]).to(self.device, torch.float32)
         self.cell_molecules[n0:] = mols
         self.cell_lifetimes[n0:] = torch.tensor([c.n_steps_alive for c in cells], dtype=torch.int32)
@@ -604,13 +604,25 @@ class World:
         old = self.cell_positions[idxs].long()
         self.cell_map[old[:, 0], old[:, 1]] = False
         pos = world_ops.free_positions(self, int(idxs.numel()))
-        self._place(idxs[: pos.size(0)], pos)
+        if pos.is_cuda:
+            self.cell_positions[idxs[: pos.size(0)]] = pos  # claimed by the kernel
+        else:
+            self._place(idxs[: pos.size(0)], pos)
 
     def _place(self, idxs: torch.Tensor, pos: torch.Tensor) -> None:
         pos = pos.to(self.device, torch.int32)
         self.cell_positions[idxs] = pos
         p = pos.long()
         self.cell_map[p[:, 0], p[:, 1]] = True
+
+    def _place_new(self, n0: int, pos: torch.Tensor) -> None:
+        """Positions of the new rows n0.. from world_ops.free_positions (on the GPU those pixels
+        are already claimed in cell_map by the claim kernel)."""
+        k = int(pos.size(0))
+        if pos.is_cuda:
+            self.cell_positions[n0 : n0 + k] = pos
+        else:
+            self._place(torch.arange(n0, n0 + k, device=self.device), pos)
 
     # ------------------------------------------------------------------ physics
     @_op("enzymatic_activity")
