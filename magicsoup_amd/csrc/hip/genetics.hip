@@ -37,6 +37,7 @@ struct TransArgs {
   int32_t* ndom;    // (2n,) max domains per strand (count pass)
   int32_t* tokens;  // (n, P, D, 5) (write pass)
   int P, D;
+  const int* dn;    // optional device item count (<= n; n is then the capacity)
 };
 
 __host__ __device__ inline size_t slot_bytes_for(int width, int cap) {
@@ -64,6 +65,8 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   // codons [2][lmax] u8, domain type at position [2][lmax] u8, counters
   const size_t slot_bytes = slot_bytes_for(a.lmax, a.cap);
   const int item = blockIdx.x * a.gpb + wid;
+  const int n_eff = a.dn ? min(*a.dn, a.n) : a.n;
+  if ((int)blockIdx.x * a.gpb >= n_eff) return;  // whole block past the device count
   uint8_t* slot = a.gslot ? a.gslot + (size_t)item * slot_bytes
                           : sm + kLutBytes + dt_bytes + (size_t)wid * slot_bytes;
   const int LW = a.lmax;
@@ -86,7 +89,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
       reinterpret_cast<uint4*>(l_dt)[i] = reinterpret_cast<const uint4*>(a.dom_type)[i];
   const uint8_t* DT = a.stage_dt ? l_dt : a.dom_type;
 
-  const bool active = wid < a.gpb && item < a.n;
+  const bool active = wid < a.gpb && item < n_eff;
   const int g = active ? (a.list ? a.list[item] : item) : 0;
   int L = 0;
   const uint8_t* s = nullptr;
@@ -260,7 +263,7 @@ constexpr int kLdsMaxLen = 1024;  // genomes up to this length use LDS slots
 static void launch(bool write, int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
                    uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                    uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t list, uintptr_t gslot,
-                   uintptr_t long_list, uintptr_t long_count, uintptr_t stream) {
+                   uintptr_t long_list, uintptr_t long_count, uintptr_t dn, uintptr_t stream) {
   if (n <= 0) return;
   if (width % 16 != 0) throw std::invalid_argument("genome arena width must be a multiple of 16");
   if (width > 65535) throw std::invalid_argument("genomes longer than 65535 nt are not supported on the GPU");
@@ -289,6 +292,8 @@ static void launch(bool write, int n, uintptr_t rows, uintptr_t arena, int width
   a.gslot = gslot ? P_<uint8_t>(gslot) : nullptr;
   a.long_list = P_<int32_t>(long_list);
   a.long_count = P_<int32_t>(long_count);
+  a.dn = dn ? P_<int>(dn) : nullptr;
+  if (a.dn && a.gslot) throw std::invalid_argument("translate: the long-genome pass needs a host count");
   // LDS pass: slots for genomes up to kLdsMaxLen (longer ones are queued); global pass: whole width
   a.lmax = a.gslot ? width : (width < kLdsMaxLen ? width : kLdsMaxLen);
   a.cap = a.lmax;  // a strand has at most one CDS per codon position
@@ -315,17 +320,17 @@ size_t translate_slot_bytes(int width) { return slot_bytes_for(width, width); }
 void translate_count(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                      uintptr_t nprot, uintptr_t ndom, uintptr_t list, uintptr_t gslot, uintptr_t long_list,
-                     uintptr_t long_count, uintptr_t stream) {
+                     uintptr_t long_count, uintptr_t dn, uintptr_t stream) {
   launch(false, n, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot,
-         ndom, 0, 0, 0, list, gslot, long_list, long_count, stream);
+         ndom, 0, 0, 0, list, gslot, long_list, long_count, dn, stream);
 }
 
 void translate_write(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                      uintptr_t nprot, int P, int D, uintptr_t tokens, uintptr_t list, uintptr_t gslot,
-                     uintptr_t stream) {
+                     uintptr_t dn, uintptr_t stream) {
   launch(true, n, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot, 0,
-         P, D, tokens, list, gslot, 0, 0, stream);
+         P, D, tokens, list, gslot, 0, 0, dn, stream);
 }
 
 }  // namespace msd

@@ -15,6 +15,8 @@
 //     buffer and every cell ORs its "still correcting" bits into one word per part. The next part
 //     (or the final scatter) picks the state where the reference's global `torch.any` loop stops.
 //   3 part launches + 1 scatter launch per enzymatic_activity; no grid barriers, no host syncs.
+#include <algorithm>
+
 #include "hip_common.h"
 #include "map_types.h"
 #include "ms_kinetics.h"
@@ -424,6 +426,7 @@ struct BuildArgs {
   int32_t* W;  // integrator layout (optional: nullptr skips it)
   float4* Q;
   int* overflow;
+  const int* dn;  // optional device row count (<= n; n is then the capacity)
 };
 
 __device__ __forceinline__ int lut(int t, int lim) { return (t >= 0 && t < lim) ? t : 0; }
@@ -434,11 +437,9 @@ __device__ __forceinline__ int lut(int t, int lim) { return (t >= 0 && t < lim) 
 // double (integer N times float energies: exact, hence order-independent) so host and device agree
 // bit for bit.
 template <int G>
-__global__ void __launch_bounds__(kBlock) build_params_kernel(BuildArgs b) {
-  const long long grp = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / G;
-  const int lane = threadIdx.x % G;
-  if (grp >= (long long)b.n * b.Pt) return;  // whole groups exit together
+__device__ __forceinline__ void build_group(const BuildArgs& b, long long grp, int lane) {
   const int ci = (int)(grp / b.Pt), p = (int)(grp - (long long)ci * b.Pt);
+  if (b.rows[ci] < 0) return;  // no row assigned (device pipeline ran out of rows)
   const size_t row = (size_t)b.rows[ci];
   const size_t o2 = row * b.Pt + p, o3 = o2 * b.s;
   const int32_t* pt = b.tokens + ((size_t)ci * b.P + (p < b.P ? p : 0)) * b.D * 5;
@@ -521,6 +522,16 @@ __global__ void __launch_bounds__(kBlock) build_params_kernel(BuildArgs b) {
   b.Vmax[o2] = vmv;
   if (b.Q) b.Q[o2] = make_float4(vmv, kmfv, kmbv, kev);
 }
+
+template <int G>
+__global__ void __launch_bounds__(kBlock) build_params_kernel(BuildArgs b) {
+  const int lane = threadIdx.x % G;
+  const long long n_eff = b.dn ? (long long)min(*b.dn, b.n) : (long long)b.n;
+  const long long groups = n_eff * b.Pt, stride = (long long)gridDim.x * (blockDim.x / G);
+  for (long long grp = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / G; grp < groups; grp += stride)
+    build_group<G>(b, grp, lane);  // whole groups iterate together
+}
+
 
 // ---------------------------------------------------------------------------------------------
 // Host launchers
@@ -648,7 +659,7 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
                   uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
                   uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
                   uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t W, uintptr_t Q, uintptr_t overflow,
-                  uintptr_t stream) {
+                  uintptr_t dn, uintptr_t stream) {
   if (n <= 0 || Pt <= 0) return;
   if ((W == 0) != (Q == 0) || (W != 0 && overflow == 0)) throw std::invalid_argument("build_params: W, Q, overflow");
   if (P > Pt) throw std::invalid_argument("build_params: token proteins exceed parameter capacity");
@@ -664,9 +675,12 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
   b.N = P_<int32_t>(N); b.Nf = P_<int32_t>(Nf); b.Nb = P_<int32_t>(Nb); b.A = P_<int32_t>(A);
   b.Kmr = P_<float>(Kmr); b.Kmf = P_<float>(Kmf); b.Kmb = P_<float>(Kmb); b.Vmax = P_<float>(Vmax); b.Ke = P_<float>(Ke);
   b.W = W ? P_<int32_t>(W) : nullptr; b.Q = Q ? P_<float4>(Q) : nullptr; b.overflow = P_<int>(overflow);
+  b.dn = dn ? P_<int>(dn) : nullptr;
   const long long groups = (long long)n * Pt;
-  if (s <= 32) build_params_kernel<32><<<cdiv(groups * 32, kBlock), kBlock, 0, S_(stream)>>>(b);
-  else build_params_kernel<64><<<cdiv(groups * 64, kBlock), kBlock, 0, S_(stream)>>>(b);
+  // with a device count the grid is capped and strides (the host passes the capacity as n)
+  auto grid = [&](int g) { const unsigned full = cdiv(groups * g, kBlock); return dn ? std::min(full, 4096u) : full; };
+  if (s <= 32) build_params_kernel<32><<<grid(32), kBlock, 0, S_(stream)>>>(b);
+  else build_params_kernel<64><<<grid(64), kBlock, 0, S_(stream)>>>(b);
   MS_LAUNCH_CHECK();
 }
 

@@ -22,7 +22,7 @@ void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo,
 void neighbor_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map, uintptr_t keys,
                     uintptr_t stream);
 void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
-                    uintptr_t tot, uintptr_t stream);
+                    uintptr_t tot, int kcap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
 // maps.hip
 size_t diffuse_partials_len(int m, int C, int H);
 void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
@@ -55,7 +55,8 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
                   uintptr_t km_w, int nk, uintptr_t signs, int nsg, uintptr_t hills, int nh, uintptr_t RM,
                   uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
                   uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
-                  uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t W, uintptr_t Q, uintptr_t overflow, uintptr_t stream);
+                  uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t W, uintptr_t Q, uintptr_t overflow,
+                  uintptr_t dn, uintptr_t stream);
 void pack_params(long long items, int s, uintptr_t N, uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Vmax,
                  uintptr_t Kmf, uintptr_t Kmb, uintptr_t Ke, uintptr_t W, uintptr_t Q, uintptr_t overflow,
                  uintptr_t stream);
@@ -69,28 +70,37 @@ void neighbor_pairs(int nf, int n, uintptr_t from, uintptr_t pos, int R, int C, 
 void translate_count(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                      uintptr_t nprot, uintptr_t ndom, uintptr_t list, uintptr_t gslot, uintptr_t long_list,
-                     uintptr_t long_count, uintptr_t stream);
+                     uintptr_t long_count, uintptr_t dn, uintptr_t stream);
 void translate_write(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                      uintptr_t nprot, int P, int D, uintptr_t tokens, uintptr_t list, uintptr_t gslot,
-                     uintptr_t stream);
+                     uintptr_t dn, uintptr_t stream);
 size_t translate_slot_bytes(int width);
 // mutations.hip
-void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
-               uintptr_t stream);
-void mut_apply(int nsel, uintptr_t sel, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t k,
-               double p_indel, double p_del, uint64_t seed, uint64_t call, uintptr_t out, int out_width,
+void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
+               uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
+void mut_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens,
+               uintptr_t k, double p_indel, double p_del, uint64_t seed, uint64_t call, uintptr_t out, int out_width,
                uintptr_t out_len, uintptr_t stream);
 void rec_count(int n, uintptr_t pairs, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
                uintptr_t stream);
-void rec_apply(int nsel, uintptr_t sel, uintptr_t pairs, uintptr_t keys, uintptr_t arena, int width, uintptr_t lens,
-               uintptr_t k, uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out, int out_width,
-               uintptr_t out_len, uintptr_t out_rows, uintptr_t stream);
-void arena_scatter(int k, uintptr_t rows, uintptr_t src, int src_width, uintptr_t src_len, uintptr_t arena, int width,
-                   uintptr_t lens, uintptr_t mark, uint64_t gen, uintptr_t flags, uintptr_t stream);
+void rec_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t pairs, uintptr_t keys, uintptr_t arena, int width,
+               uintptr_t lens, uintptr_t k, uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out,
+               int out_width, uintptr_t out_len, uintptr_t out_rows, uintptr_t stream);
+void arena_scatter(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t src, int src_width, uintptr_t src_len,
+                   uintptr_t arena, int width, uintptr_t lens, uintptr_t mark, uint64_t gen, uintptr_t flags,
+                   uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
 void place_collect(int k, uintptr_t wins, uintptr_t cells, uintptr_t result, int C, uintptr_t par, uintptr_t npos,
                    uintptr_t stream);
 // select.hip
+void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel, uintptr_t rest,
+                        uintptr_t out_dev, uintptr_t stream);
+void trans_check(int cap, uintptr_t dn, uintptr_t counts, uintptr_t ndom, uintptr_t long_count, uintptr_t per, int Pcap,
+                 int Dcap, uintptr_t flags, uintptr_t stream);
+void zero_rows(int cap, uintptr_t dn, long long row, uintptr_t buf, uintptr_t stream);
+void assign_rows(int ncap, uintptr_t dn, uintptr_t cells, uintptr_t slot, uintptr_t d_rows, long long row_cap,
+                 uintptr_t rows_out, uintptr_t flags, uintptr_t stream);
+void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t dst, uintptr_t stream);
 std::tuple<int, int, int> translate_stats(int n, uintptr_t counts, uintptr_t ndom, uintptr_t long_count, uintptr_t per,
                                           uintptr_t stream);
 std::pair<long long, int> select_indices(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel,
@@ -150,6 +160,11 @@ PYBIND11_MODULE(_hip, m) {
   m.def("place_collect", &msd::place_collect);
   m.def("translate_stats", &msd::translate_stats,
         "(max proteins, max domains, long genomes) of a translate count pass; synchronises the stream");
+  m.def("select_indices_dev", &msd::select_indices_dev);
+  m.def("trans_check", &msd::trans_check);
+  m.def("zero_rows", &msd::zero_rows);
+  m.def("assign_rows", &msd::assign_rows);
+  m.def("gather_dev", &msd::gather_dev);
   m.def("select_indices", &msd::select_indices,
         "(count, max) of an order-preserving compaction; synchronises the stream");
 }

@@ -6,6 +6,8 @@
 // wavefront per item: one lane draws the k event positions (Floyd's sorted sampling) into an LDS
 // plan, then all 64 lanes stream the new sequence into a scratch row; the host side copies the
 // rows back into the arena.
+#include <algorithm>
+
 #include "hip_common.h"
 
 namespace msd {
@@ -43,10 +45,25 @@ __device__ __forceinline__ uint8_t rand_nt(Philox& rng) {
 }
 
 // k[i] ~ Poisson(p * len(row_i))
+// Device pipelines (magicsoup_amd/ops/genome_pipeline.py): an op whose predecessor in the same
+// pending chain could not commit a genome (arena too narrow) does nothing and is replayed by the
+// host later, so the chain never works on a stale genome.
+constexpr int kGpWidth = 8, kGpSkipped = 16;
+__device__ __forceinline__ bool gp_skip(int i, const int* gflags, int* opflags) {
+  if (!gflags || !(*gflags & kGpWidth)) return false;
+  if (i == 0) atomicOr(opflags, kGpSkipped);
+  return true;
+}
+
 __global__ void __launch_bounds__(256) mut_count_kernel(int n, const int64_t* rows, const int32_t* lens, double p,
-                                                        uint64_t seed, uint64_t call, int32_t* k) {
+                                                        uint64_t seed, uint64_t call, int32_t* k, int kcap,
+                                                        const int* gflags, int* opflags) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (gp_skip(i, gflags, opflags)) {
+    k[i] = 0;
+    return;
+  }
   const int64_t r = rows ? rows[i] : i;
   const int L = lens[r];
   if (L < 1) {
@@ -55,6 +72,7 @@ __global__ void __launch_bounds__(256) mut_count_kernel(int n, const int64_t* ro
   }
   Philox rng(seed, call, (uint32_t)i);
   long long kk = poisson(rng, p * (double)L);
+  if (kcap > 0 && kk > kcap) kk = kcap;
   k[i] = (int32_t)(kk > L ? L : kk);
 }
 
@@ -83,15 +101,11 @@ __device__ __forceinline__ void wave_copy(const uint8_t* src, int a, int b, uint
 // One wavefront per selected genome: lane 0 draws the event positions and the emitted literals into
 // an LDS plan (copy segment, literal, copy segment, ...); all lanes then stream the segments.
 // Genomes with more than kFloydMax events (very high rates) take a serial selection-sampling path.
-__global__ void __launch_bounds__(64) mut_apply_kernel(int nsel, const int64_t* sel, const int64_t* rows,
-                                                       const uint8_t* arena, int width, const int32_t* lens,
-                                                       const int32_t* k, double p_indel, double p_del, uint64_t seed,
-                                                       uint64_t call, uint8_t* out, int out_width, int32_t* out_len) {
-  __shared__ int pos[kFloydMax];
-  __shared__ uint8_t lit[kFloydMax][2];
-  __shared__ int nlit[kFloydMax];
-  const int j = blockIdx.x, lane = threadIdx.x;
-  if (j >= nsel) return;
+__device__ __forceinline__ void mut_apply_item(int j, const int64_t* sel, const int64_t* rows, const uint8_t* arena,
+                                               int width, const int32_t* lens, const int32_t* k, double p_indel,
+                                               double p_del, uint64_t seed, uint64_t call, uint8_t* out, int out_width,
+                                               int32_t* out_len, int* pos, uint8_t (*lit)[2], int* nlit) {
+  const int lane = threadIdx.x;
   const int64_t i = sel[j];
   const int64_t r = rows ? rows[i] : i;
   const uint8_t* s = arena + (size_t)r * width;
@@ -137,6 +151,23 @@ __global__ void __launch_bounds__(64) mut_apply_kernel(int nsel, const int64_t* 
   if (lane == 0) out_len[j] = w < out_width ? w : out_width;
 }
 
+// dn: optional device-side item count (<= nsel): the grid strides over the items, so the host does
+// not need to know how many genomes were selected.
+__global__ void __launch_bounds__(64) mut_apply_kernel(int nsel, const int* dn, const int64_t* sel, const int64_t* rows,
+                                                       const uint8_t* arena, int width, const int32_t* lens,
+                                                       const int32_t* k, double p_indel, double p_del, uint64_t seed,
+                                                       uint64_t call, uint8_t* out, int out_width, int32_t* out_len) {
+  __shared__ int pos[kFloydMax];
+  __shared__ uint8_t lit[kFloydMax][2];
+  __shared__ int nlit[kFloydMax];
+  const int ne = dn ? min(*dn, nsel) : nsel;
+  for (int j = blockIdx.x; j < ne; j += gridDim.x) {
+    mut_apply_item(j, sel, rows, arena, width, lens, k, p_indel, p_del, seed, call, out, out_width, out_len, pos, lit,
+                   nlit);
+    __syncthreads();
+  }
+}
+
 // k[i] ~ Poisson(p * (len(a) + len(b))) for neighbour pair i
 __global__ void __launch_bounds__(256) rec_count_kernel(int n, const int32_t* pairs, const int32_t* lens, double p,
                                                         uint64_t seed, uint64_t call, int32_t* k) {
@@ -154,9 +185,15 @@ __global__ void __launch_bounds__(256) rec_count_kernel(int n, const int32_t* pa
 
 // Same draw over fixed neighbour slots (int64 keys (a << 32) | b, -1 = empty slot).
 __global__ void __launch_bounds__(256) rec_count_keys_kernel(int n, const int64_t* keys, const int32_t* lens, double p,
-                                                             uint64_t seed, uint64_t call, int32_t* k, int32_t* tot) {
+                                                             uint64_t seed, uint64_t call, int32_t* k, int32_t* tot,
+                                                             int kcap, const int* gflags, int* opflags) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (gp_skip(i, gflags, opflags)) {
+    k[i] = 0;
+    if (tot) tot[i] = 0;
+    return;
+  }
   const int64_t key = keys[i];
   if (key < 0) {
     k[i] = 0;
@@ -171,6 +208,7 @@ __global__ void __launch_bounds__(256) rec_count_keys_kernel(int n, const int64_
   }
   Philox rng(seed, call, (uint32_t)i);
   long long kk = poisson(rng, p * (double)nb);
+  if (kcap > 0 && kk > kcap) kk = kcap;
   k[i] = (int32_t)(kk > nb ? nb : kk);
 }
 
@@ -178,15 +216,12 @@ __global__ void __launch_bounds__(256) rec_count_keys_kernel(int n, const int64_
 // them at a random index into two new genomes (scratch rows 2j and 2j+1). One wavefront per pair:
 // lane 0 plans the parts (LDS for up to kFloydMax cuts, else the global `parts` scratch with
 // parts_cap entries of 3 ints), then all lanes copy them.
-__global__ void __launch_bounds__(64) rec_apply_kernel(int nsel, const int64_t* sel, const int32_t* pairs,
-                                                       const int64_t* keys, const uint8_t* arena, int width,
-                                                       const int32_t* lens, const int32_t* k, uint64_t seed,
-                                                       uint64_t call, int32_t* parts, int parts_cap, uint8_t* out,
-                                                       int out_width, int32_t* out_len, int64_t* out_rows) {
-  __shared__ int32_t lparts[(kFloydMax + 2) * 3];
-  __shared__ int meta[2];  // number of parts, split index
-  const int j = blockIdx.x, lane = threadIdx.x;
-  if (j >= nsel) return;
+__device__ __forceinline__ void rec_apply_item(int j, const int64_t* sel, const int32_t* pairs, const int64_t* keys,
+                                               const uint8_t* arena, int width, const int32_t* lens, const int32_t* k,
+                                               uint64_t seed, uint64_t call, int32_t* parts, int parts_cap,
+                                               uint8_t* out, int out_width, int32_t* out_len, int64_t* out_rows,
+                                               int32_t* lparts, int* meta) {
+  const int lane = threadIdx.x;
   const int64_t i = sel[j];
   // pairs: int32 (a, b) rows, or int64 slot keys (a << 32) | b
   const int ca = keys ? (int)(keys[i] >> 32) : pairs[2 * i];
@@ -277,52 +312,87 @@ __global__ void __launch_bounds__(64) rec_apply_kernel(int nsel, const int64_t* 
   }
 }
 
+__global__ void __launch_bounds__(64) rec_apply_kernel(int nsel, const int* dn, const int64_t* sel, const int32_t* pairs,
+                                                       const int64_t* keys, const uint8_t* arena, int width,
+                                                       const int32_t* lens, const int32_t* k, uint64_t seed,
+                                                       uint64_t call, int32_t* parts, int parts_cap, uint8_t* out,
+                                                       int out_width, int32_t* out_len, int64_t* out_rows) {
+  __shared__ int32_t lparts[(kFloydMax + 2) * 3];
+  __shared__ int meta[2];  // number of parts, split index
+  const int ne = dn ? min(*dn, nsel) : nsel;
+  for (int j = blockIdx.x; j < ne; j += gridDim.x) {
+    rec_apply_item(j, sel, pairs, keys, arena, width, lens, k, seed, call, parts, parts_cap, out, out_width, out_len,
+                   out_rows, lparts, meta);
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- arena commit
 // Last writer wins among duplicate target rows (a cell in several recombined pairs keeps the
 // result of the last pair, as the reference's sequential update does): generation-tagged 64-bit
 // marks, so the mark array never needs clearing.
-__global__ void __launch_bounds__(256) arena_mark_kernel(int k, const int64_t* rows, unsigned long long* mark,
-                                                         unsigned long long gen) {
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= k) return;
-  atomicMax(mark + rows[q], (gen << 32) | (unsigned long long)q);
+// dn (optional): device item count, scaled by dn_mul (2 for the two results of a recombined pair)
+__device__ __forceinline__ int eff_count(int k, const int* dn, int dn_mul) { return dn ? min(*dn * dn_mul, k) : k; }
+
+__global__ void __launch_bounds__(256) arena_mark_kernel(int k, const int* dn, int dn_mul, const int64_t* rows,
+                                                         unsigned long long* mark, unsigned long long gen) {
+  const int ke = eff_count(k, dn, dn_mul);
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < ke; q += gridDim.x * blockDim.x)
+    atomicMax(mark + rows[q], (gen << 32) | (unsigned long long)q);
 }
 
 // One wavefront per result row: copy it over its arena row (zero-padding the rest of the row) and
 // its length, if it won; flags[q] = won.
-__global__ void __launch_bounds__(64) arena_scatter_kernel(int k, const int64_t* rows, const uint8_t* src, int src_width,
-                                                           const int32_t* src_len, uint8_t* arena, int width,
-                                                           int32_t* lens, const unsigned long long* mark,
-                                                           unsigned long long gen, uint8_t* flags) {
-  const int q = blockIdx.x, lane = threadIdx.x;
-  if (q >= k) return;
-  const int64_t r = rows[q];
-  const bool won = !mark || mark[r] == ((gen << 32) | (unsigned long long)q);
-  if (lane == 0 && flags) flags[q] = won;
-  if (!won) return;
-  const int L = min(src_len[q], width);
-  const uint8_t* s = src + (size_t)q * src_width;
-  uint8_t* d = arena + (size_t)r * width;
-  for (int t = lane; t < width; t += 64) d[t] = t < L ? s[t] : 0;
-  if (lane == 0) lens[r] = L;
+__global__ void __launch_bounds__(64) arena_scatter_kernel(int k, const int* dn, int dn_mul, const int64_t* rows,
+                                                           const uint8_t* src, int src_width, const int32_t* src_len,
+                                                           uint8_t* arena, int width, int32_t* lens,
+                                                           const unsigned long long* mark, unsigned long long gen,
+                                                           uint8_t* flags, int* gflags, int* opflags) {
+  const int ke = eff_count(k, dn, dn_mul), lane = threadIdx.x;
+  for (int q = blockIdx.x; q < ke; q += gridDim.x) {
+    const int64_t r = rows[q];
+    const bool won = !mark || mark[r] == ((gen << 32) | (unsigned long long)q);
+    if (lane == 0 && flags) flags[q] = won;
+    if (!won) continue;
+    if (gflags && src_len[q] > width) {  // too long for the arena: left for the host (reconcile)
+      if (lane == 0) {
+        atomicOr(gflags, kGpWidth);
+        atomicOr(opflags, kGpWidth);
+      }
+      continue;
+    }
+    const int L = min(src_len[q], width);
+    const uint8_t* s = src + (size_t)q * src_width;
+    uint8_t* d = arena + (size_t)r * width;
+    for (int t = lane; t < width; t += 64) d[t] = t < L ? s[t] : 0;
+    if (lane == 0) lens[r] = L;
+  }
 }
 
-void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
-               uintptr_t stream) {
+// Item grids: with a device count (dn != 0) the launch covers at most kDevGrid blocks that stride
+// over the items; the host passes the capacity as n.
+constexpr unsigned kDevGrid = 2048;
+static unsigned item_grid(long long n, uintptr_t dn) {
+  return dn ? (unsigned)std::min<long long>(n, kDevGrid) : (unsigned)n;
+}
+
+void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
+               uintptr_t gflags, uintptr_t opflags, uintptr_t stream) {
   if (n <= 0) return;
   mut_count_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, rows ? P_<int64_t>(rows) : nullptr, P_<int32_t>(lens), p,
-                                                         seed, call, P_<int32_t>(k));
+                                                         seed, call, P_<int32_t>(k), kcap,
+                                                         gflags ? P_<int>(gflags) : nullptr, P_<int>(opflags));
   MS_LAUNCH_CHECK();
 }
 
-void mut_apply(int nsel, uintptr_t sel, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t k,
-               double p_indel, double p_del, uint64_t seed, uint64_t call, uintptr_t out, int out_width,
+void mut_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens,
+               uintptr_t k, double p_indel, double p_del, uint64_t seed, uint64_t call, uintptr_t out, int out_width,
                uintptr_t out_len, uintptr_t stream) {
   if (nsel <= 0) return;
-  mut_apply_kernel<<<nsel, 64, 0, S_(stream)>>>(nsel, P_<int64_t>(sel), rows ? P_<int64_t>(rows) : nullptr,
-                                                          P_<uint8_t>(arena), width, P_<int32_t>(lens), P_<int32_t>(k),
-                                                          p_indel, p_del, seed, call, P_<uint8_t>(out), out_width,
-                                                          P_<int32_t>(out_len));
+  mut_apply_kernel<<<item_grid(nsel, dn), 64, 0, S_(stream)>>>(
+      nsel, dn ? P_<int>(dn) : nullptr, P_<int64_t>(sel), rows ? P_<int64_t>(rows) : nullptr, P_<uint8_t>(arena),
+      width, P_<int32_t>(lens), P_<int32_t>(k), p_indel, p_del, seed, call, P_<uint8_t>(out), out_width,
+      P_<int32_t>(out_len));
   MS_LAUNCH_CHECK();
 }
 
@@ -335,37 +405,43 @@ void rec_count(int n, uintptr_t pairs, uintptr_t lens, double p, uint64_t seed, 
 }
 
 void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
-                    uintptr_t tot, uintptr_t stream) {
+                    uintptr_t tot, int kcap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream) {
   if (n <= 0) return;
   rec_count_keys_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, P_<int64_t>(keys), P_<int32_t>(lens), p, seed, call,
-                                                              P_<int32_t>(k), tot ? P_<int32_t>(tot) : nullptr);
+                                                              P_<int32_t>(k), tot ? P_<int32_t>(tot) : nullptr, kcap,
+                                                              gflags ? P_<int>(gflags) : nullptr, P_<int>(opflags));
   MS_LAUNCH_CHECK();
 }
 
-void rec_apply(int nsel, uintptr_t sel, uintptr_t pairs, uintptr_t keys, uintptr_t arena, int width, uintptr_t lens,
-               uintptr_t k, uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out, int out_width,
-               uintptr_t out_len, uintptr_t out_rows, uintptr_t stream) {
+void rec_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t pairs, uintptr_t keys, uintptr_t arena, int width,
+               uintptr_t lens, uintptr_t k, uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out,
+               int out_width, uintptr_t out_len, uintptr_t out_rows, uintptr_t stream) {
   if (nsel <= 0) return;
   if ((pairs == 0) == (keys == 0)) throw std::invalid_argument("rec_apply: give exactly one of pairs / keys");
-  rec_apply_kernel<<<nsel, 64, 0, S_(stream)>>>(nsel, P_<int64_t>(sel), pairs ? P_<int32_t>(pairs) : nullptr,
-                                                keys ? P_<int64_t>(keys) : nullptr, P_<uint8_t>(arena), width,
-                                                P_<int32_t>(lens), P_<int32_t>(k), seed, call, P_<int32_t>(parts),
-                                                parts_cap, P_<uint8_t>(out), out_width, P_<int32_t>(out_len),
-                                                out_rows ? P_<int64_t>(out_rows) : nullptr);
+  rec_apply_kernel<<<item_grid(nsel, dn), 64, 0, S_(stream)>>>(
+      nsel, dn ? P_<int>(dn) : nullptr, P_<int64_t>(sel), pairs ? P_<int32_t>(pairs) : nullptr,
+      keys ? P_<int64_t>(keys) : nullptr, P_<uint8_t>(arena), width, P_<int32_t>(lens), P_<int32_t>(k), seed, call,
+      P_<int32_t>(parts), parts_cap, P_<uint8_t>(out), out_width, P_<int32_t>(out_len),
+      out_rows ? P_<int64_t>(out_rows) : nullptr);
   MS_LAUNCH_CHECK();
 }
 
-void arena_scatter(int k, uintptr_t rows, uintptr_t src, int src_width, uintptr_t src_len, uintptr_t arena, int width,
-                   uintptr_t lens, uintptr_t mark, uint64_t gen, uintptr_t flags, uintptr_t stream) {
+// k result rows (capacity when dn != 0: then *dn * dn_mul rows are live)
+void arena_scatter(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t src, int src_width, uintptr_t src_len,
+                   uintptr_t arena, int width, uintptr_t lens, uintptr_t mark, uint64_t gen, uintptr_t flags,
+                   uintptr_t gflags, uintptr_t opflags, uintptr_t stream) {
+  if (gflags && !opflags) throw std::invalid_argument("arena_scatter: gflags needs opflags");
   if (k <= 0) return;
+  const int* d = dn ? P_<int>(dn) : nullptr;
   if (mark) {
-    arena_mark_kernel<<<cdiv(k, 256), 256, 0, S_(stream)>>>(k, P_<int64_t>(rows), P_<unsigned long long>(mark), gen);
+    const unsigned g = dn ? std::min<unsigned>(cdiv(k, 256), 256u) : cdiv(k, 256);
+    arena_mark_kernel<<<g, 256, 0, S_(stream)>>>(k, d, dn_mul, P_<int64_t>(rows), P_<unsigned long long>(mark), gen);
     MS_LAUNCH_CHECK();
   }
-  arena_scatter_kernel<<<k, 64, 0, S_(stream)>>>(k, P_<int64_t>(rows), P_<uint8_t>(src), src_width,
-                                                 P_<int32_t>(src_len), P_<uint8_t>(arena), width, P_<int32_t>(lens),
-                                                 mark ? P_<unsigned long long>(mark) : nullptr, gen,
-                                                 flags ? P_<uint8_t>(flags) : nullptr);
+  arena_scatter_kernel<<<item_grid(k, dn), 64, 0, S_(stream)>>>(
+      k, d, dn_mul, P_<int64_t>(rows), P_<uint8_t>(src), src_width, P_<int32_t>(src_len), P_<uint8_t>(arena), width,
+      P_<int32_t>(lens), mark ? P_<unsigned long long>(mark) : nullptr, gen, flags ? P_<uint8_t>(flags) : nullptr,
+      gflags ? P_<int>(gflags) : nullptr, opflags ? P_<int>(opflags) : nullptr);
   MS_LAUNCH_CHECK();
 }
 

@@ -196,6 +196,97 @@ std::tuple<int, int, int> translate_stats(int n, uintptr_t counts, uintptr_t ndo
   return {g_host[0], g_host[1], g_host[2]};
 }
 
+// ---------------------------------------------------------------- device-count pipelines
+// Sync-free genome updates (mutate / recombinate on the GPU): the selected count stays on the
+// device, later kernels stride over it, and overflow conditions the host could not rule out in
+// advance raise flag bits that the host resolves at its next synchronisation point.
+enum DevFlag { kFlagTranslate = 1, kFlagCapacity = 2, kFlagRows = 4 };
+
+// Like select_indices, but {count, max} go to device memory (out_dev) and nothing is synchronised.
+void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel, uintptr_t rest,
+                        uintptr_t out_dev, uintptr_t stream);
+
+// Per-genome protein totals and the caps of the speculative token layout: flags translation
+// overflow (more proteins than the parameter storage holds, more domains than the token slots, a
+// genome too long for the LDS pass) and a count above the capacity of the pipeline buffers.
+__global__ void __launch_bounds__(256) trans_check_kernel(int cap, const int* dn, const int32_t* counts,
+                                                          const int32_t* ndom, const int32_t* long_count,
+                                                          int32_t* per, int Pcap, int Dcap, int* flags) {
+  const int n = min(*dn, cap);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (*dn > cap) atomicOr(flags, (int)kFlagCapacity);
+    if (*long_count > 0) atomicOr(flags, (int)kFlagTranslate);
+  }
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int p = counts[2 * i] + counts[2 * i + 1];
+    per[i] = p;
+    if (p > Pcap || ndom[2 * i] > Dcap || ndom[2 * i + 1] > Dcap) atomicOr(flags, (int)kFlagTranslate);
+  }
+}
+
+// buf[i * row : (i + 1) * row] = 0 for i < min(*dn, cap)
+__global__ void __launch_bounds__(256) zero_rows_kernel(int cap, const int* dn, long long row, int32_t* buf) {
+  const long long total = (long long)min(*dn, cap) * row;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
+    buf[i] = 0;
+}
+
+// Fresh parameter rows for the rebuilt cells: rows_out[j] = base + j, slot[cells[j]] = base + j for
+// j < count, base = *d_rows (device row counter, advanced by count); rows beyond `cap` flag.
+__global__ void __launch_bounds__(1024) assign_rows_kernel(int ncap, const int* dn, const int64_t* cells, int64_t* slot,
+                                                           long long* d_rows, long long row_cap, int32_t* rows_out,
+                                                           int* flags) {
+  const int n = min(*dn, ncap);
+  const long long base = *d_rows;
+  __syncthreads();
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    const long long r = base + j;
+    if (r >= row_cap) {
+      atomicOr(flags, (int)kFlagRows);
+      rows_out[j] = -1;  // the build skips it; the host rebuilds the cell
+      continue;
+    }
+    rows_out[j] = (int32_t)r;
+    slot[cells[j]] = r;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *d_rows = base + n < row_cap ? base + n : row_cap;
+}
+
+// dst[j] = src[idx[j]] for j < min(*dn, cap)
+__global__ void __launch_bounds__(256) gather_dev_kernel(int cap, const int* dn, const int64_t* idx, const int64_t* src,
+                                                         int64_t* dst) {
+  const int n = min(*dn, cap);
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) dst[j] = src[idx[j]];
+}
+
+void trans_check(int cap, uintptr_t dn, uintptr_t counts, uintptr_t ndom, uintptr_t long_count, uintptr_t per, int Pcap,
+                 int Dcap, uintptr_t flags, uintptr_t stream) {
+  const unsigned g = std::min(cdiv(cap, 256), 64u);
+  trans_check_kernel<<<g, 256, 0, S_(stream)>>>(cap, P_<int>(dn), P_<int32_t>(counts), P_<int32_t>(ndom),
+                                                P_<int32_t>(long_count), P_<int32_t>(per), Pcap, Dcap, P_<int>(flags));
+  MS_LAUNCH_CHECK();
+}
+
+void zero_rows(int cap, uintptr_t dn, long long row, uintptr_t buf, uintptr_t stream) {
+  const unsigned g = (unsigned)std::min<long long>(cdiv((long long)cap * row, 256), 1024);
+  zero_rows_kernel<<<g, 256, 0, S_(stream)>>>(cap, P_<int>(dn), row, P_<int32_t>(buf));
+  MS_LAUNCH_CHECK();
+}
+
+void assign_rows(int ncap, uintptr_t dn, uintptr_t cells, uintptr_t slot, uintptr_t d_rows, long long row_cap,
+                 uintptr_t rows_out, uintptr_t flags, uintptr_t stream) {
+  assign_rows_kernel<<<1, 1024, 0, S_(stream)>>>(ncap, P_<int>(dn), P_<int64_t>(cells), P_<int64_t>(slot),
+                                                  P_<long long>(d_rows), row_cap, P_<int32_t>(rows_out), P_<int>(flags));
+  MS_LAUNCH_CHECK();
+}
+
+void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t dst, uintptr_t stream) {
+  const unsigned g = std::min(cdiv(cap, 256), 64u);
+  gather_dev_kernel<<<g, 256, 0, S_(stream)>>>(cap, P_<int>(dn), P_<int64_t>(idx), P_<int64_t>(src), P_<int64_t>(dst));
+  MS_LAUNCH_CHECK();
+}
+
 // Returns {count, max(vals over selected)}; synchronises `stream`. sel must hold n entries (rest too,
 // when given). Writes nothing and returns {0, 0} for n == 0.
 std::pair<long long, int> select_indices(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel,
@@ -233,6 +324,44 @@ std::pair<long long, int> select_indices(long long n, int kind, uintptr_t src, u
   const long long cnt = g_host[0];
   if (cnt < 0 || cnt > n) throw std::runtime_error("select_indices: bad count read-back");
   return {cnt, g_host[1]};
+}
+
+void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel, uintptr_t rest,
+                        uintptr_t out_dev, uintptr_t stream) {
+  hipStream_t s = S_(stream);
+  if (n <= 0) {
+    MS_HIP_CHECK(hipMemsetAsync(P_<int32_t>(out_dev), 0, 2 * sizeof(int32_t), s));
+    return;
+  }
+  if (n >= (1ll << 40)) throw std::invalid_argument("select_indices_dev: n too large");
+  const long long tiles = (n + kSelTile - 1) / kSelTile;
+  if (tiles > g_tiles_cap) {
+    if (g_tiles) {
+      MS_HIP_CHECK(hipStreamSynchronize(s));  // the old tile buffer may still be read
+      MS_HIP_CHECK(hipFree(g_tiles));
+    }
+    g_tiles_cap = std::max(tiles, 256ll);
+    MS_HIP_CHECK(hipMalloc((void**)&g_tiles, 2 * g_tiles_cap * sizeof(int32_t)));
+  }
+  const void* sp = reinterpret_cast<const void*>(src);
+  const int32_t* vp = vals ? P_<int32_t>(vals) : nullptr;
+  int32_t* tc = g_tiles;
+  int32_t* tm = g_tiles + g_tiles_cap;
+  int32_t* out = P_<int32_t>(out_dev);
+#define MS_SEL(K)                                                                                                \
+  select_count_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, vp, tc, tm);                           \
+  MS_LAUNCH_CHECK();                                                                                             \
+  select_write_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, tc, tm, P_<int64_t>(sel),              \
+                                                                 rest ? P_<int64_t>(rest) : nullptr, out);       \
+  MS_LAUNCH_CHECK();
+  switch (kind) {
+    case kMaskSet: MS_SEL(kMaskSet) break;
+    case kMaskClear: MS_SEL(kMaskClear) break;
+    case kI32Pos: MS_SEL(kI32Pos) break;
+    case kI64NonNeg: MS_SEL(kI64NonNeg) break;
+    default: throw std::invalid_argument("select_indices_dev: unknown predicate");
+  }
+#undef MS_SEL
 }
 
 }  // namespace msd

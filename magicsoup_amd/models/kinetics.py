@@ -377,6 +377,7 @@ class Kinetics:
     def copy_cell_params(self, from_idxs, to_idxs):
         """Copy the parameters of cells ``from_idxs`` to cells ``to_idxs`` (sources are read before
         any destination is written, as with ``t[to] = t[fr]``)."""
+        self._sync()
         self._copy_rows(from_idxs, to_idxs, disjoint=False)
 
     def _copy_rows(self, from_idxs, to_idxs, disjoint: bool) -> None:
@@ -426,6 +427,7 @@ class Kinetics:
         return int(self._store["N"].size(1))
 
     def _get_param(self, name: str) -> torch.Tensor:
+        self._sync()
         self._materialize()
         t = self._store[name]
         n = self.__dict__["_ncells"]
@@ -435,6 +437,7 @@ class Kinetics:
         d = self.__dict__
         if "_store_d" not in d:
             d["_store_d"], d["_slot"], d["_ncells"], d["_nrows"] = {}, None, 0, 0
+        self._sync()
         self._materialize()
         self._drop_packed()
         d.pop("_zero_row_t", None)
@@ -463,6 +466,13 @@ class Kinetics:
             d["_slot"] = torch.arange(n, device=self._store["N"].device)
             d["_nrows"] = n
 
+    def _sync(self) -> None:
+        """Resolve pending device-pipeline updates of the owning world (no-op otherwise)."""
+        ref = self.__dict__.get("_owner")
+        w = ref() if ref is not None else None
+        if w is not None and w.__dict__.get("_gp_state"):
+            w._reconcile()
+
     def _zero_row(self) -> torch.Tensor:
         """Index (int64 (1,), device) of a storage row holding all-zero parameters, shared by cells
         without a proteome. Created once per storage layout; never written afterwards (builds
@@ -481,6 +491,17 @@ class Kinetics:
         return z
 
     def _alloc_rows(self, k: int) -> torch.Tensor:
+        self._sync()
+        return self._alloc_rows_now(k)
+
+    def _reserve_rows(self, k: int) -> None:
+        """Make room for k fresh rows without taking them (the device genome pipeline takes them
+        with its own device-side row counter, magicsoup_amd.ops.genome_pipeline)."""
+        self._sync()
+        self._alloc_rows_now(k)
+        self.__dict__["_nrows"] -= k
+
+    def _alloc_rows_now(self, k: int) -> torch.Tensor:
         """k unused storage rows (int64, device) for cells whose parameters are about to be written.
         Rows of removed cells are not tracked (a row may be shared); when the storage is exhausted
         the live rows are gathered back to cell order (one pass) or the capacity grows."""
@@ -592,6 +613,7 @@ class Kinetics:
     def remove_cell_params(self, keep: torch.Tensor, removed: torch.Tensor | None = None):
         """Keep only the cells where ``keep`` is true (bool mask (c,)) or listed (ascending index
         tensor), preserving their order. ``removed`` (optional) lists the other cells."""
+        self._sync()
         idx = torch.nonzero(keep).flatten() if keep.dtype == torch.bool else keep.to(torch.long)
         d = self.__dict__
         k = int(idx.numel())
@@ -652,6 +674,7 @@ class Kinetics:
         """Grow the protein dimension of every parameter tensor to ``max_n`` (zero-filled)."""
         if max_n <= self._P():
             return
+        self._sync()
         store = self._store
         dev = store["N"].device
         if dev.type == "cuda":
@@ -683,6 +706,7 @@ class Kinetics:
         self._restamp(ok)
 
     def _to_device(self, dev: torch.device) -> None:
+        self._sync()
         self._materialize()
         self._drop_packed()
         n = self.__dict__["_ncells"]
@@ -702,6 +726,7 @@ class Kinetics:
         Returns:
             Updated signals (c, s) as a new tensor.
         """
+        self._sync()
         if self._stages_overridden():
             for trim in _TRIMS:
                 X = self._integrate_signals_part(adj_vmax=(self.Vmax * trim).clamp(0.0), X0=X)
@@ -805,10 +830,11 @@ class Kinetics:
         return torch.from_numpy(arr)
 
     def __getstate__(self):
+        self._sync()
         self._materialize()
         state = self.__dict__.copy()
         state["last_masks"] = []
-        for k in ("_spare", "_hip_scratch"):
+        for k in ("_spare", "_hip_scratch", "_owner"):
             state.pop(k, None)
         n = state["_ncells"]
         state["_store_d"] = {k: v[:n].clone() for k, v in self._store.items() if k not in _PACKED}

@@ -42,6 +42,11 @@ from magicsoup_amd.utils import profiling
 from magicsoup_amd.utils.profiling import range_pop, range_push
 
 _LABEL_LEN = 12
+# ops that neither read genomes / parameters nor change cells or positions: pending device-pipeline
+# genome updates (magicsoup_amd.ops.genome_pipeline) stay pending across them; every other op
+# resolves them first
+_PIPELINE_SAFE_OPS = frozenset({"mutate_cells", "recombinate_cells", "diffuse_molecules", "degrade_molecules",
+                                "increment_cell_lifetimes"})
 _CHECK_ENV = os.environ.get("MS_CHECK_INVARIANTS") == "1"
 
 
@@ -55,6 +60,8 @@ def _op(name: str):
         @functools.wraps(fn)
         def wrapper(self, *args, **kwargs):
             d = self.__dict__
+            if d.get("_gp_state") and name not in _PIPELINE_SAFE_OPS:
+                self._reconcile()
             timer, check = d.get("_timer"), d.get("_debug_checks", _CHECK_ENV)
             if timer is None and not check and not profiling.roctx_enabled():
                 return fn(self, *args, **kwargs)
@@ -204,6 +211,8 @@ class World:
             vector_enc_size=max(self.genetics.two_codon_map.values()),
         )
 
+        self._link_kinetics()
+
         self.n_molecules = len(chemistry.molecules)
         self._int_mol_idxs = list(range(self.n_molecules))
         self._ext_mol_idxs = list(range(self.n_molecules, 2 * self.n_molecules))
@@ -228,6 +237,19 @@ class World:
         self.__dict__["_pending_corr"] = None
         self.cell_map = torch.zeros(*self._map_shape(), dtype=torch.bool, device=dev)
         self.molecule_map = self._get_molecule_map(n=m, size=map_size, init=mol_map_init)
+
+    def _link_kinetics(self) -> None:
+        """Let the kinetics object resolve pending device-pipeline genome updates before any host
+        access to its parameters (magicsoup_amd.ops.genome_pipeline)."""
+        import weakref
+
+        self.kinetics.__dict__["_owner"] = weakref.ref(self)
+
+    def _reconcile(self) -> None:
+        if self.__dict__.get("_gp_state"):
+            from magicsoup_amd.ops import genome_pipeline
+
+            genome_pipeline.reconcile(self)
 
     def _map_shape(self) -> tuple[int, int]:
         """(rows, cols) of this process's map (a strip with halo rows in magicsoup_amd.parallel)."""
@@ -270,6 +292,7 @@ class World:
             self._set_cell_map(value)
             return
         if name == "cell_genomes":
+            self._reconcile()
             self._set_strings(self._genomes, list(value))
             return
         if name == "cell_labels":
@@ -295,6 +318,7 @@ class World:
     @property
     def cell_genomes(self) -> StringColumn:
         """Genomes ordered by cell index (a lazy ``list[str]`` view of the device arena)."""
+        self._reconcile()
         return self._genome_col
 
     @property
@@ -375,6 +399,7 @@ class World:
 
         Raises ``ValueError`` if no cell lives at ``by_position``.
         """
+        self._reconcile()
         idx = -1
         if by_idx is not None:
             idx = by_idx
@@ -658,6 +683,12 @@ class World:
         cells are re-derived."""
         if self.n_cells == 0:
             return
+        if cell_idxs is None and self._genomes.data.is_cuda:
+            from magicsoup_amd.ops import genome_pipeline
+
+            if genome_pipeline.point_mutations(self, p, p_indel, p_del):
+                return
+        self._reconcile()
         rows = None if cell_idxs is None else self._idx_tensor(cell_idxs, unique=False)
         changed = world_ops.point_mutations(self, rows, p, p_indel, p_del)
         if changed.numel() > 0:
@@ -669,6 +700,12 @@ class World:
         random re-joining); both genomes of every recombined pair are replaced."""
         if self.n_cells < 2:
             return
+        if cell_idxs is None and self._genomes.data.is_cuda:
+            from magicsoup_amd.ops import genome_pipeline
+
+            if genome_pipeline.recombinate_all(self, p):
+                return
+        self._reconcile()
         if cell_idxs is None and self._genomes.data.is_cuda:
             from magicsoup_amd.ops import hip_ops
 
@@ -718,6 +755,7 @@ class World:
         return load_world_pickle(Path(rundir) / name, device=device)
 
     def __getstate__(self):
+        self._reconcile()
         state = self.__dict__.copy()
         n = self.n_cells
         for k in ("_genome_col", "_label_col"):
@@ -729,7 +767,7 @@ class World:
         state["_cell_map"] = self.cell_map.cpu()
         state["_pending_scale"] = None
         state["_pending_corr"] = None
-        for k in ("_hip_scratch", "_idx_map", "_diff_w", "_perm_t", "_degrade_t"):
+        for k in ("_hip_scratch", "_idx_map", "_diff_w", "_perm_t", "_degrade_t", "_gp_state"):
             state.pop(k, None)
         return state
 
@@ -755,6 +793,7 @@ class World:
         self.__dict__["map_dtype"] = mdt
         self.__dict__["_molmap"] = self.__dict__["_molmap"].to(dev, mdt).contiguous()
         self._set_cell_map(cmap.to(dev))
+        self._link_kinetics()
 
     def to(self, device: str) -> "World":
         """Move all state of this world to ``device`` (returns ``self``)."""
@@ -778,12 +817,14 @@ class World:
     @_op("save_state")
     def save_state(self, statedir: Path):
         """Write the current state (tensors + ``cells.fasta``) in the reference's format."""
+        self._reconcile()
         from magicsoup_amd.utils.checkpoint import save_state
 
         save_state(self, Path(statedir))
 
     @_op("load_state")
     def load_state(self, statedir: Path, ignore_cell_params: bool = False):
+        self._reconcile()
         """Load a state written by :meth:`save_state` (re-translating genomes unless
         ``ignore_cell_params``)."""
         from magicsoup_amd.utils.checkpoint import load_state

@@ -1,0 +1,300 @@
+"""Sync-free genome updates on the GPU: ``mutate_cells()`` / ``recombinate_cells()`` (all cells).
+
+The reference API returns nothing from these two operations (``world.py:689-745``), so nothing
+forces the host to learn how many genomes changed. Here the whole chain stays on the device:
+
+    draw event counts -> select the changed genomes (count kept on the device) -> apply
+    -> commit to the genome arena -> translate -> fresh parameter rows -> parameter build
+
+Every kernel after the selection strides over the device-side count (``dn`` arguments in
+``csrc/hip``), so the host issues the chain without a synchronisation and runs ahead into the next
+operations while the GPU works. What the host cannot rule out in advance raises flag bits instead:
+
+* a result longer than the genome arena's row width is not committed (``arena_scatter``); every
+  later pipeline op of the same pending chain then does nothing (its count kernel sees the flag)
+  and is *replayed* at reconcile time with its original RNG stream, after the arena was widened and
+  the result committed -- exactly the sequential outcome;
+* a proteome with more proteins than the parameter storage holds, more domains than the token
+  slots, or a genome too long for the LDS translation pass (``trans_check``), and parameter rows
+  running out (``assign_rows``): the affected cells are rebuilt on the synchronous path.
+
+:func:`reconcile` resolves all of this; the World calls it before every op that reads genomes or
+parameters, changes cells or positions, or allocates rows (and the Kinetics object before any host
+access to its parameters), so results never depend on which path ran. Event counts are capped at
+``K_CAP`` per genome; the pipeline is only used when the expected count is far below that.
+
+Disable with ``MS_SYNC_GENETICS=1`` (always the synchronous path).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from magicsoup_amd.ops import hip_ops
+from magicsoup_amd.ops.hip_ops import _m, _p, _rng, _scratch, _stream
+
+K_CAP = 32  # event-count cap per genome (P(Poisson(lam <= 1) > 32) < 1e-35)
+D_CAP = 12  # domain slots per protein in the speculative token layout
+N_CAP = 8192  # genomes per pipeline call (the expected count is kept <= N_CAP / 4)
+# flag bits (select.hip DevFlag, mutations.hip kGp*)
+_F_TRANSLATE, _F_CAPACITY, _F_ROWS, _F_WIDTH, _F_SKIPPED = 1, 2, 4, 8, 16
+_SEL_I32POS, _SEL_SET = 2, 0
+
+
+def enabled(world) -> bool:
+    if os.environ.get("MS_SYNC_GENETICS") == "1":
+        return False
+    if not world.__dict__["_molmap"].is_cuda or getattr(world, "_geom", None) is not None:
+        return False  # GPU, single-domain worlds only
+    return True
+
+
+class _Pending:
+    """One issued pipeline call: what reconcile needs to resolve it."""
+
+    __slots__ = ("kind", "args", "rng", "cells", "host", "event", "replay")
+
+    def __init__(self, kind, args, rng, cells, host, event, replay):
+        self.kind, self.args, self.rng, self.cells = kind, args, rng, cells
+        self.host, self.event, self.replay = host, event, replay
+
+
+def _state(world) -> dict:
+    st = world.__dict__.get("_gp_state")
+    if st is None:
+        st = world.__dict__["_gp_state"] = {"pending": []}
+    return st
+
+
+def _bufs(world, kind: str) -> dict:
+    sc = _scratch(world)
+    dev = world._genomes.data.device
+    return {
+        "cnt": sc.get(f"gp_cnt_{kind}", 2, torch.int32, dev),
+        "cnt2": sc.get(f"gp_cnt2_{kind}", 2, torch.int32, dev),
+        "opflags": sc.get(f"gp_opflags_{kind}", 1, torch.int32, dev),
+        "gflags": sc.get("gp_gflags", 1, torch.int32, dev),
+        "d_rows": sc.get("gp_rows", 1, torch.int64, dev),
+    }
+
+
+def _usable(world, expected: float) -> bool:
+    return enabled(world) and expected <= N_CAP / 4
+
+
+def _begin(world, kind: str) -> dict:
+    """Per-call device state. A pending call of the same kind is resolved first (its scratch is
+    reused); with nothing pending the shared flags and the device row counter are (re)set from
+    the host, after making room for two calls' worth of fresh rows."""
+    st = _state(world)
+    if any(pd.kind == kind for pd in st["pending"]):
+        reconcile(world)
+    kin = world.kinetics
+    b = _bufs(world, kind)
+    if not st["pending"]:
+        kin._reserve_rows(2 * min(world.n_cells, N_CAP))
+        b["gflags"].zero_()
+        b["d_rows"].fill_(int(kin.__dict__["_nrows"]))
+    b["opflags"].zero_()
+    return b
+
+
+def _rebuild(world, b: dict, cells: torch.Tensor, dcnt: torch.Tensor, cap: int) -> None:
+    """Translate the genomes of ``cells[:*dcnt]`` and build their parameters into fresh rows."""
+    from magicsoup_amd.constants import GAS_CONSTANT
+    from magicsoup_amd.ops.kinetics_ops import _luts
+
+    kin = world.kinetics
+    genetics = world.genetics
+    arena = world._genomes
+    dev = arena.data.device
+    sc = _scratch(world)
+    luts = genetics.device_luts(dev)
+    tables = genetics.tables
+    P = kin._P()
+    counts = sc.get("gp_counts", 2 * cap, torch.int32, dev)
+    ndom = sc.get("gp_ndom", 2 * cap, torch.int32, dev)
+    long_list = sc.get("gp_long", cap, torch.int32, dev)
+    long_count = sc.get("gp_long_n", 1, torch.int32, dev)
+    per = sc.get("gp_per", cap, torch.int32, dev)
+    rows_out = sc.get("gp_rows_out", cap, torch.int32, dev)
+    tokens = sc.get("gp_tokens", cap * P * D_CAP * 5, torch.int32, dev)
+    long_count.zero_()
+    data, lens = arena.data, arena.lens
+    width = int(data.size(1))
+    common = (_p(luts["small"]), _p(luts["dom_type"]), int(luts["dom_type"].numel()), _p(luts["two_codon"]),
+              tables.dom_size, tables.dom_type_size)
+    st = _stream()
+    of = _p(b["opflags"])
+    _m().translate_count(cap, _p(cells), _p(data), width, _p(lens), *common, _p(counts), _p(ndom), 0, 0,
+                         _p(long_list), _p(long_count), _p(dcnt), st)
+    _m().trans_check(cap, _p(dcnt), _p(counts), _p(ndom), _p(long_count), _p(per), P, D_CAP, of, st)
+    _m().zero_rows(cap, _p(dcnt), P * D_CAP * 5, _p(tokens), st)
+    _m().translate_write(cap, _p(cells), _p(data), width, _p(lens), *common, _p(counts), P, D_CAP, _p(tokens), 0, 0,
+                         _p(dcnt), st)
+    store = kin._kernel_params()
+    kin._enter_slot_mode()
+    slot = kin.__dict__["_slot"]
+    row_cap = min(int(t.size(0)) for t in store.values())
+    _m().assign_rows(cap, _p(dcnt), _p(cells), _p(slot), _p(b["d_rows"]), row_cap, _p(rows_out), of, st)
+    kl = _luts(kin, dev)
+    n_vec = min(kl["react"].size(0), kl["trnsp"].size(0), kl["eff"].size(0))
+    for k in ("react", "trnsp", "eff"):
+        kl[k] = kl[k][:n_vec].contiguous()
+    hip_ops.build_params(kin, tokens.view(cap, P, D_CAP, 5), rows_out, kl, store, float(kin.abs_temp), GAS_CONSTANT,
+                         nprot=per, dn=dcnt)
+
+
+def _finish(world, kind: str, args: tuple, rng: tuple, b: dict, cells, dcnt, replay: dict) -> None:
+    """Queue the host read-back of {rebuilt count, op flags, row counter, selected count} and
+    record the call as pending."""
+    host = torch.empty(4, dtype=torch.int64, pin_memory=True)
+    packed = torch.cat([dcnt[:1].to(torch.int64), b["opflags"].to(torch.int64), b["d_rows"],
+                        b["cnt"][:1].to(torch.int64)])
+    host.copy_(packed, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    _state(world)["pending"].append(_Pending(kind, args, rng, cells, host, ev, replay))
+    world._genomes.version += 1
+
+
+def point_mutations(world, p: float, p_indel: float, p_del: float) -> bool:
+    """Device-pipeline ``mutate_cells()`` over all cells; False if this call should take the
+    synchronous path instead."""
+    arena = world._genomes
+    n = arena.n
+    if n == 0:
+        return True
+    L = int(arena.width)  # every genome fits its row
+    if p * L > 1.0 or not _usable(world, n * p * L):
+        return False
+    dev = arena.data.device
+    cap = min(n, N_CAP)
+    b = _begin(world, "mut")
+    sc = _scratch(world)
+    k = sc.get("gp_k", n, torch.int32, dev)
+    sel = sc.get("gp_sel", n, torch.int64, dev)
+    seed, call = _rng()
+    st = _stream()
+    _m().mut_count(n, 0, _p(arena.lens), float(p), seed, call, _p(k), K_CAP, _p(b["gflags"]), _p(b["opflags"]), st)
+    _m().select_indices_dev(n, _SEL_I32POS, _p(k), 0, _p(sel), 0, _p(b["cnt"]), st)
+    dcnt = b["cnt"]
+    out_w = (L + K_CAP + 15) // 16 * 16
+    out = sc.get("gp_out", cap * out_w, torch.uint8, dev)
+    out_len = sc.get("gp_out_len", cap, torch.int32, dev)
+    _m().mut_apply(cap, _p(dcnt), _p(sel), 0, _p(arena.data), L, _p(arena.lens), _p(k), float(p_indel), float(p_del),
+                   seed, call, _p(out), out_w, _p(out_len), st)
+    _m().arena_scatter(cap, _p(dcnt), 1, _p(sel), _p(out), out_w, _p(out_len), _p(arena.data), L, _p(arena.lens),
+                       0, 0, 0, _p(b["gflags"]), _p(b["opflags"]), st)
+    _rebuild(world, b, sel, dcnt, cap)
+    _finish(world, "mut", (p, p_indel, p_del), (seed, call), b, sel, dcnt,
+            {"rows": sel, "out": out, "out_w": out_w, "out_len": out_len})
+    return True
+
+
+def recombinate_all(world, p: float) -> bool:
+    """Device-pipeline ``recombinate_cells()`` over all cells; False for the synchronous path."""
+    arena = world._genomes
+    n = world.n_cells
+    if n < 2:
+        return True
+    L = int(arena.width)
+    expected = 8 * n * p * 2 * L  # upper bound: every neighbour slot a pair
+    if p * 2 * L > 1.0 or not _usable(world, expected):
+        return False
+    dev = arena.data.device
+    pcap = min(n, N_CAP) // 2  # pairs per call (two results each)
+    b = _begin(world, "rec")
+    sc = _scratch(world)
+    keys = hip_ops.neighbor_slot_keys(world)
+    k = sc.get("nb_k", 8 * n, torch.int32, dev)
+    sel = sc.get("gp_rsel", 8 * n, torch.int64, dev)
+    seed, call = _rng()
+    st = _stream()
+    gf, of = _p(b["gflags"]), _p(b["opflags"])
+    _m().rec_count_keys(8 * n, _p(keys), _p(arena.lens), float(p), seed, call, _p(k), 0, K_CAP, gf, of, st)
+    _m().select_indices_dev(8 * n, _SEL_I32POS, _p(k), 0, _p(sel), 0, _p(b["cnt"]), st)
+    # a selected-pair count above the capacity is flagged (never expected under the usage rule)
+    b["opflags"].bitwise_or_((b["cnt"][:1] > pcap).to(torch.int32) * _F_CAPACITY)
+    out_w = 2 * L  # a recombined genome is at most both parents
+    out = sc.get("gp_rout", 2 * pcap * out_w, torch.uint8, dev)
+    out_len = sc.get("gp_rout_len", 2 * pcap, torch.int32, dev)
+    out_rows = sc.get("gp_rout_rows", 2 * pcap, torch.int64, dev)
+    parts_cap = K_CAP + 2
+    parts = sc.get("gp_parts", pcap * parts_cap * 3, torch.int32, dev)
+    _m().rec_apply(pcap, _p(b["cnt"]), _p(sel), 0, _p(keys), _p(arena.data), L, _p(arena.lens), _p(k), seed, call,
+                   _p(parts), parts_cap, _p(out), out_w, _p(out_len), _p(out_rows), st)
+    # (a0, b0, a1, b1, ...) in pair order: the last result per cell wins (reference update order)
+    mark = sc.bufs.get("arena_mark")
+    if mark is None or mark.numel() < arena.n:
+        mark = sc.bufs["arena_mark"] = torch.zeros(max(arena.n, 1024) * 2, dtype=torch.int64, device=dev)
+        sc.bufs["arena_gen"] = 0
+    gen = sc.bufs["arena_gen"] = sc.bufs.get("arena_gen", 0) + 1
+    won = sc.get("gp_won", 2 * pcap, torch.uint8, dev)
+    won.zero_()
+    _m().arena_scatter(2 * pcap, _p(b["cnt"]), 2, _p(out_rows), _p(out), out_w, _p(out_len), _p(arena.data), L,
+                       _p(arena.lens), _p(mark), int(gen), _p(won), gf, of, st)
+    q = sc.get("gp_q", 2 * pcap, torch.int64, dev)
+    _m().select_indices_dev(2 * pcap, _SEL_SET, _p(won), 0, _p(q), 0, _p(b["cnt2"]), st)
+    cells = sc.get("gp_rcells", 2 * pcap, torch.int64, dev)
+    _m().gather_dev(2 * pcap, _p(b["cnt2"]), _p(q), _p(out_rows), _p(cells), st)
+    _rebuild(world, b, cells, b["cnt2"], 2 * pcap)
+    _finish(world, "rec", (p,), (seed, call), b, cells, b["cnt2"],
+            {"rows": out_rows, "out": out, "out_w": out_w, "out_len": out_len, "mark": mark, "gen": gen})
+    return True
+
+
+def _recommit(world, pd: _Pending) -> torch.Tensor:
+    """Commit a call's results after widening the arena to the longest one; returns the cells."""
+    arena = world._genomes
+    r = pd.replay
+    n_res = int(pd.host[0]) if pd.kind == "mut" else 2 * int(pd.host[3])
+    if n_res == 0:
+        return torch.zeros(0, dtype=torch.long, device=arena.data.device)
+    out_len = r["out_len"][:n_res]
+    need = int(out_len.max().item())
+    if need > arena.width:
+        arena.reserve(arena.n, need)
+    rows = r["rows"][:n_res]
+    _m().arena_scatter(n_res, 0, 1, _p(rows), _p(r["out"]), r["out_w"], _p(out_len), _p(arena.data),
+                       int(arena.width), _p(arena.lens), _p(r.get("mark")), int(r.get("gen", 0)), 0, 0, 0, _stream())
+    arena.version += 1
+    return torch.unique(rows)
+
+
+def reconcile(world) -> None:
+    """Resolve pending device-pipeline calls, in issue order: adopt the device row counter,
+    commit results that did not fit the arena (then replay the calls that were skipped because of
+    it), and rebuild flagged cells on the synchronous path."""
+    st = world.__dict__.get("_gp_state")
+    if not st or not st["pending"]:
+        return
+    pend = st["pending"]
+    st["pending"] = []
+    kin = world.kinetics
+    pend[-1].event.synchronize()
+    kin.__dict__["_nrows"] = max(int(kin.__dict__["_nrows"]), int(pend[-1].host[2]))
+    for pd in pend:
+        flags = int(pd.host[1])
+        if flags & _F_CAPACITY:
+            raise RuntimeError("genome pipeline capacity exceeded (rates far above the pipeline's usage rule)")
+        if flags & _F_SKIPPED:
+            # a predecessor's result did not fit the arena: run this call now, same RNG stream
+            if pd.kind == "mut":
+                changed = hip_ops.point_mutations(world, None, *pd.args, rng=pd.rng)
+            else:
+                changed = hip_ops.recombinate_all(world, *pd.args, rng=pd.rng)
+            if changed.numel():
+                world._update_params_rows(changed)
+            continue
+        if flags & _F_WIDTH:
+            cells = _recommit(world, pd)
+            if cells.numel():
+                world._update_params_rows(cells)
+            continue
+        if flags & (_F_TRANSLATE | _F_ROWS):
+            # parameters are a pure function of the current genome: rebuild on the synchronous path
+            cells = pd.cells[: int(pd.host[0])]
+            if cells.numel():
+                world._update_params_rows(torch.unique(cells))

@@ -198,7 +198,7 @@ def enzymatic_activity(world) -> None:
     _launch_integrate(kin, p, c, world=world, flags_hook=hook, slot=kin._slot_tensor())
 
 
-def build_params(kin, tokens, rows, luts, p, abs_temp: float, gas: float, nprot=None) -> None:
+def build_params(kin, tokens, rows, luts, p, abs_temp: float, gas: float, nprot=None, dn=None) -> None:
     """Fused parameter build; also writes the integrator layout when it is current."""
     packed = kin._pack_ok()
     n, P, D = int(tokens.size(0)), int(tokens.size(1)), int(tokens.size(2))
@@ -213,6 +213,7 @@ def build_params(kin, tokens, rows, luts, p, abs_temp: float, gas: float, nprot=
         _p(nprot),
         _p(p["_W"] if packed else None), _p(p["_Q"] if packed else None),
         _p(_overflow_flag(kin) if packed else None),
+        _p(dn),
         _stream(),
     )
 
@@ -553,7 +554,7 @@ def translate(genetics, data: torch.Tensor, lens: torch.Tensor, rows: torch.Tens
     common = (_p(luts["small"]), _p(luts["dom_type"]), int(luts["dom_type"].numel()), _p(luts["two_codon"]),
               tables.dom_size, tables.dom_type_size)
     _m().translate_count(n, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), _p(ndom), 0, 0,
-                         _p(long_list), _p(long_count), _stream())
+                         _p(long_list), _p(long_count), 0, _stream())
     per = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
     stats = _m().translate_stats(n, _p(counts), _p(ndom), _p(long_count), _p(per), _stream())
     n_long = int(stats[2])
@@ -561,15 +562,15 @@ def translate(genetics, data: torch.Tensor, lens: torch.Tensor, rows: torch.Tens
     if n_long:
         gslot = torch.empty(n_long * int(_m().translate_slot_bytes(width)), dtype=torch.uint8, device=dev)
         _m().translate_count(n_long, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), _p(ndom),
-                             _p(long_list), _p(gslot), _p(long_list), _p(long_count), _stream())
+                             _p(long_list), _p(gslot), _p(long_list), _p(long_count), 0, _stream())
         stats = _m().translate_stats(n, _p(counts), _p(ndom), _p(long_count), _p(per), _stream())
     P, D = max(int(stats[0]), 1), max(int(stats[1]), 1)
     tokens = torch.zeros(n, P, D, 5, dtype=torch.int32, device=dev)
     _m().translate_write(n, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), P, D, _p(tokens), 0, 0,
-                         _stream())
+                         0, _stream())
     if n_long:
         _m().translate_write(n_long, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), P, D, _p(tokens),
-                             _p(long_list), _p(gslot), _stream())
+                             _p(long_list), _p(gslot), 0, _stream())
     return tokens, per
 
 
@@ -590,8 +591,8 @@ def _arena_commit(arena, rows: torch.Tensor, out: torch.Tensor, out_len: torch.T
             sc.bufs["arena_gen"] = 0
         gen = sc.bufs["arena_gen"] = sc.bufs.get("arena_gen", 0) + 1
         flags = torch.empty(k, dtype=torch.uint8, device=rows.device)
-    _m().arena_scatter(k, _p(rows), _p(out), int(out.stride(0)), _p(out_len), _p(arena.data), int(arena.width),
-                       _p(arena.lens), _p(mark), int(gen), _p(flags), _stream())
+    _m().arena_scatter(k, 0, 1, _p(rows), _p(out), int(out.stride(0)), _p(out_len), _p(arena.data), int(arena.width),
+                       _p(arena.lens), _p(mark), int(gen), _p(flags), 0, 0, _stream())
     arena.version += 1
     if not dedupe:
         return rows
@@ -599,7 +600,8 @@ def _arena_commit(arena, rows: torch.Tensor, out: torch.Tensor, out_len: torch.T
     return rows[won]
 
 
-def point_mutations(world, rows, p: float, p_indel: float, p_del: float) -> torch.Tensor:
+def point_mutations(world, rows, p: float, p_indel: float, p_del: float, rng=None) -> torch.Tensor:
+    """Mutate arena rows (all when ``rows`` is None); ``rng`` replays a given (seed, call)."""
     arena = world._genomes
     dev = arena.data.device
     n = arena.n if rows is None else int(rows.numel())
@@ -607,8 +609,8 @@ def point_mutations(world, rows, p: float, p_indel: float, p_del: float) -> torc
         return torch.zeros(0, dtype=torch.long, device=dev)
     rows64 = None if rows is None else rows.to(torch.int64).contiguous()
     k = torch.empty(n, dtype=torch.int32, device=dev)
-    seed, call = _rng()
-    _m().mut_count(n, _p(rows64), _p(arena.lens), float(p), seed, call, _p(k), _stream())
+    seed, call = rng if rng is not None else _rng()
+    _m().mut_count(n, _p(rows64), _p(arena.lens), float(p), seed, call, _p(k), 0, 0, 0, _stream())
     # bound of a mutated genome's length: its length + k (every mutation an insertion)
     lens_k = (arena.lens[:n] if rows64 is None else arena.lens[rows64]) + k
     sel, _, bound = select(k, "i32pos", vals=lens_k)
@@ -619,7 +621,7 @@ def point_mutations(world, rows, p: float, p_indel: float, p_del: float) -> torc
     out_w = max(bound, 1)
     out = torch.empty(nsel, out_w, dtype=torch.uint8, device=dev)
     out_len = torch.empty(nsel, dtype=torch.int32, device=dev)
-    _m().mut_apply(nsel, _p(sel), _p(rows64), _p(arena.data), int(arena.data.size(1)), _p(arena.lens), _p(k),
+    _m().mut_apply(nsel, 0, _p(sel), _p(rows64), _p(arena.data), int(arena.data.size(1)), _p(arena.lens), _p(k),
                    float(p_indel), float(p_del), seed, call, _p(out), out_w, _p(out_len), _stream())
     if rows64 is not None and nsel > 1:
         # explicit rows may repeat (mutate_cells([i, i])): the last mutated copy wins
@@ -639,9 +641,10 @@ def recombinations(world, pairs: torch.Tensor, p: float) -> torch.Tensor:
     return _rec_apply(world, pairs, None, k, tot, seed, call)
 
 
-def recombinate_all(world, p: float) -> torch.Tensor:
+def recombinate_all(world, p: float, rng=None) -> torch.Tensor:
     """recombinate_cells() over all cells: neighbour pairs in fixed per-cell slots (no pair list
-    read-back), Poisson draws per slot, one sync for the selected pairs."""
+    read-back), Poisson draws per slot, one sync for the selected pairs. ``rng`` replays a given
+    (seed, call)."""
     arena = world._genomes
     dev = arena.data.device
     n = world.n_cells
@@ -649,8 +652,8 @@ def recombinate_all(world, p: float) -> torch.Tensor:
     sc = _scratch(world)
     k = sc.get("nb_k", 8 * n, torch.int32, dev)
     tot = sc.get("nb_tot", 8 * n, torch.int32, dev)
-    seed, call = _rng()
-    _m().rec_count_keys(8 * n, _p(keys), _p(arena.lens), float(p), seed, call, _p(k), _p(tot), _stream())
+    seed, call = rng if rng is not None else _rng()
+    _m().rec_count_keys(8 * n, _p(keys), _p(arena.lens), float(p), seed, call, _p(k), _p(tot), 0, 0, 0, _stream())
     return _rec_apply(world, None, keys, k, tot, seed, call)
 
 
@@ -685,7 +688,7 @@ def _rec_apply(world, pairs, keys, k: torch.Tensor, tot: torch.Tensor, seed: int
     out_len = torch.empty(2 * nsel, dtype=torch.int32, device=dev)
     out_rows = torch.empty(2 * nsel, dtype=torch.int64, device=dev)
     parts = torch.empty(nsel * parts_cap * 3, dtype=torch.int32, device=dev)
-    _m().rec_apply(nsel, _p(sel), _p(pairs), _p(keys), _p(arena.data), int(arena.data.size(1)), _p(arena.lens), _p(k),
+    _m().rec_apply(nsel, 0, _p(sel), _p(pairs), _p(keys), _p(arena.data), int(arena.data.size(1)), _p(arena.lens), _p(k),
                    seed, call, _p(parts), parts_cap, _p(out), out_w, _p(out_len), _p(out_rows), _stream())
     # (a0, b0, a1, b1, ...) in pair order: the last write per cell wins (reference update order)
     return _arena_commit(arena, out_rows, out, out_len, bound, dedupe=True, owner=world)

@@ -449,3 +449,47 @@ def test_deferred_diffusion_correction_matches_materialised():
     assert torch.allclose(a.molecule_map, b.molecule_map, rtol=1e-5, atol=1e-6)
     assert torch.allclose(a.cell_molecules, b.cell_molecules, rtol=1e-5, atol=1e-6)
     assert float(a.molecule_map.min()) >= 0.0
+
+
+def _genetics_run(monkeypatch, base, sync: bool, d_cap=None, steps=5):
+    import copy as _copy
+
+    from magicsoup_amd.ops import genome_pipeline
+
+    if sync:
+        monkeypatch.setenv("MS_SYNC_GENETICS", "1")
+    else:
+        monkeypatch.delenv("MS_SYNC_GENETICS", raising=False)
+    if d_cap is not None:
+        monkeypatch.setattr(genome_pipeline, "D_CAP", d_cap)
+    w = _copy.deepcopy(base)  # identical start (GPU spawn placement is claim-order dependent)
+    ms.set_seed(11)
+    torch.manual_seed(11)
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    for _ in range(steps):
+        w.enzymatic_activity()
+        w.kill_cells(w.cell_molecules[:, atp] < 0.3)
+        w.divide_cells_t(w.cell_molecules[:, atp] > 3.0)
+        w.recombinate_cells(p=1e-4)
+        w.mutate_cells(p=1e-3)
+        w.diffuse_molecules()
+    w.enzymatic_activity()
+    names = ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke")
+    return list(w.cell_genomes), {k: getattr(w.kinetics, k).clone() for k in names}, w.cell_molecules.clone()
+
+
+@pytest.mark.parametrize("d_cap", [None, 1])
+def test_device_genome_pipeline_matches_sync_path(monkeypatch, d_cap):
+    """Sync-free mutate / recombinate (device counts, speculative token layout, fresh rows) give
+    the same genomes, parameters and trajectory as the synchronous path; with one domain slot
+    per protein the overflow flags force the reconcile rebuild, with the same result."""
+    base = _world("cuda", map_size=64, n=800, s=400, seed=7)
+    g0, p0, x0 = _genetics_run(monkeypatch, base, sync=True)
+    g1, p1, x1 = _genetics_run(monkeypatch, base, sync=False, d_cap=d_cap)
+    assert g0 == g1
+    for k in p0:
+        P = min(p0[k].size(1), p1[k].size(1))
+        assert torch.equal(p0[k][:, :P], p1[k][:, :P]), k
+        if p1[k].size(1) > P:
+            assert not p1[k][:, P:].any(), k
+    assert torch.equal(x0, x1)
