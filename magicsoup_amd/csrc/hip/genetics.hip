@@ -3,15 +3,17 @@
 // The sequential reference scan (rust/genetics.rs:13-123; single-source host version in
 // ms_common.h) is reformulated so that all 64 lanes work at once and no lane walks the genome:
 //   1. lanes over positions: codon index of every position on both strands -> LDS;
-//   2. per strand and frame, a wave suffix-min scan gives the next in-frame stop of every position,
-//      and lanes over positions tabulate the domain type starting at each position;
+//   2. lanes over positions tabulate the domain type starting at each position; per strand and
+//      frame, wave suffix-min scans give the next in-frame stop and the next in-frame domain start
+//      of every position;
 //   3. lanes over start codons: the CDS end is one lookup; CDSs long enough go into a per-strand
 //      list (LDS atomic append, order restored next);
 //   4. rank every CDS by (stop ascending, start descending) -- exactly the reference's emission
 //      order (a stop closes its frame's pending starts latest-first);
-//   5. lanes over CDSs in that order: domain extraction from the domain-type table (count pass:
-//      #domains + "has a catalytic or transporter domain"; write pass: tokens at the protein's slot,
-//      from a wave prefix sum).
+//   5. lanes over CDSs in that order: domain extraction, jumping from domain to domain through the
+//      next-domain table (count pass: #domains + "has a catalytic or transporter domain"; write
+//      pass: tokens at the protein's slot, from a wave prefix sum; the fused pass does both).
+// The genome row is staged in LDS with 16-byte loads first, so the per-position work reads LDS only.
 // Forward-strand proteins precede reverse-strand ones (rust/genetics.rs:151-175).
 #include "hip_common.h"
 
@@ -40,8 +42,11 @@ struct TransArgs {
   const int* dn;    // optional device item count (<= n; n is then the capacity)
 };
 
+// cds [2][cap] u32 | nstop [2][w] u16 | order [2][cap] u16 | codons [2][w] u8 | domain type [2][w] u8
+// | next domain [2][w] u16 | counters
 __host__ __device__ inline size_t slot_bytes_for(int width, int cap) {
-  return ((size_t)2 * cap * 4 + (size_t)2 * width * 2 + (size_t)2 * cap * 2 + (size_t)2 * width * 2 + 16 + 15) &
+  return ((size_t)2 * cap * 4 + (size_t)2 * width * 2 + (size_t)2 * cap * 2 + (size_t)2 * width * 2 +
+          (size_t)2 * width * 2 + 16 + 15) &
          ~(size_t)15;
 }
 
@@ -51,7 +56,7 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-template <bool kWrite>
+template <bool kCount, bool kWrite>
 __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -75,7 +80,8 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   uint16_t* order = nstop + 2 * LW;
   uint8_t* cod = reinterpret_cast<uint8_t*>(order + 2 * a.cap);
   uint8_t* dtp = cod + 2 * LW;
-  int* counters = reinterpret_cast<int*>(dtp + 2 * LW);
+  uint16_t* nxd = reinterpret_cast<uint16_t*>(dtp + 2 * LW);
+  int* counters = reinterpret_cast<int*>(nxd + 2 * LW);
 
   for (int i = threadIdx.x; i < 64; i += blockDim.x) {
     l_start[i] = a.is_start[i];
@@ -102,9 +108,16 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   __syncthreads();
   if (!active) return;  // whole waves only; no block-wide barrier below
   if (L > LW) {         // LDS pass: too long for a slot -> queued for the global-slot pass
-    if (!kWrite && lane == 0) a.long_list[atomicAdd(a.long_count, 1)] = g;
+    if (kCount && lane == 0) a.long_list[atomicAdd(a.long_count, 1)] = g;
     return;
   }
+  wave_sync();
+
+  // ---- 0. stage the genome row in LDS (16-byte loads; the row width is a multiple of 16 and the
+  //         staging area -- the domain-type table, filled in step 2 -- holds 2 * LW >= L rounded up)
+  uint8_t* raw = dtp;
+  for (int i = lane * 16; i < L; i += 64 * 16)
+    *reinterpret_cast<uint4*>(raw + i) = *reinterpret_cast<const uint4*>(s + i);
   wave_sync();
 
   // ---- 1. codon index per position, both strands (0xFF past the end)
@@ -112,38 +125,22 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   for (int i = lane; i < L; i += 64) {
     uint8_t cf = 0xFF, cr = 0xFF;
     if (i < ncod) {
-      cf = (uint8_t)((ms::nt_code(s[i]) << 4) | (ms::nt_code(s[i + 1]) << 2) | ms::nt_code(s[i + 2]));
+      cf = (uint8_t)((ms::nt_code(raw[i]) << 4) | (ms::nt_code(raw[i + 1]) << 2) | ms::nt_code(raw[i + 2]));
       // reverse-complement position i covers forward bases L-1-i, L-2-i, L-3-i
-      cr = (uint8_t)((ms::nt_comp(ms::nt_code(s[L - 1 - i])) << 4) |
-                     (ms::nt_comp(ms::nt_code(s[L - 2 - i])) << 2) | ms::nt_comp(ms::nt_code(s[L - 3 - i])));
+      cr = (uint8_t)((ms::nt_comp(ms::nt_code(raw[L - 1 - i])) << 4) |
+                     (ms::nt_comp(ms::nt_code(raw[L - 2 - i])) << 2) | ms::nt_comp(ms::nt_code(raw[L - 3 - i])));
     }
     cod[i] = cf;
     cod[LW + i] = cr;
   }
   wave_sync();
 
-  // ---- 2. next in-frame stop at or after every position (suffix-min scan per strand and frame),
-  //         domain type starting at every position
+  // ---- 2. domain type starting at every position; then, per strand and frame, the next in-frame
+  //         stop and the next in-frame domain start at or after every position (suffix-min scans;
+  //         0xFFFF = none)
   const int ds = a.dom_size, dts = a.dom_type_size, ntc = dts / 3;
   for (int st = 0; st < 2; ++st) {
     const uint8_t* c = cod + st * LW;
-    uint16_t* ns = nstop + st * LW;
-    for (int f = 0; f < 3; ++f) {
-      const int nf = ncod > f ? (ncod - f + 2) / 3 : 0;  // positions f, f+3, ... < ncod
-      int carry = 0xFFFF;
-      for (int hi = nf; hi > 0; hi -= 64) {
-        const int e = hi - 64 + lane;
-        const int pe = f + 3 * e;
-        int v = (e >= 0 && l_stop[c[pe]]) ? pe : 0xFFFF;
-        for (int off = 1; off < 64; off <<= 1) {
-          const int u = __shfl_down(v, off);
-          if (lane + off < 64) v = min(v, u);
-        }
-        v = min(v, carry);
-        if (e >= 0) ns[pe] = (uint16_t)v;
-        carry = __shfl(v, 0);
-      }
-    }
     uint8_t* dt = dtp + st * LW;
     for (int p = lane; p < L; p += 64) {
       uint8_t ty = 0;
@@ -153,6 +150,38 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
         ty = DT[idx];
       }
       dt[p] = ty;
+    }
+  }
+  wave_sync();
+  for (int st = 0; st < 2; ++st) {
+    const uint8_t* c = cod + st * LW;
+    const uint8_t* dt = dtp + st * LW;
+    uint16_t* ns = nstop + st * LW;
+    uint16_t* nd = nxd + st * LW;
+    for (int f = 0; f < 3; ++f) {
+      const int nf = ncod > f ? (ncod - f + 2) / 3 : 0;  // positions f, f+3, ... < ncod
+      int carry = 0xFFFF, carry_d = 0xFFFF;
+      for (int hi = nf; hi > 0; hi -= 64) {
+        const int e = hi - 64 + lane;
+        const int pe = f + 3 * e;
+        int v = (e >= 0 && l_stop[c[pe]]) ? pe : 0xFFFF;
+        int w = (e >= 0 && dt[pe]) ? pe : 0xFFFF;
+        for (int off = 1; off < 64; off <<= 1) {
+          const int u = __shfl_down(v, off), x = __shfl_down(w, off);
+          if (lane + off < 64) {
+            v = min(v, u);
+            w = min(w, x);
+          }
+        }
+        v = min(v, carry);
+        w = min(w, carry_d);
+        if (e >= 0) {
+          ns[pe] = (uint16_t)v;
+          nd[pe] = (uint16_t)w;
+        }
+        carry = __shfl(v, 0);
+        carry_d = __shfl(w, 0);
+      }
     }
   }
   wave_sync();
@@ -196,6 +225,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   for (int st = 0; st < 2; ++st) {
     const uint8_t* c = cod + st * LW;
     const uint8_t* dt = dtp + st * LW;
+    const uint16_t* nd_s = nxd + st * LW;
     int n_prot = 0, max_dom = 0;
     for (int e0 = 0; e0 < ncds[st]; e0 += 64) {
       const int e = e0 + lane;
@@ -206,17 +236,17 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
         p = (int)(v & 0xFFFFu);
         n = (int)(v >> 16) + 3 - p;
       }
+      // domains of the CDS [p, p + n): from position x, the next one starts at nd_s[x] (same frame;
+      // every skipped position has no domain type); it counts if it ends inside the CDS
+      const int end = p + n;
       int nd = 0;
       bool useful = false;
-      for (int i = 0; i + ds <= n;) {
-        const int ty = dt[p + i];
-        if (ty) {
-          useful |= ty != 3;
-          ++nd;
-          i += ds;
-        } else {
-          i += 3;
-        }
+      for (int x = p; x < ncod;) {
+        x = nd_s[x];
+        if (x == 0xFFFF || x + ds > end) break;
+        useful |= dt[x] != 3;
+        ++nd;
+        x += ds;
       }
       const unsigned long long bal = __ballot(useful);
       const int rank = __popcll(bal & ((1ull << lane) - 1ull));
@@ -225,29 +255,27 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
         if (useful && slot_p < a.P) {
           int32_t* tk = a.tokens + ((size_t)g * a.P + slot_p) * a.D * 5;
           int d = 0;
-          for (int i = 0; i + ds <= n && d < a.D;) {
-            const int ty = dt[p + i];
-            if (ty) {
-              const int o = p + i + dts;
-              int32_t* dm = tk + d * 5;
-              dm[0] = ty;
-              dm[1] = l_one[c[o]];
-              dm[2] = l_one[c[o + 3]];
-              dm[3] = l_one[c[o + 6]];
-              dm[4] = l_two[((int)c[o + 9] << 6) | c[o + 12]];
-              ++d;
-              i += ds;
-            } else {
-              i += 3;
-            }
+          for (int x = p; x < ncod && d < a.D;) {
+            x = nd_s[x];
+            if (x == 0xFFFF || x + ds > end) break;
+            const int o = x + dts;
+            int32_t* dm = tk + d * 5;
+            dm[0] = dt[x];
+            dm[1] = l_one[c[o]];
+            dm[2] = l_one[c[o + 3]];
+            dm[3] = l_one[c[o + 6]];
+            dm[4] = l_two[((int)c[o + 9] << 6) | c[o + 12]];
+            ++d;
+            x += ds;
           }
         }
-      } else {
+      }
+      if constexpr (kCount) {
         if (useful && nd > max_dom) max_dom = nd;
       }
       n_prot += __popcll(bal);
     }
-    if constexpr (!kWrite) {
+    if constexpr (kCount) {
       for (int o = 32; o > 0; o >>= 1) max_dom = max(max_dom, __shfl_xor(max_dom, o));
       if (lane == 0) {
         a.nprot[2 * g + st] = n_prot;
@@ -260,7 +288,9 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
 
 constexpr int kLdsMaxLen = 1024;  // genomes up to this length use LDS slots
 
-static void launch(bool write, int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+// mode: 0 count pass, 1 write pass, 2 fused (counts and tokens; the caller checks the counts
+// against P / D afterwards)
+static void launch(int mode, int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
                    uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                    uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t list, uintptr_t gslot,
                    uintptr_t long_list, uintptr_t long_count, uintptr_t dn, uintptr_t stream) {
@@ -307,8 +337,9 @@ static void launch(bool write, int n, uintptr_t rows, uintptr_t arena, int width
   a.gpb = gpb;
   const size_t lds = fixed + (a.gslot ? 0 : gpb * slot);
   const unsigned grid = cdiv(n, gpb);
-  if (write) translate_kernel<true><<<grid, gpb * 64, lds, S_(stream)>>>(a);
-  else translate_kernel<false><<<grid, gpb * 64, lds, S_(stream)>>>(a);
+  if (mode == 0) translate_kernel<true, false><<<grid, gpb * 64, lds, S_(stream)>>>(a);
+  else if (mode == 1) translate_kernel<false, true><<<grid, gpb * 64, lds, S_(stream)>>>(a);
+  else translate_kernel<true, true><<<grid, gpb * 64, lds, S_(stream)>>>(a);
   MS_LAUNCH_CHECK();
 }
 
@@ -321,7 +352,7 @@ void translate_count(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                      uintptr_t nprot, uintptr_t ndom, uintptr_t list, uintptr_t gslot, uintptr_t long_list,
                      uintptr_t long_count, uintptr_t dn, uintptr_t stream) {
-  launch(false, n, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot,
+  launch(0, n, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot,
          ndom, 0, 0, 0, list, gslot, long_list, long_count, dn, stream);
 }
 
@@ -329,8 +360,18 @@ void translate_write(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                      uintptr_t nprot, int P, int D, uintptr_t tokens, uintptr_t list, uintptr_t gslot,
                      uintptr_t dn, uintptr_t stream) {
-  launch(true, n, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot, 0,
+  launch(1, n, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot, 0,
          P, D, tokens, list, gslot, 0, 0, dn, stream);
+}
+
+// Count and write in one launch (LDS pass): tokens for up to P proteins / D domains each, plus the
+// per-strand counts and the long-genome queue of the count pass.
+void translate_fused(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+                     uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
+                     uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t long_list,
+                     uintptr_t long_count, uintptr_t dn, uintptr_t stream) {
+  launch(2, n, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot, ndom,
+         P, D, tokens, 0, 0, long_list, long_count, dn, stream);
 }
 
 }  // namespace msd

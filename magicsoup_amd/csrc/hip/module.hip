@@ -75,6 +75,10 @@ void translate_write(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                      uintptr_t nprot, int P, int D, uintptr_t tokens, uintptr_t list, uintptr_t gslot,
                      uintptr_t dn, uintptr_t stream);
+void translate_fused(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+                     uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
+                     uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t long_list,
+                     uintptr_t long_count, uintptr_t dn, uintptr_t stream);
 size_t translate_slot_bytes(int width);
 // mutations.hip
 void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
@@ -151,6 +155,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("neighbor_pairs", &msd::neighbor_pairs);
   m.def("translate_count", &msd::translate_count);
   m.def("translate_write", &msd::translate_write);
+  m.def("translate_fused", &msd::translate_fused);
   m.def("translate_slot_bytes", &msd::translate_slot_bytes);
   m.def("mut_count", &msd::mut_count);
   m.def("mut_apply", &msd::mut_apply);

@@ -127,12 +127,12 @@ def _rebuild(world, b: dict, cells: torch.Tensor, dcnt: torch.Tensor, cap: int) 
               tables.dom_size, tables.dom_type_size)
     st = _stream()
     of = _p(b["opflags"])
-    _m().translate_count(cap, _p(cells), _p(data), width, _p(lens), *common, _p(counts), _p(ndom), 0, 0,
-                         _p(long_list), _p(long_count), _p(dcnt), st)
-    _m().trans_check(cap, _p(dcnt), _p(counts), _p(ndom), _p(long_count), _p(per), P, D_CAP, of, st)
+    # one fused translation pass into the speculative (P, D_CAP) layout; trans_check flags proteomes
+    # that do not fit it
     _m().zero_rows(cap, _p(dcnt), P * D_CAP * 5, _p(tokens), st)
-    _m().translate_write(cap, _p(cells), _p(data), width, _p(lens), *common, _p(counts), P, D_CAP, _p(tokens), 0, 0,
-                         _p(dcnt), st)
+    _m().translate_fused(cap, _p(cells), _p(data), width, _p(lens), *common, _p(counts), _p(ndom), P, D_CAP,
+                         _p(tokens), _p(long_list), _p(long_count), _p(dcnt), st)
+    _m().trans_check(cap, _p(dcnt), _p(counts), _p(ndom), _p(long_count), _p(per), P, D_CAP, of, st)
     store = kin._kernel_params()
     kin._enter_slot_mode()
     slot = kin.__dict__["_slot"]

@@ -29,3 +29,4 @@ pr.disable()
 st = pstats.Stats(pr)
 st.sort_stats("cumulative").print_stats(45)
 st.sort_stats("tottime").print_stats(45)
+st.sort_stats("tottime").print_stats(30)
