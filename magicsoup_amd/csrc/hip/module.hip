@@ -105,6 +105,9 @@ void zero_rows(int cap, uintptr_t dn, long long row, uintptr_t buf, uintptr_t st
 void assign_rows(int ncap, uintptr_t dn, uintptr_t cells, uintptr_t slot, uintptr_t d_rows, long long row_cap,
                  uintptr_t rows_out, uintptr_t flags, uintptr_t stream);
 void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t dst, uintptr_t stream);
+void flag_above(uintptr_t dn, int cap, uintptr_t flags, int bit, uintptr_t stream);
+int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t cnt, uintptr_t stream);
+std::tuple<long long, long long, long long, long long> status_read(int slot);
 std::tuple<int, int, int> translate_stats(int n, uintptr_t counts, uintptr_t ndom, uintptr_t long_count, uintptr_t per,
                                           uintptr_t stream);
 std::pair<long long, int> select_indices(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel,
@@ -170,6 +173,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("zero_rows", &msd::zero_rows);
   m.def("assign_rows", &msd::assign_rows);
   m.def("gather_dev", &msd::gather_dev);
+  m.def("flag_above", &msd::flag_above);
+  m.def("status_write", &msd::status_write, "pipeline status -> pinned ring slot (returns the slot)");
+  m.def("status_read", &msd::status_read);
   m.def("select_indices", &msd::select_indices,
         "(count, max) of an order-preserving compaction; synchronises the stream");
 }

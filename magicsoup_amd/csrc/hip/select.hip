@@ -281,6 +281,54 @@ void assign_rows(int ncap, uintptr_t dn, uintptr_t cells, uintptr_t slot, uintpt
   MS_LAUNCH_CHECK();
 }
 
+// flags |= bit if *dn > cap
+__global__ void flag_above_kernel(const int* dn, int cap, int* flags, int bit) {
+  if (*dn > cap) atomicOr(flags, bit);
+}
+
+void flag_above(uintptr_t dn, int cap, uintptr_t flags, int bit, uintptr_t stream) {
+  flag_above_kernel<<<1, 1, 0, S_(stream)>>>(P_<int>(dn), cap, P_<int>(flags), bit);
+  MS_LAUNCH_CHECK();
+}
+
+// Pinned status ring: a pipeline call's {count, flags, row counter, selected count} are written by
+// one single-thread kernel straight into coherent host memory; the host reads the slot after the
+// call's event completed (no copy launch, no staging tensors).
+constexpr int kStatusSlots = 64;
+long long* g_status = nullptr;
+long long* g_status_dev = nullptr;
+int g_status_next = 0;
+
+__global__ void status_write_kernel(const int* dcnt, const int* opflags, const long long* d_rows, const int* cnt,
+                                    long long* out) {
+  out[0] = *dcnt;
+  out[1] = *opflags;
+  out[2] = *d_rows;
+  out[3] = *cnt;
+}
+
+int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t cnt, uintptr_t stream) {
+  if (!g_status) {
+    MS_HIP_CHECK(hipHostMalloc((void**)&g_status, kStatusSlots * 4 * sizeof(long long),
+                               hipHostMallocMapped | hipHostMallocCoherent));
+    MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_status_dev, g_status, 0));
+  }
+  const int slot = g_status_next;
+  g_status_next = (g_status_next + 1) % kStatusSlots;
+  for (int i = 0; i < 4; ++i) g_status[slot * 4 + i] = -1;
+  status_write_kernel<<<1, 1, 0, S_(stream)>>>(P_<int>(dcnt), P_<int>(opflags), P_<long long>(d_rows), P_<int>(cnt),
+                                               g_status_dev + slot * 4);
+  MS_LAUNCH_CHECK();
+  return slot;
+}
+
+std::tuple<long long, long long, long long, long long> status_read(int slot) {
+  if (!g_status || slot < 0 || slot >= kStatusSlots) throw std::invalid_argument("status_read: bad slot");
+  const long long* v = g_status + slot * 4;
+  if (v[0] < 0) throw std::runtime_error("status_read: slot not written (event not complete?)");
+  return {v[0], v[1], v[2], v[3]};
+}
+
 void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t dst, uintptr_t stream) {
   const unsigned g = std::min(cdiv(cap, 256), 64u);
   gather_dev_kernel<<<g, 256, 0, S_(stream)>>>(cap, P_<int>(dn), P_<int64_t>(idx), P_<int64_t>(src), P_<int64_t>(dst));

@@ -834,7 +834,7 @@ class Kinetics:
         self._materialize()
         state = self.__dict__.copy()
         state["last_masks"] = []
-        for k in ("_spare", "_hip_scratch", "_owner"):
+        for k in ("_spare", "_hip_scratch", "_owner", "_lut_cache"):
             state.pop(k, None)
         n = state["_ncells"]
         state["_store_d"] = {k: v[:n].clone() for k, v in self._store.items() if k not in _PACKED}

@@ -50,6 +50,21 @@ def enabled(world) -> bool:
     return True
 
 
+class _StatusSlot:
+    """int64[4] in the extension's pinned status ring (valid once the call's event completed)."""
+
+    __slots__ = ("vals", "_slot")
+
+    def __init__(self, slot: int):
+        self.vals = None
+        self._slot = slot
+
+    def __getitem__(self, i: int) -> int:
+        if self.vals is None:
+            self.vals = _m().status_read(self._slot)
+        return self.vals[i]
+
+
 class _Pending:
     """One issued pipeline call: what reconcile needs to resolve it."""
 
@@ -103,7 +118,7 @@ def _begin(world, kind: str) -> dict:
 def _rebuild(world, b: dict, cells: torch.Tensor, dcnt: torch.Tensor, cap: int) -> None:
     """Translate the genomes of ``cells[:*dcnt]`` and build their parameters into fresh rows."""
     from magicsoup_amd.constants import GAS_CONSTANT
-    from magicsoup_amd.ops.kinetics_ops import _luts
+    from magicsoup_amd.ops.kinetics_ops import build_luts
 
     kin = world.kinetics
     genetics = world.genetics
@@ -138,21 +153,16 @@ def _rebuild(world, b: dict, cells: torch.Tensor, dcnt: torch.Tensor, cap: int) 
     slot = kin.__dict__["_slot"]
     row_cap = min(int(t.size(0)) for t in store.values())
     _m().assign_rows(cap, _p(dcnt), _p(cells), _p(slot), _p(b["d_rows"]), row_cap, _p(rows_out), of, st)
-    kl = _luts(kin, dev)
-    n_vec = min(kl["react"].size(0), kl["trnsp"].size(0), kl["eff"].size(0))
-    for k in ("react", "trnsp", "eff"):
-        kl[k] = kl[k][:n_vec].contiguous()
+    kl = build_luts(kin, dev)
     hip_ops.build_params(kin, tokens.view(cap, P, D_CAP, 5), rows_out, kl, store, float(kin.abs_temp), GAS_CONSTANT,
                          nprot=per, dn=dcnt)
 
 
 def _finish(world, kind: str, args: tuple, rng: tuple, b: dict, cells, dcnt, replay: dict) -> None:
-    """Queue the host read-back of {rebuilt count, op flags, row counter, selected count} and
-    record the call as pending."""
-    host = torch.empty(4, dtype=torch.int64, pin_memory=True)
-    packed = torch.cat([dcnt[:1].to(torch.int64), b["opflags"].to(torch.int64), b["d_rows"],
-                        b["cnt"][:1].to(torch.int64)])
-    host.copy_(packed, non_blocking=True)
+    """Have the device write {rebuilt count, op flags, row counter, selected count} into a pinned
+    host slot (one launch) and record the call as pending."""
+    slot = _m().status_write(_p(dcnt), _p(b["opflags"]), _p(b["d_rows"]), _p(b["cnt"]), _stream())
+    host = _StatusSlot(slot)
     ev = torch.cuda.Event()
     ev.record()
     _state(world)["pending"].append(_Pending(kind, args, rng, cells, host, ev, replay))
@@ -216,7 +226,7 @@ def recombinate_all(world, p: float) -> bool:
     _m().rec_count_keys(8 * n, _p(keys), _p(arena.lens), float(p), seed, call, _p(k), 0, K_CAP, gf, of, st)
     _m().select_indices_dev(8 * n, _SEL_I32POS, _p(k), 0, _p(sel), 0, _p(b["cnt"]), st)
     # a selected-pair count above the capacity is flagged (never expected under the usage rule)
-    b["opflags"].bitwise_or_((b["cnt"][:1] > pcap).to(torch.int32) * _F_CAPACITY)
+    _m().flag_above(_p(b["cnt"]), pcap, _p(b["opflags"]), _F_CAPACITY, st)
     out_w = 2 * L  # a recombined genome is at most both parents
     out = sc.get("gp_rout", 2 * pcap * out_w, torch.uint8, dev)
     out_len = sc.get("gp_rout_len", 2 * pcap, torch.int32, dev)

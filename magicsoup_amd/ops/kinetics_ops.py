@@ -52,6 +52,28 @@ def integrate(kin, X: torch.Tensor, trims, n_iters: int, reduce_mask=None) -> li
     return list(masks)
 
 
+def _lut_sources(kin):
+    return (kin.vmax_map.weights, kin.km_map.weights, kin.sign_map.signs, kin.hill_map.numbers, kin.reaction_map.M,
+            kin.transport_map.M, kin.effector_map.M, kin.mol_energies)
+
+
+def build_luts(kin, device) -> dict[str, torch.Tensor]:
+    """Token -> value LUTs in kernel layout, cached until a map tensor is replaced or modified in
+    place (identity + version counter): the device genome pipeline builds parameters twice a step."""
+    src = _lut_sources(kin)
+    key = (str(device),) + tuple((id(t), t._version) for t in src)
+    c = kin.__dict__.get("_lut_cache")
+    if c is not None and c[0] == key:
+        return c[1]
+    luts = _luts(kin, device)
+    # vector maps may be narrower than the token alphabet if a user swapped them (tests do)
+    n_vec = min(luts["react"].size(0), luts["trnsp"].size(0), luts["eff"].size(0))
+    for k in ("react", "trnsp", "eff"):
+        luts[k] = luts[k][:n_vec].contiguous()
+    kin.__dict__["_lut_cache"] = (key, luts, src)  # src keeps the ids alive
+    return luts
+
+
 def _luts(kin, device) -> dict[str, torch.Tensor]:
     return {
         "vmax": kin.vmax_map.weights.to(device=device, dtype=torch.float32).contiguous(),
@@ -74,11 +96,7 @@ def build_params(kin, rows: torch.Tensor, tokens: torch.Tensor, nprot: torch.Ten
         return
     tokens = tokens.to(device=dev, dtype=torch.int32).contiguous()
     rows = rows.to(device=dev, dtype=torch.int32).contiguous()
-    luts = _luts(kin, dev)
-    # vector maps may be narrower than the token alphabet if a user swapped them (tests do)
-    n_vec = min(luts["react"].size(0), luts["trnsp"].size(0), luts["eff"].size(0))
-    for k in ("react", "trnsp", "eff"):
-        luts[k] = luts[k][:n_vec].contiguous()
+    luts = build_luts(kin, dev)
     if dev.type == "cuda":
         from magicsoup_amd.ops import hip_ops
 
