@@ -22,6 +22,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 
 BASELINE_STEPS_PER_S = 3.3  # reference, 40k cells, latest published
@@ -71,6 +72,23 @@ def random_genomes(k: int, size: int, device) -> tuple[torch.Tensor, torch.Tenso
     return rows, torch.full((k,), size, dtype=torch.int32, device=device)
 
 
+_DILUTE = {"rng": np.random.default_rng(0), "pinned": None}
+
+
+def _dilution_sample(n: int, k: int, device) -> torch.Tensor:
+    """k distinct uniform indices < n: sampled on the host (Floyd-style, ~30 us for k = 1000) and
+    shipped through a reused pinned buffer -- a device randperm costs a full sort of n keys."""
+    idx = _DILUTE["rng"].choice(n, size=k, replace=False)
+    if device == "cpu" or str(device) == "cpu":
+        return torch.from_numpy(idx)
+    buf = _DILUTE["pinned"]
+    if buf is None or buf.numel() < k:
+        buf = _DILUTE["pinned"] = torch.empty(max(k, 4096) * 2, dtype=torch.int64, pin_memory=True)
+    # the previous step's copy out of this buffer has completed (kill_cells synchronises)
+    buf[:k].copy_(torch.from_numpy(idx))
+    return buf[:k].to(device, non_blocking=True)
+
+
 def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=None):
     def ph(name):
         import contextlib
@@ -104,7 +122,7 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
         # only tops up; on a 4096^2 map the population would otherwise grow ~6x within 25 steps)
         excess = world.n_cells - n_target
         if excess > 0:
-            world.kill_cells(torch.randperm(world.n_cells, device=world.cell_molecules.device)[:excess])
+            world.kill_cells(_dilution_sample(world.n_cells, excess, world.cell_molecules.device))
             note("diluted", excess)
     with ph("recombinate"):
         world.recombinate_cells()
@@ -149,6 +167,7 @@ def main():
     atp = chem.molname_2_idx.get("ATP", 0)
     ms.set_seed(a.seed + rank)
     torch.manual_seed(a.seed + rank)
+    _DILUTE["rng"] = np.random.default_rng(a.seed + rank)
 
     if distributed:
         from magicsoup_amd.parallel import DistributedWorld
