@@ -44,7 +44,7 @@ void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t
 void permeate(int c, int m, int R, int C, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map, int dtype,
               uintptr_t corr, uintptr_t stream);
 void gather_rows(int n, uintptr_t src_rows, uintptr_t dst_rows,
-                 const std::vector<std::tuple<uintptr_t, uintptr_t, long long, long long, long long>>& descs,
+                 const std::vector<std::tuple<uintptr_t, uintptr_t, long long, long long, long long, uintptr_t>>& descs,
                  uintptr_t stream);
 // kinetics.hip
 void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q, uintptr_t Kmr, uintptr_t cell_mols,

@@ -22,6 +22,8 @@ struct RowDesc {
   long long src_stride, dst_stride;  // bytes between rows
   int units;                         // row size in units
   int unit;                          // 16 or 4 bytes
+  const int32_t* len;                // optional: bytes used by source row r (string arenas); the
+                                     // rest of the row is not copied (padding is never read)
 };
 
 struct RowArgs {
@@ -41,6 +43,7 @@ __device__ __forceinline__ void copy_units(const RowDesc& d, unsigned total, con
   for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
     const unsigned i = t / units, c = t - i * units;
     const long long sr = src_rows ? src_rows[i] : (long long)i;
+    if (d.len && c * sizeof(U) >= (unsigned)d.len[sr]) continue;
     const long long dr = dst_rows ? dst_rows[i] : (long long)i;
     const U v = reinterpret_cast<const U*>(d.src + sr * d.src_stride)[c];
     reinterpret_cast<U*>(d.dst + dr * d.dst_stride)[c] = v;
@@ -60,7 +63,7 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(RowArgs a) {
 // descs: (src_ptr, dst_ptr, src_stride_bytes, dst_stride_bytes, row_bytes) per tensor. Row bytes and
 // strides must be multiples of 4 (of 16 for the vector path, chosen per tensor).
 void gather_rows(int n, uintptr_t src_rows, uintptr_t dst_rows,
-                 const std::vector<std::tuple<uintptr_t, uintptr_t, long long, long long, long long>>& descs,
+                 const std::vector<std::tuple<uintptr_t, uintptr_t, long long, long long, long long, uintptr_t>>& descs,
                  uintptr_t stream) {
   if (n <= 0 || descs.empty()) return;
   for (size_t b = 0; b < descs.size(); b += kMaxDescs) {
@@ -71,7 +74,7 @@ void gather_rows(int n, uintptr_t src_rows, uintptr_t dst_rows,
     int nd = 0;
     long long acc = 0;
     for (size_t q = b; q < descs.size() && nd < kMaxDescs; ++q) {
-      const auto& [sp, dp, ss, ds, rb] = descs[q];
+      const auto& [sp, dp, ss, ds, rb, lp] = descs[q];
       if (rb <= 0) continue;
       if (rb % 4 || ss % 4 || ds % 4 || sp % 4 || dp % 4)
         throw std::invalid_argument("gather_rows: rows, strides and pointers must be 4-byte aligned");
@@ -83,6 +86,7 @@ void gather_rows(int n, uintptr_t src_rows, uintptr_t dst_rows,
       d.dst_stride = ds;
       d.unit = vec ? 16 : 4;
       d.units = (int)(rb / d.unit);
+      d.len = lp ? P_<int32_t>(lp) : nullptr;
       a.first[nd] = acc;
       acc += (long long)n * d.units;
       ++nd;

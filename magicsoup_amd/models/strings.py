@@ -138,7 +138,8 @@ class StringArena:
             sp = (torch.empty(cap, self.width, dtype=torch.uint8, device=self.device),
                   torch.empty(cap, dtype=torch.int32, device=self.device))
             self.__dict__["_spare"] = sp
-        return [(self.data[: self.n], sp[0][:k]), (self.lens[: self.n], sp[1][:k])]
+        # genome rows: only the used bytes move (bytes past a row's length are never read)
+        return [(self.data[: self.n], sp[0][:k], self.lens), (self.lens[: self.n], sp[1][:k])]
 
     def commit_compact(self, k: int) -> None:
         sd, sl = self.__dict__.pop("_spare")
@@ -153,7 +154,7 @@ class StringArena:
         self.reserve(self.n + k)
         self.n += k
         self.version += 1
-        return [(self.data[: self.n], self.data[: self.n]), (self.lens[: self.n], self.lens[: self.n])]
+        return [(self.data[: self.n], self.data[: self.n], self.lens), (self.lens[: self.n], self.lens[: self.n])]
 
     def view(self) -> tuple[torch.Tensor, torch.Tensor]:
         return self.data[: self.n], self.lens[: self.n]

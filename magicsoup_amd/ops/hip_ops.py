@@ -456,11 +456,14 @@ def split_cells(world, parents: torch.Tensor, children: torch.Tensor) -> None:
 
 def gather_rows(pairs, n: int, src_rows: torch.Tensor | None = None, dst_rows: torch.Tensor | None = None) -> None:
     """dst[dst_rows[i]] = src[src_rows[i]] for i < n, for every (src, dst) tensor pair, in one launch
-    (rows are dim 0; each row contiguous; identity where an index tensor is None)."""
+    (rows are dim 0; each row contiguous; identity where an index tensor is None). A pair may carry a
+    third tensor: int32 bytes used per source row (string arenas) -- only those bytes are copied."""
     if n <= 0:
         return
     descs = []
-    for src, dst in pairs:
+    for pair in pairs:
+        src, dst = pair[0], pair[1]
+        lens = pair[2] if len(pair) > 2 else None
         es = src.element_size()
         st = src.stride()
         if not st:
@@ -472,7 +475,9 @@ def gather_rows(pairs, n: int, src_rows: torch.Tensor | None = None, dst_rows: t
             raise ValueError("gather_rows: shape mismatch")
         if len(st) > 1 and not (st[-1] == 1 and src.is_contiguous() or src[:1].is_contiguous()):
             raise ValueError("gather_rows: rows must be contiguous")
-        descs.append((src.data_ptr(), dst.data_ptr(), st[0] * es, dst.stride(0) * es, rb))
+        if lens is not None and (lens.dtype != torch.int32 or not lens.is_contiguous()):
+            raise ValueError("gather_rows: row lengths must be contiguous int32")
+        descs.append((src.data_ptr(), dst.data_ptr(), st[0] * es, dst.stride(0) * es, rb, _p(lens)))
     if not descs:
         return
     sr = None if src_rows is None else (src_rows if src_rows.dtype == torch.int64 and src_rows.is_contiguous()
@@ -492,7 +497,7 @@ def copy_row_prefixes(moves, n: int) -> None:
         rb = src[0].numel() * es if src.size(0) else 0
         assert src.is_contiguous() and dst.is_contiguous() and dst.dtype == src.dtype
         if rb:
-            descs.append((src.data_ptr(), dst.data_ptr(), src.stride(0) * es, dst.stride(0) * es, rb))
+            descs.append((src.data_ptr(), dst.data_ptr(), src.stride(0) * es, dst.stride(0) * es, rb, 0))
     if n > 0 and descs:
         _m().gather_rows(int(n), 0, 0, descs, _stream())
 
