@@ -25,6 +25,15 @@ namespace msd {
 
 constexpr int kBlock = 256;
 constexpr int kNarrowP = 12;  // LDS protein slots of the narrow integrator launch
+constexpr int kWideBlocksPerCU = 2;  // resident blocks per CU of the strided wide launch
+// binned launch mode (set_integrate_mode, for A/B on one state: scripts/integrator_bench.py):
+// bits 0-1: 0 serial (narrow then wide, full grids), 1 wide on a side stream next to the narrow
+// launch, 2 as 1 with the wide bin on a small strided grid; bit 2: 16-lane groups for the narrow
+// launch. Measured at 4096^2 / 50k (3 parts, 4 iterations): serial 532 us, concurrent 558 us,
+// 16-lane 590 us -- the kernel is VALU-throughput bound (37M wave instructions per launch, ~60 %
+// of the SIMDs' issue capacity), so overlapping the bins only adds contention. Serial is default.
+static int g_integrate_mode = 0;
+void set_integrate_mode(int mode) { g_integrate_mode = mode; }
 
 struct IntegrateArgs {
   int c, P, s;
@@ -63,12 +72,10 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// One cell (list item `item`) per G-lane group; ORs the cell's "still correcting" bits into `bits`.
 template <int G>
-__global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a) {
-  extern __shared__ __attribute__((aligned(16))) int smem[];
+__device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem, int item, unsigned& bits) {
   const int slot = threadIdx.x / G, lane = threadIdx.x % G;
-  const int cps = blockDim.x / G;
-  const int item = blockIdx.x * cps + slot;
   const bool valid = a.list ? item < *a.count : item < a.c;
   const int cell = valid ? (a.list ? a.list[item] : item) : 0;
   const int P = a.P, s = a.s, SP = a.sp, Ps = a.Ps;
@@ -252,7 +259,6 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
   wave_lds_sync();
 
   // ---- 8. equilibrium damping trajectory
-  unsigned bits = 0u;
   float inc = 0.5f;
   for (int it = 0; it < a.n_iters; ++it, inc *= 0.5f) {
     for (int k = lane; k < na; k += G) {
@@ -305,6 +311,24 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
       if (valid) sn[j] = x;
     }
     wave_lds_sync();
+  }
+}
+
+// kStride: grid-stride over groups of cells with a block-uniform trip count (the wide bin runs on
+// a small grid next to the narrow launch); otherwise one group per block.
+template <int G, bool kStride>
+__global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  const int cps = blockDim.x / G, slot = threadIdx.x / G;
+  unsigned bits = 0u;
+  if constexpr (kStride) {
+    const int limit = a.list ? *a.count : a.c;
+    for (int base = (int)blockIdx.x * cps; base < limit; base += (int)gridDim.x * cps) {
+      integrate_item<G>(a, smem, base + slot, bits);
+      wave_lds_sync();
+    }
+  } else {
+    integrate_item<G>(a, smem, (int)blockIdx.x * cps + slot, bits);
   }
 
   // ---- 9. OR the "still correcting" bits: wave -> block -> at most one atomic per block and bit,
@@ -571,7 +595,10 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     }
     MS_LAUNCH_CHECK();
   }
-  const int G = s <= 32 ? 32 : 64;
+  const int G_wide = s <= 32 ? 32 : 64;
+  // narrow launch: 16-lane groups (4 cells per wave) halve the idle lanes of the protein phases
+  // (<= kNarrowP proteins); signal phases take s / 16 passes instead
+  const int G_narrow = (g_integrate_mode & 4) ? 16 : G_wide;
   const int sp = (s % 2 == 0) ? s + 1 : s;
   // narrow / wide binning (only worth it when P is well above the typical active count)
   const bool binned = lists != 0 && P > kNarrowP;
@@ -596,9 +623,27 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
   } else {
     launches[nl++] = Launch{P, nullptr, nullptr};
   }
+  // Binned parts run the wide launch on a side stream concurrently with the narrow one: the wide
+  // bin is small but its large proteomes are long per-cell dependency chains, which then overlap
+  // with the narrow bin's throughput work instead of adding to it (fork / join per part; the next
+  // part reads both bins' flags).
+  static hipStream_t side = nullptr;
+  static hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  const bool conc = nl == 2 && (g_integrate_mode & 3) != 0;
+  if (conc && !side) {
+    MS_HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    MS_HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    MS_HIP_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+  }
   for (int part = part_begin; part < part_end; ++part) {
-    for (int li = 0; li < nl; ++li) {
+    if (conc) {
+      MS_HIP_CHECK(hipEventRecord(ev_fork, st));
+      MS_HIP_CHECK(hipStreamWaitEvent(side, ev_fork, 0));
+    }
+    for (int li = nl - 1; li >= 0; --li) {  // wide first: its long chains start early
       const Launch& L = launches[li];
+      const int G = (nl == 2 && li == 0) ? G_narrow : G_wide;
+      hipStream_t ls = (conc && li == 1) ? side : st;
       const int slot_words = slot_words_for(L.Ps, s, sp);
       const size_t slot_bytes = (size_t)slot_words * 4;
       int cps = kBlock / G;
@@ -606,7 +651,12 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
       const size_t lds = cps * slot_bytes;
       if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
       const int threads = cps * G;
-      const unsigned grid = cdiv(c, cps);
+      const bool stride = conc && li == 1 && (g_integrate_mode & 3) == 2;
+      unsigned grid = cdiv(c, cps);
+      if (stride) {  // the wide bin: at most kWideBlocksPerCU resident blocks per CU, striding
+        const long long per_cu = std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)lds));
+        grid = (unsigned)std::min<long long>(grid, 256 * per_cu);
+      }
       IntegrateArgs a{};
       a.c = c; a.P = P; a.s = s;
       a.W = P_<int32_t>(W); a.Q = P_<float4>(Q); a.Kmr = P_<float>(Kmr);
@@ -628,9 +678,20 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
       a.list = L.list;
       a.count = L.count;
       a.Ps = L.Ps;
-      if (G == 32) integrate_part_kernel<32><<<grid, threads, lds, st>>>(a);
-      else integrate_part_kernel<64><<<grid, threads, lds, st>>>(a);
+      if (G == 16) {
+        integrate_part_kernel<16, false><<<grid, threads, lds, ls>>>(a);
+      } else if (G == 32) {
+        if (stride) integrate_part_kernel<32, true><<<grid, threads, lds, ls>>>(a);
+        else integrate_part_kernel<32, false><<<grid, threads, lds, ls>>>(a);
+      } else {
+        if (stride) integrate_part_kernel<64, true><<<grid, threads, lds, ls>>>(a);
+        else integrate_part_kernel<64, false><<<grid, threads, lds, ls>>>(a);
+      }
       MS_LAUNCH_CHECK();
+    }
+    if (conc) {
+      MS_HIP_CHECK(hipEventRecord(ev_join, side));
+      MS_HIP_CHECK(hipStreamWaitEvent(st, ev_join, 0));
     }
   }
   // the write-back selects the last part's snapshot by its (possibly all-reduced) flags, so a

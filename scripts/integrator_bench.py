@@ -42,6 +42,21 @@ def main():
     out["active_mean"] = round(float(na.float().mean()), 2)
     out["active_hist"] = {str(k): int((na == k).sum()) for k in range(0, int(na.max()) + 1)}
     out["us_enzymatic_activity"] = timed(w.enzymatic_activity)
+    from magicsoup_amd.ops import native
+
+    for rep_i in range(3):  # A/B of the binned launch modes on the same state (alternating)
+        for mode in (0, 1, 4, 5):
+            native.hip().set_integrate_mode(mode)
+            Xk = X.clone()
+            out[f"us_mode{mode}_r{rep_i}"] = timed(lambda: kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4))
+    res = {}
+    for mode in (0, 1, 4, 5):  # every mode computes the same state, bit for bit
+        native.hip().set_integrate_mode(mode)
+        Xk = X.clone()
+        kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4)
+        res[mode] = Xk
+    out["modes_equal"] = all(torch.equal(res[0], v) for v in res.values())
+    native.hip().set_integrate_mode(0)
     for trims in ((0.7,), (0.7, 0.2, 0.1)):
         for it in (0, 4):
             Xk = X.clone()
