@@ -134,36 +134,42 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
   wave_lds_sync();
   const int na = valid ? *na_p : 0;
 
-  // ---- 3. stage the packed stoichiometry rows of the active proteins: 8 independent loads per
-  //         lane in flight per batch (one batch covers na * s <= 8 G words, i.e. most cells)
-  for (int base = 0; base < na * s; base += 8 * G) {
-    int w[8];
+  // ---- 3. stage the packed stoichiometry rows of the active proteins -- lanes over signals, up to
+  //         8 rows (8 independent loads per lane) in flight per batch, no index division -- and
+  //         each row's non-zero signals in ascending order from one wave ballot per row
+  for (int j0 = 0; j0 < s; j0 += G) {
+    const int j = j0 + lane;
+    for (int k0 = 0; k0 < na; k0 += 8) {
+      int w[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int idx = base + u * G + lane;
-      w[u] = 0;
-      if (idx < na * s) {
-        const int k = idx / s, j = idx - k * s;
-        w[u] = a.W[(prow * P + act[k]) * s + j];
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u;
+        w[u] = (k < na && j < s) ? a.W[(prow * P + act[k]) * s + j] : 0;
       }
-    }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int idx = base + u * G + lane;
-      if (idx < na * s) {
-        const int k = idx / s, j = idx - k * s;
-        words[k * SP + j] = w[u];
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u;
+        if (k < na && j < s) words[k * SP + j] = w[u];
       }
     }
   }
   wave_lds_sync();
-  for (int k = lane; k < na; k += G) {
-    const int* wr = words + k * SP;
-    uint8_t* nz = nzj + k * s;
-    int cnt = 0;
-    for (int j = 0; j < s; ++j)
-      if (wr[j] != 0) nz[cnt++] = (uint8_t)j;
-    nnz[k] = cnt;
+  {
+    const int gbase = (threadIdx.x & 63) - lane;  // first lane of this group inside the wave
+    for (int k = 0; k < na; ++k) {                 // group-uniform trip count
+      int cnt = 0;
+      for (int j0 = 0; j0 < s; j0 += G) {
+        const int j = j0 + lane;
+        const bool on = j < s && words[k * SP + j] != 0;
+        const unsigned long long bal = __ballot(on);
+        unsigned long long gm;
+        if constexpr (G == 64) gm = bal;
+        else gm = (bal >> gbase) & ((1ull << G) - 1ull);
+        if (on) nzj[k * s + cnt + __popcll(gm & ((1ull << lane) - 1ull))] = (uint8_t)j;
+        cnt += __popcll(gm);
+      }
+      if (lane == 0) nnz[k] = cnt;
+    }
   }
   wave_lds_sync();
 

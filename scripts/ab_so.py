@@ -1,0 +1,71 @@
+"""A/B two builds of the _hip extension on one world state, in one process: the flagship world is
+built with the in-tree module, then an integrate (3 parts, 4 iterations) on the same explicit X is
+timed alternately with module A and module B, and their results are compared bit for bit.
+
+usage: python scripts/ab_so.py A.so B.so"""
+import importlib.machinery
+import importlib.util
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import magicsoup_amd as ms  # noqa: E402
+from magicsoup_amd.ops import kinetics_ops, native  # noqa: E402
+
+
+def load(path, tag):
+    name = f"ab_{tag}._hip"
+    loader = importlib.machinery.ExtensionFileLoader(name, path)
+    spec = importlib.util.spec_from_loader(name, loader)
+    mod = importlib.util.module_from_spec(spec)
+    loader.exec_module(mod)
+    return mod
+
+
+def timed(fn, iters=20):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return round(a.elapsed_time(b) / iters * 1e3, 1)
+
+
+def main():
+    mods = {"A": load(sys.argv[1], "a"), "B": load(sys.argv[2], "b")}
+    chem = bench._chemistry("wl")
+    atp = chem.molname_2_idx["ATP"]
+    w = ms.World(chemistry=chem, map_size=4096, device="cuda", seed=0)
+    w.spawn_cells(bench.random_genomes(50000, 500, "cuda"))
+    for _ in range(5):
+        bench.step(w, 50000, 500, atp)
+    kin = w.kinetics
+    pos = w.cell_positions.long()
+    X = torch.cat([w.cell_molecules, w.molecule_map[:, pos[:, 0], pos[:, 1]].T], dim=1).contiguous()
+    kin._packed_params()
+    out, res = {"P": int(kin._P())}, {}
+    orig = native._mods.get("_hip")
+    try:
+        for rep in range(3):
+            for tag, mod in mods.items():
+                native._mods["_hip"] = mod
+                Xk = X.clone()
+                out[f"{tag}_r{rep}"] = timed(lambda: kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4))
+                Xk = X.clone()
+                kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4)
+                res[tag] = Xk
+        out["equal"] = bool(torch.equal(res["A"], res["B"]))
+    finally:
+        native._mods["_hip"] = orig
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
