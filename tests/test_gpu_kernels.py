@@ -451,7 +451,7 @@ def test_deferred_diffusion_correction_matches_materialised():
     assert float(a.molecule_map.min()) >= 0.0
 
 
-def _genetics_run(monkeypatch, base, sync: bool, d_cap=None, steps=5):
+def _genetics_run(monkeypatch, base, sync: bool, d_cap=None, steps=5, mut_kw=None, rec_p=1e-4, prep=None):
     import copy as _copy
 
     from magicsoup_amd.ops import genome_pipeline
@@ -463,6 +463,8 @@ def _genetics_run(monkeypatch, base, sync: bool, d_cap=None, steps=5):
     if d_cap is not None:
         monkeypatch.setattr(genome_pipeline, "D_CAP", d_cap)
     w = _copy.deepcopy(base)  # identical start (GPU spawn placement is claim-order dependent)
+    if prep is not None:
+        prep(w)
     ms.set_seed(11)
     torch.manual_seed(11)
     atp = CHEMISTRY.molname_2_idx["ATP"]
@@ -470,12 +472,61 @@ def _genetics_run(monkeypatch, base, sync: bool, d_cap=None, steps=5):
         w.enzymatic_activity()
         w.kill_cells(w.cell_molecules[:, atp] < 0.3)
         w.divide_cells_t(w.cell_molecules[:, atp] > 3.0)
-        w.recombinate_cells(p=1e-4)
-        w.mutate_cells(p=1e-3)
+        w.recombinate_cells(p=rec_p)
+        w.mutate_cells(**(mut_kw or {"p": 1e-3}))
         w.diffuse_molecules()
     w.enzymatic_activity()
     names = ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke")
     return list(w.cell_genomes), {k: getattr(w.kinetics, k).clone() for k in names}, w.cell_molecules.clone()
+
+
+def test_device_genome_pipeline_arena_overflow_replay(monkeypatch):
+    """Genomes exactly as wide as the arena rows, insertion-only mutations and frequent
+    recombination: results that do not fit the arena are committed at reconcile (width flag) and
+    the calls queued behind them are replayed (skipped flag) -- same genomes, parameters and
+    trajectory as the synchronous path."""
+    from magicsoup_amd.ops import genome_pipeline
+
+    seen = []
+    orig = genome_pipeline.reconcile
+
+    def spy(world):
+        st = world.__dict__.get("_gp_state")
+        if st and st["pending"]:
+            st["pending"][-1].event.synchronize()
+            seen.extend(int(pd.host[1]) for pd in st["pending"])
+        orig(world)
+
+    from magicsoup_amd.models.strings import StringArena, StringColumn
+
+    def tighten(w):
+        # re-pack the genomes into rows exactly as wide as they are (spawn leaves 2x headroom)
+        n = w._genomes.n
+        tight = StringArena(w._genomes.data.device, width=512)
+        tight.reserve(n)
+        tight.data[:n] = w._genomes.data[:n, :512]
+        tight.lens[:n] = w._genomes.lens[:n]
+        tight.n = n
+        w.__dict__["_genomes"] = tight
+        w.__dict__["_genome_col"] = StringColumn(tight)
+        assert w._genomes.width == 512 and int(tight.lens[:n].max()) <= 512
+
+    base = _world("cuda", map_size=64, n=0, seed=5)
+    base.spawn_cells([ms.random_genome(512) for _ in range(600)])
+    assert int(base._genomes.lens[: base.n_cells].max()) == 512
+    kw = dict(steps=3, mut_kw={"p": 1.5e-3, "p_indel": 1.0, "p_del": 0.0}, rec_p=2e-4, prep=tighten)
+    g0, p0, x0 = _genetics_run(monkeypatch, base, sync=True, **kw)
+    monkeypatch.setattr(genome_pipeline, "reconcile", spy)
+    g1, p1, x1 = _genetics_run(monkeypatch, base, sync=False, **kw)
+    assert any(f & genome_pipeline._F_WIDTH for f in seen), seen
+    assert any(f & genome_pipeline._F_SKIPPED for f in seen), seen
+    assert g0 == g1
+    for k in p0:
+        P = min(p0[k].size(1), p1[k].size(1))
+        assert torch.equal(p0[k][:, :P], p1[k][:, :P]), k
+        if p1[k].size(1) > P:
+            assert not p1[k][:, P:].any(), k
+    assert torch.equal(x0, x1)
 
 
 @pytest.mark.parametrize("d_cap", [None, 1])
