@@ -43,7 +43,7 @@ void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t
             uintptr_t corr, uintptr_t stream);
 void permeate(int c, int m, int R, int C, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map, int dtype,
               uintptr_t corr, uintptr_t stream);
-void gather_rows(int n, uintptr_t src_rows, uintptr_t dst_rows,
+void gather_rows(int n, uintptr_t dn, uintptr_t src_rows, uintptr_t dst_rows,
                  const std::vector<std::tuple<uintptr_t, uintptr_t, long long, long long, long long, uintptr_t>>& descs,
                  uintptr_t stream);
 // kinetics.hip
@@ -107,6 +107,7 @@ void assign_rows(int ncap, uintptr_t dn, uintptr_t cells, uintptr_t slot, uintpt
                  uintptr_t rows_out, uintptr_t flags, uintptr_t stream);
 void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t dst, uintptr_t stream);
 void flag_above(uintptr_t dn, int cap, uintptr_t flags, int bit, uintptr_t stream);
+int count_to_host(uintptr_t dcount, uintptr_t stream);
 int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t cnt, uintptr_t stream);
 std::tuple<long long, long long, long long, long long> status_read(int slot);
 std::tuple<int, int, int> translate_stats(int n, uintptr_t counts, uintptr_t ndom, uintptr_t long_count, uintptr_t per,
@@ -176,6 +177,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("assign_rows", &msd::assign_rows);
   m.def("gather_dev", &msd::gather_dev);
   m.def("flag_above", &msd::flag_above);
+  m.def("count_to_host", &msd::count_to_host, "device {count, max} -> pinned ring slot (returns the slot)");
   m.def("status_write", &msd::status_write, "pipeline status -> pinned ring slot (returns the slot)");
   m.def("status_read", &msd::status_read);
   m.def("select_indices", &msd::select_indices,

@@ -30,6 +30,7 @@ struct RowArgs {
   RowDesc d[kMaxDescs];
   long long first[kMaxDescs + 1];  // prefix of n * units over descriptors
   int nd, n;
+  const int* dn;            // optional device row count (<= n; n is then the capacity)
   const int64_t* src_rows;  // nullptr: identity
   const int64_t* dst_rows;  // nullptr: identity
 };
@@ -52,7 +53,8 @@ __device__ __forceinline__ void copy_units(const RowDesc& d, unsigned total, con
 
 __global__ void __launch_bounds__(256) gather_rows_kernel(RowArgs a) {
   const RowDesc& d = a.d[blockIdx.y];
-  const unsigned total = (unsigned)(a.first[blockIdx.y + 1] - a.first[blockIdx.y]);
+  const unsigned n_eff = (unsigned)(a.dn ? min(*a.dn, a.n) : a.n);
+  const unsigned total = n_eff * (unsigned)d.units;
   if (blockIdx.x * blockDim.x >= total) return;
   if (d.unit == 16)
     copy_units<uint4>(d, total, a.src_rows, a.dst_rows);
@@ -62,13 +64,14 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(RowArgs a) {
 
 // descs: (src_ptr, dst_ptr, src_stride_bytes, dst_stride_bytes, row_bytes) per tensor. Row bytes and
 // strides must be multiples of 4 (of 16 for the vector path, chosen per tensor).
-void gather_rows(int n, uintptr_t src_rows, uintptr_t dst_rows,
+void gather_rows(int n, uintptr_t dn, uintptr_t src_rows, uintptr_t dst_rows,
                  const std::vector<std::tuple<uintptr_t, uintptr_t, long long, long long, long long, uintptr_t>>& descs,
                  uintptr_t stream) {
   if (n <= 0 || descs.empty()) return;
   for (size_t b = 0; b < descs.size(); b += kMaxDescs) {
     RowArgs a{};
     a.n = n;
+    a.dn = dn ? P_<int>(dn) : nullptr;
     a.src_rows = src_rows ? P_<int64_t>(src_rows) : nullptr;
     a.dst_rows = dst_rows ? P_<int64_t>(dst_rows) : nullptr;
     int nd = 0;

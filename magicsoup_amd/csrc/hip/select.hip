@@ -322,6 +322,29 @@ int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t 
   return slot;
 }
 
+__global__ void count_to_host_kernel(const int* dcount, long long* out) {
+  out[0] = dcount[0];
+  out[1] = dcount[1];
+  out[2] = 0;
+  out[3] = 0;
+}
+
+// {count, max} of a device-count select into a pinned ring slot: the host launches the work that
+// depends on the count first and reads the slot after one stream synchronisation
+int count_to_host(uintptr_t dcount, uintptr_t stream) {
+  if (!g_status) {
+    MS_HIP_CHECK(hipHostMalloc((void**)&g_status, kStatusSlots * 4 * sizeof(long long),
+                               hipHostMallocMapped | hipHostMallocCoherent));
+    MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_status_dev, g_status, 0));
+  }
+  const int slot = g_status_next;
+  g_status_next = (g_status_next + 1) % kStatusSlots;
+  for (int i = 0; i < 4; ++i) g_status[slot * 4 + i] = -1;
+  count_to_host_kernel<<<1, 1, 0, S_(stream)>>>(P_<int>(dcount), g_status_dev + slot * 4);
+  MS_LAUNCH_CHECK();
+  return slot;
+}
+
 std::tuple<long long, long long, long long, long long> status_read(int slot) {
   if (!g_status || slot < 0 || slot >= kStatusSlots) throw std::invalid_argument("status_read: bad slot");
   const long long* v = g_status + slot * 4;

@@ -563,11 +563,21 @@ class World:
         if dead.is_cuda:
             from magicsoup_amd.ops import hip_ops
 
-            # survivors and the dead in one compaction pass (one stream sync for the count)
-            keep_idx, dead_idx, _ = hip_ops.select(dead, "clear", rest=True)
-            if int(keep_idx.numel()) == n:
-                return
-            self._compact(keep_idx, None, removed=dead_idx)
+            # survivors and the dead in one compaction pass; the row gather is launched with the
+            # device-side survivor count before the one stream sync that brings it to the host
+            keep_buf, dead_buf, dcount, slot = hip_ops.select_async(dead, "clear", rest=True)
+            pairs = [(col.view(n), col.spare_rows(n)) for col in self._cols.values()]
+            pairs += self._genomes.compact_pairs(n) + self._labels.compact_pairs(n)
+            hip_ops.gather_rows(pairs, n, src_rows=keep_buf, dn=dcount)
+            n_new = hip_ops.wait_count(slot)
+            if n_new == n:
+                return  # nothing removed: the spare buffers are simply not adopted
+            self.kinetics.remove_cell_params(keep=keep_buf[:n_new], removed=dead_buf[: n - n_new])
+            for col in self._cols.values():
+                col.swap()
+            self._genomes.commit_compact(n_new)
+            self._labels.commit_compact(n_new)
+            self.n_cells = n_new
             return
         keep = ~dead
         keep_idx = torch.nonzero(keep).flatten()

@@ -98,6 +98,29 @@ def select(src: torch.Tensor, kind: str, vals: torch.Tensor | None = None, rest:
     return sel[:cnt], (rst[: n - cnt] if rest else None), int(mx)
 
 
+def select_async(src: torch.Tensor, kind: str, rest: bool = False):
+    """:func:`select` without the synchronisation: (selected (n,), rejected (n,) or None, device
+    count int32[2], status slot). Launch the work that depends on the count with ``dn`` = the device
+    count, then :func:`wait_count` the slot."""
+    n = int(src.numel())
+    dev = src.device
+    if src.dtype == torch.bool:
+        src = src.view(torch.uint8)
+    src = src.contiguous()
+    sel = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    rst = torch.empty(max(n, 1), dtype=torch.int64, device=dev) if rest else None
+    dcount = torch.empty(2, dtype=torch.int32, device=dev)
+    _m().select_indices_dev(n, _SEL[kind], _p(src), 0, _p(sel), _p(rst), _p(dcount), _stream())
+    slot = _m().count_to_host(_p(dcount), _stream())
+    return sel, rst, dcount, slot
+
+
+def wait_count(slot: int) -> int:
+    """Synchronise the current stream and read a :func:`select_async` count."""
+    torch.cuda.current_stream().synchronize()
+    return int(_m().status_read(slot)[0])
+
+
 # ---------------------------------------------------------------------------- geometry
 # ---------------------------------------------------------------------------- kinetics
 _EQ = 4  # equilibrium-damping iterations per part
@@ -454,7 +477,8 @@ def split_cells(world, parents: torch.Tensor, children: torch.Tensor) -> None:
                      _p(world.cell_lifetimes), _stream())
 
 
-def gather_rows(pairs, n: int, src_rows: torch.Tensor | None = None, dst_rows: torch.Tensor | None = None) -> None:
+def gather_rows(pairs, n: int, src_rows: torch.Tensor | None = None, dst_rows: torch.Tensor | None = None,
+                dn: torch.Tensor | None = None) -> None:
     """dst[dst_rows[i]] = src[src_rows[i]] for i < n, for every (src, dst) tensor pair, in one launch
     (rows are dim 0; each row contiguous; identity where an index tensor is None). A pair may carry a
     third tensor: int32 bytes used per source row (string arenas) -- only those bytes are copied."""
@@ -484,7 +508,7 @@ def gather_rows(pairs, n: int, src_rows: torch.Tensor | None = None, dst_rows: t
                                         else src_rows.to(torch.int64).contiguous())
     dr = None if dst_rows is None else (dst_rows if dst_rows.dtype == torch.int64 and dst_rows.is_contiguous()
                                         else dst_rows.to(torch.int64).contiguous())
-    _m().gather_rows(int(n), _p(sr), _p(dr), descs, _stream())
+    _m().gather_rows(int(n), _p(dn), _p(sr), _p(dr), descs, _stream())
 
 
 def copy_row_prefixes(moves, n: int) -> None:
@@ -499,7 +523,7 @@ def copy_row_prefixes(moves, n: int) -> None:
         if rb:
             descs.append((src.data_ptr(), dst.data_ptr(), src.stride(0) * es, dst.stride(0) * es, rb, 0))
     if n > 0 and descs:
-        _m().gather_rows(int(n), 0, 0, descs, _stream())
+        _m().gather_rows(int(n), 0, 0, 0, descs, _stream())
 
 
 def _index_map(world, npix: int, dev) -> torch.Tensor:
