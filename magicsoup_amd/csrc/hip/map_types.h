@@ -90,6 +90,21 @@ __device__ __forceinline__ void st4<_Float16>(_Float16* p, const float v[4]) {
   *reinterpret_cast<h4*>(p) = q;
 }
 
+// streaming store of 4 values (the stencil's output is not re-read before the next step): fp32
+// with a nontemporal hint (-4 % on the 4096^2 x 14 fp32 stencil; nontemporal loads measured +6 %,
+// the halo rows are re-read by the neighbouring band), the narrow types as st4
+template <class T>
+__device__ __forceinline__ void st4_stream(T* p, const float v[4]) {
+  st4(p, v);
+}
+template <>
+__device__ __forceinline__ void st4_stream<float>(float* p, const float v[4]) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4 q;
+  q[0] = v[0], q[1] = v[1], q[2] = v[2], q[3] = v[3];
+  __builtin_nontemporal_store(q, reinterpret_cast<f4*>(p));
+}
+
 // runtime-typed access (cold paths: a few pixels per cell)
 __device__ __forceinline__ float ld_map(const void* base, size_t i, int dtype) {
   switch (dtype) {

@@ -188,7 +188,7 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
 #pragma unroll
       for (int j = 0; j < 4; ++j) res[j] = b * vc[j] + a * (hp[j] + hn[j] + lft[j] + rgt[j]);
       if (col) {
-        st4(dst + (size_t)row_of(o) * g.C + y0, res);
+        st4_stream(dst + (size_t)row_of(o) * g.C + y0, res);
         before += (double)((vc[0] + vc[1]) + (vc[2] + vc[3]));
         after += (double)((res[0] + res[1]) + (res[2] + res[3]));
       }
