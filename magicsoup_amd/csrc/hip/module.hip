@@ -108,6 +108,7 @@ void assign_rows(int ncap, uintptr_t dn, uintptr_t cells, uintptr_t slot, uintpt
 void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t dst, uintptr_t stream);
 void flag_above(uintptr_t dn, int cap, uintptr_t flags, int bit, uintptr_t stream);
 int count_to_host(uintptr_t dcount, uintptr_t stream);
+void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
 int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t cnt, uintptr_t stream);
 std::tuple<long long, long long, long long, long long> status_read(int slot);
 std::tuple<int, int, int> translate_stats(int n, uintptr_t counts, uintptr_t ndom, uintptr_t long_count, uintptr_t per,
@@ -177,6 +178,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("assign_rows", &msd::assign_rows);
   m.def("gather_dev", &msd::gather_dev);
   m.def("flag_above", &msd::flag_above);
+  m.def("cap_skip", &msd::cap_skip, "pipeline capacity guard: count > cap -> no-op call replayed by the host");
   m.def("count_to_host", &msd::count_to_host, "device {count, max} -> pinned ring slot (returns the slot)");
   m.def("status_write", &msd::status_write, "pipeline status -> pinned ring slot (returns the slot)");
   m.def("status_read", &msd::status_read);

@@ -291,6 +291,23 @@ void flag_above(uintptr_t dn, int cap, uintptr_t flags, int bit, uintptr_t strea
   MS_LAUNCH_CHECK();
 }
 
+// Capacity guard of a device-pipeline call: a selected count above the buffers' capacity turns the
+// call into a no-op (count 0) that the host replays on the synchronous path (opflags |= skipped)
+// and breaks the pending chain (gflags |= the arena-width bit), so later calls replay too.
+constexpr int kGpWidthBit = 8, kGpSkippedBit = 16;  // mutations.hip kGpWidth / kGpSkipped
+__global__ void cap_skip_kernel(int* dn, int cap, int* gflags, int* opflags) {
+  if (*dn > cap) {
+    *dn = 0;
+    atomicOr(opflags, kGpSkippedBit);
+    atomicOr(gflags, kGpWidthBit);
+  }
+}
+
+void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream) {
+  cap_skip_kernel<<<1, 1, 0, S_(stream)>>>(P_<int>(dn), cap, P_<int>(gflags), P_<int>(opflags));
+  MS_LAUNCH_CHECK();
+}
+
 // Pinned status ring: a pipeline call's {count, flags, row counter, selected count} are written by
 // one single-thread kernel straight into coherent host memory; the host reads the slot after the
 // call's event completed (no copy launch, no staging tensors).

@@ -37,6 +37,13 @@ from magicsoup_amd.ops.hip_ops import _m, _p, _rng, _scratch, _stream
 K_CAP = 32  # event-count cap per genome (P(Poisson(lam <= 1) > 32) < 1e-35)
 D_CAP = 12  # domain slots per protein in the speculative token layout
 N_CAP = 8192  # genomes per pipeline call (the expected count is kept <= N_CAP / 4)
+
+
+def _cap(expected: float, limit: int) -> int:
+    """Buffer / grid capacity of a call: far above the expected count (a count above it makes the
+    call a no-op that reconcile replays on the synchronous path, see cap_skip), far below N_CAP
+    for small rates, so the launches after the selection stay small."""
+    return max(1, min(limit, int(8 * expected) + 256))
 # flag bits (select.hip DevFlag, mutations.hip kGp*)
 _F_TRANSLATE, _F_CAPACITY, _F_ROWS, _F_WIDTH, _F_SKIPPED = 1, 2, 4, 8, 16
 _SEL_I32POS, _SEL_SET = 2, 0
@@ -180,7 +187,7 @@ def point_mutations(world, p: float, p_indel: float, p_del: float) -> bool:
     if p * L > 1.0 or not _usable(world, n * p * L):
         return False
     dev = arena.data.device
-    cap = min(n, N_CAP)
+    cap = _cap(n * p * L, min(n, N_CAP))
     b = _begin(world, "mut")
     sc = _scratch(world)
     k = sc.get("gp_k", n, torch.int32, dev)
@@ -189,6 +196,7 @@ def point_mutations(world, p: float, p_indel: float, p_del: float) -> bool:
     st = _stream()
     _m().mut_count(n, 0, _p(arena.lens), float(p), seed, call, _p(k), K_CAP, _p(b["gflags"]), _p(b["opflags"]), st)
     _m().select_indices_dev(n, _SEL_I32POS, _p(k), 0, _p(sel), 0, _p(b["cnt"]), st)
+    _m().cap_skip(_p(b["cnt"]), cap, _p(b["gflags"]), _p(b["opflags"]), st)
     dcnt = b["cnt"]
     out_w = (L + K_CAP + 15) // 16 * 16
     out = sc.get("gp_out", cap * out_w, torch.uint8, dev)
@@ -214,7 +222,7 @@ def recombinate_all(world, p: float) -> bool:
     if p * 2 * L > 1.0 or not _usable(world, expected):
         return False
     dev = arena.data.device
-    pcap = min(n, N_CAP) // 2  # pairs per call (two results each)
+    pcap = _cap(expected, min(n, N_CAP) // 2)  # pairs per call (two results each)
     b = _begin(world, "rec")
     sc = _scratch(world)
     keys = hip_ops.neighbor_slot_keys(world)
@@ -225,8 +233,7 @@ def recombinate_all(world, p: float) -> bool:
     gf, of = _p(b["gflags"]), _p(b["opflags"])
     _m().rec_count_keys(8 * n, _p(keys), _p(arena.lens), float(p), seed, call, _p(k), 0, K_CAP, gf, of, st)
     _m().select_indices_dev(8 * n, _SEL_I32POS, _p(k), 0, _p(sel), 0, _p(b["cnt"]), st)
-    # a selected-pair count above the capacity is flagged (never expected under the usage rule)
-    _m().flag_above(_p(b["cnt"]), pcap, _p(b["opflags"]), _F_CAPACITY, st)
+    _m().cap_skip(_p(b["cnt"]), pcap, gf, of, st)
     out_w = 2 * L  # a recombined genome is at most both parents
     out = sc.get("gp_rout", 2 * pcap * out_w, torch.uint8, dev)
     out_len = sc.get("gp_rout_len", 2 * pcap, torch.int32, dev)

@@ -529,6 +529,22 @@ def test_device_genome_pipeline_arena_overflow_replay(monkeypatch):
     assert torch.equal(x0, x1)
 
 
+def test_device_genome_pipeline_capacity_skip_replays(monkeypatch):
+    """Capacities far below the selected counts: every call turns into a no-op that reconcile
+    replays on the synchronous path -- same result as that path."""
+    from magicsoup_amd.ops import genome_pipeline
+
+    base = _world("cuda", map_size=64, n=800, s=400, seed=7)
+    g0, p0, x0 = _genetics_run(monkeypatch, base, sync=True, steps=3)
+    monkeypatch.setattr(genome_pipeline, "_cap", lambda expected, limit: 2)
+    g1, p1, x1 = _genetics_run(monkeypatch, base, sync=False, steps=3)
+    assert g0 == g1
+    for k in p0:
+        P = min(p0[k].size(1), p1[k].size(1))
+        assert torch.equal(p0[k][:, :P], p1[k][:, :P]), k
+    assert torch.equal(x0, x1)
+
+
 @pytest.mark.parametrize("d_cap", [None, 1])
 def test_device_genome_pipeline_matches_sync_path(monkeypatch, d_cap):
     """Sync-free mutate / recombinate (device counts, speculative token layout, fresh rows) give
