@@ -32,8 +32,8 @@ METRIC = "simulation steps/sec (whole node), 4096×4096 map / 50k cells, 1/2/4/8
 def _args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--map-size", type=int, default=4096)
     ap.add_argument("--cells", type=int, default=50_000)
     ap.add_argument("--genome-size", type=int, default=500)
