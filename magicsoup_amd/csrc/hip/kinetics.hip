@@ -27,8 +27,8 @@ constexpr int kBlock = 256;
 constexpr int kNarrowP = 12;  // LDS protein slots of the narrow integrator launch
 constexpr int kWideBlocksPerCU = 2;  // resident blocks per CU of the strided wide launch
 // binned launch mode (set_integrate_mode, for A/B on one state: scripts/integrator_bench.py):
-// bits 0-1: 0 serial (narrow then wide, full grids), 1 wide on a side stream next to the narrow
-// launch, 2 as 1 with the wide bin on a small strided grid; bit 2: 16-lane groups for the narrow
+// bit 0: the wide launch on a side stream next to the narrow one (else serial, wide first); bit 1:
+// the wide bin on a small strided grid (else a full grid); bit 2: 16-lane groups for the narrow
 // launch. Measured at 4096^2 / 50k (3 parts, 4 iterations): serial 532 us, concurrent 558 us,
 // 16-lane 590 us -- the kernel is VALU-throughput bound (37M wave instructions per launch, ~60 %
 // of the SIMDs' issue capacity), so overlapping the bins only adds contention. Serial is default.
@@ -635,7 +635,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
   // part reads both bins' flags).
   static hipStream_t side = nullptr;
   static hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  const bool conc = nl == 2 && (g_integrate_mode & 3) != 0;
+  const bool conc = nl == 2 && (g_integrate_mode & 1) != 0;
   if (conc && !side) {
     MS_HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
     MS_HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
@@ -657,7 +657,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
       const size_t lds = cps * slot_bytes;
       if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
       const int threads = cps * G;
-      const bool stride = conc && li == 1 && (g_integrate_mode & 3) == 2;
+      const bool stride = nl == 2 && li == 1 && (g_integrate_mode & 2) != 0;
       unsigned grid = cdiv(c, cps);
       if (stride) {  // the wide bin: at most kWideBlocksPerCU resident blocks per CU, striding
         const long long per_cu = std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)lds));

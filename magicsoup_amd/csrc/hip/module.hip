@@ -106,7 +106,6 @@ void zero_rows(int cap, uintptr_t dn, long long row, uintptr_t buf, uintptr_t st
 void assign_rows(int ncap, uintptr_t dn, uintptr_t cells, uintptr_t slot, uintptr_t d_rows, long long row_cap,
                  uintptr_t rows_out, uintptr_t flags, uintptr_t stream);
 void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t dst, uintptr_t stream);
-void flag_above(uintptr_t dn, int cap, uintptr_t flags, int bit, uintptr_t stream);
 int count_to_host(uintptr_t dcount, uintptr_t stream);
 void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
 int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t cnt, uintptr_t stream);
@@ -177,7 +176,6 @@ PYBIND11_MODULE(_hip, m) {
   m.def("zero_rows", &msd::zero_rows);
   m.def("assign_rows", &msd::assign_rows);
   m.def("gather_dev", &msd::gather_dev);
-  m.def("flag_above", &msd::flag_above);
   m.def("cap_skip", &msd::cap_skip, "pipeline capacity guard: count > cap -> no-op call replayed by the host");
   m.def("count_to_host", &msd::count_to_host, "device {count, max} -> pinned ring slot (returns the slot)");
   m.def("status_write", &msd::status_write, "pipeline status -> pinned ring slot (returns the slot)");

@@ -281,16 +281,6 @@ void assign_rows(int ncap, uintptr_t dn, uintptr_t cells, uintptr_t slot, uintpt
   MS_LAUNCH_CHECK();
 }
 
-// flags |= bit if *dn > cap
-__global__ void flag_above_kernel(const int* dn, int cap, int* flags, int bit) {
-  if (*dn > cap) atomicOr(flags, bit);
-}
-
-void flag_above(uintptr_t dn, int cap, uintptr_t flags, int bit, uintptr_t stream) {
-  flag_above_kernel<<<1, 1, 0, S_(stream)>>>(P_<int>(dn), cap, P_<int>(flags), bit);
-  MS_LAUNCH_CHECK();
-}
-
 // Capacity guard of a device-pipeline call: a selected count above the buffers' capacity turns the
 // call into a no-op (count 0) that the host replays on the synchronous path (opflags |= skipped)
 // and breaks the pending chain (gflags |= the arena-width bit), so later calls replay too.
