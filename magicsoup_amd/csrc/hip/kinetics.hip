@@ -266,7 +266,9 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
 
   // ---- 8. equilibrium damping trajectory
   float inc = 0.5f;
+  const int gbase8 = (threadIdx.x & 63) - lane;  // first lane of this group inside the wave
   for (int it = 0; it < a.n_iters; ++it, inc *= 0.5f) {
+    bool changed = false;
     for (int k = lane; k < na; k += G) {
       const int* wr = words + k * SP;
       const uint8_t* nz = nzj + k * s;
@@ -302,9 +304,28 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
       float f = f0;
       if (high) f -= inc;
       if (low) f += inc;
-      F[k] = f > 1.0f ? 1.0f : (f < 0.0f ? 0.0f : f);
+      f = f > 1.0f ? 1.0f : (f < 0.0f ? 0.0f : f);
+      changed |= f != f0;
+      F[k] = f;
     }
     wave_lds_sync();
+    {
+      // per-cell fixed point: with no factor changed, this and every later iteration reproduce the
+      // current state bit for bit (same F, same X, same decisions), so the remaining candidates are
+      // copies of it and the iterations are skipped
+      const unsigned long long bal = __ballot(changed);
+      unsigned long long gm;
+      if constexpr (G == 64) gm = bal;
+      else gm = (bal >> gbase8) & ((1ull << G) - 1ull);
+      if (gm == 0ull) {
+        for (int it2 = it + 1; it2 <= a.n_iters; ++it2) {
+          float* sn2 = snap + (size_t)it2 * s;
+          for (int j = lane; j < s; j += G)
+            if (valid) sn2[j] = Xc[j];
+        }
+        break;
+      }
+    }
     float* sn = snap + (size_t)(it + 1) * s;
     for (int j = lane; j < s; j += G) {
       float x = X0[j];
