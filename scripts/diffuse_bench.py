@@ -35,7 +35,7 @@ def main():
         nbytes = w.molecule_map.numel() * w.molecule_map.element_size()
         # stencil reads + writes the map once, the correction pass once more
         out[name] = {"ms": round(ms_it, 4), "map_MB": round(nbytes / 1e6, 1),
-                     "eff_TBps": round(4 * nbytes / (ms_it * 1e-3) / 1e12, 3)}
+                     "eff_TBps": round(2 * nbytes / (ms_it * 1e-3) / 1e12, 3)}
         del w
         torch.cuda.empty_cache()
     print(json.dumps({"size": a.size, "n_mol": len(CHEMISTRY.molecules), "diffuse": out}))
