@@ -374,6 +374,346 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Register-resident integrator (the default for s <= 64): G lanes own one cell and every lane plays
+// two roles -- lane j is signal j (X0_j, the current X_j and the column n_{0..na-1, j} of the
+// stoichiometry, packed int8 in registers) and lane k is active protein k (velocity, damping factor,
+// Ke / direction flags and its first kNzReg non-zero signals in registers). The roles exchange
+// values through two small LDS arrays: protein lanes publish one float each (read back by the
+// signal lanes as 16-byte broadcasts, four proteins per load) and signal lanes publish X_j (gathered
+// by the protein lanes, all loads independent). Entries past a protein's non-zero count are zero
+// words, which leave every product unchanged, so the protein loops run branch-free to the wave's
+// largest count. Every sum and product runs in the same order as integrate_item (ascending protein
+// / ascending signal), so both paths give bit-identical results (scripts/integrator_bench.py). A
+// cell with more than G active proteins is appended (part 0) to the wide list and integrated by
+// integrate_item with all P protein slots.
+constexpr int kNzReg = 16;  // non-zero signals per protein in the LDS lists (more: the cell goes wide)
+
+// LDS words per cell slot of the register-resident integrator
+template <int G>
+constexpr int fast_slot_words() {
+  return G * kNzReg /*entry words*/ + G * kNzReg / 4 /*entry signal indices*/ + 4 * G /*cnt, act, X, pub*/;
+}
+
+template <int G>
+__device__ __forceinline__ unsigned long long group_ballot(bool b) {
+  const unsigned long long bal = __ballot(b);
+  if constexpr (G == 64) return bal;
+  else return (threadIdx.x & 32) ? (bal >> 32) : (bal & 0xFFFFFFFFull);
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+
+// ms::ipow for |n| < 8 without branches: the same multiplications in the same order
+__device__ __forceinline__ float ipow_small(float x, int n) {
+  const int e = n < 0 ? -n : n;
+  float r = 1.0f, b = x;
+  r = (e & 1) ? r * b : r;
+  b = b * b;
+  r = (e & 2) ? r * b : r;
+  b = b * b;
+  r = (e & 4) ? r * b : r;
+  return n < 0 ? 1.0f / r : r;
+}
+
+template <int G>
+__device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int* smem, int item, unsigned& bits,
+                                                    int32_t* wide_list, int32_t* wide_count) {
+  const int slot = threadIdx.x / G, lane = threadIdx.x % G;
+  const bool listed = a.list ? item < *a.count : item < a.c;
+  const int cell = listed ? (a.list ? a.list[item] : item) : 0;
+  const int P = a.P, s = a.s;
+  const size_t prow = listed ? (a.prow ? (size_t)a.prow[cell] : (size_t)cell) : 0;
+
+  int* ents = smem + slot * fast_slot_words<G>();                // (G, kNzReg) words of the non-zeros
+  uint8_t* jl = reinterpret_cast<uint8_t*>(ents + G * kNzReg);   // (G, kNzReg) their signal indices
+  int* cnts = ents + G * kNzReg + G * kNzReg / 4;                // (G,) non-zero signals per protein
+  int* act = cnts + G;                                           // (G,) protein slot of active protein k
+  float* Xs = reinterpret_cast<float*>(act + G);                 // (G,) signal -> protein: X_j / factor
+  float* pub = Xs + G;                                           // (G,) protein -> signal: V_k / Va_k * F_k
+
+  // ---- 1. X0 of this lane's signal (independent of the compaction, issued first)
+  float x0 = 0.0f;
+  if (listed && lane < s) {
+    const int k = stop_iter(a.mask_prev, a.n_iters_prev);
+    x0 = a.snap_prev[((size_t)cell * ms::kSnap + k) * s + lane];
+  }
+
+  // ---- 2. active proteins (Vmax' != 0, NaN included) in ascending order
+  int na = 0;
+  for (int p0 = 0; p0 < P; p0 += G) {
+    const int p = p0 + lane;
+    float vmax = 0.0f;
+    if (listed && p < P) vmax = a.Q[prow * P + p].x;
+    const float vm = vmax * a.trim;
+    const bool on = listed && p < P && !(vm <= 0.0f);
+    const unsigned long long gm = group_ballot<G>(on);
+    const int k = na + __popcll(gm & ((1ull << lane) - 1ull));
+    if (on && k < G) act[k] = p;
+    na += __popcll(gm);
+  }
+  bool fits = na <= G;
+  wave_lds_sync();
+  const int nac = fits ? na : 0;
+  const int na_w = wave_max(nac);  // wave-uniform bound of the protein loops (both groups of a wave)
+  const bool sigl = listed && lane < s;
+
+  // ---- 3. this signal's stoichiometry column (int8 n per protein, packed in registers) and the
+  //         per-protein non-zero lists (one ballot per protein), 8 rows of loads in flight
+  int npk[G / 4];
+#pragma unroll
+  for (int i = 0; i < G / 4; ++i) npk[i] = 0;
+  bool wide_ok = true;  // every protein has <= kNzReg non-zeros and exponents < 32
+#pragma unroll
+  for (int k0 = 0; k0 < G; k0 += 8) {
+    if (k0 >= na_w) break;
+    int w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + u;
+      w[u] = (k < nac && sigl) ? a.W[(prow * P + act[k]) * s + lane] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + u;
+      npk[k >> 2] |= (w[u] & 0xFF) << (8 * (k & 3));
+      const bool on = w[u] != 0;
+      const unsigned long long gm = group_ballot<G>(on);
+      const int r = __popcll(gm & ((1ull << lane) - 1ull));
+      if (on && r < kNzReg) {
+        ents[k * kNzReg + r] = w[u];
+        jl[k * kNzReg + r] = (uint8_t)lane;
+      }
+      if (lane == 0 && k < nac) cnts[k] = __popcll(gm);
+      wide_ok &= __popcll(gm) <= kNzReg && w_nf(w[u]) < 32 && w_nb(w[u]) < 32;
+    }
+  }
+  fits = fits && group_ballot<G>(!wide_ok) == 0ull;
+  if (listed && !fits && lane == 0 && wide_list) wide_list[atomicAdd(wide_count, 1)] = cell;
+  const bool valid = listed && fits;
+  const bool sig = valid && lane < s;
+  const bool prot = valid && lane < na;
+  Xs[lane] = x0;
+  wave_lds_sync();
+
+  // protein lane: constants, and its non-zeros as 16-bit (signal, nf, nb) registers for the
+  // damping iterations (velocity and limiting factor read the full words from LDS once per part)
+  float vmx = 0.0f, kmf = 1.0f, kmb = 1.0f, ke = 1.0f;
+  int pk = 0, cnt = 0;
+  int e16[kNzReg / 2];
+#pragma unroll
+  for (int q = 0; q < kNzReg / 2; ++q) e16[q] = 0;
+  bool small = true;  // all exponents < 8: branch-free powers
+  if (prot) {
+    pk = act[lane];
+    const float4 q4 = a.Q[prow * P + pk];
+    const float vm = q4.x * a.trim;
+    vmx = vm > 0.0f || vm != vm ? vm : 0.0f;
+    kmf = q4.y;
+    kmb = q4.z;
+    ke = q4.w;
+    cnt = cnts[lane];
+    const int* jw = reinterpret_cast<const int*>(jl + lane * kNzReg);
+#pragma unroll
+    for (int q = 0; q < kNzReg; ++q) {
+      if (q < cnt) {
+        const int w = ents[lane * kNzReg + q];
+        const int j = (jw[q >> 2] >> (8 * (q & 3))) & 0xFF;
+        const int e = j | (w_nf(w) << 6) | (w_nb(w) << 11);
+        e16[q >> 1] |= e << (16 * (q & 1));
+        small &= w_nf(w) < 8 && w_nb(w) < 8 && w_a(w) < 8 && w_a(w) > -8;
+      }
+    }
+  }
+  const int cnt_w = wave_max(cnt);
+  const bool small_w = __ballot(!small) == 0ull;
+#define MS_E(q) ((e16[(q) >> 1] >> (16 * ((q) & 1))) & 0xFFFF)
+  auto pw = [&](float x, int n) { return small_w ? ipow_small(x, n) : ms::ipow(x, n); };
+
+  // signal lane: sum over proteins k (ascending) of op(n_kj, pub[k]); four proteins per LDS load
+  auto signal_pass = [&](auto&& op) {
+#pragma unroll
+    for (int k0 = 0; k0 < G; k0 += 4) {
+      if (k0 >= na_w) break;
+      const float4 b4 = *reinterpret_cast<const float4*>(pub + k0);
+      const float bv[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u;
+        op((int)(int8_t)(npk[k >> 2] >> (8 * (k & 3))), bv[u]);
+      }
+    }
+  };
+
+  // ---- 4. velocity (protein lane; entries past the count are zero words: no effect)
+  float v = 0.0f;
+  {
+    const float* kmr = a.Kmr + (prow * P + pk) * s;
+    float xf = 1.0f, xb = 1.0f, ar = 1.0f;
+    int nfs = 0, nbs = 0;
+#pragma unroll
+    for (int q = 0; q < kNzReg; ++q) {
+      if (q >= cnt_w) break;
+      const int w = q < cnt ? ents[lane * kNzReg + q] : 0;
+      const int j = MS_E(q) & 63;
+      const int nf = w_nf(w), nb = w_nb(w), av = w_a(w);
+      const float x = Xs[j];
+      nfs |= nf;
+      nbs |= nb;
+      xf = nf > 0 ? xf * pw(x, nf) : xf;
+      xb = nb > 0 ? xb * pw(x, nb) : xb;
+      if (av != 0) {
+        float r = pw(x, av);
+        r = r / (r + kmr[j]);
+        if (ms::f_isnan(r)) r = 1.0f;
+        ar *= r;
+      }
+    }
+    if (prot) {
+      float kf = ms::clean_prod(xf) / kmf;
+      if (nfs == 0) kf = 0.0f;
+      if (ms::f_isinf(kf)) kf = ms::kMax;
+      float kb = ms::clean_prod(xb) / kmb;
+      if (nbs == 0) kb = 0.0f;
+      if (ms::f_isinf(kb)) kb = ms::kMax;
+      if (ms::f_isinf(ar)) ar = ms::kMax;
+      const float acat = (kf - kb) / (1.0f + kf + kb);
+      v = acat * vmx * ar;
+      v = v < ms::kMin ? ms::kMin : (v > ms::kMax ? ms::kMax : v);
+    }
+  }
+  pub[lane] = v;
+  wave_lds_sync();
+
+  // ---- 5. consumption per signal -> negative-concentration factor (signal lane)
+  {
+    float cons = 0.0f;
+    signal_pass([&](int n, float vk) {
+      const float nv = (float)n * vk;
+      if (nv < 0.0f) cons += -nv;
+    });
+    const float f = x0 / cons;
+    Xs[lane] = f > 1.0f ? 1.0f : f;  // Xs holds the factors until candidate 0 exists
+  }
+  wave_lds_sync();
+
+  // ---- 6. per-protein limiting factor (protein lane)
+  float va = 0.0f, F = 1.0f;
+  int flg = 0;
+  {
+    float fmin = 1.0f;
+    bool nan = false;
+#pragma unroll
+    for (int q = 0; q < kNzReg; ++q) {
+      if (q >= cnt_w) break;
+      const int w = q < cnt ? ents[lane * kNzReg + q] : 0;
+      if ((float)w_n(w) * v < 0.0f) {
+        const float f = Xs[MS_E(q) & 63];
+        if (ms::f_isnan(f)) nan = true;
+        else if (f < fmin) fmin = f;
+      }
+    }
+    if (prot) {
+      va = v * (nan ? NAN : fmin);
+      flg = (v > 0.0f ? 1 : 0) | (fabsf(v) > 0.1f ? 2 : 0);
+    }
+  }
+  pub[lane] = va;
+  wave_lds_sync();
+
+  // ---- 7. candidate 0 (signal lane)
+  float* snap = a.snap_out + (size_t)(valid ? cell : 0) * ms::kSnap * s;
+  auto advance = [&]() -> float {  // X0 + sum_k n_k * pub_k (ascending k), clamped at 0
+    float x = x0;
+    signal_pass([&](int n, float b) {
+      if (n != 0) x += (float)n * b;
+    });
+    return x < 0.0f ? 0.0f : x;
+  };
+  float xc = advance();
+  if (sig) snap[lane] = xc;
+  Xs[lane] = xc;
+  wave_lds_sync();
+
+  // ---- 8. equilibrium damping trajectory
+  float inc = 0.5f;
+  for (int it = 0; it < a.n_iters; ++it, inc *= 0.5f) {
+    bool changed = false;
+    {
+      float pf = 1.0f, pb = 1.0f;
+      int nfs = 0, nbs = 0;
+#pragma unroll
+      for (int q = 0; q < kNzReg; ++q) {
+        if (q >= cnt_w) break;
+        const int e = MS_E(q);
+        const int nf = (e >> 6) & 31, nb = e >> 11;
+        const float x = Xs[e & 63];
+        nfs |= nf;
+        nbs |= nb;
+        pf = nf > 0 ? pf * pw(x, nf) : pf;
+        pb = nb > 0 ? pb * pw(x, nb) : pb;
+      }
+      if (prot) {
+        pf = nfs ? ms::clean_prod(pf) : 0.0f;
+        pb = nbs ? ms::clean_prod(pb) : 0.0f;
+        float Q = pb / pf;
+        if (ms::f_isnan(Q)) Q = 1.0f;
+        else Q = Q < ms::kEps ? ms::kEps : (Q > ms::kMax ? ms::kMax : Q);
+        const float qke = Q / ke;
+        const bool fwd = flg & 1, imp = flg & 2;
+        const float f0 = F;
+        bool low = fwd ? (qke < ms::kLower) : (qke > ms::kUpper);
+        if (fwd && f0 == 1.0f) low = false;
+        bool high = fwd ? (qke > ms::kUpper) : (qke < ms::kLower);
+        if (!fwd && f0 == 0.0f) high = false;
+        if ((low || high) && imp) bits |= 1u << it;
+        float f = f0;
+        if (high) f -= inc;
+        if (low) f += inc;
+        f = f > 1.0f ? 1.0f : (f < 0.0f ? 0.0f : f);
+        changed = f != f0;
+        F = f;
+      }
+    }
+    if (group_ballot<G>(changed) == 0ull) {
+      // per-cell fixed point (see integrate_item): the remaining candidates are copies
+      for (int it2 = it + 1; it2 <= a.n_iters; ++it2)
+        if (sig) snap[(size_t)it2 * s + lane] = xc;
+      break;
+    }
+    pub[lane] = va * F;
+    wave_lds_sync();  // the protein lanes of this wave finished reading Xs, published Va * F
+    xc = advance();
+    if (sig) snap[(size_t)(it + 1) * s + lane] = xc;
+    Xs[lane] = xc;
+    wave_lds_sync();
+  }
+#undef MS_E
+}
+
+template <int G>
+__global__ void __launch_bounds__(kBlock) integrate_fast_kernel(IntegrateArgs a, int32_t* wide_list,
+                                                                int32_t* wide_count) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  unsigned bits = 0u;
+  integrate_item_fast<G>(a, smem, (int)blockIdx.x * (blockDim.x / G) + (int)threadIdx.x / G, bits, wide_list,
+                         wide_count);
+  __shared__ unsigned wave_bits[kBlock / 64];
+  for (int o = 32; o > 0; o >>= 1) bits |= __shfl_xor(bits, o);
+  if ((threadIdx.x & 63) == 0) wave_bits[threadIdx.x >> 6] = bits;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned b = 0u;
+    for (int w = 0; w < (int)(blockDim.x + 63) / 64; ++w) b |= wave_bits[w];
+    for (int it = 0; it < ms::kEqIters; ++it)
+      if ((b & (1u << it)) && __hip_atomic_load(a.mask_out + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+        atomicOr(a.mask_out + it, 1u);
+  }
+}
+
 // Split the cells by their number of active proteins (Vmax > 0 or NaN; the same set for every part
 // since all trims are positive): cells with at most `pn` go to the narrow list (small LDS slots,
 // high occupancy), the others to the wide list (slots for all P proteins). List order does not
@@ -622,103 +962,137 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     }
     MS_LAUNCH_CHECK();
   }
-  const int G_wide = s <= 32 ? 32 : 64;
-  // narrow launch: 16-lane groups (4 cells per wave) halve the idle lanes of the protein phases
-  // (<= kNarrowP proteins); signal phases take s / 16 passes instead
-  const int G_narrow = (g_integrate_mode & 4) ? 16 : G_wide;
   const int sp = (s % 2 == 0) ? s + 1 : s;
-  // narrow / wide binning (only worth it when P is well above the typical active count)
-  const bool binned = lists != 0 && P > kNarrowP;
-  int32_t* lst = P_<int32_t>(lists);
-  int32_t* cnt = lst ? lst + 2 * (size_t)c : nullptr;
-  if (binned && part_begin == 0) {
-    MS_HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), st));
-    bin_cells_kernel<<<cdiv(c, 256), 256, 0, st>>>(c, P, kNarrowP, P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr,
-                                                   lst, cnt);
-    MS_LAUNCH_CHECK();
-  }
-  struct Launch {
-    int Ps;
-    const int32_t* list;
-    const int32_t* count;
+  auto part_args = [&](int part) {
+    IntegrateArgs a{};
+    a.c = c; a.P = P; a.s = s;
+    a.W = P_<int32_t>(W); a.Q = P_<float4>(Q); a.Kmr = P_<float>(Kmr);
+    a.snap_prev = part == 0 ? snaps[1] : snaps[(part - 1) & 1];
+    a.mask_prev = part == 0 ? zero_flags : mk + ms::kEqIters * (part - 1);
+    a.n_iters_prev = n_iters;
+    a.snap_out = snaps[part & 1];
+    a.mask_out = mk + ms::kEqIters * part;
+    a.trim = trims[part];
+    a.n_iters = n_iters;
+    a.sp = sp;
+    a.prow = prow ? P_<int64_t>(prow) : nullptr;
+    return a;
   };
-  Launch launches[2];
-  int nl = 0;
-  if (binned) {
-    launches[nl++] = Launch{kNarrowP, lst, cnt};
-    launches[nl++] = Launch{P, lst + c, cnt + 1};
-  } else {
-    launches[nl++] = Launch{P, nullptr, nullptr};
-  }
-  // Binned parts run the wide launch on a side stream concurrently with the narrow one: the wide
-  // bin is small but its large proteomes are long per-cell dependency chains, which then overlap
-  // with the narrow bin's throughput work instead of adding to it (fork / join per part; the next
-  // part reads both bins' flags).
-  static hipStream_t side = nullptr;
-  static hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  const bool conc = nl == 2 && (g_integrate_mode & 1) != 0;
-  if (conc && !side) {
-    MS_HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-    MS_HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
-    MS_HIP_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-  }
-  for (int part = part_begin; part < part_end; ++part) {
-    if (conc) {
-      MS_HIP_CHECK(hipEventRecord(ev_fork, st));
-      MS_HIP_CHECK(hipStreamWaitEvent(side, ev_fork, 0));
-    }
-    for (int li = nl - 1; li >= 0; --li) {  // wide first: its long chains start early
-      const Launch& L = launches[li];
-      const int G = (nl == 2 && li == 0) ? G_narrow : G_wide;
-      hipStream_t ls = (conc && li == 1) ? side : st;
-      const int slot_words = slot_words_for(L.Ps, s, sp);
-      const size_t slot_bytes = (size_t)slot_words * 4;
-      int cps = kBlock / G;
-      while (cps > 1 && cps * slot_bytes > 64 * 1024) --cps;
-      const size_t lds = cps * slot_bytes;
-      if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
-      const int threads = cps * G;
-      const bool stride = nl == 2 && li == 1 && (g_integrate_mode & 2) != 0;
-      unsigned grid = cdiv(c, cps);
-      if (stride) {  // the wide bin: at most kWideBlocksPerCU resident blocks per CU, striding
-        const long long per_cu = std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)lds));
-        grid = (unsigned)std::min<long long>(grid, 256 * per_cu);
-      }
-      IntegrateArgs a{};
-      a.c = c; a.P = P; a.s = s;
-      a.W = P_<int32_t>(W); a.Q = P_<float4>(Q); a.Kmr = P_<float>(Kmr);
-      if (part == 0) {
-        a.snap_prev = snaps[1];
-        a.mask_prev = zero_flags;
-      } else {
-        a.snap_prev = snaps[(part - 1) & 1];
-        a.mask_prev = mk + ms::kEqIters * (part - 1);
-      }
-      a.n_iters_prev = n_iters;
-      a.snap_out = snaps[part & 1];
-      a.mask_out = mk + ms::kEqIters * part;
-      a.trim = trims[part];
-      a.n_iters = n_iters;
+  // register-resident path (default for s <= 64, integrate_item_fast): one launch per part over
+  // every cell with at most G active proteins; part 0 lists the others, which a strided launch with
+  // LDS slots for all P proteins (integrate_item) integrates after it
+  if (lists != 0 && s <= 64 && (g_integrate_mode & 8) == 0) {
+    int32_t* wl = P_<int32_t>(lists) + c;
+    int32_t* wc = P_<int32_t>(lists) + 2 * (size_t)c + 1;
+    if (part_begin == 0) MS_HIP_CHECK(hipMemsetAsync(wc, 0, sizeof(int32_t), st));
+    const int G = s <= 32 ? 32 : 64;
+    const int cps = kBlock / G;
+    const size_t lds_fast = (size_t)cps * (G == 32 ? fast_slot_words<32>() : fast_slot_words<64>()) * 4;
+    const int slot_words = slot_words_for(P, s, sp);
+    const size_t slot_bytes = (size_t)slot_words * 4;
+    int cpsw = kBlock / G;
+    while (cpsw > 1 && cpsw * slot_bytes > 64 * 1024) --cpsw;
+    const size_t ldsw = cpsw * slot_bytes;
+    if (ldsw > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
+    const long long per_cu = std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)ldsw));
+    const unsigned gridw = (unsigned)std::min<long long>(cdiv(c, cpsw), 256 * per_cu);
+    for (int part = part_begin; part < part_end; ++part) {
+      IntegrateArgs a = part_args(part);
+      a.Ps = G;
+      if (G == 32) integrate_fast_kernel<32><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
+      else integrate_fast_kernel<64><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
+      MS_LAUNCH_CHECK();
+      a.list = wl;
+      a.count = wc;
+      a.Ps = P;
       a.slot_words = slot_words;
-      a.sp = sp;
-      a.prow = prow ? P_<int64_t>(prow) : nullptr;
-      a.list = L.list;
-      a.count = L.count;
-      a.Ps = L.Ps;
-      if (G == 16) {
-        integrate_part_kernel<16, false><<<grid, threads, lds, ls>>>(a);
-      } else if (G == 32) {
-        if (stride) integrate_part_kernel<32, true><<<grid, threads, lds, ls>>>(a);
-        else integrate_part_kernel<32, false><<<grid, threads, lds, ls>>>(a);
-      } else {
-        if (stride) integrate_part_kernel<64, true><<<grid, threads, lds, ls>>>(a);
-        else integrate_part_kernel<64, false><<<grid, threads, lds, ls>>>(a);
-      }
+      if (G == 32) integrate_part_kernel<32, true><<<gridw, cpsw * G, ldsw, st>>>(a);
+      else integrate_part_kernel<64, true><<<gridw, cpsw * G, ldsw, st>>>(a);
       MS_LAUNCH_CHECK();
     }
-    if (conc) {
-      MS_HIP_CHECK(hipEventRecord(ev_join, side));
-      MS_HIP_CHECK(hipStreamWaitEvent(st, ev_join, 0));
+  } else {
+    // legacy LDS-staged launches (s > 64, or mode bit 3 for A/B): narrow / wide binning (only worth
+    // it when P is well above the typical active count)
+    const int G_wide = s <= 32 ? 32 : 64;
+    // narrow launch: 16-lane groups (4 cells per wave) halve the idle lanes of the protein phases
+    // (<= kNarrowP proteins); signal phases take s / 16 passes instead
+    const int G_narrow = (g_integrate_mode & 4) ? 16 : G_wide;
+    const bool binned = lists != 0 && P > kNarrowP;
+    int32_t* lst = P_<int32_t>(lists);
+    int32_t* cnt = lst ? lst + 2 * (size_t)c : nullptr;
+    if (binned && part_begin == 0) {
+      MS_HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), st));
+      bin_cells_kernel<<<cdiv(c, 256), 256, 0, st>>>(c, P, kNarrowP, P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr,
+                                                     lst, cnt);
+      MS_LAUNCH_CHECK();
+    }
+    struct Launch {
+      int Ps;
+      const int32_t* list;
+      const int32_t* count;
+    };
+    Launch launches[2];
+    int nl = 0;
+    if (binned) {
+      launches[nl++] = Launch{kNarrowP, lst, cnt};
+      launches[nl++] = Launch{P, lst + c, cnt + 1};
+    } else {
+      launches[nl++] = Launch{P, nullptr, nullptr};
+    }
+    // Binned parts run the wide launch on a side stream concurrently with the narrow one: the wide
+    // bin is small but its large proteomes are long per-cell dependency chains, which then overlap
+    // with the narrow bin's throughput work instead of adding to it (fork / join per part; the next
+    // part reads both bins' flags).
+    static hipStream_t side = nullptr;
+    static hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    const bool conc = nl == 2 && (g_integrate_mode & 1) != 0;
+    if (conc && !side) {
+      MS_HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+      MS_HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+      MS_HIP_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+    }
+    for (int part = part_begin; part < part_end; ++part) {
+      if (conc) {
+        MS_HIP_CHECK(hipEventRecord(ev_fork, st));
+        MS_HIP_CHECK(hipStreamWaitEvent(side, ev_fork, 0));
+      }
+      for (int li = nl - 1; li >= 0; --li) {  // wide first: its long chains start early
+        const Launch& L = launches[li];
+        const int G = (nl == 2 && li == 0) ? G_narrow : G_wide;
+        hipStream_t ls = (conc && li == 1) ? side : st;
+        const int slot_words = slot_words_for(L.Ps, s, sp);
+        const size_t slot_bytes = (size_t)slot_words * 4;
+        int cps = kBlock / G;
+        while (cps > 1 && cps * slot_bytes > 64 * 1024) --cps;
+        const size_t lds = cps * slot_bytes;
+        if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
+        const int threads = cps * G;
+        const bool stride = nl == 2 && li == 1 && (g_integrate_mode & 2) != 0;
+        unsigned grid = cdiv(c, cps);
+        if (stride) {  // the wide bin: at most kWideBlocksPerCU resident blocks per CU, striding
+          const long long per_cu = std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)lds));
+          grid = (unsigned)std::min<long long>(grid, 256 * per_cu);
+        }
+        IntegrateArgs a = part_args(part);
+        a.slot_words = slot_words;
+        a.list = L.list;
+        a.count = L.count;
+        a.Ps = L.Ps;
+        if (G == 16) {
+          integrate_part_kernel<16, false><<<grid, threads, lds, ls>>>(a);
+        } else if (G == 32) {
+          if (stride) integrate_part_kernel<32, true><<<grid, threads, lds, ls>>>(a);
+          else integrate_part_kernel<32, false><<<grid, threads, lds, ls>>>(a);
+        } else {
+          if (stride) integrate_part_kernel<64, true><<<grid, threads, lds, ls>>>(a);
+          else integrate_part_kernel<64, false><<<grid, threads, lds, ls>>>(a);
+        }
+        MS_LAUNCH_CHECK();
+      }
+      if (conc) {
+        MS_HIP_CHECK(hipEventRecord(ev_join, side));
+        MS_HIP_CHECK(hipStreamWaitEvent(st, ev_join, 0));
+      }
     }
   }
   // the write-back selects the last part's snapshot by its (possibly all-reduced) flags, so a

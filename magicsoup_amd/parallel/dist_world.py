@@ -351,6 +351,20 @@ class DistributedWorld(World):
         acc_dn = f_dn.bool() if k_dn else torch.zeros(0, dtype=torch.bool, device=dev)
         return acc_up, acc_dn, got
 
+    # ------------------------------------------------------------------ physics overrides
+    def enzymatic_activity(self):
+        """Integration (collective with ``exact_global_exit``). A rank whose strip holds no cells
+        still takes part in the per-part MAX all-reduces of the iteration flags (with all-zero
+        flags), so the ranks that do have cells see the same number of collectives."""
+        hook = self.__dict__.get("_allreduce_flags")
+        if self.n_cells == 0 and hook is not None:
+            from magicsoup_amd.models.kinetics import _INCREMENTS, _TRIMS
+
+            for _ in _TRIMS:
+                hook(torch.zeros(len(_INCREMENTS), dtype=torch.int32, device=self._tensor_device()))
+            return
+        super().enzymatic_activity()
+
     # ------------------------------------------------------------------ lifecycle overrides
     def divide_cells_t(self, cell_idxs) -> tuple[torch.Tensor, torch.Tensor]:
         """Division (collective). Children landing in a neighbour's boundary row are created on

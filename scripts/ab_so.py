@@ -2,7 +2,7 @@
 built with the in-tree module, then an integrate (3 parts, 4 iterations) on the same explicit X is
 timed alternately with module A and module B, and their results are compared bit for bit.
 
-usage: python scripts/ab_so.py A.so B.so"""
+usage: python scripts/ab_so.py [--size S] [--cells C] A.so B.so [C.so ...]"""
 import importlib.machinery
 import importlib.util
 import json
@@ -39,18 +39,27 @@ def timed(fn, iters=20):
 
 
 def main():
-    mods = {"A": load(sys.argv[1], "a"), "B": load(sys.argv[2], "b")}
+    args = sys.argv[1:]
+    size, cells = 4096, 50000
+    while args and args[0].startswith("--"):
+        flag, val = args[0], int(args[1])
+        args = args[2:]
+        if flag == "--size":
+            size = val
+        else:
+            cells = val
+    mods = {chr(65 + i): load(p, f"v{i}") for i, p in enumerate(args)}
     chem = bench._chemistry("wl")
     atp = chem.molname_2_idx["ATP"]
-    w = ms.World(chemistry=chem, map_size=4096, device="cuda", seed=0)
-    w.spawn_cells(bench.random_genomes(50000, 500, "cuda"))
+    w = ms.World(chemistry=chem, map_size=size, device="cuda", seed=0)
+    w.spawn_cells(bench.random_genomes(cells, 500, "cuda"))
     for _ in range(5):
-        bench.step(w, 50000, 500, atp)
+        bench.step(w, cells, 500, atp)
     kin = w.kinetics
     pos = w.cell_positions.long()
     X = torch.cat([w.cell_molecules, w.molecule_map[:, pos[:, 0], pos[:, 1]].T], dim=1).contiguous()
     kin._packed_params()
-    out, res = {"P": int(kin._P())}, {}
+    out, res = {"P": int(kin._P()), "cells": w.n_cells}, {}
     orig = native._mods.get("_hip")
     try:
         for rep in range(3):
@@ -61,7 +70,7 @@ def main():
                 Xk = X.clone()
                 kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4)
                 res[tag] = Xk
-        out["equal"] = bool(torch.equal(res["A"], res["B"]))
+        out["equal"] = {t: bool(torch.equal(res["A"], r)) for t, r in res.items()}
     finally:
         native._mods["_hip"] = orig
     print(json.dumps(out))

@@ -292,3 +292,34 @@ def _body_local_exit(rank, ws):
 
 def test_per_rank_integrator_exit_option():
     run_ranks(_body_local_exit, 2)
+
+
+def _body_empty_rank(rank, ws):
+    # every cell sits in rank 0's strip: rank 1 has none but must still join the integrator's
+    # per-part flag all-reduces (exact global exit), or rank 0 would wait for it forever
+    g = _global_world(map_size=16, n=0)
+    ref = _global_world(map_size=16, n=0)
+    from tests.conftest import gen_genomes
+
+    genomes = gen_genomes(20, 300)
+    pos = torch.tensor([[i // 8, 2 * (i % 8)] for i in range(20)], dtype=torch.int32)
+    for w in (g, ref):
+        w._grow(20)
+        w._genomes.append_strings(genomes)
+        w._labels.append_strings([f"c{i}" for i in range(20)])
+        w._place(torch.arange(20), pos)
+        w._update_params_rows(torch.arange(20))
+    ref.kinetics = g.kinetics
+    dw = _dworld(16)
+    dw.scatter_from(g)
+    assert dw.n_cells == (20 if rank == 0 else 0)
+    for _ in range(3):
+        ref.enzymatic_activity()
+        dw.enzymatic_activity()
+    full = dw.gather()
+    if rank == 0:
+        assert torch.allclose(full.cell_molecules, ref.cell_molecules, rtol=1e-5, atol=1e-5)
+
+
+def test_distributed_rank_without_cells_joins_integrator_collectives():
+    run_ranks(_body_empty_rank, 2, timeout=120.0)

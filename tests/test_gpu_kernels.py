@@ -560,3 +560,52 @@ def test_device_genome_pipeline_matches_sync_path(monkeypatch, d_cap):
         if p1[k].size(1) > P:
             assert not p1[k][:, P:].any(), k
     assert torch.equal(x0, x1)
+
+
+def _integrate_modes(kin, X, modes=(0, 8)):
+    from magicsoup_amd.ops import kinetics_ops
+
+    out = {}
+    try:
+        for mode in modes:
+            native.hip().set_integrate_mode(mode)
+            Xk = X.clone()
+            kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4)
+            out[mode] = Xk
+    finally:
+        native.hip().set_integrate_mode(0)
+    return out
+
+
+@pytest.mark.parametrize("case", ["wl500", "wl3000", "syn20", "syn40", "big_exponents"])
+def test_register_integrator_matches_lds_integrator_bit_for_bit(case):
+    """The register-resident launches (mode 0: cells with <= 32 / 64 active proteins and <= 16
+    non-zero signals per protein; the rest through the wide LDS launch) against the legacy
+    LDS-staged launches (mode 8) on the same state: identical results, bit for bit."""
+    if case.startswith("syn"):
+        from magicsoup_amd.examples.synthetic import make_chemistry
+
+        m = int(case[3:])
+        chem = make_chemistry(m, 2 * m, seed=3)
+    else:
+        chem = CHEMISTRY
+    ms.set_seed(2)
+    torch.manual_seed(2)
+    w = ms.World(chemistry=chem, map_size=64, device="cuda", seed=2)
+    size = 3000 if case == "wl3000" else 500
+    w.spawn_cells(gen_genomes(300, size))
+    kin = w.kinetics
+    if case == "big_exponents":
+        # stoichiometries / Hill numbers beyond the branch-free power range (>= 8) in some proteins
+        Nf, A = kin.Nf.clone(), kin.A.clone()
+        Nf[::7, :, 1] = torch.where(Nf[::7, :, 1] > 0, 9, Nf[::7, :, 1])
+        A[::5, :, 2] = torch.where(A[::5, :, 2] != 0, -9, A[::5, :, 2])
+        kin.Nf, kin.A = Nf, A
+    na = (kin.Vmax > 0).sum(1)
+    if case == "wl3000":
+        assert int(na.max()) > 32  # exercises the wide launch
+    pos = w.cell_positions.long()
+    X = torch.cat([w.cell_molecules, w.molecule_map[:, pos[:, 0], pos[:, 1]].T], dim=1).contiguous()
+    out = _integrate_modes(kin, X)
+    assert torch.equal(out[0], out[8])
+    assert not torch.equal(out[0], X)
