@@ -139,14 +139,18 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if torch.cuda.is_available():
-        # one rank per GPU; more ranks than GPUs (a rehearsal on a small box) share them round-robin
-        local_rank %= max(1, torch.cuda.device_count())
     distributed = world_size > 1
+    n_dev = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    backend = (os.environ.get("MS_DIST_BACKEND", "nccl") if n_dev else "gloo") if distributed else None
+    if n_dev and local_rank >= n_dev:
+        if backend != "gloo":
+            # RCCL needs one rank per GPU: two ranks on one device hang or fail inside the communicator
+            raise SystemExit(f"LOCAL_RANK {local_rank} >= {n_dev} visible GPUs: one rank per GPU with the nccl "
+                             "backend (set MS_DIST_BACKEND=gloo to rehearse with ranks sharing GPUs)")
+        local_rank %= n_dev  # gloo rehearsal on a small box: ranks share the GPUs round-robin
     if distributed:
         import torch.distributed as dist
 
-        backend = os.environ.get("MS_DIST_BACKEND", "nccl")  # gloo: rehearsal with ranks sharing a GPU
         if torch.cuda.is_available() and backend == "nccl":
             torch.cuda.set_device(local_rank)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -154,7 +158,7 @@ def main():
             torch.cuda.set_device(local_rank)
             dist.init_process_group(backend)
         else:  # CPU rehearsal of the multi-rank path
-            dist.init_process_group("gloo")
+            dist.init_process_group(backend)
     device = f"cuda:{local_rank}" if torch.cuda.is_available() else "cpu"
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
@@ -217,6 +221,8 @@ def main():
         n_cells = world.n_cells
     ms_per_step = dt / a.steps * 1e3
     value = a.steps / dt
+    # distinct devices actually used (a gloo rehearsal may put several ranks on one GPU)
+    n_gpus = (min(world_size, n_dev) if distributed else 1) if n_dev else 0
     if rank == 0:
         if timer is not None:
             per_step = {k: v / a.steps for k, v in (stats or {}).items()}
@@ -226,7 +232,7 @@ def main():
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "steps/s",
-            "n_gpus": world_size if distributed else a.gpus,
+            "n_gpus": n_gpus,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 4),
@@ -245,6 +251,11 @@ def main():
                 "parallelism": f"spatial{world_size}" if distributed else "single",
             },
         }
+        if distributed:
+            out["config"]["ranks"] = world_size
+            out["config"]["backend"] = backend
+            if backend != "nccl" or world_size > n_dev:
+                out["rehearsal"] = True  # ranks share GPUs and/or exchange over gloo: not a scaling number
         print(json.dumps(out), flush=True)
     if distributed:
         torch.distributed.destroy_process_group()

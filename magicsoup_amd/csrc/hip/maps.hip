@@ -111,7 +111,9 @@ __global__ void __launch_bounds__(64 * kWaves) diffuse_stencil_kernel(const T* _
 
 // Vector variant for C % 4 == 0 (every practical map): a lane owns 4 adjacent columns (one
 // 16 B / 8 B access per row), a wave 256 columns; the 4 waves of a block take 4 consecutive bands
-// of the same column strip. Rows are fetched two ahead so two loads per wave are in flight.
+// of the same column strip. While row o is computed, the load of row o + 2 is in flight (row o + 1
+// arrived in the previous iteration): one row load per wave ahead. A variant with two row loads in
+// flight was measured and not kept (docs/performance.md, "Diffusion").
 // grid: (ceil(C / 256), ceil(ceil(H / kBand) / 4), m).
 constexpr int kVBand = 32;
 template <class T>

@@ -41,13 +41,18 @@ def hip():
     """The gfx950 device module ``magicsoup_amd._hip`` (built on demand; raises if unavailable)."""
     from magicsoup_amd.ops import build
 
+    fresh = "_hip" not in _mods
     try:
-        return _load("_hip", build.build_hip)
+        mod = _load("_hip", build.build_hip)
     except Exception as err:  # pragma: no cover - exercised on GPU boxes only
         raise RuntimeError(
             "magicsoup_amd: the gfx950 HIP extension (_hip) could not be loaded; GPU execution"
             " requires it (no fallback). Build it with `python -m magicsoup_amd.ops.build`."
         ) from err
+    if fresh and os.environ.get("MS_INTEGRATE_MODE"):
+        # integrator launch-mode bits for whole-run A/B (kinetics.hip, set_integrate_mode)
+        mod.set_integrate_mode(int(os.environ["MS_INTEGRATE_MODE"]))  # type: ignore[attr-defined]
+    return mod
 
 
 def set_seed(seed: int) -> None:

@@ -33,7 +33,8 @@ def main():
         torch.cuda.synchronize()
         ms_it = e0.elapsed_time(e1) / a.iters
         nbytes = w.molecule_map.numel() * w.molecule_map.element_size()
-        # stencil reads + writes the map once, the correction pass once more
+        # the fused stencil reads the map once and writes it once per call (degradation and the
+        # pending mass correction are applied inside it)
         out[name] = {"ms": round(ms_it, 4), "map_MB": round(nbytes / 1e6, 1),
                      "eff_TBps": round(2 * nbytes / (ms_it * 1e-3) / 1e12, 3)}
         del w
