@@ -6,6 +6,7 @@
 #include <pybind11/stl.h>
 
 #include <atomic>
+#include <string>
 #include <tuple>
 #include <vector>
 
@@ -114,6 +115,34 @@ std::tuple<int, int, int> translate_stats(int n, uintptr_t counts, uintptr_t ndo
                                           uintptr_t stream);
 std::pair<long long, int> select_indices(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel,
                                          uintptr_t rest, uintptr_t stream);
+// comm.hip
+int rccl_load(const std::string& path);
+std::string rccl_unique_id();
+uintptr_t rccl_init(const std::string& uid, int nranks, int rank);
+void rccl_destroy(uintptr_t comm, bool abort);
+std::string rccl_async_error(uintptr_t comm);
+void rccl_allreduce(uintptr_t comm, uintptr_t buf, long long count, int dtype, int op, uintptr_t stream);
+void rccl_exchange(uintptr_t comm, int up, int down, uintptr_t send_up, long long n_send_up, uintptr_t send_down,
+                   long long n_send_down, uintptr_t recv_down, long long n_recv_down, uintptr_t recv_up,
+                   long long n_recv_up, uintptr_t stream);
+// dist.hip
+void strip_marks(int C, int H, uintptr_t cell_map, int k, uintptr_t cells, uintptr_t pos, uintptr_t up, uintptr_t dn,
+                 uintptr_t stream);
+void strip_reserve(int C, int H, uintptr_t from_up, uintptr_t from_dn, uintptr_t cell_map, uintptr_t stream);
+void strip_clear(int C, int H, uintptr_t cell_map, uintptr_t stream);
+void place_split(int k, uintptr_t result, uintptr_t cells, int C, int H, uintptr_t par, uintptr_t npos, uintptr_t counts,
+                 uintptr_t hdr_up, uintptr_t hdr_dn, int lw, int gw, int m, uintptr_t stream);
+long long rec_record_bytes(int m, int lw, int gw);
+void rec_pack(int k_up, int k_dn, uintptr_t par_up, uintptr_t pos_up, uintptr_t par_dn, uintptr_t pos_dn,
+              uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, uintptr_t gdata, uintptr_t glen, int gw,
+              uintptr_t ldata, uintptr_t llen, int lw, int m, bool child, uintptr_t out_up, uintptr_t out_dn,
+              uintptr_t stream);
+void rec_unpack(int n0, int k_up, uintptr_t in_up, int up_lw, int up_gw, int k_dn, uintptr_t in_dn, int dn_lw,
+                int dn_gw, int C, int H, uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, uintptr_t gdata,
+                uintptr_t glen, int gw, uintptr_t ldata, uintptr_t llen, int lw, int m, uintptr_t cell_map,
+                uintptr_t stream);
+void halo_pack(int m, int C, int H, int elem, uintptr_t map, uintptr_t send_up, uintptr_t send_dn, uintptr_t stream);
+void halo_unpack(int m, int C, int H, int elem, uintptr_t map, uintptr_t from_up, uintptr_t from_dn, uintptr_t stream);
 }  // namespace msd
 
 namespace {
@@ -180,6 +209,22 @@ PYBIND11_MODULE(_hip, m) {
   m.def("count_to_host", &msd::count_to_host, "device {count, max} -> pinned ring slot (returns the slot)");
   m.def("status_write", &msd::status_write, "pipeline status -> pinned ring slot (returns the slot)");
   m.def("status_read", &msd::status_read);
+  m.def("rccl_load", &msd::rccl_load, "resolve RCCL from a loaded librccl.so path; returns its version");
+  m.def("rccl_unique_id", [](){ return py::bytes(msd::rccl_unique_id()); });
+  m.def("rccl_init", [](py::bytes uid, int nranks, int rank) { return msd::rccl_init(std::string(uid), nranks, rank); });
+  m.def("rccl_destroy", &msd::rccl_destroy);
+  m.def("rccl_async_error", &msd::rccl_async_error);
+  m.def("rccl_allreduce", &msd::rccl_allreduce, "in-place all-reduce on a stream (dtype 0 i32 1 f32 2 f64 3 i64; op 0 sum 1 max 2 min)");
+  m.def("rccl_exchange", &msd::rccl_exchange, "grouped byte send/recv with the up / down neighbours on a stream");
+  m.def("strip_marks", &msd::strip_marks, "boundary-row bytes (1 occupied, 3 dividing) for the strip neighbours");
+  m.def("strip_reserve", &msd::strip_reserve, "halo occupancy + reservations from the neighbours' marks");
+  m.def("strip_clear", &msd::strip_clear);
+  m.def("place_split", &msd::place_split, "placement winners split into local / up / down (device counts + headers)");
+  m.def("rec_record_bytes", &msd::rec_record_bytes);
+  m.def("rec_pack", &msd::rec_pack);
+  m.def("rec_unpack", &msd::rec_unpack);
+  m.def("halo_pack", &msd::halo_pack);
+  m.def("halo_unpack", &msd::halo_unpack);
   m.def("select_indices", &msd::select_indices,
         "(count, max) of an order-preserving compaction; synchronises the stream");
 }

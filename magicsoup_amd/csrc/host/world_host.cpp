@@ -66,13 +66,13 @@ py::tuple place(iarr cell_idxs, iarr positions, int64_t R, int64_t C, int64_t r_
   const int32_t* ci = cell_idxs.data();
   Grid occ(R, C, wrap);
   for (int i = 0; i < n_all; ++i) occ.set(occ.key(pos[2 * i], pos[2 * i + 1]), true);
-  if (!halo_occ.is_none()) {  // (R, C) bool/uint8: occupancy of halo rows
+  if (!halo_occ.is_none()) {
+    // (R, C) uint8 occupancy of the strip: the halo rows (neighbours' boundary rows) and pixels of
+    // the owned boundary rows reserved for a neighbour's claims (strip protocol: value 2)
     barr h = halo_occ.cast<barr>();
     const uint8_t* hp = h.data();
-    for (int64_t y = 0; y < C; ++y) {
-      if (hp[y]) occ.set(occ.key(0, y), true);
-      if (hp[(R - 1) * C + y]) occ.set(occ.key(R - 1, y), true);
-    }
+    for (int64_t px = 0; px < R * C; ++px)
+      if (hp[px]) occ.set(px, true);
   }
   auto rng = item_engine(next_call_seed(), 0);
   std::vector<int32_t> who, npos;

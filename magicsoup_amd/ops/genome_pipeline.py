@@ -52,9 +52,7 @@ _SEL_I32POS, _SEL_SET = 2, 0
 def enabled(world) -> bool:
     if os.environ.get("MS_SYNC_GENETICS") == "1":
         return False
-    if not world.__dict__["_molmap"].is_cuda or getattr(world, "_geom", None) is not None:
-        return False  # GPU, single-domain worlds only
-    return True
+    return bool(world.__dict__["_molmap"].is_cuda)  # GPU worlds (single map or strip of a decomposed one)
 
 
 class _StatusSlot:
@@ -259,6 +257,24 @@ def recombinate_all(world, p: float) -> bool:
     _rebuild(world, b, cells, b["cnt2"], 2 * pcap)
     _finish(world, "rec", (p,), (seed, call), b, cells, b["cnt2"],
             {"rows": out_rows, "out": out, "out_w": out_w, "out_len": out_len, "mark": mark, "gen": gen})
+    return True
+
+
+def rebuild_rows(world, rows: torch.Tensor) -> bool:
+    """Translate and build parameters of the cells ``rows`` (e.g. cells that arrived from another
+    rank) into fresh parameter rows without a synchronisation; resolved by :func:`reconcile` like
+    the other pipeline calls. False if the caller should take the synchronous path."""
+    k = int(rows.numel())
+    if k == 0:
+        return True
+    if not enabled(world) or k > N_CAP:
+        return False
+    b = _begin(world, "imm")
+    dcnt = b["cnt"]
+    dcnt[:1].fill_(k)
+    cells = rows.to(torch.int64).contiguous()
+    _rebuild(world, b, cells, dcnt, k)
+    _finish(world, "imm", (), None, b, cells, dcnt, {})
     return True
 
 

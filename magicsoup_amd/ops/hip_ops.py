@@ -398,9 +398,9 @@ def free_positions(world, k: int) -> torch.Tensor:
 _PLACE_ROUNDS = 8
 
 
-def _place_rounds(world, cells: torch.Tensor, vacate: bool, rounds: int = _PLACE_ROUNDS):
+def place_rounds_raw(world, cells: torch.Tensor, vacate: bool = False, rounds: int = _PLACE_ROUNDS) -> torch.Tensor:
     """Priority-ordered parallel neighbour claims resolved on the device (atomicMin per pixel, see
-    world.hip place_rounds). Returns (winner cells in list order, new pixels int32 (k', 2))."""
+    world.hip place_rounds): the claimed pixel per cell of ``cells`` (int64, -1 = none), no sync."""
     R, C, r_lo, r_hi, wrap = geom(world)
     dev = cells.device
     k = int(cells.numel())
@@ -420,6 +420,14 @@ def _place_rounds(world, cells: torch.Tensor, vacate: bool, rounds: int = _PLACE
     seed, call = _rng()
     _m().place_rounds(k, _p(cells), _p(pos), R, C, r_lo, r_hi, wrap, bool(vacate), _p(cmap), _p(pending), _p(cand),
                       _p(claim), _p(result), int(rounds), seed, call, _stream())
+    return result
+
+
+def _place_rounds(world, cells: torch.Tensor, vacate: bool, rounds: int = _PLACE_ROUNDS):
+    """:func:`place_rounds_raw`, then the winners: (cells in list order, new pixels int32 (k', 2))."""
+    C = geom(world)[1]
+    dev = cells.device
+    result = place_rounds_raw(world, cells, vacate, rounds)
     wins = select(result, "i64nonneg")[0]
     k2 = int(wins.numel())
     par = torch.empty(k2, dtype=torch.int64, device=dev)

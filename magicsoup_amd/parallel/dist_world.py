@@ -16,16 +16,28 @@ runs locally. What couples ranks:
   per-molecule mass totals of the correction are all-reduced so the global map conserves mass;
 * integration: the equilibrium-damping early exit is the reference's ``torch.any`` over all cells
   (kinetics.py:837), so the four per-part iteration flags are MAX-all-reduced between parts;
-* division / movement into a neighbour's boundary row: a claim protocol. Each rank places its
-  cells as usual, treating the halo rows (refreshed occupancy) as candidates. Claims into a halo row
-  are sent with the full cell record to the owner, which accepts a claim if the pixel is still free
-  after its own placements and appends the cell; the claimer then commits (splits the parent /
-  drops the emigrant). A rejected cell does not divide / move this step.
+* division into a neighbour's boundary row: before placement every rank sends each neighbour one
+  byte per boundary column (occupied / dividing cell). The receiver copies the occupancy into its
+  halo row and reserves its own free boundary pixels next to the neighbour's dividing cells, so
+  the claims the two ranks make into the same row can never collide: children placed into a halo
+  row are created on the owning rank from their records with no accept / reject round trip
+  (``strip.py``, ``csrc/hip/dist.hip``). One host synchronisation reads the local winner counts and
+  the neighbours' record headers together, as the single-GPU division reads its winner count.
+* movement into a neighbour's boundary row: a claim protocol. Claims into a halo row are sent
+  with the full cell record to the owner, which accepts a claim if the pixel is still free after its
+  own placements and appends the cell; the claimer then drops the emigrant. A rejected cell does not
+  move this step.
 * recombination across a strip boundary: each rank receives its lower neighbour's boundary-row
   cells as ghosts, recombines pairs that include them, and sends the ghosts' new genomes back.
 
+Communication goes through :mod:`magicsoup_amd.parallel.comm`: a native RCCL communicator driven
+from C++ on the current HIP stream for GPU ranks (``nccl`` process groups), torch.distributed
+(gloo) otherwise.
+
 Per-cell RNG streams differ per rank, so a run is reproducible for a fixed rank count but not
-bit-identical to a single-process run.
+bit-identical to a single-process run. Reserved boundary pixels make a child next to a strip
+boundary avoid a pixel that a neighbour's dividing cell could claim in the same step; away from
+strip boundaries placement is exactly the single-map algorithm.
 """
 from __future__ import annotations
 
@@ -37,8 +49,10 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from magicsoup_amd.models.world import World
+from magicsoup_amd.models.world import World, _op
 from magicsoup_amd.ops import world_ops
+from magicsoup_amd.parallel import strip
+from magicsoup_amd.parallel.comm import make_comm
 
 _U8 = torch.uint8
 
@@ -121,6 +135,7 @@ class DistributedWorld(World):
             random.setstate(own)
         g["_n_pix_global"] = map_size * map_size
         g["_stage"] = dist.get_backend(group) == "gloo" and torch.device(self.device).type == "cuda"
+        g["_comm"] = make_comm(group, self.rank, n, self.device) if n > 1 else None
         g["migrated"] = {"divided_out": 0, "divided_in": 0, "moved_out": 0, "moved_in": 0, "rejected": 0}
         if n > 1:
             # hooks the op layer calls (World has them as None): halo refresh before the diffusion
@@ -169,43 +184,12 @@ class DistributedWorld(World):
     def _exchange(self, to_up, to_down, from_down, from_up) -> None:
         """One neighbour exchange: ``to_up`` arrives at the upper neighbour as its ``from_down``,
         ``to_down`` at the lower one as its ``from_up``. ``None`` skips an op (the peer must skip
-        the matching one). Ops to the same peer are matched in issue order (RCCL) and by tag (gloo)."""
-        if self._stage:
-            return self._exchange_staged(to_up, to_down, from_down, from_up)
-        ops = []
-        if to_up is not None:
-            ops.append(dist.P2POp(dist.isend, to_up, self._up, self.group, 0))
-        if to_down is not None:
-            ops.append(dist.P2POp(dist.isend, to_down, self._down, self.group, 1))
-        if from_down is not None:
-            ops.append(dist.P2POp(dist.irecv, from_down, self._down, self.group, 0))
-        if from_up is not None:
-            ops.append(dist.P2POp(dist.irecv, from_up, self._up, self.group, 1))
-        if not ops:
-            return
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
-
-    def _exchange_staged(self, to_up, to_down, from_down, from_up) -> None:
-        """gloo with device tensors (e.g. several ranks sharing one GPU in tests): via host copies."""
-        h = [None if t is None else t.cpu() for t in (to_up, to_down)]
-        r = [None if t is None else torch.empty(t.shape, dtype=t.dtype) for t in (from_down, from_up)]
-        self.__dict__["_stage"] = False
-        try:
-            self._exchange(h[0], h[1], r[0], r[1])
-        finally:
-            self.__dict__["_stage"] = True
-        for dst, src in zip((from_down, from_up), r):
-            if dst is not None:
-                dst.copy_(src)
+        the matching one)."""
+        self._comm.exchange(to_up, to_down, from_down, from_up)
 
     def _all_reduce(self, t: torch.Tensor, op) -> None:
-        if self._stage:
-            h = t.cpu()
-            dist.all_reduce(h, op=op, group=self.group)
-            t.copy_(h)
-        else:
-            dist.all_reduce(t, op=op, group=self.group)
+        name = {dist.ReduceOp.SUM: "sum", dist.ReduceOp.MAX: "max", dist.ReduceOp.MIN: "min"}[op]
+        self._comm.allreduce_(t, name)
 
     def _exchange_var(self, up: torch.Tensor | None, down: torch.Tensor | None, meta_up=(), meta_down=()):
         """Exchange variable-size uint8 record blocks (k, B) with both neighbours. ``meta_*`` are
@@ -234,21 +218,20 @@ class DistributedWorld(World):
 
     def _do_exchange_map_halo(self) -> None:
         """Refresh the molecule-map halo rows from the neighbours' boundary rows (raw buffer: a
-        pending degradation factor is identical on every rank and applied by the stencil)."""
+        pending degradation factor is identical on every rank and applied by the stencil). One pack
+        launch, one grouped exchange, one unpack launch."""
         if self.world_size == 1:
             return
         mm = self.__dict__["_molmap"]
-        H = self.H
+        m, C = int(mm.size(0)), self.map_size
         sb = self.__dict__.get("_halo_bufs")
-        if sb is None or sb[0].shape != mm[:, 1].shape or sb[0].device != mm.device:
-            sb = tuple(torch.empty_like(mm[:, 1]) for _ in range(4))
+        if sb is None or sb.dtype != mm.dtype or sb.device != mm.device or sb.numel() != 4 * m * C:
+            sb = torch.empty(4 * m * C, dtype=mm.dtype, device=mm.device)
             self.__dict__["_halo_bufs"] = sb
-        s_up, s_dn, r_dn, r_up = sb
-        s_up.copy_(mm[:, 1])
-        s_dn.copy_(mm[:, H])
+        s_up, s_dn, r_dn, r_up = (sb[i * m * C : (i + 1) * m * C] for i in range(4))
+        strip.halo_pack(self, s_up, s_dn)
         self._exchange(s_up, s_dn, r_dn, r_up)
-        mm[:, H + 1].copy_(r_dn)
-        mm[:, 0].copy_(r_up)
+        strip.halo_unpack(self, r_up, r_dn)
 
     def _exchange_occupancy(self) -> None:
         if self.world_size == 1:
@@ -352,6 +335,7 @@ class DistributedWorld(World):
         return acc_up, acc_dn, got
 
     # ------------------------------------------------------------------ physics overrides
+    @_op("enzymatic_activity")
     def enzymatic_activity(self):
         """Integration (collective with ``exact_global_exit``). A rank whose strip holds no cells
         still takes part in the per-part MAX all-reduces of the iteration flags (with all-zero
@@ -366,65 +350,114 @@ class DistributedWorld(World):
         super().enzymatic_activity()
 
     # ------------------------------------------------------------------ lifecycle overrides
+    @_op("divide_cells")
     def divide_cells_t(self, cell_idxs) -> tuple[torch.Tensor, torch.Tensor]:
         """Division (collective). Children landing in a neighbour's boundary row are created on
-        that rank; the returned pairs cover local children only (counts in ``self.migrated``)."""
+        that rank; the returned pairs cover local children only (counts in ``self.migrated``).
+
+        Protocol (module docstring): boundary marks -> reservations -> placement rounds ->
+        winners split by destination row + record headers exchanged -> one synchronisation ->
+        child records exchanged and appended; exporting parents keep half their molecules."""
         if self.world_size == 1:
             return super().divide_cells_t(cell_idxs)
+        from magicsoup_amd.ops.hip_ops import _scratch
+
         idxs = self._idx_tensor(cell_idxs)
+        k = int(idxs.numel())
         dev = self.device
+        C, H, m = self.map_size, self.H, self.n_molecules
+        gpu = self.cell_molecules.is_cuda
+        sc = _scratch(self)
         empty = torch.zeros(0, dtype=torch.long, device=dev)
-        self._exchange_occupancy()
-        if idxs.numel():
-            parents, cpos = world_ops.divide_placement(self, idxs)
-            parents = parents.to(dev)
-            cpos = cpos.to(dev)
+        # 1. boundary bytes (occupied / dividing) to the neighbours; halo occupancy + reservations
+        mk = sc.get("dv_marks", 4 * C, _U8, torch.device(dev))
+        s_up, s_dn, r_dn, r_up = mk[:C], mk[C : 2 * C], mk[2 * C : 3 * C], mk[3 * C :]
+        strip.marks(self, idxs, s_up, s_dn)
+        self._exchange(s_up, s_dn, r_dn, r_up)
+        strip.reserve(self, r_up, r_dn)
+        # 2. placement (claims into the halo rows are final), winners by destination, headers
+        lw, gw = int(self._labels.width), int(self._genomes.width)
+        if gpu:
+            from magicsoup_amd.ops import hip_ops
+
+            cells = idxs.to(torch.int64).contiguous()
+            kk = max(k, 1)
+            result = hip_ops.place_rounds_raw(self, cells) if k else sc.get("dv_res0", 1, torch.int64, cells.device)
+            par = sc.get("dv_par", 3 * kk, torch.int64, cells.device)
+            npos = sc.get("dv_npos", 6 * kk, torch.int32, cells.device).view(3 * kk, 2)
+            st = sc.get("dv_status", 20, torch.int32, cells.device)
+            strip.split_winners_gpu(self, cells, result, par, npos, st)
+            self._exchange(st[4:8], st[8:12], st[16:20], st[12:16])
+            v = st.tolist()  # the one synchronisation: local winner counts + the neighbours' headers
+            n_loc, n_up, n_dn = v[0], v[1], v[2]
+            hdr_up, hdr_dn = v[12:16], v[16:20]
+            par_loc, pos_loc = par[:n_loc], npos[:n_loc]
+            par_up, pos_up = par[kk : kk + n_up], npos[kk : kk + n_up]
+            par_dn, pos_dn = par[2 * kk : 2 * kk + n_dn], npos[2 * kk : 2 * kk + n_dn]
         else:
-            parents, cpos = empty, torch.zeros(0, 2, dtype=torch.int32, device=dev)
-        # split the winners by destination row (local / upper halo / lower halo) with one stable
-        # sort and one read-back instead of a boolean compaction per class
-        i_loc, i_up, i_dn = self._split_by_row(cpos[:, 0])
-        p_up, p_dn = parents[i_up], parents[i_dn]
-        if not cpos.is_cuda:
-            # own children first when arbitrating claims (the GPU placement kernels already
-            # marked every claimed pixel, halo rows too)
-            lp = cpos[i_loc].long()
+            if k:
+                parents, cpos = world_ops.divide_placement(self, idxs)
+            else:
+                parents, cpos = empty, torch.zeros(0, 2, dtype=torch.int32)
+            i_loc, i_up, i_dn = strip.split_winners_cpu(self, parents, cpos)
+            par_loc, pos_loc = parents[i_loc], cpos[i_loc]
+            par_up, pos_up = parents[i_up], cpos[i_up]
+            par_dn, pos_dn = parents[i_dn], cpos[i_dn]
+            n_loc, n_up, n_dn = int(i_loc.numel()), int(i_up.numel()), int(i_dn.numel())
+            # own children first: their pixels are taken before the neighbours' records land
+            lp = pos_loc.long()
             self.cell_map[lp[:, 0], lp[:, 1]] = True
-        rec_up = self._records(p_up, cpos[i_up, 1], child=True)
-        rec_dn = self._records(p_dn, cpos[i_dn, 1], child=True)
-        acc_up, acc_dn, got = self._migrate(rec_up, rec_dn)
-        # halo claims are scratch: the halo rows are refreshed before their next use
-        self.cell_map[0] = False
-        self.cell_map[self.H + 1] = False
-        # exported children: the parent keeps half, both get divisions + 1 and lifetime 0 (masked
-        # updates of all exporters, no compaction of the accepted ones)
-        p_out = torch.cat([p_up, p_dn])
-        if p_out.numel():
-            acc = torch.cat([acc_up, acc_dn])
-            f = 1.0 - 0.5 * acc.to(torch.float32)
-            self.cell_molecules[p_out] = self.cell_molecules[p_out] * f[:, None]
-            self.cell_divisions[p_out] = self.cell_divisions[p_out] + acc.to(torch.int32)
-            self.cell_lifetimes[p_out] = torch.where(acc, 0, self.cell_lifetimes[p_out])
-            n_out = int(acc.sum())
-        else:
-            n_out = 0
-        mig = self.migrated
-        mig["divided_out"] += n_out
-        mig["divided_in"] += got
-        mig["rejected"] += int(p_out.numel()) - n_out
-        parents, cpos = parents[i_loc], cpos[i_loc]
-        k = int(parents.numel())
-        if k == 0:
-            return empty, empty
+            hs = torch.tensor([n_up, lw, gw, m, n_dn, lw, gw, m], dtype=torch.int32)
+            hr = torch.zeros(8, dtype=torch.int32)
+            self._exchange(hs[:4], hs[4:], hr[4:], hr[:4])
+            hdr_up, hdr_dn = hr[:4].tolist(), hr[4:].tolist()
+        # 3. child records to the neighbours (exact sizes from the headers)
+        B = strip.record_bytes(m, lw, gw)
+        out = sc.get("dv_out", max(1, (n_up + n_dn) * B), _U8, torch.device(dev))
+        out_up, out_dn = out[: n_up * B], out[n_up * B : (n_up + n_dn) * B]
+        strip.pack(self, par_up, pos_up, par_dn, pos_dn, True, out_up, out_dn)
+        b_up = hdr_up[0] * strip.record_bytes(m, hdr_up[1], hdr_up[2])
+        b_dn = hdr_dn[0] * strip.record_bytes(m, hdr_dn[1], hdr_dn[2])
+        inb = sc.get("dv_in", max(1, b_up + b_dn), _U8, torch.device(dev))
+        in_up, in_dn = inb[:b_up], inb[b_up : b_up + b_dn]
+        self._exchange(out_up, out_dn, in_dn, in_up)
+        # 4. exporting parents keep half their molecules (every claim into a halo row is accepted)
+        if n_up + n_dn:
+            p_out = torch.cat([par_up, par_dn])
+            world_ops.split_cells(self, p_out, p_out)
+        # 5. local children (rows n0 ..), then the arrivals
         n0 = self.n_cells
-        children = torch.arange(n0, n0 + k, device=dev)
-        self._clone_rows(parents, children)
-        if cpos.is_cuda:
-            self.cell_positions[n0 : n0 + k] = cpos
-        else:
-            self._place(children, cpos)
-        world_ops.split_cells(self, parents, children)
-        return parents, children
+        children = torch.arange(n0, n0 + n_loc, device=dev)
+        if n_loc:
+            self._clone_rows(par_loc, children)
+            self.cell_positions[n0 : n0 + n_loc] = pos_loc.to(torch.int32)
+            world_ops.split_cells(self, par_loc, children)
+        self._append_arrivals(hdr_up, in_up, hdr_dn, in_dn)
+        # 6. halo rows empty, reservations released
+        strip.clear(self)
+        mig = self.migrated
+        mig["divided_out"] += n_up + n_dn
+        mig["divided_in"] += hdr_up[0] + hdr_dn[0]
+        return (par_loc if n_loc else empty), children
+
+    def _append_arrivals(self, hdr_up, in_up, hdr_dn, in_dn) -> None:
+        """Append the records received from the upper (row 1) and lower (row H) neighbours as new
+        cells and build their parameters (device genome pipeline on the GPU: no synchronisation)."""
+        k = int(hdr_up[0]) + int(hdr_dn[0])
+        if k == 0:
+            return
+        n1 = self.n_cells
+        self._grow(k, zero=False)
+        for arena, wi in ((self._genomes, 2), (self._labels, 1)):
+            arena.reserve(n1 + k, max(int(hdr_up[wi]), int(hdr_dn[wi]), 1))
+            arena.n = n1 + k
+            arena.version += 1
+        strip.unpack(self, n1, in_up, hdr_up, in_dn, hdr_dn)
+        new = torch.arange(n1, n1 + k, device=self.device)
+        from magicsoup_amd.ops import genome_pipeline
+
+        if not (self.cell_molecules.is_cuda and genome_pipeline.rebuild_rows(self, new)):
+            self._update_params_rows(new)
 
     def _split_by_row(self, rows: torch.Tensor):
         """Indices (in order) of entries whose local row is owned / the upper halo (0) / the lower
@@ -437,6 +470,7 @@ class DistributedWorld(World):
         c = torch.bincount(cls.to(torch.int64), minlength=3).tolist()
         return order[: c[0]], order[c[0] : c[0] + c[1]], order[c[0] + c[1] :]
 
+    @_op("move_cells")
     def move_cells(self, cell_idxs=None):
         """Movement (collective). Cells moving into a neighbour's boundary row migrate to it."""
         if self.world_size == 1:
@@ -495,6 +529,7 @@ class DistributedWorld(World):
         return super().reposition_cells(cell_idxs)
 
     # ------------------------------------------------------------------ recombination
+    @_op("recombinate_cells_strips")  # not pipeline-safe: reads genomes on the host path
     def recombinate_cells(self, cell_idxs: list[int] | None = None, p: float = 1e-7):
         """Recombination between neighbouring cells (collective), including pairs across strip
         boundaries: a rank recombines its last-row cells with ghosts of the lower neighbour's first

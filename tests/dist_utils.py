@@ -14,7 +14,7 @@ def _free_port() -> int:
         return int(s.getsockname()[1])
 
 
-def _entry(rank: int, world_size: int, port: int, fn, args, errq):
+def _entry(rank: int, world_size: int, port: int, fn, args, errq, backend: str = "gloo"):
     import torch
     import torch.distributed as dist
 
@@ -22,7 +22,12 @@ def _entry(rank: int, world_size: int, port: int, fn, args, errq):
     os.environ["MASTER_PORT"] = str(port)
     os.environ["OMP_NUM_THREADS"] = "2"
     torch.set_num_threads(2)
-    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    if backend == "nccl":
+        torch.cuda.set_device(rank % torch.cuda.device_count())
+        dist.init_process_group("nccl", rank=rank, world_size=world_size,
+                                device_id=torch.device("cuda", rank % torch.cuda.device_count()))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world_size)
     try:
         fn(rank, world_size, *args)
     except BaseException:  # noqa: BLE001 - reported to the parent
@@ -32,12 +37,13 @@ def _entry(rank: int, world_size: int, port: int, fn, args, errq):
         dist.destroy_process_group()
 
 
-def run_ranks(fn, world_size: int = 2, *args, timeout: float = 300.0) -> None:
-    """Run ``fn(rank, world_size, *args)`` on ``world_size`` gloo ranks; re-raise the first failure."""
+def run_ranks(fn, world_size: int = 2, *args, timeout: float = 300.0, backend: str = "gloo") -> None:
+    """Run ``fn(rank, world_size, *args)`` on ``world_size`` ranks (gloo by default; ``nccl`` puts
+    rank r on GPU r) in spawned processes; re-raise the first failure."""
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_entry, args=(r, world_size, port, fn, args, errq)) for r in range(world_size)]
+    procs = [ctx.Process(target=_entry, args=(r, world_size, port, fn, args, errq, backend)) for r in range(world_size)]
     for p in procs:
         p.start()
     for p in procs:

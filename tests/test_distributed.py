@@ -128,6 +128,50 @@ def test_distributed_lifecycle_invariants():
     run_ranks(_body_lifecycle, 2)
 
 
+def _body_boundary_division(rank, ws):
+    """Dense boundary rows, every cell divides: the reservation protocol must never put two cells
+    on one pixel, however many claims target the strip boundaries (3 ranks: distinct neighbours)."""
+    import torch.distributed as dist
+
+    import magicsoup_amd as ms
+
+    S = 4 * ws
+    g = ms.World(chemistry=_chem(), map_size=S, seed=4)
+    g.kill_cells()
+    # every second pixel of each strip's first and last row
+    pix = [(x, y) for x in range(S) if x % 4 in (0, 3) for y in range(0, S, 2)]
+    g._grow(len(pix))
+    g._genomes.append_strings([ms.random_genome(120) for _ in pix])
+    g._labels.append_strings([f"c{i}" for i in range(len(pix))])
+    g._place(torch.arange(len(pix)), torch.tensor(pix, dtype=torch.int32))
+    g.cell_molecules[:] = 4.0
+    g._update_params_rows(torch.arange(len(pix)))
+    dw = _dworld(S, seed=9 + rank)
+    dw.scatter_from(g)
+    tot0 = dw.cell_molecules.double().sum(0) + dw.owned_molecule_map().double().sum(dim=[1, 2])
+    dist.all_reduce(tot0)
+    for it in range(4):
+        dw.divide_cells(list(range(dw.n_cells)))
+        _check_local(dw)
+        tot = dw.cell_molecules.double().sum(0) + dw.owned_molecule_map().double().sum(dim=[1, 2])
+        dist.all_reduce(tot)
+        assert torch.allclose(tot, tot0, rtol=1e-6), it
+        full = dw.gather()
+        if rank == 0:
+            _check_global(full)
+    mig = torch.tensor([dw.migrated["divided_in"], dw.migrated["divided_out"]])
+    dist.all_reduce(mig)
+    assert int(mig[0]) == int(mig[1]) > 0
+
+
+def test_distributed_boundary_division_two_ranks():
+    run_ranks(_body_boundary_division, 2)
+
+
+def test_distributed_boundary_division_three_ranks():
+    run_ranks(_body_boundary_division, 3)
+
+
 def _body_recombination(rank, ws):
     import magicsoup_amd as ms
 

@@ -95,3 +95,32 @@ def _body_steps(rank, ws):
 
 def test_gpu_distributed_steps_keep_invariants():
     run_ranks(_body_steps, 2, timeout=600)
+
+
+def _body_rccl_self(rank, ws):
+    """The native RCCL communicator on one GPU rank: exchanges with itself (up == down == self on a
+    one-rank ring) and all-reduces, enqueued on the current stream between kernels."""
+    from magicsoup_amd.parallel.comm import RcclComm, make_comm
+
+    comm = make_comm(None, 0, 1, "cuda")
+    assert isinstance(comm, RcclComm) and comm.up == comm.down == 0
+    a = torch.arange(1000, dtype=torch.float32, device="cuda")
+    b = torch.arange(1000, 1500, dtype=torch.int32, device="cuda")
+    ra = torch.empty_like(a)
+    rb = torch.empty_like(b)
+    # to_up arrives as from_down, to_down as from_up (both at ourselves)
+    comm.exchange(a, b, ra, rb)
+    torch.cuda.synchronize()
+    assert torch.equal(ra, a) and torch.equal(rb, b)
+    t = torch.tensor([3.0, -1.0], dtype=torch.float64, device="cuda")
+    comm.allreduce_(t, "max")
+    f = torch.tensor([1, 0, 2, 0], dtype=torch.int32, device="cuda")
+    comm.allreduce_(f, "sum")
+    torch.cuda.synchronize()
+    assert t.tolist() == [3.0, -1.0] and f.tolist() == [1, 0, 2, 0]
+    comm.check()
+    comm.close()
+
+
+def test_native_rccl_comm_single_rank():
+    run_ranks(_body_rccl_self, 1, timeout=300, backend="nccl")
