@@ -19,6 +19,7 @@
 #include <algorithm>
 
 #include "hip_common.h"
+#include "rec_common.h"
 
 namespace msd {
 
@@ -272,6 +273,176 @@ __global__ void __launch_bounds__(256) halo_unpack_kernel(int m, int C, int H, T
   map[j * plane + (size_t)(H + 1) * C + y] = from_dn[t];
 }
 
+
+// ---------------------------------------------------------------- recombination across a boundary
+// Every pair (upper cell at (its row H, y), lower cell at (its row 1, y + d)), d in {-1, 0, 1}, of the
+// boundary between rank u and u + 1 is item 3 y + d + 1. Both ranks of a boundary know both rows'
+// genome lengths (exchanged), draw the same Poisson counts from the boundary's stream (seed, call,
+// item), keep the same first E events, swap the involved genomes and compute the same
+// recombinations (rec_pair_apply); each keeps the result of its own cell.
+__device__ __forceinline__ int strip_cell_at(const int32_t* idx_map, const int32_t* pos, int n, int C, long long px) {
+  const int o = idx_map[px];
+  if (o < 0 || o >= n) return -1;
+  return ((long long)pos[2 * o] * C + pos[2 * o + 1]) == px ? o : -1;
+}
+
+// own boundary cells and their genome lengths (-1: no cell); word C of each length row = the
+// genome arena's row width
+__global__ void __launch_bounds__(256) xb_prep_kernel(int C, int H, int n, const int32_t* pos, const int32_t* idx_map,
+                                                      const int32_t* lens, int width, int32_t* len_up, int32_t* len_dn,
+                                                      int32_t* own1, int32_t* ownH) {
+  const int y = blockIdx.x * blockDim.x + threadIdx.x;
+  if (y == 0) {
+    len_up[C] = width;
+    len_dn[C] = width;
+  }
+  if (y >= C) return;
+  const int c1 = strip_cell_at(idx_map, pos, n, C, (long long)C + y);
+  const int cH = strip_cell_at(idx_map, pos, n, C, (long long)H * C + y);
+  own1[y] = c1;
+  ownH[y] = cH;
+  len_up[y] = c1 >= 0 ? lens[c1] : -1;
+  len_dn[y] = cH >= 0 ? lens[cH] : -1;
+}
+
+struct XbEvents {
+  int32_t* b;     // boundary of event j: 0 = below this rank (we are the upper side), 1 = above
+  int32_t* item;  // item index within the boundary
+  int32_t* k;     // strand breaks
+  int32_t* own;   // our cell
+  int32_t* slot;  // slot of the event within its boundary's exchange buffer
+  int32_t* counts;  // {events below, events above, total, dropped (beyond E)}
+};
+
+constexpr int kXbThreads = 1024;
+
+// One workgroup: draws of both boundaries, the first E events of each in item order, and a copy of
+// our genome of every event into the boundary's outgoing slots ([int32 length | slot_w bytes]).
+__global__ void __launch_bounds__(kXbThreads) xb_events_kernel(int C, int E, int slot_w, double p, int kcap,
+                                                               uint64_t seed_dn, uint64_t seed_up, uint64_t call,
+                                                               const int32_t* mine_dn, const int32_t* from_dn,
+                                                               const int32_t* mine_up, const int32_t* from_up,
+                                                               const int32_t* own1, const int32_t* ownH,
+                                                               const uint8_t* arena, int width, XbEvents ev,
+                                                               uint8_t* slots_dn, uint8_t* slots_up) {
+  constexpr int W = kXbThreads / 64;
+  __shared__ int s_wc[W];
+  __shared__ int s_base;
+  __shared__ int s_cnt[2], s_tot[2];
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  if (tid == 0) s_base = 0;
+  for (int b = 0; b < 2; ++b) {
+    // b = 0: we hold the upper cells (row H, lengths mine_dn), the lower rank the lower ones (from_dn)
+    const int32_t* la_row = b == 0 ? mine_dn : from_up;
+    const int32_t* lb_row = b == 0 ? from_dn : mine_up;
+    const int wx = min(slot_w, min(mine_dn[C], b == 0 ? from_dn[C] : from_up[C]));
+    const uint64_t seed = b == 0 ? seed_dn : seed_up;
+    int found = 0;  // events of this boundary so far (uniform across the block)
+    __syncthreads();
+    const int base0 = s_base;
+    for (int c0 = 0; c0 < 3 * C; c0 += kXbThreads) {
+      const int i = c0 + tid;
+      int kk = 0, own = -1;
+      if (i < 3 * C) {
+        const int y = i / 3, d = i - 3 * y - 1;
+        const bool ok_d = d == 0 || (d == -1 && C >= 2) || (d == 1 && C >= 3);
+        const int yb = (y + d + C) % C;
+        const int la = la_row[y], lb = lb_row[yb];
+        if (ok_d && la >= 0 && lb >= 0 && la <= wx && lb <= wx && la + lb > 0) {
+          Philox rng(seed, call, (uint32_t)i);
+          long long q = poisson(rng, p * (double)(la + lb));
+          if (kcap > 0 && q > kcap) q = kcap;
+          kk = (int)(q > la + lb ? la + lb : q);
+          own = b == 0 ? ownH[y] : own1[yb];
+        }
+      }
+      const uint64_t bal = __ballot(kk > 0);
+      if (lane == 0) s_wc[w] = __popcll(bal);
+      __syncthreads();
+      int pre = 0, tot = 0;
+      for (int q = 0; q < W; ++q) {
+        if (q < w) pre += s_wc[q];
+        tot += s_wc[q];
+      }
+      if (kk > 0) {
+        const int jb = found + pre + __popcll(bal & lt);
+        if (jb < E) {
+          const int j = base0 + jb;
+          ev.b[j] = b;
+          ev.item[j] = i;
+          ev.k[j] = kk;
+          ev.own[j] = own;
+          ev.slot[j] = jb;
+        }
+      }
+      found += tot;
+      __syncthreads();
+    }
+    if (tid == 0) {
+      s_cnt[b] = min(found, E);
+      s_tot[b] = found;
+      s_base = base0 + min(found, E);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    ev.counts[0] = s_cnt[0];
+    ev.counts[1] = s_cnt[1];
+    ev.counts[2] = s_cnt[0] + s_cnt[1];
+    ev.counts[3] += (s_tot[0] - s_cnt[0]) + (s_tot[1] - s_cnt[1]);
+  }
+  // our genome of each event into its slot (the pre-recombination copy both ranks work from)
+  const int total = s_cnt[0] + s_cnt[1];
+  for (int j = 0; j < total; ++j) {
+    const int b = ev.b[j], jb = ev.slot[j], c = ev.own[j];
+    uint8_t* slot = (b == 0 ? slots_dn : slots_up) + (size_t)jb * (4 + slot_w);
+    const int32_t* lrow = b == 0 ? mine_dn : mine_up;
+    const int item = ev.item[j];
+    const int y = item / 3, d = item - 3 * y - 1;
+    const int L = b == 0 ? lrow[y] : lrow[(y + d + C) % C];
+    if (tid == 0) *reinterpret_cast<int32_t*>(slot) = L;
+    for (int t = tid; t < L; t += kXbThreads) slot[4 + t] = arena[(size_t)c * width + t];
+  }
+}
+
+// One wavefront per event: the recombination of (upper genome, lower genome) exactly as both ranks
+// compute it; our cell's result goes to out row `base + j` (base = 2 * *pair_count when appending
+// after the local pipeline's results, else 0) with its row; the other result to scratch.
+// *nres = base + total (rows to commit).
+__global__ void __launch_bounds__(64) xb_apply_kernel(int C, int slot_w, uint64_t seed_dn, uint64_t seed_up,
+                                                      uint64_t call, XbEvents ev, const uint8_t* slots_dn,
+                                                      const uint8_t* slots_up, const uint8_t* recv_dn,
+                                                      const uint8_t* recv_up, int32_t* parts, int parts_cap,
+                                                      const int* pair_count, uint8_t* out, int out_width,
+                                                      int32_t* out_len, int64_t* out_rows, uint8_t* other,
+                                                      int* nres) {
+  __shared__ int32_t lparts[(kFloydMax + 2) * 3];
+  __shared__ int meta[2];
+  const int j = blockIdx.x, lane = threadIdx.x;
+  const int total = ev.counts[2];
+  const int base = pair_count ? 2 * *pair_count : 0;
+  if (j == 0 && lane == 0) *nres = base + total;
+  if (j >= total) return;
+  const int b = ev.b[j], jb = ev.slot[j];
+  const size_t so = (size_t)jb * (4 + slot_w);
+  // b = 0: our cell is the upper one (its copy in slots_dn), the lower one arrived in recv_dn
+  const uint8_t* ua = b == 0 ? slots_dn + so : recv_up + so;
+  const uint8_t* lb = b == 0 ? recv_dn + so : slots_up + so;
+  const int n0 = *reinterpret_cast<const int32_t*>(ua), n1 = *reinterpret_cast<const int32_t*>(lb);
+  uint8_t* mine = out + (size_t)(base + j) * out_width;
+  uint8_t* theirs = other + (size_t)j * out_width;
+  int w0, w1;
+  rec_pair_apply(ua + 4, n0, lb + 4, n1, ev.k[j], b == 0 ? seed_dn : seed_up, call, (uint32_t)ev.item[j],
+                 parts + (size_t)j * parts_cap * 3, lparts, meta, b == 0 ? mine : theirs, b == 0 ? theirs : mine,
+                 out_width, w0, w1);
+  if (lane == 0) {
+    const int wm = b == 0 ? w0 : w1;
+    out_len[base + j] = wm < out_width ? wm : out_width;
+    out_rows[base + j] = ev.own[j];
+  }
+}
+
 // ---------------------------------------------------------------- host launchers
 namespace {
 RecCols rec_cols(uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, uintptr_t gdata, uintptr_t glen, int gw,
@@ -380,6 +551,47 @@ void halo_unpack(int m, int C, int H, int elem, uintptr_t map, uintptr_t from_up
                                                             P_<uint16_t>(from_dn));
   else
     throw std::invalid_argument("halo_unpack: element size must be 2 or 4");
+  MS_LAUNCH_CHECK();
+}
+
+
+XbEvents xb_ev(uintptr_t evbuf, int E2) {
+  int32_t* e = P_<int32_t>(evbuf);
+  return XbEvents{e, e + E2, e + 2 * E2, e + 3 * E2, e + 4 * E2, e + 5 * E2};
+}
+
+// evbuf: int32[5 * 2E + 4] (event fields, then counts; counts[3] accumulates dropped events)
+void xb_prep(int C, int H, int n, uintptr_t pos, uintptr_t idx_map, uintptr_t lens, int width, uintptr_t len_up,
+             uintptr_t len_dn, uintptr_t own1, uintptr_t ownH, uintptr_t stream) {
+  xb_prep_kernel<<<cdiv(C, 256), 256, 0, S_(stream)>>>(C, H, n, P_<int32_t>(pos), P_<int32_t>(idx_map),
+                                                        P_<int32_t>(lens), width, P_<int32_t>(len_up),
+                                                        P_<int32_t>(len_dn), P_<int32_t>(own1), P_<int32_t>(ownH));
+  MS_LAUNCH_CHECK();
+}
+
+void xb_events(int C, int E, int slot_w, double p, int kcap, uint64_t seed_dn, uint64_t seed_up, uint64_t call,
+               uintptr_t mine_dn, uintptr_t from_dn, uintptr_t mine_up, uintptr_t from_up, uintptr_t own1,
+               uintptr_t ownH, uintptr_t arena, int width, uintptr_t evbuf, uintptr_t slots_dn, uintptr_t slots_up,
+               uintptr_t stream) {
+  if (E < 1 || slot_w < 4 || slot_w % 4) throw std::invalid_argument("xb_events: bad capacity / slot width");
+  xb_events_kernel<<<1, kXbThreads, 0, S_(stream)>>>(C, E, slot_w, p, kcap, seed_dn, seed_up, call,
+                                                     P_<int32_t>(mine_dn), P_<int32_t>(from_dn), P_<int32_t>(mine_up),
+                                                     P_<int32_t>(from_up), P_<int32_t>(own1), P_<int32_t>(ownH),
+                                                     P_<uint8_t>(arena), width, xb_ev(evbuf, 2 * E),
+                                                     P_<uint8_t>(slots_dn), P_<uint8_t>(slots_up));
+  MS_LAUNCH_CHECK();
+}
+
+void xb_apply(int C, int E, int slot_w, uint64_t seed_dn, uint64_t seed_up, uint64_t call, uintptr_t evbuf,
+              uintptr_t slots_dn, uintptr_t slots_up, uintptr_t recv_dn, uintptr_t recv_up, uintptr_t parts,
+              int parts_cap, uintptr_t pair_count, uintptr_t out, int out_width, uintptr_t out_len,
+              uintptr_t out_rows, uintptr_t other, uintptr_t nres, uintptr_t stream) {
+  xb_apply_kernel<<<2 * E, 64, 0, S_(stream)>>>(C, slot_w, seed_dn, seed_up, call, xb_ev(evbuf, 2 * E),
+                                                P_<uint8_t>(slots_dn), P_<uint8_t>(slots_up), P_<uint8_t>(recv_dn),
+                                                P_<uint8_t>(recv_up), P_<int32_t>(parts), parts_cap,
+                                                pair_count ? P_<int>(pair_count) : nullptr, P_<uint8_t>(out),
+                                                out_width, P_<int32_t>(out_len), P_<int64_t>(out_rows),
+                                                P_<uint8_t>(other), P_<int>(nres));
   MS_LAUNCH_CHECK();
 }
 

@@ -143,6 +143,16 @@ void rec_unpack(int n0, int k_up, uintptr_t in_up, int up_lw, int up_gw, int k_d
                 uintptr_t stream);
 void halo_pack(int m, int C, int H, int elem, uintptr_t map, uintptr_t send_up, uintptr_t send_dn, uintptr_t stream);
 void halo_unpack(int m, int C, int H, int elem, uintptr_t map, uintptr_t from_up, uintptr_t from_dn, uintptr_t stream);
+void xb_prep(int C, int H, int n, uintptr_t pos, uintptr_t idx_map, uintptr_t lens, int width, uintptr_t len_up,
+             uintptr_t len_dn, uintptr_t own1, uintptr_t ownH, uintptr_t stream);
+void xb_events(int C, int E, int slot_w, double p, int kcap, uint64_t seed_dn, uint64_t seed_up, uint64_t call,
+               uintptr_t mine_dn, uintptr_t from_dn, uintptr_t mine_up, uintptr_t from_up, uintptr_t own1,
+               uintptr_t ownH, uintptr_t arena, int width, uintptr_t evbuf, uintptr_t slots_dn, uintptr_t slots_up,
+               uintptr_t stream);
+void xb_apply(int C, int E, int slot_w, uint64_t seed_dn, uint64_t seed_up, uint64_t call, uintptr_t evbuf,
+              uintptr_t slots_dn, uintptr_t slots_up, uintptr_t recv_dn, uintptr_t recv_up, uintptr_t parts,
+              int parts_cap, uintptr_t pair_count, uintptr_t out, int out_width, uintptr_t out_len,
+              uintptr_t out_rows, uintptr_t other, uintptr_t nres, uintptr_t stream);
 }  // namespace msd
 
 namespace {
@@ -225,6 +235,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("rec_unpack", &msd::rec_unpack);
   m.def("halo_pack", &msd::halo_pack);
   m.def("halo_unpack", &msd::halo_unpack);
+  m.def("xb_prep", &msd::xb_prep);
+  m.def("xb_events", &msd::xb_events, "strip-boundary recombination events (one workgroup, both boundaries)");
+  m.def("xb_apply", &msd::xb_apply);
   m.def("select_indices", &msd::select_indices,
         "(count, max) of an order-preserving compaction; synchronises the stream");
 }

@@ -9,35 +9,9 @@
 #include <algorithm>
 
 #include "hip_common.h"
+#include "rec_common.h"
 
 namespace msd {
-
-constexpr uint64_t kApplyStream = 0x6A09E667F3BCC909ull;
-
-constexpr int kFloydMax = 32;
-
-// k distinct sorted positions in [0, n): Floyd's algorithm + insertion sort (k <= kFloydMax).
-__device__ __forceinline__ void floyd_sorted(Philox& rng, int n, int k, int* pos) {
-  int cnt = 0;
-  for (int j = n - k; j < n; ++j) {
-    int t = (int)rng.below((uint32_t)(j + 1));
-    for (int q = 0; q < cnt; ++q)
-      if (pos[q] == t) {
-        t = j;
-        break;
-      }
-    pos[cnt++] = t;
-  }
-  for (int a = 1; a < cnt; ++a) {
-    const int v = pos[a];
-    int b = a - 1;
-    while (b >= 0 && pos[b] > v) {
-      pos[b + 1] = pos[b];
-      --b;
-    }
-    pos[b + 1] = v;
-  }
-}
 
 __device__ __forceinline__ uint8_t rand_nt(Philox& rng) {
   const char nts[4] = {'A', 'C', 'T', 'G'};
@@ -88,14 +62,6 @@ __device__ __forceinline__ int mutate_at(Philox& rng, uint8_t ch, double p_indel
   }
   lit[0] = rand_nt(rng);  // substitution
   return 1;
-}
-
-// Cooperative copy of src[a, b) to dst[w, ...) by the 64 lanes of a wave (clipped at cap).
-__device__ __forceinline__ void wave_copy(const uint8_t* src, int a, int b, uint8_t* dst, int w, int cap, int lane) {
-  for (int t = a + lane; t < b; t += 64) {
-    const int o = w + (t - a);
-    if (o < cap) dst[o] = src[t];
-  }
 }
 
 // One wavefront per selected genome: lane 0 draws the event positions and the emitted literals into
@@ -212,10 +178,7 @@ __global__ void __launch_bounds__(256) rec_count_keys_kernel(int n, const int64_
   k[i] = (int32_t)(kk > nb ? nb : kk);
 }
 
-// Recombine pair sel[j]: cut both strands at k[.] sorted positions, shuffle the k+2 parts and split
-// them at a random index into two new genomes (scratch rows 2j and 2j+1). One wavefront per pair:
-// lane 0 plans the parts (LDS for up to kFloydMax cuts, else the global `parts` scratch with
-// parts_cap entries of 3 ints), then all lanes copy them.
+// Recombine pair sel[j] (rows ca, cb of the arena) into scratch rows 2j and 2j+1 (rec_pair_apply).
 __device__ __forceinline__ void rec_apply_item(int j, const int64_t* sel, const int32_t* pairs, const int64_t* keys,
                                                const uint8_t* arena, int width, const int32_t* lens, const int32_t* k,
                                                uint64_t seed, uint64_t call, int32_t* parts, int parts_cap,
@@ -226,82 +189,10 @@ __device__ __forceinline__ void rec_apply_item(int j, const int64_t* sel, const 
   // pairs: int32 (a, b) rows, or int64 slot keys (a << 32) | b
   const int ca = keys ? (int)(keys[i] >> 32) : pairs[2 * i];
   const int cb = keys ? (int)(keys[i] & 0xFFFFFFFF) : pairs[2 * i + 1];
-  const int n0 = lens[ca], n1 = lens[cb], nb = n0 + n1;
-  const int kk = k[i];
-  int32_t* pt = kk <= kFloydMax ? lparts : parts + (size_t)j * parts_cap * 3;
-  if (lane == 0) {
-    int need = kk;
-    Philox rng(seed, call ^ kApplyStream, (uint32_t)i);
-    int np = 0;
-    auto push = [&](int src, int a0, int a1) {
-      pt[3 * np] = src; pt[3 * np + 1] = a0; pt[3 * np + 2] = a1; ++np;
-    };
-    if (need <= kFloydMax) {
-      int cuts[kFloydMax];
-      floyd_sorted(rng, nb, need, cuts);
-      int start = 0, q = 0;
-      for (; q < need && cuts[q] < n0; ++q) {
-        push(0, start, cuts[q]);
-        start = cuts[q];
-      }
-      push(0, start, n0);
-      start = 0;
-      for (; q < need; ++q) {
-        push(1, start, cuts[q] - n0);
-        start = cuts[q] - n0;
-      }
-      push(1, start, n1);
-    } else {
-      int start = 0, src = 0;
-      for (int t = 0; t < nb; ++t) {
-        if (t == n0) {  // close the last part of strand a
-          push(0, start, n0);
-          start = 0;
-          src = 1;
-        }
-        if (need > 0 && rng.below((uint32_t)(nb - t)) < (uint32_t)need) {
-          --need;
-          const int pos = src == 0 ? t : t - n0;
-          push(src, start, pos);
-          start = pos;
-        }
-      }
-      if (n0 == nb) {  // strand b empty: close strand a here
-        push(0, start, n0);
-        start = 0;
-      }
-      push(1, start, n1);
-    }
-    // Fisher-Yates shuffle of the parts
-    for (int q = np - 1; q > 0; --q) {
-      const int r = (int)rng.below((uint32_t)(q + 1));
-      for (int f = 0; f < 3; ++f) {
-        const int32_t tmp = pt[3 * q + f];
-        pt[3 * q + f] = pt[3 * r + f];
-        pt[3 * r + f] = tmp;
-      }
-    }
-    meta[0] = np;
-    meta[1] = (int)rng.below((uint32_t)np);
-  }
-  __syncthreads();
-  const int np = meta[0], split = meta[1];
-  const uint8_t* sa = arena + (size_t)ca * width;
-  const uint8_t* sb = arena + (size_t)cb * width;
-  uint8_t* o0 = out + (size_t)(2 * j) * out_width;
-  uint8_t* o1 = out + (size_t)(2 * j + 1) * out_width;
-  int w0 = 0, w1 = 0;
-  for (int q = 0; q < np; ++q) {
-    const uint8_t* src = pt[3 * q] == 0 ? sa : sb;
-    const int a0 = pt[3 * q + 1], a1 = pt[3 * q + 2];
-    if (q < split) {
-      wave_copy(src, a0, a1, o0, w0, out_width, lane);
-      w0 += a1 - a0;
-    } else {
-      wave_copy(src, a0, a1, o1, w1, out_width, lane);
-      w1 += a1 - a0;
-    }
-  }
+  int w0, w1;
+  rec_pair_apply(arena + (size_t)ca * width, lens[ca], arena + (size_t)cb * width, lens[cb], k[i], seed, call,
+                 (uint32_t)i, parts + (size_t)j * parts_cap * 3, lparts, meta, out + (size_t)(2 * j) * out_width,
+                 out + (size_t)(2 * j + 1) * out_width, out_width, w0, w1);
   if (lane == 0) {
     out_len[2 * j] = w0 < out_width ? w0 : out_width;
     out_len[2 * j + 1] = w1 < out_width ? w1 : out_width;

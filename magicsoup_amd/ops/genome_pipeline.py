@@ -163,10 +163,11 @@ def _rebuild(world, b: dict, cells: torch.Tensor, dcnt: torch.Tensor, cap: int) 
                          nprot=per, dn=dcnt)
 
 
-def _finish(world, kind: str, args: tuple, rng: tuple, b: dict, cells, dcnt, replay: dict) -> None:
-    """Have the device write {rebuilt count, op flags, row counter, selected count} into a pinned
-    host slot (one launch) and record the call as pending."""
-    slot = _m().status_write(_p(dcnt), _p(b["opflags"]), _p(b["d_rows"]), _p(b["cnt"]), _stream())
+def _finish(world, kind: str, args: tuple, rng: tuple, b: dict, cells, dcnt, replay: dict, status_cnt=None) -> None:
+    """Have the device write {rebuilt count, op flags, row counter, selected count (or the number of
+    result rows, ``status_cnt``)} into a pinned host slot (one launch) and record the call as pending."""
+    cnt = b["cnt"] if status_cnt is None else status_cnt
+    slot = _m().status_write(_p(dcnt), _p(b["opflags"]), _p(b["d_rows"]), _p(cnt), _stream())
     host = _StatusSlot(slot)
     ev = torch.cuda.Event()
     ev.record()
@@ -209,8 +210,13 @@ def point_mutations(world, p: float, p_indel: float, p_del: float) -> bool:
     return True
 
 
-def recombinate_all(world, p: float) -> bool:
-    """Device-pipeline ``recombinate_cells()`` over all cells; False for the synchronous path."""
+def recombinate_all(world, p: float, extra=None) -> bool:
+    """Device-pipeline ``recombinate_cells()`` over all cells; False for the synchronous path.
+
+    ``extra`` (strip-boundary recombination of a decomposed world, magicsoup_amd.parallel) adds
+    ``extra.rows`` result rows after the local pairs' results: ``extra.apply(pair_count, out, out_w,
+    out_len, out_rows, nres)`` writes them and the number of result rows to commit; they are
+    committed after (so they override) the local results, in the same arena / parameter passes."""
     arena = world._genomes
     n = world.n_cells
     if n < 2:
@@ -233,30 +239,37 @@ def recombinate_all(world, p: float) -> bool:
     _m().select_indices_dev(8 * n, _SEL_I32POS, _p(k), 0, _p(sel), 0, _p(b["cnt"]), st)
     _m().cap_skip(_p(b["cnt"]), pcap, gf, of, st)
     out_w = 2 * L  # a recombined genome is at most both parents
-    out = sc.get("gp_rout", 2 * pcap * out_w, torch.uint8, dev)
-    out_len = sc.get("gp_rout_len", 2 * pcap, torch.int32, dev)
-    out_rows = sc.get("gp_rout_rows", 2 * pcap, torch.int64, dev)
+    nr = 2 * pcap + (0 if extra is None else int(extra.rows))
+    out = sc.get("gp_rout", nr * out_w, torch.uint8, dev)
+    out_len = sc.get("gp_rout_len", nr, torch.int32, dev)
+    out_rows = sc.get("gp_rout_rows", nr, torch.int64, dev)
     parts_cap = K_CAP + 2
     parts = sc.get("gp_parts", pcap * parts_cap * 3, torch.int32, dev)
     _m().rec_apply(pcap, _p(b["cnt"]), _p(sel), 0, _p(keys), _p(arena.data), L, _p(arena.lens), _p(k), seed, call,
                    _p(parts), parts_cap, _p(out), out_w, _p(out_len), _p(out_rows), st)
-    # (a0, b0, a1, b1, ...) in pair order: the last result per cell wins (reference update order)
+    nres = None
+    if extra is not None:
+        nres = sc.get("gp_nres", 1, torch.int32, dev)
+        extra.apply(b["cnt"], out, out_w, out_len, out_rows, nres)
+    # (a0, b0, a1, b1, ..., extra rows) in order: the last result per cell wins (reference update order)
     mark = sc.bufs.get("arena_mark")
     if mark is None or mark.numel() < arena.n:
         mark = sc.bufs["arena_mark"] = torch.zeros(max(arena.n, 1024) * 2, dtype=torch.int64, device=dev)
         sc.bufs["arena_gen"] = 0
     gen = sc.bufs["arena_gen"] = sc.bufs.get("arena_gen", 0) + 1
-    won = sc.get("gp_won", 2 * pcap, torch.uint8, dev)
+    won = sc.get("gp_won", nr, torch.uint8, dev)
     won.zero_()
-    _m().arena_scatter(2 * pcap, _p(b["cnt"]), 2, _p(out_rows), _p(out), out_w, _p(out_len), _p(arena.data), L,
+    dn, dn_mul = (b["cnt"], 2) if nres is None else (nres, 1)
+    _m().arena_scatter(nr, _p(dn), dn_mul, _p(out_rows), _p(out), out_w, _p(out_len), _p(arena.data), L,
                        _p(arena.lens), _p(mark), int(gen), _p(won), gf, of, st)
-    q = sc.get("gp_q", 2 * pcap, torch.int64, dev)
-    _m().select_indices_dev(2 * pcap, _SEL_SET, _p(won), 0, _p(q), 0, _p(b["cnt2"]), st)
-    cells = sc.get("gp_rcells", 2 * pcap, torch.int64, dev)
-    _m().gather_dev(2 * pcap, _p(b["cnt2"]), _p(q), _p(out_rows), _p(cells), st)
-    _rebuild(world, b, cells, b["cnt2"], 2 * pcap)
+    q = sc.get("gp_q", nr, torch.int64, dev)
+    _m().select_indices_dev(nr, _SEL_SET, _p(won), 0, _p(q), 0, _p(b["cnt2"]), st)
+    cells = sc.get("gp_rcells", nr, torch.int64, dev)
+    _m().gather_dev(nr, _p(b["cnt2"]), _p(q), _p(out_rows), _p(cells), st)
+    _rebuild(world, b, cells, b["cnt2"], nr)
     _finish(world, "rec", (p,), (seed, call), b, cells, b["cnt2"],
-            {"rows": out_rows, "out": out, "out_w": out_w, "out_len": out_len, "mark": mark, "gen": gen})
+            {"rows": out_rows, "out": out, "out_w": out_w, "out_len": out_len, "mark": mark, "gen": gen,
+             "direct": nres is not None}, status_cnt=nres)
     return True
 
 
@@ -282,7 +295,10 @@ def _recommit(world, pd: _Pending) -> torch.Tensor:
     """Commit a call's results after widening the arena to the longest one; returns the cells."""
     arena = world._genomes
     r = pd.replay
-    n_res = int(pd.host[0]) if pd.kind == "mut" else 2 * int(pd.host[3])
+    if pd.kind == "mut":
+        n_res = int(pd.host[0])
+    else:  # recombination: 2 rows per pair, or the counted result rows (with strip-boundary results)
+        n_res = int(pd.host[3]) if r.get("direct") else 2 * int(pd.host[3])
     if n_res == 0:
         return torch.zeros(0, dtype=torch.long, device=arena.data.device)
     out_len = r["out_len"][:n_res]

@@ -42,6 +42,7 @@ strip boundaries placement is exactly the single-map algorithm.
 from __future__ import annotations
 
 import copy
+import math
 import random
 from pathlib import Path
 
@@ -100,12 +101,17 @@ class DistributedWorld(World):
     for its own cells (one fused integrator launch, no collectives; results then differ from a
     single-process world only where one rank would stop iterating while another continues).
 
+    ``boundary_genome_cap`` (default 2048 nt): recombination across a strip boundary (both genomes
+    of a pair straddling it) is computed on both ranks from exchanged genomes of at most this length;
+    pairs with a longer genome recombine only within a strip.
+
     Local state (``cell_positions`` in local rows ``1..H``, ``molecule_map`` / ``cell_map`` with
     halo rows) is what the kernels work on; :meth:`global_positions`, :meth:`owned_molecule_map`,
     :meth:`gather` and :meth:`scatter_from` convert to and from the global picture.
     """
 
-    def __init__(self, *args, group=None, exact_global_exit: bool = True, **kwargs):
+    def __init__(self, *args, group=None, exact_global_exit: bool = True, boundary_genome_cap: int = 2048,
+                 **kwargs):
         if not dist.is_initialized():
             raise RuntimeError("DistributedWorld needs an initialised torch.distributed process group")
         g = self.__dict__
@@ -137,6 +143,11 @@ class DistributedWorld(World):
         g["_stage"] = dist.get_backend(group) == "gloo" and torch.device(self.device).type == "cuda"
         g["_comm"] = make_comm(group, self.rank, n, self.device) if n > 1 else None
         g["migrated"] = {"divided_out": 0, "divided_in": 0, "moved_out": 0, "moved_in": 0, "rejected": 0}
+        # strip-boundary recombination: a stream per boundary shared by its two ranks, genomes up to
+        # `boundary_genome_cap` nt take part (longer ones recombine with cells of their own strip only)
+        g["_xseed"] = int(shared[0]) ^ 0x5DEECE66D
+        g["_xcall"] = 0
+        g["boundary_genome_cap"] = max(16, (int(boundary_genome_cap) + 15) // 16 * 16)
         if n > 1:
             # hooks the op layer calls (World has them as None): halo refresh before the diffusion
             # stencil, MAX of the integrator's iteration flags, SUM of the diffusion mass totals
@@ -529,13 +540,127 @@ class DistributedWorld(World):
         return super().reposition_cells(cell_idxs)
 
     # ------------------------------------------------------------------ recombination
-    @_op("recombinate_cells_strips")  # not pipeline-safe: reads genomes on the host path
+    @_op("recombinate_cells")
     def recombinate_cells(self, cell_idxs: list[int] | None = None, p: float = 1e-7):
-        """Recombination between neighbouring cells (collective), including pairs across strip
-        boundaries: a rank recombines its last-row cells with ghosts of the lower neighbour's first
-        row and returns the ghosts' new genomes to their owner."""
+        """Recombination between neighbouring cells (collective), including pairs that straddle a
+        strip boundary. For all cells (the default): both ranks of a boundary exchange its rows'
+        genome lengths, draw the boundary pairs' strand breaks from the boundary's shared stream,
+        swap the involved genomes and compute the same recombinations; each keeps its own cell's
+        result, committed after the pairs inside its strip (GPU: inside the device genome pipeline,
+        no synchronisation). ``cell_idxs``: ghost-row protocol with host round trips."""
         if self.world_size == 1:
             return super().recombinate_cells(cell_idxs, p)
+        self._reconcile()
+        if cell_idxs is not None:
+            return self._recombinate_subset(cell_idxs, p)
+        self.__dict__["_xcall"] += 1
+        if self.cell_molecules.is_cuda:
+            self._recombinate_gpu(p)
+        else:
+            self._recombinate_cpu(p)
+
+    # ------------------------------------------------------------------ strip-boundary recombination
+    def _xb_params(self, p: float):
+        """(events kept per boundary E, slot width, seed of the boundary below, of the one above,
+        call): identical on both ranks of every boundary."""
+        C, W = self.map_size, self.boundary_genome_cap
+        E = int(min(3 * C, 8 * math.ceil(3 * C * p * 2 * W) + 16))
+        mix = 0x9E3779B97F4A7C15
+
+        def bseed(upper_rank: int) -> int:
+            return (self._xseed * mix + 0xD1B54A32D192ED03 * (upper_rank + 1)) & 0xFFFFFFFFFFFFFFFF
+
+        return E, W, bseed(self.rank), bseed((self.rank - 1) % self.world_size), int(self._xcall)
+
+    def _recombinate_gpu(self, p: float) -> None:
+        from magicsoup_amd.ops import genome_pipeline, hip_ops
+        from magicsoup_amd.ops.genome_pipeline import K_CAP
+
+        x = _BoundaryRecombination(self, p, K_CAP)
+        if self.n_cells >= 2 and genome_pipeline.recombinate_all(self, p, extra=x):
+            return
+        # synchronous path (very high rates / fewer than 2 cells): local pairs, then the boundary
+        if self.n_cells >= 2:
+            changed = hip_ops.recombinate_all(self, p)
+            if changed.numel():
+                self._update_params_rows(changed)
+        x.commit_standalone()
+
+    def _recombinate_cpu(self, p: float) -> None:
+        """Same protocol with numpy streams (CPU ranks: tests and rehearsals)."""
+        from magicsoup_amd.ops.genome_pipeline import K_CAP
+
+        E, W, seed_dn, seed_up, call = self._xb_params(p)
+        C, H, n = self.map_size, self.H, self.n_cells
+        g = self._genomes
+        pos = self.cell_positions.long()
+        own = {}
+        for row in (1, H):
+            o = torch.full((C,), -1, dtype=torch.long)
+            sel = torch.nonzero(pos[:, 0] == row).flatten() if n else torch.zeros(0, dtype=torch.long)
+            o[pos[sel, 1]] = sel
+            own[row] = o
+        lens_of = lambda o: torch.where(o >= 0, g.lens[o.clamp(min=0)].long(), torch.full_like(o, -1))  # noqa: E731
+        mine_up = torch.cat([lens_of(own[1]), torch.tensor([g.width])]).to(torch.int32)
+        mine_dn = torch.cat([lens_of(own[H]), torch.tensor([g.width])]).to(torch.int32)
+        from_dn, from_up = torch.empty_like(mine_dn), torch.empty_like(mine_up)
+        self._exchange(mine_up, mine_dn, from_dn, from_up)
+        # events of the boundary below (we are its upper side, b = 0) and above (b = 1)
+        events = []
+        for b, la_row, lb_row, seed in ((0, mine_dn, from_dn, seed_dn), (1, from_up, mine_up, seed_up)):
+            wx = min(W, int(mine_dn[C]), int(from_dn[C] if b == 0 else from_up[C]))
+            ys = np.repeat(np.arange(C), 3)
+            ds = np.tile(np.array([-1, 0, 1]), C)
+            ok = (ds == 0) | ((ds == -1) & (C >= 2)) | ((ds == 1) & (C >= 3))
+            yb = (ys + ds) % C
+            la, lb = la_row[:C].numpy()[ys], lb_row[:C].numpy()[yb]
+            valid = ok & (la >= 0) & (lb >= 0) & (la <= wx) & (lb <= wx) & (la + lb > 0)
+            lam = np.where(valid, p * (la + lb), 0.0)
+            k = np.random.default_rng([seed, call]).poisson(lam)
+            k = np.minimum(np.minimum(k, K_CAP), np.maximum(la + lb, 0))
+            items = np.nonzero(valid & (k > 0))[0][:E]
+            for jb, i in enumerate(items):
+                owner = int(own[H][ys[i]]) if b == 0 else int(own[1][yb[i]])
+                events.append((b, jb, int(i), int(k[i]), owner))
+        slot = 4 + W
+        send = {b: torch.zeros(E * slot, dtype=_U8) for b in (0, 1)}
+        for b, jb, i, k, c in events:
+            L = int(g.lens[c])
+            send[b][jb * slot : jb * slot + 4] = torch.tensor([L], dtype=torch.int32).view(_U8)
+            send[b][jb * slot + 4 : jb * slot + 4 + L] = g.data[c, :L]
+        recv_dn, recv_up = torch.empty_like(send[0]), torch.empty_like(send[1])
+        self._exchange(send[1], send[0], recv_dn, recv_up)
+        # pairs inside the strip first (committed), then the boundary results override
+        changed = []
+        if n >= 2:
+            idxs = torch.arange(n)
+            pairs = world_ops.neighbors(self, idxs, idxs)
+            if pairs.size(0):
+                changed.append(world_ops.recombinations(self, pairs, p).long())
+
+        def genome(buf, jb):
+            L = int(buf[jb * slot : jb * slot + 4].view(torch.int32))
+            return buf[jb * slot + 4 : jb * slot + 4 + L].numpy().tobytes()
+
+        results = {}
+        for b, jb, i, k, c in events:
+            upper, lower = (genome(send[0], jb), genome(recv_dn, jb)) if b == 0 else (genome(recv_up, jb),
+                                                                                      genome(send[1], jb))
+            r0, r1 = _recombine_pair(upper, lower, k, np.random.default_rng([seed_dn if b == 0 else seed_up, call, i]))
+            results[c] = r0 if b == 0 else r1  # last event per cell wins
+        if results:
+            rows = sorted(results)
+            from magicsoup_amd.models.strings import pack_strings
+
+            arr, lens = pack_strings([results[r].decode("ascii") for r in rows])
+            g.set_rows(torch.tensor(rows, dtype=torch.long), torch.from_numpy(arr), torch.from_numpy(lens))
+            changed.append(torch.tensor(rows, dtype=torch.long))
+        if changed:
+            self._update_params_rows(torch.unique(torch.cat(changed)))
+
+    def _recombinate_subset(self, cell_idxs, p: float) -> None:
+        """``recombinate_cells(cell_idxs)`` (collective): a rank recombines its last-row cells with
+        ghosts of the lower neighbour's first row and returns the ghosts' new genomes to their owner."""
         dev = self.device
         n = self.n_cells
         pos = self.cell_positions
@@ -736,3 +861,105 @@ class DistributedWorld(World):
             f"DistributedWorld(map_size:{self.map_size!r},rank:{self.rank}/{self.world_size},"
             f"rows:{self.row0}..{self.row0 + self.H - 1},device:{self.device!r})"
         )
+
+
+def _recombine_pair(a: bytes, b: bytes, k: int, rng) -> tuple[bytes, bytes]:
+    """Recombination of two genomes with k strand breaks (reference rust/mutations.rs:78-154): cut
+    both strands at k sorted positions, shuffle the k + 2 parts, split at a random index."""
+    n0, nb = len(a), len(a) + len(b)
+    cuts = sorted(int(c) for c in rng.choice(nb, size=min(k, nb), replace=False)) if nb else []
+    parts, start, src = [], 0, a
+    for c in cuts:
+        if c < n0:
+            parts.append(a[start:c])
+            start = c
+    parts.append(a[start:])
+    start = 0
+    for c in cuts:
+        if c >= n0:
+            parts.append(b[start : c - n0])
+            start = c - n0
+    parts.append(b[start:])
+    order = rng.permutation(len(parts))
+    parts = [parts[o] for o in order]
+    split = int(rng.integers(0, len(parts)))
+    return b"".join(parts[:split]), b"".join(parts[split:])
+
+
+class _BoundaryRecombination:
+    """GPU side of the strip-boundary recombination (dist.hip xb_*). The constructor is the
+    collective part (lengths and event genomes exchanged, no synchronisation); :meth:`apply` writes
+    this rank's results after the strip's own pair results inside the genome pipeline."""
+
+    def __init__(self, world: DistributedWorld, p: float, kcap: int):
+        from magicsoup_amd.ops import hip_ops
+        from magicsoup_amd.ops.hip_ops import _m, _p, _scratch, _stream
+
+        self.world = w = world
+        E, W, self.seed_dn, self.seed_up, self.call = world._xb_params(p)
+        self.E, self.W = E, W
+        self.rows = 2 * E
+        C, H, n = w.map_size, w.H, w.n_cells
+        dev = w._genomes.data.device
+        sc = _scratch(w)
+        st = _stream()
+        g = w._genomes
+        R = H + 2
+        idx_map = hip_ops._index_map(w, R * C, dev)
+        hip_ops._ensure_world_layout(w)
+        _m().index_map(n, _p(w.cell_positions), C, _p(idx_map), False, st)
+        lens = sc.get("xb_lens", 4 * (C + 1), torch.int32, dev)
+        mine_up, mine_dn, from_dn, from_up = (lens[i * (C + 1) : (i + 1) * (C + 1)] for i in range(4))
+        own = sc.get("xb_own", 2 * C, torch.int32, dev)
+        _m().xb_prep(C, H, n, _p(w.cell_positions), _p(idx_map), _p(g.lens), int(g.width), _p(mine_up), _p(mine_dn),
+                     _p(own[:C]), _p(own[C:]), st)
+        w._exchange(mine_up, mine_dn, from_dn, from_up)
+        nev = 5 * 2 * E + 4
+        ev = sc.bufs.get("xb_ev")
+        if ev is None or ev.numel() != nev or ev.device != dev:
+            ev = sc.bufs["xb_ev"] = torch.zeros(nev, dtype=torch.int32, device=dev)  # counts[3]: dropped total
+        self.ev = ev
+        slot = 4 + W
+        sl = sc.get("xb_slots", 4 * E * slot, torch.uint8, dev)
+        self.slots_dn, self.slots_up, self.recv_dn, self.recv_up = (sl[i * E * slot : (i + 1) * E * slot] for i in range(4))
+        _m().xb_events(C, E, W, float(p), int(kcap), self.seed_dn, self.seed_up, self.call, _p(mine_dn), _p(from_dn),
+                       _p(mine_up), _p(from_up), _p(own[:C]), _p(own[C:]), _p(g.data), int(g.width), _p(ev),
+                       _p(self.slots_dn), _p(self.slots_up), st)
+        w._exchange(self.slots_up, self.slots_dn, self.recv_dn, self.recv_up)
+        self.parts = sc.get("xb_parts", 2 * E * (kcap + 2) * 3, torch.int32, dev)
+        self.kcap = kcap
+
+    def apply(self, pair_count, out, out_w, out_len, out_rows, nres) -> None:
+        from magicsoup_amd.ops.hip_ops import _m, _p, _scratch, _stream
+
+        other = _scratch(self.world).get("xb_other", 2 * self.E * out_w, torch.uint8, out.device)
+        _m().xb_apply(self.world.map_size, self.E, self.W, self.seed_dn, self.seed_up, self.call, _p(self.ev),
+                      _p(self.slots_dn), _p(self.slots_up), _p(self.recv_dn), _p(self.recv_up), _p(self.parts),
+                      self.kcap + 2, _p(pair_count), _p(out), int(out_w), _p(out_len), _p(out_rows), _p(other),
+                      _p(nres), _stream())
+
+    def commit_standalone(self) -> None:
+        """Synchronous commit of this rank's boundary results (when the pipeline did not run)."""
+        from magicsoup_amd.ops import hip_ops
+        from magicsoup_amd.ops.hip_ops import _scratch
+
+        w = self.world
+        dev = w._genomes.data.device
+        sc = _scratch(w)
+        out_w = 2 * self.W
+        out = sc.get("xb_out", 2 * self.E * out_w, torch.uint8, dev)
+        out_len = sc.get("xb_out_len", 2 * self.E, torch.int32, dev)
+        out_rows = sc.get("xb_out_rows", 2 * self.E, torch.int64, dev)
+        nres = sc.get("xb_nres", 1, torch.int32, dev)
+        self.apply(None, out, out_w, out_len, out_rows, nres)
+        k = int(nres.item())
+        if k == 0:
+            return
+        rows = out_rows[:k]
+        need = int(out_len[:k].max().item())
+        changed = hip_ops._arena_commit(w._genomes, rows, out.view(-1, out_w)[:k], out_len[:k], need, dedupe=True,
+                                        owner=w)
+        w._update_params_rows(torch.unique(changed))
+
+    def dropped(self) -> int:
+        return int(self.ev[-1].item())

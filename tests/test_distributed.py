@@ -201,6 +201,53 @@ def test_distributed_recombination_across_boundary():
     run_ranks(_body_recombination, 2)
 
 
+def _body_boundary_pairs(rank, ws, device="cpu", p=0.01, min_frac=0.25):
+    """Isolated pairs straddling every strip boundary (upper cell at the strip's last row, column 4j;
+    lower cell at the next strip's first row, column 4j + 1): both ranks of a boundary must compute
+    the same recombination, so every pair keeps its total genome length while the genomes change."""
+    import torch.distributed as dist
+
+    import magicsoup_amd as ms
+
+    S = 48
+    H = S // ws
+    g = ms.World(chemistry=_chem(), map_size=S, seed=2)
+    g.kill_cells()
+    pos, genomes = [], []
+    ms.set_seed(17)
+    for r in range(ws):
+        for j in range(0, S // 4):
+            pos += [(r * H + H - 1, 4 * j), ((r * H + H) % S, 4 * j + 1)]
+            genomes += [ms.random_genome(300 + 7 * j), ms.random_genome(250 + 3 * r)]
+    k = len(pos)
+    g._grow(k)
+    g._genomes.append_strings(genomes)
+    g._labels.append_strings([f"c{i}" for i in range(k)])
+    g._place(torch.arange(k), torch.tensor(pos, dtype=torch.int32))
+    g._update_params_rows(torch.arange(k))
+    from magicsoup_amd.parallel import DistributedWorld
+
+    dw = DistributedWorld(chemistry=_chem(), map_size=S, seed=30 + rank, device=device)
+    dw.scatter_from(g)
+    dw.recombinate_cells(p=p)
+    full = dw.gather()
+    if rank == 0:
+        key = {tuple(q): i for i, q in enumerate(full.cell_positions.tolist())}
+        changed = 0
+        for i in range(0, k, 2):
+            a, b = key[pos[i]], key[pos[i + 1]]
+            ga, gb = full.cell_genomes[a], full.cell_genomes[b]
+            assert len(ga) + len(gb) == len(genomes[i]) + len(genomes[i + 1]), i
+            changed += (ga, gb) != (genomes[i], genomes[i + 1])
+        assert changed >= max(1, int(min_frac * k / 2)), changed
+        _check_global(full)
+    dist.barrier()
+
+
+def test_distributed_boundary_recombination_is_symmetric():
+    run_ranks(_body_boundary_pairs, 3)
+
+
 def _body_state_roundtrip(rank, ws, statedir):
     import torch.distributed as dist
 

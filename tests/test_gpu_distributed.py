@@ -124,3 +124,10 @@ def _body_rccl_self(rank, ws):
 
 def test_native_rccl_comm_single_rank():
     run_ranks(_body_rccl_self, 1, timeout=300, backend="nccl")
+
+
+@pytest.mark.parametrize("p", [0.01, 5e-4])  # synchronous path (high rate) / device genome pipeline
+def test_gpu_boundary_recombination_is_symmetric(p):
+    from tests.test_distributed import _body_boundary_pairs
+
+    run_ranks(_body_boundary_pairs, 2, "cuda", p, 0.25 if p > 1e-3 else 0.0, timeout=300)
