@@ -139,7 +139,14 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    distributed = world_size > 1
+    # MS_VIRTUAL_STRIPS=1: one rank running the multi-rank code path (strip geometry, exchanges with
+    # itself over RCCL / gloo) -- measures the protocol overhead a rank of an N-GPU job pays
+    virtual = world_size == 1 and os.environ.get("MS_VIRTUAL_STRIPS") == "1"
+    if virtual:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+    distributed = world_size > 1 or virtual
     n_dev = torch.cuda.device_count() if torch.cuda.is_available() else 0
     backend = (os.environ.get("MS_DIST_BACKEND", "nccl") if n_dev else "gloo") if distributed else None
     if n_dev and local_rank >= n_dev:
@@ -153,12 +160,13 @@ def main():
 
         if torch.cuda.is_available() and backend == "nccl":
             torch.cuda.set_device(local_rank)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), rank=rank,
+                                    world_size=world_size)
         elif torch.cuda.is_available():
             torch.cuda.set_device(local_rank)
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, rank=rank, world_size=world_size)
         else:  # CPU rehearsal of the multi-rank path
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, rank=rank, world_size=world_size)
     device = f"cuda:{local_rank}" if torch.cuda.is_available() else "cpu"
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
@@ -176,7 +184,8 @@ def main():
     if distributed:
         from magicsoup_amd.parallel import DistributedWorld
 
-        world = DistributedWorld(chemistry=chem, map_size=a.map_size, device=device, seed=a.seed, map_dtype=mdt)
+        world = DistributedWorld(chemistry=chem, map_size=a.map_size, device=device, seed=a.seed, map_dtype=mdt,
+                                 strips=True)
     else:
         world = ms.World(chemistry=chem, map_size=a.map_size, device=device, seed=a.seed, map_dtype=mdt)
 
@@ -248,14 +257,14 @@ def main():
                 "seq_len": a.genome_size,
                 "map_size": a.map_size,
                 "cells_at_end": n_cells,
-                "parallelism": f"spatial{world_size}" if distributed else "single",
+                "parallelism": ("strips1-virtual" if virtual else f"spatial{world_size}") if distributed else "single",
             },
         }
         if distributed:
             out["config"]["ranks"] = world_size
             out["config"]["backend"] = backend
-            if backend != "nccl" or world_size > n_dev:
-                out["rehearsal"] = True  # ranks share GPUs and/or exchange over gloo: not a scaling number
+            if backend != "nccl" or world_size > n_dev or virtual:
+                out["rehearsal"] = True  # ranks share GPUs, exchange over gloo or with themselves
         print(json.dumps(out), flush=True)
     if distributed:
         torch.distributed.destroy_process_group()

@@ -111,13 +111,16 @@ class DistributedWorld(World):
     """
 
     def __init__(self, *args, group=None, exact_global_exit: bool = True, boundary_genome_cap: int = 2048,
-                 **kwargs):
+                 strips: bool | None = None, **kwargs):
         if not dist.is_initialized():
             raise RuntimeError("DistributedWorld needs an initialised torch.distributed process group")
         g = self.__dict__
         g["group"] = group
         g["rank"] = dist.get_rank(group)
         g["world_size"] = dist.get_world_size(group)
+        # strip protocol even on one rank ("virtual ranks": the rank is its own up / down neighbour,
+        # halo rows are copies of its own boundary rows = the torus wrap); default: only for > 1 rank
+        g["_strips"] = self.world_size > 1 if strips is None else bool(strips)
         map_size = kwargs.get("map_size", args[1] if len(args) > 1 else 128)
         n = self.world_size
         if map_size % n != 0 or map_size // n < 2:
@@ -141,14 +144,14 @@ class DistributedWorld(World):
             random.setstate(own)
         g["_n_pix_global"] = map_size * map_size
         g["_stage"] = dist.get_backend(group) == "gloo" and torch.device(self.device).type == "cuda"
-        g["_comm"] = make_comm(group, self.rank, n, self.device) if n > 1 else None
+        g["_comm"] = make_comm(group, self.rank, n, self.device) if self._strips else None
         g["migrated"] = {"divided_out": 0, "divided_in": 0, "moved_out": 0, "moved_in": 0, "rejected": 0}
         # strip-boundary recombination: a stream per boundary shared by its two ranks, genomes up to
         # `boundary_genome_cap` nt take part (longer ones recombine with cells of their own strip only)
         g["_xseed"] = int(shared[0]) ^ 0x5DEECE66D
         g["_xcall"] = 0
         g["boundary_genome_cap"] = max(16, (int(boundary_genome_cap) + 15) // 16 * 16)
-        if n > 1:
+        if self._strips:
             # hooks the op layer calls (World has them as None): halo refresh before the diffusion
             # stencil, MAX of the integrator's iteration flags, SUM of the diffusion mass totals
             g["_exchange_map_halo"] = self._do_exchange_map_halo
@@ -160,19 +163,19 @@ class DistributedWorld(World):
 
     # ------------------------------------------------------------------ geometry
     def _map_shape(self) -> tuple[int, int]:
-        if self.world_size == 1:
+        if not self._strips:
             return self.map_size, self.map_size
         return self.H + 2, self.map_size
 
     def _geom(self) -> tuple[int, int, int, int, int]:
         S = self.map_size
-        if self.world_size == 1:
+        if not self._strips:
             return S, S, 0, S, 1
         return self.H + 2, S, 1, self.H + 1, 0
 
     @property
     def _lo(self) -> int:
-        return 0 if self.world_size == 1 else 1
+        return 1 if self._strips else 0
 
     def global_positions(self) -> torch.Tensor:
         """Cell positions in global map coordinates (int32 (n, 2))."""
@@ -231,7 +234,7 @@ class DistributedWorld(World):
         """Refresh the molecule-map halo rows from the neighbours' boundary rows (raw buffer: a
         pending degradation factor is identical on every rank and applied by the stencil). One pack
         launch, one grouped exchange, one unpack launch."""
-        if self.world_size == 1:
+        if not self._strips:
             return
         mm = self.__dict__["_molmap"]
         m, C = int(mm.size(0)), self.map_size
@@ -245,7 +248,7 @@ class DistributedWorld(World):
         strip.halo_unpack(self, r_up, r_dn)
 
     def _exchange_occupancy(self) -> None:
-        if self.world_size == 1:
+        if not self._strips:
             return
         cm = self.cell_map.view(_U8)
         H = self.H
@@ -369,7 +372,7 @@ class DistributedWorld(World):
         Protocol (module docstring): boundary marks -> reservations -> placement rounds ->
         winners split by destination row + record headers exchanged -> one synchronisation ->
         child records exchanged and appended; exporting parents keep half their molecules."""
-        if self.world_size == 1:
+        if not self._strips:
             return super().divide_cells_t(cell_idxs)
         from magicsoup_amd.ops.hip_ops import _scratch
 
@@ -484,7 +487,7 @@ class DistributedWorld(World):
     @_op("move_cells")
     def move_cells(self, cell_idxs=None):
         """Movement (collective). Cells moving into a neighbour's boundary row migrate to it."""
-        if self.world_size == 1:
+        if not self._strips:
             return super().move_cells(cell_idxs)
         if cell_idxs is None:
             cell_idxs = torch.arange(self.n_cells, device=self.device)
@@ -548,7 +551,7 @@ class DistributedWorld(World):
         swap the involved genomes and compute the same recombinations; each keeps its own cell's
         result, committed after the pairs inside its strip (GPU: inside the device genome pipeline,
         no synchronisation). ``cell_idxs``: ghost-row protocol with host round trips."""
-        if self.world_size == 1:
+        if not self._strips:
             return super().recombinate_cells(cell_idxs, p)
         self._reconcile()
         if cell_idxs is not None:
@@ -789,7 +792,7 @@ class DistributedWorld(World):
             self.cell_divisions[:] = world.cell_divisions[mine.to(world.cell_divisions.device)].to(self.device)
             if params:
                 self._update_params_rows(new)
-        if self.world_size > 1:
+        if self._strips:
             self._do_exchange_map_halo()
 
     # ------------------------------------------------------------------ global index space

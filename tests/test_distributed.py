@@ -414,3 +414,35 @@ def _body_empty_rank(rank, ws):
 
 def test_distributed_rank_without_cells_joins_integrator_collectives():
     run_ranks(_body_empty_rank, 2, timeout=120.0)
+
+
+def _body_virtual_strips(rank, ws):
+    """One rank running the strip code path (its own up / down neighbour): the halo rows are copies
+    of its own boundary rows, i.e. the torus wrap, so physics match a plain World and the lifecycle
+    protocols (self-exchanged marks, records, boundary recombination) keep the invariants."""
+    from magicsoup_amd.parallel import DistributedWorld
+    from tests.conftest import gen_genomes
+
+    g = _global_world(map_size=16, n=70)
+    ref = _global_world(map_size=16, n=70)
+    dw = DistributedWorld(chemistry=_chem(), map_size=16, seed=5, strips=True)
+    assert dw.H == 16 and dw._strips
+    dw.scatter_from(g)
+    for w in (ref, dw):
+        w.diffuse_molecules()
+        w.enzymatic_activity()
+    assert torch.allclose(dw.owned_molecule_map(), ref.molecule_map, rtol=1e-5, atol=1e-5)
+    dw.spawn_cells(gen_genomes(40, 200))
+    for _ in range(4):
+        dw.divide_cells(list(range(dw.n_cells)))
+        dw.recombinate_cells(p=1e-3)
+        dw.mutate_cells(p=1e-3)
+        dw.move_cells()
+        dw.diffuse_molecules()
+        _check_local(dw)
+        dw.kill_cells(list(range(0, dw.n_cells, 4)))
+    _check_global(dw.gather())
+
+
+def test_one_rank_virtual_strips():
+    run_ranks(_body_virtual_strips, 1)
