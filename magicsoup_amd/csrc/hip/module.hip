@@ -20,6 +20,10 @@ void split_cells(int k, int m, uintptr_t parents, uintptr_t children, uintptr_t 
 void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, bool vacate,
                   uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result, int rounds,
                   uint64_t seed, uint64_t call, uintptr_t stream);
+void place_rounds_mask(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, bool vacate,
+                       uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result,
+                       int rounds, uint64_t seed, uint64_t call, uintptr_t stream);
+void set_place_mode(int mode);
 void neighbor_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map, uintptr_t keys,
                     uintptr_t stream);
 void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
@@ -192,6 +196,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("pickup", &msd::pickup);
   m.def("spill_free_mask", &msd::spill_free_mask);
   m.def("place_rounds", &msd::place_rounds);
+  m.def("place_rounds_mask", &msd::place_rounds_mask, "cooperative placement over cells selected by a mask");
+  m.def("set_place_mode", &msd::set_place_mode, "0 cooperative single launch (default), 1 multi-launch rounds");
   m.def("split_cells", &msd::split_cells);
   m.def("permeate", &msd::permeate);
   m.def("claim_free", &msd::claim_free);

@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(256) place_collect_kernel(int k, const int64_t
   if (i >= k) return;
   const long long w = wins[i];
   const long long px = result[w];
-  par[i] = cells[w];
+  par[i] = cells ? cells[w] : w;
   npos[2 * i] = (int32_t)(px / C);
   npos[2 * i + 1] = (int32_t)(px - (px / C) * C);
 }
@@ -196,6 +196,108 @@ __global__ void __launch_bounds__(1024) place_rounds_wg_kernel(int k, const int6
   for (int i = threadIdx.x; i < k; i += blockDim.x) {
     const long long px = cand[i];
     if (px >= 0) atomicCAS(claim + px, i, kNoClaim);
+  }
+}
+
+
+// All placement rounds in ONE cooperative launch (co-resident workgroups, grid barriers between the
+// phases of a round) with an early exit once no cell is left pending: same bids / priorities / RNG
+// streams as place_bid / place_resolve. A winner's pixel becomes occupied, so no later bid targets
+// it and its claim can stay set until the final reset (no reset phase between rounds): two grid
+// barriers per round. The list is `cells` (list position = priority) or, with cells == nullptr,
+// cell i itself for i < k with `mask[i]` selecting the cells that take part (divide_cells(mask):
+// no index compaction and no host round trip before placement).
+// ctl: unsigned[2 + kMaxRounds], zeroed before the launch (barrier counter, pending per round,
+// barrier-timeout error word).
+constexpr int kMaxRounds = 16;
+
+// Grid-wide barrier of a cooperative launch. Every thread fences at agent scope on both sides, so
+// plain stores of one phase are visible to plain loads of the next one on every XCD (the L2s of the
+// XCDs are not coherent with each other for ordinary device memory).
+__device__ __forceinline__ void grid_barrier(unsigned* ctr, unsigned nblocks, unsigned& phase) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned target = (++phase) * nblocks;
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    // bounded spin: a barrier that never completes (it cannot with a cooperative launch) ends the
+    // wait after ~1 s instead of hanging the device; the error word tells the host
+    for (long long spin = 0; __hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
+      if (spin > (1ll << 24)) {
+        __hip_atomic_store(ctr + kMaxRounds + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  __threadfence();
+}
+
+__global__ void __launch_bounds__(256) place_rounds_coop_kernel(int k, const int64_t* cells, const uint8_t* mask,
+                                                                const int32_t* pos, Geom g, bool vacate,
+                                                                uint8_t* cell_map, uint8_t* pending, uint64_t seed,
+                                                                uint64_t call, long long* cand, int* claim,
+                                                                long long* result, int rounds, unsigned* ctl) {
+  const unsigned nb = gridDim.x;
+  const int stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned phase = 0;
+  __shared__ int s_left;
+  for (int r = 0; r < rounds; ++r) {
+    const uint64_t rc = call + ((uint64_t)r << 48);
+    for (int i = t0; i < k; i += stride) {
+      if (r == 0) {  // own items only: no barrier needed before the first bids
+        pending[i] = mask ? (mask[i] != 0) : 1;
+        result[i] = -1;
+        cand[i] = -1;
+      }
+      if (!pending[i]) continue;
+      const int c = cells ? (int)cells[i] : i;
+      long long nbh[8], fr[8];
+      const int cnt = moore(pos[2 * c], pos[2 * c + 1], g, nbh);
+      int nf = 0;
+      for (int q = 0; q < cnt; ++q)
+        if (!cell_map[nbh[q]]) fr[nf++] = nbh[q];
+      if (nf == 0) {
+        pending[i] = 0;
+        cand[i] = -1;
+        continue;
+      }
+      Philox rng(seed, rc, (uint32_t)i);
+      const long long px = fr[rng.below((uint32_t)nf)];
+      cand[i] = px;
+      atomicMin(claim + px, i);
+    }
+    grid_barrier(ctl, nb, phase);
+    if (threadIdx.x == 0) s_left = 0;
+    __syncthreads();
+    int left = 0;
+    for (int i = t0; i < k; i += stride) {
+      if (!pending[i]) continue;
+      const long long px = cand[i];
+      if (px >= 0 && claim[px] == i) {
+        result[i] = px;
+        pending[i] = 0;
+        cell_map[px] = 1;
+        const int x = (int)(px / g.C);
+        if (vacate && (g.wrap || (x >= g.r_lo && x < g.r_hi))) {
+          const int c = cells ? (int)cells[i] : i;
+          cell_map[(size_t)pos[2 * c] * g.C + pos[2 * c + 1]] = 0;
+        }
+      } else {
+        ++left;
+      }
+    }
+    if (left) atomicAdd(&s_left, left);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_left) atomicAdd(ctl + 1 + r, (unsigned)s_left);
+    grid_barrier(ctl, nb, phase);
+    if (__hip_atomic_load(ctl + 1 + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) break;
+  }
+  // winners release their pixels' claims (losers never hold one: a pixel's claim is its winner)
+  for (int i = t0; i < k; i += stride) {
+    const long long px = result[i];
+    if (px >= 0) claim[px] = kNoClaim;
   }
 }
 
@@ -278,12 +380,62 @@ void claim_free(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uin
 }
 
 constexpr int kPlaceWgMax = 2048;  // single-workgroup rounds up to this many cells (one CU: ~2 cells per thread)
+constexpr int kCoopBlocks = 128;   // co-resident workgroups of the cooperative placement (256 CUs)
+static int g_place_mode = 0;       // 0 cooperative, 1 multi-launch rounds (A/B, set_place_mode)
+static unsigned* g_place_ctl = nullptr;
+void set_place_mode(int mode) { g_place_mode = mode; }
+
+// Cooperative placement over `cells` (k entries) or over cells 0..k-1 selected by `mask`; returns
+// false if the device refused the cooperative launch (the caller falls back to the rounds path).
+static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, const Geom& g, bool vacate,
+                       uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result,
+                       int rounds, uint64_t seed, uint64_t call, hipStream_t s) {
+  if (!g_place_ctl) MS_HIP_CHECK(hipMalloc((void**)&g_place_ctl, (2 + kMaxRounds) * sizeof(unsigned)));
+  MS_HIP_CHECK(hipMemsetAsync(g_place_ctl, 0, (2 + kMaxRounds) * sizeof(unsigned), s));
+  int kk = k;
+  const int64_t* cp = cells ? P_<int64_t>(cells) : nullptr;
+  const uint8_t* mp = mask ? P_<uint8_t>(mask) : nullptr;
+  const int32_t* pp = P_<int32_t>(pos);
+  uint8_t* cm = P_<uint8_t>(cell_map);
+  uint8_t* pend = P_<uint8_t>(pending);
+  long long* cd = P_<long long>(cand);
+  int* cl = P_<int>(claim);
+  long long* res = P_<long long>(result);
+  int rr = std::min(rounds, kMaxRounds);
+  unsigned* ctl = g_place_ctl;
+  Geom gg = g;
+  bool vac = vacate;
+  void* args[] = {&kk, &cp, &mp, &pp, &gg, &vac, &cm, &pend, &seed, &call, &cd, &cl, &res, &rr, &ctl};
+  const unsigned grid = std::min<unsigned>(cdiv(k, 256), kCoopBlocks);
+  const hipError_t e = hipLaunchCooperativeKernel((const void*)place_rounds_coop_kernel, dim3(grid), dim3(256), args,
+                                                  0, s);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();  // clear the sticky launch error; fall back
+    return false;
+  }
+  return true;
+}
+
+// Placement with a participation mask instead of a cell list (cells 0..n-1, priority = index).
+void place_rounds_mask(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, bool vacate,
+                       uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result,
+                       int rounds, uint64_t seed, uint64_t call, uintptr_t stream) {
+  if (n <= 0) return;
+  const Geom g = geom(R, C, r_lo, r_hi, wrap);
+  if (!place_coop(n, 0, mask, pos, g, vacate, cell_map, pending, cand, claim, result, rounds, seed, call, S_(stream)))
+    throw std::runtime_error("place_rounds_mask: cooperative launch refused");
+}
 
 void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, bool vacate,
                   uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result, int rounds,
                   uint64_t seed, uint64_t call, uintptr_t stream) {
   if (k <= 0) return;
   const Geom g = geom(R, C, r_lo, r_hi, wrap);
+  if (g_place_mode == 0 &&
+      place_coop(k, cells, 0, pos, g, vacate, cell_map, pending, cand, claim, result, rounds, seed, call, S_(stream)))
+    return;
+  MS_HIP_CHECK(hipMemsetAsync(P_<uint8_t>(pending), 1, (size_t)k, S_(stream)));
+  MS_HIP_CHECK(hipMemsetAsync(P_<long long>(result), 0xFF, (size_t)k * sizeof(long long), S_(stream)));
   if (k <= kPlaceWgMax) {
     place_rounds_wg_kernel<<<1, 1024, 0, S_(stream)>>>(k, P_<int64_t>(cells), P_<int32_t>(pos), g, vacate,
                                                        P_<uint8_t>(cell_map), P_<uint8_t>(pending), seed, call,
@@ -308,7 +460,7 @@ void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo,
 void place_collect(int k, uintptr_t wins, uintptr_t cells, uintptr_t result, int C, uintptr_t par, uintptr_t npos,
                    uintptr_t stream) {
   if (k <= 0) return;
-  place_collect_kernel<<<cdiv(k, 256), 256, 0, S_(stream)>>>(k, P_<int64_t>(wins), P_<int64_t>(cells),
+  place_collect_kernel<<<cdiv(k, 256), 256, 0, S_(stream)>>>(k, P_<int64_t>(wins), cells ? P_<int64_t>(cells) : nullptr,
                                                               P_<long long>(result), C, P_<int64_t>(par),
                                                               P_<int32_t>(npos));
   MS_LAUNCH_CHECK();

@@ -514,11 +514,19 @@ class World:
     @_op("divide_cells")
     def divide_cells_t(self, cell_idxs) -> tuple[torch.Tensor, torch.Tensor]:
         """Tensor form of :meth:`divide_cells`: (parents, children) long tensors."""
-        idxs = self._idx_tensor(cell_idxs)
         empty = torch.zeros(0, dtype=torch.long, device=self.device)
-        if idxs.numel() == 0:
-            return empty, empty
-        parents, child_pos = world_ops.divide_placement(self, idxs)
+        if (isinstance(cell_idxs, torch.Tensor) and cell_idxs.dtype == torch.bool and cell_idxs.is_cuda
+                and cell_idxs.numel() == self.n_cells and self.n_cells > 0):
+            # mask on the GPU: placement over the mask (priority = cell index, as for the ascending
+            # index list), one synchronisation for the winners
+            from magicsoup_amd.ops import hip_ops
+
+            parents, child_pos = hip_ops.divide_placement_mask(self, cell_idxs)
+        else:
+            idxs = self._idx_tensor(cell_idxs)
+            if idxs.numel() == 0:
+                return empty, empty
+            parents, child_pos = world_ops.divide_placement(self, idxs)
         k = int(parents.numel())
         if k == 0:
             return empty, empty

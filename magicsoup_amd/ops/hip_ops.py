@@ -398,12 +398,18 @@ def free_positions(world, k: int) -> torch.Tensor:
 _PLACE_ROUNDS = 8
 
 
-def place_rounds_raw(world, cells: torch.Tensor, vacate: bool = False, rounds: int = _PLACE_ROUNDS) -> torch.Tensor:
+def place_rounds_raw(world, cells: torch.Tensor | None, vacate: bool = False, rounds: int = _PLACE_ROUNDS,
+                     mask: torch.Tensor | None = None) -> torch.Tensor:
     """Priority-ordered parallel neighbour claims resolved on the device (atomicMin per pixel, see
-    world.hip place_rounds): the claimed pixel per cell of ``cells`` (int64, -1 = none), no sync."""
+    world.hip place_rounds): the claimed pixel per entry of ``cells`` (int64, -1 = none), or per
+    cell 0..n-1 with ``mask`` (bool / uint8, the cells that take part), no sync."""
     R, C, r_lo, r_hi, wrap = geom(world)
-    dev = cells.device
-    k = int(cells.numel())
+    if mask is not None:
+        mask = mask.view(torch.uint8) if mask.dtype == torch.bool else mask.to(torch.uint8)
+        mask = mask.contiguous()
+        dev, k = mask.device, int(mask.numel())
+    else:
+        dev, k = cells.device, int(cells.numel())
     _ensure_world_layout(world)
     pos = world.cell_positions
     cmap = _cell_map_bytes(world)
@@ -412,14 +418,17 @@ def place_rounds_raw(world, cells: torch.Tensor, vacate: bool = False, rounds: i
     if claim is None or claim.numel() != R * C or claim.device != dev:
         claim = torch.full((R * C,), 0x7FFFFFFF, dtype=torch.int32, device=dev)
         world.__dict__["_claim_map"] = claim
+    # pending / result are initialised by the kernels (cooperative) or by the launcher (fallback)
     pending = sc.get("pl_pending", k, torch.uint8, dev)
-    pending.fill_(1)
     cand = sc.get("pl_cand", k, torch.int64, dev)
     result = sc.get("pl_result", k, torch.int64, dev)
-    result.fill_(-1)
     seed, call = _rng()
-    _m().place_rounds(k, _p(cells), _p(pos), R, C, r_lo, r_hi, wrap, bool(vacate), _p(cmap), _p(pending), _p(cand),
-                      _p(claim), _p(result), int(rounds), seed, call, _stream())
+    if mask is not None:
+        _m().place_rounds_mask(k, _p(mask), _p(pos), R, C, r_lo, r_hi, wrap, bool(vacate), _p(cmap), _p(pending),
+                               _p(cand), _p(claim), _p(result), int(rounds), seed, call, _stream())
+    else:
+        _m().place_rounds(k, _p(cells), _p(pos), R, C, r_lo, r_hi, wrap, bool(vacate), _p(cmap), _p(pending),
+                          _p(cand), _p(claim), _p(result), int(rounds), seed, call, _stream())
     return result
 
 
@@ -439,6 +448,20 @@ def _place_rounds(world, cells: torch.Tensor, vacate: bool, rounds: int = _PLACE
 def divide_placement(world, idxs: torch.Tensor):
     parents, cpos = _place_rounds(world, idxs.to(torch.int64).contiguous(), vacate=False)
     return parents, cpos
+
+
+def divide_placement_mask(world, mask: torch.Tensor):
+    """:func:`divide_placement` for the cells selected by a boolean mask over all cells, without
+    compacting the mask first: placement runs over the mask, one synchronisation for the winners."""
+    C = geom(world)[1]
+    dev = mask.device
+    result = place_rounds_raw(world, None, mask=mask)
+    wins = select(result, "i64nonneg")[0]
+    k2 = int(wins.numel())
+    par = torch.empty(k2, dtype=torch.int64, device=dev)
+    npos = torch.empty(k2, 2, dtype=torch.int32, device=dev)
+    _m().place_collect(k2, _p(wins), 0, _p(result), C, _p(par), _p(npos), _stream())
+    return par, npos
 
 
 def move_placement(world, idxs: torch.Tensor):

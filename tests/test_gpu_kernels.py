@@ -397,6 +397,35 @@ def test_divide_placement_both_paths_keep_occupancy_consistent(n):
     assert bool((d.max(dim=1).values == 1).all())
 
 
+@pytest.mark.parametrize("n", [500, 6_000, 30_000])
+@pytest.mark.parametrize("how", ["list", "mask"])
+def test_cooperative_placement_matches_multi_launch_rounds(n, how):
+    """The single cooperative launch (grid barriers, early exit) places exactly like the per-round
+    launches (same bids, priorities and RNG streams), for index lists and for masks (divide_cells
+    with a boolean mask places over the mask without compacting it first)."""
+    out = []
+    for mode in (1, 0):
+        w = _world("cuda", map_size=512 if n > 6000 else 256, n=n, s=100)
+        sel = torch.rand(w.n_cells, device="cuda") < 0.7
+        arg = sel if how == "mask" else torch.nonzero(sel).flatten()
+        native.hip().set_place_mode(mode)
+        try:
+            ms.set_seed(99)
+            par, chi = w.divide_cells_t(arg)
+        finally:
+            native.hip().set_place_mode(0)
+        out.append((par.cpu(), w.cell_positions.cpu().clone(), w.cell_map.cpu().clone()))
+        pos = w.cell_positions.long()
+        side = w.map_size
+        assert torch.unique(pos[:, 0] * side + pos[:, 1]).numel() == w.n_cells
+        assert int(w.cell_map.sum()) == w.n_cells
+        assert par.numel() > 0.3 * n
+    if how == "list":  # same list positions -> same RNG items: bit-identical placements
+        assert torch.equal(out[0][0], out[1][0])
+        assert torch.equal(out[0][1], out[1][1])
+        assert torch.equal(out[0][2], out[1][2])
+
+
 def test_recombination_commit_on_gpu():
     """Fused recombination commit: disjoint pairs conserve their total length; a cell in several
     pairs keeps one of its results; arena lengths match the materialised strings."""
