@@ -753,7 +753,17 @@ __global__ void __launch_bounds__(kBlock) integrate_scatter_kernel(int c, int s,
 }
 
 // X (c, s) -> snapshot slot 0 with an all-zero mask, so a part kernel can start from an explicit X.
-__global__ void load_x_kernel(int c, int s, const float* X, float* snap) {
+// Both input kernels also clear the launch's flag words (zero[0..nz)) and the wide-list counter
+// (zero_wc, optional) from block 0: no separate memset launches before part 0.
+__device__ __forceinline__ void clear_words(unsigned* zero, int nz, int32_t* zero_wc) {
+  if (blockIdx.x == 0) {
+    if ((int)threadIdx.x < nz) zero[threadIdx.x] = 0u;
+    if (threadIdx.x == 0 && zero_wc) *zero_wc = 0;
+  }
+}
+
+__global__ void load_x_kernel(int c, int s, const float* X, float* snap, unsigned* zero, int nz, int32_t* zero_wc) {
+  clear_words(zero, nz, zero_wc);
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long long)c * s) return;
   const int cell = (int)(t / s), j = (int)(t - (long long)cell * s);
@@ -765,7 +775,9 @@ __global__ void load_x_kernel(int c, int s, const float* X, float* snap) {
 // LDS-limited integrator's critical path.
 __global__ void __launch_bounds__(kBlock) gather_x_kernel(int c, int s, int m, int R, int C, const float* cell_mols,
                                                           const void* molmap, int map_dtype, const float* corr,
-                                                          const int32_t* positions, float* snap) {
+                                                          const int32_t* positions, float* snap, unsigned* zero,
+                                                          int nz, int32_t* zero_wc) {
+  clear_words(zero, nz, zero_wc);
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long long)c * s) return;
   const int cell = (int)(t / s), j = (int)(t - (long long)cell * s);
@@ -950,15 +962,20 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
   unsigned* mk = P_<unsigned>(masks);
   unsigned* zero_flags = mk + ms::kEqIters * nparts;
   float* snaps[2] = {P_<float>(snap_a), P_<float>(snap_b)};
+  const bool fast_path = lists != 0 && s <= 64 && (g_integrate_mode & 8) == 0;
   if (part_begin == 0) {
-    MS_HIP_CHECK(hipMemsetAsync(mk, 0, sizeof(unsigned) * ms::kEqIters * (nparts + 1), st));
-    // part 0 input -> candidate 0 of snap_b, selected through the zero flags
+    // part 0 input -> candidate 0 of snap_b, selected through the zero flags; the same launch
+    // clears all flag words and (register path) the wide-list counter
+    const int nz = ms::kEqIters * (nparts + 1);
+    if (nz > kBlock) throw std::invalid_argument("integrate: too many parts");
+    int32_t* zwc = fast_path ? P_<int32_t>(lists) + 2 * (size_t)c + 1 : nullptr;
     if (X_io) {
-      load_x_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(c, s, P_<float>(X_io), snaps[1]);
+      load_x_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(c, s, P_<float>(X_io), snaps[1], mk, nz, zwc);
     } else {
       gather_x_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(c, s, m, R, C, P_<float>(cell_mols),
                                                                           P_<void>(molmap), map_dtype, corr,
-                                                                          P_<int32_t>(positions), snaps[1]);
+                                                                          P_<int32_t>(positions), snaps[1], mk, nz,
+                                                                          zwc);
     }
     MS_LAUNCH_CHECK();
   }
@@ -981,10 +998,9 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
   // register-resident path (default for s <= 64, integrate_item_fast): one launch per part over
   // every cell with at most G active proteins; part 0 lists the others, which a strided launch with
   // LDS slots for all P proteins (integrate_item) integrates after it
-  if (lists != 0 && s <= 64 && (g_integrate_mode & 8) == 0) {
+  if (fast_path) {
     int32_t* wl = P_<int32_t>(lists) + c;
-    int32_t* wc = P_<int32_t>(lists) + 2 * (size_t)c + 1;
-    if (part_begin == 0) MS_HIP_CHECK(hipMemsetAsync(wc, 0, sizeof(int32_t), st));
+    int32_t* wc = P_<int32_t>(lists) + 2 * (size_t)c + 1;  // cleared by the input kernel of part 0
     const int G = s <= 32 ? 32 : 64;
     const int cps = kBlock / G;
     const size_t lds_fast = (size_t)cps * (G == 32 ? fast_slot_words<32>() : fast_slot_words<64>()) * 4;

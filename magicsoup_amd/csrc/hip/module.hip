@@ -112,6 +112,8 @@ void assign_rows(int ncap, uintptr_t dn, uintptr_t cells, uintptr_t slot, uintpt
                  uintptr_t rows_out, uintptr_t flags, uintptr_t stream);
 void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t dst, uintptr_t stream);
 int count_to_host(uintptr_t dcount, uintptr_t stream);
+int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
+                         uintptr_t stream);
 void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
 int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t cnt, uintptr_t stream);
 std::tuple<long long, long long, long long, long long> status_read(int slot);
@@ -222,6 +224,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("assign_rows", &msd::assign_rows);
   m.def("gather_dev", &msd::gather_dev);
   m.def("cap_skip", &msd::cap_skip, "pipeline capacity guard: count > cap -> no-op call replayed by the host");
+  m.def("select_indices_async", &msd::select_indices_async,
+        "compaction with the count on the device and in a pinned status slot (returned); no sync");
   m.def("count_to_host", &msd::count_to_host, "device {count, max} -> pinned ring slot (returns the slot)");
   m.def("status_write", &msd::status_write, "pipeline status -> pinned ring slot (returns the slot)");
   m.def("status_read", &msd::status_read);

@@ -70,7 +70,8 @@ __global__ void __launch_bounds__(kSelThreads) select_count_kernel(long long n, 
 template <int K>
 __global__ void __launch_bounds__(kSelThreads) select_write_kernel(long long n, const void* src, const int32_t* tile_count,
                                                                    const int32_t* tile_max, int64_t* sel,
-                                                                   int64_t* rest, int32_t* host_out) {
+                                                                   int64_t* rest, int32_t* host_out,
+                                                                   long long* host64 = nullptr) {
   constexpr int W = kSelThreads / 64;
   __shared__ long long s_red[W];
   __shared__ int s_wc[kSelItems][W];
@@ -124,6 +125,12 @@ __global__ void __launch_bounds__(kSelThreads) select_write_kernel(long long n, 
     for (int q = 0; q < (int)gridDim.x; ++q) m = max(m, tile_max[q]);
     host_out[0] = total;
     host_out[1] = m;
+    if (host64) {  // also into a pinned status slot (select_indices_async)
+      host64[0] = total;
+      host64[1] = m;
+      host64[2] = 0;
+      host64[3] = 0;
+    }
   }
 }
 
@@ -357,6 +364,58 @@ std::tuple<long long, long long, long long, long long> status_read(int slot) {
   const long long* v = g_status + slot * 4;
   if (v[0] < 0) throw std::runtime_error("status_read: slot not written (event not complete?)");
   return {v[0], v[1], v[2], v[3]};
+}
+
+// select_indices_dev whose last tile also writes {count, max} into a fresh pinned status slot
+// (returned): the host launches the work that depends on the count with `out_dev` as device count
+// and reads the slot after one stream synchronisation (no separate copy launch).
+int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
+                         uintptr_t stream) {
+  if (!g_status) {
+    MS_HIP_CHECK(hipHostMalloc((void**)&g_status, kStatusSlots * 4 * sizeof(long long),
+                               hipHostMallocMapped | hipHostMallocCoherent));
+    MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_status_dev, g_status, 0));
+  }
+  const int slot = g_status_next;
+  g_status_next = (g_status_next + 1) % kStatusSlots;
+  for (int i = 0; i < 4; ++i) g_status[slot * 4 + i] = -1;
+  long long* h64 = g_status_dev + slot * 4;
+  hipStream_t s = S_(stream);
+  if (n <= 0) {
+    MS_HIP_CHECK(hipMemsetAsync(P_<int32_t>(out_dev), 0, 2 * sizeof(int32_t), s));
+    count_to_host_kernel<<<1, 1, 0, s>>>(P_<int>(out_dev), h64);
+    MS_LAUNCH_CHECK();
+    return slot;
+  }
+  if (n >= (1ll << 40)) throw std::invalid_argument("select_indices_async: n too large");
+  const long long tiles = (n + kSelTile - 1) / kSelTile;
+  if (tiles > g_tiles_cap) {
+    if (g_tiles) {
+      MS_HIP_CHECK(hipStreamSynchronize(s));
+      MS_HIP_CHECK(hipFree(g_tiles));
+    }
+    g_tiles_cap = std::max(tiles, 256ll);
+    MS_HIP_CHECK(hipMalloc((void**)&g_tiles, 2 * g_tiles_cap * sizeof(int32_t)));
+  }
+  const void* sp = reinterpret_cast<const void*>(src);
+  int32_t* tc = g_tiles;
+  int32_t* tm = g_tiles + g_tiles_cap;
+  int32_t* out = P_<int32_t>(out_dev);
+#define MS_SEL(K)                                                                                                \
+  select_count_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, nullptr, tc, tm);                      \
+  MS_LAUNCH_CHECK();                                                                                             \
+  select_write_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, tc, tm, P_<int64_t>(sel),              \
+                                                                 rest ? P_<int64_t>(rest) : nullptr, out, h64);  \
+  MS_LAUNCH_CHECK();
+  switch (kind) {
+    case kMaskSet: MS_SEL(kMaskSet) break;
+    case kMaskClear: MS_SEL(kMaskClear) break;
+    case kI32Pos: MS_SEL(kI32Pos) break;
+    case kI64NonNeg: MS_SEL(kI64NonNeg) break;
+    default: throw std::invalid_argument("select_indices_async: unknown predicate");
+  }
+#undef MS_SEL
+  return slot;
 }
 
 void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t dst, uintptr_t stream) {

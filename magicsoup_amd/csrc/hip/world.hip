@@ -211,18 +211,19 @@ __global__ void __launch_bounds__(1024) place_rounds_wg_kernel(int k, const int6
 // barrier-timeout error word).
 constexpr int kMaxRounds = 16;
 
-// Grid-wide barrier of a cooperative launch. Every thread fences at agent scope on both sides, so
-// plain stores of one phase are visible to plain loads of the next one on every XCD (the L2s of the
-// XCDs are not coherent with each other for ordinary device memory).
+// Grid-wide barrier of a cooperative launch. Data shared between workgroups of different XCDs
+// (their L2s are not coherent for ordinary device memory) is only touched with device-scope atomics
+// in the cooperative kernel, so the barrier needs no cache write-back / invalidation: each wave
+// waits for its own memory operations, then one thread per workgroup arrives and spins.
 __device__ __forceinline__ void grid_barrier(unsigned* ctr, unsigned nblocks, unsigned& phase) {
-  __threadfence();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned target = (++phase) * nblocks;
-    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // bounded spin: a barrier that never completes (it cannot with a cooperative launch) ends the
     // wait after ~1 s instead of hanging the device; the error word tells the host
-    for (long long spin = 0; __hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
+    for (long long spin = 0; __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
       if (spin > (1ll << 24)) {
         __hip_atomic_store(ctr + kMaxRounds + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -231,7 +232,19 @@ __device__ __forceinline__ void grid_barrier(unsigned* ctr, unsigned nblocks, un
     }
   }
   __syncthreads();
-  __threadfence();
+}
+
+// occupancy byte px of the (4-byte padded) map, read / set / cleared coherently across XCDs
+__device__ __forceinline__ unsigned map_get(const uint8_t* cell_map, long long px) {
+  const unsigned w = __hip_atomic_load(reinterpret_cast<const unsigned*>(cell_map + (px & ~3ll)), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return (w >> (8 * (px & 3))) & 0xFFu;
+}
+__device__ __forceinline__ void map_set(uint8_t* cell_map, long long px) {
+  atomicOr(reinterpret_cast<unsigned*>(cell_map + (px & ~3ll)), 1u << (8 * (px & 3)));
+}
+__device__ __forceinline__ void map_clear(uint8_t* cell_map, long long px) {
+  atomicAnd(reinterpret_cast<unsigned*>(cell_map + (px & ~3ll)), ~(0xFFu << (8 * (px & 3))));
 }
 
 __global__ void __launch_bounds__(256) place_rounds_coop_kernel(int k, const int64_t* cells, const uint8_t* mask,
@@ -257,7 +270,7 @@ __global__ void __launch_bounds__(256) place_rounds_coop_kernel(int k, const int
       const int cnt = moore(pos[2 * c], pos[2 * c + 1], g, nbh);
       int nf = 0;
       for (int q = 0; q < cnt; ++q)
-        if (!cell_map[nbh[q]]) fr[nf++] = nbh[q];
+        if (!map_get(cell_map, nbh[q])) fr[nf++] = nbh[q];
       if (nf == 0) {
         pending[i] = 0;
         cand[i] = -1;
@@ -275,14 +288,14 @@ __global__ void __launch_bounds__(256) place_rounds_coop_kernel(int k, const int
     for (int i = t0; i < k; i += stride) {
       if (!pending[i]) continue;
       const long long px = cand[i];
-      if (px >= 0 && claim[px] == i) {
+      if (px >= 0 && __hip_atomic_load(claim + px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == i) {
         result[i] = px;
         pending[i] = 0;
-        cell_map[px] = 1;
+        map_set(cell_map, px);
         const int x = (int)(px / g.C);
         if (vacate && (g.wrap || (x >= g.r_lo && x < g.r_hi))) {
           const int c = cells ? (int)cells[i] : i;
-          cell_map[(size_t)pos[2 * c] * g.C + pos[2 * c + 1]] = 0;
+          map_clear(cell_map, (long long)pos[2 * c] * g.C + pos[2 * c + 1]);
         }
       } else {
         ++left;

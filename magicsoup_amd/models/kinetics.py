@@ -399,17 +399,21 @@ class Kinetics:
             t[to] = t[fr]
         self._restamp(ok)
 
-    def append_shared(self, from_idxs: torch.Tensor) -> None:
+    def append_shared(self, from_idxs: torch.Tensor, gathered: bool = False) -> None:
         """Append cells that share the parameter rows of cells ``from_idxs`` (children of a
         division inherit the parent's proteome; reference kinetics.py:646-665 copies the rows).
-        GPU row storage only."""
-        if int(from_idxs.numel()) == 0:
+        GPU row storage only. ``gathered``: the world's clone gather already wrote the new entries
+        (``slot_clone_pairs``)."""
+        k = int(from_idxs.numel())
+        if k == 0:
             return
         self._enter_slot_mode()
         d = self.__dict__
         slot = d["_slot"]
-        d["_slot"] = torch.cat([slot, slot[from_idxs.long()]])
-        d["_ncells"] += int(from_idxs.numel())
+        new = self._slot_append(k)
+        if not gathered:
+            torch.index_select(slot, 0, from_idxs.long(), out=new)  # `slot`: the map before growing
+        d["_ncells"] += k
 
     # ---- parameter storage ----
     # The parameters live in row-storage tensors with spare capacity; cell i's row is _slot[i]
@@ -459,12 +463,63 @@ class Kinetics:
         return self.__dict__["_slot"]
 
     def _enter_slot_mode(self) -> None:
-        """GPU: switch from dense cell-ordered rows to the cell -> row map (identity to start)."""
+        """GPU: switch from dense cell-ordered rows to the cell -> row map (identity to start). The
+        map lives in a capacity buffer (plus a spare of the same size for compactions), so the world
+        can move it together with its per-cell columns in one row gather."""
         d = self.__dict__
         if d["_slot"] is None:
             n = d["_ncells"]
-            d["_slot"] = torch.arange(n, device=self._store["N"].device)
+            dev = self._store["N"].device
+            self._slot_reserve(n, dev)
+            buf = d["_slot_buf"]
+            torch.arange(n, device=dev, out=buf[:n])
+            d["_slot"] = buf[:n]
             d["_nrows"] = n
+
+    def _slot_reserve(self, n: int, dev=None) -> None:
+        """Capacity of the slot buffers >= n (keeps the live entries)."""
+        d = self.__dict__
+        buf = d.get("_slot_buf")
+        if buf is not None and buf.numel() >= n:
+            return
+        dev = dev if dev is not None else d["_slot"].device
+        cap = max(n, int((0 if buf is None else buf.numel()) * 1.5) + 1024)
+        nb = torch.empty(cap, dtype=torch.int64, device=dev)
+        cur = d.get("_slot")
+        if cur is not None and cur.numel():
+            nb[: cur.numel()] = cur
+        d["_slot_buf"] = nb
+        d["_slot_spare"] = torch.empty(cap, dtype=torch.int64, device=dev)
+        if cur is not None:
+            d["_slot"] = nb[: cur.numel()]
+
+    def _slot_append(self, k: int) -> torch.Tensor:
+        """Grow the live slot map by k entries; returns the view of the new entries."""
+        d = self.__dict__
+        n = int(d["_slot"].numel())
+        self._slot_reserve(n + k)
+        buf = d["_slot_buf"]
+        d["_slot"] = buf[: n + k]
+        return buf[n : n + k]
+
+    def slot_compact_pairs(self, n: int) -> list:
+        """(live map, spare rows) for a world's order-preserving row gather of ``n`` cells (empty
+        when not in slot mode); adopt with ``remove_cell_params(..., gathered=True)``."""
+        d = self.__dict__
+        if d["_slot"] is None or d["_slot"].numel() != n:
+            return []
+        return [(d["_slot"], d["_slot_spare"][:n])]
+
+    def slot_clone_pairs(self, n: int, k: int) -> list:
+        """(map, map) over the first n + k entries for a world's clone gather of k new cells
+        (children at rows n..); adopt with ``append_shared(..., gathered=True)``."""
+        self._enter_slot_mode()
+        d = self.__dict__
+        if d["_slot"].numel() != n:
+            return []
+        self._slot_reserve(n + k)
+        buf = d["_slot_buf"]
+        return [(buf[: n + k], buf[: n + k])]
 
     def _sync(self) -> None:
         """Resolve pending device-pipeline updates of the owning world (no-op otherwise)."""
@@ -610,9 +665,11 @@ class Kinetics:
         d.pop("_zero_row_t", None)
         self._restamp(ok)
 
-    def remove_cell_params(self, keep: torch.Tensor, removed: torch.Tensor | None = None):
+    def remove_cell_params(self, keep: torch.Tensor, removed: torch.Tensor | None = None, gathered: bool = False):
         """Keep only the cells where ``keep`` is true (bool mask (c,)) or listed (ascending index
-        tensor), preserving their order. ``removed`` (optional) lists the other cells."""
+        tensor), preserving their order. ``removed`` (optional) lists the other cells.
+        ``gathered``: the world's compaction gather already wrote the kept map entries into the
+        spare buffer (``slot_compact_pairs``)."""
         self._sync()
         idx = torch.nonzero(keep).flatten() if keep.dtype == torch.bool else keep.to(torch.long)
         d = self.__dict__
@@ -620,8 +677,13 @@ class Kinetics:
         if idx.is_cuda:
             # only the cell -> row map is compacted; rows of removed cells (possibly shared with
             # survivors) stay until the next re-gather (_alloc_rows)
-            self._enter_slot_mode()
-            d["_slot"] = d["_slot"][idx]
+            if gathered and d["_slot"] is not None:
+                d["_slot_buf"], d["_slot_spare"] = d["_slot_spare"], d["_slot_buf"]
+            else:
+                self._enter_slot_mode()
+                torch.index_select(d["_slot"], 0, idx, out=d["_slot_spare"][:k])
+                d["_slot_buf"], d["_slot_spare"] = d["_slot_spare"], d["_slot_buf"]
+            d["_slot"] = d["_slot_buf"][:k]
             d["_ncells"] = k
             return
         self._materialize()
@@ -648,7 +710,7 @@ class Kinetics:
             # GPU row storage: the new cells share the all-zero row (a later build gives them
             # rows of their own)
             row = self._zero_row()
-            d["_slot"] = torch.cat([d["_slot"], row.expand(by_n)])
+            self._slot_append(by_n).copy_(row.expand(by_n))
             d["_ncells"] += by_n
             return
         cap = min(int(t.size(0)) for t in store.values())
@@ -714,6 +776,8 @@ class Kinetics:
             self._store[name] = t[:n].to(dev)
         self.__dict__["_nrows"] = n
         self.__dict__.pop("_spare", None)
+        self.__dict__.pop("_slot_buf", None)
+        self.__dict__.pop("_slot_spare", None)
 
     # ------------------------------------------------------------------ integration
     def integrate_signals(self, X: torch.Tensor, _reduce_mask=None) -> torch.Tensor:
@@ -834,7 +898,7 @@ class Kinetics:
         self._materialize()
         state = self.__dict__.copy()
         state["last_masks"] = []
-        for k in ("_spare", "_hip_scratch", "_owner", "_lut_cache"):
+        for k in ("_spare", "_hip_scratch", "_owner", "_lut_cache", "_slot_buf", "_slot_spare"):
             state.pop(k, None)
         n = state["_ncells"]
         state["_store_d"] = {k: v[:n].clone() for k, v in self._store.items() if k not in _PACKED}

@@ -363,13 +363,15 @@ class World:
             return
         from magicsoup_amd.ops import hip_ops
 
+        # children share their parent's parameter rows until either is re-translated: the cell ->
+        # row map is cloned in the same gather as the columns and arenas
+        slot_pairs = self.kinetics.slot_clone_pairs(n0, k)
         self._grow(k, zero=False, params=False)
         n = self.n_cells
         pairs = [(col.view(n), col.view(n)) for name, col in self._cols.items() if name != "cell_positions"]
-        pairs += self._genomes.clone_pairs(k) + self._labels.clone_pairs(k)
+        pairs += self._genomes.clone_pairs(k) + self._labels.clone_pairs(k) + slot_pairs
         hip_ops.gather_rows(pairs, k, src_rows=src, dst_rows=dst)
-        # children share their parent's parameter rows until either is re-translated
-        self.kinetics.append_shared(src)
+        self.kinetics.append_shared(src, gathered=bool(slot_pairs))
 
     def _idx_tensor(self, idxs, unique: bool = True) -> torch.Tensor:
         """Cell indices as a long tensor on the world's device (ascending and duplicate-free when
@@ -521,7 +523,12 @@ class World:
             # index list), one synchronisation for the winners
             from magicsoup_amd.ops import hip_ops
 
-            parents, child_pos = hip_ops.divide_placement_mask(self, cell_idxs)
+            def child_rows(k: int) -> torch.Tensor:  # the winners' pixels go straight to the new rows
+                n = self.n_cells
+                self._reserve(n + k)
+                return self._cols["cell_positions"].buf[n : n + k]
+
+            parents, child_pos = hip_ops.divide_placement_mask(self, cell_idxs, alloc_pos=child_rows)
         else:
             idxs = self._idx_tensor(cell_idxs)
             if idxs.numel() == 0:
@@ -535,7 +542,9 @@ class World:
         self._clone_rows(parents, children)
         if child_pos.is_cuda:
             # the placement kernels already claimed the pixels in cell_map
-            self.cell_positions[n0 : n0 + k] = child_pos
+            dst = self.cell_positions[n0 : n0 + k]
+            if dst.data_ptr() != child_pos.data_ptr():
+                dst.copy_(child_pos)
         else:
             self._place(children, child_pos)
         world_ops.split_cells(self, parents, children)
@@ -575,12 +584,14 @@ class World:
             # device-side survivor count before the one stream sync that brings it to the host
             keep_buf, dead_buf, dcount, slot = hip_ops.select_async(dead, "clear", rest=True)
             pairs = [(col.view(n), col.spare_rows(n)) for col in self._cols.values()]
-            pairs += self._genomes.compact_pairs(n) + self._labels.compact_pairs(n)
+            slot_pairs = self.kinetics.slot_compact_pairs(n)
+            pairs += self._genomes.compact_pairs(n) + self._labels.compact_pairs(n) + slot_pairs
             hip_ops.gather_rows(pairs, n, src_rows=keep_buf, dn=dcount)
             n_new = hip_ops.wait_count(slot)
             if n_new == n:
                 return  # nothing removed: the spare buffers are simply not adopted
-            self.kinetics.remove_cell_params(keep=keep_buf[:n_new], removed=dead_buf[: n - n_new])
+            self.kinetics.remove_cell_params(keep=keep_buf[:n_new], removed=dead_buf[: n - n_new],
+                                             gathered=bool(slot_pairs))
             for col in self._cols.values():
                 col.swap()
             self._genomes.commit_compact(n_new)

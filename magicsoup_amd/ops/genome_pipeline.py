@@ -155,7 +155,7 @@ def _rebuild(world, b: dict, cells: torch.Tensor, dcnt: torch.Tensor, cap: int) 
     _m().trans_check(cap, _p(dcnt), _p(counts), _p(ndom), _p(long_count), _p(per), P, D_CAP, of, st)
     store = kin._kernel_params()
     kin._enter_slot_mode()
-    slot = kin.__dict__["_slot"]
+    slot = kin._slot_tensor()
     row_cap = min(int(t.size(0)) for t in store.values())
     _m().assign_rows(cap, _p(dcnt), _p(cells), _p(slot), _p(b["d_rows"]), row_cap, _p(rows_out), of, st)
     kl = build_luts(kin, dev)

@@ -110,8 +110,7 @@ def select_async(src: torch.Tensor, kind: str, rest: bool = False):
     sel = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
     rst = torch.empty(max(n, 1), dtype=torch.int64, device=dev) if rest else None
     dcount = torch.empty(2, dtype=torch.int32, device=dev)
-    _m().select_indices_dev(n, _SEL[kind], _p(src), 0, _p(sel), _p(rst), _p(dcount), _stream())
-    slot = _m().count_to_host(_p(dcount), _stream())
+    slot = _m().select_indices_async(n, _SEL[kind], _p(src), _p(sel), _p(rst), _p(dcount), _stream())
     return sel, rst, dcount, slot
 
 
@@ -450,16 +449,18 @@ def divide_placement(world, idxs: torch.Tensor):
     return parents, cpos
 
 
-def divide_placement_mask(world, mask: torch.Tensor):
+def divide_placement_mask(world, mask: torch.Tensor, alloc_pos=None):
     """:func:`divide_placement` for the cells selected by a boolean mask over all cells, without
-    compacting the mask first: placement runs over the mask, one synchronisation for the winners."""
+    compacting the mask first: placement runs over the mask, one synchronisation for the winners.
+    ``alloc_pos(k)`` (optional) provides the int32 (k, 2) tensor the new pixels are written to (the
+    world passes the position rows of the children-to-be)."""
     C = geom(world)[1]
     dev = mask.device
     result = place_rounds_raw(world, None, mask=mask)
     wins = select(result, "i64nonneg")[0]
     k2 = int(wins.numel())
     par = torch.empty(k2, dtype=torch.int64, device=dev)
-    npos = torch.empty(k2, 2, dtype=torch.int32, device=dev)
+    npos = alloc_pos(k2) if alloc_pos is not None else torch.empty(k2, 2, dtype=torch.int32, device=dev)
     _m().place_collect(k2, _p(wins), 0, _p(result), C, _p(par), _p(npos), _stream())
     return par, npos
 
