@@ -32,11 +32,13 @@ __global__ void __launch_bounds__(256) strip_occ_kernel(int C, int H, const uint
   dn[y] = cell_map[(size_t)H * C + y] ? 1 : 0;
 }
 
-__global__ void __launch_bounds__(256) strip_div_kernel(int k, const int64_t* cells, const int32_t* pos, int C, int H,
-                                                        uint8_t* up, uint8_t* dn) {
+// dividing cells: a list (cells) or, with cells == nullptr, cells i < k with mask[i] != 0
+__global__ void __launch_bounds__(256) strip_div_kernel(int k, const int64_t* cells, const uint8_t* mask,
+                                                        const int32_t* pos, int C, int H, uint8_t* up, uint8_t* dn) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= k) return;
-  const int64_t c = cells[i];
+  if (!cells && !mask[i]) return;
+  const int64_t c = cells ? cells[i] : i;
   const int x = pos[2 * c], y = pos[2 * c + 1];
   if (x == 1) up[y] = 3;
   if (x == H) dn[y] = 3;
@@ -148,7 +150,7 @@ __global__ void __launch_bounds__(kSplitThreads) place_split_write_kernel(int k,
       if (!((bal[j][q] >> lane) & 1ull)) continue;
       const long long o = (long long)q * k + s_off[q] + s_pre[j][q][w] + __popcll(bal[j][q] & lt);
       const long long px = result[i];
-      par[o] = cells[i];
+      par[o] = cells ? cells[i] : i;
       npos[2 * o] = (int32_t)(px / C);
       npos[2 * o + 1] = (int32_t)(px - (px / C) * C);
     }
@@ -455,14 +457,16 @@ int32_t* g_split_tiles = nullptr;
 long long g_split_cap = 0;
 }  // namespace
 
-void strip_marks(int C, int H, uintptr_t cell_map, int k, uintptr_t cells, uintptr_t pos, uintptr_t up, uintptr_t dn,
-                 uintptr_t stream) {
+void strip_marks(int C, int H, uintptr_t cell_map, int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, uintptr_t up,
+                 uintptr_t dn, uintptr_t stream) {
   if (H < 2 || C < 1) throw std::invalid_argument("strip_marks: bad strip");
+  if (!cells && !mask && k > 0) throw std::invalid_argument("strip_marks: give cells or a mask");
   strip_occ_kernel<<<cdiv(C, 256), 256, 0, S_(stream)>>>(C, H, P_<uint8_t>(cell_map), P_<uint8_t>(up), P_<uint8_t>(dn));
   MS_LAUNCH_CHECK();
   if (k > 0) {
-    strip_div_kernel<<<cdiv(k, 256), 256, 0, S_(stream)>>>(k, P_<int64_t>(cells), P_<int32_t>(pos), C, H,
-                                                            P_<uint8_t>(up), P_<uint8_t>(dn));
+    strip_div_kernel<<<cdiv(k, 256), 256, 0, S_(stream)>>>(k, cells ? P_<int64_t>(cells) : nullptr,
+                                                            mask ? P_<uint8_t>(mask) : nullptr, P_<int32_t>(pos), C,
+                                                            H, P_<uint8_t>(up), P_<uint8_t>(dn));
     MS_LAUNCH_CHECK();
   }
 }
@@ -496,7 +500,8 @@ void place_split(int k, uintptr_t result, uintptr_t cells, int C, int H, uintptr
   place_split_count_kernel<<<(unsigned)tiles, kSplitThreads, 0, s>>>(k, P_<long long>(result), C, H, g_split_tiles);
   MS_LAUNCH_CHECK();
   place_split_write_kernel<<<(unsigned)tiles, kSplitThreads, 0, s>>>(
-      k, P_<long long>(result), P_<int64_t>(cells), C, H, g_split_tiles, P_<int64_t>(par), P_<int32_t>(npos),
+      k, P_<long long>(result), cells ? P_<int64_t>(cells) : nullptr, C, H, g_split_tiles, P_<int64_t>(par),
+      P_<int32_t>(npos),
       P_<int32_t>(counts), P_<int32_t>(hdr_up), P_<int32_t>(hdr_dn), lw, gw, m);
   MS_LAUNCH_CHECK();
 }

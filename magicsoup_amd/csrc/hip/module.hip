@@ -132,8 +132,8 @@ void rccl_exchange(uintptr_t comm, int up, int down, uintptr_t send_up, long lon
                    long long n_send_down, uintptr_t recv_down, long long n_recv_down, uintptr_t recv_up,
                    long long n_recv_up, uintptr_t stream);
 // dist.hip
-void strip_marks(int C, int H, uintptr_t cell_map, int k, uintptr_t cells, uintptr_t pos, uintptr_t up, uintptr_t dn,
-                 uintptr_t stream);
+void strip_marks(int C, int H, uintptr_t cell_map, int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, uintptr_t up,
+                 uintptr_t dn, uintptr_t stream);
 void strip_reserve(int C, int H, uintptr_t from_up, uintptr_t from_dn, uintptr_t cell_map, uintptr_t stream);
 void strip_clear(int C, int H, uintptr_t cell_map, uintptr_t stream);
 void place_split(int k, uintptr_t result, uintptr_t cells, int C, int H, uintptr_t par, uintptr_t npos, uintptr_t counts,

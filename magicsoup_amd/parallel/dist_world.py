@@ -376,17 +376,24 @@ class DistributedWorld(World):
             return super().divide_cells_t(cell_idxs)
         from magicsoup_amd.ops.hip_ops import _scratch
 
-        idxs = self._idx_tensor(cell_idxs)
-        k = int(idxs.numel())
         dev = self.device
         C, H, m = self.map_size, self.H, self.n_molecules
         gpu = self.cell_molecules.is_cuda
+        # GPU mask over all cells: no index compaction (and no host round trip) before placement
+        mask = None
+        if (gpu and isinstance(cell_idxs, torch.Tensor) and cell_idxs.dtype == torch.bool
+                and cell_idxs.numel() == self.n_cells and self.n_cells > 0):
+            mask = cell_idxs.to(dev).contiguous().view(_U8)
+            idxs, k = None, self.n_cells
+        else:
+            idxs = self._idx_tensor(cell_idxs)
+            k = int(idxs.numel())
         sc = _scratch(self)
         empty = torch.zeros(0, dtype=torch.long, device=dev)
         # 1. boundary bytes (occupied / dividing) to the neighbours; halo occupancy + reservations
         mk = sc.get("dv_marks", 4 * C, _U8, torch.device(dev))
         s_up, s_dn, r_dn, r_up = mk[:C], mk[C : 2 * C], mk[2 * C : 3 * C], mk[3 * C :]
-        strip.marks(self, idxs, s_up, s_dn)
+        strip.marks(self, idxs, s_up, s_dn, mask=mask)
         self._exchange(s_up, s_dn, r_dn, r_up)
         strip.reserve(self, r_up, r_dn)
         # 2. placement (claims into the halo rows are final), winners by destination, headers
@@ -394,12 +401,16 @@ class DistributedWorld(World):
         if gpu:
             from magicsoup_amd.ops import hip_ops
 
-            cells = idxs.to(torch.int64).contiguous()
+            cells = None if mask is not None else idxs.to(torch.int64).contiguous()
             kk = max(k, 1)
-            result = hip_ops.place_rounds_raw(self, cells) if k else sc.get("dv_res0", 1, torch.int64, cells.device)
-            par = sc.get("dv_par", 3 * kk, torch.int64, cells.device)
-            npos = sc.get("dv_npos", 6 * kk, torch.int32, cells.device).view(3 * kk, 2)
-            st = sc.get("dv_status", 20, torch.int32, cells.device)
+            dv = torch.device(dev)
+            if mask is not None:
+                result = hip_ops.place_rounds_raw(self, None, mask=mask)
+            else:
+                result = hip_ops.place_rounds_raw(self, cells) if k else sc.get("dv_res0", 1, torch.int64, dv)
+            par = sc.get("dv_par", 3 * kk, torch.int64, dv)
+            npos = sc.get("dv_npos", 6 * kk, torch.int32, dv).view(3 * kk, 2)
+            st = sc.get("dv_status", 20, torch.int32, dv)
             strip.split_winners_gpu(self, cells, result, par, npos, st)
             self._exchange(st[4:8], st[8:12], st[16:20], st[12:16])
             v = st.tolist()  # the one synchronisation: local winner counts + the neighbours' headers

@@ -44,14 +44,18 @@ def _cmap(world) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------------------- division: marks
-def marks(world, cells: torch.Tensor, up: torch.Tensor, dn: torch.Tensor) -> None:
+def marks(world, cells: torch.Tensor | None, up: torch.Tensor, dn: torch.Tensor, mask: torch.Tensor | None = None) -> None:
     """Bytes per column of the owned boundary rows into ``up`` (row 1) / ``dn`` (row H): 1 occupied,
-    3 occupied by one of the dividing ``cells``."""
+    3 occupied by one of the dividing ``cells`` (or, GPU, the cells selected by ``mask``)."""
     H, C = world.H, world.map_size
     cm = _cmap(world)
     if cm.is_cuda:
-        k = int(cells.numel())
-        _hip().strip_marks(C, H, _p(cm), k, _p(cells), _p(world.cell_positions), _p(up), _p(dn), _stream())
+        if mask is not None:
+            _hip().strip_marks(C, H, _p(cm), int(mask.numel()), 0, _p(mask), _p(world.cell_positions), _p(up), _p(dn),
+                               _stream())
+        else:
+            _hip().strip_marks(C, H, _p(cm), int(cells.numel()), _p(cells), 0, _p(world.cell_positions), _p(up),
+                               _p(dn), _stream())
         return
     up.copy_((cm[1] != 0).to(_U8))
     dn.copy_((cm[H] != 0).to(_U8))
@@ -93,12 +97,12 @@ def clear(world) -> None:
 
 
 # ---------------------------------------------------------------------------- division: winners
-def split_winners_gpu(world, cells: torch.Tensor, result: torch.Tensor, par: torch.Tensor, npos: torch.Tensor,
+def split_winners_gpu(world, cells: torch.Tensor | None, result: torch.Tensor, par: torch.Tensor, npos: torch.Tensor,
                       status: torch.Tensor) -> None:
     """Placement results (pixel or -1 per dividing cell) -> per class (local, up, down) the winners'
     cells ``par[c * k:]`` and pixels ``npos[c * k:]`` in list order; counts into ``status[0:3]`` and
     the outgoing headers' counts into ``status[4]`` (to up) / ``status[8]`` (to down)."""
-    k = int(cells.numel())
+    k = int(cells.numel()) if cells is not None else int(result.numel())
     _hip().place_split(k, _p(result), _p(cells), world.map_size, world.H, _p(par), _p(npos), _p(status),
                        _p(status[4:]), _p(status[8:]), int(world._labels.width), int(world._genomes.width),
                        world.n_molecules, _stream())

@@ -64,12 +64,13 @@ def _body_steps(rank, ws):
     atp = _chem().molname_2_idx["ATP"]
     tot0 = dw.owned_molecule_map().double().sum(dim=[1, 2]) + dw.cell_molecules.double().sum(0)
     dist.all_reduce(tot0)
-    for _ in range(4):
+    for it in range(4):
         dw.enzymatic_activity()
         dw.kill_cells(torch.nonzero(dw.cell_molecules[:, atp] < 1.0).flatten())
-        repl = torch.nonzero(dw.cell_molecules[:, atp] > 5.0).flatten()
-        dw.cell_molecules[repl, atp] -= 4.0
-        dw.divide_cells_t(repl)
+        repl = dw.cell_molecules[:, atp] > 5.0
+        dw.cell_molecules[:, atp] -= 4.0 * repl
+        # index list and boolean mask (placement over the mask, no compaction first)
+        dw.divide_cells_t(torch.nonzero(repl).flatten() if it % 2 else repl)
         dw.recombinate_cells(p=1e-4)
         dw.mutate_cells(p=1e-4)
         dw.degrade_molecules()
