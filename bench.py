@@ -267,6 +267,7 @@ def main():
                 out["rehearsal"] = True  # ranks share GPUs, exchange over gloo or with themselves
         print(json.dumps(out), flush=True)
     if distributed:
+        world.close()
         torch.distributed.destroy_process_group()
 
 

@@ -1,0 +1,275 @@
+// Device genome pipeline issued from C++ (magicsoup_amd/ops/genome_pipeline.py).
+//
+// mutate_cells() / recombinate_cells() over all cells run a fixed chain of ~15 dependent kernels
+// whose item counts stay on the device (draws -> selection -> apply -> arena commit -> translation
+// -> fresh parameter rows -> parameter build -> status). Issuing that chain from Python cost more
+// host time than the whole chain takes on the GPU (~180 us vs ~40 us at 6k cells), which is what a
+// rank of a multi-GPU job waits on. Here Python fills three small descriptor objects (arena and
+// counters, kinetics storage + LUTs, translation LUTs) and makes one call; the launches, scratch
+// layout and status slot are handled in C++.
+#include <pybind11/pybind11.h>
+
+#include "hip_common.h"
+
+namespace py = pybind11;
+
+namespace msd {
+
+// ---- launchers defined in the other translation units
+void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel, uintptr_t rest,
+                        uintptr_t out_dev, uintptr_t stream);
+void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
+int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t cnt, uintptr_t stream);
+void zero_rows(int cap, uintptr_t dn, long long row, uintptr_t buf, uintptr_t stream);
+void trans_check(int cap, uintptr_t dn, uintptr_t counts, uintptr_t ndom, uintptr_t long_count, uintptr_t per, int Pcap,
+                 int Dcap, uintptr_t flags, uintptr_t stream);
+void assign_rows(int ncap, uintptr_t dn, uintptr_t cells, uintptr_t slot, uintptr_t d_rows, long long row_cap,
+                 uintptr_t rows_out, uintptr_t flags, uintptr_t stream);
+void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t dst, uintptr_t stream);
+void translate_fused(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+                     uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
+                     uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t long_list,
+                     uintptr_t long_count, uintptr_t dn, uintptr_t stream);
+void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_t rows, uintptr_t vmax_w, int nw,
+                  uintptr_t km_w, int nk, uintptr_t signs, int nsg, uintptr_t hills, int nh, uintptr_t RM,
+                  uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
+                  uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
+                  uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t W, uintptr_t Q, uintptr_t overflow,
+                  uintptr_t dn, uintptr_t stream);
+void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
+               uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
+void mut_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens,
+               uintptr_t k, double p_indel, double p_del, uint64_t seed, uint64_t call, uintptr_t out, int out_width,
+               uintptr_t out_len, uintptr_t stream);
+void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
+                    uintptr_t tot, int kcap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
+void rec_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t pairs, uintptr_t keys, uintptr_t arena, int width,
+               uintptr_t lens, uintptr_t k, uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out,
+               int out_width, uintptr_t out_len, uintptr_t out_rows, uintptr_t stream);
+void arena_scatter(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t src, int src_width, uintptr_t src_len,
+                   uintptr_t arena, int width, uintptr_t lens, uintptr_t mark, uint64_t gen, uintptr_t flags,
+                   uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
+
+// ---- descriptors filled from Python
+struct GpArena {  // genome arena + the pipeline's device counters
+  uintptr_t data = 0, lens = 0;
+  int width = 0, n = 0;
+  uintptr_t cnt = 0, cnt2 = 0, opflags = 0, gflags = 0, d_rows = 0;
+};
+struct GpGen {  // translation LUTs (Genetics.device_luts)
+  uintptr_t small = 0, dom_type = 0, two_codon = 0;
+  int dt_entries = 0, dom_size = 0, dom_type_size = 0;
+};
+struct GpKin {  // parameter storage (capacity rows) + token LUTs + cell -> row map
+  uintptr_t N = 0, Nf = 0, Nb = 0, A = 0, Kmr = 0, Kmf = 0, Kmb = 0, Vmax = 0, Ke = 0;
+  uintptr_t W = 0, Q = 0, overflow = 0, slot = 0;
+  int P = 0, s = 0;
+  long long row_cap = 0;
+  uintptr_t vmax = 0, km = 0, signs = 0, hills = 0, react = 0, trnsp = 0, eff = 0, energies = 0;
+  int nw = 0, nk = 0, nsg = 0, nh = 0, nv = 0;
+  float abs_temp = 0.f, gas = 0.f;
+};
+
+namespace {
+constexpr int kSelI32Pos = 2, kSelSet = 0;
+
+// bump allocator over one scratch blob (256-byte aligned pieces)
+struct Carve {
+  uintptr_t base;
+  size_t off = 0;
+  explicit Carve(uintptr_t b) : base(b) {}
+  uintptr_t take(size_t bytes) {
+    off = (off + 255) & ~size_t(255);
+    const uintptr_t p = base + off;
+    off += bytes;
+    return p;
+  }
+};
+
+// translation + fresh rows + parameter build for cells[:*dcnt] (genome_pipeline._rebuild)
+size_t rebuild_bytes(int cap, int P, int dcap) {
+  Carve c(0);
+  c.take(8 * (size_t)cap);                        // counts (2 per cell)
+  c.take(8 * (size_t)cap);                        // ndom
+  c.take(4 * (size_t)cap);                        // long list
+  c.take(16);                                     // long count
+  c.take(4 * (size_t)cap);                        // proteins per cell
+  c.take(4 * (size_t)cap);                        // rows out
+  c.take(4 * (size_t)cap * P * dcap * 5);         // tokens
+  return c.off + 256;
+}
+
+void rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const GpGen& g, const GpKin& k, int dcap,
+             Carve& c, hipStream_t s) {
+  const uintptr_t st = reinterpret_cast<uintptr_t>(s);
+  const uintptr_t counts = c.take(8 * (size_t)cap), ndom = c.take(8 * (size_t)cap);
+  const uintptr_t long_list = c.take(4 * (size_t)cap), long_count = c.take(16);
+  const uintptr_t per = c.take(4 * (size_t)cap), rows_out = c.take(4 * (size_t)cap);
+  const uintptr_t tokens = c.take(4 * (size_t)cap * k.P * dcap * 5);
+  MS_HIP_CHECK(hipMemsetAsync(reinterpret_cast<void*>(long_count), 0, sizeof(int32_t), s));
+  zero_rows(cap, dcnt, (long long)k.P * dcap * 5, tokens, st);
+  translate_fused(cap, cells, a.data, a.width, a.lens, g.small, g.dom_type, g.dt_entries, g.two_codon, g.dom_size,
+                  g.dom_type_size, counts, ndom, k.P, dcap, tokens, long_list, long_count, dcnt, st);
+  trans_check(cap, dcnt, counts, ndom, long_count, per, k.P, dcap, a.opflags, st);
+  assign_rows(cap, dcnt, cells, k.slot, a.d_rows, k.row_cap, rows_out, a.opflags, st);
+  build_params(cap, k.P, dcap, k.P, k.s, tokens, rows_out, k.vmax, k.nw, k.km, k.nk, k.signs, k.nsg, k.hills, k.nh,
+               k.react, k.trnsp, k.eff, k.nv, k.energies, k.abs_temp, k.gas, k.N, k.Nf, k.Nb, k.A, k.Kmr, k.Kmf, k.Kmb,
+               k.Vmax, k.Ke, per, k.W, k.Q, k.overflow, dcnt, st);
+}
+}  // namespace
+
+// Scratch bytes of one call (the caller passes a blob of at least this size; the blob must stay
+// untouched until the call was reconciled: it holds the results a replay may re-commit).
+size_t gp_blob_bytes(int kind, int n, int cap, int P, int L, int dcap, int kcap, int extra_rows) {
+  Carve c(0);
+  if (kind == 0) {  // mutations
+    const int out_w = (L + kcap + 15) / 16 * 16;
+    c.take(4 * (size_t)n);                 // k
+    c.take(8 * (size_t)n);                 // sel
+    c.take((size_t)cap * out_w);           // out
+    c.take(4 * (size_t)cap);               // out_len
+    return c.off + rebuild_bytes(cap, P, dcap) + 512;
+  }
+  // recombinations: cap = pairs capacity
+  const int nr = 2 * cap + extra_rows, out_w = 2 * L;
+  c.take(4 * 8 * (size_t)n);               // k per slot
+  c.take(8 * 8 * (size_t)n);               // sel
+  c.take((size_t)nr * out_w);              // out
+  c.take(4 * (size_t)nr);                  // out_len
+  c.take(8 * (size_t)nr);                  // out_rows
+  c.take(4 * (size_t)cap * (kcap + 2) * 3);  // parts
+  c.take((size_t)nr);                      // won
+  c.take(8 * (size_t)nr);                  // q
+  c.take(8 * (size_t)nr);                  // cells
+  return c.off + rebuild_bytes(nr, P, dcap) + 512;
+}
+
+// Offsets of the pieces a reconcile may need: mutations {sel, out, out_len}; recombinations
+// {out_rows, out, out_len, cells}.
+py::dict gp_layout(int kind, int n, int cap, int L, int kcap, int extra_rows) {
+  Carve c(0);
+  py::dict d;
+  if (kind == 0) {
+    const int out_w = (L + kcap + 15) / 16 * 16;
+    c.take(4 * (size_t)n);
+    d["sel"] = c.take(8 * (size_t)n);
+    d["out"] = c.take((size_t)cap * out_w);
+    d["out_len"] = c.take(4 * (size_t)cap);
+    d["out_w"] = out_w;
+    return d;
+  }
+  const int nr = 2 * cap + extra_rows, out_w = 2 * L;
+  c.take(4 * 8 * (size_t)n);
+  c.take(8 * 8 * (size_t)n);
+  d["out"] = c.take((size_t)nr * out_w);
+  d["out_len"] = c.take(4 * (size_t)nr);
+  d["out_rows"] = c.take(8 * (size_t)nr);
+  c.take(4 * (size_t)cap * (kcap + 2) * 3);
+  c.take((size_t)nr);
+  c.take(8 * (size_t)nr);
+  d["cells"] = c.take(8 * (size_t)nr);
+  d["out_w"] = out_w;
+  d["nr"] = nr;
+  return d;
+}
+
+// Per-call counter setup in one launch: op flags cleared; with a fresh chain (nothing pending) the
+// chain flags too and the device row counter set to the host's row count.
+__global__ void gp_begin_kernel(int* opflags, int* gflags, long long* d_rows, long long nrows, int fresh) {
+  *opflags = 0;
+  if (fresh) {
+    *gflags = 0;
+    *d_rows = nrows;
+  }
+}
+
+void gp_begin(const GpArena& a, bool fresh, long long nrows, uintptr_t stream) {
+  gp_begin_kernel<<<1, 1, 0, S_(stream)>>>(P_<int>(a.opflags), P_<int>(a.gflags), P_<long long>(a.d_rows), nrows,
+                                           fresh ? 1 : 0);
+  MS_LAUNCH_CHECK();
+}
+
+// mutate_cells() over all n genomes; returns the pinned status slot {rebuilt, flags, row counter, selected}.
+int gp_mutate(const GpArena& a, const GpGen& g, const GpKin& k, double p, double p_indel, double p_del, uint64_t seed,
+              uint64_t call, int cap, int kcap, int dcap, uintptr_t blob, uintptr_t stream) {
+  hipStream_t s = S_(stream);
+  const int n = a.n, L = a.width;
+  Carve c(blob);
+  const uintptr_t kk = c.take(4 * (size_t)n), sel = c.take(8 * (size_t)n);
+  const int out_w = (L + kcap + 15) / 16 * 16;
+  const uintptr_t out = c.take((size_t)cap * out_w), out_len = c.take(4 * (size_t)cap);
+  mut_count(n, 0, a.lens, p, seed, call, kk, kcap, a.gflags, a.opflags, stream);
+  select_indices_dev(n, kSelI32Pos, kk, 0, sel, 0, a.cnt, stream);
+  cap_skip(a.cnt, cap, a.gflags, a.opflags, stream);
+  mut_apply(cap, a.cnt, sel, 0, a.data, L, a.lens, kk, p_indel, p_del, seed, call, out, out_w, out_len, stream);
+  arena_scatter(cap, a.cnt, 1, sel, out, out_w, out_len, a.data, L, a.lens, 0, 0, 0, a.gflags, a.opflags, stream);
+  rebuild(cap, sel, a.cnt, a, g, k, dcap, c, s);
+  return status_write(a.cnt, a.opflags, a.d_rows, a.cnt, stream);
+}
+
+// recombinate_cells() over neighbour slot keys (8 per cell); `extra` (optional Python object with
+// .rows and .apply(pair_count, out, out_w, out_len, out_rows, nres)) appends strip-boundary results.
+int gp_recombine(const GpArena& a, const GpGen& g, const GpKin& k, uintptr_t keys, double p, uint64_t seed,
+                 uint64_t call, int cap, int kcap, int dcap, uintptr_t mark, uint64_t gen, py::object extra,
+                 uintptr_t nres, uintptr_t blob, uintptr_t stream) {
+  hipStream_t s = S_(stream);
+  const int n = a.n, L = a.width;
+  const int xr = extra.is_none() ? 0 : extra.attr("rows").cast<int>();
+  const int nr = 2 * cap + xr, out_w = 2 * L, parts_cap = kcap + 2;
+  Carve c(blob);
+  const uintptr_t kk = c.take(4 * 8 * (size_t)n), sel = c.take(8 * 8 * (size_t)n);
+  const uintptr_t out = c.take((size_t)nr * out_w), out_len = c.take(4 * (size_t)nr), out_rows = c.take(8 * (size_t)nr);
+  const uintptr_t parts = c.take(4 * (size_t)cap * parts_cap * 3);
+  const uintptr_t won = c.take((size_t)nr), q = c.take(8 * (size_t)nr), cells = c.take(8 * (size_t)nr);
+  rec_count_keys(8 * n, keys, a.lens, p, seed, call, kk, 0, kcap, a.gflags, a.opflags, stream);
+  select_indices_dev(8ll * n, kSelI32Pos, kk, 0, sel, 0, a.cnt, stream);
+  cap_skip(a.cnt, cap, a.gflags, a.opflags, stream);
+  rec_apply(cap, a.cnt, sel, 0, keys, a.data, L, a.lens, kk, seed, call, parts, parts_cap, out, out_w, out_len,
+            out_rows, stream);
+  if (xr) {
+    extra.attr("apply")(a.cnt, out, out_w, out_len, out_rows, nres);
+  }
+  MS_HIP_CHECK(hipMemsetAsync(reinterpret_cast<void*>(won), 0, (size_t)nr, s));
+  // (a0, b0, a1, b1, ..., extra rows): the last result per cell wins (reference update order)
+  arena_scatter(nr, xr ? nres : a.cnt, xr ? 1 : 2, out_rows, out, out_w, out_len, a.data, L, a.lens, mark, gen, won,
+                a.gflags, a.opflags, stream);
+  select_indices_dev(nr, kSelSet, won, 0, q, 0, a.cnt2, stream);
+  gather_dev(nr, a.cnt2, q, out_rows, cells, stream);
+  rebuild(nr, cells, a.cnt2, a, g, k, dcap, c, s);
+  return status_write(a.cnt2, a.opflags, a.d_rows, xr ? nres : a.cnt, stream);
+}
+
+void bind_gp(py::module_& m) {
+  py::class_<GpArena>(m, "GpArena")
+      .def(py::init<>())
+      .def_readwrite("data", &GpArena::data).def_readwrite("lens", &GpArena::lens)
+      .def_readwrite("width", &GpArena::width).def_readwrite("n", &GpArena::n)
+      .def_readwrite("cnt", &GpArena::cnt).def_readwrite("cnt2", &GpArena::cnt2)
+      .def_readwrite("opflags", &GpArena::opflags).def_readwrite("gflags", &GpArena::gflags)
+      .def_readwrite("d_rows", &GpArena::d_rows);
+  py::class_<GpGen>(m, "GpGen")
+      .def(py::init<>())
+      .def_readwrite("small", &GpGen::small).def_readwrite("dom_type", &GpGen::dom_type)
+      .def_readwrite("two_codon", &GpGen::two_codon).def_readwrite("dt_entries", &GpGen::dt_entries)
+      .def_readwrite("dom_size", &GpGen::dom_size).def_readwrite("dom_type_size", &GpGen::dom_type_size);
+  py::class_<GpKin>(m, "GpKin")
+      .def(py::init<>())
+      .def_readwrite("N", &GpKin::N).def_readwrite("Nf", &GpKin::Nf).def_readwrite("Nb", &GpKin::Nb)
+      .def_readwrite("A", &GpKin::A).def_readwrite("Kmr", &GpKin::Kmr).def_readwrite("Kmf", &GpKin::Kmf)
+      .def_readwrite("Kmb", &GpKin::Kmb).def_readwrite("Vmax", &GpKin::Vmax).def_readwrite("Ke", &GpKin::Ke)
+      .def_readwrite("W", &GpKin::W).def_readwrite("Q", &GpKin::Q).def_readwrite("overflow", &GpKin::overflow)
+      .def_readwrite("slot", &GpKin::slot).def_readwrite("P", &GpKin::P).def_readwrite("s", &GpKin::s)
+      .def_readwrite("row_cap", &GpKin::row_cap).def_readwrite("vmax", &GpKin::vmax).def_readwrite("km", &GpKin::km)
+      .def_readwrite("signs", &GpKin::signs).def_readwrite("hills", &GpKin::hills)
+      .def_readwrite("react", &GpKin::react).def_readwrite("trnsp", &GpKin::trnsp).def_readwrite("eff", &GpKin::eff)
+      .def_readwrite("energies", &GpKin::energies).def_readwrite("nw", &GpKin::nw).def_readwrite("nk", &GpKin::nk)
+      .def_readwrite("nsg", &GpKin::nsg).def_readwrite("nh", &GpKin::nh).def_readwrite("nv", &GpKin::nv)
+      .def_readwrite("abs_temp", &GpKin::abs_temp).def_readwrite("gas", &GpKin::gas);
+  m.def("gp_begin", &gp_begin);
+  m.def("gp_blob_bytes", &gp_blob_bytes);
+  m.def("gp_layout", &gp_layout);
+  m.def("gp_mutate", &gp_mutate, "device-pipeline point mutations over all genomes (one call, no sync)");
+  m.def("gp_recombine", &gp_recombine, "device-pipeline recombinations over neighbour slot keys (one call, no sync)");
+}
+
+}  // namespace msd

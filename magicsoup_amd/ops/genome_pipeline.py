@@ -112,12 +112,66 @@ def _begin(world, kind: str) -> dict:
         reconcile(world)
     kin = world.kinetics
     b = _bufs(world, kind)
-    if not st["pending"]:
+    fresh = not st["pending"]
+    if fresh:
         kin._reserve_rows(2 * min(world.n_cells, N_CAP))
-        b["gflags"].zero_()
-        b["d_rows"].fill_(int(kin.__dict__["_nrows"]))
-    b["opflags"].zero_()
+    _m().gp_begin(_arena_desc(world, b), fresh, int(kin.__dict__["_nrows"]), _stream())
     return b
+
+
+def _arena_desc(world, b: dict):
+    """C++ descriptor of the genome arena and this call's device counters (gp.hip GpArena)."""
+    arena = world._genomes
+    a = _m().GpArena()
+    a.data, a.lens, a.width, a.n = _p(arena.data), _p(arena.lens), int(arena.width), int(arena.n)
+    a.cnt, a.cnt2, a.opflags, a.gflags, a.d_rows = (_p(b["cnt"]), _p(b["cnt2"]), _p(b["opflags"]), _p(b["gflags"]),
+                                                    _p(b["d_rows"]))
+    return a
+
+
+def _gen_desc(world, dev):
+    g = _m().GpGen()
+    luts = world.genetics.device_luts(dev)
+    tables = world.genetics.tables
+    g.small, g.dom_type, g.two_codon = _p(luts["small"]), _p(luts["dom_type"]), _p(luts["two_codon"])
+    g.dt_entries, g.dom_size, g.dom_type_size = int(luts["dom_type"].numel()), tables.dom_size, tables.dom_type_size
+    return g
+
+
+def _kin_desc(world, dev):
+    """Parameter storage (kernel layout, capacity rows), token LUTs and the cell -> row map."""
+    from magicsoup_amd.constants import GAS_CONSTANT
+    from magicsoup_amd.ops.kinetics_ops import build_luts
+
+    kin = world.kinetics
+    store = kin._kernel_params()
+    kin._enter_slot_mode()
+    packed = kin._pack_ok()
+    lu = build_luts(kin, dev)
+    k = _m().GpKin()
+    k.N, k.Nf, k.Nb, k.A, k.Kmr = (_p(store[n]) for n in ("N", "Nf", "Nb", "A", "Kmr"))
+    k.Kmf, k.Kmb, k.Vmax, k.Ke = (_p(store[n]) for n in ("Kmf", "Kmb", "Vmax", "Ke"))
+    if packed:
+        k.W, k.Q, k.overflow = _p(store["_W"]), _p(store["_Q"]), _p(hip_ops._overflow_flag(kin))
+    k.slot = _p(kin._slot_tensor())
+    N = store["N"]
+    k.P, k.s = int(N.size(1)), int(N.size(2))
+    k.row_cap = min(int(t.size(0)) for t in store.values())
+    k.vmax, k.km, k.signs, k.hills = _p(lu["vmax"]), _p(lu["km"]), _p(lu["signs"]), _p(lu["hills"])
+    k.react, k.trnsp, k.eff, k.energies = _p(lu["react"]), _p(lu["trnsp"]), _p(lu["eff"]), _p(lu["energies"])
+    k.nw, k.nk, k.nsg, k.nh = lu["vmax"].numel(), lu["km"].numel(), lu["signs"].numel(), lu["hills"].numel()
+    k.nv = int(lu["react"].size(0))
+    k.abs_temp, k.gas = float(kin.abs_temp), float(GAS_CONSTANT)
+    return k
+
+
+def _blob(world, kind: str, nbytes: int, dev) -> torch.Tensor:
+    return _scratch(world).get(f"gp_blob_{kind}", nbytes, torch.uint8, dev)
+
+
+def _view(blob: torch.Tensor, off: int, n: int, dtype) -> torch.Tensor:
+    es = torch.empty(0, dtype=dtype).element_size()
+    return blob[off : off + n * es].view(dtype)
 
 
 def _rebuild(world, b: dict, cells: torch.Tensor, dcnt: torch.Tensor, cap: int) -> None:
@@ -175,9 +229,17 @@ def _finish(world, kind: str, args: tuple, rng: tuple, b: dict, cells, dcnt, rep
     world._genomes.version += 1
 
 
+def _record(world, kind: str, args: tuple, rng: tuple, cells, slot: int, replay: dict) -> None:
+    """Record an issued pipeline call as pending (its status lands in pinned slot ``slot``)."""
+    ev = torch.cuda.Event()
+    ev.record()
+    _state(world)["pending"].append(_Pending(kind, args, rng, cells, _StatusSlot(slot), ev, replay))
+    world._genomes.version += 1
+
+
 def point_mutations(world, p: float, p_indel: float, p_del: float) -> bool:
-    """Device-pipeline ``mutate_cells()`` over all cells; False if this call should take the
-    synchronous path instead."""
+    """Device-pipeline ``mutate_cells()`` over all cells (one C++ call issuing the chain, gp.hip);
+    False if this call should take the synchronous path instead."""
     arena = world._genomes
     n = arena.n
     if n == 0:
@@ -188,35 +250,28 @@ def point_mutations(world, p: float, p_indel: float, p_del: float) -> bool:
     dev = arena.data.device
     cap = _cap(n * p * L, min(n, N_CAP))
     b = _begin(world, "mut")
-    sc = _scratch(world)
-    k = sc.get("gp_k", n, torch.int32, dev)
-    sel = sc.get("gp_sel", n, torch.int64, dev)
+    k = _kin_desc(world, dev)
+    nbytes = _m().gp_blob_bytes(0, n, cap, k.P, L, D_CAP, K_CAP, 0)
+    blob = _blob(world, "mut", nbytes, dev)
     seed, call = _rng()
-    st = _stream()
-    _m().mut_count(n, 0, _p(arena.lens), float(p), seed, call, _p(k), K_CAP, _p(b["gflags"]), _p(b["opflags"]), st)
-    _m().select_indices_dev(n, _SEL_I32POS, _p(k), 0, _p(sel), 0, _p(b["cnt"]), st)
-    _m().cap_skip(_p(b["cnt"]), cap, _p(b["gflags"]), _p(b["opflags"]), st)
-    dcnt = b["cnt"]
-    out_w = (L + K_CAP + 15) // 16 * 16
-    out = sc.get("gp_out", cap * out_w, torch.uint8, dev)
-    out_len = sc.get("gp_out_len", cap, torch.int32, dev)
-    _m().mut_apply(cap, _p(dcnt), _p(sel), 0, _p(arena.data), L, _p(arena.lens), _p(k), float(p_indel), float(p_del),
-                   seed, call, _p(out), out_w, _p(out_len), st)
-    _m().arena_scatter(cap, _p(dcnt), 1, _p(sel), _p(out), out_w, _p(out_len), _p(arena.data), L, _p(arena.lens),
-                       0, 0, 0, _p(b["gflags"]), _p(b["opflags"]), st)
-    _rebuild(world, b, sel, dcnt, cap)
-    _finish(world, "mut", (p, p_indel, p_del), (seed, call), b, sel, dcnt,
-            {"rows": sel, "out": out, "out_w": out_w, "out_len": out_len})
+    slot = _m().gp_mutate(_arena_desc(world, b), _gen_desc(world, dev), k, float(p), float(p_indel), float(p_del),
+                          seed, call, cap, K_CAP, D_CAP, _p(blob), _stream())
+    lay = _m().gp_layout(0, n, cap, L, K_CAP, 0)
+    sel = _view(blob, lay["sel"], n, torch.int64)
+    _record(world, "mut", (p, p_indel, p_del), (seed, call), sel, slot,
+            {"rows": sel, "out": _view(blob, lay["out"], cap * lay["out_w"], torch.uint8), "out_w": lay["out_w"],
+             "out_len": _view(blob, lay["out_len"], cap, torch.int32)})
     return True
 
 
 def recombinate_all(world, p: float, extra=None) -> bool:
-    """Device-pipeline ``recombinate_cells()`` over all cells; False for the synchronous path.
+    """Device-pipeline ``recombinate_cells()`` over all cells (one C++ call, gp.hip); False for the
+    synchronous path.
 
     ``extra`` (strip-boundary recombination of a decomposed world, magicsoup_amd.parallel) adds
     ``extra.rows`` result rows after the local pairs' results: ``extra.apply(pair_count, out, out_w,
-    out_len, out_rows, nres)`` writes them and the number of result rows to commit; they are
-    committed after (so they override) the local results, in the same arena / parameter passes."""
+    out_len, out_rows, nres)`` (device pointers) writes them and the number of result rows to
+    commit; they are committed after (so they override) the local results, in the same passes."""
     arena = world._genomes
     n = world.n_cells
     if n < 2:
@@ -230,46 +285,26 @@ def recombinate_all(world, p: float, extra=None) -> bool:
     b = _begin(world, "rec")
     sc = _scratch(world)
     keys = hip_ops.neighbor_slot_keys(world)
-    k = sc.get("nb_k", 8 * n, torch.int32, dev)
-    sel = sc.get("gp_rsel", 8 * n, torch.int64, dev)
-    seed, call = _rng()
-    st = _stream()
-    gf, of = _p(b["gflags"]), _p(b["opflags"])
-    _m().rec_count_keys(8 * n, _p(keys), _p(arena.lens), float(p), seed, call, _p(k), 0, K_CAP, gf, of, st)
-    _m().select_indices_dev(8 * n, _SEL_I32POS, _p(k), 0, _p(sel), 0, _p(b["cnt"]), st)
-    _m().cap_skip(_p(b["cnt"]), pcap, gf, of, st)
-    out_w = 2 * L  # a recombined genome is at most both parents
-    nr = 2 * pcap + (0 if extra is None else int(extra.rows))
-    out = sc.get("gp_rout", nr * out_w, torch.uint8, dev)
-    out_len = sc.get("gp_rout_len", nr, torch.int32, dev)
-    out_rows = sc.get("gp_rout_rows", nr, torch.int64, dev)
-    parts_cap = K_CAP + 2
-    parts = sc.get("gp_parts", pcap * parts_cap * 3, torch.int32, dev)
-    _m().rec_apply(pcap, _p(b["cnt"]), _p(sel), 0, _p(keys), _p(arena.data), L, _p(arena.lens), _p(k), seed, call,
-                   _p(parts), parts_cap, _p(out), out_w, _p(out_len), _p(out_rows), st)
-    nres = None
-    if extra is not None:
-        nres = sc.get("gp_nres", 1, torch.int32, dev)
-        extra.apply(b["cnt"], out, out_w, out_len, out_rows, nres)
-    # (a0, b0, a1, b1, ..., extra rows) in order: the last result per cell wins (reference update order)
+    k = _kin_desc(world, dev)
+    xr = 0 if extra is None else int(extra.rows)
+    nbytes = _m().gp_blob_bytes(1, n, pcap, k.P, L, D_CAP, K_CAP, xr)
+    blob = _blob(world, "rec", nbytes, dev)
     mark = sc.bufs.get("arena_mark")
     if mark is None or mark.numel() < arena.n:
         mark = sc.bufs["arena_mark"] = torch.zeros(max(arena.n, 1024) * 2, dtype=torch.int64, device=dev)
         sc.bufs["arena_gen"] = 0
     gen = sc.bufs["arena_gen"] = sc.bufs.get("arena_gen", 0) + 1
-    won = sc.get("gp_won", nr, torch.uint8, dev)
-    won.zero_()
-    dn, dn_mul = (b["cnt"], 2) if nres is None else (nres, 1)
-    _m().arena_scatter(nr, _p(dn), dn_mul, _p(out_rows), _p(out), out_w, _p(out_len), _p(arena.data), L,
-                       _p(arena.lens), _p(mark), int(gen), _p(won), gf, of, st)
-    q = sc.get("gp_q", nr, torch.int64, dev)
-    _m().select_indices_dev(nr, _SEL_SET, _p(won), 0, _p(q), 0, _p(b["cnt2"]), st)
-    cells = sc.get("gp_rcells", nr, torch.int64, dev)
-    _m().gather_dev(nr, _p(b["cnt2"]), _p(q), _p(out_rows), _p(cells), st)
-    _rebuild(world, b, cells, b["cnt2"], nr)
-    _finish(world, "rec", (p,), (seed, call), b, cells, b["cnt2"],
-            {"rows": out_rows, "out": out, "out_w": out_w, "out_len": out_len, "mark": mark, "gen": gen,
-             "direct": nres is not None}, status_cnt=nres)
+    nres = sc.get("gp_nres", 1, torch.int32, dev) if extra is not None else None
+    seed, call = _rng()
+    slot = _m().gp_recombine(_arena_desc(world, b), _gen_desc(world, dev), k, _p(keys), float(p), seed, call, pcap,
+                             K_CAP, D_CAP, _p(mark), int(gen), extra, _p(nres), _p(blob), _stream())
+    lay = _m().gp_layout(1, n, pcap, L, K_CAP, xr)
+    nr = lay["nr"]
+    _record(world, "rec", (p,), (seed, call), _view(blob, lay["cells"], nr, torch.int64), slot,
+            {"rows": _view(blob, lay["out_rows"], nr, torch.int64),
+             "out": _view(blob, lay["out"], nr * lay["out_w"], torch.uint8), "out_w": lay["out_w"],
+             "out_len": _view(blob, lay["out_len"], nr, torch.int32), "mark": mark, "gen": gen,
+             "direct": extra is not None})
     return True
 
 

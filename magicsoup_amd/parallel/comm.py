@@ -17,10 +17,25 @@ below (the torus wraps, so with two ranks ``up == down``).
 """
 from __future__ import annotations
 
+import atexit
 import os
+import weakref
 
 import torch
 import torch.distributed as dist
+
+_LIVE: "weakref.WeakSet" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_all() -> None:
+    """Destroy native communicators before interpreter / library teardown (their proxy threads
+    must not outlive the HIP runtime)."""
+    for c in list(_LIVE):
+        try:
+            c.close()
+        except Exception:  # noqa: BLE001 - best effort at exit
+            pass
 
 _OPS = {"sum": 0, "max": 1, "min": 2}
 _DT = {torch.int32: 0, torch.float32: 1, torch.float64: 2, torch.int64: 3}
@@ -112,6 +127,7 @@ class RcclComm:
             dist.broadcast_object_list(uid, src=src, group=group)
         with torch.cuda.device(torch.device(device)):
             self.handle = m.rccl_init(uid[0], size, rank)
+        _LIVE.add(self)
         self._raw_stream = torch._C._cuda_getCurrentRawStream
         self._cur_device = torch._C._cuda_getDevice
 
@@ -139,7 +155,9 @@ class RcclComm:
             raise RuntimeError(f"RCCL communicator error: {err}")
 
     def close(self) -> None:
+        """Destroy the communicator (collective: every rank closes at the same point)."""
         if getattr(self, "handle", 0):
+            torch.cuda.synchronize()
             self._m.rccl_destroy(self.handle, False)
             self.handle = 0
 

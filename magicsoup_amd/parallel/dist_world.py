@@ -867,6 +867,12 @@ class DistributedWorld(World):
         w.load_state(Path(statedir), ignore_cell_params=True)
         self.scatter_from(w, maps=False, params=not ignore_cell_params)
 
+    def close(self) -> None:
+        """Release the communicator (collective). The world cannot exchange afterwards."""
+        c = self.__dict__.get("_comm")
+        if c is not None:
+            c.close()
+
     def __getstate__(self):
         raise TypeError("a DistributedWorld is bound to its process group; use gather() or save_state()")
 
@@ -944,13 +950,18 @@ class _BoundaryRecombination:
         self.kcap = kcap
 
     def apply(self, pair_count, out, out_w, out_len, out_rows, nres) -> None:
-        from magicsoup_amd.ops.hip_ops import _m, _p, _scratch, _stream
+        """Write this rank's boundary results after the ``2 * *pair_count`` local result rows
+        (device pointers or tensors; ``pair_count`` None: from row 0) and the row total to ``nres``."""
+        from magicsoup_amd.ops.hip_ops import _m, _scratch, _stream
 
-        other = _scratch(self.world).get("xb_other", 2 * self.E * out_w, torch.uint8, out.device)
-        _m().xb_apply(self.world.map_size, self.E, self.W, self.seed_dn, self.seed_up, self.call, _p(self.ev),
-                      _p(self.slots_dn), _p(self.slots_up), _p(self.recv_dn), _p(self.recv_up), _p(self.parts),
-                      self.kcap + 2, _p(pair_count), _p(out), int(out_w), _p(out_len), _p(out_rows), _p(other),
-                      _p(nres), _stream())
+        def ptr(x):
+            return 0 if x is None else (x if isinstance(x, int) else x.data_ptr())
+
+        other = _scratch(self.world).get("xb_other", 2 * self.E * int(out_w), torch.uint8, self.ev.device)
+        _m().xb_apply(self.world.map_size, self.E, self.W, self.seed_dn, self.seed_up, self.call, ptr(self.ev),
+                      ptr(self.slots_dn), ptr(self.slots_up), ptr(self.recv_dn), ptr(self.recv_up), ptr(self.parts),
+                      self.kcap + 2, ptr(pair_count), ptr(out), int(out_w), ptr(out_len), ptr(out_rows), ptr(other),
+                      ptr(nres), _stream())
 
     def commit_standalone(self) -> None:
         """Synchronous commit of this rank's boundary results (when the pipeline did not run)."""
