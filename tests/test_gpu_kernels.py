@@ -640,3 +640,31 @@ def test_register_integrator_matches_lds_integrator_bit_for_bit(case):
     out = _integrate_modes(kin, X)
     assert torch.equal(out[0], out[8])
     assert not torch.equal(out[0], X)
+
+
+def test_parameter_rows_follow_genomes_through_bench_steps():
+    """After kills (the cell -> row map gathered with the columns), divisions (cloned in the same
+    gather), mutations / recombinations (device pipeline) and spawns, every cell's parameters equal
+    a fresh translation + build of its current genome."""
+    import bench
+
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    w = _world("cuda", map_size=128, n=3000, s=500)
+    for _ in range(8):
+        bench.step(w, 3000, 500, atp)
+        w.mutate_cells(p=1e-4)
+        w.recombinate_cells(p=1e-5)
+    w._reconcile()
+    ref = copy.deepcopy(w)
+    ref._update_params_rows(torch.arange(ref.n_cells, device="cuda"))
+    ka, kb = w.kinetics, ref.kinetics
+    P = min(ka.N.size(1), kb.N.size(1))
+    real = kb.Vmax[:, :P] != 0  # proteins of the current proteomes (padding has Vmax 0)
+    assert torch.equal(ka.Vmax[:, :P], kb.Vmax[:, :P])
+    assert int(real.sum()) > w.n_cells  # the population does have proteomes
+    for name in ("N", "Nf", "Nb", "A", "Kmf", "Kmb", "Ke", "Kmr"):
+        ta, tb = getattr(ka, name)[:, :P], getattr(kb, name)[:, :P]
+        assert ta.size(0) == tb.size(0) == w.n_cells
+        # padding values depend on history (a widened layout is zero-filled, a build writes the
+        # reference's padding values, as in the reference): compare the real proteins
+        assert torch.equal(ta[real], tb[real]), name
