@@ -50,6 +50,59 @@ void arena_scatter(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t sr
                    uintptr_t arena, int width, uintptr_t lens, uintptr_t mark, uint64_t gen, uintptr_t flags,
                    uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
 
+void select_indices_capped(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t out_dev, int cap,
+                           uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
+std::pair<long long*, int> status_slot();
+
+// ---- fused small steps of the rebuild chain
+// token rows of the live items cleared and the long-genome counter reset, one launch
+__global__ void __launch_bounds__(256) gp_zero_kernel(int cap, const int* dn, long long row, int32_t* buf,
+                                                      int32_t* long_count) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *long_count = 0;
+  const long long total = (long long)min(*dn, cap) * row;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
+    buf[i] = 0;
+}
+
+// One workgroup: proteome-shape checks (trans_check), fresh parameter rows (assign_rows) and the
+// call's status {rebuilt, op flags, row counter, count} into its pinned slot (status_write).
+constexpr int kFlagTranslateBit = 1, kFlagRowsBit = 4;  // select.hip DevFlag
+__global__ void __launch_bounds__(1024) gp_check_assign_kernel(int cap, const int* dn, const int32_t* counts,
+                                                               const int32_t* ndom, const int32_t* long_count,
+                                                               int32_t* per, int Pcap, int Dcap, const int64_t* cells,
+                                                               int64_t* slot, long long* d_rows, long long row_cap,
+                                                               int32_t* rows_out, int* opflags, const int* stat_cnt,
+                                                               long long* status) {
+  const int n = min(*dn, cap);
+  const long long base = *d_rows;
+  if (threadIdx.x == 0) {
+    if (*dn > cap) atomicOr(opflags, 2);  // kFlagCapacity
+    if (*long_count > 0) atomicOr(opflags, kFlagTranslateBit);
+  }
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    const int p = counts[2 * j] + counts[2 * j + 1];
+    per[j] = p;
+    if (p > Pcap || ndom[2 * j] > Dcap || ndom[2 * j + 1] > Dcap) atomicOr(opflags, kFlagTranslateBit);
+    const long long r = base + j;
+    if (r >= row_cap) {
+      atomicOr(opflags, kFlagRowsBit);
+      rows_out[j] = -1;  // the build skips it; the host rebuilds the cell
+      continue;
+    }
+    rows_out[j] = (int32_t)r;
+    slot[cells[j]] = r;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const long long nr = base + n < row_cap ? base + n : row_cap;
+    *d_rows = nr;
+    status[0] = *dn;
+    status[1] = __hip_atomic_load(opflags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    status[2] = nr;
+    status[3] = *stat_cnt;
+  }
+}
+
 // ---- descriptors filled from Python
 struct GpArena {  // genome arena + the pipeline's device counters
   uintptr_t data = 0, lens = 0;
@@ -99,22 +152,30 @@ size_t rebuild_bytes(int cap, int P, int dcap) {
   return c.off + 256;
 }
 
-void rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const GpGen& g, const GpKin& k, int dcap,
-             Carve& c, hipStream_t s) {
+// returns the status slot (written by the check / assign launch; final once the chain completed)
+int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const GpGen& g, const GpKin& k, int dcap,
+            Carve& c, uintptr_t stat_cnt, hipStream_t s) {
   const uintptr_t st = reinterpret_cast<uintptr_t>(s);
   const uintptr_t counts = c.take(8 * (size_t)cap), ndom = c.take(8 * (size_t)cap);
   const uintptr_t long_list = c.take(4 * (size_t)cap), long_count = c.take(16);
   const uintptr_t per = c.take(4 * (size_t)cap), rows_out = c.take(4 * (size_t)cap);
   const uintptr_t tokens = c.take(4 * (size_t)cap * k.P * dcap * 5);
-  MS_HIP_CHECK(hipMemsetAsync(reinterpret_cast<void*>(long_count), 0, sizeof(int32_t), s));
-  zero_rows(cap, dcnt, (long long)k.P * dcap * 5, tokens, st);
+  const long long row = (long long)k.P * dcap * 5;
+  const unsigned gz = (unsigned)std::min<long long>(cdiv((long long)cap * row, 256), 1024);
+  gp_zero_kernel<<<gz, 256, 0, s>>>(cap, P_<int>(dcnt), row, P_<int32_t>(tokens), P_<int32_t>(long_count));
+  MS_LAUNCH_CHECK();
   translate_fused(cap, cells, a.data, a.width, a.lens, g.small, g.dom_type, g.dt_entries, g.two_codon, g.dom_size,
                   g.dom_type_size, counts, ndom, k.P, dcap, tokens, long_list, long_count, dcnt, st);
-  trans_check(cap, dcnt, counts, ndom, long_count, per, k.P, dcap, a.opflags, st);
-  assign_rows(cap, dcnt, cells, k.slot, a.d_rows, k.row_cap, rows_out, a.opflags, st);
+  auto sl = status_slot();
+  gp_check_assign_kernel<<<1, 1024, 0, s>>>(cap, P_<int>(dcnt), P_<int32_t>(counts), P_<int32_t>(ndom),
+                                            P_<int32_t>(long_count), P_<int32_t>(per), k.P, dcap, P_<int64_t>(cells),
+                                            P_<int64_t>(k.slot), P_<long long>(a.d_rows), k.row_cap,
+                                            P_<int32_t>(rows_out), P_<int>(a.opflags), P_<int>(stat_cnt), sl.first);
+  MS_LAUNCH_CHECK();
   build_params(cap, k.P, dcap, k.P, k.s, tokens, rows_out, k.vmax, k.nw, k.km, k.nk, k.signs, k.nsg, k.hills, k.nh,
                k.react, k.trnsp, k.eff, k.nv, k.energies, k.abs_temp, k.gas, k.N, k.Nf, k.Nb, k.A, k.Kmr, k.Kmf, k.Kmb,
                k.Vmax, k.Ke, per, k.W, k.Q, k.overflow, dcnt, st);
+  return sl.second;
 }
 }  // namespace
 
@@ -199,12 +260,10 @@ int gp_mutate(const GpArena& a, const GpGen& g, const GpKin& k, double p, double
   const int out_w = (L + kcap + 15) / 16 * 16;
   const uintptr_t out = c.take((size_t)cap * out_w), out_len = c.take(4 * (size_t)cap);
   mut_count(n, 0, a.lens, p, seed, call, kk, kcap, a.gflags, a.opflags, stream);
-  select_indices_dev(n, kSelI32Pos, kk, 0, sel, 0, a.cnt, stream);
-  cap_skip(a.cnt, cap, a.gflags, a.opflags, stream);
+  select_indices_capped(n, kSelI32Pos, kk, sel, a.cnt, cap, a.gflags, a.opflags, stream);
   mut_apply(cap, a.cnt, sel, 0, a.data, L, a.lens, kk, p_indel, p_del, seed, call, out, out_w, out_len, stream);
   arena_scatter(cap, a.cnt, 1, sel, out, out_w, out_len, a.data, L, a.lens, 0, 0, 0, a.gflags, a.opflags, stream);
-  rebuild(cap, sel, a.cnt, a, g, k, dcap, c, s);
-  return status_write(a.cnt, a.opflags, a.d_rows, a.cnt, stream);
+  return rebuild(cap, sel, a.cnt, a, g, k, dcap, c, a.cnt, s);
 }
 
 // recombinate_cells() over neighbour slot keys (8 per cell); `extra` (optional Python object with
@@ -222,21 +281,19 @@ int gp_recombine(const GpArena& a, const GpGen& g, const GpKin& k, uintptr_t key
   const uintptr_t parts = c.take(4 * (size_t)cap * parts_cap * 3);
   const uintptr_t won = c.take((size_t)nr), q = c.take(8 * (size_t)nr), cells = c.take(8 * (size_t)nr);
   rec_count_keys(8 * n, keys, a.lens, p, seed, call, kk, 0, kcap, a.gflags, a.opflags, stream);
-  select_indices_dev(8ll * n, kSelI32Pos, kk, 0, sel, 0, a.cnt, stream);
-  cap_skip(a.cnt, cap, a.gflags, a.opflags, stream);
+  select_indices_capped(8ll * n, kSelI32Pos, kk, sel, a.cnt, cap, a.gflags, a.opflags, stream);
   rec_apply(cap, a.cnt, sel, 0, keys, a.data, L, a.lens, kk, seed, call, parts, parts_cap, out, out_w, out_len,
             out_rows, stream);
   if (xr) {
     extra.attr("apply")(a.cnt, out, out_w, out_len, out_rows, nres);
   }
-  MS_HIP_CHECK(hipMemsetAsync(reinterpret_cast<void*>(won), 0, (size_t)nr, s));
-  // (a0, b0, a1, b1, ..., extra rows): the last result per cell wins (reference update order)
+  // (a0, b0, a1, b1, ..., extra rows): the last result per cell wins (reference update order);
+  // arena_scatter also clears the `won` flags past the live rows
   arena_scatter(nr, xr ? nres : a.cnt, xr ? 1 : 2, out_rows, out, out_w, out_len, a.data, L, a.lens, mark, gen, won,
                 a.gflags, a.opflags, stream);
   select_indices_dev(nr, kSelSet, won, 0, q, 0, a.cnt2, stream);
   gather_dev(nr, a.cnt2, q, out_rows, cells, stream);
-  rebuild(nr, cells, a.cnt2, a, g, k, dcap, c, s);
-  return status_write(a.cnt2, a.opflags, a.d_rows, xr ? nres : a.cnt, stream);
+  return rebuild(nr, cells, a.cnt2, a, g, k, dcap, c, xr ? nres : a.cnt, s);
 }
 
 void bind_gp(py::module_& m) {

@@ -240,6 +240,8 @@ __global__ void __launch_bounds__(64) arena_scatter_kernel(int k, const int* dn,
                                                            const unsigned long long* mark, unsigned long long gen,
                                                            uint8_t* flags, int* gflags, int* opflags) {
   const int ke = eff_count(k, dn, dn_mul), lane = threadIdx.x;
+  if (flags)  // entries past the live count read as "not won" (no separate clearing launch)
+    for (int q = ke + blockIdx.x * 64 + lane; q < k; q += gridDim.x * 64) flags[q] = 0;
   for (int q = blockIdx.x; q < ke; q += gridDim.x) {
     const int64_t r = rows[q];
     const bool won = !mark || mark[r] == ((gen << 32) | (unsigned long long)q);

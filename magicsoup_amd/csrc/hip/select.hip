@@ -71,7 +71,9 @@ template <int K>
 __global__ void __launch_bounds__(kSelThreads) select_write_kernel(long long n, const void* src, const int32_t* tile_count,
                                                                    const int32_t* tile_max, int64_t* sel,
                                                                    int64_t* rest, int32_t* host_out,
-                                                                   long long* host64 = nullptr) {
+                                                                   long long* host64 = nullptr, int cap = -1,
+                                                                   int* cap_gflags = nullptr,
+                                                                   int* cap_opflags = nullptr) {
   constexpr int W = kSelThreads / 64;
   __shared__ long long s_red[W];
   __shared__ int s_wc[kSelItems][W];
@@ -123,6 +125,13 @@ __global__ void __launch_bounds__(kSelThreads) select_write_kernel(long long n, 
     for (int j = 0; j < kSelItems; ++j)
       for (int q = 0; q < W; ++q) total += s_wc[j][q];
     for (int q = 0; q < (int)gridDim.x; ++q) m = max(m, tile_max[q]);
+    if (cap >= 0 && total > cap) {
+      // capacity guard of a device-pipeline call (cap_skip semantics): the call becomes a no-op
+      // that the host replays on the synchronous path, and the pending chain is broken
+      total = 0;
+      atomicOr(cap_opflags, 16);  // kGpSkipped
+      atomicOr(cap_gflags, 8);    // kGpWidth
+    }
     host_out[0] = total;
     host_out[1] = m;
     if (host64) {  // also into a pinned status slot (select_indices_async)
@@ -461,6 +470,55 @@ std::pair<long long, int> select_indices(long long n, int kind, uintptr_t src, u
   const long long cnt = g_host[0];
   if (cnt < 0 || cnt > n) throw std::runtime_error("select_indices: bad count read-back");
   return {cnt, g_host[1]};
+}
+
+// select_indices_dev with the pipeline capacity guard folded into the last tile (cap_skip).
+void select_indices_capped(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t out_dev, int cap,
+                           uintptr_t gflags, uintptr_t opflags, uintptr_t stream) {
+  hipStream_t s = S_(stream);
+  if (n <= 0) {
+    MS_HIP_CHECK(hipMemsetAsync(P_<int32_t>(out_dev), 0, 2 * sizeof(int32_t), s));
+    return;
+  }
+  if (n >= (1ll << 40)) throw std::invalid_argument("select_indices_capped: n too large");
+  const long long tiles = (n + kSelTile - 1) / kSelTile;
+  if (tiles > g_tiles_cap) {
+    if (g_tiles) {
+      MS_HIP_CHECK(hipStreamSynchronize(s));
+      MS_HIP_CHECK(hipFree(g_tiles));
+    }
+    g_tiles_cap = std::max(tiles, 256ll);
+    MS_HIP_CHECK(hipMalloc((void**)&g_tiles, 2 * g_tiles_cap * sizeof(int32_t)));
+  }
+  const void* sp = reinterpret_cast<const void*>(src);
+  int32_t* tc = g_tiles;
+  int32_t* tm = g_tiles + g_tiles_cap;
+#define MS_SEL(K)                                                                                                \
+  select_count_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, nullptr, tc, tm);                      \
+  MS_LAUNCH_CHECK();                                                                                             \
+  select_write_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, tc, tm, P_<int64_t>(sel), nullptr,     \
+                                                                 P_<int32_t>(out_dev), nullptr, cap,             \
+                                                                 P_<int>(gflags), P_<int>(opflags));             \
+  MS_LAUNCH_CHECK();
+  switch (kind) {
+    case kMaskSet: MS_SEL(kMaskSet) break;
+    case kI32Pos: MS_SEL(kI32Pos) break;
+    default: throw std::invalid_argument("select_indices_capped: unsupported predicate");
+  }
+#undef MS_SEL
+}
+
+// A fresh pinned status slot: {device pointer of its 4 int64 words, slot index}.
+std::pair<long long*, int> status_slot() {
+  if (!g_status) {
+    MS_HIP_CHECK(hipHostMalloc((void**)&g_status, kStatusSlots * 4 * sizeof(long long),
+                               hipHostMallocMapped | hipHostMallocCoherent));
+    MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_status_dev, g_status, 0));
+  }
+  const int slot = g_status_next;
+  g_status_next = (g_status_next + 1) % kStatusSlots;
+  for (int i = 0; i < 4; ++i) g_status[slot * 4 + i] = -1;
+  return {g_status_dev + slot * 4, slot};
 }
 
 void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel, uintptr_t rest,
