@@ -4,9 +4,9 @@ Workload = the reference's macro benchmark loop (``performance/run_simulation.py
 BASELINE.json config: Wood-Ljungdahl chemistry, 4096x4096 map, random-normal molecule map, 500 bp
 random genomes, population topped up to >= 50,000 cells every step. One step:
 
-    top up to N cells -> enzymatic_activity -> kill (ATP < 1) -> replicate (ATP > 5: ATP -= 4,
-    divide) -> dilute back to N cells (random kills) -> recombinate_cells -> mutate_cells ->
-    degrade -> diffuse -> increment lifetimes
+    top up to N cells -> enzymatic_activity -> kill (ATP < 1, plus random cells so that the
+    divisions that follow restore ~1.01 N: chemostat dilution) -> replicate (ATP > 5: ATP -= 4, divide)
+    -> recombinate_cells -> mutate_cells -> degrade -> diffuse -> increment lifetimes
 
 Single GPU: one ``World`` on ``cuda:0``. N GPUs (``torchrun --nproc-per-node N``): one world,
 domain-decomposed over the ranks (``magicsoup_amd.parallel``; strong scaling of the fixed config).
@@ -73,6 +73,7 @@ def random_genomes(k: int, size: int, device) -> tuple[torch.Tensor, torch.Tenso
 
 
 _DILUTE = {"rng": np.random.default_rng(0), "pinned": None}
+_CHEMOSTAT = {"divided": 0, "starved": 0}  # previous step's divisions / starvation deaths (dilution estimates)
 
 
 def _dilution_sample(n: int, k: int, device) -> torch.Tensor:
@@ -108,22 +109,27 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
         world.enzymatic_activity()
     with ph("kill"):
         kill = world.cell_molecules[:, atp] < 1.0  # boolean masks: no index read-back
+        # chemostat dilution keeps the population at the configured size (the reference loop only
+        # tops up; on a 4096^2 map the population would otherwise grow ~6x within 25 steps): random
+        # cells are removed together with the starving ones, in the same kill_cells call, so that
+        # after the divisions that follow the population is back at n_target plus a 1 % margin (the
+        # previous step's divisions and starvation deaths are the estimates). The margin keeps the
+        # next step's top-up (a spawn) rare; activity always runs on >= n_target cells.
+        n0 = world.n_cells
+        keep = n_target + n_target // 100 - _CHEMOSTAT["divided"] + _CHEMOSTAT["starved"]
+        excess = min(n0 - keep, n0)
+        if excess > 0:
+            kill.index_fill_(0, _dilution_sample(n0, excess, kill.device), True)
+            note("diluted", excess)
         world.kill_cells(kill)
-        if stats is not None:
-            note("killed", kill.sum())
+        _CHEMOSTAT["starved"] = max(0, n0 - world.n_cells - max(excess, 0))
+        note("killed", n0 - world.n_cells)
     with ph("replicate"):
         repl = world.cell_molecules[:, atp] > 5.0
         world.cell_molecules[:, atp] -= 4.0 * repl
-        world.divide_cells_t(repl)
-        if stats is not None:
-            note("divided", repl.sum())
-    with ph("dilute"):
-        # chemostat-style dilution keeps the population at the configured size (the reference loop
-        # only tops up; on a 4096^2 map the population would otherwise grow ~6x within 25 steps)
-        excess = world.n_cells - n_target
-        if excess > 0:
-            world.kill_cells(_dilution_sample(world.n_cells, excess, world.cell_molecules.device))
-            note("diluted", excess)
+        parents, _ = world.divide_cells_t(repl)
+        _CHEMOSTAT["divided"] = int(parents.numel())
+        note("divided", _CHEMOSTAT["divided"])
     with ph("recombinate"):
         world.recombinate_cells()
     with ph("mutate"):

@@ -20,11 +20,6 @@ void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, ui
                         uintptr_t out_dev, uintptr_t stream);
 void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
 int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t cnt, uintptr_t stream);
-void zero_rows(int cap, uintptr_t dn, long long row, uintptr_t buf, uintptr_t stream);
-void trans_check(int cap, uintptr_t dn, uintptr_t counts, uintptr_t ndom, uintptr_t long_count, uintptr_t per, int Pcap,
-                 int Dcap, uintptr_t flags, uintptr_t stream);
-void assign_rows(int ncap, uintptr_t dn, uintptr_t cells, uintptr_t slot, uintptr_t d_rows, long long row_cap,
-                 uintptr_t rows_out, uintptr_t flags, uintptr_t stream);
 void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t dst, uintptr_t stream);
 void translate_fused(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
@@ -64,13 +59,15 @@ __global__ void __launch_bounds__(256) gp_zero_kernel(int cap, const int* dn, lo
     buf[i] = 0;
 }
 
-// One workgroup: proteome-shape checks (trans_check), fresh parameter rows (assign_rows) and the
-// call's status {rebuilt, op flags, row counter, count} into its pinned slot (status_write).
+// One workgroup: proteome-shape checks, fresh parameter rows and the call's status {rebuilt, op
+// flags, row counter, count} into its pinned slot. Fresh row j is base + j (dense storage tail) or
+// free[base + j] (recycled rows of removed cells, Kinetics._recycle_rows); row_cap bounds the counter.
 constexpr int kFlagTranslateBit = 1, kFlagRowsBit = 4;  // select.hip DevFlag
 __global__ void __launch_bounds__(1024) gp_check_assign_kernel(int cap, const int* dn, const int32_t* counts,
                                                                const int32_t* ndom, const int32_t* long_count,
                                                                int32_t* per, int Pcap, int Dcap, const int64_t* cells,
                                                                int64_t* slot, long long* d_rows, long long row_cap,
+                                                               const int64_t* free,
                                                                int32_t* rows_out, int* opflags, const int* stat_cnt,
                                                                long long* status) {
   const int n = min(*dn, cap);
@@ -89,8 +86,9 @@ __global__ void __launch_bounds__(1024) gp_check_assign_kernel(int cap, const in
       rows_out[j] = -1;  // the build skips it; the host rebuilds the cell
       continue;
     }
-    rows_out[j] = (int32_t)r;
-    slot[cells[j]] = r;
+    const long long row = free ? free[r] : r;
+    rows_out[j] = (int32_t)row;
+    slot[cells[j]] = row;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -115,7 +113,7 @@ struct GpGen {  // translation LUTs (Genetics.device_luts)
 };
 struct GpKin {  // parameter storage (capacity rows) + token LUTs + cell -> row map
   uintptr_t N = 0, Nf = 0, Nb = 0, A = 0, Kmr = 0, Kmf = 0, Kmb = 0, Vmax = 0, Ke = 0;
-  uintptr_t W = 0, Q = 0, overflow = 0, slot = 0;
+  uintptr_t W = 0, Q = 0, overflow = 0, slot = 0, free = 0;
   int P = 0, s = 0;
   long long row_cap = 0;
   uintptr_t vmax = 0, km = 0, signs = 0, hills = 0, react = 0, trnsp = 0, eff = 0, energies = 0;
@@ -161,7 +159,7 @@ int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const Gp
   const uintptr_t per = c.take(4 * (size_t)cap), rows_out = c.take(4 * (size_t)cap);
   const uintptr_t tokens = c.take(4 * (size_t)cap * k.P * dcap * 5);
   const long long row = (long long)k.P * dcap * 5;
-  const unsigned gz = (unsigned)std::min<long long>(cdiv((long long)cap * row, 256), 1024);
+  const unsigned gz = (unsigned)std::max<long long>(1, std::min<long long>(cdiv((long long)cap * row, 256), 1024));
   gp_zero_kernel<<<gz, 256, 0, s>>>(cap, P_<int>(dcnt), row, P_<int32_t>(tokens), P_<int32_t>(long_count));
   MS_LAUNCH_CHECK();
   translate_fused(cap, cells, a.data, a.width, a.lens, g.small, g.dom_type, g.dt_entries, g.two_codon, g.dom_size,
@@ -170,7 +168,8 @@ int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const Gp
   gp_check_assign_kernel<<<1, 1024, 0, s>>>(cap, P_<int>(dcnt), P_<int32_t>(counts), P_<int32_t>(ndom),
                                             P_<int32_t>(long_count), P_<int32_t>(per), k.P, dcap, P_<int64_t>(cells),
                                             P_<int64_t>(k.slot), P_<long long>(a.d_rows), k.row_cap,
-                                            P_<int32_t>(rows_out), P_<int>(a.opflags), P_<int>(stat_cnt), sl.first);
+                                            k.free ? P_<int64_t>(k.free) : nullptr, P_<int32_t>(rows_out),
+                                            P_<int>(a.opflags), P_<int>(stat_cnt), sl.first);
   MS_LAUNCH_CHECK();
   build_params(cap, k.P, dcap, k.P, k.s, tokens, rows_out, k.vmax, k.nw, k.km, k.nk, k.signs, k.nsg, k.hills, k.nh,
                k.react, k.trnsp, k.eff, k.nv, k.energies, k.abs_temp, k.gas, k.N, k.Nf, k.Nb, k.A, k.Kmr, k.Kmf, k.Kmb,
@@ -183,6 +182,7 @@ int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const Gp
 // untouched until the call was reconciled: it holds the results a replay may re-commit).
 size_t gp_blob_bytes(int kind, int n, int cap, int P, int L, int dcap, int kcap, int extra_rows) {
   Carve c(0);
+  if (kind == 2) return rebuild_bytes(cap, P, dcap) + 512;  // rebuild of listed cells
   if (kind == 0) {  // mutations
     const int out_w = (L + kcap + 15) / 16 * 16;
     c.take(4 * (size_t)n);                 // k
@@ -296,6 +296,15 @@ int gp_recombine(const GpArena& a, const GpGen& g, const GpKin& k, uintptr_t key
   return rebuild(nr, cells, a.cnt2, a, g, k, dcap, c, xr ? nres : a.cnt, s);
 }
 
+// Translation + fresh rows + parameter build of cells[:*cnt] (cnt <= cap; e.g. spawned cells or
+// cells that arrived from another rank); returns the status slot.
+int gp_rebuild(const GpArena& a, const GpGen& g, const GpKin& k, uintptr_t cells, uintptr_t cnt, int cap, int dcap,
+               uintptr_t blob, uintptr_t stream) {
+  if (cap <= 0) throw std::invalid_argument("gp_rebuild: empty");
+  Carve c(blob);
+  return rebuild(cap, cells, cnt, a, g, k, dcap, c, cnt, S_(stream));
+}
+
 void bind_gp(py::module_& m) {
   py::class_<GpArena>(m, "GpArena")
       .def(py::init<>())
@@ -315,7 +324,8 @@ void bind_gp(py::module_& m) {
       .def_readwrite("A", &GpKin::A).def_readwrite("Kmr", &GpKin::Kmr).def_readwrite("Kmf", &GpKin::Kmf)
       .def_readwrite("Kmb", &GpKin::Kmb).def_readwrite("Vmax", &GpKin::Vmax).def_readwrite("Ke", &GpKin::Ke)
       .def_readwrite("W", &GpKin::W).def_readwrite("Q", &GpKin::Q).def_readwrite("overflow", &GpKin::overflow)
-      .def_readwrite("slot", &GpKin::slot).def_readwrite("P", &GpKin::P).def_readwrite("s", &GpKin::s)
+      .def_readwrite("slot", &GpKin::slot).def_readwrite("free", &GpKin::free).def_readwrite("P", &GpKin::P)
+      .def_readwrite("s", &GpKin::s)
       .def_readwrite("row_cap", &GpKin::row_cap).def_readwrite("vmax", &GpKin::vmax).def_readwrite("km", &GpKin::km)
       .def_readwrite("signs", &GpKin::signs).def_readwrite("hills", &GpKin::hills)
       .def_readwrite("react", &GpKin::react).def_readwrite("trnsp", &GpKin::trnsp).def_readwrite("eff", &GpKin::eff)
@@ -327,6 +337,7 @@ void bind_gp(py::module_& m) {
   m.def("gp_layout", &gp_layout);
   m.def("gp_mutate", &gp_mutate, "device-pipeline point mutations over all genomes (one call, no sync)");
   m.def("gp_recombine", &gp_recombine, "device-pipeline recombinations over neighbour slot keys (one call, no sync)");
+  m.def("gp_rebuild", &gp_rebuild, "device-pipeline translation + parameter build of listed cells (no sync)");
 }
 
 }  // namespace msd

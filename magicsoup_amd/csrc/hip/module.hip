@@ -100,16 +100,15 @@ void rec_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t pairs, uintptr_t
 void arena_scatter(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t src, int src_width, uintptr_t src_len,
                    uintptr_t arena, int width, uintptr_t lens, uintptr_t mark, uint64_t gen, uintptr_t flags,
                    uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
+int divide_mask_dev(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t cell_map,
+                    uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result, int rounds, uint64_t seed,
+                    uint64_t call, uintptr_t wins, uintptr_t dcount, long long n0, int m, uintptr_t par,
+                    uintptr_t cell_mols, uintptr_t divisions, uintptr_t lifetimes, uintptr_t stream);
 void place_collect(int k, uintptr_t wins, uintptr_t cells, uintptr_t result, int C, uintptr_t par, uintptr_t npos,
                    uintptr_t stream);
 // select.hip
 void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel, uintptr_t rest,
                         uintptr_t out_dev, uintptr_t stream);
-void trans_check(int cap, uintptr_t dn, uintptr_t counts, uintptr_t ndom, uintptr_t long_count, uintptr_t per, int Pcap,
-                 int Dcap, uintptr_t flags, uintptr_t stream);
-void zero_rows(int cap, uintptr_t dn, long long row, uintptr_t buf, uintptr_t stream);
-void assign_rows(int ncap, uintptr_t dn, uintptr_t cells, uintptr_t slot, uintptr_t d_rows, long long row_cap,
-                 uintptr_t rows_out, uintptr_t flags, uintptr_t stream);
 void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t dst, uintptr_t stream);
 int count_to_host(uintptr_t dcount, uintptr_t stream);
 int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
@@ -217,12 +216,11 @@ PYBIND11_MODULE(_hip, m) {
   m.def("rec_apply", &msd::rec_apply);
   m.def("arena_scatter", &msd::arena_scatter);
   m.def("place_collect", &msd::place_collect);
+  m.def("divide_mask_dev", &msd::divide_mask_dev,
+        "divide_cells over a mask: placement, winner compaction and commit issued without a sync; returns the status slot");
   m.def("translate_stats", &msd::translate_stats,
         "(max proteins, max domains, long genomes) of a translate count pass; synchronises the stream");
   m.def("select_indices_dev", &msd::select_indices_dev);
-  m.def("trans_check", &msd::trans_check);
-  m.def("zero_rows", &msd::zero_rows);
-  m.def("assign_rows", &msd::assign_rows);
   m.def("gather_dev", &msd::gather_dev);
   m.def("cap_skip", &msd::cap_skip, "pipeline capacity guard: count > cap -> no-op call replayed by the host");
   m.def("select_indices_async", &msd::select_indices_async,

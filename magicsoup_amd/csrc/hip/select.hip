@@ -216,85 +216,16 @@ std::tuple<int, int, int> translate_stats(int n, uintptr_t counts, uintptr_t ndo
 // Sync-free genome updates (mutate / recombinate on the GPU): the selected count stays on the
 // device, later kernels stride over it, and overflow conditions the host could not rule out in
 // advance raise flag bits that the host resolves at its next synchronisation point.
-enum DevFlag { kFlagTranslate = 1, kFlagCapacity = 2, kFlagRows = 4 };
 
 // Like select_indices, but {count, max} go to device memory (out_dev) and nothing is synchronised.
 void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel, uintptr_t rest,
                         uintptr_t out_dev, uintptr_t stream);
-
-// Per-genome protein totals and the caps of the speculative token layout: flags translation
-// overflow (more proteins than the parameter storage holds, more domains than the token slots, a
-// genome too long for the LDS pass) and a count above the capacity of the pipeline buffers.
-__global__ void __launch_bounds__(256) trans_check_kernel(int cap, const int* dn, const int32_t* counts,
-                                                          const int32_t* ndom, const int32_t* long_count,
-                                                          int32_t* per, int Pcap, int Dcap, int* flags) {
-  const int n = min(*dn, cap);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    if (*dn > cap) atomicOr(flags, (int)kFlagCapacity);
-    if (*long_count > 0) atomicOr(flags, (int)kFlagTranslate);
-  }
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const int p = counts[2 * i] + counts[2 * i + 1];
-    per[i] = p;
-    if (p > Pcap || ndom[2 * i] > Dcap || ndom[2 * i + 1] > Dcap) atomicOr(flags, (int)kFlagTranslate);
-  }
-}
-
-// buf[i * row : (i + 1) * row] = 0 for i < min(*dn, cap)
-__global__ void __launch_bounds__(256) zero_rows_kernel(int cap, const int* dn, long long row, int32_t* buf) {
-  const long long total = (long long)min(*dn, cap) * row;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
-    buf[i] = 0;
-}
-
-// Fresh parameter rows for the rebuilt cells: rows_out[j] = base + j, slot[cells[j]] = base + j for
-// j < count, base = *d_rows (device row counter, advanced by count); rows beyond `cap` flag.
-__global__ void __launch_bounds__(1024) assign_rows_kernel(int ncap, const int* dn, const int64_t* cells, int64_t* slot,
-                                                           long long* d_rows, long long row_cap, int32_t* rows_out,
-                                                           int* flags) {
-  const int n = min(*dn, ncap);
-  const long long base = *d_rows;
-  __syncthreads();
-  for (int j = threadIdx.x; j < n; j += blockDim.x) {
-    const long long r = base + j;
-    if (r >= row_cap) {
-      atomicOr(flags, (int)kFlagRows);
-      rows_out[j] = -1;  // the build skips it; the host rebuilds the cell
-      continue;
-    }
-    rows_out[j] = (int32_t)r;
-    slot[cells[j]] = r;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) *d_rows = base + n < row_cap ? base + n : row_cap;
-}
 
 // dst[j] = src[idx[j]] for j < min(*dn, cap)
 __global__ void __launch_bounds__(256) gather_dev_kernel(int cap, const int* dn, const int64_t* idx, const int64_t* src,
                                                          int64_t* dst) {
   const int n = min(*dn, cap);
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) dst[j] = src[idx[j]];
-}
-
-void trans_check(int cap, uintptr_t dn, uintptr_t counts, uintptr_t ndom, uintptr_t long_count, uintptr_t per, int Pcap,
-                 int Dcap, uintptr_t flags, uintptr_t stream) {
-  const unsigned g = std::min(cdiv(cap, 256), 64u);
-  trans_check_kernel<<<g, 256, 0, S_(stream)>>>(cap, P_<int>(dn), P_<int32_t>(counts), P_<int32_t>(ndom),
-                                                P_<int32_t>(long_count), P_<int32_t>(per), Pcap, Dcap, P_<int>(flags));
-  MS_LAUNCH_CHECK();
-}
-
-void zero_rows(int cap, uintptr_t dn, long long row, uintptr_t buf, uintptr_t stream) {
-  const unsigned g = (unsigned)std::min<long long>(cdiv((long long)cap * row, 256), 1024);
-  zero_rows_kernel<<<g, 256, 0, S_(stream)>>>(cap, P_<int>(dn), row, P_<int32_t>(buf));
-  MS_LAUNCH_CHECK();
-}
-
-void assign_rows(int ncap, uintptr_t dn, uintptr_t cells, uintptr_t slot, uintptr_t d_rows, long long row_cap,
-                 uintptr_t rows_out, uintptr_t flags, uintptr_t stream) {
-  assign_rows_kernel<<<1, 1024, 0, S_(stream)>>>(ncap, P_<int>(dn), P_<int64_t>(cells), P_<int64_t>(slot),
-                                                  P_<long long>(d_rows), row_cap, P_<int32_t>(rows_out), P_<int>(flags));
-  MS_LAUNCH_CHECK();
 }
 
 // Capacity guard of a device-pipeline call: a selected count above the buffers' capacity turns the

@@ -42,6 +42,36 @@ __global__ void __launch_bounds__(256) split_cells_kernel(int k, int m, const in
   }
 }
 
+// Division commit with a device-side winner count (the host learns it after the launches): winner
+// j (wins[j], j < *dn, ascending cell index) becomes parent of the new row n0 + j, which takes the
+// claimed pixel; both get half the parent's molecules, divisions + 1 and lifetime 0 (the columns a
+// row gather would copy are all overwritten here, so only genomes / labels / parameter-row map are
+// gathered). Grid-stride over (*dn) x m.
+__global__ void __launch_bounds__(256) divide_commit_kernel(const int* dn, const int64_t* wins, const long long* result,
+                                                            int C, long long n0, int m, int64_t* par, int32_t* pos,
+                                                            float* cell_mols, int32_t* divisions, int32_t* lifetimes) {
+  const long long total = (long long)(*dn) * m;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const long long i = t / m;
+    const int j = (int)(t - i * m);
+    const long long p = wins[i], c = n0 + i;
+    const float h = cell_mols[p * m + j] * 0.5f;
+    cell_mols[p * m + j] = h;
+    cell_mols[c * m + j] = h;
+    if (j == 0) {
+      par[i] = p;
+      const long long px = result[p];
+      pos[2 * c] = (int32_t)(px / C);
+      pos[2 * c + 1] = (int32_t)(px - (px / C) * C);
+      const int32_t d = divisions[p] + 1;
+      divisions[p] = d;
+      divisions[c] = d;
+      lifetimes[p] = 0;
+      lifetimes[c] = 0;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- placement
 // Claim k uniformly random free pixels of the owned rows by rejection: atomically set the pixel's
 // byte in the (4-byte padded) bool occupancy map; out[i] = pixel or -1 after `attempts` misses.
@@ -468,6 +498,30 @@ void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo,
                                                        P_<long long>(cand), P_<int>(claim), P_<long long>(result));
     MS_LAUNCH_CHECK();
   }
+}
+
+int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
+                         uintptr_t stream);
+
+// divide_cells over a mask, everything issued before the count is known: cooperative placement
+// over the mask, winners (result >= 0) compacted with the count on the device and in a pinned
+// status slot (returned), then the commit into rows n0.. (capacity for n more rows is the caller's).
+int divide_mask_dev(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t cell_map,
+                    uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result, int rounds, uint64_t seed,
+                    uint64_t call, uintptr_t wins, uintptr_t dcount, long long n0, int m, uintptr_t par,
+                    uintptr_t cell_mols, uintptr_t divisions, uintptr_t lifetimes, uintptr_t stream) {
+  if (n <= 0) throw std::invalid_argument("divide_mask_dev: no cells");
+  const Geom g = geom(R, C, r_lo, r_hi, wrap);
+  hipStream_t s = S_(stream);
+  if (!place_coop(n, 0, mask, pos, g, false, cell_map, pending, cand, claim, result, rounds, seed, call, s))
+    throw std::runtime_error("divide_mask_dev: cooperative launch refused");
+  const int slot = select_indices_async(n, 3 /* int64 >= 0 */, result, wins, 0, dcount, stream);
+  const unsigned grid = std::min<unsigned>(cdiv((long long)n * m, 256), 512u);
+  divide_commit_kernel<<<grid, 256, 0, s>>>(P_<int>(dcount), P_<int64_t>(wins), P_<long long>(result), C, n0, m,
+                                            P_<int64_t>(par), P_<int32_t>(pos), P_<float>(cell_mols),
+                                            P_<int32_t>(divisions), P_<int32_t>(lifetimes));
+  MS_LAUNCH_CHECK();
+  return slot;
 }
 
 void place_collect(int k, uintptr_t wins, uintptr_t cells, uintptr_t result, int C, uintptr_t par, uintptr_t npos,

@@ -475,6 +475,7 @@ class Kinetics:
             torch.arange(n, device=dev, out=buf[:n])
             d["_slot"] = buf[:n]
             d["_nrows"] = n
+            d["_free"] = None
 
     def _slot_reserve(self, n: int, dev=None) -> None:
         """Capacity of the slot buffers >= n (keeps the live entries)."""
@@ -525,7 +526,7 @@ class Kinetics:
         """Resolve pending device-pipeline updates of the owning world (no-op otherwise)."""
         ref = self.__dict__.get("_owner")
         w = ref() if ref is not None else None
-        if w is not None and w.__dict__.get("_gp_state"):
+        if w is not None and (w.__dict__.get("_gp_state") or w.__dict__.get("_deferred")):
             w._reconcile()
 
     def _zero_row(self) -> torch.Tensor:
@@ -537,10 +538,9 @@ class Kinetics:
         if z is not None:
             return z
         z = self._alloc_rows(1)
-        r = int(d["_nrows"]) - 1
         ok = self._pack_ok()
         for t in self._store.values():
-            t[r : r + 1].zero_()  # packed words 0 and Q = 0 match all-zero parameters
+            t.index_fill_(0, z, 0)  # packed words 0 and Q = 0 match all-zero parameters
         self._restamp(ok)
         d["_zero_row_t"] = z
         return z
@@ -556,31 +556,69 @@ class Kinetics:
         self._alloc_rows_now(k)
         self.__dict__["_nrows"] -= k
 
+    def _row_limit(self) -> tuple[int, torch.Tensor | None]:
+        """(bound of the fresh-row counter ``_nrows``, free-row list or None). Fresh row j is
+        ``_nrows + j`` of the dense storage tail, or ``free[_nrows + j]`` once rows are recycled."""
+        d = self.__dict__
+        free = d.get("_free") if d["_slot"] is not None else None
+        if free is not None:
+            return int(free.numel()), free
+        return min(int(t.size(0)) for t in self._store.values()), None
+
     def _alloc_rows_now(self, k: int) -> torch.Tensor:
         """k unused storage rows (int64, device) for cells whose parameters are about to be written.
-        Rows of removed cells are not tracked (a row may be shared); when the storage is exhausted
-        the live rows are gathered back to cell order (one pass) or the capacity grows."""
+        Rows of removed cells are not tracked as they die (a row may be shared); when the fresh rows
+        run out, the rows no live cell maps to are collected into a free list (no parameter data
+        moves), and only when too few are free does the storage grow."""
         d = self.__dict__
         self._enter_slot_mode()
-        store = self._store
-        cap = min(int(t.size(0)) for t in store.values())
-        if d["_nrows"] + k > cap:
-            self._materialize()  # dense again: rows 0..n-1 live
-            self._enter_slot_mode()
-            n = d["_ncells"]
-            if n + k + n // 2 > cap:
-                # keep >= n/2 spare rows after a re-gather so that re-gathers stay rare (amortised)
-                new_cap = max(n + k + n // 2, int(cap * 1.5) + 64)
-                ok = self._pack_ok()
-                for name, t in list(store.items()):
-                    nb = torch.empty(new_cap, *t.shape[1:], dtype=t.dtype, device=t.device)
-                    nb[:n] = t[:n]
-                    store[name] = nb
-                d.pop("_spare", None)
-                self._restamp(ok)
+        limit, free = self._row_limit()
+        if d["_nrows"] + k > limit:
+            free = self._recycle_rows(k)
         r0 = d["_nrows"]
         d["_nrows"] = r0 + k
-        return torch.arange(r0, r0 + k, device=store["N"].device)
+        if free is not None:
+            return free[r0 : r0 + k]
+        return torch.arange(r0, r0 + k, device=self._store["N"].device)
+
+    def _recycle_rows(self, k: int) -> torch.Tensor | None:
+        """Make >= k fresh rows available: the free list of storage rows that no live cell (and not
+        the shared all-zero row) maps to, or -- below the spare target -- a dense re-gather into a
+        larger storage. Spare target: >= n/2 rows, up to 3n within a 4 GiB budget (every rebuilt
+        cell takes a fresh row, so the spare count sets how many steps pass between recycles)."""
+        d = self.__dict__
+        store = self._store
+        n = d["_ncells"]
+        cap = min(int(t.size(0)) for t in store.values())
+        row_bytes = sum(t[:1].numel() * t.element_size() for t in store.values())
+        spare = max(n // 2, min(3 * n, (4 << 30) // max(row_bytes, 1)))
+        slot = d["_slot"]
+        if slot.is_cuda and cap - n >= k + spare // 2:
+            from magicsoup_amd.ops import hip_ops
+
+            used = torch.zeros(cap, dtype=torch.uint8, device=slot.device)
+            if n:
+                used.index_fill_(0, slot, 1)
+            z = d.get("_zero_row_t")
+            if z is not None:
+                used.index_fill_(0, z, 1)
+            free = hip_ops.select(used, "clear")[0]
+            if int(free.numel()) >= k:
+                d["_free"] = free
+                d["_nrows"] = 0
+                return free
+        self._materialize()  # dense again: rows 0..n-1 live
+        self._enter_slot_mode()
+        if n + k + spare > cap:
+            new_cap = max(n + k + spare, int(cap * 1.5) + 64)
+            ok = self._pack_ok()
+            for name, t in list(store.items()):
+                nb = torch.empty(new_cap, *t.shape[1:], dtype=t.dtype, device=t.device)
+                nb[:n] = t[:n]
+                store[name] = nb
+            d.pop("_spare", None)
+            self._restamp(ok)
+        return None
 
     def _kernel_params(self) -> dict[str, torch.Tensor]:
         """Storage tensors in kernel layout (contiguous int32 / float32), rows = capacity."""
@@ -661,6 +699,7 @@ class Kinetics:
         for k in list(store):
             spare[k], store[k] = store[k], target[k]
         d["_slot"] = None
+        d["_free"] = None
         d["_nrows"] = n
         d.pop("_zero_row_t", None)
         self._restamp(ok)
@@ -746,6 +785,8 @@ class Kinetics:
 
             d = self.__dict__
             nrows = d["_nrows"] if d["_slot"] is not None else d["_ncells"]
+            if d["_slot"] is not None and d.get("_free") is not None:
+                nrows = min(int(t.size(0)) for t in store.values())  # live rows anywhere below capacity
             ok = self._pack_ok()
             moves = []
             for name, t in list(store.items()):
@@ -898,7 +939,7 @@ class Kinetics:
         self._materialize()
         state = self.__dict__.copy()
         state["last_masks"] = []
-        for k in ("_spare", "_hip_scratch", "_owner", "_lut_cache", "_slot_buf", "_slot_spare"):
+        for k in ("_spare", "_hip_scratch", "_owner", "_lut_cache", "_slot_buf", "_slot_spare", "_free"):
             state.pop(k, None)
         n = state["_ncells"]
         state["_store_d"] = {k: v[:n].clone() for k, v in self._store.items() if k not in _PACKED}

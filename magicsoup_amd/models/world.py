@@ -48,6 +48,7 @@ _LABEL_LEN = 12
 _PIPELINE_SAFE_OPS = frozenset({"mutate_cells", "recombinate_cells", "diffuse_molecules", "degrade_molecules",
                                 "increment_cell_lifetimes"})
 _CHECK_ENV = os.environ.get("MS_CHECK_INVARIANTS") == "1"
+_DEFER_ENV = os.environ.get("MS_DEFER_GENOME_OPS", "1")
 
 
 def _op(name: str):
@@ -60,7 +61,7 @@ def _op(name: str):
         @functools.wraps(fn)
         def wrapper(self, *args, **kwargs):
             d = self.__dict__
-            if d.get("_gp_state") and name not in _PIPELINE_SAFE_OPS:
+            if (d.get("_gp_state") or d.get("_deferred")) and name not in _PIPELINE_SAFE_OPS:
                 self._reconcile()
             timer, check = d.get("_timer"), d.get("_debug_checks", _CHECK_ENV)
             if timer is None and not check and not profiling.roctx_enabled():
@@ -245,7 +246,47 @@ class World:
 
         self.kinetics.__dict__["_owner"] = weakref.ref(self)
 
+    def _defer_genome_op(self) -> bool:
+        """Whether an all-cells mutate / recombinate is queued instead of issued now.
+
+        Their device-pipeline chains return nothing and touch only genomes and parameters, so the
+        ops the reference loop runs next (degrade, diffuse, lifetimes: molecules only) commute with
+        them exactly. Queuing the host-side issue until the next op that reads genomes, parameters,
+        cells or positions (that op flushes the queue first, in call order, before anything else)
+        moves ~0.2 ms of launch work per step behind the diffusion stencil already running on the
+        GPU. RNG draws happen at issue time; no op that draws can run before the flush. Off with
+        ``MS_DEFER_GENOME_OPS=0`` and while per-op timings are enabled."""
+        d = self.__dict__
+        if _DEFER_ENV == "0" or d.get("_timer") is not None or not self._genomes.data.is_cuda:
+            return False
+        from magicsoup_amd.ops import genome_pipeline
+
+        return genome_pipeline.enabled(self)
+
+    def _flush_deferred(self) -> None:
+        """Issue the queued genome ops, in call order, on a side stream: their chains run next to
+        the diffusion stencil still executing on the compute stream (disjoint state), and the compute
+        stream waits for them (device-side) before anything that follows."""
+        d = self.__dict__
+        q = d.get("_deferred")
+        if not q:
+            return
+        d["_deferred"] = []
+        side = d.get("_side_stream")
+        if side is None:
+            side = d["_side_stream"] = torch.cuda.Stream(device=self._genomes.data.device)
+        main = torch.cuda.current_stream()
+        side.wait_stream(main)
+        try:
+            with torch.cuda.stream(side):
+                for fn in q:
+                    fn()
+        finally:
+            main.wait_stream(side)
+
     def _reconcile(self) -> None:
+        if self.__dict__.get("_deferred"):
+            self._flush_deferred()
         if self.__dict__.get("_gp_state"):
             from magicsoup_amd.ops import genome_pipeline
 
@@ -471,7 +512,7 @@ class World:
         new = torch.arange(n0, n0 + k, device=self.device)
         self._place_new(n0, pos)
         world_ops.pickup_molecules(self, new, pos)
-        self._update_params_rows(new)
+        self._build_params_async(new)
         return list(range(n0, n0 + k))
 
     @_op("add_cells")
@@ -519,21 +560,11 @@ class World:
         empty = torch.zeros(0, dtype=torch.long, device=self.device)
         if (isinstance(cell_idxs, torch.Tensor) and cell_idxs.dtype == torch.bool and cell_idxs.is_cuda
                 and cell_idxs.numel() == self.n_cells and self.n_cells > 0):
-            # mask on the GPU: placement over the mask (priority = cell index, as for the ascending
-            # index list), one synchronisation for the winners
-            from magicsoup_amd.ops import hip_ops
-
-            def child_rows(k: int) -> torch.Tensor:  # the winners' pixels go straight to the new rows
-                n = self.n_cells
-                self._reserve(n + k)
-                return self._cols["cell_positions"].buf[n : n + k]
-
-            parents, child_pos = hip_ops.divide_placement_mask(self, cell_idxs, alloc_pos=child_rows)
-        else:
-            idxs = self._idx_tensor(cell_idxs)
-            if idxs.numel() == 0:
-                return empty, empty
-            parents, child_pos = world_ops.divide_placement(self, idxs)
+            return self._divide_mask_gpu(cell_idxs)
+        idxs = self._idx_tensor(cell_idxs)
+        if idxs.numel() == 0:
+            return empty, empty
+        parents, child_pos = world_ops.divide_placement(self, idxs)
         k = int(parents.numel())
         if k == 0:
             return empty, empty
@@ -542,13 +573,47 @@ class World:
         self._clone_rows(parents, children)
         if child_pos.is_cuda:
             # the placement kernels already claimed the pixels in cell_map
-            dst = self.cell_positions[n0 : n0 + k]
-            if dst.data_ptr() != child_pos.data_ptr():
-                dst.copy_(child_pos)
+            self.cell_positions[n0 : n0 + k] = child_pos
         else:
             self._place(children, child_pos)
         world_ops.split_cells(self, parents, children)
         return parents, children
+
+    def _divide_mask_gpu(self, mask: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        """Division over a GPU mask with one synchronisation at the very end: placement, winner
+        compaction, the commit of the new rows and the genome / label / parameter-row gather are
+        all issued against the device-side winner count into capacity reserved for the worst case
+        (every cell divides); the host then only adopts the count."""
+        from magicsoup_amd.ops import hip_ops
+
+        n = self.n_cells
+        self._reserve(2 * n)
+        kin = self.kinetics
+        kin._enter_slot_mode()
+        kin._slot_reserve(2 * n)
+        g, lab = self._genomes, self._labels
+        g.reserve(2 * n)
+        lab.reserve(2 * n)
+        par = torch.empty(n, dtype=torch.long, device=self.device)
+        children = torch.arange(n, 2 * n, device=self.device)
+        dcount, slot = hip_ops.divide_mask_issue(self, mask, n, par)
+        sb = kin.__dict__["_slot_buf"]
+        pairs = [(g.data[:n], g.data[n : 2 * n], g.lens), (g.lens[:n], g.lens[n : 2 * n]),
+                 (lab.data[:n], lab.data[n : 2 * n], lab.lens), (lab.lens[:n], lab.lens[n : 2 * n]),
+                 (sb[:n], sb[n : 2 * n])]
+        hip_ops.gather_rows(pairs, n, src_rows=par, dn=dcount)
+        k = hip_ops.wait_count(slot)
+        if k == 0:
+            empty = torch.zeros(0, dtype=torch.long, device=self.device)
+            return empty, empty
+        self.n_cells = n + k
+        for arena in (g, lab):
+            arena.n = n + k
+            arena.version += 1
+        kd = kin.__dict__
+        kd["_slot"] = sb[: n + k]
+        kd["_ncells"] += k
+        return par[:k], children[:k]
 
     @_op("update_cells")
     def update_cells(self, genome_idx_pairs: list[tuple[str, int]]):
@@ -575,7 +640,7 @@ class World:
             dead = torch.zeros(n, dtype=torch.bool, device=self.device)
             if t.numel() == 0:
                 return
-            dead[t.to(self.device, torch.long)] = True  # duplicates are harmless
+            dead.index_fill_(0, t.to(self.device, torch.long), True)  # duplicates are harmless
         world_ops.spill_and_free_mask(self, dead)
         if dead.is_cuda:
             from magicsoup_amd.ops import hip_ops
@@ -712,13 +777,27 @@ class World:
         cells are re-derived."""
         if self.n_cells == 0:
             return
-        if cell_idxs is None and self._genomes.data.is_cuda:
+        if cell_idxs is None and self._defer_genome_op():
+            self.__dict__.setdefault("_deferred", []).append(lambda: self._mutate_all(p, p_indel, p_del))
+            return
+        if cell_idxs is None:
+            return self._mutate_all(p, p_indel, p_del)
+        self._reconcile()
+        rows = self._idx_tensor(cell_idxs, unique=False)
+        changed = world_ops.point_mutations(self, rows, p, p_indel, p_del)
+        if changed.numel() > 0:
+            self._update_params_rows(changed)
+
+    def _mutate_all(self, p: float, p_indel: float, p_del: float) -> None:
+        if self.n_cells == 0:
+            return
+        if self._genomes.data.is_cuda:
             from magicsoup_amd.ops import genome_pipeline
 
             if genome_pipeline.point_mutations(self, p, p_indel, p_del):
                 return
         self._reconcile()
-        rows = None if cell_idxs is None else self._idx_tensor(cell_idxs, unique=False)
+        rows = None
         changed = world_ops.point_mutations(self, rows, p, p_indel, p_del)
         if changed.numel() > 0:
             self._update_params_rows(changed)
@@ -727,6 +806,14 @@ class World:
     def recombinate_cells(self, cell_idxs: list[int] | None = None, p: float = 1e-7):
         """Recombine the genomes of neighbouring cells (strand breaks with per-bp rate ``p`` and
         random re-joining); both genomes of every recombined pair are replaced."""
+        if self.n_cells < 2:
+            return
+        if cell_idxs is None and self._defer_genome_op():
+            self.__dict__.setdefault("_deferred", []).append(lambda: self._recombinate_all(p))
+            return
+        self._recombinate_all(p, cell_idxs)
+
+    def _recombinate_all(self, p: float, cell_idxs=None) -> None:
         if self.n_cells < 2:
             return
         if cell_idxs is None and self._genomes.data.is_cuda:
@@ -752,6 +839,16 @@ class World:
             self._update_params_rows(changed)
 
     # ------------------------------------------------------------------ params
+    def _build_params_async(self, rows: torch.Tensor) -> None:
+        """:meth:`_update_params_rows` through the device genome pipeline where it applies (GPU: no
+        synchronisation; resolved at the next op like mutate / recombinate)."""
+        if rows.is_cuda:
+            from magicsoup_amd.ops import genome_pipeline
+
+            if genome_pipeline.rebuild_rows(self, rows):
+                return
+        self._update_params_rows(rows)
+
     def _update_params_rows(self, rows: torch.Tensor) -> None:
         """Translate the genomes of ``rows`` and rebuild their kinetic parameters."""
         rows = rows.to(self.device, torch.long)
@@ -796,7 +893,8 @@ class World:
         state["_cell_map"] = self.cell_map.cpu()
         state["_pending_scale"] = None
         state["_pending_corr"] = None
-        for k in ("_hip_scratch", "_idx_map", "_diff_w", "_perm_t", "_degrade_t", "_gp_state"):
+        for k in ("_hip_scratch", "_idx_map", "_diff_w", "_perm_t", "_degrade_t", "_gp_state", "_deferred",
+                  "_side_stream"):
             state.pop(k, None)
         return state
 
@@ -853,9 +951,9 @@ class World:
 
     @_op("load_state")
     def load_state(self, statedir: Path, ignore_cell_params: bool = False):
-        self._reconcile()
         """Load a state written by :meth:`save_state` (re-translating genomes unless
         ``ignore_cell_params``)."""
+        self._reconcile()
         from magicsoup_amd.utils.checkpoint import load_state
 
         load_state(self, Path(statedir), ignore_cell_params=ignore_cell_params)

@@ -15,8 +15,8 @@ operations while the GPU works. What the host cannot rule out in advance raises 
   and is *replayed* at reconcile time with its original RNG stream, after the arena was widened and
   the result committed -- exactly the sequential outcome;
 * a proteome with more proteins than the parameter storage holds, more domains than the token
-  slots, or a genome too long for the LDS translation pass (``trans_check``), and parameter rows
-  running out (``assign_rows``): the affected cells are rebuilt on the synchronous path.
+  slots, or a genome too long for the LDS translation pass, and parameter rows running out
+  (``gp_check_assign_kernel``): the affected cells are rebuilt on the synchronous path.
 
 :func:`reconcile` resolves all of this; the World calls it before every op that reads genomes or
 parameters, changes cells or positions, or allocates rows (and the Kinetics object before any host
@@ -156,7 +156,8 @@ def _kin_desc(world, dev):
     k.slot = _p(kin._slot_tensor())
     N = store["N"]
     k.P, k.s = int(N.size(1)), int(N.size(2))
-    k.row_cap = min(int(t.size(0)) for t in store.values())
+    k.row_cap, free = kin._row_limit()
+    k.free = _p(free)
     k.vmax, k.km, k.signs, k.hills = _p(lu["vmax"]), _p(lu["km"]), _p(lu["signs"]), _p(lu["hills"])
     k.react, k.trnsp, k.eff, k.energies = _p(lu["react"]), _p(lu["trnsp"]), _p(lu["eff"]), _p(lu["energies"])
     k.nw, k.nk, k.nsg, k.nh = lu["vmax"].numel(), lu["km"].numel(), lu["signs"].numel(), lu["hills"].numel()
@@ -172,61 +173,6 @@ def _blob(world, kind: str, nbytes: int, dev) -> torch.Tensor:
 def _view(blob: torch.Tensor, off: int, n: int, dtype) -> torch.Tensor:
     es = torch.empty(0, dtype=dtype).element_size()
     return blob[off : off + n * es].view(dtype)
-
-
-def _rebuild(world, b: dict, cells: torch.Tensor, dcnt: torch.Tensor, cap: int) -> None:
-    """Translate the genomes of ``cells[:*dcnt]`` and build their parameters into fresh rows."""
-    from magicsoup_amd.constants import GAS_CONSTANT
-    from magicsoup_amd.ops.kinetics_ops import build_luts
-
-    kin = world.kinetics
-    genetics = world.genetics
-    arena = world._genomes
-    dev = arena.data.device
-    sc = _scratch(world)
-    luts = genetics.device_luts(dev)
-    tables = genetics.tables
-    P = kin._P()
-    counts = sc.get("gp_counts", 2 * cap, torch.int32, dev)
-    ndom = sc.get("gp_ndom", 2 * cap, torch.int32, dev)
-    long_list = sc.get("gp_long", cap, torch.int32, dev)
-    long_count = sc.get("gp_long_n", 1, torch.int32, dev)
-    per = sc.get("gp_per", cap, torch.int32, dev)
-    rows_out = sc.get("gp_rows_out", cap, torch.int32, dev)
-    tokens = sc.get("gp_tokens", cap * P * D_CAP * 5, torch.int32, dev)
-    long_count.zero_()
-    data, lens = arena.data, arena.lens
-    width = int(data.size(1))
-    common = (_p(luts["small"]), _p(luts["dom_type"]), int(luts["dom_type"].numel()), _p(luts["two_codon"]),
-              tables.dom_size, tables.dom_type_size)
-    st = _stream()
-    of = _p(b["opflags"])
-    # one fused translation pass into the speculative (P, D_CAP) layout; trans_check flags proteomes
-    # that do not fit it
-    _m().zero_rows(cap, _p(dcnt), P * D_CAP * 5, _p(tokens), st)
-    _m().translate_fused(cap, _p(cells), _p(data), width, _p(lens), *common, _p(counts), _p(ndom), P, D_CAP,
-                         _p(tokens), _p(long_list), _p(long_count), _p(dcnt), st)
-    _m().trans_check(cap, _p(dcnt), _p(counts), _p(ndom), _p(long_count), _p(per), P, D_CAP, of, st)
-    store = kin._kernel_params()
-    kin._enter_slot_mode()
-    slot = kin._slot_tensor()
-    row_cap = min(int(t.size(0)) for t in store.values())
-    _m().assign_rows(cap, _p(dcnt), _p(cells), _p(slot), _p(b["d_rows"]), row_cap, _p(rows_out), of, st)
-    kl = build_luts(kin, dev)
-    hip_ops.build_params(kin, tokens.view(cap, P, D_CAP, 5), rows_out, kl, store, float(kin.abs_temp), GAS_CONSTANT,
-                         nprot=per, dn=dcnt)
-
-
-def _finish(world, kind: str, args: tuple, rng: tuple, b: dict, cells, dcnt, replay: dict, status_cnt=None) -> None:
-    """Have the device write {rebuilt count, op flags, row counter, selected count (or the number of
-    result rows, ``status_cnt``)} into a pinned host slot (one launch) and record the call as pending."""
-    cnt = b["cnt"] if status_cnt is None else status_cnt
-    slot = _m().status_write(_p(dcnt), _p(b["opflags"]), _p(b["d_rows"]), _p(cnt), _stream())
-    host = _StatusSlot(slot)
-    ev = torch.cuda.Event()
-    ev.record()
-    _state(world)["pending"].append(_Pending(kind, args, rng, cells, host, ev, replay))
-    world._genomes.version += 1
 
 
 def _record(world, kind: str, args: tuple, rng: tuple, cells, slot: int, replay: dict) -> None:
@@ -309,20 +255,25 @@ def recombinate_all(world, p: float, extra=None) -> bool:
 
 
 def rebuild_rows(world, rows: torch.Tensor) -> bool:
-    """Translate and build parameters of the cells ``rows`` (e.g. cells that arrived from another
-    rank) into fresh parameter rows without a synchronisation; resolved by :func:`reconcile` like
-    the other pipeline calls. False if the caller should take the synchronous path."""
+    """Translate and build parameters of the cells ``rows`` (e.g. spawned cells, or cells that
+    arrived from another rank) into fresh parameter rows without a synchronisation (one C++ call,
+    gp.hip gp_rebuild); resolved by :func:`reconcile` like the other pipeline calls. False if the
+    caller should take the synchronous path."""
     k = int(rows.numel())
     if k == 0:
         return True
-    if not enabled(world) or k > N_CAP:
-        return False
+    if not enabled(world) or k > N_CAP or world.kinetics._P() == 0:
+        return False  # (no protein slots yet: the synchronous path sizes the storage)
     b = _begin(world, "imm")
     dcnt = b["cnt"]
     dcnt[:1].fill_(k)
     cells = rows.to(torch.int64).contiguous()
-    _rebuild(world, b, cells, dcnt, k)
-    _finish(world, "imm", (), None, b, cells, dcnt, {})
+    dev = cells.device
+    kd = _kin_desc(world, dev)
+    blob = _blob(world, "imm", _m().gp_blob_bytes(2, k, k, kd.P, 0, D_CAP, 0, 0), dev)
+    slot = _m().gp_rebuild(_arena_desc(world, b), _gen_desc(world, dev), kd, _p(cells), _p(dcnt), k, D_CAP,
+                           _p(blob), _stream())
+    _record(world, "imm", (), None, cells, slot, {})
     return True
 
 

@@ -465,6 +465,39 @@ def divide_placement_mask(world, mask: torch.Tensor, alloc_pos=None):
     return par, npos
 
 
+def divide_mask_issue(world, mask: torch.Tensor, n0: int, par: torch.Tensor):
+    """divide_cells over a bool mask of all cells, issued without a synchronisation (world.hip
+    divide_mask_dev): placement, winners compacted on the device and committed into rows ``n0..``
+    (positions, halved molecules, divisions, lifetimes; the caller reserved the capacity); the
+    parents go to ``par`` (int64 (n,), the first k valid). Returns (device count int32[2], status
+    slot): gather the rows that are copied with ``dn`` = the device count, then :func:`wait_count`
+    the slot for k."""
+    R, C, r_lo, r_hi, wrap = geom(world)
+    mask = mask.view(torch.uint8) if mask.dtype == torch.bool else mask.to(torch.uint8)
+    mask = mask.contiguous()
+    n = int(mask.numel())
+    dev = mask.device
+    _ensure_world_layout(world)
+    cols = world._cols
+    cmap = _cell_map_bytes(world)
+    sc = _scratch(world)
+    claim = world.__dict__.get("_claim_map")
+    if claim is None or claim.numel() != R * C or claim.device != dev:
+        claim = torch.full((R * C,), 0x7FFFFFFF, dtype=torch.int32, device=dev)
+        world.__dict__["_claim_map"] = claim
+    pending = sc.get("pl_pending", n, torch.uint8, dev)
+    cand = sc.get("pl_cand", n, torch.int64, dev)
+    result = sc.get("pl_result", n, torch.int64, dev)
+    wins = sc.get("dv_wins", n, torch.int64, dev)
+    dcount = sc.get("dv_count", 2, torch.int32, dev)
+    seed, call = _rng()
+    slot = _m().divide_mask_dev(n, _p(mask), _p(cols["cell_positions"].buf), R, C, r_lo, r_hi, wrap, _p(cmap),
+                                _p(pending), _p(cand), _p(claim), _p(result), _PLACE_ROUNDS, seed, call, _p(wins),
+                                _p(dcount), int(n0), int(world.n_molecules), _p(par), _p(cols["cell_molecules"].buf),
+                                _p(cols["cell_divisions"].buf), _p(cols["cell_lifetimes"].buf), _stream())
+    return dcount, slot
+
+
 def move_placement(world, idxs: torch.Tensor):
     return _place_rounds(world, idxs.to(torch.int64).contiguous(), vacate=True)
 

@@ -1,6 +1,7 @@
 """cProfile of repeated calls of one World op on a small GPU population (host-side cost breakdown).
 
-usage: python scripts/op_cprofile.py <op: recombinate|mutate|kill|divide|activity|spawn|diffuse> [reps]"""
+usage: python scripts/op_cprofile.py <op: recombinate|mutate|kill|kill50|divide|divide50|activity|spawn|diffuse> [reps]
+    [cells]"""
 import cProfile
 import os
 import pstats
@@ -16,10 +17,11 @@ from magicsoup_amd.examples.wood_ljungdahl import CHEMISTRY  # noqa: E402
 op = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 w = ms.World(chemistry=CHEMISTRY, map_size=1448, device="cuda", seed=0)
-w.spawn_cells(bench.random_genomes(6250, 500, "cuda"))
+ncell = int(sys.argv[3]) if len(sys.argv) > 3 else 6250
+w.spawn_cells(bench.random_genomes(ncell, 500, "cuda"))
 atp = CHEMISTRY.molname_2_idx["ATP"]
 for _ in range(10):
-    bench.step(w, 6250, 500, atp)
+    bench.step(w, ncell, 500, atp)
 torch.cuda.synchronize()
 few = torch.zeros(w.n_cells, dtype=torch.bool, device="cuda")
 fns = {
@@ -27,6 +29,8 @@ fns = {
     "mutate": lambda: w.mutate_cells(),
     "kill": lambda: w.kill_cells(torch.zeros(w.n_cells, dtype=torch.bool, device="cuda")),
     "divide": lambda: w.divide_cells_t(torch.zeros(w.n_cells, dtype=torch.bool, device="cuda")),
+    "divide50": lambda: w.divide_cells_t(torch.rand(w.n_cells, device="cuda") < 50 / w.n_cells),
+    "kill50": lambda: w.kill_cells(torch.rand(w.n_cells, device="cuda") < 50 / w.n_cells),
     "activity": lambda: w.enzymatic_activity(),
     "spawn": lambda: w.spawn_cells(bench.random_genomes(20, 500, "cuda")),
     "diffuse": lambda: w.diffuse_molecules(),

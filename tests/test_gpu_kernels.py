@@ -593,6 +593,30 @@ def test_device_genome_pipeline_matches_sync_path(monkeypatch, d_cap):
     assert torch.equal(x0, x1)
 
 
+def test_deferred_genome_ops_match_immediate_issue(monkeypatch):
+    """All-cells mutate / recombinate are queued until the next op that reads genomes, parameters
+    or cells (degrade / diffuse / lifetimes run in between): same genomes, parameters and
+    trajectory as issuing them immediately; reading ``cell_genomes`` flushes the queue."""
+    import magicsoup_amd.models.world as world_mod
+
+    base = _world("cuda", map_size=64, n=800, s=400, seed=7)
+    monkeypatch.setattr(world_mod, "_DEFER_ENV", "0")
+    g0, p0, x0 = _genetics_run(monkeypatch, base, sync=False)
+    monkeypatch.setattr(world_mod, "_DEFER_ENV", "1")
+    g1, p1, x1 = _genetics_run(monkeypatch, base, sync=False)
+    assert g0 == g1
+    for k in p0:
+        assert torch.equal(p0[k], p1[k]), k
+    assert torch.equal(x0, x1)
+    w = copy.deepcopy(base)
+    w.recombinate_cells(p=1e-4)
+    w.mutate_cells(p=1e-3)
+    w.diffuse_molecules()
+    assert len(w.__dict__.get("_deferred", [])) == 2
+    genomes = list(w.cell_genomes)
+    assert not w.__dict__["_deferred"] and len(genomes) == w.n_cells
+
+
 def _integrate_modes(kin, X, modes=(0, 8)):
     from magicsoup_amd.ops import kinetics_ops
 
@@ -642,19 +666,35 @@ def test_register_integrator_matches_lds_integrator_bit_for_bit(case):
     assert not torch.equal(out[0], X)
 
 
-def test_parameter_rows_follow_genomes_through_bench_steps():
+@pytest.mark.parametrize("recycle", [False, True])
+def test_parameter_rows_follow_genomes_through_bench_steps(monkeypatch, recycle):
     """After kills (the cell -> row map gathered with the columns), divisions (cloned in the same
     gather), mutations / recombinations (device pipeline) and spawns, every cell's parameters equal
-    a fresh translation + build of its current genome."""
+    a fresh translation + build of its current genome. ``recycle``: the fresh storage rows are
+    declared used up midway, so later builds take recycled rows of dead cells (free list)."""
     import bench
 
+    recycled = []
+    orig = Kinetics._recycle_rows
+
+    def spy(self, k):
+        out = orig(self, k)
+        recycled.append(out is not None)
+        return out
+
+    monkeypatch.setattr(Kinetics, "_recycle_rows", spy)
     atp = CHEMISTRY.molname_2_idx["ATP"]
     w = _world("cuda", map_size=128, n=3000, s=500)
-    for _ in range(8):
+    for i in range(8):
+        if recycle and i == 4:
+            w._reconcile()
+            kin = w.kinetics
+            kin.__dict__["_nrows"] = kin._row_limit()[0]  # every fresh row taken
         bench.step(w, 3000, 500, atp)
         w.mutate_cells(p=1e-4)
         w.recombinate_cells(p=1e-5)
     w._reconcile()
+    assert any(recycled) == recycle, recycled
     ref = copy.deepcopy(w)
     ref._update_params_rows(torch.arange(ref.n_cells, device="cuda"))
     ka, kb = w.kinetics, ref.kinetics
