@@ -22,7 +22,6 @@ import os
 import sys
 import time
 
-import numpy as np
 import torch
 
 BASELINE_STEPS_PER_S = 3.3  # reference, 40k cells, latest published
@@ -72,22 +71,14 @@ def random_genomes(k: int, size: int, device) -> tuple[torch.Tensor, torch.Tenso
     return rows, torch.full((k,), size, dtype=torch.int32, device=device)
 
 
-_DILUTE = {"rng": np.random.default_rng(0), "pinned": None}
 _CHEMOSTAT = {"divided": 0, "starved": 0}  # previous step's divisions / starvation deaths (dilution estimates)
 
 
 def _dilution_sample(n: int, k: int, device) -> torch.Tensor:
-    """k distinct uniform indices < n: sampled on the host (Floyd-style, ~30 us for k = 1000) and
-    shipped through a reused pinned buffer -- a device randperm costs a full sort of n keys."""
-    idx = _DILUTE["rng"].choice(n, size=k, replace=False)
-    if device == "cpu" or str(device) == "cpu":
-        return torch.from_numpy(idx)
-    buf = _DILUTE["pinned"]
-    if buf is None or buf.numel() < k:
-        buf = _DILUTE["pinned"] = torch.empty(max(k, 4096) * 2, dtype=torch.int64, pin_memory=True)
-    # the previous step's copy out of this buffer has completed (kill_cells synchronises)
-    buf[:k].copy_(torch.from_numpy(idx))
-    return buf[:k].to(device, non_blocking=True)
+    """k distinct uniform indices < n (a device permutation: one launch, no host work)."""
+    if str(device) == "cpu":
+        return torch.randperm(n)[:k]
+    return torch.randperm(n, device=device)[:k]
 
 
 def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=None):
@@ -105,6 +96,11 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
         if n < n_target:
             world.spawn_cells(random_genomes(n_target - n, genome_size, world.cell_molecules.device))
             note("spawned", n_target - n)
+        # chemostat dilution (see kill below): the random cells depend only on the population size
+        n0 = world.n_cells
+        keep = n_target + n_target // 100 - _CHEMOSTAT["divided"] + _CHEMOSTAT["starved"]
+        excess = min(n0 - keep, n0)
+        dilute = _dilution_sample(n0, excess, world.cell_molecules.device) if excess > 0 else None
     with ph("activity"):
         world.enzymatic_activity()
     with ph("kill"):
@@ -115,11 +111,8 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
         # after the divisions that follow the population is back at n_target plus a 1 % margin (the
         # previous step's divisions and starvation deaths are the estimates). The margin keeps the
         # next step's top-up (a spawn) rare; activity always runs on >= n_target cells.
-        n0 = world.n_cells
-        keep = n_target + n_target // 100 - _CHEMOSTAT["divided"] + _CHEMOSTAT["starved"]
-        excess = min(n0 - keep, n0)
-        if excess > 0:
-            kill.index_fill_(0, _dilution_sample(n0, excess, kill.device), True)
+        if dilute is not None:
+            kill.index_fill_(0, dilute, True)
             note("diluted", excess)
         world.kill_cells(kill)
         _CHEMOSTAT["starved"] = max(0, n0 - world.n_cells - max(excess, 0))
@@ -185,7 +178,6 @@ def main():
     atp = chem.molname_2_idx.get("ATP", 0)
     ms.set_seed(a.seed + rank)
     torch.manual_seed(a.seed + rank)
-    _DILUTE["rng"] = np.random.default_rng(a.seed + rank)
 
     if distributed:
         from magicsoup_amd.parallel import DistributedWorld

@@ -479,6 +479,36 @@ void spill_free_mask(int n, int m, uintptr_t dead, uintptr_t pos, int R, int C, 
   MS_LAUNCH_CHECK();
 }
 
+// Save / restore the state an enzymatic_activity changes: cell molecules and the raw map values
+// (no pending correction applied) of the cells' pixels, as (n, 2m) floats (bf16 / fp16 storage
+// round-trips exactly through float). Lets the World issue the activity before pending parameter
+// rebuilds are confirmed and undo it in the rare case one had to be redone on the host.
+__global__ void __launch_bounds__(256) cell_state_io_kernel(int n, int m, const int32_t* pos, int C, long long plane,
+                                                            void* map, int dtype, float* cell_mols, float* buf,
+                                                            int restore) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)n * m) return;
+  const int i = (int)(t / m), j = (int)(t - (long long)i * m);
+  const size_t px = (size_t)pos[2 * i] * C + pos[2 * i + 1] + (size_t)j * plane;
+  float* row = buf + (size_t)i * 2 * m;
+  if (restore) {
+    cell_mols[(size_t)i * m + j] = row[j];
+    st_map(map, px, row[m + j], dtype);
+  } else {
+    row[j] = cell_mols[(size_t)i * m + j];
+    row[m + j] = ld_map(map, px, dtype);
+  }
+}
+
+void cell_state_io(int n, int m, uintptr_t pos, int R, int C, uintptr_t map, int dtype, uintptr_t cell_mols,
+                   uintptr_t buf, bool restore, uintptr_t stream) {
+  if (n <= 0 || m <= 0) return;
+  cell_state_io_kernel<<<cdiv((long long)n * m, 256), 256, 0, S_(stream)>>>(
+      n, m, P_<int32_t>(pos), C, (long long)R * C, P_<void>(map), dtype, P_<float>(cell_mols), P_<float>(buf),
+      restore ? 1 : 0);
+  MS_LAUNCH_CHECK();
+}
+
 void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map, int dtype,
             uintptr_t corr, uintptr_t stream) {
   if (k <= 0 || m <= 0) return;

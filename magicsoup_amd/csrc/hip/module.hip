@@ -46,6 +46,8 @@ void spill_free_mask(int n, int m, uintptr_t dead, uintptr_t pos, int R, int C, 
                      uintptr_t cell_map, int dtype, uintptr_t corr, uintptr_t stream);
 void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map, int dtype,
             uintptr_t corr, uintptr_t stream);
+void cell_state_io(int n, int m, uintptr_t pos, int R, int C, uintptr_t map, int dtype, uintptr_t cell_mols,
+                   uintptr_t buf, bool restore, uintptr_t stream);
 void permeate(int c, int m, int R, int C, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map, int dtype,
               uintptr_t corr, uintptr_t stream);
 void gather_rows(int n, uintptr_t dn, uintptr_t src_rows, uintptr_t dst_rows,
@@ -216,6 +218,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("rec_apply", &msd::rec_apply);
   m.def("arena_scatter", &msd::arena_scatter);
   m.def("place_collect", &msd::place_collect);
+  m.def("cell_state_io", &msd::cell_state_io, "save / restore cell molecules + raw pixel values under the cells");
   m.def("divide_mask_dev", &msd::divide_mask_dev,
         "divide_cells over a mask: placement, winner compaction and commit issued without a sync; returns the status slot");
   m.def("translate_stats", &msd::translate_stats,

@@ -553,7 +553,7 @@ class Kinetics:
         """Make room for k fresh rows without taking them (the device genome pipeline takes them
         with its own device-side row counter, magicsoup_amd.ops.genome_pipeline)."""
         self._sync()
-        self._alloc_rows_now(k)
+        self._alloc_rows_now(k, want=False)
         self.__dict__["_nrows"] -= k
 
     def _row_limit(self) -> tuple[int, torch.Tensor | None]:
@@ -565,7 +565,7 @@ class Kinetics:
             return int(free.numel()), free
         return min(int(t.size(0)) for t in self._store.values()), None
 
-    def _alloc_rows_now(self, k: int) -> torch.Tensor:
+    def _alloc_rows_now(self, k: int, want: bool = True) -> torch.Tensor | None:
         """k unused storage rows (int64, device) for cells whose parameters are about to be written.
         Rows of removed cells are not tracked as they die (a row may be shared); when the fresh rows
         run out, the rows no live cell maps to are collected into a free list (no parameter data
@@ -577,6 +577,8 @@ class Kinetics:
             free = self._recycle_rows(k)
         r0 = d["_nrows"]
         d["_nrows"] = r0 + k
+        if not want:
+            return None
         if free is not None:
             return free[r0 : r0 + k]
         return torch.arange(r0, r0 + k, device=self._store["N"].device)

@@ -61,8 +61,13 @@ def _op(name: str):
         @functools.wraps(fn)
         def wrapper(self, *args, **kwargs):
             d = self.__dict__
+            if d.get("_spec") is not None:
+                self._reconcile()  # a speculative activity is confirmed (or redone) before anything else
             if (d.get("_gp_state") or d.get("_deferred")) and name not in _PIPELINE_SAFE_OPS:
-                self._reconcile()
+                if name == "enzymatic_activity" and self._speculate():
+                    self._flush_deferred()  # issue the queued chains; confirmed after the activity
+                else:
+                    self._reconcile()
             timer, check = d.get("_timer"), d.get("_debug_checks", _CHECK_ENV)
             if timer is None and not check and not profiling.roctx_enabled():
                 return fn(self, *args, **kwargs)
@@ -263,6 +268,28 @@ class World:
 
         return genome_pipeline.enabled(self)
 
+    def _speculate(self) -> bool:
+        """Whether enzymatic_activity may run before the pending device-pipeline calls are confirmed.
+
+        The host confirmation waits for the rebuild chains, which share the device with the
+        diffusion stencil; issuing the activity first keeps the device busy meanwhile. The state
+        the activity changes is saved first; the next access to molecules, or the next op,
+        confirms the calls and -- only if one had to be redone on the host -- restores that state
+        and runs the activity again with the corrected parameters. Single-process GPU worlds only
+        (a decomposed world's activity is collective)."""
+        d = self.__dict__
+        return (_DEFER_ENV != "0" and d.get("_timer") is None and self._genomes.data.is_cuda
+                and getattr(self, "_allreduce_flags", None) is None)
+
+    def _defer(self, fn) -> None:
+        d = self.__dict__
+        q = d.setdefault("_deferred", [])
+        if not q:
+            ev = torch.cuda.Event()
+            ev.record()
+            d["_defer_event"] = ev
+        q.append(fn)
+
     def _flush_deferred(self) -> None:
         """Issue the queued genome ops, in call order, on a side stream: their chains run next to
         the diffusion stencil still executing on the compute stream (disjoint state), and the compute
@@ -274,9 +301,13 @@ class World:
         d["_deferred"] = []
         side = d.get("_side_stream")
         if side is None:
-            side = d["_side_stream"] = torch.cuda.Stream(device=self._genomes.data.device)
+            # high priority: the short chain kernels are dispatched ahead of the stencil's waiting
+            # workgroups (the next op's reconcile waits for the chains)
+            side = d["_side_stream"] = torch.cuda.Stream(device=self._genomes.data.device, priority=-1)
         main = torch.cuda.current_stream()
-        side.wait_stream(main)
+        # the chains depend on the state as of the first queued call (recorded then), not on the
+        # molecule-only work issued since (e.g. the diffusion stencil they run next to)
+        side.wait_event(d.pop("_defer_event"))
         try:
             with torch.cuda.stream(side):
                 for fn in q:
@@ -301,8 +332,12 @@ class World:
         d = self.__dict__
         cols = d.get("_cols")
         if cols is not None and name in cols:
+            if d.get("_spec") is not None:
+                self._reconcile()
             return cols[name].view(d["n_cells"])
         if name == "molecule_map" and "_molmap" in d:
+            if d.get("_spec") is not None:
+                self._reconcile()
             if d.get("_pending_scale") is not None or d.get("_pending_corr") is not None:
                 from magicsoup_amd.ops import hip_ops
 
@@ -750,7 +785,16 @@ class World:
         the molecule map pixels under the cells)."""
         if self.n_cells == 0:
             return
+        st = self.__dict__.get("_gp_state")
+        spec = None
+        if st and st["pending"]:
+            # speculative: issued on top of unconfirmed parameter rebuilds (see _speculate)
+            from magicsoup_amd.ops import hip_ops
+
+            spec = hip_ops.save_cell_state(self)
         world_ops.enzymatic_activity(self)
+        if spec is not None:
+            self.__dict__["_spec"] = spec
 
     @_op("diffuse_molecules")
     @torch.no_grad()
@@ -778,7 +822,7 @@ class World:
         if self.n_cells == 0:
             return
         if cell_idxs is None and self._defer_genome_op():
-            self.__dict__.setdefault("_deferred", []).append(lambda: self._mutate_all(p, p_indel, p_del))
+            self._defer(lambda: self._mutate_all(p, p_indel, p_del))
             return
         if cell_idxs is None:
             return self._mutate_all(p, p_indel, p_del)
@@ -809,7 +853,7 @@ class World:
         if self.n_cells < 2:
             return
         if cell_idxs is None and self._defer_genome_op():
-            self.__dict__.setdefault("_deferred", []).append(lambda: self._recombinate_all(p))
+            self._defer(lambda: self._recombinate_all(p))
             return
         self._recombinate_all(p, cell_idxs)
 
@@ -894,7 +938,7 @@ class World:
         state["_pending_scale"] = None
         state["_pending_corr"] = None
         for k in ("_hip_scratch", "_idx_map", "_diff_w", "_perm_t", "_degrade_t", "_gp_state", "_deferred",
-                  "_side_stream"):
+                  "_side_stream", "_defer_event", "_gp_cache", "_spec"):
             state.pop(k, None)
         return state
 

@@ -87,16 +87,28 @@ def _state(world) -> dict:
     return st
 
 
+def _cache(world) -> dict:
+    """Per-world cache of the call descriptors (dropped with the world's pickled state)."""
+    c = world.__dict__.get("_gp_cache")
+    if c is None:
+        c = world.__dict__["_gp_cache"] = {}
+    return c
+
+
 def _bufs(world, kind: str) -> dict:
-    sc = _scratch(world)
-    dev = world._genomes.data.device
-    return {
-        "cnt": sc.get(f"gp_cnt_{kind}", 2, torch.int32, dev),
-        "cnt2": sc.get(f"gp_cnt2_{kind}", 2, torch.int32, dev),
-        "opflags": sc.get(f"gp_opflags_{kind}", 1, torch.int32, dev),
-        "gflags": sc.get("gp_gflags", 1, torch.int32, dev),
-        "d_rows": sc.get("gp_rows", 1, torch.int64, dev),
-    }
+    c = _cache(world)
+    b = c.get(kind)
+    if b is None:
+        sc = _scratch(world)
+        dev = world._genomes.data.device
+        b = c[kind] = {
+            "cnt": sc.get(f"gp_cnt_{kind}", 2, torch.int32, dev),
+            "cnt2": sc.get(f"gp_cnt2_{kind}", 2, torch.int32, dev),
+            "opflags": sc.get(f"gp_opflags_{kind}", 1, torch.int32, dev),
+            "gflags": sc.get("gp_gflags", 1, torch.int32, dev),
+            "d_rows": sc.get("gp_rows", 1, torch.int64, dev),
+        }
+    return b
 
 
 def _usable(world, expected: float) -> bool:
@@ -108,7 +120,7 @@ def _begin(world, kind: str) -> dict:
     reused); with nothing pending the shared flags and the device row counter are (re)set from
     the host, after making room for two calls' worth of fresh rows."""
     st = _state(world)
-    if any(pd.kind == kind for pd in st["pending"]):
+    if st["pending"] and any(pd.kind == kind for pd in st["pending"]):
         reconcile(world)
     kin = world.kinetics
     b = _bufs(world, kind)
@@ -121,48 +133,67 @@ def _begin(world, kind: str) -> dict:
 
 def _arena_desc(world, b: dict):
     """C++ descriptor of the genome arena and this call's device counters (gp.hip GpArena)."""
+    a = b.get("desc")
+    if a is None:
+        a = b["desc"] = _m().GpArena()
+        a.cnt, a.cnt2, a.opflags, a.gflags, a.d_rows = (_p(b["cnt"]), _p(b["cnt2"]), _p(b["opflags"]),
+                                                        _p(b["gflags"]), _p(b["d_rows"]))
     arena = world._genomes
-    a = _m().GpArena()
-    a.data, a.lens, a.width, a.n = _p(arena.data), _p(arena.lens), int(arena.width), int(arena.n)
-    a.cnt, a.cnt2, a.opflags, a.gflags, a.d_rows = (_p(b["cnt"]), _p(b["cnt2"]), _p(b["opflags"]), _p(b["gflags"]),
-                                                    _p(b["d_rows"]))
+    a.data, a.lens, a.width, a.n = arena.data.data_ptr(), arena.lens.data_ptr(), arena.width, arena.n
     return a
 
 
 def _gen_desc(world, dev):
-    g = _m().GpGen()
     luts = world.genetics.device_luts(dev)
+    c = _cache(world)
+    hit = c.get("gen")
+    if hit is not None and hit[0] is luts:
+        return hit[1]
+    g = _m().GpGen()
     tables = world.genetics.tables
     g.small, g.dom_type, g.two_codon = _p(luts["small"]), _p(luts["dom_type"]), _p(luts["two_codon"])
     g.dt_entries, g.dom_size, g.dom_type_size = int(luts["dom_type"].numel()), tables.dom_size, tables.dom_type_size
+    c["gen"] = (luts, g)
     return g
 
 
 def _kin_desc(world, dev):
-    """Parameter storage (kernel layout, capacity rows), token LUTs and the cell -> row map."""
-    from magicsoup_amd.constants import GAS_CONSTANT
-    from magicsoup_amd.ops.kinetics_ops import build_luts
-
+    """Parameter storage (kernel layout, capacity rows), token LUTs, the cell -> row map and the
+    free-row list. Rebuilt only when the storage layout changed; the row map pointer (swapped by
+    every compaction) is refreshed on each call."""
     kin = world.kinetics
     store = kin._kernel_params()
     kin._enter_slot_mode()
     packed = kin._pack_ok()
-    lu = build_luts(kin, dev)
-    k = _m().GpKin()
-    k.N, k.Nf, k.Nb, k.A, k.Kmr = (_p(store[n]) for n in ("N", "Nf", "Nb", "A", "Kmr"))
-    k.Kmf, k.Kmb, k.Vmax, k.Ke = (_p(store[n]) for n in ("Kmf", "Kmb", "Vmax", "Ke"))
-    if packed:
-        k.W, k.Q, k.overflow = _p(store["_W"]), _p(store["_Q"]), _p(hip_ops._overflow_flag(kin))
-    k.slot = _p(kin._slot_tensor())
+    row_cap, free = kin._row_limit()
     N = store["N"]
-    k.P, k.s = int(N.size(1)), int(N.size(2))
-    k.row_cap, free = kin._row_limit()
-    k.free = _p(free)
-    k.vmax, k.km, k.signs, k.hills = _p(lu["vmax"]), _p(lu["km"]), _p(lu["signs"]), _p(lu["hills"])
-    k.react, k.trnsp, k.eff, k.energies = _p(lu["react"]), _p(lu["trnsp"]), _p(lu["eff"]), _p(lu["energies"])
-    k.nw, k.nk, k.nsg, k.nh = lu["vmax"].numel(), lu["km"].numel(), lu["signs"].numel(), lu["hills"].numel()
-    k.nv = int(lu["react"].size(0))
-    k.abs_temp, k.gas = float(kin.abs_temp), float(GAS_CONSTANT)
+    key = (N.data_ptr(), N.size(1), N.size(2), store["Kmr"].data_ptr(), store["Vmax"].data_ptr(),
+           store["_W"].data_ptr() if packed else 0, store["_Q"].data_ptr() if packed else 0, row_cap,
+           _p(free), float(kin.abs_temp), id(store))
+    c = _cache(world)
+    hit = c.get("kin")
+    if hit is not None and hit[0] == key:
+        k = hit[1]
+    else:
+        from magicsoup_amd.constants import GAS_CONSTANT
+        from magicsoup_amd.ops.kinetics_ops import build_luts
+
+        lu = build_luts(kin, dev)
+        k = _m().GpKin()
+        k.N, k.Nf, k.Nb, k.A, k.Kmr = (_p(store[n]) for n in ("N", "Nf", "Nb", "A", "Kmr"))
+        k.Kmf, k.Kmb, k.Vmax, k.Ke = (_p(store[n]) for n in ("Kmf", "Kmb", "Vmax", "Ke"))
+        if packed:
+            k.W, k.Q, k.overflow = _p(store["_W"]), _p(store["_Q"]), _p(hip_ops._overflow_flag(kin))
+        k.P, k.s = int(N.size(1)), int(N.size(2))
+        k.row_cap, k.free = row_cap, _p(free)
+        k.vmax, k.km, k.signs, k.hills = _p(lu["vmax"]), _p(lu["km"]), _p(lu["signs"]), _p(lu["hills"])
+        k.react, k.trnsp, k.eff, k.energies = _p(lu["react"]), _p(lu["trnsp"]), _p(lu["eff"]), _p(lu["energies"])
+        k.nw, k.nk, k.nsg, k.nh = lu["vmax"].numel(), lu["km"].numel(), lu["signs"].numel(), lu["hills"].numel()
+        k.nv = int(lu["react"].size(0))
+        k.abs_temp, k.gas = float(kin.abs_temp), float(GAS_CONSTANT)
+        # the LUT tensors stay referenced by the cache entry while their pointers are in use
+        c["kin"] = (key, k, lu)
+    k.slot = kin._slot_tensor().data_ptr()
     return k
 
 
@@ -170,9 +201,27 @@ def _blob(world, kind: str, nbytes: int, dev) -> torch.Tensor:
     return _scratch(world).get(f"gp_blob_{kind}", nbytes, torch.uint8, dev)
 
 
+_ES = {torch.uint8: 1, torch.int32: 4, torch.int64: 8}
+
+
 def _view(blob: torch.Tensor, off: int, n: int, dtype) -> torch.Tensor:
-    es = torch.empty(0, dtype=dtype).element_size()
-    return blob[off : off + n * es].view(dtype)
+    return blob[off : off + n * _ES[dtype]].view(dtype)
+
+
+class _Replay:
+    """What reconcile needs to re-commit a call's results (views into the call's scratch blob,
+    made only when needed)."""
+
+    __slots__ = ("blob", "lay", "n", "mark", "gen", "direct", "rows_key")
+
+    def __init__(self, blob, lay, n, rows_key, mark=None, gen=0, direct=False):
+        self.blob, self.lay, self.n, self.rows_key = blob, lay, n, rows_key
+        self.mark, self.gen, self.direct = mark, gen, direct
+
+    def views(self):
+        lay, n, b = self.lay, self.n, self.blob
+        return (_view(b, lay[self.rows_key], n, torch.int64), _view(b, lay["out"], n * lay["out_w"], torch.uint8),
+                lay["out_w"], _view(b, lay["out_len"], n, torch.int32))
 
 
 def _record(world, kind: str, args: tuple, rng: tuple, cells, slot: int, replay: dict) -> None:
@@ -204,9 +253,7 @@ def point_mutations(world, p: float, p_indel: float, p_del: float) -> bool:
                           seed, call, cap, K_CAP, D_CAP, _p(blob), _stream())
     lay = _m().gp_layout(0, n, cap, L, K_CAP, 0)
     sel = _view(blob, lay["sel"], n, torch.int64)
-    _record(world, "mut", (p, p_indel, p_del), (seed, call), sel, slot,
-            {"rows": sel, "out": _view(blob, lay["out"], cap * lay["out_w"], torch.uint8), "out_w": lay["out_w"],
-             "out_len": _view(blob, lay["out_len"], cap, torch.int32)})
+    _record(world, "mut", (p, p_indel, p_del), (seed, call), sel, slot, _Replay(blob, lay, cap, "sel"))
     return True
 
 
@@ -247,10 +294,7 @@ def recombinate_all(world, p: float, extra=None) -> bool:
     lay = _m().gp_layout(1, n, pcap, L, K_CAP, xr)
     nr = lay["nr"]
     _record(world, "rec", (p,), (seed, call), _view(blob, lay["cells"], nr, torch.int64), slot,
-            {"rows": _view(blob, lay["out_rows"], nr, torch.int64),
-             "out": _view(blob, lay["out"], nr * lay["out_w"], torch.uint8), "out_w": lay["out_w"],
-             "out_len": _view(blob, lay["out_len"], nr, torch.int32), "mark": mark, "gen": gen,
-             "direct": extra is not None})
+            _Replay(blob, lay, nr, "out_rows", mark=mark, gen=gen, direct=extra is not None))
     return True
 
 
@@ -273,7 +317,7 @@ def rebuild_rows(world, rows: torch.Tensor) -> bool:
     blob = _blob(world, "imm", _m().gp_blob_bytes(2, k, k, kd.P, 0, D_CAP, 0, 0), dev)
     slot = _m().gp_rebuild(_arena_desc(world, b), _gen_desc(world, dev), kd, _p(cells), _p(dcnt), k, D_CAP,
                            _p(blob), _stream())
-    _record(world, "imm", (), None, cells, slot, {})
+    _record(world, "imm", (), None, cells, slot, None)
     return True
 
 
@@ -284,16 +328,17 @@ def _recommit(world, pd: _Pending) -> torch.Tensor:
     if pd.kind == "mut":
         n_res = int(pd.host[0])
     else:  # recombination: 2 rows per pair, or the counted result rows (with strip-boundary results)
-        n_res = int(pd.host[3]) if r.get("direct") else 2 * int(pd.host[3])
+        n_res = int(pd.host[3]) if r.direct else 2 * int(pd.host[3])
     if n_res == 0:
         return torch.zeros(0, dtype=torch.long, device=arena.data.device)
-    out_len = r["out_len"][:n_res]
+    rows_all, out, out_w, out_len_all = r.views()
+    out_len = out_len_all[:n_res]
     need = int(out_len.max().item())
     if need > arena.width:
         arena.reserve(arena.n, need)
-    rows = r["rows"][:n_res]
-    _m().arena_scatter(n_res, 0, 1, _p(rows), _p(r["out"]), r["out_w"], _p(out_len), _p(arena.data),
-                       int(arena.width), _p(arena.lens), _p(r.get("mark")), int(r.get("gen", 0)), 0, 0, 0, _stream())
+    rows = rows_all[:n_res]
+    _m().arena_scatter(n_res, 0, 1, _p(rows), _p(out), out_w, _p(out_len), _p(arena.data), int(arena.width),
+                       _p(arena.lens), _p(r.mark), int(r.gen), 0, 0, 0, _stream())
     arena.version += 1
     return torch.unique(rows)
 
@@ -301,12 +346,25 @@ def _recommit(world, pd: _Pending) -> torch.Tensor:
 def reconcile(world) -> None:
     """Resolve pending device-pipeline calls, in issue order: adopt the device row counter,
     commit results that did not fit the arena (then replay the calls that were skipped because of
-    it), and rebuild flagged cells on the synchronous path."""
+    it), and rebuild flagged cells on the synchronous path. An enzymatic_activity that was issued
+    on top of the pending calls (World: speculative activity) is undone and run again if any of
+    this changed parameters."""
     st = world.__dict__.get("_gp_state")
+    spec = world.__dict__.pop("_spec", None)
     if not st or not st["pending"]:
         return
     pend = st["pending"]
     st["pending"] = []
+    if _resolve(world, pend) and spec is not None:
+        from magicsoup_amd.ops import world_ops
+
+        hip_ops.restore_cell_state(world, spec)
+        world_ops.enzymatic_activity(world)
+
+
+def _resolve(world, pend: list) -> bool:
+    """True if any genome or parameter was changed on the host."""
+    rebuilt = False
     kin = world.kinetics
     pend[-1].event.synchronize()
     kin.__dict__["_nrows"] = max(int(kin.__dict__["_nrows"]), int(pend[-1].host[2]))
@@ -316,6 +374,7 @@ def reconcile(world) -> None:
             raise RuntimeError("genome pipeline capacity exceeded (rates far above the pipeline's usage rule)")
         if flags & _F_SKIPPED:
             # a predecessor's result did not fit the arena: run this call now, same RNG stream
+            rebuilt = True
             if pd.kind == "mut":
                 changed = hip_ops.point_mutations(world, None, *pd.args, rng=pd.rng)
             else:
@@ -324,12 +383,15 @@ def reconcile(world) -> None:
                 world._update_params_rows(changed)
             continue
         if flags & _F_WIDTH:
+            rebuilt = True
             cells = _recommit(world, pd)
             if cells.numel():
                 world._update_params_rows(cells)
             continue
         if flags & (_F_TRANSLATE | _F_ROWS):
             # parameters are a pure function of the current genome: rebuild on the synchronous path
+            rebuilt = True
             cells = pd.cells[: int(pd.host[0])]
             if cells.numel():
                 world._update_params_rows(torch.unique(cells))
+    return rebuilt

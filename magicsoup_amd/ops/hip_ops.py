@@ -220,6 +220,28 @@ def enzymatic_activity(world) -> None:
     _launch_integrate(kin, p, c, world=world, flags_hook=hook, slot=kin._slot_tensor())
 
 
+def save_cell_state(world) -> torch.Tensor:
+    """Snapshot of what enzymatic_activity changes (cell molecules, raw pixel values under the
+    cells) into a scratch buffer, for :func:`restore_cell_state`."""
+    d = world.__dict__
+    n, m = d["n_cells"], world.n_molecules
+    mm = d["_molmap"]
+    R, C = geom(world)[:2]
+    buf = _scratch(world).get("spec_state", 2 * n * m, torch.float32, mm.device)
+    _m().cell_state_io(n, m, _p(d["_cols"]["cell_positions"].view(n)), R, C, _p(mm), _mdt(mm),
+                       _p(d["_cols"]["cell_molecules"].view(n)), _p(buf), False, _stream())
+    return buf
+
+
+def restore_cell_state(world, buf: torch.Tensor) -> None:
+    d = world.__dict__
+    n, m = d["n_cells"], world.n_molecules
+    mm = d["_molmap"]
+    R, C = geom(world)[:2]
+    _m().cell_state_io(n, m, _p(d["_cols"]["cell_positions"].view(n)), R, C, _p(mm), _mdt(mm),
+                       _p(d["_cols"]["cell_molecules"].view(n)), _p(buf), True, _stream())
+
+
 def build_params(kin, tokens, rows, luts, p, abs_temp: float, gas: float, nprot=None, dn=None) -> None:
     """Fused parameter build; also writes the integrator layout when it is current."""
     packed = kin._pack_ok()
