@@ -323,7 +323,6 @@ static void launch(int mode, int n, uintptr_t rows, uintptr_t arena, int width, 
   a.long_list = P_<int32_t>(long_list);
   a.long_count = P_<int32_t>(long_count);
   a.dn = dn ? P_<int>(dn) : nullptr;
-  if (a.dn && a.gslot) throw std::invalid_argument("translate: the long-genome pass needs a host count");
   // LDS pass: slots for genomes up to kLdsMaxLen (longer ones are queued); global pass: whole width
   a.lmax = a.gslot ? width : (width < kLdsMaxLen ? width : kLdsMaxLen);
   a.cap = a.lmax;  // a strand has at most one CDS per codon position
@@ -372,6 +371,16 @@ void translate_fused(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_
                      uintptr_t long_count, uintptr_t dn, uintptr_t stream) {
   launch(2, n, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot, ndom,
          P, D, tokens, 0, 0, long_list, long_count, dn, stream);
+}
+
+// Long-genome pass of the fused translation with a device count: the items long_list[0..*dn)
+// (at most lcap) take global-memory slots (lcap * translate_slot_bytes(width) bytes at gslot).
+void translate_fused_long(int lcap, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+                          uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
+                          uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t long_list,
+                          uintptr_t gslot, uintptr_t dn, uintptr_t stream) {
+  launch(2, lcap, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot, ndom,
+         P, D, tokens, long_list, gslot, 0, 0, dn, stream);
 }
 
 }  // namespace msd

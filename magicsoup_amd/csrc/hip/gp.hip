@@ -25,6 +25,11 @@ void translate_fused(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                      uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t long_list,
                      uintptr_t long_count, uintptr_t dn, uintptr_t stream);
+void translate_fused_long(int lcap, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+                          uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
+                          uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t long_list,
+                          uintptr_t gslot, uintptr_t dn, uintptr_t stream);
+size_t translate_slot_bytes(int width);
 void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_t rows, uintptr_t vmax_w, int nw,
                   uintptr_t km_w, int nk, uintptr_t signs, int nsg, uintptr_t hills, int nh, uintptr_t RM,
                   uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
@@ -63,7 +68,7 @@ __global__ void __launch_bounds__(256) gp_zero_kernel(int cap, const int* dn, lo
 // flags, row counter, count} into its pinned slot. Fresh row j is base + j (dense storage tail) or
 // free[base + j] (recycled rows of removed cells, Kinetics._recycle_rows); row_cap bounds the counter.
 constexpr int kFlagTranslateBit = 1, kFlagRowsBit = 4;  // select.hip DevFlag
-__global__ void __launch_bounds__(1024) gp_check_assign_kernel(int cap, const int* dn, const int32_t* counts,
+__global__ void __launch_bounds__(1024) gp_check_assign_kernel(int cap, int lcap, const int* dn, const int32_t* counts,
                                                                const int32_t* ndom, const int32_t* long_count,
                                                                int32_t* per, int Pcap, int Dcap, const int64_t* cells,
                                                                int64_t* slot, long long* d_rows, long long row_cap,
@@ -74,7 +79,7 @@ __global__ void __launch_bounds__(1024) gp_check_assign_kernel(int cap, const in
   const long long base = *d_rows;
   if (threadIdx.x == 0) {
     if (*dn > cap) atomicOr(opflags, 2);  // kFlagCapacity
-    if (*long_count > 0) atomicOr(opflags, kFlagTranslateBit);
+    if (*long_count > lcap) atomicOr(opflags, kFlagTranslateBit);  // more long genomes than global slots
   }
   for (int j = threadIdx.x; j < n; j += blockDim.x) {
     const int p = counts[2 * j] + counts[2 * j + 1];
@@ -137,9 +142,13 @@ struct Carve {
   }
 };
 
-// translation + fresh rows + parameter build for cells[:*dcnt] (genome_pipeline._rebuild)
-size_t rebuild_bytes(int cap, int P, int dcap) {
+// genomes longer than the LDS translation slots handled per call (global-memory slots)
+int long_cap(int cap) { return std::min(cap, 1024); }
+
+// translation + fresh rows + parameter build for cells[:*dcnt]
+size_t rebuild_bytes(int cap, int P, int dcap, int width) {
   Carve c(0);
+  c.take((size_t)long_cap(cap) * translate_slot_bytes(width));  // long-genome slots
   c.take(8 * (size_t)cap);                        // counts (2 per cell)
   c.take(8 * (size_t)cap);                        // ndom
   c.take(4 * (size_t)cap);                        // long list
@@ -154,6 +163,8 @@ size_t rebuild_bytes(int cap, int P, int dcap) {
 int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const GpGen& g, const GpKin& k, int dcap,
             Carve& c, uintptr_t stat_cnt, hipStream_t s) {
   const uintptr_t st = reinterpret_cast<uintptr_t>(s);
+  const int lcap = long_cap(cap);
+  const uintptr_t gslot = c.take((size_t)lcap * translate_slot_bytes(a.width));
   const uintptr_t counts = c.take(8 * (size_t)cap), ndom = c.take(8 * (size_t)cap);
   const uintptr_t long_list = c.take(4 * (size_t)cap), long_count = c.take(16);
   const uintptr_t per = c.take(4 * (size_t)cap), rows_out = c.take(4 * (size_t)cap);
@@ -164,8 +175,12 @@ int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const Gp
   MS_LAUNCH_CHECK();
   translate_fused(cap, cells, a.data, a.width, a.lens, g.small, g.dom_type, g.dt_entries, g.two_codon, g.dom_size,
                   g.dom_type_size, counts, ndom, k.P, dcap, tokens, long_list, long_count, dcnt, st);
+  if (a.width > 1024)  // genomes longer than the LDS slots: second pass over the queued ones
+    translate_fused_long(lcap, cells, a.data, a.width, a.lens, g.small, g.dom_type, g.dt_entries, g.two_codon,
+                         g.dom_size, g.dom_type_size, counts, ndom, k.P, dcap, tokens, long_list, gslot, long_count,
+                         st);
   auto sl = status_slot();
-  gp_check_assign_kernel<<<1, 1024, 0, s>>>(cap, P_<int>(dcnt), P_<int32_t>(counts), P_<int32_t>(ndom),
+  gp_check_assign_kernel<<<1, 1024, 0, s>>>(cap, lcap, P_<int>(dcnt), P_<int32_t>(counts), P_<int32_t>(ndom),
                                             P_<int32_t>(long_count), P_<int32_t>(per), k.P, dcap, P_<int64_t>(cells),
                                             P_<int64_t>(k.slot), P_<long long>(a.d_rows), k.row_cap,
                                             k.free ? P_<int64_t>(k.free) : nullptr, P_<int32_t>(rows_out),
@@ -182,14 +197,14 @@ int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const Gp
 // untouched until the call was reconciled: it holds the results a replay may re-commit).
 size_t gp_blob_bytes(int kind, int n, int cap, int P, int L, int dcap, int kcap, int extra_rows) {
   Carve c(0);
-  if (kind == 2) return rebuild_bytes(cap, P, dcap) + 512;  // rebuild of listed cells
+  if (kind == 2) return rebuild_bytes(cap, P, dcap, L) + 512;  // rebuild of listed cells (L: arena width)
   if (kind == 0) {  // mutations
     const int out_w = (L + kcap + 15) / 16 * 16;
     c.take(4 * (size_t)n);                 // k
     c.take(8 * (size_t)n);                 // sel
     c.take((size_t)cap * out_w);           // out
     c.take(4 * (size_t)cap);               // out_len
-    return c.off + rebuild_bytes(cap, P, dcap) + 512;
+    return c.off + rebuild_bytes(cap, P, dcap, L) + 512;
   }
   // recombinations: cap = pairs capacity
   const int nr = 2 * cap + extra_rows, out_w = 2 * L;
@@ -202,7 +217,7 @@ size_t gp_blob_bytes(int kind, int n, int cap, int P, int L, int dcap, int kcap,
   c.take((size_t)nr);                      // won
   c.take(8 * (size_t)nr);                  // q
   c.take(8 * (size_t)nr);                  // cells
-  return c.off + rebuild_bytes(nr, P, dcap) + 512;
+  return c.off + rebuild_bytes(nr, P, dcap, L) + 512;
 }
 
 // Offsets of the pieces a reconcile may need: mutations {sel, out, out_len}; recombinations

@@ -479,6 +479,100 @@ void spill_free_mask(int n, int m, uintptr_t dead, uintptr_t pos, int R, int C, 
   MS_LAUNCH_CHECK();
 }
 
+// spawn_cells without a host round trip. One thread per new cell j (row n0 + j): claim a free pixel
+// of the owned rows -- random probes (as claim_free), then a linear scan from a random start, which
+// always succeeds when the caller spawns at most as many cells as there are free owned pixels (the
+// host knows that count: one cell per pixel) -- then position, lifetime 0, divisions 0, half of the
+// pixel's molecules (the pixel keeps the other half, as pickup) and a random 12-character label.
+constexpr int kLabelLen = 12;
+__global__ void __launch_bounds__(256) spawn_place_kernel(int k, int R, int C, int r_lo, int r_hi, uint8_t* cell_map,
+                                                          uint64_t seed, uint64_t call, int attempts, long long n0,
+                                                          int m, int32_t* pos, int32_t* lifetimes, int32_t* divisions,
+                                                          float* cell_mols, void* map, int dtype, const float* corr,
+                                                          uint8_t* labels, int label_w, int32_t* label_lens,
+                                                          int* failed) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= k) return;
+  Philox rng(seed, call, (uint32_t)j);
+  const long long base = (long long)r_lo * C, n_pix = (long long)(r_hi - r_lo) * C;
+  auto claim = [&](long long pix) -> bool {
+    if (cell_map[pix]) return false;
+    unsigned* word = reinterpret_cast<unsigned*>(cell_map + (pix & ~3ll));
+    const unsigned bit = 1u << (8 * (pix & 3));
+    const unsigned old = atomicOr(word, bit);
+    return !(old & (0xFFu << (8 * (pix & 3))));
+  };
+  long long got = -1;
+  for (int t = 0; t < attempts && got < 0; ++t) {
+    const long long pix = base + (long long)rng.below64((uint64_t)n_pix);
+    if (claim(pix)) got = pix;
+  }
+  if (got < 0) {
+    const long long start = (long long)rng.below64((uint64_t)n_pix);
+    for (long long s = 0; s < n_pix && got < 0; ++s) {
+      const long long pix = base + (start + s) % n_pix;
+      if (claim(pix)) got = pix;
+    }
+  }
+  const long long c = n0 + j;
+  if (got < 0) {  // more new cells than free pixels: the caller's count was wrong
+    atomicOr(failed, 1);
+    return;
+  }
+  const int x = (int)(got / C), y = (int)(got - (long long)(got / C) * C);
+  pos[2 * c] = x;
+  pos[2 * c + 1] = y;
+  lifetimes[c] = 0;
+  divisions[c] = 0;
+  const long long plane = (long long)R * C;
+  for (int q = 0; q < m; ++q) {
+    const size_t px = (size_t)q * plane + got;
+    const float v = corr_in(ld_map(map, px, dtype), corr, q);
+    const float half = v * 0.5f;
+    cell_mols[c * m + q] = half;
+    st_map(map, px, corr_out(v - half, corr, q), dtype);
+  }
+  const char* abc = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789";
+  uint8_t* lab = labels + (size_t)c * label_w;
+  for (int i = 0; i < label_w; ++i) lab[i] = i < kLabelLen ? (uint8_t)abc[rng.below(62)] : 0;
+  label_lens[c] = kLabelLen;
+}
+
+// genome rows (k, L_in) with lengths -> arena rows n0.. (width >= L_in), zero padding
+__global__ void __launch_bounds__(256) spawn_genomes_kernel(int k, int L_in, const uint8_t* rows, const int32_t* lens,
+                                                            long long n0, uint8_t* arena, int width,
+                                                            int32_t* arena_lens) {
+  const long long total = (long long)k * width;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const long long j = t / width;
+    const int b = (int)(t - j * width);
+    arena[(n0 + j) * width + b] = b < L_in ? rows[j * L_in + b] : 0;
+    if (b == 0) arena_lens[n0 + j] = lens[j];
+  }
+}
+
+void spawn_dev(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uint64_t seed, uint64_t call,
+               long long n0, int m, uintptr_t pos, uintptr_t lifetimes, uintptr_t divisions, uintptr_t cell_mols,
+               uintptr_t map, int dtype, uintptr_t corr, uintptr_t labels, int label_w, uintptr_t label_lens,
+               int L_in, uintptr_t rows, uintptr_t lens, uintptr_t arena, int width, uintptr_t arena_lens,
+               uintptr_t failed, uintptr_t stream) {
+  if (k <= 0) return;
+  if (R <= 0 || C <= 0 || r_lo < 0 || r_hi > R || r_lo >= r_hi) throw std::invalid_argument("spawn_dev: bad geometry");
+  if (label_w < kLabelLen || width < L_in) throw std::invalid_argument("spawn_dev: arena rows too narrow");
+  hipStream_t s = S_(stream);
+  spawn_place_kernel<<<cdiv(k, 256), 256, 0, s>>>(k, R, C, r_lo, r_hi, P_<uint8_t>(cell_map), seed, call, 64, n0, m,
+                                                  P_<int32_t>(pos), P_<int32_t>(lifetimes), P_<int32_t>(divisions),
+                                                  P_<float>(cell_mols), P_<void>(map), dtype,
+                                                  corr ? P_<float>(corr) : nullptr, P_<uint8_t>(labels), label_w,
+                                                  P_<int32_t>(label_lens), P_<int>(failed));
+  MS_LAUNCH_CHECK();
+  const unsigned g = (unsigned)std::min<long long>(cdiv((long long)k * width, 256), 4096);
+  spawn_genomes_kernel<<<g, 256, 0, s>>>(k, L_in, P_<uint8_t>(rows), P_<int32_t>(lens), n0, P_<uint8_t>(arena), width,
+                                         P_<int32_t>(arena_lens));
+  MS_LAUNCH_CHECK();
+}
+
 // Save / restore the state an enzymatic_activity changes: cell molecules and the raw map values
 // (no pending correction applied) of the cells' pixels, as (n, 2m) floats (bf16 / fp16 storage
 // round-trips exactly through float). Lets the World issue the activity before pending parameter

@@ -48,6 +48,11 @@ void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t
             uintptr_t corr, uintptr_t stream);
 void cell_state_io(int n, int m, uintptr_t pos, int R, int C, uintptr_t map, int dtype, uintptr_t cell_mols,
                    uintptr_t buf, bool restore, uintptr_t stream);
+void spawn_dev(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uint64_t seed, uint64_t call,
+               long long n0, int m, uintptr_t pos, uintptr_t lifetimes, uintptr_t divisions, uintptr_t cell_mols,
+               uintptr_t map, int dtype, uintptr_t corr, uintptr_t labels, int label_w, uintptr_t label_lens,
+               int L_in, uintptr_t rows, uintptr_t lens, uintptr_t arena, int width, uintptr_t arena_lens,
+               uintptr_t failed, uintptr_t stream);
 void permeate(int c, int m, int R, int C, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map, int dtype,
               uintptr_t corr, uintptr_t stream);
 void gather_rows(int n, uintptr_t dn, uintptr_t src_rows, uintptr_t dst_rows,
@@ -219,6 +224,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("arena_scatter", &msd::arena_scatter);
   m.def("place_collect", &msd::place_collect);
   m.def("cell_state_io", &msd::cell_state_io, "save / restore cell molecules + raw pixel values under the cells");
+  m.def("spawn_dev", &msd::spawn_dev, "spawn_cells without a sync: claim pixels, init rows, pick up molecules, labels, genomes");
   m.def("divide_mask_dev", &msd::divide_mask_dev,
         "divide_cells over a mask: placement, winner compaction and commit issued without a sync; returns the status slot");
   m.def("translate_stats", &msd::translate_stats,

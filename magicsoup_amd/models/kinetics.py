@@ -667,12 +667,15 @@ class Kinetics:
             return store
         from magicsoup_amd.ops import hip_ops
 
+        # pack the live rows only, in cell order (free storage rows may hold stale data)
+        self._materialize()
+        store = self._store
         self._drop_packed()
         N = store["N"]
         rows, P, s = int(N.size(0)), int(N.size(1)), int(N.size(2))
-        store["_W"] = torch.empty(rows, P, s, dtype=torch.int32, device=N.device)
-        store["_Q"] = torch.empty(rows, P, 4, dtype=torch.float32, device=N.device)
-        hip_ops.pack_params(self, store)
+        store["_W"] = torch.zeros(rows, P, s, dtype=torch.int32, device=N.device)
+        store["_Q"] = torch.zeros(rows, P, 4, dtype=torch.float32, device=N.device)
+        hip_ops.pack_params(self, store, self.__dict__["_ncells"])
         self._restamp(True)
         return store
 
@@ -781,21 +784,30 @@ class Kinetics:
         store = self._store
         dev = store["N"].device
         if dev.type == "cuda":
-            # widen in place of the row storage: every storage row (cell rows, free rows) keeps its
-            # index, so the cell -> row map stays valid and nothing is gathered back to cell order
+            # widen into new storage of the same row capacity, moving only the live cells' rows
+            # (gathered to cell order, one launch) -- not every storage row -- and zeroing only
+            # their new protein slots; the storage is dense (cell i -> row i) afterwards
             from magicsoup_amd.ops import hip_ops
 
             d = self.__dict__
-            nrows = d["_nrows"] if d["_slot"] is not None else d["_ncells"]
-            if d["_slot"] is not None and d.get("_free") is not None:
-                nrows = min(int(t.size(0)) for t in store.values())  # live rows anywhere below capacity
+            n = d["_ncells"]
+            slot = d["_slot"]
+            p_old = self._P()
             ok = self._pack_ok()
             moves = []
             for name, t in list(store.items()):
-                nb = torch.zeros(t.size(0), max_n, *t.shape[2:], dtype=t.dtype, device=dev)
+                # dense rows for all n cells (in row-storage mode cells share rows, so n may exceed
+                # the storage's row count)
+                nb = torch.empty(max(int(t.size(0)), n), max_n, *t.shape[2:], dtype=t.dtype, device=dev)
                 moves.append((t, nb))
                 store[name] = nb
-            hip_ops.copy_row_prefixes(moves, nrows)
+            hip_ops.copy_row_prefixes(moves, n, src_rows=slot)
+            for _, nb in moves:
+                nb[:n, p_old:].zero_()
+            d["_slot"] = None
+            d["_free"] = None
+            d["_nrows"] = n
+            d.pop("_zero_row_t", None)
             d.pop("_spare", None)
             self._restamp(ok)
             return

@@ -532,6 +532,8 @@ class World:
         k = int(rows.size(0))
         if k == 0:
             return []
+        if rows.is_cuda:
+            return self._spawn_gpu(rows, lens)
         pos = world_ops.free_positions(self, k)
         kp = int(pos.size(0))
         if kp == 0:
@@ -548,6 +550,35 @@ class World:
         self._place_new(n0, pos)
         world_ops.pickup_molecules(self, new, pos)
         self._build_params_async(new)
+        return list(range(n0, n0 + k))
+
+    def _spawn_gpu(self, rows: torch.Tensor, lens: torch.Tensor) -> list[int]:
+        """spawn_cells on the GPU without a host round trip: every cell occupies its own pixel, so
+        the free pixels of the owned rows are known on the host; the claim / init kernel always finds
+        one for each of at most that many cells, and the parameters are built by the device genome
+        pipeline."""
+        from magicsoup_amd.ops import hip_ops
+
+        R, C, r_lo, r_hi, _ = world_ops.geom(self)
+        n0 = self.n_cells
+        free = (r_hi - r_lo) * C - n0
+        k = int(rows.size(0))
+        if free <= 0:
+            return []
+        if k > free:
+            keep = torch.randperm(k, device=rows.device)[:free]
+            rows, lens = rows[keep], lens[keep]
+            k = free
+        self._reserve(n0 + k)
+        self._genomes.reserve(n0 + k, int(rows.size(1)))
+        self._labels.reserve(n0 + k, _LABEL_LEN)
+        hip_ops.spawn_issue(self, rows, lens, n0)
+        self.n_cells = n0 + k
+        for arena in (self._genomes, self._labels):
+            arena.n = n0 + k
+            arena.version += 1
+        self.kinetics.increase_max_cells(by_n=k, zero=True)
+        self._build_params_async(torch.arange(n0, n0 + k, device=self.device))
         return list(range(n0, n0 + k))
 
     @_op("add_cells")

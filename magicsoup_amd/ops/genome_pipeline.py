@@ -198,7 +198,14 @@ def _kin_desc(world, dev):
 
 
 def _blob(world, kind: str, nbytes: int, dev) -> torch.Tensor:
-    return _scratch(world).get(f"gp_blob_{kind}", nbytes, torch.uint8, dev)
+    """The call's scratch blob; grown with 25 % headroom so that a slowly growing population does
+    not re-allocate it every few steps."""
+    sc = _scratch(world)
+    name = f"gp_blob_{kind}"
+    t = sc.bufs.get(name)
+    if t is None or t.numel() < nbytes:
+        sc.bufs[name] = t = torch.empty(nbytes + nbytes // 4, dtype=torch.uint8, device=dev)
+    return t
 
 
 _ES = {torch.uint8: 1, torch.int32: 4, torch.int64: 8}
@@ -314,7 +321,7 @@ def rebuild_rows(world, rows: torch.Tensor) -> bool:
     cells = rows.to(torch.int64).contiguous()
     dev = cells.device
     kd = _kin_desc(world, dev)
-    blob = _blob(world, "imm", _m().gp_blob_bytes(2, k, k, kd.P, 0, D_CAP, 0, 0), dev)
+    blob = _blob(world, "imm", _m().gp_blob_bytes(2, k, k, kd.P, int(world._genomes.width), D_CAP, 0, 0), dev)
     slot = _m().gp_rebuild(_arena_desc(world, b), _gen_desc(world, dev), kd, _p(cells), _p(dcnt), k, D_CAP,
                            _p(blob), _stream())
     _record(world, "imm", (), None, cells, slot, None)

@@ -146,9 +146,13 @@ def _check_overflow(kin) -> None:
                             "integrator's packed parameter layout (|N|, |A| <= 127, Nf, Nb <= 255)")
 
 
-def pack_params(kin, store: dict) -> None:
+def pack_params(kin, store: dict, rows: int | None = None) -> None:
+    """Integrator layout of storage rows [0, rows) (all rows by default)."""
     N = store["N"]
-    rows, P, s = int(N.size(0)), int(N.size(1)), int(N.size(2))
+    P, s = int(N.size(1)), int(N.size(2))
+    rows = int(N.size(0)) if rows is None else int(rows)
+    if rows <= 0:
+        return
     _m().pack_params(rows * P, s, *(_p(store[k]) for k in ("N", "Nf", "Nb", "A", "Vmax", "Kmf", "Kmb", "Ke")),
                      _p(store["_W"]), _p(store["_Q"]), _p(_overflow_flag(kin)), _stream())
 
@@ -218,6 +222,27 @@ def enzymatic_activity(world) -> None:
     _ensure_world_layout(world)
     hook = getattr(world, "_allreduce_flags", None)
     _launch_integrate(kin, p, c, world=world, flags_hook=hook, slot=kin._slot_tensor())
+
+
+def spawn_issue(world, rows: torch.Tensor, lens: torch.Tensor, n0: int) -> None:
+    """Claim pixels for and initialise the new rows n0..n0+k (positions, lifetimes, divisions,
+    molecules picked up from the pixel, random labels, genomes) without a synchronisation; the
+    caller reserved the capacity and guarantees k <= free owned pixels."""
+    R, C, r_lo, r_hi, _ = geom(world)
+    d = world.__dict__
+    cols = d["_cols"]
+    k, L_in = int(rows.size(0)), int(rows.size(1))
+    rows = rows.contiguous()
+    lens = lens.to(torch.int32).contiguous()
+    mm, corr = map_for_pixels(world)
+    g, lab = world._genomes, world._labels
+    failed = _scratch(world).get("spawn_failed", 1, torch.int32, mm.device)
+    seed, call = _rng()
+    _m().spawn_dev(k, R, C, r_lo, r_hi, _p(_cell_map_bytes(world)), seed, call, int(n0), world.n_molecules,
+                   _p(cols["cell_positions"].buf), _p(cols["cell_lifetimes"].buf), _p(cols["cell_divisions"].buf),
+                   _p(cols["cell_molecules"].buf), _p(mm), _mdt(mm), _p(corr), _p(lab.data), int(lab.width),
+                   _p(lab.lens), L_in, _p(rows), _p(lens), _p(g.data), int(g.width), _p(g.lens), _p(failed),
+                   _stream())
 
 
 def save_cell_state(world) -> torch.Tensor:
@@ -598,10 +623,10 @@ def gather_rows(pairs, n: int, src_rows: torch.Tensor | None = None, dst_rows: t
     _m().gather_rows(int(n), _p(dn), _p(sr), _p(dr), descs, _stream())
 
 
-def copy_row_prefixes(moves, n: int) -> None:
-    """dst[i, :P_src] = src[i] for rows i < n of every (src (rows, P_src, ...), dst (rows, P_dst, ...))
-    pair with P_dst >= P_src (a wider protein dimension), in one launch: a source row is the
-    contiguous prefix of the destination row."""
+def copy_row_prefixes(moves, n: int, src_rows: torch.Tensor | None = None) -> None:
+    """dst[i, :P_src] = src[src_rows[i]] (src[i] without ``src_rows``) for rows i < n of every
+    (src (rows, P_src, ...), dst (rows, P_dst, ...)) pair with P_dst >= P_src (a wider protein
+    dimension), in one launch: a source row is the contiguous prefix of the destination row."""
     descs = []
     for src, dst in moves:
         es = src.element_size()
@@ -610,7 +635,8 @@ def copy_row_prefixes(moves, n: int) -> None:
         if rb:
             descs.append((src.data_ptr(), dst.data_ptr(), src.stride(0) * es, dst.stride(0) * es, rb, 0))
     if n > 0 and descs:
-        _m().gather_rows(int(n), 0, 0, 0, descs, _stream())
+        sr = None if src_rows is None else src_rows.to(torch.int64).contiguous()
+        _m().gather_rows(int(n), 0, _p(sr), 0, descs, _stream())
 
 
 def _index_map(world, npix: int, dev) -> torch.Tensor:

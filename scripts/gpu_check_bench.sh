@@ -1,6 +1,7 @@
 #!/bin/bash
 # Quick GPU check: selected GPU tests (pytest -k expression in $1, optional) and N flagship bench
-# runs (default 3) with per-step times; each step under its own time limit, stop at the first failure.
+# runs (default 3) as the driver runs them (no per-step synchronisation); each step under its own
+# time limit, stop at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export PYTHONPATH=$PWD
@@ -11,7 +12,7 @@ if [ -n "${1:-}" ]; then
   rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
 fi
 for i in $(seq 1 ${2:-3}); do
-  timeout -k 10 300 python bench.py --step-times ${BENCH_ARGS:-} > $O/b$i.log 2>&1 || exit 1
+  timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > $O/b$i.log 2>&1 || exit 1
   python - $O/b$i.log <<'PY'
 import json, statistics, sys
 for l in open(sys.argv[1]):

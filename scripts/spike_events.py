@@ -100,7 +100,10 @@ for _ in range(steps):
 torch.cuda.synchronize()
 times = [e0.elapsed_time(e1) for e0, e1, _ in recs]
 med = sorted(times)[len(times) // 2]
-print(f"{S}^2 / {N}: {steps} steps, median {med:.3f} ms, mean {sum(times) / len(times):.3f} ms")
+kin = w.kinetics
+print(f"{S}^2 / {N}: {steps} steps, median {med:.3f} ms, mean {sum(times) / len(times):.3f} ms; proteins P={kin._P()}, "
+      f"storage rows {min(int(t.size(0)) for t in kin._store.values())}, arena width {w._genomes.width}, "
+      f"max genome {int(w._genomes.lens[:w.n_cells].max())}")
 for (e0, e1, ev), t in zip(recs, times):
     if t > 1.25 * med or ev:
         print(f"  {t:7.3f} ms  {ev}")

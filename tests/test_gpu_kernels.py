@@ -617,6 +617,39 @@ def test_deferred_genome_ops_match_immediate_issue(monkeypatch):
     assert not w.__dict__["_deferred"] and len(genomes) == w.n_cells
 
 
+def test_widening_proteins_keeps_parameters_in_slot_mode():
+    """Growing the protein dimension while cells map to scattered (recycled) storage rows moves the
+    live rows only: every cell keeps its parameters, the new protein slots are zero."""
+    import bench
+
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    w = _world("cuda", map_size=96, n=1500, s=500)
+    for _ in range(4):
+        bench.step(w, 1500, 500, atp)
+        w.mutate_cells(p=1e-4)
+    w._reconcile()
+    kin = w.kinetics
+    kin.__dict__["_nrows"] = kin._row_limit()[0]  # force recycled rows for the next builds
+    bench.step(w, 1500, 500, atp)
+    w.mutate_cells(p=1e-4)
+    w._reconcile()
+    assert kin.__dict__["_slot"] is not None
+    names = ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke")
+    # dense copies through the public tensors (a clone of the world keeps the original's layout)
+    ref = copy.deepcopy(w)
+    before = {k: getattr(ref.kinetics, k).clone() for k in names}
+    P = kin._P()
+    kin.increase_max_proteins(P + 7)
+    assert kin._P() == P + 7
+    for k in names:
+        t = getattr(kin, k)
+        assert torch.equal(t[:, :P], before[k]), k
+        assert not t[:, P:].any(), k
+    w.enzymatic_activity()
+    ref.enzymatic_activity()
+    assert torch.equal(w.cell_molecules, ref.cell_molecules)
+
+
 def _integrate_modes(kin, X, modes=(0, 8)):
     from magicsoup_amd.ops import kinetics_ops
 
