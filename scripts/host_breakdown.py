@@ -1,7 +1,8 @@
 """Inclusive host time per call of selected internal functions inside pipelined bench steps (no
 synchronisation added): where the host spends a step.
 
-usage: python scripts/host_breakdown.py [map_size] [cells] [steps]"""
+usage: python scripts/host_breakdown.py [map_size] [cells] [steps]
+MS_VIRTUAL_STRIPS=1: a one-rank DistributedWorld running the strip protocol (RCCL to itself)."""
 import collections
 import importlib
 import os
@@ -39,6 +40,19 @@ TARGETS = [
     ("magicsoup_amd.ops.hip_ops", None, "diffuse"),
     ("magicsoup_amd.ops.hip_ops", None, "spill_and_free_mask"),
     ("magicsoup_amd.ops.hip_ops", None, "select_async"),
+    ("magicsoup_amd.parallel.dist_world", "DistributedWorld", "divide_cells_t"),
+    ("magicsoup_amd.parallel.dist_world", "DistributedWorld", "recombinate_cells"),
+    ("magicsoup_amd.parallel.dist_world", "DistributedWorld", "_exchange"),
+    ("magicsoup_amd.parallel.dist_world", "DistributedWorld", "_do_exchange_map_halo"),
+    ("magicsoup_amd.parallel.dist_world", "DistributedWorld", "_do_allreduce_flags"),
+    ("magicsoup_amd.parallel.dist_world", "DistributedWorld", "_do_allreduce_totals"),
+    ("magicsoup_amd.parallel.dist_world", "DistributedWorld", "_append_arrivals"),
+    ("magicsoup_amd.parallel.dist_world", "DistributedWorld", "_clone_rows"),
+    ("magicsoup_amd.parallel.strip", None, "marks"),
+    ("magicsoup_amd.parallel.strip", None, "reserve"),
+    ("magicsoup_amd.parallel.strip", None, "split_winners_gpu"),
+    ("magicsoup_amd.parallel.strip", None, "pack"),
+    ("magicsoup_amd.parallel.strip", None, "clear"),
 ]
 acc = collections.defaultdict(lambda: [0.0, 0])
 
@@ -55,7 +69,17 @@ def wrap(f, key):
     return w
 
 
-w = ms.World(chemistry=CHEMISTRY, map_size=S, device="cuda", seed=0)
+if os.environ.get("MS_VIRTUAL_STRIPS") == "1":
+    import torch.distributed as dist
+
+    from magicsoup_amd.parallel import DistributedWorld
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29543")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    w = DistributedWorld(chemistry=CHEMISTRY, map_size=S, device="cuda", seed=0, strips=True)
+else:
+    w = ms.World(chemistry=CHEMISTRY, map_size=S, device="cuda", seed=0)
 w.spawn_cells(bench.random_genomes(N, 500, "cuda"))
 atp = CHEMISTRY.molname_2_idx["ATP"]
 for _ in range(20):
