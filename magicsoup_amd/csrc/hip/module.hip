@@ -111,6 +111,8 @@ int divide_mask_dev(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo
                     uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result, int rounds, uint64_t seed,
                     uint64_t call, uintptr_t wins, uintptr_t dcount, long long n0, int m, uintptr_t par,
                     uintptr_t cell_mols, uintptr_t divisions, uintptr_t lifetimes, uintptr_t stream);
+void divide_commit_list(int k, uintptr_t par, uintptr_t npos, long long n0, int n_exp, uintptr_t exp, int m,
+                        uintptr_t pos, uintptr_t cell_mols, uintptr_t divisions, uintptr_t lifetimes, uintptr_t stream);
 void place_collect(int k, uintptr_t wins, uintptr_t cells, uintptr_t result, int C, uintptr_t par, uintptr_t npos,
                    uintptr_t stream);
 // select.hip
@@ -223,6 +225,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("rec_apply", &msd::rec_apply);
   m.def("arena_scatter", &msd::arena_scatter);
   m.def("place_collect", &msd::place_collect);
+  m.def("divide_commit_list", &msd::divide_commit_list, "division commit with a host count (+ exporting parents)");
   m.def("cell_state_io", &msd::cell_state_io, "save / restore cell molecules + raw pixel values under the cells");
   m.def("spawn_dev", &msd::spawn_dev, "spawn_cells without a sync: claim pixels, init rows, pick up molecules, labels, genomes");
   m.def("divide_mask_dev", &msd::divide_mask_dev,

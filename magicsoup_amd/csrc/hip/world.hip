@@ -72,6 +72,48 @@ __global__ void __launch_bounds__(256) divide_commit_kernel(const int* dn, const
   }
 }
 
+// Division commit with a host count (decomposed worlds, after their one synchronisation): child
+// n0 + j of parent par[j] takes pixel npos[j]; both halve the parent's molecules, divisions + 1,
+// lifetime 0. Exporting parents (children created on a neighbour rank) halve their molecules and
+// count the division too. Thread over (k + n_exp) x m.
+__global__ void __launch_bounds__(256) divide_commit_list_kernel(int k, const int64_t* par, const int32_t* npos,
+                                                                 long long n0, int n_exp, const int64_t* exp, int m,
+                                                                 int32_t* pos, float* cell_mols, int32_t* divisions,
+                                                                 int32_t* lifetimes) {
+  const long long total = (long long)(k + n_exp) * m;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const long long i = t / m;
+    const int j = (int)(t - i * m);
+    const bool local = i < k;
+    const long long p = local ? par[i] : exp[i - k];
+    const long long c = local ? n0 + i : p;
+    const float h = cell_mols[p * m + j] * 0.5f;
+    cell_mols[p * m + j] = h;
+    cell_mols[c * m + j] = h;
+    if (j == 0) {
+      if (local) {
+        pos[2 * c] = npos[2 * i];
+        pos[2 * c + 1] = npos[2 * i + 1];
+      }
+      const int32_t d = divisions[p] + 1;
+      divisions[p] = d;
+      divisions[c] = d;
+      lifetimes[p] = 0;
+      lifetimes[c] = 0;
+    }
+  }
+}
+
+void divide_commit_list(int k, uintptr_t par, uintptr_t npos, long long n0, int n_exp, uintptr_t exp, int m,
+                        uintptr_t pos, uintptr_t cell_mols, uintptr_t divisions, uintptr_t lifetimes, uintptr_t stream) {
+  if (k + n_exp <= 0 || m <= 0) return;
+  const unsigned grid = std::min<unsigned>(cdiv((long long)(k + n_exp) * m, 256), 512u);
+  divide_commit_list_kernel<<<grid, 256, 0, S_(stream)>>>(k, P_<int64_t>(par), P_<int32_t>(npos), n0, n_exp,
+                                                          P_<int64_t>(exp), m, P_<int32_t>(pos), P_<float>(cell_mols),
+                                                          P_<int32_t>(divisions), P_<int32_t>(lifetimes));
+  MS_LAUNCH_CHECK();
+}
+
 // ---------------------------------------------------------------- placement
 // Claim k uniformly random free pixels of the owned rows by rejection: atomically set the pixel's
 // byte in the (4-byte padded) bool occupancy map; out[i] = pixel or -1 after `attempts` misses.

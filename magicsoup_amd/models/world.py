@@ -308,11 +308,13 @@ class World:
         # the chains depend on the state as of the first queued call (recorded then), not on the
         # molecule-only work issued since (e.g. the diffusion stencil they run next to)
         side.wait_event(d.pop("_defer_event"))
+        d["_side_active"] = True  # (a decomposed world's exchanges use its side-stream communicator)
         try:
             with torch.cuda.stream(side):
                 for fn in q:
                     fn()
         finally:
+            d["_side_active"] = False
             main.wait_stream(side)
 
     def _reconcile(self) -> None:
@@ -644,6 +646,46 @@ class World:
             self._place(children, child_pos)
         world_ops.split_cells(self, parents, children)
         return parents, children
+
+    def _commit_divisions_gpu(self, par: torch.Tensor, npos: torch.Tensor, k: int,
+                              exporters: torch.Tensor | None = None) -> torch.Tensor:
+        """Children of ``par[:k]`` at pixels ``npos[:k]`` (int32 (k, 2), already claimed) as rows
+        n_cells..: one commit launch (positions, halved molecules, divisions, lifetimes; also the
+        ``exporters`` -- parents whose child lives on another rank) and one gather of the genome /
+        label / parameter-row entries. Returns the children's indices."""
+        from magicsoup_amd.ops import hip_ops
+        from magicsoup_amd.ops.hip_ops import _m, _p, _stream
+
+        n0 = self.n_cells
+        self._reserve(n0 + k)
+        kin = self.kinetics
+        kin._enter_slot_mode()
+        kin._slot_reserve(n0 + k)
+        g, lab = self._genomes, self._labels
+        g.reserve(n0 + k)
+        lab.reserve(n0 + k)
+        par = par[:k].to(torch.int64).contiguous()
+        npos = npos[:k].to(torch.int32).contiguous()
+        ne = 0 if exporters is None else int(exporters.numel())
+        exp = None if not ne else exporters.to(torch.int64).contiguous()
+        cols = self._cols
+        _m().divide_commit_list(k, _p(par), _p(npos), n0, ne, _p(exp), self.n_molecules,
+                                _p(cols["cell_positions"].buf), _p(cols["cell_molecules"].buf),
+                                _p(cols["cell_divisions"].buf), _p(cols["cell_lifetimes"].buf), _stream())
+        if k:
+            sb = kin.__dict__["_slot_buf"]
+            pairs = [(g.data[:n0], g.data[n0 : n0 + k], g.lens), (g.lens[:n0], g.lens[n0 : n0 + k]),
+                     (lab.data[:n0], lab.data[n0 : n0 + k], lab.lens), (lab.lens[:n0], lab.lens[n0 : n0 + k]),
+                     (sb[:n0], sb[n0 : n0 + k])]
+            hip_ops.gather_rows(pairs, k, src_rows=par)
+            self.n_cells = n0 + k
+            for arena in (g, lab):
+                arena.n = n0 + k
+                arena.version += 1
+            kd = kin.__dict__
+            kd["_slot"] = sb[: n0 + k]
+            kd["_ncells"] += k
+        return torch.arange(n0, n0 + k, device=self.device)
 
     def _divide_mask_gpu(self, mask: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
         """Division over a GPU mask with one synchronisation at the very end: placement, winner

@@ -53,7 +53,7 @@ import torch.distributed as dist
 from magicsoup_amd.models.world import World, _op
 from magicsoup_amd.ops import world_ops
 from magicsoup_amd.parallel import strip
-from magicsoup_amd.parallel.comm import make_comm
+from magicsoup_amd.parallel.comm import RcclComm, make_comm
 
 _U8 = torch.uint8
 
@@ -145,6 +145,12 @@ class DistributedWorld(World):
         g["_n_pix_global"] = map_size * map_size
         g["_stage"] = dist.get_backend(group) == "gloo" and torch.device(self.device).type == "cuda"
         g["_comm"] = make_comm(group, self.rank, n, self.device) if self._strips else None
+        # a second communicator for the exchanges of genome ops issued on the side stream (deferred
+        # recombination): RCCL operations of one communicator must not interleave across streams
+        side = None
+        if self._strips and isinstance(g["_comm"], RcclComm):
+            side = make_comm(group, self.rank, n, self.device)
+        g["_comm_side"] = side if side is not None else g["_comm"]
         g["migrated"] = {"divided_out": 0, "divided_in": 0, "moved_out": 0, "moved_in": 0, "rejected": 0}
         # strip-boundary recombination: a stream per boundary shared by its two ranks, genomes up to
         # `boundary_genome_cap` nt take part (longer ones recombine with cells of their own strip only)
@@ -199,11 +205,15 @@ class DistributedWorld(World):
         """One neighbour exchange: ``to_up`` arrives at the upper neighbour as its ``from_down``,
         ``to_down`` at the lower one as its ``from_up``. ``None`` skips an op (the peer must skip
         the matching one)."""
-        self._comm.exchange(to_up, to_down, from_down, from_up)
+        self._active_comm().exchange(to_up, to_down, from_down, from_up)
+
+    def _active_comm(self):
+        d = self.__dict__
+        return d["_comm_side"] if d.get("_side_active") else d["_comm"]
 
     def _all_reduce(self, t: torch.Tensor, op) -> None:
         name = {dist.ReduceOp.SUM: "sum", dist.ReduceOp.MAX: "max", dist.ReduceOp.MIN: "min"}[op]
-        self._comm.allreduce_(t, name)
+        self._active_comm().allreduce_(t, name)
 
     def _exchange_var(self, up: torch.Tensor | None, down: torch.Tensor | None, meta_up=(), meta_down=()):
         """Exchange variable-size uint8 record blocks (k, B) with both neighbours. ``meta_*`` are
@@ -446,17 +456,22 @@ class DistributedWorld(World):
         inb = sc.get("dv_in", max(1, b_up + b_dn), _U8, torch.device(dev))
         in_up, in_dn = inb[:b_up], inb[b_up : b_up + b_dn]
         self._exchange(out_up, out_dn, in_dn, in_up)
-        # 4. exporting parents keep half their molecules (every claim into a halo row is accepted)
-        if n_up + n_dn:
-            p_out = torch.cat([par_up, par_dn])
-            world_ops.split_cells(self, p_out, p_out)
+        # 4. exporting parents keep half their molecules (every claim into a halo row is accepted),
         # 5. local children (rows n0 ..), then the arrivals
         n0 = self.n_cells
-        children = torch.arange(n0, n0 + n_loc, device=dev)
-        if n_loc:
-            self._clone_rows(par_loc, children)
-            self.cell_positions[n0 : n0 + n_loc] = pos_loc.to(torch.int32)
-            world_ops.split_cells(self, par_loc, children)
+        if gpu:
+            # par holds the three winner classes at [0, kk), [kk, 2kk), [2kk, 3kk)
+            p_out = torch.cat([par_up, par_dn]) if n_up + n_dn else None
+            children = self._commit_divisions_gpu(par_loc, pos_loc, n_loc, exporters=p_out)
+        else:
+            if n_up + n_dn:
+                p_out = torch.cat([par_up, par_dn])
+                world_ops.split_cells(self, p_out, p_out)
+            children = torch.arange(n0, n0 + n_loc, device=dev)
+            if n_loc:
+                self._clone_rows(par_loc, children)
+                self.cell_positions[n0 : n0 + n_loc] = pos_loc.to(torch.int32)
+                world_ops.split_cells(self, par_loc, children)
         self._append_arrivals(hdr_up, in_up, hdr_dn, in_dn)
         # 6. halo rows empty, reservations released
         strip.clear(self)
@@ -564,11 +579,19 @@ class DistributedWorld(World):
         no synchronisation). ``cell_idxs``: ghost-row protocol with host round trips."""
         if not self._strips:
             return super().recombinate_cells(cell_idxs, p)
+        if cell_idxs is None and self._genomes.data.is_cuda and self._defer_genome_op():
+            # queued like World's: every rank flushes at the same op, in call order, and its
+            # exchanges then go through the side-stream communicator
+            self._defer(lambda: self._recombinate_strips_all(p))
+            return
         self._reconcile()
         if cell_idxs is not None:
             return self._recombinate_subset(cell_idxs, p)
+        self._recombinate_strips_all(p)
+
+    def _recombinate_strips_all(self, p: float) -> None:
         self.__dict__["_xcall"] += 1
-        if self.cell_molecules.is_cuda:
+        if self._genomes.data.is_cuda:
             self._recombinate_gpu(p)
         else:
             self._recombinate_cpu(p)
@@ -869,7 +892,11 @@ class DistributedWorld(World):
 
     def close(self) -> None:
         """Release the communicator (collective). The world cannot exchange afterwards."""
-        c = self.__dict__.get("_comm")
+        d = self.__dict__
+        side = d.get("_comm_side")
+        if side is not None and side is not d.get("_comm"):
+            side.close()
+        c = d.get("_comm")
         if c is not None:
             c.close()
 
