@@ -74,11 +74,10 @@ def random_genomes(k: int, size: int, device) -> tuple[torch.Tensor, torch.Tenso
 _CHEMOSTAT = {"divided": 0, "starved": 0}  # previous step's divisions / starvation deaths (dilution estimates)
 
 
-def _dilution_sample(n: int, k: int, device) -> torch.Tensor:
-    """k distinct uniform indices < n (a device permutation: one launch, no host work)."""
-    if str(device) == "cpu":
-        return torch.randperm(n)[:k]
-    return torch.randperm(n, device=device)[:k]
+def _dilution_mask(n: int, k: int, device) -> torch.Tensor:
+    """Each of n cells drawn with probability k / n (about k cells: the chemostat needs the rate, not
+    an exact count; one fused draw on the device, no host work)."""
+    return torch.rand(n, device=device) < (k / n)
 
 
 def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=None):
@@ -100,7 +99,7 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
         n0 = world.n_cells
         keep = n_target + n_target // 100 - _CHEMOSTAT["divided"] + _CHEMOSTAT["starved"]
         excess = min(n0 - keep, n0)
-        dilute = _dilution_sample(n0, excess, world.cell_molecules.device) if excess > 0 else None
+        dilute = _dilution_mask(n0, excess, world.cell_molecules.device) if excess > 0 else None
     with ph("activity"):
         world.enzymatic_activity()
     with ph("kill"):
@@ -112,7 +111,7 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
         # previous step's divisions and starvation deaths are the estimates). The margin keeps the
         # next step's top-up (a spawn) rare; activity always runs on >= n_target cells.
         if dilute is not None:
-            kill.index_fill_(0, dilute, True)
+            kill |= dilute
             note("diluted", excess)
         world.kill_cells(kill)
         _CHEMOSTAT["starved"] = max(0, n0 - world.n_cells - max(excess, 0))

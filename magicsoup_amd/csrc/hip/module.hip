@@ -125,6 +125,7 @@ int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, ui
 void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
 int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t cnt, uintptr_t stream);
 std::tuple<long long, long long, long long, long long> status_read(int slot);
+std::tuple<long long, long long, long long, long long> stream_sync_read(int slot, uintptr_t stream);
 std::tuple<int, int, int> translate_stats(int n, uintptr_t counts, uintptr_t ndom, uintptr_t long_count, uintptr_t per,
                                           uintptr_t stream);
 std::pair<long long, int> select_indices(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel,
@@ -240,6 +241,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("count_to_host", &msd::count_to_host, "device {count, max} -> pinned ring slot (returns the slot)");
   m.def("status_write", &msd::status_write, "pipeline status -> pinned ring slot (returns the slot)");
   m.def("status_read", &msd::status_read);
+  m.def("stream_sync_read", &msd::stream_sync_read, "synchronise a stream, then read a pinned status slot");
   m.def("rccl_load", &msd::rccl_load, "resolve RCCL from a loaded librccl.so path; returns its version");
   m.def("rccl_unique_id", [](){ return py::bytes(msd::rccl_unique_id()); });
   m.def("rccl_init", [](py::bytes uid, int nranks, int rank) { return msd::rccl_init(std::string(uid), nranks, rank); });

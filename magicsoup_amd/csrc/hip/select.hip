@@ -306,6 +306,12 @@ std::tuple<long long, long long, long long, long long> status_read(int slot) {
   return {v[0], v[1], v[2], v[3]};
 }
 
+// One stream synchronisation, then the slot (what wait_count needs, without a Python stream object).
+std::tuple<long long, long long, long long, long long> stream_sync_read(int slot, uintptr_t stream) {
+  MS_HIP_CHECK(hipStreamSynchronize(S_(stream)));
+  return status_read(slot);
+}
+
 // select_indices_dev whose last tile also writes {count, max} into a fresh pinned status slot
 // (returned): the host launches the work that depends on the count with `out_dev` as device count
 // and reads the slot after one stream synchronisation (no separate copy launch).

@@ -304,7 +304,7 @@ class World:
             # high priority: the short chain kernels are dispatched ahead of the stencil's waiting
             # workgroups (the next op's reconcile waits for the chains)
             side = d["_side_stream"] = torch.cuda.Stream(device=self._genomes.data.device, priority=-1)
-        main = torch.cuda.current_stream()
+        main = torch.cuda.current_stream(side.device)
         # the chains depend on the state as of the first queued call (recorded then), not on the
         # molecule-only work issued since (e.g. the diffusion stencil they run next to)
         side.wait_event(d.pop("_defer_event"))

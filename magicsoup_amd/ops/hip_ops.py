@@ -14,8 +14,16 @@ from magicsoup_amd.ops.world_ops import geom
 _SNAP = 5  # candidate states per cell per integration part (kinetics.py:819 has 4 increments)
 
 
+_MOD = None
+
+
 def _m():
-    return native.hip()
+    """The loaded ``_hip`` module (resolved once; native.hip() raises if it cannot be loaded)."""
+    global _MOD
+    m = _MOD
+    if m is None:
+        m = _MOD = native.hip()
+    return m
 
 
 _raw_stream = torch._C._cuda_getCurrentRawStream
@@ -116,8 +124,7 @@ def select_async(src: torch.Tensor, kind: str, rest: bool = False):
 
 def wait_count(slot: int) -> int:
     """Synchronise the current stream and read a :func:`select_async` count."""
-    torch.cuda.current_stream().synchronize()
-    return int(_m().status_read(slot)[0])
+    return int(_m().stream_sync_read(slot, _stream())[0])
 
 
 # ---------------------------------------------------------------------------- geometry
