@@ -5,7 +5,7 @@ BASELINE.json config: Wood-Ljungdahl chemistry, 4096x4096 map, random-normal mol
 random genomes, population topped up to >= 50,000 cells every step. One step:
 
     top up to N cells -> enzymatic_activity -> kill (ATP < 1, plus random cells so that the
-    divisions that follow restore ~1.01 N: chemostat dilution) -> replicate (ATP > 5: ATP -= 4, divide)
+    divisions that follow restore ~1.02 N: chemostat dilution) -> replicate (ATP > 5: ATP -= 4, divide)
     -> recombinate_cells -> mutate_cells -> degrade -> diffuse -> increment lifetimes
 
 Single GPU: one ``World`` on ``cuda:0``. N GPUs (``torchrun --nproc-per-node N``): one world,
@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -71,7 +72,7 @@ def random_genomes(k: int, size: int, device) -> tuple[torch.Tensor, torch.Tenso
     return rows, torch.full((k,), size, dtype=torch.int32, device=device)
 
 
-_CHEMOSTAT = {"divided": 0, "starved": 0}  # previous step's divisions / starvation deaths (dilution estimates)
+_CHEMOSTAT = {"divided": 0, "starved": 0, "steps": 0}  # running means of divisions / starvation deaths
 
 
 def _dilution_mask(n: int, k: int, device) -> torch.Tensor:
@@ -97,7 +98,12 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
             note("spawned", n_target - n)
         # chemostat dilution (see kill below): the random cells depend only on the population size
         n0 = world.n_cells
-        keep = n_target + n_target // 100 - _CHEMOSTAT["divided"] + _CHEMOSTAT["starved"]
+        # margin: 2 % plus three standard deviations of the step's random division / dilution counts;
+        # the estimates are running means (spawned cells divide more in their first step, and a
+        # last-step estimate makes the population oscillate around the target)
+        d_est, s_est = _CHEMOSTAT["divided"], _CHEMOSTAT["starved"]
+        margin = n_target // 50 + 3 * int(math.sqrt(d_est + 1))
+        keep = n_target + margin - d_est + s_est
         excess = min(n0 - keep, n0)
         dilute = _dilution_mask(n0, excess, world.cell_molecules.device) if excess > 0 else None
     with ph("activity"):
@@ -107,21 +113,24 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
         # chemostat dilution keeps the population at the configured size (the reference loop only
         # tops up; on a 4096^2 map the population would otherwise grow ~6x within 25 steps): random
         # cells are removed together with the starving ones, in the same kill_cells call, so that
-        # after the divisions that follow the population is back at n_target plus a 1 % margin (the
+        # after the divisions that follow the population is back at n_target plus a small margin (the
         # previous step's divisions and starvation deaths are the estimates). The margin keeps the
         # next step's top-up (a spawn) rare; activity always runs on >= n_target cells.
         if dilute is not None:
             kill |= dilute
             note("diluted", excess)
         world.kill_cells(kill)
-        _CHEMOSTAT["starved"] = max(0, n0 - world.n_cells - max(excess, 0))
+        starved = max(0, n0 - world.n_cells - max(excess, 0))
+        _CHEMOSTAT["starved"] = (_CHEMOSTAT["starved"] + starved) // 2 if _CHEMOSTAT["steps"] else starved
         note("killed", n0 - world.n_cells)
     with ph("replicate"):
         repl = world.cell_molecules[:, atp] > 5.0
         world.cell_molecules[:, atp] -= 4.0 * repl
         parents, _ = world.divide_cells_t(repl)
-        _CHEMOSTAT["divided"] = int(parents.numel())
-        note("divided", _CHEMOSTAT["divided"])
+        d = int(parents.numel())
+        _CHEMOSTAT["divided"] = (_CHEMOSTAT["divided"] + d) // 2 if _CHEMOSTAT["steps"] else d
+        _CHEMOSTAT["steps"] += 1
+        note("divided", d)
     with ph("recombinate"):
         world.recombinate_cells()
     with ph("mutate"):

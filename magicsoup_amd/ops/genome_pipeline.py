@@ -313,8 +313,12 @@ def rebuild_rows(world, rows: torch.Tensor) -> bool:
     k = int(rows.numel())
     if k == 0:
         return True
-    if not enabled(world) or k > N_CAP or world.kinetics._P() == 0:
+    if not enabled(world) or k > 8 * N_CAP or world.kinetics._P() == 0:
         return False  # (no protein slots yet: the synchronous path sizes the storage)
+    if k > N_CAP:
+        # a large batch (e.g. a big top-up): start from a fresh chain with room for all its rows
+        reconcile(world)
+        world.kinetics._reserve_rows(k + 2 * N_CAP)
     b = _begin(world, "imm")
     dcnt = b["cnt"]
     dcnt[:1].fill_(k)

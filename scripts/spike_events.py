@@ -2,7 +2,7 @@
 run) together with the rare internal events that happened in that step (storage growth, row
 recycling, parameter re-layouts, spawns, rollbacks, scratch allocations): what makes slow steps slow.
 
-usage: python scripts/spike_events.py [map_size] [cells] [steps]"""
+usage: python scripts/spike_events.py [map_size] [cells] [steps] [warmup]"""
 import collections
 import importlib
 import os
@@ -18,6 +18,7 @@ from magicsoup_amd.examples.wood_ljungdahl import CHEMISTRY  # noqa: E402
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 50000
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 80
+warm = int(sys.argv[4]) if len(sys.argv) > 4 else 20
 events = collections.Counter()
 TARGETS = [
     ("magicsoup_amd.models.kinetics", "Kinetics", "_recycle_rows"),
@@ -60,7 +61,7 @@ def wrap_growth(f, key, size_of):
 w = ms.World(chemistry=CHEMISTRY, map_size=S, device="cuda", seed=0)
 w.spawn_cells(bench.random_genomes(N, 500, "cuda"))
 atp = CHEMISTRY.molname_2_idx["ATP"]
-for _ in range(20):
+for _ in range(warm):
     bench.step(w, N, 500, atp)
 torch.cuda.synchronize()
 sizes = {
@@ -89,6 +90,20 @@ def get(self, name, numel, dtype, device, zero=False):
 
 
 hip_ops.Scratch.get = get
+import gc  # noqa: E402
+import time  # noqa: E402
+
+_gc_t = {}
+
+
+def _gc_cb(phase, info):
+    if phase == "start":
+        _gc_t["t"] = time.perf_counter()
+    else:
+        events[f"gc{info['generation']}_us"] += int((time.perf_counter() - _gc_t.get("t", time.perf_counter())) * 1e6)
+
+
+gc.callbacks.append(_gc_cb)
 recs = []
 for _ in range(steps):
     events.clear()
@@ -104,6 +119,6 @@ kin = w.kinetics
 print(f"{S}^2 / {N}: {steps} steps, median {med:.3f} ms, mean {sum(times) / len(times):.3f} ms; proteins P={kin._P()}, "
       f"storage rows {min(int(t.size(0)) for t in kin._store.values())}, arena width {w._genomes.width}, "
       f"max genome {int(w._genomes.lens[:w.n_cells].max())}")
-for (e0, e1, ev), t in zip(recs, times):
-    if t > 1.25 * med or ev:
-        print(f"  {t:7.3f} ms  {ev}")
+for i, ((e0, e1, ev), t) in enumerate(zip(recs, times)):
+    if t > 1.25 * med or ev or warm == 0:
+        print(f"  step {i:3d} {t:7.3f} ms  {ev}")
