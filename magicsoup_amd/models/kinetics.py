@@ -794,11 +794,15 @@ class Kinetics:
             slot = d["_slot"]
             p_old = self._P()
             ok = self._pack_ok()
+            # row capacity of the new layout: the live rows plus the usual spare (not the old
+            # capacity, which earlier growth may have inflated)
+            row_bytes = sum(t[:1].numel() * t.element_size() for t in store.values()) * max_n // max(p_old, 1)
+            rows_new = n + max(n // 2, min(3 * n, (4 << 30) // max(row_bytes, 1)))
             moves = []
             for name, t in list(store.items()):
                 # dense rows for all n cells (in row-storage mode cells share rows, so n may exceed
                 # the storage's row count)
-                nb = torch.empty(max(int(t.size(0)), n), max_n, *t.shape[2:], dtype=t.dtype, device=dev)
+                nb = torch.empty(rows_new, max_n, *t.shape[2:], dtype=t.dtype, device=dev)
                 moves.append((t, nb))
                 store[name] = nb
             hip_ops.copy_row_prefixes(moves, n, src_rows=slot)

@@ -975,10 +975,10 @@ class World:
         tokens, nprots = world_ops.translate(self, data, lens, rows)
         P = int(tokens.size(1))
         if P > self.kinetics._P():
-            # a new longest proteome: grow with headroom on the GPU so that mutations creeping the
-            # maximum up do not re-layout all parameter tensors every few steps (padding proteins are
-            # inert: Vmax 0)
-            self.kinetics.increase_max_proteins(P + max(4, P // 4) if data.is_cuda else P)
+            # a new longest proteome: grow with headroom on the GPU (1.5x) so that genomes growing
+            # through recombination do not re-layout the parameter storage every few dozen steps
+            # (padding proteins are inert: Vmax 0)
+            self.kinetics.increase_max_proteins(P + max(8, P // 2) if data.is_cuda else P)
         # one build launch: rows without proteins are unset in the same pass
         self.kinetics.set_cell_params_tokens(rows, tokens, nprot=nprots)
 
