@@ -465,10 +465,11 @@ void claim_free(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uin
 }
 
 constexpr int kPlaceWgMax = 2048;  // single-workgroup rounds up to this many cells (one CU: ~2 cells per thread)
-constexpr int kCoopBlocks = 128;   // co-resident workgroups of the cooperative placement (256 CUs)
+static int g_coop_blocks = 256;    // co-resident workgroups of the cooperative placement (one per CU; 128: +18 % time)
 static int g_place_mode = 0;       // 0 cooperative, 1 multi-launch rounds (A/B, set_place_mode)
 static unsigned* g_place_ctl = nullptr;
 void set_place_mode(int mode) { g_place_mode = mode; }
+void set_coop_blocks(int n) { g_coop_blocks = std::max(1, std::min(n, 1024)); }
 
 // Cooperative placement over `cells` (k entries) or over cells 0..k-1 selected by `mask`; returns
 // false if the device refused the cooperative launch (the caller falls back to the rounds path).
@@ -491,7 +492,7 @@ static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, co
   Geom gg = g;
   bool vac = vacate;
   void* args[] = {&kk, &cp, &mp, &pp, &gg, &vac, &cm, &pend, &seed, &call, &cd, &cl, &res, &rr, &ctl};
-  const unsigned grid = std::min<unsigned>(cdiv(k, 256), kCoopBlocks);
+  const unsigned grid = std::min<unsigned>(cdiv(k, 256), (unsigned)g_coop_blocks);
   const hipError_t e = hipLaunchCooperativeKernel((const void*)place_rounds_coop_kernel, dim3(grid), dim3(256), args,
                                                   0, s);
   if (e != hipSuccess) {

@@ -55,6 +55,8 @@ def hip():
     if fresh and os.environ.get("MS_PLACE_MODE"):
         # 1: per-round placement launches instead of the cooperative single launch (world.hip)
         mod.set_place_mode(int(os.environ["MS_PLACE_MODE"]))  # type: ignore[attr-defined]
+    if fresh and os.environ.get("MS_COOP_BLOCKS"):
+        mod.set_coop_blocks(int(os.environ["MS_COOP_BLOCKS"]))  # type: ignore[attr-defined]
     return mod
 
 
