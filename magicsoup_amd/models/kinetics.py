@@ -212,6 +212,13 @@ _PACK_SRC = ("N", "Nf", "Nb", "A", "Vmax", "Kmf", "Kmb", "Ke")
 _PACKED = ("_W", "_Q")
 
 
+def _spare_rows(n: int, row_bytes: int) -> int:
+    """Spare parameter-storage rows kept beyond the n live ones: up to 3n within an 8 GiB budget,
+    at least n / 8 (every rebuilt cell takes a fresh row; the spare count sets how many steps pass
+    between row recycles, which cost one mark + compaction pass each)."""
+    return max(n // 8, min(3 * n, (8 << 30) // max(row_bytes, 1)), 1024)
+
+
 class Kinetics:
     """Protein work of all cells.
 
@@ -585,17 +592,16 @@ class Kinetics:
 
     def _recycle_rows(self, k: int) -> torch.Tensor | None:
         """Make >= k fresh rows available: the free list of storage rows that no live cell (and not
-        the shared all-zero row) maps to, or -- below the spare target -- a dense re-gather into a
-        larger storage. Spare target: >= n/2 rows, up to 3n within a 4 GiB budget (every rebuilt
-        cell takes a fresh row, so the spare count sets how many steps pass between recycles)."""
+        the shared all-zero row) maps to, or -- with fewer than k plus a quarter of the spare target
+        (_spare_rows) free -- a dense re-gather into a larger storage."""
         d = self.__dict__
         store = self._store
         n = d["_ncells"]
         cap = min(int(t.size(0)) for t in store.values())
         row_bytes = sum(t[:1].numel() * t.element_size() for t in store.values())
-        spare = max(n // 2, min(3 * n, (4 << 30) // max(row_bytes, 1)))
+        spare = _spare_rows(n, row_bytes)
         slot = d["_slot"]
-        if slot.is_cuda and cap - n >= k + spare // 2:
+        if slot.is_cuda and cap - n >= k + spare // 4:
             from magicsoup_amd.ops import hip_ops
 
             used = torch.zeros(cap, dtype=torch.uint8, device=slot.device)
@@ -605,7 +611,7 @@ class Kinetics:
             if z is not None:
                 used.index_fill_(0, z, 1)
             free = hip_ops.select(used, "clear")[0]
-            if int(free.numel()) >= k:
+            if int(free.numel()) >= k + spare // 4:  # else: grow (recycling would come back soon)
                 d["_free"] = free
                 d["_nrows"] = 0
                 return free
@@ -797,7 +803,7 @@ class Kinetics:
             # row capacity of the new layout: the live rows plus the usual spare (not the old
             # capacity, which earlier growth may have inflated)
             row_bytes = sum(t[:1].numel() * t.element_size() for t in store.values()) * max_n // max(p_old, 1)
-            rows_new = n + max(n // 2, min(3 * n, (4 << 30) // max(row_bytes, 1)))
+            rows_new = n + _spare_rows(n, row_bytes)
             moves = []
             for name, t in list(store.items()):
                 # dense rows for all n cells (in row-storage mode cells share rows, so n may exceed

@@ -402,7 +402,9 @@ def degrade(world) -> None:
         cm = world.cell_molecules
         cm.mul_(f)
     pend = world.__dict__.get("_pending_scale")
-    world.__dict__["_pending_scale"] = f.clone() if pend is None else pend * f
+    # the cached factor tensor itself (pending factors are only ever read or replaced, never
+    # written in place)
+    world.__dict__["_pending_scale"] = f if pend is None else pend * f
 
 
 def apply_pending(world) -> None:

@@ -727,7 +727,8 @@ def test_parameter_rows_follow_genomes_through_bench_steps(monkeypatch, recycle)
         w.mutate_cells(p=1e-4)
         w.recombinate_cells(p=1e-5)
     w._reconcile()
-    assert any(recycled) == recycle, recycled
+    if recycle:
+        assert any(recycled), recycled  # (without forcing, recycling may or may not happen in 8 steps)
     ref = copy.deepcopy(w)
     ref._update_params_rows(torch.arange(ref.n_cells, device="cuda"))
     ka, kb = w.kinetics, ref.kinetics
