@@ -32,6 +32,7 @@ constexpr int kWideBlocksPerCU = 2;  // resident blocks per CU of the strided wi
 // launch. Measured at 4096^2 / 50k (3 parts, 4 iterations): serial 532 us, concurrent 558 us,
 // 16-lane 590 us -- the kernel is VALU-throughput bound (37M wave instructions per launch, ~60 %
 // of the SIMDs' issue capacity), so overlapping the bins only adds contention. Serial is default.
+// bit 3: legacy LDS-staged path; bit 4: register path with cells sorted by active-protein count.
 static int g_integrate_mode = 0;
 void set_integrate_mode(int mode) { g_integrate_mode = mode; }
 
@@ -755,11 +756,56 @@ __global__ void __launch_bounds__(kBlock) integrate_scatter_kernel(int c, int s,
 // X (c, s) -> snapshot slot 0 with an all-zero mask, so a part kernel can start from an explicit X.
 // Both input kernels also clear the launch's flag words (zero[0..nz)) and the wide-list counter
 // (zero_wc, optional) from block 0: no separate memset launches before part 0.
+constexpr int kSortBuckets = 34;  // active-protein counts 0..32, and "more" (the wide bin)
+
 __device__ __forceinline__ void clear_words(unsigned* zero, int nz, int32_t* zero_wc) {
   if (blockIdx.x == 0) {
     if ((int)threadIdx.x < nz) zero[threadIdx.x] = 0u;
     if (threadIdx.x == 0 && zero_wc) *zero_wc = 0;
+    // the active-protein sort's histogram and cursors follow the wide-list counter
+    if (zero_wc && (int)threadIdx.x < 2 * kSortBuckets) zero_wc[1 + threadIdx.x] = 0;
   }
+}
+
+// Active proteins per cell (Vmax > 0 or NaN: the set every part integrates, all trims being
+// positive) into a histogram; with the scatter below, the register-resident launches take the cells
+// in order of that count, so the two cells sharing a wave have similar protein / non-zero counts
+// and the wave-uniform loop bounds (the larger of the two) waste fewer lanes (mode bit 4; measured
+// slower, see the launcher).
+__global__ void __launch_bounds__(256) na_hist_kernel(int c, int P, const float4* Q, const int64_t* prow,
+                                                      uint8_t* na_out, int32_t* hist, int32_t* total) {
+  __shared__ int h[kSortBuckets];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *total = c;
+  if ((int)threadIdx.x < kSortBuckets) h[threadIdx.x] = 0;
+  __syncthreads();
+  const int cell = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cell < c) {
+    const size_t r = prow ? (size_t)prow[cell] : (size_t)cell;
+    int na = 0;
+    for (int p = 0; p < P; ++p) na += !(Q[r * P + p].x <= 0.0f);
+    const int b = na > 32 ? 33 : na;
+    na_out[cell] = (uint8_t)b;
+    atomicAdd(&h[b], 1);
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < kSortBuckets && h[threadIdx.x]) atomicAdd(hist + threadIdx.x, h[threadIdx.x]);
+}
+
+__global__ void __launch_bounds__(256) na_scatter_kernel(int c, const uint8_t* na, const int32_t* hist, int32_t* cursor,
+                                                         int32_t* order) {
+  __shared__ int base[kSortBuckets];
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int b = 0; b < kSortBuckets; ++b) {
+      base[b] = acc;
+      acc += hist[b];
+    }
+  }
+  __syncthreads();
+  const int cell = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cell >= c) return;
+  const int b = na[cell];
+  order[base[b] + atomicAdd(cursor + b, 1)] = cell;
 }
 
 __global__ void load_x_kernel(int c, int s, const float* X, float* snap, unsigned* zero, int nz, int32_t* zero_wc) {
@@ -1012,9 +1058,31 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     if (ldsw > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
     const long long per_cu = std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)ldsw));
     const unsigned gridw = (unsigned)std::min<long long>(cdiv(c, cpsw), 256 * per_cu);
+    // lists layout: [c, 2c) wide list, 2c + 1 wide count, 2c + 2 .. histogram + cursors (cleared by
+    // the input kernel of part 0), then the sort order (c) and per-cell counts (c bytes)
+    int32_t* hist = wc + 1;
+    int32_t* cursor = hist + kSortBuckets;
+    int32_t* order = cursor + kSortBuckets;
+    int32_t* total = order + c;  // = c (device count for the list launch)
+    uint8_t* na = reinterpret_cast<uint8_t*>(total + 1);
+    // off by default: on the flagship state the sorted order was 31 % slower (682 vs 521 us per
+    // 3-part integration, scripts/integrator_bench.py) -- neighbouring cells' parameter rows are
+    // neighbours in memory, and losing that locality costs more than the wasted lanes
+    const bool sorted = (g_integrate_mode & 16) != 0;
+    if (sorted && part_begin == 0) {
+      na_hist_kernel<<<cdiv(c, 256), 256, 0, st>>>(c, P, P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr, na, hist,
+                                                    total);
+      MS_LAUNCH_CHECK();
+      na_scatter_kernel<<<cdiv(c, 256), 256, 0, st>>>(c, na, hist, cursor, order);
+      MS_LAUNCH_CHECK();
+    }
     for (int part = part_begin; part < part_end; ++part) {
       IntegrateArgs a = part_args(part);
       a.Ps = G;
+      if (sorted) {
+        a.list = order;
+        a.count = total;
+      }
       if (G == 32) integrate_fast_kernel<32><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
       else integrate_fast_kernel<64><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
       MS_LAUNCH_CHECK();

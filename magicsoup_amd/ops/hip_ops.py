@@ -190,7 +190,8 @@ def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n
         [float(t) for t in trims], int(n_iters),
     ]
     slot_p = _p(None if slot is None else slot.to(torch.int64).contiguous())
-    lists = sc.get("bin_lists", 2 * c + 2, torch.int32, dev)  # narrow / wide cell lists + counts
+    # narrow / wide cell lists + counts, the active-protein sort (histogram, cursors, order, counts)
+    lists = sc.get("bin_lists", 3 * c + c // 4 + 80, torch.int32, dev)
     nparts = len(trims)
     if flags_hook is None:
         _m().integrate(*args, 0, nparts, True, slot_p, _p(lists), mdt, _p(corr), _stream())
