@@ -391,9 +391,9 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
 constexpr int kNzReg = 16;  // non-zero signals per protein in the LDS lists (more: the cell goes wide)
 
 // LDS words per cell slot of the register-resident integrator
-template <int G>
+template <int G, int NZ>
 constexpr int fast_slot_words() {
-  return G * kNzReg /*entry words*/ + G * kNzReg / 4 /*entry signal indices*/ + 4 * G /*cnt, act, X, pub*/;
+  return G * NZ /*entry words*/ + G * NZ / 4 /*entry signal indices*/ + 4 * G /*cnt, act, X, pub*/;
 }
 
 template <int G>
@@ -420,7 +420,7 @@ __device__ __forceinline__ float ipow_small(float x, int n) {
   return n < 0 ? 1.0f / r : r;
 }
 
-template <int G>
+template <int G, int NZ>
 __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int* smem, int item, unsigned& bits,
                                                     int32_t* wide_list, int32_t* wide_count) {
   const int slot = threadIdx.x / G, lane = threadIdx.x % G;
@@ -429,9 +429,9 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   const int P = a.P, s = a.s;
   const size_t prow = listed ? (a.prow ? (size_t)a.prow[cell] : (size_t)cell) : 0;
 
-  int* ents = smem + slot * fast_slot_words<G>();                // (G, kNzReg) words of the non-zeros
-  uint8_t* jl = reinterpret_cast<uint8_t*>(ents + G * kNzReg);   // (G, kNzReg) their signal indices
-  int* cnts = ents + G * kNzReg + G * kNzReg / 4;                // (G,) non-zero signals per protein
+  int* ents = smem + slot * fast_slot_words<G, NZ>();                // (G, NZ) words of the non-zeros
+  uint8_t* jl = reinterpret_cast<uint8_t*>(ents + G * NZ);   // (G, NZ) their signal indices
+  int* cnts = ents + G * NZ + G * NZ / 4;                // (G,) non-zero signals per protein
   int* act = cnts + G;                                           // (G,) protein slot of active protein k
   float* Xs = reinterpret_cast<float*>(act + G);                 // (G,) signal -> protein: X_j / factor
   float* pub = Xs + G;                                           // (G,) protein -> signal: V_k / Va_k * F_k
@@ -467,7 +467,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   int npk[G / 4];
 #pragma unroll
   for (int i = 0; i < G / 4; ++i) npk[i] = 0;
-  bool wide_ok = true;  // every protein has <= kNzReg non-zeros and exponents < 32
+  bool wide_ok = true;  // every protein has <= NZ non-zeros and exponents < 32
 #pragma unroll
   for (int k0 = 0; k0 < G; k0 += 8) {
     if (k0 >= na_w) break;
@@ -484,12 +484,12 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
       const bool on = w[u] != 0;
       const unsigned long long gm = group_ballot<G>(on);
       const int r = __popcll(gm & ((1ull << lane) - 1ull));
-      if (on && r < kNzReg) {
-        ents[k * kNzReg + r] = w[u];
-        jl[k * kNzReg + r] = (uint8_t)lane;
+      if (on && r < NZ) {
+        ents[k * NZ + r] = w[u];
+        jl[k * NZ + r] = (uint8_t)lane;
       }
       if (lane == 0 && k < nac) cnts[k] = __popcll(gm);
-      wide_ok &= __popcll(gm) <= kNzReg && w_nf(w[u]) < 32 && w_nb(w[u]) < 32;
+      wide_ok &= __popcll(gm) <= NZ && w_nf(w[u]) < 32 && w_nb(w[u]) < 32;
     }
   }
   fits = fits && group_ballot<G>(!wide_ok) == 0ull;
@@ -504,9 +504,9 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   // damping iterations (velocity and limiting factor read the full words from LDS once per part)
   float vmx = 0.0f, kmf = 1.0f, kmb = 1.0f, ke = 1.0f;
   int pk = 0, cnt = 0;
-  int e16[kNzReg / 2];
+  int e16[NZ / 2];
 #pragma unroll
-  for (int q = 0; q < kNzReg / 2; ++q) e16[q] = 0;
+  for (int q = 0; q < NZ / 2; ++q) e16[q] = 0;
   bool small = true;  // all exponents < 8: branch-free powers
   if (prot) {
     pk = act[lane];
@@ -517,11 +517,11 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     kmb = q4.z;
     ke = q4.w;
     cnt = cnts[lane];
-    const int* jw = reinterpret_cast<const int*>(jl + lane * kNzReg);
+    const int* jw = reinterpret_cast<const int*>(jl + lane * NZ);
 #pragma unroll
-    for (int q = 0; q < kNzReg; ++q) {
+    for (int q = 0; q < NZ; ++q) {
       if (q < cnt) {
-        const int w = ents[lane * kNzReg + q];
+        const int w = ents[lane * NZ + q];
         const int j = (jw[q >> 2] >> (8 * (q & 3))) & 0xFF;
         const int e = j | (w_nf(w) << 6) | (w_nb(w) << 11);
         e16[q >> 1] |= e << (16 * (q & 1));
@@ -556,9 +556,9 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     float xf = 1.0f, xb = 1.0f, ar = 1.0f;
     int nfs = 0, nbs = 0;
 #pragma unroll
-    for (int q = 0; q < kNzReg; ++q) {
+    for (int q = 0; q < NZ; ++q) {
       if (q >= cnt_w) break;
-      const int w = q < cnt ? ents[lane * kNzReg + q] : 0;
+      const int w = q < cnt ? ents[lane * NZ + q] : 0;
       const int j = MS_E(q) & 63;
       const int nf = w_nf(w), nb = w_nb(w), av = w_a(w);
       const float x = Xs[j];
@@ -608,9 +608,9 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     float fmin = 1.0f;
     bool nan = false;
 #pragma unroll
-    for (int q = 0; q < kNzReg; ++q) {
+    for (int q = 0; q < NZ; ++q) {
       if (q >= cnt_w) break;
-      const int w = q < cnt ? ents[lane * kNzReg + q] : 0;
+      const int w = q < cnt ? ents[lane * NZ + q] : 0;
       if ((float)w_n(w) * v < 0.0f) {
         const float f = Xs[MS_E(q) & 63];
         if (ms::f_isnan(f)) nan = true;
@@ -647,7 +647,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
       float pf = 1.0f, pb = 1.0f;
       int nfs = 0, nbs = 0;
 #pragma unroll
-      for (int q = 0; q < kNzReg; ++q) {
+      for (int q = 0; q < NZ; ++q) {
         if (q >= cnt_w) break;
         const int e = MS_E(q);
         const int nf = (e >> 6) & 31, nb = e >> 11;
@@ -695,13 +695,24 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
 #undef MS_E
 }
 
-template <int G>
+// kStrided: a list launch of unknown length (a.count on the device) on a small grid; each block
+// walks the list in steps of the whole grid (the bound is block-uniform, so every wave runs the
+// same number of items and the wave-wide ballots / reductions inside stay convergent)
+template <int G, int NZ, bool kStrided>
 __global__ void __launch_bounds__(kBlock) integrate_fast_kernel(IntegrateArgs a, int32_t* wide_list,
                                                                 int32_t* wide_count) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
   unsigned bits = 0u;
-  integrate_item_fast<G>(a, smem, (int)blockIdx.x * (blockDim.x / G) + (int)threadIdx.x / G, bits, wide_list,
-                         wide_count);
+  const int cpb = (int)blockDim.x / G;
+  if constexpr (kStrided) {
+    const int n = *a.count;
+    for (int base = (int)blockIdx.x * cpb; base < n; base += (int)gridDim.x * cpb) {
+      wave_lds_sync();  // the previous item's LDS reads are done before its slot is refilled
+      integrate_item_fast<G, NZ>(a, smem, base + (int)threadIdx.x / G, bits, wide_list, wide_count);
+    }
+  } else {
+    integrate_item_fast<G, NZ>(a, smem, (int)blockIdx.x * cpb + (int)threadIdx.x / G, bits, wide_list, wide_count);
+  }
   __shared__ unsigned wave_bits[kBlock / 64];
   for (int o = 32; o > 0; o >>= 1) bits |= __shfl_xor(bits, o);
   if ((threadIdx.x & 63) == 0) wave_bits[threadIdx.x >> 6] = bits;
@@ -761,7 +772,10 @@ constexpr int kSortBuckets = 34;  // active-protein counts 0..32, and "more" (th
 __device__ __forceinline__ void clear_words(unsigned* zero, int nz, int32_t* zero_wc) {
   if (blockIdx.x == 0) {
     if ((int)threadIdx.x < nz) zero[threadIdx.x] = 0u;
-    if (threadIdx.x == 0 && zero_wc) *zero_wc = 0;
+    if (threadIdx.x == 0 && zero_wc) {
+      zero_wc[0] = 0;
+      zero_wc[-1] = 0;  // the second-level wide count (cells the 64-lane fast launch cannot take)
+    }
     // the active-protein sort's histogram and cursors follow the wide-list counter
     if (zero_wc && (int)threadIdx.x < 2 * kSortBuckets) zero_wc[1 + threadIdx.x] = 0;
   }
@@ -1042,14 +1056,23 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     return a;
   };
   // register-resident path (default for s <= 64, integrate_item_fast): one launch per part over
-  // every cell with at most G active proteins; part 0 lists the others, which a strided launch with
-  // LDS slots for all P proteins (integrate_item) integrates after it
+  // every cell with at most G active proteins and kNzReg non-zeros per protein. Part 0 lists the
+  // others (wide list), which a strided 64-lane launch with 2 * kNzReg non-zeros per protein takes
+  // next; what does not fit there either (more than 64 active proteins, more non-zeros, exponents
+  // >= 32; part 0 lists it again) goes to a strided launch with LDS slots for all P proteins
+  // (integrate_item). The 64-lane launch replaced the LDS path for the wide list: that path's
+  // per-cell dependency chain made its launch ~40 us per part for a few hundred cells.
   if (fast_path) {
     int32_t* wl = P_<int32_t>(lists) + c;
     int32_t* wc = P_<int32_t>(lists) + 2 * (size_t)c + 1;  // cleared by the input kernel of part 0
+    int32_t* wl2 = P_<int32_t>(lists);
+    int32_t* wc2 = wc - 1;  // cleared with wc
     const int G = s <= 32 ? 32 : 64;
     const int cps = kBlock / G;
-    const size_t lds_fast = (size_t)cps * (G == 32 ? fast_slot_words<32>() : fast_slot_words<64>()) * 4;
+    const size_t lds_fast = (size_t)cps * (G == 32 ? fast_slot_words<32, kNzReg>() : fast_slot_words<64, kNzReg>()) * 4;
+    constexpr int kNzWide = 2 * kNzReg;
+    const size_t lds_fw = (size_t)(kBlock / 64) * fast_slot_words<64, kNzWide>() * 4;
+    const unsigned grid_fw = (unsigned)std::min<long long>(cdiv(c, kBlock / 64), 512);
     const int slot_words = slot_words_for(P, s, sp);
     const size_t slot_bytes = (size_t)slot_words * 4;
     int cpsw = kBlock / G;
@@ -1058,8 +1081,9 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     if (ldsw > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
     const long long per_cu = std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)ldsw));
     const unsigned gridw = (unsigned)std::min<long long>(cdiv(c, cpsw), 256 * per_cu);
-    // lists layout: [c, 2c) wide list, 2c + 1 wide count, 2c + 2 .. histogram + cursors (cleared by
-    // the input kernel of part 0), then the sort order (c) and per-cell counts (c bytes)
+    // lists layout: [0, c) second-level wide list, [c, 2c) wide list, 2c / 2c + 1 their counts,
+    // 2c + 2 .. histogram + cursors (cleared by the input kernel of part 0), then the sort order (c)
+    // and per-cell counts (c bytes)
     int32_t* hist = wc + 1;
     int32_t* cursor = hist + kSortBuckets;
     int32_t* order = cursor + kSortBuckets;
@@ -1069,6 +1093,8 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     // 3-part integration, scripts/integrator_bench.py) -- neighbouring cells' parameter rows are
     // neighbours in memory, and losing that locality costs more than the wasted lanes
     const bool sorted = (g_integrate_mode & 16) != 0;
+    // mode bit 5: skip the 64-lane level (the whole wide list takes the LDS path; for A/B)
+    const bool fw = (g_integrate_mode & 32) == 0;
     if (sorted && part_begin == 0) {
       na_hist_kernel<<<cdiv(c, 256), 256, 0, st>>>(c, P, P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr, na, hist,
                                                     total);
@@ -1083,11 +1109,20 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
         a.list = order;
         a.count = total;
       }
-      if (G == 32) integrate_fast_kernel<32><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
-      else integrate_fast_kernel<64><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
+      if (G == 32)
+        integrate_fast_kernel<32, kNzReg, false><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
+      else
+        integrate_fast_kernel<64, kNzReg, false><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
       MS_LAUNCH_CHECK();
       a.list = wl;
       a.count = wc;
+      if (fw) {
+        a.Ps = 64;
+        integrate_fast_kernel<64, kNzWide, true><<<grid_fw, kBlock, lds_fw, st>>>(a, part == 0 ? wl2 : nullptr, wc2);
+        MS_LAUNCH_CHECK();
+        a.list = wl2;
+        a.count = wc2;
+      }
       a.Ps = P;
       a.slot_words = slot_words;
       if (G == 32) integrate_part_kernel<32, true><<<gridw, cpsw * G, ldsw, st>>>(a);

@@ -41,16 +41,19 @@ def main():
     na = (kin.Vmax > 0).sum(1)
     out["active_mean"] = round(float(na.float().mean()), 2)
     out["active_hist"] = {str(k): int((na == k).sum()) for k in range(0, int(na.max()) + 1)}
+    nz = ((kin.N != 0).sum(2) * (kin.Vmax > 0)).amax(1)  # most non-zero signals of an active protein
+    out["wide_cells_nz16"] = int((nz > 16).sum())
+    out["wide_cells_nz32"] = int((nz > 32).sum())
     out["us_enzymatic_activity"] = timed(w.enzymatic_activity)
     from magicsoup_amd.ops import native
 
     for rep_i in range(3):  # A/B of the launch modes on the same state (alternating)
-        for mode in (0, 16):  # register path without / with the active-protein sort
+        for mode in (0, 16, 32):  # register path; + active-protein sort; wide list on the LDS path
             native.hip().set_integrate_mode(mode)
             Xk = X.clone()
             out[f"us_mode{mode}_r{rep_i}"] = timed(lambda: kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4))
     res = {}
-    for mode in (0, 8, 9, 10, 11, 12, 16):  # every mode computes the same state, bit for bit
+    for mode in (0, 8, 9, 10, 11, 12, 16, 32):  # every mode computes the same state, bit for bit
         native.hip().set_integrate_mode(mode)
         Xk = X.clone()
         kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4)

@@ -668,8 +668,10 @@ def _integrate_modes(kin, X, modes=(0, 8)):
 @pytest.mark.parametrize("case", ["wl500", "wl3000", "syn20", "syn40", "big_exponents"])
 def test_register_integrator_matches_lds_integrator_bit_for_bit(case):
     """The register-resident launches (mode 0: cells with <= 32 / 64 active proteins and <= 16
-    non-zero signals per protein; the rest through the wide LDS launch) against the legacy
-    LDS-staged launches (mode 8) on the same state: identical results, bit for bit."""
+    non-zero signals per protein; the rest through a 64-lane launch with 32 non-zeros per protein,
+    and what does not fit there through the wide LDS launch; mode 32 skips the 64-lane level)
+    against the legacy LDS-staged launches (mode 8) on the same state: identical results, bit for
+    bit."""
     if case.startswith("syn"):
         from magicsoup_amd.examples.synthetic import make_chemistry
 
@@ -694,8 +696,9 @@ def test_register_integrator_matches_lds_integrator_bit_for_bit(case):
         assert int(na.max()) > 32  # exercises the wide launch
     pos = w.cell_positions.long()
     X = torch.cat([w.cell_molecules, w.molecule_map[:, pos[:, 0], pos[:, 1]].T], dim=1).contiguous()
-    out = _integrate_modes(kin, X)
+    out = _integrate_modes(kin, X, modes=(0, 8, 32))
     assert torch.equal(out[0], out[8])
+    assert torch.equal(out[32], out[8])
     assert not torch.equal(out[0], X)
 
 
