@@ -389,6 +389,7 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
 // cell with more than G active proteins is appended (part 0) to the wide list and integrated by
 // integrate_item with all P protein slots.
 constexpr int kNzReg = 16;  // non-zero signals per protein in the LDS lists (more: the cell goes wide)
+constexpr int kNzWide = 2 * kNzReg;  // the same for the 64-lane launch of the wide list
 
 // LDS words per cell slot of the register-resident integrator
 template <int G, int NZ>
@@ -720,6 +721,43 @@ __global__ void __launch_bounds__(kBlock) integrate_fast_kernel(IntegrateArgs a,
   if (threadIdx.x == 0) {
     unsigned b = 0u;
     for (int w = 0; w < (int)(blockDim.x + 63) / 64; ++w) b |= wave_bits[w];
+    for (int it = 0; it < ms::kEqIters; ++it)
+      if ((b & (1u << it)) && __hip_atomic_load(a.mask_out + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+        atomicOr(a.mask_out + it, 1u);
+  }
+}
+
+// Parts >= 1 of the register path with the wide list (known from part 0) in the same launch: the
+// first `nwb` blocks walk the wide list with two 64-lane slots each (integrate_item_fast<64,
+// kNzWide>, the rest of the block idles), the others take the cells as integrate_fast_kernel<G>.
+// A wide cell's integration is a long dependency chain (~30 us on its own); at the front of the
+// grid it runs under the narrow blocks instead of after them. Cells that do not fit the 64-lane
+// slots either are skipped here (part 0 listed them for the LDS launch).
+template <int G>
+__global__ void __launch_bounds__(kBlock, 6) integrate_fused_kernel(IntegrateArgs a, IntegrateArgs aw, int nwb) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  static_assert(2 * fast_slot_words<64, kNzWide>() <= (kBlock / G) * fast_slot_words<G, kNzReg>(),
+                "two wide slots must fit the narrow block's LDS");
+  unsigned bits = 0u;
+  if ((int)blockIdx.x < nwb) {
+    if (threadIdx.x < 128) {
+      const int n = *aw.count;  // block-uniform bound: both waves run the same number of items
+      for (int base = (int)blockIdx.x * 2; base < n; base += nwb * 2) {
+        wave_lds_sync();
+        integrate_item_fast<64, kNzWide>(aw, smem, base + (int)threadIdx.x / 64, bits, nullptr, nullptr);
+      }
+    }
+  } else {
+    integrate_item_fast<G, kNzReg>(a, smem, ((int)blockIdx.x - nwb) * (kBlock / G) + (int)threadIdx.x / G, bits,
+                                   nullptr, nullptr);
+  }
+  __shared__ unsigned wave_bits[kBlock / 64];
+  for (int o = 32; o > 0; o >>= 1) bits |= __shfl_xor(bits, o);
+  if ((threadIdx.x & 63) == 0) wave_bits[threadIdx.x >> 6] = bits;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned b = 0u;
+    for (int w = 0; w < kBlock / 64; ++w) b |= wave_bits[w];
     for (int it = 0; it < ms::kEqIters; ++it)
       if ((b & (1u << it)) && __hip_atomic_load(a.mask_out + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
         atomicOr(a.mask_out + it, 1u);
@@ -1070,9 +1108,9 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     const int G = s <= 32 ? 32 : 64;
     const int cps = kBlock / G;
     const size_t lds_fast = (size_t)cps * (G == 32 ? fast_slot_words<32, kNzReg>() : fast_slot_words<64, kNzReg>()) * 4;
-    constexpr int kNzWide = 2 * kNzReg;
     const size_t lds_fw = (size_t)(kBlock / 64) * fast_slot_words<64, kNzWide>() * 4;
     const unsigned grid_fw = (unsigned)std::min<long long>(cdiv(c, kBlock / 64), 512);
+    constexpr int kFusedWideBlocks = 64;
     const int slot_words = slot_words_for(P, s, sp);
     const size_t slot_bytes = (size_t)slot_words * 4;
     int cpsw = kBlock / G;
@@ -1109,20 +1147,30 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
         a.list = order;
         a.count = total;
       }
-      if (G == 32)
-        integrate_fast_kernel<32, kNzReg, false><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
-      else
-        integrate_fast_kernel<64, kNzReg, false><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
-      MS_LAUNCH_CHECK();
-      a.list = wl;
-      a.count = wc;
-      if (fw) {
-        a.Ps = 64;
-        integrate_fast_kernel<64, kNzWide, true><<<grid_fw, kBlock, lds_fw, st>>>(a, part == 0 ? wl2 : nullptr, wc2);
+      IntegrateArgs aw = a;
+      aw.list = wl;
+      aw.count = wc;
+      aw.Ps = 64;
+      // mode bit 6: parts >= 1 launch the wide list separately too (A/B of the fused launch)
+      // (32-lane cells only: the 64-lane narrow path needs more registers than the fused kernel's
+      // occupancy target leaves)
+      const bool fused = G == 32 && fw && part > 0 && (g_integrate_mode & 64) == 0;
+      if (fused) {
+        integrate_fused_kernel<32><<<cdiv(c, cps) + kFusedWideBlocks, kBlock, lds_fast, st>>>(a, aw, kFusedWideBlocks);
         MS_LAUNCH_CHECK();
-        a.list = wl2;
-        a.count = wc2;
+      } else {
+        if (G == 32)
+          integrate_fast_kernel<32, kNzReg, false><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
+        else
+          integrate_fast_kernel<64, kNzReg, false><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
+        MS_LAUNCH_CHECK();
+        if (fw) {
+          integrate_fast_kernel<64, kNzWide, true><<<grid_fw, kBlock, lds_fw, st>>>(aw, part == 0 ? wl2 : nullptr, wc2);
+          MS_LAUNCH_CHECK();
+        }
       }
+      a.list = fw ? wl2 : wl;
+      a.count = fw ? wc2 : wc;
       a.Ps = P;
       a.slot_words = slot_words;
       if (G == 32) integrate_part_kernel<32, true><<<gridw, cpsw * G, ldsw, st>>>(a);

@@ -48,12 +48,12 @@ def main():
     from magicsoup_amd.ops import native
 
     for rep_i in range(3):  # A/B of the launch modes on the same state (alternating)
-        for mode in (0, 16, 32):  # register path; + active-protein sort; wide list on the LDS path
+        for mode in (0, 16, 32, 64):  # register path; + sort; wide list on the LDS path; unfused
             native.hip().set_integrate_mode(mode)
             Xk = X.clone()
             out[f"us_mode{mode}_r{rep_i}"] = timed(lambda: kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4))
     res = {}
-    for mode in (0, 8, 9, 10, 11, 12, 16, 32):  # every mode computes the same state, bit for bit
+    for mode in (0, 8, 9, 10, 11, 12, 16, 32, 64):  # every mode computes the same state, bit for bit
         native.hip().set_integrate_mode(mode)
         Xk = X.clone()
         kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4)

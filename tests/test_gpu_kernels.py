@@ -696,9 +696,10 @@ def test_register_integrator_matches_lds_integrator_bit_for_bit(case):
         assert int(na.max()) > 32  # exercises the wide launch
     pos = w.cell_positions.long()
     X = torch.cat([w.cell_molecules, w.molecule_map[:, pos[:, 0], pos[:, 1]].T], dim=1).contiguous()
-    out = _integrate_modes(kin, X, modes=(0, 8, 32))
+    out = _integrate_modes(kin, X, modes=(0, 8, 32, 64))
     assert torch.equal(out[0], out[8])
     assert torch.equal(out[32], out[8])
+    assert torch.equal(out[64], out[8])
     assert not torch.equal(out[0], X)
 
 
