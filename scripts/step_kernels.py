@@ -1,21 +1,38 @@
 """Kernels of the timed steps of a rocprofv3 kernel trace of bench.py, steps delimited by the
-diffusion stencil (one launch per step): wall / busy / launches per step and one step's launch
-sequence with the idle gap before each kernel.
+diffusion stencil (one launch per step): wall / busy / launches per step, and the launch sequence
+of the step with the median wall time: hardware queue, start / end relative to the previous
+stencil's end, and the idle gap of that queue before each kernel (side-stream work shows up on its
+own queue).
 
 usage: python scripts/step_kernels.py <kernel_trace.csv> <steps>"""
-import csv, sys, collections
+import csv
+import statistics
+import sys
+
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 marks = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("void msd::diffuse_stencil4")]
 nst = int(sys.argv[2])
-a, b = marks[-nst-1], marks[-1]
-sel = rows[a+1:b+1]
-t0 = int(rows[a]["End_Timestamp"]); t1 = int(rows[b]["End_Timestamp"])
-busy = sum(int(r["End_Timestamp"])-int(r["Start_Timestamp"]) for r in sel)
-print(f"{nst} steps: {(t1-t0)/1e3/nst:.1f} us/step wall, {busy/1e3/nst:.1f} us busy, {len(sel)/nst:.1f} launches/step")
-# one step list with gaps
-one = rows[marks[-2]+1:marks[-1]+1]
-prev = int(rows[marks[-2]]["End_Timestamp"])
+a, b = marks[-nst - 1], marks[-1]
+sel = rows[a + 1 : b + 1]
+t0 = int(rows[a]["End_Timestamp"])
+t1 = int(rows[b]["End_Timestamp"])
+busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in sel)
+print(f"{nst} steps: {(t1 - t0) / 1e3 / nst:.1f} us/step wall, {busy / 1e3 / nst:.1f} us busy, "
+      f"{len(sel) / nst:.1f} launches/step")
+walls = []
+for j in range(len(marks) - nst, len(marks)):
+    walls.append((int(rows[marks[j]]["End_Timestamp"]) - int(rows[marks[j - 1]]["End_Timestamp"]), j))
+med = sorted(walls)[len(walls) // 2]
+print(f"step walls (us): median {statistics.median(w for w, _ in walls) / 1e3:.1f}, "
+      f"min {min(walls)[0] / 1e3:.1f}, max {max(walls)[0] / 1e3:.1f}; listing the median step")
+j = med[1]
+one = rows[marks[j - 1] + 1 : marks[j] + 1]
+base = int(rows[marks[j - 1]]["End_Timestamp"])
+last = {}
 for r in one:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-    print(f"gap {(s-prev)/1e3:7.1f}  dur {(e-s)/1e3:7.1f}  {r['Kernel_Name'][:90]}")
-    prev = e
+    q = r.get("Queue_Id", "?")
+    gap = (s - last.get(q, base)) / 1e3
+    last[q] = e
+    print(f"q{q:>2} {(s - base) / 1e3:8.1f} {(e - base) / 1e3:8.1f}  gap {gap:6.1f}  dur {(e - s) / 1e3:6.1f}  "
+          f"{r['Kernel_Name'][:80]}")

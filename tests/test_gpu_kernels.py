@@ -594,9 +594,10 @@ def test_device_genome_pipeline_matches_sync_path(monkeypatch, d_cap):
 
 
 def test_deferred_genome_ops_match_immediate_issue(monkeypatch):
-    """All-cells mutate / recombinate are queued until the next op that reads genomes, parameters
-    or cells (degrade / diffuse / lifetimes run in between): same genomes, parameters and
-    trajectory as issuing them immediately; reading ``cell_genomes`` flushes the queue."""
+    """All-cells mutate / recombinate are queued until the diffusion stencil is launched or the
+    next op that reads genomes, parameters or cells (degrade runs in between): same genomes,
+    parameters and trajectory as issuing them immediately; diffuse_molecules issues the queue and
+    reading ``cell_genomes`` confirms it."""
     import magicsoup_amd.models.world as world_mod
 
     base = _world("cuda", map_size=64, n=800, s=400, seed=7)
@@ -611,10 +612,12 @@ def test_deferred_genome_ops_match_immediate_issue(monkeypatch):
     w = copy.deepcopy(base)
     w.recombinate_cells(p=1e-4)
     w.mutate_cells(p=1e-3)
-    w.diffuse_molecules()
+    w.degrade_molecules()
     assert len(w.__dict__.get("_deferred", [])) == 2
+    w.diffuse_molecules()
+    assert not w.__dict__["_deferred"]
     genomes = list(w.cell_genomes)
-    assert not w.__dict__["_deferred"] and len(genomes) == w.n_cells
+    assert not w.__dict__.get("_gp_state", {}).get("pending") and len(genomes) == w.n_cells
 
 
 def test_widening_proteins_keeps_parameters_in_slot_mode():
