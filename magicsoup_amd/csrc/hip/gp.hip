@@ -8,6 +8,9 @@
 // counters, kinetics storage + LUTs, translation LUTs) and makes one call; the launches, scratch
 // layout and status slot are handled in C++.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <tuple>
 
 #include "hip_common.h"
 
@@ -16,6 +19,9 @@ namespace py = pybind11;
 namespace msd {
 
 // ---- launchers defined in the other translation units
+void rec_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map, uintptr_t lens,
+               double p, uint64_t seed, uint64_t call, int kcap, uintptr_t gflags, uintptr_t opflags, uintptr_t keys,
+               uintptr_t k, uintptr_t sel, uintptr_t out_dev, int cap, uintptr_t stream);
 void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel, uintptr_t rest,
                         uintptr_t out_dev, uintptr_t stream);
 void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
@@ -283,9 +289,12 @@ int gp_mutate(const GpArena& a, const GpGen& g, const GpKin& k, double p, double
 
 // recombinate_cells() over neighbour slot keys (8 per cell); `extra` (optional Python object with
 // .rows and .apply(pair_count, out, out_w, out_len, out_rows, nres)) appends strip-boundary results.
-int gp_recombine(const GpArena& a, const GpGen& g, const GpKin& k, uintptr_t keys, double p, uint64_t seed,
-                 uint64_t call, int cap, int kcap, int dcap, uintptr_t mark, uint64_t gen, py::object extra,
-                 uintptr_t nres, uintptr_t blob, uintptr_t stream) {
+// keys: the neighbour slot keys (8n int64); with `nbr` = (positions, R, C, r_lo, r_hi, wrap, index
+// map) they are computed here, fused with the draws and the selection count (world.hip rec_slots),
+// otherwise read.
+int gp_recombine(const GpArena& a, const GpGen& g, const GpKin& k, uintptr_t keys, py::object nbr, double p,
+                 uint64_t seed, uint64_t call, int cap, int kcap, int dcap, uintptr_t mark, uint64_t gen,
+                 py::object extra, uintptr_t nres, uintptr_t blob, uintptr_t stream) {
   hipStream_t s = S_(stream);
   const int n = a.n, L = a.width;
   const int xr = extra.is_none() ? 0 : extra.attr("rows").cast<int>();
@@ -295,8 +304,14 @@ int gp_recombine(const GpArena& a, const GpGen& g, const GpKin& k, uintptr_t key
   const uintptr_t out = c.take((size_t)nr * out_w), out_len = c.take(4 * (size_t)nr), out_rows = c.take(8 * (size_t)nr);
   const uintptr_t parts = c.take(4 * (size_t)cap * parts_cap * 3);
   const uintptr_t won = c.take((size_t)nr), q = c.take(8 * (size_t)nr), cells = c.take(8 * (size_t)nr);
-  rec_count_keys(8 * n, keys, a.lens, p, seed, call, kk, 0, kcap, a.gflags, a.opflags, stream);
-  select_indices_capped(8ll * n, kSelI32Pos, kk, sel, a.cnt, cap, a.gflags, a.opflags, stream);
+  if (!nbr.is_none()) {
+    const auto t = nbr.cast<std::tuple<uintptr_t, int, int, int, int, int, uintptr_t>>();
+    rec_slots(n, std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t), std::get<4>(t), std::get<5>(t),
+              std::get<6>(t), a.lens, p, seed, call, kcap, a.gflags, a.opflags, keys, kk, sel, a.cnt, cap, stream);
+  } else {
+    rec_count_keys(8 * n, keys, a.lens, p, seed, call, kk, 0, kcap, a.gflags, a.opflags, stream);
+    select_indices_capped(8ll * n, kSelI32Pos, kk, sel, a.cnt, cap, a.gflags, a.opflags, stream);
+  }
   rec_apply(cap, a.cnt, sel, 0, keys, a.data, L, a.lens, kk, seed, call, parts, parts_cap, out, out_w, out_len,
             out_rows, stream);
   if (xr) {

@@ -114,7 +114,11 @@ __global__ void __launch_bounds__(64 * kWaves) diffuse_stencil_kernel(const T* _
 // of the same column strip. While row o is computed, the load of row o + 2 is in flight (row o + 1
 // arrived in the previous iteration): one row load per wave ahead. A variant with two row loads in
 // flight was measured and not kept (docs/performance.md, "Diffusion").
-// grid: (ceil(C / 256), ceil(ceil(H / kBand) / 4), m).
+// Tiles: (ceil(C / 256), ceil(ceil(H / kBand) / 4), m), x fastest; a 1-D grid of `gridDim.x`
+// blocks walks them in steps of the grid (one tile per block when the grid is the tile count). A
+// smaller grid leaves workgroup slots free on every CU, so the side stream's short pipeline kernels
+// (deferred genome chains, World._flush_deferred) start at once instead of waiting for stencil
+// workgroups to retire (set_stencil_blocks).
 constexpr int kVBand = 32;
 template <class T>
 __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restrict__ in, T* __restrict__ out,
@@ -122,12 +126,14 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
                                                                const float* __restrict__ wb,
                                                                const float* __restrict__ scale,
                                                                const float* __restrict__ corr, MGeom g,
-                                                               double* __restrict__ partials) {
+                                                               double* __restrict__ partials, int gx, int gy,
+                                                               int ntiles) {
   __shared__ double red[2][4];
-  const int mol = blockIdx.z;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  const int bx = tile % gx, by = (tile / gx) % gy, mol = tile / (gx * gy);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int H = g.r_hi - g.r_lo;
-  const int y0 = blockIdx.x * 256 + lane * 4;
+  const int y0 = bx * 256 + lane * 4;
   const bool col = y0 < g.C;
   const bool need_l = lane == 0 && col, need_r = col && (lane == 63 || y0 + 4 >= g.C);
   const int yl = y0 == 0 ? g.C - 1 : y0 - 1, yr = y0 + 4 >= g.C ? 0 : y0 + 4;
@@ -136,7 +142,7 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
   T* dst = out + (size_t)mol * plane;
   const float sc = scale ? scale[mol] : 1.0f;
   const float a = wa[mol], b = wb[mol];
-  const int o0 = (blockIdx.y * 4 + wv) * kVBand, o1 = min(H, o0 + kVBand);
+  const int o0 = (by * 4 + wv) * kVBand, o1 = min(H, o0 + kVBand);
 
   auto row_of = [&](int o) {
     int x = g.r_lo + o;
@@ -213,10 +219,12 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const size_t tiles = (size_t)gridDim.x * gridDim.y;
-    const size_t t = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    const size_t tiles = (size_t)gx * gy;
+    const size_t t = (size_t)by * gx + bx;
     partials[((size_t)mol * tiles + t) * 2] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
     partials[((size_t)mol * tiles + t) * 2 + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  }
+  __syncthreads();  // red is refilled by the next tile
   }
 }
 
@@ -392,6 +400,11 @@ static MGeom mgeom(int R, int C, int r_lo, int r_hi, int wrap) {
 
 static bool use_vec4(int C) { return C % 4 == 0; }
 
+// Blocks of the vector stencil launch (0: one per tile). 256 CUs x 6: one of the 7 workgroups of
+// 4 waves a CU holds at the stencil's register use stays free for the side stream.
+static int g_stencil_blocks = 256 * 6;
+void set_stencil_blocks(int n) { g_stencil_blocks = std::max(0, n); }
+
 size_t diffuse_partials_len(int m, int C, int H) {
   if (use_vec4(C)) return (size_t)cdiv(C, 256) * cdiv(cdiv(H, kVBand), 4) * m * 2;
   return (size_t)cdiv(C, 64 * kWaves) * cdiv(H, kBand) * m * 2;
@@ -407,9 +420,12 @@ void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_
   const bool v4 = use_vec4(C);
   const dim3 grid = v4 ? dim3(cdiv(C, 256), cdiv(cdiv(H, kVBand), 4), m) : dim3(cdiv(C, 64 * kWaves), cdiv(H, kBand), m);
   if (v4) {
-    MS_MAP_DISPATCH(dtype, (diffuse_stencil4_kernel<T><<<grid, 256, 0, st_>>>(
+    const int ntiles = (int)(grid.x * grid.y * grid.z);
+    const int blocks = g_stencil_blocks > 0 ? std::min(ntiles, g_stencil_blocks) : ntiles;
+    MS_MAP_DISPATCH(dtype, (diffuse_stencil4_kernel<T><<<blocks, 256, 0, st_>>>(
                                P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
-                               corr ? P_<float>(corr) : nullptr, g, P_<double>(partials))));
+                               corr ? P_<float>(corr) : nullptr, g, P_<double>(partials), (int)grid.x, (int)grid.y,
+                               ntiles)));
   } else {
     MS_MAP_DISPATCH(dtype, (diffuse_stencil_kernel<T><<<grid, 64 * kWaves, 0, st_>>>(
                                P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,

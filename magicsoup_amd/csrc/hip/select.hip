@@ -73,7 +73,7 @@ __global__ void __launch_bounds__(kSelThreads) select_write_kernel(long long n, 
                                                                    int64_t* rest, int32_t* host_out,
                                                                    long long* host64 = nullptr, int cap = -1,
                                                                    int* cap_gflags = nullptr,
-                                                                   int* cap_opflags = nullptr) {
+                                                                   int* cap_opflags = nullptr, int sub = 1) {
   constexpr int W = kSelThreads / 64;
   __shared__ long long s_red[W];
   __shared__ int s_wc[kSelItems][W];
@@ -82,7 +82,8 @@ __global__ void __launch_bounds__(kSelThreads) select_write_kernel(long long n, 
   const int b = blockIdx.x;
   // exclusive offset of this tile: sum of the preceding tiles' counts
   long long off = 0;
-  for (int q = threadIdx.x; q < b; q += kSelThreads) off += tile_count[q];
+  // (sub: the count pass wrote `sub` counts per tile, e.g. world.hip rec_slots_kernel)
+  for (int q = threadIdx.x; q < b * sub; q += kSelThreads) off += tile_count[q];
   for (int o = 32; o > 0; o >>= 1) off += __shfl_xor(off, o);
   if (lane == 0) s_red[w] = off;
   const long long base = (long long)b * kSelTile;
@@ -124,7 +125,7 @@ __global__ void __launch_bounds__(kSelThreads) select_write_kernel(long long n, 
     int total = (int)tile_off, m = 0;
     for (int j = 0; j < kSelItems; ++j)
       for (int q = 0; q < W; ++q) total += s_wc[j][q];
-    for (int q = 0; q < (int)gridDim.x; ++q) m = max(m, tile_max[q]);
+    for (int q = 0; q < (int)gridDim.x * sub; ++q) m = max(m, tile_max[q]);
     if (cap >= 0 && total > cap) {
       // capacity guard of a device-pipeline call (cap_skip semantics): the call becomes a no-op
       // that the host replays on the synchronous path, and the pending chain is broken
@@ -443,6 +444,31 @@ void select_indices_capped(long long n, int kind, uintptr_t src, uintptr_t sel, 
     default: throw std::invalid_argument("select_indices_capped: unsupported predicate");
   }
 #undef MS_SEL
+}
+
+// The tile buffers ({count, max} per tile, `tiles` entries each) for a caller whose own kernel
+// produces the selected counts of an int32 > 0 selection, `sub` per kSelTile items (world.hip
+// rec_slots), and the write pass of select_indices_capped over them.
+std::pair<int32_t*, int32_t*> select_tiles(long long tiles, hipStream_t s) {
+  if (tiles > g_tiles_cap) {
+    if (g_tiles) {
+      MS_HIP_CHECK(hipStreamSynchronize(s));
+      MS_HIP_CHECK(hipFree(g_tiles));
+    }
+    g_tiles_cap = std::max(tiles, 256ll);
+    MS_HIP_CHECK(hipMalloc((void**)&g_tiles, 2 * g_tiles_cap * sizeof(int32_t)));
+  }
+  return {g_tiles, g_tiles + g_tiles_cap};
+}
+
+void select_write_i32pos_capped(long long n, uintptr_t src, int32_t* tc, int32_t* tm, int sub, uintptr_t sel,
+                                uintptr_t out_dev, int cap, uintptr_t gflags, uintptr_t opflags, hipStream_t s) {
+  if (kSelTile % sub) throw std::invalid_argument("select_write_i32pos_capped: bad sub-tile count");
+  const long long tiles = (n + kSelTile - 1) / kSelTile;
+  select_write_kernel<kI32Pos><<<(unsigned)tiles, kSelThreads, 0, s>>>(
+      n, reinterpret_cast<const void*>(src), tc, tm, P_<int64_t>(sel), nullptr, P_<int32_t>(out_dev), nullptr, cap,
+      P_<int>(gflags), P_<int>(opflags), sub);
+  MS_LAUNCH_CHECK();
 }
 
 // A fresh pinned status slot: {device pointer of its 4 int64 words, slot index}.

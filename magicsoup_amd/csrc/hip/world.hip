@@ -440,6 +440,73 @@ __global__ void __launch_bounds__(256) neighbor_slots_kernel(int n, const int32_
   keys[t] = key;
 }
 
+// Neighbour slots fused with the recombination draws of the device pipeline (gp_recombine) and
+// the count pass of their selection: per tile of kSlotTile slots (16 per thread, the tiling of
+// select.hip), the key of slot t (as neighbor_slots_kernel), k[t] ~ Poisson(p * (len a + len b))
+// with the per-slot Philox stream of rec_count_keys_kernel (identical draws), and the tile's
+// number of slots with k > 0. One pass instead of three launches over the 8n slots; the write
+// pass (select.hip) follows. A chain already broken by a narrow arena (gflags width bit) draws
+// nothing and marks the call skipped, as gp_skip does.
+constexpr int kSlotItems = 4, kSlotBlock = 256 * kSlotItems;  // 1024 slots per block: a count per
+                                                                // quarter of select.hip's 4096-item tile
+__global__ void __launch_bounds__(256) rec_slots_kernel(int n, const int32_t* pos, Geom g, const int32_t* idx_map,
+                                                        const int32_t* lens, double p, uint64_t seed, uint64_t call,
+                                                        int kcap, const int* gflags, int* opflags, int64_t* keys,
+                                                        int32_t* kout, int32_t* tile_count, int32_t* tile_max) {
+  const bool skip = gflags && (*gflags & 8);  // mutations.hip kGpWidth
+  if (skip && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(opflags, 16);  // kGpSkipped
+  const long long base = (long long)blockIdx.x * kSlotBlock, total = 8LL * n;
+  // the items' dependent random loads (position -> neighbour pixel -> index map -> its position
+  // -> genome lengths) are issued item-parallel, so a thread has all its chains in flight at once
+  long long px[kSlotItems];
+  int o[kSlotItems];
+#pragma unroll
+  for (int j = 0; j < kSlotItems; ++j) {
+    const long long t = base + j * 256 + threadIdx.x;
+    px[j] = -1;
+    if (t < total) {
+      const int c = (int)(t >> 3), q = (int)(t & 7);
+      long long nb[8];
+      const int nn = moore(pos[2 * c], pos[2 * c + 1], g, nb);
+      if (q < nn) px[j] = nb[q];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kSlotItems; ++j) o[j] = px[j] >= 0 ? idx_map[px[j]] : -1;
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < kSlotItems; ++j) {
+    const long long t = base + j * 256 + threadIdx.x;
+    if (t >= total) continue;
+    const int c = (int)(t >> 3);
+    int oo = o[j];
+    if (oo < 0 || oo >= n || ((long long)pos[2 * oo] * g.C + pos[2 * oo + 1]) != px[j]) oo = -1;  // cell_at
+    int64_t key = -1;
+    int kk = 0;
+    if (oo > c) {
+      key = ((int64_t)c << 32) | oo;
+      const int L = lens[c] + lens[oo];
+      if (!skip && L >= 1) {
+        Philox rng(seed, call, (uint32_t)t);
+        long long x = poisson(rng, p * (double)L);
+        if (kcap > 0 && x > kcap) x = kcap;
+        kk = (int)(x > L ? L : x);
+      }
+    }
+    keys[t] = key;
+    kout[t] = kk;
+    cnt += kk > 0;
+  }
+  __shared__ int s_cnt[4];
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    tile_count[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    tile_max[blockIdx.x] = 0;
+  }
+}
+
 // ---------------------------------------------------------------- host launchers
 static Geom geom(int R, int C, int r_lo, int r_hi, int wrap) {
   if (R <= 0 || C <= 0 || r_lo < 0 || r_hi > R || r_lo >= r_hi) throw std::invalid_argument("bad map geometry");
@@ -590,6 +657,30 @@ void neighbor_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int 
   neighbor_slots_kernel<<<cdiv(8LL * n, 256), 256, 0, S_(stream)>>>(n, P_<int32_t>(pos), g, P_<int32_t>(idx_map),
                                                                P_<int64_t>(keys));
   MS_LAUNCH_CHECK();
+}
+
+std::pair<int32_t*, int32_t*> select_tiles(long long tiles, hipStream_t s);
+void select_write_i32pos_capped(long long n, uintptr_t src, int32_t* tc, int32_t* tm, int sub, uintptr_t sel,
+                                uintptr_t out_dev, int cap, uintptr_t gflags, uintptr_t opflags, hipStream_t s);
+
+// rec_slots_kernel + the capped selection of slots with k > 0 into sel / out_dev (gp_recombine)
+void rec_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map, uintptr_t lens,
+               double p, uint64_t seed, uint64_t call, int kcap, uintptr_t gflags, uintptr_t opflags, uintptr_t keys,
+               uintptr_t k, uintptr_t sel, uintptr_t out_dev, int cap, uintptr_t stream) {
+  if (n <= 0) throw std::invalid_argument("rec_slots: no cells");
+  const Geom g = geom(R, C, r_lo, r_hi, wrap);
+  hipStream_t s = S_(stream);
+  const long long total = 8LL * n;
+  constexpr int kSelTile = 4096;  // select.hip
+  const long long blocks = (total + kSelTile - 1) / kSelTile * (kSelTile / kSlotBlock);
+  auto tiles = select_tiles(blocks, s);
+  // (the blocks past the last slot write zero counts: the write pass reads whole tiles' counts)
+  rec_slots_kernel<<<(unsigned)blocks, 256, 0, s>>>(n, P_<int32_t>(pos), g, P_<int32_t>(idx_map), P_<int32_t>(lens), p,
+                                                    seed, call, kcap, P_<int>(gflags), P_<int>(opflags),
+                                                    P_<int64_t>(keys), P_<int32_t>(k), tiles.first, tiles.second);
+  MS_LAUNCH_CHECK();
+  select_write_i32pos_capped(total, k, tiles.first, tiles.second, kSelTile / kSlotBlock, sel, out_dev, cap, gflags,
+                             opflags, s);
 }
 
 void neighbor_pairs(int nf, int n, uintptr_t from, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map,

@@ -284,7 +284,7 @@ def recombinate_all(world, p: float, extra=None) -> bool:
     pcap = _cap(expected, min(n, N_CAP) // 2)  # pairs per call (two results each)
     b = _begin(world, "rec")
     sc = _scratch(world)
-    keys = hip_ops.neighbor_slot_keys(world)
+    keys, nbr = hip_ops.neighbor_slot_args(world)
     k = _kin_desc(world, dev)
     xr = 0 if extra is None else int(extra.rows)
     nbytes = _m().gp_blob_bytes(1, n, pcap, k.P, L, D_CAP, K_CAP, xr)
@@ -296,7 +296,7 @@ def recombinate_all(world, p: float, extra=None) -> bool:
     gen = sc.bufs["arena_gen"] = sc.bufs.get("arena_gen", 0) + 1
     nres = sc.get("gp_nres", 1, torch.int32, dev) if extra is not None else None
     seed, call = _rng()
-    slot = _m().gp_recombine(_arena_desc(world, b), _gen_desc(world, dev), k, _p(keys), float(p), seed, call, pcap,
+    slot = _m().gp_recombine(_arena_desc(world, b), _gen_desc(world, dev), k, _p(keys), nbr, float(p), seed, call, pcap,
                              K_CAP, D_CAP, _p(mark), int(gen), extra, _p(nres), _p(blob), _stream())
     lay = _m().gp_layout(1, n, pcap, L, K_CAP, xr)
     nr = lay["nr"]

@@ -824,6 +824,21 @@ def neighbor_slot_keys(world) -> torch.Tensor:
     return keys
 
 
+def neighbor_slot_args(world):
+    """The index map of the current positions plus the buffers / arguments of the fused neighbour
+    slot pass of the device pipeline (gp.hip gp_recombine -> world.hip rec_slots): the slot keys
+    buffer (8n int64, written there) and (positions, R, C, r_lo, r_hi, wrap, index map)."""
+    R, C, r_lo, r_hi, wrap = geom(world)
+    dev = world._genomes.data.device
+    n = world.n_cells
+    _ensure_world_layout(world)
+    pos = world.cell_positions
+    idx_map = _index_map(world, R * C, dev)
+    _m().index_map(n, _p(pos), C, _p(idx_map), False, _stream())
+    keys = _scratch(world).get("nb_keys", 8 * n, torch.int64, dev)
+    return keys, (_p(pos), R, C, r_lo, r_hi, wrap, _p(idx_map))
+
+
 def _rec_apply(world, pairs, keys, k: torch.Tensor, tot: torch.Tensor, seed: int, call: int) -> torch.Tensor:
     """Recombine the selected pairs (``pairs`` int32 (n, 2) or slot ``keys`` int64 (a << 32) | b)
     and commit both results of every pair; a cell in several pairs keeps its last pair's result.

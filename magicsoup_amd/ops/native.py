@@ -57,6 +57,9 @@ def hip():
         mod.set_place_mode(int(os.environ["MS_PLACE_MODE"]))  # type: ignore[attr-defined]
     if fresh and os.environ.get("MS_COOP_BLOCKS"):
         mod.set_coop_blocks(int(os.environ["MS_COOP_BLOCKS"]))  # type: ignore[attr-defined]
+    if fresh and os.environ.get("MS_STENCIL_BLOCKS"):
+        # blocks of the diffusion stencil launch (maps.hip; 0: one per tile)
+        mod.set_stencil_blocks(int(os.environ["MS_STENCIL_BLOCKS"]))  # type: ignore[attr-defined]
     return mod
 
 
