@@ -400,9 +400,12 @@ static MGeom mgeom(int R, int C, int r_lo, int r_hi, int wrap) {
 
 static bool use_vec4(int C) { return C % 4 == 0; }
 
-// Blocks of the vector stencil launch (0: one per tile). 256 CUs x 6: one of the 7 workgroups of
-// 4 waves a CU holds at the stencil's register use stays free for the side stream.
-static int g_stencil_blocks = 256 * 6;
+// Blocks of the vector stencil launch (0: one per tile). 256 CUs x 4 workgroups (4 waves per SIMD)
+// still reach the stencil's full HBM rate and leave 3 of the 7 slots a CU holds at its register use
+// to the side stream. Kernel traces of the flagship step (scripts/gpu_trace_step.sh): stencil 378 /
+// side chain done 100 us after it at 1024 blocks; 385 / 125-166 at one block per tile; 375 / 153-167
+// at 1536; 427 / 75 at 896; 500 / done before it at 512.
+static int g_stencil_blocks = 256 * 4;
 void set_stencil_blocks(int n) { g_stencil_blocks = std::max(0, n); }
 
 size_t diffuse_partials_len(int m, int C, int H) {

@@ -5,9 +5,9 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export PYTHONPATH=$PWD TMPDIR=/tmp
-O=gpurun_out/ts; rm -rf $O; mkdir -p $O
+O=${TS_OUT:-gpurun_out/ts}; rm -rf $O; mkdir -p $O
 timeout -k 10 300 rocprofv3 --kernel-trace -d $O/trace -o run --output-format csv -- \
   python bench.py --steps 20 --warmup 20 ${BENCH_ARGS:-} > $O/trace.log 2>&1
 python scripts/step_kernels.py $O/trace/run_kernel_trace.csv 19 > $O/step_kernels.txt 2>&1
-head -3 $O/step_kernels.txt
+head -6 $O/step_kernels.txt
 exit 0

@@ -28,6 +28,21 @@ print(f"step walls (us): median {statistics.median(w for w, _ in walls) / 1e3:.1
 j = med[1]
 one = rows[marks[j - 1] + 1 : marks[j] + 1]
 base = int(rows[marks[j - 1]]["End_Timestamp"])
+# per queue over the timed steps: median (first start, last end, busy) relative to the step start
+per_q = {}
+for jj in range(len(marks) - nst, len(marks)):
+    b0 = int(rows[marks[jj - 1]]["End_Timestamp"])
+    qs = {}
+    for r in rows[marks[jj - 1] + 1 : marks[jj] + 1]:
+        s, e = int(r["Start_Timestamp"]) - b0, int(r["End_Timestamp"]) - b0
+        f, l, bz = qs.get(r.get("Queue_Id", "?"), (s, e, 0))
+        qs[r.get("Queue_Id", "?")] = (min(f, s), max(l, e), bz + e - s)
+    for q, v in qs.items():
+        per_q.setdefault(q, []).append(v)
+for q, vs in sorted(per_q.items()):
+    med3 = [statistics.median(v[i] for v in vs) / 1e3 for i in range(3)]
+    print(f"queue {q}: median first start {med3[0]:8.1f}, last end {med3[1]:8.1f}, busy {med3[2]:7.1f} us "
+          f"({len(vs)} steps)")
 last = {}
 for r in one:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
