@@ -726,10 +726,12 @@ def test_parameter_rows_follow_genomes_through_bench_steps(monkeypatch, recycle)
     atp = CHEMISTRY.molname_2_idx["ATP"]
     w = _world("cuda", map_size=128, n=3000, s=500)
     for i in range(8):
-        if recycle and i == 4:
+        if recycle and i >= 4:
+            # every fresh row taken (again each step: a widening of the protein dimension in
+            # between re-packs the storage densely with fresh spare rows)
             w._reconcile()
             kin = w.kinetics
-            kin.__dict__["_nrows"] = kin._row_limit()[0]  # every fresh row taken
+            kin.__dict__["_nrows"] = kin._row_limit()[0]
         bench.step(w, 3000, 500, atp)
         w.mutate_cells(p=1e-4)
         w.recombinate_cells(p=1e-5)
