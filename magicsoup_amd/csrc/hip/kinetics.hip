@@ -26,13 +26,15 @@ namespace msd {
 constexpr int kBlock = 256;
 constexpr int kNarrowP = 12;  // LDS protein slots of the narrow integrator launch
 constexpr int kWideBlocksPerCU = 2;  // resident blocks per CU of the strided wide launch
+constexpr int kMaxParts = 4;  // speculative mode: 4 parts x 4 iterations in one 16-bit flag set
 // binned launch mode (set_integrate_mode, for A/B on one state: scripts/integrator_bench.py):
 // bit 0: the wide launch on a side stream next to the narrow one (else serial, wide first); bit 1:
 // the wide bin on a small strided grid (else a full grid); bit 2: 16-lane groups for the narrow
 // launch. Measured at 4096^2 / 50k (3 parts, 4 iterations): serial 532 us, concurrent 558 us,
 // 16-lane 590 us -- the kernel is VALU-throughput bound (37M wave instructions per launch, ~60 %
 // of the SIMDs' issue capacity), so overlapping the bins only adds contention. Serial is default.
-// bit 3: legacy LDS-staged path; bit 4: register path with cells sorted by active-protein count.
+// bit 3: legacy LDS-staged path; bit 4: register path with cells sorted by active-protein count;
+// bits 5 / 6: see the launcher; bit 7: no speculative all-parts launch (any of bits 3-7 disables it).
 static int g_integrate_mode = 0;
 void set_integrate_mode(int mode) { g_integrate_mode = mode; }
 
@@ -54,7 +56,33 @@ struct IntegrateArgs {
   const int32_t* list;        // item -> cell (nullptr: identity)
   const int32_t* count;       // number of items in `list` (device)
   int Ps;                     // LDS protein capacity of a slot (>= active proteins of listed cells)
+  // Speculative all-parts mode of the register path (spec_parts > 0, see integrate()): part p + 1
+  // starts from part p's last candidate, i.e. it assumes the reference's global loop ran all n_iters
+  // iterations of every part; part p's bits go to bit 4p + it of the speculative flag words, the
+  // final state to slot n_iters of snap_out, and no other candidate is stored.
+  int spec_parts;
+  float trims[kMaxParts];
+  int prelisted;              // cells with more than G active proteins are on another list: skip them
+  int32_t* ovf_list;          // cells whose non-zeros / exponents do not fit this launch go here ...
+  int32_t* ovf_count;
+  unsigned* unfit;            // ... or, without a list, set this flag (the speculation is void)
+  // LDS-path fallback launches: return at once when the speculation held (flags spec_check[0 ..
+  // 4 * spec_n) all set up to n_iters, unfit word spec_check[4 * spec_n] clear); the last part's
+  // launch then copies the speculative flags over the regular ones (the write-back reads those)
+  const unsigned* spec_check;
+  int spec_n;
+  unsigned* copy_to;
 };
+
+// Did the speculative all-parts launch hold? (every part ran all n_iters iterations and every cell
+// was integrated)
+__device__ __forceinline__ bool spec_held(const unsigned* w, int nparts, int n_iters) {
+  if (w[ms::kEqIters * nparts]) return false;
+  for (int p = 0; p < nparts; ++p)
+    for (int it = 0; it < n_iters; ++it)
+      if (!w[ms::kEqIters * p + it]) return false;
+  return true;
+}
 
 __device__ __forceinline__ int stop_iter(const unsigned* flags, int n_iters) {
   for (int it = 0; it < n_iters; ++it)
@@ -71,6 +99,23 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// OR the "still correcting" bits (bit b -> flag word b: 4 per part) wave -> block -> at most one
+// atomic per block and bit, skipped once the flag is set (tens of thousands of same-address atomics
+// would serialise in one L2 channel)
+__device__ __forceinline__ void or_block_bits(unsigned bits, unsigned* mask_out) {
+  __shared__ unsigned wave_bits[kBlock / 64];
+  for (int o = 32; o > 0; o >>= 1) bits |= __shfl_xor(bits, o);
+  if ((threadIdx.x & 63) == 0) wave_bits[threadIdx.x >> 6] = bits;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned b = 0u;
+    for (int w = 0; w < (int)(blockDim.x + 63) / 64; ++w) b |= wave_bits[w];
+    for (int i = 0; i < ms::kEqIters * kMaxParts; ++i)
+      if ((b & (1u << i)) && __hip_atomic_load(mask_out + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+        atomicOr(mask_out + i, 1u);
+  }
 }
 
 // One cell (list item `item`) per G-lane group; ORs the cell's "still correcting" bits into `bits`.
@@ -270,6 +315,7 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
   const int gbase8 = (threadIdx.x & 63) - lane;  // first lane of this group inside the wave
   for (int it = 0; it < a.n_iters; ++it, inc *= 0.5f) {
     bool changed = false;
+    bool cb = false;  // this cell has an impactful correction at iteration it
     for (int k = lane; k < na; k += G) {
       const int* wr = words + k * SP;
       const uint8_t* nz = nzj + k * s;
@@ -301,7 +347,10 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
       if (fwd && f0 == 1.0f) low = false;
       bool high = fwd ? (qke > ms::kUpper) : (qke < ms::kLower);
       if (!fwd && f0 == 0.0f) high = false;
-      if ((low || high) && imp) bits |= 1u << it;
+      if ((low || high) && imp) {
+        bits |= 1u << it;
+        cb = true;
+      }
       float f = f0;
       if (high) f -= inc;
       if (low) f += inc;
@@ -313,12 +362,17 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
     {
       // per-cell fixed point: with no factor changed, this and every later iteration reproduce the
       // current state bit for bit (same F, same X, same decisions), so the remaining candidates are
-      // copies of it and the iterations are skipped
+      // copies of it and the iterations are skipped. The later iterations would also repeat this
+      // one's decisions, so an impactful correction that changed nothing (a backward reaction whose
+      // factor is capped at 1) keeps the reference's global loop running: its bit is carried forward.
       const unsigned long long bal = __ballot(changed);
       unsigned long long gm;
       if constexpr (G == 64) gm = bal;
       else gm = (bal >> gbase8) & ((1ull << G) - 1ull);
       if (gm == 0ull) {
+        unsigned long long cgm = __ballot(cb);
+        if constexpr (G != 64) cgm = (cgm >> gbase8) & ((1ull << G) - 1ull);
+        if (cgm) bits |= ((1u << a.n_iters) - 1u) & ~((2u << it) - 1u);
         for (int it2 = it + 1; it2 <= a.n_iters; ++it2) {
           float* sn2 = snap + (size_t)it2 * s;
           for (int j = lane; j < s; j += G)
@@ -348,6 +402,12 @@ template <int G, bool kStride>
 __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
   const int cps = blockDim.x / G, slot = threadIdx.x / G;
+  if (a.spec_check && spec_held(a.spec_check, a.spec_n, a.n_iters)) {
+    // the speculative launch held: nothing to redo (the last part hands its flags over)
+    if (a.copy_to && blockIdx.x == 0 && (int)threadIdx.x < ms::kEqIters * a.spec_n)
+      a.copy_to[threadIdx.x] = a.spec_check[threadIdx.x];
+    return;
+  }
   unsigned bits = 0u;
   if constexpr (kStride) {
     const int limit = a.list ? *a.count : a.c;
@@ -359,20 +419,8 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
     integrate_item<G>(a, smem, (int)blockIdx.x * cps + slot, bits);
   }
 
-  // ---- 9. OR the "still correcting" bits: wave -> block -> at most one atomic per block and bit,
-  //         skipped once the flag is set (tens of thousands of same-address atomics would serialise
-  //         in one L2 channel)
-  __shared__ unsigned wave_bits[kBlock / 64];
-  for (int o = 32; o > 0; o >>= 1) bits |= __shfl_xor(bits, o);
-  if ((threadIdx.x & 63) == 0) wave_bits[threadIdx.x >> 6] = bits;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned b = 0u;
-    for (int w = 0; w < (int)(blockDim.x + 63) / 64; ++w) b |= wave_bits[w];
-    for (int it = 0; it < ms::kEqIters; ++it)
-      if ((b & (1u << it)) && __hip_atomic_load(a.mask_out + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-        atomicOr(a.mask_out + it, 1u);
-  }
+  // ---- 9. OR the "still correcting" bits
+  or_block_bits(bits, a.mask_out);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -421,7 +469,7 @@ __device__ __forceinline__ float ipow_small(float x, int n) {
   return n < 0 ? 1.0f / r : r;
 }
 
-template <int G, int NZ>
+template <int G, int NZ, bool kSpec = false>
 __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int* smem, int item, unsigned& bits,
                                                     int32_t* wide_list, int32_t* wide_count) {
   const int slot = threadIdx.x / G, lane = threadIdx.x % G;
@@ -445,13 +493,17 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   }
 
   // ---- 2. active proteins (Vmax' != 0, NaN included) in ascending order
+  constexpr bool spec = kSpec;
+  const int nparts = spec ? a.spec_parts : 1;
   int na = 0;
+  bool trim_diff = false;  // speculative mode: every part must see the same active set
   for (int p0 = 0; p0 < P; p0 += G) {
     const int p = p0 + lane;
     float vmax = 0.0f;
     if (listed && p < P) vmax = a.Q[prow * P + p].x;
-    const float vm = vmax * a.trim;
+    const float vm = vmax * (spec ? a.trims[0] : a.trim);
     const bool on = listed && p < P && !(vm <= 0.0f);
+    for (int q = 1; q < nparts; ++q) trim_diff |= on != (listed && p < P && !(vmax * a.trims[q] <= 0.0f));
     const unsigned long long gm = group_ballot<G>(on);
     const int k = na + __popcll(gm & ((1ull << lane) - 1ull));
     if (on && k < G) act[k] = p;
@@ -493,8 +545,26 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
       wide_ok &= __popcll(gm) <= NZ && w_nf(w[u]) < 32 && w_nb(w[u]) < 32;
     }
   }
-  fits = fits && group_ballot<G>(!wide_ok) == 0ull;
-  if (listed && !fits && lane == 0 && wide_list) wide_list[atomicAdd(wide_count, 1)] = cell;
+  const bool nz_ok = group_ballot<G>(!wide_ok) == 0ull;
+  if (!spec) {
+    fits = fits && nz_ok;
+    if (listed && !fits && lane == 0 && wide_list) wide_list[atomicAdd(wide_count, 1)] = cell;
+  } else if (listed && lane == 0) {
+    // too many active proteins: on the wide list already (prelisted) or the speculation is void;
+    // too many non-zeros / large exponents: the overflow list, else void; so is a cell whose active
+    // set differs between parts (a Vmax' underflowing to 0)
+    if (!fits) {
+      if (!a.prelisted) __hip_atomic_store(a.unfit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (!nz_ok) {
+      if (a.ovf_list) a.ovf_list[atomicAdd(a.ovf_count, 1)] = cell;
+      else __hip_atomic_store(a.unfit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (spec) {
+    if (listed && group_ballot<G>(trim_diff) != 0ull && lane == 0)
+      __hip_atomic_store(a.unfit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fits = fits && nz_ok;
+  }
   const bool valid = listed && fits;
   const bool sig = valid && lane < s;
   const bool prot = valid && lane < na;
@@ -503,7 +573,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
 
   // protein lane: constants, and its non-zeros as 16-bit (signal, nf, nb) registers for the
   // damping iterations (velocity and limiting factor read the full words from LDS once per part)
-  float vmx = 0.0f, kmf = 1.0f, kmb = 1.0f, ke = 1.0f;
+  float vraw = 0.0f, kmf = 1.0f, kmb = 1.0f, ke = 1.0f;
   int pk = 0, cnt = 0;
   int e16[NZ / 2];
 #pragma unroll
@@ -512,8 +582,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   if (prot) {
     pk = act[lane];
     const float4 q4 = a.Q[prow * P + pk];
-    const float vm = q4.x * a.trim;
-    vmx = vm > 0.0f || vm != vm ? vm : 0.0f;
+    vraw = q4.x;
     kmf = q4.y;
     kmb = q4.z;
     ke = q4.w;
@@ -550,6 +619,13 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     }
   };
 
+  // parts: one (the launch's trim), or all of them in the speculative mode; x0 / Xs carry the state
+  float* snap = a.snap_out + (size_t)(valid ? cell : 0) * ms::kSnap * s;
+  float xc = x0;
+  for (int part = 0; part < nparts; ++part) {
+  const float vm = vraw * (spec ? a.trims[part] : a.trim);
+  const float vmx = prot && (vm > 0.0f || vm != vm) ? vm : 0.0f;
+  const int bsh = spec ? ms::kEqIters * part : 0;  // this part's bits
   // ---- 4. velocity (protein lane; entries past the count are zero words: no effect)
   float v = 0.0f;
   {
@@ -627,7 +703,6 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   wave_lds_sync();
 
   // ---- 7. candidate 0 (signal lane)
-  float* snap = a.snap_out + (size_t)(valid ? cell : 0) * ms::kSnap * s;
   auto advance = [&]() -> float {  // X0 + sum_k n_k * pub_k (ascending k), clamped at 0
     float x = x0;
     signal_pass([&](int n, float b) {
@@ -635,15 +710,15 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     });
     return x < 0.0f ? 0.0f : x;
   };
-  float xc = advance();
-  if (sig) snap[lane] = xc;
+  xc = advance();
+  if (sig && !spec) snap[lane] = xc;
   Xs[lane] = xc;
   wave_lds_sync();
 
   // ---- 8. equilibrium damping trajectory
   float inc = 0.5f;
   for (int it = 0; it < a.n_iters; ++it, inc *= 0.5f) {
-    bool changed = false;
+    bool changed = false, cb = false;
     {
       float pf = 1.0f, pb = 1.0f;
       int nfs = 0, nbs = 0;
@@ -671,7 +746,8 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
         if (fwd && f0 == 1.0f) low = false;
         bool high = fwd ? (qke > ms::kUpper) : (qke < ms::kLower);
         if (!fwd && f0 == 0.0f) high = false;
-        if ((low || high) && imp) bits |= 1u << it;
+        cb = (low || high) && imp;
+        if (cb) bits |= 1u << (bsh + it);
         float f = f0;
         if (high) f -= inc;
         if (low) f += inc;
@@ -681,26 +757,32 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
       }
     }
     if (group_ballot<G>(changed) == 0ull) {
-      // per-cell fixed point (see integrate_item): the remaining candidates are copies
-      for (int it2 = it + 1; it2 <= a.n_iters; ++it2)
-        if (sig) snap[(size_t)it2 * s + lane] = xc;
+      // per-cell fixed point (see integrate_item): the remaining candidates are copies, and an
+      // impactful correction that changed nothing repeats in every remaining iteration
+      if (group_ballot<G>(cb) != 0ull) bits |= (((1u << a.n_iters) - 1u) & ~((2u << it) - 1u)) << bsh;
+      if (!spec)
+        for (int it2 = it + 1; it2 <= a.n_iters; ++it2)
+          if (sig) snap[(size_t)it2 * s + lane] = xc;
       break;
     }
     pub[lane] = va * F;
     wave_lds_sync();  // the protein lanes of this wave finished reading Xs, published Va * F
     xc = advance();
-    if (sig) snap[(size_t)(it + 1) * s + lane] = xc;
+    if (sig && !spec) snap[(size_t)(it + 1) * s + lane] = xc;
     Xs[lane] = xc;
     wave_lds_sync();
   }
+  x0 = xc;  // the next part starts from this part's last candidate (Xs holds it already)
+  }
+  if (spec && sig) snap[(size_t)a.n_iters * s + lane] = xc;
 #undef MS_E
 }
 
 // kStrided: a list launch of unknown length (a.count on the device) on a small grid; each block
 // walks the list in steps of the whole grid (the bound is block-uniform, so every wave runs the
 // same number of items and the wave-wide ballots / reductions inside stay convergent)
-template <int G, int NZ, bool kStrided>
-__global__ void __launch_bounds__(kBlock) integrate_fast_kernel(IntegrateArgs a, int32_t* wide_list,
+template <int G, int NZ, bool kStrided, bool kSpec = false>
+__global__ void __launch_bounds__(kBlock, G == 32 ? 6 : (NZ == kNzReg ? 4 : 1)) integrate_fast_kernel(IntegrateArgs a, int32_t* wide_list,
                                                                 int32_t* wide_count) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
   unsigned bits = 0u;
@@ -709,22 +791,13 @@ __global__ void __launch_bounds__(kBlock) integrate_fast_kernel(IntegrateArgs a,
     const int n = *a.count;
     for (int base = (int)blockIdx.x * cpb; base < n; base += (int)gridDim.x * cpb) {
       wave_lds_sync();  // the previous item's LDS reads are done before its slot is refilled
-      integrate_item_fast<G, NZ>(a, smem, base + (int)threadIdx.x / G, bits, wide_list, wide_count);
+      integrate_item_fast<G, NZ, kSpec>(a, smem, base + (int)threadIdx.x / G, bits, wide_list, wide_count);
     }
   } else {
-    integrate_item_fast<G, NZ>(a, smem, (int)blockIdx.x * cpb + (int)threadIdx.x / G, bits, wide_list, wide_count);
+    integrate_item_fast<G, NZ, kSpec>(a, smem, (int)blockIdx.x * cpb + (int)threadIdx.x / G, bits, wide_list,
+                                      wide_count);
   }
-  __shared__ unsigned wave_bits[kBlock / 64];
-  for (int o = 32; o > 0; o >>= 1) bits |= __shfl_xor(bits, o);
-  if ((threadIdx.x & 63) == 0) wave_bits[threadIdx.x >> 6] = bits;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned b = 0u;
-    for (int w = 0; w < (int)(blockDim.x + 63) / 64; ++w) b |= wave_bits[w];
-    for (int it = 0; it < ms::kEqIters; ++it)
-      if ((b & (1u << it)) && __hip_atomic_load(a.mask_out + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-        atomicOr(a.mask_out + it, 1u);
-  }
+  or_block_bits(bits, a.mask_out);
 }
 
 // Parts >= 1 of the register path with the wide list (known from part 0) in the same launch: the
@@ -733,7 +806,7 @@ __global__ void __launch_bounds__(kBlock) integrate_fast_kernel(IntegrateArgs a,
 // A wide cell's integration is a long dependency chain (~30 us on its own); at the front of the
 // grid it runs under the narrow blocks instead of after them. Cells that do not fit the 64-lane
 // slots either are skipped here (part 0 listed them for the LDS launch).
-template <int G>
+template <int G, bool kSpec = false>
 __global__ void __launch_bounds__(kBlock, 6) integrate_fused_kernel(IntegrateArgs a, IntegrateArgs aw, int nwb) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
   static_assert(2 * fast_slot_words<64, kNzWide>() <= (kBlock / G) * fast_slot_words<G, kNzReg>(),
@@ -744,24 +817,14 @@ __global__ void __launch_bounds__(kBlock, 6) integrate_fused_kernel(IntegrateArg
       const int n = *aw.count;  // block-uniform bound: both waves run the same number of items
       for (int base = (int)blockIdx.x * 2; base < n; base += nwb * 2) {
         wave_lds_sync();
-        integrate_item_fast<64, kNzWide>(aw, smem, base + (int)threadIdx.x / 64, bits, nullptr, nullptr);
+        integrate_item_fast<64, kNzWide, kSpec>(aw, smem, base + (int)threadIdx.x / 64, bits, nullptr, nullptr);
       }
     }
   } else {
-    integrate_item_fast<G, kNzReg>(a, smem, ((int)blockIdx.x - nwb) * (kBlock / G) + (int)threadIdx.x / G, bits,
+    integrate_item_fast<G, kNzReg, kSpec>(a, smem, ((int)blockIdx.x - nwb) * (kBlock / G) + (int)threadIdx.x / G, bits,
                                    nullptr, nullptr);
   }
-  __shared__ unsigned wave_bits[kBlock / 64];
-  for (int o = 32; o > 0; o >>= 1) bits |= __shfl_xor(bits, o);
-  if ((threadIdx.x & 63) == 0) wave_bits[threadIdx.x >> 6] = bits;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned b = 0u;
-    for (int w = 0; w < kBlock / 64; ++w) b |= wave_bits[w];
-    for (int it = 0; it < ms::kEqIters; ++it)
-      if ((b & (1u << it)) && __hip_atomic_load(a.mask_out + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-        atomicOr(a.mask_out + it, 1u);
-  }
+  or_block_bits(bits, a.mask_out);
 }
 
 // Split the cells by their number of active proteins (Vmax > 0 or NaN; the same set for every part
@@ -784,8 +847,9 @@ __global__ void __launch_bounds__(kBlock) integrate_scatter_kernel(int c, int s,
                                                                    const unsigned* mask, int n_iters,
                                                                    const int32_t* positions, float* cell_mols,
                                                                    void* molmap, int map_dtype, const float* corr,
-                                                                   float* X_out) {
+                                                                   float* X_out, unsigned* reset) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (reset && t == 0) reset[0] = 0u;  // the speculative path's wide-list count, for the next call
   if (t >= (long long)c * s) return;
   const int cell = (int)(t / s), j = (int)(t - (long long)cell * s);
   const int k = stop_iter(mask, n_iters);
@@ -887,6 +951,45 @@ __global__ void __launch_bounds__(kBlock) gather_x_kernel(int c, int s, int m, i
     x = corr_in(ld_map(molmap, (size_t)(j - m) * R * C + pix, map_dtype), corr, j - m);
   }
   snap[(size_t)cell * ms::kSnap * s + j] = x;
+}
+
+// Input of the speculative all-parts path (s <= 32): X (the explicit X, or gathered from the world
+// like gather_x_kernel) -> candidate 0 of `snap`, one 32-lane group per cell; the cells with more
+// than 32 active proteins go to the wide list (count wide[0], zero on entry: the write-back kernel
+// resets it) for the front blocks of the speculative launch. Block 0 clears the launch's flag words
+// and the speculative flags + unfit word (wide[4 ..]).
+__global__ void __launch_bounds__(kBlock) gather_bin_kernel(int c, int s, int m, int R, int C, int P,
+                                                            const float* X, const float* cell_mols,
+                                                            const void* molmap, int map_dtype, const float* corr,
+                                                            const int32_t* positions, const float4* Q,
+                                                            const int64_t* prow, float trim0, float* snap,
+                                                            int32_t* wide_list, unsigned* wide, unsigned* zero,
+                                                            int nz, int32_t* zero_wc) {
+  clear_words(zero, nz, zero_wc);
+  if (blockIdx.x == 0 && threadIdx.x < ms::kEqIters * kMaxParts + 1) wide[4 + threadIdx.x] = 0u;
+  const int lane = threadIdx.x & 31;
+  const int cell = (int)blockIdx.x * (kBlock / 32) + (int)threadIdx.x / 32;
+  const bool ok = cell < c;
+  if (ok && lane < s) {
+    float x;
+    if (X) {
+      x = X[(size_t)cell * s + lane];
+    } else if (lane < m) {
+      x = cell_mols[(size_t)cell * m + lane];
+    } else {
+      const size_t pix = (size_t)positions[2 * cell] * C + positions[2 * cell + 1];
+      x = corr_in(ld_map(molmap, (size_t)(lane - m) * R * C + pix, map_dtype), corr, lane - m);
+    }
+    snap[(size_t)cell * ms::kSnap * s + lane] = x;
+  }
+  const size_t r = ok ? (prow ? (size_t)prow[cell] : (size_t)cell) : 0;
+  int na = 0;
+  for (int p0 = 0; p0 < P; p0 += 32) {
+    const int p = p0 + lane;
+    const bool on = ok && p < P && !(Q[r * P + p].x * trim0 <= 0.0f);
+    na += __popcll(group_ballot<32>(on));
+  }
+  if (ok && lane == 0 && na > 32) wide_list[atomicAdd(reinterpret_cast<int*>(wide), 1)] = cell;
 }
 
 __device__ __forceinline__ int pack_word(int n, int nf, int nb, int av, int* overflow) {
@@ -1050,7 +1153,8 @@ static int slot_words_for(int P, int s, int sp) {
 void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q, uintptr_t Kmr, uintptr_t cell_mols,
                uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
                uintptr_t masks, const std::vector<float>& trims, int n_iters, int part_begin, int part_end,
-               bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t map_corr, uintptr_t stream) {
+               bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t map_corr, uintptr_t spec_buf,
+               uintptr_t stream) {
   if (c <= 0) return;
   const float* corr = map_corr ? P_<float>(map_corr) : nullptr;
   if (n_iters < 0 || n_iters > ms::kEqIters) throw std::invalid_argument("n_iters must be in 0..4");
@@ -1061,7 +1165,101 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
   unsigned* zero_flags = mk + ms::kEqIters * nparts;
   float* snaps[2] = {P_<float>(snap_a), P_<float>(snap_b)};
   const bool fast_path = lists != 0 && s <= 64 && (g_integrate_mode & 8) == 0;
-  if (part_begin == 0) {
+  // Speculative all-parts path (s <= 32, the whole part range with the write-back, mode bits 3-7
+  // clear): the reference's global exit (kinetics.py:846) cuts a part short only when no cell of the
+  // whole population still has an impactful correction, which never happened in 40-step runs of any
+  // BASELINE config (scripts/spec_rate.py: all 3 parts at 4 iterations in every step at 10k-50k
+  // cells; a 500-cell world ends early in about half the steps). So every cell runs all parts in one
+  // launch, each part starting from the previous part's last candidate: the compaction and
+  // stoichiometry staging happen once instead of once per part, no intermediate candidates are
+  // stored, and the part boundaries' launch tails disappear. The flags the cells raise show whether
+  // the assumption held; the LDS-path launches behind it redo the exact per-part integration from
+  // the gathered input only if it did not (they return at once otherwise).
+  unsigned* spec_w = P_<unsigned>(spec_buf);
+  const bool spec_path = fast_path && spec_w != nullptr && s <= 32 && part_begin == 0 && part_end == nparts &&
+                         scatter && nparts >= 1 && nparts <= kMaxParts && (g_integrate_mode & 0xF8) == 0;
+  if (spec_path) {
+    const int nz = ms::kEqIters * (nparts + 1);
+    int32_t* L = P_<int32_t>(lists);
+    int32_t* wl = L + c;                    // wide list (more than 32 active proteins)
+    int32_t* wl2 = L;                       // overflow list of the narrow blocks (non-zeros, exponents)
+    int32_t* wc2 = L + 2 * (size_t)c;       // its count, cleared with the flags below
+    int32_t* zwc = L + 2 * (size_t)c + 1;
+    unsigned* sflags = spec_w + 4;          // speculative flags (4 per part) + the unfit word
+    gather_bin_kernel<<<cdiv(c, kBlock / 32), kBlock, 0, st>>>(
+        c, s, m, R, C, P, X_io ? P_<float>(X_io) : nullptr, P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr,
+        P_<int32_t>(positions), P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr, trims[0], snaps[1], wl, spec_w, mk,
+        nz, zwc);
+    MS_LAUNCH_CHECK();
+    IntegrateArgs a{};
+    a.c = c; a.P = P; a.s = s;
+    a.W = P_<int32_t>(W); a.Q = P_<float4>(Q); a.Kmr = P_<float>(Kmr);
+    a.snap_prev = snaps[1];
+    a.mask_prev = zero_flags;
+    a.n_iters_prev = n_iters;
+    a.snap_out = snaps[(nparts - 1) & 1];  // slot n_iters: where the write-back looks after a full run
+    a.mask_out = sflags;
+    a.trim = trims[0];
+    a.n_iters = n_iters;
+    a.sp = (s % 2 == 0) ? s + 1 : s;
+    a.prow = prow ? P_<int64_t>(prow) : nullptr;
+    a.spec_parts = nparts;
+    for (int p = 0; p < nparts; ++p) a.trims[p] = trims[p];
+    a.unfit = sflags + ms::kEqIters * nparts;
+    a.Ps = 32;
+    a.prelisted = 1;
+    a.ovf_list = wl2;
+    a.ovf_count = wc2;
+    IntegrateArgs aw = a;  // front blocks: the wide list on 64-lane slots
+    aw.list = wl;
+    aw.count = reinterpret_cast<const int32_t*>(spec_w);
+    aw.Ps = 64;
+    aw.prelisted = 0;
+    aw.ovf_list = nullptr;
+    aw.ovf_count = nullptr;
+    constexpr int kFusedWideBlocks = 64;
+    const size_t lds_fast = (size_t)(kBlock / 32) * fast_slot_words<32, kNzReg>() * 4;
+    integrate_fused_kernel<32, true><<<cdiv(c, kBlock / 32) + kFusedWideBlocks, kBlock, lds_fast, st>>>(
+        a, aw, kFusedWideBlocks);
+    MS_LAUNCH_CHECK();
+    // the narrow blocks' overflow list (rare) on 64-lane slots with 2 * kNzReg non-zeros
+    IntegrateArgs ao = aw;
+    ao.list = wl2;
+    ao.count = wc2;
+    const size_t lds_fw = (size_t)(kBlock / 64) * fast_slot_words<64, kNzWide>() * 4;
+    integrate_fast_kernel<64, kNzWide, true, true><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
+    MS_LAUNCH_CHECK();
+    // exact fallback: the per-part LDS path over every cell, skipped when the speculation held
+    const int sp = a.sp;
+    const int slot_words = slot_words_for(P, s, sp);
+    const size_t slot_bytes = (size_t)slot_words * 4;
+    int cps = kBlock / 32;
+    while (cps > 1 && cps * slot_bytes > 64 * 1024) --cps;
+    const size_t lds = cps * slot_bytes;
+    if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
+    const long long per_cu = std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)lds));
+    const unsigned grid = (unsigned)std::min<long long>(cdiv(c, cps), 256 * per_cu);
+    for (int part = 0; part < nparts; ++part) {
+      IntegrateArgs f{};
+      f.c = c; f.P = P; f.s = s;
+      f.W = a.W; f.Q = a.Q; f.Kmr = a.Kmr; f.prow = a.prow;
+      f.snap_prev = part == 0 ? snaps[1] : snaps[(part - 1) & 1];
+      f.mask_prev = part == 0 ? zero_flags : mk + ms::kEqIters * (part - 1);
+      f.n_iters_prev = n_iters;
+      f.snap_out = snaps[part & 1];
+      f.mask_out = mk + ms::kEqIters * part;
+      f.trim = trims[part];
+      f.n_iters = n_iters;
+      f.sp = sp;
+      f.slot_words = slot_words;
+      f.Ps = P;
+      f.spec_check = sflags;
+      f.spec_n = nparts;
+      f.copy_to = part == nparts - 1 ? mk : nullptr;
+      integrate_part_kernel<32, true><<<grid, cps * 32, lds, st>>>(f);
+      MS_LAUNCH_CHECK();
+    }
+  } else if (part_begin == 0) {
     // part 0 input -> candidate 0 of snap_b, selected through the zero flags; the same launch
     // clears all flag words and (register path) the wide-list counter
     const int nz = ms::kEqIters * (nparts + 1);
@@ -1100,7 +1298,9 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
   // >= 32; part 0 lists it again) goes to a strided launch with LDS slots for all P proteins
   // (integrate_item). The 64-lane launch replaced the LDS path for the wide list: that path's
   // per-cell dependency chain made its launch ~40 us per part for a few hundred cells.
-  if (fast_path) {
+  if (spec_path) {
+    // launched above
+  } else if (fast_path) {
     int32_t* wl = P_<int32_t>(lists) + c;
     int32_t* wc = P_<int32_t>(lists) + 2 * (size_t)c + 1;  // cleared by the input kernel of part 0
     int32_t* wl2 = P_<int32_t>(lists);
@@ -1268,7 +1468,8 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     const int last = nparts - 1;
     integrate_scatter_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(
         c, s, m, R, C, snaps[last & 1], mk + ms::kEqIters * last, n_iters, P_<int32_t>(positions),
-        P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr, X_io ? P_<float>(X_io) : nullptr);
+        P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr, X_io ? P_<float>(X_io) : nullptr,
+        spec_path ? spec_w : nullptr);
     MS_LAUNCH_CHECK();
   }
 }

@@ -193,17 +193,22 @@ def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n
     # narrow / wide cell lists + counts, the active-protein sort (histogram, cursors, order, counts)
     lists = sc.get("bin_lists", 3 * c + c // 4 + 80, torch.int32, dev)
     nparts = len(trims)
+    # speculative all-parts launch (kinetics.hip integrate): word 0 is its wide-list count, which
+    # must be zero on entry (allocated zeroed, reset by the write-back kernel)
+    spec = sc.bufs.get("spec")
+    if spec is None or spec.device != dev:
+        spec = sc.bufs["spec"] = torch.zeros(32, dtype=torch.int32, device=dev)
     if flags_hook is None:
-        _m().integrate(*args, 0, nparts, True, slot_p, _p(lists), mdt, _p(corr), _stream())
+        _m().integrate(*args, 0, nparts, True, slot_p, _p(lists), mdt, _p(corr), _p(spec), _stream())
     else:
         # domain-decomposed world: all-reduce each part's iteration flags before the next part (or
         # the final write-back) reads them, reproducing the reference's `torch.any` over the whole
         # population
         for part in range(nparts):
-            _m().integrate(*args, part, part + 1, False, slot_p, _p(lists), mdt, _p(corr), _stream())
+            _m().integrate(*args, part, part + 1, False, slot_p, _p(lists), mdt, _p(corr), 0, _stream())
             flags_hook(masks[_EQ * part : _EQ * (part + 1)])
         if nparts:
-            _m().integrate(*args, nparts, nparts, True, slot_p, _p(lists), mdt, _p(corr), _stream())
+            _m().integrate(*args, nparts, nparts, True, slot_p, _p(lists), mdt, _p(corr), 0, _stream())
     sc.bufs["pack_overflow_host"].copy_(_overflow_flag(kin), non_blocking=True)
     return masks
 

@@ -699,11 +699,99 @@ def test_register_integrator_matches_lds_integrator_bit_for_bit(case):
         assert int(na.max()) > 32  # exercises the wide launch
     pos = w.cell_positions.long()
     X = torch.cat([w.cell_molecules, w.molecule_map[:, pos[:, 0], pos[:, 1]].T], dim=1).contiguous()
-    out = _integrate_modes(kin, X, modes=(0, 8, 32, 64))
+    out = _integrate_modes(kin, X, modes=(0, 8, 32, 64, 128))
     assert torch.equal(out[0], out[8])
     assert torch.equal(out[32], out[8])
     assert torch.equal(out[64], out[8])
+    assert torch.equal(out[128], out[8])
     assert not torch.equal(out[0], X)
+
+
+def _spec_held(kin, nparts=3, n_iters=4):
+    from magicsoup_amd.ops import hip_ops
+
+    w = hip_ops._scratch(kin).bufs["spec"].cpu().tolist()[4:]
+    return not w[4 * nparts] and all(w[4 * p + it] for p in range(nparts) for it in range(n_iters))
+
+
+@pytest.mark.parametrize("case", ["wl3000", "wl20", "syn16", "syn16_few"])
+def test_speculative_integrator_matches_per_part_launches(case):
+    """Mode 0 runs all parts in one speculative launch (each part starting from the previous part's
+    last candidate) with the exact per-part LDS launches behind it as the fallback; mode 128 runs
+    the per-part launches. Same state, same results bit for bit and the same iteration flags, both
+    when the speculation holds (thousands of cells) and when it does not (a few cells: some part's
+    global loop ends early)."""
+    from magicsoup_amd.ops import kinetics_ops
+
+    chem = CHEMISTRY
+    if case.startswith("syn"):
+        from magicsoup_amd.examples.synthetic import make_chemistry
+
+        chem = make_chemistry(16, 32, seed=3)
+    n = 3000 if case in ("wl3000", "syn16") else 20
+    ms.set_seed(4)
+    torch.manual_seed(4)
+    w = ms.World(chemistry=chem, map_size=128, device="cuda", seed=4)
+    w.spawn_cells(gen_genomes(n, 500))
+    kin = w.kinetics
+    pos = w.cell_positions.long()
+    X = torch.cat([w.cell_molecules, w.molecule_map[:, pos[:, 0], pos[:, 1]].T], dim=1).contiguous()
+    res, masks, held = {}, {}, None
+    try:
+        for mode in (0, 128):
+            native.hip().set_integrate_mode(mode)
+            Xk = X.clone()
+            masks[mode] = kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4)
+            res[mode] = Xk
+            if mode == 0:
+                held = _spec_held(kin)
+    finally:
+        native.hip().set_integrate_mode(0)
+    assert torch.equal(res[0], res[128])
+    assert masks[0] == masks[128]
+    assert held == (masks[128] == [15, 15, 15])
+    if n >= 3000:
+        assert held  # the flagship regime: the speculation holds
+
+    # the world path (gather from / scatter to cell molecules and pixels)
+    w2 = copy.deepcopy(w)
+    try:
+        native.hip().set_integrate_mode(128)
+        w2.enzymatic_activity()
+    finally:
+        native.hip().set_integrate_mode(0)
+    w.enzymatic_activity()
+    assert torch.equal(w.cell_molecules, w2.cell_molecules)
+    assert torch.equal(w.molecule_map, w2.molecule_map)
+
+
+def test_integrator_flags_match_host_core_on_small_populations():
+    """The reference's global exit depends on every cell's flags. A cell whose damping factors stop
+    changing (its remaining iterations are copies) still repeats an impactful correction that
+    changed nothing (a backward reaction with its factor capped at 1), so its flag must stay raised
+    in the remaining iterations. Small populations make single cells decide the exit: the device
+    integrator (speculative launch, fallback, fixed-point exits) must report the host core's flags
+    (which iterates without shortcuts) and its results."""
+    base = _world("cpu", n=200, seed=5)
+    gen = torch.Generator().manual_seed(5)
+    early = close = cells = 0
+    for trial in range(24):
+        keep = torch.randperm(base.n_cells, generator=gen)[: 1 + trial % 4]
+        wc = copy.deepcopy(base)
+        drop = torch.ones(wc.n_cells, dtype=torch.bool)
+        drop[keep] = False
+        wc.kill_cells(torch.nonzero(drop).flatten())
+        wg = _copy_world_cpu_to_gpu(wc)
+        pos = wc.cell_positions.long()
+        X = torch.cat([wc.cell_molecules, wc.molecule_map[:, pos[:, 0], pos[:, 1]].T], dim=1).contiguous()
+        Xc = wc.kinetics.integrate_signals(X)
+        Xg = wg.kinetics.integrate_signals(X.cuda()).cpu()
+        assert wg.kinetics.last_masks == wc.kinetics.last_masks, trial
+        close += int(torch.isclose(Xg, Xc, rtol=1e-5, atol=1e-6).all(dim=1).sum())
+        cells += wc.n_cells
+        early += wc.kinetics.last_masks != [15, 15, 15]
+    assert early > 0  # some populations end a part early
+    assert close >= 0.95 * cells, (close, cells)  # (rare last-ulp differences, as in the tests above)
 
 
 @pytest.mark.parametrize("recycle", [False, True])
