@@ -47,8 +47,13 @@ _LABEL_LEN = 12
 # resolves them first
 _PIPELINE_SAFE_OPS = frozenset({"mutate_cells", "recombinate_cells", "diffuse_molecules", "degrade_molecules",
                                 "increment_cell_lifetimes"})
+# ops an early diffusion stencil (issued by kill_cells, adopted by diffuse_molecules) survives: they
+# neither read nor write the molecule map (degrade_molecules: once, see hip_ops.spec_diffuse_issue)
+_SPEC_DIFF_SAFE_OPS = frozenset({"divide_cells", "mutate_cells", "recombinate_cells", "degrade_molecules",
+                                 "diffuse_molecules", "increment_cell_lifetimes"})
 _CHECK_ENV = os.environ.get("MS_CHECK_INVARIANTS") == "1"
 _DEFER_ENV = os.environ.get("MS_DEFER_GENOME_OPS", "1")
+_FLUSH_EARLY = os.environ.get("MS_FLUSH_EARLY", "1") == "1"
 
 
 def _op(name: str):
@@ -61,6 +66,10 @@ def _op(name: str):
         @functools.wraps(fn)
         def wrapper(self, *args, **kwargs):
             d = self.__dict__
+            if d.get("_spec_diff") is not None and name not in _SPEC_DIFF_SAFE_OPS:
+                from magicsoup_amd.ops import hip_ops
+
+                hip_ops.spec_diffuse_cancel(self)
             if d.get("_spec") is not None:
                 self._reconcile()  # a speculative activity is confirmed (or redone) before anything else
             if (d.get("_gp_state") or d.get("_deferred")) and name not in _PIPELINE_SAFE_OPS:
@@ -290,6 +299,10 @@ class World:
             ev.record()
             d["_defer_event"] = ev
         q.append(fn)
+        if d.get("_spec_diff") is not None and _FLUSH_EARLY:
+            # the diffusion stencil is running already (issued by the kill): nothing to wait for,
+            # the chains start now on the side stream (the next activity depends on them)
+            self._flush_deferred()
 
     def _flush_deferred(self) -> None:
         """Issue the queued genome ops, in call order, on a side stream: their chains run next to
@@ -339,6 +352,10 @@ class World:
                 self._reconcile()
             return cols[name].view(d["n_cells"])
         if name == "molecule_map" and "_molmap" in d:
+            if d.get("_spec_diff") is not None:
+                from magicsoup_amd.ops import hip_ops
+
+                hip_ops.spec_diffuse_cancel(self)  # the caller may read or write the map
             if d.get("_spec") is not None:
                 self._reconcile()
             if d.get("_pending_scale") is not None or d.get("_pending_corr") is not None:
@@ -359,6 +376,10 @@ class World:
             cols[name].adopt(t, int(t.size(0)))
             return
         if name == "molecule_map":
+            if self.__dict__.get("_spec_diff") is not None:
+                from magicsoup_amd.ops import hip_ops
+
+                hip_ops.spec_diffuse_cancel(self)
             t = torch.as_tensor(value, device=self.device)
             want = self.__dict__.get("map_dtype", torch.float32)
             if t.dtype != want or not t.is_contiguous():
@@ -754,6 +775,12 @@ class World:
         if dead.is_cuda:
             from magicsoup_amd.ops import hip_ops
 
+            # the map is final for this step's diffusion now: its stencil starts on a side stream,
+            # next to the compaction and the division that usually follow (adopted by
+            # diffuse_molecules; see hip_ops.spec_diffuse_issue)
+            if hip_ops.EARLY_DIFFUSE_AT == "spill":
+                hip_ops.spec_diffuse_issue(self)
+
             # survivors and the dead in one compaction pass; the row gather is launched with the
             # device-side survivor count before the one stream sync that brings it to the host
             keep_buf, dead_buf, dcount, slot = hip_ops.select_async(dead, "clear", rest=True)
@@ -762,6 +789,8 @@ class World:
             pairs += self._genomes.compact_pairs(n) + self._labels.compact_pairs(n) + slot_pairs
             hip_ops.gather_rows(pairs, n, src_rows=keep_buf, dn=dcount)
             n_new = hip_ops.wait_count(slot)
+            if hip_ops.EARLY_DIFFUSE_AT == "synced":
+                hip_ops.spec_diffuse_issue(self)  # (the compaction is done: only the division runs next to it)
             if n_new == n:
                 return  # nothing removed: the spare buffers are simply not adopted
             self.kinetics.remove_cell_params(keep=keep_buf[:n_new], removed=dead_buf[: n - n_new],
@@ -1004,6 +1033,10 @@ class World:
 
     def __getstate__(self):
         self._reconcile()
+        if self.__dict__.get("_spec_diff") is not None:
+            from magicsoup_amd.ops import hip_ops
+
+            hip_ops.spec_diffuse_cancel(self)
         state = self.__dict__.copy()
         n = self.n_cells
         for k in ("_genome_col", "_label_col"):
@@ -1016,7 +1049,8 @@ class World:
         state["_pending_scale"] = None
         state["_pending_corr"] = None
         for k in ("_hip_scratch", "_idx_map", "_diff_w", "_perm_t", "_degrade_t", "_gp_state", "_deferred",
-                  "_side_stream", "_defer_event", "_gp_cache", "_spec"):
+                  "_side_stream", "_defer_event", "_gp_cache", "_spec", "_spec_diff", "_spec_diff_miss",
+                  "_diff_stream"):
             state.pop(k, None)
         return state
 
