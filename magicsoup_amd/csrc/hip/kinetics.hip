@@ -72,6 +72,7 @@ struct IntegrateArgs {
   const unsigned* spec_check;
   int spec_n;
   unsigned* copy_to;
+  int spec_prev;              // LDS path: start from candidate n_iters_prev of snap_prev (no mask)
 };
 
 // Did the speculative all-parts launch hold? (every part ran all n_iters iterations and every cell
@@ -145,7 +146,7 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
 
   // ---- 1. load X0: the selected candidate of the previous part (part 0: the gathered X)
   if (valid) {
-    const int k = stop_iter(a.mask_prev, a.n_iters_prev);
+    const int k = a.spec_prev ? a.n_iters_prev : stop_iter(a.mask_prev, a.n_iters_prev);
     const float* src = a.snap_prev + ((size_t)cell * ms::kSnap + k) * s;
     for (int j = lane; j < s; j += G) X0[j] = src[j];
   }
@@ -423,6 +424,32 @@ __global__ void __launch_bounds__(kBlock) integrate_part_kernel(IntegrateArgs a)
   or_block_bits(bits, a.mask_out);
 }
 
+// Speculative all-parts mode for the cells no register launch can take (more than 64 active proteins,
+// more than 2 * kNzReg non-zeros, large exponents): every listed cell runs all parts on the LDS path
+// (integrate_item), part p > 0 starting from part p - 1's candidate n_iters, in place in snap_out
+// (a cell's group reads its own previous output before writing any candidate); part p's bits go to
+// flag words 4p.. (a.mask_out). a.snap_prev holds the input (slot 0), a.trims the parts' trims.
+template <int G>
+__global__ void __launch_bounds__(kBlock) integrate_spec_lds_kernel(IntegrateArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  const int cps = blockDim.x / G, slot = threadIdx.x / G;
+  unsigned bits = 0u;
+  const int limit = *a.count;
+  for (int base = (int)blockIdx.x * cps; base < limit; base += (int)gridDim.x * cps) {
+    for (int part = 0; part < a.spec_parts; ++part) {
+      IntegrateArgs ap = a;
+      ap.trim = a.trims[part];
+      ap.spec_prev = part > 0;
+      ap.snap_prev = part > 0 ? a.snap_out : a.snap_prev;
+      unsigned b = 0u;
+      integrate_item<G>(ap, smem, base + slot, b);
+      bits |= b << (ms::kEqIters * part);
+      wave_lds_sync();
+    }
+  }
+  or_block_bits(bits, a.mask_out);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Register-resident integrator (the default for s <= 64): G lanes own one cell and every lane plays
 // two roles -- lane j is signal j (X0_j, the current X_j and the column n_{0..na-1, j} of the
@@ -550,12 +577,11 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     fits = fits && nz_ok;
     if (listed && !fits && lane == 0 && wide_list) wide_list[atomicAdd(wide_count, 1)] = cell;
   } else if (listed && lane == 0) {
-    // too many active proteins: on the wide list already (prelisted) or the speculation is void;
-    // too many non-zeros / large exponents: the overflow list, else void; so is a cell whose active
-    // set differs between parts (a Vmax' underflowing to 0)
-    if (!fits) {
-      if (!a.prelisted) __hip_atomic_store(a.unfit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (!nz_ok) {
+    // too many active proteins: skipped when the cell is on the wide list already (prelisted);
+    // otherwise, and with too many non-zeros / large exponents, the cell goes to the overflow list
+    // (the next, wider launch), without one the speculation is void; so is a cell whose active set
+    // differs between parts (a Vmax' underflowing to 0)
+    if (!(!fits && a.prelisted) && (!fits || !nz_ok)) {
       if (a.ovf_list) a.ovf_list[atomicAdd(a.ovf_count, 1)] = cell;
       else __hip_atomic_store(a.unfit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1176,8 +1202,10 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
   // the assumption held; the LDS-path launches behind it redo the exact per-part integration from
   // the gathered input only if it did not (they return at once otherwise).
   unsigned* spec_w = P_<unsigned>(spec_buf);
+  // (odd part counts: the final state lands in snap_a, and snap_b keeps the input for the fallback)
   const bool spec_path = fast_path && spec_w != nullptr && s <= 32 && part_begin == 0 && part_end == nparts &&
-                         scatter && nparts >= 1 && nparts <= kMaxParts && (g_integrate_mode & 0xF8) == 0;
+                         scatter && nparts >= 1 && nparts <= kMaxParts && (nparts & 1) == 1 &&
+                         (g_integrate_mode & 0xF8) == 0;
   if (spec_path) {
     const int nz = ms::kEqIters * (nparts + 1);
     int32_t* L = P_<int32_t>(lists);
@@ -1185,6 +1213,8 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     int32_t* wl2 = L;                       // overflow list of the narrow blocks (non-zeros, exponents)
     int32_t* wc2 = L + 2 * (size_t)c;       // its count, cleared with the flags below
     int32_t* zwc = L + 2 * (size_t)c + 1;
+    int32_t* wl3 = L + 2 * (size_t)c + 2 + 2 * kSortBuckets;  // what no register launch takes (the
+    int32_t* wc3 = L + 2 * (size_t)c + 2;                      // sort order / histogram slots, unused here)
     unsigned* sflags = spec_w + 4;          // speculative flags (4 per part) + the unfit word
     gather_bin_kernel<<<cdiv(c, kBlock / 32), kBlock, 0, st>>>(
         c, s, m, R, C, P, X_io ? P_<float>(X_io) : nullptr, P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr,
@@ -1215,8 +1245,8 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     aw.count = reinterpret_cast<const int32_t*>(spec_w);
     aw.Ps = 64;
     aw.prelisted = 0;
-    aw.ovf_list = nullptr;
-    aw.ovf_count = nullptr;
+    aw.ovf_list = wl3;
+    aw.ovf_count = wc3;
     constexpr int kFusedWideBlocks = 64;
     const size_t lds_fast = (size_t)(kBlock / 32) * fast_slot_words<32, kNzReg>() * 4;
     integrate_fused_kernel<32, true><<<cdiv(c, kBlock / 32) + kFusedWideBlocks, kBlock, lds_fast, st>>>(
@@ -1229,7 +1259,6 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     const size_t lds_fw = (size_t)(kBlock / 64) * fast_slot_words<64, kNzWide>() * 4;
     integrate_fast_kernel<64, kNzWide, true, true><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
     MS_LAUNCH_CHECK();
-    // exact fallback: the per-part LDS path over every cell, skipped when the speculation held
     const int sp = a.sp;
     const int slot_words = slot_words_for(P, s, sp);
     const size_t slot_bytes = (size_t)slot_words * 4;
@@ -1239,6 +1268,17 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
     const long long per_cu = std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)lds));
     const unsigned grid = (unsigned)std::min<long long>(cdiv(c, cps), 256 * per_cu);
+    // the cells neither register launch took, all parts on the LDS path (rare: usually an empty list)
+    {
+      IntegrateArgs l = a;
+      l.list = wl3;
+      l.count = wc3;
+      l.Ps = P;
+      l.slot_words = slot_words;
+      integrate_spec_lds_kernel<32><<<std::min<unsigned>(grid, 256), cps * 32, lds, st>>>(l);
+      MS_LAUNCH_CHECK();
+    }
+    // exact fallback: the per-part LDS path over every cell, skipped when the speculation held
     for (int part = 0; part < nparts; ++part) {
       IntegrateArgs f{};
       f.c = c; f.P = P; f.s = s;

@@ -714,7 +714,7 @@ def _spec_held(kin, nparts=3, n_iters=4):
     return not w[4 * nparts] and all(w[4 * p + it] for p in range(nparts) for it in range(n_iters))
 
 
-@pytest.mark.parametrize("case", ["wl3000", "wl20", "syn16", "syn16_few"])
+@pytest.mark.parametrize("case", ["wl3000", "wl20", "syn16", "syn16_few", "wl9000bp", "exp40"])
 def test_speculative_integrator_matches_per_part_launches(case):
     """Mode 0 runs all parts in one speculative launch (each part starting from the previous part's
     last candidate) with the exact per-part LDS launches behind it as the fallback; mode 128 runs
@@ -728,12 +728,20 @@ def test_speculative_integrator_matches_per_part_launches(case):
         from magicsoup_amd.examples.synthetic import make_chemistry
 
         chem = make_chemistry(16, 32, seed=3)
-    n = 3000 if case in ("wl3000", "syn16") else 20
+    n = {"wl3000": 3000, "syn16": 3000, "wl9000bp": 400, "exp40": 3000}.get(case, 20)
     ms.set_seed(4)
     torch.manual_seed(4)
     w = ms.World(chemistry=chem, map_size=128, device="cuda", seed=4)
-    w.spawn_cells(gen_genomes(n, 500))
+    w.spawn_cells(gen_genomes(n, 9000 if case == "wl9000bp" else 500))
     kin = w.kinetics
+    if case == "wl9000bp":
+        # proteomes beyond the 64-lane slots: the speculative LDS launch takes those cells
+        assert int((kin.Vmax > 0).sum(1).max()) > 64
+    if case == "exp40":
+        # exponents beyond the register paths' 5-bit fields (same route)
+        Nf = kin.Nf.clone()
+        Nf[::9, :, 2] = torch.where(Nf[::9, :, 2] > 0, 40, Nf[::9, :, 2])
+        kin.Nf = Nf
     pos = w.cell_positions.long()
     X = torch.cat([w.cell_molecules, w.molecule_map[:, pos[:, 0], pos[:, 1]].T], dim=1).contiguous()
     res, masks, held = {}, {}, None
