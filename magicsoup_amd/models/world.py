@@ -54,6 +54,16 @@ _SPEC_DIFF_SAFE_OPS = frozenset({"divide_cells", "mutate_cells", "recombinate_ce
 _CHECK_ENV = os.environ.get("MS_CHECK_INVARIANTS") == "1"
 _DEFER_ENV = os.environ.get("MS_DEFER_GENOME_OPS", "1")
 _FLUSH_EARLY = os.environ.get("MS_FLUSH_EARLY", "1") == "1"
+# MS_EAGER_CHAINS=1 (or World._early_chains = True; single-process GPU worlds): issue the genome
+# chains as soon as recombinate_cells / mutate_cells are called and join them into the compute stream
+# only at the next op that needs their results (every op outside _PIPELINE_SAFE_OPS). Off by
+# default: the flagship step got slower (1.25 -> 1.35 ms median, profiles/r2_s3/headroom_chains_ab.txt)
+# -- the default queues them until the diffusion stencil is launched and joins at once.
+_EAGER_CHAINS = os.environ.get("MS_EAGER_CHAINS", "0") == "1"
+# genome arena row width = this x the longest genome when it (re)grows (GPU worlds; see StringArena).
+# 1 by default: wider rows removed the early widening events but made the flagship step slower
+# (profiles/r2_s3/headroom_chains_ab.txt)
+_GENOME_HEADROOM = int(os.environ.get("MS_GENOME_HEADROOM", "1"))
 
 
 def _op(name: str):
@@ -77,6 +87,8 @@ def _op(name: str):
                     self._flush_deferred()  # issue the queued chains; confirmed after the activity
                 else:
                     self._reconcile()
+            if d.get("_side_join") is not None and name not in _PIPELINE_SAFE_OPS:
+                self._join_side()
             timer, check = d.get("_timer"), d.get("_debug_checks", _CHECK_ENV)
             if timer is None and not check and not profiling.roctx_enabled():
                 return fn(self, *args, **kwargs)
@@ -185,6 +197,9 @@ class World:
         seed: Optional seed of all native RNG streams (placement, mutation, recombination).
     """
 
+    # genome arena row width = this x the longest genome when it (re)grows on a GPU (StringArena)
+    _genome_headroom = _GENOME_HEADROOM
+
     # domain-decomposition hooks of the op layer (set by magicsoup_amd.parallel.DistributedWorld)
     _exchange_map_halo = None
     _allreduce_flags = None
@@ -238,7 +253,8 @@ class World:
         dev = torch.device(device)
         m = self.n_molecules
         self.n_cells = 0
-        self._genomes = StringArena(dev, width=64)
+        hr = type(self)._genome_headroom if dev.type == "cuda" else 1
+        self._genomes = StringArena(dev, width=64, headroom=hr)
         self._labels = StringArena(dev, width=16)
         self._genome_col = StringColumn(self._genomes)
         self._label_col = StringColumn(self._labels)
@@ -299,10 +315,20 @@ class World:
             ev.record()
             d["_defer_event"] = ev
         q.append(fn)
-        if d.get("_spec_diff") is not None and _FLUSH_EARLY:
-            # the diffusion stencil is running already (issued by the kill): nothing to wait for,
-            # the chains start now on the side stream (the next activity depends on them)
+        if (d.get("_spec_diff") is not None and _FLUSH_EARLY) or self._lazy_join():
+            # nothing to wait for: the chains start now on the side stream (the next activity
+            # depends on them; an early diffusion stencil may be running already)
             self._flush_deferred()
+
+    def _lazy_join(self) -> bool:
+        d = self.__dict__
+        return d.get("_early_chains", _EAGER_CHAINS) and "_n_pix_global" not in d
+
+    def _join_side(self) -> None:
+        """The compute stream waits (device-side) for the genome chains issued so far."""
+        ev = self.__dict__.pop("_side_join", None)
+        if ev is not None:
+            torch.cuda.current_stream(self._genomes.data.device).wait_event(ev)
 
     def _flush_deferred(self) -> None:
         """Issue the queued genome ops, in call order, on a side stream: their chains run next to
@@ -329,11 +355,18 @@ class World:
                     fn()
         finally:
             d["_side_active"] = False
-            main.wait_stream(side)
+            if self._lazy_join():
+                # joined at the next op that needs the chains' results (see _EAGER_CHAINS)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                d["_side_join"] = ev
+            else:
+                main.wait_stream(side)
 
     def _reconcile(self) -> None:
         if self.__dict__.get("_deferred"):
             self._flush_deferred()
+        self._join_side()
         if self.__dict__.get("_gp_state"):
             from magicsoup_amd.ops import genome_pipeline
 
@@ -1050,7 +1083,7 @@ class World:
         state["_pending_corr"] = None
         for k in ("_hip_scratch", "_idx_map", "_diff_w", "_perm_t", "_degrade_t", "_gp_state", "_deferred",
                   "_side_stream", "_defer_event", "_gp_cache", "_spec", "_spec_diff", "_spec_diff_miss",
-                  "_diff_stream"):
+                  "_diff_stream", "_side_join"):
             state.pop(k, None)
         return state
 
@@ -1065,7 +1098,8 @@ class World:
         self.__dict__["_cols"] = {k: _Column(v.to(dev)) for k, v in cols.items()}
         for c in self._cols.values():
             c.view(int(c.buf.size(0)))
-        self.__dict__["_genomes"] = StringArena(dev, width=64)
+        hr = type(self)._genome_headroom if dev.type == "cuda" else 1
+        self.__dict__["_genomes"] = StringArena(dev, width=64, headroom=hr)
         self.__dict__["_labels"] = StringArena(dev, width=16)
         self._genomes.append_strings(genomes)
         self._labels.append_strings(labels)

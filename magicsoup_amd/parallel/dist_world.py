@@ -110,6 +110,9 @@ class DistributedWorld(World):
     :meth:`gather` and :meth:`scatter_from` convert to and from the global picture.
     """
 
+    # record exchanges append rows as wide as the sender's arena: no headroom (it would compound)
+    _genome_headroom = 1
+
     def __init__(self, *args, group=None, exact_global_exit: bool = True, boundary_genome_cap: int = 2048,
                  strips: bool | None = None, **kwargs):
         if not dist.is_initialized():

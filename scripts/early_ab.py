@@ -1,4 +1,4 @@
-"""Paired A/B of the early diffusion stencil on ONE evolving flagship world: the variants take turns
+"""Paired A/B of the early diffusion stencil and of the eager genome chains on ONE evolving flagship world: the variants take turns
 in blocks of steps (2 untimed + K timed after each switch), so population drift and box-to-box noise
 cancel out. Prints the median ms/step of each variant.
 
@@ -29,12 +29,17 @@ w = ms.World(chemistry=chem, map_size=S, device="cuda:0", seed=0)
 w.spawn_cells(bench.random_genomes(N, 500, "cuda:0"))
 for _ in range(20):
     bench.step(w, N, 500, atp)
-VARIANTS = {"off": (False, True, "spill"), "spill_flush": (True, True, "spill"), "spill_late": (True, False, "spill"),
-            "synced_flush": (True, True, "synced")}
+# (early diffusion, flush at once when it is pending, where the kill issues it, eager chains + lazy join)
+VARIANTS = {"off": (False, True, "spill", True), "off_join_at_diffuse": (False, True, "spill", False),
+            "spill_flush": (True, True, "spill", True), "synced_flush": (True, True, "synced", True)}
+if os.environ.get("AB_OLD"):
+    VARIANTS = {"off": (False, True, "spill", False), "spill_flush": (True, True, "spill", False),
+                "spill_late": (True, False, "spill", False), "synced_flush": (True, True, "synced", False)}
 res = {k: [] for k in VARIANTS}
 for b in range(blocks):
-    for name, (early, flush, at) in VARIANTS.items():
+    for name, (early, flush, at, chains) in VARIANTS.items():
         w.__dict__["_early_diffuse"] = early
+        w.__dict__["_early_chains"] = chains
         world_mod._FLUSH_EARLY = flush
         hip_ops.EARLY_DIFFUSE_AT = at
         for _ in range(2):

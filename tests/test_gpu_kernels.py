@@ -594,10 +594,9 @@ def test_device_genome_pipeline_matches_sync_path(monkeypatch, d_cap):
 
 
 def test_deferred_genome_ops_match_immediate_issue(monkeypatch):
-    """All-cells mutate / recombinate are queued until the diffusion stencil is launched or the
-    next op that reads genomes, parameters or cells (degrade runs in between): same genomes,
-    parameters and trajectory as issuing them immediately; diffuse_molecules issues the queue and
-    reading ``cell_genomes`` confirms it."""
+    """All-cells mutate / recombinate go to a side stream (issued at once and joined at the next op
+    that needs them, or queued until the diffusion stencil is launched): same genomes, parameters and
+    trajectory as issuing them on the compute stream; reading ``cell_genomes`` confirms them."""
     import magicsoup_amd.models.world as world_mod
 
     base = _world("cuda", map_size=64, n=800, s=400, seed=7)
@@ -609,6 +608,7 @@ def test_deferred_genome_ops_match_immediate_issue(monkeypatch):
     for k in p0:
         assert torch.equal(p0[k], p1[k]), k
     assert torch.equal(x0, x1)
+    # default: queued until the diffusion
     w = copy.deepcopy(base)
     w.recombinate_cells(p=1e-4)
     w.mutate_cells(p=1e-3)
@@ -617,6 +617,19 @@ def test_deferred_genome_ops_match_immediate_issue(monkeypatch):
     w.diffuse_molecules()
     assert not w.__dict__["_deferred"]
     genomes = list(w.cell_genomes)
+    assert not w.__dict__.get("_gp_state", {}).get("pending") and len(genomes) == w.n_cells
+    # eager chains (MS_EAGER_CHAINS=1): issued at once on the side stream, joined into the compute
+    # stream only by the next op that needs them (degrade / diffuse run next to them)
+    w = copy.deepcopy(base)
+    w.__dict__["_early_chains"] = True
+    w.recombinate_cells(p=1e-4)
+    w.mutate_cells(p=1e-3)
+    assert not w.__dict__.get("_deferred") and w.__dict__.get("_side_join") is not None
+    w.degrade_molecules()
+    w.diffuse_molecules()
+    assert w.__dict__.get("_side_join") is not None
+    genomes = list(w.cell_genomes)
+    assert w.__dict__.get("_side_join") is None
     assert not w.__dict__.get("_gp_state", {}).get("pending") and len(genomes) == w.n_cells
 
 
