@@ -64,6 +64,9 @@ _EAGER_CHAINS = os.environ.get("MS_EAGER_CHAINS", "0") == "1"
 # 1 by default: wider rows removed the early widening events but made the flagship step slower
 # (profiles/r2_s3/headroom_chains_ab.txt)
 _GENOME_HEADROOM = int(os.environ.get("MS_GENOME_HEADROOM", "1"))
+# ... and for the first population (an empty arena): the first recombinants outgrow rows as wide as
+# the initial genomes within a few steps, and that widening replays the pipeline calls on the host
+_GENOME_HEADROOM_INIT = int(os.environ.get("MS_GENOME_HEADROOM_INIT", "1"))
 
 
 def _op(name: str):
@@ -199,6 +202,7 @@ class World:
 
     # genome arena row width = this x the longest genome when it (re)grows on a GPU (StringArena)
     _genome_headroom = _GENOME_HEADROOM
+    _genome_headroom_init = _GENOME_HEADROOM_INIT
 
     # domain-decomposition hooks of the op layer (set by magicsoup_amd.parallel.DistributedWorld)
     _exchange_map_halo = None
@@ -254,7 +258,8 @@ class World:
         m = self.n_molecules
         self.n_cells = 0
         hr = type(self)._genome_headroom if dev.type == "cuda" else 1
-        self._genomes = StringArena(dev, width=64, headroom=hr)
+        hr0 = type(self)._genome_headroom_init if dev.type == "cuda" else 1
+        self._genomes = StringArena(dev, width=64, headroom=hr, initial_headroom=hr0)
         self._labels = StringArena(dev, width=16)
         self._genome_col = StringColumn(self._genomes)
         self._label_col = StringColumn(self._labels)
@@ -1099,7 +1104,8 @@ class World:
         for c in self._cols.values():
             c.view(int(c.buf.size(0)))
         hr = type(self)._genome_headroom if dev.type == "cuda" else 1
-        self.__dict__["_genomes"] = StringArena(dev, width=64, headroom=hr)
+        hr0 = type(self)._genome_headroom_init if dev.type == "cuda" else 1
+        self.__dict__["_genomes"] = StringArena(dev, width=64, headroom=hr, initial_headroom=hr0)
         self.__dict__["_labels"] = StringArena(dev, width=16)
         self._genomes.append_strings(genomes)
         self._labels.append_strings(labels)

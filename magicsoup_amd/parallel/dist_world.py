@@ -112,6 +112,7 @@ class DistributedWorld(World):
 
     # record exchanges append rows as wide as the sender's arena: no headroom (it would compound)
     _genome_headroom = 1
+    _genome_headroom_init = 1
 
     def __init__(self, *args, group=None, exact_global_exit: bool = True, boundary_genome_cap: int = 2048,
                  strips: bool | None = None, **kwargs):

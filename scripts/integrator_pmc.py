@@ -1,6 +1,6 @@
 """Driver for PMC passes over the integrator: a flagship-like state after a few bench steps, then
-`reps` enzymatic_activity calls with the register-resident launches (mode 0) followed by `reps`
-with the legacy LDS-staged launches (mode 8); kernel names tell the two apart.
+`reps` enzymatic_activity calls with the speculative all-parts launch (mode 0) followed by `reps`
+with the per-part register launches (mode 128); kernel names tell the two apart.
 
 usage: python scripts/integrator_pmc.py [map_size] [cells] [reps]"""
 import os
@@ -23,7 +23,7 @@ atp = CHEMISTRY.molname_2_idx["ATP"]
 for _ in range(5):
     bench.step(w, cells, 500, atp)
 torch.cuda.synchronize()
-for mode in (0, 8):
+for mode in (0, 128):  # speculative all-parts launch, per-part register launches
     native.hip().set_integrate_mode(mode)
     for _ in range(reps):
         w.enzymatic_activity()
