@@ -67,6 +67,7 @@ _GENOME_HEADROOM = int(os.environ.get("MS_GENOME_HEADROOM", "1"))
 # ... and for the first population (an empty arena): the first recombinants outgrow rows as wide as
 # the initial genomes within a few steps, and that widening replays the pipeline calls on the host
 _GENOME_HEADROOM_INIT = int(os.environ.get("MS_GENOME_HEADROOM_INIT", "1"))
+_WIDTH_WATCH = os.environ.get("MS_GENOME_WIDTH_WATCH", "0") == "1"  # opt-in, see World._watch_genome_width
 
 
 def _op(name: str):
@@ -838,12 +839,42 @@ class World:
             self._genomes.commit_compact(n_new)
             self._labels.commit_compact(n_new)
             self.n_cells = n_new
+            self._watch_genome_width()
             return
         keep = ~dead
         keep_idx = torch.nonzero(keep).flatten()
         if int(keep_idx.numel()) == n:
             return
         self._compact(keep_idx, keep)
+
+    def _watch_genome_width(self) -> None:
+        """Widen the genome arena before the device pipeline's results outgrow it. A recombinant can
+        be as long as both parents together, and a result that does not fit its row makes the
+        pipeline skip the calls after it: the host then commits and replays them and redoes the
+        speculative activity (2-20 ms). Every 4th GPU kill queues the longest genome's length into
+        pinned memory (no synchronisation); once it has arrived and exceeds 3/4 of the row width, the
+        rows double (a copy of the used rows; the pipeline is reconciled at this point). Opt-in
+        (MS_GENOME_WIDTH_WATCH=1): it removes the replays from the spike log, but five alternating
+        driver-style pairs ran 2 % slower with it (profiles/r2_s3/width_watch_ab.txt)."""
+        d = self.__dict__
+        g = self._genomes
+        if not _WIDTH_WATCH or not g.data.is_cuda or "_n_pix_global" in d:
+            return
+        w = d.get("_gw_watch")
+        if w is not None and w[1].query():
+            d["_gw_watch"] = None
+            if 4 * int(w[0][0]) > 3 * g.width and 2 * g.width <= 65535 and not (d.get("_gp_state") or {}).get("pending"):
+                g.reserve(g.n, 2 * g.width)
+        cnt = d.get("_gw_count", 0) + 1
+        d["_gw_count"] = cnt
+        if d.get("_gw_watch") is None and cnt % 4 == 0 and g.n > 0:
+            buf = d.get("_gw_pinned")
+            if buf is None:
+                buf = d["_gw_pinned"] = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            buf.copy_(g.lens[: g.n].max().view(1), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            d["_gw_watch"] = (buf, ev)
 
     def _compact(self, keep_idx: torch.Tensor, keep: torch.Tensor | None, removed: torch.Tensor | None = None) -> None:
         n_new = int(keep_idx.numel())
@@ -1088,7 +1119,7 @@ class World:
         state["_pending_corr"] = None
         for k in ("_hip_scratch", "_idx_map", "_diff_w", "_perm_t", "_degrade_t", "_gp_state", "_deferred",
                   "_side_stream", "_defer_event", "_gp_cache", "_spec", "_spec_diff", "_spec_diff_miss",
-                  "_diff_stream", "_side_join"):
+                  "_diff_stream", "_side_join", "_gw_watch", "_gw_pinned"):
             state.pop(k, None)
         return state
 

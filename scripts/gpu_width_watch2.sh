@@ -1,0 +1,21 @@
+#!/bin/bash
+# Proactive genome-arena widening on/off, driver-style runs (5 + 20 steps), 5 alternating pairs.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export PYTHONPATH="$PWD:${PYTHONPATH:-}" TMPDIR=/tmp
+O=gpurun_out/ww2; rm -rf $O; mkdir -p $O
+for r in 1 2 3 4 5; do
+  for h in 1 0; do
+    MS_GENOME_WIDTH_WATCH=$h timeout -k 10 200 python bench.py --steps 20 --warmup 5 --step-times > $O/w${h}_r$r.log 2>&1
+    rc=$?
+    python - "$O/w${h}_r$r.log" <<'PY'
+import json, statistics, sys
+t = open(sys.argv[1]).read()
+st = json.loads(t[t.index('{"step_ms"'):].splitlines()[0])["step_ms"]
+v = json.loads(t[t.index('{"metric"'):].splitlines()[0])["value"]
+print(sys.argv[1].split("/")[-1], "value", v, "median", statistics.median(st), "max", max(st))
+PY
+    case $rc in 124|134|137|139) exit $rc;; esac
+  done
+done
+exit 0
