@@ -62,7 +62,10 @@ class Scratch:
     def get(self, name: str, numel: int, dtype, device, zero: bool = False) -> torch.Tensor:
         t = self.bufs.get(name)
         if t is None or t.numel() < numel or t.dtype != dtype or t.device != device:
-            t = torch.empty(max(numel, 1), dtype=dtype, device=device)
+            # a buffer that grows takes 1.5x: populations creep up step by step, and every new size
+            # is a fresh allocation (the caching allocator has no block of it yet)
+            grow = t is not None and t.dtype == dtype and t.device == device
+            t = torch.empty(max(numel, 1, int(1.5 * t.numel()) if grow else 0), dtype=dtype, device=device)
             self.bufs[name] = t
         v = t[:numel]
         if zero:
