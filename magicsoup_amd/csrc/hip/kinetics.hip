@@ -34,7 +34,9 @@ constexpr int kMaxParts = 4;  // speculative mode: 4 parts x 4 iterations in one
 // 16-lane 590 us -- the kernel is VALU-throughput bound (37M wave instructions per launch, ~60 %
 // of the SIMDs' issue capacity), so overlapping the bins only adds contention. Serial is default.
 // bit 3: legacy LDS-staged path; bit 4: register path with cells sorted by active-protein count;
-// bits 5 / 6: see the launcher; bit 7: no speculative all-parts launch (any of bits 3-7 disables it).
+// bits 5 / 6: see the launcher; bit 7: no speculative all-parts launch (any of bits 3-7 disables it);
+// bit 8: the speculative register launches store their final states in the snapshot for the
+// write-back kernel instead of writing the world directly.
 static int g_integrate_mode = 0;
 void set_integrate_mode(int mode) { g_integrate_mode = mode; }
 
@@ -73,6 +75,16 @@ struct IntegrateArgs {
   int spec_n;
   unsigned* copy_to;
   int spec_prev;              // LDS path: start from candidate n_iters_prev of snap_prev (no mask)
+  // Speculative register launches: the final state goes straight to the world (cell molecules and
+  // the pixels under the cells, or the explicit X) instead of snap_out; the write-back kernel then
+  // only covers the LDS-list cells, or everything again if the speculation did not hold.
+  int wb;
+  float* wb_cm;
+  void* wb_map;
+  const float* wb_corr;
+  const int32_t* wb_pos;
+  float* wb_x;
+  int wb_m, wb_R, wb_C, wb_dtype;
 };
 
 // Did the speculative all-parts launch hold? (every part ran all n_iters iterations and every cell
@@ -800,7 +812,19 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   }
   x0 = xc;  // the next part starts from this part's last candidate (Xs holds it already)
   }
-  if (spec && sig) snap[(size_t)a.n_iters * s + lane] = xc;
+  if (spec && sig) {
+    if (!a.wb) {
+      snap[(size_t)a.n_iters * s + lane] = xc;
+    } else if (a.wb_x) {
+      a.wb_x[(size_t)cell * s + lane] = xc;
+    } else if (lane < a.wb_m) {
+      a.wb_cm[(size_t)cell * a.wb_m + lane] = xc;
+    } else {
+      const size_t pix = (size_t)a.wb_pos[2 * cell] * a.wb_C + a.wb_pos[2 * cell + 1];
+      st_map(a.wb_map, (size_t)(lane - a.wb_m) * a.wb_R * a.wb_C + pix, corr_out(xc, a.wb_corr, lane - a.wb_m),
+             a.wb_dtype);
+    }
+  }
 #undef MS_E
 }
 
@@ -873,11 +897,19 @@ __global__ void __launch_bounds__(kBlock) integrate_scatter_kernel(int c, int s,
                                                                    const unsigned* mask, int n_iters,
                                                                    const int32_t* positions, float* cell_mols,
                                                                    void* molmap, int map_dtype, const float* corr,
-                                                                   float* X_out, unsigned* reset) {
+                                                                   float* X_out, unsigned* reset,
+                                                                   const unsigned* spec_flags, int spec_n,
+                                                                   const int32_t* lds_list, const int32_t* lds_count) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (reset && t == 0) reset[0] = 0u;  // the speculative path's wide-list count, for the next call
   if (t >= (long long)c * s) return;
-  const int cell = (int)(t / s), j = (int)(t - (long long)cell * s);
+  int cell = (int)(t / s);
+  const int j = (int)(t - (long long)cell * s);
+  if (spec_flags && spec_held(spec_flags, spec_n, n_iters)) {
+    // the register launches wrote their cells already: only the LDS-list cells are left
+    if (cell >= *lds_count) return;
+    cell = lds_list[cell];
+  }
   const int k = stop_iter(mask, n_iters);
   const float x = snap[((size_t)cell * ms::kSnap + k) * s + j];
   if (X_out) {
@@ -1202,6 +1234,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
   // the assumption held; the LDS-path launches behind it redo the exact per-part integration from
   // the gathered input only if it did not (they return at once otherwise).
   unsigned* spec_w = P_<unsigned>(spec_buf);
+  const bool spec_wb = (g_integrate_mode & 256) == 0;  // mode bit 8: final states via snap + write-back
   // (odd part counts: the final state lands in snap_a, and snap_b keeps the input for the fallback)
   const bool spec_path = fast_path && spec_w != nullptr && s <= 32 && part_begin == 0 && part_end == nparts &&
                          scatter && nparts >= 1 && nparts <= kMaxParts && (nparts & 1) == 1 &&
@@ -1236,6 +1269,15 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     a.spec_parts = nparts;
     for (int p = 0; p < nparts; ++p) a.trims[p] = trims[p];
     a.unfit = sflags + ms::kEqIters * nparts;
+    if (spec_wb) {
+      a.wb = 1;
+      a.wb_x = X_io ? P_<float>(X_io) : nullptr;
+      a.wb_cm = P_<float>(cell_mols);
+      a.wb_map = P_<void>(molmap);
+      a.wb_corr = corr;
+      a.wb_pos = P_<int32_t>(positions);
+      a.wb_m = m; a.wb_R = R; a.wb_C = C; a.wb_dtype = map_dtype;
+    }
     a.Ps = 32;
     a.prelisted = 1;
     a.ovf_list = wl2;
@@ -1509,7 +1551,9 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     integrate_scatter_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(
         c, s, m, R, C, snaps[last & 1], mk + ms::kEqIters * last, n_iters, P_<int32_t>(positions),
         P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr, X_io ? P_<float>(X_io) : nullptr,
-        spec_path ? spec_w : nullptr);
+        spec_path ? spec_w : nullptr, spec_path && spec_wb ? spec_w + 4 : nullptr, nparts,
+        spec_path ? P_<int32_t>(lists) + 2 * (size_t)c + 2 + 2 * kSortBuckets : nullptr,
+        spec_path ? P_<int32_t>(lists) + 2 * (size_t)c + 2 : nullptr);
     MS_LAUNCH_CHECK();
   }
 }

@@ -49,12 +49,12 @@ def main():
 
     for rep_i in range(3):  # A/B of the launch modes on the same state (alternating)
         # speculative all-parts launch; per-part register launches; + unfused wide list; + sort
-        for mode in (0, 128, 64, 16):
+        for mode in (0, 256, 128, 64):
             native.hip().set_integrate_mode(mode)
             Xk = X.clone()
             out[f"us_mode{mode}_r{rep_i}"] = timed(lambda: kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4))
     res = {}
-    for mode in (0, 8, 9, 10, 11, 12, 16, 32, 64, 128):  # every mode computes the same state, bit for bit
+    for mode in (0, 8, 9, 10, 11, 12, 16, 32, 64, 128, 256):  # every mode computes the same state, bit for bit
         native.hip().set_integrate_mode(mode)
         Xk = X.clone()
         kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4)
@@ -63,6 +63,10 @@ def main():
     out["max_abs_diff_legacy"] = float((res[0] - res[8]).abs().max())
     out["us_ea_sorted"] = (native.hip().set_integrate_mode(16), timed(w.enzymatic_activity))[1]
     out["us_ea_per_part"] = (native.hip().set_integrate_mode(128), timed(w.enzymatic_activity))[1]
+    out["us_ea_spec_snap_writeback"] = (native.hip().set_integrate_mode(256), timed(w.enzymatic_activity))[1]
+    native.hip().set_integrate_mode(0)
+    out["us_ea_spec_direct"] = timed(w.enzymatic_activity)
+    out["us_ea_spec_snap_writeback_2"] = (native.hip().set_integrate_mode(256), timed(w.enzymatic_activity))[1]
     native.hip().set_integrate_mode(0)
     out["us_ea_fast"] = timed(w.enzymatic_activity)
     native.hip().set_integrate_mode(0)

@@ -712,7 +712,8 @@ def test_register_integrator_matches_lds_integrator_bit_for_bit(case):
         assert int(na.max()) > 32  # exercises the wide launch
     pos = w.cell_positions.long()
     X = torch.cat([w.cell_molecules, w.molecule_map[:, pos[:, 0], pos[:, 1]].T], dim=1).contiguous()
-    out = _integrate_modes(kin, X, modes=(0, 8, 32, 64, 128))
+    out = _integrate_modes(kin, X, modes=(0, 8, 32, 64, 128, 256))
+    assert torch.equal(out[256], out[8])
     assert torch.equal(out[0], out[8])
     assert torch.equal(out[32], out[8])
     assert torch.equal(out[64], out[8])
@@ -774,16 +775,20 @@ def test_speculative_integrator_matches_per_part_launches(case):
     if n >= 3000:
         assert held  # the flagship regime: the speculation holds
 
-    # the world path (gather from / scatter to cell molecules and pixels)
-    w2 = copy.deepcopy(w)
+    # the world path (gather from / scatter to cell molecules and pixels); mode 256: the speculative
+    # launches store their states for the write-back kernel instead of writing the world directly
+    w2, w3 = copy.deepcopy(w), copy.deepcopy(w)
     try:
         native.hip().set_integrate_mode(128)
         w2.enzymatic_activity()
+        native.hip().set_integrate_mode(256)
+        w3.enzymatic_activity()
     finally:
         native.hip().set_integrate_mode(0)
     w.enzymatic_activity()
-    assert torch.equal(w.cell_molecules, w2.cell_molecules)
-    assert torch.equal(w.molecule_map, w2.molecule_map)
+    for x in (w2, w3):
+        assert torch.equal(w.cell_molecules, x.cell_molecules)
+        assert torch.equal(w.molecule_map, x.molecule_map)
 
 
 def test_integrator_flags_match_host_core_on_small_populations():
