@@ -900,27 +900,26 @@ __global__ void __launch_bounds__(kBlock) integrate_scatter_kernel(int c, int s,
                                                                    float* X_out, unsigned* reset,
                                                                    const unsigned* spec_flags, int spec_n,
                                                                    const int32_t* lds_list, const int32_t* lds_count) {
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (reset && t == 0) reset[0] = 0u;  // the speculative path's wide-list count, for the next call
-  if (t >= (long long)c * s) return;
-  int cell = (int)(t / s);
-  const int j = (int)(t - (long long)cell * s);
-  if (spec_flags && spec_held(spec_flags, spec_n, n_iters)) {
-    // the register launches wrote their cells already: only the LDS-list cells are left
-    if (cell >= *lds_count) return;
-    cell = lds_list[cell];
-  }
+  const long long t0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (reset && t0 == 0) reset[0] = 0u;  // the speculative path's wide-list count, for the next call
+  // grid-stride (a bounded grid): after a speculation that held, the register launches wrote their
+  // cells already and only the LDS-list cells are left, usually none
+  const bool held = spec_flags && spec_held(spec_flags, spec_n, n_iters);
+  const long long total = (long long)(held ? *lds_count : c) * s;
   const int k = stop_iter(mask, n_iters);
-  const float x = snap[((size_t)cell * ms::kSnap + k) * s + j];
-  if (X_out) {
-    X_out[(size_t)cell * s + j] = x;
-    return;
-  }
-  if (j < m) {
-    cell_mols[(size_t)cell * m + j] = x;
-  } else {
-    const size_t pix = (size_t)positions[2 * cell] * C + positions[2 * cell + 1];
-    st_map(molmap, (size_t)(j - m) * R * C + pix, corr_out(x, corr, j - m), map_dtype);
+  for (long long t = t0; t < total; t += (long long)gridDim.x * blockDim.x) {
+    int cell = (int)(t / s);
+    const int j = (int)(t - (long long)cell * s);
+    if (held) cell = lds_list[cell];
+    const float x = snap[((size_t)cell * ms::kSnap + k) * s + j];
+    if (X_out) {
+      X_out[(size_t)cell * s + j] = x;
+    } else if (j < m) {
+      cell_mols[(size_t)cell * m + j] = x;
+    } else {
+      const size_t pix = (size_t)positions[2 * cell] * C + positions[2 * cell + 1];
+      st_map(molmap, (size_t)(j - m) * R * C + pix, corr_out(x, corr, j - m), map_dtype);
+    }
   }
 }
 
@@ -1548,7 +1547,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
   // domain-decomposed caller runs it as a separate call once those flags are global
   if (scatter && part_end == nparts && nparts > 0) {
     const int last = nparts - 1;
-    integrate_scatter_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(
+    integrate_scatter_kernel<<<(unsigned)std::min<long long>(cdiv((long long)c * s, kBlock), 2048), kBlock, 0, st>>>(
         c, s, m, R, C, snaps[last & 1], mk + ms::kEqIters * last, n_iters, P_<int32_t>(positions),
         P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr, X_io ? P_<float>(X_io) : nullptr,
         spec_path ? spec_w : nullptr, spec_path && spec_wb ? spec_w + 4 : nullptr, nparts,
