@@ -1021,7 +1021,7 @@ __global__ void __launch_bounds__(kBlock) gather_bin_kernel(int c, int s, int m,
                                                             const int32_t* positions, const float4* Q,
                                                             const int64_t* prow, float trim0, float* snap,
                                                             int32_t* wide_list, unsigned* wide, unsigned* zero,
-                                                            int nz, int32_t* zero_wc) {
+                                                            int nz, int32_t* zero_wc, float* save) {
   clear_words(zero, nz, zero_wc);
   if (blockIdx.x == 0 && threadIdx.x < ms::kEqIters * kMaxParts + 1) wide[4 + threadIdx.x] = 0u;
   const int lane = threadIdx.x & 31;
@@ -1033,9 +1033,12 @@ __global__ void __launch_bounds__(kBlock) gather_bin_kernel(int c, int s, int m,
       x = X[(size_t)cell * s + lane];
     } else if (lane < m) {
       x = cell_mols[(size_t)cell * m + lane];
+      if (save) save[(size_t)cell * s + lane] = x;
     } else {
       const size_t pix = (size_t)positions[2 * cell] * C + positions[2 * cell + 1];
-      x = corr_in(ld_map(molmap, (size_t)(lane - m) * R * C + pix, map_dtype), corr, lane - m);
+      const float raw = ld_map(molmap, (size_t)(lane - m) * R * C + pix, map_dtype);
+      if (save) save[(size_t)cell * s + lane] = raw;  // cell_state_io layout: (molecules | raw pixels)
+      x = corr_in(raw, corr, lane - m);
     }
     snap[(size_t)cell * ms::kSnap * s + lane] = x;
   }
@@ -1197,6 +1200,9 @@ __global__ void __launch_bounds__(kBlock) build_params_kernel(BuildArgs b) {
 // ---------------------------------------------------------------------------------------------
 // Host launchers
 
+void cell_state_io(int n, int m, uintptr_t pos, int R, int C, uintptr_t map, int dtype, uintptr_t cell_mols,
+                   uintptr_t buf, bool restore, uintptr_t stream);  // maps.hip
+
 static int slot_words_for(int P, int s, int sp) {
   int w = P * sp + P * 8 + 3 * s + 1 + P + (P * s + 3) / 4;
   return (w + 3) & ~3;  // keep every slot 16-byte aligned
@@ -1211,7 +1217,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
                uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
                uintptr_t masks, const std::vector<float>& trims, int n_iters, int part_begin, int part_end,
                bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t map_corr, uintptr_t spec_buf,
-               uintptr_t stream) {
+               uintptr_t save_buf, uintptr_t stream) {
   if (c <= 0) return;
   const float* corr = map_corr ? P_<float>(map_corr) : nullptr;
   if (n_iters < 0 || n_iters > ms::kEqIters) throw std::invalid_argument("n_iters must be in 0..4");
@@ -1238,6 +1244,11 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
   const bool spec_path = fast_path && spec_w != nullptr && s <= 32 && part_begin == 0 && part_end == nparts &&
                          scatter && nparts >= 1 && nparts <= kMaxParts && (nparts & 1) == 1 &&
                          (g_integrate_mode & 0xF8) == 0;
+  // save_buf: the state the activity changes (cell molecules, raw pixels under the cells) for a
+  // speculative activity's rollback (World._speculate) -- written by the speculative path's input
+  // kernel, else by a separate pass first
+  if (save_buf && !X_io && part_begin == 0 && !spec_path)
+    cell_state_io(c, m, positions, R, C, molmap, map_dtype, cell_mols, save_buf, false, stream);
   if (spec_path) {
     const int nz = ms::kEqIters * (nparts + 1);
     int32_t* L = P_<int32_t>(lists);
@@ -1251,7 +1262,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     gather_bin_kernel<<<cdiv(c, kBlock / 32), kBlock, 0, st>>>(
         c, s, m, R, C, P, X_io ? P_<float>(X_io) : nullptr, P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr,
         P_<int32_t>(positions), P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr, trims[0], snaps[1], wl, spec_w, mk,
-        nz, zwc);
+        nz, zwc, X_io ? nullptr : P_<float>(save_buf));
     MS_LAUNCH_CHECK();
     IntegrateArgs a{};
     a.c = c; a.P = P; a.s = s;

@@ -65,7 +65,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
                uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
                uintptr_t masks, const std::vector<float>& trims, int n_iters, int part_begin, int part_end,
                bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t map_corr, uintptr_t spec_buf,
-               uintptr_t stream);
+               uintptr_t save_buf, uintptr_t stream);
 void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_t rows, uintptr_t vmax_w, int nw,
                   uintptr_t km_w, int nk, uintptr_t signs, int nsg, uintptr_t hills, int nh, uintptr_t RM,
                   uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,

@@ -958,13 +958,17 @@ class World:
         if self.n_cells == 0:
             return
         st = self.__dict__.get("_gp_state")
-        spec = None
+        spec = save = None
         if st and st["pending"]:
-            # speculative: issued on top of unconfirmed parameter rebuilds (see _speculate)
+            # speculative: issued on top of unconfirmed parameter rebuilds (see _speculate); the
+            # fused activity snapshots what it changes in its own input pass
             from magicsoup_amd.ops import hip_ops
 
-            spec = hip_ops.save_cell_state(self)
-        world_ops.enzymatic_activity(self)
+            if world_ops.fused_activity(self):
+                spec = save = hip_ops.cell_state_buffer(self)
+            else:
+                spec = hip_ops.save_cell_state(self)
+        world_ops.enzymatic_activity(self, save=save)
         if spec is not None:
             self.__dict__["_spec"] = spec
 

@@ -170,7 +170,7 @@ def pack_params(kin, store: dict, rows: int | None = None) -> None:
 
 
 def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n_iters=4, flags_hook=None,
-                      slot=None):
+                      slot=None, save=None):
     _check_overflow(kin)
     W = p["_W"]
     P, s = int(W.size(1)), int(W.size(2))
@@ -204,16 +204,17 @@ def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n
     if spec is None or spec.device != dev:
         spec = sc.bufs["spec"] = torch.zeros(32, dtype=torch.int32, device=dev)
     if flags_hook is None:
-        _m().integrate(*args, 0, nparts, True, slot_p, _p(lists), mdt, _p(corr), _p(spec), _stream())
+        _m().integrate(*args, 0, nparts, True, slot_p, _p(lists), mdt, _p(corr), _p(spec), _p(save), _stream())
     else:
         # domain-decomposed world: all-reduce each part's iteration flags before the next part (or
         # the final write-back) reads them, reproducing the reference's `torch.any` over the whole
         # population
         for part in range(nparts):
-            _m().integrate(*args, part, part + 1, False, slot_p, _p(lists), mdt, _p(corr), 0, _stream())
+            _m().integrate(*args, part, part + 1, False, slot_p, _p(lists), mdt, _p(corr), 0,
+                           _p(save) if part == 0 else 0, _stream())
             flags_hook(masks[_EQ * part : _EQ * (part + 1)])
         if nparts:
-            _m().integrate(*args, nparts, nparts, True, slot_p, _p(lists), mdt, _p(corr), 0, _stream())
+            _m().integrate(*args, nparts, nparts, True, slot_p, _p(lists), mdt, _p(corr), 0, 0, _stream())
     sc.bufs["pack_overflow_host"].copy_(_overflow_flag(kin), non_blocking=True)
     return masks
 
@@ -230,8 +231,10 @@ def integrate(kin, X: torch.Tensor, p: dict, trims, n_iters: int, slot=None) -> 
     return _flags_to_bits(masks, len(trims))
 
 
-def enzymatic_activity(world) -> None:
-    """Fused gather -> 3-part integrate -> scatter over the world state (no host syncs)."""
+def enzymatic_activity(world, save: torch.Tensor | None = None) -> None:
+    """Fused gather -> 3-part integrate -> scatter over the world state (no host syncs). ``save``
+    (:func:`cell_state_buffer`): also snapshot what the activity changes, as :func:`save_cell_state`
+    (the integrator's input kernel writes it)."""
     kin = world.kinetics
     p = kin._packed_params()
     c = world.n_cells
@@ -239,7 +242,7 @@ def enzymatic_activity(world) -> None:
         raise ValueError("kinetics has fewer cells than the world")
     _ensure_world_layout(world)
     hook = getattr(world, "_allreduce_flags", None)
-    _launch_integrate(kin, p, c, world=world, flags_hook=hook, slot=kin._slot_tensor())
+    _launch_integrate(kin, p, c, world=world, flags_hook=hook, slot=kin._slot_tensor(), save=save)
 
 
 def spawn_issue(world, rows: torch.Tensor, lens: torch.Tensor, n0: int) -> None:
@@ -261,6 +264,13 @@ def spawn_issue(world, rows: torch.Tensor, lens: torch.Tensor, n0: int) -> None:
                    _p(cols["cell_molecules"].buf), _p(mm), _mdt(mm), _p(corr), _p(lab.data), int(lab.width),
                    _p(lab.lens), L_in, _p(rows), _p(lens), _p(g.data), int(g.width), _p(g.lens), _p(failed),
                    _stream())
+
+
+def cell_state_buffer(world) -> torch.Tensor:
+    """The scratch buffer of :func:`save_cell_state` (2 * n_cells * n_molecules floats)."""
+    d = world.__dict__
+    return _scratch(world).get("spec_state", 2 * d["n_cells"] * world.n_molecules, torch.float32,
+                               d["_molmap"].device)
 
 
 def save_cell_state(world) -> torch.Tensor:

@@ -176,10 +176,18 @@ def split_cells(world, parents: torch.Tensor, children: torch.Tensor) -> None:
 
 
 # ---------------------------------------------------------------------------- physics
-def enzymatic_activity(world) -> None:
+def fused_activity(world) -> bool:
+    """Whether :func:`enzymatic_activity` takes the fused device path (which can also snapshot the
+    state it changes, see hip_ops.enzymatic_activity)."""
+    return _is_gpu(world) and not world.kinetics._stages_overridden()
+
+
+def enzymatic_activity(world, save=None) -> None:
     kin = world.kinetics
-    if _is_gpu(world) and not kin._stages_overridden():
-        return _hip().enzymatic_activity(world)
+    if fused_activity(world):
+        return _hip().enzymatic_activity(world, save=save)
+    if save is not None:
+        raise ValueError("save: fused device path only")
     mm = _molmap(world)
     pos = world.cell_positions.long()
     xs, ys = pos[:, 0], pos[:, 1]
