@@ -172,15 +172,6 @@ def _prime_rare_paths(chem, device, mdt, genome_size: int) -> None:
 
 def main():
     a = _args()
-    if a.warmup < 10:
-        # A short warm-up leaves the population's early layout growth inside the timed steps: the
-        # first recombinants outgrow genome rows as wide as the initial genomes within a few steps,
-        # and each widening of the arena replays the pending device-pipeline calls on the host
-        # (17-29 ms). Reserve 2x the initial row width and widen ahead of need instead
-        # (World._watch_genome_width); six alternating driver-style pairs: 716 vs 566 steps/s mean,
-        # no step above 2.3 ms vs three runs with a 21-29 ms step (profiles/r2_s3/spike_ab.txt).
-        os.environ.setdefault("MS_GENOME_HEADROOM_INIT", "2")
-        os.environ.setdefault("MS_GENOME_WIDTH_WATCH", "1")
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
