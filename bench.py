@@ -225,7 +225,8 @@ def main():
         world = ms.World(chemistry=chem, map_size=a.map_size, device=device, seed=a.seed, map_dtype=mdt)
 
     t0 = time.time()
-    if torch.cuda.is_available() and not distributed:
+    if torch.cuda.is_available():
+        # (a plain world on this rank's device: no collectives; the kernels it warms are per process)
         _prime_rare_paths(chem, device, mdt, a.genome_size)
     world.spawn_cells(random_genomes(a.cells // max(1, world_size if distributed else 1), a.genome_size, device))
     setup_s = time.time() - t0
