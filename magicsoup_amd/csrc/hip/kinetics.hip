@@ -135,8 +135,10 @@ __device__ __forceinline__ void or_block_bits(unsigned bits, unsigned* mask_out)
 template <int G>
 __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem, int item, unsigned& bits) {
   const int slot = threadIdx.x / G, lane = threadIdx.x % G;
-  const bool valid = a.list ? item < *a.count : item < a.c;
-  const int cell = valid ? (a.list ? a.list[item] : item) : 0;
+  const bool valid0 = a.list ? item < *a.count : item < a.c;
+  const int cell0 = valid0 ? (a.list ? a.list[item] : item) : 0;
+  const bool valid = valid0 && (unsigned)cell0 < (unsigned)a.c;  // (a list entry is a cell index)
+  const int cell = valid ? cell0 : 0;
   const int P = a.P, s = a.s, SP = a.sp, Ps = a.Ps;
   const size_t prow = valid ? (a.prow ? (size_t)a.prow[cell] : (size_t)cell) : 0;  // parameter row
 
@@ -512,8 +514,10 @@ template <int G, int NZ, bool kSpec = false>
 __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int* smem, int item, unsigned& bits,
                                                     int32_t* wide_list, int32_t* wide_count) {
   const int slot = threadIdx.x / G, lane = threadIdx.x % G;
-  const bool listed = a.list ? item < *a.count : item < a.c;
-  const int cell = listed ? (a.list ? a.list[item] : item) : 0;
+  const bool listed0 = a.list ? item < *a.count : item < a.c;
+  const int cell0 = listed0 ? (a.list ? a.list[item] : item) : 0;
+  const bool listed = listed0 && (unsigned)cell0 < (unsigned)a.c;  // (a list entry is a cell index)
+  const int cell = listed ? cell0 : 0;
   const int P = a.P, s = a.s;
   const size_t prow = listed ? (a.prow ? (size_t)a.prow[cell] : (size_t)cell) : 0;
 
@@ -910,7 +914,10 @@ __global__ void __launch_bounds__(kBlock) integrate_scatter_kernel(int c, int s,
   for (long long t = t0; t < total; t += (long long)gridDim.x * blockDim.x) {
     int cell = (int)(t / s);
     const int j = (int)(t - (long long)cell * s);
-    if (held) cell = lds_list[cell];
+    if (held) {
+      cell = lds_list[cell];
+      if ((unsigned)cell >= (unsigned)c) continue;
+    }
     const float x = snap[((size_t)cell * ms::kSnap + k) * s + j];
     if (X_out) {
       X_out[(size_t)cell * s + j] = x;
@@ -1250,6 +1257,17 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
   if (save_buf && !X_io && part_begin == 0 && !spec_path)
     cell_state_io(c, m, positions, R, C, molmap, map_dtype, cell_mols, save_buf, false, stream);
   if (spec_path) {
+    // LDS sizing of the list / fallback launches first: nothing may throw once the input kernel has
+    // appended to the wide list (its count is only reset by the write-back at the end)
+    const int sp = (s % 2 == 0) ? s + 1 : s;
+    const int slot_words = slot_words_for(P, s, sp);
+    const size_t slot_bytes = (size_t)slot_words * 4;
+    int cps = kBlock / 32;
+    while (cps > 1 && cps * slot_bytes > 64 * 1024) --cps;
+    const size_t lds = cps * slot_bytes;
+    if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
+    const long long per_cu = std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)lds));
+    const unsigned grid = (unsigned)std::min<long long>(cdiv(c, cps), 256 * per_cu);
     const int nz = ms::kEqIters * (nparts + 1);
     int32_t* L = P_<int32_t>(lists);
     int32_t* wl = L + c;                    // wide list (more than 32 active proteins)
@@ -1274,7 +1292,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     a.mask_out = sflags;
     a.trim = trims[0];
     a.n_iters = n_iters;
-    a.sp = (s % 2 == 0) ? s + 1 : s;
+    a.sp = sp;
     a.prow = prow ? P_<int64_t>(prow) : nullptr;
     a.spec_parts = nparts;
     for (int p = 0; p < nparts; ++p) a.trims[p] = trims[p];
@@ -1311,15 +1329,6 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     const size_t lds_fw = (size_t)(kBlock / 64) * fast_slot_words<64, kNzWide>() * 4;
     integrate_fast_kernel<64, kNzWide, true, true><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
     MS_LAUNCH_CHECK();
-    const int sp = a.sp;
-    const int slot_words = slot_words_for(P, s, sp);
-    const size_t slot_bytes = (size_t)slot_words * 4;
-    int cps = kBlock / 32;
-    while (cps > 1 && cps * slot_bytes > 64 * 1024) --cps;
-    const size_t lds = cps * slot_bytes;
-    if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
-    const long long per_cu = std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)lds));
-    const unsigned grid = (unsigned)std::min<long long>(cdiv(c, cps), 256 * per_cu);
     // the cells neither register launch took, all parts on the LDS path (rare: usually an empty list)
     {
       IntegrateArgs l = a;
