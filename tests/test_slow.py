@@ -182,11 +182,14 @@ def test_genomes_are_always_translated_reproduceably():
 
 def test_point_mutations_at_scale():
     for _ in range(3):
-        # ~1 mutation per genome: a substitution can draw the same nt, so a few stay unchanged
+        # ~1 mutation per genome: a substitution can draw the same nt (p = 0.6 * 1/4 per mutation),
+        # so about 9.4 % of the ~630 mutated genomes stay unchanged: expected fraction 0.906,
+        # sigma ~0.011. The reference's bound (0.9, tests/slow/test_mutations.py:14, "highly likely")
+        # sits half a sigma below the mean and fails about one draw in three; 5 sigma here.
         genomes = gen_genomes(n=1000, s=10_000)
         res = muts.point_mutations(seqs=genomes, p=1e-4)
         assert 0 < len(res) <= len(genomes)
-        assert sum(genomes[i] != d for d, i in res) / len(res) > 0.9
+        assert sum(genomes[i] != d for d, i in res) / len(res) > 0.85
 
 
 def test_recombinations_at_scale():
