@@ -13,8 +13,10 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <mutex>
 #include <stdexcept>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -124,6 +126,45 @@ std::string rccl_async_error(uintptr_t comm) {
   ncclResult_t r = ncclSuccess;
   check(api().CommGetAsyncError(C_(comm), &r), "ncclCommGetAsyncError");
   return r == ncclSuccess ? std::string() : std::string(api().GetErrorString(r));
+}
+
+// Wait for the work queued on `stream` while polling the communicators for asynchronous errors
+// (a dead peer leaves an RCCL kernel waiting forever: a plain hipStreamSynchronize would hang).
+// Returns "" when the stream drained; otherwise every communicator in `comms` is aborted (its
+// kernels are released, the handles become unusable) and the reason is returned: the RCCL error,
+// or "timeout" after `timeout_s` seconds.
+std::string rccl_guarded_wait(const std::vector<uintptr_t>& comms, uintptr_t stream, double timeout_s) {
+  const Rccl& r = api();
+  hipStream_t s = S_(stream);
+  const auto t0 = std::chrono::steady_clock::now();
+  std::string why;
+  for (long long it = 0;; ++it) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return std::string();
+    if (q != hipErrorNotReady) MS_HIP_CHECK(q);
+    // errors are polled every 256 queries (~tens of microseconds): the common case (a healthy job
+    // waiting for its own kernels) stays a tight query loop
+    if ((it & 255) == 255) {
+      for (uintptr_t c : comms) {
+        if (!c) continue;
+        ncclResult_t e = ncclSuccess;
+        if (r.CommGetAsyncError(C_(c), &e) != ncclSuccess || (e != ncclSuccess && e != ncclInProgress)) {
+          why = std::string("rccl: asynchronous error: ") + r.GetErrorString(e);
+          break;
+        }
+      }
+      if (!why.empty()) break;
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el > timeout_s) {
+        why = "timeout";
+        break;
+      }
+      std::this_thread::yield();
+    }
+  }
+  for (uintptr_t c : comms)
+    if (c) (void)r.CommAbort(C_(c));
+  return why;
 }
 
 // In-place all-reduce of `count` elements. dtype: 0 int32, 1 float32, 2 float64, 3 int64;

@@ -26,6 +26,7 @@ void place_rounds_mask(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r
 void set_coop_blocks(int n);
 void set_stencil_blocks(int n);
 void set_place_mode(int mode);
+int place_error_take();
 void neighbor_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map, uintptr_t keys,
                     uintptr_t stream);
 void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
@@ -139,6 +140,7 @@ std::string rccl_unique_id();
 uintptr_t rccl_init(const std::string& uid, int nranks, int rank);
 void rccl_destroy(uintptr_t comm, bool abort);
 std::string rccl_async_error(uintptr_t comm);
+std::string rccl_guarded_wait(const std::vector<uintptr_t>& comms, uintptr_t stream, double timeout_s);
 void rccl_allreduce(uintptr_t comm, uintptr_t buf, long long count, int dtype, int op, uintptr_t stream);
 void rccl_exchange(uintptr_t comm, int up, int down, uintptr_t send_up, long long n_send_up, uintptr_t send_down,
                    long long n_send_down, uintptr_t recv_down, long long n_recv_down, uintptr_t recv_up,
@@ -187,6 +189,12 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("next_call", []() { return py::make_tuple(g_seed.load(), g_call.fetch_add(1) + 1); },
         "(seed, call) for a fresh Philox stream family");
+  m.def("get_rng_state", []() { return py::make_tuple(g_seed.load(), g_call.load()); },
+        "(seed, calls drawn) of the device Philox streams");
+  m.def("set_rng_state", [](uint64_t s, uint64_t c) {
+    g_seed.store(s);
+    g_call.store(c);
+  }, "restore a get_rng_state() value");
   m.def("device_arch", []() {
     hipDeviceProp_t p;
     int dev = 0;
@@ -215,6 +223,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("set_coop_blocks", &msd::set_coop_blocks, "workgroups of the cooperative placement (A/B)");
   m.def("set_stencil_blocks", &msd::set_stencil_blocks, "blocks of the vector diffusion stencil (0: one per tile)");
   m.def("set_place_mode", &msd::set_place_mode, "0 cooperative single launch (default), 1 multi-launch rounds");
+  m.def("place_error_take", &msd::place_error_take,
+        "1 if a cooperative placement's grid barrier timed out since the last call (clears the flag)");
   m.def("split_cells", &msd::split_cells);
   m.def("permeate", &msd::permeate);
   m.def("claim_free", &msd::claim_free);
@@ -252,6 +262,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("rccl_init", [](py::bytes uid, int nranks, int rank) { return msd::rccl_init(std::string(uid), nranks, rank); });
   m.def("rccl_destroy", &msd::rccl_destroy);
   m.def("rccl_async_error", &msd::rccl_async_error);
+  m.def("rccl_guarded_wait", &msd::rccl_guarded_wait, py::call_guard<py::gil_scoped_release>(),
+        "wait for a stream while polling RCCL errors; aborts the communicators on error / timeout");
   m.def("rccl_allreduce", &msd::rccl_allreduce, "in-place all-reduce on a stream (dtype 0 i32 1 f32 2 f64 3 i64; op 0 sum 1 max 2 min)");
   m.def("rccl_exchange", &msd::rccl_exchange, "grouped byte send/recv with the up / down neighbours on a stream");
   m.def("strip_marks", &msd::strip_marks, "boundary-row bytes (1 occupied, 3 dividing) for the strip neighbours");

@@ -11,6 +11,7 @@
 //                         indices; the last tile writes {count, max} straight into pinned host memory
 //
 // Predicates: u8 mask != 0, u8 mask == 0, int32 > 0, int64 >= 0.
+#include <unordered_map>
 #include <algorithm>
 #include <tuple>
 
@@ -183,8 +184,26 @@ __global__ void __launch_bounds__(256) translate_stats_kernel(int n, const int32
 namespace {
 int32_t* g_host = nullptr;  // pinned, coherent {count, max}
 int32_t* g_host_dev = nullptr;
-int32_t* g_tiles = nullptr;  // device {count[tiles], max[tiles]}
-long long g_tiles_cap = 0;
+// device {count[tiles], max[tiles]} per stream: selections on different streams (the compute
+// stream and the genome chains' side stream) may run at the same time
+struct TileBuf {
+  int32_t* p = nullptr;
+  long long cap = 0;
+};
+std::unordered_map<hipStream_t, TileBuf> g_tiles;
+// the tile buffer of stream s with room for `tiles` tiles: {counts, maxima}
+std::pair<int32_t*, int32_t*> tiles_for(hipStream_t s, long long tiles) {
+  TileBuf& b = g_tiles[s];
+  if (tiles > b.cap) {
+    if (b.p) {
+      MS_HIP_CHECK(hipStreamSynchronize(s));  // the old buffer may still be read by this stream
+      MS_HIP_CHECK(hipFree(b.p));
+    }
+    b.cap = std::max(tiles, 256ll);
+    MS_HIP_CHECK(hipMalloc((void**)&b.p, 2 * b.cap * sizeof(int32_t)));
+  }
+  return {b.p, b.p + b.cap};
+}
 int32_t* g_tacc = nullptr;  // device {max proteins, max domains, done blocks}, zero between calls
 
 void ensure_host() {
@@ -336,17 +355,10 @@ int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, ui
   }
   if (n >= (1ll << 40)) throw std::invalid_argument("select_indices_async: n too large");
   const long long tiles = (n + kSelTile - 1) / kSelTile;
-  if (tiles > g_tiles_cap) {
-    if (g_tiles) {
-      MS_HIP_CHECK(hipStreamSynchronize(s));
-      MS_HIP_CHECK(hipFree(g_tiles));
-    }
-    g_tiles_cap = std::max(tiles, 256ll);
-    MS_HIP_CHECK(hipMalloc((void**)&g_tiles, 2 * g_tiles_cap * sizeof(int32_t)));
-  }
   const void* sp = reinterpret_cast<const void*>(src);
-  int32_t* tc = g_tiles;
-  int32_t* tm = g_tiles + g_tiles_cap;
+  auto tb = tiles_for(s, tiles);
+  int32_t* tc = tb.first;
+  int32_t* tm = tb.second;
   int32_t* out = P_<int32_t>(out_dev);
 #define MS_SEL(K)                                                                                                \
   select_count_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, nullptr, tc, tm);                      \
@@ -379,17 +391,13 @@ std::pair<long long, int> select_indices(long long n, int kind, uintptr_t src, u
   if (n >= (1ll << 40)) throw std::invalid_argument("select_indices: n too large");
   ensure_host();
   const long long tiles = (n + kSelTile - 1) / kSelTile;
-  if (tiles > g_tiles_cap) {
-    if (g_tiles) MS_HIP_CHECK(hipFree(g_tiles));
-    g_tiles_cap = std::max(tiles, 256ll);
-    MS_HIP_CHECK(hipMalloc((void**)&g_tiles, 2 * g_tiles_cap * sizeof(int32_t)));
-  }
   g_host[0] = -1;
   hipStream_t s = S_(stream);
   const void* sp = reinterpret_cast<const void*>(src);
   const int32_t* vp = vals ? P_<int32_t>(vals) : nullptr;
-  int32_t* tc = g_tiles;
-  int32_t* tm = g_tiles + g_tiles_cap;
+  auto tb = tiles_for(s, tiles);
+  int32_t* tc = tb.first;
+  int32_t* tm = tb.second;
 #define MS_SEL(K)                                                                                               \
   select_count_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, vp, tc, tm);                          \
   MS_LAUNCH_CHECK();                                                                                            \
@@ -420,17 +428,10 @@ void select_indices_capped(long long n, int kind, uintptr_t src, uintptr_t sel, 
   }
   if (n >= (1ll << 40)) throw std::invalid_argument("select_indices_capped: n too large");
   const long long tiles = (n + kSelTile - 1) / kSelTile;
-  if (tiles > g_tiles_cap) {
-    if (g_tiles) {
-      MS_HIP_CHECK(hipStreamSynchronize(s));
-      MS_HIP_CHECK(hipFree(g_tiles));
-    }
-    g_tiles_cap = std::max(tiles, 256ll);
-    MS_HIP_CHECK(hipMalloc((void**)&g_tiles, 2 * g_tiles_cap * sizeof(int32_t)));
-  }
   const void* sp = reinterpret_cast<const void*>(src);
-  int32_t* tc = g_tiles;
-  int32_t* tm = g_tiles + g_tiles_cap;
+  auto tb = tiles_for(s, tiles);
+  int32_t* tc = tb.first;
+  int32_t* tm = tb.second;
 #define MS_SEL(K)                                                                                                \
   select_count_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, nullptr, tc, tm);                      \
   MS_LAUNCH_CHECK();                                                                                             \
@@ -449,17 +450,7 @@ void select_indices_capped(long long n, int kind, uintptr_t src, uintptr_t sel, 
 // The tile buffers ({count, max} per tile, `tiles` entries each) for a caller whose own kernel
 // produces the selected counts of an int32 > 0 selection, `sub` per kSelTile items (world.hip
 // rec_slots), and the write pass of select_indices_capped over them.
-std::pair<int32_t*, int32_t*> select_tiles(long long tiles, hipStream_t s) {
-  if (tiles > g_tiles_cap) {
-    if (g_tiles) {
-      MS_HIP_CHECK(hipStreamSynchronize(s));
-      MS_HIP_CHECK(hipFree(g_tiles));
-    }
-    g_tiles_cap = std::max(tiles, 256ll);
-    MS_HIP_CHECK(hipMalloc((void**)&g_tiles, 2 * g_tiles_cap * sizeof(int32_t)));
-  }
-  return {g_tiles, g_tiles + g_tiles_cap};
-}
+std::pair<int32_t*, int32_t*> select_tiles(long long tiles, hipStream_t s) { return tiles_for(s, tiles); }
 
 void select_write_i32pos_capped(long long n, uintptr_t src, int32_t* tc, int32_t* tm, int sub, uintptr_t sel,
                                 uintptr_t out_dev, int cap, uintptr_t gflags, uintptr_t opflags, hipStream_t s) {
@@ -493,18 +484,11 @@ void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, ui
   }
   if (n >= (1ll << 40)) throw std::invalid_argument("select_indices_dev: n too large");
   const long long tiles = (n + kSelTile - 1) / kSelTile;
-  if (tiles > g_tiles_cap) {
-    if (g_tiles) {
-      MS_HIP_CHECK(hipStreamSynchronize(s));  // the old tile buffer may still be read
-      MS_HIP_CHECK(hipFree(g_tiles));
-    }
-    g_tiles_cap = std::max(tiles, 256ll);
-    MS_HIP_CHECK(hipMalloc((void**)&g_tiles, 2 * g_tiles_cap * sizeof(int32_t)));
-  }
   const void* sp = reinterpret_cast<const void*>(src);
   const int32_t* vp = vals ? P_<int32_t>(vals) : nullptr;
-  int32_t* tc = g_tiles;
-  int32_t* tm = g_tiles + g_tiles_cap;
+  auto tb = tiles_for(s, tiles);
+  int32_t* tc = tb.first;
+  int32_t* tm = tb.second;
   int32_t* out = P_<int32_t>(out_dev);
 #define MS_SEL(K)                                                                                                \
   select_count_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, vp, tc, tm);                           \

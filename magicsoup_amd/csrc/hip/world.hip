@@ -280,14 +280,15 @@ __global__ void __launch_bounds__(1024) place_rounds_wg_kernel(int k, const int6
 // cell i itself for i < k with `mask[i]` selecting the cells that take part (divide_cells(mask):
 // no index compaction and no host round trip before placement).
 // ctl: unsigned[2 + kMaxRounds], zeroed before the launch (barrier counter, pending per round,
-// barrier-timeout error word).
+// barrier-timeout error word). A barrier timeout is also reported in `err_host` (pinned, mapped),
+// which the host checks after the placement's one synchronisation (place_error_take).
 constexpr int kMaxRounds = 16;
 
 // Grid-wide barrier of a cooperative launch. Data shared between workgroups of different XCDs
 // (their L2s are not coherent for ordinary device memory) is only touched with device-scope atomics
 // in the cooperative kernel, so the barrier needs no cache write-back / invalidation: each wave
 // waits for its own memory operations, then one thread per workgroup arrives and spins.
-__device__ __forceinline__ void grid_barrier(unsigned* ctr, unsigned nblocks, unsigned& phase) {
+__device__ __forceinline__ void grid_barrier(unsigned* ctr, unsigned nblocks, unsigned& phase, unsigned* err_host) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -298,6 +299,7 @@ __device__ __forceinline__ void grid_barrier(unsigned* ctr, unsigned nblocks, un
     for (long long spin = 0; __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
       if (spin > (1ll << 24)) {
         __hip_atomic_store(ctr + kMaxRounds + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (err_host) __hip_atomic_store(err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -323,7 +325,8 @@ __global__ void __launch_bounds__(256) place_rounds_coop_kernel(int k, const int
                                                                 const int32_t* pos, Geom g, bool vacate,
                                                                 uint8_t* cell_map, uint8_t* pending, uint64_t seed,
                                                                 uint64_t call, long long* cand, int* claim,
-                                                                long long* result, int rounds, unsigned* ctl) {
+                                                                long long* result, int rounds, unsigned* ctl,
+                                                                unsigned* err_host) {
   const unsigned nb = gridDim.x;
   const int stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
   unsigned phase = 0;
@@ -353,7 +356,7 @@ __global__ void __launch_bounds__(256) place_rounds_coop_kernel(int k, const int
       cand[i] = px;
       atomicMin(claim + px, i);
     }
-    grid_barrier(ctl, nb, phase);
+    grid_barrier(ctl, nb, phase, err_host);
     if (threadIdx.x == 0) s_left = 0;
     __syncthreads();
     int left = 0;
@@ -376,7 +379,7 @@ __global__ void __launch_bounds__(256) place_rounds_coop_kernel(int k, const int
     if (left) atomicAdd(&s_left, left);
     __syncthreads();
     if (threadIdx.x == 0 && s_left) atomicAdd(ctl + 1 + r, (unsigned)s_left);
-    grid_barrier(ctl, nb, phase);
+    grid_barrier(ctl, nb, phase, err_host);
     if (__hip_atomic_load(ctl + 1 + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) break;
   }
   // winners release their pixels' claims (losers never hold one: a pixel's claim is its winner)
@@ -535,8 +538,19 @@ void claim_free(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uin
 constexpr int kPlaceWgMax = 2048;  // single-workgroup rounds up to this many cells (one CU: ~2 cells per thread)
 static int g_coop_blocks = 256;    // co-resident workgroups of the cooperative placement (one per CU; 128: +18 % time)
 static int g_place_mode = 0;       // 0 cooperative, 1 multi-launch rounds (A/B, set_place_mode)
-static unsigned* g_place_ctl = nullptr;
+constexpr int kMaxDevices = 64;
+static unsigned* g_place_ctl[kMaxDevices] = {};  // per device: the control words of the cooperative launch
+static unsigned* g_place_err = nullptr;           // pinned, mapped: a barrier timed out (any device)
+static unsigned* g_place_err_dev = nullptr;
 void set_place_mode(int mode) { g_place_mode = mode; }
+
+// 1 if a cooperative placement's grid barrier timed out since the last call (then its claims may
+// have raced: the caller treats the world state as corrupt); clears the word.
+int place_error_take() {
+  if (!g_place_err) return 0;
+  const unsigned v = __atomic_exchange_n(g_place_err, 0u, __ATOMIC_ACQ_REL);
+  return v ? 1 : 0;
+}
 void set_coop_blocks(int n) { g_coop_blocks = std::max(1, std::min(n, 1024)); }
 
 // Cooperative placement over `cells` (k entries) or over cells 0..k-1 selected by `mask`; returns
@@ -544,8 +558,16 @@ void set_coop_blocks(int n) { g_coop_blocks = std::max(1, std::min(n, 1024)); }
 static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, const Geom& g, bool vacate,
                        uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result,
                        int rounds, uint64_t seed, uint64_t call, hipStream_t s) {
-  if (!g_place_ctl) MS_HIP_CHECK(hipMalloc((void**)&g_place_ctl, (2 + kMaxRounds) * sizeof(unsigned)));
-  MS_HIP_CHECK(hipMemsetAsync(g_place_ctl, 0, (2 + kMaxRounds) * sizeof(unsigned), s));
+  int dev = 0;
+  MS_HIP_CHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= kMaxDevices) throw std::runtime_error("place_coop: device index out of range");
+  if (!g_place_ctl[dev]) MS_HIP_CHECK(hipMalloc((void**)&g_place_ctl[dev], (2 + kMaxRounds) * sizeof(unsigned)));
+  if (!g_place_err) {
+    MS_HIP_CHECK(hipHostMalloc((void**)&g_place_err, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
+    *g_place_err = 0;
+    MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_place_err_dev, g_place_err, 0));
+  }
+  MS_HIP_CHECK(hipMemsetAsync(g_place_ctl[dev], 0, (2 + kMaxRounds) * sizeof(unsigned), s));
   int kk = k;
   const int64_t* cp = cells ? P_<int64_t>(cells) : nullptr;
   const uint8_t* mp = mask ? P_<uint8_t>(mask) : nullptr;
@@ -556,10 +578,11 @@ static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, co
   int* cl = P_<int>(claim);
   long long* res = P_<long long>(result);
   int rr = std::min(rounds, kMaxRounds);
-  unsigned* ctl = g_place_ctl;
+  unsigned* ctl = g_place_ctl[dev];
+  unsigned* err = g_place_err_dev;
   Geom gg = g;
   bool vac = vacate;
-  void* args[] = {&kk, &cp, &mp, &pp, &gg, &vac, &cm, &pend, &seed, &call, &cd, &cl, &res, &rr, &ctl};
+  void* args[] = {&kk, &cp, &mp, &pp, &gg, &vac, &cm, &pend, &seed, &call, &cd, &cl, &res, &rr, &ctl, &err};
   const unsigned grid = std::min<unsigned>(cdiv(k, 256), (unsigned)g_coop_blocks);
   const hipError_t e = hipLaunchCooperativeKernel((const void*)place_rounds_coop_kernel, dim3(grid), dim3(256), args,
                                                   0, s);

@@ -19,6 +19,12 @@ void set_seed(uint64_t seed) {
   g_seed.store(seed);
   g_calls.store(0);
 }
+// (seed, calls drawn): the whole state of the host streams, for checkpoints
+std::pair<uint64_t, uint64_t> get_rng_state() { return {g_seed.load(), g_calls.load()}; }
+void set_rng_state(uint64_t seed, uint64_t calls) {
+  g_seed.store(seed);
+  g_calls.store(calls);
+}
 
 int seq_index(const std::string& s) {
   int v = 0;
@@ -249,6 +255,8 @@ void bind_genetics(py::module_& m) {
   m.def("extract_domains", &extract_domains);
   m.def("reverse_complement", &reverse_complement);
   m.def("set_seed", &set_seed, "Seed the host RNG streams (mutations, placement).");
+  m.def("get_rng_state", &get_rng_state, "(seed, calls) of the host RNG streams");
+  m.def("set_rng_state", &set_rng_state, "restore a get_rng_state() value");
 }
 
 }  // namespace ms_host

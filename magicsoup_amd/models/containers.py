@@ -97,6 +97,11 @@ class Molecule:
     def __getnewargs__(self):
         return (self.name, self.energy, self.half_life, self.diffusivity, self.permeability)
 
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+        # string hashes are salted per process: a pickled hash would break dict lookups here
+        self._hash = hash(self.name)
+
     def __hash__(self) -> int:
         return self._hash
 

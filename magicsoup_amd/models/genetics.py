@@ -157,6 +157,13 @@ class Genetics:
         state["_device_luts"] = {}
         return state
 
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+        # (a reference pickle has no native-table cache)
+        self.__dict__.setdefault("_tables", None)
+        self.__dict__.setdefault("_tables_key", None)
+        self.__dict__.setdefault("_device_luts", {})
+
     # ------------------------------------------------------------------ API
     def translate_genomes(self, genomes: list[str]) -> list[list[ProteinSpecType]]:
         """Translate genomes into proteome specifications.

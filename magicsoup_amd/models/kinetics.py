@@ -971,6 +971,14 @@ class Kinetics:
         state["_nrows"] = n
         return state
 
+    def __setstate__(self, state):
+        if "_store_d" not in state and "N" in state:
+            # a reference pickle (magicsoup.kinetics.Kinetics, kinetics.py:390-460)
+            from magicsoup_amd.utils.checkpoint import reference_kinetics_state
+
+            state = reference_kinetics_state(state)
+        self.__dict__.update(state)
+
     def _i32_tensor(self, d: Any) -> torch.Tensor:
         return torch.tensor(d, device=self.device, dtype=torch.int32)
 

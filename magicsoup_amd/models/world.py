@@ -408,6 +408,10 @@ class World:
 
     def __setattr__(self, name, value):
         cols = self.__dict__.get("_cols")
+        if self.__dict__.get("_spec") is not None and (name == "molecule_map" or (cols is not None and name in cols)):
+            # a speculative activity is confirmed (or redone) before the user's values replace the
+            # state it changed: a later rollback must not overwrite them
+            self._reconcile()
         if cols is not None and name in cols:
             t = torch.as_tensor(value, device=self.device)
             want = torch.float32 if name == "cell_molecules" else torch.int32
@@ -772,6 +776,7 @@ class World:
                  (sb[:n], sb[n : 2 * n])]
         hip_ops.gather_rows(pairs, n, src_rows=par, dn=dcount)
         k = hip_ops.wait_count(slot)
+        hip_ops.check_placement()
         if k == 0:
             empty = torch.zeros(0, dtype=torch.long, device=self.device)
             return empty, empty
@@ -1128,6 +1133,11 @@ class World:
         return state
 
     def __setstate__(self, state):
+        if "_cols" not in state and "cell_molecules" in state:
+            # a reference pickle (magicsoup.world.World, world.py:161-204): convert its layout
+            from magicsoup_amd.utils.checkpoint import reference_world_state
+
+            state = reference_world_state(state)
         dev = torch.device(state["device"] if torch.cuda.is_available() else "cpu")
         if dev.type == "cpu":
             state["device"] = "cpu"
@@ -1174,20 +1184,22 @@ class World:
 
     @_op("save_state")
     def save_state(self, statedir: Path):
-        """Write the current state (tensors + ``cells.fasta``) in the reference's format."""
+        """Write the current state (tensors + ``cells.fasta``) in the reference's format, plus the
+        random streams (``rng_state.pt``, ignored by the reference)."""
         self._reconcile()
         from magicsoup_amd.utils.checkpoint import save_state
 
         save_state(self, Path(statedir))
 
     @_op("load_state")
-    def load_state(self, statedir: Path, ignore_cell_params: bool = False):
+    def load_state(self, statedir: Path, ignore_cell_params: bool = False, restore_rng: bool = True):
         """Load a state written by :meth:`save_state` (re-translating genomes unless
-        ``ignore_cell_params``)."""
+        ``ignore_cell_params``). If the state holds an ``rng_state.pt`` (written by this package),
+        the random streams are restored too (``restore_rng``), so the run continues exactly."""
         self._reconcile()
         from magicsoup_amd.utils.checkpoint import load_state
 
-        load_state(self, Path(statedir), ignore_cell_params=ignore_cell_params)
+        load_state(self, Path(statedir), ignore_cell_params=ignore_cell_params, restore_rng=restore_rng)
 
     # ------------------------------------------------------------------ internals
     def _as_packed(self, genomes) -> tuple[torch.Tensor, torch.Tensor]:

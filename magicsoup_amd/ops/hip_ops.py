@@ -127,9 +127,31 @@ def select_async(src: torch.Tensor, kind: str, rest: bool = False):
     return sel, rst, dcount, slot
 
 
+_GUARD: list = []  # magicsoup_amd.parallel.comm.guarded_sync once a native communicator exists
+
+
 def wait_count(slot: int) -> int:
-    """Synchronise the current stream and read a :func:`select_async` count."""
+    """Synchronise the current stream and read a :func:`select_async` count (with RCCL
+    communicators alive, the wait polls them for peer failures first: a dead peer raises
+    ``CommError`` instead of hanging the host)."""
+    if _GUARD:
+        _GUARD[0]()
     return int(_m().stream_sync_read(slot, _stream())[0])
+
+
+def guarded_sync() -> None:
+    """Before a blocking read-back of a decomposed world: wait for the current stream with peer
+    failure detection (no-op without native communicators)."""
+    if _GUARD:
+        _GUARD[0]()
+
+
+def check_placement() -> None:
+    """Raise if a cooperative placement's grid barrier timed out (its claims may have raced, so two
+    cells could share a pixel). Called after the synchronisation that follows a placement."""
+    if _m().place_error_take():
+        raise RuntimeError("cell placement: a grid barrier of the cooperative launch timed out; the occupancy "
+                           "map may be inconsistent")
 
 
 # ---------------------------------------------------------------------------- geometry
@@ -630,6 +652,7 @@ def _place_rounds(world, cells: torch.Tensor, vacate: bool, rounds: int = _PLACE
     dev = cells.device
     result = place_rounds_raw(world, cells, vacate, rounds)
     wins = select(result, "i64nonneg")[0]
+    check_placement()
     k2 = int(wins.numel())
     par = torch.empty(k2, dtype=torch.int64, device=dev)
     npos = torch.empty(k2, 2, dtype=torch.int32, device=dev)
@@ -651,6 +674,7 @@ def divide_placement_mask(world, mask: torch.Tensor, alloc_pos=None):
     dev = mask.device
     result = place_rounds_raw(world, None, mask=mask)
     wins = select(result, "i64nonneg")[0]
+    check_placement()
     k2 = int(wins.numel())
     par = torch.empty(k2, dtype=torch.int64, device=dev)
     npos = alloc_pos(k2) if alloc_pos is not None else torch.empty(k2, 2, dtype=torch.int32, device=dev)

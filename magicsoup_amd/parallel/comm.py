@@ -18,6 +18,7 @@ below (the torus wraps, so with two ranks ``up == down``).
 from __future__ import annotations
 
 import atexit
+import datetime
 import os
 import weakref
 
@@ -25,12 +26,37 @@ import torch
 import torch.distributed as dist
 
 _LIVE: "weakref.WeakSet" = weakref.WeakSet()
+# fail-stop bound of every blocking wait on a peer (seconds): a rank whose neighbour died raises
+# instead of hanging (RCCL: guarded stream waits, gloo: work timeouts)
+TIMEOUT_S = float(os.environ.get("MS_COMM_TIMEOUT_S", "300"))
+
+
+class CommError(RuntimeError):
+    """A peer failed or did not answer within ``MS_COMM_TIMEOUT_S``; the communicators of this
+    process are aborted (the job is fail-stop: restart from a checkpoint)."""
+
+
+def guarded_sync() -> None:
+    """Wait for the current HIP stream while polling every live RCCL communicator of this process
+    for asynchronous errors, with the :data:`TIMEOUT_S` bound. On a failure all communicators are
+    aborted and :class:`CommError` is raised. Called before the host synchronisations of a
+    decomposed world's step (magicsoup_amd.ops.hip_ops.wait_count)."""
+    live = [c for c in list(_LIVE) if getattr(c, "handle", 0)]
+    if not live:
+        return
+    m = live[0]._m
+    why = m.rccl_guarded_wait([c.handle for c in live], live[0]._stream(), TIMEOUT_S)
+    if why:
+        for c in live:
+            c.handle = 0  # aborted by the wait
+        raise CommError(f"communication failed ({why}): a peer rank died or stalled")
 
 
 @atexit.register
 def _close_all() -> None:
     """Destroy native communicators before interpreter / library teardown (their proxy threads
-    must not outlive the HIP runtime)."""
+    must not outlive the HIP runtime). Never blocks past :data:`TIMEOUT_S`: a communicator with an
+    error, or a device that does not drain, is aborted instead."""
     for c in list(_LIVE):
         try:
             c.close()
@@ -77,6 +103,13 @@ class TorchComm:
             return
         self._p2p(to_up, to_down, from_down, from_up)
 
+    @staticmethod
+    def _wait(work) -> None:
+        try:
+            work.wait(datetime.timedelta(seconds=TIMEOUT_S))
+        except RuntimeError as e:  # gloo: timeout or a closed connection (peer died)
+            raise CommError(f"communication failed: {e}") from e
+
     def _p2p(self, to_up, to_down, from_down, from_up) -> None:
         ops = []
         g = self.group
@@ -90,16 +123,16 @@ class TorchComm:
             ops.append(dist.P2POp(dist.irecv, from_up, self.up, g, 1))
         if ops:
             for req in dist.batch_isend_irecv(ops):
-                req.wait()
+                self._wait(req)
 
     def allreduce_(self, t: torch.Tensor, op: str = "sum") -> None:
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
         if self.stage:
             h = t.cpu()
-            dist.all_reduce(h, op=rop, group=self.group)
+            self._wait(dist.all_reduce(h, op=rop, group=self.group, async_op=True))
             t.copy_(h)
         else:
-            dist.all_reduce(t, op=rop, group=self.group)
+            self._wait(dist.all_reduce(t, op=rop, group=self.group, async_op=True))
 
     def close(self) -> None:
         pass
@@ -128,6 +161,10 @@ class RcclComm:
         with torch.cuda.device(torch.device(device)):
             self.handle = m.rccl_init(uid[0], size, rank)
         _LIVE.add(self)
+        from magicsoup_amd.ops import hip_ops
+
+        if not hip_ops._GUARD:
+            hip_ops._GUARD.append(guarded_sync)
         self._raw_stream = torch._C._cuda_getCurrentRawStream
         self._cur_device = torch._C._cuda_getDevice
 
@@ -155,11 +192,22 @@ class RcclComm:
             raise RuntimeError(f"RCCL communicator error: {err}")
 
     def close(self) -> None:
-        """Destroy the communicator (collective: every rank closes at the same point)."""
-        if getattr(self, "handle", 0):
-            torch.cuda.synchronize()
-            self._m.rccl_destroy(self.handle, False)
+        """Destroy the communicator (collective: every rank closes at the same point). If the
+        communicator reported an error, or the device does not drain within :data:`TIMEOUT_S`
+        (a peer died mid-exchange), it is aborted instead, so exit never hangs."""
+        h = getattr(self, "handle", 0)
+        if not h:
+            return
+        if self._m.rccl_async_error(h):
             self.handle = 0
+            self._m.rccl_destroy(h, True)
+            return
+        why = self._m.rccl_guarded_wait([h], self._stream(), TIMEOUT_S)
+        self.handle = 0
+        if why:
+            return  # aborted by the wait
+        torch.cuda.synchronize()
+        self._m.rccl_destroy(h, False)
 
 
 def make_comm(group, rank: int, size: int, device):

@@ -427,7 +427,9 @@ class DistributedWorld(World):
             st = sc.get("dv_status", 20, torch.int32, dv)
             strip.split_winners_gpu(self, cells, result, par, npos, st)
             self._exchange(st[4:8], st[8:12], st[16:20], st[12:16])
+            hip_ops.guarded_sync()  # (peer failures raise instead of hanging the read-back)
             v = st.tolist()  # the one synchronisation: local winner counts + the neighbours' headers
+            hip_ops.check_placement()
             n_loc, n_up, n_dn = v[0], v[1], v[2]
             hdr_up, hdr_dn = v[12:16], v[16:20]
             par_loc, pos_loc = par[:n_loc], npos[:n_loc]
@@ -880,8 +882,9 @@ class DistributedWorld(World):
             w.save_state(Path(statedir))
         dist.barrier(group=self.group)
 
-    def load_state(self, statedir: Path, ignore_cell_params: bool = False):
-        """Collective: every rank reads the global state and keeps its strip."""
+    def load_state(self, statedir: Path, ignore_cell_params: bool = False, restore_rng: bool = False):
+        """Collective: every rank reads the global state and keeps its strip. (The random streams
+        are per rank; a gathered state's ``rng_state.pt`` is rank 0's and is not restored.)"""
         w = World(
             chemistry=self.chemistry,
             map_size=self.map_size,
@@ -891,7 +894,7 @@ class DistributedWorld(World):
             stop_codons=self.genetics.stop_codons,
             device="cpu",
         )
-        w.load_state(Path(statedir), ignore_cell_params=True)
+        w.load_state(Path(statedir), ignore_cell_params=True, restore_rng=False)
         self.scatter_from(w, maps=False, params=not ignore_cell_params)
 
     def close(self) -> None:

@@ -67,7 +67,14 @@ def marks(world, cells: torch.Tensor | None, up: torch.Tensor, dn: torch.Tensor,
 
 def reserve(world, from_up: torch.Tensor, from_dn: torch.Tensor) -> None:
     """Halo occupancy from the neighbours' marks; owned boundary pixels next to a neighbour's
-    dividing cell reserved (2) for that neighbour's claims."""
+    dividing cell reserved (2) for that neighbour's claims.
+
+    Known statistical deviation from a single map (documented in docs/architecture.md): the
+    reference places all children in one random priority order over the whole population
+    (rust/world.rs:59-97). Here a reserved pixel is closed to the owning rank's own dividing cells
+    even when the neighbour's cell ends up claiming a different pixel, so next to a strip boundary
+    children favour the neighbour's side. The effect is confined to the two boundary rows per strip
+    and keeps the protocol free of an accept / reject round trip."""
     H, C = world.H, world.map_size
     cm = _cmap(world)
     if cm.is_cuda:

@@ -5,19 +5,34 @@
   ``cell_positions.pt``, ``cell_divisions.pt`` (``torch.save`` of the tensors) and ``cells.fasta``
   with entries ``>{idx} {label}\\n{genome}``. States from either implementation load in the other.
   Tensors are written from host copies and loaded with ``weights_only=True``.
-* Optionally an ``rng_state.pt`` with the native RNG seeds is written (new; ignored by the reference).
-* ``load_world_pickle`` restores :meth:`World.save` pickles, remapping tensor storages onto the
-  requested device like the reference's ``_CPU_Unpickler`` (``world.py:17-33``).
+* ``rng_state.pt`` (new; the reference ignores unknown files and keeps no RNG state, SURVEY §2.8
+  item 9) holds every random stream a step draws from: the device and host native streams
+  (seed, calls drawn), torch's CPU / device generators, the placement helper's generator and
+  Python's ``random``. ``load_state`` restores it when present, so save -> load -> N steps equals N
+  uninterrupted steps (``tests/test_world.py::test_save_load_state_resumes_rng_streams``).
+* ``load_world_pickle`` restores :meth:`World.save` pickles -- this package's own and the
+  reference's (``magicsoup.world.World`` with ``Conv2d`` diffusion kernels, ``world.py:161-204``) --
+  through a restricted unpickler: only the classes of ``magicsoup`` / ``magicsoup_amd``, torch's
+  tensor / parameter rebuild functions, dtypes and storages and a few builtin containers can be
+  named by the file; tensor storages are read with ``torch.load(weights_only=True)`` onto the
+  requested device, like the reference's ``_CPU_Unpickler`` (``world.py:17-33``) but without
+  executing anything else from the file. Reference pickles are converted to this package's layout
+  (``reference_world_state`` / ``reference_kinetics_state``). No reference pickle ships with the
+  reference repository, so that path is covered by a hand-built pickle of the same structure
+  (parity unpinned, ``tests/test_world.py::test_from_file_reads_reference_layout_pickle``).
 """
 from __future__ import annotations
 
+import collections
 import io
 import pickle
+import random
 from pathlib import Path
 
 import torch
 
 _FILES = ("cell_molecules", "cell_map", "molecule_map", "cell_lifetimes", "cell_positions", "cell_divisions")
+RNG_FILE = "rng_state.pt"
 
 
 def save_state(world, statedir: Path) -> None:
@@ -32,6 +47,47 @@ def save_state(world, statedir: Path) -> None:
     text = "\n".join(f">{i} {lab}\n{g}" for i, (g, lab) in enumerate(zip(genomes, labels)))
     with open(statedir / "cells.fasta", "w", encoding="utf-8") as fh:
         fh.write(text)
+    torch.save(rng_state(world.device), statedir / RNG_FILE)
+
+
+def rng_state(device) -> dict:
+    """Every random stream a world op draws from, as plain ints / tensors (``weights_only``-safe)."""
+    from magicsoup_amd.ops import native, world_ops
+
+    st = {
+        "host": list(native.host().get_rng_state()),
+        "torch_cpu": torch.get_rng_state(),
+        "placement_cpu": world_ops._gen_cpu.get_state(),
+        "python": _py_state_to_list(random.getstate()),
+    }
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        st["hip"] = list(native.hip().get_rng_state())
+        st["torch_cuda"] = torch.cuda.get_rng_state(dev)
+    return st
+
+
+def set_rng_state(st: dict, device) -> None:
+    """Restore :func:`rng_state` (entries for a device type this process does not use are skipped)."""
+    from magicsoup_amd.ops import native, world_ops
+
+    native.host().set_rng_state(*[int(x) for x in st["host"]])
+    torch.set_rng_state(st["torch_cpu"])
+    world_ops._gen_cpu.set_state(st["placement_cpu"])
+    random.setstate(_py_state_from_list(st["python"]))
+    dev = torch.device(device)
+    if dev.type == "cuda" and "hip" in st:
+        native.hip().set_rng_state(*[int(x) for x in st["hip"]])
+        torch.cuda.set_rng_state(st["torch_cuda"], dev)
+
+
+def _py_state_to_list(s) -> list:
+    version, internal, gauss = s
+    return [int(version), [int(x) for x in internal], gauss]
+
+
+def _py_state_from_list(v) -> tuple:
+    return (int(v[0]), tuple(int(x) for x in v[1]), v[2])
 
 
 def _parse_fasta(text: str) -> tuple[list[str], list[str]]:
@@ -46,7 +102,7 @@ def _parse_fasta(text: str) -> tuple[list[str], list[str]]:
     return genomes, labels
 
 
-def load_state(world, statedir: Path, ignore_cell_params: bool = False) -> None:
+def load_state(world, statedir: Path, ignore_cell_params: bool = False, restore_rng: bool = True) -> None:
     if world.n_cells > 0:
         world.kill_cells()
     dev = torch.device(world.device)
@@ -72,10 +128,47 @@ def load_state(world, statedir: Path, ignore_cell_params: bool = False) -> None:
     world._labels.append_strings(labels)
     if not ignore_cell_params and n > 0:
         world._update_params_rows(torch.arange(n, device=dev))
+    rng_file = statedir / RNG_FILE
+    if restore_rng and rng_file.exists():
+        set_rng_state(torch.load(rng_file, map_location="cpu", weights_only=True), world.device)
 
 
-class _MapLocationUnpickler(pickle.Unpickler):
-    """Load tensor storages of our own world pickles onto ``map_location``."""
+# ---------------------------------------------------------------------------- world pickles
+class _RefModule:
+    """Stand-in for a ``torch.nn.Module`` in a reference pickle (the reference keeps one
+    ``Conv2d`` per molecule as its diffusion kernel, ``world.py:948-984``): only its state is kept,
+    nothing of the module is constructed or run."""
+
+    def __setstate__(self, state):
+        self.__dict__["state"] = state
+
+    def weight(self) -> torch.Tensor | None:
+        params = self.__dict__.get("state", {}).get("_parameters") or {}
+        return params.get("weight")
+
+
+_TORCH_FUNCS = {
+    ("torch._utils", "_rebuild_tensor"),
+    ("torch._utils", "_rebuild_tensor_v2"),
+    ("torch._utils", "_rebuild_parameter"),
+    ("torch._utils", "_rebuild_parameter_with_state"),
+    ("torch._utils", "_rebuild_device_tensor_from_numpy"),
+}
+_BUILTINS = {
+    ("collections", "OrderedDict"): collections.OrderedDict,
+    ("builtins", "set"): set,
+    ("builtins", "frozenset"): frozenset,
+    ("builtins", "slice"): slice,
+    ("builtins", "complex"): complex,
+    ("torch", "Size"): torch.Size,
+    ("torch", "device"): torch.device,
+}
+_OWN_PACKAGES = ("magicsoup", "magicsoup_amd")
+
+
+class _WorldUnpickler(pickle.Unpickler):
+    """Restricted unpickler for world pickles (ours and the reference's): see the module docstring
+    for what a file may name; anything else raises ``pickle.UnpicklingError``."""
 
     def __init__(self, fh, map_location):
         super().__init__(fh)
@@ -84,14 +177,92 @@ class _MapLocationUnpickler(pickle.Unpickler):
     def find_class(self, module, name):
         if module == "torch.storage" and name == "_load_from_bytes":
             loc = self._loc
-            return lambda b: torch.load(io.BytesIO(b), map_location=loc, weights_only=False)
-        return super().find_class(module, name)
+            return lambda b: torch.load(io.BytesIO(b), map_location=loc, weights_only=True)
+        if (module, name) in _TORCH_FUNCS:
+            return super().find_class(module, name)
+        if (module, name) in _BUILTINS:
+            return _BUILTINS[(module, name)]
+        if module == "torch" and isinstance(getattr(torch, name, None), torch.dtype):
+            return getattr(torch, name)
+        if module == "torch" and name.endswith("Storage") and name[:1].isupper():
+            return super().find_class(module, name)
+        if module.startswith("torch.nn.modules."):
+            return _RefModule
+        root = module.split(".", 1)[0]
+        if root in _OWN_PACKAGES:
+            if root == "magicsoup":
+                import magicsoup  # noqa: F401 - installs the reference-path aliases
+            obj = super().find_class(module, name)
+            if isinstance(obj, type) and obj.__module__.split(".", 1)[0] == "magicsoup_amd":
+                return obj
+            raise pickle.UnpicklingError(f"{module}.{name} is not a magicsoup class")
+        raise pickle.UnpicklingError(f"world pickles may not reference {module}.{name}")
 
 
 def load_world_pickle(path: Path, device: str | None = None):
     loc = device if device is not None else ("cuda" if torch.cuda.is_available() else "cpu")
     with open(path, "rb") as fh:
-        world = _MapLocationUnpickler(fh, loc).load()
+        world = _WorldUnpickler(fh, loc).load()
     if device is not None and str(world.device) != str(device):
         world.to(device)
     return world
+
+
+def reference_world_state(st: dict) -> dict:
+    """A reference ``World.__dict__`` (``world.py:161-204``: list genomes / labels, dense per-cell
+    tensors, one ``Conv2d`` per molecule) in this package's pickled layout (World.__getstate__)."""
+    from magicsoup_amd.models.world import _diffusion_weights
+
+    st = dict(st)
+    out = {k: st[k] for k in ("device", "batch_size", "map_size", "abs_temp", "chemistry", "genetics", "kinetics")}
+    m = int(st.get("n_molecules", len(st["chemistry"].molecules)))
+    out["n_molecules"] = m
+    out["_int_mol_idxs"] = list(range(m))
+    out["_ext_mol_idxs"] = list(range(m, 2 * m))
+    out["_mol_degrads"] = [float(x) for x in st["_mol_degrads"]]
+    out["_permeation"] = [float(x) for x in st["_permeation"]]
+    diff = []
+    for conv, mol in zip(st.get("_diffusion", []), st["chemistry"].molecules):
+        w = conv.weight() if isinstance(conv, _RefModule) else None
+        if w is not None and w.numel() == 9:
+            w = w.detach().reshape(3, 3).float().cpu()
+            diff.append((float(w[0, 0]), float(w[1, 1])))  # kernel [[a,a,a],[a,b,a],[a,a,a]]
+        else:
+            diff.append(_diffusion_weights(mol.diffusivity))
+    out["_diffusion"] = diff
+    n = int(st["n_cells"])
+    out["n_cells"] = n
+    out["map_dtype"] = torch.float32
+    out["_cols"] = {
+        "cell_molecules": st["cell_molecules"].detach().float().cpu(),
+        "cell_positions": st["cell_positions"].detach().int().cpu(),
+        "cell_lifetimes": st["cell_lifetimes"].detach().int().cpu(),
+        "cell_divisions": st["cell_divisions"].detach().int().cpu(),
+    }
+    out["_genomes"] = list(st["cell_genomes"])
+    out["_labels"] = list(st["cell_labels"])
+    out["_molmap"] = st["molecule_map"].detach().float().cpu()
+    out["_cell_map"] = st["cell_map"].detach().bool().cpu()
+    out["_pending_scale"] = None
+    out["_pending_corr"] = None
+    return out
+
+
+def reference_kinetics_state(st: dict) -> dict:
+    """A reference ``Kinetics.__dict__`` (``kinetics.py:390-460``: dense parameter tensors as
+    attributes) in this package's layout (dense row storage, one row per cell)."""
+    from magicsoup_amd.models.kinetics import _PARAMS
+
+    st = dict(st)
+    store = {}
+    for name in _PARAMS:
+        t = st.pop(name)
+        store[name] = t.detach().contiguous()
+    n = int(store["N"].size(0))
+    st["_store_d"] = store
+    st["_slot"] = None
+    st["_ncells"] = n
+    st["_nrows"] = n
+    st.setdefault("n_signals", int(st["mol_energies"].numel()))
+    st["last_masks"] = []
+    return st

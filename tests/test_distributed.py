@@ -446,3 +446,42 @@ def _body_virtual_strips(rank, ws):
 
 def test_one_rank_virtual_strips():
     run_ranks(_body_virtual_strips, 1)
+
+
+# ---------------------------------------------------------------------------------------------
+def _body_peer_failure(rank, ws, mode):
+    import os
+    import time
+
+    from magicsoup_amd.parallel import comm
+
+    comm.TIMEOUT_S = 4.0
+    dw = _dworld(16)
+    dw.spawn_cells_global([__import__("magicsoup_amd").random_genome(300) for _ in range(20)])
+    dw.diffuse_molecules()
+    if rank == 1:
+        if mode == "exit":
+            os._exit(0)  # the peer dies mid-run without closing anything
+        time.sleep(15)  # the peer stalls
+        os._exit(0)
+    t0 = time.time()
+    try:
+        for _ in range(5):
+            dw.enzymatic_activity()
+            dw.diffuse_molecules()
+    except comm.CommError:
+        assert time.time() - t0 < 12.0
+        return
+    raise AssertionError("a dead / stalled peer did not raise CommError")
+
+
+def test_peer_death_raises_instead_of_hanging():
+    """Fail-stop: when a neighbour rank exits mid-run, the surviving rank's next exchange raises
+    CommError (gloo: closed connection) instead of hanging."""
+    run_ranks(_body_peer_failure, 2, "exit", timeout=120)
+
+
+def test_stalled_peer_times_out():
+    """A neighbour that stops answering makes the waiting rank raise CommError after
+    ``MS_COMM_TIMEOUT_S`` (here 4 s) instead of blocking forever."""
+    run_ranks(_body_peer_failure, 2, "stall", timeout=120)

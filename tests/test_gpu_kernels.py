@@ -593,6 +593,26 @@ def test_device_genome_pipeline_matches_sync_path(monkeypatch, d_cap):
     assert torch.equal(x0, x1)
 
 
+def test_assignment_after_speculative_activity_survives_rollback(monkeypatch):
+    """A speculative enzymatic_activity (issued on top of unconfirmed genome-pipeline rebuilds)
+    whose rebuilds must be redone on the host is rolled back and re-run at the next confirmation.
+    Assigning ``cell_molecules`` / ``molecule_map`` confirms it first, so the user's values are what
+    the world holds afterwards (one domain slot per protein forces the host rebuild)."""
+    from magicsoup_amd.ops import genome_pipeline
+
+    monkeypatch.delenv("MS_SYNC_GENETICS", raising=False)
+    monkeypatch.setattr(genome_pipeline, "D_CAP", 1)
+    for target in ("cell_molecules", "molecule_map"):
+        w = _world("cuda", map_size=64, n=600, s=500, seed=5)
+        w.mutate_cells(p=1e-3)  # queued / pending device-pipeline rebuilds
+        w.enzymatic_activity()
+        assert w.__dict__.get("_spec") is not None
+        x = torch.full_like(w.__dict__["_molmap"] if target == "molecule_map" else w._cols[target].view(w.n_cells), 3.0)
+        setattr(w, target, x.clone())
+        assert w.__dict__.get("_spec") is None
+        assert torch.equal(getattr(w, target), x), target
+
+
 def test_deferred_genome_ops_match_immediate_issue(monkeypatch):
     """All-cells mutate / recombinate go to a side stream (issued at once and joined at the next op
     that needs them, or queued until the diffusion stencil is launched): same genomes, parameters and

@@ -184,8 +184,10 @@ def test_point_mutations_at_scale():
     for _ in range(3):
         # ~1 mutation per genome: a substitution can draw the same nt (p = 0.6 * 1/4 per mutation),
         # so about 9.4 % of the ~630 mutated genomes stay unchanged: expected fraction 0.906,
-        # sigma ~0.011. The reference's bound (0.9, tests/slow/test_mutations.py:14, "highly likely")
-        # sits half a sigma below the mean and fails about one draw in three; 5 sigma here.
+        # sigma ~0.011 at this n (1000 genomes; the reference uses 10,000, tests/slow/test_mutations.py:9,
+        # where its 0.9 bound sits ~1.6 sigma below the mean). At n = 1000 that bound is half a
+        # sigma below the mean, so the bound is rescaled to 5 sigma for this n (a doubled
+        # same-nucleotide rate, fraction ~0.81, still fails it).
         genomes = gen_genomes(n=1000, s=10_000)
         res = muts.point_mutations(seqs=genomes, p=1e-4)
         assert 0 < len(res) <= len(genomes)

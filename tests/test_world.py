@@ -434,3 +434,160 @@ def test_load_without_then_with_cell_params(tmp_path):
     assert world.n_cells == 6 and len(world.cell_genomes) == 6
     assert world.kinetics.N.size(0) == 6
     assert int(world.cell_map.sum()) == 6
+
+
+def _evolve(w, steps):
+    from magicsoup_amd.examples.wood_ljungdahl import CHEMISTRY
+
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    for _ in range(steps):
+        w.enzymatic_activity()
+        w.kill_cells(torch.nonzero(w.cell_molecules[:, atp] < 1.0).flatten().tolist())
+        w.divide_cells(torch.nonzero(w.cell_molecules[:, atp] > 3.0).flatten().tolist())
+        w.recombinate_cells(p=1e-4)
+        w.mutate_cells(p=1e-3)
+        w.degrade_molecules()
+        w.diffuse_molecules()
+        w.increment_cell_lifetimes()
+
+
+def test_save_load_state_resumes_rng_streams(tmp_path):
+    """save_state writes rng_state.pt; load_state restores it: save -> load -> N steps gives
+    exactly what N uninterrupted steps give (placement, mutations, recombination, labels)."""
+    from magicsoup_amd.examples.wood_ljungdahl import CHEMISTRY
+
+    ms.set_seed(21)
+    torch.manual_seed(21)
+    w = ms.World(chemistry=CHEMISTRY, map_size=24, seed=21)
+    w.spawn_cells([ms.random_genome(400) for _ in range(120)])
+    _evolve(w, 2)
+    w.save_state(tmp_path / "s")
+    assert (tmp_path / "s" / "rng_state.pt").exists()
+    _evolve(w, 3)
+    w.spawn_cells([ms.random_genome(300) for _ in range(5)])
+    ms.set_seed(21)
+    w2 = ms.World(chemistry=CHEMISTRY, map_size=24, seed=21)  # same codon / kinetics maps
+    ms.set_seed(99)  # streams that would diverge without the restore
+    w2.load_state(tmp_path / "s")
+    _evolve(w2, 3)
+    w2.spawn_cells([ms.random_genome(300) for _ in range(5)])
+    assert list(w2.cell_genomes) == list(w.cell_genomes)
+    assert list(w2.cell_labels) == list(w.cell_labels)
+    assert torch.equal(w2.cell_positions, w.cell_positions)
+    assert torch.equal(w2.cell_molecules, w.cell_molecules)
+    assert torch.equal(w2.molecule_map, w.molecule_map)
+
+
+class _RefClass:
+    """Marks a stand-in class as the reference class ``_ref_path`` when pickled."""
+
+
+def _ref_cls(path, base=object, **attrs):
+    return type(path[1], (base,), {"_ref_path": path, **attrs})
+
+
+def _reference_pickle(w) -> bytes:
+    """A pickle with the reference's structure (magicsoup.world.World with list genomes, dense
+    parameter tensors, Conv2d diffusion kernels; world.py:161-204, kinetics.py:390-460), built from
+    a world of this package: the reference's own pickles cannot be produced here."""
+    import io
+    import pickle
+
+    class RefPickler(pickle._Pickler):
+        def save_global(self, obj, name=None):
+            ref = obj.__dict__.get("_ref_path") if isinstance(obj, type) else None
+            if ref is None:
+                return super().save_global(obj, name)
+            self.save(ref[0])
+            self.save(ref[1])
+            self.write(pickle.STACK_GLOBAL)
+            self.memoize(obj)
+
+    RW = _ref_cls(("magicsoup.world", "World"))
+    RK = _ref_cls(("magicsoup.kinetics", "Kinetics"))
+    RG = _ref_cls(("magicsoup.genetics", "Genetics"))
+    maps = {}
+    kin = w.kinetics
+    for attr, cls_name in (("km_map", "_LogNormWeightMapFact"), ("vmax_map", "_LogNormWeightMapFact"),
+                           ("sign_map", "_SignMapFact"), ("hill_map", "_HillMapFact"),
+                           ("reaction_map", "_ReactionMapFact"), ("transport_map", "_TransporterMapFact"),
+                           ("effector_map", "_RegulatoryMapFact")):
+        o = _ref_cls(("magicsoup.kinetics", cls_name))()
+        o.__dict__.update({k: v for k, v in vars(getattr(kin, attr)).items() if isinstance(v, torch.Tensor)})
+        maps[attr] = o
+    rk = RK()
+    rk.__dict__.update(abs_temp=kin.abs_temp, device="cpu", mol_names=list(kin.mol_names),
+                       mol_energies=kin.mol_energies.clone(), **{k: getattr(kin, k).clone() for k in
+                                                                ("Ke", "Kmf", "Kmb", "Kmr", "Vmax", "N", "Nf", "Nb", "A")},
+                       **maps, km_2_idxs=kin.km_2_idxs, vmax_2_idxs=kin.vmax_2_idxs, sign_2_idxs=kin.sign_2_idxs,
+                       hill_2_idxs=kin.hill_2_idxs, trnsp_2_idxs=kin.trnsp_2_idxs, regul_2_idxs=kin.regul_2_idxs,
+                       catal_2_idxs=kin.catal_2_idxs)
+    rg = RG()
+    g = w.genetics
+    rg.__dict__.update({k: getattr(g, k) for k in ("start_codons", "stop_codons", "dom_size", "dom_type_size",
+                                                   "domain_types", "domain_map", "one_codon_map", "two_codon_map",
+                                                   "idx_2_one_codon", "idx_2_two_codon")})
+    convs = []
+    for a, b in w._diffusion:
+        c = torch.nn.Conv2d(1, 1, 3, padding=1, padding_mode="circular", bias=False)
+        c.weight.data = torch.tensor([[a, a, a], [a, b, a], [a, a, a]], dtype=torch.float32).view(1, 1, 3, 3)
+        c.weight.requires_grad_(False)
+        convs.append(c)
+    rw = RW()
+    rw.__dict__.update(device="cpu", batch_size=None, map_size=w.map_size, abs_temp=w.abs_temp, chemistry=w.chemistry,
+                       genetics=rg, kinetics=rk, _mol_degrads=list(w._mol_degrads), _diffusion=convs,
+                       _permeation=list(w._permeation), n_molecules=w.n_molecules,
+                       _int_mol_idxs=list(w._int_mol_idxs), _ext_mol_idxs=list(w._ext_mol_idxs), n_cells=w.n_cells,
+                       cell_genomes=list(w.cell_genomes), cell_labels=list(w.cell_labels), cell_map=w.cell_map.clone(),
+                       cell_positions=w.cell_positions.clone(), cell_lifetimes=w.cell_lifetimes.clone(),
+                       cell_divisions=w.cell_divisions.clone(), cell_molecules=w.cell_molecules.clone(),
+                       molecule_map=w.molecule_map.clone())
+    buf = io.BytesIO()
+    RefPickler(buf, protocol=4).dump(rw)
+    return buf.getvalue()
+
+
+def test_from_file_reads_reference_layout_pickle(tmp_path):
+    """World.from_file converts a reference-layout pickle (magicsoup.world.World etc.) into this
+    package's World: same cells, maps, parameters and diffusion weights; usable afterwards.
+    Parity unpinned: no reference pickle fixture exists, the file is built with the reference's
+    structure (world.py:161-204)."""
+    from magicsoup_amd.examples.wood_ljungdahl import CHEMISTRY
+
+    ms.set_seed(3)
+    w = ms.World(chemistry=CHEMISTRY, map_size=16)
+    w.spawn_cells([ms.random_genome(500) for _ in range(30)])
+    w.cell_lifetimes[3] = 7
+    w._diffusion[0] = (0.05, 0.6)  # a non-default kernel must survive the round trip
+    (tmp_path / "world.pkl").write_bytes(_reference_pickle(w))
+    w2 = ms.World.from_file(tmp_path)
+    assert type(w2) is ms.World and w2.n_cells == w.n_cells
+    assert list(w2.cell_genomes) == list(w.cell_genomes)
+    assert list(w2.cell_labels) == list(w.cell_labels)
+    for k in ("cell_positions", "cell_lifetimes", "cell_divisions", "cell_molecules", "molecule_map", "cell_map"):
+        assert torch.equal(getattr(w2, k), getattr(w, k)), k
+    for k in ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke"):
+        assert torch.equal(getattr(w2.kinetics, k), getattr(w.kinetics, k)), k
+    got = [x for ab in w2._diffusion for x in ab]
+    want = [x for ab in w._diffusion for x in ab]
+    assert got == pytest.approx(want, rel=1e-6)  # (fp32 kernel weights)
+    assert w2.genetics.two_codon_map == w.genetics.two_codon_map
+    w.enzymatic_activity()
+    w2.enzymatic_activity()
+    assert torch.equal(w2.cell_molecules, w.cell_molecules)
+    w2.spawn_cells([ms.random_genome(300)])  # the converted world keeps working
+    w2.diffuse_molecules()
+
+
+def test_world_unpickler_refuses_foreign_globals(tmp_path):
+    """from_file runs nothing a pickle names outside magicsoup / torch tensor rebuilds."""
+    import os
+    import pickle
+
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ("echo pwned",))
+
+    (tmp_path / "world.pkl").write_bytes(pickle.dumps(Evil()))
+    with pytest.raises(pickle.UnpicklingError):
+        ms.World.from_file(tmp_path)
