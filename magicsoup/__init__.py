@@ -12,6 +12,7 @@ from magicsoup_amd import *  # noqa: F401,F403
 from magicsoup_amd import set_seed, __version__  # noqa: F401
 
 _ALIASES = {
+    "_lib": "magicsoup_amd._lib",
     "constants": "magicsoup_amd.constants",
     "util": "magicsoup_amd.utils.util",
     "containers": "magicsoup_amd.models.containers",

@@ -109,6 +109,9 @@ def bench_world_mutations(device, n, s, reps):
     def fn(_):
         w.mutate_cells()
         w.recombinate_cells()
+        # all-cells mutate / recombinate are queued for the device genome pipeline: issue and
+        # confirm them inside the timed region (what the next op of a step would do)
+        w._reconcile()
 
     return _timed(device, lambda: None, fn, reps)
 
