@@ -174,6 +174,7 @@ void xb_apply(int C, int E, int slot_w, uint64_t seed_dn, uint64_t seed_up, uint
               int parts_cap, uintptr_t pair_count, uintptr_t out, int out_width, uintptr_t out_len,
               uintptr_t out_rows, uintptr_t other, uintptr_t nres, uintptr_t stream);
 void bind_gp(py::module_& m);
+void bind_fast(py::module_& m);
 }  // namespace msd
 
 namespace {
@@ -278,6 +279,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("xb_prep", &msd::xb_prep);
   m.def("xb_events", &msd::xb_events, "strip-boundary recombination events (one workgroup, both boundaries)");
   m.def("xb_apply", &msd::xb_apply);
+  msd::bind_fast(m);
   msd::bind_gp(m);
   m.def("select_indices", &msd::select_indices,
         "(count, max) of an order-preserving compaction; synchronises the stream");

@@ -754,40 +754,102 @@ class World:
 
     def _divide_mask_gpu(self, mask: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
         """Division over a GPU mask with one synchronisation at the very end: placement, winner
-        compaction, the commit of the new rows and the genome / label / parameter-row gather are
-        all issued against the device-side winner count into capacity reserved for the worst case
-        (every cell divides); the host then only adopts the count."""
+        compaction, the commit of the new rows and the genome / label / parameter-row clone are all
+        issued against the device-side winner count (one native call, fast.hip fast_divide) into
+        capacity reserved for the worst case (every cell divides); the host then only adopts the
+        count."""
         from magicsoup_amd.ops import hip_ops
 
         n = self.n_cells
-        self._reserve(2 * n)
-        kin = self.kinetics
-        kin._enter_slot_mode()
-        kin._slot_reserve(2 * n)
-        g, lab = self._genomes, self._labels
-        g.reserve(2 * n)
-        lab.reserve(2 * n)
-        par = torch.empty(n, dtype=torch.long, device=self.device)
-        children = torch.arange(n, 2 * n, device=self.device)
-        dcount, slot = hip_ops.divide_mask_issue(self, mask, n, par)
-        sb = kin.__dict__["_slot_buf"]
-        pairs = [(g.data[:n], g.data[n : 2 * n], g.lens), (g.lens[:n], g.lens[n : 2 * n]),
-                 (lab.data[:n], lab.data[n : 2 * n], lab.lens), (lab.lens[:n], lab.lens[n : 2 * n]),
-                 (sb[:n], sb[n : 2 * n])]
-        hip_ops.gather_rows(pairs, n, src_rows=par, dn=dcount)
+        fw = self._fast_world(2 * n)
+        mask = mask.view(torch.uint8) if mask.dtype == torch.bool else mask.to(torch.uint8)
+        seed, call = hip_ops._rng()
+        slot = hip_ops._m().fast_divide(fw, n, mask.contiguous().data_ptr(), seed, call, hip_ops._stream())
         k = hip_ops.wait_count(slot)
         hip_ops.check_placement()
         if k == 0:
             empty = torch.zeros(0, dtype=torch.long, device=self.device)
             return empty, empty
-        self.n_cells = n + k
-        for arena in (g, lab):
-            arena.n = n + k
+        self._adopt_count(n + k)
+        # (the parents' scratch buffer is reused by the next division)
+        par = self.__dict__["_fw_bufs"]["par"][:k].clone()
+        return par, torch.arange(n, n + k, device=self.device)
+
+    def _adopt_count(self, n: int) -> None:
+        """A native operation left ``n`` valid rows in every per-cell buffer (columns, arenas, the
+        kinetics cell -> row map): adopt the count on the host."""
+        self.n_cells = n
+        for arena in (self._genomes, self._labels):
+            arena.n = n
             arena.version += 1
+        kd = self.kinetics.__dict__
+        kd["_slot"] = kd["_slot_buf"][:n]
+        kd["_ncells"] = n
+
+    def _fast_world(self, need: int):
+        """The FastWorld descriptor of this world's per-cell buffers (csrc/hip/fast.hip) with room
+        for ``need`` rows. Buffers are grown first if needed (1.5x); the descriptor is rebuilt
+        whenever any of its buffers was reallocated (its key is their addresses), so it never
+        points at freed memory."""
+        d = self.__dict__
+        kin = self.kinetics
+        kin._enter_slot_mode()
+        cols = self._cols
+        g, lab = self._genomes, self._labels
         kd = kin.__dict__
-        kd["_slot"] = sb[: n + k]
-        kd["_ncells"] += k
-        return par[:k], children[:k]
+        cap = min(min(int(c.buf.size(0)) for c in cols.values()), g.capacity, lab.capacity,
+                  int(kd["_slot_buf"].numel()))
+        if cap < need:
+            target = max(need, int(cap * 1.5) + 64)
+            self._reserve(target)
+            g.reserve(target)
+            lab.reserve(target)
+            kin._slot_reserve(target)
+            cap = min(min(int(c.buf.size(0)) for c in cols.values()), g.capacity, lab.capacity,
+                      int(kd["_slot_buf"].numel()))
+        fw = d.get("_fw")
+        key = (cap, g.width, lab.width, g.data.data_ptr(), g.lens.data_ptr(), lab.data.data_ptr(),
+               lab.lens.data_ptr(), kd["_slot_buf"].data_ptr(), kd["_slot_spare"].data_ptr(),
+               self.__dict__["_cell_map"].data_ptr(), *(c.buf.data_ptr() for c in cols.values()))
+        if fw is not None and d.get("_fw_key") == key:
+            return fw
+        from magicsoup_amd.ops import hip_ops
+
+        for c in cols.values():
+            c.spare_rows(cap)
+        g.compact_pairs(cap)  # (allocates the arenas' spares at their capacity and width)
+        lab.compact_pairs(cap)
+        dev = g.data.device
+        R, C, r_lo, r_hi, wrap = world_ops.geom(self)
+        claim = d.get("_claim_map")
+        if claim is None or claim.numel() != R * C or claim.device != dev:
+            claim = torch.full((R * C,), 0x7FFFFFFF, dtype=torch.int32, device=dev)
+            d["_claim_map"] = claim
+        bufs = {name: torch.empty(cap, dtype=dt, device=dev) for name, dt in (
+            ("sel", torch.int64), ("pending", torch.uint8), ("cand", torch.int64), ("result", torch.int64),
+            ("wins", torch.int64), ("par", torch.int64))}
+        bufs["dcount"] = torch.zeros(4, dtype=torch.int32, device=dev)
+        fw = hip_ops._m().FastWorld()
+        fw.R, fw.C, fw.r_lo, fw.r_hi, fw.wrap, fw.m, fw.cap = R, C, r_lo, r_hi, int(wrap), self.n_molecules, cap
+        names = ("cell_molecules", "cell_positions", "cell_lifetimes", "cell_divisions")
+        fw.mols, fw.pos, fw.life, fw.div = (cols[k].buf.data_ptr() for k in names)
+        fw.mols_sp, fw.pos_sp, fw.life_sp, fw.div_sp = (cols[k].spare.data_ptr() for k in names)
+        gs, ls = g.__dict__["_spare"], lab.__dict__["_spare"]
+        fw.g_data, fw.g_lens, fw.g_data_sp, fw.g_lens_sp = (g.data.data_ptr(), g.lens.data_ptr(), gs[0].data_ptr(),
+                                                            gs[1].data_ptr())
+        fw.l_data, fw.l_lens, fw.l_data_sp, fw.l_lens_sp = (lab.data.data_ptr(), lab.lens.data_ptr(),
+                                                            ls[0].data_ptr(), ls[1].data_ptr())
+        fw.g_width, fw.l_width = int(g.width), int(lab.width)
+        fw.slot, fw.slot_sp = kd["_slot_buf"].data_ptr(), kd["_slot_spare"].data_ptr()
+        fw.cell_map = hip_ops._cell_map_bytes(self).data_ptr()
+        fw.sel, fw.pending, fw.cand, fw.result, fw.wins, fw.par = (bufs[k].data_ptr() for k in (
+            "sel", "pending", "cand", "result", "wins", "par"))
+        fw.dcount, fw.dcount2 = bufs["dcount"].data_ptr(), bufs["dcount"].data_ptr() + 8
+        fw.claim = claim.data_ptr()
+        fw.rounds = hip_ops._PLACE_ROUNDS
+        fw.finalize()
+        d["_fw"], d["_fw_key"], d["_fw_bufs"] = fw, key, bufs
+        return fw
 
     @_op("update_cells")
     def update_cells(self, genome_idx_pairs: list[tuple[str, int]]):
@@ -815,37 +877,32 @@ class World:
             if t.numel() == 0:
                 return
             dead.index_fill_(0, t.to(self.device, torch.long), True)  # duplicates are harmless
-        world_ops.spill_and_free_mask(self, dead)
         if dead.is_cuda:
             from magicsoup_amd.ops import hip_ops
 
-            # the map is final for this step's diffusion now: its stencil starts on a side stream,
-            # next to the compaction and the division that usually follow (adopted by
-            # diffuse_molecules; see hip_ops.spec_diffuse_issue)
-            if hip_ops.EARLY_DIFFUSE_AT == "spill":
-                hip_ops.spec_diffuse_issue(self)
-
-            # survivors and the dead in one compaction pass; the row gather is launched with the
+            # spill, survivor selection and the order-preserving compaction of every per-cell
+            # buffer (into the spares and back) in one native call, launched against the
             # device-side survivor count before the one stream sync that brings it to the host
-            keep_buf, dead_buf, dcount, slot = hip_ops.select_async(dead, "clear", rest=True)
-            pairs = [(col.view(n), col.spare_rows(n)) for col in self._cols.values()]
-            slot_pairs = self.kinetics.slot_compact_pairs(n)
-            pairs += self._genomes.compact_pairs(n) + self._labels.compact_pairs(n) + slot_pairs
-            hip_ops.gather_rows(pairs, n, src_rows=keep_buf, dn=dcount)
+            early = hip_ops.EARLY_DIFFUSE_AT == "spill" and self.__dict__.get("_early_diffuse", hip_ops._SPEC_DIFF_ENV == "1")
+            if early:
+                # the map is final for this step's diffusion after the spill: its stencil starts on
+                # a side stream, next to the compaction and the division that usually follow
+                # (adopted by diffuse_molecules; see hip_ops.spec_diffuse_issue)
+                world_ops.spill_and_free_mask(self, dead)
+                hip_ops.spec_diffuse_issue(self)
+            fw = self._fast_world(n)
+            mm, corr = hip_ops.map_for_pixels(self) if not early else (self.__dict__["_molmap"], None)
+            mask = dead.view(torch.uint8) if dead.dtype == torch.bool else dead.to(torch.uint8)
+            slot = hip_ops._m().fast_kill(fw, n, mask.contiguous().data_ptr(), mm.data_ptr(), hip_ops._mdt(mm),
+                                          hip_ops._p(corr), not early, hip_ops._stream())
             n_new = hip_ops.wait_count(slot)
             if hip_ops.EARLY_DIFFUSE_AT == "synced":
                 hip_ops.spec_diffuse_issue(self)  # (the compaction is done: only the division runs next to it)
-            if n_new == n:
-                return  # nothing removed: the spare buffers are simply not adopted
-            self.kinetics.remove_cell_params(keep=keep_buf[:n_new], removed=dead_buf[: n - n_new],
-                                             gathered=bool(slot_pairs))
-            for col in self._cols.values():
-                col.swap()
-            self._genomes.commit_compact(n_new)
-            self._labels.commit_compact(n_new)
-            self.n_cells = n_new
-            self._watch_genome_width()
+            if n_new != n:
+                self._adopt_count(n_new)
+                self._watch_genome_width()
             return
+        world_ops.spill_and_free_mask(self, dead)
         keep = ~dead
         keep_idx = torch.nonzero(keep).flatten()
         if int(keep_idx.numel()) == n:
@@ -1128,7 +1185,7 @@ class World:
         state["_pending_corr"] = None
         for k in ("_hip_scratch", "_idx_map", "_diff_w", "_perm_t", "_degrade_t", "_gp_state", "_deferred",
                   "_side_stream", "_defer_event", "_gp_cache", "_spec", "_spec_diff", "_spec_diff_miss",
-                  "_diff_stream", "_side_join", "_gw_watch", "_gw_pinned"):
+                  "_diff_stream", "_side_join", "_gw_watch", "_gw_pinned", "_fw", "_fw_key", "_fw_bufs"):
             state.pop(k, None)
         return state
 

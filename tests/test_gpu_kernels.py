@@ -602,11 +602,19 @@ def test_assignment_after_speculative_activity_survives_rollback(monkeypatch):
 
     monkeypatch.delenv("MS_SYNC_GENETICS", raising=False)
     monkeypatch.setattr(genome_pipeline, "D_CAP", 1)
+    atp = CHEMISTRY.molname_2_idx["ATP"]
     for target in ("cell_molecules", "molecule_map"):
         w = _world("cuda", map_size=64, n=600, s=500, seed=5)
+        for _ in range(2):  # parameter storage and the pipeline are set up
+            w.enzymatic_activity()
+            w.kill_cells(w.cell_molecules[:, atp] < 0.3)
+            w.divide_cells_t(w.cell_molecules[:, atp] > 3.0)
+            w.diffuse_molecules()
+        w.recombinate_cells(p=1e-4)
         w.mutate_cells(p=1e-3)  # queued / pending device-pipeline rebuilds
         w.enzymatic_activity()
-        assert w.__dict__.get("_spec") is not None
+        st = w.__dict__.get("_gp_state")
+        assert w.__dict__.get("_spec") is not None, (st, w.__dict__.get("_deferred"))
         x = torch.full_like(w.__dict__["_molmap"] if target == "molecule_map" else w._cols[target].view(w.n_cells), 3.0)
         setattr(w, target, x.clone())
         assert w.__dict__.get("_spec") is None
