@@ -611,7 +611,7 @@ def test_assignment_after_speculative_activity_survives_rollback(monkeypatch):
             w.divide_cells_t(w.cell_molecules[:, atp] > 3.0)
             w.diffuse_molecules()
         w.recombinate_cells(p=1e-4)
-        w.mutate_cells(p=1e-3)  # queued / pending device-pipeline rebuilds
+        w.mutate_cells(p=2e-4)  # queued / pending device-pipeline rebuilds (p * row width <= 1)
         w.enzymatic_activity()
         st = w.__dict__.get("_gp_state")
         assert w.__dict__.get("_spec") is not None, (st, w.__dict__.get("_deferred"))

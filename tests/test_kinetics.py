@@ -98,8 +98,8 @@ def _prod_pow(x, n):
     return min(r, MAX), True
 
 
-def _oracle_part(p, X0, trim, n_iters):
-    """One integration part for one cell (float64)."""
+def _velocity_part(p, X0, trim):
+    """Velocities, negative-guarded NV and the undamped candidate of one part for one cell (float64)."""
     P, s = p["N"].shape
     V = np.zeros(P)
     for k in range(P):
@@ -129,27 +129,72 @@ def _oracle_part(p, X0, trim, n_iters):
             if NV[k, j] < 0:
                 fmin[k] = min(fmin[k], F[j]) if not math.isnan(F[j]) else math.nan
     NV = NV * fmin[:, None]
-    X1 = np.maximum(X0 + NV.sum(0), 0.0)
-    if n_iters == 0:
-        return X1
-    Fa = np.ones(P)
-    imp, fwd = np.abs(V) > 0.1, V > 0
-    for inc in (0.5, 0.25, 0.125, 0.0625)[:n_iters]:
-        q = np.zeros(P)
-        for k in range(P):
-            pb, bi = _prod_pow(X1, p["Nb"][k])
-            ps, si = _prod_pow(X1, p["Nf"][k])
-            with np.errstate(divide="ignore", invalid="ignore"):
-                qq = np.float64(pb if bi else 0.0) / np.float64(ps if si else 0.0)
-            q[k] = 1.0 if math.isnan(qq) else min(max(qq, EPS), MAX)
-        qke = q / p["Ke"]
-        low = np.where(fwd, qke < 1 / 1.5, qke > 1.5) & ~(fwd & (Fa == 1.0))
-        high = np.where(fwd, qke > 1.5, qke < 1 / 1.5) & ~(~fwd & (Fa == 0.0))
-        if not ((low | high) & imp).any():
-            return X1
-        Fa = np.clip(Fa - inc * high + inc * low, 0, 1)
-        X1 = np.maximum(X0 + (NV * Fa[:, None]).sum(0), 0.0)
-    return X1
+    return V, NV, np.maximum(X0 + NV.sum(0), 0.0)
+
+
+def _qke(p, X1):
+    P = p["N"].shape[0]
+    q = np.zeros(P)
+    for k in range(P):
+        pb, bi = _prod_pow(X1, p["Nb"][k])
+        ps, si = _prod_pow(X1, p["Nf"][k])
+        with np.errstate(divide="ignore", invalid="ignore"):
+            qq = np.float64(pb if bi else 0.0) / np.float64(ps if si else 0.0)
+        q[k] = 1.0 if math.isnan(qq) else min(max(qq, EPS), MAX)
+    return q / p["Ke"]
+
+
+def _oracle_population(params, X, trims, n_iters, exits=None, margin=1e-4):
+    """The reference's integration over a whole population (float64): per part, velocities and the
+    negative guard per cell, then the equilibrium damping whose early exit is the population-wide
+    ``torch.any`` (kinetics.py:846). ``exits`` (per part: damping iterations that ran, from the
+    native core's flags) replays the native exit decisions instead of deciding in float64.
+
+    Returns (X, borderline): ``borderline[c]`` is True if one of the cell's damping decisions had
+    Q/Ke within a relative ``margin`` of a threshold (1.5, 1/1.5) -- such a decision can go either
+    way between float32 and float64 and is not a meaningful disagreement."""
+    X = [np.array(x, dtype=np.float64) for x in X]
+    border = [False] * len(X)
+    for part, trim in enumerate(trims):
+        parts = [_velocity_part(p, x, trim) for p, x in zip(params, X)]
+        X0 = X
+        X1 = [c[2] for c in parts]
+        if n_iters:
+            Fa = [np.ones(p["N"].shape[0]) for p in params]
+            for it, inc in enumerate((0.5, 0.25, 0.125, 0.0625)[:n_iters]):
+                lows, highs, anyflag = [], [], False
+                for c, p in enumerate(params):
+                    V, NV, _ = parts[c]
+                    qke = _qke(p, X1[c])
+                    imp, fwd = np.abs(V) > 0.1, V > 0
+                    near = (np.abs(qke * 1.5 - 1.0) < margin) | (np.abs(qke / 1.5 - 1.0) < margin)
+                    if (near & (NV != 0).any(axis=1)).any():
+                        border[c] = True
+                    low = np.where(fwd, qke < 1 / 1.5, qke > 1.5) & ~(fwd & (Fa[c] == 1.0))
+                    high = np.where(fwd, qke > 1.5, qke < 1 / 1.5) & ~(~fwd & (Fa[c] == 0.0))
+                    lows.append(low)
+                    highs.append(high)
+                    anyflag |= bool(((low | high) & imp).any())
+                stop = (it >= exits[part]) if exits is not None else not anyflag
+                if stop:
+                    break
+                for c, p in enumerate(params):
+                    Fa[c] = np.clip(Fa[c] - inc * highs[c] + inc * lows[c], 0, 1)
+                    X1[c] = np.maximum(X0[c] + (parts[c][1] * Fa[c][:, None]).sum(0), 0.0)
+        X = X1
+    return X, border
+
+
+def _exits(masks, n_iters):
+    """Damping iterations each part ran, from the native per-part flag bits (bit i: iteration i
+    still had an impactful correction somewhere)."""
+    out = []
+    for bits in masks:
+        k = 0
+        while k < n_iters and (bits >> k) & 1:
+            k += 1
+        out.append(k)
+    return out
 
 
 # --------------------------------------------------------------------------------------------- helpers
@@ -284,21 +329,26 @@ def _params_np(kin, c):
 
 @pytest.mark.parametrize("n_iters", [0, 4])
 def test_integrator_matches_float64_oracle(n_iters):
+    """Native integrator vs the float64 population oracle, decision-aware: the oracle replays the
+    native core's population-wide exit decisions, and cells with a damping decision within 1e-4 of
+    a Q/Ke threshold (which float32 vs float64 rounding may flip) are set aside -- few of them,
+    and every other cell must agree."""
     kin, _ = _setup(n_cells=60, seed=1)
     rng = np.random.default_rng(3)
     X = torch.from_numpy(rng.gamma(2.0, 2.0, size=(60, kin.n_signals)).astype(np.float32))
     Xk = X.clone()
-    kinetics_ops.integrate(kin, Xk, trims=(0.7, 0.2, 0.1), n_iters=n_iters)
-    close = []
-    for c in range(60):
-        p = _params_np(kin, c)
-        x = X[c].double().numpy()
-        for trim in (0.7, 0.2, 0.1):
-            x = _oracle_part(p, x, trim, n_iters)
-        close.append(np.allclose(Xk[c].double().numpy(), x, rtol=2e-3, atol=2e-3))
-    # with damping, per-cell decisions (Q vs Ke thresholds) can flip on float32 vs float64
-    # rounding, and the early exit is population-wide; the bulk must agree
-    assert np.mean(close) >= (0.98 if n_iters == 0 else 0.8), np.mean(close)
+    masks = kinetics_ops.integrate(kin, Xk, trims=(0.7, 0.2, 0.1), n_iters=n_iters)
+    params = [_params_np(kin, c) for c in range(60)]
+    exits = _exits(masks, n_iters) if n_iters else None
+    ref, border = _oracle_population(params, X.double().numpy(), (0.7, 0.2, 0.1), n_iters, exits=exits)
+    close = np.array([np.allclose(Xk[c].double().numpy(), ref[c], rtol=2e-3, atol=2e-3) for c in range(60)])
+    border = np.array(border)
+    assert border.mean() <= 0.05, border.mean()
+    assert close[~border].mean() >= 0.999, (close[~border].mean(), np.nonzero(~close & ~border))
+    # and the exits the native core took are the ones float64 takes (no cell is that borderline)
+    if n_iters and not border.any():
+        ref2, _ = _oracle_population(params, X.double().numpy(), (0.7, 0.2, 0.1), n_iters)
+        assert all(np.allclose(a, b, rtol=2e-3, atol=2e-3) for a, b in zip(ref, ref2))
 
 
 def test_empty_cells_are_unchanged_and_outputs_non_negative():
@@ -400,5 +450,10 @@ def test_torch_stage_oracle_agrees_with_native():
     kin.__class__ = Staged
     Z = kin.integrate_signals(X)
     kin.__class__ = Kinetics
-    close = torch.isclose(Y, Z, rtol=1e-3, atol=1e-3).all(dim=1).float().mean()
-    assert close > 0.85
+    close = torch.isclose(Y, Z, rtol=1e-3, atol=1e-3).all(dim=1).numpy()
+    # both are float32 with different operation orders: only cells with a damping decision at a
+    # Q/Ke threshold (float64 oracle, relative margin 1e-3) may differ
+    params = [_params_np(kin, c) for c in range(40)]
+    _, border = _oracle_population(params, X.double().numpy(), (0.7, 0.2, 0.1), 4, margin=1e-3)
+    border = np.array(border)
+    assert border.mean() <= 0.1 and close[~border].all(), (border.mean(), np.nonzero(~close & ~border))
