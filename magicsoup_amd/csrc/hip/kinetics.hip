@@ -480,10 +480,10 @@ __global__ void __launch_bounds__(kBlock) integrate_spec_lds_kernel(IntegrateArg
 constexpr int kNzReg = 16;  // non-zero signals per protein in the LDS lists (more: the cell goes wide)
 constexpr int kNzWide = 2 * kNzReg;  // the same for the 64-lane launch of the wide list
 
-// LDS words per cell slot of the register-resident integrator
-template <int G, int NZ>
+// LDS words per cell slot of the register-resident integrator (SPL signals per lane: s <= SPL * G)
+template <int G, int NZ, int SPL = 1>
 constexpr int fast_slot_words() {
-  return G * NZ /*entry words*/ + G * NZ / 4 /*entry signal indices*/ + 4 * G /*cnt, act, X, pub*/;
+  return G * NZ /*entry words*/ + G * NZ / 4 /*entry signal indices*/ + 3 * G /*cnt, act, pub*/ + SPL * G /*X*/;
 }
 
 template <int G>
@@ -510,9 +510,27 @@ __device__ __forceinline__ float ipow_small(float x, int n) {
   return n < 0 ? 1.0f / r : r;
 }
 
-template <int G, int NZ, bool kSpec = false>
+// A protein's non-zero entry in 16 bits: signal j, forward / backward exponents. SPL == 1 (s <= 64):
+// j 6 bits, nf / nb 5 bits (< 32); SPL == 2 (s <= 128): j 7 bits, nf / nb 4 bits (< 16: a larger
+// exponent sends the cell to the LDS path, which has no such limit).
+template <int SPL>
+struct E16 {
+  static constexpr int kJ = SPL == 1 ? 6 : 7, kN = SPL == 1 ? 5 : 4;
+  static constexpr int kMaxExp = 1 << kN;
+  __device__ static int pack(int j, int nf, int nb) { return j | (nf << kJ) | (nb << (kJ + kN)); }
+  __device__ static int j(int e) { return e & ((1 << kJ) - 1); }
+  __device__ static int nf(int e) { return (e >> kJ) & ((1 << kN) - 1); }
+  __device__ static int nb(int e) { return (e >> (kJ + kN)) & ((1 << kN) - 1); }
+};
+
+// Register-resident integration of one cell (see above). SPL = 2 (the wide chemistries, s <= 128):
+// lane l plays signals l and l + G; the per-signal sums still run over proteins in ascending order
+// and a protein's products over its non-zero signals in ascending signal order (half 0 before half
+// 1), exactly as integrate_item, so all paths stay bit-identical.
+template <int G, int NZ, bool kSpec = false, int SPL = 1>
 __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int* smem, int item, unsigned& bits,
                                                     int32_t* wide_list, int32_t* wide_count) {
+  using EP = E16<SPL>;
   const int slot = threadIdx.x / G, lane = threadIdx.x % G;
   const bool listed0 = a.list ? item < *a.count : item < a.c;
   const int cell0 = listed0 ? (a.list ? a.list[item] : item) : 0;
@@ -521,18 +539,22 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   const int P = a.P, s = a.s;
   const size_t prow = listed ? (a.prow ? (size_t)a.prow[cell] : (size_t)cell) : 0;
 
-  int* ents = smem + slot * fast_slot_words<G, NZ>();                // (G, NZ) words of the non-zeros
+  int* ents = smem + slot * fast_slot_words<G, NZ, SPL>();       // (G, NZ) words of the non-zeros
   uint8_t* jl = reinterpret_cast<uint8_t*>(ents + G * NZ);   // (G, NZ) their signal indices
   int* cnts = ents + G * NZ + G * NZ / 4;                // (G,) non-zero signals per protein
   int* act = cnts + G;                                           // (G,) protein slot of active protein k
-  float* Xs = reinterpret_cast<float*>(act + G);                 // (G,) signal -> protein: X_j / factor
-  float* pub = Xs + G;                                           // (G,) protein -> signal: V_k / Va_k * F_k
+  float* pub = reinterpret_cast<float*>(act + G);                // (G,) protein -> signal: V_k / Va_k * F_k
+  float* Xs = pub + G;                                           // (SPL * G,) signal -> protein: X_j / factor
 
-  // ---- 1. X0 of this lane's signal (independent of the compaction, issued first)
-  float x0 = 0.0f;
-  if (listed && lane < s) {
-    const int k = stop_iter(a.mask_prev, a.n_iters_prev);
-    x0 = a.snap_prev[((size_t)cell * ms::kSnap + k) * s + lane];
+  // ---- 1. X0 of this lane's signals (independent of the compaction, issued first)
+  float x0[SPL];
+  {
+    const int k = listed ? stop_iter(a.mask_prev, a.n_iters_prev) : 0;
+#pragma unroll
+    for (int h = 0; h < SPL; ++h) {
+      const int j = lane + h * G;
+      x0[h] = (listed && j < s) ? a.snap_prev[((size_t)cell * ms::kSnap + k) * s + j] : 0.0f;
+    }
   }
 
   // ---- 2. active proteins (Vmax' != 0, NaN included) in ascending order
@@ -556,36 +578,45 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   wave_lds_sync();
   const int nac = fits ? na : 0;
   const int na_w = wave_max(nac);  // wave-uniform bound of the protein loops (both groups of a wave)
-  const bool sigl = listed && lane < s;
 
-  // ---- 3. this signal's stoichiometry column (int8 n per protein, packed in registers) and the
-  //         per-protein non-zero lists (one ballot per protein), 8 rows of loads in flight
-  int npk[G / 4];
+  // ---- 3. this lane's signals' stoichiometry columns (int8 n per protein, packed in registers) and
+  //         the per-protein non-zero lists (one ballot per protein and half), 8 rows of loads in flight
+  int npk[SPL][G / 4];
 #pragma unroll
-  for (int i = 0; i < G / 4; ++i) npk[i] = 0;
-  bool wide_ok = true;  // every protein has <= NZ non-zeros and exponents < 32
+  for (int h = 0; h < SPL; ++h)
+#pragma unroll
+    for (int i = 0; i < G / 4; ++i) npk[h][i] = 0;
+  bool wide_ok = true;  // every protein has <= NZ non-zeros and exponents below the entry limit
 #pragma unroll
   for (int k0 = 0; k0 < G; k0 += 8) {
     if (k0 >= na_w) break;
-    int w[8];
+    int w[SPL][8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int k = k0 + u;
-      w[u] = (k < nac && sigl) ? a.W[(prow * P + act[k]) * s + lane] : 0;
-    }
+    for (int h = 0; h < SPL; ++h)
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int k = k0 + u;
-      npk[k >> 2] |= (w[u] & 0xFF) << (8 * (k & 3));
-      const bool on = w[u] != 0;
-      const unsigned long long gm = group_ballot<G>(on);
-      const int r = __popcll(gm & ((1ull << lane) - 1ull));
-      if (on && r < NZ) {
-        ents[k * NZ + r] = w[u];
-        jl[k * NZ + r] = (uint8_t)lane;
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u, j = lane + h * G;
+        w[h][u] = (k < nac && listed && j < s) ? a.W[(prow * P + act[k]) * s + j] : 0;
       }
-      if (lane == 0 && k < nac) cnts[k] = __popcll(gm);
-      wide_ok &= __popcll(gm) <= NZ && w_nf(w[u]) < 32 && w_nb(w[u]) < 32;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + u;
+      int base = 0;
+#pragma unroll
+      for (int h = 0; h < SPL; ++h) {
+        npk[h][k >> 2] |= (w[h][u] & 0xFF) << (8 * (k & 3));
+        const bool on = w[h][u] != 0;
+        const unsigned long long gm = group_ballot<G>(on);
+        const int r = base + __popcll(gm & ((1ull << lane) - 1ull));
+        if (on && r < NZ) {
+          ents[k * NZ + r] = w[h][u];
+          jl[k * NZ + r] = (uint8_t)(lane + h * G);
+        }
+        base += __popcll(gm);
+        wide_ok &= w_nf(w[h][u]) < EP::kMaxExp && w_nb(w[h][u]) < EP::kMaxExp;
+      }
+      if (lane == 0 && k < nac) cnts[k] = base;
+      wide_ok &= base <= NZ;
     }
   }
   const bool nz_ok = group_ballot<G>(!wide_ok) == 0ull;
@@ -608,9 +639,12 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     fits = fits && nz_ok;
   }
   const bool valid = listed && fits;
-  const bool sig = valid && lane < s;
+  bool sig[SPL];
+#pragma unroll
+  for (int h = 0; h < SPL; ++h) sig[h] = valid && lane + h * G < s;
   const bool prot = valid && lane < na;
-  Xs[lane] = x0;
+#pragma unroll
+  for (int h = 0; h < SPL; ++h) Xs[lane + h * G] = x0[h];
   wave_lds_sync();
 
   // protein lane: constants, and its non-zeros as 16-bit (signal, nf, nb) registers for the
@@ -635,7 +669,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
       if (q < cnt) {
         const int w = ents[lane * NZ + q];
         const int j = (jw[q >> 2] >> (8 * (q & 3))) & 0xFF;
-        const int e = j | (w_nf(w) << 6) | (w_nb(w) << 11);
+        const int e = EP::pack(j, w_nf(w), w_nb(w));
         e16[q >> 1] |= e << (16 * (q & 1));
         small &= w_nf(w) < 8 && w_nb(w) < 8 && w_a(w) < 8 && w_a(w) > -8;
       }
@@ -646,7 +680,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
 #define MS_E(q) ((e16[(q) >> 1] >> (16 * ((q) & 1))) & 0xFFFF)
   auto pw = [&](float x, int n) { return small_w ? ipow_small(x, n) : ms::ipow(x, n); };
 
-  // signal lane: sum over proteins k (ascending) of op(n_kj, pub[k]); four proteins per LDS load
+  // signal lane, half h: sum over proteins k (ascending) of op(n_kj, pub[k]); four proteins per LDS load
   auto signal_pass = [&](auto&& op) {
 #pragma unroll
     for (int k0 = 0; k0 < G; k0 += 4) {
@@ -656,14 +690,17 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int k = k0 + u;
-        op((int)(int8_t)(npk[k >> 2] >> (8 * (k & 3))), bv[u]);
+#pragma unroll
+        for (int h = 0; h < SPL; ++h) op(h, (int)(int8_t)(npk[h][k >> 2] >> (8 * (k & 3))), bv[u]);
       }
     }
   };
 
   // parts: one (the launch's trim), or all of them in the speculative mode; x0 / Xs carry the state
   float* snap = a.snap_out + (size_t)(valid ? cell : 0) * ms::kSnap * s;
-  float xc = x0;
+  float xc[SPL];
+#pragma unroll
+  for (int h = 0; h < SPL; ++h) xc[h] = x0[h];
   for (int part = 0; part < nparts; ++part) {
   const float vm = vraw * (spec ? a.trims[part] : a.trim);
   const float vmx = prot && (vm > 0.0f || vm != vm) ? vm : 0.0f;
@@ -678,7 +715,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     for (int q = 0; q < NZ; ++q) {
       if (q >= cnt_w) break;
       const int w = q < cnt ? ents[lane * NZ + q] : 0;
-      const int j = MS_E(q) & 63;
+      const int j = EP::j(MS_E(q));
       const int nf = w_nf(w), nb = w_nb(w), av = w_a(w);
       const float x = Xs[j];
       nfs |= nf;
@@ -710,13 +747,18 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
 
   // ---- 5. consumption per signal -> negative-concentration factor (signal lane)
   {
-    float cons = 0.0f;
-    signal_pass([&](int n, float vk) {
+    float cons[SPL];
+#pragma unroll
+    for (int h = 0; h < SPL; ++h) cons[h] = 0.0f;
+    signal_pass([&](int h, int n, float vk) {
       const float nv = (float)n * vk;
-      if (nv < 0.0f) cons += -nv;
+      if (nv < 0.0f) cons[h] += -nv;
     });
-    const float f = x0 / cons;
-    Xs[lane] = f > 1.0f ? 1.0f : f;  // Xs holds the factors until candidate 0 exists
+#pragma unroll
+    for (int h = 0; h < SPL; ++h) {
+      const float f = x0[h] / cons[h];
+      Xs[lane + h * G] = f > 1.0f ? 1.0f : f;  // Xs holds the factors until candidate 0 exists
+    }
   }
   wave_lds_sync();
 
@@ -731,7 +773,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
       if (q >= cnt_w) break;
       const int w = q < cnt ? ents[lane * NZ + q] : 0;
       if ((float)w_n(w) * v < 0.0f) {
-        const float f = Xs[MS_E(q) & 63];
+        const float f = Xs[EP::j(MS_E(q))];
         if (ms::f_isnan(f)) nan = true;
         else if (f < fmin) fmin = f;
       }
@@ -745,16 +787,22 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   wave_lds_sync();
 
   // ---- 7. candidate 0 (signal lane)
-  auto advance = [&]() -> float {  // X0 + sum_k n_k * pub_k (ascending k), clamped at 0
-    float x = x0;
-    signal_pass([&](int n, float b) {
-      if (n != 0) x += (float)n * b;
+  auto advance = [&]() {  // X0 + sum_k n_k * pub_k (ascending k), clamped at 0
+    float x[SPL];
+#pragma unroll
+    for (int h = 0; h < SPL; ++h) x[h] = x0[h];
+    signal_pass([&](int h, int n, float b) {
+      if (n != 0) x[h] += (float)n * b;
     });
-    return x < 0.0f ? 0.0f : x;
+#pragma unroll
+    for (int h = 0; h < SPL; ++h) xc[h] = x[h] < 0.0f ? 0.0f : x[h];
   };
-  xc = advance();
-  if (sig && !spec) snap[lane] = xc;
-  Xs[lane] = xc;
+  advance();
+#pragma unroll
+  for (int h = 0; h < SPL; ++h) {
+    if (sig[h] && !spec) snap[lane + h * G] = xc[h];
+    Xs[lane + h * G] = xc[h];
+  }
   wave_lds_sync();
 
   // ---- 8. equilibrium damping trajectory
@@ -768,8 +816,8 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
       for (int q = 0; q < NZ; ++q) {
         if (q >= cnt_w) break;
         const int e = MS_E(q);
-        const int nf = (e >> 6) & 31, nb = e >> 11;
-        const float x = Xs[e & 63];
+        const int nf = EP::nf(e), nb = EP::nb(e);
+        const float x = Xs[EP::j(e)];
         nfs |= nf;
         nbs |= nb;
         pf = nf > 0 ? pf * pw(x, nf) : pf;
@@ -804,29 +852,40 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
       if (group_ballot<G>(cb) != 0ull) bits |= (((1u << a.n_iters) - 1u) & ~((2u << it) - 1u)) << bsh;
       if (!spec)
         for (int it2 = it + 1; it2 <= a.n_iters; ++it2)
-          if (sig) snap[(size_t)it2 * s + lane] = xc;
+#pragma unroll
+          for (int h = 0; h < SPL; ++h)
+            if (sig[h]) snap[(size_t)it2 * s + lane + h * G] = xc[h];
       break;
     }
     pub[lane] = va * F;
     wave_lds_sync();  // the protein lanes of this wave finished reading Xs, published Va * F
-    xc = advance();
-    if (sig && !spec) snap[(size_t)(it + 1) * s + lane] = xc;
-    Xs[lane] = xc;
+    advance();
+#pragma unroll
+    for (int h = 0; h < SPL; ++h) {
+      if (sig[h] && !spec) snap[(size_t)(it + 1) * s + lane + h * G] = xc[h];
+      Xs[lane + h * G] = xc[h];
+    }
     wave_lds_sync();
   }
-  x0 = xc;  // the next part starts from this part's last candidate (Xs holds it already)
+#pragma unroll
+  for (int h = 0; h < SPL; ++h) x0[h] = xc[h];  // the next part starts from this part's last candidate
   }
-  if (spec && sig) {
-    if (!a.wb) {
-      snap[(size_t)a.n_iters * s + lane] = xc;
-    } else if (a.wb_x) {
-      a.wb_x[(size_t)cell * s + lane] = xc;
-    } else if (lane < a.wb_m) {
-      a.wb_cm[(size_t)cell * a.wb_m + lane] = xc;
-    } else {
-      const size_t pix = (size_t)a.wb_pos[2 * cell] * a.wb_C + a.wb_pos[2 * cell + 1];
-      st_map(a.wb_map, (size_t)(lane - a.wb_m) * a.wb_R * a.wb_C + pix, corr_out(xc, a.wb_corr, lane - a.wb_m),
-             a.wb_dtype);
+  if (spec) {
+#pragma unroll
+    for (int h = 0; h < SPL; ++h) {
+      if (!sig[h]) continue;
+      const int j = lane + h * G;
+      if (!a.wb) {
+        snap[(size_t)a.n_iters * s + j] = xc[h];
+      } else if (a.wb_x) {
+        a.wb_x[(size_t)cell * s + j] = xc[h];
+      } else if (j < a.wb_m) {
+        a.wb_cm[(size_t)cell * a.wb_m + j] = xc[h];
+      } else {
+        const size_t pix = (size_t)a.wb_pos[2 * cell] * a.wb_C + a.wb_pos[2 * cell + 1];
+        st_map(a.wb_map, (size_t)(j - a.wb_m) * a.wb_R * a.wb_C + pix, corr_out(xc[h], a.wb_corr, j - a.wb_m),
+               a.wb_dtype);
+      }
     }
   }
 #undef MS_E
@@ -835,7 +894,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
 // kStrided: a list launch of unknown length (a.count on the device) on a small grid; each block
 // walks the list in steps of the whole grid (the bound is block-uniform, so every wave runs the
 // same number of items and the wave-wide ballots / reductions inside stay convergent)
-template <int G, int NZ, bool kStrided, bool kSpec = false>
+template <int G, int NZ, bool kStrided, bool kSpec = false, int SPL = 1>
 __global__ void __launch_bounds__(kBlock, G == 32 ? 6 : (NZ == kNzReg ? 4 : 1)) integrate_fast_kernel(IntegrateArgs a, int32_t* wide_list,
                                                                 int32_t* wide_count) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
@@ -845,11 +904,11 @@ __global__ void __launch_bounds__(kBlock, G == 32 ? 6 : (NZ == kNzReg ? 4 : 1)) 
     const int n = *a.count;
     for (int base = (int)blockIdx.x * cpb; base < n; base += (int)gridDim.x * cpb) {
       wave_lds_sync();  // the previous item's LDS reads are done before its slot is refilled
-      integrate_item_fast<G, NZ, kSpec>(a, smem, base + (int)threadIdx.x / G, bits, wide_list, wide_count);
+      integrate_item_fast<G, NZ, kSpec, SPL>(a, smem, base + (int)threadIdx.x / G, bits, wide_list, wide_count);
     }
   } else {
-    integrate_item_fast<G, NZ, kSpec>(a, smem, (int)blockIdx.x * cpb + (int)threadIdx.x / G, bits, wide_list,
-                                      wide_count);
+    integrate_item_fast<G, NZ, kSpec, SPL>(a, smem, (int)blockIdx.x * cpb + (int)threadIdx.x / G, bits, wide_list,
+                                           wide_count);
   }
   or_block_bits(bits, a.mask_out);
 }
@@ -1234,7 +1293,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
   unsigned* mk = P_<unsigned>(masks);
   unsigned* zero_flags = mk + ms::kEqIters * nparts;
   float* snaps[2] = {P_<float>(snap_a), P_<float>(snap_b)};
-  const bool fast_path = lists != 0 && s <= 64 && (g_integrate_mode & 8) == 0;
+  const bool fast_path = lists != 0 && s <= 128 && (g_integrate_mode & 8) == 0;
   // Speculative all-parts path (s <= 32, the whole part range with the write-back, mode bits 3-7
   // clear): the reference's global exit (kinetics.py:846) cuts a part short only when no cell of the
   // whole population still has an impactful correction, which never happened in 40-step runs of any
@@ -1407,9 +1466,13 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     int32_t* wl2 = P_<int32_t>(lists);
     int32_t* wc2 = wc - 1;  // cleared with wc
     const int G = s <= 32 ? 32 : 64;
+    const bool two = s > 64;  // two signals per lane (64-lane groups, s <= 128)
     const int cps = kBlock / G;
-    const size_t lds_fast = (size_t)cps * (G == 32 ? fast_slot_words<32, kNzReg>() : fast_slot_words<64, kNzReg>()) * 4;
-    const size_t lds_fw = (size_t)(kBlock / 64) * fast_slot_words<64, kNzWide>() * 4;
+    const size_t lds_fast = (size_t)cps *
+                            (G == 32 ? fast_slot_words<32, kNzReg>()
+                                     : (two ? fast_slot_words<64, kNzReg, 2>() : fast_slot_words<64, kNzReg>())) * 4;
+    const size_t lds_fw =
+        (size_t)(kBlock / 64) * (two ? fast_slot_words<64, kNzWide, 2>() : fast_slot_words<64, kNzWide>()) * 4;
     const unsigned grid_fw = (unsigned)std::min<long long>(cdiv(c, kBlock / 64), 512);
     constexpr int kFusedWideBlocks = 64;
     const int slot_words = slot_words_for(P, s, sp);
@@ -1462,11 +1525,18 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
       } else {
         if (G == 32)
           integrate_fast_kernel<32, kNzReg, false><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
+        else if (two)
+          integrate_fast_kernel<64, kNzReg, false, false, 2><<<cdiv(c, cps), kBlock, lds_fast, st>>>(
+              a, part == 0 ? wl : nullptr, wc);
         else
           integrate_fast_kernel<64, kNzReg, false><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
         MS_LAUNCH_CHECK();
         if (fw) {
-          integrate_fast_kernel<64, kNzWide, true><<<grid_fw, kBlock, lds_fw, st>>>(aw, part == 0 ? wl2 : nullptr, wc2);
+          if (two)
+            integrate_fast_kernel<64, kNzWide, true, false, 2><<<grid_fw, kBlock, lds_fw, st>>>(
+                aw, part == 0 ? wl2 : nullptr, wc2);
+          else
+            integrate_fast_kernel<64, kNzWide, true><<<grid_fw, kBlock, lds_fw, st>>>(aw, part == 0 ? wl2 : nullptr, wc2);
           MS_LAUNCH_CHECK();
         }
       }

@@ -105,6 +105,62 @@ __device__ __forceinline__ void st4_stream<float>(float* p, const float v[4]) {
   __builtin_nontemporal_store(q, reinterpret_cast<f4*>(p));
 }
 
+// 8 consecutive, 8-element-aligned values: fp32 as two 16 B accesses, bf16 / fp16 as one 16 B
+// access with the packed hardware conversions (gfx950 v_cvt_pk_bf16_f32: round to nearest even,
+// as st<bf16_t>)
+template <class T>
+__device__ __forceinline__ void ld8(const T* p, float v[8]);
+template <>
+__device__ __forceinline__ void ld8<float>(const float* p, float v[8]) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+}
+template <>
+__device__ __forceinline__ void ld8<bf16_t>(const bf16_t* p, float v[8]) {
+  const uint4 q = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = __uint_as_float(w[j] << 16);
+    v[2 * j + 1] = __uint_as_float(w[j] & 0xFFFF0000u);
+  }
+}
+template <>
+__device__ __forceinline__ void ld8<_Float16>(const _Float16* p, float v[8]) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  const h8 q = *reinterpret_cast<const h8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)q[j];
+}
+
+template <class T>
+__device__ __forceinline__ void st8_stream(T* p, const float v[8]);
+template <>
+__device__ __forceinline__ void st8_stream<float>(float* p, const float v[8]) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4 a, b;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) a[j] = v[j], b[j] = v[j + 4];
+  __builtin_nontemporal_store(a, reinterpret_cast<f4*>(p));
+  __builtin_nontemporal_store(b, reinterpret_cast<f4*>(p) + 1);
+}
+template <>
+__device__ __forceinline__ void st8_stream<bf16_t>(bf16_t* p, const float v[8]) {
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  b8 q;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) q[j] = (__bf16)v[j];
+  *reinterpret_cast<b8*>(p) = q;
+}
+template <>
+__device__ __forceinline__ void st8_stream<_Float16>(_Float16* p, const float v[8]) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  h8 q;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) q[j] = (_Float16)v[j];
+  *reinterpret_cast<h8*>(p) = q;
+}
+
 // runtime-typed access (cold paths: a few pixels per cell)
 __device__ __forceinline__ float ld_map(const void* base, size_t i, int dtype) {
   switch (dtype) {

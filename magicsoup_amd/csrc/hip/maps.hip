@@ -228,6 +228,128 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
   }
 }
 
+// Eight columns per lane (C % 8 == 0): a wave covers 512 columns with 16 B accesses only (fp32:
+// two per row, bf16 / fp16: one, converted with packed instructions), so every wave keeps twice the
+// bytes of the 4-column kernel in flight per row and half the instructions per byte -- the
+// 4-column kernel reached ~5 TB/s on fp32 and stayed issue-bound on the 2-byte types. Same tiling
+// (4 waves = 4 consecutive 32-row bands of one column strip), same one-row-ahead prefetch, same
+// fp64 partials (the 8 values of a row are summed in fp32 first, as pairs of 4).
+template <class T>
+__global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                               const float* __restrict__ wa,
+                                                               const float* __restrict__ wb,
+                                                               const float* __restrict__ scale,
+                                                               const float* __restrict__ corr, MGeom g,
+                                                               double* __restrict__ partials, int gx, int gy,
+                                                               int ntiles) {
+  __shared__ double red[2][4];
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int bx = tile % gx, by = (tile / gx) % gy, mol = tile / (gx * gy);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int H = g.r_hi - g.r_lo;
+    const int y0 = bx * 512 + lane * 8;
+    const bool col = y0 < g.C;
+    const bool need_l = lane == 0 && col, need_r = col && (lane == 63 || y0 + 8 >= g.C);
+    const int yl = y0 == 0 ? g.C - 1 : y0 - 1, yr = y0 + 8 >= g.C ? 0 : y0 + 8;
+    const size_t plane = (size_t)g.R * g.C;
+    const T* src = in + (size_t)mol * plane;
+    T* dst = out + (size_t)mol * plane;
+    const float sc = scale ? scale[mol] : 1.0f;
+    const float a = wa[mol], b = wb[mol];
+    const bool has_c = corr != nullptr;
+    const float cm = has_c ? corr[mol] : 0.0f;
+    const int o0 = (by * 4 + wv) * kVBand, o1 = min(H, o0 + kVBand);
+
+    auto row_of = [&](int o) {
+      int x = g.r_lo + o;
+      if (x < 0) x += g.R;
+      if (x >= g.R) x -= g.R;
+      return x;
+    };
+    struct Raw {
+      float v[8], el, er;
+    };
+    auto fetch = [&](int o, Raw& r) {
+      const size_t base = (size_t)row_of(o) * g.C;
+      if (col) {
+        ld8(src + base + y0, r.v);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r.v[j] = 0.0f;
+      }
+      r.el = need_l ? ld(src + base + yl) : 0.0f;
+      r.er = need_r ? ld(src + base + yr) : 0.0f;
+    };
+    auto cin = [&](float raw) { return (has_c ? fmaxf(raw + cm, 0.0f) : raw) * sc; };
+    auto finish = [&](const Raw& r, float v[8], float& L, float& Rn) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = cin(r.v[j]);
+      const float up = __shfl_up(v[7], 1), dn = __shfl_down(v[0], 1);
+      L = need_l ? cin(r.el) : up;
+      Rn = need_r ? cin(r.er) : dn;
+    };
+    auto hsum = [](const float v[8], float L, float Rn, float h[8]) {
+      h[0] = L + v[0] + v[1];
+#pragma unroll
+      for (int j = 1; j < 7; ++j) h[j] = v[j - 1] + v[j] + v[j + 1];
+      h[7] = v[6] + v[7] + Rn;
+    };
+
+    double before = 0.0, after = 0.0;
+    if (o0 < H) {
+      Raw rp, rc, rn, rn2;
+      fetch(o0 - 1, rp);
+      fetch(o0, rc);
+      fetch(o0 + 1, rn);
+      float vp[8], Lp, Rp, vc[8], Lc, Rc, hp[8], hc[8];
+      finish(rp, vp, Lp, Rp);
+      finish(rc, vc, Lc, Rc);
+      hsum(vp, Lp, Rp, hp);
+      hsum(vc, Lc, Rc, hc);
+      for (int o = o0; o < o1; ++o) {
+        if (o + 2 <= o1) fetch(o + 2, rn2);  // row o + 2 (at most the halo row below the band)
+        float vn[8], Ln, Rn, hn[8];
+        finish(rn, vn, Ln, Rn);
+        hsum(vn, Ln, Rn, hn);
+        float res[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float lft = j == 0 ? Lc : vc[j - 1], rgt = j == 7 ? Rc : vc[j + 1];
+          res[j] = b * vc[j] + a * (hp[j] + hn[j] + lft + rgt);
+        }
+        if (col) {
+          st8_stream(dst + (size_t)row_of(o) * g.C + y0, res);
+          before += (double)((vc[0] + vc[1]) + (vc[2] + vc[3])) + (double)((vc[4] + vc[5]) + (vc[6] + vc[7]));
+          after += (double)((res[0] + res[1]) + (res[2] + res[3])) + (double)((res[4] + res[5]) + (res[6] + res[7]));
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          hp[j] = hc[j];
+          hc[j] = hn[j];
+          vc[j] = vn[j];
+        }
+        Lc = Ln;
+        Rc = Rn;
+        rn = rn2;
+      }
+    }
+    before = wave_sum_d(before);
+    after = wave_sum_d(after);
+    if (lane == 0) {
+      red[0][wv] = before;
+      red[1][wv] = after;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const size_t tiles = (size_t)gx * gy;
+      const size_t t = (size_t)by * gx + bx;
+      partials[((size_t)mol * tiles + t) * 2] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+      partials[((size_t)mol * tiles + t) * 2 + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    }
+    __syncthreads();  // red is refilled by the next tile
+  }
+}
+
 // one block per molecule: totals[mol] = (sum before, sum after) over the owned rows
 __global__ void __launch_bounds__(256) diffuse_reduce_kernel(const double* partials, int tiles, double* totals) {
   __shared__ double sb[4], sa[4];
@@ -398,7 +520,12 @@ static MGeom mgeom(int R, int C, int r_lo, int r_hi, int wrap) {
     default: throw std::invalid_argument("unknown molecule map dtype");  \
   }
 
-static bool use_vec4(int C) { return C % 4 == 0; }
+// stencil variant: 8 columns per lane when C % 8 == 0 (default), 4 when C % 4 == 0 (also selectable
+// with set_stencil_vec(4) for A/Bs), else 1
+static int g_stencil_vec = 8;
+void set_stencil_vec(int v) { g_stencil_vec = v; }
+static bool use_vec8(int C) { return g_stencil_vec >= 8 && C % 8 == 0; }
+static bool use_vec4(int C) { return g_stencil_vec >= 4 && C % 4 == 0; }
 
 // Blocks of the vector stencil launch (0: one per tile). 256 CUs x 4 workgroups (4 waves per SIMD)
 // still reach the stencil's full HBM rate and leave 3 of the 7 slots a CU holds at its register use
@@ -409,8 +536,11 @@ static int g_stencil_blocks = 256 * 4;
 void set_stencil_blocks(int n) { g_stencil_blocks = std::max(0, n); }
 
 size_t diffuse_partials_len(int m, int C, int H) {
-  if (use_vec4(C)) return (size_t)cdiv(C, 256) * cdiv(cdiv(H, kVBand), 4) * m * 2;
-  return (size_t)cdiv(C, 64 * kWaves) * cdiv(H, kBand) * m * 2;
+  // (the largest layout of any variant: the variant may be switched between calls)
+  const size_t v8 = (size_t)cdiv(C, 512) * cdiv(cdiv(H, kVBand), 4) * m * 2;
+  const size_t v4 = (size_t)cdiv(C, 256) * cdiv(cdiv(H, kVBand), 4) * m * 2;
+  const size_t v1 = (size_t)cdiv(C, 64 * kWaves) * cdiv(H, kBand) * m * 2;
+  return std::max(v8, std::max(v4, v1));
 }
 
 void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
@@ -420,9 +550,18 @@ void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_
   const MGeom g = mgeom(R, C, r_lo, r_hi, wrap);
   hipStream_t st_ = S_(stream);
   const int H = r_hi - r_lo;
-  const bool v4 = use_vec4(C);
-  const dim3 grid = v4 ? dim3(cdiv(C, 256), cdiv(cdiv(H, kVBand), 4), m) : dim3(cdiv(C, 64 * kWaves), cdiv(H, kBand), m);
-  if (v4) {
+  const bool v8 = use_vec8(C), v4 = !v8 && use_vec4(C);
+  const dim3 grid = v8   ? dim3(cdiv(C, 512), cdiv(cdiv(H, kVBand), 4), m)
+                    : v4 ? dim3(cdiv(C, 256), cdiv(cdiv(H, kVBand), 4), m)
+                         : dim3(cdiv(C, 64 * kWaves), cdiv(H, kBand), m);
+  if (v8) {
+    const int ntiles = (int)(grid.x * grid.y * grid.z);
+    const int blocks = g_stencil_blocks > 0 ? std::min(ntiles, g_stencil_blocks) : ntiles;
+    MS_MAP_DISPATCH(dtype, (diffuse_stencil8_kernel<T><<<blocks, 256, 0, st_>>>(
+                               P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
+                               corr ? P_<float>(corr) : nullptr, g, P_<double>(partials), (int)grid.x, (int)grid.y,
+                               ntiles)));
+  } else if (v4) {
     const int ntiles = (int)(grid.x * grid.y * grid.z);
     const int blocks = g_stencil_blocks > 0 ? std::min(ntiles, g_stencil_blocks) : ntiles;
     MS_MAP_DISPATCH(dtype, (diffuse_stencil4_kernel<T><<<blocks, 256, 0, st_>>>(

@@ -25,7 +25,8 @@ struct CellParams {
 // all kEqIters iterations). Writes the kSnap candidate states to snap[k*s + j] and returns the
 // per-iteration "impactful correction" bits.
 unsigned cell_part(const CellParams& q, int np, int s, const float* X0, float trim, int n_iters, float* snap,
-                   float* V, float* Va, float* F, unsigned char* fwd, unsigned char* imp, float* cons, float* fs) {
+                   float* V, float* Va, float* F, unsigned char* fwd, unsigned char* imp, float* cons, float* fs,
+                   uint8_t* dec, int dec_stride) {
   // velocities (kinetics.py:771-806). A protein with Vmax' == 0 has V == 0 and contributes nothing
   // to any later stage (no NV, no impact flag), so it is skipped by marking V = 0 early.
   for (int p = 0; p < np; ++p) {
@@ -143,6 +144,7 @@ unsigned cell_part(const CellParams& q, int np, int s, const float* X0, float tr
       bool high = fwd[p] ? (qke > ms::kUpper) : (qke < ms::kLower);
       if (!fwd[p] && F[p] == 0.0f) high = false;
       if ((low || high) && imp[p]) bits |= 1u << it;
+      if (dec) dec[(size_t)it * dec_stride + p] = (uint8_t)((low ? 1 : 0) | (high ? 2 : 0));
       float f = F[p];
       if (high) f -= inc;
       if (low) f += inc;
@@ -170,7 +172,7 @@ unsigned cell_part(const CellParams& q, int np, int s, const float* X0, float tr
 // world ORs the masks of all ranks, reproducing the reference's `torch.any` over the population).
 py::list integrate_signals(farr X, iarr N, iarr Nf, iarr Nb, iarr A, farr Kmr, farr Kmf, farr Kmb, farr Vmax,
                            farr Ke, py::object nprot_obj, std::vector<float> trims, int n_iters,
-                           py::object reduce_mask) {
+                           py::object reduce_mask, py::object decisions_obj) {
   if (X.ndim() != 2 || N.ndim() != 3) throw std::invalid_argument("X must be (c,s) and N (c,p,s)");
   const int c = (int)X.shape(0), s = (int)X.shape(1), P = (int)N.shape(1);
   if (N.shape(0) < c || N.shape(2) != s) throw std::invalid_argument("param/signal shape mismatch");
@@ -181,9 +183,20 @@ py::list integrate_signals(farr X, iarr N, iarr Nf, iarr Nb, iarr A, farr Kmr, f
     np_arr = nprot_obj.cast<iarr>();
     nprot = np_arr.data();
   }
+  // decisions (optional, diagnostics / decision-aware oracle tests): uint8 (c, parts, kEqIters, P),
+  // bit 0 "low" (factor raised), bit 1 "high" (factor lowered) of every damping iteration
+  uint8_t* dec = nullptr;
+  py::array_t<uint8_t, py::array::c_style> dec_arr;
+  if (!decisions_obj.is_none()) {
+    dec_arr = decisions_obj.cast<py::array_t<uint8_t, py::array::c_style>>();
+    if (dec_arr.size() < (py::ssize_t)((size_t)c * trims.size() * ms::kEqIters * P))
+      throw std::invalid_argument("decisions buffer too small");
+    dec = dec_arr.mutable_data();
+  }
   float* x = X.mutable_data();
   std::vector<float> snaps((size_t)c * ms::kSnap * s);
   py::list masks;
+  int part = 0;
   for (float trim : trims) {
     unsigned mask = 0;
     {
@@ -199,8 +212,9 @@ py::list integrate_signals(farr X, iarr N, iarr Nf, iarr Nb, iarr A, farr Kmr, f
                        Kmf.data() + o2, Kmb.data() + o2, Vmax.data() + o2, Ke.data() + o2};
           int np = nprot ? nprot[i] : P;
           if (np > P) np = P;
+          uint8_t* d = dec ? dec + (((size_t)i * trims.size() + part) * ms::kEqIters) * P : nullptr;
           mask |= cell_part(q, np, s, x + (size_t)i * s, trim, n_iters, snaps.data() + (size_t)i * ms::kSnap * s,
-                            V.data(), Va.data(), F.data(), fwd.data(), imp.data(), cons.data(), fs.data());
+                            V.data(), Va.data(), F.data(), fwd.data(), imp.data(), cons.data(), fs.data(), d, P);
         }
       }
     }
@@ -218,6 +232,7 @@ py::list integrate_signals(farr X, iarr N, iarr Nf, iarr Nb, iarr A, farr Kmr, f
         std::memcpy(x + (size_t)i * s, snaps.data() + ((size_t)i * ms::kSnap + stop) * s, sizeof(float) * s);
     }
     masks.append(mask);
+    ++part;
   }
   return masks;
 }
@@ -325,7 +340,8 @@ void build_params(iarr tokens, iarr rows, farr vmax_w, farr km_w, iarr signs, ia
 void bind_kinetics(py::module_& m) {
   m.def("integrate_signals", &integrate_signals, py::arg("X"), py::arg("N"), py::arg("Nf"), py::arg("Nb"),
         py::arg("A"), py::arg("Kmr"), py::arg("Kmf"), py::arg("Kmb"), py::arg("Vmax"), py::arg("Ke"),
-        py::arg("nprot"), py::arg("trims"), py::arg("n_iters"), py::arg("reduce_mask") = py::none());
+        py::arg("nprot"), py::arg("trims"), py::arg("n_iters"), py::arg("reduce_mask") = py::none(),
+        py::arg("decisions") = py::none());
   m.def("build_params", &build_params);
 }
 

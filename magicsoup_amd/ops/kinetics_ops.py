@@ -24,9 +24,11 @@ def _np(t: torch.Tensor):
     return t.detach().numpy()
 
 
-def integrate(kin, X: torch.Tensor, trims, n_iters: int, reduce_mask=None) -> list[int]:
+def integrate(kin, X: torch.Tensor, trims, n_iters: int, reduce_mask=None, decisions=None) -> list[int]:
     """Fused integrate_signals on X (c, s) in place; returns the per-part iteration masks.
-    ``reduce_mask`` (host path) maps a part's local iteration mask to the global one."""
+    ``reduce_mask`` (host path) maps a part's local iteration mask to the global one.
+    ``decisions`` (host path, diagnostics): a uint8 numpy array (c, parts, 4, P) receiving every
+    protein's damping decision per iteration (bit 0 low, bit 1 high)."""
     c = X.size(0)
     if c == 0:
         return []
@@ -48,6 +50,7 @@ def integrate(kin, X: torch.Tensor, trims, n_iters: int, reduce_mask=None) -> li
         [float(t) for t in trims],
         int(n_iters),
         reduce_mask,
+        decisions,
     )
     return list(masks)
 

@@ -16,7 +16,21 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--vec", type=int, nargs="*", default=[8], help="stencil variants (columns per lane) to A/B")
+    ap.add_argument("--blocks", type=int, nargs="*", default=[1024], help="stencil grid sizes (0: one block per tile)")
     a = ap.parse_args()
+    from magicsoup_amd.ops import native
+
+    for vec in a.vec:
+        for blocks in a.blocks:
+            native.hip().set_stencil_vec(vec)
+            native.hip().set_stencil_blocks(blocks)
+            run(a, f"vec{vec}_blocks{blocks}")
+    native.hip().set_stencil_vec(8)
+    native.hip().set_stencil_blocks(1024)
+
+
+def run(a, tag):
     out = {}
     for name, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16), ("fp16", torch.float16)):
         w = ms.World(chemistry=CHEMISTRY, map_size=a.size, device="cuda", seed=0, map_dtype=dt)
@@ -39,7 +53,7 @@ def main():
                      "eff_TBps": round(2 * nbytes / (ms_it * 1e-3) / 1e12, 3)}
         del w
         torch.cuda.empty_cache()
-    print(json.dumps({"size": a.size, "n_mol": len(CHEMISTRY.molecules), "diffuse": out}))
+    print(json.dumps({"variant": tag, "size": a.size, "n_mol": len(CHEMISTRY.molecules), "diffuse": out}), flush=True)
 
 
 if __name__ == "__main__":

@@ -38,6 +38,8 @@ for s in "$@"; do case "$s" in
   tflag) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/tflag -o run --output-format csv -- \
             python bench.py --steps 20 --warmup 20 > $O/tflag.log 2>&1;
           python scripts/step_kernels.py $O/tflag/run_kernel_trace.csv 19 > $O/tflag_steps.txt 2>&1; echo "   traced" ;;
+  dbench) run diffuse_bench 300 python scripts/diffuse_bench.py --vec 4 8 --blocks 1024 0 2048 ;;
+  dtests) run dtests 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "diffusion or reduced_precision or permeation" ;;
   *) echo "unknown step $s"; exit 2 ;;
 esac; done
 exit 0

@@ -97,8 +97,22 @@ def test_integrator_matches_torch_oracle(n_iters):
     # reduction tree vs our per-signal loop), and Q = 0 vs Q = tiny can flip such a decision. This is
     # a property of the reference algorithm (its CPU and CUDA paths differ the same way), so the
     # oracle comparison is per cell; exact agreement is required between our two native cores.
-    close = torch.isclose(Xk, Xr, rtol=1e-3, atol=1e-3).all(dim=1)
-    assert close.float().mean() > (0.999 if n_iters == 0 else 0.85), close.float().mean()
+    close = torch.isclose(Xk, Xr, rtol=1e-3, atol=1e-3).all(dim=1).cpu().numpy()
+    if n_iters == 0:
+        assert close.mean() > 0.999, close.mean()
+        return
+    # decision-aware: only cells with a damping decision at a Q/Ke threshold (float64 population
+    # oracle, relative margin 1e-3) may differ between two float32 operation orders
+    import numpy as np
+
+    from tests.test_kinetics import _oracle_population
+
+    params = [{k: getattr(kin, k)[c].double().cpu().numpy() for k in ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb",
+                                                                       "Vmax", "Ke")} for c in range(X.size(0))]
+    _, border = _oracle_population(params, X.double().cpu().numpy(), (0.7, 0.2, 0.1), n_iters, margin=1e-3)
+    border = np.array(border)
+    # (a cell counts as ill-conditioned when any of its decisions is: the bulk still agrees outright)
+    assert close.mean() >= 0.9 and close[~border].all(), (close.mean(), np.nonzero(~close & ~border))
 
 
 def test_integrator_matches_host_core():
@@ -709,7 +723,7 @@ def _integrate_modes(kin, X, modes=(0, 8)):
     return out
 
 
-@pytest.mark.parametrize("case", ["wl500", "wl3000", "syn20", "syn40", "big_exponents"])
+@pytest.mark.parametrize("case", ["wl500", "wl3000", "syn20", "syn40", "syn64", "big_exponents", "syn64_big_exponents"])
 def test_register_integrator_matches_lds_integrator_bit_for_bit(case):
     """The register-resident launches (mode 0: cells with <= 32 / 64 active proteins and <= 16
     non-zero signals per protein; the rest through a 64-lane launch with 32 non-zeros per protein,
@@ -719,7 +733,7 @@ def test_register_integrator_matches_lds_integrator_bit_for_bit(case):
     if case.startswith("syn"):
         from magicsoup_amd.examples.synthetic import make_chemistry
 
-        m = int(case[3:])
+        m = int(case[3:].split("_")[0])
         chem = make_chemistry(m, 2 * m, seed=3)
     else:
         chem = CHEMISTRY
@@ -729,10 +743,12 @@ def test_register_integrator_matches_lds_integrator_bit_for_bit(case):
     size = 3000 if case == "wl3000" else 500
     w.spawn_cells(gen_genomes(300, size))
     kin = w.kinetics
-    if case == "big_exponents":
-        # stoichiometries / Hill numbers beyond the branch-free power range (>= 8) in some proteins
+    if case.endswith("big_exponents"):
+        # stoichiometries / Hill numbers beyond the branch-free power range (>= 8) in some proteins,
+        # and (two signals per lane) beyond its 16-bit entries' exponent range (>= 16)
         Nf, A = kin.Nf.clone(), kin.A.clone()
         Nf[::7, :, 1] = torch.where(Nf[::7, :, 1] > 0, 9, Nf[::7, :, 1])
+        Nf[::11, :, 0] = torch.where(Nf[::11, :, 0] > 0, 17, Nf[::11, :, 0])
         A[::5, :, 2] = torch.where(A[::5, :, 2] != 0, -9, A[::5, :, 2])
         kin.Nf, kin.A = Nf, A
     na = (kin.Vmax > 0).sum(1)
