@@ -341,6 +341,7 @@ class DistributedWorld(World):
         cmap = self.cell_map
         got = 0
         flags = {}
+        arrived = {"up": 0, "dn": 0}
         # records from the upper neighbour land on our first row, from the lower one on our last
         for key, buf, meta, row in (("up", b_up, m_up, 1), ("dn", b_dn, m_dn, self.H)):
             if buf.size(0) == 0:
@@ -349,7 +350,9 @@ class DistributedWorld(World):
             r = self._unpack_records(buf, meta)
             ys = r["ys"].long()
             ok = ~cmap[row, ys]
-            got += self._append_records(r, row, ok)
+            got_k = self._append_records(r, row, ok)
+            got += got_k
+            arrived[key] = got_k
             flags[key] = ok.to(_U8)
         k_up = 0 if rec_up[0] is None else int(rec_up[0].size(0))
         k_dn = 0 if rec_dn[0] is None else int(rec_dn[0].size(0))
@@ -360,6 +363,7 @@ class DistributedWorld(World):
         self._exchange(flags["up"], flags["dn"], f_dn, f_up)
         acc_up = f_up.bool() if k_up else torch.zeros(0, dtype=torch.bool, device=dev)
         acc_dn = f_dn.bool() if k_dn else torch.zeros(0, dtype=torch.bool, device=dev)
+        self.__dict__["_arrived"] = (arrived["up"], arrived["dn"])
         return acc_up, acc_dn, got
 
     # ------------------------------------------------------------------ physics overrides
@@ -484,6 +488,8 @@ class DistributedWorld(World):
         mig = self.migrated
         mig["divided_out"] += n_up + n_dn
         mig["divided_in"] += hdr_up[0] + hdr_dn[0]
+        # what crossed a boundary, in record order (read by the global-index view, GlobalWorld)
+        self.__dict__["_xfer"] = (par_up, par_dn, int(hdr_up[0]), int(hdr_dn[0]))
         return (par_loc if n_loc else empty), children
 
     def _append_arrivals(self, hdr_up, in_up, hdr_dn, in_dn) -> None:
@@ -548,7 +554,9 @@ class DistributedWorld(World):
         acc_up, acc_dn, got = self._migrate(rec_up, rec_dn)
         self.cell_map[0] = False
         self.cell_map[self.H + 1] = False
-        gone = torch.cat([m_up[acc_up], m_dn[acc_dn]])
+        out_up, out_dn = m_up[acc_up], m_dn[acc_dn]
+        gone = torch.cat([out_up, out_dn])
+        self.__dict__["_xfer"] = (out_up, out_dn) + tuple(self.__dict__.pop("_arrived"))
         mig = self.migrated
         mig["moved_in"] += got
         mig["moved_out"] += int(gone.numel())
@@ -869,6 +877,13 @@ class DistributedWorld(World):
         lo = int(np.sum(counts[: self.rank]))
         mine = [genomes[int(i)] for i in order[lo : lo + int(counts[self.rank])]]
         return self.spawn_cells(mine) if mine else []
+
+    def global_view(self):
+        """Collective: a :class:`~magicsoup_amd.parallel.GlobalWorld` over this world (the
+        reference ``World`` API with global cell indices)."""
+        from magicsoup_amd.parallel.global_world import GlobalWorld
+
+        return GlobalWorld(self)
 
     def kill_cells_local_all(self) -> None:
         """Remove every local cell without spilling molecules (state reset)."""

@@ -1,0 +1,171 @@
+"""GlobalWorld: the reference World API with global cell indices over a DistributedWorld (CPU, gloo).
+
+The reference's index semantics are the oracle (python/magicsoup/world.py): new cells are appended
+at the end (spawn 318, add 374, divide 451), kill shifts later indices down (506-510), move and
+reposition keep indices; cells are identified across ops by their unique random labels."""
+import torch
+
+from tests.dist_utils import run_ranks
+from tests.test_distributed import _chem
+
+
+def _view(ws_strips=None, map_size=16, seed=5):
+    from magicsoup_amd.parallel import DistributedWorld, GlobalWorld
+
+    dw = DistributedWorld(chemistry=_chem(), map_size=map_size, seed=seed, strips=ws_strips)
+    return dw, GlobalWorld(dw)
+
+
+def _check(gw):
+    import numpy as np
+    import torch.distributed as dist
+
+    pos = gw.cell_positions.long()  # (collective: settles the numbering first)
+    n = gw.n_cells
+    S = gw.map_size
+    assert (pos[:, 0] * S + pos[:, 1]).unique().numel() == n
+    cmap = gw.cell_map
+    assert int(cmap.sum()) == n and bool(cmap[pos[:, 0], pos[:, 1]].all())
+    # the table is identical on every rank and a bijection onto each rank's rows
+    tabs = [None] * gw.dw.world_size
+    dist.all_gather_object(tabs, (gw._rank.tolist(), gw._local.tolist()))
+    assert all(t == tabs[0] for t in tabs)
+    mine = np.sort(gw._local[gw._rank == gw.dw.rank])
+    assert mine.tolist() == list(range(gw.dw.n_cells))
+    assert len(gw.cell_genomes) == n == len(gw.cell_labels)
+
+
+def _mass(gw):
+    return float(gw.molecule_map.double().sum() + gw.cell_molecules.double().sum())
+
+
+def _torus_dist(a, b, S):
+    d = (a.long() - b.long()).abs()
+    return torch.minimum(d, S - d).max(dim=1).values
+
+
+def _body(rank, ws, strips, map_size=16):
+    import random
+
+    import magicsoup_amd as ms
+
+    random.seed(21)  # the same genome list on every rank
+    genomes = [ms.random_genome(200) for _ in range(70)]
+    dw, gw = _view(strips, map_size)
+    S = gw.map_size
+    assert gw.spawn_cells(genomes) == list(range(70))
+    assert gw.cell_genomes == genomes
+    labels = gw.cell_labels
+    assert len(set(labels)) == 70
+    _check(gw)
+    if ws > 1:  # uniform over the whole torus: every strip got cells
+        assert dw.n_cells > 10
+    m0 = _mass(gw)
+
+    # kill: removed indices disappear, later ones shift down, the molecules spill
+    mols = gw.cell_molecules
+    kill = [0, 5, 17, 69, 33, 5]
+    gw.kill_cells(kill)
+    keep = [i for i in range(70) if i not in kill]
+    assert gw.cell_labels == [labels[i] for i in keep]
+    assert torch.equal(gw.cell_molecules, mols[keep])
+    assert abs(_mass(gw) - m0) < 1e-6 * m0
+    _check(gw)
+
+    # divide: parents keep their index, children are appended in parent order, molecules halve
+    labels, pos, mols, divs = gw.cell_labels, gw.cell_positions, gw.cell_molecules, gw.cell_divisions
+    n0 = gw.n_cells
+    pairs = gw.divide_cells(list(range(0, n0, 2)) + [1])
+    assert len(pairs) > 10
+    assert [c for _, c in pairs] == list(range(n0, n0 + len(pairs)))
+    assert [p for p, _ in pairs] == sorted(p for p, _ in pairs)
+    nl, npos, nm, nd = gw.cell_labels, gw.cell_positions, gw.cell_molecules, gw.cell_divisions
+    assert nl[:n0] == labels and torch.equal(npos[:n0], pos)
+    par = torch.tensor([p for p, _ in pairs])
+    ch = torch.tensor([c for _, c in pairs])
+    assert [nl[c] for c in ch.tolist()] == [labels[p] for p in par.tolist()]
+    assert bool((_torus_dist(npos[ch], pos[par], S) == 1).all())
+    torch.testing.assert_close(nm[ch], mols[par] * 0.5)
+    torch.testing.assert_close(nm[par], mols[par] * 0.5)
+    assert torch.equal(nd[ch], divs[par] + 1) and torch.equal(nd[par], divs[par] + 1)
+    assert abs(_mass(gw) - m0) < 1e-5 * m0
+    if ws > 1:  # children were born across strip boundaries (the arrival bookkeeping is exercised)
+        assert sum(gw._gather(dw.migrated["divided_in"])) > 0
+    _check(gw)
+
+    # move: indices and labels stay, every cell moves at most one pixel
+    labels, pos, mols = gw.cell_labels, gw.cell_positions, gw.cell_molecules
+    gw.move_cells()
+    assert gw.cell_labels == labels
+    assert torch.equal(gw.cell_molecules, mols)
+    assert bool((_torus_dist(gw.cell_positions, pos, S) <= 1).all())
+    if ws > 1:
+        assert sum(gw._gather(dw.migrated["moved_in"])) > 0
+    _check(gw)
+
+    # reposition: indices, labels and molecules stay, cells change rank
+    before = gw._rank.copy()
+    gw.reposition_cells()
+    assert gw.cell_labels == labels
+    assert torch.equal(gw.cell_molecules, mols)
+    if ws > 1:
+        assert (gw._rank != before).any()
+    _check(gw)
+
+    # get_cell by index / position / label
+    c = gw.get_cell(by_idx=3)
+    assert c.label == labels[3] and c.idx == 3
+    assert gw.get_cell(by_position=c.position).idx == 3
+    assert gw.get_cell(by_label=labels[7]).idx == 7
+    torch.testing.assert_close(torch.as_tensor(c.int_molecules), mols[3])
+
+    # add_cells keeps state; the new cells are appended
+    n1 = gw.n_cells
+    cells = [gw.get_cell(by_idx=i) for i in range(4)]
+    new = gw.add_cells(cells)
+    assert new == list(range(n1, n1 + 4))
+    assert gw.cell_labels[n1:] == [c.label for c in cells]
+    torch.testing.assert_close(gw.cell_molecules[n1:], torch.stack([torch.as_tensor(c.int_molecules) for c in cells]))
+    _check(gw)
+
+    # neighbours over the global torus agree with a brute-force scan of the positions
+    pos = gw.cell_positions.long()
+    n = gw.n_cells
+    want = sorted((a, b) for a in range(n) for b in range(a + 1, n) if int(_torus_dist(pos[a : a + 1], pos[b : b + 1], S)) == 1)
+    assert gw.get_neighbors(list(range(n))) == want
+
+    # update / mutate / recombinate by global index
+    gw.update_cells([(genomes[0], 2)])
+    assert gw.cell_genomes[2] == genomes[0]
+    g_before = gw.cell_genomes
+    gw.mutate_cells([0, 1], p=0.05)
+    g_after = gw.cell_genomes
+    assert g_after[2:] == g_before[2:] and g_after[:2] != g_before[:2]
+    gw.recombinate_cells(p=1e-3)
+    gw.enzymatic_activity()
+    gw.diffuse_molecules()
+    gw.degrade_molecules()
+    gw.increment_cell_lifetimes()
+    _check(gw)
+
+    # rank-local ops invalidate the numbering: the next call renumbers rank by rank
+    dw.kill_cells([0])
+    n_loc = gw._gather(dw.n_cells)
+    _check(gw)
+    assert gw.n_cells == sum(n_loc)
+
+
+def test_global_view_two_ranks():
+    run_ranks(_body, 2, None)
+
+
+def test_global_view_three_ranks():
+    run_ranks(_body, 3, None, 18)
+
+
+def test_global_view_one_rank_virtual_strips():
+    run_ranks(_body, 1, True)
+
+
+def test_global_view_one_rank_plain():
+    run_ranks(_body, 1, False)
