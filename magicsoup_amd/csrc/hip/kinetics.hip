@@ -894,8 +894,11 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
 // kStrided: a list launch of unknown length (a.count on the device) on a small grid; each block
 // walks the list in steps of the whole grid (the bound is block-uniform, so every wave runs the
 // same number of items and the wave-wide ballots / reductions inside stay convergent)
+#ifndef MS_SPL2_WAVES
+#define MS_SPL2_WAVES 4  // waves per SIMD the two-signals-per-lane launches are compiled for
+#endif
 template <int G, int NZ, bool kStrided, bool kSpec = false, int SPL = 1>
-__global__ void __launch_bounds__(kBlock, G == 32 ? 6 : (NZ == kNzReg ? 4 : 1)) integrate_fast_kernel(IntegrateArgs a, int32_t* wide_list,
+__global__ void __launch_bounds__(kBlock, G == 32 ? 6 : (NZ == kNzReg ? (SPL == 2 ? MS_SPL2_WAVES : 4) : 1)) integrate_fast_kernel(IntegrateArgs a, int32_t* wide_list,
                                                                 int32_t* wide_count) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
   unsigned bits = 0u;
@@ -1076,38 +1079,45 @@ __global__ void __launch_bounds__(kBlock) gather_x_kernel(int c, int s, int m, i
   snap[(size_t)cell * ms::kSnap * s + j] = x;
 }
 
-// Input of the speculative all-parts path (s <= 32): X (the explicit X, or gathered from the world
+// Input of the speculative all-parts path: X (the explicit X, or gathered from the world
 // like gather_x_kernel) -> candidate 0 of `snap`, one 32-lane group per cell; the cells with more
 // than 32 active proteins go to the wide list (count wide[0], zero on entry: the write-back kernel
 // resets it) for the front blocks of the speculative launch. Block 0 clears the launch's flag words
 // and the speculative flags + unfit word (wide[4 ..]).
+// G = 64 (s in 33..128): 64 lanes per cell, each lane loads signals lane, lane + 64; no wide list
+// (the register launches pass cells they cannot take on to the next level themselves).
+template <int G>
 __global__ void __launch_bounds__(kBlock) gather_bin_kernel(int c, int s, int m, int R, int C, int P,
                                                             const float* X, const float* cell_mols,
                                                             const void* molmap, int map_dtype, const float* corr,
                                                             const int32_t* positions, const float4* Q,
                                                             const int64_t* prow, float trim0, float* snap,
                                                             int32_t* wide_list, unsigned* wide, unsigned* zero,
-                                                            int nz, int32_t* zero_wc, float* save) {
+                                                            int nz, int32_t* zero_wc, float* save, int nparts,
+                                                            bool void_spec) {
   clear_words(zero, nz, zero_wc);
-  if (blockIdx.x == 0 && threadIdx.x < ms::kEqIters * kMaxParts + 1) wide[4 + threadIdx.x] = 0u;
-  const int lane = threadIdx.x & 31;
-  const int cell = (int)blockIdx.x * (kBlock / 32) + (int)threadIdx.x / 32;
+  // (void_spec, mode bit 9, for tests: the unfit word starts set, so the exact launches run)
+  if (blockIdx.x == 0 && threadIdx.x < ms::kEqIters * kMaxParts + 1)
+    wide[4 + threadIdx.x] = (void_spec && threadIdx.x == ms::kEqIters * nparts) ? 1u : 0u;
+  const int lane = threadIdx.x & (G - 1);
+  const int cell = (int)blockIdx.x * (kBlock / G) + (int)threadIdx.x / G;
   const bool ok = cell < c;
-  if (ok && lane < s) {
+  for (int j = lane; ok && j < s; j += G) {
     float x;
     if (X) {
-      x = X[(size_t)cell * s + lane];
-    } else if (lane < m) {
-      x = cell_mols[(size_t)cell * m + lane];
-      if (save) save[(size_t)cell * s + lane] = x;
+      x = X[(size_t)cell * s + j];
+    } else if (j < m) {
+      x = cell_mols[(size_t)cell * m + j];
+      if (save) save[(size_t)cell * s + j] = x;
     } else {
       const size_t pix = (size_t)positions[2 * cell] * C + positions[2 * cell + 1];
-      const float raw = ld_map(molmap, (size_t)(lane - m) * R * C + pix, map_dtype);
-      if (save) save[(size_t)cell * s + lane] = raw;  // cell_state_io layout: (molecules | raw pixels)
-      x = corr_in(raw, corr, lane - m);
+      const float raw = ld_map(molmap, (size_t)(j - m) * R * C + pix, map_dtype);
+      if (save) save[(size_t)cell * s + j] = raw;  // cell_state_io layout: (molecules | raw pixels)
+      x = corr_in(raw, corr, j - m);
     }
-    snap[(size_t)cell * ms::kSnap * s + lane] = x;
+    snap[(size_t)cell * ms::kSnap * s + j] = x;
   }
+  if constexpr (G == 64) return;
   const size_t r = ok ? (prow ? (size_t)prow[cell] : (size_t)cell) : 0;
   int na = 0;
   for (int p0 = 0; p0 < P; p0 += 32) {
@@ -1279,12 +1289,20 @@ static int slot_words_for(int P, int s, int sp) {
 // otherwise gather from / scatter to the world state (cell_mols, molmap, positions). `masks` holds
 // 4 flags per part plus a zero block; the caller may all-reduce (MAX) a part's flags across ranks
 // between launches for the reference's global early exit over a domain-decomposed population.
-void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q, uintptr_t Kmr, uintptr_t cell_mols,
+// Would an integration of `s` signals in `nparts` parts take the speculative path (given the cell
+// lists and the speculation buffer)? Every rank of a decomposed world sees the same answer, also a
+// rank without cells (it still joins the all-reduces of the protocol it implies).
+bool integrate_spec_ok(int s, int nparts) {
+  return s <= 128 && (g_integrate_mode & 8) == 0 && nparts >= 1 && nparts <= kMaxParts && (nparts & 1) == 1 &&
+         (g_integrate_mode & 0xF8) == 0;
+}
+
+int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q, uintptr_t Kmr, uintptr_t cell_mols,
                uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
                uintptr_t masks, const std::vector<float>& trims, int n_iters, int part_begin, int part_end,
                bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t map_corr, uintptr_t spec_buf,
-               uintptr_t save_buf, uintptr_t stream) {
-  if (c <= 0) return;
+               uintptr_t save_buf, int dist_stage, uintptr_t stream) {
+  if (c <= 0) return 0;
   const float* corr = map_corr ? P_<float>(map_corr) : nullptr;
   if (n_iters < 0 || n_iters > ms::kEqIters) throw std::invalid_argument("n_iters must be in 0..4");
   const int nparts = (int)trims.size();
@@ -1294,7 +1312,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
   unsigned* zero_flags = mk + ms::kEqIters * nparts;
   float* snaps[2] = {P_<float>(snap_a), P_<float>(snap_b)};
   const bool fast_path = lists != 0 && s <= 128 && (g_integrate_mode & 8) == 0;
-  // Speculative all-parts path (s <= 32, the whole part range with the write-back, mode bits 3-7
+  // Speculative all-parts path (s <= 128, the whole part range with the write-back, mode bits 3-7
   // clear): the reference's global exit (kinetics.py:846) cuts a part short only when no cell of the
   // whole population still has an impactful correction, which never happened in 40-step runs of any
   // BASELINE config (scripts/spec_rate.py: all 3 parts at 4 iterations in every step at 10k-50k
@@ -1307,21 +1325,36 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
   unsigned* spec_w = P_<unsigned>(spec_buf);
   const bool spec_wb = (g_integrate_mode & 256) == 0;  // mode bit 8: final states via snap + write-back
   // (odd part counts: the final state lands in snap_a, and snap_b keeps the input for the fallback)
-  const bool spec_path = fast_path && spec_w != nullptr && s <= 32 && part_begin == 0 && part_end == nparts &&
-                         scatter && nparts >= 1 && nparts <= kMaxParts && (nparts & 1) == 1 &&
-                         (g_integrate_mode & 0xF8) == 0;
+  //
+  // Domain-decomposed callers (the flags all-reduced across ranks) split it into stages:
+  //   dist_stage 1: the speculative launches only (input, register launches, LDS list); returns 1 if
+  //                 they were issued (0: the caller uses the plain per-part protocol instead). The
+  //                 caller then MAX-reduces the 4 * nparts speculative flags + the unfit word
+  //                 (spec_buf[4 ..]) across ranks: "held" is then a global verdict.
+  //   dist_stage 2: the exact fallback launches of parts [part_begin, part_end) (return at once when
+  //                 the global speculation held; the caller all-reduces each part's flags as in the
+  //                 per-part protocol), and with `scatter` the write-back of what is left.
+  const bool spec_ok = fast_path && spec_w != nullptr && integrate_spec_ok(s, nparts);
+  if (dist_stage < 0 || dist_stage > 2) throw std::invalid_argument("integrate: dist_stage must be 0, 1 or 2");
+  if (dist_stage == 1 && !spec_ok) return 0;
+  if (dist_stage == 2 && !spec_ok) throw std::invalid_argument("integrate: dist_stage 2 without the speculative path");
+  const bool spec_path = spec_ok && (dist_stage == 1 || (dist_stage == 0 && part_begin == 0 && part_end == nparts &&
+                                                         scatter));
+  const bool spec_any = spec_path || dist_stage == 2;
   // save_buf: the state the activity changes (cell molecules, raw pixels under the cells) for a
   // speculative activity's rollback (World._speculate) -- written by the speculative path's input
   // kernel, else by a separate pass first
-  if (save_buf && !X_io && part_begin == 0 && !spec_path)
+  if (save_buf && !X_io && part_begin == 0 && !spec_any)
     cell_state_io(c, m, positions, R, C, molmap, map_dtype, cell_mols, save_buf, false, stream);
-  if (spec_path) {
+  if (spec_any) {
     // LDS sizing of the list / fallback launches first: nothing may throw once the input kernel has
     // appended to the wide list (its count is only reset by the write-back at the end)
     const int sp = (s % 2 == 0) ? s + 1 : s;
     const int slot_words = slot_words_for(P, s, sp);
     const size_t slot_bytes = (size_t)slot_words * 4;
-    int cps = kBlock / 32;
+    const int Gs = s <= 32 ? 32 : 64;  // lanes per cell (64: s in 33..128, two signals per lane above 64)
+    const bool two = s > 64;
+    int cps = kBlock / Gs;
     while (cps > 1 && cps * slot_bytes > 64 * 1024) --cps;
     const size_t lds = cps * slot_bytes;
     if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
@@ -1336,10 +1369,17 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     int32_t* wl3 = L + 2 * (size_t)c + 2 + 2 * kSortBuckets;  // what no register launch takes (the
     int32_t* wc3 = L + 2 * (size_t)c + 2;                      // sort order / histogram slots, unused here)
     unsigned* sflags = spec_w + 4;          // speculative flags (4 per part) + the unfit word
-    gather_bin_kernel<<<cdiv(c, kBlock / 32), kBlock, 0, st>>>(
-        c, s, m, R, C, P, X_io ? P_<float>(X_io) : nullptr, P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr,
-        P_<int32_t>(positions), P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr, trims[0], snaps[1], wl, spec_w, mk,
-        nz, zwc, X_io ? nullptr : P_<float>(save_buf));
+    if (spec_path) {
+    if (Gs == 32)
+      gather_bin_kernel<32><<<cdiv(c, kBlock / 32), kBlock, 0, st>>>(
+          c, s, m, R, C, P, X_io ? P_<float>(X_io) : nullptr, P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr,
+          P_<int32_t>(positions), P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr, trims[0], snaps[1], wl, spec_w, mk,
+          nz, zwc, X_io ? nullptr : P_<float>(save_buf), nparts, (g_integrate_mode & 512) != 0);
+    else
+      gather_bin_kernel<64><<<cdiv(c, kBlock / 64), kBlock, 0, st>>>(
+          c, s, m, R, C, P, X_io ? P_<float>(X_io) : nullptr, P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr,
+          P_<int32_t>(positions), P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr, trims[0], snaps[1], wl, spec_w, mk,
+          nz, zwc, X_io ? nullptr : P_<float>(save_buf), nparts, (g_integrate_mode & 512) != 0);
     MS_LAUNCH_CHECK();
     IntegrateArgs a{};
     a.c = c; a.P = P; a.s = s;
@@ -1376,18 +1416,42 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     aw.prelisted = 0;
     aw.ovf_list = wl3;
     aw.ovf_count = wc3;
-    constexpr int kFusedWideBlocks = 64;
-    const size_t lds_fast = (size_t)(kBlock / 32) * fast_slot_words<32, kNzReg>() * 4;
-    integrate_fused_kernel<32, true><<<cdiv(c, kBlock / 32) + kFusedWideBlocks, kBlock, lds_fast, st>>>(
-        a, aw, kFusedWideBlocks);
-    MS_LAUNCH_CHECK();
-    // the narrow blocks' overflow list (rare) on 64-lane slots with 2 * kNzReg non-zeros
-    IntegrateArgs ao = aw;
+    IntegrateArgs ao = aw;  // the overflow list (rare) on 64-lane slots with 2 * kNzReg non-zeros
     ao.list = wl2;
     ao.count = wc2;
-    const size_t lds_fw = (size_t)(kBlock / 64) * fast_slot_words<64, kNzWide>() * 4;
-    integrate_fast_kernel<64, kNzWide, true, true><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
-    MS_LAUNCH_CHECK();
+    if (Gs == 32) {
+      constexpr int kFusedWideBlocks = 64;
+      const size_t lds_fast = (size_t)(kBlock / 32) * fast_slot_words<32, kNzReg>() * 4;
+      integrate_fused_kernel<32, true><<<cdiv(c, kBlock / 32) + kFusedWideBlocks, kBlock, lds_fast, st>>>(
+          a, aw, kFusedWideBlocks);
+      MS_LAUNCH_CHECK();
+      const size_t lds_fw = (size_t)(kBlock / 64) * fast_slot_words<64, kNzWide>() * 4;
+      integrate_fast_kernel<64, kNzWide, true, true><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
+      MS_LAUNCH_CHECK();
+    } else {
+      // 64-lane cells: no wider register level for more than 64 active proteins, so the narrow
+      // launch passes every cell it cannot take (too many proteins, non-zeros or large exponents) to
+      // the overflow list; the 64-lane kNzWide launch passes what it cannot take on to the LDS list
+      IntegrateArgs an = a;
+      an.Ps = 64;
+      an.prelisted = 0;
+      const size_t lds_n = (size_t)(kBlock / 64) *
+                           (two ? fast_slot_words<64, kNzReg, 2>() : fast_slot_words<64, kNzReg>()) * 4;
+      const size_t lds_fw =
+          (size_t)(kBlock / 64) * (two ? fast_slot_words<64, kNzWide, 2>() : fast_slot_words<64, kNzWide>()) * 4;
+      if (two) {
+        integrate_fast_kernel<64, kNzReg, false, true, 2><<<cdiv(c, kBlock / 64), kBlock, lds_n, st>>>(an, nullptr,
+                                                                                                     nullptr);
+        MS_LAUNCH_CHECK();
+        integrate_fast_kernel<64, kNzWide, true, true, 2><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
+      } else {
+        integrate_fast_kernel<64, kNzReg, false, true><<<cdiv(c, kBlock / 64), kBlock, lds_n, st>>>(an, nullptr,
+                                                                                                 nullptr);
+        MS_LAUNCH_CHECK();
+        integrate_fast_kernel<64, kNzWide, true, true><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
+      }
+      MS_LAUNCH_CHECK();
+    }
     // the cells neither register launch took, all parts on the LDS path (rare: usually an empty list)
     {
       IntegrateArgs l = a;
@@ -1395,14 +1459,18 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
       l.count = wc3;
       l.Ps = P;
       l.slot_words = slot_words;
-      integrate_spec_lds_kernel<32><<<std::min<unsigned>(grid, 256), cps * 32, lds, st>>>(l);
+      if (Gs == 32) integrate_spec_lds_kernel<32><<<std::min<unsigned>(grid, 256), cps * 32, lds, st>>>(l);
+      else integrate_spec_lds_kernel<64><<<std::min<unsigned>(grid, 256), cps * 64, lds, st>>>(l);
       MS_LAUNCH_CHECK();
     }
+    }  // spec_path
+    if (dist_stage == 1) return 1;
     // exact fallback: the per-part LDS path over every cell, skipped when the speculation held
-    for (int part = 0; part < nparts; ++part) {
+    const int fb0 = dist_stage == 2 ? part_begin : 0, fb1 = dist_stage == 2 ? part_end : nparts;
+    for (int part = fb0; part < fb1; ++part) {
       IntegrateArgs f{};
       f.c = c; f.P = P; f.s = s;
-      f.W = a.W; f.Q = a.Q; f.Kmr = a.Kmr; f.prow = a.prow;
+      f.W = P_<int32_t>(W); f.Q = P_<float4>(Q); f.Kmr = P_<float>(Kmr); f.prow = prow ? P_<int64_t>(prow) : nullptr;
       f.snap_prev = part == 0 ? snaps[1] : snaps[(part - 1) & 1];
       f.mask_prev = part == 0 ? zero_flags : mk + ms::kEqIters * (part - 1);
       f.n_iters_prev = n_iters;
@@ -1416,7 +1484,8 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
       f.spec_check = sflags;
       f.spec_n = nparts;
       f.copy_to = part == nparts - 1 ? mk : nullptr;
-      integrate_part_kernel<32, true><<<grid, cps * 32, lds, st>>>(f);
+      if (Gs == 32) integrate_part_kernel<32, true><<<grid, cps * 32, lds, st>>>(f);
+      else integrate_part_kernel<64, true><<<grid, cps * 64, lds, st>>>(f);
       MS_LAUNCH_CHECK();
     }
   } else if (part_begin == 0) {
@@ -1458,7 +1527,7 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
   // >= 32; part 0 lists it again) goes to a strided launch with LDS slots for all P proteins
   // (integrate_item). The 64-lane launch replaced the LDS path for the wide list: that path's
   // per-cell dependency chain made its launch ~40 us per part for a few hundred cells.
-  if (spec_path) {
+  if (spec_any) {
     // launched above
   } else if (fast_path) {
     int32_t* wl = P_<int32_t>(lists) + c;
@@ -1640,11 +1709,12 @@ void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t 
     integrate_scatter_kernel<<<(unsigned)std::min<long long>(cdiv((long long)c * s, kBlock), 2048), kBlock, 0, st>>>(
         c, s, m, R, C, snaps[last & 1], mk + ms::kEqIters * last, n_iters, P_<int32_t>(positions),
         P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr, X_io ? P_<float>(X_io) : nullptr,
-        spec_path ? spec_w : nullptr, spec_path && spec_wb ? spec_w + 4 : nullptr, nparts,
-        spec_path ? P_<int32_t>(lists) + 2 * (size_t)c + 2 + 2 * kSortBuckets : nullptr,
-        spec_path ? P_<int32_t>(lists) + 2 * (size_t)c + 2 : nullptr);
+        spec_any ? spec_w : nullptr, spec_any && spec_wb ? spec_w + 4 : nullptr, nparts,
+        spec_any ? P_<int32_t>(lists) + 2 * (size_t)c + 2 + 2 * kSortBuckets : nullptr,
+        spec_any ? P_<int32_t>(lists) + 2 * (size_t)c + 2 : nullptr);
     MS_LAUNCH_CHECK();
   }
+  return spec_path ? 1 : 0;
 }
 
 void pack_params(long long items, int s, uintptr_t N, uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Vmax,

@@ -520,12 +520,17 @@ static MGeom mgeom(int R, int C, int r_lo, int r_hi, int wrap) {
     default: throw std::invalid_argument("unknown molecule map dtype");  \
   }
 
-// stencil variant: 8 columns per lane when C % 8 == 0 (default), 4 when C % 4 == 0 (also selectable
-// with set_stencil_vec(4) for A/Bs), else 1
-static int g_stencil_vec = 8;
+// stencil variant (set_stencil_vec; 0 = auto): 8 columns per lane for 2-byte maps (4096^2 x 14:
+// bf16 0.35 -> 0.27-0.31 ms, fp16 0.35 -> 0.31 ms), 4 for fp32 (0.37 ms; the 8-column variant
+// measured 0.40-0.43: one 16 B access per row and lane is already enough in flight there,
+// profiles/r3/diffuse_bench_4096.jsonl); 1 when C % 4 != 0
+static int g_stencil_vec = 0;
 void set_stencil_vec(int v) { g_stencil_vec = v; }
-static bool use_vec8(int C) { return g_stencil_vec >= 8 && C % 8 == 0; }
-static bool use_vec4(int C) { return g_stencil_vec >= 4 && C % 4 == 0; }
+static bool use_vec8(int C, int dtype) {
+  const int v = g_stencil_vec ? g_stencil_vec : (dtype == kF32 ? 4 : 8);
+  return v >= 8 && C % 8 == 0;
+}
+static bool use_vec4(int C) { return (g_stencil_vec == 0 || g_stencil_vec >= 4) && C % 4 == 0; }
 
 // Blocks of the vector stencil launch (0: one per tile). 256 CUs x 4 workgroups (4 waves per SIMD)
 // still reach the stencil's full HBM rate and leave 3 of the 7 slots a CU holds at its register use
@@ -550,7 +555,7 @@ void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_
   const MGeom g = mgeom(R, C, r_lo, r_hi, wrap);
   hipStream_t st_ = S_(stream);
   const int H = r_hi - r_lo;
-  const bool v8 = use_vec8(C), v4 = !v8 && use_vec4(C);
+  const bool v8 = use_vec8(C, dtype), v4 = !v8 && use_vec4(C);
   const dim3 grid = v8   ? dim3(cdiv(C, 512), cdiv(cdiv(H, kVBand), 4), m)
                     : v4 ? dim3(cdiv(C, 256), cdiv(cdiv(H, kVBand), 4), m)
                          : dim3(cdiv(C, 64 * kWaves), cdiv(H, kBand), m);

@@ -63,11 +63,12 @@ void gather_rows(int n, uintptr_t dn, uintptr_t src_rows, uintptr_t dst_rows,
                  const std::vector<std::tuple<uintptr_t, uintptr_t, long long, long long, long long, uintptr_t>>& descs,
                  uintptr_t stream);
 // kinetics.hip
-void integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q, uintptr_t Kmr, uintptr_t cell_mols,
-               uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
-               uintptr_t masks, const std::vector<float>& trims, int n_iters, int part_begin, int part_end,
-               bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t map_corr, uintptr_t spec_buf,
-               uintptr_t save_buf, uintptr_t stream);
+bool integrate_spec_ok(int s, int nparts);
+int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q, uintptr_t Kmr, uintptr_t cell_mols,
+              uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
+              uintptr_t masks, const std::vector<float>& trims, int n_iters, int part_begin, int part_end,
+              bool scatter, uintptr_t prow, uintptr_t lists, int map_dtype, uintptr_t map_corr, uintptr_t spec_buf,
+              uintptr_t save_buf, int dist_stage, uintptr_t stream);
 void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_t rows, uintptr_t vmax_w, int nw,
                   uintptr_t km_w, int nk, uintptr_t signs, int nsg, uintptr_t hills, int nh, uintptr_t RM,
                   uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
@@ -205,6 +206,7 @@ PYBIND11_MODULE(_hip, m) {
     return std::string(p.gcnArchName);
   });
   m.def("integrate", &msd::integrate);
+  m.def("integrate_spec_ok", &msd::integrate_spec_ok);
   m.def("build_params", &msd::build_params);
   m.def("pack_params", &msd::pack_params);
   m.def("diffuse_stencil", &msd::diffuse_stencil);

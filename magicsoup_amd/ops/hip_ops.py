@@ -226,19 +226,43 @@ def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n
     if spec is None or spec.device != dev:
         spec = sc.bufs["spec"] = torch.zeros(32, dtype=torch.int32, device=dev)
     if flags_hook is None:
-        _m().integrate(*args, 0, nparts, True, slot_p, _p(lists), mdt, _p(corr), _p(spec), _p(save), _stream())
+        _m().integrate(*args, 0, nparts, True, slot_p, _p(lists), mdt, _p(corr), _p(spec), _p(save), 0, _stream())
+    elif _m().integrate(*args, 0, 0, False, slot_p, _p(lists), mdt, _p(corr), _p(spec), _p(save), 1, _stream()):
+        # domain-decomposed world, speculative: every rank integrates all parts in one go, then ONE
+        # MAX all-reduce of the speculative flags + unfit word makes "every part ran all iterations
+        # somewhere in the job" a global verdict; the exact per-part launches (with their per-part
+        # all-reduces) return at once when it held, and redo the reference's global early exit
+        # (kinetics.py:846) exactly otherwise
+        flags_hook(spec[4 : 4 + _EQ * nparts + 1])
+        for part in range(nparts):
+            _m().integrate(*args, part, part + 1, False, slot_p, _p(lists), mdt, _p(corr), _p(spec), 0, 2, _stream())
+            flags_hook(masks[_EQ * part : _EQ * (part + 1)])
+        _m().integrate(*args, nparts, nparts, True, slot_p, _p(lists), mdt, _p(corr), _p(spec), 0, 2, _stream())
     else:
         # domain-decomposed world: all-reduce each part's iteration flags before the next part (or
         # the final write-back) reads them, reproducing the reference's `torch.any` over the whole
         # population
         for part in range(nparts):
             _m().integrate(*args, part, part + 1, False, slot_p, _p(lists), mdt, _p(corr), 0,
-                           _p(save) if part == 0 else 0, _stream())
+                           _p(save) if part == 0 else 0, 0, _stream())
             flags_hook(masks[_EQ * part : _EQ * (part + 1)])
         if nparts:
-            _m().integrate(*args, nparts, nparts, True, slot_p, _p(lists), mdt, _p(corr), 0, 0, _stream())
+            _m().integrate(*args, nparts, nparts, True, slot_p, _p(lists), mdt, _p(corr), 0, 0, 0, _stream())
     sc.bufs["pack_overflow_host"].copy_(_overflow_flag(kin), non_blocking=True)
     return masks
+
+
+def integrate_idle(world, trims=(0.7, 0.2, 0.1)) -> None:
+    """A decomposed world's rank without cells: join the flag all-reduces of the integration
+    protocol the other ranks run (see _launch_integrate) with all-zero flags."""
+    hook = world._allreduce_flags
+    dev = world._tensor_device()
+    nparts = len(trims)
+    s = world.n_molecules * 2
+    if _m().integrate_spec_ok(s, nparts):
+        hook(torch.zeros(_EQ * nparts + 1, dtype=torch.int32, device=dev))
+    for _ in range(nparts):
+        hook(torch.zeros(_EQ, dtype=torch.int32, device=dev))
 
 
 def _flags_to_bits(masks: torch.Tensor, nparts: int) -> list[int]:

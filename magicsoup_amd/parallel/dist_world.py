@@ -376,6 +376,11 @@ class DistributedWorld(World):
         if self.n_cells == 0 and hook is not None:
             from magicsoup_amd.models.kinetics import _INCREMENTS, _TRIMS
 
+            if self._molmap.is_cuda:
+                from magicsoup_amd.ops import hip_ops
+
+                hip_ops.integrate_idle(self, _TRIMS)
+                return
             for _ in _TRIMS:
                 hook(torch.zeros(len(_INCREMENTS), dtype=torch.int32, device=self._tensor_device()))
             return

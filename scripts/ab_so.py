@@ -2,7 +2,11 @@
 built with the in-tree module, then an integrate (3 parts, 4 iterations) on the same explicit X is
 timed alternately with module A and module B, and their results are compared bit for bit.
 
-usage: python scripts/ab_so.py [--size S] [--cells C] A.so B.so [C.so ...]"""
+Each module is timed in every integrate mode of --modes (comma list, default 0); results must be
+bit-identical across modules and modes.
+
+usage: python scripts/ab_so.py [--size S] [--cells C] [--chem wl|synthetic:M:R] [--modes 0,128]
+                               A.so B.so [C.so ...]"""
 import importlib.machinery
 import importlib.util
 import json
@@ -40,17 +44,21 @@ def timed(fn, iters=20):
 
 def main():
     args = sys.argv[1:]
-    size, cells = 4096, 50000
+    size, cells, chem_spec, modes = 4096, 50000, "wl", [0]
     while args and args[0].startswith("--"):
-        flag, val = args[0], int(args[1])
+        flag, val = args[0], args[1]
         args = args[2:]
         if flag == "--size":
-            size = val
+            size = int(val)
+        elif flag == "--cells":
+            cells = int(val)
+        elif flag == "--chem":
+            chem_spec = val
         else:
-            cells = val
+            modes = [int(v) for v in val.split(",")]
     mods = {chr(65 + i): load(p, f"v{i}") for i, p in enumerate(args)}
-    chem = bench._chemistry("wl")
-    atp = chem.molname_2_idx["ATP"]
+    chem = bench._chemistry(chem_spec)
+    atp = chem.molname_2_idx.get("ATP", 0)
     w = ms.World(chemistry=chem, map_size=size, device="cuda", seed=0)
     w.spawn_cells(bench.random_genomes(cells, 500, "cuda"))
     for _ in range(5):
@@ -65,12 +73,16 @@ def main():
         for rep in range(3):
             for tag, mod in mods.items():
                 native._mods["_hip"] = mod
-                Xk = X.clone()
-                out[f"{tag}_r{rep}"] = timed(lambda: kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4))
-                Xk = X.clone()
-                kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4)
-                res[tag] = Xk
-        out["equal"] = {t: bool(torch.equal(res["A"], r)) for t, r in res.items()}
+                for mode in modes:
+                    mod.set_integrate_mode(mode)
+                    Xk = X.clone()
+                    out[f"{tag}_m{mode}_r{rep}"] = timed(lambda: kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4))
+                    Xk = X.clone()
+                    kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4)
+                    res[f"{tag}_m{mode}"] = Xk
+                mod.set_integrate_mode(0)
+        first = next(iter(res.values()))
+        out["equal"] = {t: bool(torch.equal(first, r)) for t, r in res.items()}
     finally:
         native._mods["_hip"] = orig
     print(json.dumps(out))

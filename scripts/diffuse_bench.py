@@ -16,7 +16,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--iters", type=int, default=30)
-    ap.add_argument("--vec", type=int, nargs="*", default=[8], help="stencil variants (columns per lane) to A/B")
+    ap.add_argument("--vec", type=int, nargs="*", default=[0], help="stencil variants (columns per lane, 0 auto) to A/B")
     ap.add_argument("--blocks", type=int, nargs="*", default=[1024], help="stencil grid sizes (0: one block per tile)")
     a = ap.parse_args()
     from magicsoup_amd.ops import native
@@ -26,7 +26,7 @@ def main():
             native.hip().set_stencil_vec(vec)
             native.hip().set_stencil_blocks(blocks)
             run(a, f"vec{vec}_blocks{blocks}")
-    native.hip().set_stencil_vec(8)
+    native.hip().set_stencil_vec(0)
     native.hip().set_stencil_blocks(1024)
 
 

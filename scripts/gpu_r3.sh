@@ -40,6 +40,10 @@ for s in "$@"; do case "$s" in
           python scripts/step_kernels.py $O/tflag/run_kernel_trace.csv 19 > $O/tflag_steps.txt 2>&1; echo "   traced" ;;
   dbench) run diffuse_bench 300 python scripts/diffuse_bench.py --vec 4 8 --blocks 1024 0 2048 ;;
   dtests) run dtests 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "diffusion or reduced_precision or permeation" ;;
+  tc64) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/tc64 -o run --output-format csv -- \
+            python bench.py --chemistry synthetic:64:256 --steps 10 --warmup 5 > $O/tc64.log 2>&1;
+          python scripts/step_kernels.py $O/tc64/run_kernel_trace.csv 9 > $O/tc64_steps.txt 2>&1; echo "   traced" ;;
+  spk1m) MS_MAP_DTYPE=fp16 run spikes_1m 600 python scripts/spike_events.py 16384 1000000 40 5 ;;
   *) echo "unknown step $s"; exit 2 ;;
 esac; done
 exit 0

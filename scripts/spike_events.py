@@ -19,6 +19,7 @@ S = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 50000
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 80
 warm = int(sys.argv[4]) if len(sys.argv) > 4 else 20
+_MDT = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[os.environ.get("MS_MAP_DTYPE", "fp32")]
 events = collections.Counter()
 TARGETS = [
     ("magicsoup_amd.models.kinetics", "Kinetics", "_recycle_rows"),
@@ -58,7 +59,7 @@ def wrap_growth(f, key, size_of):
     return w
 
 
-w = ms.World(chemistry=CHEMISTRY, map_size=S, device="cuda", seed=0)
+w = ms.World(chemistry=CHEMISTRY, map_size=S, device="cuda", seed=0, map_dtype=_MDT)
 w.spawn_cells(bench.random_genomes(N, 500, "cuda"))
 atp = CHEMISTRY.molname_2_idx["ATP"]
 for _ in range(warm):

@@ -132,3 +132,47 @@ def test_gpu_boundary_recombination_is_symmetric(p):
     from tests.test_distributed import _body_boundary_pairs
 
     run_ranks(_body_boundary_pairs, 2, "cuda", p, 0.25 if p > 1e-3 else 0.0, timeout=300)
+
+
+def _body_spec_fallback(rank, ws):
+    """The decomposed speculative integration: one all-reduce of the speculative flags decides for
+    the whole job. Voiding the speculation on rank 0 only (integrate mode bit 9) must make BOTH ranks
+    run the exact per-part launches, and those give the same state bit for bit as the speculation
+    that held."""
+    import magicsoup_amd as ms
+    from magicsoup_amd.ops import hip_ops, native
+    from magicsoup_amd.parallel import DistributedWorld
+    from tests.conftest import gen_genomes
+
+    ms.set_seed(4)
+    torch.manual_seed(4)
+    g = ms.World(chemistry=_chem(), map_size=64, seed=4, device="cpu")
+    g.spawn_cells(gen_genomes(800, 300))
+    dw = DistributedWorld(chemistry=_chem(), map_size=64, seed=5, device="cuda")
+    dw.scatter_from(g)
+    dw.diffuse_molecules()
+    cm0, mm0 = dw.cell_molecules.clone(), dw.molecule_map.clone()
+    spec = hip_ops._scratch(dw.kinetics).bufs
+
+    dw.enzymatic_activity()
+    torch.cuda.synchronize()
+    held = spec["spec"][4:17].tolist()
+    cm1, mm1 = dw.cell_molecules.clone(), dw.molecule_map.clone()
+    assert held[12] == 0 and all(held[:12])  # the speculation held on the whole job
+
+    dw.cell_molecules = cm0.clone()
+    dw.molecule_map = mm0.clone()
+    if rank == 0:
+        native.hip().set_integrate_mode(512)
+    try:
+        dw.enzymatic_activity()
+        torch.cuda.synchronize()
+    finally:
+        native.hip().set_integrate_mode(0)
+    assert spec["spec"][16].item() == 1  # global: void on every rank
+    assert torch.equal(dw.cell_molecules, cm1)
+    assert torch.equal(dw.molecule_map, mm1)
+
+
+def test_gpu_distributed_speculation_is_a_global_decision():
+    run_ranks(_body_spec_fallback, 2, timeout=600)
