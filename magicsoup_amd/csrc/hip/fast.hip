@@ -117,7 +117,7 @@ int fast_divide(const FastWorld& f, int n, uintptr_t mask, uint64_t seed, uint64
 
 void bind_fast(pybind11::module_& m) {
   namespace py = pybind11;
-  py::class_<FastWorld>(m, "FastWorld")
+  py::class_<FastWorld>(m, "FastWorld", py::module_local())
       .def(py::init<>())
       .def_readwrite("R", &FastWorld::R)
       .def_readwrite("C", &FastWorld::C)

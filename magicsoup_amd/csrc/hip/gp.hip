@@ -336,19 +336,19 @@ int gp_rebuild(const GpArena& a, const GpGen& g, const GpKin& k, uintptr_t cells
 }
 
 void bind_gp(py::module_& m) {
-  py::class_<GpArena>(m, "GpArena")
+  py::class_<GpArena>(m, "GpArena", py::module_local())
       .def(py::init<>())
       .def_readwrite("data", &GpArena::data).def_readwrite("lens", &GpArena::lens)
       .def_readwrite("width", &GpArena::width).def_readwrite("n", &GpArena::n)
       .def_readwrite("cnt", &GpArena::cnt).def_readwrite("cnt2", &GpArena::cnt2)
       .def_readwrite("opflags", &GpArena::opflags).def_readwrite("gflags", &GpArena::gflags)
       .def_readwrite("d_rows", &GpArena::d_rows);
-  py::class_<GpGen>(m, "GpGen")
+  py::class_<GpGen>(m, "GpGen", py::module_local())
       .def(py::init<>())
       .def_readwrite("small", &GpGen::small).def_readwrite("dom_type", &GpGen::dom_type)
       .def_readwrite("two_codon", &GpGen::two_codon).def_readwrite("dt_entries", &GpGen::dt_entries)
       .def_readwrite("dom_size", &GpGen::dom_size).def_readwrite("dom_type_size", &GpGen::dom_type_size);
-  py::class_<GpKin>(m, "GpKin")
+  py::class_<GpKin>(m, "GpKin", py::module_local())
       .def(py::init<>())
       .def_readwrite("N", &GpKin::N).def_readwrite("Nf", &GpKin::Nf).def_readwrite("Nb", &GpKin::Nb)
       .def_readwrite("A", &GpKin::A).def_readwrite("Kmr", &GpKin::Kmr).def_readwrite("Kmf", &GpKin::Kmf)

@@ -351,7 +351,8 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
 }
 
 // one block per molecule: totals[mol] = (sum before, sum after) over the owned rows
-__global__ void __launch_bounds__(256) diffuse_reduce_kernel(const double* partials, int tiles, double* totals) {
+__global__ void __launch_bounds__(256) diffuse_reduce_kernel(const double* partials, int tiles, double* totals,
+                                                             bool accumulate) {
   __shared__ double sb[4], sa[4];
   const int mol = blockIdx.x;
   double b = 0.0, a = 0.0;
@@ -367,8 +368,9 @@ __global__ void __launch_bounds__(256) diffuse_reduce_kernel(const double* parti
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    totals[2 * mol] = sb[0] + sb[1] + sb[2] + sb[3];
-    totals[2 * mol + 1] = sa[0] + sa[1] + sa[2] + sa[3];
+    const double b4 = sb[0] + sb[1] + sb[2] + sb[3], a4 = sa[0] + sa[1] + sa[2] + sa[3];
+    totals[2 * mol] = accumulate ? totals[2 * mol] + b4 : b4;
+    totals[2 * mol + 1] = accumulate ? totals[2 * mol + 1] + a4 : a4;
   }
 }
 
@@ -550,8 +552,10 @@ size_t diffuse_partials_len(int m, int C, int H) {
 
 void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
                      uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t totals, int dtype,
-                     uintptr_t stream) {
-  if (m <= 0) return;
+                     int accumulate, uintptr_t stream) {
+  // rows [r_lo, r_hi) of the map; `accumulate`: add this launch's mass totals to `totals` (a strip's
+  // stencil split into interior rows, issued while the halo rows are exchanged, and boundary rows)
+  if (m <= 0 || r_hi <= r_lo) return;
   const MGeom g = mgeom(R, C, r_lo, r_hi, wrap);
   hipStream_t st_ = S_(stream);
   const int H = r_hi - r_lo;
@@ -579,9 +583,50 @@ void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_
                                corr ? P_<float>(corr) : nullptr, g, P_<double>(partials))));
   }
   MS_LAUNCH_CHECK();
-  diffuse_reduce_kernel<<<m, 256, 0, st_>>>(P_<double>(partials), (int)(grid.x * grid.y), P_<double>(totals));
+  diffuse_reduce_kernel<<<m, 256, 0, st_>>>(P_<double>(partials), (int)(grid.x * grid.y), P_<double>(totals),
+                                            accumulate != 0);
   MS_LAUNCH_CHECK();
 }
+
+// The two boundary rows r_lo and r_hi - 1 of a strip (after its halo rows arrived; the interior rows
+// r_lo + 1 .. r_hi - 2 were computed by a diffuse_stencil launch issued before the exchange): one
+// single-row stencil launch each, partials side by side, one reduce adding to `totals`.
+void diffuse_boundary(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t wa,
+                      uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t totals, int dtype,
+                      uintptr_t stream) {
+  if (m <= 0 || r_hi - r_lo < 2) throw std::invalid_argument("diffuse_boundary: a strip of at least 2 rows");
+  hipStream_t st_ = S_(stream);
+  const bool v8 = use_vec8(C, dtype), v4 = !v8 && use_vec4(C);
+  const int gx = v8 ? cdiv(C, 512) : v4 ? cdiv(C, 256) : cdiv(C, 64 * kWaves);
+  const int tiles = gx * m;  // per row (grid.y = 1 for a single row)
+  for (int b = 0; b < 2; ++b) {
+    const int row = b == 0 ? r_lo : r_hi - 1;
+    const MGeom g = mgeom(R, C, row, row + 1, 0);
+    double* part = P_<double>(partials) + (size_t)b * tiles * 2;
+    if (v8) {
+      MS_MAP_DISPATCH(dtype, (diffuse_stencil8_kernel<T><<<tiles, 256, 0, st_>>>(
+                                 P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
+                                 corr ? P_<float>(corr) : nullptr, g, part, gx, 1, tiles)));
+    } else if (v4) {
+      MS_MAP_DISPATCH(dtype, (diffuse_stencil4_kernel<T><<<tiles, 256, 0, st_>>>(
+                                 P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
+                                 corr ? P_<float>(corr) : nullptr, g, part, gx, 1, tiles)));
+    } else {
+      MS_MAP_DISPATCH(dtype, (diffuse_stencil_kernel<T><<<dim3(gx, 1, m), 64 * kWaves, 0, st_>>>(
+                                 P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
+                                 corr ? P_<float>(corr) : nullptr, g, part)));
+    }
+    MS_LAUNCH_CHECK();
+  }
+  // partials of both launches: (mol, tile) pairs, launch b at offset b * tiles; reduce them as one
+  // (2 * gx)-tile layout per molecule requires mol-major order, so reduce each launch and accumulate
+  diffuse_reduce_kernel<<<m, 256, 0, st_>>>(P_<double>(partials), gx, P_<double>(totals), true);
+  MS_LAUNCH_CHECK();
+  diffuse_reduce_kernel<<<m, 256, 0, st_>>>(P_<double>(partials) + (size_t)tiles * 2, gx, P_<double>(totals), true);
+  MS_LAUNCH_CHECK();
+}
+
+size_t diffuse_boundary_partials_len(int m, int C) { return (size_t)4 * cdiv(C, 64) * m; }
 
 void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t totals,
                      double n_pix, int dtype, uintptr_t stream) {

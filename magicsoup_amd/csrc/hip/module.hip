@@ -35,9 +35,13 @@ void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t se
 // maps.hip
 size_t diffuse_partials_len(int m, int C, int H);
 void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
-                     uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t totals, int dtype,
+                     uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t totals, int dtype, int accumulate,
                      uintptr_t stream);
 void diffuse_corr(int m, uintptr_t totals, double n_pix, uintptr_t corr, uintptr_t stream);
+void diffuse_boundary(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t wa,
+                      uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t totals, int dtype,
+                      uintptr_t stream);
+size_t diffuse_boundary_partials_len(int m, int C);
 void apply_pending(int m, long long plane, uintptr_t map, uintptr_t corr, uintptr_t f, int dtype, uintptr_t stream);
 void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t totals,
                      double n_pix, int dtype, uintptr_t stream);
@@ -212,6 +216,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("diffuse_stencil", &msd::diffuse_stencil);
   m.def("diffuse_correct", &msd::diffuse_correct);
   m.def("diffuse_corr", &msd::diffuse_corr);
+  m.def("diffuse_boundary", &msd::diffuse_boundary);
+  m.def("diffuse_boundary_partials_len", &msd::diffuse_boundary_partials_len);
   m.def("apply_pending", &msd::apply_pending);
   m.def("diffuse_partials_len", &msd::diffuse_partials_len);
   m.def("scale_planes", &msd::scale_planes);

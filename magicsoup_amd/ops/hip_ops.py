@@ -398,7 +398,10 @@ def diffuse(world) -> None:
     if d.get("_spec_diff") is not None and _spec_diffuse_adopt(world):
         return
     halo = getattr(world, "_exchange_map_halo", None)
-    if halo is not None:
+    # a strip exchanging over RCCL: the interior rows' stencil runs while the halo rows travel (the
+    # exchange on a stream of its own), the two boundary rows after they arrived
+    split = halo is not None and r_hi - r_lo >= 3 and _HALO_OVERLAP and getattr(world, "_halo_async", False)
+    if halo is not None and not split:
         halo()
     mm = d["_molmap"]
     m = int(mm.size(0))
@@ -412,8 +415,23 @@ def diffuse(world) -> None:
     # neighbours' unscaled boundary rows carry the same pending factor (and the same correction:
     # it is computed from all-reduced totals)
     scale, corr = d.get("_pending_scale"), d.get("_pending_corr")
-    _m().diffuse_stencil(m, R, C, r_lo, r_hi, wrap, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale), _p(corr),
-                         _p(partials), _p(totals), _mdt(mm), _stream())
+    if split:
+        main = torch.cuda.current_stream(dev)
+        hs = d.get("_halo_stream")
+        if hs is None:
+            hs = d["_halo_stream"] = torch.cuda.Stream(device=dev)
+        hs.wait_stream(main)
+        with torch.cuda.stream(hs):
+            halo()
+        _m().diffuse_stencil(m, R, C, r_lo + 1, r_hi - 1, wrap, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale),
+                             _p(corr), _p(partials), _p(totals), _mdt(mm), 0, _stream())
+        main.wait_stream(hs)
+        pb = sc.get("diff_partials_b", int(_m().diffuse_boundary_partials_len(m, C)), torch.float64, dev)
+        _m().diffuse_boundary(m, R, C, r_lo, r_hi, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale), _p(corr), _p(pb),
+                              _p(totals), _mdt(mm), _stream())
+    else:
+        _m().diffuse_stencil(m, R, C, r_lo, r_hi, wrap, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale), _p(corr),
+                             _p(partials), _p(totals), _mdt(mm), 0, _stream())
     reduce = getattr(world, "_allreduce_totals", None)
     if reduce is not None:
         reduce(totals)
@@ -425,6 +443,10 @@ def diffuse(world) -> None:
     sc.bufs["diff_tmp"] = mm.view(-1)
     d["_pending_scale"] = None
     d["_pending_corr"] = new_corr
+
+
+# interior / boundary split of a strip's stencil around the halo exchange (MS_HALO_OVERLAP=0: off)
+_HALO_OVERLAP = os.environ.get("MS_HALO_OVERLAP", "1") != "0"
 
 
 def _diff_weights(world):
@@ -495,7 +517,7 @@ def spec_diffuse_issue(world) -> None:
     n_pix = float(R * C if wrap else (r_hi - r_lo) * C)
     with torch.cuda.stream(side):
         _m().diffuse_stencil(m, R, C, r_lo, r_hi, wrap, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(f), _p(corr),
-                             _p(partials), _p(totals), _mdt(mm), _stream())
+                             _p(partials), _p(totals), _mdt(mm), 0, _stream())
         _m().diffuse_corr(m, _p(totals), n_pix, _p(new_corr), _stream())
         ev = torch.cuda.Event()
         ev.record(side)

@@ -155,6 +155,9 @@ class DistributedWorld(World):
         if self._strips and isinstance(g["_comm"], RcclComm):
             side = make_comm(group, self.rank, n, self.device)
         g["_comm_side"] = side if side is not None else g["_comm"]
+        # RCCL exchanges are stream-ordered device work: the halo exchange can run on a stream of its
+        # own next to the interior stencil (ops/hip_ops.py diffuse); gloo exchanges are host-side
+        g["_halo_async"] = isinstance(g["_comm"], RcclComm)
         g["migrated"] = {"divided_out": 0, "divided_in": 0, "moved_out": 0, "moved_in": 0, "rejected": 0}
         # strip-boundary recombination: a stream per boundary shared by its two ranks, genomes up to
         # `boundary_genome_cap` nt take part (longer ones recombine with cells of their own strip only)

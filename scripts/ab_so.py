@@ -22,6 +22,10 @@ from magicsoup_amd.ops import kinetics_ops, native  # noqa: E402
 
 
 def load(path, tag):
+    # the in-tree module itself: a second load of the same file would re-run its module init on the
+    # same shared object (pybind11 refuses the repeated class registrations)
+    if os.path.realpath(path) == os.path.realpath(native.hip().__file__):
+        return native.hip()
     name = f"ab_{tag}._hip"
     loader = importlib.machinery.ExtensionFileLoader(name, path)
     spec = importlib.util.spec_from_loader(name, loader)

@@ -32,6 +32,10 @@ for s in "$@"; do case "$s" in
   hb) run host_breakdown 300 python scripts/host_breakdown.py 4096 50000 40 ;;
   hbv) MS_VIRTUAL_STRIPS=1 run host_breakdown_proxy8_virtual 300 python scripts/host_breakdown.py 1448 6250 60 ;;
   hbp) run host_breakdown_proxy8 300 python scripts/host_breakdown.py 1448 6250 60 ;;
+  cpv) MS_VIRTUAL_STRIPS=1 run cprofile_proxy8_virtual 300 python scripts/step_cprofile.py 1448 6250 100 ;;
+  cpp) run cprofile_proxy8 300 python scripts/step_cprofile.py 1448 6250 100 ;;
+  wide) run wide_c4096_50k_64x256 300 python bench.py --preset wide ;;
+  m1b) run m1_bench 600 python bench.py --preset m1 --steps 60 --warmup 10 --step-times ;;
   tproxy) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/tproxy -o run --output-format csv -- \
             python bench.py --map-size 1448 --cells 6250 --steps 40 --warmup 20 > $O/tproxy.log 2>&1;
           python scripts/step_kernels.py $O/tproxy/run_kernel_trace.csv 39 > $O/tproxy_steps.txt 2>&1; echo "   traced" ;;

@@ -176,3 +176,35 @@ def _body_spec_fallback(rank, ws):
 
 def test_gpu_distributed_speculation_is_a_global_decision():
     run_ranks(_body_spec_fallback, 2, timeout=600)
+
+
+def _body_halo_overlap(rank, ws):
+    """One rank, strips over RCCL (virtual: the rank is its own neighbour): the stencil split into
+    interior rows (issued while the halo rows are exchanged on a stream of their own) and the two
+    boundary rows gives the single-launch result and the plain world's (up to the order of the fp64
+    mass sums behind the correction)."""
+    import magicsoup_amd as ms
+    from magicsoup_amd.parallel import DistributedWorld
+
+    dw = DistributedWorld(chemistry=_chem(), map_size=256, seed=2, device="cuda", strips=True)
+    assert dw._halo_async
+    mm0 = dw.molecule_map.clone()
+    out = {}
+    for split in (True, False):
+        dw.molecule_map = mm0.clone()
+        dw.__dict__["_halo_async"] = split
+        for _ in range(3):
+            dw.degrade_molecules()
+            dw.diffuse_molecules()
+        out[split] = dw.owned_molecule_map().clone()
+    w = ms.World(chemistry=_chem(), map_size=256, seed=2, device="cuda")
+    w.molecule_map = mm0[:, 1:257].clone()
+    for _ in range(3):
+        w.degrade_molecules()
+        w.diffuse_molecules()
+    torch.testing.assert_close(out[True], out[False], rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(out[True], w.molecule_map, rtol=1e-6, atol=1e-6)
+
+
+def test_gpu_halo_exchange_overlaps_interior_stencil():
+    run_ranks(_body_halo_overlap, 1, timeout=300, backend="nccl")

@@ -282,16 +282,25 @@ def test_mutations_on_gpu_change_genomes():
     assert all(len(g) <= len(b) for g, b in zip(w.cell_genomes, after))
 
 
-def test_integrator_split_parts_match_fused():
-    """The per-part launches a domain-decomposed world uses (flags all-reduced between parts)
-    reproduce the fused single launch exactly."""
+@pytest.mark.parametrize("mode", [0, 128])
+def test_integrator_split_parts_match_fused(mode):
+    """The launches a domain-decomposed world uses (flags all-reduced across ranks) reproduce the
+    fused single launch exactly: the speculative protocol (one all-reduce of the 12 speculative
+    flags + unfit word, then the per-part flags of the exact launches) and, with the speculation
+    off (mode bit 7), the plain per-part protocol."""
+    from magicsoup_amd.ops import native
+
     wa = _world("cuda", n=500)
     wa2 = copy.deepcopy(wa)  # (GPU placement is race-resolved: clone rather than rebuild)
     calls = []
     wa2.__dict__["_allreduce_flags"] = lambda flags: calls.append(int(flags.numel()))
-    wa.enzymatic_activity()
-    wa2.enzymatic_activity()
-    assert calls == [4, 4, 4]
+    native.hip().set_integrate_mode(mode)
+    try:
+        wa.enzymatic_activity()
+        wa2.enzymatic_activity()
+    finally:
+        native.hip().set_integrate_mode(0)
+    assert calls == ([13, 4, 4, 4] if mode == 0 else [4, 4, 4])
     assert torch.equal(wa.cell_molecules, wa2.cell_molecules)
     assert torch.equal(wa.molecule_map, wa2.molecule_map)
 
