@@ -600,4 +600,10 @@ void xb_apply(int C, int E, int slot_w, uint64_t seed_dn, uint64_t seed_up, uint
   MS_LAUNCH_CHECK();
 }
 
+void release_dist_buffers() {
+  if (g_split_tiles) MS_HIP_CHECK(hipFree(g_split_tiles));
+  g_split_tiles = nullptr;
+  g_split_cap = 0;
+}
+
 }  // namespace msd

@@ -1,0 +1,85 @@
+// Pooled HIP events for the host-side ordering of the op layer (stream joins, pending genome-pipeline
+// calls): one native call per record / wait / query instead of torch.cuda.Event + current_stream(),
+// which resolve the device in Python (~10 us per call on the step's critical host path).
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+
+#include <cstdint>
+#include <mutex>
+#include <vector>
+
+#include "hip_common.h"
+
+namespace py = pybind11;
+
+namespace msd {
+namespace {
+std::mutex g_ev_mu;
+std::vector<hipEvent_t> g_ev_free;
+std::vector<hipEvent_t> g_ev_all;
+}  // namespace
+
+uintptr_t ev_acquire() {
+  std::lock_guard<std::mutex> lk(g_ev_mu);
+  if (!g_ev_free.empty()) {
+    hipEvent_t e = g_ev_free.back();
+    g_ev_free.pop_back();
+    return reinterpret_cast<uintptr_t>(e);
+  }
+  hipEvent_t e = nullptr;
+  MS_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  g_ev_all.push_back(e);
+  return reinterpret_cast<uintptr_t>(e);
+}
+
+void ev_release(uintptr_t e) {
+  if (!e) return;
+  std::lock_guard<std::mutex> lk(g_ev_mu);
+  g_ev_free.push_back(reinterpret_cast<hipEvent_t>(e));
+}
+
+void ev_record(uintptr_t e, uintptr_t stream) {
+  MS_HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(e), reinterpret_cast<hipStream_t>(stream)));
+}
+
+// `stream` waits (device-side) for the work recorded in `e`
+void ev_wait(uintptr_t stream, uintptr_t e) {
+  MS_HIP_CHECK(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), reinterpret_cast<hipEvent_t>(e), 0));
+}
+
+bool ev_query(uintptr_t e) {
+  const hipError_t r = hipEventQuery(reinterpret_cast<hipEvent_t>(e));
+  if (r == hipErrorNotReady) return false;
+  MS_HIP_CHECK(r);
+  return true;
+}
+
+void ev_sync(uintptr_t e) { MS_HIP_CHECK(hipEventSynchronize(reinterpret_cast<hipEvent_t>(e))); }
+
+// `dst` waits for everything issued to `src` so far (a fresh pooled event in between)
+void stream_join(uintptr_t dst, uintptr_t src) {
+  if (dst == src) return;
+  const uintptr_t e = ev_acquire();
+  ev_record(e, src);
+  ev_wait(dst, e);
+  ev_release(e);  // (re-recording later is fine: the wait already captured this record)
+}
+
+void release_events() {
+  std::lock_guard<std::mutex> lk(g_ev_mu);
+  for (hipEvent_t e : g_ev_all) MS_HIP_CHECK(hipEventDestroy(e));
+  g_ev_all.clear();
+  g_ev_free.clear();
+}
+
+void bind_events(py::module_& m) {
+  m.def("ev_acquire", &ev_acquire);
+  m.def("ev_release", &ev_release);
+  m.def("ev_record", &ev_record);
+  m.def("ev_wait", &ev_wait);
+  m.def("ev_query", &ev_query);
+  m.def("ev_sync", &ev_sync, py::call_guard<py::gil_scoped_release>());
+  m.def("stream_join", &stream_join);
+}
+
+}  // namespace msd

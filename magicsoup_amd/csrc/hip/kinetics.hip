@@ -38,6 +38,16 @@ constexpr int kMaxParts = 4;  // speculative mode: 4 parts x 4 iterations in one
 // bit 8: the speculative register launches store their final states in the snapshot for the
 // write-back kernel instead of writing the world directly.
 static int g_integrate_mode = 0;
+// side stream + fork / join events of the legacy binned LDS launches (mode bit 0), created on first use
+static hipStream_t g_lds_side = nullptr;
+static hipEvent_t g_lds_fork = nullptr, g_lds_join = nullptr;
+void release_kinetics_streams() {
+  if (g_lds_side) MS_HIP_CHECK(hipStreamDestroy(g_lds_side));
+  if (g_lds_fork) MS_HIP_CHECK(hipEventDestroy(g_lds_fork));
+  if (g_lds_join) MS_HIP_CHECK(hipEventDestroy(g_lds_join));
+  g_lds_side = nullptr;
+  g_lds_fork = g_lds_join = nullptr;
+}
 void set_integrate_mode(int mode) { g_integrate_mode = mode; }
 
 struct IntegrateArgs {
@@ -1650,8 +1660,8 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
     // bin is small but its large proteomes are long per-cell dependency chains, which then overlap
     // with the narrow bin's throughput work instead of adding to it (fork / join per part; the next
     // part reads both bins' flags).
-    static hipStream_t side = nullptr;
-    static hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipStream_t& side = g_lds_side;
+    hipEvent_t &ev_fork = g_lds_fork, &ev_join = g_lds_join;
     const bool conc = nl == 2 && (g_integrate_mode & 1) != 0;
     if (conc && !side) {
       MS_HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));

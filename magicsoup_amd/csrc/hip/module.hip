@@ -68,6 +68,23 @@ void gather_rows(int n, uintptr_t dn, uintptr_t src_rows, uintptr_t dst_rows,
                  uintptr_t stream);
 // kinetics.hip
 bool integrate_spec_ok(int s, int nparts);
+void release_select_buffers();
+void release_dist_buffers();
+void release_world_buffers();
+void release_kinetics_streams();
+void release_events();
+void bind_events(py::module_& m);
+// Exit path (registered with Python's atexit by ops/native.py): drain the device and free the
+// process-wide pinned / device buffers and streams of the extension while the HIP runtime (and a
+// profiler's interception layer, which finalises in the C exit handlers after Python's) is intact.
+void release_static() {
+  MS_HIP_CHECK(hipDeviceSynchronize());
+  release_select_buffers();
+  release_dist_buffers();
+  release_world_buffers();
+  release_kinetics_streams();
+  release_events();
+}
 int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q, uintptr_t Kmr, uintptr_t cell_mols,
               uintptr_t molmap, uintptr_t positions, uintptr_t X_io, uintptr_t snap_a, uintptr_t snap_b,
               uintptr_t masks, const std::vector<float>& trims, int n_iters, int part_begin, int part_end,
@@ -211,6 +228,8 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("integrate", &msd::integrate);
   m.def("integrate_spec_ok", &msd::integrate_spec_ok);
+  m.def("release_static", &msd::release_static);
+  msd::bind_events(m);
   m.def("build_params", &msd::build_params);
   m.def("pack_params", &msd::pack_params);
   m.def("diffuse_stencil", &msd::diffuse_stencil);

@@ -506,4 +506,17 @@ void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, ui
 #undef MS_SEL
 }
 
+// Free the process-wide pinned / device buffers of this file (exit path, see release_static).
+void release_select_buffers() {
+  if (g_host) MS_HIP_CHECK(hipHostFree(g_host));
+  g_host = g_host_dev = nullptr;
+  if (g_tacc) MS_HIP_CHECK(hipFree(g_tacc));
+  g_tacc = nullptr;
+  if (g_status) MS_HIP_CHECK(hipHostFree(g_status));
+  g_status = g_status_dev = nullptr;
+  for (auto& kv : g_tiles)
+    if (kv.second.p) MS_HIP_CHECK(hipFree(kv.second.p));
+  g_tiles.clear();
+}
+
 }  // namespace msd

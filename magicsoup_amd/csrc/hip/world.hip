@@ -166,7 +166,7 @@ __global__ void __launch_bounds__(256) place_bid_kernel(int k, const int64_t* ce
                                                         uint64_t call, long long* cand, int* claim) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= k || !pending[i]) return;
-  const int c = (int)cells[i];
+  const int c = cells ? (int)cells[i] : i;
   long long nb[8], fr[8];
   const int cnt = moore(pos[2 * c], pos[2 * c + 1], g, nb);
   int nf = 0;
@@ -197,9 +197,18 @@ __global__ void __launch_bounds__(256) place_resolve_kernel(int k, const int64_t
   // a move into a halo row is committed only after the owning rank accepts it: keep the pixel
   const int x = (int)(px / g.C);
   if (vacate && (g.wrap || (x >= g.r_lo && x < g.r_hi))) {
-    const int c = (int)cells[i];
+    const int c = cells ? (int)cells[i] : i;
     cell_map[(size_t)pos[2 * c] * g.C + pos[2 * c + 1]] = 0;
   }
+}
+
+// rounds path over a participation mask (cells 0..k-1): pending from the mask, no result yet
+__global__ void __launch_bounds__(256) place_init_mask_kernel(int k, const uint8_t* mask, uint8_t* pending,
+                                                              long long* result) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k) return;
+  pending[i] = mask[i] != 0;
+  result[i] = -1;
 }
 
 // Winners of the placement rounds (wins = ascending list positions with result >= 0): the cell and
@@ -593,14 +602,53 @@ static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, co
   return true;
 }
 
+static void place_rounds_launches(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, const Geom& g, bool vacate,
+                                  uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim,
+                                  uintptr_t result, int rounds, uint64_t seed, uint64_t call, hipStream_t s);
+
 // Placement with a participation mask instead of a cell list (cells 0..n-1, priority = index).
 void place_rounds_mask(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, bool vacate,
                        uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result,
                        int rounds, uint64_t seed, uint64_t call, uintptr_t stream) {
   if (n <= 0) return;
   const Geom g = geom(R, C, r_lo, r_hi, wrap);
-  if (!place_coop(n, 0, mask, pos, g, vacate, cell_map, pending, cand, claim, result, rounds, seed, call, S_(stream)))
-    throw std::runtime_error("place_rounds_mask: cooperative launch refused");
+  if (g_place_mode == 0 &&
+      place_coop(n, 0, mask, pos, g, vacate, cell_map, pending, cand, claim, result, rounds, seed, call, S_(stream)))
+    return;
+  place_rounds_launches(n, 0, mask, pos, g, vacate, cell_map, pending, cand, claim, result, rounds, seed, call,
+                        S_(stream));
+}
+
+// The multi-launch rounds (bid / resolve per round; the same draws and winners as the cooperative
+// single launch). With a mask: cells 0..k-1 that take part.
+static void place_rounds_launches(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, const Geom& g, bool vacate,
+                                  uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim,
+                                  uintptr_t result, int rounds, uint64_t seed, uint64_t call, hipStream_t s) {
+  if (mask) {
+    place_init_mask_kernel<<<cdiv(k, 256), 256, 0, s>>>(k, P_<uint8_t>(mask), P_<uint8_t>(pending), P_<long long>(result));
+    MS_LAUNCH_CHECK();
+  } else {
+    MS_HIP_CHECK(hipMemsetAsync(P_<uint8_t>(pending), 1, (size_t)k, s));
+    MS_HIP_CHECK(hipMemsetAsync(P_<long long>(result), 0xFF, (size_t)k * sizeof(long long), s));
+  }
+  const int64_t* cp = cells ? P_<int64_t>(cells) : nullptr;
+  if (k <= kPlaceWgMax && cells) {
+    place_rounds_wg_kernel<<<1, 1024, 0, s>>>(k, cp, P_<int32_t>(pos), g, vacate, P_<uint8_t>(cell_map),
+                                              P_<uint8_t>(pending), seed, call, P_<long long>(cand), P_<int>(claim),
+                                              P_<long long>(result), rounds);
+    MS_LAUNCH_CHECK();
+    return;
+  }
+  const unsigned grid = cdiv(k, 256);
+  for (int r = 0; r < rounds; ++r) {
+    place_bid_kernel<<<grid, 256, 0, s>>>(k, cp, P_<int32_t>(pos), g, P_<uint8_t>(cell_map), P_<uint8_t>(pending),
+                                          seed, call + ((uint64_t)r << 48), P_<long long>(cand), P_<int>(claim));
+    MS_LAUNCH_CHECK();
+    place_resolve_kernel<<<grid, 256, 0, s>>>(k, cp, P_<int32_t>(pos), g, vacate, P_<uint8_t>(cell_map),
+                                              P_<uint8_t>(pending), P_<long long>(cand), P_<int>(claim),
+                                              P_<long long>(result));
+    MS_LAUNCH_CHECK();
+  }
 }
 
 void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, bool vacate,
@@ -611,27 +659,8 @@ void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo,
   if (g_place_mode == 0 &&
       place_coop(k, cells, 0, pos, g, vacate, cell_map, pending, cand, claim, result, rounds, seed, call, S_(stream)))
     return;
-  MS_HIP_CHECK(hipMemsetAsync(P_<uint8_t>(pending), 1, (size_t)k, S_(stream)));
-  MS_HIP_CHECK(hipMemsetAsync(P_<long long>(result), 0xFF, (size_t)k * sizeof(long long), S_(stream)));
-  if (k <= kPlaceWgMax) {
-    place_rounds_wg_kernel<<<1, 1024, 0, S_(stream)>>>(k, P_<int64_t>(cells), P_<int32_t>(pos), g, vacate,
-                                                       P_<uint8_t>(cell_map), P_<uint8_t>(pending), seed, call,
-                                                       P_<long long>(cand), P_<int>(claim), P_<long long>(result),
-                                                       rounds);
-    MS_LAUNCH_CHECK();
-    return;
-  }
-  const unsigned grid = cdiv(k, 256);
-  for (int r = 0; r < rounds; ++r) {
-    place_bid_kernel<<<grid, 256, 0, S_(stream)>>>(k, P_<int64_t>(cells), P_<int32_t>(pos), g, P_<uint8_t>(cell_map),
-                                                   P_<uint8_t>(pending), seed, call + ((uint64_t)r << 48), P_<long long>(cand),
-                                                   P_<int>(claim));
-    MS_LAUNCH_CHECK();
-    place_resolve_kernel<<<grid, 256, 0, S_(stream)>>>(k, P_<int64_t>(cells), P_<int32_t>(pos), g, vacate,
-                                                       P_<uint8_t>(cell_map), P_<uint8_t>(pending),
-                                                       P_<long long>(cand), P_<int>(claim), P_<long long>(result));
-    MS_LAUNCH_CHECK();
-  }
+  place_rounds_launches(k, cells, 0, pos, g, vacate, cell_map, pending, cand, claim, result, rounds, seed, call,
+                        S_(stream));
 }
 
 int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
@@ -647,8 +676,9 @@ int divide_mask_dev(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo
   if (n <= 0) throw std::invalid_argument("divide_mask_dev: no cells");
   const Geom g = geom(R, C, r_lo, r_hi, wrap);
   hipStream_t s = S_(stream);
-  if (!place_coop(n, 0, mask, pos, g, false, cell_map, pending, cand, claim, result, rounds, seed, call, s))
-    throw std::runtime_error("divide_mask_dev: cooperative launch refused");
+  if (g_place_mode != 0 ||
+      !place_coop(n, 0, mask, pos, g, false, cell_map, pending, cand, claim, result, rounds, seed, call, s))
+    place_rounds_launches(n, 0, mask, pos, g, false, cell_map, pending, cand, claim, result, rounds, seed, call, s);
   const int slot = select_indices_async(n, 3 /* int64 >= 0 */, result, wins, 0, dcount, stream);
   const unsigned grid = std::min<unsigned>(cdiv((long long)n * m, 256), 512u);
   divide_commit_kernel<<<grid, 256, 0, s>>>(P_<int>(dcount), P_<int64_t>(wins), P_<long long>(result), C, n0, m,
@@ -715,6 +745,21 @@ void neighbor_pairs(int nf, int n, uintptr_t from, uintptr_t pos, int R, int C, 
                                                                P_<uint8_t>(in_to), P_<int>(counter), cap,
                                                                P_<int64_t>(pairs));
   MS_LAUNCH_CHECK();
+}
+
+void release_world_buffers() {
+  int cur = 0;
+  MS_HIP_CHECK(hipGetDevice(&cur));
+  for (int d = 0; d < kMaxDevices; ++d) {
+    if (!g_place_ctl[d]) continue;
+    MS_HIP_CHECK(hipSetDevice(d));
+    MS_HIP_CHECK(hipFree(g_place_ctl[d]));
+    g_place_ctl[d] = nullptr;
+  }
+  MS_HIP_CHECK(hipSetDevice(cur));
+  if (g_place_err) MS_HIP_CHECK(hipHostFree(g_place_err));
+  g_place_err = nullptr;
+  g_place_err_dev = nullptr;
 }
 
 }  // namespace msd

@@ -317,9 +317,9 @@ class World:
         d = self.__dict__
         q = d.setdefault("_deferred", [])
         if not q:
-            ev = torch.cuda.Event()
-            ev.record()
-            d["_defer_event"] = ev
+            from magicsoup_amd.ops.streams import NEvent
+
+            d["_defer_event"] = NEvent().record()
         q.append(fn)
         if (d.get("_spec_diff") is not None and _FLUSH_EARLY) or self._lazy_join():
             # nothing to wait for: the chains start now on the side stream (the next activity
@@ -334,12 +334,15 @@ class World:
         """The compute stream waits (device-side) for the genome chains issued so far."""
         ev = self.__dict__.pop("_side_join", None)
         if ev is not None:
-            torch.cuda.current_stream(self._genomes.data.device).wait_event(ev)
+            ev.wait()  # (the current stream)
 
     def _flush_deferred(self) -> None:
         """Issue the queued genome ops, in call order, on a side stream: their chains run next to
         the diffusion stencil still executing on the compute stream (disjoint state), and the compute
         stream waits for them (device-side) before anything that follows."""
+        from magicsoup_amd.ops.hip_ops import _stream
+        from magicsoup_amd.ops.streams import NEvent, join, on_stream
+
         d = self.__dict__
         q = d.get("_deferred")
         if not q:
@@ -350,24 +353,23 @@ class World:
             # high priority: the short chain kernels are dispatched ahead of the stencil's waiting
             # workgroups (the next op's reconcile waits for the chains)
             side = d["_side_stream"] = torch.cuda.Stream(device=self._genomes.data.device, priority=-1)
-        main = torch.cuda.current_stream(side.device)
+        main = _stream()
+        side_raw = side.cuda_stream
         # the chains depend on the state as of the first queued call (recorded then), not on the
         # molecule-only work issued since (e.g. the diffusion stencil they run next to)
-        side.wait_event(d.pop("_defer_event"))
+        d.pop("_defer_event").wait(side_raw)
         d["_side_active"] = True  # (a decomposed world's exchanges use its side-stream communicator)
         try:
-            with torch.cuda.stream(side):
+            with on_stream(side):
                 for fn in q:
                     fn()
         finally:
             d["_side_active"] = False
             if self._lazy_join():
                 # joined at the next op that needs the chains' results (see _EAGER_CHAINS)
-                ev = torch.cuda.Event()
-                ev.record(side)
-                d["_side_join"] = ev
+                d["_side_join"] = NEvent().record(side_raw)
             else:
-                main.wait_stream(side)
+                join(main, side_raw)
 
     def _reconcile(self) -> None:
         if self.__dict__.get("_deferred"):
@@ -1185,7 +1187,7 @@ class World:
         state["_pending_corr"] = None
         for k in ("_hip_scratch", "_idx_map", "_diff_w", "_perm_t", "_degrade_t", "_gp_state", "_deferred",
                   "_side_stream", "_defer_event", "_gp_cache", "_spec", "_spec_diff", "_spec_diff_miss",
-                  "_diff_stream", "_side_join", "_gw_watch", "_gw_pinned", "_fw", "_fw_key", "_fw_bufs"):
+                  "_diff_stream", "_halo_stream", "_side_join", "_gw_watch", "_gw_pinned", "_fw", "_fw_key", "_fw_bufs"):
             state.pop(k, None)
         return state
 

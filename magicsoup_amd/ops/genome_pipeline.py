@@ -33,6 +33,7 @@ import torch
 
 from magicsoup_amd.ops import hip_ops
 from magicsoup_amd.ops.hip_ops import _m, _p, _rng, _scratch, _stream
+from magicsoup_amd.ops.streams import NEvent
 
 K_CAP = 32  # event-count cap per genome (P(Poisson(lam <= 1) > 32) < 1e-35)
 D_CAP = 12  # domain slots per protein in the speculative token layout
@@ -49,8 +50,11 @@ _F_TRANSLATE, _F_CAPACITY, _F_ROWS, _F_WIDTH, _F_SKIPPED = 1, 2, 4, 8, 16
 _SEL_I32POS, _SEL_SET = 2, 0
 
 
+_SYNC_ENV = os.environ.get("MS_SYNC_GENETICS") == "1"
+
+
 def enabled(world) -> bool:
-    if os.environ.get("MS_SYNC_GENETICS") == "1":
+    if _SYNC_ENV:
         return False
     return bool(world.__dict__["_molmap"].is_cuda)  # GPU worlds (single map or strip of a decomposed one)
 
@@ -233,8 +237,7 @@ class _Replay:
 
 def _record(world, kind: str, args: tuple, rng: tuple, cells, slot: int, replay: dict) -> None:
     """Record an issued pipeline call as pending (its status lands in pinned slot ``slot``)."""
-    ev = torch.cuda.Event()
-    ev.record()
+    ev = NEvent().record()
     _state(world)["pending"].append(_Pending(kind, args, rng, cells, _StatusSlot(slot), ev, replay))
     world._genomes.version += 1
 

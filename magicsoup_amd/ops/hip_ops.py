@@ -58,9 +58,17 @@ class Scratch:
 
     def __init__(self):
         self.bufs: dict[str, torch.Tensor] = {}
+        self._views: dict[str, tuple] = {}  # name -> (buffer, numel, dtype, view): the last view handed out
 
     def get(self, name: str, numel: int, dtype, device, zero: bool = False) -> torch.Tensor:
         t = self.bufs.get(name)
+        c = self._views.get(name)
+        if c is not None and c[0] is t and c[1] == numel and c[2] is dtype:
+            # (the same buffer, size and dtype as last time: a buffer's device never changes)
+            v = c[3]
+            if zero:
+                v.zero_()
+            return v
         if t is None or t.numel() < numel or t.dtype != dtype or t.device != device:
             # a buffer that grows takes 1.5x: populations creep up step by step, and every new size
             # is a fresh allocation (the caching allocator has no block of it yet)
@@ -68,6 +76,7 @@ class Scratch:
             t = torch.empty(max(numel, 1, int(1.5 * t.numel()) if grow else 0), dtype=dtype, device=device)
             self.bufs[name] = t
         v = t[:numel]
+        self._views[name] = (t, numel, dtype, v)
         if zero:
             v.zero_()
         return v
@@ -416,16 +425,19 @@ def diffuse(world) -> None:
     # it is computed from all-reduced totals)
     scale, corr = d.get("_pending_scale"), d.get("_pending_corr")
     if split:
-        main = torch.cuda.current_stream(dev)
+        from magicsoup_amd.ops.streams import join, on_stream
+
+        main = _stream()
         hs = d.get("_halo_stream")
         if hs is None:
             hs = d["_halo_stream"] = torch.cuda.Stream(device=dev)
-        hs.wait_stream(main)
-        with torch.cuda.stream(hs):
+        hs_raw = hs.cuda_stream
+        join(hs_raw, main)
+        with on_stream(hs):
             halo()
         _m().diffuse_stencil(m, R, C, r_lo + 1, r_hi - 1, wrap, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale),
-                             _p(corr), _p(partials), _p(totals), _mdt(mm), 0, _stream())
-        main.wait_stream(hs)
+                             _p(corr), _p(partials), _p(totals), _mdt(mm), 0, main)
+        join(main, hs_raw)
         pb = sc.get("diff_partials_b", int(_m().diffuse_boundary_partials_len(m, C)), torch.float64, dev)
         _m().diffuse_boundary(m, R, C, r_lo, r_hi, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale), _p(corr), _p(pb),
                               _p(totals), _mdt(mm), _stream())

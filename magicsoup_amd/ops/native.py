@@ -7,6 +7,7 @@ eager-PyTorch implementation.
 """
 from __future__ import annotations
 
+import atexit
 import importlib
 import os
 import threading
@@ -30,6 +31,21 @@ def _load(name: str, builder) -> object:
         return mod
 
 
+def _profiled() -> bool:
+    """Running under rocprofv3 (its launcher exports the tool's ROCPROF_* settings)."""
+    return any(k.startswith("ROCPROF") for k in os.environ)
+
+
+def _release_static(mod) -> None:
+    """Free the extension's process-wide HIP buffers before the C exit handlers run (a profiler's
+    interception layer finalises there; the HIP runtime's own teardown of leftover allocations
+    after that point ended profiled runs in SIGSEGV)."""
+    try:
+        mod.release_static()
+    except Exception:  # noqa: BLE001 - exit path: a dead device must not turn into a traceback
+        pass
+
+
 def host():
     """The OpenMP host module ``magicsoup_amd._host`` (built on demand)."""
     from magicsoup_amd.ops import build
@@ -49,9 +65,16 @@ def hip():
             "magicsoup_amd: the gfx950 HIP extension (_hip) could not be loaded; GPU execution"
             " requires it (no fallback). Build it with `python -m magicsoup_amd.ops.build`."
         ) from err
+    if fresh and os.environ.get("MS_RELEASE_AT_EXIT", "1") == "1":
+        atexit.register(_release_static, mod)
     if fresh and os.environ.get("MS_INTEGRATE_MODE"):
         # integrator launch-mode bits for whole-run A/B (kinetics.hip, set_integrate_mode)
         mod.set_integrate_mode(int(os.environ["MS_INTEGRATE_MODE"]))  # type: ignore[attr-defined]
+    if fresh and not os.environ.get("MS_PLACE_MODE") and _profiled():
+        # under rocprofv3 a process that made cooperative launches dies in SIGSEGV at exit (the HIP
+        # runtime's teardown calls into the already finalised profiler layer; docs/performance.md):
+        # the per-round placement launches place identically
+        mod.set_place_mode(1)  # type: ignore[attr-defined]
     if fresh and os.environ.get("MS_PLACE_MODE"):
         # 1: per-round placement launches instead of the cooperative single launch (world.hip)
         mod.set_place_mode(int(os.environ["MS_PLACE_MODE"]))  # type: ignore[attr-defined]

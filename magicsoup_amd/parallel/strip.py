@@ -20,9 +20,9 @@ HDR = 4  # header words: record count, label row width, genome row width, molecu
 
 
 def _hip():
-    from magicsoup_amd.ops import native
+    from magicsoup_amd.ops.hip_ops import _m
 
-    return native.hip()
+    return _m()
 
 
 def _stream() -> int:

@@ -16,6 +16,16 @@ run() {  # run <name> <seconds> <cmd...>
   if fatal $rc; then echo "fatal rc=$rc in $name"; tail -30 "$O/$name.log"; exit $rc; fi
   return 0
 }
+trace() {  # trace <name> <steps-to-summarise> <bench args...>: kernel trace + --stats of a bench run
+  local name="$1" k="$2"; shift 2
+  echo "== trace $name $(date +%T)"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$name -o run --output-format csv -- python bench.py "$@" \
+    > $O/$name.log 2>&1
+  local rc=$?
+  echo "   rc=$rc $(grep -h '^{"metric"' "$O/$name.log" | cut -c100-200)"
+  if fatal $rc; then echo "fatal rc=$rc in $name"; tail -30 "$O/$name.log"; exit $rc; fi
+  python scripts/step_kernels.py $O/$name/run_kernel_trace.csv $k > $O/${name}_steps.txt 2>&1
+}
 for s in "$@"; do case "$s" in
   tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
   smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -32,21 +42,24 @@ for s in "$@"; do case "$s" in
   hb) run host_breakdown 300 python scripts/host_breakdown.py 4096 50000 40 ;;
   hbv) MS_VIRTUAL_STRIPS=1 run host_breakdown_proxy8_virtual 300 python scripts/host_breakdown.py 1448 6250 60 ;;
   hbp) run host_breakdown_proxy8 300 python scripts/host_breakdown.py 1448 6250 60 ;;
+  hsv) MS_VIRTUAL_STRIPS=1 run host_split_proxy8_virtual 300 python scripts/host_split.py 1448 6250 60 ;;
+  hsp) run host_split_proxy8 300 python scripts/host_split.py 1448 6250 60 ;;
+  hsn) MS_NATIVE_TIMES=1 MS_VIRTUAL_STRIPS=1 run host_native_proxy8_virtual 300 python scripts/host_split.py 1448 6250 60 ;;
+  hsnp) MS_NATIVE_TIMES=1 run host_native_proxy8 300 python scripts/host_split.py 1448 6250 60 ;;
+  hsf) run host_split_flagship 300 python scripts/host_split.py 4096 50000 40 ;;
   cpv) MS_VIRTUAL_STRIPS=1 run cprofile_proxy8_virtual 300 python scripts/step_cprofile.py 1448 6250 100 ;;
+  cpvc) MS_PROF_LINES=90 MS_VIRTUAL_STRIPS=1 run cprofile_proxy8_virtual_cum 300 python scripts/step_cprofile.py 1448 6250 100 cumulative ;;
+  cpvn) MS_PROF_LINES=60 MS_VIRTUAL_STRIPS=1 run cprofile_proxy8_virtual_ncalls 300 python scripts/step_cprofile.py 1448 6250 100 ncalls ;;
   cpp) run cprofile_proxy8 300 python scripts/step_cprofile.py 1448 6250 100 ;;
   wide) run wide_c4096_50k_64x256 300 python bench.py --preset wide ;;
   m1b) run m1_bench 600 python bench.py --preset m1 --steps 60 --warmup 10 --step-times ;;
-  tproxy) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/tproxy -o run --output-format csv -- \
-            python bench.py --map-size 1448 --cells 6250 --steps 40 --warmup 20 > $O/tproxy.log 2>&1;
-          python scripts/step_kernels.py $O/tproxy/run_kernel_trace.csv 39 > $O/tproxy_steps.txt 2>&1; echo "   traced" ;;
-  tflag) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/tflag -o run --output-format csv -- \
-            python bench.py --steps 20 --warmup 20 > $O/tflag.log 2>&1;
-          python scripts/step_kernels.py $O/tflag/run_kernel_trace.csv 19 > $O/tflag_steps.txt 2>&1; echo "   traced" ;;
+  tproxy) trace tproxy 39 --map-size 1448 --cells 6250 --steps 40 --warmup 20 ;;
+  tvirt) MS_VIRTUAL_STRIPS=1 trace tvirt 39 --map-size 1448 --cells 6250 --steps 40 --warmup 20 ;;
+  tflag) trace tflag 19 --steps 20 --warmup 20 ;;
+  tenv) timeout -k 10 120 rocprofv3 --kernel-trace -d $O/tenv -o run --output-format csv -- python -c "import os; print(sorted(k for k in os.environ if 'ROC' in k))" > $O/tenv.log 2>&1; echo "   rc=$?" ;;
   dbench) run diffuse_bench 300 python scripts/diffuse_bench.py --vec 4 8 --blocks 1024 0 2048 ;;
   dtests) run dtests 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "diffusion or reduced_precision or permeation" ;;
-  tc64) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/tc64 -o run --output-format csv -- \
-            python bench.py --chemistry synthetic:64:256 --steps 10 --warmup 5 > $O/tc64.log 2>&1;
-          python scripts/step_kernels.py $O/tc64/run_kernel_trace.csv 9 > $O/tc64_steps.txt 2>&1; echo "   traced" ;;
+  tc64) trace tc64 9 --preset wide --steps 10 --warmup 5 ;;
   spk1m) MS_MAP_DTYPE=fp16 run spikes_1m 600 python scripts/spike_events.py 16384 1000000 40 5 ;;
   *) echo "unknown step $s"; exit 2 ;;
 esac; done

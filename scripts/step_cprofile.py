@@ -48,6 +48,6 @@ pr.disable()
 dt = time.perf_counter() - t0
 print(f"{S}^2 / {N} {'virtual' if virtual else 'plain'}: {dt / steps * 1e6:.0f} us per step under cProfile")
 st = pstats.Stats(pr)
-st.sort_stats(sort).print_stats(45)
+st.sort_stats(sort).print_stats(int(os.environ.get("MS_PROF_LINES", "45")))
 if virtual:
     w.close()
