@@ -1727,6 +1727,34 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
   return spec_path ? 1 : 0;
 }
 
+void rccl_allreduce(uintptr_t comm, uintptr_t buf, long long count, int dtype, int op, uintptr_t stream);  // comm.hip
+
+// The decomposed world's speculative protocol (integrate(), dist_stage 1 / 2) in one call, its flag
+// all-reduces (int32 MAX) issued here on the native RCCL communicator `comm`: the speculative launch,
+// one all-reduce of its 4 * nparts flags + unfit word, the exact per-part launches (return at once
+// when the speculation held globally) each followed by its part's all-reduce, and the write-back.
+// Returns 0 without issuing anything when the speculative path does not apply (the caller runs the
+// per-part protocol instead; every rank decides alike, see integrate_spec_ok).
+int integrate_dist(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q, uintptr_t Kmr,
+                   uintptr_t cell_mols, uintptr_t molmap, uintptr_t positions, uintptr_t snap_a, uintptr_t snap_b,
+                   uintptr_t masks, const std::vector<float>& trims, int n_iters, uintptr_t prow, uintptr_t lists,
+                   int map_dtype, uintptr_t map_corr, uintptr_t spec_buf, uintptr_t save_buf, uintptr_t comm,
+                   uintptr_t stream) {
+  const int nparts = (int)trims.size();
+  if (!integrate(c, P, s, m, R, C, W, Q, Kmr, cell_mols, molmap, positions, 0, snap_a, snap_b, masks, trims, n_iters,
+                 0, 0, false, prow, lists, map_dtype, map_corr, spec_buf, save_buf, 1, stream))
+    return 0;
+  rccl_allreduce(comm, spec_buf + 4 * sizeof(unsigned), ms::kEqIters * nparts + 1, 0, 1, stream);
+  for (int part = 0; part < nparts; ++part) {
+    integrate(c, P, s, m, R, C, W, Q, Kmr, cell_mols, molmap, positions, 0, snap_a, snap_b, masks, trims, n_iters,
+              part, part + 1, false, prow, lists, map_dtype, map_corr, spec_buf, 0, 2, stream);
+    rccl_allreduce(comm, masks + (size_t)ms::kEqIters * part * sizeof(unsigned), ms::kEqIters, 0, 1, stream);
+  }
+  integrate(c, P, s, m, R, C, W, Q, Kmr, cell_mols, molmap, positions, 0, snap_a, snap_b, masks, trims, n_iters,
+            nparts, nparts, true, prow, lists, map_dtype, map_corr, spec_buf, 0, 2, stream);
+  return 1;
+}
+
 void pack_params(long long items, int s, uintptr_t N, uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Vmax,
                  uintptr_t Kmf, uintptr_t Kmb, uintptr_t Ke, uintptr_t W, uintptr_t Q, uintptr_t overflow,
                  uintptr_t stream) {

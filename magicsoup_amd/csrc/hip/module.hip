@@ -68,6 +68,11 @@ void gather_rows(int n, uintptr_t dn, uintptr_t src_rows, uintptr_t dst_rows,
                  uintptr_t stream);
 // kinetics.hip
 bool integrate_spec_ok(int s, int nparts);
+int integrate_dist(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q, uintptr_t Kmr,
+                   uintptr_t cell_mols, uintptr_t molmap, uintptr_t positions, uintptr_t snap_a, uintptr_t snap_b,
+                   uintptr_t masks, const std::vector<float>& trims, int n_iters, uintptr_t prow, uintptr_t lists,
+                   int map_dtype, uintptr_t map_corr, uintptr_t spec_buf, uintptr_t save_buf, uintptr_t comm,
+                   uintptr_t stream);
 void release_select_buffers();
 void release_dist_buffers();
 void release_world_buffers();
@@ -228,6 +233,7 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("integrate", &msd::integrate);
   m.def("integrate_spec_ok", &msd::integrate_spec_ok);
+  m.def("integrate_dist", &msd::integrate_dist);
   m.def("release_static", &msd::release_static);
   msd::bind_events(m);
   m.def("build_params", &msd::build_params);

@@ -234,8 +234,17 @@ def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n
     spec = sc.bufs.get("spec")
     if spec is None or spec.device != dev:
         spec = sc.bufs["spec"] = torch.zeros(32, dtype=torch.int32, device=dev)
+    rccl = None
+    if flags_hook is not None and X_io is None:
+        f = getattr(world, "_rccl_handle", None)
+        rccl = f() if f is not None else None
     if flags_hook is None:
         _m().integrate(*args, 0, nparts, True, slot_p, _p(lists), mdt, _p(corr), _p(spec), _p(save), 0, _stream())
+    elif rccl is not None and _m().integrate_dist(c, P, s, m, R, C, _p(W), _p(p["_Q"]), _p(p["Kmr"]), _p(cm), _p(mm),
+                                                 _p(pos), _p(snap_a), _p(snap_b), _p(masks),
+                                                 [float(t) for t in trims], int(n_iters), slot_p, _p(lists), mdt,
+                                                 _p(corr), _p(spec), _p(save), rccl, _stream()):
+        pass  # the same protocol as below, issued natively with its all-reduces (one call)
     elif _m().integrate(*args, 0, 0, False, slot_p, _p(lists), mdt, _p(corr), _p(spec), _p(save), 1, _stream()):
         # domain-decomposed world, speculative: every rank integrates all parts in one go, then ONE
         # MAX all-reduce of the speculative flags + unfit word makes "every part ran all iterations

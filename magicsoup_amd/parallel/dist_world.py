@@ -275,6 +275,12 @@ class DistributedWorld(World):
         cm[H + 1].copy_(r_dn)
         cm[0].copy_(r_up)
 
+    def _rccl_handle(self) -> int | None:
+        """Handle of the native RCCL communicator in use (None: exchanges go through torch /
+        gloo), for native code that issues its collectives itself (hip_ops integrate_dist)."""
+        c = self._active_comm()
+        return c.handle if isinstance(c, RcclComm) and self.__dict__.get("_allreduce_flags") else None
+
     def _do_allreduce_flags(self, flags: torch.Tensor) -> None:
         self._all_reduce(flags, dist.ReduceOp.MAX)
 
