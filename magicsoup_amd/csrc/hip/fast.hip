@@ -115,6 +115,95 @@ int fast_divide(const FastWorld& f, int n, uintptr_t mask, uint64_t seed, uint64
   return slot;
 }
 
+// ---- the strip protocol of a decomposed world's divide_cells over a mask (parallel/dist_world.py),
+// its neighbour exchanges issued here on the native RCCL communicator `comm` (comm.hip)
+void strip_marks(int C, int H, uintptr_t cell_map, int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, uintptr_t up,
+                 uintptr_t dn, uintptr_t stream);
+void strip_reserve(int C, int H, uintptr_t from_up, uintptr_t from_dn, uintptr_t cell_map, uintptr_t stream);
+void strip_clear(int C, int H, uintptr_t cell_map, uintptr_t stream);
+void place_rounds_mask(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, bool vacate,
+                       uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result,
+                       int rounds, uint64_t seed, uint64_t call, uintptr_t stream);
+void place_split(int k, uintptr_t result, uintptr_t cells, int C, int H, uintptr_t par, uintptr_t npos, uintptr_t counts,
+                 uintptr_t hdr_up, uintptr_t hdr_dn, int lw, int gw, int m, uintptr_t stream);
+void rec_pack(int k_up, int k_dn, uintptr_t par_up, uintptr_t pos_up, uintptr_t par_dn, uintptr_t pos_dn,
+              uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, uintptr_t gdata, uintptr_t glen, int gw,
+              uintptr_t ldata, uintptr_t llen, int lw, int m, bool child, uintptr_t out_up, uintptr_t out_dn,
+              uintptr_t stream);
+void rec_unpack(int n0, int k_up, uintptr_t in_up, int up_lw, int up_gw, int k_dn, uintptr_t in_dn, int dn_lw,
+                int dn_gw, int C, int H, uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, uintptr_t gdata,
+                uintptr_t glen, int gw, uintptr_t ldata, uintptr_t llen, int lw, int m, uintptr_t cell_map,
+                uintptr_t stream);
+void divide_commit_list(int k, uintptr_t par, uintptr_t npos, long long n0, int n_exp, uintptr_t exp, int m,
+                        uintptr_t pos, uintptr_t cell_mols, uintptr_t divisions, uintptr_t lifetimes, uintptr_t stream);
+void rccl_exchange(uintptr_t comm, int up, int down, uintptr_t send_up, long long n_send_up, uintptr_t send_down,
+                   long long n_send_down, uintptr_t recv_down, long long n_recv_down, uintptr_t recv_up,
+                   long long n_recv_up, uintptr_t stream);
+
+static long long rec_bytes(int m, int lw, int gw) { return 4ll * (5 + m) + lw + gw; }
+
+__global__ void fill_i64_kernel(int64_t* dst, const int64_t* val, int k) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < k) dst[i] = *val;
+}
+
+// Phase A (up to the one synchronisation): boundary marks -> exchange -> reservations of the
+// neighbours' dividing cells -> placement over the mask -> winners split by destination (local /
+// upper halo / lower halo: par3 / npos3 at offsets 0, n, 2n) with the record headers -> header
+// exchange. st (int32[20]): counts [0:3], headers to up [4:8] / down [8:12], from up [12:16] / down
+// [16:20]. marks: 4 C bytes.
+void fast_dist_divide_a(const FastWorld& f, int n, uintptr_t mask, uintptr_t comm, int up, int down, uint64_t seed,
+                        uint64_t call, uintptr_t marks, uintptr_t par3, uintptr_t npos3, uintptr_t st, int lw, int gw,
+                        uintptr_t stream) {
+  if (!f.ready) throw std::invalid_argument("fast_dist_divide_a: descriptor not finalized");
+  if (n <= 0 || n > f.cap) throw std::invalid_argument("fast_dist_divide_a: cell count outside the capacity");
+  if (f.wrap || f.r_lo != 1 || f.R != f.r_hi + 1) throw std::invalid_argument("fast_dist_divide_a: not a strip");
+  const int C = f.C, H = f.r_hi - f.r_lo;
+  const uintptr_t s_up = marks, s_dn = marks + C, r_dn = marks + 2 * (size_t)C, r_up = marks + 3 * (size_t)C;
+  strip_marks(C, H, f.cell_map, n, 0, mask, f.pos, s_up, s_dn, stream);
+  rccl_exchange(comm, up, down, s_up, C, s_dn, C, r_dn, C, r_up, C, stream);
+  strip_reserve(C, H, r_up, r_dn, f.cell_map, stream);
+  place_rounds_mask(n, mask, f.pos, f.R, C, f.r_lo, f.r_hi, 0, false, f.cell_map, f.pending, f.cand, f.claim, f.result,
+                    f.rounds, seed, call, stream);
+  place_split(n, f.result, 0, C, H, par3, npos3, st, st + 16, st + 32, lw, gw, f.m, stream);
+  rccl_exchange(comm, up, down, st + 16, 16, st + 32, 16, st + 64, 16, st + 48, 16, stream);
+}
+
+// Phase B (after the synchronisation, counts known): child records of the exporting parents packed
+// and exchanged, local children committed as rows n0.. (positions, halved molecules, divisions,
+// lifetimes; exporters halved too) with their genome / label / parameter-row entries cloned, the
+// arrivals unpacked as rows n0 + n_loc.. (their parameter rows: the all-zero row `zero_row` until
+// the caller's rebuild), the halo rows cleared. The descriptor has room for every row.
+void fast_dist_divide_b(const FastWorld& f, long long n0, uintptr_t comm, int up, int down, uintptr_t par3,
+                        uintptr_t npos3, int kk, int n_loc, int n_up, int n_dn, int lw, int gw, uintptr_t out,
+                        uintptr_t in, int in_up, int up_lw, int up_gw, int in_dn, int dn_lw, int dn_gw,
+                        uintptr_t zero_row, uintptr_t stream) {
+  if (!f.ready) throw std::invalid_argument("fast_dist_divide_b: descriptor not finalized");
+  if (n0 + n_loc + in_up + in_dn > f.cap) throw std::invalid_argument("fast_dist_divide_b: capacity");
+  const int C = f.C, H = f.r_hi - f.r_lo, m = f.m;
+  const uintptr_t par_up = par3 + 8ull * kk, par_dn = par3 + 16ull * kk;
+  const uintptr_t pos_up = npos3 + 8ull * kk, pos_dn = npos3 + 16ull * kk;
+  const long long B = rec_bytes(m, lw, gw);
+  const uintptr_t out_up = out, out_dn = out + (size_t)n_up * B;
+  rec_pack(n_up, n_dn, par_up, pos_up, par_dn, pos_dn, f.mols, f.pos, f.life, f.div, f.g_data, f.g_lens, f.g_width,
+           f.l_data, f.l_lens, f.l_width, m, true, out_up, out_dn, stream);
+  const long long b_up = in_up * rec_bytes(m, up_lw, up_gw), b_dn = in_dn * rec_bytes(m, dn_lw, dn_gw);
+  const uintptr_t rin_up = in, rin_dn = in + (size_t)b_up;
+  rccl_exchange(comm, up, down, out_up, n_up * B, out_dn, n_dn * B, rin_dn, b_dn, rin_up, b_up, stream);
+  hipStream_t s = S_(stream);
+  divide_commit_list(n_loc, par3, npos3, n0, n_up, par_up, m, f.pos, f.mols, f.div, f.life, stream);
+  if (n_dn) divide_commit_list(0, 0, 0, n0, n_dn, par_dn, m, f.pos, f.mols, f.div, f.life, stream);
+  if (n_loc) launch_row_args(f.clone, n_loc, nullptr, P_<int64_t>(par3), nullptr, n0, s);
+  const int k_in = in_up + in_dn;
+  if (k_in) {
+    rec_unpack((int)(n0 + n_loc), in_up, rin_up, up_lw, up_gw, in_dn, rin_dn, dn_lw, dn_gw, C, H, f.mols, f.pos, f.life,
+               f.div, f.g_data, f.g_lens, f.g_width, f.l_data, f.l_lens, f.l_width, m, f.cell_map, stream);
+    fill_i64_kernel<<<cdiv(k_in, 256), 256, 0, s>>>(P_<int64_t>(f.slot) + n0 + n_loc, P_<int64_t>(zero_row), k_in);
+    MS_LAUNCH_CHECK();
+  }
+  strip_clear(C, H, f.cell_map, stream);
+}
+
 void bind_fast(pybind11::module_& m) {
   namespace py = pybind11;
   py::class_<FastWorld>(m, "FastWorld", py::module_local())
@@ -160,6 +249,8 @@ void bind_fast(pybind11::module_& m) {
       .def("finalize", &FastWorld::finalize);
   m.def("fast_kill", &fast_kill, "kill_cells(mask) in one call (status slot of the survivor count)");
   m.def("fast_divide", &fast_divide, "divide_cells(mask) in one call (status slot of the winner count)");
+  m.def("fast_dist_divide_a", &fast_dist_divide_a, "strip divide protocol up to the synchronisation");
+  m.def("fast_dist_divide_b", &fast_dist_divide_b, "strip divide protocol after the synchronisation");
 }
 
 }  // namespace msd

@@ -42,6 +42,7 @@ strip boundaries placement is exactly the single-map algorithm.
 from __future__ import annotations
 
 import copy
+import os
 import math
 import random
 from pathlib import Path
@@ -56,6 +57,9 @@ from magicsoup_amd.parallel import strip
 from magicsoup_amd.parallel.comm import RcclComm, make_comm
 
 _U8 = torch.uint8
+# divide_cells over a mask as native calls when the exchanges go over RCCL (MS_NATIVE_DIVIDE=0: the
+# Python protocol)
+_NATIVE_DIVIDE = os.environ.get("MS_NATIVE_DIVIDE", "1") != "0"
 
 
 def _pack(cols: list[torch.Tensor], k: int) -> torch.Tensor:
@@ -420,6 +424,8 @@ class DistributedWorld(World):
         else:
             idxs = self._idx_tensor(cell_idxs)
             k = int(idxs.numel())
+        if mask is not None and self._rccl_native():
+            return self._divide_mask_native(mask)
         sc = _scratch(self)
         empty = torch.zeros(0, dtype=torch.long, device=dev)
         # 1. boundary bytes (occupied / dividing) to the neighbours; halo occupancy + reservations
@@ -505,6 +511,65 @@ class DistributedWorld(World):
         # what crossed a boundary, in record order (read by the global-index view, GlobalWorld)
         self.__dict__["_xfer"] = (par_up, par_dn, int(hdr_up[0]), int(hdr_dn[0]))
         return (par_loc if n_loc else empty), children
+
+    def _rccl_native(self) -> bool:
+        """Exchanges of the main stream go over the native RCCL communicator (the strip protocol
+        can then run as native calls that issue their own exchanges)."""
+        d = self.__dict__
+        return not d.get("_side_active") and isinstance(d.get("_comm"), RcclComm) and _NATIVE_DIVIDE
+
+    def _divide_mask_native(self, mask: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        """divide_cells_t over a GPU mask as two native calls around the one synchronisation
+        (csrc/hip/fast.hip fast_dist_divide_a / _b): the same protocol, kernels and exchanges as the
+        Python path below."""
+        from magicsoup_amd.ops import genome_pipeline, hip_ops
+        from magicsoup_amd.ops.hip_ops import _m, _p, _scratch, _stream
+
+        comm = self.__dict__["_comm"]
+        dev = self._tensor_device()
+        n0, C, m = self.n_cells, self.map_size, self.n_molecules
+        lw, gw = int(self._labels.width), int(self._genomes.width)
+        fw = self._fast_world(n0)
+        sc = _scratch(self)
+        mk = sc.get("dv_marks", 4 * C, _U8, dev)
+        par = sc.get("dv_par", 3 * n0, torch.int64, dev)
+        npos = sc.get("dv_npos", 6 * n0, torch.int32, dev)
+        st = sc.get("dv_status", 20, torch.int32, dev)
+        seed, call = hip_ops._rng()
+        _m().fast_dist_divide_a(fw, n0, _p(mask), comm.handle, comm.up, comm.down, seed, call, _p(mk), _p(par),
+                                _p(npos), _p(st), lw, gw, _stream())
+        hip_ops.guarded_sync()  # (peer failures raise instead of hanging the read-back)
+        v = st.tolist()  # the one synchronisation: local winner counts + the neighbours' headers
+        hip_ops.check_placement()
+        n_loc, n_up, n_dn = v[0], v[1], v[2]
+        hdr_up, hdr_dn = v[12:16], v[16:20]
+        k_in = hdr_up[0] + hdr_dn[0]
+        B = strip.record_bytes(m, lw, gw)
+        out = sc.get("dv_out", max(1, (n_up + n_dn) * B), _U8, dev)
+        b_in = hdr_up[0] * strip.record_bytes(m, hdr_up[1], hdr_up[2]) + hdr_dn[0] * strip.record_bytes(
+            m, hdr_dn[1], hdr_dn[2])
+        inb = sc.get("dv_in", max(1, b_in), _U8, dev)
+        n_new = n0 + n_loc + k_in
+        if k_in:
+            for arena, wi in ((self._genomes, 2), (self._labels, 1)):
+                w = max(int(hdr_up[wi]), int(hdr_dn[wi]), 1)
+                if w > arena.width:
+                    arena.reserve(n_new, w)
+        fw = self._fast_world(n_new)
+        zero_row = self.kinetics._zero_row()
+        _m().fast_dist_divide_b(fw, n0, comm.handle, comm.up, comm.down, _p(par), _p(npos), n0, n_loc, n_up, n_dn, lw,
+                                gw, _p(out), _p(inb), hdr_up[0], hdr_up[1], hdr_up[2], hdr_dn[0], hdr_dn[1],
+                                hdr_dn[2], _p(zero_row), _stream())
+        self._adopt_count(n_new)
+        if k_in:
+            new = torch.arange(n0 + n_loc, n_new, device=self.device)
+            if not genome_pipeline.rebuild_rows(self, new):
+                self._update_params_rows(new)
+        mig = self.migrated
+        mig["divided_out"] += n_up + n_dn
+        mig["divided_in"] += k_in
+        self.__dict__["_xfer"] = (par[n0 : n0 + n_up], par[2 * n0 : 2 * n0 + n_dn], int(hdr_up[0]), int(hdr_dn[0]))
+        return par[:n_loc], torch.arange(n0, n0 + n_loc, device=self.device)
 
     def _append_arrivals(self, hdr_up, in_up, hdr_dn, in_dn) -> None:
         """Append the records received from the upper (row 1) and lower (row H) neighbours as new

@@ -238,3 +238,48 @@ def _body_native_dist_integrate(rank, ws):
 
 def test_gpu_native_decomposed_integration_matches_plain_world():
     run_ranks(_body_native_dist_integrate, 1, timeout=300, backend="nccl")
+
+
+def _body_native_divide(rank, ws):
+    """One rank over RCCL (virtual strips, the rank is its own neighbour): divide_cells over a mask
+    as the two native calls (fast.hip fast_dist_divide_a / _b) gives the Python protocol's result
+    exactly -- placements, migrated children, molecules, genomes, labels and parameters."""
+    import magicsoup_amd as ms
+    from magicsoup_amd.parallel import DistributedWorld
+    from magicsoup_amd.parallel import dist_world as dwm
+    from tests.conftest import gen_genomes
+
+    ms.set_seed(8)
+    torch.manual_seed(8)
+    w = ms.World(chemistry=_chem(), map_size=64, seed=8, device="cpu")
+    w.spawn_cells(gen_genomes(1200, 300))
+    atp = _chem().molname_2_idx["ATP"]
+    out = {}
+    for native in (True, False):
+        dw = DistributedWorld(chemistry=_chem(), map_size=64, seed=9, device="cuda", strips=True)
+        dw.adopt_maps(w)
+        dw.scatter_from(w, maps=False)
+        dwm._NATIVE_DIVIDE = native
+        try:
+            for it in range(3):
+                dw.enzymatic_activity()
+                mask = dw.cell_molecules[:, atp] > 2.0
+                ms.set_seed(11 + it)
+                par, ch = dw.divide_cells_t(mask)
+        finally:
+            dwm._NATIVE_DIVIDE = True
+        dw.enzymatic_activity()
+        torch.cuda.synchronize()
+        out[native] = (par.cpu(), ch.cpu(), dw.cell_positions.cpu(), dw.cell_molecules.cpu(), dw.cell_divisions.cpu(),
+                       dw.cell_lifetimes.cpu(), list(dw.cell_genomes), list(dw.cell_labels), dw.cell_map.cpu(),
+                       dict(dw.migrated))
+        dw.close()
+    a, b = out[True], out[False]
+    assert a[9]["divided_in"] > 0  # children crossed the (self-)boundary
+    for x, y in zip(a[:6], b[:6]):
+        assert torch.equal(x, y)
+    assert a[6] == b[6] and a[7] == b[7] and torch.equal(a[8], b[8]) and a[9] == b[9]
+
+
+def test_gpu_native_strip_divide_matches_python_protocol():
+    run_ranks(_body_native_divide, 1, timeout=300, backend="nccl")
