@@ -1193,20 +1193,25 @@ __device__ __forceinline__ void build_group(const BuildArgs& b, long long grp, i
   const size_t row = (size_t)b.rows[ci];
   const size_t o2 = row * b.Pt + p, o3 = o2 * b.s;
   const int32_t* pt = b.tokens + ((size_t)ci * b.P + (p < b.P ? p : 0)) * b.D * 5;
+  // (b.full: the eight unpacked parameter tensors are held too; compact storage has W / Q / Kmr only)
   if (b.nprot && b.nprot[ci] == 0) {  // empty proteome: unset_cell_params semantics (all zero)
     for (int j = lane; j < b.s; j += G) {
-      b.N[o3 + j] = 0;
-      b.Nf[o3 + j] = 0;
-      b.Nb[o3 + j] = 0;
-      b.A[o3 + j] = 0;
+      if (b.N) {
+        b.N[o3 + j] = 0;
+        b.Nf[o3 + j] = 0;
+        b.Nb[o3 + j] = 0;
+        b.A[o3 + j] = 0;
+      }
       b.Kmr[o3 + j] = 0.0f;
       if (b.W) b.W[o3 + j] = 0;
     }
     if (lane == 0) {
-      b.Ke[o2] = 0.0f;
-      b.Kmf[o2] = 0.0f;
-      b.Kmb[o2] = 0.0f;
-      b.Vmax[o2] = 0.0f;
+      if (b.Ke) {
+        b.Ke[o2] = 0.0f;
+        b.Kmf[o2] = 0.0f;
+        b.Kmb[o2] = 0.0f;
+        b.Vmax[o2] = 0.0f;
+      }
       if (b.Q) b.Q[o2] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     return;
@@ -1241,10 +1246,12 @@ __device__ __forceinline__ void build_group(const BuildArgs& b, long long grp, i
         if (ndv > 0) nb += ndv;
       }
     }
-    b.N[o3 + j] = n;
-    b.Nf[o3 + j] = nf;
-    b.Nb[o3 + j] = nb;
-    b.A[o3 + j] = av;
+    if (b.N) {
+      b.N[o3 + j] = n;
+      b.Nf[o3 + j] = nf;
+      b.Nb[o3 + j] = nb;
+      b.A[o3 + j] = av;
+    }
     if (b.W) b.W[o3 + j] = pack_word(n, nf, nb, av, b.overflow);
     b.Kmr[o3 + j] = powf(kc > 0 ? ks / (float)kc : 0.0f, (float)av);
     E += (double)n * (double)b.energies[j];
@@ -1266,10 +1273,12 @@ __device__ __forceinline__ void build_group(const BuildArgs& b, long long grp, i
   kmfv = kmfv < ms::kEps ? ms::kEps : (kmfv > ms::kMax ? ms::kMax : kmfv);
   kmbv = kmbv < ms::kEps ? ms::kEps : (kmbv > ms::kMax ? ms::kMax : kmbv);
   const float vmv = vm.value0();
-  b.Ke[o2] = kev;
-  b.Kmf[o2] = kmfv;
-  b.Kmb[o2] = kmbv;
-  b.Vmax[o2] = vmv;
+  if (b.Ke) {
+    b.Ke[o2] = kev;
+    b.Kmf[o2] = kmfv;
+    b.Kmb[o2] = kmbv;
+    b.Vmax[o2] = vmv;
+  }
   if (b.Q) b.Q[o2] = make_float4(vmv, kmfv, kmbv, kev);
 }
 
@@ -1773,6 +1782,7 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
                   uintptr_t dn, uintptr_t stream) {
   if (n <= 0 || Pt <= 0) return;
   if ((W == 0) != (Q == 0) || (W != 0 && overflow == 0)) throw std::invalid_argument("build_params: W, Q, overflow");
+  if ((N == 0 || Ke == 0) && W == 0) throw std::invalid_argument("build_params: no parameter layout to write");
   if (P > Pt) throw std::invalid_argument("build_params: token proteins exceed parameter capacity");
   BuildArgs b{};
   b.n = n; b.P = P; b.D = D; b.Pt = Pt; b.s = s;

@@ -19,8 +19,9 @@ against, and they run when a subclass overrides them (e.g. to switch stages off 
 from __future__ import annotations
 
 import math
-import weakref
+import os
 import random
+import weakref
 from typing import Any
 
 import numpy as np
@@ -210,6 +211,8 @@ _I32_PARAMS = ("N", "Nf", "Nb", "A")
 # (Vmax, Kmf, Kmb, Ke); derived from these API tensors, kept in the same row storage
 _PACK_SRC = ("N", "Nf", "Nb", "A", "Vmax", "Kmf", "Kmb", "Ke")
 _PACKED = ("_W", "_Q")
+# compact GPU parameter storage (Kinetics._compact_store); MS_COMPACT_PARAMS=0 keeps all tensors
+_COMPACT = os.environ.get("MS_COMPACT_PARAMS", "1") != "0"
 
 
 def _spare_rows(n: int, row_bytes: int) -> int:
@@ -392,7 +395,7 @@ class Kinetics:
         copy; rows are never written in place while in row-storage mode). ``disjoint`` is kept for
         callers that know no destination is also a source."""
         store = self._store
-        dev = store["N"].device
+        dev = store["Kmr"].device
         if dev.type == "cuda":
             self._enter_slot_mode()
             slot = self.__dict__["_slot"]
@@ -435,7 +438,7 @@ class Kinetics:
         return self.__dict__["_store_d"]
 
     def _P(self) -> int:
-        return int(self._store["N"].size(1))
+        return int(self._store["Kmr"].size(1))
 
     def _get_param(self, name: str) -> torch.Tensor:
         self._sync()
@@ -476,13 +479,15 @@ class Kinetics:
         d = self.__dict__
         if d["_slot"] is None:
             n = d["_ncells"]
-            dev = self._store["N"].device
+            dev = self._store["Kmr"].device
             self._slot_reserve(n, dev)
             buf = d["_slot_buf"]
             torch.arange(n, device=dev, out=buf[:n])
             d["_slot"] = buf[:n]
             d["_nrows"] = n
             d["_free"] = None
+        if not d.get("_compact") and _COMPACT and d["_slot"].is_cuda and self._pack_ok():
+            self._compact_store()
 
     def _slot_reserve(self, n: int, dev=None) -> None:
         """Capacity of the slot buffers >= n (keeps the live entries)."""
@@ -588,7 +593,7 @@ class Kinetics:
             return None
         if free is not None:
             return free[r0 : r0 + k]
-        return torch.arange(r0, r0 + k, device=self._store["N"].device)
+        return torch.arange(r0, r0 + k, device=self._store["Kmr"].device)
 
     def _recycle_rows(self, k: int) -> torch.Tensor | None:
         """Make >= k fresh rows available: the free list of storage rows that no live cell (and not
@@ -648,6 +653,8 @@ class Kinetics:
 
     def _pack_ok(self) -> bool:
         d = self.__dict__
+        if d.get("_compact"):
+            return True  # the packed layout is the only one held (see _compact_store)
         st = d.get("_packed_stamp")
         store = d.get("_store_d", {})
         if st is None or any(k not in store for k in _PACKED) or len(st) != len(_PACK_SRC):
@@ -660,6 +667,8 @@ class Kinetics:
             self.__dict__["_packed_stamp"] = self._pack_stamp()
 
     def _drop_packed(self) -> None:
+        if self.__dict__.get("_compact"):
+            self._expand_store()
         store = self.__dict__.get("_store_d", {})
         for k in _PACKED:
             store.pop(k, None)
@@ -685,10 +694,43 @@ class Kinetics:
         self._restamp(True)
         return store
 
+    # ---- compact GPU storage: in row-storage mode the integrator layout (_W: packed int8 N / Nf /
+    # Nb / A per (protein, signal), _Q: Vmax / Kmf / Kmb / Ke per protein) plus Kmr is all a row holds;
+    # the eight parameter tensors it packs are unpacked only when the dense API tensors are read
+    # (_materialize). A row takes 8 bytes per (protein, signal) instead of 24, which is what the
+    # parameter builds, row clones, storage growth and protein-slot growth move.
+    def _compact_store(self) -> None:
+        d = self.__dict__
+        store = self._store
+        if not all(k in store for k in _PACKED):
+            return
+        for k in _PACK_SRC:
+            store.pop(k, None)
+            d.get("_spare", {}).pop(k, None)
+        d["_compact"] = True
+        d.pop("_packed_stamp", None)
+
+    def _expand_store(self) -> None:
+        """Unpack the eight parameter tensors from _W / _Q (same rows) and leave compact mode."""
+        d = self.__dict__
+        if not d.get("_compact"):
+            return
+        store = self._store
+        W, Q = store["_W"], store["_Q"]
+        store["N"] = ((W << 24) >> 24).contiguous()
+        store["Nf"] = ((W >> 8) & 0xFF).contiguous()
+        store["Nb"] = ((W >> 16) & 0xFF).contiguous()
+        store["A"] = (W >> 24).contiguous()
+        for i, k in enumerate(("Vmax", "Kmf", "Kmb", "Ke")):
+            store[k] = Q[..., i].contiguous()
+        d["_compact"] = False
+        self._restamp(True)
+
     def _materialize(self) -> None:
         d = self.__dict__
         slot = d.get("_slot")
         if slot is None:
+            self._expand_store()
             return
         ok = self._pack_ok()
         n = d["_ncells"]
@@ -714,6 +756,7 @@ class Kinetics:
         d["_nrows"] = n
         d.pop("_zero_row_t", None)
         self._restamp(ok)
+        self._expand_store()
 
     def remove_cell_params(self, keep: torch.Tensor, removed: torch.Tensor | None = None, gathered: bool = False):
         """Keep only the cells where ``keep`` is true (bool mask (c,)) or listed (ascending index
@@ -788,7 +831,7 @@ class Kinetics:
             return
         self._sync()
         store = self._store
-        dev = store["N"].device
+        dev = store["Kmr"].device
         if dev.type == "cuda":
             # widen into new storage of the same row capacity, moving only the live cells' rows
             # (gathered to cell order, one launch) -- not every storage row -- and zeroing only

@@ -170,8 +170,8 @@ def _kin_desc(world, dev):
     kin._enter_slot_mode()
     packed = kin._pack_ok()
     row_cap, free = kin._row_limit()
-    N = store["N"]
-    key = (N.data_ptr(), N.size(1), N.size(2), store["Kmr"].data_ptr(), store["Vmax"].data_ptr(),
+    N = store["Kmr"]  # (compact storage holds no N: Kmr has the same (rows, P, s) shape)
+    key = (_p(store.get("N")), N.size(1), N.size(2), store["Kmr"].data_ptr(), _p(store.get("Vmax")),
            store["_W"].data_ptr() if packed else 0, store["_Q"].data_ptr() if packed else 0, row_cap,
            _p(free), float(kin.abs_temp), id(store))
     c = _cache(world)
@@ -184,8 +184,8 @@ def _kin_desc(world, dev):
 
         lu = build_luts(kin, dev)
         k = _m().GpKin()
-        k.N, k.Nf, k.Nb, k.A, k.Kmr = (_p(store[n]) for n in ("N", "Nf", "Nb", "A", "Kmr"))
-        k.Kmf, k.Kmb, k.Vmax, k.Ke = (_p(store[n]) for n in ("Kmf", "Kmb", "Vmax", "Ke"))
+        k.N, k.Nf, k.Nb, k.A, k.Kmr = (_p(store.get(n)) for n in ("N", "Nf", "Nb", "A", "Kmr"))
+        k.Kmf, k.Kmb, k.Vmax, k.Ke = (_p(store.get(n)) for n in ("Kmf", "Kmb", "Vmax", "Ke"))
         if packed:
             k.W, k.Q, k.overflow = _p(store["_W"]), _p(store["_Q"]), _p(hip_ops._overflow_flag(kin))
         k.P, k.s = int(N.size(1)), int(N.size(2))

@@ -174,7 +174,7 @@ def _overflow_flag(kin) -> torch.Tensor:
     sc = _scratch(kin)
     f = sc.bufs.get("pack_overflow")
     if f is None:
-        f = sc.bufs["pack_overflow"] = torch.zeros(1, dtype=torch.int32, device=kin._store["N"].device)
+        f = sc.bufs["pack_overflow"] = torch.zeros(1, dtype=torch.int32, device=kin._store["Kmr"].device)
         sc.bufs["pack_overflow_host"] = torch.zeros(1, dtype=torch.int32, pin_memory=True)
     return f
 
@@ -367,14 +367,14 @@ def build_params(kin, tokens, rows, luts, p, abs_temp: float, gas: float, nprot=
     """Fused parameter build; also writes the integrator layout when it is current."""
     packed = kin._pack_ok()
     n, P, D = int(tokens.size(0)), int(tokens.size(1)), int(tokens.size(2))
-    Pt, s = int(p["N"].size(1)), int(p["N"].size(2))
+    Pt, s = int(p["Kmr"].size(1)), int(p["Kmr"].size(2))
     _m().build_params(
         n, P, D, Pt, s, _p(tokens), _p(rows),
         _p(luts["vmax"]), luts["vmax"].numel(), _p(luts["km"]), luts["km"].numel(),
         _p(luts["signs"]), luts["signs"].numel(), _p(luts["hills"]), luts["hills"].numel(),
         _p(luts["react"]), _p(luts["trnsp"]), _p(luts["eff"]), int(luts["react"].size(0)),
         _p(luts["energies"]), float(abs_temp), float(gas),
-        *(_p(p[k]) for k in ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke")),
+        *(_p(p.get(k)) for k in ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke")),  # (compact: W / Q only)
         _p(nprot),
         _p(p["_W"] if packed else None), _p(p["_Q"] if packed else None),
         _p(_overflow_flag(kin) if packed else None),

@@ -94,7 +94,10 @@ def build_params(kin, rows: torch.Tensor, tokens: torch.Tensor, nprot: torch.Ten
     """Write parameter rows ``rows`` from dense tokens (n, P, D, 5). With ``nprot`` (GPU), rows
     whose proteome is empty are unset (all zero) in the same launch."""
     p = _canonical_params(kin)
-    dev = p["N"].device
+    dev = p["Kmr"].device
+    if dev.type != "cuda":
+        kin._materialize()  # (host builds write the full parameter set)
+        p = _canonical_params(kin)
     if rows.numel() == 0:
         return
     tokens = tokens.to(device=dev, dtype=torch.int32).contiguous()

@@ -60,7 +60,8 @@ for s in "$@"; do case "$s" in
   dbench) run diffuse_bench 300 python scripts/diffuse_bench.py --vec 4 8 --blocks 1024 0 2048 ;;
   dtests) run dtests 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "diffusion or reduced_precision or permeation" ;;
   tc64) trace tc64 9 --preset wide --steps 10 --warmup 5 ;;
-  spk1m) MS_MAP_DTYPE=fp16 run spikes_1m 600 python scripts/spike_events.py 16384 1000000 40 5 ;;
+  spk1m) MS_MAP_DTYPE=fp16 run spikes_1m 600 python scripts/spike_events.py 16384 1000000 70 10 ;;
+  spk1mw) MS_GENOME_WIDTH_WATCH=1 MS_MAP_DTYPE=fp16 run spikes_1m_watch 600 python scripts/spike_events.py 16384 1000000 70 10 ;;
   *) echo "unknown step $s"; exit 2 ;;
 esac; done
 exit 0

@@ -372,7 +372,7 @@ def test_param_row_storage_fuzz_matches_dense_model():
             dense.__dict__.update(kin.__dict__)
             dense.__dict__.update(_store_d={k: model[k].clone() for k in names}, _slot=None, _hip_scratch=None,
                                   _ncells=model["N"].size(0), _nrows=model["N"].size(0), _packed_stamp=None,
-                                  _spare={})
+                                  _spare={}, _compact=False)
             dense.__dict__.pop("_hip_scratch")
             Xa, Xb = X.clone(), X.clone()
             kinetics_ops.integrate(kin, Xa, (0.7, 0.2, 0.1), 4)
