@@ -97,6 +97,13 @@ struct IntegrateArgs {
   int wb_m, wb_R, wb_C, wb_dtype;
 };
 
+// a.trims[q] without dynamic indexing (a dynamically indexed kernel-argument array is copied to
+// scratch memory: the speculative register kernels spilled there)
+__device__ __forceinline__ float trim_of(const IntegrateArgs& a, int q) {
+  static_assert(kMaxParts == 4, "trim_of selects among 4 parts");
+  return q == 0 ? a.trims[0] : (q == 1 ? a.trims[1] : (q == 2 ? a.trims[2] : a.trims[3]));
+}
+
 // Did the speculative all-parts launch hold? (every part ran all n_iters iterations and every cell
 // was integrated)
 __device__ __forceinline__ bool spec_held(const unsigned* w, int nparts, int n_iters) {
@@ -462,7 +469,7 @@ __global__ void __launch_bounds__(kBlock) integrate_spec_lds_kernel(IntegrateArg
   for (int base = (int)blockIdx.x * cps; base < limit; base += (int)gridDim.x * cps) {
     for (int part = 0; part < a.spec_parts; ++part) {
       IntegrateArgs ap = a;
-      ap.trim = a.trims[part];
+      ap.trim = trim_of(a, part);
       ap.spec_prev = part > 0;
       ap.snap_prev = part > 0 ? a.snap_out : a.snap_prev;
       unsigned b = 0u;
@@ -578,7 +585,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     if (listed && p < P) vmax = a.Q[prow * P + p].x;
     const float vm = vmax * (spec ? a.trims[0] : a.trim);
     const bool on = listed && p < P && !(vm <= 0.0f);
-    for (int q = 1; q < nparts; ++q) trim_diff |= on != (listed && p < P && !(vmax * a.trims[q] <= 0.0f));
+    for (int q = 1; q < nparts; ++q) trim_diff |= on != (listed && p < P && !(vmax * trim_of(a, q) <= 0.0f));
     const unsigned long long gm = group_ballot<G>(on);
     const int k = na + __popcll(gm & ((1ull << lane) - 1ull));
     if (on && k < G) act[k] = p;
@@ -712,7 +719,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
 #pragma unroll
   for (int h = 0; h < SPL; ++h) xc[h] = x0[h];
   for (int part = 0; part < nparts; ++part) {
-  const float vm = vraw * (spec ? a.trims[part] : a.trim);
+  const float vm = vraw * (spec ? trim_of(a, part) : a.trim);
   const float vmx = prot && (vm > 0.0f || vm != vm) ? vm : 0.0f;
   const int bsh = spec ? ms::kEqIters * part : 0;  // this part's bits
   // ---- 4. velocity (protein lane; entries past the count are zero words: no effect)

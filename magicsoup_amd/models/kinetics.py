@@ -620,7 +620,7 @@ class Kinetics:
                 d["_free"] = free
                 d["_nrows"] = 0
                 return free
-        self._materialize()  # dense again: rows 0..n-1 live
+        self._materialize(expand=False)  # dense again: rows 0..n-1 live
         self._enter_slot_mode()
         if n + k + spare > cap:
             new_cap = max(n + k + spare, int(cap * 1.5) + 64)
@@ -726,11 +726,14 @@ class Kinetics:
         d["_compact"] = False
         self._restamp(True)
 
-    def _materialize(self) -> None:
+    def _materialize(self, expand: bool = True) -> None:
+        """Dense, cell-ordered rows (leaves row-storage mode). ``expand``: also unpack the API
+        tensors of compact storage (internal re-layouts keep it compact)."""
         d = self.__dict__
         slot = d.get("_slot")
         if slot is None:
-            self._expand_store()
+            if expand:
+                self._expand_store()
             return
         ok = self._pack_ok()
         n = d["_ncells"]
@@ -756,7 +759,8 @@ class Kinetics:
         d["_nrows"] = n
         d.pop("_zero_row_t", None)
         self._restamp(ok)
-        self._expand_store()
+        if expand:
+            self._expand_store()
 
     def remove_cell_params(self, keep: torch.Tensor, removed: torch.Tensor | None = None, gathered: bool = False):
         """Keep only the cells where ``keep`` is true (bool mask (c,)) or listed (ascending index

@@ -26,6 +26,15 @@ trace() {  # trace <name> <steps-to-summarise> <bench args...>: kernel trace + -
   if fatal $rc; then echo "fatal rc=$rc in $name"; tail -30 "$O/$name.log"; exit $rc; fi
   python scripts/step_kernels.py $O/$name/run_kernel_trace.csv $k > $O/${name}_steps.txt 2>&1
 }
+pmc() {  # pmc <name> <kernel regex> <counters> -- <bench args...>: one counter pass (no tracing domains)
+  local name="$1" kr="$2" ctr="$3"; shift 4
+  echo "== pmc $name $(date +%T)"
+  timeout -s KILL 180 rocprofv3 --pmc $ctr --kernel-include-regex "$kr" -d $O/$name -o run --output-format csv -- \
+    python bench.py "$@" > $O/$name.log 2>&1
+  local rc=$?
+  echo "   rc=$rc"
+  if fatal $rc; then echo "fatal rc=$rc in $name"; tail -30 "$O/$name.log"; exit $rc; fi
+}
 for s in "$@"; do case "$s" in
   tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
   smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -60,6 +69,10 @@ for s in "$@"; do case "$s" in
   dbench) run diffuse_bench 300 python scripts/diffuse_bench.py --vec 4 8 --blocks 1024 0 2048 ;;
   dtests) run dtests 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "diffusion or reduced_precision or permeation" ;;
   tc64) trace tc64 9 --preset wide --steps 10 --warmup 5 ;;
+  tm1) trace tm1 19 --preset m1 --steps 20 --warmup 10 ;;
+  pmcw1) pmc pmc_wide_sq "integrate|gather_bin|diffuse_stencil" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" -- --preset wide --steps 3 --warmup 3 ;;
+  pmcw2) pmc pmc_wide_fetch "integrate|diffuse_stencil" "FETCH_SIZE" -- --preset wide --steps 3 --warmup 3 ;;
+  pmcw3) pmc pmc_wide_write "integrate|diffuse_stencil" "WRITE_SIZE" -- --preset wide --steps 3 --warmup 3 ;;
   spk1m) MS_MAP_DTYPE=fp16 run spikes_1m 600 python scripts/spike_events.py 16384 1000000 70 10 ;;
   spk1mw) MS_GENOME_WIDTH_WATCH=1 MS_MAP_DTYPE=fp16 run spikes_1m_watch 600 python scripts/spike_events.py 16384 1000000 70 10 ;;
   *) echo "unknown step $s"; exit 2 ;;
