@@ -431,7 +431,9 @@ __global__ void __launch_bounds__(64) xb_apply_kernel(int C, int slot_w, uint64_
   // b = 0: our cell is the upper one (its copy in slots_dn), the lower one arrived in recv_dn
   const uint8_t* ua = b == 0 ? slots_dn + so : recv_up + so;
   const uint8_t* lb = b == 0 ? recv_dn + so : slots_up + so;
-  const int n0 = *reinterpret_cast<const int32_t*>(ua), n1 = *reinterpret_cast<const int32_t*>(lb);
+  // (lengths clamped to the slot: a corrupted exchange must not send the pair past its buffers)
+  const int n0 = min(max(*reinterpret_cast<const int32_t*>(ua), 0), slot_w);
+  const int n1 = min(max(*reinterpret_cast<const int32_t*>(lb), 0), slot_w);
   uint8_t* mine = out + (size_t)(base + j) * out_width;
   uint8_t* theirs = other + (size_t)j * out_width;
   int w0, w1;
@@ -604,6 +606,31 @@ void release_dist_buffers() {
   if (g_split_tiles) MS_HIP_CHECK(hipFree(g_split_tiles));
   g_split_tiles = nullptr;
   g_split_cap = 0;
+}
+
+void index_map(int c, uintptr_t pos, int C, uintptr_t idx_map, bool clear, uintptr_t stream);
+void rccl_exchange(uintptr_t comm, int up, int down, uintptr_t send_up, long long n_send_up, uintptr_t send_down,
+                   long long n_send_down, uintptr_t recv_down, long long n_recv_down, uintptr_t recv_up,
+                   long long n_recv_up, uintptr_t stream);
+
+// The collective part of the strip-boundary recombination (parallel/dist_world.py
+// _BoundaryRecombination) in one call over the native RCCL communicator `comm`: the index map, the
+// boundary rows' genome lengths exchanged, the events drawn and the event genomes exchanged.
+// lens: int32 4 (C + 1) = mine up | mine down | from down | from up; own: int32 2 C; slots: 4 E
+// (4 + slot_w) bytes = to down | to up | from down | from up.
+void xb_begin(int C, int H, int n, uintptr_t pos, uintptr_t idx_map, uintptr_t glens, uintptr_t gdata, int width,
+              uintptr_t lens, uintptr_t own, int E, int slot_w, double p, int kcap, uint64_t seed_dn, uint64_t seed_up,
+              uint64_t call, uintptr_t evbuf, uintptr_t slots, uintptr_t comm, int up, int down, uintptr_t stream) {
+  const size_t lb = 4ull * (C + 1);
+  const uintptr_t mine_up = lens, mine_dn = lens + lb, from_dn = lens + 2 * lb, from_up = lens + 3 * lb;
+  index_map(n, pos, C, idx_map, false, stream);
+  xb_prep(C, H, n, pos, idx_map, glens, width, mine_up, mine_dn, own, own + 4ull * C, stream);
+  rccl_exchange(comm, up, down, mine_up, lb, mine_dn, lb, from_dn, lb, from_up, lb, stream);
+  const size_t sb = (size_t)E * (4 + slot_w);  // a slot: 4 header bytes + slot_w genome bytes
+  const uintptr_t slots_dn = slots, slots_up = slots + sb, recv_dn = slots + 2 * sb, recv_up = slots + 3 * sb;
+  xb_events(C, E, slot_w, p, kcap, seed_dn, seed_up, call, mine_dn, from_dn, mine_up, from_up, own, own + 4ull * C,
+            gdata, width, evbuf, slots_dn, slots_up, stream);
+  rccl_exchange(comm, up, down, slots_up, sb, slots_dn, sb, recv_dn, sb, recv_up, sb, stream);
 }
 
 }  // namespace msd

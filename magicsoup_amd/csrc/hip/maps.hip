@@ -628,6 +628,40 @@ void diffuse_boundary(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, ui
 
 size_t diffuse_boundary_partials_len(int m, int C) { return (size_t)4 * cdiv(C, 64) * m; }
 
+void halo_pack(int m, int C, int H, int elem, uintptr_t map, uintptr_t send_up, uintptr_t send_dn, uintptr_t stream);
+void halo_unpack(int m, int C, int H, int elem, uintptr_t map, uintptr_t from_up, uintptr_t from_dn, uintptr_t stream);
+void rccl_exchange(uintptr_t comm, int up, int down, uintptr_t send_up, long long n_send_up, uintptr_t send_down,
+                   long long n_send_down, uintptr_t recv_down, long long n_recv_down, uintptr_t recv_up,
+                   long long n_recv_up, uintptr_t stream);
+void rccl_allreduce(uintptr_t comm, uintptr_t buf, long long count, int dtype, int op, uintptr_t stream);
+void stream_join(uintptr_t dst, uintptr_t src);
+void diffuse_corr(int m, uintptr_t totals, double n_pix, uintptr_t corr, uintptr_t stream);
+
+// One diffusion step of a strip of a decomposed world over the native RCCL communicator, in one call:
+// the halo rows travel on `halo_stream` (pack, exchange, unpack) while the interior rows' stencil runs
+// on `stream`; then the two boundary rows, the all-reduce (SUM) of the mass totals and the new
+// correction. Same kernels and order as ops/hip_ops.py diffuse (split path).
+void diffuse_strip(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t wa, uintptr_t wb,
+                   uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t partials_b, uintptr_t totals,
+                   uintptr_t new_corr, double n_pix, int dtype, uintptr_t comm, int up, int down, uintptr_t halo_bufs,
+                   uintptr_t halo_stream, uintptr_t stream) {
+  const int H = r_hi - r_lo;
+  if (m <= 0 || H < 3 || r_lo != 1 || R != r_hi + 1) throw std::invalid_argument("diffuse_strip: not a strip of >= 3 rows");
+  const int elem = dtype == kF32 ? 4 : 2;
+  const long long plane_b = (long long)m * C * elem;  // one halo row of every species, bytes
+  const uintptr_t s_up = halo_bufs, s_dn = halo_bufs + plane_b, r_dn = halo_bufs + 2 * plane_b,
+                  r_up = halo_bufs + 3 * plane_b;
+  stream_join(halo_stream, stream);
+  halo_pack(m, C, H, elem, map, s_up, s_dn, halo_stream);
+  rccl_exchange(comm, up, down, s_up, plane_b, s_dn, plane_b, r_dn, plane_b, r_up, plane_b, halo_stream);
+  halo_unpack(m, C, H, elem, map, r_up, r_dn, halo_stream);
+  diffuse_stencil(m, R, C, r_lo + 1, r_hi - 1, 0, map, tmp, wa, wb, scale, corr, partials, totals, dtype, 0, stream);
+  stream_join(stream, halo_stream);
+  diffuse_boundary(m, R, C, r_lo, r_hi, map, tmp, wa, wb, scale, corr, partials_b, totals, dtype, stream);
+  rccl_allreduce(comm, totals, 2ll * m, 2 /* float64 */, 0 /* sum */, stream);
+  diffuse_corr(m, totals, n_pix, new_corr, stream);
+}
+
 void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t totals,
                      double n_pix, int dtype, uintptr_t stream) {
   if (m <= 0) return;

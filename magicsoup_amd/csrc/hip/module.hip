@@ -42,6 +42,10 @@ void diffuse_boundary(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, ui
                       uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t totals, int dtype,
                       uintptr_t stream);
 size_t diffuse_boundary_partials_len(int m, int C);
+void diffuse_strip(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t wa, uintptr_t wb,
+                   uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t partials_b, uintptr_t totals,
+                   uintptr_t new_corr, double n_pix, int dtype, uintptr_t comm, int up, int down, uintptr_t halo_bufs,
+                   uintptr_t halo_stream, uintptr_t stream);
 void apply_pending(int m, long long plane, uintptr_t map, uintptr_t corr, uintptr_t f, int dtype, uintptr_t stream);
 void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t totals,
                      double n_pix, int dtype, uintptr_t stream);
@@ -193,6 +197,9 @@ void halo_pack(int m, int C, int H, int elem, uintptr_t map, uintptr_t send_up, 
 void halo_unpack(int m, int C, int H, int elem, uintptr_t map, uintptr_t from_up, uintptr_t from_dn, uintptr_t stream);
 void xb_prep(int C, int H, int n, uintptr_t pos, uintptr_t idx_map, uintptr_t lens, int width, uintptr_t len_up,
              uintptr_t len_dn, uintptr_t own1, uintptr_t ownH, uintptr_t stream);
+void xb_begin(int C, int H, int n, uintptr_t pos, uintptr_t idx_map, uintptr_t glens, uintptr_t gdata, int width,
+              uintptr_t lens, uintptr_t own, int E, int slot_w, double p, int kcap, uint64_t seed_dn, uint64_t seed_up,
+              uint64_t call, uintptr_t evbuf, uintptr_t slots, uintptr_t comm, int up, int down, uintptr_t stream);
 void xb_events(int C, int E, int slot_w, double p, int kcap, uint64_t seed_dn, uint64_t seed_up, uint64_t call,
                uintptr_t mine_dn, uintptr_t from_dn, uintptr_t mine_up, uintptr_t from_up, uintptr_t own1,
                uintptr_t ownH, uintptr_t arena, int width, uintptr_t evbuf, uintptr_t slots_dn, uintptr_t slots_up,
@@ -243,6 +250,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("diffuse_corr", &msd::diffuse_corr);
   m.def("diffuse_boundary", &msd::diffuse_boundary);
   m.def("diffuse_boundary_partials_len", &msd::diffuse_boundary_partials_len);
+  m.def("diffuse_strip", &msd::diffuse_strip);
   m.def("apply_pending", &msd::apply_pending);
   m.def("diffuse_partials_len", &msd::diffuse_partials_len);
   m.def("scale_planes", &msd::scale_planes);
@@ -313,6 +321,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("halo_unpack", &msd::halo_unpack);
   m.def("xb_prep", &msd::xb_prep);
   m.def("xb_events", &msd::xb_events, "strip-boundary recombination events (one workgroup, both boundaries)");
+  m.def("xb_begin", &msd::xb_begin);
   m.def("xb_apply", &msd::xb_apply);
   msd::bind_fast(m);
   msd::bind_gp(m);

@@ -433,6 +433,24 @@ def diffuse(world) -> None:
     # neighbours' unscaled boundary rows carry the same pending factor (and the same correction:
     # it is computed from all-reduced totals)
     scale, corr = d.get("_pending_scale"), d.get("_pending_corr")
+    rcomm = world._rccl_comm() if split and hasattr(world, "_rccl_comm") else None
+    if rcomm is not None:
+        # the whole split step natively: halo exchange on its own stream next to the interior
+        # stencil, boundary rows, all-reduced mass totals, new correction (maps.hip diffuse_strip)
+        hs = d.get("_halo_stream")
+        if hs is None:
+            hs = d["_halo_stream"] = torch.cuda.Stream(device=dev)
+        pb = sc.get("diff_partials_b", int(_m().diffuse_boundary_partials_len(m, C)), torch.float64, dev)
+        new_corr = sc.get("diff_corr", m, torch.float32, dev)
+        n_pix = float(getattr(world, "_n_pix_global", R * C if wrap else (r_hi - r_lo) * C))
+        _m().diffuse_strip(m, R, C, r_lo, r_hi, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale), _p(corr), _p(partials),
+                           _p(pb), _p(totals), _p(new_corr), n_pix, _mdt(mm), rcomm.handle, rcomm.up, rcomm.down,
+                           _p(world._halo_buffers()), hs.cuda_stream, _stream())
+        d["_molmap"] = tmp.view(mm.shape)
+        sc.bufs["diff_tmp"] = mm.view(-1)
+        d["_pending_scale"] = None
+        d["_pending_corr"] = new_corr
+        return
     if split:
         from magicsoup_amd.ops.streams import join, on_stream
 

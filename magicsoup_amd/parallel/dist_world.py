@@ -251,6 +251,22 @@ class DistributedWorld(World):
 
         return (block(b_dn, hd), hd[2:]), (block(b_up, hu), hu[2:])
 
+    def _halo_buffers(self) -> torch.Tensor:
+        """(send up | send down | from down | from up) halo rows of every species, map dtype."""
+        mm = self.__dict__["_molmap"]
+        m, C = int(mm.size(0)), self.map_size
+        sb = self.__dict__.get("_halo_bufs")
+        if sb is None or sb.dtype != mm.dtype or sb.device != mm.device or sb.numel() != 4 * m * C:
+            sb = torch.empty(4 * m * C, dtype=mm.dtype, device=mm.device)
+            self.__dict__["_halo_bufs"] = sb
+        return sb
+
+    def _rccl_comm(self):
+        """The native RCCL communicator of the main stream (None: exchanges go through torch)."""
+        d = self.__dict__
+        c = d.get("_comm")
+        return c if isinstance(c, RcclComm) and not d.get("_side_active") else None
+
     def _do_exchange_map_halo(self) -> None:
         """Refresh the molecule-map halo rows from the neighbours' boundary rows (raw buffer: a
         pending degradation factor is identical on every rank and applied by the stencil). One pack
@@ -259,10 +275,7 @@ class DistributedWorld(World):
             return
         mm = self.__dict__["_molmap"]
         m, C = int(mm.size(0)), self.map_size
-        sb = self.__dict__.get("_halo_bufs")
-        if sb is None or sb.dtype != mm.dtype or sb.device != mm.device or sb.numel() != 4 * m * C:
-            sb = torch.empty(4 * m * C, dtype=mm.dtype, device=mm.device)
-            self.__dict__["_halo_bufs"] = sb
+        sb = self._halo_buffers()
         s_up, s_dn, r_dn, r_up = (sb[i * m * C : (i + 1) * m * C] for i in range(4))
         strip.halo_pack(self, s_up, s_dn)
         self._exchange(s_up, s_dn, r_dn, r_up)
@@ -1055,13 +1068,8 @@ class _BoundaryRecombination:
         R = H + 2
         idx_map = hip_ops._index_map(w, R * C, dev)
         hip_ops._ensure_world_layout(w)
-        _m().index_map(n, _p(w.cell_positions), C, _p(idx_map), False, st)
         lens = sc.get("xb_lens", 4 * (C + 1), torch.int32, dev)
-        mine_up, mine_dn, from_dn, from_up = (lens[i * (C + 1) : (i + 1) * (C + 1)] for i in range(4))
         own = sc.get("xb_own", 2 * C, torch.int32, dev)
-        _m().xb_prep(C, H, n, _p(w.cell_positions), _p(idx_map), _p(g.lens), int(g.width), _p(mine_up), _p(mine_dn),
-                     _p(own[:C]), _p(own[C:]), st)
-        w._exchange(mine_up, mine_dn, from_dn, from_up)
         nev = 5 * 2 * E + 4
         ev = sc.bufs.get("xb_ev")
         if ev is None or ev.numel() != nev or ev.device != dev:
@@ -1070,10 +1078,22 @@ class _BoundaryRecombination:
         slot = 4 + W
         sl = sc.get("xb_slots", 4 * E * slot, torch.uint8, dev)
         self.slots_dn, self.slots_up, self.recv_dn, self.recv_up = (sl[i * E * slot : (i + 1) * E * slot] for i in range(4))
-        _m().xb_events(C, E, W, float(p), int(kcap), self.seed_dn, self.seed_up, self.call, _p(mine_dn), _p(from_dn),
-                       _p(mine_up), _p(from_up), _p(own[:C]), _p(own[C:]), _p(g.data), int(g.width), _p(ev),
-                       _p(self.slots_dn), _p(self.slots_up), st)
-        w._exchange(self.slots_up, self.slots_dn, self.recv_dn, self.recv_up)
+        comm = w._active_comm()
+        if isinstance(comm, RcclComm):
+            # index map, lengths exchange, events, event-genome exchange: one native call (dist.hip)
+            _m().xb_begin(C, H, n, _p(w.cell_positions), _p(idx_map), _p(g.lens), _p(g.data), int(g.width), _p(lens),
+                          _p(own), E, W, float(p), int(kcap), self.seed_dn, self.seed_up, self.call, _p(ev), _p(sl),
+                          comm.handle, comm.up, comm.down, st)
+        else:
+            _m().index_map(n, _p(w.cell_positions), C, _p(idx_map), False, st)
+            mine_up, mine_dn, from_dn, from_up = (lens[i * (C + 1) : (i + 1) * (C + 1)] for i in range(4))
+            _m().xb_prep(C, H, n, _p(w.cell_positions), _p(idx_map), _p(g.lens), int(g.width), _p(mine_up),
+                         _p(mine_dn), _p(own[:C]), _p(own[C:]), st)
+            w._exchange(mine_up, mine_dn, from_dn, from_up)
+            _m().xb_events(C, E, W, float(p), int(kcap), self.seed_dn, self.seed_up, self.call, _p(mine_dn),
+                           _p(from_dn), _p(mine_up), _p(from_up), _p(own[:C]), _p(own[C:]), _p(g.data), int(g.width),
+                           _p(ev), _p(self.slots_dn), _p(self.slots_up), st)
+            w._exchange(self.slots_up, self.slots_dn, self.recv_dn, self.recv_up)
         self.parts = sc.get("xb_parts", 2 * E * (kcap + 2) * 3, torch.int32, dev)
         self.kcap = kcap
 

@@ -1,7 +1,8 @@
 """Build a variant of the _hip module for in-process A/B (scripts/ab_so.py): the in-tree objects of
 every HIP source except one, plus that source replaced by a variant file, linked into OUT.
 
-usage: python scripts/build_variant.py <variant.hip> <replaced source name, e.g. kinetics.hip> <OUT.so>"""
+usage: python scripts/build_variant.py <variant.hip> <replaced source name, e.g. kinetics.hip> <OUT.so>
+VARIANT_CFLAGS: extra compiler flags for the variant source only."""
 import os
 import shutil
 import subprocess
@@ -27,7 +28,8 @@ def main():
         src = Path(td) / name
         shutil.copy(variant, src)
         obj = Path(td) / "variant.o"
-        subprocess.run([hipcc, *cflags, "-c", str(src), "-o", str(obj)], check=True)
+        extra = os.environ.get("VARIANT_CFLAGS", "").split()  # e.g. -ffp-contract=fast (later flags win)
+        subprocess.run([hipcc, *cflags, *extra, "-c", str(src), "-o", str(obj)], check=True)
         objs = [str(objdir / (p.stem + ".o")) for p in sorted(hipdir.glob("*.hip")) if p.name != name]
         out.parent.mkdir(parents=True, exist_ok=True)
         subprocess.run([hipcc, "-shared", f"--offload-arch={build.ARCH}", *objs, str(obj), "-o", str(out)], check=True)

@@ -283,3 +283,44 @@ def _body_native_divide(rank, ws):
 
 def test_gpu_native_strip_divide_matches_python_protocol():
     run_ranks(_body_native_divide, 1, timeout=300, backend="nccl")
+
+
+def _body_native_xb(rank, ws):
+    """One rank over RCCL (virtual strips): the collective part of the strip-boundary recombination
+    as one native call (dist.hip xb_begin) gives the Python protocol's genomes exactly."""
+    import random
+
+    import magicsoup_amd as ms
+    from magicsoup_amd.parallel import DistributedWorld
+    from magicsoup_amd.parallel import dist_world as dwm
+    from tests.conftest import gen_genomes
+
+    ms.set_seed(12)
+    torch.manual_seed(12)
+    w = ms.World(chemistry=_chem(), map_size=64, seed=12, device="cpu")
+    w.spawn_cells(gen_genomes(1500, 300))
+    out = {}
+    real = dwm.RcclComm
+    for native in (True, False):
+        random.seed(77)
+        dw = DistributedWorld(chemistry=_chem(), map_size=64, seed=13, device="cuda", strips=True)
+        dw.adopt_maps(w)
+        dw.scatter_from(w, maps=False)
+        if not native:
+            dwm.RcclComm = type("NotRccl", (), {})  # the isinstance check fails: the Python exchanges
+        try:
+            for it in range(3):
+                ms.set_seed(40 + it)
+                dw.recombinate_cells(p=2e-3)
+            genomes = list(dw.cell_genomes)
+        finally:
+            dwm.RcclComm = real
+        out[native] = (genomes, dw.kinetics.N.cpu().clone())
+        dw.close()
+    assert out[True][0] == out[False][0]
+    assert torch.equal(out[True][1], out[False][1])
+    assert out[True][0] != list(w.cell_genomes)  # something recombined
+
+
+def test_gpu_native_boundary_recombination_matches_python_protocol():
+    run_ranks(_body_native_xb, 1, timeout=300, backend="nccl")
