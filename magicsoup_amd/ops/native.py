@@ -20,6 +20,18 @@ def _load(name: str, builder) -> object:
     with _lock:
         if name in _mods:
             return _mods[name]
+        override = os.environ.get("MS_HOST_SO") if name == "_host" else None
+        if override:
+            # an instrumented build of the host core (scripts/sanitize_host.sh: ASan + UBSan)
+            import importlib.util
+            import sys
+
+            spec = importlib.util.spec_from_file_location(f"magicsoup_amd.{name}", override)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            sys.modules[f"magicsoup_amd.{name}"] = mod
+            _mods[name] = mod
+            return mod
         try:
             mod = importlib.import_module(f"magicsoup_amd.{name}")
         except ImportError:
