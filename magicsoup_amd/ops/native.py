@@ -9,7 +9,9 @@ from __future__ import annotations
 
 import atexit
 import importlib
+import importlib.util
 import os
+import sys
 import threading
 
 _lock = threading.Lock()
@@ -23,9 +25,6 @@ def _load(name: str, builder) -> object:
         override = os.environ.get("MS_HOST_SO") if name == "_host" else None
         if override:
             # an instrumented build of the host core (scripts/sanitize_host.sh: ASan + UBSan)
-            import importlib.util
-            import sys
-
             spec = importlib.util.spec_from_file_location(f"magicsoup_amd.{name}", override)
             mod = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(mod)
