@@ -96,7 +96,9 @@ def random_genomes(k: int, size: int, device) -> tuple[torch.Tensor, torch.Tenso
     return rows, torch.full((k,), size, dtype=torch.int32, device=device)
 
 
-_CHEMOSTAT = {"divided": 0, "starved": 0, "steps": 0}  # running means of divisions / starvation deaths
+# running means of divisions / starvation deaths; "after_kill": the population after the previous
+# step's kill (its division count is known at the next step's start: n_cells - after_kill)
+_CHEMOSTAT = {"divided": 0, "starved": 0, "steps": 0, "after_kill": None}
 
 
 def _dilution_mask(n: int, k: int, device) -> torch.Tensor:
@@ -117,6 +119,14 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
 
     with ph("top_up"):
         n = world.n_cells
+        if _CHEMOSTAT["after_kill"] is not None:
+            # the previous step's divisions (issued without waiting for their count: the reference
+            # loop discards the pairs, and the count is long on the host by now)
+            d = max(0, n - _CHEMOSTAT["after_kill"])
+            _CHEMOSTAT["divided"] = (_CHEMOSTAT["divided"] + d) // 2 if _CHEMOSTAT["steps"] else d
+            _CHEMOSTAT["steps"] += 1
+            _CHEMOSTAT["after_kill"] = None
+            note("divided", d)
         if n < n_target:
             world.spawn_cells(random_genomes(n_target - n, genome_size, world.cell_molecules.device))
             note("spawned", n_target - n)
@@ -144,17 +154,14 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
             kill |= dilute
             note("diluted", excess)
         world.kill_cells(kill)
+        _CHEMOSTAT["after_kill"] = world.n_cells
         starved = max(0, n0 - world.n_cells - max(excess, 0))
         _CHEMOSTAT["starved"] = (_CHEMOSTAT["starved"] + starved) // 2 if _CHEMOSTAT["steps"] else starved
         note("killed", n0 - world.n_cells)
     with ph("replicate"):
         repl = world.cell_molecules[:, atp] > 5.0
         world.cell_molecules[:, atp] -= 4.0 * repl
-        parents, _ = world.divide_cells_t(repl)
-        d = int(parents.numel())
-        _CHEMOSTAT["divided"] = (_CHEMOSTAT["divided"] + d) // 2 if _CHEMOSTAT["steps"] else d
-        _CHEMOSTAT["steps"] += 1
-        note("divided", d)
+        world.divide_cells_t(repl, lazy=True)
     with ph("recombinate"):
         world.recombinate_cells()
     with ph("mutate"):
@@ -190,7 +197,7 @@ def _prime_rare_paths(chem, device, mdt, genome_size: int) -> None:
     step(w, 300, genome_size, atp)
     torch.cuda.synchronize()
     del w
-    _CHEMOSTAT.update(divided=0, starved=0, steps=0)
+    _CHEMOSTAT.update(divided=0, starved=0, steps=0, after_kill=None)
 
 
 def main():

@@ -538,7 +538,8 @@ class Kinetics:
         """Resolve pending device-pipeline updates of the owning world (no-op otherwise)."""
         ref = self.__dict__.get("_owner")
         w = ref() if ref is not None else None
-        if w is not None and (w.__dict__.get("_gp_state") or w.__dict__.get("_deferred")):
+        if w is not None and (w.__dict__.get("_gp_state") or w.__dict__.get("_deferred")
+                              or w.__dict__.get("_count_pending") is not None):
             w._reconcile()
 
     def _zero_row(self) -> torch.Tensor:

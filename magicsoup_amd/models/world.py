@@ -51,6 +51,10 @@ _PIPELINE_SAFE_OPS = frozenset({"mutate_cells", "recombinate_cells", "diffuse_mo
 # neither read nor write the molecule map (degrade_molecules: once, see hip_ops.spec_diffuse_issue)
 _SPEC_DIFF_SAFE_OPS = frozenset({"divide_cells", "mutate_cells", "recombinate_cells", "degrade_molecules",
                                  "diffuse_molecules", "increment_cell_lifetimes"})
+# ops that may run while the cell count of a division issued without a synchronisation
+# (divide_cells_t(lazy=True)) is still on its way to the host: they queue genome chains or only touch
+# the map / all capacity rows; diffuse_molecules adopts the count after its stencil launch
+_COUNT_SAFE_OPS = frozenset({"mutate_cells", "recombinate_cells", "degrade_molecules", "diffuse_molecules"})
 _CHECK_ENV = os.environ.get("MS_CHECK_INVARIANTS") == "1"
 _DEFER_ENV = os.environ.get("MS_DEFER_GENOME_OPS", "1")
 _FLUSH_EARLY = os.environ.get("MS_FLUSH_EARLY", "1") == "1"
@@ -80,6 +84,8 @@ def _op(name: str):
         @functools.wraps(fn)
         def wrapper(self, *args, **kwargs):
             d = self.__dict__
+            if d.get("_count_pending") is not None and name not in _COUNT_SAFE_OPS:
+                self._resolve_count()
             if d.get("_spec_diff") is not None and name not in _SPEC_DIFF_SAFE_OPS:
                 from magicsoup_amd.ops import hip_ops
 
@@ -347,6 +353,8 @@ class World:
         q = d.get("_deferred")
         if not q:
             return
+        if d.get("_count_pending") is not None:
+            self._resolve_count()  # (the chains are sized by the cell count)
         d["_deferred"] = []
         side = d.get("_side_stream")
         if side is None:
@@ -372,6 +380,8 @@ class World:
                 join(main, side_raw)
 
     def _reconcile(self) -> None:
+        if self.__dict__.get("_count_pending") is not None:
+            self._resolve_count()
         if self.__dict__.get("_deferred"):
             self._flush_deferred()
         self._join_side()
@@ -389,7 +399,7 @@ class World:
         d = self.__dict__
         cols = d.get("_cols")
         if cols is not None and name in cols:
-            if d.get("_spec") is not None:
+            if d.get("_spec") is not None or d.get("_count_pending") is not None:
                 self._reconcile()
             return cols[name].view(d["n_cells"])
         if name == "molecule_map" and "_molmap" in d:
@@ -469,7 +479,43 @@ class World:
     @property
     def cell_labels(self) -> StringColumn:
         """Labels ordered by cell index (a lazy ``list[str]`` view)."""
+        if self.__dict__.get("_count_pending") is not None:
+            self._resolve_count()
         return self._label_col
+
+    @property
+    def n_cells(self) -> int:
+        """Number of living cells (adopts a pending division count first, see :meth:`divide_cells_t`)."""
+        d = self.__dict__
+        if d.get("_count_pending") is not None:
+            self._resolve_count()
+        return d["n_cells"]
+
+    @n_cells.setter
+    def n_cells(self, n: int) -> None:
+        self.__dict__["n_cells"] = n
+
+    def _n_floor(self) -> int:
+        """A lower bound of the cell count that never waits for the device (a pending division only
+        adds cells)."""
+        d = self.__dict__
+        pend = d.get("_count_pending")
+        return pend[0] if pend is not None else d["n_cells"]
+
+    def _resolve_count(self) -> None:
+        """Adopt the winner count of a division issued with ``lazy=True``: wait for the event
+        recorded after its launches (not for work queued since, e.g. a diffusion stencil), read the
+        count from its pinned status slot and adopt the grown population."""
+        from magicsoup_amd.ops import hip_ops
+
+        n0, slot, ev = self.__dict__.pop("_count_pending")
+        if hip_ops._GUARD:
+            hip_ops._GUARD[0]()  # (communicators alive: a peer failure raises instead of hanging)
+        ev.synchronize()
+        k = int(hip_ops._m().status_read(slot)[0])
+        hip_ops.check_placement()
+        if k:
+            self._adopt_count(n0 + k)
 
     def _set_strings(self, arena: StringArena, strs: list[str]) -> None:
         arena.clear()
@@ -690,12 +736,19 @@ class World:
         return list(zip(parents.tolist(), children.tolist()))
 
     @_op("divide_cells")
-    def divide_cells_t(self, cell_idxs) -> tuple[torch.Tensor, torch.Tensor]:
-        """Tensor form of :meth:`divide_cells`: (parents, children) long tensors."""
+    def divide_cells_t(self, cell_idxs, lazy: bool = False) -> tuple[torch.Tensor, torch.Tensor] | None:
+        """Tensor form of :meth:`divide_cells`: (parents, children) long tensors.
+
+        ``lazy=True`` (a boolean GPU mask over all cells; the reference loop discards the pairs,
+        ``performance/run_simulation.py:91``): returns None and does not wait for the division. The
+        winner count travels to pinned memory and is adopted when the host next needs it -- reading
+        ``n_cells`` or a cell attribute, or any operation other than the genome ops, degradation
+        and diffusion, which are issued against the device state meanwhile (diffusion adopts it
+        after launching its stencil, by when the division has long finished on the device)."""
         empty = torch.zeros(0, dtype=torch.long, device=self.device)
         if (isinstance(cell_idxs, torch.Tensor) and cell_idxs.dtype == torch.bool and cell_idxs.is_cuda
                 and cell_idxs.numel() == self.n_cells and self.n_cells > 0):
-            return self._divide_mask_gpu(cell_idxs)
+            return self._divide_mask_gpu(cell_idxs, lazy=lazy)
         idxs = self._idx_tensor(cell_idxs)
         if idxs.numel() == 0:
             return empty, empty
@@ -754,7 +807,7 @@ class World:
             kd["_ncells"] += k
         return torch.arange(n0, n0 + k, device=self.device)
 
-    def _divide_mask_gpu(self, mask: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    def _divide_mask_gpu(self, mask: torch.Tensor, lazy: bool = False) -> tuple[torch.Tensor, torch.Tensor] | None:
         """Division over a GPU mask with one synchronisation at the very end: placement, winner
         compaction, the commit of the new rows and the genome / label / parameter-row clone are all
         issued against the device-side winner count (one native call, fast.hip fast_divide) into
@@ -767,6 +820,11 @@ class World:
         mask = mask.view(torch.uint8) if mask.dtype == torch.bool else mask.to(torch.uint8)
         seed, call = hip_ops._rng()
         slot = hip_ops._m().fast_divide(fw, n, mask.contiguous().data_ptr(), seed, call, hip_ops._stream())
+        if lazy:
+            from magicsoup_amd.ops.streams import NEvent
+
+            self.__dict__["_count_pending"] = (n, slot, NEvent().record())
+            return None
         k = hip_ops.wait_count(slot)
         hip_ops.check_placement()
         if k == 0:
@@ -1041,7 +1099,7 @@ class World:
     def diffuse_molecules(self):
         """One step of diffusion over the molecule map, then membrane permeation."""
         world_ops.diffuse(self)
-        if self.n_cells > 0:
+        if self.n_cells > 0:  # (adopts a pending division count: the stencil is queued already)
             world_ops.permeate(self)
         if self.__dict__.get("_deferred"):
             # the stencil is queued: issue the deferred genome chains now, so that they start next to
@@ -1063,7 +1121,7 @@ class World:
     def mutate_cells(self, cell_idxs: list[int] | None = None, p: float = 1e-6, p_indel: float = 0.4, p_del: float = 0.66):
         """Point mutations (substitutions and indels) with per-bp rate ``p``; proteomes of mutated
         cells are re-derived."""
-        if self.n_cells == 0:
+        if self._n_floor() == 0 and self.n_cells == 0:
             return
         if cell_idxs is None and self._defer_genome_op():
             self._defer(lambda: self._mutate_all(p, p_indel, p_del))
@@ -1094,7 +1152,7 @@ class World:
     def recombinate_cells(self, cell_idxs: list[int] | None = None, p: float = 1e-7):
         """Recombine the genomes of neighbouring cells (strand breaks with per-bp rate ``p`` and
         random re-joining); both genomes of every recombined pair are replaced."""
-        if self.n_cells < 2:
+        if self._n_floor() < 2 and self.n_cells < 2:
             return
         if cell_idxs is None and self._defer_genome_op():
             self._defer(lambda: self._recombinate_all(p))

@@ -634,7 +634,11 @@ def degrade(world) -> None:
     """Cells decay now; the map decay is deferred and fused into the next diffusion stencil
     (or applied by :func:`apply_pending_scale` on any other access to ``molecule_map``)."""
     f = _degrade_factors(world)
-    if world.n_cells > 0:
+    if world.__dict__.get("_count_pending") is not None:
+        # a division's count is still on its way to the host: every capacity row (the children
+        # are among them; rows past the population are dead and get overwritten before use)
+        world._cols["cell_molecules"].buf.mul_(f)
+    elif world.n_cells > 0:
         cm = world.cell_molecules
         cm.mul_(f)
     sd = world.__dict__.get("_spec_diff")

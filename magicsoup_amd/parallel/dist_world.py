@@ -414,15 +414,17 @@ class DistributedWorld(World):
 
     # ------------------------------------------------------------------ lifecycle overrides
     @_op("divide_cells")
-    def divide_cells_t(self, cell_idxs) -> tuple[torch.Tensor, torch.Tensor]:
+    def divide_cells_t(self, cell_idxs, lazy: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
         """Division (collective). Children landing in a neighbour's boundary row are created on
         that rank; the returned pairs cover local children only (counts in ``self.migrated``).
+        ``lazy`` is accepted for the World signature: the strip protocol synchronises once in the
+        middle anyway (the record sizes), so the pairs are always returned.
 
         Protocol (module docstring): boundary marks -> reservations -> placement rounds ->
         winners split by destination row + record headers exchanged -> one synchronisation ->
         child records exchanged and appended; exporting parents keep half their molecules."""
         if not self._strips:
-            return super().divide_cells_t(cell_idxs)
+            return super().divide_cells_t(cell_idxs, lazy=lazy)
         from magicsoup_amd.ops.hip_ops import _scratch
 
         dev = self.device

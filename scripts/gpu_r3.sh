@@ -60,6 +60,7 @@ for s in "$@"; do case "$s" in
   cpvc) MS_PROF_LINES=90 MS_VIRTUAL_STRIPS=1 run cprofile_proxy8_virtual_cum 300 python scripts/step_cprofile.py 1448 6250 100 cumulative ;;
   cpvn) MS_PROF_LINES=60 MS_VIRTUAL_STRIPS=1 run cprofile_proxy8_virtual_ncalls 300 python scripts/step_cprofile.py 1448 6250 100 ncalls ;;
   cpp) run cprofile_proxy8 300 python scripts/step_cprofile.py 1448 6250 100 ;;
+  cppc) MS_PROF_LINES=90 run cprofile_proxy8_cum 300 python scripts/step_cprofile.py 1448 6250 100 cumulative ;;
   wide) run wide_c4096_50k_64x256 300 python bench.py --preset wide ;;
   m1b) run m1_bench 600 python bench.py --preset m1 --steps 60 --warmup 10 --step-times ;;
   tproxy) trace tproxy 39 --map-size 1448 --cells 6250 --steps 40 --warmup 20 ;;

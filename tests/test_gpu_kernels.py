@@ -920,3 +920,58 @@ def test_parameter_rows_follow_genomes_through_bench_steps(monkeypatch, recycle)
         # padding values depend on history (a widened layout is zero-filled, a build writes the
         # reference's padding values, as in the reference): compare the real proteins
         assert torch.equal(ta[real], tb[real]), name
+
+
+@pytest.mark.parametrize("probe", [None, "n_cells", "cell_positions", "cell_genomes", "kinetics"])
+def test_lazy_division_matches_synchronous_division(probe):
+    """divide_cells_t(mask, lazy=True) (the bench loop: the reference discards the pairs) leaves the
+    winner count pending; the genome ops and degradation are issued against the device state, the
+    diffusion adopts the count after its stencil launch, and any earlier read (``probe``) adopts it
+    at once. The world evolves bit for bit as with the synchronous division."""
+    base = _world("cuda", map_size=64, n=900, s=400, seed=7)
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+
+    def run(lazy: bool):
+        w = copy.deepcopy(base)
+        ms.set_seed(3)
+        torch.manual_seed(3)
+        sizes = []
+        for _ in range(6):
+            w.enzymatic_activity()
+            w.kill_cells(w.cell_molecules[:, atp] < 1.0)
+            repl = w.cell_molecules[:, atp] > 5.0
+            w.cell_molecules[:, atp] -= 4.0 * repl
+            n_before = w.n_cells
+            out = w.divide_cells_t(repl, lazy=lazy)
+            if lazy:
+                assert out is None and w.__dict__.get("_count_pending") is not None
+                if probe == "n_cells":
+                    assert w.n_cells >= n_before
+                elif probe == "cell_positions":
+                    assert w.cell_positions.size(0) == w.n_cells
+                elif probe == "cell_genomes":
+                    assert len(w.cell_genomes) == w.n_cells
+                elif probe == "kinetics":
+                    assert w.kinetics.Vmax.size(0) == w.n_cells
+                if probe is not None:
+                    assert w.__dict__.get("_count_pending") is None
+            w.recombinate_cells(p=1e-4)
+            w.mutate_cells(p=1e-3)
+            w.degrade_molecules()
+            if lazy and probe is None:
+                assert w.__dict__.get("_count_pending") is not None  # nothing so far needed the count
+            w.diffuse_molecules()
+            assert w.__dict__.get("_count_pending") is None
+            w.increment_cell_lifetimes()
+            sizes.append(w.n_cells)
+        torch.cuda.synchronize()
+        state = {k: getattr(w, k).clone() for k in ("cell_molecules", "cell_positions", "cell_lifetimes",
+                                                     "cell_divisions", "molecule_map", "cell_map")}
+        state["Vmax"] = w.kinetics.Vmax.clone()
+        return sizes, list(w.cell_genomes), state
+
+    s0, g0, st0 = run(False)
+    s1, g1, st1 = run(True)
+    assert s0 == s1 and g0 == g1
+    for k in st0:
+        assert torch.equal(st0[k], st1[k]), k
