@@ -133,6 +133,61 @@ __device__ __forceinline__ void ld8<_Float16>(const _Float16* p, float v[8]) {
   for (int j = 0; j < 8; ++j) v[j] = (float)q[j];
 }
 
+// Raw bits of 8 consecutive values (fp32: two 16 B words, bf16 / fp16: one), loaded without
+// converting: a prefetched row's load stays in flight until the row is used (a conversion right
+// after the load would wait for it there)
+template <class T>
+struct Bits8 {
+  uint4 q[sizeof(T) == 4 ? 2 : 1];
+};
+template <class T>
+__device__ __forceinline__ void ld8_bits(const T* p, Bits8<T>& r) {
+  const uint4* w = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(r.q) / sizeof(uint4)); ++i) r.q[i] = w[i];
+}
+template <class T>
+__device__ __forceinline__ void zero8_bits(Bits8<T>& r) {
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(r.q) / sizeof(uint4)); ++i) r.q[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+template <class T>
+__device__ __forceinline__ void cvt8(const Bits8<T>& r, float v[8]);
+template <>
+__device__ __forceinline__ void cvt8<float>(const Bits8<float>& r, float v[8]) {
+  const uint32_t w[8] = {r.q[0].x, r.q[0].y, r.q[0].z, r.q[0].w, r.q[1].x, r.q[1].y, r.q[1].z, r.q[1].w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = __uint_as_float(w[j]);
+}
+template <>
+__device__ __forceinline__ void cvt8<bf16_t>(const Bits8<bf16_t>& r, float v[8]) {
+  const uint32_t w[4] = {r.q[0].x, r.q[0].y, r.q[0].z, r.q[0].w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = __uint_as_float(w[j] << 16);
+    v[2 * j + 1] = __uint_as_float(w[j] & 0xFFFF0000u);
+  }
+}
+template <>
+__device__ __forceinline__ void cvt8<_Float16>(const Bits8<_Float16>& r, float v[8]) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  const h8 q = __builtin_bit_cast(h8, r.q[0]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)q[j];
+}
+// one value as raw bits (zero-extended) and back
+template <class T>
+__device__ __forceinline__ uint32_t ld_bits(const T* p) {
+  if constexpr (sizeof(T) == 4) return *reinterpret_cast<const uint32_t*>(p);
+  else return *reinterpret_cast<const uint16_t*>(p);
+}
+template <class T>
+__device__ __forceinline__ float from_bits(uint32_t u) {
+  if constexpr (sizeof(T) == 4) return __uint_as_float(u);
+  else if constexpr (__is_same(T, bf16_t)) return __uint_as_float(u << 16);
+  else return (float)__builtin_bit_cast(_Float16, (uint16_t)u);
+}
+
 template <class T>
 __device__ __forceinline__ void st8_stream(T* p, const float v[8]);
 template <>

@@ -120,7 +120,39 @@ __global__ void __launch_bounds__(64 * kWaves) diffuse_stencil_kernel(const T* _
 // (deferred genome chains, World._flush_deferred) start at once instead of waiting for stencil
 // workgroups to retire (set_stencil_blocks).
 constexpr int kVBand = 32;
-template <class T>
+
+// The rows of a wave's band: row_step(o, raw row o + 1) for o in [o0, o1); `first` holds raw row
+// o0 + 1 on entry. PF = 0: one raw row ahead, fetched into `spare` under a branch and copied (the
+// register copy waits for the loads at the end of the same row). PF >= 1: PF rows ahead in a ring of
+// PF + 1 raw buffers, unrolled by the ring size so every buffer is a fixed register set: a row's
+// loads are only waited for by the step that uses them, PF steps later. Rows past the band are
+// clamped to o1 (the halo row below it, already the last row the PF = 0 loop loads).
+template <int PF, class Raw, class Fetch, class Step>
+__device__ __forceinline__ void band_loop(int o0, int o1, Raw& first, Raw& spare, Fetch&& fetch, Step&& row_step) {
+  if constexpr (PF == 0) {
+    for (int o = o0; o < o1; ++o) {
+      if (o + 2 <= o1) fetch(o + 2, spare);
+      row_step(o, first);
+      first = spare;
+    }
+  } else {
+    constexpr int NB = PF + 1;
+    Raw ring[NB];
+    ring[0] = first;
+#pragma unroll
+    for (int d = 1; d < PF; ++d) fetch(min(o0 + 1 + d, o1), ring[d]);
+    for (int o = o0; o < o1; o += NB) {
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        if (o + u < o1) {
+          fetch(min(o + u + 1 + PF, o1), ring[(u + PF) % NB]);
+          row_step(o + u, ring[u]);
+        }
+      }
+    }
+  }
+}
+template <class T, int PF>
 __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restrict__ in, T* __restrict__ out,
                                                                const float* __restrict__ wa,
                                                                const float* __restrict__ wb,
@@ -150,23 +182,32 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
     if (x >= g.R) x -= g.R;
     return x;
   };
-  struct Raw {
-    float v[4], el, er;
+  struct Raw {  // raw bits: converted in finish(), so a prefetched row's loads stay in flight
+    uint32_t v[4], el, er;
   };
   auto fetch = [&](int o, Raw& r) {
     const size_t base = (size_t)row_of(o) * g.C;
-    if (col) ld4(src + base + y0, r.v);
-    else r.v[0] = r.v[1] = r.v[2] = r.v[3] = 0.0f;
-    r.el = need_l ? ld(src + base + yl) : 0.0f;
-    r.er = need_r ? ld(src + base + yr) : 0.0f;
+    if (col) {
+      if constexpr (sizeof(T) == 4) {
+        const uint4 q = *reinterpret_cast<const uint4*>(src + base + y0);
+        r.v[0] = q.x, r.v[1] = q.y, r.v[2] = q.z, r.v[3] = q.w;
+      } else {
+        const uint2 q = *reinterpret_cast<const uint2*>(src + base + y0);
+        r.v[0] = q.x & 0xFFFFu, r.v[1] = q.x >> 16, r.v[2] = q.y & 0xFFFFu, r.v[3] = q.y >> 16;
+      }
+    } else {
+      r.v[0] = r.v[1] = r.v[2] = r.v[3] = 0u;
+    }
+    r.el = need_l ? ld_bits(src + base + yl) : 0u;
+    r.er = need_r ? ld_bits(src + base + yr) : 0u;
   };
   // scaled values of the row plus the left neighbour of column y0 and the right one of y0 + 3
   auto finish = [&](const Raw& r, float v[4], float& L, float& Rn) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = corr_in(r.v[j], corr, mol) * sc;
+    for (int j = 0; j < 4; ++j) v[j] = corr_in(from_bits<T>(r.v[j]), corr, mol) * sc;
     const float up = __shfl_up(v[3], 1), dn = __shfl_down(v[0], 1);
-    L = need_l ? corr_in(r.el, corr, mol) * sc : up;
-    Rn = need_r ? corr_in(r.er, corr, mol) * sc : dn;
+    L = need_l ? corr_in(from_bits<T>(r.el), corr, mol) * sc : up;
+    Rn = need_r ? corr_in(from_bits<T>(r.er), corr, mol) * sc : dn;
   };
   auto hsum = [](const float v[4], float L, float Rn, float h[4]) {
     h[0] = L + v[0] + v[1];
@@ -186,10 +227,10 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
     finish(rc, vc, Lc, Rc);
     hsum(vp, Lp, Rp, hp);
     hsum(vc, Lc, Rc, hc);
-    for (int o = o0; o < o1; ++o) {
-      if (o + 2 <= o1) fetch(o + 2, rn2);  // row o + 2 (at most the halo row below the band)
+    // row o from rows o - 1, o (in registers) and the raw row o + 1 (see band_loop)
+    auto row_step = [&](int o, const Raw& r_next) {
       float vn[4], Ln, Rn, hn[4];
-      finish(rn, vn, Ln, Rn);
+      finish(r_next, vn, Ln, Rn);
       hsum(vn, Ln, Rn, hn);
       float res[4];
       const float lft[4] = {Lc, vc[0], vc[1], vc[2]}, rgt[4] = {vc[1], vc[2], vc[3], Rc};
@@ -208,8 +249,8 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
       }
       Lc = Ln;
       Rc = Rn;
-      rn = rn2;
-    }
+    };
+    band_loop<PF>(o0, o1, rn, rn2, fetch, row_step);
   }
   before = wave_sum_d(before);
   after = wave_sum_d(after);
@@ -234,7 +275,7 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
 // 4-column kernel reached ~5 TB/s on fp32 and stayed issue-bound on the 2-byte types. Same tiling
 // (4 waves = 4 consecutive 32-row bands of one column strip), same one-row-ahead prefetch, same
 // fp64 partials (the 8 values of a row are summed in fp32 first, as pairs of 4).
-template <class T>
+template <class T, int PF>
 __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restrict__ in, T* __restrict__ out,
                                                                const float* __restrict__ wa,
                                                                const float* __restrict__ wb,
@@ -266,27 +307,25 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
       if (x >= g.R) x -= g.R;
       return x;
     };
-    struct Raw {
-      float v[8], el, er;
+    struct Raw {  // raw bits: converted in finish(), so a prefetched row's loads stay in flight
+      Bits8<T> v;
+      uint32_t el, er;
     };
     auto fetch = [&](int o, Raw& r) {
       const size_t base = (size_t)row_of(o) * g.C;
-      if (col) {
-        ld8(src + base + y0, r.v);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) r.v[j] = 0.0f;
-      }
-      r.el = need_l ? ld(src + base + yl) : 0.0f;
-      r.er = need_r ? ld(src + base + yr) : 0.0f;
+      if (col) ld8_bits(src + base + y0, r.v);
+      else zero8_bits(r.v);
+      r.el = need_l ? ld_bits(src + base + yl) : 0u;
+      r.er = need_r ? ld_bits(src + base + yr) : 0u;
     };
     auto cin = [&](float raw) { return (has_c ? fmaxf(raw + cm, 0.0f) : raw) * sc; };
     auto finish = [&](const Raw& r, float v[8], float& L, float& Rn) {
+      cvt8(r.v, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = cin(r.v[j]);
+      for (int j = 0; j < 8; ++j) v[j] = cin(v[j]);
       const float up = __shfl_up(v[7], 1), dn = __shfl_down(v[0], 1);
-      L = need_l ? cin(r.el) : up;
-      Rn = need_r ? cin(r.er) : dn;
+      L = need_l ? cin(from_bits<T>(r.el)) : up;
+      Rn = need_r ? cin(from_bits<T>(r.er)) : dn;
     };
     auto hsum = [](const float v[8], float L, float Rn, float h[8]) {
       h[0] = L + v[0] + v[1];
@@ -306,10 +345,10 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
       finish(rc, vc, Lc, Rc);
       hsum(vp, Lp, Rp, hp);
       hsum(vc, Lc, Rc, hc);
-      for (int o = o0; o < o1; ++o) {
-        if (o + 2 <= o1) fetch(o + 2, rn2);  // row o + 2 (at most the halo row below the band)
+      // (as diffuse_stencil4_kernel, see band_loop)
+      auto row_step = [&](int o, const Raw& r_next) {
         float vn[8], Ln, Rn, hn[8];
-        finish(rn, vn, Ln, Rn);
+        finish(r_next, vn, Ln, Rn);
         hsum(vn, Ln, Rn, hn);
         float res[8];
 #pragma unroll
@@ -330,8 +369,8 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
         }
         Lc = Ln;
         Rc = Rn;
-        rn = rn2;
-      }
+      };
+      band_loop<PF>(o0, o1, rn, rn2, fetch, row_step);
     }
     before = wave_sum_d(before);
     after = wave_sum_d(after);
@@ -534,6 +573,22 @@ static bool use_vec8(int C, int dtype) {
 }
 static bool use_vec4(int C) { return (g_stencil_vec == 0 || g_stencil_vec >= 4) && C % 4 == 0; }
 
+// rows in flight ahead of the vector stencils' current row (band_loop; set_stencil_prefetch, -1 =
+// auto = 0). Measured at 4096^2 x 14 (profiles/r3/stencil_pf/): the one-row loop is fastest for
+// every map type once rows stay raw bits until used (2-byte maps: 0.27-0.31 -> 0.217-0.225 ms; their
+// conversion right after the loads had waited for them); the PF-deep rings (1-3) are slower.
+static int g_stencil_pf = -1;
+void set_stencil_prefetch(int pf) { g_stencil_pf = pf < -1 ? -1 : (pf > 3 ? 3 : pf); }
+static int stencil_pf(int) { return g_stencil_pf >= 0 ? g_stencil_pf : 0; }
+// launch LAUNCH with the compile-time prefetch distance PF (and the map type T of MS_MAP_DISPATCH)
+#define MS_PF_DISPATCH(pf, LAUNCH)                                  \
+  switch (pf) {                                                     \
+    case 0: { constexpr int PF = 0; LAUNCH; } break;                \
+    case 1: { constexpr int PF = 1; LAUNCH; } break;                \
+    case 2: { constexpr int PF = 2; LAUNCH; } break;                \
+    default: { constexpr int PF = 3; LAUNCH; } break;               \
+  }
+
 // Blocks of the vector stencil launch (0: one per tile). 256 CUs x 4 workgroups (4 waves per SIMD)
 // still reach the stencil's full HBM rate and leave 3 of the 7 slots a CU holds at its register use
 // to the side stream. Kernel traces of the flagship step (scripts/gpu_trace_step.sh): stencil 378 /
@@ -566,17 +621,17 @@ void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_
   if (v8) {
     const int ntiles = (int)(grid.x * grid.y * grid.z);
     const int blocks = g_stencil_blocks > 0 ? std::min(ntiles, g_stencil_blocks) : ntiles;
-    MS_MAP_DISPATCH(dtype, (diffuse_stencil8_kernel<T><<<blocks, 256, 0, st_>>>(
+    MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), (diffuse_stencil8_kernel<T, PF><<<blocks, 256, 0, st_>>>(
                                P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
                                corr ? P_<float>(corr) : nullptr, g, P_<double>(partials), (int)grid.x, (int)grid.y,
-                               ntiles)));
+                               ntiles))));
   } else if (v4) {
     const int ntiles = (int)(grid.x * grid.y * grid.z);
     const int blocks = g_stencil_blocks > 0 ? std::min(ntiles, g_stencil_blocks) : ntiles;
-    MS_MAP_DISPATCH(dtype, (diffuse_stencil4_kernel<T><<<blocks, 256, 0, st_>>>(
+    MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), (diffuse_stencil4_kernel<T, PF><<<blocks, 256, 0, st_>>>(
                                P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
                                corr ? P_<float>(corr) : nullptr, g, P_<double>(partials), (int)grid.x, (int)grid.y,
-                               ntiles)));
+                               ntiles))));
   } else {
     MS_MAP_DISPATCH(dtype, (diffuse_stencil_kernel<T><<<grid, 64 * kWaves, 0, st_>>>(
                                P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
@@ -604,13 +659,13 @@ void diffuse_boundary(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, ui
     const MGeom g = mgeom(R, C, row, row + 1, 0);
     double* part = P_<double>(partials) + (size_t)b * tiles * 2;
     if (v8) {
-      MS_MAP_DISPATCH(dtype, (diffuse_stencil8_kernel<T><<<tiles, 256, 0, st_>>>(
+      MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), (diffuse_stencil8_kernel<T, PF><<<tiles, 256, 0, st_>>>(
                                  P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
-                                 corr ? P_<float>(corr) : nullptr, g, part, gx, 1, tiles)));
+                                 corr ? P_<float>(corr) : nullptr, g, part, gx, 1, tiles))));
     } else if (v4) {
-      MS_MAP_DISPATCH(dtype, (diffuse_stencil4_kernel<T><<<tiles, 256, 0, st_>>>(
+      MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), (diffuse_stencil4_kernel<T, PF><<<tiles, 256, 0, st_>>>(
                                  P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
-                                 corr ? P_<float>(corr) : nullptr, g, part, gx, 1, tiles)));
+                                 corr ? P_<float>(corr) : nullptr, g, part, gx, 1, tiles))));
     } else {
       MS_MAP_DISPATCH(dtype, (diffuse_stencil_kernel<T><<<dim3(gx, 1, m), 64 * kWaves, 0, st_>>>(
                                  P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,

@@ -18,16 +18,20 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--vec", type=int, nargs="*", default=[0], help="stencil variants (columns per lane, 0 auto) to A/B")
     ap.add_argument("--blocks", type=int, nargs="*", default=[1024], help="stencil grid sizes (0: one block per tile)")
+    ap.add_argument("--pf", type=int, nargs="*", default=[-1], help="rows loaded ahead by the vector stencils (-1 auto)")
     a = ap.parse_args()
     from magicsoup_amd.ops import native
 
     for vec in a.vec:
         for blocks in a.blocks:
-            native.hip().set_stencil_vec(vec)
-            native.hip().set_stencil_blocks(blocks)
-            run(a, f"vec{vec}_blocks{blocks}")
+            for pf in a.pf:
+                native.hip().set_stencil_vec(vec)
+                native.hip().set_stencil_blocks(blocks)
+                native.hip().set_stencil_prefetch(pf)
+                run(a, f"vec{vec}_blocks{blocks}" + (f"_pf{pf}" if pf >= 0 else ""))
     native.hip().set_stencil_vec(0)
     native.hip().set_stencil_blocks(1024)
+    native.hip().set_stencil_prefetch(-1)
 
 
 def run(a, tag):

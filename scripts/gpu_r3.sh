@@ -55,6 +55,8 @@ for s in "$@"; do case "$s" in
   hsp) run host_split_proxy8 300 python scripts/host_split.py 1448 6250 60 ;;
   hsn) MS_NATIVE_TIMES=1 MS_VIRTUAL_STRIPS=1 run host_native_proxy8_virtual 300 python scripts/host_split.py 1448 6250 60 ;;
   hsnp) MS_NATIVE_TIMES=1 run host_native_proxy8 300 python scripts/host_split.py 1448 6250 60 ;;
+  hspy) MS_PY_TIMES=1 MS_NATIVE_TIMES=1 run host_py_proxy8 300 python scripts/host_split.py 1448 6250 60 ;;
+  hspyv) MS_PY_TIMES=1 MS_NATIVE_TIMES=1 MS_VIRTUAL_STRIPS=1 run host_py_proxy8_virtual 300 python scripts/host_split.py 1448 6250 60 ;;
   hsf) run host_split_flagship 300 python scripts/host_split.py 4096 50000 40 ;;
   cpv) MS_VIRTUAL_STRIPS=1 run cprofile_proxy8_virtual 300 python scripts/step_cprofile.py 1448 6250 100 ;;
   cpvc) MS_PROF_LINES=90 MS_VIRTUAL_STRIPS=1 run cprofile_proxy8_virtual_cum 300 python scripts/step_cprofile.py 1448 6250 100 cumulative ;;
@@ -68,6 +70,7 @@ for s in "$@"; do case "$s" in
   tflag) trace tflag 19 --steps 20 --warmup 20 ;;
   tenv) timeout -k 10 120 rocprofv3 --kernel-trace -d $O/tenv -o run --output-format csv -- python -c "import os; print(sorted(k for k in os.environ if 'ROC' in k))" > $O/tenv.log 2>&1; echo "   rc=$?" ;;
   dbench) run diffuse_bench 300 python scripts/diffuse_bench.py --vec 4 8 --blocks 1024 0 2048 ;;
+  dbpf) run diffuse_bench_pf 300 python scripts/diffuse_bench.py --vec 4 8 --blocks 1024 2048 --pf 0 1 2 3 ;;
   dtests) run dtests 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "diffusion or reduced_precision or permeation" ;;
   tc64) trace tc64 9 --preset wide --steps 10 --warmup 5 ;;
   tm1) trace tm1 19 --preset m1 --steps 20 --warmup 10 ;;

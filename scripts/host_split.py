@@ -95,6 +95,48 @@ if os.environ.get("MS_NATIVE_TIMES") == "1":
 
     native._mods["_hip"] = _Timed(native.hip())
 
+# MS_PY_TIMES=1: inclusive host time of selected Python helpers (nested calls counted in each)
+py_t = collections.defaultdict(float)
+py_n = collections.defaultdict(int)
+
+
+def _timed_py(f, name):
+    def w(*a, **k):
+        t0 = time.perf_counter()
+        try:
+            return f(*a, **k)
+        finally:
+            py_t[name] += time.perf_counter() - t0
+            py_n[name] += 1
+    return w
+
+
+if os.environ.get("MS_PY_TIMES") == "1":
+    from magicsoup_amd.models import kinetics as kin_mod
+    from magicsoup_amd.models import world as world_mod
+    from magicsoup_amd.ops import genome_pipeline, streams, world_ops
+
+    targets = [
+        (genome_pipeline, ["recombinate_all", "point_mutations", "_begin", "_kin_desc", "_arena_desc", "_gen_desc",
+                           "_blob", "_record", "reconcile", "_resolve"]),
+        (hip_ops, ["diffuse", "permeate", "enzymatic_activity", "_launch_integrate", "degrade", "neighbor_slot_args",
+                   "map_for_pixels", "_rng", "_check_overflow", "cell_state_buffer"]),
+        (world_ops, ["diffuse", "permeate", "enzymatic_activity", "fused_activity", "degrade"]),
+        (world_mod.World, ["_flush_deferred", "_reconcile", "_fast_world", "_adopt_count", "_defer", "_resolve_count",
+                           "_divide_mask_gpu", "_watch_genome_width", "_join_side", "_defer_genome_op"]),
+        (kin_mod.Kinetics, ["_kernel_params", "_row_limit", "_reserve_rows", "_enter_slot_mode", "_slot_tensor",
+                            "_sync", "_pack_ok"]),
+        (streams.NEvent, ["record", "wait", "synchronize", "__init__"]),
+        (streams, ["join"]),
+    ]
+    for obj, names in targets:
+        for nm in names:
+            f = obj.__dict__.get(nm) if isinstance(obj, type) else getattr(obj, nm, None)
+            if f is None:
+                continue
+            label = f"{getattr(obj, '__name__', '?').split('.')[-1]}.{nm}"
+            setattr(obj, nm, _timed_py(f, label))
+
 virtual = os.environ.get("MS_VIRTUAL_STRIPS") == "1"
 if virtual:
     import torch.distributed as dist
@@ -118,7 +160,7 @@ atp = CHEMISTRY.molname_2_idx["ATP"]
 for _ in range(20):
     bench.step(w, N, 500, atp)
 torch.cuda.synchronize()
-for d in (busy, blocked, calls, native_t, native_n):
+for d in (busy, blocked, calls, native_t, native_n, py_t, py_n):
     d.clear()
 blk[0] = 0.0
 t0 = time.perf_counter()
@@ -136,5 +178,9 @@ if native_t:
     print(f"  native entry points: {sum(native_t.values()) / steps * 1e6:.0f} us/step host in {sum(native_n.values()) / steps:.0f} calls")
     for name in sorted(native_t, key=lambda k: -native_t[k])[:40]:
         print(f"    {name:32s} {native_t[name] / steps * 1e6:8.1f} us {native_n[name] / steps:6.2f} calls")
+if py_t:
+    print("  python helpers (inclusive us/step, calls/step):")
+    for name in sorted(py_t, key=lambda k: -py_t[k]):
+        print(f"    {name:40s} {py_t[name] / steps * 1e6:8.1f} us {py_n[name] / steps:6.2f} calls")
 if virtual:
     w.close()
