@@ -1146,7 +1146,9 @@ __global__ void __launch_bounds__(kBlock) gather_bin_kernel(int c, int s, int m,
 }
 
 __device__ __forceinline__ int pack_word(int n, int nf, int nb, int av, int* overflow) {
-  if (n < -128 || n > 127 || nf < 0 || nf > 255 || nb < 0 || nb > 255 || av < -128 || av > 127) atomicOr(overflow, 1);
+  // (the flag lives in mapped host memory: a plain system-scope store, read by the host directly)
+  if (n < -128 || n > 127 || nf < 0 || nf > 255 || nb < 0 || nb > 255 || av < -128 || av > 127)
+    __hip_atomic_store(overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   return (n & 0xFF) | ((nf & 0xFF) << 8) | ((nb & 0xFF) << 16) | ((av & 0xFF) << 24);
 }
 

@@ -390,8 +390,11 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
 }
 
 // one block per molecule: totals[mol] = (sum before, sum after) over the owned rows
+// (corr_out: also the new per-species correction of a single-process map, (before - after) / n_pix,
+// which otherwise takes a diffuse_corr launch after the totals were all-reduced)
 __global__ void __launch_bounds__(256) diffuse_reduce_kernel(const double* partials, int tiles, double* totals,
-                                                             bool accumulate) {
+                                                             bool accumulate, float* corr_out = nullptr,
+                                                             double n_pix = 1.0) {
   __shared__ double sb[4], sa[4];
   const int mol = blockIdx.x;
   double b = 0.0, a = 0.0;
@@ -408,8 +411,10 @@ __global__ void __launch_bounds__(256) diffuse_reduce_kernel(const double* parti
   __syncthreads();
   if (threadIdx.x == 0) {
     const double b4 = sb[0] + sb[1] + sb[2] + sb[3], a4 = sa[0] + sa[1] + sa[2] + sa[3];
-    totals[2 * mol] = accumulate ? totals[2 * mol] + b4 : b4;
-    totals[2 * mol + 1] = accumulate ? totals[2 * mol + 1] + a4 : a4;
+    const double tb = accumulate ? totals[2 * mol] + b4 : b4, ta = accumulate ? totals[2 * mol + 1] + a4 : a4;
+    totals[2 * mol] = tb;
+    totals[2 * mol + 1] = ta;
+    if (corr_out) corr_out[mol] = (float)((tb - ta) / n_pix);  // (as diffuse_corr_kernel)
   }
 }
 
@@ -607,7 +612,7 @@ size_t diffuse_partials_len(int m, int C, int H) {
 
 void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
                      uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t totals, int dtype,
-                     int accumulate, uintptr_t stream) {
+                     int accumulate, uintptr_t stream, uintptr_t corr_out, double n_pix) {
   // rows [r_lo, r_hi) of the map; `accumulate`: add this launch's mass totals to `totals` (a strip's
   // stencil split into interior rows, issued while the halo rows are exchanged, and boundary rows)
   if (m <= 0 || r_hi <= r_lo) return;
@@ -639,7 +644,7 @@ void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_
   }
   MS_LAUNCH_CHECK();
   diffuse_reduce_kernel<<<m, 256, 0, st_>>>(P_<double>(partials), (int)(grid.x * grid.y), P_<double>(totals),
-                                            accumulate != 0);
+                                            accumulate != 0, corr_out ? P_<float>(corr_out) : nullptr, n_pix);
   MS_LAUNCH_CHECK();
 }
 
@@ -710,7 +715,8 @@ void diffuse_strip(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintp
   halo_pack(m, C, H, elem, map, s_up, s_dn, halo_stream);
   rccl_exchange(comm, up, down, s_up, plane_b, s_dn, plane_b, r_dn, plane_b, r_up, plane_b, halo_stream);
   halo_unpack(m, C, H, elem, map, r_up, r_dn, halo_stream);
-  diffuse_stencil(m, R, C, r_lo + 1, r_hi - 1, 0, map, tmp, wa, wb, scale, corr, partials, totals, dtype, 0, stream);
+  diffuse_stencil(m, R, C, r_lo + 1, r_hi - 1, 0, map, tmp, wa, wb, scale, corr, partials, totals, dtype, 0, stream, 0,
+                  1.0);
   stream_join(stream, halo_stream);
   diffuse_boundary(m, R, C, r_lo, r_hi, map, tmp, wa, wb, scale, corr, partials_b, totals, dtype, stream);
   rccl_allreduce(comm, totals, 2ll * m, 2 /* float64 */, 0 /* sum */, stream);

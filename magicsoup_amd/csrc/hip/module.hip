@@ -37,7 +37,7 @@ void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t se
 size_t diffuse_partials_len(int m, int C, int H);
 void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
                      uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t totals, int dtype, int accumulate,
-                     uintptr_t stream);
+                     uintptr_t stream, uintptr_t corr_out, double n_pix);
 void diffuse_corr(int m, uintptr_t totals, double n_pix, uintptr_t corr, uintptr_t stream);
 void diffuse_boundary(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t wa,
                       uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t totals, int dtype,
@@ -162,6 +162,8 @@ int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, ui
 void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
 int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t cnt, uintptr_t stream);
 std::tuple<long long, long long, long long, long long> status_read(int slot);
+std::pair<uintptr_t, uintptr_t> mapped_flag();
+int mapped_flag_read(uintptr_t host);
 std::tuple<long long, long long, long long, long long> stream_sync_read(int slot, uintptr_t stream);
 std::tuple<int, int, int> translate_stats(int n, uintptr_t counts, uintptr_t ndom, uintptr_t long_count, uintptr_t per,
                                           uintptr_t stream);
@@ -302,6 +304,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("count_to_host", &msd::count_to_host, "device {count, max} -> pinned ring slot (returns the slot)");
   m.def("status_write", &msd::status_write, "pipeline status -> pinned ring slot (returns the slot)");
   m.def("status_read", &msd::status_read);
+  m.def("mapped_flag", &msd::mapped_flag, "a zeroed int in mapped pinned memory: (host pointer, device pointer)");
+  m.def("mapped_flag_read", &msd::mapped_flag_read);
   m.def("stream_sync_read", &msd::stream_sync_read, "synchronise a stream, then read a pinned status slot");
   m.def("rccl_load", &msd::rccl_load, "resolve RCCL from a loaded librccl.so path; returns its version");
   m.def("rccl_unique_id", [](){ return py::bytes(msd::rccl_unique_id()); });

@@ -15,6 +15,9 @@
 #include <algorithm>
 #include <tuple>
 
+#include <cstring>
+#include <vector>
+
 #include "hip_common.h"
 
 namespace msd {
@@ -506,8 +509,31 @@ void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, ui
 #undef MS_SEL
 }
 
+// Mapped pinned int flags (kernels store into host memory; the host reads them without a copy or a
+// synchronisation): handed out from blocks of kFlagBlock, never reused, freed at exit.
+constexpr int kFlagBlock = 1024;
+static std::vector<int*> g_flag_blocks;
+static int g_flag_next = kFlagBlock;
+std::pair<uintptr_t, uintptr_t> mapped_flag() {
+  if (g_flag_next == kFlagBlock) {
+    int* h = nullptr;
+    MS_HIP_CHECK(hipHostMalloc((void**)&h, kFlagBlock * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(h, 0, kFlagBlock * sizeof(int));
+    g_flag_blocks.push_back(h);
+    g_flag_next = 0;
+  }
+  int* h = g_flag_blocks.back() + g_flag_next++;
+  int* d = nullptr;
+  MS_HIP_CHECK(hipHostGetDevicePointer((void**)&d, h, 0));
+  return {reinterpret_cast<uintptr_t>(h), reinterpret_cast<uintptr_t>(d)};
+}
+int mapped_flag_read(uintptr_t host) { return *reinterpret_cast<volatile const int*>(host); }
+
 // Free the process-wide pinned / device buffers of this file (exit path, see release_static).
 void release_select_buffers() {
+  for (int* h : g_flag_blocks) MS_HIP_CHECK(hipHostFree(h));
+  g_flag_blocks.clear();
+  g_flag_next = kFlagBlock;
   if (g_host) MS_HIP_CHECK(hipHostFree(g_host));
   g_host = g_host_dev = nullptr;
   if (g_tacc) MS_HIP_CHECK(hipFree(g_tacc));

@@ -168,23 +168,37 @@ def check_placement() -> None:
 _EQ = 4  # equilibrium-damping iterations per part
 
 
-def _overflow_flag(kin) -> torch.Tensor:
-    """Device flag set by the packed-parameter writers when a stoichiometry / Hill sum does not
-    fit in int8 (checked lazily, see _check_overflow)."""
+class _HostFlag:
+    """An int in mapped pinned memory (select.hip mapped_flag): kernels store into it, the host reads
+    it directly -- no copy launch, no synchronisation. ``data_ptr()`` is the device address."""
+
+    __slots__ = ("host", "dev")
+
+    def __init__(self):
+        self.host, self.dev = _m().mapped_flag()
+
+    def data_ptr(self) -> int:
+        return self.dev
+
+    def read(self) -> int:
+        return _m().mapped_flag_read(self.host)
+
+
+def _overflow_flag(kin) -> _HostFlag:
+    """Flag set by the packed-parameter writers when a stoichiometry / Hill sum does not fit in int8
+    (checked lazily, see _check_overflow)."""
     sc = _scratch(kin)
-    f = sc.bufs.get("pack_overflow")
+    f = getattr(sc, "overflow", None)
     if f is None:
-        f = sc.bufs["pack_overflow"] = torch.zeros(1, dtype=torch.int32, device=kin._store["Kmr"].device)
-        sc.bufs["pack_overflow_host"] = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        f = sc.overflow = _HostFlag()
     return f
 
 
 def _check_overflow(kin) -> None:
-    """Raise if a previous pack / build reported an int8 overflow (the host copy was queued at the
-    end of the previous integration, so this never waits on the device)."""
-    sc = _scratch(kin)
-    h = sc.bufs.get("pack_overflow_host")
-    if h is not None and int(h[0]) != 0:
+    """Raise if a pack / build reported an int8 overflow (a read of mapped host memory: it never
+    waits on the device; a build still running is seen at the next integration)."""
+    f = getattr(_scratch(kin), "overflow", None)
+    if f is not None and f.read() != 0:
         raise OverflowError("a protein's stoichiometry or allosteric exponent exceeds the int8 range of the "
                             "integrator's packed parameter layout (|N|, |A| <= 127, Nf, Nb <= 255)")
 
@@ -266,7 +280,6 @@ def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n
             flags_hook(masks[_EQ * part : _EQ * (part + 1)])
         if nparts:
             _m().integrate(*args, nparts, nparts, True, slot_p, _p(lists), mdt, _p(corr), 0, 0, 0, _stream())
-    sc.bufs["pack_overflow_host"].copy_(_overflow_flag(kin), non_blocking=True)
     return masks
 
 
@@ -463,20 +476,22 @@ def diffuse(world) -> None:
         with on_stream(hs):
             halo()
         _m().diffuse_stencil(m, R, C, r_lo + 1, r_hi - 1, wrap, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale),
-                             _p(corr), _p(partials), _p(totals), _mdt(mm), 0, main)
+                             _p(corr), _p(partials), _p(totals), _mdt(mm), 0, main, 0, 1.0)
         join(main, hs_raw)
         pb = sc.get("diff_partials_b", int(_m().diffuse_boundary_partials_len(m, C)), torch.float64, dev)
         _m().diffuse_boundary(m, R, C, r_lo, r_hi, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale), _p(corr), _p(pb),
                               _p(totals), _mdt(mm), _stream())
-    else:
-        _m().diffuse_stencil(m, R, C, r_lo, r_hi, wrap, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale), _p(corr),
-                             _p(partials), _p(totals), _mdt(mm), 0, _stream())
     reduce = getattr(world, "_allreduce_totals", None)
-    if reduce is not None:
-        reduce(totals)
     n_pix = float(getattr(world, "_n_pix_global", R * C if wrap else (r_hi - r_lo) * C))
     new_corr = sc.get("diff_corr", m, torch.float32, dev)
-    _m().diffuse_corr(m, _p(totals), n_pix, _p(new_corr), _stream())
+    if not split:
+        # a single map: the reduce launch also writes the new correction (no diffuse_corr launch)
+        _m().diffuse_stencil(m, R, C, r_lo, r_hi, wrap, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(scale), _p(corr),
+                             _p(partials), _p(totals), _mdt(mm), 0, _stream(), 0 if reduce else _p(new_corr), n_pix)
+    if reduce is not None:
+        reduce(totals)
+    if split or reduce is not None:
+        _m().diffuse_corr(m, _p(totals), n_pix, _p(new_corr), _stream())
     # swap: the stencil output is the map now; the old map buffer is the next scratch
     d["_molmap"] = tmp.view(mm.shape)
     sc.bufs["diff_tmp"] = mm.view(-1)
@@ -556,8 +571,7 @@ def spec_diffuse_issue(world) -> None:
     n_pix = float(R * C if wrap else (r_hi - r_lo) * C)
     with torch.cuda.stream(side):
         _m().diffuse_stencil(m, R, C, r_lo, r_hi, wrap, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(f), _p(corr),
-                             _p(partials), _p(totals), _mdt(mm), 0, _stream())
-        _m().diffuse_corr(m, _p(totals), n_pix, _p(new_corr), _stream())
+                             _p(partials), _p(totals), _mdt(mm), 0, _stream(), _p(new_corr), n_pix)
         ev = torch.cuda.Event()
         ev.record(side)
     d["_spec_diff"] = {"ev": ev, "mm": mm, "f": f, "corr": corr, "w": w, "tmp": tmp, "new_corr": new_corr,

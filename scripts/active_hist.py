@@ -19,5 +19,5 @@ for i in range(40):
     if i % 10 == 9:
         na = (w.kinetics.Vmax > 0).sum(1)
         h = torch.bincount(na.cpu(), minlength=1)
-        print(f"step {i+1}: P={w.kinetics.Vmax.size(1)} n={w.n_cells} >12: {int((na > 12).sum())} "
+        print(f"step {i+1}: P={w.kinetics.Vmax.size(1)} n={w.n_cells} >12: {int((na > 12).sum())} >16: {int((na > 16).sum())} "
               f"max={int(na.max())} mean={float(na.float().mean()):.1f} hist={h.tolist()[:40]}", flush=True)

@@ -26,6 +26,17 @@ trace() {  # trace <name> <steps-to-summarise> <bench args...>: kernel trace + -
   if fatal $rc; then echo "fatal rc=$rc in $name"; tail -30 "$O/$name.log"; exit $rc; fi
   python scripts/step_kernels.py $O/$name/run_kernel_trace.csv $k > $O/${name}_steps.txt 2>&1
 }
+htrace() {  # htrace <name> <steps> <bench args...>: HIP API + kernel trace, host / device timeline of a bench run
+  local name="$1" k="$2"; shift 2
+  echo "== htrace $name $(date +%T)"
+  timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace -d $O/$name -o run --output-format csv -- python bench.py "$@" \
+    > $O/$name.log 2>&1
+  local rc=$?
+  echo "   rc=$rc"
+  if fatal $rc; then echo "fatal rc=$rc in $name"; tail -30 "$O/$name.log"; exit $rc; fi
+  python scripts/host_timeline.py $O/$name $k > $O/${name}_host.txt 2>&1
+  rm -f $O/$name/run_hip_api_trace.csv
+}
 pmc() {  # pmc <name> <kernel regex> <counters> -- <bench args...>: one counter pass (no tracing domains)
   local name="$1" kr="$2" ctr="$3"; shift 4
   echo "== pmc $name $(date +%T)"
@@ -68,6 +79,8 @@ for s in "$@"; do case "$s" in
   tproxy) trace tproxy 39 --map-size 1448 --cells 6250 --steps 40 --warmup 20 ;;
   tvirt) MS_VIRTUAL_STRIPS=1 trace tvirt 39 --map-size 1448 --cells 6250 --steps 40 --warmup 20 ;;
   tflag) trace tflag 19 --steps 20 --warmup 20 ;;
+  htflag) htrace htflag 10 --steps 12 --warmup 20 ;;
+  htproxy) htrace htproxy 10 --map-size 1448 --cells 6250 --steps 12 --warmup 20 ;;
   tenv) timeout -k 10 120 rocprofv3 --kernel-trace -d $O/tenv -o run --output-format csv -- python -c "import os; print(sorted(k for k in os.environ if 'ROC' in k))" > $O/tenv.log 2>&1; echo "   rc=$?" ;;
   dbench) run diffuse_bench 300 python scripts/diffuse_bench.py --vec 4 8 --blocks 1024 0 2048 ;;
   dbpf) run diffuse_bench_pf 300 python scripts/diffuse_bench.py --vec 4 8 --blocks 1024 2048 --pf 0 1 2 3 ;;

@@ -975,3 +975,19 @@ def test_lazy_division_matches_synchronous_division(probe):
     assert s0 == s1 and g0 == g1
     for k in st0:
         assert torch.equal(st0[k], st1[k]), k
+
+
+def test_int8_overflow_of_packed_parameters_raises():
+    """A stoichiometry outside the integrator's packed int8 layout is reported through the mapped
+    host flag (no copy launch): the next integration raises instead of computing with a wrapped
+    coefficient."""
+    w = _world("cuda", map_size=32, n=60, s=500, seed=4)
+    w.enzymatic_activity()
+    kin = w.kinetics
+    N = kin.N.clone()
+    N[0, 0, 0] = 300
+    kin.N = N
+    with pytest.raises(OverflowError):
+        w.enzymatic_activity()
+        torch.cuda.synchronize()
+        w.enzymatic_activity()
