@@ -64,6 +64,9 @@ _FLUSH_EARLY = os.environ.get("MS_FLUSH_EARLY", "1") == "1"
 # default: the flagship step got slower (1.25 -> 1.35 ms median, profiles/r2_s3/headroom_chains_ab.txt)
 # -- the default queues them until the diffusion stencil is launched and joins at once.
 _EAGER_CHAINS = os.environ.get("MS_EAGER_CHAINS", "0") == "1"
+# the same for the strips of a decomposed world (MS_EAGER_CHAINS_DIST=1): their activity is not
+# speculative, so it waits for the chains on the host; issued early they are done by then
+_EAGER_CHAINS_DIST = os.environ.get("MS_EAGER_CHAINS_DIST", "0") == "1"
 # genome arena row width = this x the longest genome when it (re)grows (GPU worlds; see StringArena).
 # 1 by default: wider rows removed the early widening events but made the flagship step slower
 # (profiles/r2_s3/headroom_chains_ab.txt)
@@ -316,8 +319,10 @@ class World:
         and runs the activity again with the corrected parameters. Single-process GPU worlds only
         (a decomposed world's activity is collective)."""
         d = self.__dict__
+        # (a decomposed world speculates when it can agree on a redo: every rank then rolls back
+        # and redoes its collective activity together, see genome_pipeline.reconcile)
         return (_DEFER_ENV != "0" and d.get("_timer") is None and self._genomes.data.is_cuda
-                and getattr(self, "_allreduce_flags", None) is None)
+                and (getattr(self, "_allreduce_flags", None) is None or d.get("_agree_redo") is not None))
 
     def _defer(self, fn) -> None:
         d = self.__dict__
@@ -334,7 +339,9 @@ class World:
 
     def _lazy_join(self) -> bool:
         d = self.__dict__
-        return d.get("_early_chains", _EAGER_CHAINS) and "_n_pix_global" not in d
+        if "_n_pix_global" in d:  # a strip of a decomposed world (magicsoup_amd.parallel)
+            return d.get("_early_chains", _EAGER_CHAINS_DIST)
+        return d.get("_early_chains", _EAGER_CHAINS)
 
     def _join_side(self) -> None:
         """The compute stream waits (device-side) for the genome chains issued so far."""
@@ -385,7 +392,7 @@ class World:
         if self.__dict__.get("_deferred"):
             self._flush_deferred()
         self._join_side()
-        if self.__dict__.get("_gp_state"):
+        if self.__dict__.get("_gp_state") or self.__dict__.get("_spec") is not None:
             from magicsoup_amd.ops import genome_pipeline
 
             genome_pipeline.reconcile(self)
@@ -1079,9 +1086,13 @@ class World:
         the molecule map pixels under the cells)."""
         if self.n_cells == 0:
             return
-        st = self.__dict__.get("_gp_state")
+        d = self.__dict__
+        st = d.get("_gp_state")
         spec = save = None
-        if st and st["pending"]:
+        # a decomposed world speculates on every rank (the confirmation is collective), unless this
+        # is the redo of a rolled-back activity
+        collective = d.get("_agree_redo") is not None and not d.pop("_redo_activity", False) and self._speculate()
+        if (st and st["pending"]) or collective:
             # speculative: issued on top of unconfirmed parameter rebuilds (see _speculate); the
             # fused activity snapshots what it changes in its own input pass
             from magicsoup_amd.ops import hip_ops

@@ -92,6 +92,13 @@ def _copy_maps(dst: World, src: World) -> None:
         setattr(kin, name, mp)
 
 
+# MS_DIST_SPECULATE=1: speculative activity in decomposed GPU worlds, confirmed collectively
+# (genome_pipeline.reconcile). Off by default: measured no faster (virtual-strip A/Bs, flagship
+# 1.56-1.64 vs 1.54-1.56 ms, N = 8 proxy 0.92-1.07 vs 0.84-0.89 ms, profiles/r3/dist_spec/): the
+# host wait it removes overlaps device work (the genome chains) rather than leaving the GPU idle
+_DIST_SPECULATE = os.environ.get("MS_DIST_SPECULATE", "0") == "1"
+
+
 class DistributedWorld(World):
     """:class:`~magicsoup_amd.World` over the ranks of ``group`` (default: the whole job).
 
@@ -142,7 +149,14 @@ class DistributedWorld(World):
             kwargs["seed"] = int(seed) + 1_000_003 * self.rank  # independent streams per rank
         # Genetics (codon maps) and Kinetics (parameter maps) are random draws from Python's
         # `random`: every rank must hold the same ones, so build them from rank 0's stream
-        shared = [random.getrandbits(63) if self.rank == 0 else 0]
+        # (with a seed, rank 0 derives it from its seed, so the maps and the strip-boundary
+        # recombination streams of a seeded world do not depend on Python's global `random` state)
+        if self.rank != 0:
+            shared = [0]
+        elif seed is not None:
+            shared = [(int(seed) * 0x9E3779B97F4A7C15 + 0xD1B54A32D192ED03) & ((1 << 63) - 1)]
+        else:
+            shared = [random.getrandbits(63)]
         dist.broadcast_object_list(shared, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
         own = random.getstate()
         random.seed(shared[0])
@@ -174,6 +188,9 @@ class DistributedWorld(World):
             g["_exchange_map_halo"] = self._do_exchange_map_halo
             if exact_global_exit:
                 g["_allreduce_flags"] = self._do_allreduce_flags
+                if g["_halo_async"] and _DIST_SPECULATE:
+                    # speculative activity with a collective confirmation (genome_pipeline.reconcile)
+                    g["_agree_redo"] = self._do_agree_redo
             g["_allreduce_totals"] = self._do_allreduce_totals
             self._exchange_occupancy()  # first p2p call is collective on every rank
             self._do_exchange_map_halo()
@@ -304,6 +321,17 @@ class DistributedWorld(World):
     def _do_allreduce_totals(self, totals: torch.Tensor) -> None:
         self._all_reduce(totals, dist.ReduceOp.SUM)
 
+    def _do_agree_redo(self, redo: bool) -> bool:
+        """MAX of every rank's "my pipeline calls changed parameters" (collective, one read-back:
+        it waits for the speculative activity, which the kill after it waits for anyway)."""
+        from magicsoup_amd.ops import hip_ops
+
+        t = hip_ops._scratch(self).get("agree_redo", 1, torch.int32, self._tensor_device())
+        t.fill_(1 if redo else 0)
+        self._all_reduce(t, dist.ReduceOp.MAX)
+        hip_ops.guarded_sync()
+        return bool(int(t.item()))
+
     # ------------------------------------------------------------------ cell records
     def _records(self, cells: torch.Tensor, ys: torch.Tensor, child: bool) -> tuple[torch.Tensor, tuple[int, int]]:
         """Full records of ``cells`` landing on columns ``ys`` of a neighbour's boundary row: the
@@ -403,9 +431,12 @@ class DistributedWorld(World):
             from magicsoup_amd.models.kinetics import _INCREMENTS, _TRIMS
 
             if self._molmap.is_cuda:
-                from magicsoup_amd.ops import hip_ops
+                from magicsoup_amd.ops import genome_pipeline, hip_ops
 
                 hip_ops.integrate_idle(self, _TRIMS)
+                d = self.__dict__
+                if d.get("_agree_redo") is not None and not d.get("_redo_activity") and self._speculate():
+                    d["_spec"] = genome_pipeline.NO_STATE  # (joins the collective confirmation)
                 return
             for _ in _TRIMS:
                 hook(torch.zeros(len(_INCREMENTS), dtype=torch.int32, device=self._tensor_device()))

@@ -79,6 +79,8 @@ for s in "$@"; do case "$s" in
   tproxy) trace tproxy 39 --map-size 1448 --cells 6250 --steps 40 --warmup 20 ;;
   tvirt) MS_VIRTUAL_STRIPS=1 trace tvirt 39 --map-size 1448 --cells 6250 --steps 40 --warmup 20 ;;
   tflag) trace tflag 19 --steps 20 --warmup 20 ;;
+  tfvirt) MS_VIRTUAL_STRIPS=1 trace tfvirt 19 --steps 20 --warmup 20 ;;
+  hsfv) MS_PY_TIMES=1 MS_NATIVE_TIMES=1 MS_VIRTUAL_STRIPS=1 run host_py_flagship_virtual 300 python scripts/host_split.py 4096 50000 40 ;;
   htflag) htrace htflag 10 --steps 12 --warmup 20 ;;
   htproxy) htrace htproxy 10 --map-size 1448 --cells 6250 --steps 12 --warmup 20 ;;
   tenv) timeout -k 10 120 rocprofv3 --kernel-trace -d $O/tenv -o run --output-format csv -- python -c "import os; print(sorted(k for k in os.environ if 'ROC' in k))" > $O/tenv.log 2>&1; echo "   rc=$?" ;;
