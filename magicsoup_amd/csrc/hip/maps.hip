@@ -119,7 +119,15 @@ __global__ void __launch_bounds__(64 * kWaves) diffuse_stencil_kernel(const T* _
 // smaller grid leaves workgroup slots free on every CU, so the side stream's short pipeline kernels
 // (deferred genome chains, World._flush_deferred) start at once instead of waiting for stencil
 // workgroups to retire (set_stencil_blocks).
-constexpr int kVBand = 32;
+constexpr int kVBand = 32;     // rows per wave band of the vector stencils (default)
+constexpr int kMinVBand = 16;  // the narrowest band set_stencil_band accepts
+// rows per wave band (set_stencil_band; 0 = the default 32): a band re-reads one halo row above and
+// below it, so taller bands read less but leave fewer tiles per block of the grid-stride launch.
+// Same-box A/Bs at 4096^2 x 64 fp32 disagreed between boxes (64 rows: 1.529 vs 1.597 ms on one,
+// 1.77 vs 1.67 on another; profiles/r3/stencil_band/), 14 molecules preferred 32: the default stays.
+static int g_vband = kVBand;
+void set_stencil_band(int b) { g_vband = b <= 0 ? kVBand : (b < kMinVBand ? kMinVBand : (b > 256 ? 256 : b)); }
+static int stencil_band(int, int, int, int, int) { return g_vband; }
 
 // The rows of a wave's band: row_step(o, raw row o + 1) for o in [o0, o1); `first` holds raw row
 // o0 + 1 on entry. PF = 0: one raw row ahead, fetched into `spare` under a branch and copied (the
@@ -159,7 +167,7 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
                                                                const float* __restrict__ scale,
                                                                const float* __restrict__ corr, MGeom g,
                                                                double* __restrict__ partials, int gx, int gy,
-                                                               int ntiles) {
+                                                               int ntiles, int vband) {
   __shared__ double red[2][4];
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   const int bx = tile % gx, by = (tile / gx) % gy, mol = tile / (gx * gy);
@@ -174,7 +182,7 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
   T* dst = out + (size_t)mol * plane;
   const float sc = scale ? scale[mol] : 1.0f;
   const float a = wa[mol], b = wb[mol];
-  const int o0 = (by * 4 + wv) * kVBand, o1 = min(H, o0 + kVBand);
+  const int o0 = (by * 4 + wv) * vband, o1 = min(H, o0 + vband);
 
   auto row_of = [&](int o) {
     int x = g.r_lo + o;
@@ -282,7 +290,7 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
                                                                const float* __restrict__ scale,
                                                                const float* __restrict__ corr, MGeom g,
                                                                double* __restrict__ partials, int gx, int gy,
-                                                               int ntiles) {
+                                                               int ntiles, int vband) {
   __shared__ double red[2][4];
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int bx = tile % gx, by = (tile / gx) % gy, mol = tile / (gx * gy);
@@ -299,7 +307,7 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
     const float a = wa[mol], b = wb[mol];
     const bool has_c = corr != nullptr;
     const float cm = has_c ? corr[mol] : 0.0f;
-    const int o0 = (by * 4 + wv) * kVBand, o1 = min(H, o0 + kVBand);
+    const int o0 = (by * 4 + wv) * vband, o1 = min(H, o0 + vband);
 
     auto row_of = [&](int o) {
       int x = g.r_lo + o;
@@ -604,8 +612,9 @@ void set_stencil_blocks(int n) { g_stencil_blocks = std::max(0, n); }
 
 size_t diffuse_partials_len(int m, int C, int H) {
   // (the largest layout of any variant: the variant may be switched between calls)
-  const size_t v8 = (size_t)cdiv(C, 512) * cdiv(cdiv(H, kVBand), 4) * m * 2;
-  const size_t v4 = (size_t)cdiv(C, 256) * cdiv(cdiv(H, kVBand), 4) * m * 2;
+  // (sized for the narrowest band set_stencil_band allows)
+  const size_t v8 = (size_t)cdiv(C, 512) * cdiv(cdiv(H, kMinVBand), 4) * m * 2;
+  const size_t v4 = (size_t)cdiv(C, 256) * cdiv(cdiv(H, kMinVBand), 4) * m * 2;
   const size_t v1 = (size_t)cdiv(C, 64 * kWaves) * cdiv(H, kBand) * m * 2;
   return std::max(v8, std::max(v4, v1));
 }
@@ -620,8 +629,9 @@ void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_
   hipStream_t st_ = S_(stream);
   const int H = r_hi - r_lo;
   const bool v8 = use_vec8(C, dtype), v4 = !v8 && use_vec4(C);
-  const dim3 grid = v8   ? dim3(cdiv(C, 512), cdiv(cdiv(H, kVBand), 4), m)
-                    : v4 ? dim3(cdiv(C, 256), cdiv(cdiv(H, kVBand), 4), m)
+  const int vband = stencil_band(C, H, m, v8 ? 512 : 256, g_stencil_blocks);
+  const dim3 grid = v8   ? dim3(cdiv(C, 512), cdiv(cdiv(H, vband), 4), m)
+                    : v4 ? dim3(cdiv(C, 256), cdiv(cdiv(H, vband), 4), m)
                          : dim3(cdiv(C, 64 * kWaves), cdiv(H, kBand), m);
   if (v8) {
     const int ntiles = (int)(grid.x * grid.y * grid.z);
@@ -629,14 +639,14 @@ void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_
     MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), (diffuse_stencil8_kernel<T, PF><<<blocks, 256, 0, st_>>>(
                                P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
                                corr ? P_<float>(corr) : nullptr, g, P_<double>(partials), (int)grid.x, (int)grid.y,
-                               ntiles))));
+                               ntiles, vband))));
   } else if (v4) {
     const int ntiles = (int)(grid.x * grid.y * grid.z);
     const int blocks = g_stencil_blocks > 0 ? std::min(ntiles, g_stencil_blocks) : ntiles;
     MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), (diffuse_stencil4_kernel<T, PF><<<blocks, 256, 0, st_>>>(
                                P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
                                corr ? P_<float>(corr) : nullptr, g, P_<double>(partials), (int)grid.x, (int)grid.y,
-                               ntiles))));
+                               ntiles, vband))));
   } else {
     MS_MAP_DISPATCH(dtype, (diffuse_stencil_kernel<T><<<grid, 64 * kWaves, 0, st_>>>(
                                P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
@@ -666,11 +676,11 @@ void diffuse_boundary(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, ui
     if (v8) {
       MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), (diffuse_stencil8_kernel<T, PF><<<tiles, 256, 0, st_>>>(
                                  P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
-                                 corr ? P_<float>(corr) : nullptr, g, part, gx, 1, tiles))));
+                                 corr ? P_<float>(corr) : nullptr, g, part, gx, 1, tiles, kVBand))));
     } else if (v4) {
       MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), (diffuse_stencil4_kernel<T, PF><<<tiles, 256, 0, st_>>>(
                                  P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
-                                 corr ? P_<float>(corr) : nullptr, g, part, gx, 1, tiles))));
+                                 corr ? P_<float>(corr) : nullptr, g, part, gx, 1, tiles, kVBand))));
     } else {
       MS_MAP_DISPATCH(dtype, (diffuse_stencil_kernel<T><<<dim3(gx, 1, m), 64 * kWaves, 0, st_>>>(
                                  P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,

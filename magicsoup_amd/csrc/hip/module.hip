@@ -26,6 +26,7 @@ void place_rounds_mask(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r
 void set_coop_blocks(int n);
 void set_stencil_vec(int v);
 void set_stencil_prefetch(int pf);
+void set_stencil_band(int b);
 void set_stencil_blocks(int n);
 void set_place_mode(int mode);
 int place_error_take();
@@ -269,6 +270,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("set_coop_blocks", &msd::set_coop_blocks, "workgroups of the cooperative placement (A/B)");
   m.def("set_stencil_vec", &msd::set_stencil_vec, "diffusion stencil columns per lane: 8 (default), 4 or 1");
   m.def("set_stencil_prefetch", &msd::set_stencil_prefetch, "rows the vector stencils load ahead (-1 auto, 0-3)");
+  m.def("set_stencil_band", &msd::set_stencil_band, "rows per wave band of the vector stencils (16-256; 0 = the default 32)");
   m.def("set_stencil_blocks", &msd::set_stencil_blocks, "blocks of the vector diffusion stencil (0: one per tile)");
   m.def("set_place_mode", &msd::set_place_mode, "0 cooperative single launch (default), 1 multi-launch rounds");
   m.def("place_error_take", &msd::place_error_take,

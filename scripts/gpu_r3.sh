@@ -85,8 +85,10 @@ for s in "$@"; do case "$s" in
   htproxy) htrace htproxy 10 --map-size 1448 --cells 6250 --steps 12 --warmup 20 ;;
   tenv) timeout -k 10 120 rocprofv3 --kernel-trace -d $O/tenv -o run --output-format csv -- python -c "import os; print(sorted(k for k in os.environ if 'ROC' in k))" > $O/tenv.log 2>&1; echo "   rc=$?" ;;
   dbench) run diffuse_bench 300 python scripts/diffuse_bench.py --vec 4 8 --blocks 1024 0 2048 ;;
+  dbband) run diffuse_bench_band 400 python scripts/diffuse_bench.py --vec 0 --blocks 1024 2048 --band 16 32 48 64 --dtypes fp32 fp16 && run diffuse_bench_band64 400 python scripts/diffuse_bench.py --chem synthetic:64:256 --vec 0 --blocks 1024 2048 --band 16 32 64 --dtypes fp32 --iters 10 ;;
   dbpf) run diffuse_bench_pf 300 python scripts/diffuse_bench.py --vec 4 8 --blocks 1024 2048 --pf 0 1 2 3 ;;
   dtests) run dtests 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "diffusion or reduced_precision or permeation" ;;
+  dbauto) run diffuse_bench_auto 400 python scripts/diffuse_bench.py --vec 0 --blocks 1024 --band 0 32 --dtypes fp32 fp16 && run diffuse_bench_auto64 400 python scripts/diffuse_bench.py --chem synthetic:64:256 --vec 0 --blocks 1024 --band 0 32 --dtypes fp32 --iters 10 ;;
   tc64) trace tc64 9 --preset wide --steps 10 --warmup 5 ;;
   tm1) trace tm1 19 --preset m1 --steps 20 --warmup 10 ;;
   pmcw1) pmc pmc_wide_sq "integrate|gather_bin|diffuse_stencil" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" -- --preset wide --steps 3 --warmup 3 ;;

@@ -148,6 +148,27 @@ def test_diffusion_matches_host(size):
     assert torch.allclose(wg.molecule_map.cpu(), wc.molecule_map, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("band", [16, 48, 64, 128])
+@pytest.mark.parametrize("vec", [4, 8])
+def test_diffusion_band_heights_match_host(band, vec):
+    """The vector stencils' wave bands (set_stencil_band: taller bands re-read fewer halo rows) and
+    both column widths give the host result for any band height, including bands taller than the
+    map and partial last bands."""
+    try:
+        native.hip().set_stencil_band(band)
+        native.hip().set_stencil_vec(vec)
+        for size in (40, 200):
+            wc = _world("cpu", map_size=size, n=0)
+            wg = _copy_world_cpu_to_gpu(wc)
+            for w in (wc, wg):
+                w.degrade_molecules()
+                w.diffuse_molecules()
+            assert torch.allclose(wg.molecule_map.cpu(), wc.molecule_map, rtol=1e-5, atol=1e-5), size
+    finally:
+        native.hip().set_stencil_band(0)
+        native.hip().set_stencil_vec(0)
+
+
 def test_diffusion_conserves_mass():
     w = _world("cuda", map_size=512, n=0)
     before = w.molecule_map.double().sum(dim=[1, 2])
