@@ -262,6 +262,9 @@ def main():
     setup_s = time.time() - t0
 
     def sync():
+        # (World.synchronize: also confirms the last step's queued genome operations on the host,
+        # so their confirmation -- and any replay it triggers -- is inside the timed window)
+        world.synchronize()
         if torch.cuda.is_available():
             torch.cuda.synchronize()
         if distributed:

@@ -1365,6 +1365,16 @@ class World:
         return torch.tensor(d, device=self.device, dtype=torch.float32)
 
     # ------------------------------------------------------------------ observability
+    def synchronize(self) -> None:
+        """Settle everything issued so far: adopt a pending division count, issue and confirm the
+        queued genome operations (replaying or rebuilding on the host where the device pipeline
+        flagged it, redoing a speculative activity if that changed parameters), then wait for the
+        device. After it the world's state is final and the GPU is idle (benchmarks stop their
+        clock after this, so the last step's confirmation is inside the timed region)."""
+        self._reconcile()
+        if self._molmap.is_cuda:
+            torch.cuda.synchronize(self._molmap.device)
+
     def enable_timings(self, sync: bool = False) -> None:
         """Time every public operation with HIP events (wall clock on CPU); read with
         :meth:`step_timings`. ``sync=True`` drains the device around each op (exact attribution of

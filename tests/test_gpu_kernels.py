@@ -1012,3 +1012,21 @@ def test_int8_overflow_of_packed_parameters_raises():
         w.enzymatic_activity()
         torch.cuda.synchronize()
         w.enzymatic_activity()
+
+
+def test_synchronize_settles_pending_work():
+    """World.synchronize() (what bench.py stops its clock after): a lazy division's count adopted,
+    queued genome ops issued and confirmed, a speculative activity confirmed, the device idle."""
+    w = _world("cuda", map_size=64, n=600, s=400, seed=3)
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    w.enzymatic_activity()
+    w.divide_cells_t(w.cell_molecules[:, atp] > 2.0, lazy=True)
+    w.recombinate_cells(p=1e-4)
+    w.mutate_cells(p=1e-3)
+    w.degrade_molecules()
+    w.enzymatic_activity()  # speculative on top of the queued chains
+    w.synchronize()
+    d = w.__dict__
+    assert d.get("_count_pending") is None and not d.get("_deferred") and d.get("_spec") is None
+    assert not (d.get("_gp_state") or {}).get("pending")
+    assert len(w.cell_genomes) == w.n_cells == w.kinetics.Vmax.size(0)
