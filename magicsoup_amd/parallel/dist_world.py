@@ -97,6 +97,9 @@ def _copy_maps(dst: World, src: World) -> None:
 # 1.56-1.64 vs 1.54-1.56 ms, N = 8 proxy 0.92-1.07 vs 0.84-0.89 ms, profiles/r3/dist_spec/): the
 # host wait it removes overlaps device work (the genome chains) rather than leaving the GPU idle
 _DIST_SPECULATE = os.environ.get("MS_DIST_SPECULATE", "0") == "1"
+# issue the boundary recombination's collective part at the recombinate_cells() call (MS_XB_EARLY=0:
+# at the flush after the diffusion stencil, as before)
+_XB_EARLY = os.environ.get("MS_XB_EARLY", "1") != "0"
 
 
 class DistributedWorld(World):
@@ -720,20 +723,49 @@ class DistributedWorld(World):
             return super().recombinate_cells(cell_idxs, p)
         if cell_idxs is None and self._genomes.data.is_cuda and self._defer_genome_op():
             # queued like World's: every rank flushes at the same op, in call order, and its
-            # exchanges then go through the side-stream communicator
-            self._defer(lambda: self._recombinate_strips_all(p))
+            # exchanges then go through the side-stream communicator. The boundary part's collective
+            # (lengths / event genomes exchanged) is issued now on the side stream (_xb_pre_issue)
+            # (only as the first queued genome op: its genomes are then final for this call; a later
+            # queued call computes its boundary part at the flush, after the earlier results)
+            early = (_XB_EARLY and not self.__dict__.get("_deferred")
+                     and isinstance(self.__dict__.get("_comm_side"), RcclComm))
+            pre = self._xb_pre_issue(p) if early else None
+            self._defer(lambda: self._recombinate_strips_all(p, pre))
             return
         self._reconcile()
         if cell_idxs is not None:
             return self._recombinate_subset(cell_idxs, p)
         self._recombinate_strips_all(p)
 
-    def _recombinate_strips_all(self, p: float) -> None:
-        self.__dict__["_xcall"] += 1
+    def _recombinate_strips_all(self, p: float, pre: "_BoundaryRecombination | None" = None) -> None:
+        if pre is None:
+            self.__dict__["_xcall"] += 1
         if self._genomes.data.is_cuda:
-            self._recombinate_gpu(p)
+            self._recombinate_gpu(p, pre)
         else:
             self._recombinate_cpu(p)
+
+    def _xb_pre_issue(self, p: float) -> "_BoundaryRecombination":
+        """The collective part of the boundary recombination of a queued recombinate_cells(), issued
+        at the call on the side stream (after the state so far, an event), instead of at the flush
+        behind the diffusion stencil: there its RCCL kernel waited for the stencil's workgroups
+        (~0.2 ms at 4096^2) and the genome chains after it no longer overlapped the stencil. Every
+        rank issues it at the same call, so the side communicator's order is unchanged."""
+        from magicsoup_amd.ops.genome_pipeline import K_CAP
+        from magicsoup_amd.ops.streams import NEvent, on_stream
+
+        d = self.__dict__
+        side = d.get("_side_stream")
+        if side is None:
+            side = d["_side_stream"] = torch.cuda.Stream(device=self._genomes.data.device, priority=-1)
+        NEvent().record().wait(side.cuda_stream)
+        d["_side_active"] = True
+        try:
+            d["_xcall"] += 1
+            with on_stream(side):
+                return _BoundaryRecombination(self, p, K_CAP)
+        finally:
+            d["_side_active"] = False
 
     # ------------------------------------------------------------------ strip-boundary recombination
     def _xb_params(self, p: float):
@@ -748,11 +780,11 @@ class DistributedWorld(World):
 
         return E, W, bseed(self.rank), bseed((self.rank - 1) % self.world_size), int(self._xcall)
 
-    def _recombinate_gpu(self, p: float) -> None:
+    def _recombinate_gpu(self, p: float, pre: "_BoundaryRecombination | None" = None) -> None:
         from magicsoup_amd.ops import genome_pipeline, hip_ops
         from magicsoup_amd.ops.genome_pipeline import K_CAP
 
-        x = _BoundaryRecombination(self, p, K_CAP)
+        x = pre if pre is not None else _BoundaryRecombination(self, p, K_CAP)
         if self.n_cells >= 2 and genome_pipeline.recombinate_all(self, p, extra=x):
             return
         # synchronous path (very high rates / fewer than 2 cells): local pairs, then the boundary

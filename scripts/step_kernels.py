@@ -10,7 +10,12 @@ import statistics
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-marks = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("void msd::diffuse_stencil4")]
+# step marker: the stencil (one launch per step), or with MARKER=<prefix> another once-per-step kernel
+# (a strip world splits its stencil into interior + boundary launches: use msd::diffuse_corr_kernel)
+import os  # noqa: E402
+
+marker = os.environ.get("MARKER", "void msd::diffuse_stencil4")
+marks = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(marker)]
 nst = int(sys.argv[2])
 a, b = marks[-nst - 1], marks[-1]
 sel = rows[a + 1 : b + 1]
