@@ -346,7 +346,7 @@ def spawn_issue(world, rows: torch.Tensor, lens: torch.Tensor, n0: int) -> None:
 def cell_state_buffer(world) -> torch.Tensor:
     """The scratch buffer of :func:`save_cell_state` (2 * n_cells * n_molecules floats)."""
     d = world.__dict__
-    return _scratch(world).get("spec_state", 2 * d["n_cells"] * world.n_molecules, torch.float32,
+    return _scratch(world).get("spec_state", 2 * world.n_cells * world.n_molecules, torch.float32,
                                d["_molmap"].device)
 
 
@@ -356,7 +356,7 @@ def save_cell_state(world) -> torch.Tensor:
     if world.__dict__.get("_spec_diff") is not None:
         spec_diffuse_cancel(world)
     d = world.__dict__
-    n, m = d["n_cells"], world.n_molecules
+    n, m = world.n_cells, world.n_molecules
     mm = d["_molmap"]
     R, C = geom(world)[:2]
     buf = _scratch(world).get("spec_state", 2 * n * m, torch.float32, mm.device)
@@ -369,7 +369,7 @@ def restore_cell_state(world, buf: torch.Tensor) -> None:
     if world.__dict__.get("_spec_diff") is not None:
         spec_diffuse_cancel(world)
     d = world.__dict__
-    n, m = d["n_cells"], world.n_molecules
+    n, m = world.n_cells, world.n_molecules
     mm = d["_molmap"]
     R, C = geom(world)[:2]
     _m().cell_state_io(n, m, _p(d["_cols"]["cell_positions"].view(n)), R, C, _p(mm), _mdt(mm),
