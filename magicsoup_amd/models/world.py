@@ -64,6 +64,10 @@ _FLUSH_EARLY = os.environ.get("MS_FLUSH_EARLY", "1") == "1"
 # default: the flagship step got slower (1.25 -> 1.35 ms median, profiles/r2_s3/headroom_chains_ab.txt)
 # -- the default queues them until the diffusion stencil is launched and joins at once.
 _EAGER_CHAINS = os.environ.get("MS_EAGER_CHAINS", "0") == "1"
+# the compute stream joins the flushed chains at the next op that needs them (the activity, or a
+# read of genomes / parameters), not right after the flush: the molecule-only work in between (the
+# lifetimes, the loop's masks) runs while the chains finish (MS_LAZY_JOIN=0: join at the flush)
+_LAZY_JOIN = os.environ.get("MS_LAZY_JOIN", "1") == "1"
 # the same for the strips of a decomposed world (MS_EAGER_CHAINS_DIST=1): their activity is not
 # speculative, so it waits for the chains on the host; issued early they are done by then
 _EAGER_CHAINS_DIST = os.environ.get("MS_EAGER_CHAINS_DIST", "0") == "1"
@@ -380,7 +384,7 @@ class World:
                     fn()
         finally:
             d["_side_active"] = False
-            if self._lazy_join():
+            if self._lazy_join() or (_LAZY_JOIN and "_n_pix_global" not in d):
                 # joined at the next op that needs the chains' results (see _EAGER_CHAINS)
                 d["_side_join"] = NEvent().record(side_raw)
             else:
