@@ -320,8 +320,9 @@ class World:
         diffusion stencil; issuing the activity first keeps the device busy meanwhile. The state
         the activity changes is saved first; the next access to molecules, or the next op,
         confirms the calls and -- only if one had to be redone on the host -- restores that state
-        and runs the activity again with the corrected parameters. Single-process GPU worlds only
-        (a decomposed world's activity is collective)."""
+        and runs the activity again with the corrected parameters. Single-process GPU worlds, and
+        decomposed ones only with ``MS_DIST_SPECULATE=1`` (their activity is collective, so the
+        confirmation is too: genome_pipeline.reconcile)."""
         d = self.__dict__
         # (a decomposed world speculates when it can agree on a redo: every rank then rolls back
         # and redoes its collective activity together, see genome_pipeline.reconcile)
