@@ -5,6 +5,8 @@
 #include <omp.h>
 
 #include <algorithm>
+#include <deque>
+#include <string_view>
 
 #include "host_common.h"
 
@@ -47,13 +49,15 @@ int64_t poisson(std::mt19937_64& rng, double lam) {
   return d(rng);
 }
 
-// Apply point mutations to one sequence; returns false if no mutation was drawn.
-bool mutate_one(std::string& seq, std::mt19937_64& rng, double p, double p_indel, double p_del) {
+// Number of mutations drawn for a sequence of length len (the first draw of mutate_one).
+int64_t draw_mutations(std::mt19937_64& rng, int64_t len, double p) {
+  if (len < 1) return 0;
+  return std::min(poisson(rng, p * (double)len), len);
+}
+
+// Apply k >= 1 drawn point mutations to one sequence.
+void apply_mutations(std::string& seq, int64_t k, std::mt19937_64& rng, double p_indel, double p_del) {
   const int64_t len = (int64_t)seq.size();
-  if (len < 1) return false;
-  int64_t k = poisson(rng, p * (double)len);
-  if (k < 1) return false;
-  k = std::min(k, len);
   std::vector<int64_t> pos = sample_sorted(rng, len, k);
   std::bernoulli_distribution indel(p_indel), del(p_del);
   std::uniform_int_distribution<int> nt(0, 3);
@@ -72,11 +76,18 @@ bool mutate_one(std::string& seq, std::mt19937_64& rng, double p, double p_indel
       seq[(size_t)at] = kNts[nt(rng)];
     }
   }
+}
+
+// Apply point mutations to one sequence; returns false if no mutation was drawn.
+bool mutate_one(std::string& seq, std::mt19937_64& rng, double p, double p_indel, double p_del) {
+  const int64_t k = draw_mutations(rng, (int64_t)seq.size(), p);
+  if (k < 1) return false;
+  apply_mutations(seq, k, rng, p_indel, p_del);
   return true;
 }
 
 // Recombine one pair; returns false if no strand break was drawn.
-bool recombine_one(const std::string& s0, const std::string& s1, std::mt19937_64& rng, double p,
+bool recombine_one(std::string_view s0, std::string_view s1, std::mt19937_64& rng, double p,
                    std::string& o0, std::string& o1) {
   const int64_t n0 = (int64_t)s0.size(), n1 = (int64_t)s1.size(), nb = n0 + n1;
   if (nb < 1) return false;
@@ -84,7 +95,7 @@ bool recombine_one(const std::string& s0, const std::string& s1, std::mt19937_64
   if (k < 1) return false;
   k = std::min(k, nb);
   std::vector<int64_t> cuts = sample_sorted(rng, nb, k);
-  std::vector<std::pair<const std::string*, std::pair<int64_t, int64_t>>> parts;
+  std::vector<std::pair<const std::string_view*, std::pair<int64_t, int64_t>>> parts;
   parts.reserve(k + 2);
   int64_t i = 0;
   for (int64_t c : cuts)
@@ -108,19 +119,34 @@ bool recombine_one(const std::string& s0, const std::string& s1, std::mt19937_64
   for (size_t j = 0; j < parts.size(); ++j) {
     auto& pr = parts[j];
     std::string& dst = j < s ? o0 : o1;
-    dst.append(*pr.first, (size_t)pr.second.first, (size_t)(pr.second.second - pr.second.first));
+    dst.append(pr.first->substr((size_t)pr.second.first, (size_t)(pr.second.second - pr.second.first)));
   }
   return true;
 }
 
 }  // namespace
 
-// list[str] -> list[(str, idx)] of mutated sequences (reference _lib.point_mutations)
+// Borrowed views of Python str items: a compact str's UTF-8 buffer is read in place (no copy; the
+// caller's list keeps the objects alive for the call), anything else is converted into `owned`.
+std::string_view seq_view(PyObject* o, std::deque<std::string>& owned) {
+  if (PyUnicode_Check(o)) {
+    Py_ssize_t n = 0;
+    const char* d = PyUnicode_AsUTF8AndSize(o, &n);
+    if (d == nullptr) throw py::error_already_set();
+    return {d, (size_t)n};
+  }
+  owned.push_back(py::reinterpret_borrow<py::object>(o).cast<std::string>());
+  return owned.back();
+}
+
+// list[str] -> list[(str, idx)] of mutated sequences (reference _lib.point_mutations). Only the
+// sequences that draw a mutation are copied: at p ~ 1e-6 that is a few in 10k.
 py::list point_mutations(const py::list& seqs, double p, double p_indel, double p_del) {
-  std::vector<std::string> v;
-  v.reserve(seqs.size());
-  for (auto s : seqs) v.push_back(s.cast<std::string>());
-  const int n = (int)v.size();
+  const int n = (int)seqs.size();
+  std::deque<std::string> owned;
+  std::vector<std::string_view> v(n);
+  for (int i = 0; i < n; ++i) v[i] = seq_view(PyList_GET_ITEM(seqs.ptr(), i), owned);
+  std::vector<std::string> res(n);
   std::vector<uint8_t> hit(n, 0);
   const uint64_t cs = next_call_seed();
   {
@@ -128,24 +154,39 @@ py::list point_mutations(const py::list& seqs, double p, double p_indel, double 
 #pragma omp parallel for schedule(static, 256)
     for (int i = 0; i < n; ++i) {
       auto rng = item_engine(cs, (uint64_t)i);
-      hit[i] = mutate_one(v[i], rng, p, p_indel, p_del);
+      const int64_t k = draw_mutations(rng, (int64_t)v[i].size(), p);
+      if (k < 1) continue;
+      res[i].assign(v[i]);
+      apply_mutations(res[i], k, rng, p_indel, p_del);
+      hit[i] = 1;
     }
   }
   py::list out;
   for (int i = 0; i < n; ++i)
-    if (hit[i]) out.append(py::make_tuple(v[i], i));
+    if (hit[i]) out.append(py::make_tuple(res[i], i));
   return out;
 }
 
-// list[(str, str)] -> list[(str, str, idx)] (reference _lib.recombinations)
+// list[(str, str)] -> list[(str, str, idx)] (reference _lib.recombinations); inputs are read in place.
 py::list recombinations(const py::list& pairs, double p) {
   const int n = (int)pairs.size();
-  std::vector<std::string> a(n), b(n), oa(n), ob(n);
+  std::deque<std::string> owned;
+  std::vector<std::string_view> a(n), b(n);
   for (int i = 0; i < n; ++i) {
-    py::tuple t = pairs[i].cast<py::tuple>();
-    a[i] = t[0].cast<std::string>();
-    b[i] = t[1].cast<std::string>();
+    PyObject* t = PyList_GET_ITEM(pairs.ptr(), i);
+    if (PyTuple_Check(t) && PyTuple_GET_SIZE(t) == 2) {
+      a[i] = seq_view(PyTuple_GET_ITEM(t, 0), owned);
+      b[i] = seq_view(PyTuple_GET_ITEM(t, 1), owned);
+    } else {
+      py::sequence sq = py::reinterpret_borrow<py::sequence>(t);
+      if (sq.size() != 2) throw py::value_error("recombinations: every item must be a pair of sequences");
+      owned.push_back(sq[0].cast<std::string>());
+      a[i] = owned.back();
+      owned.push_back(sq[1].cast<std::string>());
+      b[i] = owned.back();
+    }
   }
+  std::vector<std::string> oa(n), ob(n);
   std::vector<uint8_t> hit(n, 0);
   const uint64_t cs = next_call_seed();
   {

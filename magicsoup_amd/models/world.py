@@ -22,6 +22,7 @@ MI355X-first design:
 from __future__ import annotations
 
 import functools
+import gc
 import math
 import os
 import pickle
@@ -630,8 +631,17 @@ class World:
         Each cell of ``cell_idxs`` pairs with neighbouring cells of ``nghbr_idxs`` (default:
         ``cell_idxs`` itself).
         """
-        pairs = self.get_neighbors_t(cell_idxs, nghbr_idxs)
-        return [tuple(d) for d in pairs.tolist()]
+        pairs = self.get_neighbors_t(cell_idxs, nghbr_idxs).cpu()
+        # tens of thousands of new tuples: with the collector running, their allocation triggers
+        # full collections over every tracked object of the process (~40 ms each at 24k pairs)
+        paused = gc.isenabled()
+        if paused:
+            gc.disable()
+        try:
+            return list(zip(pairs[:, 0].tolist(), pairs[:, 1].tolist()))
+        finally:
+            if paused:
+                gc.enable()
 
     @_op("get_neighbors")
     def get_neighbors_t(self, cell_idxs, nghbr_idxs=None) -> torch.Tensor:

@@ -57,6 +57,7 @@ for s in "$@"; do case "$s" in
   fvirt) MS_VIRTUAL_STRIPS=1 run flagship_virtual 300 python bench.py ;;
   c64) run c4096_50k_64x256 400 python bench.py --chemistry synthetic:64:256 --steps 20 --warmup 5 ;;
   c256) run c256_40k 300 python bench.py --map-size 256 --cells 40000 ;;
+  c1024f) run c1024_10k_16x32_fp32 300 python bench.py --map-size 1024 --cells 10000 --chemistry synthetic:16:32 --map-dtype fp32 --steps 30 --warmup 5 ;;
   c1024) run c1024_10k_16x32_bf16 300 python bench.py --map-size 1024 --cells 10000 --chemistry synthetic:16:32 --map-dtype bf16 --steps 30 --warmup 5 ;;
   m1) run c16384_1m_fp16 600 python bench.py --map-size 16384 --cells 1000000 --map-dtype fp16 --steps 50 --warmup 5 --step-times ;;
   hb) run host_breakdown 300 python scripts/host_breakdown.py 4096 50000 40 ;;
