@@ -97,3 +97,25 @@ def test_world_recombination_pairs_neighbours_only():
     assert h[2:] == g[2:]
     assert len(h[0]) + len(h[1]) == 400
     assert (h[0], h[1]) != (g[0], g[1])
+
+
+def test_list_api_inputs_read_in_place_are_left_untouched():
+    # the host core reads str inputs in place: outputs are fresh strings, the inputs never change,
+    # and pairs may be given as lists as well as tuples
+    seqs = ["ACGT" * 50 for _ in range(200)]
+    before = list(seqs)
+    out = muts.point_mutations(seqs=seqs, p=0.05)
+    assert out and seqs == before
+    pairs = [["A" * 40, "C" * 40] for _ in range(100)]
+    rec = muts.recombinations(seq_pairs=pairs, p=0.1)
+    assert rec and all(p == ["A" * 40, "C" * 40] for p in pairs)
+    for s0, s1, i in rec:
+        assert sorted(s0 + s1) == sorted("A" * 40 + "C" * 40) and 0 <= i < 100
+
+
+def test_get_neighbors_returns_int_tuples():
+    w = ms.World(chemistry=ms.Chemistry(molecules=[ms.Molecule("nbtest_a", 10.0)], reactions=[]), map_size=8)
+    w.spawn_cells(genomes=["ACGT" * 20] * 30)
+    pairs = w.get_neighbors(cell_idxs=list(range(w.n_cells)))
+    assert pairs and all(type(p) is tuple and len(p) == 2 and type(p[0]) is int and p[0] < p[1] for p in pairs)
+    assert len(set(pairs)) == len(pairs)
