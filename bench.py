@@ -8,9 +8,11 @@ random genomes, population topped up to >= 50,000 cells every step. One step:
     divisions that follow restore ~1.02 N: chemostat dilution) -> replicate (ATP > 5: ATP -= 4, divide)
     -> recombinate_cells -> mutate_cells -> degrade -> diffuse -> increment lifetimes
 
-Single GPU: one ``World`` on ``cuda:0``. N GPUs (``torchrun --nproc-per-node N``): one world,
-domain-decomposed over the ranks (``magicsoup_amd.parallel``; strong scaling of the fixed config).
-Rank 0 prints one JSON line; ``value`` is steps/s of the whole job (max time over ranks).
+Single GPU: one ``World`` on ``cuda:0``. N GPUs: one world, domain-decomposed over N ranks, one per
+GPU (``magicsoup_amd.parallel``; strong scaling of the fixed config). ``--gpus N`` launches the N ranks
+itself (``torch.distributed.run`` on 127.0.0.1) unless a launcher already did (``WORLD_SIZE`` set).
+Rank 0 prints one JSON line; ``value`` is steps/s of the whole job (max time over ranks); ``n_gpus``
+is the size of the RCCL communicator the exchanges ran over, ``devices`` each rank's GPU.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--map-size S] [--cells C] [--preset P]
 
@@ -200,9 +202,37 @@ def _prime_rare_paths(chem, device, mdt, genome_size: int) -> None:
     _CHEMOSTAT.update(divided=0, starved=0, steps=0, after_kill=None)
 
 
+def _self_launch(a) -> int | None:
+    """``--gpus N`` (N > 1) without a launcher: start N ranks of this script under
+    ``torch.distributed.run`` (one per GPU, rendezvous on 127.0.0.1) and return their exit code.
+    Runs before anything touches the GPU in this process (the children initialise their own
+    devices); rank 0's JSON line reaches stdout directly. A failing rank makes the launcher, and so
+    this process, exit non-zero."""
+    if a.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = int(sk.getsockname()[1])
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL between processes)
+    env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 8) // (2 * a.gpus))))
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     a = _args()
+    rc = _self_launch(a)
+    if rc is not None:
+        sys.exit(rc)
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_size > 1 and a.gpus not in (1, world_size):
+        print(f"bench.py: --gpus {a.gpus} but the launcher started {world_size} ranks; reporting "
+              f"{world_size}", file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # MS_VIRTUAL_STRIPS=1: one rank running the multi-rank code path (strip geometry, exchanges with
@@ -306,8 +336,16 @@ def main():
         n_cells = world.n_cells
     ms_per_step = dt / a.steps * 1e3
     value = a.steps / dt
-    # distinct devices actually used (a gloo rehearsal may put several ranks on one GPU)
-    n_gpus = (min(world_size, n_dev) if distributed else 1) if n_dev else 0
+    # distinct devices actually used (a gloo rehearsal may put several ranks on one GPU); with RCCL,
+    # the size of the communicator the exchanges ran over
+    devices = [local_rank if n_dev else -1]
+    comm_size = None
+    if distributed:
+        devices = [None] * world_size
+        torch.distributed.all_gather_object(devices, local_rank if n_dev else -1)
+        c = world.__dict__.get("_comm")
+        comm_size = getattr(c, "size", None) if getattr(c, "native", False) else None
+    n_gpus = (len({d for d in devices if d is not None and d >= 0}) if comm_size is None else comm_size) if n_dev else 0
     if rank == 0:
         if timer is not None:
             per_step = {k: v / a.steps for k, v in (stats or {}).items()}
@@ -339,9 +377,13 @@ def main():
                 "parallelism": ("strips1-virtual" if virtual else f"spatial{world_size}") if distributed else "single",
             },
         }
+        out["ranks"] = world_size if distributed else 1
+        out["devices"] = devices
         if distributed:
             out["config"]["ranks"] = world_size
             out["config"]["backend"] = backend
+            if comm_size is not None:
+                out["config"]["rccl_comm_size"] = comm_size
             if backend != "nccl" or world_size > n_dev or virtual:
                 out["rehearsal"] = True  # ranks share GPUs, exchange over gloo or with themselves
         print(json.dumps(out), flush=True)

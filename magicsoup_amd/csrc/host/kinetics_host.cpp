@@ -188,7 +188,12 @@ py::list integrate_signals(farr X, iarr N, iarr Nf, iarr Nb, iarr A, farr Kmr, f
   uint8_t* dec = nullptr;
   py::array_t<uint8_t, py::array::c_style> dec_arr;
   if (!decisions_obj.is_none()) {
-    dec_arr = decisions_obj.cast<py::array_t<uint8_t, py::array::c_style>>();
+    // written in place: an array of another dtype or layout would be converted into a temporary
+    // copy and the decisions silently dropped, so only an exact uint8 C-contiguous array is taken
+    if (!py::isinstance<py::array_t<uint8_t, py::array::c_style>>(decisions_obj))
+      throw std::invalid_argument("decisions must be a C-contiguous uint8 array");
+    dec_arr = py::reinterpret_borrow<py::array_t<uint8_t, py::array::c_style>>(decisions_obj);
+    if (!dec_arr.writeable()) throw std::invalid_argument("decisions must be writeable");
     if (dec_arr.size() < (py::ssize_t)((size_t)c * trims.size() * ms::kEqIters * P))
       throw std::invalid_argument("decisions buffer too small");
     dec = dec_arr.mutable_data();

@@ -351,9 +351,35 @@ class World:
 
     def _join_side(self) -> None:
         """The compute stream waits (device-side) for the genome chains issued so far."""
-        ev = self.__dict__.pop("_side_join", None)
+        d = self.__dict__
+        ev = d.pop("_side_join", None)
         if ev is not None:
             ev.wait()  # (the current stream)
+        # the tensors the chains were issued against may return to the allocator now: any later
+        # compute-stream allocation is ordered after the wait above
+        d.pop("_side_keep", None)
+
+    def _storage_refs(self) -> list:
+        """Every per-cell storage tensor a genome chain may read while it runs on the side stream
+        (columns and spares, genome / label arenas, kinetics row storage, its spares, the cell ->
+        row map and free list). Issuing a chain can replace some of them (storage growth, a row
+        recycle, an arena widening); holding these references until the compute stream has joined
+        the chains keeps a replaced block out of the caching allocator, which would otherwise hand
+        it to a compute-stream allocation while a side-stream kernel still reads it."""
+        refs: list = []
+        for col in self._cols.values():
+            refs.append(col.buf)
+            refs.append(col.spare)
+        for arena in (self._genomes, self._labels):
+            refs.append(arena.data)
+            refs.append(arena.lens)
+            refs.append(arena.__dict__.get("_spare"))
+        kd = self.kinetics.__dict__
+        refs.extend(kd.get("_store_d", {}).values())
+        refs.extend(kd.get("_spare", {}).values())
+        for k in ("_slot_buf", "_slot_spare", "_free", "_zero_row_t"):
+            refs.append(kd.get(k))
+        return refs
 
     def _flush_deferred(self) -> None:
         """Issue the queued genome ops, in call order, on a side stream: their chains run next to
@@ -380,14 +406,20 @@ class World:
         # molecule-only work issued since (e.g. the diffusion stencil they run next to)
         d.pop("_defer_event").wait(side_raw)
         d["_side_active"] = True  # (a decomposed world's exchanges use its side-stream communicator)
+        lazy = self._lazy_join() or (_LAZY_JOIN and "_n_pix_global" not in d)
+        # (the queued closures hold compute-stream tensors the chains read, e.g. index lists)
+        keep = [q, self._storage_refs()] if lazy else None
         try:
             with on_stream(side):
                 for fn in q:
                     fn()
         finally:
             d["_side_active"] = False
-            if self._lazy_join() or (_LAZY_JOIN and "_n_pix_global" not in d):
-                # joined at the next op that needs the chains' results (see _EAGER_CHAINS)
+            if lazy:
+                # joined at the next op that needs the chains' results (see _EAGER_CHAINS); what the
+                # chains read stays referenced until then (see _storage_refs)
+                prev = d.get("_side_keep")
+                d["_side_keep"] = keep if prev is None else (prev, keep)
                 d["_side_join"] = NEvent().record(side_raw)
             else:
                 join(main, side_raw)
@@ -521,11 +553,15 @@ class World:
         count from its pinned status slot and adopt the grown population."""
         from magicsoup_amd.ops import hip_ops
 
-        n0, slot, ev = self.__dict__.pop("_count_pending")
+        d = self.__dict__
+        n0, slot, ev = d["_count_pending"]
         if hip_ops._GUARD:
             hip_ops._GUARD[0]()  # (communicators alive: a peer failure raises instead of hanging)
         ev.synchronize()
         k = int(hip_ops._m().status_read(slot)[0])
+        # (the pending entry stays until the count is read: a failure above leaves it for a retry
+        # instead of a world whose device rows and host count disagree)
+        d["_count_pending"] = None
         hip_ops.check_placement()
         if k:
             self._adopt_count(n0 + k)
@@ -1335,7 +1371,7 @@ class World:
         save_state(self, Path(statedir))
 
     @_op("load_state")
-    def load_state(self, statedir: Path, ignore_cell_params: bool = False, restore_rng: bool = True):
+    def load_state(self, statedir: Path, ignore_cell_params: bool = False, restore_rng: bool = False):
         """Load a state written by :meth:`save_state` (re-translating genomes unless
         ``ignore_cell_params``). If the state holds an ``rng_state.pt`` (written by this package),
         the random streams are restored too (``restore_rng``), so the run continues exactly."""

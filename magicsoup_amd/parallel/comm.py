@@ -72,12 +72,21 @@ def _nbytes(t: torch.Tensor | None) -> int:
 
 
 class TorchComm:
-    """torch.distributed exchanges (``stage``: device tensors over gloo go through host copies)."""
+    """torch.distributed exchanges (``stage``: device tensors over gloo go through host copies).
+
+    ``tagless`` (default: ``MS_COMM_TAGLESS=1``) reproduces the matching contract of
+    :class:`RcclComm`: every point-to-point op uses tag 0 and the four ops are posted in exactly the
+    order ``rccl_exchange`` posts them (send up, send down, receive from down, receive from up,
+    ``csrc/hip/comm.hip``), so between two ranks sends and receives match by issue order alone,
+    as in RCCL. The tagged mode (up-bound messages tag 0, down-bound tag 1) would hide a protocol
+    whose correctness depends on that order; running the multi-rank tests in both modes pins the
+    RCCL contract on CPU (``tests/test_distributed.py``)."""
 
     native = False
 
-    def __init__(self, group, rank: int, size: int, stage: bool):
+    def __init__(self, group, rank: int, size: int, stage: bool, tagless: bool | None = None):
         self.group, self.rank, self.size, self.stage = group, rank, size, stage
+        self.tagless = os.environ.get("MS_COMM_TAGLESS", "0") == "1" if tagless is None else bool(tagless)
         glob = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
         self.up = glob((rank - 1) % size)
         self.down = glob((rank + 1) % size)
@@ -113,14 +122,15 @@ class TorchComm:
     def _p2p(self, to_up, to_down, from_down, from_up) -> None:
         ops = []
         g = self.group
+        t_dn = 0 if self.tagless else 1  # (tagless: matched by issue order, like RCCL)
         if to_up is not None:
             ops.append(dist.P2POp(dist.isend, to_up, self.up, g, 0))
         if to_down is not None:
-            ops.append(dist.P2POp(dist.isend, to_down, self.down, g, 1))
+            ops.append(dist.P2POp(dist.isend, to_down, self.down, g, t_dn))
         if from_down is not None:
             ops.append(dist.P2POp(dist.irecv, from_down, self.down, g, 0))
         if from_up is not None:
-            ops.append(dist.P2POp(dist.irecv, from_up, self.up, g, 1))
+            ops.append(dist.P2POp(dist.irecv, from_up, self.up, g, t_dn))
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 self._wait(req)

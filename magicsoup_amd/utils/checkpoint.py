@@ -8,13 +8,15 @@
 * ``rng_state.pt`` (new; the reference ignores unknown files and keeps no RNG state, SURVEY §2.8
   item 9) holds every random stream a step draws from: the device and host native streams
   (seed, calls drawn), torch's CPU / device generators, the placement helper's generator and
-  Python's ``random``. ``load_state`` restores it when present, so save -> load -> N steps equals N
-  uninterrupted steps (``tests/test_world.py::test_save_load_state_resumes_rng_streams``).
+  Python's ``random``. ``load_state(restore_rng=True)`` restores it (opt-in: by default, like the
+  reference, loading a state leaves every random stream alone, so replicate runs started from one
+  checkpoint diverge), and then save -> load -> N steps equals N uninterrupted steps (``tests/test_world.py::test_save_load_state_resumes_rng_streams``).
 * ``load_world_pickle`` restores :meth:`World.save` pickles -- this package's own and the
   reference's (``magicsoup.world.World`` with ``Conv2d`` diffusion kernels, ``world.py:161-204``) --
-  through a restricted unpickler: only the classes of ``magicsoup`` / ``magicsoup_amd``, torch's
-  tensor / parameter rebuild functions, dtypes and storages and a few builtin containers can be
-  named by the file; tensor storages are read with ``torch.load(weights_only=True)`` onto the
+  through a restricted unpickler: only an explicit list of data classes (World, Chemistry,
+  Molecule, Genetics, Kinetics and its map factories, the domain containers), torch's tensor /
+  parameter rebuild functions, dtypes and storages and a few builtin containers can be named by
+  the file, and only the rebuild functions and plain containers can be called by it; tensor storages are read with ``torch.load(weights_only=True)`` onto the
   requested device, like the reference's ``_CPU_Unpickler`` (``world.py:17-33``) but without
   executing anything else from the file. Reference pickles are converted to this package's layout
   (``reference_world_state`` / ``reference_kinetics_state``). No reference pickle ships with the
@@ -102,7 +104,7 @@ def _parse_fasta(text: str) -> tuple[list[str], list[str]]:
     return genomes, labels
 
 
-def load_state(world, statedir: Path, ignore_cell_params: bool = False, restore_rng: bool = True) -> None:
+def load_state(world, statedir: Path, ignore_cell_params: bool = False, restore_rng: bool = False) -> None:
     if world.n_cells > 0:
         world.kill_cells()
     dev = torch.device(world.device)
@@ -163,40 +165,85 @@ _BUILTINS = {
     ("torch", "Size"): torch.Size,
     ("torch", "device"): torch.device,
 }
-_OWN_PACKAGES = ("magicsoup", "magicsoup_amd")
+# the data classes a world pickle holds (module-relative names; ``magicsoup.*`` reference paths are
+# aliased onto these by the ``magicsoup`` package). Only these may be named by a file, and of them
+# only the plain containers may be *called* (REDUCE): the others are rebuilt with ``cls.__new__`` and
+# their state, never their constructor (a World / Kinetics constructor allocates device memory)
+_DATA_CLASSES = {
+    "models.containers": ("Molecule", "Chemistry", "CatalyticDomain", "TransporterDomain",
+                          "RegulatoryDomain", "Protein"),
+    "models.genetics": ("Genetics",),
+    "models.kinetics": ("Kinetics", "_HillMapFact", "_LogNormWeightMapFact", "_SignMapFact",
+                        "_VectorMapFact", "_ReactionMapFact", "_TransporterMapFact", "_RegulatoryMapFact"),
+    "models.world": ("World",),
+}
+# reference module paths (python/magicsoup/*.py) -> ours
+_REF_MODULES = {"containers": "models.containers", "genetics": "models.genetics",
+                "kinetics": "models.kinetics", "world": "models.world"}
 
 
-class _WorldUnpickler(pickle.Unpickler):
+def _allowed_class(module: str, name: str):
+    root, _, rest = module.partition(".")
+    if root == "magicsoup":
+        rest = _REF_MODULES.get(rest, rest)
+    elif root != "magicsoup_amd":
+        return None
+    if name not in _DATA_CLASSES.get(rest, ()):
+        return None
+    import importlib
+
+    return getattr(importlib.import_module(f"magicsoup_amd.{rest}"), name)
+
+
+class _WorldUnpickler(pickle._Unpickler):  # the pure-Python unpickler: its opcode table is reachable
     """Restricted unpickler for world pickles (ours and the reference's): see the module docstring
-    for what a file may name; anything else raises ``pickle.UnpicklingError``."""
+    for what a file may name; anything else raises ``pickle.UnpicklingError``. Besides the name
+    check (``find_class``), REDUCE -- calling an object the file named -- is refused for everything
+    but torch's tensor rebuild functions, the storage loader and the builtin containers."""
+
+    dispatch = dict(pickle._Unpickler.dispatch)
 
     def __init__(self, fh, map_location):
         super().__init__(fh)
         self._loc = map_location
+        self._callable: set[int] = set()
+
+    def _ok_call(self, obj):
+        self._callable.add(id(obj))
+        return obj
 
     def find_class(self, module, name):
         if module == "torch.storage" and name == "_load_from_bytes":
             loc = self._loc
-            return lambda b: torch.load(io.BytesIO(b), map_location=loc, weights_only=True)
+            return self._ok_call(lambda b: torch.load(io.BytesIO(b), map_location=loc, weights_only=True))
         if (module, name) in _TORCH_FUNCS:
-            return super().find_class(module, name)
+            return self._ok_call(super().find_class(module, name))
         if (module, name) in _BUILTINS:
-            return _BUILTINS[(module, name)]
+            return self._ok_call(_BUILTINS[(module, name)])
         if module == "torch" and isinstance(getattr(torch, name, None), torch.dtype):
             return getattr(torch, name)
         if module == "torch" and name.endswith("Storage") and name[:1].isupper():
             return super().find_class(module, name)
         if module.startswith("torch.nn.modules."):
             return _RefModule
-        root = module.split(".", 1)[0]
-        if root in _OWN_PACKAGES:
-            if root == "magicsoup":
+        cls = _allowed_class(module, name)
+        if cls is not None:
+            if module.startswith("magicsoup.") or module == "magicsoup":
                 import magicsoup  # noqa: F401 - installs the reference-path aliases
-            obj = super().find_class(module, name)
-            if isinstance(obj, type) and obj.__module__.split(".", 1)[0] == "magicsoup_amd":
-                return obj
-            raise pickle.UnpicklingError(f"{module}.{name} is not a magicsoup class")
+            if name in ("Molecule", "Chemistry"):
+                return self._ok_call(cls)  # plain containers (Molecule: __getnewargs__ by name)
+            return cls
         raise pickle.UnpicklingError(f"world pickles may not reference {module}.{name}")
+
+    def _load_reduce(self):
+        stack = self.stack
+        args = stack.pop()
+        func = stack[-1]
+        if id(func) not in self._callable:
+            raise pickle.UnpicklingError(f"world pickles may not call {func!r}")
+        stack[-1] = func(*args)
+
+    dispatch[pickle.REDUCE[0]] = _load_reduce
 
 
 def load_world_pickle(path: Path, device: str | None = None):

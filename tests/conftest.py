@@ -23,6 +23,19 @@ from magicsoup_amd.utils.util import random_genome  # noqa: E402
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X)")
     config.addinivalue_line("markers", "slow: long-running statistical / invariant checks")
+    config.addinivalue_line("markers", "one_comm_mode: multi-rank test run in the tagged comm mode only")
+
+
+@pytest.fixture(params=["tagged", "tagless"])
+def comm_mode(request, monkeypatch):
+    """Multi-rank CPU tests run twice: with tagged gloo point-to-point ops, and ``tagless`` -- every
+    op tag 0, posted in the order the RCCL exchange posts them (``MS_COMM_TAGLESS=1``,
+    magicsoup_amd.parallel.comm.TorchComm) -- which pins the issue-order matching contract RCCL
+    relies on. Spawned ranks inherit the environment."""
+    if request.param == "tagless" and request.node.get_closest_marker("one_comm_mode"):
+        pytest.skip("comm-mode independent")
+    monkeypatch.setenv("MS_COMM_TAGLESS", "1" if request.param == "tagless" else "0")
+    return request.param
 
 
 def pytest_collection_modifyitems(config, items):

@@ -5,9 +5,12 @@ reproduce its diffusion and enzymatic activity, and every lifecycle operation mu
 invariants (one cell per pixel, occupancy map consistent, molecules conserved)."""
 import tempfile
 
+import pytest
 import torch
 
 from tests.dist_utils import run_ranks
+
+pytestmark = pytest.mark.usefixtures("comm_mode")
 
 
 def _chem():
@@ -475,13 +478,44 @@ def _body_peer_failure(rank, ws, mode):
     raise AssertionError("a dead / stalled peer did not raise CommError")
 
 
+@pytest.mark.one_comm_mode
 def test_peer_death_raises_instead_of_hanging():
     """Fail-stop: when a neighbour rank exits mid-run, the surviving rank's next exchange raises
     CommError (gloo: closed connection) instead of hanging."""
     run_ranks(_body_peer_failure, 2, "exit", timeout=120)
 
 
+@pytest.mark.one_comm_mode
 def test_stalled_peer_times_out():
     """A neighbour that stops answering makes the waiting rank raise CommError after
     ``MS_COMM_TIMEOUT_S`` (here 4 s) instead of blocking forever."""
     run_ranks(_body_peer_failure, 2, "stall", timeout=120)
+
+
+# ---------------------------------------------------------------------------------------------
+def _body_exchange_contract(rank, ws):
+    """The exchange protocol's skip rule: a side that has nothing to send posts no op, and the peer
+    posts no matching receive; everything else still arrives where it belongs."""
+    import torch.distributed as dist
+
+    from magicsoup_amd.parallel.comm import TorchComm
+
+    c = TorchComm(None, rank, ws, stage=False)
+    # rank r sends (r, "up") up and (r, "down") down; rank 0 has nothing for its upper neighbour,
+    # so that neighbour (rank ws - 1) expects nothing from below
+    up_empty = rank == 0
+    to_up = torch.zeros(0) if up_empty else torch.full((3 + rank,), float(rank) + 0.25)
+    to_down = torch.full((5 + rank,), float(rank) + 0.5)
+    below, above = (rank + 1) % ws, (rank - 1) % ws
+    from_down = torch.zeros(0) if below == 0 else torch.empty(3 + below)
+    from_up = torch.empty(5 + above)
+    c.exchange(to_up, to_down, from_down, from_up)
+    if below != 0:
+        assert torch.equal(from_down, torch.full((3 + below,), float(below) + 0.25))
+    assert torch.equal(from_up, torch.full((5 + above,), float(above) + 0.5))
+    dist.barrier()
+
+
+@pytest.mark.parametrize("ws", [2, 3, 4])
+def test_exchange_skips_empty_ops_on_both_sides(ws):
+    run_ranks(_body_exchange_contract, ws)

@@ -3,9 +3,12 @@
 The reference's index semantics are the oracle (python/magicsoup/world.py): new cells are appended
 at the end (spawn 318, add 374, divide 451), kill shifts later indices down (506-510), move and
 reposition keep indices; cells are identified across ops by their unique random labels."""
+import pytest
 import torch
 
 from tests.dist_utils import run_ranks
+
+pytestmark = pytest.mark.usefixtures("comm_mode")
 from tests.test_distributed import _chem
 
 

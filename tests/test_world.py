@@ -452,7 +452,7 @@ def _evolve(w, steps):
 
 
 def test_save_load_state_resumes_rng_streams(tmp_path):
-    """save_state writes rng_state.pt; load_state restores it: save -> load -> N steps gives
+    """save_state writes rng_state.pt; load_state(restore_rng=True) restores it: save -> load -> N steps gives
     exactly what N uninterrupted steps give (placement, mutations, recombination, labels)."""
     from magicsoup_amd.examples.wood_ljungdahl import CHEMISTRY
 
@@ -468,7 +468,7 @@ def test_save_load_state_resumes_rng_streams(tmp_path):
     ms.set_seed(21)
     w2 = ms.World(chemistry=CHEMISTRY, map_size=24, seed=21)  # same codon / kinetics maps
     ms.set_seed(99)  # streams that would diverge without the restore
-    w2.load_state(tmp_path / "s")
+    w2.load_state(tmp_path / "s", restore_rng=True)
     _evolve(w2, 3)
     w2.spawn_cells([ms.random_genome(300) for _ in range(5)])
     assert list(w2.cell_genomes) == list(w.cell_genomes)
