@@ -1,0 +1,156 @@
+"""HBM sizing: what a world costs per pixel and per cell, and the largest config that fits a GPU.
+
+The reference keeps everything in one process on one device and never sizes anything
+(``python/magicsoup/world.py:195-204``: one (m, S, S) map, per-cell tensors grown by ``torch.cat``).
+Here a config is planned for the 288 GB of HBM3E of an MI355X (BASELINE.json ``configs[4]``: fp16
+maps "sized to fill 288 GB HBM per GPU across 8 GPUs"): :func:`footprint` models every device
+buffer a GPU world holds, :func:`plan` inverts the model (the largest map side whose strip fits each
+GPU of a decomposed world, for a cell density and genome size), and :func:`measured` walks a live
+world's tensors so the model is checked against reality (``tests/test_gpu_kernels.py``; the
+``hbm`` bench preset runs the planned config).
+
+Per pixel (owned rows of a rank, plus two halo rows when decomposed):
+
+* molecule map, ``m`` species x map dtype, twice: the stencil writes a second buffer and the two
+  are swapped (``ops/hip_ops.py`` diffuse);
+* occupancy map (1 B), placement claim map (int32) and cell-index map (int32, neighbour search /
+  recombination pairs).
+
+Per cell (capacity-managed buffers: up to 1.5x the live count, each with a spare of the same size
+for order-preserving compactions):
+
+* intracellular molecules (``m`` fp32), position (2 int32), lifetime and divisions (int32);
+* genome arena row (one byte per nt, the row width is the longest genome rounded up) + length, and
+  a label row (16 B);
+* the cell -> parameter-row map (int64) and the division / kill scratch of the native fast path;
+* parameter rows in compact storage: per (protein, signal) the packed N/Nf/Nb/A word (int32) and
+  Kmr (fp32), per protein Vmax/Kmf/Kmb/Ke (4 fp32), for the live cells plus the spare rows fresh
+  builds take (``models/kinetics.py`` ``_spare_rows``: up to 3n within 8 GiB).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+_ESIZE = {torch.float32: 4, torch.bfloat16: 2, torch.float16: 2, "fp32": 4, "bf16": 2, "fp16": 2}
+_CAP = 1.5  # capacity growth factor of the per-cell buffers (worst case right after a growth)
+_KIN_SPARE_BUDGET = 8 << 30  # bytes of spare parameter rows (models/kinetics.py _spare_rows)
+
+GiB = float(1 << 30)
+MI355X_HBM = 288e9  # bytes of HBM3E per GPU
+
+
+def _round_width(n: int) -> int:
+    from magicsoup_amd.models.strings import _round_width as rw
+
+    return rw(max(1, int(n)))
+
+
+def proteins_per_genome(genome_len: int) -> int:
+    """Protein slots ``P`` (the longest proteome of the population) for random genomes of
+    ``genome_len`` nt: about one protein per 21 nt at the tail of the distribution (24 slots at
+    500 nt, 40 at 1 kbp; SURVEY.md §2.3 measured p_max)."""
+    return max(8, int(math.ceil(genome_len / 21.0)))
+
+
+def footprint(map_size: int, n_molecules: int, cells: int, map_dtype=torch.float32, genome_len: int = 500,
+              p_max: int | None = None, ranks: int = 1, genome_width: int | None = None) -> dict:
+    """Modelled device bytes of one rank of a GPU world (``ranks`` > 1: a strip of a
+    domain-decomposed ``map_size``² world holding ``cells / ranks`` cells). Returns the per-part
+    breakdown and the total in bytes."""
+    m = int(n_molecules)
+    es = _ESIZE[map_dtype]
+    rows = math.ceil(map_size / ranks) + (2 if ranks > 1 else 0)
+    pix = rows * map_size
+    n = int(math.ceil(cells / ranks))
+    cap = int(n * _CAP)
+    P = p_max if p_max is not None else proteins_per_genome(genome_len)
+    s = 2 * m
+    width = genome_width if genome_width is not None else _round_width(int(genome_len * 1.25))
+    row_bytes = P * s * 8 + P * 16  # packed word + Kmr per (protein, signal); Vmax/Kmf/Kmb/Ke per protein
+    spare_rows = max(n // 8, min(3 * n, _KIN_SPARE_BUDGET // max(row_bytes, 1)), 1024)
+    parts = {
+        "molecule_map": pix * m * es * 2,
+        "pixel_maps": pix * (1 + 4 + 4),
+        "cell_columns": cap * (m * 4 + 8 + 4 + 4) * 2,
+        "genome_arena": cap * (width + 4) * 2,
+        "label_arena": cap * (16 + 4) * 2,
+        "row_maps": cap * (8 * 2 + 6 * 8 + 1),
+        "kinetics_rows": int((n + spare_rows) * row_bytes * 1.0),
+    }
+    parts["total"] = sum(parts.values())
+    parts.update(map_size=map_size, ranks=ranks, cells_per_rank=n, p_max=P, genome_width=width)
+    return parts
+
+
+def plan(hbm_bytes: float = MI355X_HBM, ranks: int = 8, n_molecules: int = 14, map_dtype="fp16",
+         cells_per_pixel: float = 1e6 / 16384**2, genome_len: int = 500, reserve: float = 0.12,
+         multiple: int = 256) -> dict:
+    """The largest map side ``S`` (a multiple of ``multiple``) whose per-rank share -- ``S / ranks``
+    owned rows plus halos, ``cells_per_pixel * S²`` cells spread over the ranks -- fits
+    ``hbm_bytes * (1 - reserve)`` on every GPU (the reserve covers the runtime, the RCCL buffers,
+    the genome pipeline's scratch and allocator fragmentation). Returns the config and its
+    :func:`footprint`."""
+    budget = hbm_bytes * (1.0 - reserve)
+
+    def cost(S: int) -> int:
+        return footprint(S, n_molecules, int(cells_per_pixel * S * S), map_dtype, genome_len, ranks=ranks)["total"]
+
+    lo, hi = multiple, multiple
+    while cost(hi) <= budget:
+        lo, hi = hi, hi * 2
+    while hi - lo > multiple:
+        mid = (lo + hi) // 2 // multiple * multiple
+        if mid <= lo:
+            break
+        if cost(mid) <= budget:
+            lo = mid
+        else:
+            hi = mid
+    fp = footprint(lo, n_molecules, int(cells_per_pixel * lo * lo), map_dtype, genome_len, ranks=ranks)
+    return {"map_size": lo, "cells": int(cells_per_pixel * lo * lo), "ranks": ranks, "map_dtype": str(map_dtype),
+            "n_molecules": n_molecules, "budget_bytes": int(budget), "per_rank": fp,
+            "fill": fp["total"] / hbm_bytes}
+
+
+def measured(world) -> dict:
+    """Device bytes held by a live world's own tensors (columns and spares, arenas, maps, kinetics
+    storage, scratch), each storage counted once; compare with :func:`footprint`."""
+    seen: set[int] = set()
+    total = {"bytes": 0}
+
+    def add(t):
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            st = t.untyped_storage()
+            key = st.data_ptr()
+            if key not in seen:
+                seen.add(key)
+                total["bytes"] += st.nbytes()
+        elif isinstance(t, dict):
+            for v in t.values():
+                add(v)
+        elif isinstance(t, (list, tuple)):
+            for v in t:
+                add(v)
+
+    d = world.__dict__
+    for k, v in d.items():
+        if k in ("kinetics", "genetics", "chemistry"):
+            continue
+        add(v)
+    for col in d.get("_cols", {}).values():
+        add(col.buf)
+        add(col.spare)
+    for a in (d.get("_genomes"), d.get("_labels")):
+        if a is not None:
+            add(a.data)
+            add(a.lens)
+            add(a.__dict__.get("_spare"))
+    sc = d.get("_hip_scratch")
+    if sc is not None:
+        add(getattr(sc, "bufs", {}))
+    kd = world.kinetics.__dict__
+    for k, v in kd.items():
+        add(v)
+    return {"bytes": total["bytes"]}
