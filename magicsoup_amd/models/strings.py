@@ -18,9 +18,6 @@ import torch
 _MIN_WIDTH = 16
 
 
-_HEADROOM_CAP = 16384
-
-
 def _round_width(n: int) -> int:
     w = _MIN_WIDTH
     while w < n:
@@ -44,14 +41,9 @@ def pack_strings(strs: list[str], width: int | None = None) -> tuple[np.ndarray,
 class StringArena:
     """Rows of bytes with per-row lengths and a row capacity (amortised O(1) appends)."""
 
-    def __init__(self, device, width: int = 64, capacity: int = 0, headroom: int = 1, initial_headroom: int = 1):
+    def __init__(self, device, width: int = 64, capacity: int = 0):
         self.device = torch.device(device)
         self.width = _round_width(width)
-        # widen to headroom x the needed width: a genome arena on the GPU widens while results of the
-        # device pipeline wait (their commit and the calls after it are replayed on the host), so
-        # growing recombinant genomes should hit that rarely (a row's unused bytes are never moved)
-        self.headroom = int(headroom)
-        self.initial_headroom = int(initial_headroom)  # ... while the arena is still empty
         self.data = torch.zeros(capacity, self.width, dtype=torch.uint8, device=self.device)
         self.lens = torch.zeros(capacity, dtype=torch.int32, device=self.device)
         self.n = 0
@@ -63,14 +55,7 @@ class StringArena:
         return int(self.data.size(0))
 
     def reserve(self, rows: int, width: int | None = None) -> None:
-        if width is None or _round_width(width) <= self.width:
-            width = self.width
-        else:
-            # headroom up to 16 knt rows (a request can be an already padded width: never compound)
-            hr = getattr(self, "headroom", 1)
-            if self.n == 0:
-                hr = max(hr, getattr(self, "initial_headroom", 1))
-            width = _round_width(max(width, min(width * hr, _HEADROOM_CAP)))
+        width = self.width if width is None or _round_width(width) <= self.width else _round_width(width)
         if rows <= self.capacity and width == self.width:
             return
         cap = max(rows, int(self.capacity * 1.5) + 16) if rows > self.capacity else self.capacity

@@ -48,38 +48,16 @@ _LABEL_LEN = 12
 # resolves them first
 _PIPELINE_SAFE_OPS = frozenset({"mutate_cells", "recombinate_cells", "diffuse_molecules", "degrade_molecules",
                                 "increment_cell_lifetimes"})
-# ops an early diffusion stencil (issued by kill_cells, adopted by diffuse_molecules) survives: they
-# neither read nor write the molecule map (degrade_molecules: once, see hip_ops.spec_diffuse_issue)
-_SPEC_DIFF_SAFE_OPS = frozenset({"divide_cells", "mutate_cells", "recombinate_cells", "degrade_molecules",
-                                 "diffuse_molecules", "increment_cell_lifetimes"})
 # ops that may run while the cell count of a division issued without a synchronisation
 # (divide_cells_t(lazy=True)) is still on its way to the host: they queue genome chains or only touch
 # the map / all capacity rows; diffuse_molecules adopts the count after its stencil launch
 _COUNT_SAFE_OPS = frozenset({"mutate_cells", "recombinate_cells", "degrade_molecules", "diffuse_molecules"})
 _CHECK_ENV = os.environ.get("MS_CHECK_INVARIANTS") == "1"
 _DEFER_ENV = os.environ.get("MS_DEFER_GENOME_OPS", "1")
-_FLUSH_EARLY = os.environ.get("MS_FLUSH_EARLY", "1") == "1"
-# MS_EAGER_CHAINS=1 (or World._early_chains = True; single-process GPU worlds): issue the genome
-# chains as soon as recombinate_cells / mutate_cells are called and join them into the compute stream
-# only at the next op that needs their results (every op outside _PIPELINE_SAFE_OPS). Off by
-# default: the flagship step got slower (1.25 -> 1.35 ms median, profiles/r2_s3/headroom_chains_ab.txt)
-# -- the default queues them until the diffusion stencil is launched and joins at once.
-_EAGER_CHAINS = os.environ.get("MS_EAGER_CHAINS", "0") == "1"
-# the compute stream joins the flushed chains at the next op that needs them (the activity, or a
-# read of genomes / parameters), not right after the flush: the molecule-only work in between (the
-# lifetimes, the loop's masks) runs while the chains finish (MS_LAZY_JOIN=0: join at the flush)
-_LAZY_JOIN = os.environ.get("MS_LAZY_JOIN", "1") == "1"
-# the same for the strips of a decomposed world (MS_EAGER_CHAINS_DIST=1): their activity is not
-# speculative, so it waits for the chains on the host; issued early they are done by then
-_EAGER_CHAINS_DIST = os.environ.get("MS_EAGER_CHAINS_DIST", "0") == "1"
-# genome arena row width = this x the longest genome when it (re)grows (GPU worlds; see StringArena).
-# 1 by default: wider rows removed the early widening events but made the flagship step slower
-# (profiles/r2_s3/headroom_chains_ab.txt)
-_GENOME_HEADROOM = int(os.environ.get("MS_GENOME_HEADROOM", "1"))
-# ... and for the first population (an empty arena): the first recombinants outgrow rows as wide as
-# the initial genomes within a few steps, and that widening replays the pipeline calls on the host
-_GENOME_HEADROOM_INIT = int(os.environ.get("MS_GENOME_HEADROOM_INIT", "1"))
-_WIDTH_WATCH = os.environ.get("MS_GENOME_WIDTH_WATCH", "0") == "1"  # opt-in, see World._watch_genome_width
+# The genome chains flushed onto the side stream (World._flush_deferred) are joined into the compute
+# stream at the next op that needs their results (the activity, or a read of genomes / parameters),
+# not right after the flush: the molecule-only work in between (the lifetimes, the loop's masks)
+# runs while the chains finish (single-process worlds; a strip of a decomposed world joins at once).
 
 
 def _op(name: str):
@@ -94,10 +72,6 @@ def _op(name: str):
             d = self.__dict__
             if d.get("_count_pending") is not None and name not in _COUNT_SAFE_OPS:
                 self._resolve_count()
-            if d.get("_spec_diff") is not None and name not in _SPEC_DIFF_SAFE_OPS:
-                from magicsoup_amd.ops import hip_ops
-
-                hip_ops.spec_diffuse_cancel(self)
             if d.get("_spec") is not None:
                 self._reconcile()  # a speculative activity is confirmed (or redone) before anything else
             if (d.get("_gp_state") or d.get("_deferred")) and name not in _PIPELINE_SAFE_OPS:
@@ -215,10 +189,6 @@ class World:
         seed: Optional seed of all native RNG streams (placement, mutation, recombination).
     """
 
-    # genome arena row width = this x the longest genome when it (re)grows on a GPU (StringArena)
-    _genome_headroom = _GENOME_HEADROOM
-    _genome_headroom_init = _GENOME_HEADROOM_INIT
-
     # domain-decomposition hooks of the op layer (set by magicsoup_amd.parallel.DistributedWorld)
     _exchange_map_halo = None
     _allreduce_flags = None
@@ -272,9 +242,7 @@ class World:
         dev = torch.device(device)
         m = self.n_molecules
         self.n_cells = 0
-        hr = type(self)._genome_headroom if dev.type == "cuda" else 1
-        hr0 = type(self)._genome_headroom_init if dev.type == "cuda" else 1
-        self._genomes = StringArena(dev, width=64, headroom=hr, initial_headroom=hr0)
+        self._genomes = StringArena(dev, width=64)
         self._labels = StringArena(dev, width=16)
         self._genome_col = StringColumn(self._genomes)
         self._label_col = StringColumn(self._labels)
@@ -321,14 +289,12 @@ class World:
         diffusion stencil; issuing the activity first keeps the device busy meanwhile. The state
         the activity changes is saved first; the next access to molecules, or the next op,
         confirms the calls and -- only if one had to be redone on the host -- restores that state
-        and runs the activity again with the corrected parameters. Single-process GPU worlds, and
-        decomposed ones only with ``MS_DIST_SPECULATE=1`` (their activity is collective, so the
-        confirmation is too: genome_pipeline.reconcile)."""
+        and runs the activity again with the corrected parameters. Single-process GPU worlds only: a
+        decomposed world's activity is collective, so a redo would have to be agreed by all ranks
+        (measured no faster than waiting for the chains, which its strips issue early anyway)."""
         d = self.__dict__
-        # (a decomposed world speculates when it can agree on a redo: every rank then rolls back
-        # and redoes its collective activity together, see genome_pipeline.reconcile)
         return (_DEFER_ENV != "0" and d.get("_timer") is None and self._genomes.data.is_cuda
-                and (getattr(self, "_allreduce_flags", None) is None or d.get("_agree_redo") is not None))
+                and getattr(self, "_allreduce_flags", None) is None)
 
     def _defer(self, fn) -> None:
         d = self.__dict__
@@ -338,16 +304,6 @@ class World:
 
             d["_defer_event"] = NEvent().record()
         q.append(fn)
-        if (d.get("_spec_diff") is not None and _FLUSH_EARLY) or self._lazy_join():
-            # nothing to wait for: the chains start now on the side stream (the next activity
-            # depends on them; an early diffusion stencil may be running already)
-            self._flush_deferred()
-
-    def _lazy_join(self) -> bool:
-        d = self.__dict__
-        if "_n_pix_global" in d:  # a strip of a decomposed world (magicsoup_amd.parallel)
-            return d.get("_early_chains", _EAGER_CHAINS_DIST)
-        return d.get("_early_chains", _EAGER_CHAINS)
 
     def _join_side(self) -> None:
         """The compute stream waits (device-side) for the genome chains issued so far."""
@@ -406,7 +362,7 @@ class World:
         # molecule-only work issued since (e.g. the diffusion stencil they run next to)
         d.pop("_defer_event").wait(side_raw)
         d["_side_active"] = True  # (a decomposed world's exchanges use its side-stream communicator)
-        lazy = self._lazy_join() or (_LAZY_JOIN and "_n_pix_global" not in d)
+        lazy = "_n_pix_global" not in d  # (see the note at the top of this module)
         # (the queued closures hold compute-stream tensors the chains read, e.g. index lists)
         keep = [q, self._storage_refs()] if lazy else None
         try:
@@ -416,8 +372,8 @@ class World:
         finally:
             d["_side_active"] = False
             if lazy:
-                # joined at the next op that needs the chains' results (see _EAGER_CHAINS); what the
-                # chains read stays referenced until then (see _storage_refs)
+                # joined at the next op that needs the chains' results; what the chains read stays
+                # referenced until then (see _storage_refs)
                 prev = d.get("_side_keep")
                 d["_side_keep"] = keep if prev is None else (prev, keep)
                 d["_side_join"] = NEvent().record(side_raw)
@@ -448,10 +404,6 @@ class World:
                 self._reconcile()
             return cols[name].view(d["n_cells"])
         if name == "molecule_map" and "_molmap" in d:
-            if d.get("_spec_diff") is not None:
-                from magicsoup_amd.ops import hip_ops
-
-                hip_ops.spec_diffuse_cancel(self)  # the caller may read or write the map
             if d.get("_spec") is not None:
                 self._reconcile()
             if d.get("_pending_scale") is not None or d.get("_pending_corr") is not None:
@@ -476,10 +428,6 @@ class World:
             cols[name].adopt(t, int(t.size(0)))
             return
         if name == "molecule_map":
-            if self.__dict__.get("_spec_diff") is not None:
-                from magicsoup_amd.ops import hip_ops
-
-                hip_ops.spec_diffuse_cancel(self)
             t = torch.as_tensor(value, device=self.device)
             want = self.__dict__.get("map_dtype", torch.float32)
             if t.dtype != want or not t.is_contiguous():
@@ -1001,24 +949,14 @@ class World:
             # spill, survivor selection and the order-preserving compaction of every per-cell
             # buffer (into the spares and back) in one native call, launched against the
             # device-side survivor count before the one stream sync that brings it to the host
-            early = hip_ops.EARLY_DIFFUSE_AT == "spill" and self.__dict__.get("_early_diffuse", hip_ops._SPEC_DIFF_ENV == "1")
-            if early:
-                # the map is final for this step's diffusion after the spill: its stencil starts on
-                # a side stream, next to the compaction and the division that usually follow
-                # (adopted by diffuse_molecules; see hip_ops.spec_diffuse_issue)
-                world_ops.spill_and_free_mask(self, dead)
-                hip_ops.spec_diffuse_issue(self)
             fw = self._fast_world(n)
-            mm, corr = hip_ops.map_for_pixels(self) if not early else (self.__dict__["_molmap"], None)
+            mm, corr = hip_ops.map_for_pixels(self)
             mask = dead.view(torch.uint8) if dead.dtype == torch.bool else dead.to(torch.uint8)
             slot = hip_ops._m().fast_kill(fw, n, mask.contiguous().data_ptr(), mm.data_ptr(), hip_ops._mdt(mm),
-                                          hip_ops._p(corr), not early, hip_ops._stream())
+                                          hip_ops._p(corr), True, hip_ops._stream())
             n_new = hip_ops.wait_count(slot)
-            if hip_ops.EARLY_DIFFUSE_AT == "synced":
-                hip_ops.spec_diffuse_issue(self)  # (the compaction is done: only the division runs next to it)
             if n_new != n:
                 self._adopt_count(n_new)
-                self._watch_genome_width()
             return
         world_ops.spill_and_free_mask(self, dead)
         keep = ~dead
@@ -1026,35 +964,6 @@ class World:
         if int(keep_idx.numel()) == n:
             return
         self._compact(keep_idx, keep)
-
-    def _watch_genome_width(self) -> None:
-        """Widen the genome arena before the device pipeline's results outgrow it. A recombinant can
-        be as long as both parents together, and a result that does not fit its row makes the
-        pipeline skip the calls after it: the host then commits and replays them and redoes the
-        speculative activity (2-20 ms). Every 4th GPU kill queues the longest genome's length into
-        pinned memory (no synchronisation); once it has arrived and exceeds 3/4 of the row width, the
-        rows double (a copy of the used rows; the pipeline is reconciled at this point). Opt-in
-        (MS_GENOME_WIDTH_WATCH=1): it removes the replays from the spike log, but five alternating
-        driver-style pairs ran 2 % slower with it (profiles/r2_s3/width_watch_ab.txt)."""
-        d = self.__dict__
-        g = self._genomes
-        if not _WIDTH_WATCH or not g.data.is_cuda or "_n_pix_global" in d:
-            return
-        w = d.get("_gw_watch")
-        if w is not None and w[1].query():
-            d["_gw_watch"] = None
-            if 4 * int(w[0][0]) > 3 * g.width and 2 * g.width <= 65535 and not (d.get("_gp_state") or {}).get("pending"):
-                g.reserve(g.n, 2 * g.width)
-        cnt = d.get("_gw_count", 0) + 1
-        d["_gw_count"] = cnt
-        if d.get("_gw_watch") is None and cnt % 4 == 0 and g.n > 0:
-            buf = d.get("_gw_pinned")
-            if buf is None:
-                buf = d["_gw_pinned"] = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-            buf.copy_(g.lens[: g.n].max().view(1), non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            d["_gw_watch"] = (buf, ev)
 
     def _compact(self, keep_idx: torch.Tensor, keep: torch.Tensor | None, removed: torch.Tensor | None = None) -> None:
         n_new = int(keep_idx.numel())
@@ -1140,10 +1049,7 @@ class World:
         d = self.__dict__
         st = d.get("_gp_state")
         spec = save = None
-        # a decomposed world speculates on every rank (the confirmation is collective), unless this
-        # is the redo of a rolled-back activity
-        collective = d.get("_agree_redo") is not None and not d.pop("_redo_activity", False) and self._speculate()
-        if (st and st["pending"]) or collective:
+        if st and st["pending"]:
             # speculative: issued on top of unconfirmed parameter rebuilds (see _speculate); the
             # fused activity snapshots what it changes in its own input pass
             from magicsoup_amd.ops import hip_ops
@@ -1290,10 +1196,6 @@ class World:
 
     def __getstate__(self):
         self._reconcile()
-        if self.__dict__.get("_spec_diff") is not None:
-            from magicsoup_amd.ops import hip_ops
-
-            hip_ops.spec_diffuse_cancel(self)
         state = self.__dict__.copy()
         n = self.n_cells
         for k in ("_genome_col", "_label_col"):
@@ -1306,8 +1208,8 @@ class World:
         state["_pending_scale"] = None
         state["_pending_corr"] = None
         for k in ("_hip_scratch", "_idx_map", "_diff_w", "_perm_t", "_degrade_t", "_gp_state", "_deferred",
-                  "_side_stream", "_defer_event", "_gp_cache", "_spec", "_spec_diff", "_spec_diff_miss",
-                  "_diff_stream", "_halo_stream", "_side_join", "_gw_watch", "_gw_pinned", "_fw", "_fw_key", "_fw_bufs"):
+                  "_side_stream", "_defer_event", "_gp_cache", "_spec", "_halo_stream", "_side_join",
+                  "_side_keep", "_fw", "_fw_key", "_fw_bufs"):
             state.pop(k, None)
         return state
 
@@ -1327,9 +1229,7 @@ class World:
         self.__dict__["_cols"] = {k: _Column(v.to(dev)) for k, v in cols.items()}
         for c in self._cols.values():
             c.view(int(c.buf.size(0)))
-        hr = type(self)._genome_headroom if dev.type == "cuda" else 1
-        hr0 = type(self)._genome_headroom_init if dev.type == "cuda" else 1
-        self.__dict__["_genomes"] = StringArena(dev, width=64, headroom=hr, initial_headroom=hr0)
+        self.__dict__["_genomes"] = StringArena(dev, width=64)
         self.__dict__["_labels"] = StringArena(dev, width=16)
         self._genomes.append_strings(genomes)
         self._labels.append_strings(labels)

@@ -357,42 +357,21 @@ def _recommit(world, pd: _Pending) -> torch.Tensor:
     return torch.unique(rows)
 
 
-NO_STATE = object()  # the speculation marker of a decomposed world's rank without cells (nothing to restore)
-
-
 def reconcile(world) -> None:
     """Resolve pending device-pipeline calls, in issue order: adopt the device row counter,
     commit results that did not fit the arena (then replay the calls that were skipped because of
     it), and rebuild flagged cells on the synchronous path. An enzymatic_activity that was issued
-    on top of the pending calls (World: speculative activity) is undone and run again if any of
-    this changed parameters.
-
-    A decomposed world (``_agree_redo``, magicsoup_amd.parallel) speculates on every rank; the
-    confirmation is collective: one MAX all-reduce of "this rank changed parameters" makes the redo
-    a job-wide decision, and every rank then restores its state and redoes the (collective)
-    activity together."""
+    on top of the pending calls (World: speculative activity, single-process worlds) is undone and
+    run again if any of this changed parameters."""
     d = world.__dict__
     st = d.get("_gp_state")
     spec = d.pop("_spec", None)
-    agree = d.get("_agree_redo") if spec is not None else None
     pend = st["pending"] if st else []
-    if not pend and agree is None:
+    if not pend:
         return
-    if st:
-        st["pending"] = []
-    redo = _resolve(world, pend) if pend else False
-    if agree is not None:
-        redo = agree(redo)
+    st["pending"] = []
+    redo = _resolve(world, pend)
     if not redo or spec is None:
-        return
-    if agree is not None:
-        if spec is not NO_STATE:
-            hip_ops.restore_cell_state(world, spec)
-        d["_redo_activity"] = True  # (the redo itself is not speculative)
-        try:
-            world.enzymatic_activity()
-        finally:
-            d.pop("_redo_activity", None)
         return
     from magicsoup_amd.ops import world_ops
 

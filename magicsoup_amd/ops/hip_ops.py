@@ -353,8 +353,6 @@ def cell_state_buffer(world) -> torch.Tensor:
 def save_cell_state(world) -> torch.Tensor:
     """Snapshot of what enzymatic_activity changes (cell molecules, raw pixel values under the
     cells) into a scratch buffer, for :func:`restore_cell_state`."""
-    if world.__dict__.get("_spec_diff") is not None:
-        spec_diffuse_cancel(world)
     d = world.__dict__
     n, m = world.n_cells, world.n_molecules
     mm = d["_molmap"]
@@ -366,8 +364,6 @@ def save_cell_state(world) -> torch.Tensor:
 
 
 def restore_cell_state(world, buf: torch.Tensor) -> None:
-    if world.__dict__.get("_spec_diff") is not None:
-        spec_diffuse_cancel(world)
     d = world.__dict__
     n, m = world.n_cells, world.n_molecules
     mm = d["_molmap"]
@@ -412,8 +408,6 @@ def map_for_pixels(world):
     pending degradation is applied first (together with any correction, one full pass); a pending
     correction alone is handed to the kernel (maps.hip corr_in / corr_out)."""
     d = world.__dict__
-    if d.get("_spec_diff") is not None:
-        spec_diffuse_cancel(world)  # the caller reads or writes pixels: an early stencil is void
     if d.get("_pending_scale") is not None:
         apply_pending(world)
     return d["_molmap"], d.get("_pending_corr")
@@ -426,8 +420,6 @@ def diffuse(world) -> None:
     refreshes its halo rows first and all-reduces the totals (see magicsoup_amd.parallel)."""
     R, C, r_lo, r_hi, wrap = geom(world)
     d = world.__dict__
-    if d.get("_spec_diff") is not None and _spec_diffuse_adopt(world):
-        return
     halo = getattr(world, "_exchange_map_halo", None)
     # a strip exchanging over RCCL: the interior rows' stencil runs while the halo rows travel (the
     # exchange on a stream of its own), the two boundary rows after they arrived
@@ -515,98 +507,6 @@ def _diff_weights(world):
     return w
 
 
-# ---------------------------------------------------------------------------- early diffusion
-# The reference's step runs kill -> divide -> recombinate / mutate -> degrade -> diffuse
-# (performance/run_simulation.py:57-100). The stencil only needs the map after the kill's spill:
-# divisions, genome operations and lifetimes never touch the map, and the degradation it fuses is a
-# per-species factor known in advance. So kill_cells issues the stencil of "degrade, then diffuse"
-# right after its spill, on a side stream, into the spare map buffer; it then runs next to the
-# kill's compaction and the division (host-synchronised and launch-bound, so the device is mostly
-# idle there). diffuse_molecules adopts the result (a buffer swap, bit for bit what it would have
-# computed) when exactly that happened in between: one degrade_molecules, no other op that reads or
-# writes the map or its pending state. Anything else voids it (the main stream then waits for the
-# side stream, so the spare buffer is free again) and the normal path runs.
-# Off by default (MS_EARLY_DIFFUSE=1 or World._early_diffuse = True turn it on): in paired A/Bs on
-# one evolving flagship world (scripts/early_ab.py) the overlap was cancelled by contention -- the
-# HBM-bound stencil slows the compaction's row gather (20 -> 80-120 us) and the division's
-# placement (47 -> 108 us), which sit before host synchronisations, and the genome chains it used to
-# hide lose their cover (profiles/r2_s3/early_ab.txt).
-_SPEC_DIFF_ENV = os.environ.get("MS_EARLY_DIFFUSE", "0")
-# where kill_cells issues it: right after the spill ("spill") or after the compaction's sync ("synced")
-EARLY_DIFFUSE_AT = os.environ.get("MS_EARLY_DIFFUSE_AT", "spill")
-
-
-def spec_diffuse_issue(world) -> None:
-    d = world.__dict__
-    if (not d.get("_early_diffuse", _SPEC_DIFF_ENV == "1") or d.get("_spec_diff") is not None
-            or d.get("_pending_scale") is not None or d.get("_timer") is not None
-            or "_n_pix_global" in d):  # (single-process worlds only)
-        return
-    # a loop without diffusion after its kills would only waste the stencil: after two voided
-    # speculations in a row, try again on every 32nd kill only
-    miss = d.get("_spec_diff_miss", 0)
-    if miss >= 2:
-        d["_spec_diff_miss"] = miss + 1
-        if miss % 32:
-            return
-    R, C, r_lo, r_hi, wrap = geom(world)
-    mm = d["_molmap"]
-    m = int(mm.size(0))
-    sc = _scratch(world)
-    dev = mm.device
-    tmp = sc.get("diff_tmp", mm.numel(), mm.dtype, dev)
-    partials = sc.get("diff_partials_s", int(_m().diffuse_partials_len(m, C, r_hi - r_lo)), torch.float64, dev)
-    totals = sc.get("diff_totals_s", 2 * m, torch.float64, dev)
-    corr = d.get("_pending_corr")
-    # the new correction goes to a buffer that is not the pending one (main-stream readers of the
-    # pending correction may still run before the adoption or a voiding)
-    c0 = sc.get("diff_corr_s0", m, torch.float32, dev)
-    new_corr = sc.get("diff_corr_s1", m, torch.float32, dev) if corr is not None and corr.data_ptr() == c0.data_ptr() else c0
-    f = _degrade_factors(world)
-    w = _diff_weights(world)
-    side = d.get("_diff_stream")
-    if side is None:
-        side = d["_diff_stream"] = torch.cuda.Stream(device=dev)
-    side.wait_stream(torch.cuda.current_stream(dev))
-    n_pix = float(R * C if wrap else (r_hi - r_lo) * C)
-    with torch.cuda.stream(side):
-        _m().diffuse_stencil(m, R, C, r_lo, r_hi, wrap, _p(mm), _p(tmp), _p(w[1]), _p(w[2]), _p(f), _p(corr),
-                             _p(partials), _p(totals), _mdt(mm), 0, _stream(), _p(new_corr), n_pix)
-        ev = torch.cuda.Event()
-        ev.record(side)
-    d["_spec_diff"] = {"ev": ev, "mm": mm, "f": f, "corr": corr, "w": w, "tmp": tmp, "new_corr": new_corr,
-                       "degraded": False}
-
-
-def spec_diffuse_cancel(world) -> None:
-    """Void a pending early stencil: the main stream waits for it (its buffers are free again)."""
-    d = world.__dict__
-    sd = d.pop("_spec_diff", None)
-    if sd is None:
-        return
-    torch.cuda.current_stream(sd["mm"].device).wait_event(sd["ev"])
-    d["_spec_diff_miss"] = max(1, d.get("_spec_diff_miss", 0) + 1)
-
-
-def _spec_diffuse_adopt(world) -> bool:
-    d = world.__dict__
-    sd = d["_spec_diff"]
-    ok = (sd["degraded"] and d["_molmap"] is sd["mm"] and d.get("_pending_scale") is sd["f"]
-          and d.get("_pending_corr") is sd["corr"] and _diff_weights(world) is sd["w"])
-    if not ok:
-        spec_diffuse_cancel(world)
-        return False
-    d.pop("_spec_diff")
-    mm = sd["mm"]
-    torch.cuda.current_stream(mm.device).wait_event(sd["ev"])
-    d["_molmap"] = sd["tmp"].view(mm.shape)
-    _scratch(world).bufs["diff_tmp"] = mm.view(-1)
-    d["_pending_scale"] = None
-    d["_pending_corr"] = sd["new_corr"]
-    d["_spec_diff_miss"] = 0
-    return True
-
-
 def health_flags(world) -> torch.Tensor:
     mm = world.molecule_map
     R, C, r_lo, r_hi, _ = geom(world)
@@ -655,12 +555,6 @@ def degrade(world) -> None:
     elif world.n_cells > 0:
         cm = world.cell_molecules
         cm.mul_(f)
-    sd = world.__dict__.get("_spec_diff")
-    if sd is not None:
-        if sd["degraded"]:
-            spec_diffuse_cancel(world)  # the early stencil fused exactly one degradation
-        else:
-            sd["degraded"] = True
     pend = world.__dict__.get("_pending_scale")
     # the cached factor tensor itself (pending factors are only ever read or replaced, never
     # written in place)
@@ -670,8 +564,6 @@ def degrade(world) -> None:
 def apply_pending(world) -> None:
     """Materialise a pending correction and / or degradation of the map (one full pass)."""
     d = world.__dict__
-    if d.get("_spec_diff") is not None:
-        spec_diffuse_cancel(world)
     f, corr = d.get("_pending_scale"), d.get("_pending_corr")
     if f is None and corr is None:
         return

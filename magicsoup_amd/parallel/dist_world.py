@@ -92,11 +92,6 @@ def _copy_maps(dst: World, src: World) -> None:
         setattr(kin, name, mp)
 
 
-# MS_DIST_SPECULATE=1: speculative activity in decomposed GPU worlds, confirmed collectively
-# (genome_pipeline.reconcile). Off by default: measured no faster (virtual-strip A/Bs, flagship
-# 1.56-1.64 vs 1.54-1.56 ms, N = 8 proxy 0.92-1.07 vs 0.84-0.89 ms, profiles/r3/dist_spec/): the
-# host wait it removes overlaps device work (the genome chains) rather than leaving the GPU idle
-_DIST_SPECULATE = os.environ.get("MS_DIST_SPECULATE", "0") == "1"
 # issue the boundary recombination's collective part at the recombinate_cells() call (MS_XB_EARLY=0:
 # at the flush after the diffusion stencil, as before)
 _XB_EARLY = os.environ.get("MS_XB_EARLY", "1") != "0"
@@ -123,10 +118,6 @@ class DistributedWorld(World):
     halo rows) is what the kernels work on; :meth:`global_positions`, :meth:`owned_molecule_map`,
     :meth:`gather` and :meth:`scatter_from` convert to and from the global picture.
     """
-
-    # record exchanges append rows as wide as the sender's arena: no headroom (it would compound)
-    _genome_headroom = 1
-    _genome_headroom_init = 1
 
     def __init__(self, *args, group=None, exact_global_exit: bool = True, boundary_genome_cap: int = 2048,
                  strips: bool | None = None, **kwargs):
@@ -191,9 +182,6 @@ class DistributedWorld(World):
             g["_exchange_map_halo"] = self._do_exchange_map_halo
             if exact_global_exit:
                 g["_allreduce_flags"] = self._do_allreduce_flags
-                if g["_halo_async"] and _DIST_SPECULATE:
-                    # speculative activity with a collective confirmation (genome_pipeline.reconcile)
-                    g["_agree_redo"] = self._do_agree_redo
             g["_allreduce_totals"] = self._do_allreduce_totals
             self._exchange_occupancy()  # first p2p call is collective on every rank
             self._do_exchange_map_halo()
@@ -324,17 +312,6 @@ class DistributedWorld(World):
     def _do_allreduce_totals(self, totals: torch.Tensor) -> None:
         self._all_reduce(totals, dist.ReduceOp.SUM)
 
-    def _do_agree_redo(self, redo: bool) -> bool:
-        """MAX of every rank's "my pipeline calls changed parameters" (collective, one read-back:
-        it waits for the speculative activity, which the kill after it waits for anyway)."""
-        from magicsoup_amd.ops import hip_ops
-
-        t = hip_ops._scratch(self).get("agree_redo", 1, torch.int32, self._tensor_device())
-        t.fill_(1 if redo else 0)
-        self._all_reduce(t, dist.ReduceOp.MAX)
-        hip_ops.guarded_sync()
-        return bool(int(t.item()))
-
     # ------------------------------------------------------------------ cell records
     def _records(self, cells: torch.Tensor, ys: torch.Tensor, child: bool) -> tuple[torch.Tensor, tuple[int, int]]:
         """Full records of ``cells`` landing on columns ``ys`` of a neighbour's boundary row: the
@@ -434,12 +411,9 @@ class DistributedWorld(World):
             from magicsoup_amd.models.kinetics import _INCREMENTS, _TRIMS
 
             if self._molmap.is_cuda:
-                from magicsoup_amd.ops import genome_pipeline, hip_ops
+                from magicsoup_amd.ops import hip_ops
 
                 hip_ops.integrate_idle(self, _TRIMS)
-                d = self.__dict__
-                if d.get("_agree_redo") is not None and not d.get("_redo_activity") and self._speculate():
-                    d["_spec"] = genome_pipeline.NO_STATE  # (joins the collective confirmation)
                 return
             for _ in _TRIMS:
                 hook(torch.zeros(len(_INCREMENTS), dtype=torch.int32, device=self._tensor_device()))

@@ -324,70 +324,3 @@ def _body_native_xb(rank, ws):
 
 def test_gpu_native_boundary_recombination_matches_python_protocol():
     run_ranks(_body_native_xb, 1, timeout=300, backend="nccl")
-
-
-def _body_dist_speculation(rank, ws):
-    """One rank over RCCL (virtual strips): the decomposed world's speculative activity (issued on
-    top of unconfirmed genome chains, confirmed by a collective MAX of "parameters changed", rolled
-    back and redone on every rank together) evolves exactly like the round-2 protocol that confirms
-    the chains on the host before every activity. One domain slot per protein in the pipeline's
-    token layout makes every call rebuild on the host, so the rollback runs in every step."""
-    import magicsoup_amd as ms
-    from magicsoup_amd.ops import genome_pipeline
-    from magicsoup_amd.parallel import DistributedWorld
-    from magicsoup_amd.parallel import dist_world as dwm
-    from tests.conftest import gen_genomes
-
-    ms.set_seed(8)
-    torch.manual_seed(8)
-    w = ms.World(chemistry=_chem(), map_size=64, seed=8, device="cpu")
-    w.spawn_cells(gen_genomes(900, 300))
-    atp = _chem().molname_2_idx["ATP"]
-    genome_pipeline.D_CAP = 1
-    redos = []
-    orig = genome_pipeline._resolve
-
-    def spy(world, pend):
-        r = orig(world, pend)
-        redos.append(r)
-        return r
-
-    genome_pipeline._resolve = spy
-    out = {}
-    try:
-        for spec in (True, False):
-            dwm._DIST_SPECULATE = spec
-            dw = DistributedWorld(chemistry=_chem(), map_size=64, seed=9, device="cuda", strips=True)
-            assert (dw.__dict__.get("_agree_redo") is not None) == spec
-            dw.adopt_maps(w)
-            dw.scatter_from(w, maps=False)
-            ms.set_seed(21)
-            torch.manual_seed(21)
-            redos.clear()
-            for _ in range(4):
-                dw.enzymatic_activity()
-                assert (dw.__dict__.get("_spec") is not None) == spec
-                dw.kill_cells(dw.cell_molecules[:, atp] < 0.3)
-                dw.divide_cells_t(dw.cell_molecules[:, atp] > 3.0)
-                dw.recombinate_cells(p=1e-4)
-                dw.mutate_cells(p=1e-3)
-                dw.degrade_molecules()
-                dw.diffuse_molecules()
-            dw.enzymatic_activity()
-            torch.cuda.synchronize()
-            out[spec] = (dw.cell_molecules.cpu(), dw.cell_positions.cpu(), list(dw.cell_genomes),
-                         dw.owned_molecule_map().cpu(), dw.kinetics.Vmax.cpu(), any(redos))
-            dw.close()
-    finally:
-        dwm._DIST_SPECULATE = True
-        genome_pipeline.D_CAP = 12
-        genome_pipeline._resolve = orig
-    a, b = out[True], out[False]
-    assert a[5]  # host rebuilds happened, i.e. the speculative activities were rolled back and redone
-    assert a[2] == b[2]
-    for x, y in zip(a[:2] + a[3:5], b[:2] + b[3:5]):
-        assert torch.equal(x, y)
-
-
-def test_gpu_decomposed_speculative_activity_matches_host_confirmation():
-    run_ranks(_body_dist_speculation, 1, timeout=300, backend="nccl")

@@ -692,19 +692,6 @@ def test_deferred_genome_ops_match_immediate_issue(monkeypatch):
     assert not w.__dict__["_deferred"]
     genomes = list(w.cell_genomes)
     assert not w.__dict__.get("_gp_state", {}).get("pending") and len(genomes) == w.n_cells
-    # eager chains (MS_EAGER_CHAINS=1): issued at once on the side stream, joined into the compute
-    # stream only by the next op that needs them (degrade / diffuse run next to them)
-    w = copy.deepcopy(base)
-    w.__dict__["_early_chains"] = True
-    w.recombinate_cells(p=1e-4)
-    w.mutate_cells(p=1e-3)
-    assert not w.__dict__.get("_deferred") and w.__dict__.get("_side_join") is not None
-    w.degrade_molecules()
-    w.diffuse_molecules()
-    assert w.__dict__.get("_side_join") is not None
-    genomes = list(w.cell_genomes)
-    assert w.__dict__.get("_side_join") is None
-    assert not w.__dict__.get("_gp_state", {}).get("pending") and len(genomes) == w.n_cells
 
 
 def test_widening_proteins_keeps_parameters_in_slot_mode():
