@@ -11,7 +11,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <stdexcept>
+#include <string_view>
 
 #include "host_common.h"
 
@@ -218,7 +220,59 @@ void diffuse_correct(farr mol_map, farr out, py::array_t<double, py::array::c_st
   }
 }
 
+// Strings concatenated in `joined` (lengths `lens`) -> zero-padded rows (n, width): the bulk upload
+// format of the genome / label arenas (models/strings.py pack_strings), one pass instead of a
+// Python slice assignment per string.
+barr pack_rows(py::bytes joined, iarr lens, int64_t width) {
+  std::string_view buf = joined;
+  const int64_t n = lens.shape(0);
+  const int32_t* L = lens.data();
+  std::vector<int64_t> off((size_t)n + 1, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    if (L[i] < 0 || L[i] > width) throw std::invalid_argument("pack_rows: a string is longer than the row width");
+    off[(size_t)i + 1] = off[(size_t)i] + L[i];
+  }
+  if (off[(size_t)n] != (int64_t)buf.size()) throw std::invalid_argument("pack_rows: lengths do not add up");
+  barr out({n, width});
+  uint8_t* o = out.mutable_data();
+  const char* src = buf.data();
+  {
+    py::gil_scoped_release nogil;
+#pragma omp parallel for schedule(static) if (n > 256)
+    for (int64_t i = 0; i < n; ++i) {
+      uint8_t* row = o + i * width;
+      std::memcpy(row, src + off[(size_t)i], (size_t)L[i]);
+      std::memset(row + L[i], 0, (size_t)(width - L[i]));
+    }
+  }
+  return out;
+}
+
+// The inverse of pack_rows: the first lens[i] bytes of every row, concatenated (one buffer the
+// caller decodes once and slices into strings).
+py::bytes unpack_rows(barr rows, iarr lens) {
+  if (rows.ndim() != 2 || lens.shape(0) != rows.shape(0)) throw std::invalid_argument("unpack_rows: shapes");
+  const int64_t n = rows.shape(0), w = rows.shape(1);
+  const int32_t* L = lens.data();
+  std::vector<int64_t> off((size_t)n + 1, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    if (L[i] < 0 || L[i] > w) throw std::invalid_argument("unpack_rows: a length exceeds the row width");
+    off[(size_t)i + 1] = off[(size_t)i] + L[i];
+  }
+  std::string out((size_t)off[(size_t)n], '\0');
+  const uint8_t* src = rows.data();
+  char* dst = out.data();
+  {
+    py::gil_scoped_release nogil;
+#pragma omp parallel for schedule(static) if (n > 256)
+    for (int64_t i = 0; i < n; ++i) std::memcpy(dst + off[(size_t)i], src + i * w, (size_t)L[i]);
+  }
+  return py::bytes(out);
+}
+
 void bind_world(py::module_& m) {
+  m.def("unpack_rows", &unpack_rows, "first lens[i] bytes of every uint8 row, concatenated");
+  m.def("pack_rows", &pack_rows, "concatenated strings + lengths -> zero-padded uint8 rows (n, width)");
   m.def("get_neighbors", &get_neighbors);
   m.def("divide_cells", &divide_cells);
   m.def("move_cells", &move_cells);

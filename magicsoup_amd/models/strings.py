@@ -27,15 +27,18 @@ def _round_width(n: int) -> int:
 
 
 def pack_strings(strs: list[str], width: int | None = None) -> tuple[np.ndarray, np.ndarray]:
-    """Pack strings into a zero-padded uint8 array (n, width) and int32 lengths."""
-    data = [s.encode("ascii") for s in strs]
-    lens = np.fromiter((len(d) for d in data), dtype=np.int32, count=len(data))
-    w = int(lens.max()) if len(data) else 0
+    """Pack strings into a zero-padded uint8 array (n, width) and int32 lengths: one join + encode
+    of all strings and one native pass writing the rows (host core ``pack_rows``)."""
+    strs = strs if isinstance(strs, list) else list(strs)
+    lens = np.fromiter(map(len, strs), dtype=np.int32, count=len(strs))
+    w = int(lens.max()) if len(strs) else 0
     width = max(width or 0, _round_width(max(w, 1)))
-    buf = bytearray(len(data) * width)
-    for i, d in enumerate(data):
-        buf[i * width : i * width + len(d)] = d
-    return np.frombuffer(bytes(buf), dtype=np.uint8).reshape(len(data), width).copy(), lens
+    joined = "".join(strs).encode("ascii")
+    if len(joined) != int(lens.sum(dtype=np.int64)):
+        raise ValueError("genomes and labels must be ASCII strings")
+    from magicsoup_amd.ops import native
+
+    return native.host().pack_rows(joined, lens, width), lens
 
 
 class StringArena:
@@ -161,6 +164,9 @@ class StringArena:
 
     # ---------------------------------------------------------------- materialisation
     def to_strings(self, rows: Iterable[int] | None = None) -> list[str]:
+        """The strings of all rows (or of ``rows``): the rows (cut to the longest string) are copied
+        to the host in one transfer, the host core concatenates their used bytes, and that buffer is
+        decoded once; the strings are slices of it."""
         if rows is None:
             data, lens = self.data[: self.n], self.lens[: self.n]
         else:
@@ -168,12 +174,18 @@ class StringArena:
             data, lens = self.data[idx], self.lens[idx]
         if data.numel() == 0:
             return [""] * int(lens.numel())
-        lmax = int(lens.max().item()) if lens.numel() else 0
-        arr = data[:, :lmax].cpu().numpy()
-        ls = lens.cpu().numpy()
-        raw = arr.tobytes()
-        w = arr.shape[1]
-        return [raw[i * w : i * w + int(l)].decode("ascii") for i, l in enumerate(ls)]
+        ls = lens.cpu()
+        lmax = int(ls.max()) if ls.numel() else 0
+        if lmax == 0:
+            return [""] * int(ls.numel())
+        from magicsoup_amd.ops import native
+
+        # rows cut to the longest string, one transfer; the host core concatenates the used bytes
+        sub = data[:, :lmax].contiguous().cpu().numpy()
+        raw = native.host().unpack_rows(sub, ls.numpy().astype(np.int32, copy=False)).decode("ascii")
+        ends = np.cumsum(ls.numpy(), dtype=np.int64).tolist()
+        starts = [0] + ends[:-1]
+        return [raw[a:b] for a, b in zip(starts, ends)]
 
 
 class StringColumn:

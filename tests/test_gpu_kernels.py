@@ -122,9 +122,21 @@ def test_integrator_matches_host_core():
     X = torch.cat([wc.cell_molecules, wc.molecule_map[:, pos[:, 0], pos[:, 1]].T], dim=1).contiguous()
     Xc = wc.kinetics.integrate_signals(X)
     Xg = wg.kinetics.integrate_signals(X.cuda()).cpu()
-    # same algorithm, same operation order, no FMA contraction on either side
-    close = torch.isclose(Xg, Xc, rtol=1e-5, atol=1e-6).all(dim=1)
-    assert close.float().mean() > 0.99, close.float().mean()
+    # same algorithm and operation order, no FMA contraction on either side; the device's exp / pow
+    # may differ from the host libm by an ulp, which can only matter where a damping decision sits
+    # on its Q/Ke threshold. Decision-aware: every cell whose decisions all clear the thresholds by
+    # a relative margin of 1e-4 (float64 population oracle) must agree to 1e-5; no blanket allowance.
+    import numpy as np
+
+    from tests.test_kinetics import _oracle_population
+
+    close = torch.isclose(Xg, Xc, rtol=1e-5, atol=1e-6).all(dim=1).numpy()
+    kin = wc.kinetics
+    params = [{k: getattr(kin, k)[c].double().numpy() for k in ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax",
+                                                               "Ke")} for c in range(X.size(0))]
+    _, border = _oracle_population(params, X.double().numpy(), (0.7, 0.2, 0.1), 4, margin=1e-4)
+    border = np.array(border)
+    assert close[~border].all(), np.nonzero(~close & ~border)
     assert wg.kinetics.last_masks == wc.kinetics.last_masks
 
 
@@ -910,6 +922,12 @@ def test_parameter_rows_follow_genomes_through_bench_steps(monkeypatch, recycle)
             kin = w.kinetics
             kin.__dict__["_nrows"] = kin._row_limit()[0]
         bench.step(w, 3000, 500, atp)
+        # the step's genome chains were flushed onto the side stream and are joined lazily (at the
+        # next activity): compute-stream allocations of storage-sized blocks now must not receive
+        # storage the chains' issue replaced (a recycle / growth inside the flush) while they still
+        # read it (World._storage_refs keeps it referenced until the join)
+        junk = [torch.full_like(t, 3) for t in w.kinetics.__dict__["_store_d"].values()]
+        del junk
         w.mutate_cells(p=1e-4)
         w.recombinate_cells(p=1e-5)
     w._reconcile()
