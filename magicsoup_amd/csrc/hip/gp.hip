@@ -335,7 +335,107 @@ int gp_rebuild(const GpArena& a, const GpGen& g, const GpKin& k, uintptr_t cells
   return rebuild(cap, cells, cnt, a, g, k, dcap, c, cnt, S_(stream));
 }
 
+// ---- recombinate_cells() + mutate_cells() as one chain (the reference loop calls them back to
+// back, performance/run_simulation.py:92-93): the recombination is applied and committed, the point
+// mutations are drawn over the recombined genomes and committed, and the union of the changed cells
+// is translated and built ONCE (a cell's parameters are a function of its final genome). Against two
+// separate calls this drops one translation + build (and its zero / check launches) from the side
+// stream, which is what the next activity waits for.
+
+// union list: recombined cells, then mutated ones (a cell in both is built twice into two fresh rows
+// from the same final genome; either row is right) + the parts' status {pairs, rec flags, mutated,
+// mut flags} into a pinned slot
+__global__ void __launch_bounds__(256) gp_union_kernel(int ucap, int mcap, const int* rec_cnt, const int64_t* rec_cells,
+                                                       const int* mut_cnt, const int64_t* mut_sel, int64_t* cells,
+                                                       int* cnt_u, const int* rec_pairs, const int* rec_opflags,
+                                                       const int* mut_opflags, long long* parts_status) {
+  const int cr = *rec_cnt, cm = min(*mut_cnt, mcap);
+  const int nr = min(cr, ucap), nm = min(cm, ucap - nr);
+  for (int j = threadIdx.x; j < nr; j += blockDim.x) cells[j] = rec_cells[j];
+  for (int j = threadIdx.x; j < nm; j += blockDim.x) cells[nr + j] = mut_sel[j];
+  if (threadIdx.x == 0) {
+    cnt_u[0] = nr + nm;
+    parts_status[0] = *rec_pairs;
+    parts_status[1] = __hip_atomic_load(rec_opflags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    parts_status[2] = *mut_cnt;
+    parts_status[3] = __hip_atomic_load(mut_opflags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ void gp_begin3_kernel(int* f0, int* f1, int* f2, int* gflags, long long* d_rows, long long nrows, int fresh) {
+  *f0 = 0;
+  *f1 = 0;
+  *f2 = 0;
+  if (fresh) {
+    *gflags = 0;
+    *d_rows = nrows;
+  }
+}
+
+size_t gp_evolve_union_bytes(int ucap, int P, int dcap, int L) {
+  Carve c(0);
+  c.take(8 * (size_t)ucap);  // union cells
+  c.take(16);                // union count
+  return c.off + rebuild_bytes(ucap, P, dcap, L) + 512;
+}
+
+// ar / am / au: the recombination's, the mutation's and the union rebuild's counters (the arena
+// fields are the same in all three). Returns (union status slot {count, flags, row counter, count},
+// parts status slot {pairs, rec flags, mutated, mut flags}).
+std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpArena& au, const GpGen& g, const GpKin& k,
+                              uintptr_t keys, py::object nbr, double p_rec, uint64_t seed_r, uint64_t call_r, int pcap,
+                              double p, double p_indel, double p_del, uint64_t seed_m, uint64_t call_m, int mcap,
+                              int kcap, int dcap, uintptr_t mark, uint64_t gen, uintptr_t blob_r, uintptr_t blob_m,
+                              uintptr_t blob_u, bool fresh, long long nrows, uintptr_t stream) {
+  hipStream_t s = S_(stream);
+  const int n = ar.n, L = ar.width;
+  gp_begin3_kernel<<<1, 1, 0, s>>>(P_<int>(ar.opflags), P_<int>(am.opflags), P_<int>(au.opflags), P_<int>(ar.gflags),
+                                   P_<long long>(ar.d_rows), nrows, fresh ? 1 : 0);
+  MS_LAUNCH_CHECK();
+  // recombination (gp_recombine's layout of blob_r, without its rebuild)
+  const int nr = 2 * pcap, out_w = 2 * L, parts_cap = kcap + 2;
+  Carve cr(blob_r);
+  const uintptr_t kk = cr.take(4 * 8 * (size_t)n), sel = cr.take(8 * 8 * (size_t)n);
+  const uintptr_t out = cr.take((size_t)nr * out_w), out_len = cr.take(4 * (size_t)nr), out_rows = cr.take(8 * (size_t)nr);
+  const uintptr_t parts = cr.take(4 * (size_t)pcap * parts_cap * 3);
+  const uintptr_t won = cr.take((size_t)nr), q = cr.take(8 * (size_t)nr), cells = cr.take(8 * (size_t)nr);
+  const auto t = nbr.cast<std::tuple<uintptr_t, int, int, int, int, int, uintptr_t>>();
+  rec_slots(n, std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t), std::get<4>(t), std::get<5>(t),
+            std::get<6>(t), ar.lens, p_rec, seed_r, call_r, kcap, ar.gflags, ar.opflags, keys, kk, sel, ar.cnt, pcap,
+            stream);
+  rec_apply(pcap, ar.cnt, sel, 0, keys, ar.data, L, ar.lens, kk, seed_r, call_r, parts, parts_cap, out, out_w, out_len,
+            out_rows, stream);
+  arena_scatter(nr, ar.cnt, 2, out_rows, out, out_w, out_len, ar.data, L, ar.lens, mark, gen, won, ar.gflags,
+                ar.opflags, stream);
+  select_indices_dev(nr, kSelSet, won, 0, q, 0, ar.cnt2, stream);
+  gather_dev(nr, ar.cnt2, q, out_rows, cells, stream);
+  // point mutations over the recombined genomes (gp_mutate's layout of blob_m, without its rebuild)
+  Carve cm(blob_m);
+  const uintptr_t mk = cm.take(4 * (size_t)n), msel = cm.take(8 * (size_t)n);
+  const int mout_w = (L + kcap + 15) / 16 * 16;
+  const uintptr_t mout = cm.take((size_t)mcap * mout_w), mout_len = cm.take(4 * (size_t)mcap);
+  mut_count(n, 0, am.lens, p, seed_m, call_m, mk, kcap, am.gflags, am.opflags, stream);
+  select_indices_capped(n, kSelI32Pos, mk, msel, am.cnt, mcap, am.gflags, am.opflags, stream);
+  mut_apply(mcap, am.cnt, msel, 0, am.data, L, am.lens, mk, p_indel, p_del, seed_m, call_m, mout, mout_w, mout_len,
+            stream);
+  arena_scatter(mcap, am.cnt, 1, msel, mout, mout_w, mout_len, am.data, L, am.lens, 0, 0, 0, am.gflags, am.opflags,
+                stream);
+  // union of the changed cells -> one translation + build
+  const int ucap = nr + mcap;
+  Carve cu(blob_u);
+  const uintptr_t ucells = cu.take(8 * (size_t)ucap), ucnt = cu.take(16);
+  auto ps = status_slot();
+  gp_union_kernel<<<1, 256, 0, s>>>(ucap, mcap, P_<int>(ar.cnt2), P_<int64_t>(cells), P_<int>(am.cnt),
+                                    P_<int64_t>(msel), P_<int64_t>(ucells), P_<int>(ucnt), P_<int>(ar.cnt),
+                                    P_<int>(ar.opflags), P_<int>(am.opflags), ps.first);
+  MS_LAUNCH_CHECK();
+  const int slot_u = rebuild(ucap, ucells, ucnt, au, g, k, dcap, cu, ucnt, s);
+  return {slot_u, ps.second};
+}
+
 void bind_gp(py::module_& m) {
+  m.def("gp_evolve", &gp_evolve, "device-pipeline recombinate_cells() + mutate_cells() with one rebuild (no sync)");
+  m.def("gp_evolve_union_bytes", &gp_evolve_union_bytes);
   py::class_<GpArena>(m, "GpArena", py::module_local())
       .def(py::init<>())
       .def_readwrite("data", &GpArena::data).def_readwrite("lens", &GpArena::lens)

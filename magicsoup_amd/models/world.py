@@ -60,6 +60,19 @@ _DEFER_ENV = os.environ.get("MS_DEFER_GENOME_OPS", "1")
 # runs while the chains finish (single-process worlds; a strip of a decomposed world joins at once).
 
 
+class _Deferred:
+    """A queued all-cells genome operation (World._defer): the call, plus its kind ("rec" / "mut")
+    and rates so that a recombination followed by a mutation can be issued as one device chain."""
+
+    __slots__ = ("fn", "kind", "args")
+
+    def __init__(self, fn, kind: str, args: tuple):
+        self.fn, self.kind, self.args = fn, kind, args
+
+    def __call__(self):
+        return self.fn()
+
+
 def _op(name: str):
     """Instrument a public World operation: roctx range (``MS_ROCTX=1``), per-op HIP-event timing
     (:meth:`World.enable_timings`) and invariant checks after the op (:meth:`World.set_debug_checks`
@@ -305,6 +318,11 @@ class World:
             d["_defer_event"] = NEvent().record()
         q.append(fn)
 
+    def _evolve(self, p_rec: float, p: float, p_indel: float, p_del: float) -> bool:
+        from magicsoup_amd.ops import genome_pipeline
+
+        return genome_pipeline.evolve(self, p_rec, p, p_indel, p_del)
+
     def _join_side(self) -> None:
         """The compute stream waits (device-side) for the genome chains issued so far."""
         d = self.__dict__
@@ -367,8 +385,15 @@ class World:
         keep = [q, self._storage_refs()] if lazy else None
         try:
             with on_stream(side):
-                for fn in q:
-                    fn()
+                i = 0
+                while i < len(q):
+                    # recombinate_cells() then mutate_cells(): one chain with one rebuild (gp_evolve)
+                    if (i + 1 < len(q) and getattr(q[i], "kind", None) == "rec" and getattr(q[i + 1], "kind", None) == "mut"
+                            and self.n_cells >= 2 and self._evolve(q[i].args[0], *q[i + 1].args)):
+                        i += 2
+                        continue
+                    q[i]()
+                    i += 1
         finally:
             d["_side_active"] = False
             if lazy:
@@ -1092,7 +1117,7 @@ class World:
         if self._n_floor() == 0 and self.n_cells == 0:
             return
         if cell_idxs is None and self._defer_genome_op():
-            self._defer(lambda: self._mutate_all(p, p_indel, p_del))
+            self._defer(_Deferred(lambda: self._mutate_all(p, p_indel, p_del), "mut", (p, p_indel, p_del)))
             return
         if cell_idxs is None:
             return self._mutate_all(p, p_indel, p_del)
@@ -1123,7 +1148,7 @@ class World:
         if self._n_floor() < 2 and self.n_cells < 2:
             return
         if cell_idxs is None and self._defer_genome_op():
-            self._defer(lambda: self._recombinate_all(p))
+            self._defer(_Deferred(lambda: self._recombinate_all(p), "rec", (p,)))
             return
         self._recombinate_all(p, cell_idxs)
 

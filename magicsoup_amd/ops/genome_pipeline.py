@@ -308,6 +308,118 @@ def recombinate_all(world, p: float, extra=None) -> bool:
     return True
 
 
+class _Part:
+    """One half of a merged ``evolve`` call, shaped like a :class:`_Pending` for :func:`_recommit`."""
+
+    __slots__ = ("kind", "host", "replay")
+
+    def __init__(self, kind, host, replay):
+        self.kind, self.host, self.replay = kind, host, replay
+
+
+class _PartHost:
+    """Status words of one half of an ``evolve`` call: the parts slot holds {pairs, rec flags,
+    mutated, mut flags}; presented as {count, flags, -, pairs} like a single call's slot."""
+
+    __slots__ = ("parts", "kind")
+
+    def __init__(self, parts: _StatusSlot, kind: str):
+        self.parts, self.kind = parts, kind
+
+    def __getitem__(self, i: int) -> int:
+        if self.kind == "rec":
+            return {0: 0, 1: self.parts[1], 2: 0, 3: self.parts[0]}[i]
+        return {0: self.parts[2], 1: self.parts[3], 2: 0, 3: self.parts[2]}[i]
+
+
+def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float) -> bool:
+    """``recombinate_cells(p=p_rec)`` followed by ``mutate_cells(p, p_indel, p_del)`` over all cells
+    as ONE device chain (gp.hip gp_evolve): both are applied and committed in order, then the union
+    of the changed cells is translated and built once -- the same genomes and parameters as the two
+    calls one after the other, with one translation + build less on the side stream. False if either
+    call should take its own path (rates above the pipeline's usage rule, a decomposed world's
+    boundary recombination, too few cells)."""
+    arena = world._genomes
+    n = world.n_cells
+    if n < 2 or "_n_pix_global" in world.__dict__:
+        return False
+    L = int(arena.width)
+    exp_rec = 8 * n * p_rec * 2 * L
+    if p_rec * 2 * L > 1.0 or p * L > 1.0 or not _usable(world, exp_rec) or not _usable(world, n * p * L):
+        return False
+    st = _state(world)
+    if any(pd.kind in ("rec", "mut", "evo") for pd in st["pending"]):
+        reconcile(world)
+    dev = arena.data.device
+    pcap = _cap(exp_rec, min(n, N_CAP) // 2)
+    mcap = _cap(n * p * L, min(n, N_CAP))
+    kin = world.kinetics
+    fresh = not st["pending"]
+    if fresh:
+        kin._reserve_rows(2 * min(n, N_CAP))
+    br, bm, bu = _bufs(world, "rec"), _bufs(world, "mut"), _bufs(world, "evo")
+    ar, am, au = _arena_desc(world, br), _arena_desc(world, bm), _arena_desc(world, bu)
+    sc = hip_ops._scratch(world)
+    keys, nbr = hip_ops.neighbor_slot_args(world)
+    k = _kin_desc(world, dev)
+    blob_r = _blob(world, "rec", _m().gp_blob_bytes(1, n, pcap, k.P, L, D_CAP, K_CAP, 0), dev)
+    blob_m = _blob(world, "mut", _m().gp_blob_bytes(0, n, mcap, k.P, L, D_CAP, K_CAP, 0), dev)
+    ucap = 2 * pcap + mcap
+    blob_u = _blob(world, "evo", _m().gp_evolve_union_bytes(ucap, k.P, D_CAP, L), dev)
+    mark = sc.bufs.get("arena_mark")
+    if mark is None or mark.numel() < arena.n:
+        mark = sc.bufs["arena_mark"] = torch.zeros(max(arena.n, 1024) * 2, dtype=torch.int64, device=dev)
+        sc.bufs["arena_gen"] = 0
+    gen = sc.bufs["arena_gen"] = sc.bufs.get("arena_gen", 0) + 1
+    rng_r, rng_m = _rng(), _rng()
+    slot_u, slot_p = _m().gp_evolve(ar, am, au, _gen_desc(world, dev), k, _p(keys), nbr, float(p_rec), rng_r[0],
+                                    rng_r[1], pcap, float(p), float(p_indel), float(p_del), rng_m[0], rng_m[1], mcap,
+                                    K_CAP, D_CAP, _p(mark), int(gen), _p(blob_r), _p(blob_m), _p(blob_u), fresh,
+                                    int(kin.__dict__["_nrows"]), _stream())
+    lay_r = _m().gp_layout(1, n, pcap, L, K_CAP, 0)
+    lay_m = _m().gp_layout(0, n, mcap, L, K_CAP, 0)
+    parts = _StatusSlot(slot_p)
+    replay = {
+        "rec": _Part("rec", _PartHost(parts, "rec"), _Replay(blob_r, lay_r, lay_r["nr"], "out_rows", mark=mark, gen=gen)),
+        "mut": _Part("mut", _PartHost(parts, "mut"), _Replay(blob_m, lay_m, mcap, "sel")),
+    }
+    cells = _view(blob_u, 0, ucap, torch.int64)
+    _record(world, "evo", (p_rec, p, p_indel, p_del), (rng_r, rng_m), cells, slot_u, replay)
+    return True
+
+
+def _resolve_evo(world, pd) -> bool:
+    """Reconcile a merged ``evolve`` call: each half like a call of its own (replay when skipped,
+    re-commit when a result outgrew the arena), then the union's translation flags."""
+    p_rec, p, p_indel, p_del = pd.args
+    rng_r, rng_m = pd.rng
+    rec, mut = pd.replay["rec"], pd.replay["mut"]
+    fr, fm = int(rec.host[1]), int(mut.host[1])
+    if (fr | fm) & _F_CAPACITY:
+        raise RuntimeError("genome pipeline capacity exceeded (rates far above the pipeline's usage rule)")
+    changed = []
+    rebuilt = False
+    if fr & (_F_SKIPPED | _F_WIDTH):
+        rebuilt = True
+        if fr & _F_SKIPPED:
+            changed.append(hip_ops.recombinate_all(world, p_rec, rng=rng_r))
+        else:
+            changed.append(_recommit(world, rec))
+    if fm & _F_SKIPPED:  # (also whenever the recombination overflowed: the chain stopped there)
+        rebuilt = True
+        changed.append(hip_ops.point_mutations(world, None, p, p_indel, p_del, rng=rng_m))
+    elif fm & _F_WIDTH:
+        rebuilt = True
+        changed.append(_recommit(world, mut))
+    if int(pd.host[1]) & (_F_TRANSLATE | _F_ROWS):
+        rebuilt = True
+        changed.append(pd.cells[: int(pd.host[0])])
+    changed = [c for c in changed if c.numel()]
+    if changed:
+        world._update_params_rows(torch.unique(torch.cat([c.to(torch.long) for c in changed])))
+    return rebuilt
+
+
 def rebuild_rows(world, rows: torch.Tensor) -> bool:
     """Translate and build parameters of the cells ``rows`` (e.g. spawned cells, or cells that
     arrived from another rank) into fresh parameter rows without a synchronisation (one C++ call,
@@ -386,6 +498,9 @@ def _resolve(world, pend: list) -> bool:
     pend[-1].event.synchronize()
     kin.__dict__["_nrows"] = max(int(kin.__dict__["_nrows"]), int(pend[-1].host[2]))
     for pd in pend:
+        if pd.kind == "evo":
+            rebuilt |= _resolve_evo(world, pd)
+            continue
         flags = int(pd.host[1])
         if flags & _F_CAPACITY:
             raise RuntimeError("genome pipeline capacity exceeded (rates far above the pipeline's usage rule)")

@@ -583,7 +583,10 @@ def test_device_genome_pipeline_arena_overflow_replay(monkeypatch):
         st = world.__dict__.get("_gp_state")
         if st and st["pending"]:
             st["pending"][-1].event.synchronize()
-            seen.extend(int(pd.host[1]) for pd in st["pending"])
+            for pd in st["pending"]:
+                seen.append(int(pd.host[1]))
+                if pd.kind == "evo":  # (a merged recombinate + mutate call: the halves' flags)
+                    seen.extend(int(pd.replay[h].host[1]) for h in ("rec", "mut"))
         orig(world)
 
     from magicsoup_amd.models.strings import StringArena, StringColumn
@@ -648,6 +651,60 @@ def test_device_genome_pipeline_matches_sync_path(monkeypatch, d_cap):
         assert torch.equal(p0[k][:, :P], p1[k][:, :P]), k
         if p1[k].size(1) > P:
             assert not p1[k][:, P:].any(), k
+    assert torch.equal(x0, x1)
+
+
+@pytest.mark.parametrize("mode", ["plain", "overflow", "capacity", "dcap"])
+def test_merged_recombinate_mutate_chain_matches_separate_calls(monkeypatch, mode):
+    """recombinate_cells() + mutate_cells() queued back to back run as one device chain with one
+    rebuild of the union of changed cells (genome_pipeline.evolve, gp.hip gp_evolve): same genomes,
+    parameters and trajectory as two separate pipeline calls -- also when results outgrow the arena
+    (re-commit + replay), when the selections exceed the call capacities (replay of both halves), and
+    when proteomes exceed the token slots (union rebuilt on the host)."""
+    import magicsoup_amd.models.world as world_mod
+    from magicsoup_amd.models.strings import StringArena, StringColumn
+    from magicsoup_amd.ops import genome_pipeline
+
+    calls = []
+    orig = genome_pipeline.evolve
+
+    def spy(world, *a):
+        ok = orig(world, *a)
+        calls.append(ok)
+        return ok
+
+    def tighten(w):
+        n = w._genomes.n
+        tight = StringArena(w._genomes.data.device, width=512)
+        tight.reserve(n)
+        tight.data[:n] = w._genomes.data[:n, :512]
+        tight.lens[:n] = w._genomes.lens[:n]
+        tight.n = n
+        w.__dict__["_genomes"] = tight
+        w.__dict__["_genome_col"] = StringColumn(tight)
+
+    kw = dict(steps=4)
+    if mode == "overflow":
+        base = _world("cuda", map_size=64, n=0, seed=5)
+        base.spawn_cells([ms.random_genome(512) for _ in range(600)])
+        kw.update(mut_kw={"p": 1.5e-3, "p_indel": 1.0, "p_del": 0.0}, rec_p=2e-4, prep=tighten)
+    else:
+        base = _world("cuda", map_size=64, n=800, s=400, seed=7)
+    if mode == "capacity":
+        monkeypatch.setattr(genome_pipeline, "_cap", lambda expected, limit: 2)
+    d_cap = 1 if mode == "dcap" else None
+    monkeypatch.setattr(world_mod.World, "_evolve", lambda self, *a: False)
+    g0, p0, x0 = _genetics_run(monkeypatch, base, sync=False, d_cap=d_cap, **kw)
+    monkeypatch.undo()
+    if mode == "capacity":
+        monkeypatch.setattr(genome_pipeline, "_cap", lambda expected, limit: 2)
+    monkeypatch.setattr(genome_pipeline, "evolve", spy)
+    g1, p1, x1 = _genetics_run(monkeypatch, base, sync=False, d_cap=d_cap, **kw)
+    assert calls and all(calls), calls  # the merged chain ran
+    assert g0 == g1
+    for k in p0:
+        P = min(p0[k].size(1), p1[k].size(1))
+        assert torch.equal(p0[k][:, :P], p1[k][:, :P]), k
     assert torch.equal(x0, x1)
 
 
