@@ -172,13 +172,18 @@ __global__ void __launch_bounds__(kSplitThreads) place_split_write_kernel(int k,
 
 // ---------------------------------------------------------------- cell records
 // Record layout (4-byte words): y, genome length, label length, divisions, lifetime, m molecules,
-// then the label row (lw bytes) and the genome row (gw bytes); lw, gw are multiples of 4.
+// then the label row (lw bytes) and the genome (gw bytes: the sender's genome length bound, zero
+// padded); lw, gw are multiples of 4. Genomes come from / go to the genome pool (hip_common.h).
 struct RecCols {
   float* mols;
   int32_t* pos;
   int32_t* life;
   int32_t* div;
-  uint8_t* gdata;
+  uint8_t* pool;
+  int64_t* off;
+  unsigned long long* top;
+  long long pool_cap;
+  int* pool_failed;
   int32_t* glen;
   int gw;
   uint8_t* ldata;
@@ -215,9 +220,10 @@ __global__ void __launch_bounds__(64) rec_pack_kernel(int k_up, int k_dn, const 
   const uint32_t* ls = reinterpret_cast<const uint32_t*>(w.ldata + (size_t)c * w.lw);
   uint32_t* ld = reinterpret_cast<uint32_t*>(r + 4 * (5 + w.m));
   for (int q = lane; q < w.lw / 4; q += 64) ld[q] = ls[q];
-  const uint32_t* gs = reinterpret_cast<const uint32_t*>(w.gdata + (size_t)c * w.gw);
-  uint32_t* gd = reinterpret_cast<uint32_t*>(r + 4 * (5 + w.m) + w.lw);
-  for (int q = lane; q < w.gw / 4; q += 64) gd[q] = gs[q];
+  const uint8_t* gs = w.pool + w.off[c];
+  uint8_t* gd = r + 4 * (5 + w.m) + w.lw;
+  const int gl = min(w.glen[c], w.gw);
+  for (int q = lane; q < w.gw; q += 64) gd[q] = q < gl ? gs[q] : 0;
 }
 
 // Append k_up records from the upper neighbour (landing on row 1) and k_dn from the lower one
@@ -250,7 +256,21 @@ __global__ void __launch_bounds__(64) rec_unpack_kernel(int n0, int k_up, const 
   const uint8_t* ls = r + 4 * (5 + w.m);
   for (int q = lane; q < w.lw; q += 64) w.ldata[c * w.lw + q] = q < ll ? ls[q] : 0;
   const uint8_t* gs = ls + slw;
-  for (int q = lane; q < w.gw; q += 64) w.gdata[c * w.gw + q] = q < gl ? gs[q] : 0;
+  // the genome into fresh pool space (the host made room for every record before the launch)
+  long long o = 0;
+  if (lane == 0) o = pool_alloc(w.top, w.pool_cap, gl);
+  o = (long long)(((unsigned long long)(unsigned)__shfl((int)(o >> 32), 0) << 32) |
+                  (unsigned long long)(unsigned)__shfl((int)(o & 0xFFFFFFFFll), 0));
+  if (o < 0) {
+    if (lane == 0) {
+      if (w.pool_failed) atomicOr(w.pool_failed, 1);
+      w.off[c] = 0;
+      w.glen[c] = 0;
+    }
+    return;
+  }
+  for (int q = lane; q < gl; q += 64) w.pool[o + q] = gs[q];
+  if (lane == 0) w.off[c] = o;
 }
 
 // ---------------------------------------------------------------- diffusion halo rows
@@ -289,7 +309,7 @@ __device__ __forceinline__ int strip_cell_at(const int32_t* idx_map, const int32
 }
 
 // own boundary cells and their genome lengths (-1: no cell); word C of each length row = the
-// genome arena's row width
+// genome length bound of the pool (PoolArena.width)
 __global__ void __launch_bounds__(256) xb_prep_kernel(int C, int H, int n, const int32_t* pos, const int32_t* idx_map,
                                                       const int32_t* lens, int width, int32_t* len_up, int32_t* len_dn,
                                                       int32_t* own1, int32_t* ownH) {
@@ -325,7 +345,7 @@ __global__ void __launch_bounds__(kXbThreads) xb_events_kernel(int C, int E, int
                                                                const int32_t* mine_dn, const int32_t* from_dn,
                                                                const int32_t* mine_up, const int32_t* from_up,
                                                                const int32_t* own1, const int32_t* ownH,
-                                                               const uint8_t* arena, int width, XbEvents ev,
+                                                               const uint8_t* arena, const int64_t* off, XbEvents ev,
                                                                uint8_t* slots_dn, uint8_t* slots_up) {
   constexpr int W = kXbThreads / 64;
   __shared__ int s_wc[W];
@@ -404,7 +424,8 @@ __global__ void __launch_bounds__(kXbThreads) xb_events_kernel(int C, int E, int
     const int y = item / 3, d = item - 3 * y - 1;
     const int L = b == 0 ? lrow[y] : lrow[(y + d + C) % C];
     if (tid == 0) *reinterpret_cast<int32_t*>(slot) = L;
-    for (int t = tid; t < L; t += kXbThreads) slot[4 + t] = arena[(size_t)c * width + t];
+    const uint8_t* g = arena + off[c];
+    for (int t = tid; t < L; t += kXbThreads) slot[4 + t] = g[t];
   }
 }
 
@@ -449,10 +470,11 @@ __global__ void __launch_bounds__(64) xb_apply_kernel(int C, int slot_w, uint64_
 
 // ---------------------------------------------------------------- host launchers
 namespace {
-RecCols rec_cols(uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, uintptr_t gdata, uintptr_t glen, int gw,
-                 uintptr_t ldata, uintptr_t llen, int lw, int m) {
+RecCols rec_cols(uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, const GenomePoolArgs& g, uintptr_t glen,
+                 int gw, uintptr_t ldata, uintptr_t llen, int lw, int m) {
   if (gw % 4 || lw % 4) throw std::invalid_argument("records: row widths must be multiples of 4");
-  return RecCols{P_<float>(mols), P_<int32_t>(pos), P_<int32_t>(life), P_<int32_t>(div), P_<uint8_t>(gdata),
+  return RecCols{P_<float>(mols), P_<int32_t>(pos), P_<int32_t>(life), P_<int32_t>(div), P_<uint8_t>(g.pool),
+                 P_<int64_t>(g.off), P_<unsigned long long>(g.top), g.cap, g.failed ? P_<int>(g.failed) : nullptr,
                  P_<int32_t>(glen), gw, P_<uint8_t>(ldata), P_<int32_t>(llen), lw, m};
 }
 int32_t* g_split_tiles = nullptr;
@@ -511,11 +533,11 @@ void place_split(int k, uintptr_t result, uintptr_t cells, int C, int H, uintptr
 long long rec_record_bytes(int m, int lw, int gw) { return rec_bytes(m, lw, gw); }
 
 void rec_pack(int k_up, int k_dn, uintptr_t par_up, uintptr_t pos_up, uintptr_t par_dn, uintptr_t pos_dn,
-              uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, uintptr_t gdata, uintptr_t glen, int gw,
-              uintptr_t ldata, uintptr_t llen, int lw, int m, bool child, uintptr_t out_up, uintptr_t out_dn,
+              uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, const GenomePoolArgs& gp, uintptr_t glen,
+              int gw, uintptr_t ldata, uintptr_t llen, int lw, int m, bool child, uintptr_t out_up, uintptr_t out_dn,
               uintptr_t stream) {
   if (k_up + k_dn <= 0) return;
-  const RecCols w = rec_cols(mols, pos, life, div, gdata, glen, gw, ldata, llen, lw, m);
+  const RecCols w = rec_cols(mols, pos, life, div, gp, glen, gw, ldata, llen, lw, m);
   rec_pack_kernel<<<k_up + k_dn, 64, 0, S_(stream)>>>(k_up, k_dn, P_<int64_t>(par_up), P_<int32_t>(pos_up),
                                                       P_<int64_t>(par_dn), P_<int32_t>(pos_dn), w, child,
                                                       P_<uint8_t>(out_up), P_<uint8_t>(out_dn));
@@ -523,12 +545,12 @@ void rec_pack(int k_up, int k_dn, uintptr_t par_up, uintptr_t pos_up, uintptr_t 
 }
 
 void rec_unpack(int n0, int k_up, uintptr_t in_up, int up_lw, int up_gw, int k_dn, uintptr_t in_dn, int dn_lw,
-                int dn_gw, int C, int H, uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, uintptr_t gdata,
-                uintptr_t glen, int gw, uintptr_t ldata, uintptr_t llen, int lw, int m, uintptr_t cell_map,
-                uintptr_t stream) {
+                int dn_gw, int C, int H, uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div,
+                const GenomePoolArgs& gp, uintptr_t glen, int gw, uintptr_t ldata, uintptr_t llen, int lw, int m,
+                uintptr_t cell_map, uintptr_t stream) {
   if (k_up + k_dn <= 0) return;
   if (up_lw % 4 || up_gw % 4 || dn_lw % 4 || dn_gw % 4) throw std::invalid_argument("rec_unpack: bad sender widths");
-  const RecCols w = rec_cols(mols, pos, life, div, gdata, glen, gw, ldata, llen, lw, m);
+  const RecCols w = rec_cols(mols, pos, life, div, gp, glen, gw, ldata, llen, lw, m);
   rec_unpack_kernel<<<k_up + k_dn, 64, 0, S_(stream)>>>(n0, k_up, P_<uint8_t>(in_up), up_lw, up_gw, k_dn,
                                                         P_<uint8_t>(in_dn), dn_lw, dn_gw, C, H, w,
                                                         P_<uint8_t>(cell_map));
@@ -578,13 +600,13 @@ void xb_prep(int C, int H, int n, uintptr_t pos, uintptr_t idx_map, uintptr_t le
 
 void xb_events(int C, int E, int slot_w, double p, int kcap, uint64_t seed_dn, uint64_t seed_up, uint64_t call,
                uintptr_t mine_dn, uintptr_t from_dn, uintptr_t mine_up, uintptr_t from_up, uintptr_t own1,
-               uintptr_t ownH, uintptr_t arena, int width, uintptr_t evbuf, uintptr_t slots_dn, uintptr_t slots_up,
+               uintptr_t ownH, uintptr_t arena, uintptr_t off, uintptr_t evbuf, uintptr_t slots_dn, uintptr_t slots_up,
                uintptr_t stream) {
   if (E < 1 || slot_w < 4 || slot_w % 4) throw std::invalid_argument("xb_events: bad capacity / slot width");
   xb_events_kernel<<<1, kXbThreads, 0, S_(stream)>>>(C, E, slot_w, p, kcap, seed_dn, seed_up, call,
                                                      P_<int32_t>(mine_dn), P_<int32_t>(from_dn), P_<int32_t>(mine_up),
                                                      P_<int32_t>(from_up), P_<int32_t>(own1), P_<int32_t>(ownH),
-                                                     P_<uint8_t>(arena), width, xb_ev(evbuf, 2 * E),
+                                                     P_<uint8_t>(arena), P_<int64_t>(off), xb_ev(evbuf, 2 * E),
                                                      P_<uint8_t>(slots_dn), P_<uint8_t>(slots_up));
   MS_LAUNCH_CHECK();
 }
@@ -618,7 +640,8 @@ void rccl_exchange(uintptr_t comm, int up, int down, uintptr_t send_up, long lon
 // boundary rows' genome lengths exchanged, the events drawn and the event genomes exchanged.
 // lens: int32 4 (C + 1) = mine up | mine down | from down | from up; own: int32 2 C; slots: 4 E
 // (4 + slot_w) bytes = to down | to up | from down | from up.
-void xb_begin(int C, int H, int n, uintptr_t pos, uintptr_t idx_map, uintptr_t glens, uintptr_t gdata, int width,
+void xb_begin(int C, int H, int n, uintptr_t pos, uintptr_t idx_map, uintptr_t glens, uintptr_t gdata, uintptr_t goff,
+              int width,
               uintptr_t lens, uintptr_t own, int E, int slot_w, double p, int kcap, uint64_t seed_dn, uint64_t seed_up,
               uint64_t call, uintptr_t evbuf, uintptr_t slots, uintptr_t comm, int up, int down, uintptr_t stream) {
   const size_t lb = 4ull * (C + 1);
@@ -629,7 +652,7 @@ void xb_begin(int C, int H, int n, uintptr_t pos, uintptr_t idx_map, uintptr_t g
   const size_t sb = (size_t)E * (4 + slot_w);  // a slot: 4 header bytes + slot_w genome bytes
   const uintptr_t slots_dn = slots, slots_up = slots + sb, recv_dn = slots + 2 * sb, recv_up = slots + 3 * sb;
   xb_events(C, E, slot_w, p, kcap, seed_dn, seed_up, call, mine_dn, from_dn, mine_up, from_up, own, own + 4ull * C,
-            gdata, width, evbuf, slots_dn, slots_up, stream);
+            gdata, goff, evbuf, slots_dn, slots_up, stream);
   rccl_exchange(comm, up, down, slots_up, sb, slots_dn, sb, recv_dn, sb, recv_up, sb, stream);
 }
 

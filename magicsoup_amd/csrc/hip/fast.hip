@@ -33,10 +33,13 @@ struct FastWorld {
   long long cap = 0;  // rows every per-cell buffer below holds
   // per-cell columns (molecules f32 (cap, m), positions i32 (cap, 2), lifetimes, divisions) + spares
   uintptr_t mols = 0, pos = 0, life = 0, div = 0, mols_sp = 0, pos_sp = 0, life_sp = 0, div_sp = 0;
-  // genome / label arenas (rows of `width` bytes + int32 lengths) + spares of the same shape
-  uintptr_t g_data = 0, g_lens = 0, g_data_sp = 0, g_lens_sp = 0;
+  // genomes: per-cell pool offsets (int64) + int32 lengths and their spares (the bytes stay where they
+  // are: compaction and cloning move offsets only; records read / write the pool `gpool`); labels:
+  // rows of `l_width` bytes + int32 lengths + spares
+  uintptr_t g_off = 0, g_lens = 0, g_off_sp = 0, g_lens_sp = 0;
+  GenomePoolArgs gpool{};
   uintptr_t l_data = 0, l_lens = 0, l_data_sp = 0, l_lens_sp = 0;
-  int g_width = 0, l_width = 0;
+  int l_width = 0;
   uintptr_t slot = 0, slot_sp = 0;  // kinetics cell -> parameter row map (int64)
   uintptr_t cell_map = 0;           // occupancy bytes (4-byte padded)
   // scratch, `cap` entries each (claim: R * C)
@@ -47,9 +50,9 @@ struct FastWorld {
   bool ready = false;
 
   void finalize() {
-    if (cap <= 0 || !mols || !pos || !life || !div || !g_data || !l_data || !slot || !cell_map)
+    if (cap <= 0 || !mols || !pos || !life || !div || !g_off || !gpool.pool || !l_data || !slot || !cell_map)
       throw std::invalid_argument("FastWorld: incomplete descriptor");
-    if (!mols_sp || !pos_sp || !life_sp || !div_sp || !g_data_sp || !l_data_sp || !slot_sp)
+    if (!mols_sp || !pos_sp || !life_sp || !div_sp || !g_off_sp || !l_data_sp || !slot_sp)
       throw std::invalid_argument("FastWorld: missing spare buffers");
     const long long mb = 4ll * m;
     std::vector<RowDescTuple> f = {
@@ -57,7 +60,7 @@ struct FastWorld {
         {pos, pos_sp, 8, 8, 8, 0},
         {life, life_sp, 4, 4, 4, 0},
         {div, div_sp, 4, 4, 4, 0},
-        {g_data, g_data_sp, g_width, g_width, g_width, g_lens},
+        {g_off, g_off_sp, 8, 8, 8, 0},
         {g_lens, g_lens_sp, 4, 4, 4, 0},
         {l_data, l_data_sp, l_width, l_width, l_width, l_lens},
         {l_lens, l_lens_sp, 4, 4, 4, 0},
@@ -67,11 +70,11 @@ struct FastWorld {
     for (const auto& t : f) {
       const auto& [s, d, ss, ds, rb, lp] = t;
       // copy back: the spare's lengths bound the used bytes of a copied arena row
-      const uintptr_t l = lp == g_lens ? g_lens_sp : (lp == l_lens ? l_lens_sp : 0);
+      const uintptr_t l = lp == l_lens ? l_lens_sp : 0;
       b.emplace_back(d, s, ds, ss, rb, l);
     }
     std::vector<RowDescTuple> c = {
-        {g_data, g_data, g_width, g_width, g_width, g_lens},
+        {g_off, g_off, 8, 8, 8, 0},
         {g_lens, g_lens, 4, 4, 4, 0},
         {l_data, l_data, l_width, l_width, l_width, l_lens},
         {l_lens, l_lens, 4, 4, 4, 0},
@@ -127,13 +130,13 @@ void place_rounds_mask(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r
 void place_split(int k, uintptr_t result, uintptr_t cells, int C, int H, uintptr_t par, uintptr_t npos, uintptr_t counts,
                  uintptr_t hdr_up, uintptr_t hdr_dn, int lw, int gw, int m, uintptr_t stream);
 void rec_pack(int k_up, int k_dn, uintptr_t par_up, uintptr_t pos_up, uintptr_t par_dn, uintptr_t pos_dn,
-              uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, uintptr_t gdata, uintptr_t glen, int gw,
-              uintptr_t ldata, uintptr_t llen, int lw, int m, bool child, uintptr_t out_up, uintptr_t out_dn,
+              uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, const GenomePoolArgs& gp, uintptr_t glen,
+              int gw, uintptr_t ldata, uintptr_t llen, int lw, int m, bool child, uintptr_t out_up, uintptr_t out_dn,
               uintptr_t stream);
 void rec_unpack(int n0, int k_up, uintptr_t in_up, int up_lw, int up_gw, int k_dn, uintptr_t in_dn, int dn_lw,
-                int dn_gw, int C, int H, uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, uintptr_t gdata,
-                uintptr_t glen, int gw, uintptr_t ldata, uintptr_t llen, int lw, int m, uintptr_t cell_map,
-                uintptr_t stream);
+                int dn_gw, int C, int H, uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div,
+                const GenomePoolArgs& gp, uintptr_t glen, int gw, uintptr_t ldata, uintptr_t llen, int lw, int m,
+                uintptr_t cell_map, uintptr_t stream);
 void divide_commit_list(int k, uintptr_t par, uintptr_t npos, long long n0, int n_exp, uintptr_t exp, int m,
                         uintptr_t pos, uintptr_t cell_mols, uintptr_t divisions, uintptr_t lifetimes, uintptr_t stream);
 void rccl_exchange(uintptr_t comm, int up, int down, uintptr_t send_up, long long n_send_up, uintptr_t send_down,
@@ -185,8 +188,8 @@ void fast_dist_divide_b(const FastWorld& f, long long n0, uintptr_t comm, int up
   const uintptr_t pos_up = npos3 + 8ull * kk, pos_dn = npos3 + 16ull * kk;
   const long long B = rec_bytes(m, lw, gw);
   const uintptr_t out_up = out, out_dn = out + (size_t)n_up * B;
-  rec_pack(n_up, n_dn, par_up, pos_up, par_dn, pos_dn, f.mols, f.pos, f.life, f.div, f.g_data, f.g_lens, f.g_width,
-           f.l_data, f.l_lens, f.l_width, m, true, out_up, out_dn, stream);
+  rec_pack(n_up, n_dn, par_up, pos_up, par_dn, pos_dn, f.mols, f.pos, f.life, f.div, f.gpool, f.g_lens, gw, f.l_data,
+           f.l_lens, f.l_width, m, true, out_up, out_dn, stream);
   const long long b_up = in_up * rec_bytes(m, up_lw, up_gw), b_dn = in_dn * rec_bytes(m, dn_lw, dn_gw);
   const uintptr_t rin_up = in, rin_dn = in + (size_t)b_up;
   rccl_exchange(comm, up, down, out_up, n_up * B, out_dn, n_dn * B, rin_dn, b_dn, rin_up, b_up, stream);
@@ -197,7 +200,8 @@ void fast_dist_divide_b(const FastWorld& f, long long n0, uintptr_t comm, int up
   const int k_in = in_up + in_dn;
   if (k_in) {
     rec_unpack((int)(n0 + n_loc), in_up, rin_up, up_lw, up_gw, in_dn, rin_dn, dn_lw, dn_gw, C, H, f.mols, f.pos, f.life,
-               f.div, f.g_data, f.g_lens, f.g_width, f.l_data, f.l_lens, f.l_width, m, f.cell_map, stream);
+               f.div, f.gpool, f.g_lens, std::max(up_gw, dn_gw), f.l_data, f.l_lens, f.l_width, m, f.cell_map,
+               stream);
     fill_i64_kernel<<<cdiv(k_in, 256), 256, 0, s>>>(P_<int64_t>(f.slot) + n0 + n_loc, P_<int64_t>(zero_row), k_in);
     MS_LAUNCH_CHECK();
   }
@@ -223,15 +227,15 @@ void bind_fast(pybind11::module_& m) {
       .def_readwrite("pos_sp", &FastWorld::pos_sp)
       .def_readwrite("life_sp", &FastWorld::life_sp)
       .def_readwrite("div_sp", &FastWorld::div_sp)
-      .def_readwrite("g_data", &FastWorld::g_data)
+      .def_readwrite("g_off", &FastWorld::g_off)
       .def_readwrite("g_lens", &FastWorld::g_lens)
-      .def_readwrite("g_data_sp", &FastWorld::g_data_sp)
+      .def_readwrite("g_off_sp", &FastWorld::g_off_sp)
       .def_readwrite("g_lens_sp", &FastWorld::g_lens_sp)
+      .def_readwrite("gpool", &FastWorld::gpool)
       .def_readwrite("l_data", &FastWorld::l_data)
       .def_readwrite("l_lens", &FastWorld::l_lens)
       .def_readwrite("l_data_sp", &FastWorld::l_data_sp)
       .def_readwrite("l_lens_sp", &FastWorld::l_lens_sp)
-      .def_readwrite("g_width", &FastWorld::g_width)
       .def_readwrite("l_width", &FastWorld::l_width)
       .def_readwrite("slot", &FastWorld::slot)
       .def_readwrite("slot_sp", &FastWorld::slot_sp)

@@ -30,7 +30,8 @@ struct TransArgs {
   int32_t *long_list, *long_count;  // LDS count pass: genomes longer than lmax
   bool stage_dt;
   const int64_t* rows;
-  const uint8_t* arena;
+  const uint8_t* arena;  // genome pool (cell r: lens[r] bytes at arena + off[r])
+  const int64_t* off;
   const int32_t* lens;
   const uint8_t *is_start, *is_stop, *one_codon, *dom_type;
   const uint16_t* two_codon;
@@ -102,7 +103,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   if (active) {
     const int64_t r = a.rows[g];
     L = a.lens[r];
-    s = a.arena + (size_t)r * a.width;
+    s = a.arena + a.off[r];
     if (lane < 2) counters[lane] = 0;
   }
   __syncthreads();
@@ -113,8 +114,9 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   }
   wave_sync();
 
-  // ---- 0. stage the genome row in LDS (16-byte loads; the row width is a multiple of 16 and the
-  //         staging area -- the domain-type table, filled in step 2 -- holds 2 * LW >= L rounded up)
+  // ---- 0. stage the genome in LDS (16-byte loads: pool allocations are 16-byte aligned and
+  //         rounded up; the staging area -- the domain-type table, filled in step 2 -- holds
+  //         2 * LW >= L rounded up)
   uint8_t* raw = dtp;
   for (int i = lane * 16; i < L; i += 64 * 16)
     *reinterpret_cast<uint4*>(raw + i) = *reinterpret_cast<const uint4*>(s + i);
@@ -290,12 +292,14 @@ constexpr int kLdsMaxLen = 1024;  // genomes up to this length use LDS slots
 
 // mode: 0 count pass, 1 write pass, 2 fused (counts and tokens; the caller checks the counts
 // against P / D afterwards)
-static void launch(int mode, int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+static void launch(int mode, int n, uintptr_t rows, uintptr_t arena, uintptr_t off, int width, uintptr_t lens,
+                   uintptr_t luts,
                    uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                    uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t list, uintptr_t gslot,
                    uintptr_t long_list, uintptr_t long_count, uintptr_t dn, uintptr_t stream) {
   if (n <= 0) return;
-  if (width % 16 != 0) throw std::invalid_argument("genome arena width must be a multiple of 16");
+  if (width % 16 != 0) throw std::invalid_argument("genome length bound must be a multiple of 16");
+  if (!off) throw std::invalid_argument("translate: genome offsets required");
   if (width > 65535) throw std::invalid_argument("genomes longer than 65535 nt are not supported on the GPU");
   TransArgs a{};
   a.n = n;
@@ -303,6 +307,7 @@ static void launch(int mode, int n, uintptr_t rows, uintptr_t arena, int width, 
   a.dt_entries = dt_entries;
   a.rows = P_<int64_t>(rows);
   a.arena = P_<uint8_t>(arena);
+  a.off = P_<int64_t>(off);
   a.lens = P_<int32_t>(lens);
   const uint8_t* l = P_<uint8_t>(luts);  // is_start | is_stop | one_codon (64 bytes each)
   a.is_start = l;
@@ -347,39 +352,39 @@ size_t translate_slot_bytes(int width) { return slot_bytes_for(width, width); }
 // n items; list: item -> genome index into rows (0 = identity); gslot: global slots for the
 // long-genome pass (n * translate_slot_bytes(width) bytes) or 0 for the LDS pass, which queues
 // genomes longer than its slots in long_list / long_count.
-void translate_count(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+void translate_count(int n, uintptr_t rows, uintptr_t arena, uintptr_t off, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                      uintptr_t nprot, uintptr_t ndom, uintptr_t list, uintptr_t gslot, uintptr_t long_list,
                      uintptr_t long_count, uintptr_t dn, uintptr_t stream) {
-  launch(0, n, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot,
+  launch(0, n, rows, arena, off, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot,
          ndom, 0, 0, 0, list, gslot, long_list, long_count, dn, stream);
 }
 
-void translate_write(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+void translate_write(int n, uintptr_t rows, uintptr_t arena, uintptr_t off, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                      uintptr_t nprot, int P, int D, uintptr_t tokens, uintptr_t list, uintptr_t gslot,
                      uintptr_t dn, uintptr_t stream) {
-  launch(1, n, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot, 0,
+  launch(1, n, rows, arena, off, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot, 0,
          P, D, tokens, list, gslot, 0, 0, dn, stream);
 }
 
 // Count and write in one launch (LDS pass): tokens for up to P proteins / D domains each, plus the
 // per-strand counts and the long-genome queue of the count pass.
-void translate_fused(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+void translate_fused(int n, uintptr_t rows, uintptr_t arena, uintptr_t off, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                      uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t long_list,
                      uintptr_t long_count, uintptr_t dn, uintptr_t stream) {
-  launch(2, n, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot, ndom,
+  launch(2, n, rows, arena, off, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot, ndom,
          P, D, tokens, 0, 0, long_list, long_count, dn, stream);
 }
 
 // Long-genome pass of the fused translation with a device count: the items long_list[0..*dn)
 // (at most lcap) take global-memory slots (lcap * translate_slot_bytes(width) bytes at gslot).
-void translate_fused_long(int lcap, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+void translate_fused_long(int lcap, uintptr_t rows, uintptr_t arena, uintptr_t off, int width, uintptr_t lens, uintptr_t luts,
                           uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                           uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t long_list,
                           uintptr_t gslot, uintptr_t dn, uintptr_t stream) {
-  launch(2, lcap, rows, arena, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot, ndom,
+  launch(2, lcap, rows, arena, off, width, lens, luts, dom_type, dt_entries, two_codon, dom_size, dom_type_size, nprot, ndom,
          P, D, tokens, long_list, gslot, 0, 0, dn, stream);
 }
 

@@ -27,11 +27,12 @@ void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, ui
 void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
 int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t cnt, uintptr_t stream);
 void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t dst, uintptr_t stream);
-void translate_fused(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+void translate_fused(int n, uintptr_t rows, uintptr_t arena, uintptr_t off, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                      uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t long_list,
                      uintptr_t long_count, uintptr_t dn, uintptr_t stream);
-void translate_fused_long(int lcap, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+void translate_fused_long(int lcap, uintptr_t rows, uintptr_t arena, uintptr_t off, int width, uintptr_t lens,
+                          uintptr_t luts,
                           uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                           uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t long_list,
                           uintptr_t gslot, uintptr_t dn, uintptr_t stream);
@@ -44,17 +45,18 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
                   uintptr_t dn, uintptr_t stream);
 void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
                uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
-void mut_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens,
+void mut_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t rows, uintptr_t arena, uintptr_t off, uintptr_t lens,
                uintptr_t k, double p_indel, double p_del, uint64_t seed, uint64_t call, uintptr_t out, int out_width,
                uintptr_t out_len, uintptr_t stream);
 void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
                     uintptr_t tot, int kcap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
-void rec_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t pairs, uintptr_t keys, uintptr_t arena, int width,
+void rec_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t pairs, uintptr_t keys, uintptr_t arena, uintptr_t off,
                uintptr_t lens, uintptr_t k, uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out,
                int out_width, uintptr_t out_len, uintptr_t out_rows, uintptr_t stream);
 void arena_scatter(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t src, int src_width, uintptr_t src_len,
-                   uintptr_t arena, int width, uintptr_t lens, uintptr_t mark, uint64_t gen, uintptr_t flags,
-                   uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
+                   uintptr_t pool, uintptr_t off, uintptr_t top, long long pool_cap, int width, uintptr_t lens,
+                   uintptr_t mark, uint64_t gen, uintptr_t flags, uintptr_t gflags, uintptr_t opflags,
+                   uintptr_t stream);
 
 void select_indices_capped(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t out_dev, int cap,
                            uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
@@ -113,9 +115,10 @@ __global__ void __launch_bounds__(1024) gp_check_assign_kernel(int cap, int lcap
 }
 
 // ---- descriptors filled from Python
-struct GpArena {  // genome arena + the pipeline's device counters
-  uintptr_t data = 0, lens = 0;
-  int width = 0, n = 0;
+struct GpArena {  // genome pool + the pipeline's device counters
+  uintptr_t data = 0, lens = 0, off = 0, top = 0;  // pool bytes, per-cell lengths / offsets, bump counter
+  long long pool_cap = 0;
+  int width = 0, n = 0;  // width: the genome length bound of the call's scratch (PoolArena.width)
   uintptr_t cnt = 0, cnt2 = 0, opflags = 0, gflags = 0, d_rows = 0;
 };
 struct GpGen {  // translation LUTs (Genetics.device_luts)
@@ -179,10 +182,10 @@ int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const Gp
   const unsigned gz = (unsigned)std::max<long long>(1, std::min<long long>(cdiv((long long)cap * row, 256), 1024));
   gp_zero_kernel<<<gz, 256, 0, s>>>(cap, P_<int>(dcnt), row, P_<int32_t>(tokens), P_<int32_t>(long_count));
   MS_LAUNCH_CHECK();
-  translate_fused(cap, cells, a.data, a.width, a.lens, g.small, g.dom_type, g.dt_entries, g.two_codon, g.dom_size,
+  translate_fused(cap, cells, a.data, a.off, a.width, a.lens, g.small, g.dom_type, g.dt_entries, g.two_codon, g.dom_size,
                   g.dom_type_size, counts, ndom, k.P, dcap, tokens, long_list, long_count, dcnt, st);
   if (a.width > 1024)  // genomes longer than the LDS slots: second pass over the queued ones
-    translate_fused_long(lcap, cells, a.data, a.width, a.lens, g.small, g.dom_type, g.dt_entries, g.two_codon,
+    translate_fused_long(lcap, cells, a.data, a.off, a.width, a.lens, g.small, g.dom_type, g.dt_entries, g.two_codon,
                          g.dom_size, g.dom_type_size, counts, ndom, k.P, dcap, tokens, long_list, gslot, long_count,
                          st);
   auto sl = status_slot();
@@ -282,8 +285,9 @@ int gp_mutate(const GpArena& a, const GpGen& g, const GpKin& k, double p, double
   const uintptr_t out = c.take((size_t)cap * out_w), out_len = c.take(4 * (size_t)cap);
   mut_count(n, 0, a.lens, p, seed, call, kk, kcap, a.gflags, a.opflags, stream);
   select_indices_capped(n, kSelI32Pos, kk, sel, a.cnt, cap, a.gflags, a.opflags, stream);
-  mut_apply(cap, a.cnt, sel, 0, a.data, L, a.lens, kk, p_indel, p_del, seed, call, out, out_w, out_len, stream);
-  arena_scatter(cap, a.cnt, 1, sel, out, out_w, out_len, a.data, L, a.lens, 0, 0, 0, a.gflags, a.opflags, stream);
+  mut_apply(cap, a.cnt, sel, 0, a.data, a.off, a.lens, kk, p_indel, p_del, seed, call, out, out_w, out_len, stream);
+  arena_scatter(cap, a.cnt, 1, sel, out, out_w, out_len, a.data, a.off, a.top, a.pool_cap, L, a.lens, 0, 0, 0,
+                a.gflags, a.opflags, stream);
   return rebuild(cap, sel, a.cnt, a, g, k, dcap, c, a.cnt, s);
 }
 
@@ -312,14 +316,15 @@ int gp_recombine(const GpArena& a, const GpGen& g, const GpKin& k, uintptr_t key
     rec_count_keys(8 * n, keys, a.lens, p, seed, call, kk, 0, kcap, a.gflags, a.opflags, stream);
     select_indices_capped(8ll * n, kSelI32Pos, kk, sel, a.cnt, cap, a.gflags, a.opflags, stream);
   }
-  rec_apply(cap, a.cnt, sel, 0, keys, a.data, L, a.lens, kk, seed, call, parts, parts_cap, out, out_w, out_len,
+  rec_apply(cap, a.cnt, sel, 0, keys, a.data, a.off, a.lens, kk, seed, call, parts, parts_cap, out, out_w, out_len,
             out_rows, stream);
   if (xr) {
     extra.attr("apply")(a.cnt, out, out_w, out_len, out_rows, nres);
   }
   // (a0, b0, a1, b1, ..., extra rows): the last result per cell wins (reference update order);
   // arena_scatter also clears the `won` flags past the live rows
-  arena_scatter(nr, xr ? nres : a.cnt, xr ? 1 : 2, out_rows, out, out_w, out_len, a.data, L, a.lens, mark, gen, won,
+  arena_scatter(nr, xr ? nres : a.cnt, xr ? 1 : 2, out_rows, out, out_w, out_len, a.data, a.off, a.top, a.pool_cap, L,
+                a.lens, mark, gen, won,
                 a.gflags, a.opflags, stream);
   select_indices_dev(nr, kSelSet, won, 0, q, 0, a.cnt2, stream);
   gather_dev(nr, a.cnt2, q, out_rows, cells, stream);
@@ -403,9 +408,11 @@ std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpAren
   rec_slots(n, std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t), std::get<4>(t), std::get<5>(t),
             std::get<6>(t), ar.lens, p_rec, seed_r, call_r, kcap, ar.gflags, ar.opflags, keys, kk, sel, ar.cnt, pcap,
             stream);
-  rec_apply(pcap, ar.cnt, sel, 0, keys, ar.data, L, ar.lens, kk, seed_r, call_r, parts, parts_cap, out, out_w, out_len,
+  rec_apply(pcap, ar.cnt, sel, 0, keys, ar.data, ar.off, ar.lens, kk, seed_r, call_r, parts, parts_cap, out, out_w,
+            out_len,
             out_rows, stream);
-  arena_scatter(nr, ar.cnt, 2, out_rows, out, out_w, out_len, ar.data, L, ar.lens, mark, gen, won, ar.gflags,
+  arena_scatter(nr, ar.cnt, 2, out_rows, out, out_w, out_len, ar.data, ar.off, ar.top, ar.pool_cap, L, ar.lens, mark,
+                gen, won, ar.gflags,
                 ar.opflags, stream);
   select_indices_dev(nr, kSelSet, won, 0, q, 0, ar.cnt2, stream);
   gather_dev(nr, ar.cnt2, q, out_rows, cells, stream);
@@ -416,9 +423,10 @@ std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpAren
   const uintptr_t mout = cm.take((size_t)mcap * mout_w), mout_len = cm.take(4 * (size_t)mcap);
   mut_count(n, 0, am.lens, p, seed_m, call_m, mk, kcap, am.gflags, am.opflags, stream);
   select_indices_capped(n, kSelI32Pos, mk, msel, am.cnt, mcap, am.gflags, am.opflags, stream);
-  mut_apply(mcap, am.cnt, msel, 0, am.data, L, am.lens, mk, p_indel, p_del, seed_m, call_m, mout, mout_w, mout_len,
+  mut_apply(mcap, am.cnt, msel, 0, am.data, am.off, am.lens, mk, p_indel, p_del, seed_m, call_m, mout, mout_w, mout_len,
             stream);
-  arena_scatter(mcap, am.cnt, 1, msel, mout, mout_w, mout_len, am.data, L, am.lens, 0, 0, 0, am.gflags, am.opflags,
+  arena_scatter(mcap, am.cnt, 1, msel, mout, mout_w, mout_len, am.data, am.off, am.top, am.pool_cap, L, am.lens, 0, 0,
+                0, am.gflags, am.opflags,
                 stream);
   // union of the changed cells -> one translation + build
   const int ucap = nr + mcap;
@@ -439,6 +447,8 @@ void bind_gp(py::module_& m) {
   py::class_<GpArena>(m, "GpArena", py::module_local())
       .def(py::init<>())
       .def_readwrite("data", &GpArena::data).def_readwrite("lens", &GpArena::lens)
+      .def_readwrite("off", &GpArena::off).def_readwrite("top", &GpArena::top)
+      .def_readwrite("pool_cap", &GpArena::pool_cap)
       .def_readwrite("width", &GpArena::width).def_readwrite("n", &GpArena::n)
       .def_readwrite("cnt", &GpArena::cnt).def_readwrite("cnt2", &GpArena::cnt2)
       .def_readwrite("opflags", &GpArena::opflags).def_readwrite("gflags", &GpArena::gflags)

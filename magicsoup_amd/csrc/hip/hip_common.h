@@ -97,6 +97,23 @@ __device__ __forceinline__ long long poisson(Philox& rng, double lam) {
   return k < 0 ? 0 : k;
 }
 
+// ---------------------------------------------------------------- genome pool
+// GPU genomes live in one byte pool (models/strings.py PoolArena): cell i's genome is the lens[i]
+// bytes at pool + off[i], allocations 16-byte aligned and never written again (new genomes take new
+// space, so cells can share a genome). An allocation is an atomic bump of the device counter `top`;
+// -1 when the pool is full (the caller raises a flag; the host collects or grows the pool).
+__device__ __forceinline__ long long pool_alloc(unsigned long long* top, long long cap, int len) {
+  const unsigned long long sz = ((unsigned long long)(len > 0 ? len : 0) + 15ull) & ~15ull;
+  const unsigned long long o = atomicAdd(top, sz);
+  return (long long)(o + sz) <= cap ? (long long)o : -1;
+}
+
+// The pool as kernel launchers take it (filled from Python: PoolArena.args()).
+struct GenomePoolArgs {
+  uintptr_t pool = 0, off = 0, top = 0, failed = 0;  // bytes, per-cell offsets, bump counter, error word
+  long long cap = 0;                                 // pool bytes
+};
+
 // ---------------------------------------------------------------- wave helpers
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 

@@ -851,28 +851,17 @@ __global__ void __launch_bounds__(256) spawn_place_kernel(int k, int R, int C, i
   label_lens[c] = kLabelLen;
 }
 
-// genome rows (k, L_in) with lengths -> arena rows n0.. (width >= L_in), zero padding
-__global__ void __launch_bounds__(256) spawn_genomes_kernel(int k, int L_in, const uint8_t* rows, const int32_t* lens,
-                                                            long long n0, uint8_t* arena, int width,
-                                                            int32_t* arena_lens) {
-  const long long total = (long long)k * width;
-  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (long long)gridDim.x * blockDim.x) {
-    const long long j = t / width;
-    const int b = (int)(t - j * width);
-    arena[(n0 + j) * width + b] = b < L_in ? rows[j * L_in + b] : 0;
-    if (b == 0) arena_lens[n0 + j] = lens[j];
-  }
-}
+void pool_write(int k, int L_in, uintptr_t rows, uintptr_t lens, uintptr_t dst, long long n0, uintptr_t pool,
+                uintptr_t off, uintptr_t top, long long cap, uintptr_t out_lens, uintptr_t failed, uintptr_t stream);
 
 void spawn_dev(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uint64_t seed, uint64_t call,
                long long n0, int m, uintptr_t pos, uintptr_t lifetimes, uintptr_t divisions, uintptr_t cell_mols,
                uintptr_t map, int dtype, uintptr_t corr, uintptr_t labels, int label_w, uintptr_t label_lens,
-               int L_in, uintptr_t rows, uintptr_t lens, uintptr_t arena, int width, uintptr_t arena_lens,
-               uintptr_t failed, uintptr_t stream) {
+               int L_in, uintptr_t rows, uintptr_t lens, uintptr_t pool, uintptr_t off, uintptr_t top,
+               long long pool_cap, uintptr_t arena_lens, uintptr_t failed, uintptr_t pool_failed, uintptr_t stream) {
   if (k <= 0) return;
   if (R <= 0 || C <= 0 || r_lo < 0 || r_hi > R || r_lo >= r_hi) throw std::invalid_argument("spawn_dev: bad geometry");
-  if (label_w < kLabelLen || width < L_in) throw std::invalid_argument("spawn_dev: arena rows too narrow");
+  if (label_w < kLabelLen) throw std::invalid_argument("spawn_dev: label rows too narrow");
   hipStream_t s = S_(stream);
   spawn_place_kernel<<<cdiv(k, 256), 256, 0, s>>>(k, R, C, r_lo, r_hi, P_<uint8_t>(cell_map), seed, call, 64, n0, m,
                                                   P_<int32_t>(pos), P_<int32_t>(lifetimes), P_<int32_t>(divisions),
@@ -880,10 +869,8 @@ void spawn_dev(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uint
                                                   corr ? P_<float>(corr) : nullptr, P_<uint8_t>(labels), label_w,
                                                   P_<int32_t>(label_lens), P_<int>(failed));
   MS_LAUNCH_CHECK();
-  const unsigned g = (unsigned)std::min<long long>(cdiv((long long)k * width, 256), 4096);
-  spawn_genomes_kernel<<<g, 256, 0, s>>>(k, L_in, P_<uint8_t>(rows), P_<int32_t>(lens), n0, P_<uint8_t>(arena), width,
-                                         P_<int32_t>(arena_lens));
-  MS_LAUNCH_CHECK();
+  // the genomes into fresh pool space (pool.hip)
+  pool_write(k, L_in, rows, lens, 0, n0, pool, off, top, pool_cap, arena_lens, pool_failed, stream);
 }
 
 // Save / restore the state an enzymatic_activity changes: cell molecules and the raw map values

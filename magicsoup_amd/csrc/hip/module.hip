@@ -65,8 +65,8 @@ void cell_state_io(int n, int m, uintptr_t pos, int R, int C, uintptr_t map, int
 void spawn_dev(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uint64_t seed, uint64_t call,
                long long n0, int m, uintptr_t pos, uintptr_t lifetimes, uintptr_t divisions, uintptr_t cell_mols,
                uintptr_t map, int dtype, uintptr_t corr, uintptr_t labels, int label_w, uintptr_t label_lens,
-               int L_in, uintptr_t rows, uintptr_t lens, uintptr_t arena, int width, uintptr_t arena_lens,
-               uintptr_t failed, uintptr_t stream);
+               int L_in, uintptr_t rows, uintptr_t lens, uintptr_t pool, uintptr_t off, uintptr_t top,
+               long long pool_cap, uintptr_t arena_lens, uintptr_t failed, uintptr_t pool_failed, uintptr_t stream);
 void permeate(int c, int m, int R, int C, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map, int dtype,
               uintptr_t corr, uintptr_t stream);
 void gather_rows(int n, uintptr_t dn, uintptr_t src_rows, uintptr_t dst_rows,
@@ -117,15 +117,15 @@ void index_map(int c, uintptr_t pos, int C, uintptr_t idx_map, bool clear, uintp
 void neighbor_pairs(int nf, int n, uintptr_t from, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map,
                     uintptr_t in_from, uintptr_t in_to, uintptr_t counter, int cap, uintptr_t pairs, uintptr_t stream);
 // genetics.hip
-void translate_count(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+void translate_count(int n, uintptr_t rows, uintptr_t arena, uintptr_t off, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                      uintptr_t nprot, uintptr_t ndom, uintptr_t list, uintptr_t gslot, uintptr_t long_list,
                      uintptr_t long_count, uintptr_t dn, uintptr_t stream);
-void translate_write(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+void translate_write(int n, uintptr_t rows, uintptr_t arena, uintptr_t off, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                      uintptr_t nprot, int P, int D, uintptr_t tokens, uintptr_t list, uintptr_t gslot,
                      uintptr_t dn, uintptr_t stream);
-void translate_fused(int n, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens, uintptr_t luts,
+void translate_fused(int n, uintptr_t rows, uintptr_t arena, uintptr_t off, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
                      uintptr_t nprot, uintptr_t ndom, int P, int D, uintptr_t tokens, uintptr_t long_list,
                      uintptr_t long_count, uintptr_t dn, uintptr_t stream);
@@ -134,17 +134,18 @@ void set_integrate_mode(int mode);
 // mutations.hip
 void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
                uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
-void mut_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens,
+void mut_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t rows, uintptr_t arena, uintptr_t off, uintptr_t lens,
                uintptr_t k, double p_indel, double p_del, uint64_t seed, uint64_t call, uintptr_t out, int out_width,
                uintptr_t out_len, uintptr_t stream);
 void rec_count(int n, uintptr_t pairs, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
                uintptr_t stream);
-void rec_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t pairs, uintptr_t keys, uintptr_t arena, int width,
+void rec_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t pairs, uintptr_t keys, uintptr_t arena, uintptr_t off,
                uintptr_t lens, uintptr_t k, uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out,
                int out_width, uintptr_t out_len, uintptr_t out_rows, uintptr_t stream);
 void arena_scatter(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t src, int src_width, uintptr_t src_len,
-                   uintptr_t arena, int width, uintptr_t lens, uintptr_t mark, uint64_t gen, uintptr_t flags,
-                   uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
+                   uintptr_t pool, uintptr_t off, uintptr_t top, long long pool_cap, int width, uintptr_t lens,
+                   uintptr_t mark, uint64_t gen, uintptr_t flags, uintptr_t gflags, uintptr_t opflags,
+                   uintptr_t stream);
 int divide_mask_dev(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t cell_map,
                     uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result, int rounds, uint64_t seed,
                     uint64_t call, uintptr_t wins, uintptr_t dcount, long long n0, int m, uintptr_t par,
@@ -190,29 +191,31 @@ void place_split(int k, uintptr_t result, uintptr_t cells, int C, int H, uintptr
                  uintptr_t hdr_up, uintptr_t hdr_dn, int lw, int gw, int m, uintptr_t stream);
 long long rec_record_bytes(int m, int lw, int gw);
 void rec_pack(int k_up, int k_dn, uintptr_t par_up, uintptr_t pos_up, uintptr_t par_dn, uintptr_t pos_dn,
-              uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, uintptr_t gdata, uintptr_t glen, int gw,
-              uintptr_t ldata, uintptr_t llen, int lw, int m, bool child, uintptr_t out_up, uintptr_t out_dn,
+              uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, const GenomePoolArgs& gp, uintptr_t glen,
+              int gw, uintptr_t ldata, uintptr_t llen, int lw, int m, bool child, uintptr_t out_up, uintptr_t out_dn,
               uintptr_t stream);
 void rec_unpack(int n0, int k_up, uintptr_t in_up, int up_lw, int up_gw, int k_dn, uintptr_t in_dn, int dn_lw,
-                int dn_gw, int C, int H, uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, uintptr_t gdata,
-                uintptr_t glen, int gw, uintptr_t ldata, uintptr_t llen, int lw, int m, uintptr_t cell_map,
-                uintptr_t stream);
+                int dn_gw, int C, int H, uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div,
+                const GenomePoolArgs& gp, uintptr_t glen, int gw, uintptr_t ldata, uintptr_t llen, int lw, int m,
+                uintptr_t cell_map, uintptr_t stream);
 void halo_pack(int m, int C, int H, int elem, uintptr_t map, uintptr_t send_up, uintptr_t send_dn, uintptr_t stream);
 void halo_unpack(int m, int C, int H, int elem, uintptr_t map, uintptr_t from_up, uintptr_t from_dn, uintptr_t stream);
 void xb_prep(int C, int H, int n, uintptr_t pos, uintptr_t idx_map, uintptr_t lens, int width, uintptr_t len_up,
              uintptr_t len_dn, uintptr_t own1, uintptr_t ownH, uintptr_t stream);
-void xb_begin(int C, int H, int n, uintptr_t pos, uintptr_t idx_map, uintptr_t glens, uintptr_t gdata, int width,
+void xb_begin(int C, int H, int n, uintptr_t pos, uintptr_t idx_map, uintptr_t glens, uintptr_t gdata, uintptr_t goff,
+              int width,
               uintptr_t lens, uintptr_t own, int E, int slot_w, double p, int kcap, uint64_t seed_dn, uint64_t seed_up,
               uint64_t call, uintptr_t evbuf, uintptr_t slots, uintptr_t comm, int up, int down, uintptr_t stream);
 void xb_events(int C, int E, int slot_w, double p, int kcap, uint64_t seed_dn, uint64_t seed_up, uint64_t call,
                uintptr_t mine_dn, uintptr_t from_dn, uintptr_t mine_up, uintptr_t from_up, uintptr_t own1,
-               uintptr_t ownH, uintptr_t arena, int width, uintptr_t evbuf, uintptr_t slots_dn, uintptr_t slots_up,
+               uintptr_t ownH, uintptr_t arena, uintptr_t off, uintptr_t evbuf, uintptr_t slots_dn, uintptr_t slots_up,
                uintptr_t stream);
 void xb_apply(int C, int E, int slot_w, uint64_t seed_dn, uint64_t seed_up, uint64_t call, uintptr_t evbuf,
               uintptr_t slots_dn, uintptr_t slots_up, uintptr_t recv_dn, uintptr_t recv_up, uintptr_t parts,
               int parts_cap, uintptr_t pair_count, uintptr_t out, int out_width, uintptr_t out_len,
               uintptr_t out_rows, uintptr_t other, uintptr_t nres, uintptr_t stream);
 void bind_gp(py::module_& m);
+void bind_pool(py::module_& m);
 void bind_fast(py::module_& m);
 }  // namespace msd
 
@@ -333,6 +336,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("xb_apply", &msd::xb_apply);
   msd::bind_fast(m);
   msd::bind_gp(m);
+  msd::bind_pool(m);
   m.def("select_indices", &msd::select_indices,
         "(count, max) of an order-preserving compaction; synchronises the stream");
 }

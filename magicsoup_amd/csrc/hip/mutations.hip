@@ -4,8 +4,8 @@
 // Both are two-phase: a cheap per-item Poisson draw over all genomes / neighbour pairs, then an
 // apply kernel for the (usually few) items that drew at least one event. An apply kernel runs one
 // wavefront per item: one lane draws the k event positions (Floyd's sorted sampling) into an LDS
-// plan, then all 64 lanes stream the new sequence into a scratch row; the host side copies the
-// rows back into the arena.
+// plan, then all 64 lanes stream the new sequence into a scratch row; arena_scatter commits the rows
+// into fresh space of the genome pool.
 #include <algorithm>
 
 #include "hip_common.h"
@@ -68,13 +68,13 @@ __device__ __forceinline__ int mutate_at(Philox& rng, uint8_t ch, double p_indel
 // an LDS plan (copy segment, literal, copy segment, ...); all lanes then stream the segments.
 // Genomes with more than kFloydMax events (very high rates) take a serial selection-sampling path.
 __device__ __forceinline__ void mut_apply_item(int j, const int64_t* sel, const int64_t* rows, const uint8_t* arena,
-                                               int width, const int32_t* lens, const int32_t* k, double p_indel,
+                                               const int64_t* off, const int32_t* lens, const int32_t* k, double p_indel,
                                                double p_del, uint64_t seed, uint64_t call, uint8_t* out, int out_width,
                                                int32_t* out_len, int* pos, uint8_t (*lit)[2], int* nlit) {
   const int lane = threadIdx.x;
   const int64_t i = sel[j];
   const int64_t r = rows ? rows[i] : i;
-  const uint8_t* s = arena + (size_t)r * width;
+  const uint8_t* s = arena + off[r];
   const int L = lens[r];
   const int kk = k[i];
   uint8_t* o = out + (size_t)j * out_width;
@@ -120,7 +120,7 @@ __device__ __forceinline__ void mut_apply_item(int j, const int64_t* sel, const 
 // dn: optional device-side item count (<= nsel): the grid strides over the items, so the host does
 // not need to know how many genomes were selected.
 __global__ void __launch_bounds__(64) mut_apply_kernel(int nsel, const int* dn, const int64_t* sel, const int64_t* rows,
-                                                       const uint8_t* arena, int width, const int32_t* lens,
+                                                       const uint8_t* arena, const int64_t* off, const int32_t* lens,
                                                        const int32_t* k, double p_indel, double p_del, uint64_t seed,
                                                        uint64_t call, uint8_t* out, int out_width, int32_t* out_len) {
   __shared__ int pos[kFloydMax];
@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(64) mut_apply_kernel(int nsel, const int* dn, 
   __shared__ int nlit[kFloydMax];
   const int ne = dn ? min(*dn, nsel) : nsel;
   for (int j = blockIdx.x; j < ne; j += gridDim.x) {
-    mut_apply_item(j, sel, rows, arena, width, lens, k, p_indel, p_del, seed, call, out, out_width, out_len, pos, lit,
+    mut_apply_item(j, sel, rows, arena, off, lens, k, p_indel, p_del, seed, call, out, out_width, out_len, pos, lit,
                    nlit);
     __syncthreads();
   }
@@ -180,7 +180,8 @@ __global__ void __launch_bounds__(256) rec_count_keys_kernel(int n, const int64_
 
 // Recombine pair sel[j] (rows ca, cb of the arena) into scratch rows 2j and 2j+1 (rec_pair_apply).
 __device__ __forceinline__ void rec_apply_item(int j, const int64_t* sel, const int32_t* pairs, const int64_t* keys,
-                                               const uint8_t* arena, int width, const int32_t* lens, const int32_t* k,
+                                               const uint8_t* arena, const int64_t* off, const int32_t* lens,
+                                               const int32_t* k,
                                                uint64_t seed, uint64_t call, int32_t* parts, int parts_cap,
                                                uint8_t* out, int out_width, int32_t* out_len, int64_t* out_rows,
                                                int32_t* lparts, int* meta) {
@@ -190,7 +191,7 @@ __device__ __forceinline__ void rec_apply_item(int j, const int64_t* sel, const 
   const int ca = keys ? (int)(keys[i] >> 32) : pairs[2 * i];
   const int cb = keys ? (int)(keys[i] & 0xFFFFFFFF) : pairs[2 * i + 1];
   int w0, w1;
-  rec_pair_apply(arena + (size_t)ca * width, lens[ca], arena + (size_t)cb * width, lens[cb], k[i], seed, call,
+  rec_pair_apply(arena + off[ca], lens[ca], arena + off[cb], lens[cb], k[i], seed, call,
                  (uint32_t)i, parts + (size_t)j * parts_cap * 3, lparts, meta, out + (size_t)(2 * j) * out_width,
                  out + (size_t)(2 * j + 1) * out_width, out_width, w0, w1);
   if (lane == 0) {
@@ -204,7 +205,7 @@ __device__ __forceinline__ void rec_apply_item(int j, const int64_t* sel, const 
 }
 
 __global__ void __launch_bounds__(64) rec_apply_kernel(int nsel, const int* dn, const int64_t* sel, const int32_t* pairs,
-                                                       const int64_t* keys, const uint8_t* arena, int width,
+                                                       const int64_t* keys, const uint8_t* arena, const int64_t* off,
                                                        const int32_t* lens, const int32_t* k, uint64_t seed,
                                                        uint64_t call, int32_t* parts, int parts_cap, uint8_t* out,
                                                        int out_width, int32_t* out_len, int64_t* out_rows) {
@@ -212,7 +213,7 @@ __global__ void __launch_bounds__(64) rec_apply_kernel(int nsel, const int* dn, 
   __shared__ int meta[2];  // number of parts, split index
   const int ne = dn ? min(*dn, nsel) : nsel;
   for (int j = blockIdx.x; j < ne; j += gridDim.x) {
-    rec_apply_item(j, sel, pairs, keys, arena, width, lens, k, seed, call, parts, parts_cap, out, out_width, out_len,
+    rec_apply_item(j, sel, pairs, keys, arena, off, lens, k, seed, call, parts, parts_cap, out, out_width, out_len,
                    out_rows, lparts, meta);
     __syncthreads();
   }
@@ -234,20 +235,27 @@ __global__ void __launch_bounds__(256) arena_mark_kernel(int k, const int* dn, i
 
 // One wavefront per result row: copy it over its arena row (zero-padding the rest of the row) and
 // its length, if it won; flags[q] = won.
+// Commit result rows into fresh space of the genome pool: every row that won its cell (mark: the
+// last result per cell) gets a new 16-byte aligned allocation (pool_alloc), its bytes, and the
+// cell's offset and length. A result longer than `width` (the pipeline's genome length bound) or a
+// full pool is left for the host (flags; reconcile raises the bound / collects the pool and
+// re-commits), so pending calls never see a genome longer than the bound they were sized for.
 __global__ void __launch_bounds__(64) arena_scatter_kernel(int k, const int* dn, int dn_mul, const int64_t* rows,
                                                            const uint8_t* src, int src_width, const int32_t* src_len,
-                                                           uint8_t* arena, int width, int32_t* lens,
+                                                           uint8_t* pool, int64_t* off, unsigned long long* top,
+                                                           long long pool_cap, int width, int32_t* lens,
                                                            const unsigned long long* mark, unsigned long long gen,
                                                            uint8_t* flags, int* gflags, int* opflags) {
   const int ke = eff_count(k, dn, dn_mul), lane = threadIdx.x;
   if (flags)  // entries past the live count read as "not won" (no separate clearing launch)
     for (int q = ke + blockIdx.x * 64 + lane; q < k; q += gridDim.x * 64) flags[q] = 0;
+  const bool vec = (src_width & 15) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0;
   for (int q = blockIdx.x; q < ke; q += gridDim.x) {
     const int64_t r = rows[q];
     const bool won = !mark || mark[r] == ((gen << 32) | (unsigned long long)q);
     if (lane == 0 && flags) flags[q] = won;
     if (!won) continue;
-    if (gflags && src_len[q] > width) {  // too long for the arena: left for the host (reconcile)
+    if (gflags && src_len[q] > width) {  // longer than the bound: left for the host (reconcile)
       if (lane == 0) {
         atomicOr(gflags, kGpWidth);
         atomicOr(opflags, kGpWidth);
@@ -255,15 +263,31 @@ __global__ void __launch_bounds__(64) arena_scatter_kernel(int k, const int* dn,
       continue;
     }
     const int L = min(src_len[q], width);
+    long long o = 0;
+    if (lane == 0) o = pool_alloc(top, pool_cap, L);
+    o = (long long)(((unsigned long long)(unsigned)__shfl((int)(o >> 32), 0) << 32) |
+                    (unsigned long long)(unsigned)__shfl((int)(o & 0xFFFFFFFFll), 0));
+    if (o < 0) {  // pool full: the same route as a too long result
+      if (lane == 0 && gflags) {
+        atomicOr(gflags, kGpWidth);
+        atomicOr(opflags, kGpWidth);
+      }
+      continue;
+    }
     const uint8_t* s = src + (size_t)q * src_width;
-    uint8_t* d = arena + (size_t)r * width;
-    for (int t = lane; t < width; t += 64) d[t] = t < L ? s[t] : 0;
-    if (lane == 0) lens[r] = L;
+    uint8_t* d = pool + o;
+    if (vec) {
+      for (int t = lane * 16; t < L; t += 64 * 16) *reinterpret_cast<uint4*>(d + t) = *reinterpret_cast<const uint4*>(s + t);
+    } else {
+      for (int t = lane; t < L; t += 64) d[t] = s[t];
+    }
+    if (lane == 0) {
+      off[r] = o;
+      lens[r] = L;
+    }
   }
 }
 
-// Item grids: with a device count (dn != 0) the launch covers at most kDevGrid blocks that stride
-// over the items; the host passes the capacity as n.
 constexpr unsigned kDevGrid = 2048;
 static unsigned item_grid(long long n, uintptr_t dn) {
   return dn ? (unsigned)std::min<long long>(n, kDevGrid) : (unsigned)n;
@@ -278,13 +302,13 @@ void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, u
   MS_LAUNCH_CHECK();
 }
 
-void mut_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t rows, uintptr_t arena, int width, uintptr_t lens,
+void mut_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t rows, uintptr_t arena, uintptr_t off, uintptr_t lens,
                uintptr_t k, double p_indel, double p_del, uint64_t seed, uint64_t call, uintptr_t out, int out_width,
                uintptr_t out_len, uintptr_t stream) {
   if (nsel <= 0) return;
   mut_apply_kernel<<<item_grid(nsel, dn), 64, 0, S_(stream)>>>(
       nsel, dn ? P_<int>(dn) : nullptr, P_<int64_t>(sel), rows ? P_<int64_t>(rows) : nullptr, P_<uint8_t>(arena),
-      width, P_<int32_t>(lens), P_<int32_t>(k), p_indel, p_del, seed, call, P_<uint8_t>(out), out_width,
+      P_<int64_t>(off), P_<int32_t>(lens), P_<int32_t>(k), p_indel, p_del, seed, call, P_<uint8_t>(out), out_width,
       P_<int32_t>(out_len));
   MS_LAUNCH_CHECK();
 }
@@ -306,14 +330,15 @@ void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t se
   MS_LAUNCH_CHECK();
 }
 
-void rec_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t pairs, uintptr_t keys, uintptr_t arena, int width,
+void rec_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t pairs, uintptr_t keys, uintptr_t arena, uintptr_t off,
                uintptr_t lens, uintptr_t k, uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out,
                int out_width, uintptr_t out_len, uintptr_t out_rows, uintptr_t stream) {
   if (nsel <= 0) return;
   if ((pairs == 0) == (keys == 0)) throw std::invalid_argument("rec_apply: give exactly one of pairs / keys");
   rec_apply_kernel<<<item_grid(nsel, dn), 64, 0, S_(stream)>>>(
       nsel, dn ? P_<int>(dn) : nullptr, P_<int64_t>(sel), pairs ? P_<int32_t>(pairs) : nullptr,
-      keys ? P_<int64_t>(keys) : nullptr, P_<uint8_t>(arena), width, P_<int32_t>(lens), P_<int32_t>(k), seed, call,
+      keys ? P_<int64_t>(keys) : nullptr, P_<uint8_t>(arena), P_<int64_t>(off), P_<int32_t>(lens), P_<int32_t>(k), seed,
+      call,
       P_<int32_t>(parts), parts_cap, P_<uint8_t>(out), out_width, P_<int32_t>(out_len),
       out_rows ? P_<int64_t>(out_rows) : nullptr);
   MS_LAUNCH_CHECK();
@@ -321,8 +346,9 @@ void rec_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t pairs, uintptr_t
 
 // k result rows (capacity when dn != 0: then *dn * dn_mul rows are live)
 void arena_scatter(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t src, int src_width, uintptr_t src_len,
-                   uintptr_t arena, int width, uintptr_t lens, uintptr_t mark, uint64_t gen, uintptr_t flags,
-                   uintptr_t gflags, uintptr_t opflags, uintptr_t stream) {
+                   uintptr_t pool, uintptr_t off, uintptr_t top, long long pool_cap, int width, uintptr_t lens,
+                   uintptr_t mark, uint64_t gen, uintptr_t flags, uintptr_t gflags, uintptr_t opflags,
+                   uintptr_t stream) {
   if (gflags && !opflags) throw std::invalid_argument("arena_scatter: gflags needs opflags");
   if (k <= 0) return;
   const int* d = dn ? P_<int>(dn) : nullptr;
@@ -332,8 +358,8 @@ void arena_scatter(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t sr
     MS_LAUNCH_CHECK();
   }
   arena_scatter_kernel<<<item_grid(k, dn), 64, 0, S_(stream)>>>(
-      k, d, dn_mul, P_<int64_t>(rows), P_<uint8_t>(src), src_width, P_<int32_t>(src_len), P_<uint8_t>(arena), width,
-      P_<int32_t>(lens), mark ? P_<unsigned long long>(mark) : nullptr, gen, flags ? P_<uint8_t>(flags) : nullptr,
+      k, d, dn_mul, P_<int64_t>(rows), P_<uint8_t>(src), src_width, P_<int32_t>(src_len), P_<uint8_t>(pool),
+      P_<int64_t>(off), P_<unsigned long long>(top), pool_cap, width, P_<int32_t>(lens), mark ? P_<unsigned long long>(mark) : nullptr, gen, flags ? P_<uint8_t>(flags) : nullptr,
       gflags ? P_<int>(gflags) : nullptr, opflags ? P_<int>(opflags) : nullptr);
   MS_LAUNCH_CHECK();
 }

@@ -1,0 +1,129 @@
+// The GPU genome pool (models/strings.py PoolArena): genomes of every length in one byte buffer at
+// per-cell offsets, instead of rows as wide as the longest genome.
+//
+// The reference keeps each genome as its own Python string (python/magicsoup/world.py:192-194) and
+// its Rust mutates strings one by one (rust/mutations.rs:11-154). Here a cell's genome is the
+// lens[i] bytes at pool + off[i]; storage is allocated by an atomic bump of a device counter
+// (hip_common.h pool_alloc, 16-byte aligned) and never written again: a mutated or recombined genome
+// takes new space, a dividing cell's child shares its parent's bytes (only off / lens are copied), a
+// killed cell only leaves its offset behind. The space of genomes nobody references any more is
+// reclaimed by a compaction that keeps shared genomes shared (pool_compact, PoolArena.collect).
+#include <pybind11/pybind11.h>
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "hip_common.h"
+
+namespace msd {
+
+// One wavefront per genome j: bytes rows[j, :lens[j]] (row stride L_in) -> a new allocation; cell
+// dst[j] (or n0 + j) gets its offset and length. A full pool sets *failed (the host sized the pool
+// so that it never is; the flag makes a sizing bug loud instead of silent).
+__global__ void __launch_bounds__(64) pool_write_kernel(int k, int L_in, const uint8_t* rows, const int32_t* lens,
+                                                        const int64_t* dst, long long n0, uint8_t* pool, int64_t* off,
+                                                        unsigned long long* top, long long cap, int32_t* out_lens,
+                                                        int* failed) {
+  const int lane = threadIdx.x;
+  const bool vec = (L_in & 15) == 0 && (reinterpret_cast<uintptr_t>(rows) & 15) == 0;
+  for (int j = blockIdx.x; j < k; j += gridDim.x) {
+    const int L = min(max(lens[j], 0), L_in);
+    long long o = 0;
+    if (lane == 0) o = pool_alloc(top, cap, L);
+    o = (long long)(((unsigned long long)(unsigned)__shfl((int)(o >> 32), 0) << 32) |
+                    (unsigned long long)(unsigned)__shfl((int)(o & 0xFFFFFFFFll), 0));
+    const long long c = dst ? dst[j] : n0 + j;
+    if (o < 0) {
+      if (lane == 0) {
+        if (failed) atomicOr(failed, 1);
+        off[c] = 0;
+        out_lens[c] = 0;
+      }
+      continue;
+    }
+    const uint8_t* s = rows + (size_t)j * L_in;
+    uint8_t* d = pool + o;
+    if (vec) {
+      for (int t = lane * 16; t < L; t += 64 * 16) *reinterpret_cast<uint4*>(d + t) = *reinterpret_cast<const uint4*>(s + t);
+    } else {
+      for (int t = lane; t < L; t += 64) d[t] = s[t];
+    }
+    if (lane == 0) {
+      off[c] = o;
+      out_lens[c] = L;
+    }
+  }
+}
+
+// Genomes of cells src[j] (or j) -> zero-padded rows out[j, :W] (at most W bytes each).
+__global__ void __launch_bounds__(64) pool_read_kernel(int k, const int64_t* src, const uint8_t* pool,
+                                                       const int64_t* off, const int32_t* lens, uint8_t* out, int W) {
+  const int lane = threadIdx.x;
+  for (int j = blockIdx.x; j < k; j += gridDim.x) {
+    const long long c = src ? src[j] : j;
+    const int L = min(lens[c], W);
+    const uint8_t* s = pool + off[c];
+    uint8_t* d = out + (size_t)j * W;
+    for (int t = lane; t < W; t += 64) d[t] = t < L ? s[t] : 0;
+  }
+}
+
+// Compaction: unique genome u (old offset old_off[u], size bytes) -> new_pool + new_off[u].
+__global__ void __launch_bounds__(64) pool_compact_kernel(int nu, const uint8_t* old_pool, const int64_t* old_off,
+                                                          const int64_t* sizes, uint8_t* new_pool,
+                                                          const int64_t* new_off) {
+  const int lane = threadIdx.x;
+  for (int u = blockIdx.x; u < nu; u += gridDim.x) {
+    const uint4* s = reinterpret_cast<const uint4*>(old_pool + old_off[u]);
+    uint4* d = reinterpret_cast<uint4*>(new_pool + new_off[u]);
+    const long long n16 = sizes[u] / 16;  // allocations are 16-byte multiples
+    for (long long t = lane; t < n16; t += 64) d[t] = s[t];
+  }
+}
+
+static unsigned grid_for(long long k) { return (unsigned)std::max<long long>(1, std::min<long long>(k, 8192)); }
+
+void pool_write(int k, int L_in, uintptr_t rows, uintptr_t lens, uintptr_t dst, long long n0, uintptr_t pool,
+                uintptr_t off, uintptr_t top, long long cap, uintptr_t out_lens, uintptr_t failed, uintptr_t stream) {
+  if (k <= 0) return;
+  if (L_in < 0) throw std::invalid_argument("pool_write: negative row width");
+  pool_write_kernel<<<grid_for(k), 64, 0, S_(stream)>>>(k, L_in, P_<uint8_t>(rows), P_<int32_t>(lens),
+                                                        dst ? P_<int64_t>(dst) : nullptr, n0, P_<uint8_t>(pool),
+                                                        P_<int64_t>(off), P_<unsigned long long>(top), cap,
+                                                        P_<int32_t>(out_lens), failed ? P_<int>(failed) : nullptr);
+  MS_LAUNCH_CHECK();
+}
+
+void pool_read(int k, uintptr_t src, uintptr_t pool, uintptr_t off, uintptr_t lens, uintptr_t out, int W,
+               uintptr_t stream) {
+  if (k <= 0 || W <= 0) return;
+  pool_read_kernel<<<grid_for(k), 64, 0, S_(stream)>>>(k, src ? P_<int64_t>(src) : nullptr, P_<uint8_t>(pool),
+                                                       P_<int64_t>(off), P_<int32_t>(lens), P_<uint8_t>(out), W);
+  MS_LAUNCH_CHECK();
+}
+
+void pool_compact(int nu, uintptr_t old_pool, uintptr_t old_off, uintptr_t sizes, uintptr_t new_pool,
+                  uintptr_t new_off, uintptr_t stream) {
+  if (nu <= 0) return;
+  if ((old_pool | new_pool) & 15) throw std::invalid_argument("pool_compact: pools must be 16-byte aligned");
+  pool_compact_kernel<<<grid_for(nu), 64, 0, S_(stream)>>>(nu, P_<uint8_t>(old_pool), P_<int64_t>(old_off),
+                                                           P_<int64_t>(sizes), P_<uint8_t>(new_pool),
+                                                           P_<int64_t>(new_off));
+  MS_LAUNCH_CHECK();
+}
+
+void bind_pool(pybind11::module_& m) {
+  namespace py = pybind11;
+  py::class_<GenomePoolArgs>(m, "GenomePoolArgs", py::module_local())
+      .def(py::init<>())
+      .def_readwrite("pool", &GenomePoolArgs::pool)
+      .def_readwrite("off", &GenomePoolArgs::off)
+      .def_readwrite("top", &GenomePoolArgs::top)
+      .def_readwrite("failed", &GenomePoolArgs::failed)
+      .def_readwrite("cap", &GenomePoolArgs::cap);
+  m.def("pool_write", &pool_write, "genome rows (k, L) -> new pool allocations of cells dst[j] (or n0 + j)");
+  m.def("pool_read", &pool_read, "genomes of cells -> zero-padded rows (k, W)");
+  m.def("pool_compact", &pool_compact, "copy unique genomes into a new pool (PoolArena.collect)");
+}
+
+}  // namespace msd

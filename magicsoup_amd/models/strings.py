@@ -2,9 +2,11 @@
 
 The reference keeps ``world.cell_genomes`` / ``world.cell_labels`` as Python ``list[str]``
 (``world.py:192-194``) and copies every genome across the Rust FFI on each mutation step. Here the
-strings live in a byte arena on the world's device — one row of ``width`` bytes per cell plus a
-length — so translation, mutation, recombination, division and compaction kernels work on them in
-place. ``StringColumn`` is the list-like view users see: indexing, iteration, comparison and
+strings live on the world's device: GPU genomes in a ragged byte pool (:class:`PoolArena`: per-cell
+offsets and lengths, no padding, shared between a parent and its children), labels and CPU genomes
+in a row arena (:class:`StringArena`: one row of ``width`` bytes per cell plus a length, what the
+OpenMP host core works on). Translation, mutation, recombination, division and compaction kernels
+work on them in place. ``StringColumn`` is the list-like view users see: indexing, iteration, comparison and
 assignment materialise / upload only what is touched, and a full materialisation is cached until the
 arena changes.
 """
@@ -162,6 +164,14 @@ class StringArena:
     def view(self) -> tuple[torch.Tensor, torch.Tensor]:
         return self.data[: self.n], self.lens[: self.n]
 
+    def rows_of(self, cells: torch.Tensor | None, width: int | None = None) -> torch.Tensor:
+        """Rows of ``cells`` (all when None), cut or zero-padded to ``width`` (default: the row width)."""
+        rows = self.data[: self.n] if cells is None else self.data[cells.to(self.device, torch.long)]
+        w = self.width if width is None else int(width)
+        if w <= rows.size(1):
+            return rows[:, :w]
+        return torch.nn.functional.pad(rows, (0, w - rows.size(1)))
+
     # ---------------------------------------------------------------- materialisation
     def to_strings(self, rows: Iterable[int] | None = None) -> list[str]:
         """The strings of all rows (or of ``rows``): the rows (cut to the longest string) are copied
@@ -183,6 +193,257 @@ class StringArena:
         # rows cut to the longest string, one transfer; the host core concatenates the used bytes
         sub = data[:, :lmax].contiguous().cpu().numpy()
         raw = native.host().unpack_rows(sub, ls.numpy().astype(np.int32, copy=False)).decode("ascii")
+        ends = np.cumsum(ls.numpy(), dtype=np.int64).tolist()
+        starts = [0] + ends[:-1]
+        return [raw[a:b] for a, b in zip(starts, ends)]
+
+
+_POOL_MIN = 16 << 20  # bytes
+
+
+def _r16(n: int) -> int:
+    return (int(n) + 15) // 16 * 16
+
+
+class PoolArena:
+    """GPU genomes of every length in one byte pool (``csrc/hip/pool.hip``).
+
+    Cell i's genome is the ``lens[i]`` bytes at ``data[off[i]:]``. Storage is taken by an atomic bump
+    of the device counter ``top`` (16-byte aligned) and never written again: mutated or recombined
+    genomes get new space (the device pipeline's commit), a dividing cell's child shares its parent's
+    bytes (only ``off`` / ``lens`` are cloned), a kill compacts ``off`` / ``lens`` only. Nothing is as
+    wide as the longest genome: one 20 kbp genome costs 20 kB, and no event re-lays the population
+    out (the reference keeps one Python string per cell, ``world.py:192-194``).
+
+    ``width`` is not a row width but the genome length bound the device pipeline sizes its scratch
+    for: a result longer than it is committed on the host at reconcile (which raises the bound, an
+    O(1) change). ``top_ub`` is the host's upper bound of the device counter; :meth:`ensure` collects
+    (:meth:`collect`: unreferenced space is dropped, shared genomes stay shared) or grows the pool
+    before an allocation could overrun it. Callers collect only with no device work pending on the
+    pool (the World reconciles its genome pipeline first)."""
+
+    def __init__(self, device, width: int = 64, capacity: int = 0):
+        self.device = torch.device(device)
+        self.width = _round_width(width)
+        self.lens = torch.zeros(capacity, dtype=torch.int32, device=self.device)
+        self.off = torch.zeros(capacity, dtype=torch.int64, device=self.device)
+        self.data = torch.empty(_POOL_MIN, dtype=torch.uint8, device=self.device)
+        self.top = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.failed = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.top_ub = 0
+        self.n = 0
+        self.version = 0
+
+    # ---------------------------------------------------------------- capacity
+    @property
+    def capacity(self) -> int:
+        return int(self.lens.size(0))
+
+    @property
+    def pool_cap(self) -> int:
+        return int(self.data.numel())
+
+    def args(self):
+        """The pool as the kernels take it (GenomePoolArgs)."""
+        from magicsoup_amd.ops import native
+
+        a = native.hip().GenomePoolArgs()
+        a.pool, a.off, a.top = self.data.data_ptr(), self.off.data_ptr(), self.top.data_ptr()
+        a.failed, a.cap = self.failed.data_ptr(), self.pool_cap
+        return a
+
+    def reserve(self, rows: int, width: int | None = None) -> None:
+        """Room for ``rows`` cells; ``width`` raises the genome length bound (no data moves)."""
+        if width is not None and _round_width(width) > self.width:
+            self.width = _round_width(width)
+        if rows <= self.capacity:
+            return
+        cap = max(rows, int(self.capacity * 1.5) + 16)
+        lens = torch.zeros(cap, dtype=torch.int32, device=self.device)
+        off = torch.zeros(cap, dtype=torch.int64, device=self.device)
+        if self.n:
+            lens[: self.n] = self.lens[: self.n]
+            off[: self.n] = self.off[: self.n]
+        self.lens, self.off = lens, off
+        self.__dict__.pop("_spare", None)
+        self.version += 1
+
+    def ensure(self, need: int) -> None:
+        """Room for ``need`` more bytes of allocations: first a re-read of the device counter (the host
+        bound adds worst cases), then a collection / growth of the pool."""
+        if self.top_ub + need <= self.pool_cap:
+            return
+        self.top_ub = int(self.top.item())
+        if self.top_ub + need <= self.pool_cap:
+            return
+        self.collect(need)
+
+    def collect(self, extra: int = 0) -> None:
+        """Move the referenced genomes into a fresh pool (each distinct genome once, in offset order)
+        with room for ``extra`` more bytes; unreferenced space is dropped. One synchronisation."""
+        from magicsoup_amd.ops import native
+        from magicsoup_amd.ops.hip_ops import _stream
+
+        n = self.n
+        if n == 0:
+            self.data = torch.empty(max(_POOL_MIN, 2 * _r16(extra)), dtype=torch.uint8, device=self.device)
+            self.top.zero_()
+            self.top_ub = 0
+            return
+        off, lens = self.off[:n], self.lens[:n]
+        uo, inv = torch.unique(off, return_inverse=True)
+        size_u = torch.zeros_like(uo)
+        size_u.scatter_(0, inv, ((lens.to(torch.int64) + 15) // 16) * 16)
+        new_u = torch.cumsum(size_u, 0) - size_u
+        total = int((new_u[-1] + size_u[-1]).item())
+        cap = max(_POOL_MIN, 2 * (total + _r16(extra)))
+        new = torch.empty(cap, dtype=torch.uint8, device=self.device)
+        native.hip().pool_compact(int(uo.numel()), self.data.data_ptr(), uo.data_ptr(), size_u.data_ptr(),
+                                  new.data_ptr(), new_u.data_ptr(), _stream())
+        self.off[:n] = new_u[inv]
+        self.data = new
+        self.top.fill_(total)
+        self.top_ub = total
+        self.version += 1
+
+    def _write(self, rows: torch.Tensor, lens: torch.Tensor, dst: torch.Tensor | None, n0: int) -> None:
+        """Genome rows (k, L) -> new allocations of cells ``dst`` (or n0 + j)."""
+        from magicsoup_amd.ops import native
+        from magicsoup_amd.ops.hip_ops import _stream
+
+        k, L = int(rows.size(0)), int(rows.size(1))
+        if k == 0:
+            return
+        rows = rows.to(self.device, torch.uint8).contiguous()
+        lens = lens.to(self.device, torch.int32).contiguous()
+        self.reserve(self.capacity if dst is not None else n0 + k, L)
+        need = k * _r16(L)
+        self.ensure(need)
+        dst = None if dst is None else dst.to(self.device, torch.int64).contiguous()
+        native.hip().pool_write(k, L, rows.data_ptr(), lens.data_ptr(), 0 if dst is None else dst.data_ptr(), n0,
+                                self.data.data_ptr(), self.off.data_ptr(), self.top.data_ptr(), self.pool_cap,
+                                self.lens.data_ptr(), self.failed.data_ptr(), _stream())
+        self.top_ub += need
+
+    def check(self) -> None:
+        """Raise if an allocation ever found the pool full (a sizing bug; one read of the flag)."""
+        if int(self.failed.item()):
+            raise RuntimeError("genome pool overflow: an allocation found the pool full")
+
+    # ---------------------------------------------------------------- bulk ops (StringArena's interface)
+    def append_packed(self, rows: torch.Tensor, lens: torch.Tensor) -> None:
+        k = int(rows.size(0))
+        if k == 0:
+            return
+        self.reserve(self.n + k, int(rows.size(1)))
+        self._write(rows, lens, None, self.n)
+        self.n += k
+        self.version += 1
+
+    def append_strings(self, strs: list[str]) -> None:
+        if not strs:
+            return
+        arr, lens = pack_strings(strs)
+        self.append_packed(torch.from_numpy(arr), torch.from_numpy(lens))
+
+    def append_rows_from(self, src_rows: torch.Tensor) -> None:
+        """Append cells sharing the genomes of ``src_rows`` (children inherit their parent's)."""
+        k = int(src_rows.numel())
+        if k == 0:
+            return
+        self.reserve(self.n + k)
+        src_rows = src_rows.to(self.device, torch.long)
+        self.off[self.n : self.n + k] = self.off[src_rows]
+        self.lens[self.n : self.n + k] = self.lens[src_rows]
+        self.n += k
+        self.version += 1
+
+    def set_rows(self, rows: torch.Tensor, packed: torch.Tensor, lens: torch.Tensor) -> None:
+        if rows.numel() == 0:
+            return
+        self._write(packed, lens, rows.to(torch.int64), 0)
+        self.version += 1
+
+    def set_strings(self, rows: list[int], strs: list[str]) -> None:
+        if not rows:
+            return
+        arr, lens = pack_strings(strs)
+        self.set_rows(torch.tensor(rows, dtype=torch.long), torch.from_numpy(arr), torch.from_numpy(lens))
+
+    def keep(self, keep_idx: torch.Tensor) -> None:
+        k = int(keep_idx.numel())
+        self.off[:k] = self.off[keep_idx]
+        self.lens[:k] = self.lens[keep_idx]
+        self.n = k
+        self.version += 1
+
+    def clear(self) -> None:
+        self.n = 0
+        self.top.zero_()
+        self.top_ub = 0
+        self.version += 1
+
+    # ---------------------------------------------------------------- fused row movement (device)
+    def compact_pairs(self, k: int) -> list[tuple[torch.Tensor, torch.Tensor]]:
+        """(source, target) per-cell tensors (offsets, lengths) of an order-preserving compaction to
+        ``k`` cells into the spares (see :meth:`commit_compact`); no genome byte moves."""
+        sp = self.__dict__.get("_spare")
+        cap = max(k, self.capacity)
+        if sp is None or sp[0].size(0) < cap or sp[0].device != self.off.device:
+            sp = (torch.empty(cap, dtype=torch.int64, device=self.device),
+                  torch.empty(cap, dtype=torch.int32, device=self.device))
+            self.__dict__["_spare"] = sp
+        return [(self.off[: self.n], sp[0][:k]), (self.lens[: self.n], sp[1][:k])]
+
+    def commit_compact(self, k: int) -> None:
+        so, sl = self.__dict__.pop("_spare")
+        self.__dict__["_spare"] = (self.off, self.lens)
+        self.off, self.lens = so, sl
+        self.n = k
+        self.version += 1
+
+    def clone_pairs(self, k: int) -> list[tuple[torch.Tensor, torch.Tensor]]:
+        """Append ``k`` cells; in-place (source, target) offset / length tensors over old and new
+        cells for cloning existing cells' entries into the new ones (shared genomes)."""
+        self.reserve(self.n + k)
+        self.n += k
+        self.version += 1
+        return [(self.off[: self.n], self.off[: self.n]), (self.lens[: self.n], self.lens[: self.n])]
+
+    def rows_of(self, cells: torch.Tensor | None, width: int | None = None) -> torch.Tensor:
+        """Genomes of ``cells`` (all when None) as zero-padded uint8 rows (k, width) on the device
+        (width: the longest of them, rounded up to 16, unless given)."""
+        from magicsoup_amd.ops import native
+        from magicsoup_amd.ops.hip_ops import _stream
+
+        idx = None if cells is None else cells.to(self.device, torch.int64).contiguous()
+        k = self.n if idx is None else int(idx.numel())
+        if width is None:
+            ls = self.lens[: self.n] if idx is None else self.lens[idx]
+            width = _r16(int(ls.max().item())) if k else 16
+        out = torch.empty(k, max(int(width), 1), dtype=torch.uint8, device=self.device)
+        if k:
+            native.hip().pool_read(k, 0 if idx is None else idx.data_ptr(), self.data.data_ptr(), self.off.data_ptr(),
+                                   self.lens.data_ptr(), out.data_ptr(), int(out.size(1)), _stream())
+        return out
+
+    def view(self) -> tuple[torch.Tensor, torch.Tensor]:
+        """(rows (n, width), lengths) -- padded copies of the genomes (the pool holds no rows)."""
+        return self.rows_of(None), self.lens[: self.n]
+
+    # ---------------------------------------------------------------- materialisation
+    def to_strings(self, rows: Iterable[int] | None = None) -> list[str]:
+        idx = None if rows is None else torch.as_tensor(list(rows), dtype=torch.long, device=self.device)
+        lens = self.lens[: self.n] if idx is None else self.lens[idx]
+        ls = lens.cpu()
+        k = int(ls.numel())
+        lmax = int(ls.max()) if k else 0
+        if lmax == 0:
+            return [""] * k
+        from magicsoup_amd.ops import native
+
+        data = self.rows_of(idx, _r16(lmax)).cpu().numpy()
+        raw = native.host().unpack_rows(data, ls.numpy().astype(np.int32, copy=False)).decode("ascii")
         ends = np.cumsum(ls.numpy(), dtype=np.int64).tolist()
         starts = [0] + ends[:-1]
         return [raw[a:b] for a, b in zip(starts, ends)]

@@ -36,7 +36,7 @@ import torch
 from magicsoup_amd.models.containers import Cell, Chemistry
 from magicsoup_amd.models.genetics import Genetics
 from magicsoup_amd.models.kinetics import Kinetics
-from magicsoup_amd.models.strings import StringArena, StringColumn, pack_strings
+from magicsoup_amd.models.strings import PoolArena, StringArena, StringColumn, pack_strings
 from magicsoup_amd.ops import world_ops
 from magicsoup_amd.utils.util import randstr
 from magicsoup_amd.utils import profiling
@@ -255,7 +255,9 @@ class World:
         dev = torch.device(device)
         m = self.n_molecules
         self.n_cells = 0
-        self._genomes = StringArena(dev, width=64)
+        # GPU genomes: a ragged pool (per-cell offsets, shared by parents and children); CPU worlds
+        # keep rows, which the OpenMP host core works on
+        self._genomes = PoolArena(dev) if dev.type == "cuda" else StringArena(dev, width=64)
         self._labels = StringArena(dev, width=16)
         self._genome_col = StringColumn(self._genomes)
         self._label_col = StringColumn(self._labels)
@@ -348,6 +350,7 @@ class World:
             refs.append(arena.data)
             refs.append(arena.lens)
             refs.append(arena.__dict__.get("_spare"))
+            refs.append(arena.__dict__.get("off"))
         kd = self.kinetics.__dict__
         refs.extend(kd.get("_store_d", {}).values())
         refs.extend(kd.get("_spare", {}).values())
@@ -825,7 +828,8 @@ class World:
                                 _p(cols["cell_divisions"].buf), _p(cols["cell_lifetimes"].buf), _stream())
         if k:
             sb = kin.__dict__["_slot_buf"]
-            pairs = [(g.data[:n0], g.data[n0 : n0 + k], g.lens), (g.lens[:n0], g.lens[n0 : n0 + k]),
+            # (children share their parent's genome: offsets and lengths only)
+            pairs = [(g.off[:n0], g.off[n0 : n0 + k]), (g.lens[:n0], g.lens[n0 : n0 + k]),
                      (lab.data[:n0], lab.data[n0 : n0 + k], lab.lens), (lab.lens[:n0], lab.lens[n0 : n0 + k]),
                      (sb[:n0], sb[n0 : n0 + k])]
             hip_ops.gather_rows(pairs, k, src_rows=par)
@@ -899,7 +903,7 @@ class World:
             cap = min(min(int(c.buf.size(0)) for c in cols.values()), g.capacity, lab.capacity,
                       int(kd["_slot_buf"].numel()))
         fw = d.get("_fw")
-        key = (cap, g.width, lab.width, g.data.data_ptr(), g.lens.data_ptr(), lab.data.data_ptr(),
+        key = (cap, lab.width, g.data.data_ptr(), g.off.data_ptr(), g.lens.data_ptr(), g.pool_cap, lab.data.data_ptr(),
                lab.lens.data_ptr(), kd["_slot_buf"].data_ptr(), kd["_slot_spare"].data_ptr(),
                self.__dict__["_cell_map"].data_ptr(), *(c.buf.data_ptr() for c in cols.values()))
         if fw is not None and d.get("_fw_key") == key:
@@ -926,11 +930,12 @@ class World:
         fw.mols, fw.pos, fw.life, fw.div = (cols[k].buf.data_ptr() for k in names)
         fw.mols_sp, fw.pos_sp, fw.life_sp, fw.div_sp = (cols[k].spare.data_ptr() for k in names)
         gs, ls = g.__dict__["_spare"], lab.__dict__["_spare"]
-        fw.g_data, fw.g_lens, fw.g_data_sp, fw.g_lens_sp = (g.data.data_ptr(), g.lens.data_ptr(), gs[0].data_ptr(),
-                                                            gs[1].data_ptr())
+        fw.g_off, fw.g_lens, fw.g_off_sp, fw.g_lens_sp = (g.off.data_ptr(), g.lens.data_ptr(), gs[0].data_ptr(),
+                                                          gs[1].data_ptr())
+        fw.gpool = g.args()
         fw.l_data, fw.l_lens, fw.l_data_sp, fw.l_lens_sp = (lab.data.data_ptr(), lab.lens.data_ptr(),
                                                             ls[0].data_ptr(), ls[1].data_ptr())
-        fw.g_width, fw.l_width = int(g.width), int(lab.width)
+        fw.l_width = int(lab.width)
         fw.slot, fw.slot_sp = kd["_slot_buf"].data_ptr(), kd["_slot_spare"].data_ptr()
         fw.cell_map = hip_ops._cell_map_bytes(self).data_ptr()
         fw.sel, fw.pending, fw.cand, fw.result, fw.wins, fw.par = (bufs[k].data_ptr() for k in (
@@ -1193,14 +1198,13 @@ class World:
         rows = rows.to(self.device, torch.long)
         if rows.numel() == 0:
             return
-        data, lens = self._genomes.view()
-        tokens, nprots = world_ops.translate(self, data, lens, rows)
+        tokens, nprots = world_ops.translate(self, rows)
         P = int(tokens.size(1))
         if P > self.kinetics._P():
             # a new longest proteome: grow with headroom on the GPU (1.5x) so that genomes growing
             # through recombination do not re-layout the parameter storage every few dozen steps
             # (padding proteins are inert: Vmax 0)
-            self.kinetics.increase_max_proteins(P + max(8, P // 2) if data.is_cuda else P)
+            self.kinetics.increase_max_proteins(P + max(8, P // 2) if rows.is_cuda else P)
         # one build launch: rows without proteins are unset in the same pass
         self.kinetics.set_cell_params_tokens(rows, tokens, nprot=nprots)
 
@@ -1254,7 +1258,7 @@ class World:
         self.__dict__["_cols"] = {k: _Column(v.to(dev)) for k, v in cols.items()}
         for c in self._cols.values():
             c.view(int(c.buf.size(0)))
-        self.__dict__["_genomes"] = StringArena(dev, width=64)
+        self.__dict__["_genomes"] = PoolArena(dev) if dev.type == "cuda" else StringArena(dev, width=64)
         self.__dict__["_labels"] = StringArena(dev, width=16)
         self._genomes.append_strings(genomes)
         self._labels.append_strings(labels)

@@ -10,10 +10,11 @@ Every kernel after the selection strides over the device-side count (``dn`` argu
 ``csrc/hip``), so the host issues the chain without a synchronisation and runs ahead into the next
 operations while the GPU works. What the host cannot rule out in advance raises flag bits instead:
 
-* a result longer than the genome arena's row width is not committed (``arena_scatter``); every
+* a result longer than the genome pool's length bound (``PoolArena.width``, what the calls' scratch
+  rows are sized for), or one that finds the pool full, is not committed (``arena_scatter``); every
   later pipeline op of the same pending chain then does nothing (its count kernel sees the flag)
-  and is *replayed* at reconcile time with its original RNG stream, after the arena was widened and
-  the result committed -- exactly the sequential outcome;
+  and is *replayed* at reconcile time with its original RNG stream, after the bound was raised /
+  the pool collected and the result committed -- exactly the sequential outcome;
 * a proteome with more proteins than the parameter storage holds, more domains than the token
   slots, or a genome too long for the LDS translation pass, and parameter rows running out
   (``gp_check_assign_kernel``): the affected cells are rebuilt on the synchronous path.
@@ -136,7 +137,7 @@ def _begin(world, kind: str) -> dict:
 
 
 def _arena_desc(world, b: dict):
-    """C++ descriptor of the genome arena and this call's device counters (gp.hip GpArena)."""
+    """C++ descriptor of the genome pool and this call's device counters (gp.hip GpArena)."""
     a = b.get("desc")
     if a is None:
         a = b["desc"] = _m().GpArena()
@@ -144,7 +145,20 @@ def _arena_desc(world, b: dict):
                                                         _p(b["gflags"]), _p(b["d_rows"]))
     arena = world._genomes
     a.data, a.lens, a.width, a.n = arena.data.data_ptr(), arena.lens.data_ptr(), arena.width, arena.n
+    a.off, a.top, a.pool_cap = arena.off.data_ptr(), arena.top.data_ptr(), arena.pool_cap
     return a
+
+
+def _r16(n: int) -> int:
+    return (int(n) + 15) // 16 * 16
+
+
+def _room(world, need: int) -> None:
+    """Pool space for a call's worst case of committed results (every selected result as long as
+    its scratch row); counted into the host bound of the device counter."""
+    arena = world._genomes
+    arena.ensure(need)
+    arena.top_ub += need
 
 
 def _gen_desc(world, dev):
@@ -255,6 +269,7 @@ def point_mutations(world, p: float, p_indel: float, p_del: float) -> bool:
     dev = arena.data.device
     cap = _cap(n * p * L, min(n, N_CAP))
     b = _begin(world, "mut")
+    _room(world, cap * _r16(L + K_CAP))
     k = _kin_desc(world, dev)
     nbytes = _m().gp_blob_bytes(0, n, cap, k.P, L, D_CAP, K_CAP, 0)
     blob = _blob(world, "mut", nbytes, dev)
@@ -286,6 +301,7 @@ def recombinate_all(world, p: float, extra=None) -> bool:
     dev = arena.data.device
     pcap = _cap(expected, min(n, N_CAP) // 2)  # pairs per call (two results each)
     b = _begin(world, "rec")
+    _room(world, (2 * pcap + (0 if extra is None else int(extra.rows))) * _r16(2 * L))
     sc = _scratch(world)
     keys, nbr = hip_ops.neighbor_slot_args(world)
     k = _kin_desc(world, dev)
@@ -357,6 +373,7 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float) -> bool:
     fresh = not st["pending"]
     if fresh:
         kin._reserve_rows(2 * min(n, N_CAP))
+    _room(world, 2 * pcap * _r16(2 * L) + mcap * _r16(L + K_CAP))
     br, bm, bu = _bufs(world, "rec"), _bufs(world, "mut"), _bufs(world, "evo")
     ar, am, au = _arena_desc(world, br), _arena_desc(world, bm), _arena_desc(world, bu)
     sc = hip_ops._scratch(world)
@@ -461,10 +478,12 @@ def _recommit(world, pd: _Pending) -> torch.Tensor:
     out_len = out_len_all[:n_res]
     need = int(out_len.max().item())
     if need > arena.width:
-        arena.reserve(arena.n, need)
+        arena.reserve(arena.n, need)  # (the pool's length bound: nothing moves)
     rows = rows_all[:n_res]
-    _m().arena_scatter(n_res, 0, 1, _p(rows), _p(out), out_w, _p(out_len), _p(arena.data), int(arena.width),
-                       _p(arena.lens), _p(r.mark), int(r.gen), 0, 0, 0, _stream())
+    _room(world, n_res * _r16(min(out_w, arena.width)))
+    _m().arena_scatter(n_res, 0, 1, _p(rows), _p(out), out_w, _p(out_len), _p(arena.data), _p(arena.off),
+                       _p(arena.top), arena.pool_cap, int(arena.width), _p(arena.lens), _p(r.mark), int(r.gen), 0, 0, 0,
+                       _stream())
     arena.version += 1
     return torch.unique(rows)
 

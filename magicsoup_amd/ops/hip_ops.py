@@ -335,12 +335,15 @@ def spawn_issue(world, rows: torch.Tensor, lens: torch.Tensor, n0: int) -> None:
     mm, corr = map_for_pixels(world)
     g, lab = world._genomes, world._labels
     failed = _scratch(world).get("spawn_failed", 1, torch.int32, mm.device)
+    need = k * ((L_in + 15) // 16 * 16)
+    g.ensure(need)  # (the genomes go to fresh pool space)
     seed, call = _rng()
     _m().spawn_dev(k, R, C, r_lo, r_hi, _p(_cell_map_bytes(world)), seed, call, int(n0), world.n_molecules,
                    _p(cols["cell_positions"].buf), _p(cols["cell_lifetimes"].buf), _p(cols["cell_divisions"].buf),
                    _p(cols["cell_molecules"].buf), _p(mm), _mdt(mm), _p(corr), _p(lab.data), int(lab.width),
-                   _p(lab.lens), L_in, _p(rows), _p(lens), _p(g.data), int(g.width), _p(g.lens), _p(failed),
-                   _stream())
+                   _p(lab.lens), L_in, _p(rows), _p(lens), _p(g.data), _p(g.off), _p(g.top), g.pool_cap, _p(g.lens),
+                   _p(failed), _p(g.failed), _stream())
+    g.top_ub += need
 
 
 def cell_state_buffer(world) -> torch.Tensor:
@@ -843,24 +846,26 @@ def neighbors(world, frm: torch.Tensor, to: torch.Tensor, pos: torch.Tensor | No
 
 
 # ---------------------------------------------------------------------------- genomes
-def translate(genetics, data: torch.Tensor, lens: torch.Tensor, rows: torch.Tensor):
-    """Two-pass device translation of arena rows ``rows`` -> (tokens (k, P, D, 5), n_prots (k,)).
+def translate(genetics, arena, rows: torch.Tensor):
+    """Two-pass device translation of the genomes of cells ``rows`` (a GPU genome pool,
+    models/strings.py PoolArena) -> (tokens (k, P, D, 5), n_prots (k,)).
 
     Genomes up to 1024 nt are translated from LDS slots; longer ones are queued by the count pass
     and translated in a second launch with global-memory slots (only when there are any)."""
+    data, lens, off = arena.data, arena.lens, arena.off
     dev = data.device
     n = int(rows.numel())
     tables = genetics.tables
     luts = genetics.device_luts(dev)
     rows64 = rows.to(torch.int64).contiguous()
-    width = int(data.size(1))
+    width = int(arena.width)
     counts = torch.empty(2 * n, dtype=torch.int32, device=dev)
     ndom = torch.empty(2 * n, dtype=torch.int32, device=dev)
     long_list = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     long_count = torch.zeros(1, dtype=torch.int32, device=dev)
     common = (_p(luts["small"]), _p(luts["dom_type"]), int(luts["dom_type"].numel()), _p(luts["two_codon"]),
               tables.dom_size, tables.dom_type_size)
-    _m().translate_count(n, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), _p(ndom), 0, 0,
+    _m().translate_count(n, _p(rows64), _p(data), _p(off), width, _p(lens), *common, _p(counts), _p(ndom), 0, 0,
                          _p(long_list), _p(long_count), 0, _stream())
     per = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
     stats = _m().translate_stats(n, _p(counts), _p(ndom), _p(long_count), _p(per), _stream())
@@ -868,27 +873,30 @@ def translate(genetics, data: torch.Tensor, lens: torch.Tensor, rows: torch.Tens
     gslot = None
     if n_long:
         gslot = torch.empty(n_long * int(_m().translate_slot_bytes(width)), dtype=torch.uint8, device=dev)
-        _m().translate_count(n_long, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), _p(ndom),
+        _m().translate_count(n_long, _p(rows64), _p(data), _p(off), width, _p(lens), *common, _p(counts), _p(ndom),
                              _p(long_list), _p(gslot), _p(long_list), _p(long_count), 0, _stream())
         stats = _m().translate_stats(n, _p(counts), _p(ndom), _p(long_count), _p(per), _stream())
     P, D = max(int(stats[0]), 1), max(int(stats[1]), 1)
     tokens = torch.zeros(n, P, D, 5, dtype=torch.int32, device=dev)
-    _m().translate_write(n, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), P, D, _p(tokens), 0, 0,
+    _m().translate_write(n, _p(rows64), _p(data), _p(off), width, _p(lens), *common, _p(counts), P, D, _p(tokens), 0, 0,
                          0, _stream())
     if n_long:
-        _m().translate_write(n_long, _p(rows64), _p(data), width, _p(lens), *common, _p(counts), P, D, _p(tokens),
+        _m().translate_write(n_long, _p(rows64), _p(data), _p(off), width, _p(lens), *common, _p(counts), P, D, _p(tokens),
                              _p(long_list), _p(gslot), 0, _stream())
     return tokens, per
 
 
 def _arena_commit(arena, rows: torch.Tensor, out: torch.Tensor, out_len: torch.Tensor, need_width: int,
                   dedupe: bool = False, owner=None) -> torch.Tensor:
-    """Write result rows ``out`` (k, w) / ``out_len`` over the arena rows ``rows`` in one launch
-    (arena_scatter); widens the arena first if a result may not fit. With ``dedupe`` the last result
-    per row wins and the winning rows are returned (one more select)."""
+    """Commit result rows ``out`` (k, w) / ``out_len`` as the genomes of cells ``rows`` in one launch
+    (arena_scatter: fresh pool space); raises the genome length bound first if a result may exceed
+    it, and makes room in the pool. With ``dedupe`` the last result per cell wins and the winning
+    cells are returned (one more select)."""
     k = int(rows.numel())
     if need_width > arena.width:
         arena.reserve(arena.n, need_width)
+    need = k * ((min(int(out.size(1)), arena.width) + 15) // 16 * 16)
+    arena.ensure(need)
     mark, gen, flags = None, 0, None
     if dedupe:
         sc = _scratch(owner)
@@ -898,8 +906,10 @@ def _arena_commit(arena, rows: torch.Tensor, out: torch.Tensor, out_len: torch.T
             sc.bufs["arena_gen"] = 0
         gen = sc.bufs["arena_gen"] = sc.bufs.get("arena_gen", 0) + 1
         flags = torch.empty(k, dtype=torch.uint8, device=rows.device)
-    _m().arena_scatter(k, 0, 1, _p(rows), _p(out), int(out.stride(0)), _p(out_len), _p(arena.data), int(arena.width),
-                       _p(arena.lens), _p(mark), int(gen), _p(flags), 0, 0, _stream())
+    _m().arena_scatter(k, 0, 1, _p(rows), _p(out), int(out.stride(0)), _p(out_len), _p(arena.data), _p(arena.off),
+                       _p(arena.top), arena.pool_cap, int(arena.width), _p(arena.lens), _p(mark), int(gen), _p(flags),
+                       0, 0, _stream())
+    arena.top_ub += need
     arena.version += 1
     if not dedupe:
         return rows
@@ -928,7 +938,7 @@ def point_mutations(world, rows, p: float, p_indel: float, p_del: float, rng=Non
     out_w = max(bound, 1)
     out = torch.empty(nsel, out_w, dtype=torch.uint8, device=dev)
     out_len = torch.empty(nsel, dtype=torch.int32, device=dev)
-    _m().mut_apply(nsel, 0, _p(sel), _p(rows64), _p(arena.data), int(arena.data.size(1)), _p(arena.lens), _p(k),
+    _m().mut_apply(nsel, 0, _p(sel), _p(rows64), _p(arena.data), _p(arena.off), _p(arena.lens), _p(k),
                    float(p_indel), float(p_del), seed, call, _p(out), out_w, _p(out_len), _stream())
     if rows64 is not None and nsel > 1:
         # explicit rows may repeat (mutate_cells([i, i])): the last mutated copy wins
@@ -1010,7 +1020,7 @@ def _rec_apply(world, pairs, keys, k: torch.Tensor, tot: torch.Tensor, seed: int
     out_len = torch.empty(2 * nsel, dtype=torch.int32, device=dev)
     out_rows = torch.empty(2 * nsel, dtype=torch.int64, device=dev)
     parts = torch.empty(nsel * parts_cap * 3, dtype=torch.int32, device=dev)
-    _m().rec_apply(nsel, 0, _p(sel), _p(pairs), _p(keys), _p(arena.data), int(arena.data.size(1)), _p(arena.lens), _p(k),
+    _m().rec_apply(nsel, 0, _p(sel), _p(pairs), _p(keys), _p(arena.data), _p(arena.off), _p(arena.lens), _p(k),
                    seed, call, _p(parts), parts_cap, _p(out), out_w, _p(out_len), _p(out_rows), _stream())
     # (a0, b0, a1, b1, ...) in pair order: the last write per cell wins (reference update order)
     return _arena_commit(arena, out_rows, out, out_len, bound, dedupe=True, owner=world)

@@ -281,10 +281,12 @@ def health_flags(world) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------------------- genomes
-def translate(world, data: torch.Tensor, lens: torch.Tensor, rows: torch.Tensor):
-    """Dense tokens (k, P, D, 5) int32 and protein counts (k,) for arena rows ``rows``."""
-    if data.is_cuda:
-        return _hip().translate(world.genetics, data, lens, rows)
+def translate(world, rows: torch.Tensor):
+    """Dense tokens (k, P, D, 5) int32 and protein counts (k,) for the genomes of cells ``rows``."""
+    arena = world._genomes
+    if arena.data.is_cuda:
+        return _hip().translate(world.genetics, arena, rows)
+    data, lens = arena.view()
     sub = data[rows].contiguous()
     sl = lens[rows].contiguous()
     tokens, nprots = world.genetics.tables.translate_tokens(sub.numpy(), sl.numpy())

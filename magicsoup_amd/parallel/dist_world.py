@@ -335,7 +335,7 @@ class DistributedWorld(World):
             life.to(torch.int32),
             mol.to(torch.float32),
             self._labels.data[cells],
-            self._genomes.data[cells],
+            self._genomes.rows_of(cells, gw),
         ]
         return _pack(cols, k), (gw, lw)
 
@@ -578,6 +578,10 @@ class DistributedWorld(World):
                 w = max(int(hdr_up[wi]), int(hdr_dn[wi]), 1)
                 if w > arena.width:
                     arena.reserve(n_new, w)
+            # the arrivals' genomes go to fresh pool space (before the descriptor: a collection moves it)
+            need = hdr_up[0] * ((int(hdr_up[2]) + 15) // 16 * 16) + hdr_dn[0] * ((int(hdr_dn[2]) + 15) // 16 * 16)
+            self._genomes.ensure(need)
+            self._genomes.top_ub += need
         fw = self._fast_world(n_new)
         zero_row = self.kinetics._zero_row()
         _m().fast_dist_divide_b(fw, n0, comm.handle, comm.up, comm.down, _p(par), _p(npos), n0, n_loc, n_up, n_dn, lw,
@@ -855,7 +859,8 @@ class DistributedWorld(World):
         k = int(first.numel())
         send = None
         if k:
-            send = _pack([first.to(torch.int32), pos[first, 1], self._genomes.lens[first], self._genomes.data[first]], k)
+            send = _pack([first.to(torch.int32), pos[first, 1], self._genomes.lens[first],
+                          self._genomes.rows_of(first, int(self._genomes.width))], k)
         (g_buf, g_meta), _ = self._exchange_var(send, None, (int(self._genomes.width),), (0,))
         ng = int(g_buf.size(0))
         changed_local = torch.zeros(0, dtype=torch.long, device=dev)
@@ -878,7 +883,8 @@ class DistributedWorld(World):
                     cg = changed[changed >= n] - n
                     if cg.numel():
                         rows = cg + n
-                        upd = _pack([gi[cg], self._genomes.lens[rows], self._genomes.data[rows]], int(cg.numel()))
+                        upd = _pack([gi[cg], self._genomes.lens[rows], self._genomes.rows_of(rows, int(self._genomes.width))],
+                                    int(cg.numel()))
             finally:
                 if ng:
                     self._genomes.n = n
@@ -1120,7 +1126,8 @@ class _BoundaryRecombination:
         comm = w._active_comm()
         if isinstance(comm, RcclComm):
             # index map, lengths exchange, events, event-genome exchange: one native call (dist.hip)
-            _m().xb_begin(C, H, n, _p(w.cell_positions), _p(idx_map), _p(g.lens), _p(g.data), int(g.width), _p(lens),
+            _m().xb_begin(C, H, n, _p(w.cell_positions), _p(idx_map), _p(g.lens), _p(g.data), _p(g.off), int(g.width),
+                          _p(lens),
                           _p(own), E, W, float(p), int(kcap), self.seed_dn, self.seed_up, self.call, _p(ev), _p(sl),
                           comm.handle, comm.up, comm.down, st)
         else:
@@ -1130,7 +1137,7 @@ class _BoundaryRecombination:
                          _p(mine_dn), _p(own[:C]), _p(own[C:]), st)
             w._exchange(mine_up, mine_dn, from_dn, from_up)
             _m().xb_events(C, E, W, float(p), int(kcap), self.seed_dn, self.seed_up, self.call, _p(mine_dn),
-                           _p(from_dn), _p(mine_up), _p(from_up), _p(own[:C]), _p(own[C:]), _p(g.data), int(g.width),
+                           _p(from_dn), _p(mine_up), _p(from_up), _p(own[:C]), _p(own[C:]), _p(g.data), _p(g.off),
                            _p(ev), _p(self.slots_dn), _p(self.slots_up), st)
             w._exchange(self.slots_up, self.slots_dn, self.recv_dn, self.recv_up)
         self.parts = sc.get("xb_parts", 2 * E * (kcap + 2) * 3, torch.int32, dev)

@@ -9,7 +9,8 @@ Cell records (division children and migrants) share one byte layout on both path
     int32 y, genome length, label length, divisions, lifetime | float32 molecules[m]
     | label row (lw bytes) | genome row (gw bytes)
 
-``lw`` / ``gw`` are the sender's arena row widths (multiples of 16), announced in the header.
+``lw`` / ``gw`` are the sender's label row width and genome length bound (multiples of 16),
+announced in the header; GPU genomes are read from / written to the genome pool.
 """
 from __future__ import annotations
 
@@ -136,7 +137,7 @@ def pack(world, par_up, pos_up, par_dn, pos_dn, child: bool, out_up: torch.Tenso
     m = world.n_molecules
     if world.cell_molecules.is_cuda:
         _hip().rec_pack(k_up, k_dn, _p(par_up), _p(pos_up), _p(par_dn), _p(pos_dn), _p(world.cell_molecules),
-                        _p(world.cell_positions), _p(world.cell_lifetimes), _p(world.cell_divisions), _p(g.data),
+                        _p(world.cell_positions), _p(world.cell_lifetimes), _p(world.cell_divisions), g.args(),
                         _p(g.lens), int(g.width), _p(lab.data), _p(lab.lens), int(lab.width), m, bool(child),
                         _p(out_up), _p(out_dn), _stream())
         return
@@ -164,9 +165,14 @@ def unpack(world, n0: int, buf_up, hdr_up, buf_dn, hdr_dn) -> None:
     g, lab = world._genomes, world._labels
     m, H, C = world.n_molecules, world.H, world.map_size
     if world.cell_molecules.is_cuda:
+        # (the genomes go to fresh space of the genome pool)
+        need = k_up * ((int(hdr_up[2]) + 15) // 16 * 16) + k_dn * ((int(hdr_dn[2]) + 15) // 16 * 16)
+        g.ensure(need)
+        g.top_ub += need
         _hip().rec_unpack(n0, k_up, _p(buf_up), int(hdr_up[1]), int(hdr_up[2]), k_dn, _p(buf_dn), int(hdr_dn[1]),
                           int(hdr_dn[2]), C, H, _p(world.cell_molecules), _p(world.cell_positions),
-                          _p(world.cell_lifetimes), _p(world.cell_divisions), _p(g.data), _p(g.lens), int(g.width),
+                          _p(world.cell_lifetimes), _p(world.cell_divisions), g.args(), _p(g.lens),
+                          max(int(hdr_up[2]), int(hdr_dn[2])),
                           _p(lab.data), _p(lab.lens), int(lab.width), m, _p(_cmap(world)), _stream())
         return
     cm = _cmap(world)

@@ -20,8 +20,8 @@ Per cell (capacity-managed buffers: up to 1.5x the live count, each with a spare
 for order-preserving compactions):
 
 * intracellular molecules (``m`` fp32), position (2 int32), lifetime and divisions (int32);
-* genome arena row (one byte per nt, the row width is the longest genome rounded up) + length, and
-  a label row (16 B);
+* the genome pool (one byte per nt, ragged: offsets + lengths per cell, no padding to the longest
+  genome; twice the live bytes between collections) and a label row (16 B);
 * the cell -> parameter-row map (int64) and the division / kill scratch of the native fast path;
 * parameter rows in compact storage: per (protein, signal) the packed N/Nf/Nb/A word (int32) and
   Kmr (fp32), per protein Vmax/Kmf/Kmb/Ke (4 fp32), for the live cells plus the spare rows fresh
@@ -41,12 +41,6 @@ GiB = float(1 << 30)
 MI355X_HBM = 288e9  # bytes of HBM3E per GPU
 
 
-def _round_width(n: int) -> int:
-    from magicsoup_amd.models.strings import _round_width as rw
-
-    return rw(max(1, int(n)))
-
-
 def proteins_per_genome(genome_len: int) -> int:
     """Protein slots ``P`` (the longest proteome of the population) for random genomes of
     ``genome_len`` nt: about one protein per 21 nt at the tail of the distribution (24 slots at
@@ -55,7 +49,7 @@ def proteins_per_genome(genome_len: int) -> int:
 
 
 def footprint(map_size: int, n_molecules: int, cells: int, map_dtype=torch.float32, genome_len: int = 500,
-              p_max: int | None = None, ranks: int = 1, genome_width: int | None = None) -> dict:
+              p_max: int | None = None, ranks: int = 1) -> dict:
     """Modelled device bytes of one rank of a GPU world (``ranks`` > 1: a strip of a
     domain-decomposed ``map_size``² world holding ``cells / ranks`` cells). Returns the per-part
     breakdown and the total in bytes."""
@@ -67,20 +61,21 @@ def footprint(map_size: int, n_molecules: int, cells: int, map_dtype=torch.float
     cap = int(n * _CAP)
     P = p_max if p_max is not None else proteins_per_genome(genome_len)
     s = 2 * m
-    width = genome_width if genome_width is not None else _round_width(int(genome_len * 1.25))
     row_bytes = P * s * 8 + P * 16  # packed word + Kmr per (protein, signal); Vmax/Kmf/Kmb/Ke per protein
     spare_rows = max(n // 8, min(3 * n, _KIN_SPARE_BUDGET // max(row_bytes, 1)), 1024)
     parts = {
         "molecule_map": pix * m * es * 2,
         "pixel_maps": pix * (1 + 4 + 4),
         "cell_columns": cap * (m * 4 + 8 + 4 + 4) * 2,
-        "genome_arena": cap * (width + 4) * 2,
+        # the ragged pool: offsets + lengths (and spares) per cell, the bytes of the live genomes
+        # (16-byte granules) with 2x room for new ones between collections
+        "genome_pool": cap * (8 + 4) * 2 + max(16 << 20, 2 * n * ((int(genome_len * 1.1) + 15) // 16 * 16)),
         "label_arena": cap * (16 + 4) * 2,
         "row_maps": cap * (8 * 2 + 6 * 8 + 1),
         "kinetics_rows": int((n + spare_rows) * row_bytes * 1.0),
     }
     parts["total"] = sum(parts.values())
-    parts.update(map_size=map_size, ranks=ranks, cells_per_rank=n, p_max=P, genome_width=width)
+    parts.update(map_size=map_size, ranks=ranks, cells_per_rank=n, p_max=P)
     return parts
 
 
@@ -146,6 +141,7 @@ def measured(world) -> dict:
         if a is not None:
             add(a.data)
             add(a.lens)
+            add(a.__dict__.get("off"))
             add(a.__dict__.get("_spare"))
     sc = d.get("_hip_scratch")
     if sc is not None:

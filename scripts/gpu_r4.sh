@@ -1,0 +1,47 @@
+#!/bin/bash
+# Round-4 GPU driver: gpu_r4.sh <outdir> <step>...  Steps: tests (maxfail 5), smoke, flagship, drv,
+# proxy, virt, hsf, hsp, hsv, check, m1, wide, c1024, c256, tflag (kernel trace). Each GPU step has
+# its own time limit; a fatal exit (timeout, abort, segfault) ends the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export PYTHONPATH="$PWD:${PYTHONPATH:-}" TMPDIR=/tmp
+O=gpurun_out/$1; shift; rm -rf "$O"; mkdir -p "$O"
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+run() {  # run <name> <seconds> <cmd...>
+  local name="$1" secs="$2"; shift 2
+  echo "== $name $(date +%T)"
+  timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc $(grep -h '^{"metric"' "$O/$name.log" | cut -c100-200)"
+  if [ $rc -ne 0 ]; then tail -5 "$O/$name.log"; fi
+  if fatal $rc; then echo "fatal rc=$rc in $name"; tail -30 "$O/$name.log"; exit $rc; fi
+  return 0
+}
+trace() {  # trace <name> <steps-to-summarise> <bench args...>
+  local name="$1" k="$2"; shift 2
+  echo "== trace $name $(date +%T)"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$name -o run --output-format csv -- python bench.py "$@" \
+    > $O/$name.log 2>&1
+  local rc=$?
+  echo "   rc=$rc"
+  if fatal $rc; then echo "fatal rc=$rc in $name"; tail -30 "$O/$name.log"; exit $rc; fi
+  python scripts/step_kernels.py $O/$name/run_kernel_trace.csv $k > $O/${name}_steps.txt 2>&1
+}
+for s in "$@"; do case "$s" in
+  tests) run tests 1000 python -u -m pytest tests -m gpu -q --maxfail 5 --timeout 120 --timeout-method thread ;;
+  smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+  flagship) run flagship 300 python bench.py ;;
+  drv) run drv 300 python bench.py --steps 20 --warmup 5 ;;
+  proxy) run proxy8_plain 300 python bench.py --map-size 1448 --cells 6250 ;;
+  virt) MS_VIRTUAL_STRIPS=1 run proxy8_virtual 300 python bench.py --map-size 1448 --cells 6250 ;;
+  hsf) run host_split_flagship 300 python scripts/host_split.py 4096 50000 40 ;;
+  hsp) run host_split_proxy8 300 python scripts/host_split.py 1448 6250 60 ;;
+  hsv) MS_VIRTUAL_STRIPS=1 run host_split_proxy8_virtual 300 python scripts/host_split.py 1448 6250 60 ;;
+  check) run check 600 python performance/check.py ;;
+  m1) run m1_bench 600 python bench.py --preset m1 --steps 60 --warmup 10 --step-times ;;
+  wide) run wide 300 python bench.py --preset wide ;;
+  c1024) run c1024 300 python bench.py --preset c1024 --steps 30 --warmup 5 ;;
+  c256) run c256_40k 300 python bench.py --map-size 256 --cells 40000 ;;
+  tflag) trace tflag 19 --steps 20 --warmup 20 ;;
+  *) echo "unknown step $s" ;;
+esac; done
