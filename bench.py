@@ -21,6 +21,7 @@ Presets (BASELINE.json's other configs; explicit flags override a preset's value
     m1        16384^2, 1M cells, fp16 maps (8 GPUs: torchrun --nproc-per-node 8 bench.py --preset m1)
     wide      4096^2, 50k cells, synthetic 64 molecules / 256 reactions
     c1024     1024^2, 10k cells, synthetic 16 molecules / 32 reactions, bf16 maps
+    hbm       fp16 maps, 1M cells per 16384^2, sized by utils.memory.plan to fill each GPU's HBM
 """
 from __future__ import annotations
 
@@ -43,6 +44,9 @@ PRESETS = {
     "m1": dict(map_size=16384, cells=1_000_000, chemistry="wood_ljungdahl", map_dtype="fp16"),
     "wide": dict(map_size=4096, cells=50_000, chemistry="synthetic:64:256", map_dtype="fp32"),
     "c1024": dict(map_size=1024, cells=10_000, chemistry="synthetic:16:32", map_dtype="bf16"),
+    # the largest fp16 world (the m1 config's cell density) that fills each GPU's HBM: map side and
+    # cell count from utils.memory.plan for the device's memory and the number of ranks
+    "hbm": dict(chemistry="wood_ljungdahl", map_dtype="fp16"),
 }
 
 
@@ -272,6 +276,17 @@ def main():
 
     chem = _chemistry(a.chemistry)
     mdt = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[a.map_dtype]
+    if a.map_size is None or a.cells is None:  # the hbm preset: plan the config for this device
+        from magicsoup_amd.utils import memory
+
+        hbm = torch.cuda.get_device_properties(device).total_memory if torch.cuda.is_available() else 4 << 30
+        plan = memory.plan(hbm_bytes=hbm, ranks=world_size if distributed else 1, n_molecules=len(chem.molecules),
+                           map_dtype=a.map_dtype, genome_len=a.genome_size, reserve=0.2)
+        a.map_size = a.map_size or plan["map_size"]
+        a.cells = a.cells or plan["cells"]
+        if rank == 0:
+            print(json.dumps({"hbm_plan": {k: v for k, v in plan.items() if k != "per_rank"},
+                              "per_rank_gib": round(plan["per_rank"]["total"] / 2**30, 1)}), file=sys.stderr)
     atp = chem.molname_2_idx.get("ATP", 0)
     ms.set_seed(a.seed + rank)
     torch.manual_seed(a.seed + rank)
@@ -288,7 +303,11 @@ def main():
     if torch.cuda.is_available():
         # (a plain world on this rank's device: no collectives; the kernels it warms are per process)
         _prime_rare_paths(chem, device, mdt, a.genome_size)
-    world.spawn_cells(random_genomes(a.cells // max(1, world_size if distributed else 1), a.genome_size, device))
+    todo = a.cells // max(1, world_size if distributed else 1)
+    while todo > 0:  # (batches: a multi-million-cell population's random genomes stay a few hundred MB)
+        k = min(todo, 500_000)
+        world.spawn_cells(random_genomes(k, a.genome_size, device))
+        todo -= k
     setup_s = time.time() - t0
 
     def sync():

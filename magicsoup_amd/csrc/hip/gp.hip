@@ -385,20 +385,25 @@ size_t gp_evolve_union_bytes(int ucap, int P, int dcap, int L) {
 }
 
 // ar / am / au: the recombination's, the mutation's and the union rebuild's counters (the arena
-// fields are the same in all three). Returns (union status slot {count, flags, row counter, count},
-// parts status slot {pairs, rec flags, mutated, mut flags}).
+// fields are the same in all three). `extra` / `nres`: strip-boundary recombination results of a
+// decomposed world, appended after the local pairs' results (as in gp_recombine; the parts status
+// then counts result rows instead of pairs). Returns (union status slot {count, flags, row counter,
+// count}, parts status slot {pairs or result rows, rec flags, mutated, mut flags}).
 std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpArena& au, const GpGen& g, const GpKin& k,
                               uintptr_t keys, py::object nbr, double p_rec, uint64_t seed_r, uint64_t call_r, int pcap,
                               double p, double p_indel, double p_del, uint64_t seed_m, uint64_t call_m, int mcap,
                               int kcap, int dcap, uintptr_t mark, uint64_t gen, uintptr_t blob_r, uintptr_t blob_m,
-                              uintptr_t blob_u, bool fresh, long long nrows, uintptr_t stream) {
+                              uintptr_t blob_u, bool fresh, long long nrows, py::object extra, uintptr_t nres,
+                              uintptr_t stream) {
   hipStream_t s = S_(stream);
   const int n = ar.n, L = ar.width;
+  const int xr = extra.is_none() ? 0 : extra.attr("rows").cast<int>();
+  if (xr && !nres) throw std::invalid_argument("gp_evolve: boundary rows need the result-row counter");
   gp_begin3_kernel<<<1, 1, 0, s>>>(P_<int>(ar.opflags), P_<int>(am.opflags), P_<int>(au.opflags), P_<int>(ar.gflags),
                                    P_<long long>(ar.d_rows), nrows, fresh ? 1 : 0);
   MS_LAUNCH_CHECK();
   // recombination (gp_recombine's layout of blob_r, without its rebuild)
-  const int nr = 2 * pcap, out_w = 2 * L, parts_cap = kcap + 2;
+  const int nr = 2 * pcap + xr, out_w = 2 * L, parts_cap = kcap + 2;
   Carve cr(blob_r);
   const uintptr_t kk = cr.take(4 * 8 * (size_t)n), sel = cr.take(8 * 8 * (size_t)n);
   const uintptr_t out = cr.take((size_t)nr * out_w), out_len = cr.take(4 * (size_t)nr), out_rows = cr.take(8 * (size_t)nr);
@@ -409,11 +414,10 @@ std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpAren
             std::get<6>(t), ar.lens, p_rec, seed_r, call_r, kcap, ar.gflags, ar.opflags, keys, kk, sel, ar.cnt, pcap,
             stream);
   rec_apply(pcap, ar.cnt, sel, 0, keys, ar.data, ar.off, ar.lens, kk, seed_r, call_r, parts, parts_cap, out, out_w,
-            out_len,
-            out_rows, stream);
-  arena_scatter(nr, ar.cnt, 2, out_rows, out, out_w, out_len, ar.data, ar.off, ar.top, ar.pool_cap, L, ar.lens, mark,
-                gen, won, ar.gflags,
-                ar.opflags, stream);
+            out_len, out_rows, stream);
+  if (xr) extra.attr("apply")(ar.cnt, out, out_w, out_len, out_rows, nres);
+  arena_scatter(nr, xr ? nres : ar.cnt, xr ? 1 : 2, out_rows, out, out_w, out_len, ar.data, ar.off, ar.top,
+                ar.pool_cap, L, ar.lens, mark, gen, won, ar.gflags, ar.opflags, stream);
   select_indices_dev(nr, kSelSet, won, 0, q, 0, ar.cnt2, stream);
   gather_dev(nr, ar.cnt2, q, out_rows, cells, stream);
   // point mutations over the recombined genomes (gp_mutate's layout of blob_m, without its rebuild)
@@ -434,7 +438,7 @@ std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpAren
   const uintptr_t ucells = cu.take(8 * (size_t)ucap), ucnt = cu.take(16);
   auto ps = status_slot();
   gp_union_kernel<<<1, 256, 0, s>>>(ucap, mcap, P_<int>(ar.cnt2), P_<int64_t>(cells), P_<int>(am.cnt),
-                                    P_<int64_t>(msel), P_<int64_t>(ucells), P_<int>(ucnt), P_<int>(ar.cnt),
+                                    P_<int64_t>(msel), P_<int64_t>(ucells), P_<int>(ucnt), P_<int>(xr ? nres : ar.cnt),
                                     P_<int>(ar.opflags), P_<int>(am.opflags), ps.first);
   MS_LAUNCH_CHECK();
   const int slot_u = rebuild(ucap, ucells, ucnt, au, g, k, dcap, cu, ucnt, s);

@@ -102,8 +102,9 @@ __device__ __forceinline__ long long poisson(Philox& rng, double lam) {
 // bytes at pool + off[i], allocations 16-byte aligned and never written again (new genomes take new
 // space, so cells can share a genome). An allocation is an atomic bump of the device counter `top`;
 // -1 when the pool is full (the caller raises a flag; the host collects or grows the pool).
+// (an empty genome takes 16 bytes too: every allocation has an offset of its own)
 __device__ __forceinline__ long long pool_alloc(unsigned long long* top, long long cap, int len) {
-  const unsigned long long sz = ((unsigned long long)(len > 0 ? len : 0) + 15ull) & ~15ull;
+  const unsigned long long sz = ((unsigned long long)(len > 1 ? len : 1) + 15ull) & ~15ull;
   const unsigned long long o = atomicAdd(top, sz);
   return (long long)(o + sz) <= cap ? (long long)o : -1;
 }

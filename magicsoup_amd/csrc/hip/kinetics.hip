@@ -497,10 +497,21 @@ __global__ void __launch_bounds__(kBlock) integrate_spec_lds_kernel(IntegrateArg
 constexpr int kNzReg = 16;  // non-zero signals per protein in the LDS lists (more: the cell goes wide)
 constexpr int kNzWide = 2 * kNzReg;  // the same for the 64-lane launch of the wide list
 
+// LDS row strides of the per-protein non-zero lists: NZ entry words + 1 and NZ index bytes + 4 (an
+// odd number of words). Protein lanes read entry q of their own row in lock step, so with a stride
+// of NZ words (a multiple of the bank count's divisors) all lanes of a wave hit 64 / NZ banks: 16-
+// to 32-way bank conflicts on every entry read (profiles/r3/wide/pmc_wide_integrator_stencil.txt:
+// 2.47 M per dispatch). An odd stride spreads the lanes over all banks.
+template <int NZ>
+constexpr int ent_stride() { return NZ + 1; }
+template <int NZ>
+constexpr int jl_stride() { return NZ + 4; }
+
 // LDS words per cell slot of the register-resident integrator (SPL signals per lane: s <= SPL * G)
 template <int G, int NZ, int SPL = 1>
 constexpr int fast_slot_words() {
-  return G * NZ /*entry words*/ + G * NZ / 4 /*entry signal indices*/ + 3 * G /*cnt, act, pub*/ + SPL * G /*X*/;
+  return G * ent_stride<NZ>() /*entry words*/ + G * jl_stride<NZ>() / 4 /*entry signal indices*/ +
+         3 * G /*cnt, act, pub*/ + SPL * G /*X*/;
 }
 
 template <int G>
@@ -556,9 +567,10 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   const int P = a.P, s = a.s;
   const size_t prow = listed ? (a.prow ? (size_t)a.prow[cell] : (size_t)cell) : 0;
 
-  int* ents = smem + slot * fast_slot_words<G, NZ, SPL>();       // (G, NZ) words of the non-zeros
-  uint8_t* jl = reinterpret_cast<uint8_t*>(ents + G * NZ);   // (G, NZ) their signal indices
-  int* cnts = ents + G * NZ + G * NZ / 4;                // (G,) non-zero signals per protein
+  constexpr int ES = ent_stride<NZ>(), JS = jl_stride<NZ>();
+  int* ents = smem + slot * fast_slot_words<G, NZ, SPL>();   // (G, ES) words of the non-zeros
+  uint8_t* jl = reinterpret_cast<uint8_t*>(ents + G * ES);  // (G, JS) bytes: their signal indices
+  int* cnts = ents + G * ES + G * JS / 4;                    // (G,) non-zero signals per protein
   int* act = cnts + G;                                           // (G,) protein slot of active protein k
   float* pub = reinterpret_cast<float*>(act + G);                // (G,) protein -> signal: V_k / Va_k * F_k
   float* Xs = pub + G;                                           // (SPL * G,) signal -> protein: X_j / factor
@@ -626,8 +638,8 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
         const unsigned long long gm = group_ballot<G>(on);
         const int r = base + __popcll(gm & ((1ull << lane) - 1ull));
         if (on && r < NZ) {
-          ents[k * NZ + r] = w[h][u];
-          jl[k * NZ + r] = (uint8_t)(lane + h * G);
+          ents[k * ES + r] = w[h][u];
+          jl[k * JS + r] = (uint8_t)(lane + h * G);
         }
         base += __popcll(gm);
         wide_ok &= w_nf(w[h][u]) < EP::kMaxExp && w_nb(w[h][u]) < EP::kMaxExp;
@@ -680,11 +692,11 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     kmb = q4.z;
     ke = q4.w;
     cnt = cnts[lane];
-    const int* jw = reinterpret_cast<const int*>(jl + lane * NZ);
+    const int* jw = reinterpret_cast<const int*>(jl + lane * JS);
 #pragma unroll
     for (int q = 0; q < NZ; ++q) {
       if (q < cnt) {
-        const int w = ents[lane * NZ + q];
+        const int w = ents[lane * ES + q];
         const int j = (jw[q >> 2] >> (8 * (q & 3))) & 0xFF;
         const int e = EP::pack(j, w_nf(w), w_nb(w));
         e16[q >> 1] |= e << (16 * (q & 1));
@@ -731,7 +743,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
 #pragma unroll
     for (int q = 0; q < NZ; ++q) {
       if (q >= cnt_w) break;
-      const int w = q < cnt ? ents[lane * NZ + q] : 0;
+      const int w = q < cnt ? ents[lane * ES + q] : 0;
       const int j = EP::j(MS_E(q));
       const int nf = w_nf(w), nb = w_nb(w), av = w_a(w);
       const float x = Xs[j];
@@ -788,7 +800,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
 #pragma unroll
     for (int q = 0; q < NZ; ++q) {
       if (q >= cnt_w) break;
-      const int w = q < cnt ? ents[lane * NZ + q] : 0;
+      const int w = q < cnt ? ents[lane * ES + q] : 0;
       if ((float)w_n(w) * v < 0.0f) {
         const float f = Xs[EP::j(MS_E(q))];
         if (ms::f_isnan(f)) nan = true;

@@ -275,7 +275,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("set_stencil_prefetch", &msd::set_stencil_prefetch, "rows the vector stencils load ahead (-1 auto, 0-3)");
   m.def("set_stencil_band", &msd::set_stencil_band, "rows per wave band of the vector stencils (16-256; 0 = the default 32)");
   m.def("set_stencil_blocks", &msd::set_stencil_blocks, "blocks of the vector diffusion stencil (0: one per tile)");
-  m.def("set_place_mode", &msd::set_place_mode, "0 cooperative single launch (default), 1 multi-launch rounds");
+  m.def("set_place_mode", &msd::set_place_mode, "0 single-launch placement, ordinary launch (default), 1 multi-launch rounds, 2 single launch as a cooperative launch");
   m.def("place_error_take", &msd::place_error_take,
         "1 if a cooperative placement's grid barrier timed out since the last call (clears the flag)");
   m.def("split_cells", &msd::split_cells);

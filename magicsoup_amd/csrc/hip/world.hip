@@ -547,8 +547,17 @@ void claim_free(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uin
 }
 
 constexpr int kPlaceWgMax = 2048;  // single-workgroup rounds up to this many cells (one CU: ~2 cells per thread)
-static int g_coop_blocks = 256;    // co-resident workgroups of the cooperative placement (one per CU; 128: +18 % time)
-static int g_place_mode = 0;       // 0 cooperative, 1 multi-launch rounds (A/B, set_place_mode)
+static int g_coop_blocks = 256;    // co-resident workgroups of the single-launch placement (one per CU; 128: +18 % time)
+// 0: the single-launch placement as an ordinary launch of at most as many workgroups as the device
+// holds at once (its grid barrier is software: device-scope atomics with a bounded spin, see
+// grid_barrier), 1: multi-launch rounds, 2: the same kernel through hipLaunchCooperativeKernel.
+// Mode 2 was the default until it was traced as the cause of the SIGSEGV at exit of profiled
+// processes: a cooperative launch makes the HIP runtime create its cooperative queue, and at exit
+// the runtime's teardown of it (libamdhip64 -> libhsa-runtime64) touches a device mapping the
+// already finalised rocprofiler-sdk tool released (profiles/r3/profexit: the faulting address is in
+// a /dev/dri render-node mapping, frames hip exit handler -> hsa runtime -> fault). An ordinary
+// launch never creates that queue, so profiles now time the production path.
+static int g_place_mode = 0;
 constexpr int kMaxDevices = 64;
 static unsigned* g_place_ctl[kMaxDevices] = {};  // per device: the control words of the cooperative launch
 static unsigned* g_place_err = nullptr;           // pinned, mapped: a barrier timed out (any device)
@@ -594,13 +603,27 @@ static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, co
   Geom gg = g;
   bool vac = vacate;
   void* args[] = {&kk, &cp, &mp, &pp, &gg, &vac, &cm, &pend, &seed, &call, &cd, &cl, &res, &rr, &ctl, &err};
-  const unsigned grid = std::min<unsigned>(cdiv(k, 256), (unsigned)g_coop_blocks);
-  const hipError_t e = hipLaunchCooperativeKernel((const void*)place_rounds_coop_kernel, dim3(grid), dim3(256), args,
-                                                  0, s);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();  // clear the sticky launch error; fall back
-    return false;
+  unsigned grid = std::min<unsigned>(cdiv(k, 256), (unsigned)g_coop_blocks);
+  if (g_place_mode == 2) {
+    const hipError_t e = hipLaunchCooperativeKernel((const void*)place_rounds_coop_kernel, dim3(grid), dim3(256), args,
+                                                    0, s);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();  // clear the sticky launch error; fall back
+      return false;
+    }
+    return true;
   }
+  // ordinary launch: the grid must fit the device at once (every workgroup reaches the barriers)
+  static int resident[kMaxDevices] = {};
+  if (!resident[dev]) {
+    int per_cu = 0, cus = 0;
+    MS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)place_rounds_coop_kernel, 256, 0));
+    MS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    resident[dev] = std::max(1, per_cu * cus);
+  }
+  grid = std::min<unsigned>(grid, (unsigned)resident[dev]);
+  place_rounds_coop_kernel<<<grid, 256, 0, s>>>(kk, cp, mp, pp, gg, vac, cm, pend, seed, call, cd, cl, res, rr, ctl, err);
+  MS_LAUNCH_CHECK();
   return true;
 }
 
@@ -614,7 +637,7 @@ void place_rounds_mask(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r
                        int rounds, uint64_t seed, uint64_t call, uintptr_t stream) {
   if (n <= 0) return;
   const Geom g = geom(R, C, r_lo, r_hi, wrap);
-  if (g_place_mode == 0 &&
+  if (g_place_mode != 1 &&
       place_coop(n, 0, mask, pos, g, vacate, cell_map, pending, cand, claim, result, rounds, seed, call, S_(stream)))
     return;
   place_rounds_launches(n, 0, mask, pos, g, vacate, cell_map, pending, cand, claim, result, rounds, seed, call,
@@ -658,7 +681,7 @@ void place_rounds(int k, uintptr_t cells, uintptr_t pos, int R, int C, int r_lo,
                   uint64_t seed, uint64_t call, uintptr_t stream) {
   if (k <= 0) return;
   const Geom g = geom(R, C, r_lo, r_hi, wrap);
-  if (g_place_mode == 0 &&
+  if (g_place_mode != 1 &&
       place_coop(k, cells, 0, pos, g, vacate, cell_map, pending, cand, claim, result, rounds, seed, call, S_(stream)))
     return;
   place_rounds_launches(k, cells, 0, pos, g, vacate, cell_map, pending, cand, claim, result, rounds, seed, call,
@@ -678,7 +701,7 @@ int divide_mask_dev(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo
   if (n <= 0) throw std::invalid_argument("divide_mask_dev: no cells");
   const Geom g = geom(R, C, r_lo, r_hi, wrap);
   hipStream_t s = S_(stream);
-  if (g_place_mode != 0 ||
+  if (g_place_mode == 1 ||
       !place_coop(n, 0, mask, pos, g, false, cell_map, pending, cand, claim, result, rounds, seed, call, s))
     place_rounds_launches(n, 0, mask, pos, g, false, cell_map, pending, cand, claim, result, rounds, seed, call, s);
   const int slot = select_indices_async(n, 3 /* int64 >= 0 */, result, wins, 0, dcount, stream);

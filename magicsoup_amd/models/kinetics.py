@@ -755,6 +755,14 @@ class Kinetics:
                 torch.index_select(store[k], 0, slot, out=target[k][:n])
         for k in list(store):
             spare[k], store[k] = store[k], target[k]
+        if slot.is_cuda:
+            # the old storage is not kept as the next re-gather's target: a dense re-gather is rare
+            # (rows are recycled in place first), and keeping it would hold the parameter storage
+            # twice in HBM (utils/memory.py plans without it); freed once the gather above ran
+            cur = torch.cuda.current_stream(slot.device)
+            for t in spare.values():
+                t.record_stream(cur)
+            spare.clear()
         d["_slot"] = None
         d["_free"] = None
         d["_nrows"] = n

@@ -69,6 +69,8 @@ class StringArena:
         if self.n:
             data[: self.n, : self.width] = self.data[: self.n]
             lens[: self.n] = self.lens[: self.n]
+        _retire(self.data)
+        _retire(self.lens)
         self.data, self.lens, self.width = data, lens, width
         self.version += 1
 
@@ -205,6 +207,14 @@ def _r16(n: int) -> int:
     return (int(n) + 15) // 16 * 16
 
 
+def _retire(t: torch.Tensor | None) -> None:
+    """A device tensor about to be dropped while work on the current stream may still read it (a
+    copy out of it was just queued): its block returns to the caching allocator only after that
+    work, even if the tensor was allocated on another stream."""
+    if t is not None and t.is_cuda:
+        t.record_stream(torch.cuda.current_stream(t.device))
+
+
 class PoolArena:
     """GPU genomes of every length in one byte pool (``csrc/hip/pool.hip``).
 
@@ -253,9 +263,11 @@ class PoolArena:
         return a
 
     def reserve(self, rows: int, width: int | None = None) -> None:
-        """Room for ``rows`` cells; ``width`` raises the genome length bound (no data moves)."""
-        if width is not None and _round_width(width) > self.width:
-            self.width = _round_width(width)
+        """Room for ``rows`` cells; ``width`` raises the genome length bound (no data moves). The
+        bound follows the longest genome closely (64-multiples), not in powers of two: the device
+        pipeline's gates and scratch scale with it."""
+        if width is not None and int(width) > self.width:
+            self.width = (int(width) + 63) // 64 * 64
         if rows <= self.capacity:
             return
         cap = max(rows, int(self.capacity * 1.5) + 16)
@@ -264,6 +276,8 @@ class PoolArena:
         if self.n:
             lens[: self.n] = self.lens[: self.n]
             off[: self.n] = self.off[: self.n]
+        _retire(self.lens)
+        _retire(self.off)
         self.lens, self.off = lens, off
         self.__dict__.pop("_spare", None)
         self.version += 1
@@ -293,7 +307,9 @@ class PoolArena:
         off, lens = self.off[:n], self.lens[:n]
         uo, inv = torch.unique(off, return_inverse=True)
         size_u = torch.zeros_like(uo)
-        size_u.scatter_(0, inv, ((lens.to(torch.int64) + 15) // 16) * 16)
+        # bytes per allocation (16-byte granules, at least one: pool_alloc); the longest genome per
+        # offset (cells sharing an allocation have one length, the reduction only guards that)
+        size_u.scatter_reduce_(0, inv, ((lens.to(torch.int64).clamp(min=1) + 15) // 16) * 16, reduce="amax")
         new_u = torch.cumsum(size_u, 0) - size_u
         total = int((new_u[-1] + size_u[-1]).item())
         cap = max(_POOL_MIN, 2 * (total + _r16(extra)))
@@ -301,6 +317,7 @@ class PoolArena:
         native.hip().pool_compact(int(uo.numel()), self.data.data_ptr(), uo.data_ptr(), size_u.data_ptr(),
                                   new.data_ptr(), new_u.data_ptr(), _stream())
         self.off[:n] = new_u[inv]
+        _retire(self.data)
         self.data = new
         self.top.fill_(total)
         self.top_ub = total

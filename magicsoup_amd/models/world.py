@@ -320,10 +320,13 @@ class World:
             d["_defer_event"] = NEvent().record()
         q.append(fn)
 
-    def _evolve(self, p_rec: float, p: float, p_indel: float, p_del: float) -> bool:
+    def _evolve(self, rec: "_Deferred", mut: "_Deferred") -> int:
+        """Issue a queued recombinate_cells() + mutate_cells() pair as one device chain. Returns how
+        many of the two calls were issued, in order (2: merged; 1: the recombination only, e.g. a
+        decomposed world whose collective part has run; 0: neither -- the caller issues them)."""
         from magicsoup_amd.ops import genome_pipeline
 
-        return genome_pipeline.evolve(self, p_rec, p, p_indel, p_del)
+        return 2 if self.n_cells >= 2 and genome_pipeline.evolve(self, rec.args[0], *mut.args) else 0
 
     def _join_side(self) -> None:
         """The compute stream waits (device-side) for the genome chains issued so far."""
@@ -391,10 +394,12 @@ class World:
                 i = 0
                 while i < len(q):
                     # recombinate_cells() then mutate_cells(): one chain with one rebuild (gp_evolve)
-                    if (i + 1 < len(q) and getattr(q[i], "kind", None) == "rec" and getattr(q[i + 1], "kind", None) == "mut"
-                            and self.n_cells >= 2 and self._evolve(q[i].args[0], *q[i + 1].args)):
-                        i += 2
-                        continue
+                    if (i + 1 < len(q) and getattr(q[i], "kind", None) == "rec"
+                            and getattr(q[i + 1], "kind", None) == "mut"):
+                        done = self._evolve(q[i], q[i + 1])
+                        if done:
+                            i += done
+                            continue
                     q[i]()
                     i += 1
         finally:

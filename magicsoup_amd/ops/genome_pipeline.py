@@ -39,6 +39,9 @@ from magicsoup_amd.ops.streams import NEvent
 K_CAP = 32  # event-count cap per genome (P(Poisson(lam <= 1) > 32) < 1e-35)
 D_CAP = 12  # domain slots per protein in the speculative token layout
 N_CAP = 8192  # genomes per pipeline call (the expected count is kept <= N_CAP / 4)
+# largest Poisson mean of events per genome (rate x the genome length bound) a pipeline call takes:
+# the per-genome event count is capped at K_CAP, and P(Poisson(4) > 32) < 1e-18
+LAM_MAX = 4.0
 
 
 def _cap(expected: float, limit: int) -> int:
@@ -116,8 +119,8 @@ def _bufs(world, kind: str) -> dict:
     return b
 
 
-def _usable(world, expected: float) -> bool:
-    return enabled(world) and expected <= N_CAP / 4
+def _usable(world, expected: float, limit: float = N_CAP / 4) -> bool:
+    return enabled(world) and expected <= limit
 
 
 def _begin(world, kind: str) -> dict:
@@ -264,7 +267,7 @@ def point_mutations(world, p: float, p_indel: float, p_del: float) -> bool:
     if n == 0:
         return True
     L = int(arena.width)  # every genome fits its row
-    if p * L > 1.0 or not _usable(world, n * p * L):
+    if p * L > LAM_MAX or not _usable(world, n * p * L):
         return False
     dev = arena.data.device
     cap = _cap(n * p * L, min(n, N_CAP))
@@ -295,8 +298,11 @@ def recombinate_all(world, p: float, extra=None) -> bool:
     if n < 2:
         return True
     L = int(arena.width)
-    expected = 8 * n * p * 2 * L  # upper bound: every neighbour slot a pair
-    if p * 2 * L > 1.0 or not _usable(world, expected):
+    # upper bound: at most 4n neighbour pairs (each in one slot), both genomes at the length bound;
+    # real counts are several times lower (occupancy, mean lengths), so the bound may reach N_CAP:
+    # a count above the pair capacity makes the call a no-op that reconcile replays (cap_skip)
+    expected = 4 * n * p * 2 * L
+    if p * 2 * L > LAM_MAX or not _usable(world, expected, N_CAP):
         return False
     dev = arena.data.device
     pcap = _cap(expected, min(n, N_CAP) // 2)  # pairs per call (two results each)
@@ -348,20 +354,21 @@ class _PartHost:
         return {0: self.parts[2], 1: self.parts[3], 2: 0, 3: self.parts[2]}[i]
 
 
-def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float) -> bool:
+def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=None) -> bool:
     """``recombinate_cells(p=p_rec)`` followed by ``mutate_cells(p, p_indel, p_del)`` over all cells
     as ONE device chain (gp.hip gp_evolve): both are applied and committed in order, then the union
     of the changed cells is translated and built once -- the same genomes and parameters as the two
-    calls one after the other, with one translation + build less on the side stream. False if either
-    call should take its own path (rates above the pipeline's usage rule, a decomposed world's
-    boundary recombination, too few cells)."""
+    calls one after the other, with one translation + build less on the side stream. ``extra``: a
+    decomposed world's strip-boundary recombination (as for :func:`recombinate_all`). False if either
+    call should take its own path (rates above the pipeline's usage rule, too few cells)."""
     arena = world._genomes
     n = world.n_cells
-    if n < 2 or "_n_pix_global" in world.__dict__:
+    if n < 2:
         return False
     L = int(arena.width)
-    exp_rec = 8 * n * p_rec * 2 * L
-    if p_rec * 2 * L > 1.0 or p * L > 1.0 or not _usable(world, exp_rec) or not _usable(world, n * p * L):
+    exp_rec = 4 * n * p_rec * 2 * L
+    if (p_rec * 2 * L > LAM_MAX or p * L > LAM_MAX or not _usable(world, exp_rec, N_CAP)
+            or not _usable(world, n * p * L)):
         return False
     st = _state(world)
     if any(pd.kind in ("rec", "mut", "evo") for pd in st["pending"]):
@@ -373,15 +380,17 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float) -> bool:
     fresh = not st["pending"]
     if fresh:
         kin._reserve_rows(2 * min(n, N_CAP))
-    _room(world, 2 * pcap * _r16(2 * L) + mcap * _r16(L + K_CAP))
+    xr = 0 if extra is None else int(extra.rows)
+    _room(world, (2 * pcap + xr) * _r16(2 * L) + mcap * _r16(L + K_CAP))
     br, bm, bu = _bufs(world, "rec"), _bufs(world, "mut"), _bufs(world, "evo")
     ar, am, au = _arena_desc(world, br), _arena_desc(world, bm), _arena_desc(world, bu)
     sc = hip_ops._scratch(world)
     keys, nbr = hip_ops.neighbor_slot_args(world)
     k = _kin_desc(world, dev)
-    blob_r = _blob(world, "rec", _m().gp_blob_bytes(1, n, pcap, k.P, L, D_CAP, K_CAP, 0), dev)
+    blob_r = _blob(world, "rec", _m().gp_blob_bytes(1, n, pcap, k.P, L, D_CAP, K_CAP, xr), dev)
     blob_m = _blob(world, "mut", _m().gp_blob_bytes(0, n, mcap, k.P, L, D_CAP, K_CAP, 0), dev)
-    ucap = 2 * pcap + mcap
+    nres = sc.get("gp_nres", 1, torch.int32, dev) if extra is not None else None
+    ucap = 2 * pcap + xr + mcap
     blob_u = _blob(world, "evo", _m().gp_evolve_union_bytes(ucap, k.P, D_CAP, L), dev)
     mark = sc.bufs.get("arena_mark")
     if mark is None or mark.numel() < arena.n:
@@ -392,12 +401,13 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float) -> bool:
     slot_u, slot_p = _m().gp_evolve(ar, am, au, _gen_desc(world, dev), k, _p(keys), nbr, float(p_rec), rng_r[0],
                                     rng_r[1], pcap, float(p), float(p_indel), float(p_del), rng_m[0], rng_m[1], mcap,
                                     K_CAP, D_CAP, _p(mark), int(gen), _p(blob_r), _p(blob_m), _p(blob_u), fresh,
-                                    int(kin.__dict__["_nrows"]), _stream())
-    lay_r = _m().gp_layout(1, n, pcap, L, K_CAP, 0)
+                                    int(kin.__dict__["_nrows"]), extra, _p(nres), _stream())
+    lay_r = _m().gp_layout(1, n, pcap, L, K_CAP, xr)
     lay_m = _m().gp_layout(0, n, mcap, L, K_CAP, 0)
     parts = _StatusSlot(slot_p)
     replay = {
-        "rec": _Part("rec", _PartHost(parts, "rec"), _Replay(blob_r, lay_r, lay_r["nr"], "out_rows", mark=mark, gen=gen)),
+        "rec": _Part("rec", _PartHost(parts, "rec"), _Replay(blob_r, lay_r, lay_r["nr"], "out_rows", mark=mark, gen=gen,
+                                                              direct=extra is not None)),
         "mut": _Part("mut", _PartHost(parts, "mut"), _Replay(blob_m, lay_m, mcap, "sel")),
     }
     cells = _view(blob_u, 0, ucap, torch.int64)
@@ -416,6 +426,10 @@ def _resolve_evo(world, pd) -> bool:
         raise RuntimeError("genome pipeline capacity exceeded (rates far above the pipeline's usage rule)")
     changed = []
     rebuilt = False
+    if fr & _F_SKIPPED and rec.replay.direct:
+        # (the recombination is the first call of a fresh chain: nothing before it can break the
+        # chain, and a replay of the local pairs alone would lose the strip-boundary results)
+        raise RuntimeError("genome pipeline: merged chain with boundary recombination was skipped")
     if fr & (_F_SKIPPED | _F_WIDTH):
         rebuilt = True
         if fr & _F_SKIPPED:

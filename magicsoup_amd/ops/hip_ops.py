@@ -889,13 +889,15 @@ def translate(genetics, arena, rows: torch.Tensor):
 def _arena_commit(arena, rows: torch.Tensor, out: torch.Tensor, out_len: torch.Tensor, need_width: int,
                   dedupe: bool = False, owner=None) -> torch.Tensor:
     """Commit result rows ``out`` (k, w) / ``out_len`` as the genomes of cells ``rows`` in one launch
-    (arena_scatter: fresh pool space); raises the genome length bound first if a result may exceed
-    it, and makes room in the pool. With ``dedupe`` the last result per cell wins and the winning
-    cells are returned (one more select)."""
+    (arena_scatter: fresh pool space) and make room in the pool first. With ``dedupe`` the last
+    result per cell wins and the winning cells are returned (one more select, which also reads back
+    the longest committed genome). The genome length bound (PoolArena.width) is raised to the longest
+    committed result -- not to ``need_width``, the worst case (both parents of a recombination):
+    raising the bound to that would double it per call and push later calls off the device
+    pipeline (its gates scale with the bound)."""
     k = int(rows.numel())
-    if need_width > arena.width:
-        arena.reserve(arena.n, need_width)
-    need = k * ((min(int(out.size(1)), arena.width) + 15) // 16 * 16)
+    sw = max(int(arena.width), min(int(need_width), int(out.size(1))))  # no result is truncated
+    need = k * ((sw + 15) // 16 * 16)
     arena.ensure(need)
     mark, gen, flags = None, 0, None
     if dedupe:
@@ -907,13 +909,17 @@ def _arena_commit(arena, rows: torch.Tensor, out: torch.Tensor, out_len: torch.T
         gen = sc.bufs["arena_gen"] = sc.bufs.get("arena_gen", 0) + 1
         flags = torch.empty(k, dtype=torch.uint8, device=rows.device)
     _m().arena_scatter(k, 0, 1, _p(rows), _p(out), int(out.stride(0)), _p(out_len), _p(arena.data), _p(arena.off),
-                       _p(arena.top), arena.pool_cap, int(arena.width), _p(arena.lens), _p(mark), int(gen), _p(flags),
+                       _p(arena.top), arena.pool_cap, sw, _p(arena.lens), _p(mark), int(gen), _p(flags),
                        0, 0, _stream())
     arena.top_ub += need
     arena.version += 1
     if not dedupe:
+        if need_width > arena.width:
+            arena.reserve(arena.n, need_width)  # mutations: the bound is tight (length + events)
         return rows
-    won = select(flags, "set")[0]
+    won, _, longest = select(flags, "set", vals=out_len[:k])
+    if longest > arena.width:
+        arena.reserve(arena.n, longest)
     return rows[won]
 
 

@@ -42,11 +42,6 @@ def _load(name: str, builder) -> object:
         return mod
 
 
-def _profiled() -> bool:
-    """Running under rocprofv3 (its launcher exports the tool's ROCPROF_* settings)."""
-    return any(k.startswith("ROCPROF") for k in os.environ)
-
-
 def _release_static(mod) -> None:
     """Free the extension's process-wide HIP buffers before the C exit handlers run (a profiler's
     interception layer finalises there; the HIP runtime's own teardown of leftover allocations
@@ -81,13 +76,8 @@ def hip():
     if fresh and os.environ.get("MS_INTEGRATE_MODE"):
         # integrator launch-mode bits for whole-run A/B (kinetics.hip, set_integrate_mode)
         mod.set_integrate_mode(int(os.environ["MS_INTEGRATE_MODE"]))  # type: ignore[attr-defined]
-    if fresh and not os.environ.get("MS_PLACE_MODE") and _profiled():
-        # under rocprofv3 a process that made cooperative launches dies in SIGSEGV at exit (the HIP
-        # runtime's teardown calls into the already finalised profiler layer; docs/performance.md):
-        # the per-round placement launches place identically
-        mod.set_place_mode(1)  # type: ignore[attr-defined]
     if fresh and os.environ.get("MS_PLACE_MODE"):
-        # 1: per-round placement launches instead of the cooperative single launch (world.hip)
+        # 1: per-round placement launches, 2: the single launch as a cooperative launch (world.hip)
         mod.set_place_mode(int(os.environ["MS_PLACE_MODE"]))  # type: ignore[attr-defined]
     if fresh and os.environ.get("MS_COOP_BLOCKS"):
         mod.set_coop_blocks(int(os.environ["MS_COOP_BLOCKS"]))  # type: ignore[attr-defined]

@@ -51,7 +51,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from magicsoup_amd.models.world import World, _op
+from magicsoup_amd.models.world import World, _Deferred, _op
 from magicsoup_amd.ops import world_ops
 from magicsoup_amd.parallel import strip
 from magicsoup_amd.parallel.comm import RcclComm, make_comm
@@ -708,12 +708,31 @@ class DistributedWorld(World):
             early = (_XB_EARLY and not self.__dict__.get("_deferred")
                      and isinstance(self.__dict__.get("_comm_side"), RcclComm))
             pre = self._xb_pre_issue(p) if early else None
-            self._defer(lambda: self._recombinate_strips_all(p, pre))
+            self._defer(_Deferred(lambda: self._recombinate_strips_all(p, pre), "rec", (p, pre)))
             return
         self._reconcile()
         if cell_idxs is not None:
             return self._recombinate_subset(cell_idxs, p)
         self._recombinate_strips_all(p)
+
+    def _evolve(self, rec, mut) -> int:
+        """A queued recombinate_cells() + mutate_cells() pair: the boundary part's collective runs as
+        for a recombination of its own (every rank, once per call), then the local pairs, the
+        boundary results and the mutations go into one device chain (genome_pipeline.evolve with the
+        boundary rows); if the pipeline declines, the recombination is issued on its own (1)."""
+        if not self._strips:
+            return super()._evolve(rec, mut)
+        from magicsoup_amd.ops import genome_pipeline
+        from magicsoup_amd.ops.genome_pipeline import K_CAP
+
+        p, pre = rec.args
+        if pre is None:
+            self.__dict__["_xcall"] += 1
+        x = pre if pre is not None else _BoundaryRecombination(self, p, K_CAP)
+        if self.n_cells >= 2 and genome_pipeline.evolve(self, p, *mut.args, extra=x):
+            return 2
+        self._recombinate_gpu(p, x)
+        return 1
 
     def _recombinate_strips_all(self, p: float, pre: "_BoundaryRecombination | None" = None) -> None:
         if pre is None:

@@ -60,6 +60,7 @@ def footprint(map_size: int, n_molecules: int, cells: int, map_dtype=torch.float
     n = int(math.ceil(cells / ranks))
     cap = int(n * _CAP)
     P = p_max if p_max is not None else proteins_per_genome(genome_len)
+    P = P + max(8, P // 2)  # the storage's protein dimension grows with headroom (World._update_params_rows)
     s = 2 * m
     row_bytes = P * s * 8 + P * 16  # packed word + Kmr per (protein, signal); Vmax/Kmf/Kmb/Ke per protein
     spare_rows = max(n // 8, min(3 * n, _KIN_SPARE_BUDGET // max(row_bytes, 1)), 1024)

@@ -37,6 +37,11 @@ for s in "$@"; do case "$s" in
   hsf) run host_split_flagship 300 python scripts/host_split.py 4096 50000 40 ;;
   hsp) run host_split_proxy8 300 python scripts/host_split.py 1448 6250 60 ;;
   hsv) MS_VIRTUAL_STRIPS=1 run host_split_proxy8_virtual 300 python scripts/host_split.py 1448 6250 60 ;;
+  hspn) MS_NATIVE_TIMES=1 MS_PY_TIMES=1 run host_split_proxy8_detail 300 python scripts/host_split.py 1448 6250 60 ;;
+  hsvn) MS_VIRTUAL_STRIPS=1 MS_NATIVE_TIMES=1 MS_PY_TIMES=1 run host_split_proxy8_virtual_detail 300 python scripts/host_split.py 1448 6250 60 ;;
+  hspc) MS_CPROFILE=1 run host_split_proxy8_cprofile 300 python scripts/host_split.py 1448 6250 60 ;;
+  hsvc) MS_VIRTUAL_STRIPS=1 MS_CPROFILE=1 run host_split_proxy8_virtual_cprofile 300 python scripts/host_split.py 1448 6250 60 ;;
+  upd) PROBE_PROFILE=1 run update_cells_probe 300 python scripts/update_cells_probe.py ;;
   check) run check 600 python performance/check.py ;;
   m1) run m1_bench 600 python bench.py --preset m1 --steps 60 --warmup 10 --step-times ;;
   wide) run wide 300 python bench.py --preset wide ;;

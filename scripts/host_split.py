@@ -4,7 +4,9 @@ event syncs) and BUSY (issuing work). The busy total is the step's host floor; b
 the device running ahead of the host's need.
 
 usage: python scripts/host_split.py [map_size] [cells] [steps]
-MS_VIRTUAL_STRIPS=1: a one-rank DistributedWorld running the strip protocol (RCCL to itself)."""
+MS_VIRTUAL_STRIPS=1: a one-rank DistributedWorld running the strip protocol (RCCL to itself).
+MS_NATIVE_TIMES=1 / MS_PY_TIMES=1: host time per native entry point / selected Python helper;
+MS_CPROFILE=1: cProfile of the timed steps (inflates the totals; read the ranking)."""
 import collections
 import os
 import sys
@@ -163,11 +165,25 @@ torch.cuda.synchronize()
 for d in (busy, blocked, calls, native_t, native_n, py_t, py_n):
     d.clear()
 blk[0] = 0.0
+prof = None
+if os.environ.get("MS_CPROFILE") == "1":  # per-function host time (tottime) of the timed steps
+    import cProfile
+
+    prof = cProfile.Profile()
+    prof.enable()
 t0 = time.perf_counter()
 for _ in range(steps):
     bench.step(w, N, 500, atp)
 torch.cuda.synchronize()
 wall = (time.perf_counter() - t0) / steps * 1e6
+if prof is not None:
+    import io
+    import pstats
+
+    prof.disable()
+    buf = io.StringIO()
+    pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(45)
+    print(buf.getvalue())
 tb, tk = sum(busy.values()) / steps * 1e6, sum(blocked.values()) / steps * 1e6
 print(f"{S}^2 / {N}{' virtual' if virtual else ''}: wall {wall:.0f} us/step; inside ops: busy {tb:.0f}, blocked {tk:.0f}; "
       f"outside ops (bench glue) {wall - tb - tk:.0f}")

@@ -35,12 +35,13 @@ def test_translation_matches_host():
 
     arr, lens = pack_strings(genomes)
     tok_h, np_h = genetics.tables.translate_tokens(arr, lens)
+    from magicsoup_amd.models.strings import PoolArena
     from magicsoup_amd.ops import hip_ops
 
-    data = torch.from_numpy(arr).cuda()
-    ln = torch.from_numpy(lens).cuda()
+    pool = PoolArena("cuda")  # (the GPU genome store: ragged, one byte per nt)
+    pool.append_packed(torch.from_numpy(arr), torch.from_numpy(lens))
     rows = torch.arange(len(genomes), device="cuda")
-    tok_d, np_d = hip_ops.translate(genetics, data, ln, rows)
+    tok_d, np_d = hip_ops.translate(genetics, pool, rows)
     assert torch.equal(np_d.cpu(), torch.as_tensor(np_h))
     assert torch.equal(tok_d.cpu(), torch.as_tensor(tok_h))
 
@@ -53,10 +54,9 @@ def _copy_world_cpu_to_gpu(wc):
 def test_param_build_matches_host():
     wc = _world("cpu", n=200)
     rows = torch.arange(wc.n_cells)
-    data, lens = wc._genomes.view()
     from magicsoup_amd.ops import world_ops, hip_ops, kinetics_ops
 
-    tokens, nprot = world_ops.translate(wc, data, lens, rows)
+    tokens, nprot = world_ops.translate(wc, rows)
     wg = _copy_world_cpu_to_gpu(wc)
     kg = wg.kinetics
     for name in ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke"):
@@ -566,7 +566,31 @@ def _genetics_run(monkeypatch, base, sync: bool, d_cap=None, steps=5, mut_kw=Non
         w.diffuse_molecules()
     w.enzymatic_activity()
     names = ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke")
-    return list(w.cell_genomes), {k: getattr(w.kinetics, k).clone() for k in names}, w.cell_molecules.clone()
+    params = {k: getattr(w.kinetics, k).clone() for k in names}
+    from magicsoup_amd.ops import world_ops
+
+    params["_nprot"] = world_ops.translate(w, torch.arange(w.n_cells, device=w.device))[1]
+    return list(w.cell_genomes), params, w.cell_molecules.clone()
+
+
+def _real(p: dict) -> dict:
+    return {k: v for k, v in p.items() if not k.startswith("_")}
+
+
+def _assert_params_equal(p0: dict, p1: dict, nprot: torch.Tensor) -> None:
+    """Parameters of two runs agree on every real protein (p < the cell's protein count); padding
+    slots are inert in both (no stoichiometry, no Vmax). Padding Km / Ke values depend on history,
+    as in the reference: a widened layout is zero-filled, a build writes the values of an empty
+    protein (kinetics.py:577-625 over the batch's protein dimension)."""
+    for k in p0:
+        a, b = p0[k], p1[k]
+        P = min(a.size(1), b.size(1))
+        real = torch.arange(P, device=a.device)[None, :] < nprot.to(a.device)[:, None]
+        m = real if a.dim() == 2 else real[:, :, None].expand(-1, -1, a.size(2))
+        assert torch.equal(a[:, :P][m], b[:, :P][m]), k
+        if k in ("N", "Nf", "Nb", "A", "Vmax"):
+            for t in (a, b):
+                assert not t[:, :P][~m].any() and not t[:, P:].any(), k
 
 
 def test_device_genome_pipeline_arena_overflow_replay(monkeypatch):
@@ -606,11 +630,7 @@ def test_device_genome_pipeline_arena_overflow_replay(monkeypatch):
     assert any(f & genome_pipeline._F_WIDTH for f in seen), seen
     assert any(f & genome_pipeline._F_SKIPPED for f in seen), seen
     assert g0 == g1
-    for k in p0:
-        P = min(p0[k].size(1), p1[k].size(1))
-        assert torch.equal(p0[k][:, :P], p1[k][:, :P]), k
-        if p1[k].size(1) > P:
-            assert not p1[k][:, P:].any(), k
+    _assert_params_equal(_real(p0), _real(p1), p0["_nprot"])
     assert torch.equal(x0, x1)
 
 
@@ -624,9 +644,7 @@ def test_device_genome_pipeline_capacity_skip_replays(monkeypatch):
     monkeypatch.setattr(genome_pipeline, "_cap", lambda expected, limit: 2)
     g1, p1, x1 = _genetics_run(monkeypatch, base, sync=False, steps=3)
     assert g0 == g1
-    for k in p0:
-        P = min(p0[k].size(1), p1[k].size(1))
-        assert torch.equal(p0[k][:, :P], p1[k][:, :P]), k
+    _assert_params_equal(_real(p0), _real(p1), p0["_nprot"])
     assert torch.equal(x0, x1)
 
 
@@ -639,11 +657,7 @@ def test_device_genome_pipeline_matches_sync_path(monkeypatch, d_cap):
     g0, p0, x0 = _genetics_run(monkeypatch, base, sync=True)
     g1, p1, x1 = _genetics_run(monkeypatch, base, sync=False, d_cap=d_cap)
     assert g0 == g1
-    for k in p0:
-        P = min(p0[k].size(1), p1[k].size(1))
-        assert torch.equal(p0[k][:, :P], p1[k][:, :P]), k
-        if p1[k].size(1) > P:
-            assert not p1[k][:, P:].any(), k
+    _assert_params_equal(_real(p0), _real(p1), p0["_nprot"])
     assert torch.equal(x0, x1)
 
 
@@ -660,15 +674,15 @@ def test_merged_recombinate_mutate_chain_matches_separate_calls(monkeypatch, mod
     calls = []
     orig = genome_pipeline.evolve
 
-    def spy(world, *a):
-        ok = orig(world, *a)
+    def spy(world, *a, **kw):
+        ok = orig(world, *a, **kw)
         calls.append(ok)
         return ok
 
     def tighten(w):
         w._genomes.width = 512
 
-    # (mutation rate * genome length bound <= 1 keeps the mutations on the device pipeline)
+    # (mutation rate * genome length bound <= genome_pipeline.LAM_MAX keeps the mutations on the pipeline)
     kw = dict(steps=4, mut_kw={"p": 2e-4})
     if mode == "overflow":
         base = _world("cuda", map_size=64, n=0, seed=5)
@@ -679,7 +693,7 @@ def test_merged_recombinate_mutate_chain_matches_separate_calls(monkeypatch, mod
     if mode == "capacity":
         monkeypatch.setattr(genome_pipeline, "_cap", lambda expected, limit: 2)
     d_cap = 1 if mode == "dcap" else None
-    monkeypatch.setattr(world_mod.World, "_evolve", lambda self, *a: False)
+    monkeypatch.setattr(world_mod.World, "_evolve", lambda self, *a: 0)
     g0, p0, x0 = _genetics_run(monkeypatch, base, sync=False, d_cap=d_cap, **kw)
     monkeypatch.undo()
     if mode == "capacity":
@@ -690,9 +704,7 @@ def test_merged_recombinate_mutate_chain_matches_separate_calls(monkeypatch, mod
     # past what the mutation rate allows on the device pipeline)
     assert any(calls) and (all(calls) or mode == "overflow"), calls
     assert g0 == g1
-    for k in p0:
-        P = min(p0[k].size(1), p1[k].size(1))
-        assert torch.equal(p0[k][:, :P], p1[k][:, :P]), k
+    _assert_params_equal(_real(p0), _real(p1), p0["_nprot"])
     assert torch.equal(x0, x1)
 
 
@@ -736,8 +748,7 @@ def test_deferred_genome_ops_match_immediate_issue(monkeypatch):
     monkeypatch.setattr(world_mod, "_DEFER_ENV", "1")
     g1, p1, x1 = _genetics_run(monkeypatch, base, sync=False)
     assert g0 == g1
-    for k in p0:
-        assert torch.equal(p0[k], p1[k]), k
+    _assert_params_equal(_real(p0), _real(p1), p0["_nprot"])
     assert torch.equal(x0, x1)
     # default: queued until the diffusion
     w = copy.deepcopy(base)
@@ -1124,6 +1135,23 @@ def test_genome_pool_is_ragged_and_shared():
     w.check_invariants()
 
 
+def test_genome_pool_collect_keeps_genomes_next_to_empty_ones():
+    """An empty genome still takes a 16-byte allocation (hip_common.h pool_alloc): every allocation
+    has an offset of its own, before and after a collection, and the genome allocated right after
+    an empty one survives the collection intact."""
+    w = _world("cuda", map_size=64, n=200, s=300)
+    g = w._genomes
+    w._reconcile()
+    w.update_cells([("", 5)])
+    w.update_cells([(ms.random_genome(700), 6)])
+    w._reconcile()
+    assert int(g.off[6]) == int(g.off[5]) + 16 and int(g.lens[5]) == 0 and int(g.lens[6]) == 700
+    before = list(w.cell_genomes)
+    g.collect()
+    assert list(w.cell_genomes) == before
+    assert int(g.off[5]) != int(g.off[6])
+
+
 def test_genome_pool_grows_and_collects_under_pressure():
     """A pool too small for what the steps allocate collects / grows on demand (host writes and the
     device pipeline's worst cases are accounted for before any allocation); genomes stay exact."""
@@ -1146,3 +1174,25 @@ def test_genome_pool_grows_and_collects_under_pressure():
     assert int(g.top.item()) <= g.pool_cap
     assert all(len(x) == int(n) for x, n in zip(w.cell_genomes, g.lens[: g.n].tolist()))
     assert g.pool_cap >= cap0 or strings._POOL_MIN == cap0
+
+
+def test_memory_model_matches_a_live_world():
+    """utils/memory.py models what a GPU world holds: the modelled footprint of a world after some
+    steps is within 25 % of the bytes its tensors hold (utils.memory.measured) and of what the
+    caching allocator has handed out."""
+    import bench
+    from magicsoup_amd.utils import memory
+
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    w = ms.World(chemistry=CHEMISTRY, map_size=2048, device="cuda", seed=3)
+    w.spawn_cells(bench.random_genomes(20_000, 500, "cuda"))
+    for _ in range(5):
+        bench.step(w, 20_000, 500, atp)
+    w.synchronize()
+    model = memory.footprint(2048, len(CHEMISTRY.molecules), w.n_cells, torch.float32, 500)["total"]
+    held = memory.measured(w)["bytes"]
+    alloc = torch.cuda.memory_allocated() - base
+    assert 0.75 * held <= model <= 1.25 * held, (model, held)
+    assert held <= alloc * 1.05, (held, alloc)

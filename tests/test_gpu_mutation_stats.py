@@ -43,8 +43,15 @@ def _binom(hits: int, n: int, p: float, what: str) -> None:
     _within(hits / n, p, math.sqrt(p * (1 - p) / n), what)
 
 
+def _offsets(n: int, length: int) -> torch.Tensor:
+    """Per-genome byte offsets of rows laid out back to back (the kernels read genome i at
+    pool + off[i], models/strings.py PoolArena)."""
+    return (torch.arange(n, dtype=torch.int64, device="cuda") * length).contiguous()
+
+
 def _point_mutations(p: float, p_indel: float, p_del: float, seed: int):
     data = _genomes(N, L, seed)
+    off = _offsets(N, L)
     lens = torch.full((N,), L, dtype=torch.int32, device="cuda")
     k = torch.empty(N, dtype=torch.int32, device="cuda")
     m = _m()
@@ -54,7 +61,8 @@ def _point_mutations(p: float, p_indel: float, p_del: float, seed: int):
     out_w = L + int(k.max().item()) + 16
     out = torch.zeros(nsel, out_w, dtype=torch.uint8, device="cuda")
     out_len = torch.empty(nsel, dtype=torch.int32, device="cuda")
-    m.mut_apply(nsel, 0, sel.data_ptr(), 0, data.data_ptr(), L, lens.data_ptr(), k.data_ptr(), p_indel, p_del, seed, 7,
+    m.mut_apply(nsel, 0, sel.data_ptr(), 0, data.data_ptr(), off.data_ptr(), lens.data_ptr(), k.data_ptr(), p_indel,
+                p_del, seed, 7,
                 out.data_ptr(), out_w, out_len.data_ptr(), _stream())
     torch.cuda.synchronize()
     return data.cpu().numpy(), k.cpu().numpy(), sel.cpu().numpy(), out.cpu().numpy(), out_len.cpu().numpy()
@@ -129,6 +137,7 @@ def test_recombination_breaks_and_conservation():
     p = 5e-4  # lambda = p * 2L = 1 break per pair
     n_pairs = N // 2
     data = _genomes(2 * n_pairs, L, seed=21)
+    off = _offsets(2 * n_pairs, L)
     lens = torch.full((2 * n_pairs,), L, dtype=torch.int32, device="cuda")
     pairs = torch.arange(2 * n_pairs, dtype=torch.int32, device="cuda").view(n_pairs, 2).contiguous()
     k = torch.empty(n_pairs, dtype=torch.int32, device="cuda")
@@ -146,7 +155,8 @@ def test_recombination_breaks_and_conservation():
     out_len = torch.empty(2 * nsel, dtype=torch.int32, device="cuda")
     out_rows = torch.empty(2 * nsel, dtype=torch.int64, device="cuda")
     parts = torch.empty(nsel * parts_cap * 3, dtype=torch.int32, device="cuda")
-    m.rec_apply(nsel, 0, sel.data_ptr(), pairs.data_ptr(), 0, data.data_ptr(), L, lens.data_ptr(), k.data_ptr(), 21, 3,
+    m.rec_apply(nsel, 0, sel.data_ptr(), pairs.data_ptr(), 0, data.data_ptr(), off.data_ptr(), lens.data_ptr(),
+                k.data_ptr(), 21, 3,
                 parts.data_ptr(), parts_cap, out.data_ptr(), out_w, out_len.data_ptr(), out_rows.data_ptr(), _stream())
     torch.cuda.synchronize()
     d, o, ol, rows, s = data.cpu().numpy(), out.cpu().numpy(), out_len.cpu().numpy(), out_rows.cpu().numpy(), sel.cpu().numpy()
