@@ -945,14 +945,25 @@ __global__ void __launch_bounds__(kBlock, G == 32 ? 6 : (NZ == kNzReg ? (SPL == 
   or_block_bits(bits, a.mask_out);
 }
 
+// The narrow cells of the speculative all-parts launch on their own, compiled for W waves per SIMD
+// (A/B of the occupancy / register-spill trade: at 6 waves the path spills, at 5 it does not).
+template <int W>
+__global__ void __launch_bounds__(kBlock, W) integrate_narrow_spec_kernel(IntegrateArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  unsigned bits = 0u;
+  integrate_item_fast<32, kNzReg, true>(a, smem, (int)blockIdx.x * (kBlock / 32) + (int)threadIdx.x / 32, bits, nullptr,
+                                         nullptr);
+  or_block_bits(bits, a.mask_out);
+}
+
 // Parts >= 1 of the register path with the wide list (known from part 0) in the same launch: the
 // first `nwb` blocks walk the wide list with two 64-lane slots each (integrate_item_fast<64,
 // kNzWide>, the rest of the block idles), the others take the cells as integrate_fast_kernel<G>.
 // A wide cell's integration is a long dependency chain (~30 us on its own); at the front of the
 // grid it runs under the narrow blocks instead of after them. Cells that do not fit the 64-lane
 // slots either are skipped here (part 0 listed them for the LDS launch).
-template <int G, bool kSpec = false>
-__global__ void __launch_bounds__(kBlock, 6) integrate_fused_kernel(IntegrateArgs a, IntegrateArgs aw, int nwb) {
+template <int G, bool kSpec = false, int W = 6>
+__global__ void __launch_bounds__(kBlock, W) integrate_fused_kernel(IntegrateArgs a, IntegrateArgs aw, int nwb) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
   static_assert(2 * fast_slot_words<64, kNzWide>() <= (kBlock / G) * fast_slot_words<G, kNzReg>(),
                 "two wide slots must fit the narrow block's LDS");
@@ -1462,10 +1473,25 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
     if (Gs == 32) {
       constexpr int kFusedWideBlocks = 64;
       const size_t lds_fast = (size_t)(kBlock / 32) * fast_slot_words<32, kNzReg>() * 4;
-      integrate_fused_kernel<32, true><<<cdiv(c, kBlock / 32) + kFusedWideBlocks, kBlock, lds_fast, st>>>(
-          a, aw, kFusedWideBlocks);
-      MS_LAUNCH_CHECK();
       const size_t lds_fw = (size_t)(kBlock / 64) * fast_slot_words<64, kNzWide>() * 4;
+      if (g_integrate_mode & 1024) {
+        // (A/B) the wide list and the narrow cells as two launches: each kernel gets the registers
+        // its path needs (the fused kernel holds both paths in the narrow path's 80 VGPRs, and the
+        // 64-lane path spills there)
+        integrate_fast_kernel<64, kNzWide, true, true><<<kFusedWideBlocks, kBlock, lds_fw, st>>>(aw, nullptr, nullptr);
+        MS_LAUNCH_CHECK();
+        if (g_integrate_mode & 2048)
+          integrate_narrow_spec_kernel<5><<<cdiv(c, kBlock / 32), kBlock, lds_fast, st>>>(a);
+        else
+          integrate_narrow_spec_kernel<6><<<cdiv(c, kBlock / 32), kBlock, lds_fast, st>>>(a);
+      } else if (g_integrate_mode & 4096) {
+        integrate_fused_kernel<32, true, 5><<<cdiv(c, kBlock / 32) + kFusedWideBlocks, kBlock, lds_fast, st>>>(
+            a, aw, kFusedWideBlocks);
+      } else {
+        integrate_fused_kernel<32, true><<<cdiv(c, kBlock / 32) + kFusedWideBlocks, kBlock, lds_fast, st>>>(
+            a, aw, kFusedWideBlocks);
+      }
+      MS_LAUNCH_CHECK();
       integrate_fast_kernel<64, kNzWide, true, true><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
       MS_LAUNCH_CHECK();
     } else {

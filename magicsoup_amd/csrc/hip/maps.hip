@@ -224,9 +224,11 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
     h[3] = v[2] + v[3] + Rn;
   };
 
-  // mass sums: fp32 per lane over the band (at most 4 x 256 values of one species, so the
-  // rounding stays ~1e-7 of a lane's sum), fp64 across lanes and tiles
-  float bsum = 0.0f, asum = 0.0f;
+  // mass sums in fp64 per row: fp32 sums per band were tried (round 4) and rejected -- their
+  // rounding scales with the largest concentrations of a species, and the correction spreads it
+  // over every pixel, so a decomposed map no longer matched the single-process one to 1e-4
+  // (tests/test_gpu_distributed.py); the two fp64 adds per row are not what bounds the kernel
+  double before = 0.0, after = 0.0;
   if (o0 < H) {
     Raw rp, rc, rn, rn2;
     fetch(o0 - 1, rp);
@@ -248,8 +250,8 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
       for (int j = 0; j < 4; ++j) res[j] = b * vc[j] + a * (hp[j] + hn[j] + lft[j] + rgt[j]);
       if (col) {
         st4_stream(dst + (size_t)row_of(o) * g.C + y0, res);
-        bsum += (vc[0] + vc[1]) + (vc[2] + vc[3]);
-        asum += (res[0] + res[1]) + (res[2] + res[3]);
+        before += (double)((vc[0] + vc[1]) + (vc[2] + vc[3]));
+        after += (double)((res[0] + res[1]) + (res[2] + res[3]));
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -262,7 +264,8 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
     };
     band_loop<PF>(o0, o1, rn, rn2, fetch, row_step);
   }
-  const double before = wave_sum_d((double)bsum), after = wave_sum_d((double)asum);
+  before = wave_sum_d(before);
+  after = wave_sum_d(after);
   if (lane == 0) {
     red[0][wv] = before;
     red[1][wv] = after;
@@ -343,7 +346,7 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
       h[7] = v[6] + v[7] + Rn;
     };
 
-    float bsum = 0.0f, asum = 0.0f;  // (as diffuse_stencil4_kernel)
+    double before = 0.0, after = 0.0;
     if (o0 < H) {
       Raw rp, rc, rn, rn2;
       fetch(o0 - 1, rp);
@@ -367,8 +370,8 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
         }
         if (col) {
           st8_stream(dst + (size_t)row_of(o) * g.C + y0, res);
-          bsum += ((vc[0] + vc[1]) + (vc[2] + vc[3])) + ((vc[4] + vc[5]) + (vc[6] + vc[7]));
-          asum += ((res[0] + res[1]) + (res[2] + res[3])) + ((res[4] + res[5]) + (res[6] + res[7]));
+          before += (double)((vc[0] + vc[1]) + (vc[2] + vc[3])) + (double)((vc[4] + vc[5]) + (vc[6] + vc[7]));
+          after += (double)((res[0] + res[1]) + (res[2] + res[3])) + (double)((res[4] + res[5]) + (res[6] + res[7]));
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -381,7 +384,8 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
       };
       band_loop<PF>(o0, o1, rn, rn2, fetch, row_step);
     }
-    const double before = wave_sum_d((double)bsum), after = wave_sum_d((double)asum);
+    before = wave_sum_d(before);
+    after = wave_sum_d(after);
     if (lane == 0) {
       red[0][wv] = before;
       red[1][wv] = after;

@@ -114,8 +114,9 @@ void pack_params(long long items, int s, uintptr_t N, uintptr_t Nf, uintptr_t Nb
 void claim_free(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uint64_t seed, uint64_t call,
                 int attempts, uintptr_t out, uintptr_t stream);
 void index_map(int c, uintptr_t pos, int C, uintptr_t idx_map, bool clear, uintptr_t stream);
-void neighbor_pairs(int nf, int n, uintptr_t from, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map,
-                    uintptr_t in_from, uintptr_t in_to, uintptr_t counter, int cap, uintptr_t pairs, uintptr_t stream);
+void neighbor_pairs_sorted(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map,
+                           uintptr_t in_from, uintptr_t in_to, uintptr_t keys, uintptr_t stream);
+
 // genetics.hip
 void translate_count(int n, uintptr_t rows, uintptr_t arena, uintptr_t off, int width, uintptr_t lens, uintptr_t luts,
                      uintptr_t dom_type, int dt_entries, uintptr_t two_codon, int dom_size, int dom_type_size,
@@ -282,7 +283,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("permeate", &msd::permeate);
   m.def("claim_free", &msd::claim_free);
   m.def("index_map", &msd::index_map);
-  m.def("neighbor_pairs", &msd::neighbor_pairs);
+  m.def("neighbor_pairs_sorted", &msd::neighbor_pairs_sorted, "unique neighbour pairs in (a, b)-sorted slots");
   m.def("translate_count", &msd::translate_count);
   m.def("translate_write", &msd::translate_write);
   m.def("translate_fused", &msd::translate_fused);

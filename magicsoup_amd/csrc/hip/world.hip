@@ -414,22 +414,38 @@ __global__ void __launch_bounds__(256) index_map_kernel(int c, const int32_t* po
   idx_map[(size_t)pos[2 * i] * C + pos[2 * i + 1]] = clear ? -1 : i;
 }
 
-__global__ void __launch_bounds__(256) neighbor_pairs_kernel(int nf, int n, const int64_t* from, const int32_t* pos, Geom g,
-                                                             const int32_t* idx_map, const uint8_t* in_from,
-                                                             const uint8_t* in_to, int* counter, int cap,
-                                                             int64_t* pairs) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nf) return;
-  const int c = (int)from[i];
-  long long nb[8];
-  const int cnt = moore(pos[2 * c], pos[2 * c + 1], g, nb);
-  for (int q = 0; q < cnt; ++q) {
-    const int o = cell_at(idx_map, pos, n, g.C, nb[q]);
-    if (o < 0 || o == c || !in_to[o]) continue;
-    if (in_from[o] && in_to[c] && o < c) continue;  // found from the other side
-    const int slot = atomicAdd(counter, 1);
-    if (slot < cap) pairs[slot] = c < o ? ((int64_t)c << 32) | o : ((int64_t)o << 32) | c;
+// Unique neighbour pairs (a < b) between the cells marked in_from and the cells marked in_to, in
+// fixed slots: slot a*8 + j holds (a << 32) | b for the j-th smallest qualifying neighbour b > a of
+// cell a (a pair belongs to its smaller cell: no pair twice, no atomics), else -1. An
+// order-preserving compaction of the 8n slots then lists the pairs sorted by (a, b) -- no sort, no
+// de-duplication pass (a neighbour met twice in a tiny wrapped map is kept once).
+__global__ void __launch_bounds__(256) neighbor_pairs_sorted_kernel(int n, const int32_t* pos, Geom g,
+                                                                    const int32_t* idx_map, const uint8_t* in_from,
+                                                                    const uint8_t* in_to, int64_t* keys) {
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= n) return;
+  const bool fa = in_from[a] != 0, ta = in_to[a] != 0;
+  int cand[8];
+  int m = 0;
+  if (fa || ta) {
+    long long nb[8];
+    const int cnt = moore(pos[2 * a], pos[2 * a + 1], g, nb);
+    for (int q = 0; q < cnt; ++q) {
+      const int o = cell_at(idx_map, pos, n, g.C, nb[q]);
+      if (o <= a || !((fa && in_to[o]) || (ta && in_from[o]))) continue;
+      int j = m;
+      bool dup = false;
+      for (int t = 0; t < m; ++t) dup |= cand[t] == o;
+      if (dup) continue;
+      while (j > 0 && cand[j - 1] > o) {  // insertion: cand stays ascending
+        cand[j] = cand[j - 1];
+        --j;
+      }
+      cand[j] = o;
+      ++m;
+    }
   }
+  for (int j = 0; j < 8; ++j) keys[(size_t)a * 8 + j] = j < m ? (((int64_t)a << 32) | cand[j]) : -1;
 }
 
 // All neighbour pairs of all cells in fixed slots: slot c*8 + q holds (c << 32) | o for the q-th
@@ -761,16 +777,16 @@ void rec_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap,
                              opflags, s);
 }
 
-void neighbor_pairs(int nf, int n, uintptr_t from, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map,
-                    uintptr_t in_from, uintptr_t in_to, uintptr_t counter, int cap, uintptr_t pairs, uintptr_t stream) {
-  if (nf <= 0) return;
+void neighbor_pairs_sorted(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map,
+                           uintptr_t in_from, uintptr_t in_to, uintptr_t keys, uintptr_t stream) {
+  if (n <= 0) return;
   const Geom g = geom(R, C, r_lo, r_hi, wrap);
-  neighbor_pairs_kernel<<<cdiv(nf, 256), 256, 0, S_(stream)>>>(nf, n, P_<int64_t>(from), P_<int32_t>(pos), g,
-                                                               P_<int32_t>(idx_map), P_<uint8_t>(in_from),
-                                                               P_<uint8_t>(in_to), P_<int>(counter), cap,
-                                                               P_<int64_t>(pairs));
+  neighbor_pairs_sorted_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, P_<int32_t>(pos), g, P_<int32_t>(idx_map),
+                                                                     P_<uint8_t>(in_from), P_<uint8_t>(in_to),
+                                                                     P_<int64_t>(keys));
   MS_LAUNCH_CHECK();
 }
+
 
 void release_world_buffers() {
   int cur = 0;

@@ -955,11 +955,21 @@ class World:
     @_op("update_cells")
     def update_cells(self, genome_idx_pairs: list[tuple[str, int]]):
         """Replace the genomes of existing cells and re-derive their proteomes."""
-        if len(genome_idx_pairs) == 0:
+        k = len(genome_idx_pairs)
+        if k == 0:
             return
-        genomes, idxs = zip(*genome_idx_pairs)
-        self._genomes.set_strings(list(idxs), list(genomes))
-        self._update_params_rows(torch.tensor(list(idxs), dtype=torch.long, device=self.device))
+        paused = gc.isenabled()  # (tens of thousands of short-lived containers: see get_neighbors)
+        if paused:
+            gc.disable()
+        try:
+            genomes, idxs = zip(*genome_idx_pairs)
+            rows = torch.from_numpy(np.fromiter(idxs, dtype=np.int64, count=k))
+            arr, lens = pack_strings(list(genomes))
+        finally:
+            if paused:
+                gc.enable()
+        self._genomes.set_rows(rows, torch.from_numpy(arr), torch.from_numpy(lens))
+        self._update_params_rows(rows.to(self.device))
 
     @_op("kill_cells")
     def kill_cells(self, cell_idxs=None):

@@ -832,17 +832,14 @@ def neighbors(world, frm: torch.Tensor, to: torch.Tensor, pos: torch.Tensor | No
     in_to = sc.get("nb_to", n, torch.uint8, dev, zero=True)
     in_from[frm] = 1
     in_to[to] = 1
-    frm64 = frm.to(torch.int64).contiguous()
-    cap = 8 * int(frm64.numel())
-    pairs = sc.get("nb_pairs", cap, torch.int64, dev)
-    counter = sc.get("nb_count", 1, torch.int32, dev, zero=True)
-    _m().neighbor_pairs(int(frm64.numel()), int(n), _p(frm64), _p(pos), R, C, r_lo, r_hi, wrap, _p(idx_map), _p(in_from),
-                        _p(in_to), _p(counter), cap, _p(pairs), _stream())
-    cnt = int(counter.item())
-    keys = torch.sort(pairs[:cnt]).values
-    if keys.numel() > 1:
-        keys = torch.unique_consecutive(keys)
-    return torch.stack([keys >> 32, keys & 0xFFFFFFFF], dim=1).to(torch.int32)
+    # pairs in per-cell slots, owned by their smaller cell and sorted there; one order-preserving
+    # compaction lists them sorted by (a, b) (no sort / unique pass)
+    keys = sc.get("nb_keys_sorted", 8 * int(n), torch.int64, dev)
+    _m().neighbor_pairs_sorted(int(n), _p(pos), R, C, r_lo, r_hi, wrap, _p(idx_map), _p(in_from), _p(in_to), _p(keys),
+                               _stream())
+    sel = select(keys[: 8 * int(n)], "i64nonneg")[0]
+    k = keys[sel]
+    return torch.stack([k >> 32, k & 0xFFFFFFFF], dim=1).to(torch.int32)
 
 
 # ---------------------------------------------------------------------------- genomes

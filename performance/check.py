@@ -11,6 +11,7 @@ ours.
 from __future__ import annotations
 
 import json
+import os
 import random
 import sys
 import time
@@ -43,15 +44,32 @@ def _genomes(n: int, s: int, d: float = 0.1) -> list[str]:
     return [ms.random_genome(s + random.choice(pop)) for _ in range(n)]
 
 
+_PROFILE = os.environ.get("MS_CHECK_PROFILE") == "1"  # cProfile of every timed call (stderr)
+
+
 def _timed(device: str, setup, fn, reps: int) -> list[float]:
     out = []
     for _ in range(reps):
         state = setup()
         _sync(device)
+        prof = None
+        if _PROFILE:
+            import cProfile
+
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         fn(state)
         _sync(device)
         out.append(time.perf_counter() - t0)
+        if prof is not None:
+            import io
+            import pstats
+
+            prof.disable()
+            buf = io.StringIO()
+            pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(12)
+            print(f"--- {1e3 * out[-1]:.1f} ms\n{buf.getvalue()}", file=sys.stderr)
     return out
 
 

@@ -42,6 +42,10 @@ for s in "$@"; do case "$s" in
   hspc) MS_CPROFILE=1 run host_split_proxy8_cprofile 300 python scripts/host_split.py 1448 6250 60 ;;
   hsvc) MS_VIRTUAL_STRIPS=1 MS_CPROFILE=1 run host_split_proxy8_virtual_cprofile 300 python scripts/host_split.py 1448 6250 60 ;;
   upd) PROBE_PROFILE=1 run update_cells_probe 300 python scripts/update_cells_probe.py ;;
+  isweep) run integrator_sweep 300 python scripts/integrator_sweep.py ;;
+  dbench) run diffuse_bench 300 python scripts/diffuse_bench.py --dtypes fp32 --blocks 1024 2048 0 --band 0 64 ;;
+  iab) for i in 1 2; do for m in 0 4096; do MS_INTEGRATE_MODE=$m run iab_${m}_$i 300 python bench.py --steps 60 --warmup 20; done; done ;;
+  checkp) MS_CHECK_PROFILE=1 run check_profile 600 python performance/check.py --parts update_cells mutations ;;
   check) run check 600 python performance/check.py ;;
   m1) run m1_bench 600 python bench.py --preset m1 --steps 60 --warmup 10 --step-times ;;
   wide) run wide 300 python bench.py --preset wide ;;

@@ -23,10 +23,28 @@ def t():
     return time.perf_counter()
 
 
+# garbage-collector pauses (generation 2 collections walk every tracked object of the process)
+import gc  # noqa: E402
+
+_gc = {"t0": 0.0, "total": 0.0, "n2": 0}
+
+
+def _gc_cb(phase, info):
+    if phase == "start":
+        _gc["t0"] = time.perf_counter()
+    else:
+        _gc["total"] += time.perf_counter() - _gc["t0"]
+        _gc["n2"] += info.get("generation") == 2
+
+
+gc.callbacks.append(_gc_cb)
+
+
 for rep in range(6):
     w = ms.World(chemistry=CHEMISTRY, device="cuda")
     w.spawn_cells(genomes=genomes(10_000, 1000))
     t0 = t()
+    _gc["total"], _gc["n2"] = 0.0, 0
     gs = list(w.cell_genomes)
     t1 = t()
     pairs = [(g, i) for i, g in enumerate(gs)]
@@ -39,7 +57,7 @@ for rep in range(6):
     t5 = t()
     print(f"rep {rep}: materialise {1e3 * (t1 - t0):.1f} ms, pairs {1e3 * (t2 - t1):.1f}, update host "
           f"{1e3 * (t3 - t2):.1f}, device {1e3 * (t4 - t3):.1f}, reconcile {1e3 * (t5 - t4):.1f}; "
-          f"total {1e3 * (t4 - t0):.1f}", flush=True)
+          f"total {1e3 * (t4 - t0):.1f} (gc {1e3 * _gc['total']:.1f} ms, {_gc['n2']} full)", flush=True)
 
 if os.environ.get("PROBE_PROFILE") == "1":
     import cProfile
