@@ -49,6 +49,9 @@ void release_kinetics_streams() {
   g_lds_fork = g_lds_join = nullptr;
 }
 void set_integrate_mode(int mode) { g_integrate_mode = mode; }
+// workgroups of the fused speculative launch that walk the wide list (two 64-lane slots each)
+static int g_fused_wide_blocks = 64;
+void set_fused_wide_blocks(int n) { g_fused_wide_blocks = n < 1 ? 1 : (n > 1024 ? 1024 : n); }
 
 struct IntegrateArgs {
   int c, P, s;
@@ -1471,7 +1474,7 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
     ao.list = wl2;
     ao.count = wc2;
     if (Gs == 32) {
-      constexpr int kFusedWideBlocks = 64;
+      const int kFusedWideBlocks = g_fused_wide_blocks;
       const size_t lds_fast = (size_t)(kBlock / 32) * fast_slot_words<32, kNzReg>() * 4;
       const size_t lds_fw = (size_t)(kBlock / 64) * fast_slot_words<64, kNzWide>() * 4;
       if (g_integrate_mode & 1024) {

@@ -76,6 +76,8 @@ def hip():
     if fresh and os.environ.get("MS_INTEGRATE_MODE"):
         # integrator launch-mode bits for whole-run A/B (kinetics.hip, set_integrate_mode)
         mod.set_integrate_mode(int(os.environ["MS_INTEGRATE_MODE"]))  # type: ignore[attr-defined]
+    if fresh and os.environ.get("MS_FUSED_WIDE_BLOCKS"):
+        mod.set_fused_wide_blocks(int(os.environ["MS_FUSED_WIDE_BLOCKS"]))  # type: ignore[attr-defined]
     if fresh and os.environ.get("MS_PLACE_MODE"):
         # 1: per-round placement launches, 2: the single launch as a cooperative launch (world.hip)
         mod.set_place_mode(int(os.environ["MS_PLACE_MODE"]))  # type: ignore[attr-defined]

@@ -45,6 +45,9 @@ for s in "$@"; do case "$s" in
   isweep) run integrator_sweep 300 python scripts/integrator_sweep.py ;;
   dbench) run diffuse_bench 300 python scripts/diffuse_bench.py --dtypes fp32 --blocks 1024 2048 0 --band 0 64 ;;
   iab) for i in 1 2; do for m in 0 4096; do MS_INTEGRATE_MODE=$m run iab_${m}_$i 300 python bench.py --steps 60 --warmup 20; done; done ;;
+  wab) for i in 1 2; do for b in 64 128 256; do MS_FUSED_WIDE_BLOCKS=$b run wab_${b}_$i 300 python bench.py --steps 60 --warmup 20; done; done
+       for b in 64 256; do MS_FUSED_WIDE_BLOCKS=$b run wsweep_$b 300 python scripts/integrator_sweep.py 44000 50000 54000 60000; done ;;
+  tcheck) echo "== trace tcheck"; timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/tcheck -o run --output-format csv -- python performance/check.py --parts update_cells > $O/tcheck.log 2>&1; echo "   rc=$?" ;;
   checkp) MS_CHECK_PROFILE=1 run check_profile 600 python performance/check.py --parts update_cells mutations ;;
   check) run check 600 python performance/check.py ;;
   m1) run m1_bench 600 python bench.py --preset m1 --steps 60 --warmup 10 --step-times ;;
