@@ -80,17 +80,26 @@ def footprint(map_size: int, n_molecules: int, cells: int, map_dtype=torch.float
     return parts
 
 
+MAX_MAP = 65280  # (a multiple of 256 below 2^16: the reference's positions are u16, rust/world.rs)
+MAX_RANK_PIXELS = 1 << 30  # pixels of one rank's map: the kernels index a rank's map with 32-bit ints
+
+
 def plan(hbm_bytes: float = MI355X_HBM, ranks: int = 8, n_molecules: int = 14, map_dtype="fp16",
          cells_per_pixel: float = 1e6 / 16384**2, genome_len: int = 500, reserve: float = 0.12,
-         multiple: int = 256) -> dict:
+         multiple: int = 256, max_map: int = MAX_MAP, max_rank_pixels: int = MAX_RANK_PIXELS) -> dict:
     """The largest map side ``S`` (a multiple of ``multiple``) whose per-rank share -- ``S / ranks``
     owned rows plus halos, ``cells_per_pixel * S²`` cells spread over the ranks -- fits
     ``hbm_bytes * (1 - reserve)`` on every GPU (the reserve covers the runtime, the RCCL buffers,
-    the genome pipeline's scratch and allocator fragmentation). Returns the config and its
-    :func:`footprint`."""
+    the genome pipeline's scratch and allocator fragmentation), within the index widths: a side of at
+    most ``max_map`` (16-bit positions, as in the reference) and at most ``max_rank_pixels`` pixels per
+    rank (32-bit pixel indices in the kernels). At 1M cells per 16384² the index widths bind before
+    HBM does (``fill`` < 1). Returns the config and its :func:`footprint`."""
     budget = hbm_bytes * (1.0 - reserve)
 
-    def cost(S: int) -> int:
+    def cost(S: int) -> float:
+        rows = math.ceil(S / ranks) + (2 if ranks > 1 else 0)
+        if S > max_map or rows * S > max_rank_pixels:
+            return math.inf
         return footprint(S, n_molecules, int(cells_per_pixel * S * S), map_dtype, genome_len, ranks=ranks)["total"]
 
     lo, hi = multiple, multiple

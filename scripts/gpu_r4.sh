@@ -50,6 +50,7 @@ for s in "$@"; do case "$s" in
   tcheck) echo "== trace tcheck"; timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/tcheck -o run --output-format csv -- python performance/check.py --parts update_cells > $O/tcheck.log 2>&1; echo "   rc=$?" ;;
   checkp) MS_CHECK_PROFILE=1 run check_profile 600 python performance/check.py --parts update_cells mutations ;;
   check) run check 600 python performance/check.py ;;
+  hbm) run hbm_bench 900 python bench.py --preset hbm --steps 10 --warmup 3 --step-times ;;
   m1) run m1_bench 600 python bench.py --preset m1 --steps 60 --warmup 10 --step-times ;;
   wide) run wide 300 python bench.py --preset wide ;;
   c1024) run c1024 300 python bench.py --preset c1024 --steps 30 --warmup 5 ;;
