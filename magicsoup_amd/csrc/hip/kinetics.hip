@@ -959,6 +959,20 @@ __global__ void __launch_bounds__(kBlock, W) integrate_narrow_spec_kernel(Integr
   or_block_bits(bits, a.mask_out);
 }
 
+// The two-signals-per-lane narrow cells (s <= 128: the wide chemistries) of the speculative launch,
+// compiled for W waves per SIMD: the path needs ~256 VGPRs to run without spills (316 B/lane of
+// scratch at 4 waves, 208 at 3, 44 at 2), so occupancy and spills trade (set_spl2_waves).
+template <int W>
+__global__ void __launch_bounds__(kBlock, W) integrate_spl2_spec_kernel(IntegrateArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  unsigned bits = 0u;
+  integrate_item_fast<64, kNzReg, true, 2>(a, smem, (int)blockIdx.x * (kBlock / 64) + (int)threadIdx.x / 64, bits,
+                                           nullptr, nullptr);
+  or_block_bits(bits, a.mask_out);
+}
+static int g_spl2_waves = 4;
+void set_spl2_waves(int w) { g_spl2_waves = w <= 2 ? 2 : (w >= 4 ? 4 : 3); }
+
 // Parts >= 1 of the register path with the wide list (known from part 0) in the same launch: the
 // first `nwb` blocks walk the wide list with two 64-lane slots each (integrate_item_fast<64,
 // kNzWide>, the rest of the block idles), the others take the cells as integrate_fast_kernel<G>.
@@ -1509,8 +1523,10 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
       const size_t lds_fw =
           (size_t)(kBlock / 64) * (two ? fast_slot_words<64, kNzWide, 2>() : fast_slot_words<64, kNzWide>()) * 4;
       if (two) {
-        integrate_fast_kernel<64, kNzReg, false, true, 2><<<cdiv(c, kBlock / 64), kBlock, lds_n, st>>>(an, nullptr,
-                                                                                                     nullptr);
+        const unsigned g2 = cdiv(c, kBlock / 64);
+        if (g_spl2_waves == 2) integrate_spl2_spec_kernel<2><<<g2, kBlock, lds_n, st>>>(an);
+        else if (g_spl2_waves == 3) integrate_spl2_spec_kernel<3><<<g2, kBlock, lds_n, st>>>(an);
+        else integrate_spl2_spec_kernel<4><<<g2, kBlock, lds_n, st>>>(an);
         MS_LAUNCH_CHECK();
         integrate_fast_kernel<64, kNzWide, true, true, 2><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
       } else {

@@ -155,6 +155,7 @@ class Genetics:
         state["_tables"] = None
         state["_tables_key"] = None
         state["_device_luts"] = {}
+        state.pop("_hip_scratch", None)  # (device scratch of the translation launches)
         return state
 
     def __setstate__(self, state):

@@ -843,6 +843,10 @@ def neighbors(world, frm: torch.Tensor, to: torch.Tensor, pos: torch.Tensor | No
 
 
 # ---------------------------------------------------------------------------- genomes
+_TRANSLATE_TIMES = os.environ.get("MS_TRANSLATE_TIMES") == "1"  # (diagnostics: per-pass times)
+_LONG_SLOT_BYTES = 64 << 20  # global translation slots of the long-genome pass, reused chunk by chunk
+
+
 def translate(genetics, arena, rows: torch.Tensor):
     """Two-pass device translation of the genomes of cells ``rows`` (a GPU genome pool,
     models/strings.py PoolArena) -> (tokens (k, P, D, 5), n_prots (k,)).
@@ -867,19 +871,35 @@ def translate(genetics, arena, rows: torch.Tensor):
     per = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
     stats = _m().translate_stats(n, _p(counts), _p(ndom), _p(long_count), _p(per), _stream())
     n_long = int(stats[2])
-    gslot = None
+    gslot, chunk = None, 0
     if n_long:
-        gslot = torch.empty(n_long * int(_m().translate_slot_bytes(width)), dtype=torch.uint8, device=dev)
-        _m().translate_count(n_long, _p(rows64), _p(data), _p(off), width, _p(lens), *common, _p(counts), _p(ndom),
-                             _p(long_list), _p(gslot), _p(long_list), _p(long_count), 0, _stream())
+        # global slots (tens of kB per genome) for at most _LONG_SLOT_BYTES at a time: the long genomes
+        # go in chunks through one reused scratch buffer instead of one allocation of n_long slots
+        sb = int(_m().translate_slot_bytes(width))
+        chunk = max(1, min(n_long, _LONG_SLOT_BYTES // sb))
+        gslot = _scratch(genetics).get("long_slots", chunk * sb, torch.uint8, dev)
+        for c0 in range(0, n_long, chunk):
+            _m().translate_count(min(chunk, n_long - c0), _p(rows64), _p(data), _p(off), width, _p(lens), *common,
+                                 _p(counts), _p(ndom), _p(long_list) + 4 * c0, _p(gslot), _p(long_list),
+                                 _p(long_count), 0, _stream())
         stats = _m().translate_stats(n, _p(counts), _p(ndom), _p(long_count), _p(per), _stream())
     P, D = max(int(stats[0]), 1), max(int(stats[1]), 1)
     tokens = torch.zeros(n, P, D, 5, dtype=torch.int32, device=dev)
+    if _TRANSLATE_TIMES:
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record()
     _m().translate_write(n, _p(rows64), _p(data), _p(off), width, _p(lens), *common, _p(counts), P, D, _p(tokens), 0, 0,
                          0, _stream())
-    if n_long:
-        _m().translate_write(n_long, _p(rows64), _p(data), _p(off), width, _p(lens), *common, _p(counts), P, D, _p(tokens),
-                             _p(long_list), _p(gslot), 0, _stream())
+    if _TRANSLATE_TIMES:
+        ev[1].record()
+    for c0 in range(0, n_long, max(chunk, 1)):
+        _m().translate_write(min(chunk, n_long - c0), _p(rows64), _p(data), _p(off), width, _p(lens), *common,
+                             _p(counts), P, D, _p(tokens), _p(long_list) + 4 * c0, _p(gslot), 0, _stream())
+    if _TRANSLATE_TIMES:
+        ev[2].record()
+        ev[2].synchronize()
+        print(f"translate: n {n} long {n_long} P {P} D {D} width {width} write {ev[0].elapsed_time(ev[1]):.2f} ms "
+              f"long write {ev[1].elapsed_time(ev[2]):.2f} ms", flush=True)
     return tokens, per
 
 

@@ -76,6 +76,8 @@ def hip():
     if fresh and os.environ.get("MS_INTEGRATE_MODE"):
         # integrator launch-mode bits for whole-run A/B (kinetics.hip, set_integrate_mode)
         mod.set_integrate_mode(int(os.environ["MS_INTEGRATE_MODE"]))  # type: ignore[attr-defined]
+    if fresh and os.environ.get("MS_SPL2_WAVES"):
+        mod.set_spl2_waves(int(os.environ["MS_SPL2_WAVES"]))  # type: ignore[attr-defined]
     if fresh and os.environ.get("MS_FUSED_WIDE_BLOCKS"):
         mod.set_fused_wide_blocks(int(os.environ["MS_FUSED_WIDE_BLOCKS"]))  # type: ignore[attr-defined]
     if fresh and os.environ.get("MS_PLACE_MODE"):

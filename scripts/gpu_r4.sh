@@ -48,6 +48,9 @@ for s in "$@"; do case "$s" in
   wab) for i in 1 2; do for b in 64 128 256; do MS_FUSED_WIDE_BLOCKS=$b run wab_${b}_$i 300 python bench.py --steps 60 --warmup 20; done; done
        for b in 64 256; do MS_FUSED_WIDE_BLOCKS=$b run wsweep_$b 300 python scripts/integrator_sweep.py 44000 50000 54000 60000; done ;;
   tcheck) echo "== trace tcheck"; timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/tcheck -o run --output-format csv -- python performance/check.py --parts update_cells > $O/tcheck.log 2>&1; echo "   rc=$?" ;;
+  sab) for i in 1 2; do for w in 4 3 2; do MS_SPL2_WAVES=$w run sab_${w}_$i 300 python bench.py --preset wide --steps 40 --warmup 10; done; done ;;
+  tcheck2) MS_TRANSLATE_TIMES=1 run check_translate 300 python performance/check.py --parts update_cells ;;
+  tprobe) run translate_probe 300 python scripts/translate_probe.py ;;
   checkp) MS_CHECK_PROFILE=1 run check_profile 600 python performance/check.py --parts update_cells mutations ;;
   check) run check 600 python performance/check.py ;;
   hbm) run hbm_bench 900 python bench.py --preset hbm --steps 10 --warmup 3 --step-times ;;
