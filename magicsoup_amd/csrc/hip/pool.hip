@@ -68,6 +68,26 @@ __global__ void __launch_bounds__(64) pool_read_kernel(int k, const int64_t* src
   }
 }
 
+// Genomes of cells src[j] (or j) back to back: out[dst_off[j] : dst_off[j] + lens] (no padding;
+// StringColumn materialisation copies exactly the genome bytes to the host).
+__global__ void __launch_bounds__(64) pool_read_packed_kernel(int k, const int64_t* src, const uint8_t* pool,
+                                                              const int64_t* off, const int32_t* lens,
+                                                              const int64_t* dst_off, uint8_t* out) {
+  const int lane = threadIdx.x;
+  for (int j = blockIdx.x; j < k; j += gridDim.x) {
+    const long long c = src ? src[j] : j;
+    const int L = lens[c];
+    const uint8_t* s = pool + off[c];
+    uint8_t* d = out + dst_off[j];
+    for (int t = lane * 16; t < L; t += 64 * 16) {  // 16-byte loads (allocations are 16-byte aligned)
+      const uint4 q = *reinterpret_cast<const uint4*>(s + t);
+      const uint8_t* b = reinterpret_cast<const uint8_t*>(&q);
+      const int e = min(16, L - t);
+      for (int u = 0; u < e; ++u) d[t + u] = b[u];
+    }
+  }
+}
+
 // Compaction: unique genome u (old offset old_off[u], size bytes) -> new_pool + new_off[u].
 __global__ void __launch_bounds__(64) pool_compact_kernel(int nu, const uint8_t* old_pool, const int64_t* old_off,
                                                           const int64_t* sizes, uint8_t* new_pool,
@@ -102,6 +122,15 @@ void pool_read(int k, uintptr_t src, uintptr_t pool, uintptr_t off, uintptr_t le
   MS_LAUNCH_CHECK();
 }
 
+void pool_read_packed(int k, uintptr_t src, uintptr_t pool, uintptr_t off, uintptr_t lens, uintptr_t dst_off,
+                      uintptr_t out, uintptr_t stream) {
+  if (k <= 0) return;
+  pool_read_packed_kernel<<<grid_for(k), 64, 0, S_(stream)>>>(k, src ? P_<int64_t>(src) : nullptr, P_<uint8_t>(pool),
+                                                              P_<int64_t>(off), P_<int32_t>(lens), P_<int64_t>(dst_off),
+                                                              P_<uint8_t>(out));
+  MS_LAUNCH_CHECK();
+}
+
 void pool_compact(int nu, uintptr_t old_pool, uintptr_t old_off, uintptr_t sizes, uintptr_t new_pool,
                   uintptr_t new_off, uintptr_t stream) {
   if (nu <= 0) return;
@@ -123,6 +152,7 @@ void bind_pool(pybind11::module_& m) {
       .def_readwrite("cap", &GenomePoolArgs::cap);
   m.def("pool_write", &pool_write, "genome rows (k, L) -> new pool allocations of cells dst[j] (or n0 + j)");
   m.def("pool_read", &pool_read, "genomes of cells -> zero-padded rows (k, W)");
+  m.def("pool_read_packed", &pool_read_packed, "genomes of cells back to back (no padding)");
   m.def("pool_compact", &pool_compact, "copy unique genomes into a new pool (PoolArena.collect)");
 }
 

@@ -458,11 +458,21 @@ class PoolArena:
         if lmax == 0:
             return [""] * k
         from magicsoup_amd.ops import native
+        from magicsoup_amd.ops.hip_ops import _stream
 
-        data = self.rows_of(idx, _r16(lmax)).cpu().numpy()
-        raw = native.host().unpack_rows(data, ls.numpy().astype(np.int32, copy=False)).decode("ascii")
-        ends = np.cumsum(ls.numpy(), dtype=np.int64).tolist()
-        starts = [0] + ends[:-1]
+        # the genomes back to back on the device (exclusive prefix sum of the lengths), one
+        # transfer of exactly their bytes, one decode; the strings are slices of it
+        ends_np = np.cumsum(ls.numpy(), dtype=np.int64)
+        total = int(ends_np[-1])
+        starts_np = ends_np - ls.numpy()
+        dst_off = torch.from_numpy(starts_np).to(self.device)
+        out = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
+        native.hip().pool_read_packed(k, 0 if idx is None else idx.data_ptr(), self.data.data_ptr(),
+                                      self.off.data_ptr(), self.lens.data_ptr(), dst_off.data_ptr(), out.data_ptr(),
+                                      _stream())
+        raw = str(memoryview(out[:total].cpu().numpy()), "ascii")
+        ends = ends_np.tolist()
+        starts = starts_np.tolist()
         return [raw[a:b] for a, b in zip(starts, ends)]
 
 

@@ -49,6 +49,13 @@ for s in "$@"; do case "$s" in
        for b in 64 256; do MS_FUSED_WIDE_BLOCKS=$b run wsweep_$b 300 python scripts/integrator_sweep.py 44000 50000 54000 60000; done ;;
   tcheck) echo "== trace tcheck"; timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/tcheck -o run --output-format csv -- python performance/check.py --parts update_cells > $O/tcheck.log 2>&1; echo "   rc=$?" ;;
   sab) for i in 1 2; do for w in 4 3 2; do MS_SPL2_WAVES=$w run sab_${w}_$i 300 python bench.py --preset wide --steps 40 --warmup 10; done; done ;;
+  pmcw|pmcf) # PMC of the integrator / stencil kernels (one pass, 8 SQ counters, kernel filter, no trace domains)
+     preset=$([ "$s" = pmcw ] && echo wide || echo flagship)
+     echo "== pmc $preset"
+     (cd /tmp && timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS \
+        --kernel-include-regex "integrate|diffuse_stencil" -d "$OLDPWD/$O/pmc_$preset" -o run --output-format csv \
+        -- python3 "$OLDPWD/bench.py" --preset $preset --steps 3 --warmup 2 > "$OLDPWD/$O/pmc_$preset.log" 2>&1)
+     rc=$?; echo "   rc=$rc"; if fatal $rc; then exit $rc; fi ;;
   tcheck2) MS_TRANSLATE_TIMES=1 run check_translate 300 python performance/check.py --parts update_cells ;;
   tprobe) run translate_probe 300 python scripts/translate_probe.py ;;
   checkp) MS_CHECK_PROFILE=1 run check_profile 600 python performance/check.py --parts update_cells mutations ;;
