@@ -66,5 +66,6 @@ for s in "$@"; do case "$s" in
   c1024) run c1024 300 python bench.py --preset c1024 --steps 30 --warmup 5 ;;
   c256) run c256_40k 300 python bench.py --map-size 256 --cells 40000 ;;
   tflag) trace tflag 19 --steps 20 --warmup 20 ;;
+  overlap) run overlap 300 python scripts/overlap_probe.py 4096 50000 20 ;;
   *) echo "unknown step $s" ;;
 esac; done
