@@ -132,14 +132,17 @@ std::string rccl_async_error(uintptr_t comm) {
 // (a dead peer leaves an RCCL kernel waiting forever: a plain hipStreamSynchronize would hang).
 // Returns "" when the stream drained; otherwise every communicator in `comms` is aborted (its
 // kernels are released, the handles become unusable) and the reason is returned: the RCCL error,
-// or "timeout" after `timeout_s` seconds.
-std::string rccl_guarded_wait(const std::vector<uintptr_t>& comms, uintptr_t stream, double timeout_s) {
+// or "timeout" after `timeout_s` seconds. `event` (optional): wait for that event instead of the
+// whole stream (a deferred read-back that must not wait for work queued after it).
+std::string rccl_guarded_wait(const std::vector<uintptr_t>& comms, uintptr_t stream, double timeout_s,
+                              uintptr_t event) {
   const Rccl& r = api();
   hipStream_t s = S_(stream);
+  hipEvent_t ev = reinterpret_cast<hipEvent_t>(event);
   const auto t0 = std::chrono::steady_clock::now();
   std::string why;
   for (long long it = 0;; ++it) {
-    const hipError_t q = hipStreamQuery(s);
+    const hipError_t q = ev ? hipEventQuery(ev) : hipStreamQuery(s);
     if (q == hipSuccess) return std::string();
     if (q != hipErrorNotReady) MS_HIP_CHECK(q);
     // errors are polled every 256 queries (~tens of microseconds): the common case (a healthy job

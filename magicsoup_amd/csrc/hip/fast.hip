@@ -154,10 +154,11 @@ __global__ void fill_i64_kernel(int64_t* dst, const int64_t* val, int k) {
 // neighbours' dividing cells -> placement over the mask -> winners split by destination (local /
 // upper halo / lower halo: par3 / npos3 at offsets 0, n, 2n) with the record headers -> header
 // exchange. st (int32[20]): counts [0:3], headers to up [4:8] / down [8:12], from up [12:16] / down
-// [16:20]. marks: 4 C bytes.
+// [16:20]. marks: 4 C bytes. host_st (optional, pinned host memory): st is copied there at the end,
+// so the host reads it after an event instead of with a stream-synchronising read-back.
 void fast_dist_divide_a(const FastWorld& f, int n, uintptr_t mask, uintptr_t comm, int up, int down, uint64_t seed,
                         uint64_t call, uintptr_t marks, uintptr_t par3, uintptr_t npos3, uintptr_t st, int lw, int gw,
-                        uintptr_t stream) {
+                        uintptr_t host_st, uintptr_t stream) {
   if (!f.ready) throw std::invalid_argument("fast_dist_divide_a: descriptor not finalized");
   if (n <= 0 || n > f.cap) throw std::invalid_argument("fast_dist_divide_a: cell count outside the capacity");
   if (f.wrap || f.r_lo != 1 || f.R != f.r_hi + 1) throw std::invalid_argument("fast_dist_divide_a: not a strip");
@@ -170,6 +171,9 @@ void fast_dist_divide_a(const FastWorld& f, int n, uintptr_t mask, uintptr_t com
                     f.rounds, seed, call, stream);
   place_split(n, f.result, 0, C, H, par3, npos3, st, st + 16, st + 32, lw, gw, f.m, stream);
   rccl_exchange(comm, up, down, st + 16, 16, st + 32, 16, st + 64, 16, st + 48, 16, stream);
+  if (host_st)
+    MS_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(host_st), reinterpret_cast<const void*>(st),
+                                20 * sizeof(int32_t), hipMemcpyDeviceToHost, S_(stream)));
 }
 
 // Phase B (after the synchronisation, counts known): child records of the exporting parents packed

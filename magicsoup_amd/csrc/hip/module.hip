@@ -180,7 +180,8 @@ std::string rccl_unique_id();
 uintptr_t rccl_init(const std::string& uid, int nranks, int rank);
 void rccl_destroy(uintptr_t comm, bool abort);
 std::string rccl_async_error(uintptr_t comm);
-std::string rccl_guarded_wait(const std::vector<uintptr_t>& comms, uintptr_t stream, double timeout_s);
+std::string rccl_guarded_wait(const std::vector<uintptr_t>& comms, uintptr_t stream, double timeout_s,
+                              uintptr_t event);
 void rccl_allreduce(uintptr_t comm, uintptr_t buf, long long count, int dtype, int op, uintptr_t stream);
 void rccl_exchange(uintptr_t comm, int up, int down, uintptr_t send_up, long long n_send_up, uintptr_t send_down,
                    long long n_send_down, uintptr_t recv_down, long long n_recv_down, uintptr_t recv_up,
@@ -322,8 +323,10 @@ PYBIND11_MODULE(_hip, m) {
   m.def("rccl_init", [](py::bytes uid, int nranks, int rank) { return msd::rccl_init(std::string(uid), nranks, rank); });
   m.def("rccl_destroy", &msd::rccl_destroy);
   m.def("rccl_async_error", &msd::rccl_async_error);
-  m.def("rccl_guarded_wait", &msd::rccl_guarded_wait, py::call_guard<py::gil_scoped_release>(),
-        "wait for a stream while polling RCCL errors; aborts the communicators on error / timeout");
+  m.def("rccl_guarded_wait", &msd::rccl_guarded_wait, py::call_guard<py::gil_scoped_release>(), py::arg("comms"),
+        py::arg("stream"), py::arg("timeout_s"), py::arg("event") = 0,
+        "wait for a stream (or one event on it) while polling RCCL errors; aborts the communicators on error / "
+        "timeout");
   m.def("rccl_allreduce", &msd::rccl_allreduce, "in-place all-reduce on a stream (dtype 0 i32 1 f32 2 f64 3 i64; op 0 sum 1 max 2 min)");
   m.def("rccl_exchange", &msd::rccl_exchange, "grouped byte send/recv with the up / down neighbours on a stream");
   m.def("strip_marks", &msd::strip_marks, "boundary-row bytes (1 occupied, 3 dividing) for the strip neighbours");

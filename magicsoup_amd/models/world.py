@@ -536,9 +536,9 @@ class World:
 
         d = self.__dict__
         n0, slot, ev = d["_count_pending"]
-        if hip_ops._GUARD:
-            hip_ops._GUARD[0]()  # (communicators alive: a peer failure raises instead of hanging)
-        ev.synchronize()
+        # (only the division's work: not what was queued since, e.g. a diffusion stencil; with
+        # communicators alive a peer failure raises instead of hanging)
+        hip_ops.guarded_sync(ev)
         k = int(hip_ops._m().status_read(slot)[0])
         # (the pending entry stays until the count is read: a failure above leaves it for a retry
         # instead of a world whose device rows and host count disagree)

@@ -148,11 +148,14 @@ def wait_count(slot: int) -> int:
     return int(_m().stream_sync_read(slot, _stream())[0])
 
 
-def guarded_sync() -> None:
-    """Before a blocking read-back of a decomposed world: wait for the current stream with peer
-    failure detection (no-op without native communicators)."""
+def guarded_sync(event=None) -> None:
+    """Before a blocking read-back of a decomposed world: wait for the current stream (or only
+    for ``event``, an ops.streams.NEvent) with peer failure detection (without native
+    communicators: a plain wait for the event, if given)."""
     if _GUARD:
-        _GUARD[0]()
+        _GUARD[0](0 if event is None else event.h)
+    elif event is not None:
+        event.synchronize()
 
 
 def check_placement() -> None:

@@ -36,8 +36,9 @@ class CommError(RuntimeError):
     process are aborted (the job is fail-stop: restart from a checkpoint)."""
 
 
-def guarded_sync() -> None:
-    """Wait for the current HIP stream while polling every live RCCL communicator of this process
+def guarded_sync(event: int = 0) -> None:
+    """Wait for the current HIP stream (or only for the native ``event`` handle, see
+    magicsoup_amd.ops.streams.NEvent) while polling every live RCCL communicator of this process
     for asynchronous errors, with the :data:`TIMEOUT_S` bound. On a failure all communicators are
     aborted and :class:`CommError` is raised. Called before the host synchronisations of a
     decomposed world's step (magicsoup_amd.ops.hip_ops.wait_count)."""
@@ -45,7 +46,7 @@ def guarded_sync() -> None:
     if not live:
         return
     m = live[0]._m
-    why = m.rccl_guarded_wait([c.handle for c in live], live[0]._stream(), TIMEOUT_S)
+    why = m.rccl_guarded_wait([c.handle for c in live], live[0]._stream(), TIMEOUT_S, event)
     if why:
         for c in live:
             c.handle = 0  # aborted by the wait

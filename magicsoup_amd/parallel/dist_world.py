@@ -425,8 +425,8 @@ class DistributedWorld(World):
     def divide_cells_t(self, cell_idxs, lazy: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
         """Division (collective). Children landing in a neighbour's boundary row are created on
         that rank; the returned pairs cover local children only (counts in ``self.migrated``).
-        ``lazy`` is accepted for the World signature: the strip protocol synchronises once in the
-        middle anyway (the record sizes), so the pairs are always returned.
+        ``lazy`` (GPU mask over RCCL, see :meth:`_divide_mask_native`): returns None and completes
+        the division when the cell count is next needed; otherwise the pairs are returned.
 
         Protocol (module docstring): boundary marks -> reservations -> placement rounds ->
         winners split by destination row + record headers exchanged -> one synchronisation ->
@@ -448,7 +448,7 @@ class DistributedWorld(World):
             idxs = self._idx_tensor(cell_idxs)
             k = int(idxs.numel())
         if mask is not None and self._rccl_native():
-            return self._divide_mask_native(mask)
+            return self._divide_mask_native(mask, lazy=lazy)
         sc = _scratch(self)
         empty = torch.zeros(0, dtype=torch.long, device=dev)
         # 1. boundary bytes (occupied / dividing) to the neighbours; halo occupancy + reservations
@@ -541,16 +541,24 @@ class DistributedWorld(World):
         d = self.__dict__
         return not d.get("_side_active") and isinstance(d.get("_comm"), RcclComm) and _NATIVE_DIVIDE
 
-    def _divide_mask_native(self, mask: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
-        """divide_cells_t over a GPU mask as two native calls around the one synchronisation
-        (csrc/hip/fast.hip fast_dist_divide_a / _b): the same protocol, kernels and exchanges as the
-        Python path below."""
-        from magicsoup_amd.ops import genome_pipeline, hip_ops
+    def _divide_mask_native(self, mask: torch.Tensor, lazy: bool = False) -> tuple[torch.Tensor, torch.Tensor] | None:
+        """divide_cells_t over a GPU mask as two native calls around the one read-back of the
+        counts (csrc/hip/fast.hip fast_dist_divide_a / _b): the same protocol, kernels and exchanges
+        as the Python path below.
+
+        ``lazy``: phase A (marks, reservations, placement, winners split by destination, headers
+        exchanged) is issued and the call returns None; the read-back and phase B (child records
+        exchanged, children committed, arrivals appended) follow when the cell count is next needed
+        (:meth:`_resolve_count`: at the latest the next diffusion, before its stencil). What runs in
+        between only queues genome operations or scales all capacity rows (degradation: halving a
+        parent's molecules afterwards gives the same bits, the factor 0.5 is exact), so the result
+        equals the eager protocol's, without the host waiting for the placement."""
+        from magicsoup_amd.ops import hip_ops
         from magicsoup_amd.ops.hip_ops import _m, _p, _scratch, _stream
 
         comm = self.__dict__["_comm"]
         dev = self._tensor_device()
-        n0, C, m = self.n_cells, self.map_size, self.n_molecules
+        n0, C = self.n_cells, self.map_size
         lw, gw = int(self._labels.width), int(self._genomes.width)
         fw = self._fast_world(n0)
         sc = _scratch(self)
@@ -558,11 +566,34 @@ class DistributedWorld(World):
         par = sc.get("dv_par", 3 * n0, torch.int64, dev)
         npos = sc.get("dv_npos", 6 * n0, torch.int32, dev)
         st = sc.get("dv_status", 20, torch.int32, dev)
+        host_st = self.__dict__.get("_dv_host_st")
+        if host_st is None:
+            host_st = self.__dict__["_dv_host_st"] = torch.zeros(20, dtype=torch.int32, pin_memory=True)
         seed, call = hip_ops._rng()
         _m().fast_dist_divide_a(fw, n0, _p(mask), comm.handle, comm.up, comm.down, seed, call, _p(mk), _p(par),
-                                _p(npos), _p(st), lw, gw, _stream())
+                                _p(npos), _p(st), lw, gw, host_st.data_ptr(), _stream())
+        if lazy:
+            from magicsoup_amd.ops.streams import NEvent
+
+            self.__dict__["_count_pending"] = (n0, None, NEvent().record(), "strip", lw, gw)
+            return None
         hip_ops.guarded_sync()  # (peer failures raise instead of hanging the read-back)
-        v = st.tolist()  # the one synchronisation: local winner counts + the neighbours' headers
+        return self._divide_phase_b(n0, lw, gw)
+
+    def _divide_phase_b(self, n0: int, lw: int, gw: int) -> tuple[torch.Tensor, torch.Tensor]:
+        """Phase B of :meth:`_divide_mask_native` once phase A's counts are on the host (its pinned
+        status copy is complete): records out, children in, arrivals appended and their parameter
+        rows rebuilt on the device."""
+        from magicsoup_amd.ops import genome_pipeline, hip_ops
+        from magicsoup_amd.ops.hip_ops import _m, _p, _scratch, _stream
+
+        comm = self.__dict__["_comm"]
+        dev = self._tensor_device()
+        m = self.n_molecules
+        sc = _scratch(self)
+        par = sc.get("dv_par", 3 * n0, torch.int64, dev)
+        npos = sc.get("dv_npos", 6 * n0, torch.int32, dev)
+        v = self.__dict__["_dv_host_st"].tolist()  # local winner counts + the neighbours' headers
         hip_ops.check_placement()
         n_loc, n_up, n_dn = v[0], v[1], v[2]
         hdr_up, hdr_dn = v[12:16], v[16:20]
@@ -597,6 +628,43 @@ class DistributedWorld(World):
         mig["divided_in"] += k_in
         self.__dict__["_xfer"] = (par[n0 : n0 + n_up], par[2 * n0 : 2 * n0 + n_dn], int(hdr_up[0]), int(hdr_dn[0]))
         return par[:n_loc], torch.arange(n0, n0 + n_loc, device=self.device)
+
+    def _resolve_count(self) -> None:
+        """Adopt a pending division: World's (a winner count) or a strip division issued with
+        ``lazy=True`` (wait for its phase A only, then issue phase B, see _divide_mask_native). Queued
+        genome operations then depend on phase B: their chains wait for it, not for the state when
+        they were queued."""
+        d = self.__dict__
+        pend = d.get("_count_pending")
+        if pend is None or len(pend) < 4:
+            return super()._resolve_count()
+        from magicsoup_amd.ops import hip_ops
+
+        n0, _, ev, _, lw, gw = pend
+        hip_ops.guarded_sync(ev)
+        # (the entry stays until the counts are read: a failure above leaves it for a retry)
+        d["_count_pending"] = None
+        # the genome ops queued since the division stay queued during phase B: its parameter
+        # rebuild of the arrivals reconciles the world (Kinetics._sync), which would otherwise issue
+        # them against the state before phase B
+        queued = d.get("_deferred")
+        d["_deferred"] = []
+        try:
+            self._divide_phase_b(n0, lw, gw)
+        finally:
+            if queued:
+                from magicsoup_amd.ops.streams import NEvent
+
+                d["_deferred"] = queued + d["_deferred"]
+                d["_defer_event"] = NEvent().record()
+
+    @_op("diffuse_molecules")
+    def diffuse_molecules(self):
+        """World's diffusion; a strip division issued lazily is completed first, so that its record
+        exchange and commit are queued before the stencil and the genome chains that follow it."""
+        if self._strips and self.__dict__.get("_count_pending") is not None:
+            self._resolve_count()
+        return super().diffuse_molecules()
 
     def _append_arrivals(self, hdr_up, in_up, hdr_dn, in_dn) -> None:
         """Append the records received from the upper (row 1) and lower (row H) neighbours as new
@@ -705,7 +773,9 @@ class DistributedWorld(World):
             # (lengths / event genomes exchanged) is issued now on the side stream (_xb_pre_issue)
             # (only as the first queued genome op: its genomes are then final for this call; a later
             # queued call computes its boundary part at the flush, after the earlier results)
-            early = (_XB_EARLY and not self.__dict__.get("_deferred")
+            # (not while a lazy division is pending: its children and arrivals exist only after the
+            # count is resolved, at the latest before the diffusion stencil; the chains follow it)
+            early = (_XB_EARLY and not self.__dict__.get("_deferred") and self.__dict__.get("_count_pending") is None
                      and isinstance(self.__dict__.get("_comm_side"), RcclComm))
             pre = self._xb_pre_issue(p) if early else None
             self._defer(_Deferred(lambda: self._recombinate_strips_all(p, pre), "rec", (p, pre)))

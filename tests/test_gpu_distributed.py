@@ -324,3 +324,72 @@ def _body_native_xb(rank, ws):
 
 def test_gpu_native_boundary_recombination_matches_python_protocol():
     run_ranks(_body_native_xb, 1, timeout=300, backend="nccl")
+
+
+def _body_lazy_strip_divide(rank, ws):
+    """One rank over RCCL (virtual strips): the reference loop with divide_cells_t(mask, lazy=True)
+    -- phase B deferred to the next diffusion, the boundary recombination issued at the flush --
+    ends in exactly the state of the eager protocol (positions, molecules, divisions, lifetimes,
+    genomes, labels, parameters, occupancy, map, migration counters)."""
+    import random
+
+    import magicsoup_amd as ms
+    from magicsoup_amd.parallel import DistributedWorld
+    from tests.conftest import gen_genomes
+
+    ms.set_seed(21)
+    torch.manual_seed(21)
+    w = ms.World(chemistry=_chem(), map_size=64, seed=21, device="cpu")
+    w.spawn_cells(gen_genomes(1200, 300))
+    atp = _chem().molname_2_idx["ATP"]
+    out = {}
+    for lazy in (False, True, "again"):
+        random.seed(5)
+        dw = DistributedWorld(chemistry=_chem(), map_size=64, seed=22, device="cuda", strips=True)
+        dw.adopt_maps(w)
+        dw.scatter_from(w, maps=False)
+        ms.set_seed(23)
+        for it in range(4):
+            dw.enzymatic_activity()
+            dw.kill_cells(dw.cell_molecules[:, atp] < 0.5)
+            repl = dw.cell_molecules[:, atp] > 2.0
+            dw.cell_molecules[:, atp] -= 1.0 * repl
+            r = dw.divide_cells_t(repl, lazy=lazy is True)
+            assert (r is None) == (lazy is True)
+            if lazy is True:
+                assert dw.__dict__.get("_count_pending") is not None
+            dw.recombinate_cells(p=1e-4)
+            dw.mutate_cells(p=1e-4)
+            dw.degrade_molecules()
+            dw.diffuse_molecules()
+            assert dw.__dict__.get("_count_pending") is None  # completed before the stencil
+            dw.increment_cell_lifetimes()
+        dw.synchronize()
+        out[lazy] = (dw.cell_positions.cpu(), dw.cell_molecules.cpu(), dw.cell_divisions.cpu(),
+                     dw.cell_lifetimes.cpu(), dw.cell_map.cpu(), dw.owned_molecule_map().cpu(), dw.kinetics.N.cpu().clone(),
+                     list(dw.cell_genomes), list(dw.cell_labels), dict(dw.migrated))
+        dw.close()
+    names = ("positions", "molecules", "divisions", "lifetimes", "cell_map", "molecule_map", "N", "genomes",
+             "labels", "migrated")
+
+    def diff(a, b):
+        bad = []
+        for name, x, y in zip(names, a, b):
+            same = torch.equal(x, y) if isinstance(x, torch.Tensor) and x.shape == y.shape else x == y
+            if not same:
+                extra = ""
+                if isinstance(x, torch.Tensor) and x.shape == y.shape and x.is_floating_point():
+                    extra = f" max abs diff {float((x - y).abs().max())}"
+                elif isinstance(x, torch.Tensor):
+                    extra = f" shapes {tuple(x.shape)} {tuple(y.shape)}"
+                bad.append(name + extra)
+        return bad
+
+    a, b, c = out[False], out[True], out["again"]
+    assert a[9]["divided_in"] > 0
+    assert not diff(a, c), f"eager protocol not reproducible: {diff(a, c)}"
+    assert not diff(a, b), f"lazy differs from eager: {diff(a, b)} ({a[9]} vs {b[9]})"
+
+
+def test_gpu_lazy_strip_divide_matches_eager():
+    run_ranks(_body_lazy_strip_divide, 1, timeout=300, backend="nccl")
