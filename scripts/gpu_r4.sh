@@ -34,6 +34,7 @@ for s in "$@"; do case "$s" in
   drv) run drv 300 python bench.py --steps 20 --warmup 5 ;;
   proxy) run proxy8_plain 300 python bench.py --map-size 1448 --cells 6250 ;;
   virt) MS_VIRTUAL_STRIPS=1 run proxy8_virtual 300 python bench.py --map-size 1448 --cells 6250 ;;
+  fvirt) MS_VIRTUAL_STRIPS=1 run flagship_virtual 300 python bench.py ;;
   hsf) run host_split_flagship 300 python scripts/host_split.py 4096 50000 40 ;;
   hsp) run host_split_proxy8 300 python scripts/host_split.py 1448 6250 60 ;;
   hsv) MS_VIRTUAL_STRIPS=1 run host_split_proxy8_virtual 300 python scripts/host_split.py 1448 6250 60 ;;
