@@ -664,7 +664,23 @@ class DistributedWorld(World):
         exchange and commit are queued before the stencil and the genome chains that follow it."""
         if self._strips and self.__dict__.get("_count_pending") is not None:
             self._resolve_count()
+            self._xb_pre_issue_queued()
         return super().diffuse_molecules()
+
+    def _xb_pre_issue_queued(self) -> None:
+        """After a lazy division completed: issue the boundary recombination's collective part of
+        the first queued recombinate_cells() now, before the stencil (what recombinate_cells() does
+        at the call when no division is pending). Issued behind the stencil instead, its RCCL kernel
+        waits for the stencil's workgroups (243 us at 4096^2) and the genome chain after it misses
+        the stencil it should run next to (profiles/r4/s6/tfvirt_steps.txt)."""
+        d = self.__dict__
+        q = d.get("_deferred")
+        if not (_XB_EARLY and q and getattr(q[0], "kind", None) == "rec" and q[0].args[1] is None
+                and isinstance(d.get("_comm_side"), RcclComm)):
+            return
+        p = q[0].args[0]
+        pre = self._xb_pre_issue(p)
+        q[0] = _Deferred(lambda: self._recombinate_strips_all(p, pre), "rec", (p, pre))
 
     def _append_arrivals(self, hdr_up, in_up, hdr_dn, in_dn) -> None:
         """Append the records received from the upper (row 1) and lower (row H) neighbours as new

@@ -25,7 +25,7 @@ trace() {  # trace <name> <steps-to-summarise> <bench args...>
   local rc=$?
   echo "   rc=$rc"
   if fatal $rc; then echo "fatal rc=$rc in $name"; tail -30 "$O/$name.log"; exit $rc; fi
-  python scripts/step_kernels.py $O/$name/run_kernel_trace.csv $k > $O/${name}_steps.txt 2>&1
+  MARKER=${MARKER:-void msd::diffuse_stencil4} python scripts/step_kernels.py $O/$name/run_kernel_trace.csv $k > $O/${name}_steps.txt 2>&1
 }
 for s in "$@"; do case "$s" in
   tests) run tests 1000 python -u -m pytest tests -m gpu -q --maxfail 5 --timeout 120 --timeout-method thread ;;
@@ -67,6 +67,8 @@ for s in "$@"; do case "$s" in
   c1024) run c1024 300 python bench.py --preset c1024 --steps 30 --warmup 5 ;;
   c256) run c256_40k 300 python bench.py --map-size 256 --cells 40000 ;;
   tflag) trace tflag 19 --steps 20 --warmup 20 ;;
+  tfvirt) MARKER=msd::diffuse_corr_kernel MS_VIRTUAL_STRIPS=1 trace tfvirt 19 --steps 20 --warmup 20 ;;
+  hsfv) MS_VIRTUAL_STRIPS=1 MS_NATIVE_TIMES=1 MS_PY_TIMES=1 run host_split_flagship_virtual 300 python scripts/host_split.py 4096 50000 40 ;;
   overlap) run overlap 300 python scripts/overlap_probe.py 4096 50000 20 ;;
   *) echo "unknown step $s" ;;
 esac; done
