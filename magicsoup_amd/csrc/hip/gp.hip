@@ -43,6 +43,8 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
                   uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
                   uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t W, uintptr_t Q, uintptr_t overflow,
                   uintptr_t dn, uintptr_t stream);
+void mut_count_select(int n, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
+                      uintptr_t gflags, uintptr_t opflags, uintptr_t sel, uintptr_t out_dev, int cap, uintptr_t stream);
 void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
                uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
 void mut_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t rows, uintptr_t arena, uintptr_t off, uintptr_t lens,
@@ -283,8 +285,7 @@ int gp_mutate(const GpArena& a, const GpGen& g, const GpKin& k, double p, double
   const uintptr_t kk = c.take(4 * (size_t)n), sel = c.take(8 * (size_t)n);
   const int out_w = (L + kcap + 15) / 16 * 16;
   const uintptr_t out = c.take((size_t)cap * out_w), out_len = c.take(4 * (size_t)cap);
-  mut_count(n, 0, a.lens, p, seed, call, kk, kcap, a.gflags, a.opflags, stream);
-  select_indices_capped(n, kSelI32Pos, kk, sel, a.cnt, cap, a.gflags, a.opflags, stream);
+  mut_count_select(n, a.lens, p, seed, call, kk, kcap, a.gflags, a.opflags, sel, a.cnt, cap, stream);
   mut_apply(cap, a.cnt, sel, 0, a.data, a.off, a.lens, kk, p_indel, p_del, seed, call, out, out_w, out_len, stream);
   arena_scatter(cap, a.cnt, 1, sel, out, out_w, out_len, a.data, a.off, a.top, a.pool_cap, L, a.lens, 0, 0, 0,
                 a.gflags, a.opflags, stream);
@@ -425,8 +426,7 @@ std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpAren
   const uintptr_t mk = cm.take(4 * (size_t)n), msel = cm.take(8 * (size_t)n);
   const int mout_w = (L + kcap + 15) / 16 * 16;
   const uintptr_t mout = cm.take((size_t)mcap * mout_w), mout_len = cm.take(4 * (size_t)mcap);
-  mut_count(n, 0, am.lens, p, seed_m, call_m, mk, kcap, am.gflags, am.opflags, stream);
-  select_indices_capped(n, kSelI32Pos, mk, msel, am.cnt, mcap, am.gflags, am.opflags, stream);
+  mut_count_select(n, am.lens, p, seed_m, call_m, mk, kcap, am.gflags, am.opflags, msel, am.cnt, mcap, stream);
   mut_apply(mcap, am.cnt, msel, 0, am.data, am.off, am.lens, mk, p_indel, p_del, seed_m, call_m, mout, mout_w, mout_len,
             stream);
   arena_scatter(mcap, am.cnt, 1, msel, mout, mout_w, mout_len, am.data, am.off, am.top, am.pool_cap, L, am.lens, 0, 0,

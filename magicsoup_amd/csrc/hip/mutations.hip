@@ -50,6 +50,38 @@ __global__ void __launch_bounds__(256) mut_count_kernel(int n, const int64_t* ro
   k[i] = (int32_t)(kk > L ? L : kk);
 }
 
+// mut_count_kernel over all n genomes (rows = identity) that also writes each block's number of
+// genomes with events into tile_count[block] (tile_max[block] = 0): the counts of the order-preserving
+// selection that follows (select.hip select_write_i32pos_capped with 16 blocks per 4096-item tile),
+// so the chain needs no separate count pass over k. The grid covers whole selection tiles; blocks
+// past n write zero counts.
+__global__ void __launch_bounds__(256) mut_count_tiles_kernel(int n, const int32_t* lens, double p, uint64_t seed,
+                                                              uint64_t call, int32_t* k, int kcap, const int* gflags,
+                                                              int* opflags, int32_t* tile_count, int32_t* tile_max) {
+  __shared__ int s_cnt[4];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int kk = 0;
+  if (i < n) {
+    if (!gp_skip(i, gflags, opflags)) {
+      const int L = lens[i];
+      if (L >= 1) {
+        Philox rng(seed, call, (uint32_t)i);
+        long long d = poisson(rng, p * (double)L);
+        if (kcap > 0 && d > kcap) d = kcap;
+        kk = (int)(d > L ? L : d);
+      }
+    }
+    k[i] = kk;
+  }
+  const int c = __popcll(__ballot(kk > 0));
+  if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    tile_count[blockIdx.x] = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
+    tile_max[blockIdx.x] = 0;
+  }
+}
+
 // One mutation event at nucleotide `ch`: the 0..2 nucleotides it emits (reference
 // rust/mutations.rs:30-60: indel with p_indel, then deletion with p_del, else insertion before ch;
 // otherwise a substitution that may repeat the old nucleotide).
@@ -300,6 +332,26 @@ void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, u
                                                          seed, call, P_<int32_t>(k), kcap,
                                                          gflags ? P_<int>(gflags) : nullptr, P_<int>(opflags));
   MS_LAUNCH_CHECK();
+}
+
+std::pair<int32_t*, int32_t*> select_tiles(long long tiles, hipStream_t s);
+void select_write_i32pos_capped(long long n, uintptr_t src, int32_t* tc, int32_t* tm, int sub, uintptr_t sel,
+                                uintptr_t out_dev, int cap, uintptr_t gflags, uintptr_t opflags, hipStream_t s);
+
+// mut_count over all n genomes + the capped selection of those with events into sel / out_dev (the
+// device pipeline's mutation chain): two launches instead of three (the count pass is fused).
+void mut_count_select(int n, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
+                      uintptr_t gflags, uintptr_t opflags, uintptr_t sel, uintptr_t out_dev, int cap, uintptr_t stream) {
+  if (n <= 0) throw std::invalid_argument("mut_count_select: no genomes");
+  hipStream_t s = S_(stream);
+  constexpr int kSelTile = 4096, kBlock = 256;  // select.hip tile; 16 count blocks per tile
+  const long long blocks = ((long long)n + kSelTile - 1) / kSelTile * (kSelTile / kBlock);
+  auto tiles = select_tiles(blocks, s);
+  mut_count_tiles_kernel<<<(unsigned)blocks, kBlock, 0, s>>>(n, P_<int32_t>(lens), p, seed, call, P_<int32_t>(k), kcap,
+                                                            gflags ? P_<int>(gflags) : nullptr, P_<int>(opflags),
+                                                            tiles.first, tiles.second);
+  MS_LAUNCH_CHECK();
+  select_write_i32pos_capped(n, k, tiles.first, tiles.second, kSelTile / kBlock, sel, out_dev, cap, gflags, opflags, s);
 }
 
 void mut_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t rows, uintptr_t arena, uintptr_t off, uintptr_t lens,

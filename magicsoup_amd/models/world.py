@@ -1112,12 +1112,14 @@ class World:
     def diffuse_molecules(self):
         """One step of diffusion over the molecule map, then membrane permeation."""
         world_ops.diffuse(self)
-        if self.n_cells > 0:  # (adopts a pending division count: the stencil is queued already)
-            world_ops.permeate(self)
         if self.__dict__.get("_deferred"):
             # the stencil is queued: issue the deferred genome chains now, so that they start next to
-            # it on the side stream instead of after the host has reached the next op (~0.1 ms later)
+            # it on the side stream instead of after the host has reached the next op (~0.1 ms later);
+            # before the permeation's launch (molecules only: it commutes with the chains), which would
+            # only delay them
             self._flush_deferred()
+        if self.n_cells > 0:  # (adopts a pending division count: the stencil is queued already)
+            world_ops.permeate(self)
 
     @_op("degrade_molecules")
     def degrade_molecules(self):
