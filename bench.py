@@ -181,7 +181,7 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
 def _prime_rare_paths(chem, device, mdt, genome_size: int) -> None:
     """Setup: run the rarely taken paths once on a small throw-away world -- the host replay after an
     arena widening, the synchronous genetics path, the parameter rebuild after a protein-dimension
-    widening, the rollback of a speculative activity. Their first launches (code-object loading of
+    widening, the rollback of a speculative activity, a genome-pool collection. Their first launches (code-object loading of
     kernels the steady state never uses, first allocations) otherwise land in whichever timed step
     first needs them (15-29 ms steps with a short warm-up)."""
     import magicsoup_amd as ms
@@ -201,6 +201,11 @@ def _prime_rare_paths(chem, device, mdt, genome_size: int) -> None:
     hip_ops.restore_cell_state(w, buf)
     w.enzymatic_activity()
     step(w, 300, genome_size, atp)
+    # a genome-pool collection (dense worlds churn the pool: 256^2 / 40k collects every ~30 steps);
+    # its first call loads the torch kernels it uses (~0.2 s once per process)
+    w._reconcile()
+    torch.cuda.synchronize()
+    w._genomes.collect()
     torch.cuda.synchronize()
     del w
     _CHEMOSTAT.update(divided=0, starved=0, steps=0, after_kill=None)

@@ -67,6 +67,10 @@ for s in "$@"; do case "$s" in
   c1024) run c1024 300 python bench.py --preset c1024 --steps 30 --warmup 5 ;;
   c256) run c256_40k 300 python bench.py --map-size 256 --cells 40000 ;;
   tflag) trace tflag 19 --steps 20 --warmup 20 ;;
+  tc256) trace tc256 19 --map-size 256 --cells 40000 --steps 20 --warmup 20 ;;
+  hs256) MS_NATIVE_TIMES=1 MS_PY_TIMES=1 run host_split_c256 300 python scripts/host_split.py 256 40000 40 ;;
+  hs256c) MS_CPROFILE=1 MS_CPROFILE_SORT=cumulative MS_CPROFILE_N=70 run host_split_c256_cprofile 300 python scripts/host_split.py 256 40000 60 ;;
+  tm1) MARKER=_ZN3msd23diffuse_stencil8_kernel trace tm1 9 --preset m1 --steps 10 --warmup 5 ;;
   tfvirt) MARKER=msd::diffuse_corr_kernel MS_VIRTUAL_STRIPS=1 trace tfvirt 19 --steps 20 --warmup 20 ;;
   hsfv) MS_VIRTUAL_STRIPS=1 MS_NATIVE_TIMES=1 MS_PY_TIMES=1 run host_split_flagship_virtual 300 python scripts/host_split.py 4096 50000 40 ;;
   overlap) run overlap 300 python scripts/overlap_probe.py 4096 50000 20 ;;

@@ -182,7 +182,7 @@ if prof is not None:
 
     prof.disable()
     buf = io.StringIO()
-    pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(45)
+    pstats.Stats(prof, stream=buf).sort_stats(os.environ.get("MS_CPROFILE_SORT", "tottime")).print_stats(int(os.environ.get("MS_CPROFILE_N", "45")))
     print(buf.getvalue())
 tb, tk = sum(busy.values()) / steps * 1e6, sum(blocked.values()) / steps * 1e6
 print(f"{S}^2 / {N}{' virtual' if virtual else ''}: wall {wall:.0f} us/step; inside ops: busy {tb:.0f}, blocked {tk:.0f}; "
