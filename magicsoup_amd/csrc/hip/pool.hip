@@ -101,6 +101,114 @@ __global__ void __launch_bounds__(64) pool_compact_kernel(int nu, const uint8_t*
   }
 }
 
+// ---- collection on the device (PoolArena.collect): no sort, no host loop over genomes.
+// Pool space is in 16-byte granules. Every allocation starts at a granule that some cell's offset
+// names; cells sharing an allocation (a parent and its children) name the same one. mark: per cell,
+// the allocation's size (the longest genome naming it, at least one granule, as pool_alloc) and its
+// owner (the lowest cell index naming it) into per-granule arrays; scan: exclusive prefix sum of the
+// sizes over the granules = the allocations' new offsets, in old-offset order; move: the owner copies
+// the allocation, every cell takes the new offset. The layout equals the one of sorting the distinct
+// offsets and summing their sizes in that order.
+__global__ void __launch_bounds__(256) pool_mark_kernel(int n, const int64_t* off, const int32_t* lens,
+                                                        int32_t* size_g, int32_t* owner_g) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long long g = off[i] >> 4;
+  const int sz = max(1, (max(lens[i], 0) + 15) >> 4);
+  atomicMax(size_g + g, sz);
+  atomicMin(owner_g + g, i);
+}
+
+constexpr int kScanThreads = 256, kScanItems = 4, kScanTile = kScanThreads * kScanItems;
+
+__device__ __forceinline__ long long block_excl_scan(long long v, long long* s_w, long long& total) {
+  // exclusive scan of one value per thread over the block (4 waves of 64)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  long long x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_w[w] = x;
+  __syncthreads();
+  long long base = 0;
+  total = 0;
+  for (int q = 0; q < kScanThreads / 64; ++q) {
+    if (q < w) base += s_w[q];
+    total += s_w[q];
+  }
+  __syncthreads();
+  return base + x - v;
+}
+
+// tile t of the granules: exclusive scan within the tile -> new_g, the tile's total -> tile_sum[t]
+__global__ void __launch_bounds__(kScanThreads) pool_scan_tiles_kernel(long long G, const int32_t* size_g,
+                                                                       int32_t* new_g, long long* tile_sum) {
+  __shared__ long long s_w[kScanThreads / 64];
+  const long long base = (long long)blockIdx.x * kScanTile + (long long)threadIdx.x * kScanItems;
+  int v[kScanItems];
+  long long mine = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    v[j] = base + j < G ? size_g[base + j] : 0;
+    mine += v[j];
+  }
+  long long total;
+  long long pre = block_excl_scan(mine, s_w, total);
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    if (base + j < G) new_g[base + j] = (int32_t)pre;
+    pre += v[j];
+  }
+  if (threadIdx.x == 0) tile_sum[blockIdx.x] = total;
+}
+
+// one block: exclusive scan of the tile totals in place; the grand total (granules) -> *total
+__global__ void __launch_bounds__(kScanThreads) pool_scan_sums_kernel(long long tiles, long long* tile_sum,
+                                                                      long long* total_out) {
+  __shared__ long long s_w[kScanThreads / 64];
+  __shared__ long long s_carry;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (long long b0 = 0; b0 < tiles; b0 += kScanThreads) {
+    const long long t = b0 + threadIdx.x;
+    const long long v = t < tiles ? tile_sum[t] : 0;
+    long long total;
+    const long long pre = block_excl_scan(v, s_w, total);
+    const long long carry = s_carry;
+    if (t < tiles) tile_sum[t] = carry + pre;
+    __syncthreads();
+    if (threadIdx.x == 0) s_carry = carry + total;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total_out = s_carry;
+}
+
+__global__ void __launch_bounds__(kScanThreads) pool_scan_add_kernel(long long G, int32_t* new_g,
+                                                                     const long long* tile_sum) {
+  const long long g = (long long)blockIdx.x * kScanThreads + threadIdx.x;
+  if (g < G) new_g[g] += (int32_t)tile_sum[g / kScanTile];
+}
+
+// one wavefront per cell: the owner of its allocation copies it; every cell takes the new offset
+__global__ void __launch_bounds__(64) pool_move_kernel(int n, int64_t* off, const uint8_t* old_pool,
+                                                       uint8_t* new_pool, const int32_t* size_g,
+                                                       const int32_t* owner_g, const int32_t* new_g) {
+  const int lane = threadIdx.x;
+  for (int c = blockIdx.x; c < n; c += gridDim.x) {
+    const long long g = off[c] >> 4;
+    const long long d = (long long)new_g[g] << 4;
+    if (owner_g[g] == c) {
+      const uint4* s = reinterpret_cast<const uint4*>(old_pool + (g << 4));
+      uint4* t = reinterpret_cast<uint4*>(new_pool + d);
+      const int n16 = size_g[g];
+      for (int q = lane; q < n16; q += 64) t[q] = s[q];
+    }
+    if (lane == 0) off[c] = d;
+  }
+}
+
 static unsigned grid_for(long long k) { return (unsigned)std::max<long long>(1, std::min<long long>(k, 8192)); }
 
 void pool_write(int k, int L_in, uintptr_t rows, uintptr_t lens, uintptr_t dst, long long n0, uintptr_t pool,
@@ -141,6 +249,41 @@ void pool_compact(int nu, uintptr_t old_pool, uintptr_t old_off, uintptr_t sizes
   MS_LAUNCH_CHECK();
 }
 
+// Phase 1 of a collection over the G granules below the pool's top: sizes / owners per granule and
+// their exclusive scan; the total (granules) -> total_out (device int64). size_g, owner_g, new_g:
+// int32[G]; tile_sum: int64[ceil(G / 1024)].
+void pool_collect_plan(int n, uintptr_t off, uintptr_t lens, long long G, uintptr_t size_g, uintptr_t owner_g,
+                       uintptr_t new_g, uintptr_t tile_sum, uintptr_t total_out, uintptr_t stream) {
+  if (n <= 0 || G <= 0) throw std::invalid_argument("pool_collect_plan: empty pool");
+  if (G >= (1ll << 31)) throw std::invalid_argument("pool_collect_plan: pool too large for int32 granule offsets");
+  hipStream_t s = S_(stream);
+  MS_HIP_CHECK(hipMemsetAsync(P_<int32_t>(size_g), 0, (size_t)G * 4, s));
+  MS_HIP_CHECK(hipMemsetAsync(P_<int32_t>(owner_g), 0x7F, (size_t)G * 4, s));
+  pool_mark_kernel<<<cdiv(n, 256), 256, 0, s>>>(n, P_<int64_t>(off), P_<int32_t>(lens), P_<int32_t>(size_g),
+                                                P_<int32_t>(owner_g));
+  MS_LAUNCH_CHECK();
+  const long long tiles = (G + kScanTile - 1) / kScanTile;
+  pool_scan_tiles_kernel<<<(unsigned)tiles, kScanThreads, 0, s>>>(G, P_<int32_t>(size_g), P_<int32_t>(new_g),
+                                                                  P_<long long>(tile_sum));
+  MS_LAUNCH_CHECK();
+  pool_scan_sums_kernel<<<1, kScanThreads, 0, s>>>(tiles, P_<long long>(tile_sum), P_<long long>(total_out));
+  MS_LAUNCH_CHECK();
+  pool_scan_add_kernel<<<(unsigned)cdiv(G, kScanThreads), kScanThreads, 0, s>>>(G, P_<int32_t>(new_g),
+                                                                                P_<long long>(tile_sum));
+  MS_LAUNCH_CHECK();
+}
+
+// Phase 2: copy every allocation into new_pool (sized for the total) and remap the offsets.
+void pool_collect_move(int n, uintptr_t off, uintptr_t old_pool, uintptr_t new_pool, uintptr_t size_g,
+                       uintptr_t owner_g, uintptr_t new_g, uintptr_t stream) {
+  if (n <= 0) return;
+  if ((old_pool | new_pool) & 15) throw std::invalid_argument("pool_collect_move: pools must be 16-byte aligned");
+  pool_move_kernel<<<grid_for(n), 64, 0, S_(stream)>>>(n, P_<int64_t>(off), P_<uint8_t>(old_pool),
+                                                       P_<uint8_t>(new_pool), P_<int32_t>(size_g),
+                                                       P_<int32_t>(owner_g), P_<int32_t>(new_g));
+  MS_LAUNCH_CHECK();
+}
+
 void bind_pool(pybind11::module_& m) {
   namespace py = pybind11;
   py::class_<GenomePoolArgs>(m, "GenomePoolArgs", py::module_local())
@@ -153,7 +296,9 @@ void bind_pool(pybind11::module_& m) {
   m.def("pool_write", &pool_write, "genome rows (k, L) -> new pool allocations of cells dst[j] (or n0 + j)");
   m.def("pool_read", &pool_read, "genomes of cells -> zero-padded rows (k, W)");
   m.def("pool_read_packed", &pool_read_packed, "genomes of cells back to back (no padding)");
-  m.def("pool_compact", &pool_compact, "copy unique genomes into a new pool (PoolArena.collect)");
+  m.def("pool_compact", &pool_compact, "copy unique genomes into a new pool");
+  m.def("pool_collect_plan", &pool_collect_plan, "collection phase 1: per-granule sizes / owners and their scan");
+  m.def("pool_collect_move", &pool_collect_move, "collection phase 2: copy the allocations, remap the offsets");
 }
 
 }  // namespace msd

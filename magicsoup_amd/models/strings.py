@@ -294,7 +294,7 @@ class PoolArena:
 
     def collect(self, extra: int = 0) -> None:
         """Move the referenced genomes into a fresh pool (each distinct genome once, in offset order)
-        with room for ``extra`` more bytes; unreferenced space is dropped. One synchronisation."""
+        with room for ``extra`` more bytes; unreferenced space is dropped. Two synchronisations (the top, the new total)."""
         from magicsoup_amd.ops import native
         from magicsoup_amd.ops.hip_ops import _stream
 
@@ -304,20 +304,28 @@ class PoolArena:
             self.top.zero_()
             self.top_ub = 0
             return
-        off, lens = self.off[:n], self.lens[:n]
-        uo, inv = torch.unique(off, return_inverse=True)
-        size_u = torch.zeros_like(uo)
-        # bytes per allocation (16-byte granules, at least one: pool_alloc); the longest genome per
-        # offset (cells sharing an allocation have one length, the reduction only guards that)
-        size_u.scatter_reduce_(0, inv, ((lens.to(torch.int64).clamp(min=1) + 15) // 16) * 16, reduce="amax")
-        new_u = torch.cumsum(size_u, 0) - size_u
-        total = int((new_u[-1] + size_u[-1]).item())
+        # on the device (pool.hip pool_collect_plan / _move): per 16-byte granule below the top, the
+        # size of the allocation starting there (the longest genome naming it, at least one granule,
+        # as pool_alloc) and its owner cell, a scan of the sizes (the new offsets, in old-offset
+        # order), then the owners copy and every cell takes its new offset
+        m = native.hip()
+        st = _stream()
+        G = max(1, (int(self.top.item()) + 15) // 16)
+        dev = self.device
+        size_g = torch.empty(G, dtype=torch.int32, device=dev)
+        owner_g = torch.empty(G, dtype=torch.int32, device=dev)
+        new_g = torch.empty(G, dtype=torch.int32, device=dev)
+        tile_sum = torch.empty((G + 1023) // 1024, dtype=torch.int64, device=dev)
+        total_g = torch.empty(1, dtype=torch.int64, device=dev)
+        m.pool_collect_plan(n, self.off.data_ptr(), self.lens.data_ptr(), G, size_g.data_ptr(), owner_g.data_ptr(),
+                            new_g.data_ptr(), tile_sum.data_ptr(), total_g.data_ptr(), st)
+        total = 16 * int(total_g.item())
         cap = max(_POOL_MIN, 2 * (total + _r16(extra)))
-        new = torch.empty(cap, dtype=torch.uint8, device=self.device)
-        native.hip().pool_compact(int(uo.numel()), self.data.data_ptr(), uo.data_ptr(), size_u.data_ptr(),
-                                  new.data_ptr(), new_u.data_ptr(), _stream())
-        self.off[:n] = new_u[inv]
-        _retire(self.data)
+        new = torch.empty(cap, dtype=torch.uint8, device=dev)
+        m.pool_collect_move(n, self.off.data_ptr(), self.data.data_ptr(), new.data_ptr(), size_g.data_ptr(),
+                            owner_g.data_ptr(), new_g.data_ptr(), st)
+        for t in (self.data, size_g, owner_g, new_g):
+            _retire(t)
         self.data = new
         self.top.fill_(total)
         self.top_ub = total

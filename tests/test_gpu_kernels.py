@@ -1196,3 +1196,30 @@ def test_memory_model_matches_a_live_world():
     alloc = torch.cuda.memory_allocated() - base
     assert 0.75 * held <= model <= 1.25 * held, (model, held)
     assert held <= alloc * 1.05, (held, alloc)
+
+
+def test_genome_pool_collect_layout_matches_sorted_reference():
+    """The device collection (pool.hip pool_collect_plan / _move: per-granule sizes and owners, a
+    scan, owner copies) lays the pool out exactly as sorting the distinct offsets and summing their
+    allocation sizes in that order (plain torch, below), and keeps every genome's bytes."""
+    w = _world("cuda", map_size=96, n=1500, s=400)
+    g = w._genomes
+    for _ in range(3):
+        w.divide_cells_t(torch.arange(0, w.n_cells, 3, device="cuda"))
+        w.mutate_cells(p=1e-3)
+        w.recombinate_cells(p=1e-5)
+        w.kill_cells(torch.arange(0, w.n_cells, 5, device="cuda"))
+    w._reconcile()
+    torch.cuda.synchronize()
+    n = g.n
+    off, lens = g.off[:n].clone(), g.lens[:n].clone()
+    uo, inv = torch.unique(off, return_inverse=True)
+    size_u = torch.zeros_like(uo)
+    size_u.scatter_reduce_(0, inv, ((lens.to(torch.int64).clamp(min=1) + 15) // 16) * 16, reduce="amax")
+    want = (torch.cumsum(size_u, 0) - size_u)[inv]
+    before = list(w.cell_genomes)
+    g.collect()
+    assert torch.equal(g.off[:n], want)
+    assert int(g.top.item()) == int(size_u.sum())
+    assert list(w.cell_genomes) == before
+    g.check()
