@@ -26,6 +26,7 @@ Presets (BASELINE.json's other configs; explicit flags override a preset's value
 from __future__ import annotations
 
 import argparse
+import contextlib
 import gc
 import json
 import math
@@ -113,11 +114,12 @@ def _dilution_mask(n: int, k: int, device) -> torch.Tensor:
     return torch.rand(n, device=device) < (k / n)
 
 
+_NULL = contextlib.nullcontext()
+
+
 def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=None):
     def ph(name):
-        import contextlib
-
-        return timer.phase(name) if timer is not None else contextlib.nullcontext()
+        return timer.phase(name) if timer is not None else _NULL
 
     def note(key, val):
         if stats is not None:
