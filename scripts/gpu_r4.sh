@@ -70,6 +70,9 @@ for s in "$@"; do case "$s" in
   tc256) trace tc256 19 --map-size 256 --cells 40000 --steps 20 --warmup 20 ;;
   hs256) MS_NATIVE_TIMES=1 MS_PY_TIMES=1 run host_split_c256 300 python scripts/host_split.py 256 40000 40 ;;
   hs256c) MS_CPROFILE=1 MS_CPROFILE_SORT=cumulative MS_CPROFILE_N=70 run host_split_c256_cprofile 300 python scripts/host_split.py 256 40000 60 ;;
+  twide) trace twide 19 --preset wide --steps 20 --warmup 20 ;;
+  tlong) trace tlong 19 --steps 420 --warmup 20 ;;
+  long500) run long500 600 python bench.py --steps 500 --warmup 20 --step-times ;;
   tm1) MARKER=_ZN3msd23diffuse_stencil8_kernel trace tm1 9 --preset m1 --steps 10 --warmup 5 ;;
   tfvirt) MARKER=msd::diffuse_corr_kernel MS_VIRTUAL_STRIPS=1 trace tfvirt 19 --steps 20 --warmup 20 ;;
   hsfv) MS_VIRTUAL_STRIPS=1 MS_NATIVE_TIMES=1 MS_PY_TIMES=1 run host_split_flagship_virtual 300 python scripts/host_split.py 4096 50000 40 ;;
