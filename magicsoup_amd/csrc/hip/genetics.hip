@@ -288,7 +288,12 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   }
 }
 
-constexpr int kLdsMaxLen = 1024;  // genomes up to this length use LDS slots
+// genomes up to this length use LDS slots (24 B per nt and strand pair: 2048 nt = 49 KB, one wave per
+// workgroup, three workgroups per CU); longer ones go to the global-slot pass. At 1024 the genomes
+// of a long flagship run (lengths grow past 1024 after a few hundred steps) took the global pass,
+// 100 us per chain under the diffusion stencil (profiles/r4/s17/tlong_steps.txt)
+constexpr int kLdsMaxLen = 2048;
+int translate_lds_max() { return kLdsMaxLen; }
 
 // mode: 0 count pass, 1 write pass, 2 fused (counts and tokens; the caller checks the counts
 // against P / D afterwards)

@@ -43,6 +43,7 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
                   uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
                   uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t W, uintptr_t Q, uintptr_t overflow,
                   uintptr_t dn, uintptr_t stream);
+int translate_lds_max();  // genetics.hip: the longest genome of the LDS translation pass
 void mut_count_select(int n, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
                       uintptr_t gflags, uintptr_t opflags, uintptr_t sel, uintptr_t out_dev, int cap, uintptr_t stream);
 void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
@@ -186,7 +187,7 @@ int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const Gp
   MS_LAUNCH_CHECK();
   translate_fused(cap, cells, a.data, a.off, a.width, a.lens, g.small, g.dom_type, g.dt_entries, g.two_codon, g.dom_size,
                   g.dom_type_size, counts, ndom, k.P, dcap, tokens, long_list, long_count, dcnt, st);
-  if (a.width > 1024)  // genomes longer than the LDS slots: second pass over the queued ones
+  if (a.width > translate_lds_max())  // genomes longer than the LDS slots: second pass over the queued ones
     translate_fused_long(lcap, cells, a.data, a.off, a.width, a.lens, g.small, g.dom_type, g.dt_entries, g.two_codon,
                          g.dom_size, g.dom_type_size, counts, ndom, k.P, dcap, tokens, long_list, gslot, long_count,
                          st);

@@ -854,7 +854,7 @@ def translate(genetics, arena, rows: torch.Tensor):
     """Two-pass device translation of the genomes of cells ``rows`` (a GPU genome pool,
     models/strings.py PoolArena) -> (tokens (k, P, D, 5), n_prots (k,)).
 
-    Genomes up to 1024 nt are translated from LDS slots; longer ones are queued by the count pass
+    Genomes up to 2048 nt are translated from LDS slots; longer ones are queued by the count pass
     and translated in a second launch with global-memory slots (only when there are any)."""
     data, lens, off = arena.data, arena.lens, arena.off
     dev = data.device

@@ -28,9 +28,9 @@ def test_extension_is_gfx950():
 
 def test_translation_matches_host():
     genetics = ms.Genetics()
-    # short genomes use LDS slots, the long ones (> 1024 nt) the global-slot pass
+    # short genomes use LDS slots, the long ones (> 2048 nt) the global-slot pass
     genomes = gen_genomes(500, 800) + ["", "ATG", ms.random_genome(30), ms.random_genome(3000), ms.random_genome(9000)]
-    genomes += gen_genomes(50, 1100)
+    genomes += gen_genomes(50, 1100) + gen_genomes(20, 2000)
     from magicsoup_amd.models.strings import pack_strings
 
     arr, lens = pack_strings(genomes)
