@@ -31,6 +31,7 @@ for s in "$@"; do case "$s" in
   tests) run tests 1000 python -u -m pytest tests -m gpu -q --maxfail 5 --timeout 120 --timeout-method thread ;;
   smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   flagship) run flagship 300 python bench.py ;;
+  flagship2) run flagship2 300 python bench.py ;;
   drv) run drv 300 python bench.py --steps 20 --warmup 5 ;;
   proxy) run proxy8_plain 300 python bench.py --map-size 1448 --cells 6250 ;;
   virt) MS_VIRTUAL_STRIPS=1 run proxy8_virtual 300 python bench.py --map-size 1448 --cells 6250 ;;
