@@ -77,6 +77,9 @@ for s in "$@"; do case "$s" in
   tm1) MARKER=_ZN3msd23diffuse_stencil8_kernel trace tm1 9 --preset m1 --steps 10 --warmup 5 ;;
   tfvirt) MARKER=msd::diffuse_corr_kernel MS_VIRTUAL_STRIPS=1 trace tfvirt 19 --steps 20 --warmup 20 ;;
   hsfv) MS_VIRTUAL_STRIPS=1 MS_NATIVE_TIMES=1 MS_PY_TIMES=1 run host_split_flagship_virtual 300 python scripts/host_split.py 4096 50000 40 ;;
+  tpx) trace tpx 19 --map-size 1448 --cells 6250 --steps 20 --warmup 20 ;;
+  tpxv) MARKER=msd::diffuse_corr_kernel MS_VIRTUAL_STRIPS=1 trace tpxv 19 --map-size 1448 --cells 6250 --steps 20 --warmup 20 ;;
+
   overlap) run overlap 300 python scripts/overlap_probe.py 4096 50000 20 ;;
   *) echo "unknown step $s" ;;
 esac; done
