@@ -350,18 +350,21 @@ int gp_rebuild(const GpArena& a, const GpGen& g, const GpKin& k, uintptr_t cells
 // stream, which is what the next activity waits for.
 
 // union list: recombined cells, then mutated ones (a cell in both is built twice into two fresh rows
-// from the same final genome; either row is right) + the parts' status {pairs, rec flags, mutated,
-// mut flags} into a pinned slot
+// from the same final genome; either row is right), then the cells [arr0, arr0 + narr) (a strip's
+// arrivals of the division before, whose parameters are built here instead of by a rebuild chain of
+// their own) + the parts' status {pairs, rec flags, mutated, mut flags} into a pinned slot
 __global__ void __launch_bounds__(256) gp_union_kernel(int ucap, int mcap, const int* rec_cnt, const int64_t* rec_cells,
-                                                       const int* mut_cnt, const int64_t* mut_sel, int64_t* cells,
-                                                       int* cnt_u, const int* rec_pairs, const int* rec_opflags,
-                                                       const int* mut_opflags, long long* parts_status) {
+                                                       const int* mut_cnt, const int64_t* mut_sel, long long arr0,
+                                                       int narr, int64_t* cells, int* cnt_u, const int* rec_pairs,
+                                                       const int* rec_opflags, const int* mut_opflags,
+                                                       long long* parts_status) {
   const int cr = *rec_cnt, cm = min(*mut_cnt, mcap);
-  const int nr = min(cr, ucap), nm = min(cm, ucap - nr);
+  const int nr = min(cr, ucap - narr), nm = min(cm, ucap - narr - nr);
   for (int j = threadIdx.x; j < nr; j += blockDim.x) cells[j] = rec_cells[j];
   for (int j = threadIdx.x; j < nm; j += blockDim.x) cells[nr + j] = mut_sel[j];
+  for (int j = threadIdx.x; j < narr; j += blockDim.x) cells[nr + nm + j] = arr0 + j;
   if (threadIdx.x == 0) {
-    cnt_u[0] = nr + nm;
+    cnt_u[0] = nr + nm + narr;
     parts_status[0] = *rec_pairs;
     parts_status[1] = __hip_atomic_load(rec_opflags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     parts_status[2] = *mut_cnt;
@@ -389,15 +392,18 @@ size_t gp_evolve_union_bytes(int ucap, int P, int dcap, int L) {
 // ar / am / au: the recombination's, the mutation's and the union rebuild's counters (the arena
 // fields are the same in all three). `extra` / `nres`: strip-boundary recombination results of a
 // decomposed world, appended after the local pairs' results (as in gp_recombine; the parts status
-// then counts result rows instead of pairs). Returns (union status slot {count, flags, row counter,
-// count}, parts status slot {pairs or result rows, rec flags, mutated, mut flags}).
+// then counts result rows instead of pairs). `arr0` / `narr`: cells whose parameters are built with
+// the union (a strip's arrivals, magicsoup_amd/parallel/dist_world.py _divide_phase_b). Returns
+// (union status slot {count, flags, row counter, count}, parts status slot {pairs or result rows, rec
+// flags, mutated, mut flags}).
 std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpArena& au, const GpGen& g, const GpKin& k,
                               uintptr_t keys, py::object nbr, double p_rec, uint64_t seed_r, uint64_t call_r, int pcap,
                               double p, double p_indel, double p_del, uint64_t seed_m, uint64_t call_m, int mcap,
                               int kcap, int dcap, uintptr_t mark, uint64_t gen, uintptr_t blob_r, uintptr_t blob_m,
                               uintptr_t blob_u, bool fresh, long long nrows, py::object extra, uintptr_t nres,
-                              uintptr_t stream) {
+                              long long arr0, int narr, uintptr_t stream) {
   hipStream_t s = S_(stream);
+  if (narr < 0) throw std::invalid_argument("gp_evolve: negative arrival count");
   const int n = ar.n, L = ar.width;
   const int xr = extra.is_none() ? 0 : extra.attr("rows").cast<int>();
   if (xr && !nres) throw std::invalid_argument("gp_evolve: boundary rows need the result-row counter");
@@ -434,12 +440,13 @@ std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpAren
                 0, am.gflags, am.opflags,
                 stream);
   // union of the changed cells -> one translation + build
-  const int ucap = nr + mcap;
+  const int ucap = nr + mcap + narr;
   Carve cu(blob_u);
   const uintptr_t ucells = cu.take(8 * (size_t)ucap), ucnt = cu.take(16);
   auto ps = status_slot();
   gp_union_kernel<<<1, 256, 0, s>>>(ucap, mcap, P_<int>(ar.cnt2), P_<int64_t>(cells), P_<int>(am.cnt),
-                                    P_<int64_t>(msel), P_<int64_t>(ucells), P_<int>(ucnt), P_<int>(xr ? nres : ar.cnt),
+                                    P_<int64_t>(msel), arr0, narr, P_<int64_t>(ucells), P_<int>(ucnt),
+                                    P_<int>(xr ? nres : ar.cnt),
                                     P_<int>(ar.opflags), P_<int>(am.opflags), ps.first);
   MS_LAUNCH_CHECK();
   const int slot_u = rebuild(ucap, ucells, ucnt, au, g, k, dcap, cu, ucnt, s);

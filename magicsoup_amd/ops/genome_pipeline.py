@@ -354,13 +354,15 @@ class _PartHost:
         return {0: self.parts[2], 1: self.parts[3], 2: 0, 3: self.parts[2]}[i]
 
 
-def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=None) -> bool:
+def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=None, arrivals=None) -> bool:
     """``recombinate_cells(p=p_rec)`` followed by ``mutate_cells(p, p_indel, p_del)`` over all cells
     as ONE device chain (gp.hip gp_evolve): both are applied and committed in order, then the union
     of the changed cells is translated and built once -- the same genomes and parameters as the two
     calls one after the other, with one translation + build less on the side stream. ``extra``: a
-    decomposed world's strip-boundary recombination (as for :func:`recombinate_all`). False if either
-    call should take its own path (rates above the pipeline's usage rule, too few cells)."""
+    decomposed world's strip-boundary recombination (as for :func:`recombinate_all`). ``arrivals``:
+    ``(first, count)``, cells whose parameters are built with the union (instead of by a
+    :func:`rebuild_rows` chain of their own; at most ``N_CAP``). False if either call should take its
+    own path (rates above the pipeline's usage rule, too few cells)."""
     arena = world._genomes
     n = world.n_cells
     if n < 2:
@@ -377,9 +379,10 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
     pcap = _cap(exp_rec, min(n, N_CAP) // 2)
     mcap = _cap(n * p * L, min(n, N_CAP))
     kin = world.kinetics
+    arr0, narr = (0, 0) if arrivals is None else (int(arrivals[0]), int(arrivals[1]))
     fresh = not st["pending"]
     if fresh:
-        kin._reserve_rows(2 * min(n, N_CAP))
+        kin._reserve_rows(2 * min(n, N_CAP) + narr)
     xr = 0 if extra is None else int(extra.rows)
     _room(world, (2 * pcap + xr) * _r16(2 * L) + mcap * _r16(L + K_CAP))
     br, bm, bu = _bufs(world, "rec"), _bufs(world, "mut"), _bufs(world, "evo")
@@ -390,7 +393,7 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
     blob_r = _blob(world, "rec", _m().gp_blob_bytes(1, n, pcap, k.P, L, D_CAP, K_CAP, xr), dev)
     blob_m = _blob(world, "mut", _m().gp_blob_bytes(0, n, mcap, k.P, L, D_CAP, K_CAP, 0), dev)
     nres = sc.get("gp_nres", 1, torch.int32, dev) if extra is not None else None
-    ucap = 2 * pcap + xr + mcap
+    ucap = 2 * pcap + xr + mcap + narr
     blob_u = _blob(world, "evo", _m().gp_evolve_union_bytes(ucap, k.P, D_CAP, L), dev)
     mark = sc.bufs.get("arena_mark")
     if mark is None or mark.numel() < arena.n:
@@ -401,7 +404,7 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
     slot_u, slot_p = _m().gp_evolve(ar, am, au, _gen_desc(world, dev), k, _p(keys), nbr, float(p_rec), rng_r[0],
                                     rng_r[1], pcap, float(p), float(p_indel), float(p_del), rng_m[0], rng_m[1], mcap,
                                     K_CAP, D_CAP, _p(mark), int(gen), _p(blob_r), _p(blob_m), _p(blob_u), fresh,
-                                    int(kin.__dict__["_nrows"]), extra, _p(nres), _stream())
+                                    int(kin.__dict__["_nrows"]), extra, _p(nres), arr0, narr, _stream())
     lay_r = _m().gp_layout(1, n, pcap, L, K_CAP, xr)
     lay_m = _m().gp_layout(0, n, mcap, L, K_CAP, 0)
     parts = _StatusSlot(slot_p)

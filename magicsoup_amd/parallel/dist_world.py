@@ -95,6 +95,8 @@ def _copy_maps(dst: World, src: World) -> None:
 # issue the boundary recombination's collective part at the recombinate_cells() call (MS_XB_EARLY=0:
 # at the flush after the diffusion stencil, as before)
 _XB_EARLY = os.environ.get("MS_XB_EARLY", "1") != "0"
+# a lazy division's arrivals are built by the queued genome chain that follows (_divide_phase_b)
+_ARRIVALS_MERGE = True
 
 
 class DistributedWorld(World):
@@ -580,10 +582,13 @@ class DistributedWorld(World):
         hip_ops.guarded_sync()  # (peer failures raise instead of hanging the read-back)
         return self._divide_phase_b(n0, lw, gw)
 
-    def _divide_phase_b(self, n0: int, lw: int, gw: int) -> tuple[torch.Tensor, torch.Tensor]:
+    def _divide_phase_b(self, n0: int, lw: int, gw: int, defer_arrivals: bool = False
+                        ) -> tuple[torch.Tensor, torch.Tensor]:
         """Phase B of :meth:`_divide_mask_native` once phase A's counts are on the host (its pinned
         status copy is complete): records out, children in, arrivals appended and their parameter
-        rows rebuilt on the device."""
+        rows rebuilt on the device -- or, with ``defer_arrivals`` (a queued recombinate_cells() +
+        mutate_cells() pair follows), built by that pair's device chain with the cells it changed
+        (``_arrivals``, consumed by :meth:`_evolve`; one translation + build less per step)."""
         from magicsoup_amd.ops import genome_pipeline, hip_ops
         from magicsoup_amd.ops.hip_ops import _m, _p, _scratch, _stream
 
@@ -620,9 +625,12 @@ class DistributedWorld(World):
                                 hdr_dn[2], _p(zero_row), _stream())
         self._adopt_count(n_new)
         if k_in:
-            new = torch.arange(n0 + n_loc, n_new, device=self.device)
-            if not genome_pipeline.rebuild_rows(self, new):
-                self._update_params_rows(new)
+            d = self.__dict__
+            if (defer_arrivals and d.get("_arrivals") is None and k_in <= genome_pipeline.N_CAP
+                    and genome_pipeline.enabled(self) and self.kinetics._P() > 0):
+                d["_arrivals"] = (n0 + n_loc, k_in)
+            else:
+                self._rebuild_arrivals((n0 + n_loc, k_in))
         mig = self.migrated
         mig["divided_out"] += n_up + n_dn
         mig["divided_in"] += k_in
@@ -649,8 +657,10 @@ class DistributedWorld(World):
         # them against the state before phase B
         queued = d.get("_deferred")
         d["_deferred"] = []
+        pair = (_ARRIVALS_MERGE and queued is not None and len(queued) >= 2 and getattr(queued[0], "kind", None) == "rec"
+                and getattr(queued[1], "kind", None) == "mut")
         try:
-            self._divide_phase_b(n0, lw, gw)
+            self._divide_phase_b(n0, lw, gw, defer_arrivals=pair)
         finally:
             if queued:
                 from magicsoup_amd.ops.streams import NEvent
@@ -815,10 +825,27 @@ class DistributedWorld(World):
         if pre is None:
             self.__dict__["_xcall"] += 1
         x = pre if pre is not None else _BoundaryRecombination(self, p, K_CAP)
-        if self.n_cells >= 2 and genome_pipeline.evolve(self, p, *mut.args, extra=x):
+        arr = self.__dict__.pop("_arrivals", None)
+        if self.n_cells >= 2 and genome_pipeline.evolve(self, p, *mut.args, extra=x, arrivals=arr):
             return 2
+        if arr is not None:
+            self._rebuild_arrivals(arr)
         self._recombinate_gpu(p, x)
         return 1
+
+    def _rebuild_arrivals(self, arr: tuple[int, int]) -> None:
+        """Parameter rows of the cells [first, first + count) (a division's arrivals)."""
+        from magicsoup_amd.ops import genome_pipeline
+
+        new = torch.arange(arr[0], arr[0] + arr[1], device=self.device)
+        if not genome_pipeline.rebuild_rows(self, new):
+            self._update_params_rows(new)
+
+    def _flush_deferred(self) -> None:
+        super()._flush_deferred()
+        arr = self.__dict__.pop("_arrivals", None)
+        if arr is not None:  # (the pair was not issued as one chain: e.g. fewer than 2 cells)
+            self._rebuild_arrivals(arr)
 
     def _recombinate_strips_all(self, p: float, pre: "_BoundaryRecombination | None" = None) -> None:
         if pre is None:
