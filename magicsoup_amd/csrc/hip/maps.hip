@@ -430,6 +430,36 @@ __global__ void __launch_bounds__(256) diffuse_reduce_kernel(const double* parti
   }
 }
 
+// diffuse_reduce_kernel over a strip's three stencil launches at once (diffuse_strip): the interior
+// rows' partials (`ti` tiles per molecule) and the two boundary rows' (`gx` tiles per molecule each,
+// launch b at offset b * gx * m); totals overwritten
+__global__ void __launch_bounds__(256) diffuse_reduce_strip_kernel(const double* pi, int ti, const double* pb, int gx,
+                                                                   int m, double* totals) {
+  __shared__ double sb[4], sa[4];
+  const int mol = blockIdx.x;
+  double b = 0.0, a = 0.0;
+  for (int t = threadIdx.x; t < ti; t += blockDim.x) {
+    b += pi[((size_t)mol * ti + t) * 2];
+    a += pi[((size_t)mol * ti + t) * 2 + 1];
+  }
+  for (int t = threadIdx.x; t < 2 * gx; t += blockDim.x) {
+    const double* p = pb + (size_t)(t / gx) * gx * m * 2 + ((size_t)mol * gx + t % gx) * 2;
+    b += p[0];
+    a += p[1];
+  }
+  b = wave_sum_d(b);
+  a = wave_sum_d(a);
+  if ((threadIdx.x & 63) == 0) {
+    sb[threadIdx.x >> 6] = b;
+    sa[threadIdx.x >> 6] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    totals[2 * mol] = sb[0] + sb[1] + sb[2] + sb[3];
+    totals[2 * mol + 1] = sa[0] + sa[1] + sa[2] + sa[3];
+  }
+}
+
 // Deferred correction: instead of a second full pass map = max(tmp + (before - after) / n_pix, 0),
 // only the per-species constant is computed; the stencil output becomes the map (buffer swap) with
 // the constant pending, and every later reader applies max(raw + corr, 0) (corr_in) -- the next
@@ -623,12 +653,10 @@ size_t diffuse_partials_len(int m, int C, int H) {
   return std::max(v8, std::max(v4, v1));
 }
 
-void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
-                     uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t totals, int dtype,
-                     int accumulate, uintptr_t stream, uintptr_t corr_out, double n_pix) {
-  // rows [r_lo, r_hi) of the map; `accumulate`: add this launch's mass totals to `totals` (a strip's
-  // stencil split into interior rows, issued while the halo rows are exchanged, and boundary rows)
-  if (m <= 0 || r_hi <= r_lo) return;
+// the stencil launch of diffuse_stencil (partials per tile, no reduce); returns the tiles per molecule
+static int stencil_launch(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp,
+                          uintptr_t wa, uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, int dtype,
+                          uintptr_t stream) {
   const MGeom g = mgeom(R, C, r_lo, r_hi, wrap);
   hipStream_t st_ = S_(stream);
   const int H = r_hi - r_lo;
@@ -657,18 +685,28 @@ void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_
                                corr ? P_<float>(corr) : nullptr, g, P_<double>(partials))));
   }
   MS_LAUNCH_CHECK();
-  diffuse_reduce_kernel<<<m, 256, 0, st_>>>(P_<double>(partials), (int)(grid.x * grid.y), P_<double>(totals),
-                                            accumulate != 0, corr_out ? P_<float>(corr_out) : nullptr, n_pix);
+  return (int)(grid.x * grid.y);
+}
+
+void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
+                     uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t totals, int dtype,
+                     int accumulate, uintptr_t stream, uintptr_t corr_out, double n_pix) {
+  // rows [r_lo, r_hi) of the map; `accumulate`: add this launch's mass totals to `totals` (a strip's
+  // stencil split into interior rows, issued while the halo rows are exchanged, and boundary rows)
+  if (m <= 0 || r_hi <= r_lo) return;
+  const int tiles = stencil_launch(m, R, C, r_lo, r_hi, wrap, map, tmp, wa, wb, scale, corr, partials, dtype, stream);
+  diffuse_reduce_kernel<<<m, 256, 0, S_(stream)>>>(P_<double>(partials), tiles, P_<double>(totals), accumulate != 0,
+                                                   corr_out ? P_<float>(corr_out) : nullptr, n_pix);
   MS_LAUNCH_CHECK();
 }
 
 // The two boundary rows r_lo and r_hi - 1 of a strip (after its halo rows arrived; the interior rows
 // r_lo + 1 .. r_hi - 2 were computed by a diffuse_stencil launch issued before the exchange): one
 // single-row stencil launch each, partials side by side, one reduce adding to `totals`.
-void diffuse_boundary(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t wa,
-                      uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t totals, int dtype,
-                      uintptr_t stream) {
-  if (m <= 0 || r_hi - r_lo < 2) throw std::invalid_argument("diffuse_boundary: a strip of at least 2 rows");
+// the two single-row launches of diffuse_boundary; returns the tiles per molecule and launch
+static int boundary_launch(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t wa,
+                           uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, int dtype,
+                           uintptr_t stream) {
   hipStream_t st_ = S_(stream);
   const bool v8 = use_vec8(C, dtype), v4 = !v8 && use_vec4(C);
   const int gx = v8 ? cdiv(C, 512) : v4 ? cdiv(C, 256) : cdiv(C, 64 * kWaves);
@@ -692,6 +730,16 @@ void diffuse_boundary(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, ui
     }
     MS_LAUNCH_CHECK();
   }
+  return gx;
+}
+
+void diffuse_boundary(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t wa,
+                      uintptr_t wb, uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t totals, int dtype,
+                      uintptr_t stream) {
+  if (m <= 0 || r_hi - r_lo < 2) throw std::invalid_argument("diffuse_boundary: a strip of at least 2 rows");
+  hipStream_t st_ = S_(stream);
+  const int gx = boundary_launch(m, R, C, r_lo, r_hi, map, tmp, wa, wb, scale, corr, partials, dtype, stream);
+  const int tiles = gx * m;
   // partials of both launches: (mol, tile) pairs, launch b at offset b * tiles; reduce them as one
   // (2 * gx)-tile layout per molecule requires mol-major order, so reduce each launch and accumulate
   diffuse_reduce_kernel<<<m, 256, 0, st_>>>(P_<double>(partials), gx, P_<double>(totals), true);
@@ -713,8 +761,8 @@ void diffuse_corr(int m, uintptr_t totals, double n_pix, uintptr_t corr, uintptr
 
 // One diffusion step of a strip of a decomposed world over the native RCCL communicator, in one call:
 // the halo rows travel on `halo_stream` (pack, exchange, unpack) while the interior rows' stencil runs
-// on `stream`; then the two boundary rows, the all-reduce (SUM) of the mass totals and the new
-// correction. Same kernels and order as ops/hip_ops.py diffuse (split path).
+// on `stream`; then the two boundary rows, one reduce of the three launches' partials, the all-reduce
+// (SUM) of the mass totals and the new correction. Same kernels as ops/hip_ops.py diffuse (split path).
 void diffuse_strip(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t wa, uintptr_t wb,
                    uintptr_t scale, uintptr_t corr, uintptr_t partials, uintptr_t partials_b, uintptr_t totals,
                    uintptr_t new_corr, double n_pix, int dtype, uintptr_t comm, int up, int down, uintptr_t halo_bufs,
@@ -729,10 +777,12 @@ void diffuse_strip(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintp
   halo_pack(m, C, H, elem, map, s_up, s_dn, halo_stream);
   rccl_exchange(comm, up, down, s_up, plane_b, s_dn, plane_b, r_dn, plane_b, r_up, plane_b, halo_stream);
   halo_unpack(m, C, H, elem, map, r_up, r_dn, halo_stream);
-  diffuse_stencil(m, R, C, r_lo + 1, r_hi - 1, 0, map, tmp, wa, wb, scale, corr, partials, totals, dtype, 0, stream, 0,
-                  1.0);
+  const int ti = stencil_launch(m, R, C, r_lo + 1, r_hi - 1, 0, map, tmp, wa, wb, scale, corr, partials, dtype, stream);
   stream_join(stream, halo_stream);
-  diffuse_boundary(m, R, C, r_lo, r_hi, map, tmp, wa, wb, scale, corr, partials_b, totals, dtype, stream);
+  const int gx = boundary_launch(m, R, C, r_lo, r_hi, map, tmp, wa, wb, scale, corr, partials_b, dtype, stream);
+  diffuse_reduce_strip_kernel<<<m, 256, 0, S_(stream)>>>(P_<double>(partials), ti, P_<double>(partials_b), gx, m,
+                                                         P_<double>(totals));
+  MS_LAUNCH_CHECK();
   rccl_allreduce(comm, totals, 2ll * m, 2 /* float64 */, 0 /* sum */, stream);
   diffuse_corr(m, totals, n_pix, new_corr, stream);
 }
