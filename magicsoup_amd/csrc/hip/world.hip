@@ -335,8 +335,12 @@ __global__ void __launch_bounds__(256) place_rounds_coop_kernel(int k, const int
                                                                 uint8_t* cell_map, uint8_t* pending, uint64_t seed,
                                                                 uint64_t call, long long* cand, int* claim,
                                                                 long long* result, int rounds, unsigned* ctl,
-                                                                unsigned* err_host) {
+                                                                unsigned* ctl_next, unsigned* err_host) {
   const unsigned nb = gridDim.x;
+  // the other control buffer, used by the next launch on this stream (which starts after this one
+  // ended), cleared here: no memset launch before every placement
+  if (blockIdx.x == 0)
+    for (int j = threadIdx.x; j < kMaxRounds + 2; j += blockDim.x) ctl_next[j] = 0u;
   const int stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
   unsigned phase = 0;
   __shared__ int s_left;
@@ -575,7 +579,10 @@ static int g_coop_blocks = 256;    // co-resident workgroups of the single-launc
 // launch never creates that queue, so profiles now time the production path.
 static int g_place_mode = 0;
 constexpr int kMaxDevices = 64;
-static unsigned* g_place_ctl[kMaxDevices] = {};  // per device: the control words of the cooperative launch
+// per device: two sets of control words of the cooperative launch, used in turn (a launch clears
+// the set of the next one)
+static unsigned* g_place_ctl[kMaxDevices] = {};
+static int g_place_par[kMaxDevices] = {};
 static unsigned* g_place_err = nullptr;           // pinned, mapped: a barrier timed out (any device)
 static unsigned* g_place_err_dev = nullptr;
 void set_place_mode(int mode) { g_place_mode = mode; }
@@ -597,13 +604,16 @@ static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, co
   int dev = 0;
   MS_HIP_CHECK(hipGetDevice(&dev));
   if (dev < 0 || dev >= kMaxDevices) throw std::runtime_error("place_coop: device index out of range");
-  if (!g_place_ctl[dev]) MS_HIP_CHECK(hipMalloc((void**)&g_place_ctl[dev], (2 + kMaxRounds) * sizeof(unsigned)));
+  if (!g_place_ctl[dev]) {
+    MS_HIP_CHECK(hipMalloc((void**)&g_place_ctl[dev], 2 * (2 + kMaxRounds) * sizeof(unsigned)));
+    MS_HIP_CHECK(hipMemset(g_place_ctl[dev], 0, 2 * (2 + kMaxRounds) * sizeof(unsigned)));
+    g_place_par[dev] = 0;
+  }
   if (!g_place_err) {
     MS_HIP_CHECK(hipHostMalloc((void**)&g_place_err, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
     *g_place_err = 0;
     MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_place_err_dev, g_place_err, 0));
   }
-  MS_HIP_CHECK(hipMemsetAsync(g_place_ctl[dev], 0, (2 + kMaxRounds) * sizeof(unsigned), s));
   int kk = k;
   const int64_t* cp = cells ? P_<int64_t>(cells) : nullptr;
   const uint8_t* mp = mask ? P_<uint8_t>(mask) : nullptr;
@@ -614,11 +624,12 @@ static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, co
   int* cl = P_<int>(claim);
   long long* res = P_<long long>(result);
   int rr = std::min(rounds, kMaxRounds);
-  unsigned* ctl = g_place_ctl[dev];
+  unsigned* ctl = g_place_ctl[dev] + g_place_par[dev] * (2 + kMaxRounds);
+  unsigned* ctl_next = g_place_ctl[dev] + (1 - g_place_par[dev]) * (2 + kMaxRounds);
   unsigned* err = g_place_err_dev;
   Geom gg = g;
   bool vac = vacate;
-  void* args[] = {&kk, &cp, &mp, &pp, &gg, &vac, &cm, &pend, &seed, &call, &cd, &cl, &res, &rr, &ctl, &err};
+  void* args[] = {&kk, &cp, &mp, &pp, &gg, &vac, &cm, &pend, &seed, &call, &cd, &cl, &res, &rr, &ctl, &ctl_next, &err};
   unsigned grid = std::min<unsigned>(cdiv(k, 256), (unsigned)g_coop_blocks);
   if (g_place_mode == 2) {
     const hipError_t e = hipLaunchCooperativeKernel((const void*)place_rounds_coop_kernel, dim3(grid), dim3(256), args,
@@ -627,6 +638,7 @@ static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, co
       (void)hipGetLastError();  // clear the sticky launch error; fall back
       return false;
     }
+    g_place_par[dev] ^= 1;
     return true;
   }
   // ordinary launch: the grid must fit the device at once (every workgroup reaches the barriers)
@@ -638,8 +650,10 @@ static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, co
     resident[dev] = std::max(1, per_cu * cus);
   }
   grid = std::min<unsigned>(grid, (unsigned)resident[dev]);
-  place_rounds_coop_kernel<<<grid, 256, 0, s>>>(kk, cp, mp, pp, gg, vac, cm, pend, seed, call, cd, cl, res, rr, ctl, err);
+  place_rounds_coop_kernel<<<grid, 256, 0, s>>>(kk, cp, mp, pp, gg, vac, cm, pend, seed, call, cd, cl, res, rr, ctl,
+                                                 ctl_next, err);
   MS_LAUNCH_CHECK();
+  g_place_par[dev] ^= 1;
   return true;
 }
 
