@@ -343,9 +343,18 @@ def _body_lazy_strip_divide(rank, ws):
     w.spawn_cells(gen_genomes(1200, 300))
     atp = _chem().molname_2_idx["ATP"]
     out = {}
+    rebuilds = {}
+    orig_rebuild = DistributedWorld._rebuild_arrivals
+
+    def counting_rebuild(self, arr):
+        rebuilds[self._lazy_tag] = rebuilds.get(self._lazy_tag, 0) + 1
+        return orig_rebuild(self, arr)
+
+    DistributedWorld._rebuild_arrivals = counting_rebuild
     for lazy in (False, True, "again"):
         random.seed(5)
         dw = DistributedWorld(chemistry=_chem(), map_size=64, seed=22, device="cuda", strips=True)
+        dw.__dict__["_lazy_tag"] = lazy
         dw.adopt_maps(w)
         dw.scatter_from(w, maps=False)
         ms.set_seed(23)
@@ -385,8 +394,11 @@ def _body_lazy_strip_divide(rank, ws):
                 bad.append(name + extra)
         return bad
 
+    DistributedWorld._rebuild_arrivals = orig_rebuild
     a, b, c = out[False], out[True], out["again"]
     assert a[9]["divided_in"] > 0
+    # eager: the arrivals get a rebuild chain of their own; lazy: the queued genome chain builds them
+    assert rebuilds.get(False, 0) > 0 and rebuilds.get(True, 0) == 0, rebuilds
     assert not diff(a, c), f"eager protocol not reproducible: {diff(a, c)}"
     assert not diff(a, b), f"lazy differs from eager: {diff(a, b)} ({a[9]} vs {b[9]})"
 
