@@ -1231,3 +1231,50 @@ def test_genome_pool_collect_layout_matches_sorted_reference():
     assert int(g.top.item()) == int(size_u.sum())
     assert list(w.cell_genomes) == before
     g.check()
+
+
+@pytest.mark.gpu
+def test_gpu_step_loop_is_deterministic():
+    """The reference loop as bench.py issues it (activity, kill, lazy division, queued
+    recombination + mutation chain, degradation, diffusion next to the chain, lifetimes; no host
+    synchronisation besides the API's own) replayed twice from one state with the same seeds ends in
+    bit-identical worlds: the device placement, selections, genome chains, speculative activity and
+    stencil reductions do not depend on thread timing. (Only the spawn's pixel claims race -- both
+    runs start from one deep-copied world and spawn nothing.)"""
+    import random
+
+    import bench
+
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    base = ms.World(chemistry=CHEMISTRY, map_size=128, device="cuda", seed=3)
+    base.spawn_cells(bench.random_genomes(2500, 500, "cuda"))
+    base.synchronize()
+    runs = []
+    for _ in range(2):
+        w = copy.deepcopy(base)
+        random.seed(9)
+        ms.set_seed(9)
+        torch.manual_seed(9)
+        for _ in range(10):
+            w.enzymatic_activity()
+            w.kill_cells(w.cell_molecules[:, atp] < 1.0)
+            repl = w.cell_molecules[:, atp] > 5.0
+            w.cell_molecules[:, atp] -= 4.0 * repl
+            w.divide_cells_t(repl, lazy=True)
+            w.recombinate_cells(p=1e-5)
+            w.mutate_cells(p=1e-4)
+            w.degrade_molecules()
+            w.diffuse_molecules()
+            w.increment_cell_lifetimes()
+        w.synchronize()
+        k = w.kinetics
+        runs.append({
+            "n": w.n_cells, "positions": w.cell_positions.clone(), "molecules": w.cell_molecules.clone(),
+            "lifetimes": w.cell_lifetimes.clone(), "divisions": w.cell_divisions.clone(),
+            "cell_map": w.cell_map.clone(), "map": w.molecule_map.clone(), "genomes": list(w.cell_genomes),
+            "labels": list(w.cell_labels), **{p: getattr(k, p).clone() for p in ("N", "A", "Kmr", "Vmax", "Ke")},
+        })
+    a, b = runs
+    assert a["n"] > 500 and int(a["divisions"].sum()) > 0
+    bad = [key for key in a if not (torch.equal(a[key], b[key]) if isinstance(a[key], torch.Tensor) else a[key] == b[key])]
+    assert not bad, bad
