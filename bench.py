@@ -58,8 +58,11 @@ def _count(n: int) -> str:
 def _args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=60)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 60; --sustained: 200)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps first (default 20; --sustained: 200)")
+    ap.add_argument("--sustained", action="store_true",
+                    help="time an evolved population: steps 201-400 by default (the reference's macro run is "
+                         "200 steps of an evolving population, performance/run_simulation.py:120)")
     ap.add_argument("--preset", default="flagship", choices=sorted(PRESETS))
     ap.add_argument("--map-size", type=int, default=None)
     ap.add_argument("--cells", type=int, default=None)
@@ -74,6 +77,10 @@ def _args():
     ap.add_argument("--phase-sync", action="store_true", help="with --profile-phases: drain the GPU at phase "
                     "boundaries (for attributing a kernel trace to phases; slows the step)")
     a = ap.parse_args()
+    if a.steps is None:
+        a.steps = 200 if a.sustained else 60
+    if a.warmup is None:
+        a.warmup = 200 if a.sustained else 20
     for k, v in PRESETS[a.preset].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
@@ -403,6 +410,8 @@ def main():
                 "parallelism": ("strips1-virtual" if virtual else f"spatial{world_size}") if distributed else "single",
             },
         }
+        if a.sustained:
+            out["window"] = f"steps {a.warmup + 1}-{a.warmup + a.steps} of an evolving population"
         out["ranks"] = world_size if distributed else 1
         out["devices"] = devices
         if distributed:

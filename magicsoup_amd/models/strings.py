@@ -339,9 +339,12 @@ class PoolArena:
         k, L = int(rows.size(0)), int(rows.size(1))
         if k == 0:
             return
+        # the length bound tracks the longest genome, not the row stride (pack_strings pads rows to a
+        # power of two): lengths still on the host are read for free, device ones would cost a sync
+        bound = int(lens.max()) if not lens.is_cuda else L
         rows = rows.to(self.device, torch.uint8).contiguous()
         lens = lens.to(self.device, torch.int32).contiguous()
-        self.reserve(self.capacity if dst is not None else n0 + k, L)
+        self.reserve(self.capacity if dst is not None else n0 + k, max(bound, 1))
         need = k * _r16(L)
         self.ensure(need)
         dst = None if dst is None else dst.to(self.device, torch.int64).contiguous()

@@ -1331,8 +1331,10 @@ class World:
     @_op("load_state")
     def load_state(self, statedir: Path, ignore_cell_params: bool = False, restore_rng: bool = False):
         """Load a state written by :meth:`save_state` (re-translating genomes unless
-        ``ignore_cell_params``). If the state holds an ``rng_state.pt`` (written by this package),
-        the random streams are restored too (``restore_rng``), so the run continues exactly."""
+        ``ignore_cell_params``). Restoring the random streams is opt-in: with ``restore_rng=True``
+        and an ``rng_state.pt`` in the state (written by this package) the run continues exactly as
+        an uninterrupted one would; by default (like the reference, which saves no RNG state) the
+        streams continue from wherever this process's are."""
         self._reconcile()
         from magicsoup_amd.utils.checkpoint import load_state
 

@@ -49,6 +49,13 @@ def _cap(expected: float, limit: int) -> int:
     call a no-op that reconcile replays on the synchronous path, see cap_skip), far below N_CAP
     for small rates, so the launches after the selection stay small."""
     return max(1, min(limit, int(8 * expected) + 256))
+
+
+def _cap_truncated(expected: float, limit: int) -> bool:
+    """Whether ``limit`` cuts the capacity :func:`_cap` wants: a count above it then becomes likely.
+    A skipped call is replayed on the synchronous path -- except a decomposed world's recombination,
+    whose strip-boundary results the replay cannot reproduce: such calls must not be issued then."""
+    return int(8 * expected) + 256 > limit
 # flag bits (select.hip DevFlag, mutations.hip kGp*)
 _F_TRANSLATE, _F_CAPACITY, _F_ROWS, _F_WIDTH, _F_SKIPPED = 1, 2, 4, 8, 16
 _SEL_I32POS, _SEL_SET = 2, 0
@@ -304,6 +311,8 @@ def recombinate_all(world, p: float, extra=None) -> bool:
     expected = 4 * n * p * 2 * L
     if p * 2 * L > LAM_MAX or not _usable(world, expected, N_CAP):
         return False
+    if extra is not None and _cap_truncated(expected, min(n, N_CAP) // 2):
+        return False  # (the synchronous path commits the boundary results itself)
     dev = arena.data.device
     pcap = _cap(expected, min(n, N_CAP) // 2)  # pairs per call (two results each)
     b = _begin(world, "rec")
@@ -372,6 +381,8 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
     if (p_rec * 2 * L > LAM_MAX or p * L > LAM_MAX or not _usable(world, exp_rec, N_CAP)
             or not _usable(world, n * p * L)):
         return False
+    if extra is not None and _cap_truncated(exp_rec, min(n, N_CAP) // 2):
+        return False  # (the caller issues the recombination on its own: see _cap_truncated)
     st = _state(world)
     if any(pd.kind in ("rec", "mut", "evo") for pd in st["pending"]):
         reconcile(world)

@@ -149,13 +149,15 @@ def wait_count(slot: int) -> int:
 
 
 def guarded_sync(event=None) -> None:
-    """Before a blocking read-back of a decomposed world: wait for the current stream (or only
-    for ``event``, an ops.streams.NEvent) with peer failure detection (without native
-    communicators: a plain wait for the event, if given)."""
-    if _GUARD:
-        _GUARD[0](0 if event is None else event.h)
-    elif event is not None:
+    """Before a blocking read-back: wait for the current stream (or only for ``event``, an
+    ops.streams.NEvent), with peer failure detection while native RCCL communicators are live
+    (without any -- none ever created, or all of them closed since -- a plain wait)."""
+    if _GUARD and _GUARD[0](0 if event is None else event.h):
+        return
+    if event is not None:
         event.synchronize()
+    elif torch.cuda.is_available():
+        torch.cuda.current_stream().synchronize()
 
 
 def check_placement() -> None:

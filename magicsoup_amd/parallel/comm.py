@@ -36,21 +36,25 @@ class CommError(RuntimeError):
     process are aborted (the job is fail-stop: restart from a checkpoint)."""
 
 
-def guarded_sync(event: int = 0) -> None:
+def guarded_sync(event: int = 0) -> bool:
     """Wait for the current HIP stream (or only for the native ``event`` handle, see
     magicsoup_amd.ops.streams.NEvent) while polling every live RCCL communicator of this process
     for asynchronous errors, with the :data:`TIMEOUT_S` bound. On a failure all communicators are
     aborted and :class:`CommError` is raised. Called before the host synchronisations of a
-    decomposed world's step (magicsoup_amd.ops.hip_ops.wait_count)."""
+    decomposed world's step (magicsoup_amd.ops.hip_ops.wait_count).
+
+    Returns False, without waiting, when no communicator is live (all closed, aborted or
+    collected): the caller then waits for the stream / event itself."""
     live = [c for c in list(_LIVE) if getattr(c, "handle", 0)]
     if not live:
-        return
+        return False
     m = live[0]._m
     why = m.rccl_guarded_wait([c.handle for c in live], live[0]._stream(), TIMEOUT_S, event)
     if why:
         for c in live:
             c.handle = 0  # aborted by the wait
         raise CommError(f"communication failed ({why}): a peer rank died or stalled")
+    return True
 
 
 @atexit.register
@@ -75,7 +79,7 @@ def _nbytes(t: torch.Tensor | None) -> int:
 class TorchComm:
     """torch.distributed exchanges (``stage``: device tensors over gloo go through host copies).
 
-    ``tagless`` (default: ``MS_COMM_TAGLESS=1``) reproduces the matching contract of
+    ``tagless`` (off by default; on with ``MS_COMM_TAGLESS=1`` or ``tagless=True``) reproduces the matching contract of
     :class:`RcclComm`: every point-to-point op uses tag 0 and the four ops are posted in exactly the
     order ``rccl_exchange`` posts them (send up, send down, receive from down, receive from up,
     ``csrc/hip/comm.hip``), so between two ranks sends and receives match by issue order alone,

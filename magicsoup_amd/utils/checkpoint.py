@@ -198,8 +198,10 @@ def _allowed_class(module: str, name: str):
 class _WorldUnpickler(pickle._Unpickler):  # the pure-Python unpickler: its opcode table is reachable
     """Restricted unpickler for world pickles (ours and the reference's): see the module docstring
     for what a file may name; anything else raises ``pickle.UnpicklingError``. Besides the name
-    check (``find_class``), REDUCE -- calling an object the file named -- is refused for everything
-    but torch's tensor rebuild functions, the storage loader and the builtin containers."""
+    check (``find_class``), calling an object the file named -- REDUCE, INST, OBJ -- is refused for
+    everything but torch's tensor rebuild functions, the storage loader and the builtin containers;
+    NEWOBJ / NEWOBJ_EX (``cls.__new__`` only) are limited to those and this package's data
+    classes."""
 
     dispatch = dict(pickle._Unpickler.dispatch)
 
@@ -244,6 +246,38 @@ class _WorldUnpickler(pickle._Unpickler):  # the pure-Python unpickler: its opco
         stack[-1] = func(*args)
 
     dispatch[pickle.REDUCE[0]] = _load_reduce
+
+    def _instantiate(self, klass, args):
+        # INST ('i') and OBJ ('o') call the class itself: the same rule as REDUCE
+        if id(klass) not in self._callable:
+            raise pickle.UnpicklingError(f"world pickles may not instantiate {klass!r}")
+        super()._instantiate(klass, args)
+
+    def _newobj_ok(self, cls) -> bool:
+        # NEWOBJ / NEWOBJ_EX run only ``cls.__new__`` (no constructor): allowed for the callable
+        # containers and this package's data classes, never for a torch storage class (whose
+        # ``__new__`` allocates whatever size the file names)
+        if not isinstance(cls, type) or (cls.__module__ or "").startswith("torch"):
+            return False
+        return id(cls) in self._callable or (cls.__module__ or "").startswith("magicsoup_amd.")
+
+    def _load_newobj(self):
+        args = self.stack.pop()
+        cls = self.stack[-1]
+        if not self._newobj_ok(cls):
+            raise pickle.UnpicklingError(f"world pickles may not create {cls!r}")
+        self.stack[-1] = cls.__new__(cls, *args)
+
+    def _load_newobj_ex(self):
+        kwargs = self.stack.pop()
+        args = self.stack.pop()
+        cls = self.stack[-1]
+        if not self._newobj_ok(cls):
+            raise pickle.UnpicklingError(f"world pickles may not create {cls!r}")
+        self.stack[-1] = cls.__new__(cls, *args, **kwargs)
+
+    dispatch[pickle.NEWOBJ[0]] = _load_newobj
+    dispatch[pickle.NEWOBJ_EX[0]] = _load_newobj_ex
 
 
 def load_world_pickle(path: Path, device: str | None = None):

@@ -1,7 +1,9 @@
 """Per-operation micro-benchmarks (the workloads of the reference's ``performance/check.py``).
 
 Wood-Ljungdahl chemistry, default 128^2 map, 10k cells with random genomes of 1000 bp +-10 %, mean
-+- sd over R repetitions. Every timed region ends with a device synchronisation. The reference's
++- sd over R repetitions. Every timed region ends with ``World.synchronize()`` of the worlds involved
+(deferred genome chains issued and confirmed, a speculative activity confirmed or redone, a lazy
+count adopted) and a device synchronisation. The reference's
 published numbers (v0.14.1, NVIDIA T4 / i5-10210U, ``performance/check.py:6-26``) are printed next to
 ours.
 
@@ -34,9 +36,23 @@ REFERENCE = {
 }
 
 
-def _sync(device: str) -> None:
+def _sync(device: str, *worlds) -> None:
+    """End of a timed region: every world settles its deferred work first (World.synchronize: a
+    pending division count, queued genome chains and their host confirmation -- replays included --,
+    a speculative activity's confirmation or redo), then the device drains."""
+    for w in worlds:
+        if isinstance(w, ms.World):
+            w.synchronize()
     if device.startswith("cuda"):
         torch.cuda.synchronize()
+
+
+def _worlds(state) -> list:
+    if isinstance(state, ms.World):
+        return [state]
+    if isinstance(state, tuple):
+        return [x for x in state if isinstance(x, ms.World)]
+    return []
 
 
 def _genomes(n: int, s: int, d: float = 0.1) -> list[str]:
@@ -47,11 +63,13 @@ def _genomes(n: int, s: int, d: float = 0.1) -> list[str]:
 _PROFILE = os.environ.get("MS_CHECK_PROFILE") == "1"  # cProfile of every timed call (stderr)
 
 
-def _timed(device: str, setup, fn, reps: int) -> list[float]:
+def _timed(device: str, setup, fn, reps: int, worlds=()) -> list[float]:
+    """``reps`` timings of ``fn(setup())``; the clock stops after :func:`_sync` of the state's worlds
+    (and of ``worlds``, for closures over a world), so no confirmation falls outside it."""
     out = []
     for _ in range(reps):
         state = setup()
-        _sync(device)
+        _sync(device, *_worlds(state), *worlds)
         prof = None
         if _PROFILE:
             import cProfile
@@ -60,7 +78,7 @@ def _timed(device: str, setup, fn, reps: int) -> list[float]:
             prof.enable()
         t0 = time.perf_counter()
         fn(state)
-        _sync(device)
+        _sync(device, *_worlds(state), *worlds)
         out.append(time.perf_counter() - t0)
         if prof is not None:
             import io
@@ -116,7 +134,7 @@ def bench_mutations(device, n, s, reps):
         pairs = w.get_neighbors(cell_idxs=list(range(w.n_cells)))
         ms.recombinations(seq_pairs=[(genomes[a], genomes[b]) for a, b in pairs])
 
-    return _timed(device, lambda: None, fn, reps)
+    return _timed(device, lambda: None, fn, reps, worlds=(w,))
 
 
 def bench_world_mutations(device, n, s, reps):
@@ -127,11 +145,10 @@ def bench_world_mutations(device, n, s, reps):
     def fn(_):
         w.mutate_cells()
         w.recombinate_cells()
-        # all-cells mutate / recombinate are queued for the device genome pipeline: issue and
-        # confirm them inside the timed region (what the next op of a step would do)
-        w._reconcile()
+        # all-cells mutate / recombinate are queued for the device genome pipeline: they are
+        # issued and confirmed inside the timed region (_sync -> World.synchronize)
 
-    return _timed(device, lambda: None, fn, reps)
+    return _timed(device, lambda: None, fn, reps, worlds=(w,))
 
 
 PARTS = {

@@ -405,3 +405,66 @@ def _body_lazy_strip_divide(rank, ws):
 
 def test_gpu_lazy_strip_divide_matches_eager():
     run_ranks(_body_lazy_strip_divide, 1, timeout=300, backend="nccl")
+
+
+def _body_lazy_divide_after_closed_comm(rank, ws):
+    """A communicator that existed and was closed leaves the peer-failure guard registered but with
+    no live communicator: a lazy division's count must still wait for the division's kernels
+    (the guard returned without waiting and the count was read stale)."""
+    import magicsoup_amd as ms
+    from magicsoup_amd.ops import hip_ops
+    from magicsoup_amd.parallel.comm import make_comm
+
+    comm = make_comm(None, 0, 1, "cuda")
+    comm.close()
+    del comm
+    assert hip_ops._GUARD  # registered once, stays registered
+    chem = _chem()
+    atp = chem.molname_2_idx["ATP"]
+    for lazy in (False, True):
+        ms.set_seed(11)
+        torch.manual_seed(11)
+        w = ms.World(chemistry=chem, map_size=96, device="cuda", seed=11)
+        w.spawn_cells([ms.random_genome(400) for _ in range(2500)])
+        w.enzymatic_activity()
+        repl = w.cell_molecules[:, atp] > -1.0  # every cell tries to divide
+        w.divide_cells_t(repl, lazy=lazy)
+        n = w.n_cells
+        w.check_invariants("lazy division after a closed communicator")
+        if lazy:
+            assert n == n_sync, (n, n_sync)
+        else:
+            n_sync = n
+            assert n > 2500
+
+
+def test_lazy_division_waits_after_communicator_closed():
+    run_ranks(_body_lazy_divide_after_closed_comm, 1, timeout=300, backend="nccl")
+
+
+def _body_dense_strip_recombination(rank, ws):
+    """A dense strip at a recombination rate whose pair count can exceed the device chain's pair
+    capacity: the merged recombinate + mutate chain must not be issued with the boundary results
+    (a skip there cannot be replayed); the strip takes the synchronous path instead."""
+    import magicsoup_amd as ms
+    from magicsoup_amd.parallel import DistributedWorld
+    from tests.conftest import gen_genomes
+
+    ms.set_seed(31)
+    torch.manual_seed(31)
+    dw = DistributedWorld(chemistry=_chem(), map_size=48, seed=31, device="cuda", strips=True)
+    dw.spawn_cells(gen_genomes(2100, 500))
+    n0 = dw.n_cells
+    for _ in range(3):
+        dw.recombinate_cells(p=3e-4)
+        dw.mutate_cells(p=1e-4)
+        dw.diffuse_molecules()
+        dw.synchronize()
+    assert dw.n_cells == n0
+    assert sum(len(g) for g in dw.cell_genomes) > 0
+    dw.check_invariants("dense strip recombination")
+    dw.close()
+
+
+def test_dense_strip_recombination_does_not_skip_boundary_results():
+    run_ranks(_body_dense_strip_recombination, 1, timeout=300, backend="nccl")

@@ -591,3 +591,21 @@ def test_world_unpickler_refuses_foreign_globals(tmp_path):
     (tmp_path / "world.pkl").write_bytes(pickle.dumps(Evil()))
     with pytest.raises(pickle.UnpicklingError):
         ms.World.from_file(tmp_path)
+
+
+@pytest.mark.parametrize("payload", [
+    # protocol 0 INST: World(...) -- a constructor that would allocate a map
+    b"(I64\ni" b"magicsoup_amd.models.world\nWorld\n.",
+    # OBJ: the class and its args after a MARK
+    b"(cmagicsoup_amd.models.world\nWorld\nI64\no.",
+    # NEWOBJ on a torch storage class (``__new__`` allocates what the file asks for)
+    b"\x80\x02ctorch\nFloatStorage\nJ\x00\x00\x00\x40\x85\x81.",
+])
+def test_world_unpickler_refuses_constructor_opcodes(tmp_path, payload):
+    """INST / OBJ may not call a data class (only REDUCE-callable containers); NEWOBJ may not create
+    torch storages."""
+    import pickle
+
+    (tmp_path / "world.pkl").write_bytes(payload)
+    with pytest.raises(pickle.UnpicklingError):
+        ms.World.from_file(tmp_path)
