@@ -24,6 +24,14 @@
 namespace msd {
 
 constexpr int kBlock = 256;
+// Canonical summation order of the per-signal sums over a cell's active proteins (consumption, the
+// candidate states): chunks of kChunk proteins in ascending order, each summed in ascending protein
+// order -- the first chunk from the initial value (X0_j, or 0 for the consumption), the others from
+// 0 -- and the chunk sums added to the running total in ascending chunk order. For cells with at most
+// kChunk active proteins this is the plain ascending sum. Every path (LDS staging, register lanes,
+// multi-group cells, the host core) sums this way, so all of them agree bit for bit, and a cell with
+// many proteins can be split over several lane groups (one chunk each) without changing results.
+constexpr int kChunk = 32;
 constexpr int kNarrowP = 12;  // LDS protein slots of the narrow integrator launch
 constexpr int kWideBlocksPerCU = 2;  // resident blocks per CU of the strided wide launch
 constexpr int kMaxParts = 4;  // speculative mode: 4 parts x 4 iterations in one 16-bit flag set
@@ -49,9 +57,6 @@ void release_kinetics_streams() {
   g_lds_fork = g_lds_join = nullptr;
 }
 void set_integrate_mode(int mode) { g_integrate_mode = mode; }
-// workgroups of the fused speculative launch that walk the wide list (two 64-lane slots each)
-static int g_fused_wide_blocks = 64;
-void set_fused_wide_blocks(int n) { g_fused_wide_blocks = n < 1 ? 1 : (n > 1024 ? 1024 : n); }
 
 struct IntegrateArgs {
   int c, P, s;
@@ -296,12 +301,18 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
   }
   wave_lds_sync();
 
-  // ---- 5. consumption per signal and the negative-concentration factors (signal phase)
+  // ---- 5. consumption per signal and the negative-concentration factors (signal phase; sums in the
+  //         canonical chunk order, see kChunk)
   for (int j = lane; j < s; j += G) {
     float cons = 0.0f;
-    for (int k = 0; k < na; ++k) {
-      const float nv = (float)w_n(words[k * SP + j]) * V[k];
-      if (nv < 0.0f) cons += -nv;
+    for (int k0 = 0; k0 < na; k0 += kChunk) {
+      const int k1 = min(k0 + kChunk, na);
+      float part = 0.0f;
+      for (int k = k0; k < k1; ++k) {
+        const float nv = (float)w_n(words[k * SP + j]) * V[k];
+        if (nv < 0.0f) part += -nv;
+      }
+      cons = k0 == 0 ? part : cons + part;
     }
     const float f = X0[j] / cons;
     fs[j] = f > 1.0f ? 1.0f : f;
@@ -332,13 +343,23 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
   wave_lds_sync();
 
   // ---- 7. X1 (signal phase), candidate 0
+  // X0_j + sum_k n_kj * w_k over the active proteins in the canonical chunk order
+  auto chunk_sum = [&](int j, auto&& w_of) {
+    float x = X0[j];
+    for (int k0 = 0; k0 < na; k0 += kChunk) {
+      const int k1 = min(k0 + kChunk, na);
+      float part = k0 == 0 ? x : 0.0f;
+      for (int k = k0; k < k1; ++k) {
+        const int n = w_n(words[k * SP + j]);
+        if (n != 0) part += (float)n * w_of(k);
+      }
+      x = k0 == 0 ? part : x + part;
+    }
+    return x;
+  };
   float* snap = a.snap_out + (size_t)(valid ? cell : 0) * ms::kSnap * s;
   for (int j = lane; j < s; j += G) {
-    float x = X0[j];
-    for (int k = 0; k < na; ++k) {
-      const int n = w_n(words[k * SP + j]);
-      if (n != 0) x += (float)n * Va[k];
-    }
+    float x = chunk_sum(j, [&](int k) { return Va[k]; });
     x = x < 0.0f ? 0.0f : x;
     Xc[j] = x;
     if (valid) snap[j] = x;
@@ -418,11 +439,7 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
     }
     float* sn = snap + (size_t)(it + 1) * s;
     for (int j = lane; j < s; j += G) {
-      float x = X0[j];
-      for (int k = 0; k < na; ++k) {
-        const int n = w_n(words[k * SP + j]);
-        if (n != 0) x += (float)n * (Va[k] * F[k]);
-      }
+      float x = chunk_sum(j, [&](int k) { return Va[k] * F[k]; });
       x = x < 0.0f ? 0.0f : x;
       Xc[j] = x;
       if (valid) sn[j] = x;
@@ -558,11 +575,30 @@ struct E16 {
 // lane l plays signals l and l + G; the per-signal sums still run over proteins in ascending order
 // and a protein's products over its non-zero signals in ascending signal order (half 0 before half
 // 1), exactly as integrate_item, so all paths stay bit-identical.
-template <int G, int NZ, bool kSpec = false, int SPL = 1>
+// Multi-group cells (NG > 1, G == 32, SPL == 1): the NG groups of a block share ONE cell. Group g holds
+// active proteins [g * G, g * G + G) -- one canonical chunk (kChunk == G) -- with the same register
+// and LDS layout as a single-group cell; the per-signal sums are formed per chunk and combined across
+// the groups through LDS in ascending chunk order (the canonical order, so the results are those of
+// every other path bit for bit). A cell with up to NG * G active proteins then runs as G-protein
+// chains plus one block barrier per signal pass, instead of one 64-lane chain (or an LDS-path chain)
+// over all of them. The cross-group words need no LDS of their own (the block keeps the narrow
+// launch's 6 blocks per CU): each group publishes its votes in the padding words of its slot's
+// entry-index rows (bytes NZ .. JS of a row are never written) and its chunk sums in the entry-index
+// bytes (jl) past those rows' votes, which are dead once the protein lanes hold their entries in
+// registers.
+template <int NZ>
+constexpr int vote_word(int v) { return (v * jl_stride<NZ>() + NZ) / 4; }  // row v's pad
+constexpr int kMgSumWord = 16;  // first jl word of the chunk-sum buffers (past the vote rows 0..2)
+
+template <int G, int NZ, bool kSpec = false, int SPL = 1, int NG = 1>
 __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int* smem, int item, unsigned& bits,
                                                     int32_t* wide_list, int32_t* wide_count) {
   using EP = E16<SPL>;
+  static_assert(NG == 1 || (G == kChunk && SPL == 1 && kSpec && NG * G <= kBlock),
+                "multi-group cells: 32-lane groups, one signal per lane, speculative launches");
+  static_assert(G == kChunk || G == 2 * kChunk, "a group covers one or two canonical chunks");
   const int slot = threadIdx.x / G, lane = threadIdx.x % G;
+  const int grp = NG > 1 ? slot : 0;  // this group's chunk of the cell's active proteins
   const bool listed0 = a.list ? item < *a.count : item < a.c;
   const int cell0 = listed0 ? (a.list ? a.list[item] : item) : 0;
   const bool listed = listed0 && (unsigned)cell0 < (unsigned)a.c;  // (a list entry is a cell index)
@@ -571,12 +607,14 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   const size_t prow = listed ? (a.prow ? (size_t)a.prow[cell] : (size_t)cell) : 0;
 
   constexpr int ES = ent_stride<NZ>(), JS = jl_stride<NZ>();
-  int* ents = smem + slot * fast_slot_words<G, NZ, SPL>();   // (G, ES) words of the non-zeros
+  constexpr int SW = fast_slot_words<G, NZ, SPL>();
+  int* ents = smem + slot * SW;                                  // (G, ES) words of the non-zeros
   uint8_t* jl = reinterpret_cast<uint8_t*>(ents + G * ES);  // (G, JS) bytes: their signal indices
   int* cnts = ents + G * ES + G * JS / 4;                    // (G,) non-zero signals per protein
   int* act = cnts + G;                                           // (G,) protein slot of active protein k
   float* pub = reinterpret_cast<float*>(act + G);                // (G,) protein -> signal: V_k / Va_k * F_k
   float* Xs = pub + G;                                           // (SPL * G,) signal -> protein: X_j / factor
+  int pass = 0;                                                  // multi-group: chunk-sum buffer parity
 
   // ---- 1. X0 of this lane's signals (independent of the compaction, issued first)
   float x0[SPL];
@@ -589,7 +627,8 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     }
   }
 
-  // ---- 2. active proteins (Vmax' != 0, NaN included) in ascending order
+  // ---- 2. active proteins (Vmax' != 0, NaN included) in ascending order; group grp keeps entries
+  //         [grp * G, grp * G + G) of the compacted list
   constexpr bool spec = kSpec;
   const int nparts = spec ? a.spec_parts : 1;
   int na = 0;
@@ -602,13 +641,13 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     const bool on = listed && p < P && !(vm <= 0.0f);
     for (int q = 1; q < nparts; ++q) trim_diff |= on != (listed && p < P && !(vmax * trim_of(a, q) <= 0.0f));
     const unsigned long long gm = group_ballot<G>(on);
-    const int k = na + __popcll(gm & ((1ull << lane) - 1ull));
-    if (on && k < G) act[k] = p;
+    const int k = na + __popcll(gm & ((1ull << lane) - 1ull)) - grp * G;
+    if (on && k >= 0 && k < G) act[k] = p;
     na += __popcll(gm);
   }
-  bool fits = na <= G;
+  bool fits = na <= NG * G;
   wave_lds_sync();
-  const int nac = fits ? na : 0;
+  const int nac = fits ? min(max(na - grp * G, 0), G) : 0;  // this group's active proteins
   const int na_w = wave_max(nac);  // wave-uniform bound of the protein loops (both groups of a wave)
 
   // ---- 3. this lane's signals' stoichiometry columns (int8 n per protein, packed in registers) and
@@ -651,11 +690,23 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
       wide_ok &= base <= NZ;
     }
   }
-  const bool nz_ok = group_ballot<G>(!wide_ok) == 0ull;
+  bool nz_ok = group_ballot<G>(!wide_ok) == 0ull;
+  // multi-group: word v of group g's votes (a pad word of its slot's entry-index rows)
+  auto vote = [&](int g, int v) -> int& { return smem[g * SW + G * ES + vote_word<NZ>(v)]; };
+  if constexpr (NG > 1) {
+    static_assert(JS - NZ >= 4 && vote_word<NZ>(2) < kMgSumWord, "vote words must be row padding");
+    // the cell fits only if every group's proteins do (one block-wide vote)
+    if (lane == 0) vote(grp, 0) = nz_ok ? 1 : 0;
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < NG; ++g) nz_ok &= vote(g, 0) != 0;
+  }
+  // (multi-group: one report per cell, from group 0)
+  const bool reporter = listed && lane == 0 && grp == 0;
   if (!spec) {
     fits = fits && nz_ok;
-    if (listed && !fits && lane == 0 && wide_list) wide_list[atomicAdd(wide_count, 1)] = cell;
-  } else if (listed && lane == 0) {
+    if (!fits && reporter && wide_list) wide_list[atomicAdd(wide_count, 1)] = cell;
+  } else if (reporter) {
     // too many active proteins: skipped when the cell is on the wide list already (prelisted);
     // otherwise, and with too many non-zeros / large exponents, the cell goes to the overflow list
     // (the next, wider launch), without one the speculation is void; so is a cell whose active set
@@ -673,8 +724,9 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   const bool valid = listed && fits;
   bool sig[SPL];
 #pragma unroll
-  for (int h = 0; h < SPL; ++h) sig[h] = valid && lane + h * G < s;
-  const bool prot = valid && lane < na;
+  for (int h = 0; h < SPL; ++h) sig[h] = valid && lane + h * G < s && grp == 0;  // (the writer of the cell)
+  const bool prot = valid && lane < nac;
+  const int nchunks = valid ? (na + kChunk - 1) / kChunk : 0;  // (multi-group: uniform over the block)
 #pragma unroll
   for (int h = 0; h < SPL; ++h) Xs[lane + h * G] = x0[h];
   wave_lds_sync();
@@ -712,8 +764,14 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
 #define MS_E(q) ((e16[(q) >> 1] >> (16 * ((q) & 1))) & 0xFFFF)
   auto pw = [&](float x, int n) { return small_w ? ipow_small(x, n) : ms::ipow(x, n); };
 
-  // signal lane, half h: sum over proteins k (ascending) of op(n_kj, pub[k]); four proteins per LDS load
-  auto signal_pass = [&](auto&& op) {
+  // signal lane, half h: acc[h] (the initial value) + sum over this group's proteins k (ascending) of
+  // op(n_kj, pub[k]), four proteins per LDS load, in the canonical chunk order: a 64-lane group sums
+  // its second chunk (proteins 32..63) separately and adds it after the first. Multi-group cells
+  // then combine the groups' chunk sums (combine below).
+  auto signal_pass = [&](float (&acc)[SPL], auto&& op) {
+    float part[SPL];
+#pragma unroll
+    for (int h = 0; h < SPL; ++h) part[h] = 0.0f;
 #pragma unroll
     for (int k0 = 0; k0 < G; k0 += 4) {
       if (k0 >= na_w) break;
@@ -723,8 +781,49 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
       for (int u = 0; u < 4; ++u) {
         const int k = k0 + u;
 #pragma unroll
-        for (int h = 0; h < SPL; ++h) op(h, (int)(int8_t)(npk[h][k >> 2] >> (8 * (k & 3))), bv[u]);
+        for (int h = 0; h < SPL; ++h) {
+          const int n = (int)(int8_t)(npk[h][k >> 2] >> (8 * (k & 3)));
+          if (k < kChunk) op(acc[h], n, bv[u]);
+          else op(part[h], n, bv[u]);
+        }
       }
+    }
+    if constexpr (G > kChunk) {
+      if (nac > kChunk) {
+#pragma unroll
+        for (int h = 0; h < SPL; ++h) acc[h] += part[h];
+      }
+    }
+  };
+  // multi-group: group g's chunk sum (group 0's includes the initial value) -> the cell's sum, read by
+  // every group from the others' slots in ascending chunk order (double-buffered by pass parity: a
+  // group writing pass i + 2 has passed pass i + 1's barrier, so every group has read pass i)
+  auto combine = [&](float (&x)[SPL]) {
+    if constexpr (NG > 1) {
+      constexpr int kJlWords = G * JS / 4;
+      static_assert(kMgSumWord + 2 * G <= kJlWords, "chunk-sum buffers must fit the entry-index bytes");
+      const int off = kMgSumWord + (pass & 1) * G + lane;
+      reinterpret_cast<float*>(jl)[off] = x[0];
+      __syncthreads();
+      float t = x[0];
+      if (grp != 0) t = reinterpret_cast<const float*>(smem + G * ES)[off];
+      for (int g = 1; g < nchunks; ++g) t += reinterpret_cast<const float*>(smem + g * SW + G * ES)[off];
+      x[0] = t;
+      ++pass;
+    }
+  };
+  // multi-group: a predicate over the cell's protein lanes (one block barrier); else over the group
+  auto cell_any = [&](bool b, int word) {
+    if constexpr (NG > 1) {
+      const bool gb = group_ballot<G>(b) != 0ull;  // (all lanes: a ballot under lane == 0 sees one lane)
+      if (lane == 0) vote(grp, 1 + word) = gb ? 1 : 0;
+      __syncthreads();
+      int any = 0;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) any |= vote(g, 1 + word);
+      return any != 0;
+    } else {
+      return group_ballot<G>(b) != 0ull;
     }
   };
 
@@ -782,10 +881,11 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     float cons[SPL];
 #pragma unroll
     for (int h = 0; h < SPL; ++h) cons[h] = 0.0f;
-    signal_pass([&](int h, int n, float vk) {
+    signal_pass(cons, [](float& acc, int n, float vk) {
       const float nv = (float)n * vk;
-      if (nv < 0.0f) cons[h] += -nv;
+      if (nv < 0.0f) acc += -nv;
     });
+    combine(cons);
 #pragma unroll
     for (int h = 0; h < SPL; ++h) {
       const float f = x0[h] / cons[h];
@@ -819,13 +919,14 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   wave_lds_sync();
 
   // ---- 7. candidate 0 (signal lane)
-  auto advance = [&]() {  // X0 + sum_k n_k * pub_k (ascending k), clamped at 0
+  auto advance = [&]() {  // X0 + sum_k n_k * pub_k (canonical order), clamped at 0
     float x[SPL];
 #pragma unroll
-    for (int h = 0; h < SPL; ++h) x[h] = x0[h];
-    signal_pass([&](int h, int n, float b) {
-      if (n != 0) x[h] += (float)n * b;
+    for (int h = 0; h < SPL; ++h) x[h] = grp == 0 ? x0[h] : 0.0f;  // (multi-group: chunk 0 starts from X0)
+    signal_pass(x, [](float& acc, int n, float b) {
+      if (n != 0) acc += (float)n * b;
     });
+    combine(x);
 #pragma unroll
     for (int h = 0; h < SPL; ++h) xc[h] = x[h] < 0.0f ? 0.0f : x[h];
   };
@@ -878,10 +979,10 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
         F = f;
       }
     }
-    if (group_ballot<G>(changed) == 0ull) {
+    if (!cell_any(changed, 0)) {
       // per-cell fixed point (see integrate_item): the remaining candidates are copies, and an
       // impactful correction that changed nothing repeats in every remaining iteration
-      if (group_ballot<G>(cb) != 0ull) bits |= (((1u << a.n_iters) - 1u) & ~((2u << it) - 1u)) << bsh;
+      if (cell_any(cb, 1)) bits |= (((1u << a.n_iters) - 1u) & ~((2u << it) - 1u)) << bsh;
       if (!spec)
         for (int it2 = it + 1; it2 <= a.n_iters; ++it2)
 #pragma unroll
@@ -997,6 +1098,32 @@ __global__ void __launch_bounds__(kBlock, W) integrate_fused_kernel(IntegrateArg
     integrate_item_fast<G, kNzReg, kSpec>(a, smem, ((int)blockIdx.x - nwb) * (kBlock / G) + (int)threadIdx.x / G, bits,
                                    nullptr, nullptr);
   }
+  or_block_bits(bits, a.mask_out);
+}
+
+// The speculative all-parts launch for the 32-lane chemistries (s <= 32): every block first takes
+// cells of the wide list (more than 32 active proteins, listed by gather_bin_kernel), strided over
+// the whole grid, each as ONE multi-group cell (the block's 8 groups: up to 256 active proteins, one
+// canonical chunk per group), then its own 8 narrow cells. A grown population's wide cells thus run
+// at the front of the grid with as many blocks as there are such cells, each as 32-protein chains,
+// under the narrow cells' throughput work instead of after it. Cells that fit neither role (too
+// many proteins or non-zeros, large exponents) go to the overflow lists for the launches behind.
+__device__ __forceinline__ void integrate_wide_cells(const IntegrateArgs& aw, int* smem, unsigned& bits) {
+  const int nw = *aw.count;  // (block-uniform: the multi-group cell's barriers need every wave)
+  for (int item = (int)blockIdx.x; item < nw; item += (int)gridDim.x) {
+    integrate_item_fast<32, kNzReg, true, 1, kBlock / 32>(aw, smem, item, bits, nullptr, nullptr);
+    __syncthreads();  // the cell's slots and votes are reused by the next item
+  }
+}
+
+template <int W>
+__global__ void __launch_bounds__(kBlock, W) integrate_spec_fused_kernel(IntegrateArgs a, IntegrateArgs aw) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  constexpr int kGroups = kBlock / 32;
+  unsigned bits = 0u;
+  if ((int)blockIdx.x < *aw.count) integrate_wide_cells(aw, smem, bits);
+  integrate_item_fast<32, kNzReg, true>(a, smem, (int)blockIdx.x * kGroups + (int)threadIdx.x / 32, bits, nullptr,
+                                        nullptr);
   or_block_bits(bits, a.mask_out);
 }
 
@@ -1488,26 +1615,11 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
     ao.list = wl2;
     ao.count = wc2;
     if (Gs == 32) {
-      const int kFusedWideBlocks = g_fused_wide_blocks;
       const size_t lds_fast = (size_t)(kBlock / 32) * fast_slot_words<32, kNzReg>() * 4;
       const size_t lds_fw = (size_t)(kBlock / 64) * fast_slot_words<64, kNzWide>() * 4;
-      if (g_integrate_mode & 1024) {
-        // (A/B) the wide list and the narrow cells as two launches: each kernel gets the registers
-        // its path needs (the fused kernel holds both paths in the narrow path's 80 VGPRs, and the
-        // 64-lane path spills there)
-        integrate_fast_kernel<64, kNzWide, true, true><<<kFusedWideBlocks, kBlock, lds_fw, st>>>(aw, nullptr, nullptr);
-        MS_LAUNCH_CHECK();
-        if (g_integrate_mode & 2048)
-          integrate_narrow_spec_kernel<5><<<cdiv(c, kBlock / 32), kBlock, lds_fast, st>>>(a);
-        else
-          integrate_narrow_spec_kernel<6><<<cdiv(c, kBlock / 32), kBlock, lds_fast, st>>>(a);
-      } else if (g_integrate_mode & 4096) {
-        integrate_fused_kernel<32, true, 5><<<cdiv(c, kBlock / 32) + kFusedWideBlocks, kBlock, lds_fast, st>>>(
-            a, aw, kFusedWideBlocks);
-      } else {
-        integrate_fused_kernel<32, true><<<cdiv(c, kBlock / 32) + kFusedWideBlocks, kBlock, lds_fast, st>>>(
-            a, aw, kFusedWideBlocks);
-      }
+      // (6 waves per SIMD: measured faster than 5 -- 96 VGPRs, fewer spills -- by 3-5 % on the
+      // flagship state, profiles/r5/ab_integrator_*.log)
+      integrate_spec_fused_kernel<6><<<cdiv(c, kBlock / 32), kBlock, lds_fast, st>>>(a, aw);
       MS_LAUNCH_CHECK();
       integrate_fast_kernel<64, kNzWide, true, true><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
       MS_LAUNCH_CHECK();

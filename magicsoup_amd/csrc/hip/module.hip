@@ -132,7 +132,6 @@ void translate_fused(int n, uintptr_t rows, uintptr_t arena, uintptr_t off, int 
                      uintptr_t long_count, uintptr_t dn, uintptr_t stream);
 size_t translate_slot_bytes(int width);
 void set_integrate_mode(int mode);
-void set_fused_wide_blocks(int n);
 void set_spl2_waves(int w);
 // mutations.hip
 void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
@@ -291,7 +290,6 @@ PYBIND11_MODULE(_hip, m) {
   m.def("translate_write", &msd::translate_write);
   m.def("translate_fused", &msd::translate_fused);
   m.def("set_spl2_waves", &msd::set_spl2_waves, "waves per SIMD of the wide chemistries' narrow launch (2-4)");
-  m.def("set_fused_wide_blocks", &msd::set_fused_wide_blocks, "wide-list workgroups of the fused integrator launch");
   m.def("set_integrate_mode", &msd::set_integrate_mode, "binned integrator launches: 0 serial, 1 concurrent, 2 concurrent + strided wide bin");
   m.def("translate_slot_bytes", &msd::translate_slot_bytes);
   m.def("mut_count", &msd::mut_count);

@@ -2,7 +2,9 @@
 // CPU counterpart of hip/kinetics.hip; semantics documented in ms_kinetics.h.
 #include <omp.h>
 
+#include <algorithm>
 #include <cstring>
+#include <vector>
 #include <stdexcept>
 
 #include "host_common.h"
@@ -24,6 +26,8 @@ struct CellParams {
 // Trajectory of one integration part for one cell (kinetics.py:753-859 with the loop unrolled to
 // all kEqIters iterations). Writes the kSnap candidate states to snap[k*s + j] and returns the
 // per-iteration "impactful correction" bits.
+constexpr int kChunk = 32;  // canonical chunk of the per-signal sums (kinetics.hip kChunk)
+
 unsigned cell_part(const CellParams& q, int np, int s, const float* X0, float trim, int n_iters, float* snap,
                    float* V, float* Va, float* F, unsigned char* fwd, unsigned char* imp, float* cons, float* fs,
                    uint8_t* dec, int dec_stride) {
@@ -70,14 +74,26 @@ unsigned cell_part(const CellParams& q, int np, int s, const float* X0, float tr
     v = v < ms::kMin ? ms::kMin : (v > ms::kMax ? ms::kMax : v);
     V[p] = v;
   }
+  // The per-signal sums over proteins run over the active proteins (Vmax' != 0; an inactive one adds
+  // exact zeros) in the device's canonical chunk order (kinetics.hip kChunk): chunks of 32 active
+  // proteins, the first from the initial value, the others from 0, added to the total in order.
+  thread_local std::vector<int> act;
+  act.resize((size_t)np);
+  int na = 0;
+  for (int p = 0; p < np; ++p)
+    if (!(q.Vmax[p] * trim <= 0.0f)) act[na++] = p;
   // negative-concentration guard (kinetics.py:861-879)
   for (int j = 0; j < s; ++j) cons[j] = 0.0f;
-  for (int p = 0; p < np; ++p) {
-    const int32_t* n = q.N + (size_t)p * s;
-    if (V[p] == 0.0f) continue;
+  for (int k0 = 0; k0 < na; k0 += kChunk) {
+    const int k1 = std::min(k0 + kChunk, na);
     for (int j = 0; j < s; ++j) {
-      const float nv = (float)n[j] * V[p];
-      if (nv < 0.0f) cons[j] += -nv;
+      float part = 0.0f;
+      for (int k = k0; k < k1; ++k) {
+        const int p = act[k];
+        const float nv = (float)q.N[(size_t)p * s + j] * V[p];
+        if (nv < 0.0f) part += -nv;
+      }
+      cons[j] = k0 == 0 ? part : cons[j] + part;
     }
   }
   for (int j = 0; j < s; ++j) {
@@ -96,16 +112,26 @@ unsigned cell_part(const CellParams& q, int np, int s, const float* X0, float tr
     }
     Va[p] = V[p] * (nan ? NAN : fmin);
   }
+  // x_j = X0_j + sum_k n_kj * w(k) over the active proteins, canonical chunk order
+  auto chunk_sum = [&](float* x, auto&& w_of) {
+    for (int j = 0; j < s; ++j) {
+      float tot = X0[j];
+      for (int k0 = 0; k0 < na; k0 += kChunk) {
+        const int k1 = std::min(k0 + kChunk, na);
+        float part = k0 == 0 ? tot : 0.0f;
+        for (int k = k0; k < k1; ++k) {
+          const int p = act[k];
+          const int32_t n = q.N[(size_t)p * s + j];
+          if (n != 0) part += (float)n * w_of(p);
+        }
+        tot = k0 == 0 ? part : tot + part;
+      }
+      x[j] = tot < 0.0f ? 0.0f : tot;
+    }
+  };
   // X1 = X0 + sum_p NV_adj (clamped at 0)
   float* x1 = snap;
-  for (int j = 0; j < s; ++j) x1[j] = X0[j];
-  for (int p = 0; p < np; ++p) {
-    const int32_t* n = q.N + (size_t)p * s;
-    for (int j = 0; j < s; ++j)
-      if (n[j] != 0) x1[j] += (float)n[j] * Va[p];
-  }
-  for (int j = 0; j < s; ++j)
-    if (x1[j] < 0.0f) x1[j] = 0.0f;
+  chunk_sum(x1, [&](int p) { return Va[p]; });
 
   // equilibrium damping trajectory (kinetics.py:808-859)
   unsigned bits = 0;
@@ -150,15 +176,7 @@ unsigned cell_part(const CellParams& q, int np, int s, const float* X0, float tr
       if (low) f += inc;
       F[p] = f > 1.0f ? 1.0f : (f < 0.0f ? 0.0f : f);
     }
-    for (int j = 0; j < s; ++j) xn[j] = X0[j];
-    for (int p = 0; p < np; ++p) {
-      const int32_t* n = q.N + (size_t)p * s;
-      const float w = Va[p] * F[p];
-      for (int j = 0; j < s; ++j)
-        if (n[j] != 0) xn[j] += (float)n[j] * w;
-    }
-    for (int j = 0; j < s; ++j)
-      if (xn[j] < 0.0f) xn[j] = 0.0f;
+    chunk_sum(xn, [&](int p) { return Va[p] * F[p]; });
   }
   return bits;
 }

@@ -28,6 +28,7 @@ Disable with ``MS_SYNC_GENETICS=1`` (always the synchronous path).
 """
 from __future__ import annotations
 
+import math
 import os
 
 import torch
@@ -51,11 +52,17 @@ def _cap(expected: float, limit: int) -> int:
     return max(1, min(limit, int(8 * expected) + 256))
 
 
-def _cap_truncated(expected: float, limit: int) -> bool:
-    """Whether ``limit`` cuts the capacity :func:`_cap` wants: a count above it then becomes likely.
-    A skipped call is replayed on the synchronous path -- except a decomposed world's recombination,
-    whose strip-boundary results the replay cannot reproduce: such calls must not be issued then."""
-    return int(8 * expected) + 256 > limit
+def _pair_cap(n: int, expected: float, extra) -> int | None:
+    """Pair capacity of a recombination call over ``n`` cells whose pair count has the (worst-case)
+    mean ``expected``; None if the call must not be issued. A count above the capacity makes the call
+    a no-op that reconcile replays on the synchronous path -- except for a decomposed world's call
+    carrying strip-boundary results (``extra``), which the replay cannot reproduce: such a call is
+    issued only while its capacity clears the mean by 8 standard deviations (a skip then has a
+    probability below 1e-15); beyond, the caller issues the recombination on its own."""
+    limit = min(n, N_CAP) // 2
+    if extra is not None and expected + 8.0 * math.sqrt(expected) + 64 > limit:
+        return None
+    return _cap(expected, limit)
 # flag bits (select.hip DevFlag, mutations.hip kGp*)
 _F_TRANSLATE, _F_CAPACITY, _F_ROWS, _F_WIDTH, _F_SKIPPED = 1, 2, 4, 8, 16
 _SEL_I32POS, _SEL_SET = 2, 0
@@ -311,10 +318,10 @@ def recombinate_all(world, p: float, extra=None) -> bool:
     expected = 4 * n * p * 2 * L
     if p * 2 * L > LAM_MAX or not _usable(world, expected, N_CAP):
         return False
-    if extra is not None and _cap_truncated(expected, min(n, N_CAP) // 2):
+    pcap = _pair_cap(n, expected, extra)  # pairs per call (two results each)
+    if pcap is None:
         return False  # (the synchronous path commits the boundary results itself)
     dev = arena.data.device
-    pcap = _cap(expected, min(n, N_CAP) // 2)  # pairs per call (two results each)
     b = _begin(world, "rec")
     _room(world, (2 * pcap + (0 if extra is None else int(extra.rows))) * _r16(2 * L))
     sc = _scratch(world)
@@ -381,13 +388,13 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
     if (p_rec * 2 * L > LAM_MAX or p * L > LAM_MAX or not _usable(world, exp_rec, N_CAP)
             or not _usable(world, n * p * L)):
         return False
-    if extra is not None and _cap_truncated(exp_rec, min(n, N_CAP) // 2):
-        return False  # (the caller issues the recombination on its own: see _cap_truncated)
+    pcap = _pair_cap(n, exp_rec, extra)
+    if pcap is None:
+        return False  # (the caller issues the recombination on its own: see _pair_cap)
     st = _state(world)
     if any(pd.kind in ("rec", "mut", "evo") for pd in st["pending"]):
         reconcile(world)
     dev = arena.data.device
-    pcap = _cap(exp_rec, min(n, N_CAP) // 2)
     mcap = _cap(n * p * L, min(n, N_CAP))
     kin = world.kinetics
     arr0, narr = (0, 0) if arrivals is None else (int(arrivals[0]), int(arrivals[1]))

@@ -5,7 +5,7 @@ timed alternately with module A and module B, and their results are compared bit
 Each module is timed in every integrate mode of --modes (comma list, default 0); results must be
 bit-identical across modules and modes.
 
-usage: python scripts/ab_so.py [--size S] [--cells C] [--chem wl|synthetic:M:R] [--modes 0,128]
+usage: python scripts/ab_so.py [--size S] [--cells C] [--chem wl|synthetic:M:R] [--modes 0,128] [--steps K]
                                A.so B.so [C.so ...]"""
 import importlib.machinery
 import importlib.util
@@ -48,7 +48,7 @@ def timed(fn, iters=20):
 
 def main():
     args = sys.argv[1:]
-    size, cells, chem_spec, modes = 4096, 50000, "wl", [0]
+    size, cells, chem_spec, modes, steps = 4096, 50000, "wl", [0], 5
     while args and args[0].startswith("--"):
         flag, val = args[0], args[1]
         args = args[2:]
@@ -58,6 +58,8 @@ def main():
             cells = int(val)
         elif flag == "--chem":
             chem_spec = val
+        elif flag == "--steps":
+            steps = int(val)
         else:
             modes = [int(v) for v in val.split(",")]
     mods = {chr(65 + i): load(p, f"v{i}") for i, p in enumerate(args)}
@@ -65,18 +67,22 @@ def main():
     atp = chem.molname_2_idx.get("ATP", 0)
     w = ms.World(chemistry=chem, map_size=size, device="cuda", seed=0)
     w.spawn_cells(bench.random_genomes(cells, 500, "cuda"))
-    for _ in range(5):
+    for _ in range(steps):
         bench.step(w, cells, 500, atp)
+    w.synchronize()
     kin = w.kinetics
     pos = w.cell_positions.long()
     X = torch.cat([w.cell_molecules, w.molecule_map[:, pos[:, 0], pos[:, 1]].T], dim=1).contiguous()
     kin._packed_params()
     out, res = {"P": int(kin._P()), "cells": w.n_cells}, {}
+    from magicsoup_amd.ops import hip_ops
+
     orig = native._mods.get("_hip")
     try:
         for rep in range(3):
             for tag, mod in mods.items():
-                native._mods["_hip"] = mod
+                # (hip_ops caches the module it resolved first: swap both handles)
+                native._mods["_hip"] = hip_ops._MOD = mod
                 for mode in modes:
                     mod.set_integrate_mode(mode)
                     Xk = X.clone()
@@ -88,7 +94,7 @@ def main():
         first = next(iter(res.values()))
         out["equal"] = {t: bool(torch.equal(first, r)) for t, r in res.items()}
     finally:
-        native._mods["_hip"] = orig
+        native._mods["_hip"] = hip_ops._MOD = orig
     print(json.dumps(out))
 
 

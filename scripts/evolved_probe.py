@@ -3,7 +3,7 @@
 distribution of the population and the time of one enzymatic_activity on that state.
 
     python scripts/evolved_probe.py [--steps 500] [--every 50] [--map-size 4096] [--cells 50000]
-        [--wide-blocks 64,256,1024]
+        [--modes 128]
 
 The reference's macro benchmark runs 200 steps of an evolving population
 (``performance/run_simulation.py:120``); a freshly spawned population (the first few dozen steps)
@@ -77,7 +77,7 @@ def main() -> None:
     ap.add_argument("--every", type=int, default=50)
     ap.add_argument("--map-size", type=int, default=4096)
     ap.add_argument("--cells", type=int, default=50_000)
-    ap.add_argument("--wide-blocks", default="")
+    ap.add_argument("--modes", default="", help="comma-separated integrator modes to time as well")
     ap.add_argument("--seed", type=int, default=0)
     a = ap.parse_args()
     ms.set_seed(a.seed)
@@ -101,11 +101,11 @@ def main() -> None:
         rec = {"step": done, "ms_per_step": round(dt, 4)}
         rec.update(population_stats(w))
         rec["us_activity"] = timed_activity(w)
-        for wb in [int(x) for x in a.wide_blocks.split(",") if x]:
-            native.hip().set_fused_wide_blocks(wb)
-            rec[f"us_activity_wb{wb}"] = timed_activity(w)
-        if a.wide_blocks:
-            native.hip().set_fused_wide_blocks(64)
+        for mode in [int(x) for x in a.modes.split(",") if x]:  # integrator launch modes (A/B)
+            native.hip().set_integrate_mode(mode)
+            rec[f"us_activity_mode{mode}"] = timed_activity(w)
+        if a.modes:
+            native.hip().set_integrate_mode(0)
         print(json.dumps(rec), flush=True)
     w.synchronize()
     print(json.dumps({"total_s": round(time.perf_counter() - t0, 2), "steps": a.steps}), flush=True)

@@ -80,7 +80,7 @@ for s in "$@"; do case "$s" in
   tpx) trace tpx 19 --map-size 1448 --cells 6250 --steps 20 --warmup 20 ;;
   tpxv) MARKER=msd::diffuse_corr_kernel MS_VIRTUAL_STRIPS=1 trace tpxv 19 --map-size 1448 --cells 6250 --steps 20 --warmup 20 ;;
 
-  evolved) run evolved 600 python scripts/evolved_probe.py --steps 500 --every 50 --wide-blocks 256,1024 ;;
+  evolved) run evolved 600 python scripts/evolved_probe.py --steps 500 --every 50 --modes 128 ;;
   sustained) run sustained 600 python bench.py --sustained --steps 200 --warmup 200 ;;
   overlap) run overlap 300 python scripts/overlap_probe.py 4096 50000 20 ;;
   *) echo "unknown step $s" ;;

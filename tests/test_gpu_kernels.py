@@ -818,7 +818,8 @@ def _integrate_modes(kin, X, modes=(0, 8)):
     return out
 
 
-@pytest.mark.parametrize("case", ["wl500", "wl3000", "syn20", "syn40", "syn64", "big_exponents", "syn64_big_exponents"])
+@pytest.mark.parametrize("case", ["wl500", "wl3000", "wl8000", "syn20", "syn40", "syn64", "big_exponents",
+                                  "syn64_big_exponents"])
 def test_register_integrator_matches_lds_integrator_bit_for_bit(case):
     """The register-resident launches (mode 0: cells with <= 32 / 64 active proteins and <= 16
     non-zero signals per protein; the rest through a 64-lane launch with 32 non-zeros per protein,
@@ -835,7 +836,7 @@ def test_register_integrator_matches_lds_integrator_bit_for_bit(case):
     ms.set_seed(2)
     torch.manual_seed(2)
     w = ms.World(chemistry=chem, map_size=64, device="cuda", seed=2)
-    size = 3000 if case == "wl3000" else 500
+    size = {"wl3000": 3000, "wl8000": 8000}.get(case, 500)
     w.spawn_cells(gen_genomes(300, size))
     kin = w.kinetics
     if case.endswith("big_exponents"):
@@ -849,6 +850,9 @@ def test_register_integrator_matches_lds_integrator_bit_for_bit(case):
     na = (kin.Vmax > 0).sum(1)
     if case == "wl3000":
         assert int(na.max()) > 32  # exercises the wide launch
+    if case == "wl8000":
+        # multi-group cells beyond two chunks (the speculative launch's wide role: 8 groups of 32)
+        assert int(na.max()) > 64 and int(((na > 64) & (na <= 256)).sum()) >= 10
     pos = w.cell_positions.long()
     X = torch.cat([w.cell_molecules, w.molecule_map[:, pos[:, 0], pos[:, 1]].T], dim=1).contiguous()
     out = _integrate_modes(kin, X, modes=(0, 8, 32, 64, 128, 256))
