@@ -110,9 +110,9 @@ def random_genomes(k: int, size: int, device) -> tuple[torch.Tensor, torch.Tenso
     return rows, torch.full((k,), size, dtype=torch.int32, device=device)
 
 
-# running means of divisions / starvation deaths; "after_kill": the population after the previous
-# step's kill (its division count is known at the next step's start: n_cells - after_kill)
-_CHEMOSTAT = {"divided": 0, "starved": 0, "steps": 0, "after_kill": None}
+# running means of divisions / starvation deaths, and the previous step's dilution (its kill and
+# division counts are only read at the next step's start, when the population is known anyway)
+_CHEMOSTAT = {"divided": 0, "starved": 0, "steps": 0, "excess": None}
 
 
 def _dilution_mask(n: int, k: int, device) -> torch.Tensor:
@@ -134,14 +134,20 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
 
     with ph("top_up"):
         n = world.n_cells
-        if _CHEMOSTAT["after_kill"] is not None:
-            # the previous step's divisions (issued without waiting for their count: the reference
-            # loop discards the pairs, and the count is long on the host by now)
-            d = max(0, n - _CHEMOSTAT["after_kill"])
-            _CHEMOSTAT["divided"] = (_CHEMOSTAT["divided"] + d) // 2 if _CHEMOSTAT["steps"] else d
+        last = world.__dict__.get("last_kill")
+        if _CHEMOSTAT["excess"] is not None and last is not None:
+            # the previous step's kill and divisions (issued without waiting for their counts: the
+            # reference loop discards the pairs, and the counts are long on the host by now)
+            n_before, after_kill = last
+            d = max(0, n - after_kill)
+            starved = max(0, n_before - after_kill - _CHEMOSTAT["excess"])
+            first = not _CHEMOSTAT["steps"]
+            _CHEMOSTAT["divided"] = d if first else (_CHEMOSTAT["divided"] + d) // 2
+            _CHEMOSTAT["starved"] = starved if first else (_CHEMOSTAT["starved"] + starved) // 2
             _CHEMOSTAT["steps"] += 1
-            _CHEMOSTAT["after_kill"] = None
+            _CHEMOSTAT["excess"] = None
             note("divided", d)
+            note("killed", n_before - after_kill)
         if n < n_target:
             world.spawn_cells(random_genomes(n_target - n, genome_size, world.cell_molecules.device))
             note("spawned", n_target - n)
@@ -157,26 +163,27 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
         dilute = _dilution_mask(n0, excess, world.cell_molecules.device) if excess > 0 else None
     with ph("activity"):
         world.enzymatic_activity()
-    with ph("kill"):
-        kill = world.cell_molecules[:, atp] < 1.0  # boolean masks: no index read-back
-        # chemostat dilution keeps the population at the configured size (the reference loop only
+    with ph("kill_replicate"):
+        # kill (ATP < 1) and replicate (ATP > 5: ATP -= 4, divide), performance/run_simulation.py:80-92.
+        # Boolean masks, no index read-back. The replicate mask is taken before the kill, over the
+        # survivors: the kill does not change their molecules, so it selects the reference's cells,
+        # and the killed cells spill unchanged molecules. Both go to the world in one call that never
+        # waits for the device (World.kill_divide_t).
+        # Chemostat dilution keeps the population at the configured size (the reference loop only
         # tops up; on a 4096^2 map the population would otherwise grow ~6x within 25 steps): random
-        # cells are removed together with the starving ones, in the same kill_cells call, so that
-        # after the divisions that follow the population is back at n_target plus a small margin (the
-        # previous step's divisions and starvation deaths are the estimates). The margin keeps the
-        # next step's top-up (a spawn) rare; activity always runs on >= n_target cells.
+        # cells are removed together with the starving ones, so that after the divisions that follow
+        # the population is back at n_target plus a small margin (the previous steps' divisions and
+        # starvation deaths are the estimates). The margin keeps the next step's top-up (a spawn)
+        # rare; activity always runs on >= n_target cells.
+        a = world.cell_molecules[:, atp]
+        kill = a < 1.0
         if dilute is not None:
             kill |= dilute
             note("diluted", excess)
-        world.kill_cells(kill)
-        _CHEMOSTAT["after_kill"] = world.n_cells
-        starved = max(0, n0 - world.n_cells - max(excess, 0))
-        _CHEMOSTAT["starved"] = (_CHEMOSTAT["starved"] + starved) // 2 if _CHEMOSTAT["steps"] else starved
-        note("killed", n0 - world.n_cells)
-    with ph("replicate"):
-        repl = world.cell_molecules[:, atp] > 5.0
-        world.cell_molecules[:, atp] -= 4.0 * repl
-        world.divide_cells_t(repl, lazy=True)
+        repl = (a > 5.0) & ~kill
+        a -= 4.0 * repl
+        world.kill_divide_t(kill, repl)
+        _CHEMOSTAT["excess"] = max(excess, 0)
     with ph("recombinate"):
         world.recombinate_cells()
     with ph("mutate"):
@@ -217,7 +224,7 @@ def _prime_rare_paths(chem, device, mdt, genome_size: int) -> None:
     w._genomes.collect()
     torch.cuda.synchronize()
     del w
-    _CHEMOSTAT.update(divided=0, starved=0, steps=0, after_kill=None)
+    _CHEMOSTAT.update(divided=0, starved=0, steps=0, excess=None)
 
 
 def _self_launch(a) -> int | None:

@@ -9,6 +9,7 @@
 // call. Compactions gather into spare buffers and copy back (a few MB at most) instead of swapping,
 // so buffer addresses stay fixed between reallocations and the prebuilt row plans stay valid.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <algorithm>
 #include <stdexcept>
@@ -26,6 +27,11 @@ int divide_mask_dev(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo
                     uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result, int rounds, uint64_t seed,
                     uint64_t call, uintptr_t wins, uintptr_t dcount, long long n0, int m, uintptr_t par,
                     uintptr_t cell_mols, uintptr_t divisions, uintptr_t lifetimes, uintptr_t stream);
+int divide_mask_dev_at(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap,
+                       uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result,
+                       int rounds, uint64_t seed, uint64_t call, uintptr_t wins, uintptr_t dcount, long long n0,
+                       uintptr_t n0_dev, int m, uintptr_t par, uintptr_t cell_mols, uintptr_t divisions,
+                       uintptr_t lifetimes, uintptr_t stream);
 
 struct FastWorld {
   // local map geometry (a strip of a decomposed world: halo rows, no wrap)
@@ -44,6 +50,7 @@ struct FastWorld {
   uintptr_t cell_map = 0;           // occupancy bytes (4-byte padded)
   // scratch, `cap` entries each (claim: R * C)
   uintptr_t sel = 0, dcount = 0, pending = 0, cand = 0, result = 0, wins = 0, par = 0, claim = 0, dcount2 = 0;
+  uintptr_t dmask = 0;  // (cap bytes) the division mask of kill_divide, compacted with the survivors
   int rounds = 8;
   // prebuilt row plans: compaction into the spares, copy back, children cloned from parents
   RowArgs fwd{}, back{}, clone{};
@@ -116,6 +123,40 @@ int fast_divide(const FastWorld& f, int n, uintptr_t mask, uint64_t seed, uint64
                                    f.div, f.life, stream);
   launch_row_args(f.clone, n, P_<int>(f.dcount2), P_<int64_t>(f.par), nullptr, n, S_(stream));
   return slot;
+}
+
+// The division mask (over the n cells before the kill) compacted with the survivors: dmask[i] =
+// mask[sel[i]] for the dn survivors, 0 up to n (the rows past the survivors are stale).
+__global__ void __launch_bounds__(256) compact_mask_kernel(int n, const int* dn, const int64_t* sel, const uint8_t* mask,
+                                                           uint8_t* dmask) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  dmask[i] = i < *dn ? mask[sel[i]] : (uint8_t)0;
+}
+
+// kill_cells(kill) then divide_cells(divide restricted to the survivors) without a synchronisation
+// in between: the kill as fast_kill, the division mask compacted with the survivors, the division
+// over it with the children appended after the device survivor count (rows dn..). Both masks are
+// uint8 over the same n cells. Returns the status slots of the survivor count and of the winner
+// count; the population is their sum.
+std::pair<int, int> fast_kill_divide(const FastWorld& f, int n, uintptr_t kill, uintptr_t divide, uintptr_t map,
+                                     int mdt, uintptr_t corr, uint64_t seed, uint64_t call, uintptr_t stream) {
+  if (!f.ready) throw std::invalid_argument("fast_kill_divide: descriptor not finalized");
+  if (n <= 0 || 2ll * n > f.cap) throw std::invalid_argument("fast_kill_divide: 2 x cell count exceeds the capacity");
+  if (!f.dmask) throw std::invalid_argument("fast_kill_divide: no mask scratch");
+  hipStream_t s = S_(stream);
+  spill_free_mask(n, f.m, kill, f.pos, f.R, f.C, f.mols, map, f.cell_map, mdt, corr, stream);
+  const int slot_k = select_indices_async(n, 1 /* clear */, kill, f.sel, 0, f.dcount, stream);
+  const int* dn = P_<int>(f.dcount);
+  launch_row_args(f.fwd, n, dn, P_<int64_t>(f.sel), nullptr, 0, s);
+  launch_row_args(f.back, n, dn, nullptr, nullptr, 0, s);
+  compact_mask_kernel<<<cdiv(n, 256), 256, 0, s>>>(n, dn, P_<int64_t>(f.sel), P_<uint8_t>(divide), P_<uint8_t>(f.dmask));
+  MS_LAUNCH_CHECK();
+  const int slot_d = divide_mask_dev_at(n, f.dmask, f.pos, f.R, f.C, f.r_lo, f.r_hi, f.wrap, f.cell_map, f.pending,
+                                        f.cand, f.claim, f.result, f.rounds, seed, call, f.wins, f.dcount2, 0, f.dcount,
+                                        f.m, f.par, f.mols, f.div, f.life, stream);
+  launch_row_args(f.clone, n, P_<int>(f.dcount2), P_<int64_t>(f.par), nullptr, 0, s, dn);
+  return {slot_k, slot_d};
 }
 
 // ---- the strip protocol of a decomposed world's divide_cells over a mask (parallel/dist_world.py),
@@ -253,10 +294,13 @@ void bind_fast(pybind11::module_& m) {
       .def_readwrite("par", &FastWorld::par)
       .def_readwrite("claim", &FastWorld::claim)
       .def_readwrite("dcount2", &FastWorld::dcount2)
+      .def_readwrite("dmask", &FastWorld::dmask)
       .def_readwrite("rounds", &FastWorld::rounds)
       .def("finalize", &FastWorld::finalize);
   m.def("fast_kill", &fast_kill, "kill_cells(mask) in one call (status slot of the survivor count)");
   m.def("fast_divide", &fast_divide, "divide_cells(mask) in one call (status slot of the winner count)");
+  m.def("fast_kill_divide", &fast_kill_divide,
+        "kill_cells(kill) + divide_cells(divide & survivors) in one call (status slots of both counts)");
   m.def("fast_dist_divide_a", &fast_dist_divide_a, "strip divide protocol up to the synchronisation");
   m.def("fast_dist_divide_b", &fast_dist_divide_b, "strip divide protocol after the synchronisation");
 }

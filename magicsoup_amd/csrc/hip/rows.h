@@ -24,6 +24,7 @@ struct RowArgs {
   RowDesc d[kMaxDescs];
   int nd, n;
   long long dst_off;        // added to every destination row
+  const int* dst_base;      // optional device value, also added to every destination row
   const int* dn;            // optional device row count (<= n; n is then the capacity)
   const int64_t* src_rows;  // nullptr: identity
   const int64_t* dst_rows;  // nullptr: identity
@@ -35,6 +36,6 @@ using RowDescTuple = std::tuple<uintptr_t, uintptr_t, long long, long long, long
 RowArgs make_row_args(const std::vector<RowDescTuple>& descs, size_t first = 0, size_t* next = nullptr);
 // One launch of a prebuilt plan over rows [0, n) (device count dn optional).
 void launch_row_args(const RowArgs& plan, int n, const int* dn, const int64_t* src_rows, const int64_t* dst_rows,
-                     long long dst_off, hipStream_t s);
+                     long long dst_off, hipStream_t s, const int* dst_base = nullptr);
 
 }  // namespace msd

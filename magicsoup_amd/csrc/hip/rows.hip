@@ -35,10 +35,11 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(RowArgs a) {
   const unsigned n_eff = (unsigned)(a.dn ? min(*a.dn, a.n) : a.n);
   const unsigned total = n_eff * (unsigned)d.units;
   if (blockIdx.x * blockDim.x >= total) return;
+  const long long off = a.dst_off + (a.dst_base ? (long long)*a.dst_base : 0ll);
   if (d.unit == 16)
-    copy_units<uint4>(d, total, a.src_rows, a.dst_rows, a.dst_off);
+    copy_units<uint4>(d, total, a.src_rows, a.dst_rows, off);
   else
-    copy_units<uint32_t>(d, total, a.src_rows, a.dst_rows, a.dst_off);
+    copy_units<uint32_t>(d, total, a.src_rows, a.dst_rows, off);
 }
 
 RowArgs make_row_args(const std::vector<RowDescTuple>& descs, size_t first, size_t* next) {
@@ -67,7 +68,7 @@ RowArgs make_row_args(const std::vector<RowDescTuple>& descs, size_t first, size
 }
 
 void launch_row_args(const RowArgs& plan, int n, const int* dn, const int64_t* src_rows, const int64_t* dst_rows,
-                     long long dst_off, hipStream_t s) {
+                     long long dst_off, hipStream_t s, const int* dst_base) {
   if (n <= 0 || plan.nd == 0) return;
   RowArgs a = plan;
   a.n = n;
@@ -75,6 +76,7 @@ void launch_row_args(const RowArgs& plan, int n, const int* dn, const int64_t* s
   a.src_rows = src_rows;
   a.dst_rows = dst_rows;
   a.dst_off = dst_off;
+  a.dst_base = dst_base;
   long long widest = 0;
   for (int q = 0; q < a.nd; ++q) widest = std::max(widest, (long long)n * a.d[q].units);
   if (widest >= (1ll << 31)) throw std::invalid_argument("gather_rows: too many units per tensor");

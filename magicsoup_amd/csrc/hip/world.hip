@@ -48,9 +48,11 @@ __global__ void __launch_bounds__(256) split_cells_kernel(int k, int m, const in
 // row gather would copy are all overwritten here, so only genomes / labels / parameter-row map are
 // gathered). Grid-stride over (*dn) x m.
 __global__ void __launch_bounds__(256) divide_commit_kernel(const int* dn, const int64_t* wins, const long long* result,
-                                                            int C, long long n0, int m, int64_t* par, int32_t* pos,
-                                                            float* cell_mols, int32_t* divisions, int32_t* lifetimes) {
+                                                            int C, long long n0, const int* n0_dev, int m, int64_t* par,
+                                                            int32_t* pos, float* cell_mols, int32_t* divisions,
+                                                            int32_t* lifetimes) {
   const long long total = (long long)(*dn) * m;
+  if (n0_dev) n0 += *n0_dev;  // (children after a device-side row count: a kill issued just before)
   for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
     const long long i = t / m;
     const int j = (int)(t - i * m);
@@ -724,10 +726,12 @@ int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, ui
 // divide_cells over a mask, everything issued before the count is known: cooperative placement
 // over the mask, winners (result >= 0) compacted with the count on the device and in a pinned
 // status slot (returned), then the commit into rows n0.. (capacity for n more rows is the caller's).
-int divide_mask_dev(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t cell_map,
-                    uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result, int rounds, uint64_t seed,
-                    uint64_t call, uintptr_t wins, uintptr_t dcount, long long n0, int m, uintptr_t par,
-                    uintptr_t cell_mols, uintptr_t divisions, uintptr_t lifetimes, uintptr_t stream) {
+// (n0_dev: optional device int added to n0 -- the survivor count of a kill issued just before)
+int divide_mask_dev_at(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap,
+                       uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result,
+                       int rounds, uint64_t seed, uint64_t call, uintptr_t wins, uintptr_t dcount, long long n0,
+                       uintptr_t n0_dev, int m, uintptr_t par, uintptr_t cell_mols, uintptr_t divisions,
+                       uintptr_t lifetimes, uintptr_t stream) {
   if (n <= 0) throw std::invalid_argument("divide_mask_dev: no cells");
   const Geom g = geom(R, C, r_lo, r_hi, wrap);
   hipStream_t s = S_(stream);
@@ -736,11 +740,20 @@ int divide_mask_dev(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo
     place_rounds_launches(n, 0, mask, pos, g, false, cell_map, pending, cand, claim, result, rounds, seed, call, s);
   const int slot = select_indices_async(n, 3 /* int64 >= 0 */, result, wins, 0, dcount, stream);
   const unsigned grid = std::min<unsigned>(cdiv((long long)n * m, 256), 512u);
-  divide_commit_kernel<<<grid, 256, 0, s>>>(P_<int>(dcount), P_<int64_t>(wins), P_<long long>(result), C, n0, m,
+  divide_commit_kernel<<<grid, 256, 0, s>>>(P_<int>(dcount), P_<int64_t>(wins), P_<long long>(result), C, n0,
+                                            n0_dev ? P_<int>(n0_dev) : nullptr, m,
                                             P_<int64_t>(par), P_<int32_t>(pos), P_<float>(cell_mols),
                                             P_<int32_t>(divisions), P_<int32_t>(lifetimes));
   MS_LAUNCH_CHECK();
   return slot;
+}
+
+int divide_mask_dev(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t cell_map,
+                    uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result, int rounds, uint64_t seed,
+                    uint64_t call, uintptr_t wins, uintptr_t dcount, long long n0, int m, uintptr_t par,
+                    uintptr_t cell_mols, uintptr_t divisions, uintptr_t lifetimes, uintptr_t stream) {
+  return divide_mask_dev_at(n, mask, pos, R, C, r_lo, r_hi, wrap, cell_map, pending, cand, claim, result, rounds, seed,
+                            call, wins, dcount, n0, 0, m, par, cell_mols, divisions, lifetimes, stream);
 }
 
 void place_collect(int k, uintptr_t wins, uintptr_t cells, uintptr_t result, int C, uintptr_t par, uintptr_t npos,

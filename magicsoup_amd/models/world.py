@@ -52,6 +52,9 @@ _PIPELINE_SAFE_OPS = frozenset({"mutate_cells", "recombinate_cells", "diffuse_mo
 # (divide_cells_t(lazy=True)) is still on its way to the host: they queue genome chains or only touch
 # the map / all capacity rows; diffuse_molecules adopts the count after its stencil launch
 _COUNT_SAFE_OPS = frozenset({"mutate_cells", "recombinate_cells", "degrade_molecules", "diffuse_molecules"})
+# (kill_divide's kill leaves rows past the survivors stale and children after them: until its counts
+# are adopted only the ops above may run -- the degradation scales all capacity rows, which is
+# harmless for stale ones)
 _CHECK_ENV = os.environ.get("MS_CHECK_INVARIANTS") == "1"
 _DEFER_ENV = os.environ.get("MS_DEFER_GENOME_OPS", "1")
 # The genome chains flushed onto the side stream (World._flush_deferred) are joined into the compute
@@ -539,6 +542,15 @@ class World:
         # (only the division's work: not what was queued since, e.g. a diffusion stencil; with
         # communicators alive a peer failure raises instead of hanging)
         hip_ops.guarded_sync(ev)
+        if isinstance(slot, tuple):  # kill_divide_t: survivors, then the winners appended after them
+            n_k = int(hip_ops._m().status_read(slot[0])[0])
+            k = int(hip_ops._m().status_read(slot[1])[0])
+            d["_count_pending"] = None
+            d["last_kill"] = (n0, n_k)
+            hip_ops.check_placement()
+            if n_k + k != n0:
+                self._adopt_count(n_k + k)
+            return
         k = int(hip_ops._m().status_read(slot)[0])
         # (the pending entry stays until the count is read: a failure above leaves it for a retry
         # instead of a world whose device rows and host count disagree)
@@ -939,7 +951,7 @@ class World:
             d["_claim_map"] = claim
         bufs = {name: torch.empty(cap, dtype=dt, device=dev) for name, dt in (
             ("sel", torch.int64), ("pending", torch.uint8), ("cand", torch.int64), ("result", torch.int64),
-            ("wins", torch.int64), ("par", torch.int64))}
+            ("wins", torch.int64), ("par", torch.int64), ("dmask", torch.uint8))}
         bufs["dcount"] = torch.zeros(4, dtype=torch.int32, device=dev)
         fw = hip_ops._m().FastWorld()
         fw.R, fw.C, fw.r_lo, fw.r_hi, fw.wrap, fw.m, fw.cap = R, C, r_lo, r_hi, int(wrap), self.n_molecules, cap
@@ -958,6 +970,7 @@ class World:
         fw.sel, fw.pending, fw.cand, fw.result, fw.wins, fw.par = (bufs[k].data_ptr() for k in (
             "sel", "pending", "cand", "result", "wins", "par"))
         fw.dcount, fw.dcount2 = bufs["dcount"].data_ptr(), bufs["dcount"].data_ptr() + 8
+        fw.dmask = bufs["dmask"].data_ptr()
         fw.claim = claim.data_ptr()
         fw.rounds = hip_ops._PLACE_ROUNDS
         fw.finalize()
@@ -982,6 +995,43 @@ class World:
                 gc.enable()
         self._genomes.set_rows(rows, torch.from_numpy(arr), torch.from_numpy(lens))
         self._update_params_rows(rows.to(self.device))
+
+    @_op("kill_divide")
+    def kill_divide_t(self, kill_mask: torch.Tensor, divide_mask: torch.Tensor) -> None:
+        """``kill_cells(kill_mask)`` followed by ``divide_cells_t(divide_mask[~kill_mask], lazy=True)``
+        in one call that never waits for the device: both masks are boolean over the current cells
+        (the reference loop's kill and replicate steps, ``performance/run_simulation.py:80-92``, with
+        the replicate mask taken before the kill -- the kill does not change a survivor's molecules,
+        so it selects the same cells). On the GPU the survivors are compacted, the division mask with
+        them, and the children appended after the device-side survivor count; both counts reach the
+        host like a lazy division's (:meth:`divide_cells_t`). ``last_kill`` then holds the
+        ``(cells before, survivors)`` of the last such call."""
+        n = self.n_cells
+        kill_mask = kill_mask.to(self.device, torch.bool)
+        divide_mask = divide_mask.to(self.device, torch.bool)
+        if kill_mask.numel() != n or divide_mask.numel() != n:
+            raise ValueError(f"kill_divide_t: masks of {kill_mask.numel()} / {divide_mask.numel()} cells for {n}")
+        if n == 0:
+            return
+        if not kill_mask.is_cuda or getattr(self, "_exchange_map_halo", None) is not None:
+            # CPU worlds, and a decomposed world's strips (their division is a collective protocol):
+            # the two calls
+            div = divide_mask[~kill_mask]
+            self.kill_cells(kill_mask)
+            self.__dict__["last_kill"] = (n, self.n_cells)
+            if self.n_cells > 0:
+                self.divide_cells_t(div, lazy=kill_mask.is_cuda)
+            return
+        from magicsoup_amd.ops import hip_ops
+        from magicsoup_amd.ops.streams import NEvent
+
+        fw = self._fast_world(2 * n)
+        mm, corr = hip_ops.map_for_pixels(self)
+        seed, call = hip_ops._rng()
+        slots = hip_ops._m().fast_kill_divide(fw, n, kill_mask.view(torch.uint8).contiguous().data_ptr(),
+                                              divide_mask.view(torch.uint8).contiguous().data_ptr(), mm.data_ptr(),
+                                              hip_ops._mdt(mm), hip_ops._p(corr), seed, call, hip_ops._stream())
+        self.__dict__["_count_pending"] = (n, tuple(slots), NEvent().record())
 
     @_op("kill_cells")
     def kill_cells(self, cell_idxs=None):

@@ -1282,3 +1282,49 @@ def test_gpu_step_loop_is_deterministic():
     assert a["n"] > 500 and int(a["divisions"].sum()) > 0
     bad = [key for key in a if not (torch.equal(a[key], b[key]) if isinstance(a[key], torch.Tensor) else a[key] == b[key])]
     assert not bad, bad
+
+
+def test_lazy_kill_divide_matches_synchronous_calls():
+    """World.kill_divide_t on the GPU (kill, division mask compacted with the survivors, children
+    after the device survivor count, no synchronisation) evolves the world bit for bit as
+    kill_cells + divide_cells_t(mask[~kill]) do; ops queued meanwhile run against the device state."""
+    base = _world("cuda", map_size=64, n=1500, s=400, seed=8)
+    base.synchronize()
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+
+    def run(fused: bool):
+        w = copy.deepcopy(base)
+        ms.set_seed(3)
+        torch.manual_seed(3)
+        sizes = []
+        for _ in range(5):
+            w.enzymatic_activity()
+            a = w.cell_molecules[:, atp]
+            kill = a < 1.0
+            repl = (a > 3.0) & ~kill
+            a -= 2.0 * repl
+            if fused:
+                w.kill_divide_t(kill, repl)
+                assert w.__dict__.get("_count_pending") is not None
+            else:
+                w.kill_cells(kill)
+                w.divide_cells_t(repl[~kill].clone())
+            w.recombinate_cells(p=1e-4)
+            w.mutate_cells(p=1e-3)
+            w.degrade_molecules()
+            w.diffuse_molecules()
+            assert w.__dict__.get("_count_pending") is None
+            w.increment_cell_lifetimes()
+            sizes.append(w.n_cells)
+        w.synchronize()
+        w.check_invariants()
+        state = {k: getattr(w, k).clone() for k in ("cell_molecules", "cell_positions", "cell_lifetimes",
+                                                     "cell_divisions", "molecule_map", "cell_map")}
+        state["Vmax"] = w.kinetics.Vmax.clone()
+        return sizes, list(w.cell_genomes), list(w.cell_labels), state
+
+    s0, g0, l0, st0 = run(False)
+    s1, g1, l1, st1 = run(True)
+    assert s0 == s1 and g0 == g1 and l0 == l1
+    for k in st0:
+        assert torch.equal(st0[k], st1[k]), k

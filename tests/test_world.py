@@ -609,3 +609,37 @@ def test_world_unpickler_refuses_constructor_opcodes(tmp_path, payload):
     (tmp_path / "world.pkl").write_bytes(payload)
     with pytest.raises(pickle.UnpicklingError):
         ms.World.from_file(tmp_path)
+
+
+def test_kill_divide_matches_kill_then_divide():
+    """World.kill_divide_t(kill, divide) == kill_cells(kill) + divide_cells_t(divide[~kill]) (the
+    bench loop's fused call), and ``last_kill`` records the counts."""
+    import copy
+
+    from magicsoup_amd.examples.wood_ljungdahl import CHEMISTRY
+
+    ms.set_seed(5)
+    torch.manual_seed(5)
+    base = ms.World(chemistry=CHEMISTRY, map_size=24)
+    base.spawn_cells([ms.random_genome(300) for _ in range(150)])
+    base.enzymatic_activity()
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    a = base.cell_molecules[:, atp]
+    kill = a < torch.quantile(a, 0.3)
+    div = (a > torch.quantile(a, 0.5)) & ~kill
+    w1, w2 = copy.deepcopy(base), copy.deepcopy(base)
+    ms.set_seed(9)
+    w1.kill_divide_t(kill, div)
+    ms.set_seed(9)
+    n = w2.n_cells
+    w2.kill_cells(kill)
+    after = w2.n_cells
+    w2.divide_cells_t(div[~kill])
+    assert w1.last_kill == (n, after)
+    assert w1.n_cells == w2.n_cells > after
+    for k in ("cell_molecules", "cell_positions", "cell_lifetimes", "cell_divisions", "molecule_map", "cell_map"):
+        assert torch.equal(getattr(w1, k), getattr(w2, k)), k
+    assert list(w1.cell_genomes) == list(w2.cell_genomes)
+    w1.check_invariants()
+    with pytest.raises(ValueError):
+        w1.kill_divide_t(kill, div)  # masks of the old population
