@@ -74,6 +74,8 @@ def _args():
     ap.add_argument("--profile-phases", action="store_true", help="print per-phase times to stderr")
     ap.add_argument("--step-times", action="store_true", help="print each timed step's wall time to stderr "
                     "(synchronises after every step)")
+    ap.add_argument("--memory-report", action="store_true", help="print the world's device bytes (utils.memory."
+                    "measured) against the model (utils.memory.footprint) to stderr (default for --preset hbm)")
     ap.add_argument("--phase-sync", action="store_true", help="with --profile-phases: drain the GPU at phase "
                     "boundaries (for attributing a kernel trace to phases; slows the step)")
     a = ap.parse_args()
@@ -324,11 +326,17 @@ def main():
     if torch.cuda.is_available():
         # (a plain world on this rank's device: no collectives; the kernels it warms are per process)
         _prime_rare_paths(chem, device, mdt, a.genome_size)
-    todo = a.cells // max(1, world_size if distributed else 1)
+    total = todo = a.cells // max(1, world_size if distributed else 1)
     while todo > 0:  # (batches: a multi-million-cell population's random genomes stay a few hundred MB)
         k = min(todo, 500_000)
         world.spawn_cells(random_genomes(k, a.genome_size, device))
         todo -= k
+        if todo > 0 and k == total - todo:
+            # the first batch fixed the protein dimension: the whole population's storage at once
+            # (the bench's chemostat holds it at ~1.03x the target)
+            from magicsoup_amd.utils import memory
+
+            world.reserve_cells(int(total * 1.05), int(a.genome_size * 1.1), memory.protein_slots(a.genome_size))
     setup_s = time.time() - t0
 
     def sync():
@@ -363,7 +371,20 @@ def main():
     sync()
     gc.enable()
     if per_step and rank == 0:
-        print(json.dumps({"step_ms": per_step}), file=sys.stderr)
+        srt = sorted(per_step)
+        print(json.dumps({"step_ms": per_step, "median_ms": srt[len(srt) // 2], "max_ms": srt[-1]}), file=sys.stderr)
+    if (a.memory_report or a.preset == "hbm") and torch.cuda.is_available() and rank == 0:
+        from magicsoup_amd.utils import memory
+
+        held = memory.measured(world)["bytes"]
+        fp = memory.footprint(a.map_size, len(chem.molecules), a.cells, a.map_dtype, a.genome_size,
+                              ranks=world_size if distributed else 1)
+        print(json.dumps({"memory": {"measured_gib": round(held / 2**30, 2), "model_gib": round(fp["total"] / 2**30, 2),
+                                     "model_over_measured": round(fp["total"] / held, 3),
+                                     "allocated_gib": round(torch.cuda.memory_allocated() / 2**30, 2),
+                                     "reserved_gib": round(torch.cuda.memory_reserved() / 2**30, 2),
+                                     "parts_gib": {k: round(v / 2**30, 2) for k, v in fp.items()
+                                                   if isinstance(v, int) and v > (1 << 20)}}}), file=sys.stderr)
     dt = time.perf_counter() - t0
     if distributed:
         t = torch.tensor([dt], dtype=torch.float64, device=device)

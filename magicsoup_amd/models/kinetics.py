@@ -806,6 +806,29 @@ class Kinetics:
         d["_ncells"] = d["_nrows"] = k
         self._restamp(ok)
 
+    def reserve_cells(self, n: int) -> None:
+        """Row capacity of the parameter storage for ``n`` cells plus the usual spare rows, allocated
+        at once (no-op if it holds them already, or before the first proteome fixed the protein
+        dimension). Growing a large population in batches otherwise re-allocates the storage by
+        1.5x each time, with the old and the new storage alive together (an HBM-sized world would
+        need 2.5x its parameter bytes for a moment)."""
+        store = self._store
+        if not store or self._P() == 0:
+            return
+        cap = min(int(t.size(0)) for t in store.values())
+        row_bytes = sum(t[:1].numel() * t.element_size() for t in store.values())
+        want = n + _spare_rows(n, row_bytes)
+        if want <= cap:
+            return
+        self._sync()
+        ok = self._pack_ok()
+        for name, t in list(store.items()):
+            nb = torch.empty(want, *t.shape[1:], dtype=t.dtype, device=t.device)
+            nb[:cap] = t[:cap]  # (every row: the cell -> row map may point anywhere below cap)
+            store[name] = nb
+        self.__dict__.pop("_spare", None)
+        self._restamp(ok)
+
     def increase_max_cells(self, by_n: int, zero: bool = True):
         """Append ``by_n`` cells (parameters zero-filled unless the caller writes them all)."""
         if by_n <= 0:

@@ -564,6 +564,29 @@ class World:
         arena.append_strings(strs)
 
     # ------------------------------------------------------------------ capacity helpers
+    def reserve_cells(self, n: int, genome_len: int | None = None, proteins: int | None = None) -> None:
+        """Allocate capacity for a population of ``n`` cells at once: per-cell columns, label and
+        genome-pool bookkeeping, genome bytes (``genome_len`` nt per cell, 1 byte each, with the
+        pool grows its own headroom) and -- once a first proteome has fixed the protein dimension -- the
+        kinetics parameter rows, ``proteins`` slots wide (utils.memory.protein_slots: room for the
+        longer proteomes recombination creates, so the storage never widens). Large worlds (utils.memory.plan: hundreds of GB) should be grown
+        this way: batch-wise growth re-allocates each buffer 1.5x at a time with the old and the new
+        copy alive together."""
+        self._reconcile()
+        self._reserve(n)
+        self._genomes.reserve(n)
+        self._labels.reserve(n)
+        if genome_len and isinstance(self._genomes, PoolArena):
+            self._genomes.ensure(max(0, n - self.n_cells) * ((int(genome_len) + 15) // 16 * 16))
+        if self._genomes.data.is_cuda and self.n_cells and self.kinetics._P():
+            # the GPU's compact parameter storage (packed words + Kmr) before the reservation: a
+            # first large batch built the dense reference layout (2.5x the bytes per row)
+            self.kinetics._packed_params()
+            self.kinetics._enter_slot_mode()
+            if proteins and proteins > self.kinetics._P():
+                self.kinetics.increase_max_proteins(int(proteins))
+        self.kinetics.reserve_cells(n)
+
     def _reserve(self, n_new: int) -> None:
         for col in self._cols.values():
             col.reserve(self.n_cells, n_new)
@@ -1272,10 +1295,17 @@ class World:
                 return
         self._update_params_rows(rows)
 
+    _PARAM_CHUNK = 1 << 18  # cells per translation + build: the token tensor is (k, P, D, 5) int32
+
     def _update_params_rows(self, rows: torch.Tensor) -> None:
-        """Translate the genomes of ``rows`` and rebuild their kinetic parameters."""
+        """Translate the genomes of ``rows`` and rebuild their kinetic parameters (in chunks: the
+        token tensor of a multi-million-cell batch would take tens of GB)."""
         rows = rows.to(self.device, torch.long)
         if rows.numel() == 0:
+            return
+        if rows.numel() > self._PARAM_CHUNK:
+            for c0 in range(0, int(rows.numel()), self._PARAM_CHUNK):
+                self._update_params_rows(rows[c0 : c0 + self._PARAM_CHUNK])
             return
         tokens, nprots = world_ops.translate(self, rows)
         P = int(tokens.size(1))
@@ -1410,7 +1440,17 @@ class World:
         if init == "zeros":
             return torch.zeros(*shape, dtype=self.map_dtype, device=self.device)
         if init == "randn":
-            return (torch.randn(*shape, dtype=torch.float32, device=self.device) + 10.0).abs().to(self.map_dtype)
+            if self.map_dtype == torch.float32 and n * shape[1] * shape[2] <= (1 << 28):
+                return (torch.randn(*shape, dtype=torch.float32, device=self.device) + 10.0).abs()
+            # |N(10, 1)| drawn in chunks of rows: an HBM-sized map (hundreds of GB in fp16) has no
+            # room for full-size fp32 temporaries
+            mm = torch.empty(*shape, dtype=self.map_dtype, device=self.device)
+            rows = max(1, (1 << 26) // shape[2])
+            for i in range(n):
+                for r in range(0, shape[1], rows):
+                    blk = mm[i, r : r + rows]
+                    blk.copy_((torch.randn(blk.shape, dtype=torch.float32, device=self.device) + 10.0).abs_())
+            return mm
         raise ValueError(f"Didnt recognize mol_map_init={init}. Should be one of: 'zeros', 'randn'.")
 
     def _get_permeate(self, mol_perm_rate: float) -> float:

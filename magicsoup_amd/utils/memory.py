@@ -25,7 +25,8 @@ for order-preserving compactions):
 * the cell -> parameter-row map (int64) and the division / kill scratch of the native fast path;
 * parameter rows in compact storage: per (protein, signal) the packed N/Nf/Nb/A word (int32) and
   Kmr (fp32), per protein Vmax/Kmf/Kmb/Ke (4 fp32), for the live cells plus the spare rows fresh
-  builds take (``models/kinetics.py`` ``_spare_rows``: up to 3n within 8 GiB).
+  builds take (``models/kinetics.py`` ``_spare_rows``: up to 3n within 8 GiB);
+* the ops' per-cell scratch (integrator snapshots, neighbour keys, placement lists).
 """
 from __future__ import annotations
 
@@ -43,15 +44,29 @@ MI355X_HBM = 288e9  # bytes of HBM3E per GPU
 
 def proteins_per_genome(genome_len: int) -> int:
     """Protein slots ``P`` (the longest proteome of the population) for random genomes of
-    ``genome_len`` nt: about one protein per 21 nt at the tail of the distribution (24 slots at
-    500 nt, 40 at 1 kbp; SURVEY.md §2.3 measured p_max)."""
-    return max(8, int(math.ceil(genome_len / 21.0)))
+    ``genome_len`` nt: about one protein per 16 nt at the tail of a large population's distribution
+    (31 slots at 500 nt: the longest proteome among 500k random 500 nt genomes, measured on MI355X,
+    profiles/r5/hbm_probe.log; SURVEY.md §2.3 measured 24 at 500 nt and 40 at 1 kbp for ~10k
+    cells -- the tail grows with the population)."""
+    return max(8, int(math.ceil(genome_len / 16.0)))
+
+
+def protein_slots(genome_len: int) -> int:
+    """Protein dimension of the parameter storage for an evolving population of random genomes of
+    ``genome_len`` nt: recombination joins fragments of genomes, so the longest proteome of a grown
+    population far exceeds that of the random ones -- the flagship's storage widens from 45 to 82
+    slots within 100 steps (profiles/r5/evolved_probe_500.log), a 5M-cell world's to 148 within 5
+    steps (profiles/r5/hbm_widen.log) -- plus the storage's 50 % widening headroom
+    (World._update_params_rows). World.reserve_cells(proteins=...) takes it up front, so a large
+    world never re-allocates its parameter storage to widen it (old and new copy alive together)."""
+    return 5 * proteins_per_genome(genome_len)
 
 
 def footprint(map_size: int, n_molecules: int, cells: int, map_dtype=torch.float32, genome_len: int = 500,
               p_max: int | None = None, ranks: int = 1) -> dict:
     """Modelled device bytes of one rank of a GPU world (``ranks`` > 1: a strip of a
-    domain-decomposed ``map_size``² world holding ``cells / ranks`` cells). Returns the per-part
+    domain-decomposed ``map_size``² world holding ``cells / ranks`` cells); ``p_max``: the protein
+    dimension of the parameter storage (default :func:`protein_slots`). Returns the per-part
     breakdown and the total in bytes."""
     m = int(n_molecules)
     es = _ESIZE[map_dtype]
@@ -59,8 +74,7 @@ def footprint(map_size: int, n_molecules: int, cells: int, map_dtype=torch.float
     pix = rows * map_size
     n = int(math.ceil(cells / ranks))
     cap = int(n * _CAP)
-    P = p_max if p_max is not None else proteins_per_genome(genome_len)
-    P = P + max(8, P // 2)  # the storage's protein dimension grows with headroom (World._update_params_rows)
+    P = p_max if p_max is not None else protein_slots(genome_len)
     s = 2 * m
     row_bytes = P * s * 8 + P * 16  # packed word + Kmr per (protein, signal); Vmax/Kmf/Kmb/Ke per protein
     spare_rows = max(n // 8, min(3 * n, _KIN_SPARE_BUDGET // max(row_bytes, 1)), 1024)
@@ -74,6 +88,10 @@ def footprint(map_size: int, n_molecules: int, cells: int, map_dtype=torch.float
         "label_arena": cap * (16 + 4) * 2,
         "row_maps": cap * (8 * 2 + 6 * 8 + 1),
         "kinetics_rows": int((n + spare_rows) * row_bytes * 1.0),
+        # per-cell scratch of the ops (ops/hip_ops.py): the integrator's two candidate snapshots
+        # (5 states of s signals each) and cell lists, the speculative activity's saved state, the
+        # neighbour-slot keys / event counts, the placement and division lists
+        "op_scratch": n * (2 * 5 * s * 4 + 13 + 2 * m * 4 + 8 * 8 + 2 * 8 * 4 + 25),
     }
     parts["total"] = sum(parts.values())
     parts.update(map_size=map_size, ranks=ranks, cells_per_rank=n, p_max=P)
@@ -81,7 +99,10 @@ def footprint(map_size: int, n_molecules: int, cells: int, map_dtype=torch.float
 
 
 MAX_MAP = 65280  # (a multiple of 256 below 2^16: the reference's positions are u16, rust/world.rs)
-MAX_RANK_PIXELS = 1 << 30  # pixels of one rank's map: the kernels index a rank's map with 32-bit ints
+# pixels of one rank's map: every kernel addresses the map with 64-bit offsets (plane * pixels +
+# pixel; the neighbour / placement pixel indices are long long), positions are int32 (x, y) pairs,
+# so the bound is the 16-bit side above, not an index width (round 4 capped a rank at 2^30 pixels)
+MAX_RANK_PIXELS = 1 << 40
 
 
 def plan(hbm_bytes: float = MI355X_HBM, ranks: int = 8, n_molecules: int = 14, map_dtype="fp16",
@@ -90,10 +111,9 @@ def plan(hbm_bytes: float = MI355X_HBM, ranks: int = 8, n_molecules: int = 14, m
     """The largest map side ``S`` (a multiple of ``multiple``) whose per-rank share -- ``S / ranks``
     owned rows plus halos, ``cells_per_pixel * S²`` cells spread over the ranks -- fits
     ``hbm_bytes * (1 - reserve)`` on every GPU (the reserve covers the runtime, the RCCL buffers,
-    the genome pipeline's scratch and allocator fragmentation), within the index widths: a side of at
-    most ``max_map`` (16-bit positions, as in the reference) and at most ``max_rank_pixels`` pixels per
-    rank (32-bit pixel indices in the kernels). At 1M cells per 16384² the index widths bind before
-    HBM does (``fill`` < 1). Returns the config and its :func:`footprint`."""
+    the genome pipeline's scratch and allocator fragmentation), within a side of at most ``max_map``
+    (16-bit positions, as in the reference; ``max_rank_pixels`` optionally caps a rank's pixels).
+    Returns the config and its :func:`footprint`."""
     budget = hbm_bytes * (1.0 - reserve)
 
     def cost(S: int) -> float:

@@ -28,6 +28,7 @@ trace() {  # trace <name> <steps-to-summarise> <bench args...>
   MARKER=${MARKER:-void msd::diffuse_stencil4} python scripts/step_kernels.py $O/$name/run_kernel_trace.csv $k > $O/${name}_steps.txt 2>&1
 }
 for s in "$@"; do case "$s" in
+  tmem) run tests_mem 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -k "memory_model or past_2_31" --timeout 300 --timeout-method thread ;;
   tests) run tests 1000 python -u -m pytest tests -m gpu -q --maxfail 5 --timeout 120 --timeout-method thread ;;
   smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   flagship) run flagship 300 python bench.py ;;
@@ -62,7 +63,7 @@ for s in "$@"; do case "$s" in
   tprobe) run translate_probe 300 python scripts/translate_probe.py ;;
   checkp) MS_CHECK_PROFILE=1 run check_profile 600 python performance/check.py --parts update_cells mutations ;;
   check) run check 600 python performance/check.py ;;
-  hbm) run hbm_bench 900 python bench.py --preset hbm --steps 10 --warmup 3 --step-times ;;
+  hbm) run hbm_bench 900 python bench.py --preset hbm --steps 60 --warmup 20 --step-times ;;
   m1) run m1_bench 600 python bench.py --preset m1 --steps 60 --warmup 10 --step-times ;;
   wide) run wide 300 python bench.py --preset wide ;;
   c1024) run c1024 300 python bench.py --preset c1024 --steps 30 --warmup 5 ;;

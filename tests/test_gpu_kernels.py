@@ -1188,26 +1188,53 @@ def test_genome_pool_grows_and_collects_under_pressure():
     assert g.pool_cap >= cap0 or strings._POOL_MIN == cap0
 
 
-def test_memory_model_matches_a_live_world():
+@pytest.mark.parametrize("size,cells,dtype", [(2048, 20_000, torch.float32), (12800, 60_000, torch.float16)])
+def test_memory_model_matches_a_live_world(size, cells, dtype):
     """utils/memory.py models what a GPU world holds: the modelled footprint of a world after some
     steps is within 25 % of the bytes its tensors hold (utils.memory.measured) and of what the
-    caching allocator has handed out."""
+    caching allocator has handed out. The fp16 case holds a 4.6 GB map (2.3G values: offsets past
+    2^31 in every map kernel)."""
     import bench
     from magicsoup_amd.utils import memory
 
     atp = CHEMISTRY.molname_2_idx["ATP"]
     torch.cuda.synchronize()
     base = torch.cuda.memory_allocated()
-    w = ms.World(chemistry=CHEMISTRY, map_size=2048, device="cuda", seed=3)
-    w.spawn_cells(bench.random_genomes(20_000, 500, "cuda"))
+    w = ms.World(chemistry=CHEMISTRY, map_size=size, device="cuda", seed=3, map_dtype=dtype)
+    w.spawn_cells(bench.random_genomes(cells, 500, "cuda"))
     for _ in range(5):
-        bench.step(w, 20_000, 500, atp)
+        bench.step(w, cells, 500, atp)
     w.synchronize()
-    model = memory.footprint(2048, len(CHEMISTRY.molecules), w.n_cells, torch.float32, 500)["total"]
+    if size > 8192:
+        assert w.molecule_map.numel() > 2**31
+        w.check_invariants()
+        assert torch.isfinite(w.molecule_map[-1, -64:, -64:].float()).all()
+    # (the storage's actual protein dimension: the model's default budgets for recombinants)
+    model = memory.footprint(size, len(CHEMISTRY.molecules), w.n_cells, dtype, 500, p_max=w.kinetics._P())["total"]
     held = memory.measured(w)["bytes"]
     alloc = torch.cuda.memory_allocated() - base
     assert 0.75 * held <= model <= 1.25 * held, (model, held)
     assert held <= alloc * 1.05, (held, alloc)
+
+
+def test_diffusion_past_2_31_map_values():
+    """A map of more than 2^31 values (fp16, 14 x 13056^2): the last plane, which starts past 2^31,
+    diffuses exactly as a circular 3x3 convolution of its own values (plus the mass correction)."""
+    import torch.nn.functional as F
+
+    w = ms.World(chemistry=CHEMISTRY, map_size=13056, device="cuda", seed=4, map_dtype=torch.float16)
+    mm = w.molecule_map
+    assert mm.numel() > 2**31 and (mm.size(0) - 1) * mm[0].numel() > 2**31
+    j = mm.size(0) - 1
+    x = mm[j].float().clone()
+    a, b = w._diffusion[j]
+    w.diffuse_molecules()
+    k = torch.full((3, 3), a, device="cuda")
+    k[1, 1] = b
+    ref = F.conv2d(F.pad(x[None, None], (1, 1, 1, 1), mode="circular"), k[None, None])[0, 0]
+    ref = (ref + (x.double().sum() - ref.double().sum()) / x.numel()).clamp(min=0.0)
+    got = w.molecule_map[j].float()
+    assert torch.allclose(got, ref.float(), rtol=2e-3, atol=2e-3)
 
 
 def test_genome_pool_collect_layout_matches_sorted_reference():

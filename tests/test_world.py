@@ -643,3 +643,24 @@ def test_kill_divide_matches_kill_then_divide():
     w1.check_invariants()
     with pytest.raises(ValueError):
         w1.kill_divide_t(kill, div)  # masks of the old population
+
+
+def test_reserve_cells_keeps_state_and_results():
+    """World.reserve_cells pre-allocates capacity; the world then evolves exactly as without it."""
+    import copy
+
+    from magicsoup_amd.examples.wood_ljungdahl import CHEMISTRY
+
+    ms.set_seed(6)
+    w = ms.World(chemistry=CHEMISTRY, map_size=32)
+    w.spawn_cells([ms.random_genome(300) for _ in range(40)])
+    w2 = copy.deepcopy(w)
+    w2.reserve_cells(500, genome_len=330)
+    assert w2._cols["cell_molecules"].buf.size(0) >= 500
+    for x in (w, w2):
+        ms.set_seed(7)
+        x.spawn_cells([ms.random_genome(300) for _ in range(60)])
+        x.enzymatic_activity()
+    assert torch.equal(w.cell_molecules, w2.cell_molecules)
+    assert torch.equal(w.kinetics.Vmax, w2.kinetics.Vmax)
+    w2.check_invariants()
