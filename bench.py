@@ -117,12 +117,6 @@ def random_genomes(k: int, size: int, device) -> tuple[torch.Tensor, torch.Tenso
 _CHEMOSTAT = {"divided": 0, "starved": 0, "steps": 0, "excess": None}
 
 
-def _dilution_mask(n: int, k: int, device) -> torch.Tensor:
-    """Each of n cells drawn with probability k / n (about k cells: the chemostat needs the rate, not
-    an exact count; one fused draw on the device, no host work)."""
-    return torch.rand(n, device=device) < (k / n)
-
-
 _NULL = contextlib.nullcontext()
 
 
@@ -162,29 +156,25 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
         margin = n_target // 50 + 3 * int(math.sqrt(d_est + 1))
         keep = n_target + margin - d_est + s_est
         excess = min(n0 - keep, n0)
-        dilute = _dilution_mask(n0, excess, world.cell_molecules.device) if excess > 0 else None
     with ph("activity"):
         world.enzymatic_activity()
     with ph("kill_replicate"):
-        # kill (ATP < 1) and replicate (ATP > 5: ATP -= 4, divide), performance/run_simulation.py:80-92.
-        # Boolean masks, no index read-back. The replicate mask is taken before the kill, over the
-        # survivors: the kill does not change their molecules, so it selects the reference's cells,
-        # and the killed cells spill unchanged molecules. Both go to the world in one call that never
-        # waits for the device (World.kill_divide_t).
+        # kill (ATP < 1) and replicate (ATP > 5: ATP -= 4, divide), performance/run_simulation.py:80-92,
+        # as one call that never waits for the device (World.kill_divide_where: the threshold masks,
+        # the ATP payment, the kill and the division in one native call -- the same as building the
+        # masks with torch and calling kill_divide_t; the replicate mask is taken over the survivors
+        # before the kill, which does not change their molecules).
         # Chemostat dilution keeps the population at the configured size (the reference loop only
-        # tops up; on a 4096^2 map the population would otherwise grow ~6x within 25 steps): random
-        # cells are removed together with the starving ones, so that after the divisions that follow
-        # the population is back at n_target plus a small margin (the previous steps' divisions and
-        # starvation deaths are the estimates). The margin keeps the next step's top-up (a spawn)
-        # rare; activity always runs on >= n_target cells.
-        a = world.cell_molecules[:, atp]
-        kill = a < 1.0
-        if dilute is not None:
-            kill |= dilute
+        # tops up; on a 4096^2 map the population would otherwise grow ~6x within 25 steps): each
+        # cell also dies with probability excess / n (drawn on the device: the chemostat needs the
+        # rate, not an exact count), so that after the divisions that follow the population is back
+        # at n_target plus a small margin (the previous steps' divisions and starvation deaths are
+        # the estimates). The margin keeps the next step's top-up (a spawn) rare; activity always
+        # runs on >= n_target cells.
+        if excess > 0:
             note("diluted", excess)
-        repl = (a > 5.0) & ~kill
-        a -= 4.0 * repl
-        world.kill_divide_t(kill, repl)
+        world.kill_divide_where(atp, kill_below=1.0, divide_above=5.0, divide_cost=4.0,
+                                kill_fraction=excess / n0 if excess > 0 else 0.0)
         _CHEMOSTAT["excess"] = max(excess, 0)
     with ph("recombinate"):
         world.recombinate_cells()

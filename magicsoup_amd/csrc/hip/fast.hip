@@ -134,6 +134,28 @@ __global__ void __launch_bounds__(256) compact_mask_kernel(int n, const int* dn,
   dmask[i] = i < *dn ? mask[sel[i]] : (uint8_t)0;
 }
 
+// Threshold masks of the reference loop's kill / replicate step (performance/run_simulation.py:80-92)
+// in one pass over the cells: a cell dies if its molecule `mol` is below `kill_below` (or, with
+// probability `kill_p`, at random: a chemostat dilution), a surviving cell with more than
+// `divide_above` pays `cost` of it and divides.
+__global__ void __launch_bounds__(256) threshold_masks_kernel(int n, int m, int mol, float kill_below, float divide_above,
+                                                              float cost, float kill_p, uint64_t seed, uint64_t call,
+                                                              float* mols, uint8_t* kill, uint8_t* divide) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float* x = mols + (size_t)i * m + mol;
+  const float v = *x;
+  bool k = v < kill_below;
+  if (kill_p > 0.0f) {
+    Philox rng(seed, call, (uint32_t)i);
+    k |= rng.uniform() < kill_p;
+  }
+  const bool d = !k && v > divide_above;
+  if (d) *x = v - cost;
+  kill[i] = k;
+  divide[i] = d;
+}
+
 // kill_cells(kill) then divide_cells(divide restricted to the survivors) without a synchronisation
 // in between: the kill as fast_kill, the division mask compacted with the survivors, the division
 // over it with the children appended after the device survivor count (rows dn..). Both masks are
@@ -157,6 +179,40 @@ std::pair<int, int> fast_kill_divide(const FastWorld& f, int n, uintptr_t kill, 
                                         f.m, f.par, f.mols, f.div, f.life, stream);
   launch_row_args(f.clone, n, P_<int>(f.dcount2), P_<int64_t>(f.par), nullptr, 0, s, dn);
   return {slot_k, slot_d};
+}
+
+// The threshold masks alone (a decomposed world's strips: their division is a collective protocol)
+void fast_threshold_masks(const FastWorld& f, int n, int mol, float kill_below, float divide_above, float cost,
+                          float kill_p, uint64_t seed, uint64_t call, uintptr_t kill, uintptr_t divide,
+                          uintptr_t stream) {
+  if (!f.ready) throw std::invalid_argument("fast_threshold_masks: descriptor not finalized");
+  if (n <= 0 || mol < 0 || mol >= f.m) throw std::invalid_argument("fast_threshold_masks: bad cell count or molecule");
+  threshold_masks_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, f.m, mol, kill_below, divide_above, cost, kill_p, seed,
+                                                                  call, P_<float>(f.mols), P_<uint8_t>(kill),
+                                                                  P_<uint8_t>(divide));
+  MS_LAUNCH_CHECK();
+}
+
+// A mask over the n cells before the last fast_kill compacted with its survivors (f.sel, f.dcount)
+void fast_compact_mask(const FastWorld& f, int n, uintptr_t mask, uintptr_t out, uintptr_t stream) {
+  if (!f.ready || n <= 0) throw std::invalid_argument("fast_compact_mask: descriptor / count");
+  compact_mask_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, P_<int>(f.dcount), P_<int64_t>(f.sel), P_<uint8_t>(mask),
+                                                               P_<uint8_t>(out));
+  MS_LAUNCH_CHECK();
+}
+
+// fast_kill_divide with the masks from threshold_masks_kernel (written to kill / divide, uint8 n)
+std::pair<int, int> fast_kill_divide_where(const FastWorld& f, int n, int mol, float kill_below, float divide_above,
+                                           float cost, float kill_p, uint64_t mseed, uint64_t mcall, uintptr_t kill,
+                                           uintptr_t divide, uintptr_t map, int mdt, uintptr_t corr, uint64_t seed,
+                                           uint64_t call, uintptr_t stream) {
+  if (!f.ready) throw std::invalid_argument("fast_kill_divide_where: descriptor not finalized");
+  if (n <= 0 || mol < 0 || mol >= f.m) throw std::invalid_argument("fast_kill_divide_where: bad cell count or molecule");
+  threshold_masks_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, f.m, mol, kill_below, divide_above, cost, kill_p,
+                                                                  mseed, mcall, P_<float>(f.mols), P_<uint8_t>(kill),
+                                                                  P_<uint8_t>(divide));
+  MS_LAUNCH_CHECK();
+  return fast_kill_divide(f, n, kill, divide, map, mdt, corr, seed, call, stream);
 }
 
 // ---- the strip protocol of a decomposed world's divide_cells over a mask (parallel/dist_world.py),
@@ -299,6 +355,10 @@ void bind_fast(pybind11::module_& m) {
       .def("finalize", &FastWorld::finalize);
   m.def("fast_kill", &fast_kill, "kill_cells(mask) in one call (status slot of the survivor count)");
   m.def("fast_divide", &fast_divide, "divide_cells(mask) in one call (status slot of the winner count)");
+  m.def("fast_threshold_masks", &fast_threshold_masks, "threshold kill / replicate masks (and the payment)");
+  m.def("fast_compact_mask", &fast_compact_mask, "a mask compacted with the last fast_kill's survivors");
+  m.def("fast_kill_divide_where", &fast_kill_divide_where,
+        "threshold kill / replicate masks + fast_kill_divide in one call (status slots of both counts)");
   m.def("fast_kill_divide", &fast_kill_divide,
         "kill_cells(kill) + divide_cells(divide & survivors) in one call (status slots of both counts)");
   m.def("fast_dist_divide_a", &fast_dist_divide_a, "strip divide protocol up to the synchronisation");

@@ -1127,6 +1127,162 @@ __global__ void __launch_bounds__(kBlock, W) integrate_spec_fused_kernel(Integra
   or_block_bits(bits, a.mask_out);
 }
 
+// Everything behind the speculative fused launch of a single-process world in two launches (the
+// 32-lane chemistries; decomposed worlds all-reduce flags between these stages and keep the separate
+// launches). Usually every list is empty and the speculation held: each block reads a few words and
+// writes nothing back -- two launches instead of the five that used to return at once plus the
+// write-back. The grid is co-resident (at most one block per CU, like the placement's cooperative
+// launch), so phases that feed each other are separated by a software grid barrier, taken only when
+// the phase before had work:
+//   A. (a launch of its own before this one: inlined here, its 64-lane registers spilled) the narrow
+//      launch's overflow list (at most 32 active proteins, more non-zeros / large exponents) on
+//      64-lane slots with 2 * kNzReg non-zeros; what these cannot take goes on to list B;
+//   B. the cells no register path took, all parts on the LDS path (cps cells per block);
+//   C. only if the speculation failed (some part's reference loop ended early for the whole
+//      population, or a cell was unfit): the exact per-part LDS integration of every cell, a grid
+//      barrier after each part (part p + 1 starts from part p's candidate the global flags select);
+//   D. the write-back: the list-B cells' final states when the speculation held (the register paths
+//      wrote theirs), every cell's selected candidate when it did not.
+struct RescueArgs {
+  IntegrateArgs lb;      // phase B (list wl3 / count wc3, LDS slots of slot_words)
+  IntegrateArgs fb;      // phase C, part 0 (the later parts differ in the fields below)
+  const float* fb_snap_prev[kMaxParts];
+  const unsigned* fb_mask_prev[kMaxParts];
+  float* fb_snap_out[kMaxParts];
+  unsigned* fb_mask_out[kMaxParts];
+  int cps;               // LDS-path cells per block
+  int nparts, n_iters;
+  const unsigned* sflags;  // speculative flags (4 per part) + unfit word
+  unsigned* masks;       // regular per-part flags (the host reads these)
+  unsigned* barrier;     // grid-barrier counter (zeroed by the input kernel)
+  unsigned* err_host;    // barrier timeout (mapped host word), optional
+  int* wide_reset;       // the wide-list count, zeroed for the next call
+  int all_from_snap;     // the register launches left their final states in snap_spec (mode bit 8)
+  // write-back
+  int c, s, m, R, C, map_dtype;
+  const float* snap_spec;  // where the speculative LDS path left its final states (slot n_iters)
+  const float* snap_last;  // the exact path's last part
+  const int32_t* positions;
+  float* cell_mols;
+  void* molmap;
+  const float* corr;
+  float* X_out;
+};
+
+// v[q] of a kernel-argument array without dynamic indexing (that copies the array to scratch)
+template <class T>
+__device__ __forceinline__ T sel4(const T (&v)[kMaxParts], int q) {
+  static_assert(kMaxParts == 4, "sel4 selects among 4 parts");
+  return q == 0 ? v[0] : (q == 1 ? v[1] : (q == 2 ? v[2] : v[3]));
+}
+
+__device__ void rescue_barrier(unsigned* ctr, unsigned& phase, unsigned* err_host) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();  // this block's stores (snapshots, outputs) reach agent scope before the arrival
+    const unsigned target = (++phase) * gridDim.x;
+    atomicAdd(ctr, 1u);
+    for (long long spin = 0; __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
+      if (spin > (1ll << 24)) {  // a grid that is not co-resident: report instead of hanging
+        if (err_host) __hip_atomic_store(err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __threadfence();  // the other blocks' stores are visible to this CU's waves
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void rescue_store(const RescueArgs& r, int cell, int j, float x) {
+  if (r.X_out) {
+    r.X_out[(size_t)cell * r.s + j] = x;
+  } else if (j < r.m) {
+    r.cell_mols[(size_t)cell * r.m + j] = x;
+  } else {
+    const size_t pix = (size_t)r.positions[2 * cell] * r.C + r.positions[2 * cell + 1];
+    st_map(r.molmap, (size_t)(j - r.m) * r.R * r.C + pix, corr_out(x, r.corr, j - r.m), r.map_dtype);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock, 1) integrate_rescue_kernel(RescueArgs r) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  unsigned phase = 0;
+  unsigned bits = 0u;
+  // ---- B (list A ran in the launch before: its 64-lane path in this kernel spilled ~1 KB per lane)
+  const int cB = *r.lb.count;
+  const int slot = (int)threadIdx.x / 32;
+  if (cB > 0) {
+    for (int base = (int)blockIdx.x * r.cps; base < cB; base += (int)gridDim.x * r.cps) {
+      if (slot < r.cps) {
+        for (int part = 0; part < r.nparts; ++part) {
+          IntegrateArgs ap = r.lb;
+          ap.trim = trim_of(r.lb, part);
+          ap.spec_prev = part > 0;
+          ap.snap_prev = part > 0 ? r.lb.snap_out : r.lb.snap_prev;
+          unsigned b = 0u;
+          integrate_item<32>(ap, smem, base + slot, b);
+          bits |= b << (ms::kEqIters * part);
+          wave_lds_sync();
+        }
+      }
+      __syncthreads();  // (slots are refilled by the next items)
+    }
+    or_block_bits(bits, r.lb.mask_out);
+    bits = 0u;
+    rescue_barrier(r.barrier, phase, r.err_host);  // (flags and snapshots for the verdict / write-back)
+  }
+  const bool held = spec_held(r.sflags, r.nparts, r.n_iters);
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
+  if (held) {
+    // the regular flags are the speculative ones (the host reads those)
+    if (blockIdx.x == 0 && (int)threadIdx.x < ms::kEqIters * r.nparts) r.masks[threadIdx.x] = r.sflags[threadIdx.x];
+    // ---- D (held): list-B cells (or every cell, all_from_snap), candidate n_iters of the
+    //      speculative snapshots
+    const long long nb = r.all_from_snap ? r.c : cB;
+    for (long long t = tid; t < nb * r.s; t += nth) {
+      const int i = (int)(t / r.s), j = (int)(t - (long long)i * r.s);
+      const int cell = r.all_from_snap ? i : r.lb.list[i];
+      if ((unsigned)cell >= (unsigned)r.c) continue;
+      rescue_store(r, cell, j, r.snap_spec[((size_t)cell * ms::kSnap + r.n_iters) * r.s + j]);
+    }
+  } else {
+    // ---- C: the exact per-part path over every cell
+    for (int part = 0; part < r.nparts; ++part) {
+      IntegrateArgs f = r.fb;
+      f.snap_prev = sel4(r.fb_snap_prev, part);
+      f.mask_prev = sel4(r.fb_mask_prev, part);
+      f.snap_out = sel4(r.fb_snap_out, part);
+      f.mask_out = sel4(r.fb_mask_out, part);
+      f.trim = trim_of(r.fb, part);
+      for (int base = (int)blockIdx.x * r.cps; base < r.c; base += (int)gridDim.x * r.cps) {
+        if (slot < r.cps) integrate_item<32>(f, smem, base + slot, bits);
+        __syncthreads();
+      }
+      or_block_bits(bits, f.mask_out);
+      bits = 0u;
+      rescue_barrier(r.barrier, phase, r.err_host);  // (part + 1 selects by these global flags)
+    }
+    // ---- D (not held): every cell's selected candidate of the last part
+    const int k = stop_iter(r.masks + ms::kEqIters * (r.nparts - 1), r.n_iters);
+    for (long long t = tid; t < (long long)r.c * r.s; t += nth) {
+      const int cell = (int)(t / r.s), j = (int)(t - (long long)cell * r.s);
+      rescue_store(r, cell, j, r.snap_last[((size_t)cell * ms::kSnap + k) * r.s + j]);
+    }
+  }
+  if (tid == 0) r.wide_reset[0] = 0;  // (the wide-list count, for the next call)
+}
+
+static int g_rescue_mode = 1;  // 0: the separate launches (A/B)
+void set_rescue_mode(int m) { g_rescue_mode = m; }
+static unsigned g_rescue_blocks = 0;  // co-resident grid: one block per CU
+static unsigned* g_rescue_err = nullptr;
+static unsigned* g_rescue_err_dev = nullptr;
+int rescue_error_take() {
+  if (!g_rescue_err) return 0;
+  return __atomic_exchange_n(g_rescue_err, 0u, __ATOMIC_ACQ_REL) ? 1 : 0;
+}
+
 // Split the cells by their number of active proteins (Vmax > 0 or NaN; the same set for every part
 // since all trims are positive): cells with at most `pn` go to the narrow list (small LDS slots,
 // high occupancy), the others to the wide list (slots for all P proteins). List order does not
@@ -1283,6 +1439,7 @@ __global__ void __launch_bounds__(kBlock) gather_bin_kernel(int c, int s, int m,
   // (void_spec, mode bit 9, for tests: the unfit word starts set, so the exact launches run)
   if (blockIdx.x == 0 && threadIdx.x < ms::kEqIters * kMaxParts + 1)
     wide[4 + threadIdx.x] = (void_spec && threadIdx.x == ms::kEqIters * nparts) ? 1u : 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) wide[1] = 0u;  // (the rescue launch's grid-barrier counter)
   const int lane = threadIdx.x & (G - 1);
   const int cell = (int)blockIdx.x * (kBlock / G) + (int)threadIdx.x / G;
   const bool ok = cell < c;
@@ -1621,6 +1778,66 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
       // flagship state, profiles/r5/ab_integrator_*.log)
       integrate_spec_fused_kernel<6><<<cdiv(c, kBlock / 32), kBlock, lds_fast, st>>>(a, aw);
       MS_LAUNCH_CHECK();
+      if (dist_stage == 0 && g_rescue_mode && scatter) {
+        // one launch for the overflow lists, the exact fallback and the write-back (see
+        // integrate_rescue_kernel); the barrier counter was zeroed by the input kernel
+        if (!g_rescue_blocks) {
+          int dev = 0, cus = 0;
+          MS_HIP_CHECK(hipGetDevice(&dev));
+          MS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+          g_rescue_blocks = (unsigned)std::max(1, std::min(cus, 256));
+          MS_HIP_CHECK(hipHostMalloc((void**)&g_rescue_err, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
+          *g_rescue_err = 0;
+          MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_rescue_err_dev, g_rescue_err, 0));
+        }
+        integrate_fast_kernel<64, kNzWide, true, true><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
+        MS_LAUNCH_CHECK();
+        RescueArgs r{};
+        r.lb = a;
+        r.lb.list = wl3;
+        r.lb.count = wc3;
+        r.lb.Ps = P;
+        r.lb.slot_words = slot_words;
+        r.lb.wb = 0;  // (phase D writes the list-B cells back)
+        r.cps = std::min(cps, kBlock / 32);
+        r.nparts = nparts;
+        r.n_iters = n_iters;
+        {
+          IntegrateArgs& f = r.fb;
+          f.c = c; f.P = P; f.s = s;
+          f.W = P_<int32_t>(W); f.Q = P_<float4>(Q); f.Kmr = P_<float>(Kmr); f.prow = prow ? P_<int64_t>(prow) : nullptr;
+          f.n_iters_prev = n_iters;
+          f.n_iters = n_iters;
+          f.sp = sp;
+          f.slot_words = slot_words;
+          f.Ps = P;
+          for (int part = 0; part < nparts; ++part) {
+            f.trims[part] = trims[part];
+            r.fb_snap_prev[part] = part == 0 ? snaps[1] : snaps[(part - 1) & 1];
+            r.fb_mask_prev[part] = part == 0 ? zero_flags : mk + ms::kEqIters * (part - 1);
+            r.fb_snap_out[part] = snaps[part & 1];
+            r.fb_mask_out[part] = mk + ms::kEqIters * part;
+          }
+        }
+        r.sflags = sflags;
+        r.masks = mk;
+        r.barrier = spec_w + 1;
+        r.err_host = g_rescue_err_dev;
+        r.wide_reset = reinterpret_cast<int*>(spec_w);
+        r.c = c; r.s = s; r.m = m; r.R = R; r.C = C; r.map_dtype = map_dtype;
+        r.snap_spec = a.snap_out;
+        r.snap_last = snaps[(nparts - 1) & 1];
+        r.positions = P_<int32_t>(positions);
+        r.cell_mols = P_<float>(cell_mols);
+        r.molmap = P_<void>(molmap);
+        r.corr = corr;
+        r.X_out = X_io ? P_<float>(X_io) : nullptr;
+        r.all_from_snap = spec_wb ? 0 : 1;
+        const size_t lds_r = (size_t)r.cps * slot_bytes;
+        integrate_rescue_kernel<<<g_rescue_blocks, kBlock, lds_r, st>>>(r);
+        MS_LAUNCH_CHECK();
+        return 1;
+      }
       integrate_fast_kernel<64, kNzWide, true, true><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
       MS_LAUNCH_CHECK();
     } else {

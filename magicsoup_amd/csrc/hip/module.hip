@@ -133,6 +133,8 @@ void translate_fused(int n, uintptr_t rows, uintptr_t arena, uintptr_t off, int 
 size_t translate_slot_bytes(int width);
 void set_integrate_mode(int mode);
 void set_spl2_waves(int w);
+void set_rescue_mode(int m);
+int rescue_error_take();
 // mutations.hip
 void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
                uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
@@ -290,6 +292,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("translate_write", &msd::translate_write);
   m.def("translate_fused", &msd::translate_fused);
   m.def("set_spl2_waves", &msd::set_spl2_waves, "waves per SIMD of the wide chemistries' narrow launch (2-4)");
+  m.def("set_rescue_mode", &msd::set_rescue_mode, "1: one launch behind the speculative integrator (0: separate)");
+  m.def("rescue_error_take", &msd::rescue_error_take, "1 if the integrator rescue launch's grid barrier timed out");
   m.def("set_integrate_mode", &msd::set_integrate_mode, "binned integrator launches: 0 serial, 1 concurrent, 2 concurrent + strided wide bin");
   m.def("translate_slot_bytes", &msd::translate_slot_bytes);
   m.def("mut_count", &msd::mut_count);

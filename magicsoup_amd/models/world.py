@@ -1056,6 +1056,75 @@ class World:
                                               hip_ops._mdt(mm), hip_ops._p(corr), seed, call, hip_ops._stream())
         self.__dict__["_count_pending"] = (n, tuple(slots), NEvent().record())
 
+    @_op("kill_divide")
+    def kill_divide_where(self, molecule, kill_below: float, divide_above: float, divide_cost: float = 0.0,
+                          kill_fraction: float = 0.0) -> None:
+        """The reference loop's kill / replicate step as one call: cells whose ``molecule`` (index
+        or name) is below ``kill_below`` die -- and, with ``kill_fraction`` > 0, each cell also dies
+        with that probability (a chemostat dilution) --, surviving cells with more than
+        ``divide_above`` of it pay ``divide_cost`` and divide (``performance/run_simulation.py:80-92``:
+        kill below 1, divide above 5 at a cost of 4). Same semantics as building the two masks and
+        calling :meth:`kill_divide_t`; on the GPU the masks, the payment, the kill and the division
+        are one native call with no host synchronisation."""
+        mol = self.chemistry.molname_2_idx[molecule] if isinstance(molecule, str) else int(molecule)
+        if not 0 <= mol < self.n_molecules:
+            raise ValueError(f"kill_divide_where: molecule index {mol} out of range")
+        n = self.n_cells
+        if n == 0:
+            return
+        if self._genomes.data.is_cuda and getattr(self, "_exchange_map_halo", None) is not None:
+            # a decomposed world's strip: native masks and kill (its one synchronisation), the
+            # division mask compacted with the survivors on the device, then the strip's lazy
+            # division protocol
+            from magicsoup_amd.ops import hip_ops
+
+            fw = self._fast_world(2 * n)
+            bufs = self.__dict__["_fw_bufs"]
+            cap = int(bufs["sel"].numel())
+            if bufs.get("kmask") is None or bufs["kmask"].numel() < cap:
+                bufs["kmask"] = torch.empty(cap, dtype=torch.uint8, device=self._genomes.data.device)
+                bufs["dvmask"] = torch.empty_like(bufs["kmask"])
+                bufs["dvmask2"] = torch.empty_like(bufs["kmask"])
+            seed, call = hip_ops._rng() if kill_fraction > 0.0 else (0, 0)  # (no draws: no stream used)
+            m_ = hip_ops._m()
+            m_.fast_threshold_masks(fw, n, mol, float(kill_below), float(divide_above), float(divide_cost),
+                                    float(kill_fraction), seed ^ 0x6A09E667F3BCC909, call, bufs["kmask"].data_ptr(),
+                                    bufs["dvmask"].data_ptr(), hip_ops._stream())
+            self.kill_cells(bufs["kmask"][:n].view(torch.bool))
+            n_after = self.n_cells
+            self.__dict__["last_kill"] = (n, n_after)
+            if n_after > 0:
+                fw = self._fast_world(n_after)  # (the kill's survivor indices are in this descriptor's sel)
+                m_.fast_compact_mask(fw, n, bufs["dvmask"].data_ptr(), bufs["dvmask2"].data_ptr(), hip_ops._stream())
+                self.divide_cells_t(bufs["dvmask2"][:n_after].view(torch.bool), lazy=True)
+            return
+        if not self._genomes.data.is_cuda:
+            a = self.cell_molecules[:, mol]
+            kill = a < kill_below
+            if kill_fraction > 0.0:
+                kill |= torch.rand(n, device=a.device) < kill_fraction
+            div = (a > divide_above) & ~kill
+            a -= divide_cost * div
+            self.kill_divide_t(kill, div)
+            return
+        from magicsoup_amd.ops import hip_ops
+        from magicsoup_amd.ops.streams import NEvent
+
+        fw = self._fast_world(2 * n)
+        mm, corr = hip_ops.map_for_pixels(self)
+        bufs = self.__dict__["_fw_bufs"]
+        kill = bufs.get("kmask")
+        if kill is None or kill.numel() < int(bufs["sel"].numel()):
+            kill = bufs["kmask"] = torch.empty(int(bufs["sel"].numel()), dtype=torch.uint8, device=mm.device)
+            bufs["dvmask"] = torch.empty_like(kill)
+        seed, call = hip_ops._rng()  # (the dilution draws use a key of their own on the same call)
+        slots = hip_ops._m().fast_kill_divide_where(
+            fw, n, mol, float(kill_below), float(divide_above), float(divide_cost), float(kill_fraction),
+            seed ^ 0x6A09E667F3BCC909, call,
+            kill.data_ptr(), bufs["dvmask"].data_ptr(), mm.data_ptr(), hip_ops._mdt(mm), hip_ops._p(corr), seed, call,
+            hip_ops._stream())
+        self.__dict__["_count_pending"] = (n, tuple(slots), NEvent().record())
+
     @_op("kill_cells")
     def kill_cells(self, cell_idxs=None):
         """Remove cells; their molecules spill onto their pixel. Remaining cells keep their order

@@ -166,6 +166,9 @@ def check_placement() -> None:
     if _m().place_error_take():
         raise RuntimeError("cell placement: a grid barrier of the cooperative launch timed out; the occupancy "
                            "map may be inconsistent")
+    if _m().rescue_error_take():
+        raise RuntimeError("integrator: a grid barrier of the rescue launch timed out (grid not co-resident); "
+                           "the activity's results may be wrong")
 
 
 # ---------------------------------------------------------------------------- geometry

@@ -78,6 +78,9 @@ def hip():
         mod.set_integrate_mode(int(os.environ["MS_INTEGRATE_MODE"]))  # type: ignore[attr-defined]
     if fresh and os.environ.get("MS_SPL2_WAVES"):
         mod.set_spl2_waves(int(os.environ["MS_SPL2_WAVES"]))  # type: ignore[attr-defined]
+    if fresh and os.environ.get("MS_RESCUE_MODE"):
+        # 0: the separate launches behind the speculative integrator (A/B of the rescue launch)
+        mod.set_rescue_mode(int(os.environ["MS_RESCUE_MODE"]))  # type: ignore[attr-defined]
     if fresh and os.environ.get("MS_PLACE_MODE"):
         # 1: per-round placement launches, 2: the single launch as a cooperative launch (world.hip)
         mod.set_place_mode(int(os.environ["MS_PLACE_MODE"]))  # type: ignore[attr-defined]

@@ -474,3 +474,48 @@ def _body_dense_strip_recombination(rank, ws):
 
 def test_dense_strip_recombination_does_not_skip_boundary_results():
     run_ranks(_body_dense_strip_recombination, 1, timeout=300, backend="nccl")
+
+
+def _body_strip_kill_divide_where(rank, ws):
+    """A strip world's kill_divide_where (native masks, kill, division mask compacted on the device,
+    lazy strip division) evolves the strip exactly as the torch masks + kill_cells + divide_cells_t
+    do."""
+    import magicsoup_amd as ms
+    from magicsoup_amd.parallel import DistributedWorld
+    from tests.conftest import gen_genomes
+
+    ms.set_seed(41)
+    torch.manual_seed(41)
+    w = ms.World(chemistry=_chem(), map_size=64, seed=41, device="cpu")
+    w.spawn_cells(gen_genomes(1200, 300))
+    atp = _chem().molname_2_idx["ATP"]
+    out = {}
+    for fused in (False, True):
+        dw = DistributedWorld(chemistry=_chem(), map_size=64, seed=42, device="cuda", strips=True)
+        dw.adopt_maps(w)
+        dw.scatter_from(w, maps=False)
+        ms.set_seed(43)
+        for it in range(3):
+            dw.enzymatic_activity()
+            if fused:
+                dw.kill_divide_where(atp, 0.5, 2.0, 1.0)
+            else:
+                a = dw.cell_molecules[:, atp]
+                kill = a < 0.5
+                repl = (a > 2.0) & ~kill
+                a -= 1.0 * repl
+                dw.kill_cells(kill)
+                dw.divide_cells_t(repl[~kill], lazy=True)
+            dw.degrade_molecules()
+            dw.diffuse_molecules()
+            dw.increment_cell_lifetimes()
+        dw.synchronize()
+        dw.check_invariants("strip kill_divide_where")
+        out[fused] = (dw.cell_positions.cpu(), dw.cell_molecules.cpu(), dw.cell_divisions.cpu(), list(dw.cell_genomes))
+        dw.close()
+    a, b = out[False], out[True]
+    assert all(torch.equal(x, y) for x, y in zip(a[:3], b[:3])) and a[3] == b[3]
+
+
+def test_strip_kill_divide_where_matches_masks():
+    run_ranks(_body_strip_kill_divide_where, 1, timeout=300, backend="nccl")

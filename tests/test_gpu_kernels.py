@@ -1355,3 +1355,29 @@ def test_lazy_kill_divide_matches_synchronous_calls():
     assert s0 == s1 and g0 == g1 and l0 == l1
     for k in st0:
         assert torch.equal(st0[k], st1[k]), k
+
+
+def test_kill_divide_where_matches_masks_on_gpu():
+    """The fused threshold kill / replicate (one native call: masks, payment, kill, division) leaves
+    the world bit for bit as the torch masks + kill_divide_t do; a dilution fraction kills about
+    that share at random."""
+    base = _world("cuda", map_size=64, n=1500, s=400, seed=12)
+    base.enzymatic_activity()
+    base.synchronize()
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    w1, w2 = copy.deepcopy(base), copy.deepcopy(base)
+    ms.set_seed(4)
+    w1.kill_divide_where(atp, 1.0, 3.0, 2.0)
+    ms.set_seed(4)
+    a = w2.cell_molecules[:, atp]
+    kill = a < 1.0
+    div = (a > 3.0) & ~kill
+    a -= 2.0 * div
+    w2.kill_divide_t(kill, div)
+    for k in ("cell_molecules", "cell_positions", "cell_divisions", "cell_lifetimes", "molecule_map", "cell_map"):
+        assert torch.equal(getattr(w1, k), getattr(w2, k)), k
+    assert list(w1.cell_genomes) == list(w2.cell_genomes) and w1.last_kill == w2.last_kill
+    n = w1.n_cells
+    w1.kill_divide_where(atp, -1.0, 1e9, kill_fraction=0.3)
+    assert 0.6 * n < w1.n_cells < 0.8 * n
+    w1.check_invariants()

@@ -664,3 +664,33 @@ def test_reserve_cells_keeps_state_and_results():
     assert torch.equal(w.cell_molecules, w2.cell_molecules)
     assert torch.equal(w.kinetics.Vmax, w2.kinetics.Vmax)
     w2.check_invariants()
+
+
+def test_kill_divide_where_matches_masks():
+    """kill_divide_where(molecule, below, above, cost) == the reference loop's masks + kill_divide_t."""
+    import copy
+
+    from magicsoup_amd.examples.wood_ljungdahl import CHEMISTRY
+
+    ms.set_seed(8)
+    base = ms.World(chemistry=CHEMISTRY, map_size=24)
+    base.spawn_cells([ms.random_genome(300) for _ in range(150)])
+    base.enzymatic_activity()
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    a = base.cell_molecules[:, atp]
+    lo, hi = float(torch.quantile(a, 0.3)), float(torch.quantile(a, 0.6))
+    w1, w2 = copy.deepcopy(base), copy.deepcopy(base)
+    ms.set_seed(2)
+    w1.kill_divide_where("ATP", lo, hi, 0.5)
+    ms.set_seed(2)
+    b = w2.cell_molecules[:, atp]
+    kill = b < lo
+    div = (b > hi) & ~kill
+    b -= 0.5 * div
+    w2.kill_divide_t(kill, div)
+    for k in ("cell_molecules", "cell_positions", "cell_divisions", "molecule_map", "cell_map"):
+        assert torch.equal(getattr(w1, k), getattr(w2, k)), k
+    assert w1.last_kill == w2.last_kill
+    n = w1.n_cells
+    w1.kill_divide_where(atp, -1.0, 1e9, kill_fraction=0.5)  # dilution only: about half die
+    assert 0.25 * n < w1.n_cells < 0.75 * n
