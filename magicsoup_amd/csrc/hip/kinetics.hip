@@ -772,6 +772,13 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     float part[SPL];
 #pragma unroll
     for (int h = 0; h < SPL; ++h) part[h] = 0.0f;
+    // the stoichiometry bytes are loop-invariant over the parts and damping iterations: without this
+    // (empty) redefinition LICM hoists all G * SPL sign-extended n's out of the loops, into registers
+    // (128 of them for SPL == 2: 296 B/lane of scratch at 4 waves, 204 in the flagship's fused launch)
+#pragma unroll
+    for (int h = 0; h < SPL; ++h)
+#pragma unroll
+      for (int i = 0; i < G / 4; ++i) asm volatile("" : "+v"(npk[h][i]));
 #pragma unroll
     for (int k0 = 0; k0 < G; k0 += 4) {
       if (k0 >= na_w) break;
@@ -942,6 +949,8 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   float inc = 0.5f;
   for (int it = 0; it < a.n_iters; ++it, inc *= 0.5f) {
     bool changed = false, cb = false;
+#pragma unroll
+    for (int q = 0; q < NZ / 2; ++q) asm volatile("" : "+v"(e16[q]));  // (the same for the entry fields)
     {
       float pf = 1.0f, pb = 1.0f;
       int nfs = 0, nbs = 0;

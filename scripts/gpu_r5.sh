@@ -48,8 +48,9 @@ for s in "$@"; do case "$s" in
   isweep) run integrator_sweep 300 python scripts/integrator_sweep.py ;;
   dbench) run diffuse_bench 300 python scripts/diffuse_bench.py --dtypes fp32 --blocks 1024 2048 0 --band 0 64 ;;
   iab) for i in 1 2; do for m in 0 4096; do MS_INTEGRATE_MODE=$m run iab_${m}_$i 300 python bench.py --steps 60 --warmup 20; done; done ;;
-  wab) for i in 1 2; do for b in 64 128 256; do MS_FUSED_WIDE_BLOCKS=$b run wab_${b}_$i 300 python bench.py --steps 60 --warmup 20; done; done
-       for b in 64 256; do MS_FUSED_WIDE_BLOCKS=$b run wsweep_$b 300 python scripts/integrator_sweep.py 44000 50000 54000 60000; done ;;
+  abf) run ab_flagship 300 python scripts/ab_so.py abso/head.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so
+       run ab_flagship_grown 300 python scripts/ab_so.py --steps 150 abso/head.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so ;;
+  abw) run ab_wide 300 python scripts/ab_so.py --chem synthetic:64:256 abso/head.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so ;;
   tcheck) echo "== trace tcheck"; timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/tcheck -o run --output-format csv -- python performance/check.py --parts update_cells > $O/tcheck.log 2>&1; echo "   rc=$?" ;;
   sab) for i in 1 2; do for w in 4 3 2; do MS_SPL2_WAVES=$w run sab_${w}_$i 300 python bench.py --preset wide --steps 40 --warmup 10; done; done ;;
   pmcw|pmcf) # PMC of the integrator / stencil kernels (one pass, 8 SQ counters, kernel filter, no trace domains)
