@@ -31,6 +31,9 @@ constexpr int kBlock = 256;
 // kChunk active proteins this is the plain ascending sum. Every path (LDS staging, register lanes,
 // multi-group cells, the host core) sums this way, so all of them agree bit for bit, and a cell with
 // many proteins can be split over several lane groups (one chunk each) without changing results.
+// A candidate-state term is one fused multiply-add, fma(n_kj, w_k, sum), for every active protein
+// (n_kj == 0 included: a NaN velocity turns the cell's every signal into NaN, as the reference's
+// X0 + (N * V).sum(1) does, kinetics.py:759-763).
 constexpr int kChunk = 32;
 constexpr int kNarrowP = 12;  // LDS protein slots of the narrow integrator launch
 constexpr int kWideBlocksPerCU = 2;  // resident blocks per CU of the strided wide launch
@@ -351,7 +354,7 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
       float part = k0 == 0 ? x : 0.0f;
       for (int k = k0; k < k1; ++k) {
         const int n = w_n(words[k * SP + j]);
-        if (n != 0) part += (float)n * w_of(k);
+        part = fmaf((float)n, w_of(k), part);
       }
       x = k0 == 0 ? part : x + part;
     }
@@ -648,7 +651,8 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   bool fits = na <= NG * G;
   wave_lds_sync();
   const int nac = fits ? min(max(na - grp * G, 0), G) : 0;  // this group's active proteins
-  const int na_w = wave_max(nac);  // wave-uniform bound of the protein loops (both groups of a wave)
+  // wave-uniform bound of the protein loops (both groups of a wave), in an SGPR: scalar loop exits
+  const int na_w = __builtin_amdgcn_readfirstlane(wave_max(nac));
 
   // ---- 3. this lane's signals' stoichiometry columns (int8 n per protein, packed in registers) and
   //         the per-protein non-zero lists (one ballot per protein and half), 8 rows of loads in flight
@@ -739,6 +743,8 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
 #pragma unroll
   for (int q = 0; q < NZ / 2; ++q) e16[q] = 0;
   bool small = true;  // all exponents < 8: branch-free powers
+  bool both = false;  // an entry with forward and backward exponents (a signal consumed and produced)
+  int nfs_p = 0, nbs_p = 0;  // any forward / backward exponent of this protein
   if (prot) {
     pk = act[lane];
     const float4 q4 = a.Q[prow * P + pk];
@@ -756,11 +762,15 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
         const int e = EP::pack(j, w_nf(w), w_nb(w));
         e16[q >> 1] |= e << (16 * (q & 1));
         small &= w_nf(w) < 8 && w_nb(w) < 8 && w_a(w) < 8 && w_a(w) > -8;
+        both |= w_nf(w) > 0 && w_nb(w) > 0;
+        nfs_p |= w_nf(w);
+        nbs_p |= w_nb(w);
       }
     }
   }
-  const int cnt_w = wave_max(cnt);
+  const int cnt_w = __builtin_amdgcn_readfirstlane(wave_max(cnt));
   const bool small_w = __ballot(!small) == 0ull;
+  const bool one_w = __ballot(both) == 0ull;  // every entry has one exponent: one power per entry
 #define MS_E(q) ((e16[(q) >> 1] >> (16 * ((q) & 1))) & 0xFFFF)
   auto pw = [&](float x, int n) { return small_w ? ipow_small(x, n) : ms::ipow(x, n); };
 
@@ -851,20 +861,21 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     int nfs = 0, nbs = 0;
 #pragma unroll
     for (int q = 0; q < NZ; ++q) {
-      if (q >= cnt_w) break;
-      const int w = q < cnt ? ents[lane * ES + q] : 0;
-      const int j = EP::j(MS_E(q));
-      const int nf = w_nf(w), nb = w_nb(w), av = w_a(w);
-      const float x = Xs[j];
-      nfs |= nf;
-      nbs |= nb;
-      xf = nf > 0 ? xf * pw(x, nf) : xf;
-      xb = nb > 0 ? xb * pw(x, nb) : xb;
-      if (av != 0) {
-        float r = pw(x, av);
-        r = r / (r + kmr[j]);
-        if (ms::f_isnan(r)) r = 1.0f;
-        ar *= r;
+      if (q < cnt_w) {
+        const int w = q < cnt ? ents[lane * ES + q] : 0;
+        const int j = EP::j(MS_E(q));
+        const int nf = w_nf(w), nb = w_nb(w), av = w_a(w);
+        const float x = Xs[j];
+        nfs |= nf;
+        nbs |= nb;
+        xf = nf > 0 ? xf * pw(x, nf) : xf;
+        xb = nb > 0 ? xb * pw(x, nb) : xb;
+        if (av != 0) {
+          float r = pw(x, av);
+          r = r / (r + kmr[j]);
+          if (ms::f_isnan(r)) r = 1.0f;
+          ar *= r;
+        }
       }
     }
     if (prot) {
@@ -889,8 +900,8 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
 #pragma unroll
     for (int h = 0; h < SPL; ++h) cons[h] = 0.0f;
     signal_pass(cons, [](float& acc, int n, float vk) {
-      const float nv = (float)n * vk;
-      if (nv < 0.0f) acc += -nv;
+      // (acc - min(nv, 0): the sum of the consumptions -nv > 0, bit for bit; a NaN nv adds nothing)
+      acc -= fminf((float)n * vk, 0.0f);
     });
     combine(cons);
 #pragma unroll
@@ -909,12 +920,13 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     bool nan = false;
 #pragma unroll
     for (int q = 0; q < NZ; ++q) {
-      if (q >= cnt_w) break;
-      const int w = q < cnt ? ents[lane * ES + q] : 0;
-      if ((float)w_n(w) * v < 0.0f) {
-        const float f = Xs[EP::j(MS_E(q))];
-        if (ms::f_isnan(f)) nan = true;
-        else if (f < fmin) fmin = f;
+      if (q < cnt_w) {
+        const int w = q < cnt ? ents[lane * ES + q] : 0;
+        if ((float)w_n(w) * v < 0.0f) {
+          const float f = Xs[EP::j(MS_E(q))];
+          if (ms::f_isnan(f)) nan = true;
+          else if (f < fmin) fmin = f;
+        }
       }
     }
     if (prot) {
@@ -931,7 +943,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
 #pragma unroll
     for (int h = 0; h < SPL; ++h) x[h] = grp == 0 ? x0[h] : 0.0f;  // (multi-group: chunk 0 starts from X0)
     signal_pass(x, [](float& acc, int n, float b) {
-      if (n != 0) acc += (float)n * b;
+      acc = fmaf((float)n, b, acc);
     });
     combine(x);
 #pragma unroll
@@ -953,21 +965,25 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     for (int q = 0; q < NZ / 2; ++q) asm volatile("" : "+v"(e16[q]));  // (the same for the entry fields)
     {
       float pf = 1.0f, pb = 1.0f;
-      int nfs = 0, nbs = 0;
 #pragma unroll
       for (int q = 0; q < NZ; ++q) {
-        if (q >= cnt_w) break;
-        const int e = MS_E(q);
-        const int nf = EP::nf(e), nb = EP::nb(e);
-        const float x = Xs[EP::j(e)];
-        nfs |= nf;
-        nbs |= nb;
-        pf = nf > 0 ? pf * pw(x, nf) : pf;
-        pb = nb > 0 ? pb * pw(x, nb) : pb;
+        if (q < cnt_w) {
+          const int e = MS_E(q);
+          const int nf = EP::nf(e), nb = EP::nb(e);
+          const float x = Xs[EP::j(e)];
+          if (one_w) {  // (nf == 0 or nb == 0: x^(nf | nb) is the one power the entry needs)
+            const float p = pw(x, nf | nb);
+            pf = nf > 0 ? pf * p : pf;
+            pb = nb > 0 ? pb * p : pb;
+          } else {
+            pf = nf > 0 ? pf * pw(x, nf) : pf;
+            pb = nb > 0 ? pb * pw(x, nb) : pb;
+          }
+        }
       }
       if (prot) {
-        pf = nfs ? ms::clean_prod(pf) : 0.0f;
-        pb = nbs ? ms::clean_prod(pb) : 0.0f;
+        pf = nfs_p ? ms::clean_prod(pf) : 0.0f;
+        pb = nbs_p ? ms::clean_prod(pb) : 0.0f;
         float Q = pb / pf;
         if (ms::f_isnan(Q)) Q = 1.0f;
         else Q = Q < ms::kEps ? ms::kEps : (Q > ms::kMax ? ms::kMax : Q);

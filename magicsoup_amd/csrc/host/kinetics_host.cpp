@@ -122,7 +122,7 @@ unsigned cell_part(const CellParams& q, int np, int s, const float* X0, float tr
         for (int k = k0; k < k1; ++k) {
           const int p = act[k];
           const int32_t n = q.N[(size_t)p * s + j];
-          if (n != 0) part += (float)n * w_of(p);
+          part = std::fmaf((float)n, w_of(p), part);
         }
         tot = k0 == 0 ? part : tot + part;
       }

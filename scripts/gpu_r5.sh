@@ -28,6 +28,7 @@ trace() {  # trace <name> <steps-to-summarise> <bench args...>
   MARKER=${MARKER:-void msd::diffuse_stencil4} python scripts/step_kernels.py $O/$name/run_kernel_trace.csv $k > $O/${name}_steps.txt 2>&1
 }
 for s in "$@"; do case "$s" in
+  kt) run tests_kin 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -x -k "integrat or enzymatic or activity or kinetic" --timeout 300 --timeout-method thread ;;
   tmem) run tests_mem 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -k "memory_model or past_2_31" --timeout 300 --timeout-method thread ;;
   tests) run tests 1000 python -u -m pytest tests -m gpu -q --maxfail 5 --timeout 120 --timeout-method thread ;;
   smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -48,11 +49,9 @@ for s in "$@"; do case "$s" in
   isweep) run integrator_sweep 300 python scripts/integrator_sweep.py ;;
   dbench) run diffuse_bench 300 python scripts/diffuse_bench.py --dtypes fp32 --blocks 1024 2048 0 --band 0 64 ;;
   iab) for i in 1 2; do for m in 0 4096; do MS_INTEGRATE_MODE=$m run iab_${m}_$i 300 python bench.py --steps 60 --warmup 20; done; done ;;
-  abf) run ab_flagship 300 python scripts/ab_so.py abso/head.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so
-       run ab_flagship_grown 300 python scripts/ab_so.py --steps 150 abso/head.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so ;;
-  abw) run ab_wide 300 python scripts/ab_so.py --chem synthetic:64:256 abso/head.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so ;;
-  tcheck) echo "== trace tcheck"; timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/tcheck -o run --output-format csv -- python performance/check.py --parts update_cells > $O/tcheck.log 2>&1; echo "   rc=$?" ;;
-  sab) for i in 1 2; do for w in 4 3 2; do MS_SPL2_WAVES=$w run sab_${w}_$i 300 python bench.py --preset wide --steps 40 --warmup 10; done; done ;;
+  abf) run ab_flagship 300 python scripts/ab_so.py ${ABSO:-abso/head.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so}
+       run ab_flagship_grown 300 python scripts/ab_so.py --steps 150 ${ABSO:-abso/head.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so} ;;
+  abw) run ab_wide 300 python scripts/ab_so.py --chem synthetic:64:256 ${ABSO:-abso/head.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so} ;;
   pmcw|pmcf) # PMC of the integrator / stencil kernels (one pass, 8 SQ counters, kernel filter, no trace domains)
      preset=$([ "$s" = pmcw ] && echo wide || echo flagship)
      echo "== pmc $preset"
