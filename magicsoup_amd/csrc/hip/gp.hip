@@ -20,8 +20,9 @@ namespace msd {
 
 // ---- launchers defined in the other translation units
 void rec_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map, uintptr_t lens,
-               double p, uint64_t seed, uint64_t call, int kcap, uintptr_t gflags, uintptr_t opflags, uintptr_t keys,
-               uintptr_t k, uintptr_t sel, uintptr_t out_dev, int cap, uintptr_t stream);
+               uintptr_t lw_word, double p, uint64_t seed, uint64_t call, int kcap, uintptr_t gflags,
+               uintptr_t opflags, uintptr_t keys, uintptr_t k, uintptr_t sel, uintptr_t out_dev, int cap,
+               uintptr_t cand, uintptr_t stream);
 void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel, uintptr_t rest,
                         uintptr_t out_dev, uintptr_t stream);
 void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
@@ -52,7 +53,8 @@ void mut_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t rows, uintptr_t 
                uintptr_t k, double p_indel, double p_del, uint64_t seed, uint64_t call, uintptr_t out, int out_width,
                uintptr_t out_len, uintptr_t stream);
 void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
-                    uintptr_t tot, int kcap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
+                    uintptr_t tot, int kcap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream,
+                    uintptr_t lw_word);
 void rec_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t pairs, uintptr_t keys, uintptr_t arena, uintptr_t off,
                uintptr_t lens, uintptr_t k, uint64_t seed, uint64_t call, uintptr_t parts, int parts_cap, uintptr_t out,
                int out_width, uintptr_t out_len, uintptr_t out_rows, uintptr_t stream);
@@ -229,6 +231,7 @@ size_t gp_blob_bytes(int kind, int n, int cap, int P, int L, int dcap, int kcap,
   c.take((size_t)nr);                      // won
   c.take(8 * (size_t)nr);                  // q
   c.take(8 * (size_t)nr);                  // cells
+  c.take(8 * (size_t)cap);                 // thinned-draw candidates (world.hip rec_slots)
   return c.off + rebuild_bytes(nr, P, dcap, L) + 512;
 }
 
@@ -296,7 +299,7 @@ int gp_mutate(const GpArena& a, const GpGen& g, const GpKin& k, double p, double
 // recombinate_cells() over neighbour slot keys (8 per cell); `extra` (optional Python object with
 // .rows and .apply(pair_count, out, out_w, out_len, out_rows, nres)) appends strip-boundary results.
 // keys: the neighbour slot keys (8n int64); with `nbr` = (positions, R, C, r_lo, r_hi, wrap, index
-// map) they are computed here, fused with the draws and the selection count (world.hip rec_slots),
+// map, longest-genome word of index_map_lmax) they are computed here, fused with the draws and the selection count (world.hip rec_slots),
 // otherwise read.
 int gp_recombine(const GpArena& a, const GpGen& g, const GpKin& k, uintptr_t keys, py::object nbr, double p,
                  uint64_t seed, uint64_t call, int cap, int kcap, int dcap, uintptr_t mark, uint64_t gen,
@@ -310,12 +313,14 @@ int gp_recombine(const GpArena& a, const GpGen& g, const GpKin& k, uintptr_t key
   const uintptr_t out = c.take((size_t)nr * out_w), out_len = c.take(4 * (size_t)nr), out_rows = c.take(8 * (size_t)nr);
   const uintptr_t parts = c.take(4 * (size_t)cap * parts_cap * 3);
   const uintptr_t won = c.take((size_t)nr), q = c.take(8 * (size_t)nr), cells = c.take(8 * (size_t)nr);
+  const uintptr_t cand = c.take(8 * (size_t)cap);
   if (!nbr.is_none()) {
-    const auto t = nbr.cast<std::tuple<uintptr_t, int, int, int, int, int, uintptr_t>>();
+    const auto t = nbr.cast<std::tuple<uintptr_t, int, int, int, int, int, uintptr_t, uintptr_t>>();
     rec_slots(n, std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t), std::get<4>(t), std::get<5>(t),
-              std::get<6>(t), a.lens, p, seed, call, kcap, a.gflags, a.opflags, keys, kk, sel, a.cnt, cap, stream);
+              std::get<6>(t), a.lens, std::get<7>(t), p, seed, call, kcap, a.gflags, a.opflags, keys, kk, sel, a.cnt,
+              cap, cand, stream);
   } else {
-    rec_count_keys(8 * n, keys, a.lens, p, seed, call, kk, 0, kcap, a.gflags, a.opflags, stream);
+    rec_count_keys(8 * n, keys, a.lens, p, seed, call, kk, 0, kcap, a.gflags, a.opflags, stream, 0);
     select_indices_capped(8ll * n, kSelI32Pos, kk, sel, a.cnt, cap, a.gflags, a.opflags, stream);
   }
   rec_apply(cap, a.cnt, sel, 0, keys, a.data, a.off, a.lens, kk, seed, call, parts, parts_cap, out, out_w, out_len,
@@ -417,10 +422,11 @@ std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpAren
   const uintptr_t out = cr.take((size_t)nr * out_w), out_len = cr.take(4 * (size_t)nr), out_rows = cr.take(8 * (size_t)nr);
   const uintptr_t parts = cr.take(4 * (size_t)pcap * parts_cap * 3);
   const uintptr_t won = cr.take((size_t)nr), q = cr.take(8 * (size_t)nr), cells = cr.take(8 * (size_t)nr);
-  const auto t = nbr.cast<std::tuple<uintptr_t, int, int, int, int, int, uintptr_t>>();
+  const uintptr_t cand = cr.take(8 * (size_t)pcap);
+  const auto t = nbr.cast<std::tuple<uintptr_t, int, int, int, int, int, uintptr_t, uintptr_t>>();
   rec_slots(n, std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t), std::get<4>(t), std::get<5>(t),
-            std::get<6>(t), ar.lens, p_rec, seed_r, call_r, kcap, ar.gflags, ar.opflags, keys, kk, sel, ar.cnt, pcap,
-            stream);
+            std::get<6>(t), ar.lens, std::get<7>(t), p_rec, seed_r, call_r, kcap, ar.gflags, ar.opflags, keys, kk, sel,
+            ar.cnt, pcap, cand, stream);
   rec_apply(pcap, ar.cnt, sel, 0, keys, ar.data, ar.off, ar.lens, kk, seed_r, call_r, parts, parts_cap, out, out_w,
             out_len, out_rows, stream);
   if (xr) extra.attr("apply")(ar.cnt, out, out_w, out_len, out_rows, nres);

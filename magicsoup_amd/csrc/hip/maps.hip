@@ -119,12 +119,13 @@ __global__ void __launch_bounds__(64 * kWaves) diffuse_stencil_kernel(const T* _
 // smaller grid leaves workgroup slots free on every CU, so the side stream's short pipeline kernels
 // (deferred genome chains, World._flush_deferred) start at once instead of waiting for stencil
 // workgroups to retire (set_stencil_blocks).
-constexpr int kVBand = 32;     // rows per wave band of the vector stencils (default)
+constexpr int kVBand = 64;     // rows per wave band of the vector stencils (default)
 constexpr int kMinVBand = 16;  // the narrowest band set_stencil_band accepts
-// rows per wave band (set_stencil_band; 0 = the default 32): a band re-reads one halo row above and
+// rows per wave band (set_stencil_band; 0 = the default 64): a band re-reads one halo row above and
 // below it, so taller bands read less but leave fewer tiles per block of the grid-stride launch.
-// Same-box A/Bs at 4096^2 x 64 fp32 disagreed between boxes (64 rows: 1.529 vs 1.597 ms on one,
-// 1.77 vs 1.67 on another; profiles/r3/stencil_band/), 14 molecules preferred 32: the default stays.
+// With the branch-free ring (band_loop) 64 rows win at every map type: 4096^2 x 14, diffuse step
+// fp32 0.391 (32 rows, 1 row ahead, 1024 blocks) -> 0.357 ms (64 rows, 2 ahead, 768 blocks), bf16 /
+// fp16 0.212 / 0.220 -> 0.196 / 0.199 ms (3 ahead) (profiles/r5/stencil_ring.txt).
 static int g_vband = kVBand;
 void set_stencil_band(int b) { g_vband = b <= 0 ? kVBand : (b < kMinVBand ? kMinVBand : (b > 256 ? 256 : b)); }
 static int stencil_band(int, int, int, int, int) { return g_vband; }
@@ -134,7 +135,11 @@ static int stencil_band(int, int, int, int, int) { return g_vband; }
 // register copy waits for the loads at the end of the same row). PF >= 1: PF rows ahead in a ring of
 // PF + 1 raw buffers, unrolled by the ring size so every buffer is a fixed register set: a row's
 // loads are only waited for by the step that uses them, PF steps later. Rows past the band are
-// clamped to o1 (the halo row below it, already the last row the PF = 0 loop loads).
+// clamped to o1 (the halo row below it, already the last row the PF = 0 loop loads). Whole turns of
+// the ring run without a branch (and the fetches themselves are branch-free): the compiler's vmcnt
+// waits only count exactly across straight-line code, so a guard per row made every step wait for
+// all but the newest loads and the ring collapsed to one row in flight (scripts/stencil_lab.hip:
+// 4096^2 x 14 fp32, 360 -> 328-333 us at 3 rows ahead, 64-row bands, 512-768 blocks).
 template <int PF, class Raw, class Fetch, class Step>
 __device__ __forceinline__ void band_loop(int o0, int o1, Raw& first, Raw& spare, Fetch&& fetch, Step&& row_step) {
   if constexpr (PF == 0) {
@@ -149,7 +154,15 @@ __device__ __forceinline__ void band_loop(int o0, int o1, Raw& first, Raw& spare
     ring[0] = first;
 #pragma unroll
     for (int d = 1; d < PF; ++d) fetch(min(o0 + 1 + d, o1), ring[d]);
-    for (int o = o0; o < o1; o += NB) {
+    int o = o0;
+    for (; o + NB <= o1; o += NB) {
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        fetch(min(o + u + 1 + PF, o1), ring[(u + PF) % NB]);
+        row_step(o + u, ring[u]);
+      }
+    }
+    if (o < o1) {  // the band's last partial turn
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
         if (o + u < o1) {
@@ -160,7 +173,8 @@ __device__ __forceinline__ void band_loop(int o0, int o1, Raw& first, Raw& spare
     }
   }
 }
-template <class T, int PF>
+// FULL: every lane's columns exist (C a multiple of the wave's columns): no per-lane store branch
+template <class T, int PF, bool FULL = false>
 __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restrict__ in, T* __restrict__ out,
                                                                const float* __restrict__ wa,
                                                                const float* __restrict__ wb,
@@ -174,7 +188,7 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int H = g.r_hi - g.r_lo;
   const int y0 = bx * 256 + lane * 4;
-  const bool col = y0 < g.C;
+  const bool col = FULL || y0 < g.C;
   const bool need_l = lane == 0 && col, need_r = col && (lane == 63 || y0 + 4 >= g.C);
   const int yl = y0 == 0 ? g.C - 1 : y0 - 1, yr = y0 + 4 >= g.C ? 0 : y0 + 4;
   const size_t plane = (size_t)g.R * g.C;
@@ -193,29 +207,32 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
   struct Raw {  // raw bits: converted in finish(), so a prefetched row's loads stay in flight
     uint32_t v[4], el, er;
   };
+  // branch-free (see band_loop): every lane loads -- a lane past the last column its strip's first
+  // columns, zeroed after; the halo loads of the inner lanes their own first column (the same line)
+  const int yc = col ? y0 : bx * 256;
   auto fetch = [&](int o, Raw& r) {
     const size_t base = (size_t)row_of(o) * g.C;
-    if (col) {
-      if constexpr (sizeof(T) == 4) {
-        const uint4 q = *reinterpret_cast<const uint4*>(src + base + y0);
-        r.v[0] = q.x, r.v[1] = q.y, r.v[2] = q.z, r.v[3] = q.w;
-      } else {
-        const uint2 q = *reinterpret_cast<const uint2*>(src + base + y0);
-        r.v[0] = q.x & 0xFFFFu, r.v[1] = q.x >> 16, r.v[2] = q.y & 0xFFFFu, r.v[3] = q.y >> 16;
-      }
+    if constexpr (sizeof(T) == 4) {
+      const uint4 q = *reinterpret_cast<const uint4*>(src + base + yc);
+      r.v[0] = q.x, r.v[1] = q.y, r.v[2] = q.z, r.v[3] = q.w;
     } else {
-      r.v[0] = r.v[1] = r.v[2] = r.v[3] = 0u;
+      const uint2 q = *reinterpret_cast<const uint2*>(src + base + yc);
+      r.v[0] = q.x & 0xFFFFu, r.v[1] = q.x >> 16, r.v[2] = q.y & 0xFFFFu, r.v[3] = q.y >> 16;
     }
-    r.el = need_l ? ld_bits(src + base + yl) : 0u;
-    r.er = need_r ? ld_bits(src + base + yr) : 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r.v[j] = col ? r.v[j] : 0u;
+    r.el = ld_bits(src + base + (need_l ? yl : yc));
+    r.er = ld_bits(src + base + (need_r ? yr : yc));
   };
   // scaled values of the row plus the left neighbour of column y0 and the right one of y0 + 3
   auto finish = [&](const Raw& r, float v[4], float& L, float& Rn) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = corr_in(from_bits<T>(r.v[j]), corr, mol) * sc;
     const float up = __shfl_up(v[3], 1), dn = __shfl_down(v[0], 1);
-    L = need_l ? corr_in(from_bits<T>(r.el), corr, mol) * sc : up;
-    Rn = need_r ? corr_in(from_bits<T>(r.er), corr, mol) * sc : dn;
+    // (both edge values computed by every lane and selected: no branch, see band_loop)
+    const float el = corr_in(from_bits<T>(r.el), corr, mol) * sc, er = corr_in(from_bits<T>(r.er), corr, mol) * sc;
+    L = need_l ? el : up;
+    Rn = need_r ? er : dn;
   };
   auto hsum = [](const float v[4], float L, float Rn, float h[4]) {
     h[0] = L + v[0] + v[1];
@@ -287,7 +304,8 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
 // 4-column kernel reached ~5 TB/s on fp32 and stayed issue-bound on the 2-byte types. Same tiling
 // (4 waves = 4 consecutive 32-row bands of one column strip), same one-row-ahead prefetch, same
 // fp64 partials (the 8 values of a row are summed in fp32 first, as pairs of 4).
-template <class T, int PF>
+// FULL: every lane's columns exist (C a multiple of the wave's columns): no per-lane store branch
+template <class T, int PF, bool FULL = false>
 __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restrict__ in, T* __restrict__ out,
                                                                const float* __restrict__ wa,
                                                                const float* __restrict__ wb,
@@ -301,7 +319,7 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int H = g.r_hi - g.r_lo;
     const int y0 = bx * 512 + lane * 8;
-    const bool col = y0 < g.C;
+    const bool col = FULL || y0 < g.C;
     const bool need_l = lane == 0 && col, need_r = col && (lane == 63 || y0 + 8 >= g.C);
     const int yl = y0 == 0 ? g.C - 1 : y0 - 1, yr = y0 + 8 >= g.C ? 0 : y0 + 8;
     const size_t plane = (size_t)g.R * g.C;
@@ -323,12 +341,19 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
       Bits8<T> v;
       uint32_t el, er;
     };
-    auto fetch = [&](int o, Raw& r) {
+    const int yc = col ? y0 : bx * 512;
+    auto fetch = [&](int o, Raw& r) {  // (branch-free, as in diffuse_stencil4_kernel)
       const size_t base = (size_t)row_of(o) * g.C;
-      if (col) ld8_bits(src + base + y0, r.v);
-      else zero8_bits(r.v);
-      r.el = need_l ? ld_bits(src + base + yl) : 0u;
-      r.er = need_r ? ld_bits(src + base + yr) : 0u;
+      ld8_bits(src + base + yc, r.v);
+#pragma unroll
+      for (int i = 0; i < (int)(sizeof(r.v.q) / sizeof(uint4)); ++i) {
+        r.v.q[i].x = col ? r.v.q[i].x : 0u;
+        r.v.q[i].y = col ? r.v.q[i].y : 0u;
+        r.v.q[i].z = col ? r.v.q[i].z : 0u;
+        r.v.q[i].w = col ? r.v.q[i].w : 0u;
+      }
+      r.el = ld_bits(src + base + (need_l ? yl : yc));
+      r.er = ld_bits(src + base + (need_r ? yr : yc));
     };
     auto cin = [&](float raw) { return (has_c ? fmaxf(raw + cm, 0.0f) : raw) * sc; };
     auto finish = [&](const Raw& r, float v[8], float& L, float& Rn) {
@@ -336,8 +361,9 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = cin(v[j]);
       const float up = __shfl_up(v[7], 1), dn = __shfl_down(v[0], 1);
-      L = need_l ? cin(from_bits<T>(r.el)) : up;
-      Rn = need_r ? cin(from_bits<T>(r.er)) : dn;
+      const float el = cin(from_bits<T>(r.el)), er = cin(from_bits<T>(r.er));  // (selected: no branch)
+      L = need_l ? el : up;
+      Rn = need_r ? er : dn;
     };
     auto hsum = [](const float v[8], float L, float Rn, float h[8]) {
       h[0] = L + v[0] + v[1];
@@ -621,27 +647,30 @@ static bool use_vec8(int C, int dtype) {
 static bool use_vec4(int C) { return (g_stencil_vec == 0 || g_stencil_vec >= 4) && C % 4 == 0; }
 
 // rows in flight ahead of the vector stencils' current row (band_loop; set_stencil_prefetch, -1 =
-// auto = 0). Measured at 4096^2 x 14 (profiles/r3/stencil_pf/): the one-row loop is fastest for
-// every map type once rows stay raw bits until used (2-byte maps: 0.27-0.31 -> 0.217-0.225 ms; their
-// conversion right after the loads had waited for them); the PF-deep rings (1-3) are slower.
+// auto: 2 for fp32 maps, 3 for 2-byte maps). Round 3 measured the rings slower than one row ahead
+// (profiles/r3/stencil_pf/) -- their per-row guards and branchy edge loads made the compiler wait for
+// every load at each row, so they never had more than one row in flight; branch-free whole turns do.
 static int g_stencil_pf = -1;
 void set_stencil_prefetch(int pf) { g_stencil_pf = pf < -1 ? -1 : (pf > 3 ? 3 : pf); }
-static int stencil_pf(int) { return g_stencil_pf >= 0 ? g_stencil_pf : 0; }
+static int stencil_pf(int dtype) { return g_stencil_pf >= 0 ? g_stencil_pf : (dtype == kF32 ? 2 : 3); }
 // launch LAUNCH with the compile-time prefetch distance PF (and the map type T of MS_MAP_DISPATCH)
-#define MS_PF_DISPATCH(pf, LAUNCH)                                  \
+#define MS_PF_DISPATCH1(pf, LAUNCH)                                 \
   switch (pf) {                                                     \
     case 0: { constexpr int PF = 0; LAUNCH; } break;                \
     case 1: { constexpr int PF = 1; LAUNCH; } break;                \
     case 2: { constexpr int PF = 2; LAUNCH; } break;                \
     default: { constexpr int PF = 3; LAUNCH; } break;               \
   }
+// (and FULL: whether every lane of every strip has its columns, see diffuse_stencil4_kernel)
+#define MS_PF_DISPATCH(pf, full, LAUNCH)                                            \
+  if (full) { constexpr bool FULL = true; MS_PF_DISPATCH1(pf, LAUNCH) }             \
+  else { constexpr bool FULL = false; MS_PF_DISPATCH1(pf, LAUNCH) }
 
-// Blocks of the vector stencil launch (0: one per tile). 256 CUs x 4 workgroups (4 waves per SIMD)
-// still reach the stencil's full HBM rate and leave 3 of the 7 slots a CU holds at its register use
-// to the side stream. Kernel traces of the flagship step (scripts/gpu_trace_step.sh): stencil 378 /
-// side chain done 100 us after it at 1024 blocks; 385 / 125-166 at one block per tile; 375 / 153-167
-// at 1536; 427 / 75 at 896; 500 / done before it at 512.
-static int g_stencil_blocks = 256 * 4;
+// Blocks of the vector stencil launch (0: one per tile). 256 CUs x 3 workgroups (3 waves per SIMD)
+// with 2-3 rows in flight per wave reach the stencil's full HBM rate and leave most workgroup slots
+// of every CU to the side stream. Round 4 (one row in flight): stencil 378 / side chain done 100 us
+// after it at 1024 blocks; 385 / 125-166 at one block per tile; 427 / 75 at 896; 500 at 512.
+static int g_stencil_blocks = 256 * 3;
 void set_stencil_blocks(int n) { g_stencil_blocks = std::max(0, n); }
 
 size_t diffuse_partials_len(int m, int C, int H) {
@@ -668,14 +697,14 @@ static int stencil_launch(int m, int R, int C, int r_lo, int r_hi, int wrap, uin
   if (v8) {
     const int ntiles = (int)(grid.x * grid.y * grid.z);
     const int blocks = g_stencil_blocks > 0 ? std::min(ntiles, g_stencil_blocks) : ntiles;
-    MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), (diffuse_stencil8_kernel<T, PF><<<blocks, 256, 0, st_>>>(
+    MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), C % 512 == 0, (diffuse_stencil8_kernel<T, PF, FULL><<<blocks, 256, 0, st_>>>(
                                P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
                                corr ? P_<float>(corr) : nullptr, g, P_<double>(partials), (int)grid.x, (int)grid.y,
                                ntiles, vband))));
   } else if (v4) {
     const int ntiles = (int)(grid.x * grid.y * grid.z);
     const int blocks = g_stencil_blocks > 0 ? std::min(ntiles, g_stencil_blocks) : ntiles;
-    MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), (diffuse_stencil4_kernel<T, PF><<<blocks, 256, 0, st_>>>(
+    MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), C % 256 == 0, (diffuse_stencil4_kernel<T, PF, FULL><<<blocks, 256, 0, st_>>>(
                                P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
                                corr ? P_<float>(corr) : nullptr, g, P_<double>(partials), (int)grid.x, (int)grid.y,
                                ntiles, vband))));
@@ -716,11 +745,11 @@ static int boundary_launch(int m, int R, int C, int r_lo, int r_hi, uintptr_t ma
     const MGeom g = mgeom(R, C, row, row + 1, 0);
     double* part = P_<double>(partials) + (size_t)b * tiles * 2;
     if (v8) {
-      MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), (diffuse_stencil8_kernel<T, PF><<<tiles, 256, 0, st_>>>(
+      MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), C % 512 == 0, (diffuse_stencil8_kernel<T, PF, FULL><<<tiles, 256, 0, st_>>>(
                                  P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
                                  corr ? P_<float>(corr) : nullptr, g, part, gx, 1, tiles, kVBand))));
     } else if (v4) {
-      MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), (diffuse_stencil4_kernel<T, PF><<<tiles, 256, 0, st_>>>(
+      MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), C % 256 == 0, (diffuse_stencil4_kernel<T, PF, FULL><<<tiles, 256, 0, st_>>>(
                                  P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
                                  corr ? P_<float>(corr) : nullptr, g, part, gx, 1, tiles, kVBand))));
     } else {

@@ -33,7 +33,8 @@ int place_error_take();
 void neighbor_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map, uintptr_t keys,
                     uintptr_t stream);
 void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
-                    uintptr_t tot, int kcap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
+                    uintptr_t tot, int kcap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream,
+                    uintptr_t lw_word);
 // maps.hip
 size_t diffuse_partials_len(int m, int C, int H);
 void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t map, uintptr_t tmp, uintptr_t wa,
@@ -114,6 +115,8 @@ void pack_params(long long items, int s, uintptr_t N, uintptr_t Nf, uintptr_t Nb
 void claim_free(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uint64_t seed, uint64_t call,
                 int attempts, uintptr_t out, uintptr_t stream);
 void index_map(int c, uintptr_t pos, int C, uintptr_t idx_map, bool clear, uintptr_t stream);
+void index_map_lmax(int c, uintptr_t pos, int C, uintptr_t idx_map, uintptr_t lens, uintptr_t word, uint64_t gen,
+                    uintptr_t stream);
 void neighbor_pairs_sorted(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map,
                            uintptr_t in_from, uintptr_t in_to, uintptr_t keys, uintptr_t stream);
 
@@ -132,6 +135,7 @@ void translate_fused(int n, uintptr_t rows, uintptr_t arena, uintptr_t off, int 
                      uintptr_t long_count, uintptr_t dn, uintptr_t stream);
 size_t translate_slot_bytes(int width);
 void set_integrate_mode(int mode);
+void set_rec_thinning(int on);
 void set_spl2_waves(int w);
 void set_rescue_mode(int m);
 int rescue_error_take();
@@ -278,7 +282,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("set_coop_blocks", &msd::set_coop_blocks, "workgroups of the cooperative placement (A/B)");
   m.def("set_stencil_vec", &msd::set_stencil_vec, "diffusion stencil columns per lane: 8 (default), 4 or 1");
   m.def("set_stencil_prefetch", &msd::set_stencil_prefetch, "rows the vector stencils load ahead (-1 auto, 0-3)");
-  m.def("set_stencil_band", &msd::set_stencil_band, "rows per wave band of the vector stencils (16-256; 0 = the default 32)");
+  m.def("set_stencil_band", &msd::set_stencil_band, "rows per wave band of the vector stencils (16-256; 0 = the default 64)");
   m.def("set_stencil_blocks", &msd::set_stencil_blocks, "blocks of the vector diffusion stencil (0: one per tile)");
   m.def("set_place_mode", &msd::set_place_mode, "0 single-launch placement, ordinary launch (default), 1 multi-launch rounds, 2 single launch as a cooperative launch");
   m.def("place_error_take", &msd::place_error_take,
@@ -287,11 +291,13 @@ PYBIND11_MODULE(_hip, m) {
   m.def("permeate", &msd::permeate);
   m.def("claim_free", &msd::claim_free);
   m.def("index_map", &msd::index_map);
+  m.def("index_map_lmax", &msd::index_map_lmax, "index map + the longest genome into a (gen << 32 | length) word");
   m.def("neighbor_pairs_sorted", &msd::neighbor_pairs_sorted, "unique neighbour pairs in (a, b)-sorted slots");
   m.def("translate_count", &msd::translate_count);
   m.def("translate_write", &msd::translate_write);
   m.def("translate_fused", &msd::translate_fused);
   m.def("set_spl2_waves", &msd::set_spl2_waves, "waves per SIMD of the wide chemistries' narrow launch (2-4)");
+  m.def("set_rec_thinning", &msd::set_rec_thinning, "1: recombination draws by thinning + sort (0: per-slot draws + selection pass)");
   m.def("set_rescue_mode", &msd::set_rescue_mode, "1: one launch behind the speculative integrator (0: separate)");
   m.def("rescue_error_take", &msd::rescue_error_take, "1 if the integrator rescue launch's grid barrier timed out");
   m.def("set_integrate_mode", &msd::set_integrate_mode, "binned integrator launches: 0 serial, 1 concurrent, 2 concurrent + strided wide bin");

@@ -181,10 +181,14 @@ __global__ void __launch_bounds__(256) rec_count_kernel(int n, const int32_t* pa
   k[i] = (int32_t)(kk > nb ? nb : kk);
 }
 
-// Same draw over fixed neighbour slots (int64 keys (a << 32) | b, -1 = empty slot).
+// Same draw over fixed neighbour slots (int64 keys (a << 32) | b, -1 = empty slot). With `lw_word`
+// (world.hip index_map_lmax: the longest genome): by thinning against the bound len(a) + longest,
+// as world.hip rec_slot_draw (the device pipeline's draw: the same stream and order, so both paths
+// select the same pairs); without: directly.
 __global__ void __launch_bounds__(256) rec_count_keys_kernel(int n, const int64_t* keys, const int32_t* lens, double p,
                                                              uint64_t seed, uint64_t call, int32_t* k, int32_t* tot,
-                                                             int kcap, const int* gflags, int* opflags) {
+                                                             int kcap, const int* gflags, int* opflags,
+                                                             const unsigned long long* lw_word) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (gp_skip(i, gflags, opflags)) {
@@ -198,14 +202,25 @@ __global__ void __launch_bounds__(256) rec_count_keys_kernel(int n, const int64_
     if (tot) tot[i] = 0;
     return;
   }
-  const int nb = lens[key >> 32] + lens[key & 0xFFFFFFFF];
+  const int la = lens[key >> 32];
+  const int nb = la + lens[key & 0xFFFFFFFF];
   if (tot) tot[i] = nb;
-  if (nb < 1) {
-    k[i] = 0;
-    return;
+  long long kk = 0;
+  if (lw_word) {
+    const double lb = (double)la + (double)(int)(*lw_word & 0xFFFFFFFFull);
+    if (lb >= 1.0) {
+      Philox rng(seed, call, (uint32_t)i);
+      const long long nev = poisson(rng, p * lb);
+      for (long long e = 0; e < nev; ++e) kk += rng.uniform_d() * lb < (double)nb ? 1 : 0;
+    }
+  } else {
+    if (nb < 1) {
+      k[i] = 0;
+      return;
+    }
+    Philox rng(seed, call, (uint32_t)i);
+    kk = poisson(rng, p * (double)nb);
   }
-  Philox rng(seed, call, (uint32_t)i);
-  long long kk = poisson(rng, p * (double)nb);
   if (kcap > 0 && kk > kcap) kk = kcap;
   k[i] = (int32_t)(kk > nb ? nb : kk);
 }
@@ -374,11 +389,13 @@ void rec_count(int n, uintptr_t pairs, uintptr_t lens, double p, uint64_t seed, 
 }
 
 void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
-                    uintptr_t tot, int kcap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream) {
+                    uintptr_t tot, int kcap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream,
+                    uintptr_t lw_word) {
   if (n <= 0) return;
   rec_count_keys_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, P_<int64_t>(keys), P_<int32_t>(lens), p, seed, call,
                                                               P_<int32_t>(k), tot ? P_<int32_t>(tot) : nullptr, kcap,
-                                                              gflags ? P_<int>(gflags) : nullptr, P_<int>(opflags));
+                                                              gflags ? P_<int>(gflags) : nullptr, P_<int>(opflags),
+                                                              lw_word ? P_<unsigned long long>(lw_word) : nullptr);
   MS_LAUNCH_CHECK();
 }
 

@@ -9,6 +9,8 @@
 // domain-decomposed world (magicsoup_amd.parallel) has one halo row above and below its owned rows
 // (R = H + 2, r_lo = 1, r_hi = H + 1, no x wrap: the halo rows hold the neighbours' boundary rows).
 // The y axis always wraps (columns are never split).
+#include <unordered_map>
+
 #include "hip_common.h"
 
 namespace msd {
@@ -420,6 +422,24 @@ __global__ void __launch_bounds__(256) index_map_kernel(int c, const int32_t* po
   idx_map[(size_t)pos[2 * i] * C + pos[2 * i + 1]] = clear ? -1 : i;
 }
 
+// index_map_kernel + the longest genome of the c cells into `word` as (gen << 32) | length (one
+// atomicMax per wave; a larger `gen` than the last call's overrides it, so the word is never reset):
+// the bound of the recombination draws' thinning (rec_slot_draw), computed from the genomes alone so
+// the device pipeline and the synchronous path draw against the same bound
+__global__ void __launch_bounds__(256) index_map_lmax_kernel(int c, const int32_t* pos, int C, int32_t* idx_map,
+                                                             const int32_t* lens, unsigned long long* word,
+                                                             unsigned long long gen) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int l = 0;
+  if (i < c) {
+    idx_map[(size_t)pos[2 * i] * C + pos[2 * i + 1]] = i;
+    l = lens[i];
+  }
+  for (int o = 32; o > 0; o >>= 1) l = max(l, __shfl_xor(l, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(word, (gen << 32) | (unsigned long long)(unsigned)max(l, 0));
+}
+__device__ __forceinline__ int lmax_of(const unsigned long long* word) { return (int)(*word & 0xFFFFFFFFull); }
+
 // Unique neighbour pairs (a < b) between the cells marked in_from and the cells marked in_to, in
 // fixed slots: slot a*8 + j holds (a << 32) | b for the j-th smallest qualifying neighbour b > a of
 // cell a (a pair belongs to its smaller cell: no pair twice, no atomics), else -1. An
@@ -474,59 +494,66 @@ __global__ void __launch_bounds__(256) neighbor_slots_kernel(int n, const int32_
   keys[t] = key;
 }
 
+// The recombination draw of slot t (cell c = t / 8, its q-th Moore neighbour o), by thinning:
+// N ~ Poisson(p * Lb), Lb = len(c) + lw >= len(c) + len(o) (lw: the longest genome, index_map_lmax),
+// from the slot's Philox stream; each of the N events is kept with probability L / Lb (L = len(c) +
+// len(o)), so the kept count is Poisson(p * L), the per-slot rate of the reference's pairs. Only the
+// ~p * Lb of slots with N > 0 look up their neighbour: the 8n dependent random chains (position ->
+// neighbour pixel -> index map -> its position -> its length) of a direct draw ran next to the
+// diffusion stencil on the side stream, where every random load waits behind the stencil's HBM
+// stream (rec_slots 20 us alone, 53-83 us beside it: profiles/r5/side_chain.txt). The same stream
+// and draw order as rec_count_keys_kernel with lw >= 0 (the synchronous path): identical results.
+// Returns the clamped event count (0: no recombination) and the pair key.
+__device__ __forceinline__ int rec_slot_draw(long long t, int n, const int32_t* pos, const Geom& g,
+                                             const int32_t* idx_map, const int32_t* lens, int lw, double p,
+                                             uint64_t seed, uint64_t call, int kcap, int64_t& key) {
+  const int c = (int)(t >> 3);
+  const int lc = lens[c];
+  const double lb = (double)lc + (double)lw;
+  if (!(lb >= 1.0)) return 0;
+  Philox rng(seed, call, (uint32_t)t);
+  const long long nev = poisson(rng, p * lb);
+  if (nev == 0) return 0;
+  long long nb[8];
+  const int nn = moore(pos[2 * c], pos[2 * c + 1], g, nb);
+  const int q = (int)(t & 7);
+  if (q >= nn) return 0;
+  const int oo = cell_at(idx_map, pos, n, g.C, nb[q]);
+  if (oo <= c) return 0;  // (the pair belongs to its smaller cell; -1: no cell there)
+  const int L = lc + lens[oo];
+  long long x = 0;
+  for (long long e = 0; e < nev; ++e) x += rng.uniform_d() * lb < (double)L ? 1 : 0;
+  if (kcap > 0 && x > kcap) x = kcap;
+  key = ((int64_t)c << 32) | oo;
+  return (int)(x > L ? L : x);
+}
+
 // Neighbour slots fused with the recombination draws of the device pipeline (gp_recombine) and
 // the count pass of their selection: per tile of kSlotTile slots (16 per thread, the tiling of
-// select.hip), the key of slot t (as neighbor_slots_kernel), k[t] ~ Poisson(p * (len a + len b))
-// with the per-slot Philox stream of rec_count_keys_kernel (identical draws), and the tile's
+// select.hip), the key and draw of slot t (rec_slot_draw: Poisson(p * (len a + len b)), the draws of
+// rec_count_keys_kernel over neighbor_slots_kernel's keys), and the tile's
 // number of slots with k > 0. One pass instead of three launches over the 8n slots; the write
 // pass (select.hip) follows. A chain already broken by a narrow arena (gflags width bit) draws
 // nothing and marks the call skipped, as gp_skip does.
 constexpr int kSlotItems = 4, kSlotBlock = 256 * kSlotItems;  // 1024 slots per block: a count per
                                                                 // quarter of select.hip's 4096-item tile
 __global__ void __launch_bounds__(256) rec_slots_kernel(int n, const int32_t* pos, Geom g, const int32_t* idx_map,
-                                                        const int32_t* lens, double p, uint64_t seed, uint64_t call,
-                                                        int kcap, const int* gflags, int* opflags, int64_t* keys,
-                                                        int32_t* kout, int32_t* tile_count, int32_t* tile_max) {
+                                                        const int32_t* lens, const unsigned long long* lw_word,
+                                                        double p, uint64_t seed,
+                                                        uint64_t call, int kcap, const int* gflags, int* opflags,
+                                                        int64_t* keys, int32_t* kout, int32_t* tile_count,
+                                                        int32_t* tile_max) {
   const bool skip = gflags && (*gflags & 8);  // mutations.hip kGpWidth
   if (skip && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(opflags, 16);  // kGpSkipped
   const long long base = (long long)blockIdx.x * kSlotBlock, total = 8LL * n;
-  // the items' dependent random loads (position -> neighbour pixel -> index map -> its position
-  // -> genome lengths) are issued item-parallel, so a thread has all its chains in flight at once
-  long long px[kSlotItems];
-  int o[kSlotItems];
-#pragma unroll
-  for (int j = 0; j < kSlotItems; ++j) {
-    const long long t = base + j * 256 + threadIdx.x;
-    px[j] = -1;
-    if (t < total) {
-      const int c = (int)(t >> 3), q = (int)(t & 7);
-      long long nb[8];
-      const int nn = moore(pos[2 * c], pos[2 * c + 1], g, nb);
-      if (q < nn) px[j] = nb[q];
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < kSlotItems; ++j) o[j] = px[j] >= 0 ? idx_map[px[j]] : -1;
+  const int lw = lmax_of(lw_word);
   int cnt = 0;
 #pragma unroll
   for (int j = 0; j < kSlotItems; ++j) {
     const long long t = base + j * 256 + threadIdx.x;
     if (t >= total) continue;
-    const int c = (int)(t >> 3);
-    int oo = o[j];
-    if (oo < 0 || oo >= n || ((long long)pos[2 * oo] * g.C + pos[2 * oo + 1]) != px[j]) oo = -1;  // cell_at
     int64_t key = -1;
-    int kk = 0;
-    if (oo > c) {
-      key = ((int64_t)c << 32) | oo;
-      const int L = lens[c] + lens[oo];
-      if (!skip && L >= 1) {
-        Philox rng(seed, call, (uint32_t)t);
-        long long x = poisson(rng, p * (double)L);
-        if (kcap > 0 && x > kcap) x = kcap;
-        kk = (int)(x > L ? L : x);
-      }
-    }
+    const int kk = skip ? 0 : rec_slot_draw(t, n, pos, g, idx_map, lens, lw, p, seed, call, kcap, key);
     // (the pipeline reads keys only at the selected slots, kk > 0: ~1e-4 of them at the bench's
     // rate, so the other 8n - k key stores are skipped)
     if (kk > 0) keys[t] = key;
@@ -540,6 +567,82 @@ __global__ void __launch_bounds__(256) rec_slots_kernel(int n, const int32_t* po
   if (threadIdx.x == 0) {
     tile_count[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
     tile_max[blockIdx.x] = 0;
+  }
+}
+
+// The selection of rec_slots_kernel's draws without its count array and selection pass (the default
+// when the pair capacity fits rec_sort_kernel): the slots with events are appended (one atomic each,
+// ~1e-4 of the slots at the bench's rate) and put in slot order by rec_sort_kernel.
+constexpr int kRecSortCap = 4096;  // pair capacity of the thinned path (rec_sort_kernel's LDS)
+__global__ void __launch_bounds__(256) rec_draw_kernel(int n, const int32_t* pos, Geom g, const int32_t* idx_map,
+                                                       const int32_t* lens, const unsigned long long* lw_word,
+                                                       double p, uint64_t seed,
+                                                       uint64_t call, int kcap, const int* gflags, int* opflags,
+                                                       int64_t* keys, int32_t* kout, int64_t* cand, int* cand_count,
+                                                       int cap) {
+  const bool skip = gflags && (*gflags & 8);  // mutations.hip kGpWidth
+  if (skip) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(opflags, 16);  // kGpSkipped
+    return;
+  }
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 8LL * n) return;
+  int64_t key = -1;
+  const int kk = rec_slot_draw(t, n, pos, g, idx_map, lens, lmax_of(lw_word), p, seed, call, kcap, key);
+  if (kk <= 0) return;
+  keys[t] = key;
+  kout[t] = kk;
+  const int j = atomicAdd(cand_count, 1);
+  if (j < cap) cand[j] = t;
+}
+
+// One workgroup: the appended candidate slots into ascending slot order (bitonic sort in LDS) ->
+// sel[0 : count] and out_dev = {count, 0}, as the capped selection pass writes them; more candidates
+// than `cap` void the call (kGpSkipped / kGpWidth, the host replays it: select.hip cap semantics).
+// The counter is reset for the next call on this stream.
+__global__ void __launch_bounds__(1024) rec_sort_kernel(const int64_t* cand, int* cand_count, int cap, int64_t* sel,
+                                                        int32_t* out_dev, int* gflags, int* opflags) {
+  __shared__ int64_t s_v[kRecSortCap];
+  __shared__ int s_total;
+  if (threadIdx.x == 0) {
+    s_total = *cand_count;
+    *cand_count = 0;
+  }
+  __syncthreads();
+  int total = s_total;
+  if (total > cap) {
+    if (threadIdx.x == 0) {
+      atomicOr(opflags, 16);  // kGpSkipped
+      atomicOr(gflags, 8);    // kGpWidth
+      out_dev[0] = 0;
+      out_dev[1] = 0;
+    }
+    return;
+  }
+  int np2 = 1;
+  while (np2 < total) np2 <<= 1;
+  for (int i = threadIdx.x; i < np2; i += blockDim.x) s_v[i] = i < total ? cand[i] : INT64_MAX;
+  __syncthreads();
+  for (int k = 2; k <= np2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < np2; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const int64_t a = s_v[i], b = s_v[l];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) {
+            s_v[i] = b;
+            s_v[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < total; i += blockDim.x) sel[i] = s_v[i];
+  if (threadIdx.x == 0) {
+    out_dev[0] = total;
+    out_dev[1] = 0;
   }
 }
 
@@ -771,6 +874,15 @@ void index_map(int c, uintptr_t pos, int C, uintptr_t idx_map, bool clear, uintp
   MS_LAUNCH_CHECK();
 }
 
+void index_map_lmax(int c, uintptr_t pos, int C, uintptr_t idx_map, uintptr_t lens, uintptr_t word, uint64_t gen,
+                    uintptr_t stream) {
+  if (c <= 0) return;
+  if (gen == 0 || gen >= (1ull << 31)) throw std::invalid_argument("index_map_lmax: generation out of range");
+  index_map_lmax_kernel<<<cdiv(c, 256), 256, 0, S_(stream)>>>(c, P_<int32_t>(pos), C, P_<int32_t>(idx_map),
+                                                               P_<int32_t>(lens), P_<unsigned long long>(word), gen);
+  MS_LAUNCH_CHECK();
+}
+
 void neighbor_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map, uintptr_t keys,
                     uintptr_t stream) {
   if (n <= 0) return;
@@ -784,20 +896,46 @@ std::pair<int32_t*, int32_t*> select_tiles(long long tiles, hipStream_t s);
 void select_write_i32pos_capped(long long n, uintptr_t src, int32_t* tc, int32_t* tm, int sub, uintptr_t sel,
                                 uintptr_t out_dev, int cap, uintptr_t gflags, uintptr_t opflags, hipStream_t s);
 
-// rec_slots_kernel + the capped selection of slots with k > 0 into sel / out_dev (gp_recombine)
+// per-stream candidate counters of rec_draw_kernel (zero between calls: rec_sort_kernel resets them)
+static std::unordered_map<hipStream_t, int*> g_rec_cnt;
+static int g_rec_thin = 1;  // 0: the count + selection passes for every capacity (A/B)
+void set_rec_thinning(int on) { g_rec_thin = on; }
+
+// The recombination draws of all slots (rec_slot_draw) + the capped selection of slots with k > 0
+// into sel / out_dev (gp_recombine): appended and sorted (rec_draw_kernel + rec_sort_kernel) with a
+// pair capacity of at most kRecSortCap, else rec_slots_kernel + the selection pass. `lw`: the
+// longest genome (index_map_lmax's word). `cand`: 8 * cap bytes of scratch.
 void rec_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map, uintptr_t lens,
-               double p, uint64_t seed, uint64_t call, int kcap, uintptr_t gflags, uintptr_t opflags, uintptr_t keys,
-               uintptr_t k, uintptr_t sel, uintptr_t out_dev, int cap, uintptr_t stream) {
+               uintptr_t lw_word, double p, uint64_t seed, uint64_t call, int kcap, uintptr_t gflags,
+               uintptr_t opflags, uintptr_t keys, uintptr_t k, uintptr_t sel, uintptr_t out_dev, int cap,
+               uintptr_t cand, uintptr_t stream) {
   if (n <= 0) throw std::invalid_argument("rec_slots: no cells");
   const Geom g = geom(R, C, r_lo, r_hi, wrap);
   hipStream_t s = S_(stream);
   const long long total = 8LL * n;
+  if (!lw_word) throw std::invalid_argument("rec_slots: the longest-genome word of index_map_lmax is required");
+  const auto* lw = P_<unsigned long long>(lw_word);
+  if (g_rec_thin && cand && cap <= kRecSortCap) {
+    int*& cnt = g_rec_cnt[s];
+    if (!cnt) {
+      MS_HIP_CHECK(hipMalloc((void**)&cnt, sizeof(int)));
+      MS_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int), s));
+    }
+    rec_draw_kernel<<<(unsigned)cdiv(total, 256), 256, 0, s>>>(
+        n, P_<int32_t>(pos), g, P_<int32_t>(idx_map), P_<int32_t>(lens), lw, p, seed, call, kcap, P_<int>(gflags),
+        P_<int>(opflags), P_<int64_t>(keys), P_<int32_t>(k), P_<int64_t>(cand), cnt, cap);
+    MS_LAUNCH_CHECK();
+    rec_sort_kernel<<<1, 1024, 0, s>>>(P_<int64_t>(cand), cnt, cap, P_<int64_t>(sel), P_<int32_t>(out_dev),
+                                       P_<int>(gflags), P_<int>(opflags));
+    MS_LAUNCH_CHECK();
+    return;
+  }
   constexpr int kSelTile = 4096;  // select.hip
   const long long blocks = (total + kSelTile - 1) / kSelTile * (kSelTile / kSlotBlock);
   auto tiles = select_tiles(blocks, s);
   // (the blocks past the last slot write zero counts: the write pass reads whole tiles' counts)
-  rec_slots_kernel<<<(unsigned)blocks, 256, 0, s>>>(n, P_<int32_t>(pos), g, P_<int32_t>(idx_map), P_<int32_t>(lens), p,
-                                                    seed, call, kcap, P_<int>(gflags), P_<int>(opflags),
+  rec_slots_kernel<<<(unsigned)blocks, 256, 0, s>>>(n, P_<int32_t>(pos), g, P_<int32_t>(idx_map), P_<int32_t>(lens), lw,
+                                                    p, seed, call, kcap, P_<int>(gflags), P_<int>(opflags),
                                                     P_<int64_t>(keys), P_<int32_t>(k), tiles.first, tiles.second);
   MS_LAUNCH_CHECK();
   select_write_i32pos_capped(total, k, tiles.first, tiles.second, kSelTile / kSlotBlock, sel, out_dev, cap, gflags,

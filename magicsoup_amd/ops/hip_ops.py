@@ -441,7 +441,7 @@ def diffuse(world) -> None:
     m = int(mm.size(0))
     sc = _scratch(world)
     dev = mm.device
-    tmp = sc.get("diff_tmp", mm.numel(), mm.dtype, dev)
+    tmp = _diff_tmp(sc, mm)
     partials = sc.get("diff_partials", int(_m().diffuse_partials_len(m, C, r_hi - r_lo)), torch.float64, dev)
     totals = sc.get("diff_totals", 2 * m, torch.float64, dev)
     w = _diff_weights(world)
@@ -500,6 +500,28 @@ def diffuse(world) -> None:
     sc.bufs["diff_tmp"] = mm.view(-1)
     d["_pending_scale"] = None
     d["_pending_corr"] = new_corr
+
+
+# The stencil's output buffer sits at an address offset of _MAP_SKEW (mod 2 MiB) against the map's: a
+# read stream and a write stream whose addresses differ by a multiple of 1 MiB hit the same HBM
+# channels at the same time (scripts/stencil_lab.hip, 4096^2 x 14 fp32 on MI355X: a float4 copy
+# 5.50 TB/s at offset 0 or 1 MiB, 5.90-5.96 at 4 KiB, 1 MiB + 4 KiB or 2 MiB + 8 KiB; the pipelined
+# stencil 350-355 -> 328-333 us). The two buffers swap every step, so the offset holds both ways.
+_MAP_SKEW = int(os.environ.get("MS_MAP_SKEW", 8192))
+_SKEW_PERIOD = 2 << 20
+
+
+def _diff_tmp(sc, mm):
+    t = sc.bufs.get("diff_tmp")
+    n = mm.numel()
+    if t is not None and t.numel() == n and t.dtype == mm.dtype and t.device == mm.device:
+        return t
+    es = mm.element_size()
+    buf = torch.empty(n + _SKEW_PERIOD // es, dtype=mm.dtype, device=mm.device)
+    off = ((_MAP_SKEW - (buf.data_ptr() - mm.data_ptr())) % _SKEW_PERIOD) // es
+    t = buf[off:off + n]
+    sc.bufs["diff_tmp"] = t
+    return t
 
 
 # interior / boundary split of a strip's stencil around the halo exchange (MS_HALO_OVERLAP=0: off)
@@ -1001,7 +1023,10 @@ def recombinate_all(world, p: float, rng=None) -> torch.Tensor:
     k = sc.get("nb_k", 8 * n, torch.int32, dev)
     tot = sc.get("nb_tot", 8 * n, torch.int32, dev)
     seed, call = rng if rng is not None else _rng()
-    _m().rec_count_keys(8 * n, _p(keys), _p(arena.lens), float(p), seed, call, _p(k), _p(tot), 0, 0, 0, _stream())
+    # (drawn by thinning against the longest genome, as the device pipeline's slot pass: the same
+    # pairs on both paths, world.hip rec_slot_draw)
+    _m().rec_count_keys(8 * n, _p(keys), _p(arena.lens), float(p), seed, call, _p(k), _p(tot), 0, 0, 0, _stream(),
+                        _p(_lmax_word(world)))
     return _rec_apply(world, None, keys, k, tot, seed, call)
 
 
@@ -1014,25 +1039,45 @@ def neighbor_slot_keys(world) -> torch.Tensor:
     _ensure_world_layout(world)
     pos = world.cell_positions
     idx_map = _index_map(world, R * C, dev)
-    _m().index_map(n, _p(pos), C, _p(idx_map), False, _stream())
+    _index_map_lmax(world, n, pos, C, idx_map)
     keys = _scratch(world).get("nb_keys", 8 * n, torch.int64, dev)
     _m().neighbor_slots(n, _p(pos), R, C, r_lo, r_hi, wrap, _p(idx_map), _p(keys), _stream())
     return keys
 
 
+def _lmax_word(world) -> torch.Tensor:
+    """The (generation << 32) | longest-genome word of index_map_lmax (one per world, never reset)."""
+    sc = _scratch(world)
+    w = sc.bufs.get("lmax_word")
+    if w is None:
+        w = sc.bufs["lmax_word"] = torch.zeros(1, dtype=torch.int64, device=world._genomes.data.device)
+    return w
+
+
+def _index_map_lmax(world, n, pos, C, idx_map) -> None:
+    """The index map of the current positions + the longest genome into _lmax_word (the bound of
+    the recombination draws' thinning, world.hip rec_slot_draw)."""
+    sc = _scratch(world)
+    gen = sc.bufs["lmax_gen"] = sc.bufs.get("lmax_gen", 0) % ((1 << 31) - 1) + 1
+    if gen == 1:  # (the generation wrapped or starts: a fresh word)
+        _lmax_word(world).zero_()
+    _m().index_map_lmax(n, _p(pos), C, _p(idx_map), _p(world._genomes.lens), _p(_lmax_word(world)), gen, _stream())
+
+
 def neighbor_slot_args(world):
     """The index map of the current positions plus the buffers / arguments of the fused neighbour
     slot pass of the device pipeline (gp.hip gp_recombine -> world.hip rec_slots): the slot keys
-    buffer (8n int64, written there) and (positions, R, C, r_lo, r_hi, wrap, index map)."""
+    buffer (8n int64, written there) and (positions, R, C, r_lo, r_hi, wrap, index map, the
+    longest-genome word of the thinned draws)."""
     R, C, r_lo, r_hi, wrap = geom(world)
     dev = world._genomes.data.device
     n = world.n_cells
     _ensure_world_layout(world)
     pos = world.cell_positions
     idx_map = _index_map(world, R * C, dev)
-    _m().index_map(n, _p(pos), C, _p(idx_map), False, _stream())
+    _index_map_lmax(world, n, pos, C, idx_map)
     keys = _scratch(world).get("nb_keys", 8 * n, torch.int64, dev)
-    return keys, (_p(pos), R, C, r_lo, r_hi, wrap, _p(idx_map))
+    return keys, (_p(pos), R, C, r_lo, r_hi, wrap, _p(idx_map), _p(_lmax_word(world)))
 
 
 def _rec_apply(world, pairs, keys, k: torch.Tensor, tot: torch.Tensor, seed: int, call: int) -> torch.Tensor:

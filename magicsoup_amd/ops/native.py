@@ -89,6 +89,15 @@ def hip():
     if fresh and os.environ.get("MS_STENCIL_BLOCKS"):
         # blocks of the diffusion stencil launch (maps.hip; 0: one per tile)
         mod.set_stencil_blocks(int(os.environ["MS_STENCIL_BLOCKS"]))  # type: ignore[attr-defined]
+    if fresh and os.environ.get("MS_REC_THIN"):
+        # 0: the per-slot recombination draws + selection pass (world.hip rec_slots) for A/B
+        mod.set_rec_thinning(int(os.environ["MS_REC_THIN"]))  # type: ignore[attr-defined]
+    if fresh and os.environ.get("MS_STENCIL_PF"):
+        # rows in flight ahead of the stencil's current row (-1: auto, 0-3)
+        mod.set_stencil_prefetch(int(os.environ["MS_STENCIL_PF"]))  # type: ignore[attr-defined]
+    if fresh and os.environ.get("MS_STENCIL_BAND"):
+        # rows per wave band of the vector stencils (0: auto)
+        mod.set_stencil_band(int(os.environ["MS_STENCIL_BAND"]))  # type: ignore[attr-defined]
     return mod
 
 

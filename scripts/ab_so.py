@@ -5,7 +5,7 @@ timed alternately with module A and module B, and their results are compared bit
 Each module is timed in every integrate mode of --modes (comma list, default 0); results must be
 bit-identical across modules and modes.
 
-usage: python scripts/ab_so.py [--size S] [--cells C] [--chem wl|synthetic:M:R] [--modes 0,128] [--steps K]
+usage: python scripts/ab_so.py [--size S] [--cells C] [--chem wl|synthetic:M:R] [--modes 0,128] [--steps K] [--iters I]
                                A.so B.so [C.so ...]"""
 import importlib.machinery
 import importlib.util
@@ -48,7 +48,7 @@ def timed(fn, iters=20):
 
 def main():
     args = sys.argv[1:]
-    size, cells, chem_spec, modes, steps = 4096, 50000, "wl", [0], 5
+    size, cells, chem_spec, modes, steps, iters = 4096, 50000, "wl", [0], 5, 4
     while args and args[0].startswith("--"):
         flag, val = args[0], args[1]
         args = args[2:]
@@ -60,6 +60,8 @@ def main():
             chem_spec = val
         elif flag == "--steps":
             steps = int(val)
+        elif flag == "--iters":
+            iters = int(val)
         else:
             modes = [int(v) for v in val.split(",")]
     mods = {chr(65 + i): load(p, f"v{i}") for i, p in enumerate(args)}
@@ -86,9 +88,9 @@ def main():
                 for mode in modes:
                     mod.set_integrate_mode(mode)
                     Xk = X.clone()
-                    out[f"{tag}_m{mode}_r{rep}"] = timed(lambda: kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4))
+                    out[f"{tag}_m{mode}_r{rep}"] = timed(lambda: kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), iters))
                     Xk = X.clone()
-                    kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), 4)
+                    kinetics_ops.integrate(kin, Xk, (0.7, 0.2, 0.1), iters)
                     res[f"{tag}_m{mode}"] = Xk
                 mod.set_integrate_mode(0)
         first = next(iter(res.values()))

@@ -29,6 +29,9 @@ trace() {  # trace <name> <steps-to-summarise> <bench args...>
 }
 for s in "$@"; do case "$s" in
   kt) run tests_kin 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -x -k "integrat or enzymatic or activity or kinetic" --timeout 300 --timeout-method thread ;;
+  dt) run tests_diff 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_distributed.py -m gpu -q -x -k "diffus or stencil or mass or halo or strip" --timeout 300 --timeout-method thread ;;
+  gt) run tests_gen 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_mutation_stats.py tests/test_gpu_distributed.py -m gpu -q -x -k "pipeline or recomb or evolve or merged or mutat or genetic" --timeout 300 --timeout-method thread ;;
+  rthin) for i in 1 2; do for t in 1 0; do MS_REC_THIN=$t run rthin_${t}_$i 300 python bench.py; done; done ;;
   tmem) run tests_mem 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -k "memory_model or past_2_31" --timeout 300 --timeout-method thread ;;
   tests) run tests 1000 python -u -m pytest tests -m gpu -q --maxfail 5 --timeout 120 --timeout-method thread ;;
   smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -39,6 +42,8 @@ for s in "$@"; do case "$s" in
   virt) MS_VIRTUAL_STRIPS=1 run proxy8_virtual 300 python bench.py --map-size 1448 --cells 6250 ;;
   fvirt) MS_VIRTUAL_STRIPS=1 run flagship_virtual 300 python bench.py ;;
   hsf) run host_split_flagship 300 python scripts/host_split.py 4096 50000 40 ;;
+  hsfc) MS_CPROFILE=1 MS_CPROFILE_SORT=cumulative MS_CPROFILE_N=80 run host_split_flagship_cprofile 300 python scripts/host_split.py 4096 50000 40 ;;
+  hsfn) MS_NATIVE_TIMES=1 MS_PY_TIMES=1 run host_split_flagship_detail 300 python scripts/host_split.py 4096 50000 40 ;;
   hsp) run host_split_proxy8 300 python scripts/host_split.py 1448 6250 60 ;;
   hsv) MS_VIRTUAL_STRIPS=1 run host_split_proxy8_virtual 300 python scripts/host_split.py 1448 6250 60 ;;
   hspn) MS_NATIVE_TIMES=1 MS_PY_TIMES=1 run host_split_proxy8_detail 300 python scripts/host_split.py 1448 6250 60 ;;
@@ -47,10 +52,15 @@ for s in "$@"; do case "$s" in
   hsvc) MS_VIRTUAL_STRIPS=1 MS_CPROFILE=1 run host_split_proxy8_virtual_cprofile 300 python scripts/host_split.py 1448 6250 60 ;;
   upd) PROBE_PROFILE=1 run update_cells_probe 300 python scripts/update_cells_probe.py ;;
   isweep) run integrator_sweep 300 python scripts/integrator_sweep.py ;;
+  sab2) for i in 1 2; do for cfg in ${SAB2:-0,32,1024 2,64,768 2,64,512 3,64,512 1,64,768 2,64,1024 1,32,1024}; do IFS=, read pf bd bl <<< "$cfg"
+         MS_STENCIL_PF=$pf MS_STENCIL_BAND=$bd MS_STENCIL_BLOCKS=$bl run sab2_${pf}_${bd}_${bl}_$i 300 python bench.py; done; done ;;
+  dlab) for sk in 0 8192; do MS_MAP_SKEW=$sk run dlab_skew$sk 300 python scripts/diffuse_bench.py --dtypes fp32 --pf 0 1 2 3 --band 0 64 --blocks 768 1024; done ;;
+  dlab2) run dlab2 300 python scripts/diffuse_bench.py --dtypes fp32 bf16 fp16 --pf 0 2 3 --band 0 64 --blocks 512 768 0 ;;
   dbench) run diffuse_bench 300 python scripts/diffuse_bench.py --dtypes fp32 --blocks 1024 2048 0 --band 0 64 ;;
   iab) for i in 1 2; do for m in 0 4096; do MS_INTEGRATE_MODE=$m run iab_${m}_$i 300 python bench.py --steps 60 --warmup 20; done; done ;;
   abf) run ab_flagship 300 python scripts/ab_so.py ${ABSO:-abso/head.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so}
        run ab_flagship_grown 300 python scripts/ab_so.py --steps 150 ${ABSO:-abso/head.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so} ;;
+  itc) for it in 0 1 2 4; do run itc_$it 300 python scripts/ab_so.py --iters $it magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so; done ;;
   abw) run ab_wide 300 python scripts/ab_so.py --chem synthetic:64:256 ${ABSO:-abso/head.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so} ;;
   pmcw|pmcf) # PMC of the integrator / stencil kernels (one pass, 8 SQ counters, kernel filter, no trace domains)
      preset=$([ "$s" = pmcw ] && echo wide || echo flagship)
@@ -69,6 +79,7 @@ for s in "$@"; do case "$s" in
   c1024) run c1024 300 python bench.py --preset c1024 --steps 30 --warmup 5 ;;
   c256) run c256_40k 300 python bench.py --map-size 256 --cells 40000 ;;
   tflag) trace tflag 19 --steps 20 --warmup 20 ;;
+  tnodefer) MS_DEFER_GENOME_OPS=0 trace tnodefer 19 --steps 20 --warmup 20 ;;
   tc256) trace tc256 19 --map-size 256 --cells 40000 --steps 20 --warmup 20 ;;
   hs256) MS_NATIVE_TIMES=1 MS_PY_TIMES=1 run host_split_c256 300 python scripts/host_split.py 256 40000 40 ;;
   hs256c) MS_CPROFILE=1 MS_CPROFILE_SORT=cumulative MS_CPROFILE_N=70 run host_split_c256_cprofile 300 python scripts/host_split.py 256 40000 60 ;;

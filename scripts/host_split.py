@@ -24,7 +24,7 @@ S = int(sys.argv[1]) if len(sys.argv) > 1 else 1448
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 6250
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 60
 
-OPS = ["spawn_cells", "enzymatic_activity", "kill_cells", "divide_cells_t", "recombinate_cells", "mutate_cells",
+OPS = ["spawn_cells", "enzymatic_activity", "kill_divide_where", "kill_divide_t", "kill_cells", "divide_cells_t", "recombinate_cells", "mutate_cells",
        "degrade_molecules", "diffuse_molecules", "increment_cell_lifetimes"]
 busy = collections.defaultdict(float)
 blocked = collections.defaultdict(float)
