@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 
+#include <chrono>
 #include <cstdint>
 #include <mutex>
 #include <vector>
@@ -54,7 +55,31 @@ bool ev_query(uintptr_t e) {
   return true;
 }
 
-void ev_sync(uintptr_t e) { MS_HIP_CHECK(hipEventSynchronize(reinterpret_cast<hipEvent_t>(e))); }
+// Host wait for an event. hipEventSynchronize spins only briefly and then blocks on an interrupt:
+// the op layer's waits (a kill_divide waiting for the previous genome chain, a flush for a
+// division's count) last 0.1-0.3 ms, and the thread woke tens of microseconds after the event, with
+// the step's next launches behind it. Spinning on the event (query + pause) for up to kSpinNs first
+// returns within a microsecond of the completion; longer waits still block (set_event_spin(0): block
+// at once).
+static int g_ev_spin = 1;
+void set_event_spin(int on) { g_ev_spin = on; }
+void ev_sync(uintptr_t e) {
+  hipEvent_t ev = reinterpret_cast<hipEvent_t>(e);
+  if (g_ev_spin) {
+    constexpr int64_t kSpinNs = 20'000'000;  // 20 ms
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 0;; ++it) {
+      const hipError_t r = hipEventQuery(ev);
+      if (r == hipSuccess) return;
+      if (r != hipErrorNotReady) MS_HIP_CHECK(r);
+      __builtin_ia32_pause();
+      if ((it & 255u) == 255u &&
+          std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() > kSpinNs)
+        break;
+    }
+  }
+  MS_HIP_CHECK(hipEventSynchronize(ev));
+}
 
 // `dst` waits for everything issued to `src` so far (a fresh pooled event in between)
 void stream_join(uintptr_t dst, uintptr_t src) {
@@ -79,6 +104,7 @@ void bind_events(py::module_& m) {
   m.def("ev_wait", &ev_wait);
   m.def("ev_query", &ev_query);
   m.def("ev_sync", &ev_sync, py::call_guard<py::gil_scoped_release>());
+  m.def("set_event_spin", &set_event_spin, "1: host event waits spin before blocking (0: block at once)");
   m.def("stream_join", &stream_join);
 }
 

@@ -22,7 +22,7 @@ namespace msd {
 void rec_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map, uintptr_t lens,
                uintptr_t lw_word, double p, uint64_t seed, uint64_t call, int kcap, uintptr_t gflags,
                uintptr_t opflags, uintptr_t keys, uintptr_t k, uintptr_t sel, uintptr_t out_dev, int cap,
-               uintptr_t cand, uintptr_t stream);
+               uintptr_t cand, uintptr_t stream, uintptr_t na, uintptr_t nb);
 void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, uintptr_t sel, uintptr_t rest,
                         uintptr_t out_dev, uintptr_t stream);
 void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
@@ -46,7 +46,8 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
                   uintptr_t dn, uintptr_t stream);
 int translate_lds_max();  // genetics.hip: the longest genome of the LDS translation pass
 void mut_count_select(int n, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
-                      uintptr_t gflags, uintptr_t opflags, uintptr_t sel, uintptr_t out_dev, int cap, uintptr_t stream);
+                      uintptr_t gflags, uintptr_t opflags, uintptr_t sel, uintptr_t out_dev, int cap, uintptr_t cand,
+                      uintptr_t stream, uintptr_t na, uintptr_t nb);
 void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
                uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
 void mut_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t rows, uintptr_t arena, uintptr_t off, uintptr_t lens,
@@ -65,6 +66,16 @@ void arena_scatter(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t sr
 
 void select_indices_capped(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t out_dev, int cap,
                            uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
+void arena_scatter_app(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t src, int src_width, uintptr_t src_len,
+                       uintptr_t pool, uintptr_t off, uintptr_t top, long long pool_cap, int width, uintptr_t lens,
+                       uintptr_t mark, uint64_t gen, uintptr_t gflags, uintptr_t opflags, uintptr_t cand,
+                       uintptr_t stream);
+int* append_counter(hipStream_t s);
+void sel_sort(uintptr_t cand, int* cnt, int cap, uintptr_t sel, uintptr_t out_dev, uintptr_t gflags, uintptr_t opflags,
+              hipStream_t s, uintptr_t gather);
+int sel_sort_cap();
+extern int g_mut_append;
+
 std::pair<long long*, int> status_slot();
 
 // ---- fused small steps of the rebuild chain
@@ -207,6 +218,26 @@ int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const Gp
 }
 }  // namespace
 
+// The recombination's commit and the list of its changed cells: the winning result rows (the last
+// result per cell) committed and their cells listed in result order -- appended by the commit and
+// sorted + gathered in one launch (sel_sort), or (more result rows than the sort holds, or the
+// append paths off) the `won` flags, their selection and a gather.
+void commit_rec_results(int nr, uintptr_t dn, int dn_mul, uintptr_t out_rows, uintptr_t out, int out_w,
+                        uintptr_t out_len, const GpArena& a, int L, uintptr_t mark, uint64_t gen, uintptr_t won,
+                        uintptr_t q, uintptr_t cells, uintptr_t stream) {
+  if (g_mut_append && nr <= sel_sort_cap()) {
+    arena_scatter_app(nr, dn, dn_mul, out_rows, out, out_w, out_len, a.data, a.off, a.top, a.pool_cap, L, a.lens, mark,
+                      gen, a.gflags, a.opflags, q, stream);
+    hipStream_t s = S_(stream);
+    sel_sort(q, append_counter(s), nr, cells, a.cnt2, 0, 0, s, out_rows);
+    return;
+  }
+  arena_scatter(nr, dn, dn_mul, out_rows, out, out_w, out_len, a.data, a.off, a.top, a.pool_cap, L, a.lens, mark, gen,
+                won, a.gflags, a.opflags, stream);
+  select_indices_dev(nr, kSelSet, won, 0, q, 0, a.cnt2, stream);
+  gather_dev(nr, a.cnt2, q, out_rows, cells, stream);
+}
+
 // Scratch bytes of one call (the caller passes a blob of at least this size; the blob must stay
 // untouched until the call was reconciled: it holds the results a replay may re-commit).
 size_t gp_blob_bytes(int kind, int n, int cap, int P, int L, int dcap, int kcap, int extra_rows) {
@@ -218,6 +249,7 @@ size_t gp_blob_bytes(int kind, int n, int cap, int P, int L, int dcap, int kcap,
     c.take(8 * (size_t)n);                 // sel
     c.take((size_t)cap * out_w);           // out
     c.take(4 * (size_t)cap);               // out_len
+    c.take(8 * (size_t)cap);               // appended draws (mutations.hip mut_count_select)
     return c.off + rebuild_bytes(cap, P, dcap, L) + 512;
   }
   // recombinations: cap = pairs capacity
@@ -289,7 +321,8 @@ int gp_mutate(const GpArena& a, const GpGen& g, const GpKin& k, double p, double
   const uintptr_t kk = c.take(4 * (size_t)n), sel = c.take(8 * (size_t)n);
   const int out_w = (L + kcap + 15) / 16 * 16;
   const uintptr_t out = c.take((size_t)cap * out_w), out_len = c.take(4 * (size_t)cap);
-  mut_count_select(n, a.lens, p, seed, call, kk, kcap, a.gflags, a.opflags, sel, a.cnt, cap, stream);
+  const uintptr_t cand = c.take(8 * (size_t)cap);
+  mut_count_select(n, a.lens, p, seed, call, kk, kcap, a.gflags, a.opflags, sel, a.cnt, cap, cand, stream, 0, 0);
   mut_apply(cap, a.cnt, sel, 0, a.data, a.off, a.lens, kk, p_indel, p_del, seed, call, out, out_w, out_len, stream);
   arena_scatter(cap, a.cnt, 1, sel, out, out_w, out_len, a.data, a.off, a.top, a.pool_cap, L, a.lens, 0, 0, 0,
                 a.gflags, a.opflags, stream);
@@ -318,7 +351,7 @@ int gp_recombine(const GpArena& a, const GpGen& g, const GpKin& k, uintptr_t key
     const auto t = nbr.cast<std::tuple<uintptr_t, int, int, int, int, int, uintptr_t, uintptr_t>>();
     rec_slots(n, std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t), std::get<4>(t), std::get<5>(t),
               std::get<6>(t), a.lens, std::get<7>(t), p, seed, call, kcap, a.gflags, a.opflags, keys, kk, sel, a.cnt,
-              cap, cand, stream);
+              cap, cand, stream, 0, 0);
   } else {
     rec_count_keys(8 * n, keys, a.lens, p, seed, call, kk, 0, kcap, a.gflags, a.opflags, stream, 0);
     select_indices_capped(8ll * n, kSelI32Pos, kk, sel, a.cnt, cap, a.gflags, a.opflags, stream);
@@ -328,13 +361,9 @@ int gp_recombine(const GpArena& a, const GpGen& g, const GpKin& k, uintptr_t key
   if (xr) {
     extra.attr("apply")(a.cnt, out, out_w, out_len, out_rows, nres);
   }
-  // (a0, b0, a1, b1, ..., extra rows): the last result per cell wins (reference update order);
-  // arena_scatter also clears the `won` flags past the live rows
-  arena_scatter(nr, xr ? nres : a.cnt, xr ? 1 : 2, out_rows, out, out_w, out_len, a.data, a.off, a.top, a.pool_cap, L,
-                a.lens, mark, gen, won,
-                a.gflags, a.opflags, stream);
-  select_indices_dev(nr, kSelSet, won, 0, q, 0, a.cnt2, stream);
-  gather_dev(nr, a.cnt2, q, out_rows, cells, stream);
+  // (a0, b0, a1, b1, ..., extra rows): the last result per cell wins (reference update order)
+  commit_rec_results(nr, xr ? nres : a.cnt, xr ? 1 : 2, out_rows, out, out_w, out_len, a, L, mark, gen, won, q, cells,
+                     stream);
   return rebuild(nr, cells, a.cnt2, a, g, k, dcap, c, xr ? nres : a.cnt, s);
 }
 
@@ -398,7 +427,8 @@ size_t gp_evolve_union_bytes(int ucap, int P, int dcap, int L) {
 // fields are the same in all three). `extra` / `nres`: strip-boundary recombination results of a
 // decomposed world, appended after the local pairs' results (as in gp_recombine; the parts status
 // then counts result rows instead of pairs). `arr0` / `narr`: cells whose parameters are built with
-// the union (a strip's arrivals, magicsoup_amd/parallel/dist_world.py _divide_phase_b). Returns
+// the union (a strip's arrivals, magicsoup_amd/parallel/dist_world.py _divide_phase_b). `nd_a` /
+// `nd_b`: device words whose sum is the cell count, `ar.n` its bound (World._chain_bound), or 0. Returns
 // (union status slot {count, flags, row counter, count}, parts status slot {pairs or result rows, rec
 // flags, mutated, mut flags}).
 std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpArena& au, const GpGen& g, const GpKin& k,
@@ -406,7 +436,7 @@ std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpAren
                               double p, double p_indel, double p_del, uint64_t seed_m, uint64_t call_m, int mcap,
                               int kcap, int dcap, uintptr_t mark, uint64_t gen, uintptr_t blob_r, uintptr_t blob_m,
                               uintptr_t blob_u, bool fresh, long long nrows, py::object extra, uintptr_t nres,
-                              long long arr0, int narr, uintptr_t stream) {
+                              long long arr0, int narr, uintptr_t nd_a, uintptr_t nd_b, uintptr_t stream) {
   hipStream_t s = S_(stream);
   if (narr < 0) throw std::invalid_argument("gp_evolve: negative arrival count");
   const int n = ar.n, L = ar.width;
@@ -426,20 +456,20 @@ std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpAren
   const auto t = nbr.cast<std::tuple<uintptr_t, int, int, int, int, int, uintptr_t, uintptr_t>>();
   rec_slots(n, std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t), std::get<4>(t), std::get<5>(t),
             std::get<6>(t), ar.lens, std::get<7>(t), p_rec, seed_r, call_r, kcap, ar.gflags, ar.opflags, keys, kk, sel,
-            ar.cnt, pcap, cand, stream);
+            ar.cnt, pcap, cand, stream, nd_a, nd_b);
   rec_apply(pcap, ar.cnt, sel, 0, keys, ar.data, ar.off, ar.lens, kk, seed_r, call_r, parts, parts_cap, out, out_w,
             out_len, out_rows, stream);
   if (xr) extra.attr("apply")(ar.cnt, out, out_w, out_len, out_rows, nres);
-  arena_scatter(nr, xr ? nres : ar.cnt, xr ? 1 : 2, out_rows, out, out_w, out_len, ar.data, ar.off, ar.top,
-                ar.pool_cap, L, ar.lens, mark, gen, won, ar.gflags, ar.opflags, stream);
-  select_indices_dev(nr, kSelSet, won, 0, q, 0, ar.cnt2, stream);
-  gather_dev(nr, ar.cnt2, q, out_rows, cells, stream);
+  commit_rec_results(nr, xr ? nres : ar.cnt, xr ? 1 : 2, out_rows, out, out_w, out_len, ar, L, mark, gen, won, q, cells,
+                     stream);
   // point mutations over the recombined genomes (gp_mutate's layout of blob_m, without its rebuild)
   Carve cm(blob_m);
   const uintptr_t mk = cm.take(4 * (size_t)n), msel = cm.take(8 * (size_t)n);
   const int mout_w = (L + kcap + 15) / 16 * 16;
   const uintptr_t mout = cm.take((size_t)mcap * mout_w), mout_len = cm.take(4 * (size_t)mcap);
-  mut_count_select(n, am.lens, p, seed_m, call_m, mk, kcap, am.gflags, am.opflags, msel, am.cnt, mcap, stream);
+  const uintptr_t mcand = cm.take(8 * (size_t)mcap);
+  mut_count_select(n, am.lens, p, seed_m, call_m, mk, kcap, am.gflags, am.opflags, msel, am.cnt, mcap, mcand, stream,
+                   nd_a, nd_b);
   mut_apply(mcap, am.cnt, msel, 0, am.data, am.off, am.lens, mk, p_indel, p_del, seed_m, call_m, mout, mout_w, mout_len,
             stream);
   arena_scatter(mcap, am.cnt, 1, msel, mout, mout_w, mout_len, am.data, am.off, am.top, am.pool_cap, L, am.lens, 0, 0,

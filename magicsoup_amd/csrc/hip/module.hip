@@ -116,7 +116,8 @@ void claim_free(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uin
                 int attempts, uintptr_t out, uintptr_t stream);
 void index_map(int c, uintptr_t pos, int C, uintptr_t idx_map, bool clear, uintptr_t stream);
 void index_map_lmax(int c, uintptr_t pos, int C, uintptr_t idx_map, uintptr_t lens, uintptr_t word, uint64_t gen,
-                    uintptr_t stream);
+                    uintptr_t na, uintptr_t nb, uintptr_t stream);
+int sel_sort_cap();
 void neighbor_pairs_sorted(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map,
                            uintptr_t in_from, uintptr_t in_to, uintptr_t keys, uintptr_t stream);
 
@@ -292,12 +293,13 @@ PYBIND11_MODULE(_hip, m) {
   m.def("claim_free", &msd::claim_free);
   m.def("index_map", &msd::index_map);
   m.def("index_map_lmax", &msd::index_map_lmax, "index map + the longest genome into a (gen << 32 | length) word");
+  m.def("sel_sort_cap", &msd::sel_sort_cap, "capacity of the append + sort selections of the genome pipeline");
   m.def("neighbor_pairs_sorted", &msd::neighbor_pairs_sorted, "unique neighbour pairs in (a, b)-sorted slots");
   m.def("translate_count", &msd::translate_count);
   m.def("translate_write", &msd::translate_write);
   m.def("translate_fused", &msd::translate_fused);
   m.def("set_spl2_waves", &msd::set_spl2_waves, "waves per SIMD of the wide chemistries' narrow launch (2-4)");
-  m.def("set_rec_thinning", &msd::set_rec_thinning, "1: recombination draws by thinning + sort (0: per-slot draws + selection pass)");
+  m.def("set_rec_thinning", &msd::set_rec_thinning, "1: recombination (thinned) and mutation draws appended + sorted (0: count + selection passes)");
   m.def("set_rescue_mode", &msd::set_rescue_mode, "1: one launch behind the speculative integrator (0: separate)");
   m.def("rescue_error_take", &msd::rescue_error_take, "1 if the integrator rescue launch's grid barrier timed out");
   m.def("set_integrate_mode", &msd::set_integrate_mode, "binned integrator launches: 0 serial, 1 concurrent, 2 concurrent + strided wide bin");

@@ -82,6 +82,27 @@ __global__ void __launch_bounds__(256) mut_count_tiles_kernel(int n, const int32
   }
 }
 
+// mut_count_tiles_kernel's draws with the cells that mutate appended (one atomic each, ~n p L of the
+// n cells) instead of a count array and a selection pass; world.hip sel_sort puts them in cell order.
+__global__ void __launch_bounds__(256) mut_draw_kernel(int n, const int32_t* lens, double p, uint64_t seed,
+                                                       uint64_t call, int32_t* k, int kcap, const int* gflags,
+                                                       int* opflags, int64_t* cand, int* cand_count, int cap,
+                                                       const int* na, const int* nb) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (na) n = min(n, *na + *nb);  // (a chain issued on a device cell count, world.hip dev_count)
+  if (i >= n || gp_skip(i, gflags, opflags)) return;
+  const int L = lens[i];
+  if (L < 1) return;
+  Philox rng(seed, call, (uint32_t)i);
+  long long d = poisson(rng, p * (double)L);
+  if (kcap > 0 && d > kcap) d = kcap;
+  const int kk = (int)(d > L ? L : d);
+  if (kk <= 0) return;
+  k[i] = kk;
+  const int j = atomicAdd(cand_count, 1);
+  if (j < cap) cand[j] = i;
+}
+
 // One mutation event at nucleotide `ch`: the 0..2 nucleotides it emits (reference
 // rust/mutations.rs:30-60: indel with p_indel, then deletion with p_del, else insertion before ch;
 // otherwise a substitution that may repeat the old nucleotide).
@@ -292,7 +313,8 @@ __global__ void __launch_bounds__(64) arena_scatter_kernel(int k, const int* dn,
                                                            uint8_t* pool, int64_t* off, unsigned long long* top,
                                                            long long pool_cap, int width, int32_t* lens,
                                                            const unsigned long long* mark, unsigned long long gen,
-                                                           uint8_t* flags, int* gflags, int* opflags) {
+                                                           uint8_t* flags, int* gflags, int* opflags,
+                                                           int64_t* app_cand = nullptr, int* app_cnt = nullptr) {
   const int ke = eff_count(k, dn, dn_mul), lane = threadIdx.x;
   if (flags)  // entries past the live count read as "not won" (no separate clearing launch)
     for (int q = ke + blockIdx.x * 64 + lane; q < k; q += gridDim.x * 64) flags[q] = 0;
@@ -302,6 +324,7 @@ __global__ void __launch_bounds__(64) arena_scatter_kernel(int k, const int* dn,
     const bool won = !mark || mark[r] == ((gen << 32) | (unsigned long long)q);
     if (lane == 0 && flags) flags[q] = won;
     if (!won) continue;
+    if (lane == 0 && app_cnt) app_cand[atomicAdd(app_cnt, 1)] = q;  // (winners appended: world.hip sel_sort)
     if (gflags && src_len[q] > width) {  // longer than the bound: left for the host (reconcile)
       if (lane == 0) {
         atomicOr(gflags, kGpWidth);
@@ -353,12 +376,33 @@ std::pair<int32_t*, int32_t*> select_tiles(long long tiles, hipStream_t s);
 void select_write_i32pos_capped(long long n, uintptr_t src, int32_t* tc, int32_t* tm, int sub, uintptr_t sel,
                                 uintptr_t out_dev, int cap, uintptr_t gflags, uintptr_t opflags, hipStream_t s);
 
+int* append_counter(hipStream_t s);
+void sel_sort(uintptr_t cand, int* cnt, int cap, uintptr_t sel, uintptr_t out_dev, uintptr_t gflags, uintptr_t opflags,
+              hipStream_t s, uintptr_t gather = 0);
+int sel_sort_cap();
+extern int g_mut_append;
+int g_mut_append = 1;  // 0: the count + selection passes for every capacity (A/B, set_rec_thinning)
+
 // mut_count over all n genomes + the capped selection of those with events into sel / out_dev (the
-// device pipeline's mutation chain): two launches instead of three (the count pass is fused).
+// device pipeline's mutation chain): the draws appended + sorted (mut_draw_kernel, world.hip
+// sel_sort; `cand`: 8 * cap bytes of scratch) when the capacity fits the sort, else the fused count
+// pass + the selection pass.
 void mut_count_select(int n, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
-                      uintptr_t gflags, uintptr_t opflags, uintptr_t sel, uintptr_t out_dev, int cap, uintptr_t stream) {
+                      uintptr_t gflags, uintptr_t opflags, uintptr_t sel, uintptr_t out_dev, int cap, uintptr_t cand,
+                      uintptr_t stream, uintptr_t na, uintptr_t nb) {
   if (n <= 0) throw std::invalid_argument("mut_count_select: no genomes");
   hipStream_t s = S_(stream);
+  if (g_mut_append && cand && cap <= sel_sort_cap()) {
+    int* cnt = append_counter(s);
+    mut_draw_kernel<<<cdiv(n, 256), 256, 0, s>>>(n, P_<int32_t>(lens), p, seed, call, P_<int32_t>(k), kcap,
+                                                 gflags ? P_<int>(gflags) : nullptr, P_<int>(opflags),
+                                                 P_<int64_t>(cand), cnt, cap, na ? P_<int>(na) : nullptr,
+                                                 nb ? P_<int>(nb) : nullptr);
+    MS_LAUNCH_CHECK();
+    sel_sort(cand, cnt, cap, sel, out_dev, gflags, opflags, s);
+    return;
+  }
+  if (na) throw std::invalid_argument("mut_count_select: a device cell count needs the append path");
   constexpr int kSelTile = 4096, kBlock = 256;  // select.hip tile; 16 count blocks per tile
   const long long blocks = ((long long)n + kSelTile - 1) / kSelTile * (kSelTile / kBlock);
   auto tiles = select_tiles(blocks, s);
@@ -414,10 +458,11 @@ void rec_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t pairs, uintptr_t
 }
 
 // k result rows (capacity when dn != 0: then *dn * dn_mul rows are live)
-void arena_scatter(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t src, int src_width, uintptr_t src_len,
-                   uintptr_t pool, uintptr_t off, uintptr_t top, long long pool_cap, int width, uintptr_t lens,
-                   uintptr_t mark, uint64_t gen, uintptr_t flags, uintptr_t gflags, uintptr_t opflags,
-                   uintptr_t stream) {
+static void arena_scatter_impl(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t src, int src_width,
+                               uintptr_t src_len, uintptr_t pool, uintptr_t off, uintptr_t top, long long pool_cap,
+                               int width, uintptr_t lens, uintptr_t mark, uint64_t gen, uintptr_t flags,
+                               uintptr_t gflags, uintptr_t opflags, uintptr_t stream, int64_t* app_cand,
+                               int* app_cnt) {
   if (gflags && !opflags) throw std::invalid_argument("arena_scatter: gflags needs opflags");
   if (k <= 0) return;
   const int* d = dn ? P_<int>(dn) : nullptr;
@@ -429,8 +474,26 @@ void arena_scatter(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t sr
   arena_scatter_kernel<<<item_grid(k, dn), 64, 0, S_(stream)>>>(
       k, d, dn_mul, P_<int64_t>(rows), P_<uint8_t>(src), src_width, P_<int32_t>(src_len), P_<uint8_t>(pool),
       P_<int64_t>(off), P_<unsigned long long>(top), pool_cap, width, P_<int32_t>(lens), mark ? P_<unsigned long long>(mark) : nullptr, gen, flags ? P_<uint8_t>(flags) : nullptr,
-      gflags ? P_<int>(gflags) : nullptr, opflags ? P_<int>(opflags) : nullptr);
+      gflags ? P_<int>(gflags) : nullptr, opflags ? P_<int>(opflags) : nullptr, app_cand, app_cnt);
   MS_LAUNCH_CHECK();
+}
+
+void arena_scatter(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t src, int src_width, uintptr_t src_len,
+                   uintptr_t pool, uintptr_t off, uintptr_t top, long long pool_cap, int width, uintptr_t lens,
+                   uintptr_t mark, uint64_t gen, uintptr_t flags, uintptr_t gflags, uintptr_t opflags,
+                   uintptr_t stream) {
+  arena_scatter_impl(k, dn, dn_mul, rows, src, src_width, src_len, pool, off, top, pool_cap, width, lens, mark, gen,
+                     flags, gflags, opflags, stream, nullptr, nullptr);
+}
+
+// arena_scatter with the winning result rows appended to `cand` (k int64 entries) on the stream's
+// append counter instead of `won` flags for a selection pass (gp.hip: world.hip sel_sort orders them)
+void arena_scatter_app(int k, uintptr_t dn, int dn_mul, uintptr_t rows, uintptr_t src, int src_width, uintptr_t src_len,
+                       uintptr_t pool, uintptr_t off, uintptr_t top, long long pool_cap, int width, uintptr_t lens,
+                       uintptr_t mark, uint64_t gen, uintptr_t gflags, uintptr_t opflags, uintptr_t cand,
+                       uintptr_t stream) {
+  arena_scatter_impl(k, dn, dn_mul, rows, src, src_width, src_len, pool, off, top, pool_cap, width, lens, mark, gen, 0,
+                     gflags, opflags, stream, P_<int64_t>(cand), append_counter(S_(stream)));
 }
 
 }  // namespace msd

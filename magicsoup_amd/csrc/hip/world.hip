@@ -422,16 +422,22 @@ __global__ void __launch_bounds__(256) index_map_kernel(int c, const int32_t* po
   idx_map[(size_t)pos[2 * i] * C + pos[2 * i + 1]] = clear ? -1 : i;
 }
 
+// the cell count of a chain issued before the host knows it (World._chain_bound): n is the bound,
+// the count the sum of two device words (a kill_divide's survivors and placed children)
+__device__ __forceinline__ int dev_count(int n, const int* na, const int* nb) {
+  return na ? min(n, *na + *nb) : n;
+}
+
 // index_map_kernel + the longest genome of the c cells into `word` as (gen << 32) | length (one
 // atomicMax per wave; a larger `gen` than the last call's overrides it, so the word is never reset):
 // the bound of the recombination draws' thinning (rec_slot_draw), computed from the genomes alone so
 // the device pipeline and the synchronous path draw against the same bound
 __global__ void __launch_bounds__(256) index_map_lmax_kernel(int c, const int32_t* pos, int C, int32_t* idx_map,
                                                              const int32_t* lens, unsigned long long* word,
-                                                             unsigned long long gen) {
+                                                             unsigned long long gen, const int* na, const int* nb) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   int l = 0;
-  if (i < c) {
+  if (i < dev_count(c, na, nb)) {
     idx_map[(size_t)pos[2 * i] * C + pos[2 * i + 1]] = i;
     l = lens[i];
   }
@@ -579,13 +585,14 @@ __global__ void __launch_bounds__(256) rec_draw_kernel(int n, const int32_t* pos
                                                        double p, uint64_t seed,
                                                        uint64_t call, int kcap, const int* gflags, int* opflags,
                                                        int64_t* keys, int32_t* kout, int64_t* cand, int* cand_count,
-                                                       int cap) {
+                                                       int cap, const int* na, const int* nb) {
   const bool skip = gflags && (*gflags & 8);  // mutations.hip kGpWidth
   if (skip) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(opflags, 16);  // kGpSkipped
     return;
   }
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  n = dev_count(n, na, nb);
   if (t >= 8LL * n) return;
   int64_t key = -1;
   const int kk = rec_slot_draw(t, n, pos, g, idx_map, lens, lmax_of(lw_word), p, seed, call, kcap, key);
@@ -599,9 +606,10 @@ __global__ void __launch_bounds__(256) rec_draw_kernel(int n, const int32_t* pos
 // One workgroup: the appended candidate slots into ascending slot order (bitonic sort in LDS) ->
 // sel[0 : count] and out_dev = {count, 0}, as the capped selection pass writes them; more candidates
 // than `cap` void the call (kGpSkipped / kGpWidth, the host replays it: select.hip cap semantics).
-// The counter is reset for the next call on this stream.
+// The counter is reset for the next call on this stream. With `gather`: sel[i] = gather[sorted i].
 __global__ void __launch_bounds__(1024) rec_sort_kernel(const int64_t* cand, int* cand_count, int cap, int64_t* sel,
-                                                        int32_t* out_dev, int* gflags, int* opflags) {
+                                                        int32_t* out_dev, int* gflags, int* opflags,
+                                                        const int64_t* gather) {
   __shared__ int64_t s_v[kRecSortCap];
   __shared__ int s_total;
   if (threadIdx.x == 0) {
@@ -612,8 +620,8 @@ __global__ void __launch_bounds__(1024) rec_sort_kernel(const int64_t* cand, int
   int total = s_total;
   if (total > cap) {
     if (threadIdx.x == 0) {
-      atomicOr(opflags, 16);  // kGpSkipped
-      atomicOr(gflags, 8);    // kGpWidth
+      if (opflags) atomicOr(opflags, 16);  // kGpSkipped
+      if (gflags) atomicOr(gflags, 8);     // kGpWidth
       out_dev[0] = 0;
       out_dev[1] = 0;
     }
@@ -639,7 +647,7 @@ __global__ void __launch_bounds__(1024) rec_sort_kernel(const int64_t* cand, int
       __syncthreads();
     }
   }
-  for (int i = threadIdx.x; i < total; i += blockDim.x) sel[i] = s_v[i];
+  for (int i = threadIdx.x; i < total; i += blockDim.x) sel[i] = gather ? gather[s_v[i]] : s_v[i];
   if (threadIdx.x == 0) {
     out_dev[0] = total;
     out_dev[1] = 0;
@@ -875,11 +883,13 @@ void index_map(int c, uintptr_t pos, int C, uintptr_t idx_map, bool clear, uintp
 }
 
 void index_map_lmax(int c, uintptr_t pos, int C, uintptr_t idx_map, uintptr_t lens, uintptr_t word, uint64_t gen,
-                    uintptr_t stream) {
+                    uintptr_t na, uintptr_t nb, uintptr_t stream) {
   if (c <= 0) return;
   if (gen == 0 || gen >= (1ull << 31)) throw std::invalid_argument("index_map_lmax: generation out of range");
+  if ((na == 0) != (nb == 0)) throw std::invalid_argument("index_map_lmax: give both device count words or neither");
   index_map_lmax_kernel<<<cdiv(c, 256), 256, 0, S_(stream)>>>(c, P_<int32_t>(pos), C, P_<int32_t>(idx_map),
-                                                               P_<int32_t>(lens), P_<unsigned long long>(word), gen);
+                                                               P_<int32_t>(lens), P_<unsigned long long>(word), gen,
+                                                               na ? P_<int>(na) : nullptr, nb ? P_<int>(nb) : nullptr);
   MS_LAUNCH_CHECK();
 }
 
@@ -896,10 +906,27 @@ std::pair<int32_t*, int32_t*> select_tiles(long long tiles, hipStream_t s);
 void select_write_i32pos_capped(long long n, uintptr_t src, int32_t* tc, int32_t* tm, int sub, uintptr_t sel,
                                 uintptr_t out_dev, int cap, uintptr_t gflags, uintptr_t opflags, hipStream_t s);
 
-// per-stream candidate counters of rec_draw_kernel (zero between calls: rec_sort_kernel resets them)
-static std::unordered_map<hipStream_t, int*> g_rec_cnt;
+// per-stream append counters of the draw kernels (rec_draw_kernel, mutations.hip mut_draw_kernel):
+// zero between calls, rec_sort_kernel resets them (the calls of one stream run one after another)
+static std::unordered_map<hipStream_t, int*> g_sel_cnt;
+int* append_counter(hipStream_t s) {
+  int*& cnt = g_sel_cnt[s];
+  if (!cnt) {
+    MS_HIP_CHECK(hipMalloc((void**)&cnt, sizeof(int)));
+    MS_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int), s));
+  }
+  return cnt;
+}
+void sel_sort(uintptr_t cand, int* cnt, int cap, uintptr_t sel, uintptr_t out_dev, uintptr_t gflags, uintptr_t opflags,
+              hipStream_t s, uintptr_t gather) {
+  rec_sort_kernel<<<1, 1024, 0, s>>>(P_<int64_t>(cand), cnt, cap, P_<int64_t>(sel), P_<int32_t>(out_dev),
+                                     P_<int>(gflags), P_<int>(opflags), gather ? P_<int64_t>(gather) : nullptr);
+  MS_LAUNCH_CHECK();
+}
+int sel_sort_cap() { return kRecSortCap; }
 static int g_rec_thin = 1;  // 0: the count + selection passes for every capacity (A/B)
-void set_rec_thinning(int on) { g_rec_thin = on; }
+extern int g_mut_append;     // (mutations.hip: the same for the mutation draws)
+void set_rec_thinning(int on) { g_rec_thin = g_mut_append = on; }
 
 // The recombination draws of all slots (rec_slot_draw) + the capped selection of slots with k > 0
 // into sel / out_dev (gp_recombine): appended and sorted (rec_draw_kernel + rec_sort_kernel) with a
@@ -908,7 +935,7 @@ void set_rec_thinning(int on) { g_rec_thin = on; }
 void rec_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t idx_map, uintptr_t lens,
                uintptr_t lw_word, double p, uint64_t seed, uint64_t call, int kcap, uintptr_t gflags,
                uintptr_t opflags, uintptr_t keys, uintptr_t k, uintptr_t sel, uintptr_t out_dev, int cap,
-               uintptr_t cand, uintptr_t stream) {
+               uintptr_t cand, uintptr_t stream, uintptr_t na, uintptr_t nb) {
   if (n <= 0) throw std::invalid_argument("rec_slots: no cells");
   const Geom g = geom(R, C, r_lo, r_hi, wrap);
   hipStream_t s = S_(stream);
@@ -916,20 +943,16 @@ void rec_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap,
   if (!lw_word) throw std::invalid_argument("rec_slots: the longest-genome word of index_map_lmax is required");
   const auto* lw = P_<unsigned long long>(lw_word);
   if (g_rec_thin && cand && cap <= kRecSortCap) {
-    int*& cnt = g_rec_cnt[s];
-    if (!cnt) {
-      MS_HIP_CHECK(hipMalloc((void**)&cnt, sizeof(int)));
-      MS_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int), s));
-    }
+    int* cnt = append_counter(s);
     rec_draw_kernel<<<(unsigned)cdiv(total, 256), 256, 0, s>>>(
         n, P_<int32_t>(pos), g, P_<int32_t>(idx_map), P_<int32_t>(lens), lw, p, seed, call, kcap, P_<int>(gflags),
-        P_<int>(opflags), P_<int64_t>(keys), P_<int32_t>(k), P_<int64_t>(cand), cnt, cap);
+        P_<int>(opflags), P_<int64_t>(keys), P_<int32_t>(k), P_<int64_t>(cand), cnt, cap, na ? P_<int>(na) : nullptr,
+        nb ? P_<int>(nb) : nullptr);
     MS_LAUNCH_CHECK();
-    rec_sort_kernel<<<1, 1024, 0, s>>>(P_<int64_t>(cand), cnt, cap, P_<int64_t>(sel), P_<int32_t>(out_dev),
-                                       P_<int>(gflags), P_<int>(opflags));
-    MS_LAUNCH_CHECK();
+    sel_sort(cand, cnt, cap, sel, out_dev, gflags, opflags, s, 0);
     return;
   }
+  if (na) throw std::invalid_argument("rec_slots: a device cell count needs the append path (cap <= the sort's)");
   constexpr int kSelTile = 4096;  // select.hip
   const long long blocks = (total + kSelTile - 1) / kSelTile * (kSelTile / kSlotBlock);
   auto tiles = select_tiles(blocks, s);

@@ -562,12 +562,23 @@ class Kinetics:
         self._sync()
         return self._alloc_rows_now(k)
 
-    def _reserve_rows(self, k: int) -> None:
+    def _reserve_rows(self, k: int, sync: bool = True) -> None:
         """Make room for k fresh rows without taking them (the device genome pipeline takes them
-        with its own device-side row counter, magicsoup_amd.ops.genome_pipeline)."""
-        self._sync()
+        with its own device-side row counter, magicsoup_amd.ops.genome_pipeline). ``sync=False``: the
+        owner's pending state is not resolved first (a chain issued on a device count; the caller
+        checked :meth:`_rows_available`)."""
+        if sync:
+            self._sync()
         self._alloc_rows_now(k, want=False)
         self.__dict__["_nrows"] -= k
+
+    def _rows_available(self, k: int) -> bool:
+        """Whether k fresh rows exist without a recycling or a growth (slot mode)."""
+        d = self.__dict__
+        if d.get("_slot") is None:
+            return False
+        limit, _ = self._row_limit()
+        return d["_nrows"] + k <= limit
 
     def _row_limit(self) -> tuple[int, torch.Tensor | None]:
         """(bound of the fresh-row counter ``_nrows``, free-row list or None). Fresh row j is

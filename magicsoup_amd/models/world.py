@@ -57,6 +57,9 @@ _COUNT_SAFE_OPS = frozenset({"mutate_cells", "recombinate_cells", "degrade_molec
 # harmless for stale ones)
 _CHECK_ENV = os.environ.get("MS_CHECK_INVARIANTS") == "1"
 _DEFER_ENV = os.environ.get("MS_DEFER_GENOME_OPS", "1")
+# issue a queued recombinate + mutate pair on a pending kill_divide's device count (World._chain_bound;
+# MS_CHAIN_BOUND=0: wait for the count on the host first)
+_CHAIN_BOUND = os.environ.get("MS_CHAIN_BOUND", "1") != "0"
 # The genome chains flushed onto the side stream (World._flush_deferred) are joined into the compute
 # stream at the next op that needs their results (the activity, or a read of genomes / parameters),
 # not right after the flush: the molecule-only work in between (the lifetimes, the loop's masks)
@@ -323,13 +326,46 @@ class World:
             d["_defer_event"] = NEvent().record()
         q.append(fn)
 
-    def _evolve(self, rec: "_Deferred", mut: "_Deferred") -> int:
+    def _evolve(self, rec: "_Deferred", mut: "_Deferred", bound=None) -> int:
         """Issue a queued recombinate_cells() + mutate_cells() pair as one device chain. Returns how
         many of the two calls were issued, in order (2: merged; 1: the recombination only, e.g. a
-        decomposed world whose collective part has run; 0: neither -- the caller issues them)."""
+        decomposed world whose collective part has run; 0: neither -- the caller issues them).
+        ``bound``: issue on the device count of a pending kill_divide (see :meth:`_chain_bound`)."""
         from magicsoup_amd.ops import genome_pipeline
 
+        if bound is not None:
+            return 2 if self._n_floor() >= 1 and genome_pipeline.evolve(self, rec.args[0], *mut.args, bound=bound) else 0
         return 2 if self.n_cells >= 2 and genome_pipeline.evolve(self, rec.args[0], *mut.args) else 0
+
+    def _chain_bound(self, q: list):
+        """(upper bound, device count words) for issuing the queued recombinate_cells() +
+        mutate_cells() pair before a pending kill_divide's counts reach the host, or None.
+
+        The flush used to wait for those counts (the chains are sized by the population) and issue the
+        chain only then: ~0.27 ms of host wait, after which the chain's Python and launches put its
+        first kernel ~60 us behind the division's last (profiles/r5/call_order.txt). Instead the chain
+        is issued on the bound 2 n0 (a kill_divide at most doubles the population) with its kernels
+        reading the count from the division's device counters (survivors + placed children), and it
+        starts on the device the moment the division ends. Only a single-process GPU world, with
+        nothing else pending and nothing of the host state the chain's issue needs depending on the
+        count (no pipeline call to reconcile, no speculative activity, the parameter storage compact
+        with rows to spare, the genome pool with room: genome_pipeline.evolve checks the last two)."""
+        d = self.__dict__
+        pend = d["_count_pending"]
+        if not _CHAIN_BOUND or len(pend) < 4 or not isinstance(pend[1], tuple) or len(q) != 2:
+            return None
+        if getattr(q[0], "kind", None) != "rec" or getattr(q[1], "kind", None) != "mut":
+            return None
+        if "_n_pix_global" in d or d.get("_spec") is not None or not self._genomes.data.is_cuda:
+            return None
+        st = d.get("_gp_state")
+        if st and st["pending"]:
+            return None
+        kd = self.kinetics.__dict__
+        if kd.get("_slot") is None or not kd.get("_compact"):
+            return None
+        dc = pend[3]
+        return (2 * int(pend[0]), dc.data_ptr(), dc.data_ptr() + 8)
 
     def _join_side(self) -> None:
         """The compute stream waits (device-side) for the genome chains issued so far."""
@@ -375,8 +411,11 @@ class World:
         q = d.get("_deferred")
         if not q:
             return
+        bound = None
         if d.get("_count_pending") is not None:
-            self._resolve_count()  # (the chains are sized by the cell count)
+            bound = self._chain_bound(q)
+            if bound is None:
+                self._resolve_count()  # (the chains are sized by the cell count)
         d["_deferred"] = []
         side = d.get("_side_stream")
         if side is None:
@@ -399,10 +438,18 @@ class World:
                     # recombinate_cells() then mutate_cells(): one chain with one rebuild (gp_evolve)
                     if (i + 1 < len(q) and getattr(q[i], "kind", None) == "rec"
                             and getattr(q[i + 1], "kind", None) == "mut"):
-                        done = self._evolve(q[i], q[i + 1])
+                        done = self._evolve(q[i], q[i + 1], bound) if bound is not None else 0
+                        if not done:
+                            if bound is not None:
+                                bound = None
+                                self._resolve_count()
+                            done = self._evolve(q[i], q[i + 1])
                         if done:
                             i += done
                             continue
+                    if bound is not None:
+                        bound = None
+                        self._resolve_count()
                     q[i]()
                     i += 1
         finally:
@@ -538,7 +585,7 @@ class World:
         from magicsoup_amd.ops import hip_ops
 
         d = self.__dict__
-        n0, slot, ev = d["_count_pending"]
+        n0, slot, ev = d["_count_pending"][:3]
         # (only the division's work: not what was queued since, e.g. a diffusion stencil; with
         # communicators alive a peer failure raises instead of hanging)
         hip_ops.guarded_sync(ev)
@@ -1054,7 +1101,9 @@ class World:
         slots = hip_ops._m().fast_kill_divide(fw, n, kill_mask.view(torch.uint8).contiguous().data_ptr(),
                                               divide_mask.view(torch.uint8).contiguous().data_ptr(), mm.data_ptr(),
                                               hip_ops._mdt(mm), hip_ops._p(corr), seed, call, hip_ops._stream())
-        self.__dict__["_count_pending"] = (n, tuple(slots), NEvent().record())
+        # (+ the device counters {survivors, max, winners, max}: a genome chain may be issued on them
+        # before the counts reach the host, see _chain_bound)
+        self.__dict__["_count_pending"] = (n, tuple(slots), NEvent().record(), self.__dict__["_fw_bufs"]["dcount"])
 
     @_op("kill_divide")
     def kill_divide_where(self, molecule, kill_below: float, divide_above: float, divide_cost: float = 0.0,
@@ -1123,7 +1172,7 @@ class World:
             seed ^ 0x6A09E667F3BCC909, call,
             kill.data_ptr(), bufs["dvmask"].data_ptr(), mm.data_ptr(), hip_ops._mdt(mm), hip_ops._p(corr), seed, call,
             hip_ops._stream())
-        self.__dict__["_count_pending"] = (n, tuple(slots), NEvent().record())
+        self.__dict__["_count_pending"] = (n, tuple(slots), NEvent().record(), bufs["dcount"])
 
     @_op("kill_cells")
     def kill_cells(self, cell_idxs=None):

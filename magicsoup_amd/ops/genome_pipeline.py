@@ -370,7 +370,8 @@ class _PartHost:
         return {0: self.parts[2], 1: self.parts[3], 2: 0, 3: self.parts[2]}[i]
 
 
-def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=None, arrivals=None) -> bool:
+def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=None, arrivals=None,
+           bound=None) -> bool:
     """``recombinate_cells(p=p_rec)`` followed by ``mutate_cells(p, p_indel, p_del)`` over all cells
     as ONE device chain (gp.hip gp_evolve): both are applied and committed in order, then the union
     of the changed cells is translated and built once -- the same genomes and parameters as the two
@@ -378,9 +379,12 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
     decomposed world's strip-boundary recombination (as for :func:`recombinate_all`). ``arrivals``:
     ``(first, count)``, cells whose parameters are built with the union (instead of by a
     :func:`rebuild_rows` chain of their own; at most ``N_CAP``). False if either call should take its
-    own path (rates above the pipeline's usage rule, too few cells)."""
+    own path (rates above the pipeline's usage rule, too few cells). ``bound``: (cell bound, device
+    count words) -- issued while a kill_divide's counts are still on the device (World._chain_bound):
+    sized for the bound, the kernels read the count; False (nothing issued) where the host state the
+    issue touches would depend on the count."""
     arena = world._genomes
-    n = world.n_cells
+    n = int(bound[0]) if bound is not None else world.n_cells
     if n < 2:
         return False
     L = int(arena.width)
@@ -393,20 +397,39 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
         return False  # (the caller issues the recombination on its own: see _pair_cap)
     st = _state(world)
     if any(pd.kind in ("rec", "mut", "evo") for pd in st["pending"]):
+        if bound is not None:
+            return False
         reconcile(world)
     dev = arena.data.device
     mcap = _cap(n * p * L, min(n, N_CAP))
     kin = world.kinetics
     arr0, narr = (0, 0) if arrivals is None else (int(arrivals[0]), int(arrivals[1]))
     fresh = not st["pending"]
-    if fresh:
-        kin._reserve_rows(2 * min(n, N_CAP) + narr)
     xr = 0 if extra is None else int(extra.rows)
-    _room(world, (2 * pcap + xr) * _r16(2 * L) + mcap * _r16(L + K_CAP))
+    room = (2 * pcap + xr) * _r16(2 * L) + mcap * _r16(L + K_CAP)
+    if bound is not None:
+        # nothing here may wait for the count: the selections must fit the append + sort paths (the
+        # count + selection passes size their grids by the count), the fresh rows must exist without
+        # a recycling (it scans the live cells' row map) and the pool must have room without a
+        # collection (it moves the live cells' genomes)
+        sc_cap = int(_m().sel_sort_cap())
+        if extra is not None or narr or max(pcap, mcap, 2 * pcap) > sc_cap:
+            return False
+        if fresh and not kin._rows_available(2 * min(n, N_CAP)):
+            return False
+        if arena.top_ub + room > arena.pool_cap:
+            return False
+    if fresh:
+        kin._reserve_rows(2 * min(n, N_CAP) + narr, sync=bound is None)
+    _room(world, room)
     br, bm, bu = _bufs(world, "rec"), _bufs(world, "mut"), _bufs(world, "evo")
     ar, am, au = _arena_desc(world, br), _arena_desc(world, bm), _arena_desc(world, bu)
+    nd = (0, 0)
+    if bound is not None:
+        ar.n = am.n = au.n = n  # (grids and scratch for the bound; the kernels read the count)
+        nd = (int(bound[1]), int(bound[2]))
     sc = hip_ops._scratch(world)
-    keys, nbr = hip_ops.neighbor_slot_args(world)
+    keys, nbr = hip_ops.neighbor_slot_args(world, bound)
     k = _kin_desc(world, dev)
     blob_r = _blob(world, "rec", _m().gp_blob_bytes(1, n, pcap, k.P, L, D_CAP, K_CAP, xr), dev)
     blob_m = _blob(world, "mut", _m().gp_blob_bytes(0, n, mcap, k.P, L, D_CAP, K_CAP, 0), dev)
@@ -414,15 +437,16 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
     ucap = 2 * pcap + xr + mcap + narr
     blob_u = _blob(world, "evo", _m().gp_evolve_union_bytes(ucap, k.P, D_CAP, L), dev)
     mark = sc.bufs.get("arena_mark")
-    if mark is None or mark.numel() < arena.n:
-        mark = sc.bufs["arena_mark"] = torch.zeros(max(arena.n, 1024) * 2, dtype=torch.int64, device=dev)
+    na = max(arena.n, n)
+    if mark is None or mark.numel() < na:
+        mark = sc.bufs["arena_mark"] = torch.zeros(max(na, 1024) * 2, dtype=torch.int64, device=dev)
         sc.bufs["arena_gen"] = 0
     gen = sc.bufs["arena_gen"] = sc.bufs.get("arena_gen", 0) + 1
     rng_r, rng_m = _rng(), _rng()
     slot_u, slot_p = _m().gp_evolve(ar, am, au, _gen_desc(world, dev), k, _p(keys), nbr, float(p_rec), rng_r[0],
                                     rng_r[1], pcap, float(p), float(p_indel), float(p_del), rng_m[0], rng_m[1], mcap,
                                     K_CAP, D_CAP, _p(mark), int(gen), _p(blob_r), _p(blob_m), _p(blob_u), fresh,
-                                    int(kin.__dict__["_nrows"]), extra, _p(nres), arr0, narr, _stream())
+                                    int(kin.__dict__["_nrows"]), extra, _p(nres), arr0, narr, nd[0], nd[1], _stream())
     lay_r = _m().gp_layout(1, n, pcap, L, K_CAP, xr)
     lay_m = _m().gp_layout(0, n, mcap, L, K_CAP, 0)
     parts = _StatusSlot(slot_p)

@@ -1054,28 +1054,36 @@ def _lmax_word(world) -> torch.Tensor:
     return w
 
 
-def _index_map_lmax(world, n, pos, C, idx_map) -> None:
+def _index_map_lmax(world, n, pos, C, idx_map, nd=(0, 0)) -> None:
     """The index map of the current positions + the longest genome into _lmax_word (the bound of
-    the recombination draws' thinning, world.hip rec_slot_draw)."""
+    the recombination draws' thinning, world.hip rec_slot_draw). ``nd``: device count words (their
+    sum is the cell count, ``n`` its bound; 0: ``n`` is the count)."""
     sc = _scratch(world)
     gen = sc.bufs["lmax_gen"] = sc.bufs.get("lmax_gen", 0) % ((1 << 31) - 1) + 1
     if gen == 1:  # (the generation wrapped or starts: a fresh word)
         _lmax_word(world).zero_()
-    _m().index_map_lmax(n, _p(pos), C, _p(idx_map), _p(world._genomes.lens), _p(_lmax_word(world)), gen, _stream())
+    _m().index_map_lmax(n, _p(pos), C, _p(idx_map), _p(world._genomes.lens), _p(_lmax_word(world)), gen, nd[0], nd[1],
+                        _stream())
 
 
-def neighbor_slot_args(world):
+def neighbor_slot_args(world, bound=None):
     """The index map of the current positions plus the buffers / arguments of the fused neighbour
     slot pass of the device pipeline (gp.hip gp_recombine -> world.hip rec_slots): the slot keys
     buffer (8n int64, written there) and (positions, R, C, r_lo, r_hi, wrap, index map, the
-    longest-genome word of the thinned draws)."""
+    longest-genome word of the thinned draws). ``bound``: (cell bound, device count words) of a
+    kill_divide whose count is still on the device (the positions' capacity buffer, no host count)."""
     R, C, r_lo, r_hi, wrap = geom(world)
     dev = world._genomes.data.device
-    n = world.n_cells
-    _ensure_world_layout(world)
-    pos = world.cell_positions
     idx_map = _index_map(world, R * C, dev)
-    _index_map_lmax(world, n, pos, C, idx_map)
+    if bound is not None:
+        n = int(bound[0])
+        pos = world._cols["cell_positions"].buf  # (int32 (capacity, 2): the layout the kernels need)
+        _index_map_lmax(world, n, pos, C, idx_map, (int(bound[1]), int(bound[2])))
+    else:
+        n = world.n_cells
+        _ensure_world_layout(world)
+        pos = world.cell_positions
+        _index_map_lmax(world, n, pos, C, idx_map)
     keys = _scratch(world).get("nb_keys", 8 * n, torch.int64, dev)
     return keys, (_p(pos), R, C, r_lo, r_hi, wrap, _p(idx_map), _p(_lmax_word(world)))
 

@@ -89,6 +89,9 @@ def hip():
     if fresh and os.environ.get("MS_STENCIL_BLOCKS"):
         # blocks of the diffusion stencil launch (maps.hip; 0: one per tile)
         mod.set_stencil_blocks(int(os.environ["MS_STENCIL_BLOCKS"]))  # type: ignore[attr-defined]
+    if fresh and os.environ.get("MS_EVENT_SPIN"):
+        # 0: host event waits block at once (events.hip ev_sync)
+        mod.set_event_spin(int(os.environ["MS_EVENT_SPIN"]))  # type: ignore[attr-defined]
     if fresh and os.environ.get("MS_REC_THIN"):
         # 0: the per-slot recombination draws + selection pass (world.hip rec_slots) for A/B
         mod.set_rec_thinning(int(os.environ["MS_REC_THIN"]))  # type: ignore[attr-defined]

@@ -31,6 +31,9 @@ for s in "$@"; do case "$s" in
   kt) run tests_kin 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -x -k "integrat or enzymatic or activity or kinetic" --timeout 300 --timeout-method thread ;;
   dt) run tests_diff 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_distributed.py -m gpu -q -x -k "diffus or stencil or mass or halo or strip" --timeout 300 --timeout-method thread ;;
   gt) run tests_gen 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_mutation_stats.py tests/test_gpu_distributed.py -m gpu -q -x -k "pipeline or recomb or evolve or merged or mutat or genetic" --timeout 300 --timeout-method thread ;;
+  cbt) run tests_cb 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -x -k "chain_issued or pipeline or merged or recomb or kill_divide or lazy" --timeout 300 --timeout-method thread ;;
+  spin) for i in 1 2; do for t in 1 0; do MS_EVENT_SPIN=$t run spin_${t}_$i 300 python bench.py; done; done ;;
+  cbab) for i in 1 2; do for t in 1 0; do MS_CHAIN_BOUND=$t run cbab_${t}_$i 300 python bench.py; done; done ;;
   rthin) for i in 1 2; do for t in 1 0; do MS_REC_THIN=$t run rthin_${t}_$i 300 python bench.py; done; done ;;
   tmem) run tests_mem 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -k "memory_model or past_2_31" --timeout 300 --timeout-method thread ;;
   tests) run tests 1000 python -u -m pytest tests -m gpu -q --maxfail 5 --timeout 120 --timeout-method thread ;;

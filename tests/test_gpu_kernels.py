@@ -1381,3 +1381,58 @@ def test_kill_divide_where_matches_masks_on_gpu():
     w1.kill_divide_where(atp, -1.0, 1e9, kill_fraction=0.3)
     assert 0.6 * n < w1.n_cells < 0.8 * n
     w1.check_invariants()
+
+
+@pytest.mark.gpu
+def test_chain_issued_on_device_count_matches_resolved_count(monkeypatch):
+    """A recombinate + mutate pair queued behind a kill_divide is issued before the division's count
+    reaches the host (World._chain_bound: sized for 2 n0, the kernels read the device count): the
+    same genomes, parameters, molecules and population as issuing it after the count was read."""
+    import copy
+
+    from magicsoup_amd.models import world as world_mod
+
+    base = _world("cuda", map_size=96, n=1500, seed=13)
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    used = []
+    orig = world_mod.World._chain_bound
+
+    def spy(self, q):
+        b = orig(self, q)
+        used.append(b is not None)
+        return b
+
+    monkeypatch.setattr(world_mod.World, "_chain_bound", spy)
+
+    def run(on: bool):
+        monkeypatch.setattr(world_mod, "_CHAIN_BOUND", on)
+        w = copy.deepcopy(base)
+        ms.set_seed(5)
+        torch.manual_seed(5)
+        for _ in range(6):
+            w.enzymatic_activity()
+            w.kill_divide_where(atp, kill_below=0.5, divide_above=2.0, divide_cost=1.0)
+            w.recombinate_cells(p=2e-5)
+            w.mutate_cells(p=2e-4)
+            w.degrade_molecules()
+            w.diffuse_molecules()
+            w.increment_cell_lifetimes()
+        w.enzymatic_activity()
+        w.synchronize()
+        names = ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke")
+        params = {k: getattr(w.kinetics, k).clone() for k in names}
+        from magicsoup_amd.ops import world_ops
+
+        params["_nprot"] = world_ops.translate(w, torch.arange(w.n_cells, device=w.device))[1]
+        return w.n_cells, list(w.cell_genomes), params, w.cell_molecules.clone(), w.molecule_map.clone()
+
+    a = run(True)
+    assert any(used), "the chain was never issued on the device count"
+    used.clear()
+    b = run(False)
+    assert not any(used)
+    assert a[0] == b[0]
+    assert a[1] == b[1]
+    _assert_params_equal(_real(a[2]), _real(b[2]), a[2]["_nprot"])
+    assert torch.equal(a[3], b[3])
+    assert torch.equal(a[4], b[4])
