@@ -666,11 +666,14 @@ static int stencil_pf(int dtype) { return g_stencil_pf >= 0 ? g_stencil_pf : (dt
   if (full) { constexpr bool FULL = true; MS_PF_DISPATCH1(pf, LAUNCH) }             \
   else { constexpr bool FULL = false; MS_PF_DISPATCH1(pf, LAUNCH) }
 
-// Blocks of the vector stencil launch (0: one per tile). 256 CUs x 3 workgroups (3 waves per SIMD)
-// with 2-3 rows in flight per wave reach the stencil's full HBM rate and leave most workgroup slots
-// of every CU to the side stream. Round 4 (one row in flight): stencil 378 / side chain done 100 us
-// after it at 1024 blocks; 385 / 125-166 at one block per tile; 427 / 75 at 896; 500 at 512.
-static int g_stencil_blocks = 256 * 3;
+// Blocks of the vector stencil launch (0: one per tile). 256 CUs x 2 workgroups (2 waves per SIMD)
+// with 2-3 rows in flight per wave keep the stencil within 1 % of its full-grid time alone (diffuse
+// step 0.361 vs 0.357 ms at 768 blocks) and leave the most room to the genome chain it runs next to
+// on the side stream, whose latency-bound kernels are the step's other critical path: flagship 300
+// timed steps 1178 / 1178 steps/s at 512 blocks, 1100-1122 at 768, 1166-1168 with round 4's one row
+// in flight at 1024 (profiles/r5/stencil_blocks_flagship.txt). Round 4 (one row in flight): stencil
+// 378 / side chain done 100 us after it at 1024 blocks; 427 / 75 at 896; 500 at 512.
+static int g_stencil_blocks = 256 * 2;
 void set_stencil_blocks(int n) { g_stencil_blocks = std::max(0, n); }
 
 size_t diffuse_partials_len(int m, int C, int H) {

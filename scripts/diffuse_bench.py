@@ -35,7 +35,7 @@ def main():
                     native.hip().set_stencil_band(band)
                     run(a, f"vec{vec}_blocks{blocks}" + (f"_pf{pf}" if pf >= 0 else "") + f"_band{band}")
     native.hip().set_stencil_vec(0)
-    native.hip().set_stencil_blocks(768)
+    native.hip().set_stencil_blocks(512)
     native.hip().set_stencil_prefetch(-1)
     native.hip().set_stencil_band(0)
 

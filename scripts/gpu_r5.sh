@@ -56,7 +56,7 @@ for s in "$@"; do case "$s" in
   upd) PROBE_PROFILE=1 run update_cells_probe 300 python scripts/update_cells_probe.py ;;
   isweep) run integrator_sweep 300 python scripts/integrator_sweep.py ;;
   sab2) for i in 1 2; do for cfg in ${SAB2:-0,32,1024 2,64,768 2,64,512 3,64,512 1,64,768 2,64,1024 1,32,1024}; do IFS=, read pf bd bl <<< "$cfg"
-         MS_STENCIL_PF=$pf MS_STENCIL_BAND=$bd MS_STENCIL_BLOCKS=$bl run sab2_${pf}_${bd}_${bl}_$i 300 python bench.py; done; done ;;
+         MS_STENCIL_PF=$pf MS_STENCIL_BAND=$bd MS_STENCIL_BLOCKS=$bl run sab2_${pf}_${bd}_${bl}_$i 300 python bench.py ${SAB2_ARGS:-}; done; done ;;
   dlab) for sk in 0 8192; do MS_MAP_SKEW=$sk run dlab_skew$sk 300 python scripts/diffuse_bench.py --dtypes fp32 --pf 0 1 2 3 --band 0 64 --blocks 768 1024; done ;;
   dlab2) run dlab2 300 python scripts/diffuse_bench.py --dtypes fp32 bf16 fp16 --pf 0 2 3 --band 0 64 --blocks 512 768 0 ;;
   dbench) run diffuse_bench 300 python scripts/diffuse_bench.py --dtypes fp32 --blocks 1024 2048 0 --band 0 64 ;;
