@@ -81,6 +81,10 @@ __device__ __forceinline__ long long poisson(Philox& rng, double lam) {
   if (!(lam > 0.0)) return 0;
   if (lam < 30.0) {
     const double u = rng.uniform_d();
+    // k = 0 iff u <= exp(-lam) >= 1 - lam: below 1 - lam (less a few ulps for the rounding of both
+    // sides) the answer is 0 without the exp -- the same draw, for all but ~lam of the calls (the
+    // genome pipeline draws per neighbour slot at lam ~ 1e-4)
+    if (u <= (1.0 - lam) - 1e-15) return 0;
     double p = exp(-lam), cum = p;
     long long k = 0;
     while (u > cum && k < 1000) {
