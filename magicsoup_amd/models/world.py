@@ -262,7 +262,12 @@ class World:
         m = self.n_molecules
         self.n_cells = 0
         # GPU genomes: a ragged pool (per-cell offsets, shared by parents and children); CPU worlds
-        # keep rows, which the OpenMP host core works on
+        # keep fixed-width rows on purpose: the OpenMP host core (csrc/host: translation, mutations,
+        # recombination) runs one thread per genome over contiguous row-major bytes, a division
+        # copies rows with memcpy, and the pool's reasons -- no device-side widening when one genome
+        # grows, parents and children sharing bytes without a copy kernel, a device bump allocator --
+        # do not apply to host memory, where a row widening is one realloc of a few MB. Both stores
+        # expose the same StringColumn / rows_of interface, so every op is storage-agnostic.
         self._genomes = PoolArena(dev) if dev.type == "cuda" else StringArena(dev, width=64)
         self._labels = StringArena(dev, width=16)
         self._genome_col = StringColumn(self._genomes)

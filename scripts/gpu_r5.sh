@@ -65,6 +65,12 @@ for s in "$@"; do case "$s" in
        run ab_flagship_grown 300 python scripts/ab_so.py --steps 150 ${ABSO:-abso/head.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so} ;;
   itc) for it in 0 1 2 4; do run itc_$it 300 python scripts/ab_so.py --iters $it magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so; done ;;
   abw) run ab_wide 300 python scripts/ab_so.py --chem synthetic:64:256 ${ABSO:-abso/head.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so} ;;
+  pmcst) # HBM bytes of the stencil (FETCH_SIZE: 3 TCC counters, WRITE_SIZE: 2 -> two passes)
+     for c in FETCH_SIZE WRITE_SIZE; do
+       (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex "diffuse_stencil" -d "$OLDPWD/$O/pmc_stencil_$c" -o run --output-format csv \
+          -- python3 "$OLDPWD/scripts/diffuse_bench.py" --dtypes fp32 --iters 5 > "$OLDPWD/$O/pmc_stencil_$c.log" 2>&1)
+       rc=$?; echo "   pmc $c rc=$rc"; if fatal $rc; then exit $rc; fi
+     done ;;
   pmcw|pmcf) # PMC of the integrator / stencil kernels (one pass, 8 SQ counters, kernel filter, no trace domains)
      preset=$([ "$s" = pmcw ] && echo wide || echo flagship)
      echo "== pmc $preset"
