@@ -744,6 +744,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   for (int q = 0; q < NZ / 2; ++q) e16[q] = 0;
   bool small = true;  // all exponents < 8: branch-free powers
   bool both = false;  // an entry with forward and backward exponents (a signal consumed and produced)
+  bool allo = false;  // an allosteric entry (a != 0)
   int nfs_p = 0, nbs_p = 0;  // any forward / backward exponent of this protein
   if (prot) {
     pk = act[lane];
@@ -763,6 +764,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
         e16[q >> 1] |= e << (16 * (q & 1));
         small &= w_nf(w) < 8 && w_nb(w) < 8 && w_a(w) < 8 && w_a(w) > -8;
         both |= w_nf(w) > 0 && w_nb(w) > 0;
+        allo |= w_a(w) != 0;
         nfs_p |= w_nf(w);
         nbs_p |= w_nb(w);
       }
@@ -771,6 +773,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   const int cnt_w = __builtin_amdgcn_readfirstlane(wave_max(cnt));
   const bool small_w = __ballot(!small) == 0ull;
   const bool one_w = __ballot(both) == 0ull;  // every entry has one exponent: one power per entry
+  const bool allo_w = __ballot(allo) != 0ull;  // any allosteric entry in the wave (else no word reads)
 #define MS_E(q) ((e16[(q) >> 1] >> (16 * ((q) & 1))) & 0xFFFF)
   auto pw = [&](float x, int n) { return small_w ? ipow_small(x, n) : ms::ipow(x, n); };
 
@@ -858,32 +861,39 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   {
     const float* kmr = a.Kmr + (prow * P + pk) * s;
     float xf = 1.0f, xb = 1.0f, ar = 1.0f;
-    int nfs = 0, nbs = 0;
+#pragma unroll
+    for (int q = 0; q < NZ; ++q) asm volatile("" : "+v"(e16[q >> 1]));  // (no hoisting, see signal_pass)
 #pragma unroll
     for (int q = 0; q < NZ; ++q) {
       if (q < cnt_w) {
-        const int w = q < cnt ? ents[lane * ES + q] : 0;
-        const int j = EP::j(MS_E(q));
-        const int nf = w_nf(w), nb = w_nb(w), av = w_a(w);
+        const int e = MS_E(q);
+        const int j = EP::j(e), nf = EP::nf(e), nb = EP::nb(e);
         const float x = Xs[j];
-        nfs |= nf;
-        nbs |= nb;
-        xf = nf > 0 ? xf * pw(x, nf) : xf;
-        xb = nb > 0 ? xb * pw(x, nb) : xb;
-        if (av != 0) {
-          float r = pw(x, av);
-          r = r / (r + kmr[j]);
-          if (ms::f_isnan(r)) r = 1.0f;
-          ar *= r;
+        if (one_w) {  // (as in the damping loop: the entry's one power)
+          const float p = pw(x, nf | nb);
+          xf = nf > 0 ? xf * p : xf;
+          xb = nb > 0 ? xb * p : xb;
+        } else {
+          xf = nf > 0 ? xf * pw(x, nf) : xf;
+          xb = nb > 0 ? xb * pw(x, nb) : xb;
+        }
+        if (allo_w) {  // (the allosteric exponent is in the full word only)
+          const int av = w_a(q < cnt ? ents[lane * ES + q] : 0);
+          if (av != 0) {
+            float r = pw(x, av);
+            r = r / (r + kmr[j]);
+            if (ms::f_isnan(r)) r = 1.0f;
+            ar *= r;
+          }
         }
       }
     }
     if (prot) {
       float kf = ms::clean_prod(xf) / kmf;
-      if (nfs == 0) kf = 0.0f;
+      if (nfs_p == 0) kf = 0.0f;
       if (ms::f_isinf(kf)) kf = ms::kMax;
       float kb = ms::clean_prod(xb) / kmb;
-      if (nbs == 0) kb = 0.0f;
+      if (nbs_p == 0) kb = 0.0f;
       if (ms::f_isinf(kb)) kb = ms::kMax;
       if (ms::f_isinf(ar)) ar = ms::kMax;
       const float acat = (kf - kb) / (1.0f + kf + kb);
