@@ -19,10 +19,15 @@
 
 namespace msd {
 
+void threshold_spill(int n, int m, int mol, float kill_below, float divide_above, float cost, float kill_p, uint64_t seed,
+                     uint64_t call, uintptr_t mols, uintptr_t kill, uintptr_t divide, uintptr_t pos, int R, int C,
+                     uintptr_t map, uintptr_t cell_map, int dtype, uintptr_t corr, uintptr_t stream);
 void spill_free_mask(int n, int m, uintptr_t dead, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
                      uintptr_t cell_map, int dtype, uintptr_t corr, uintptr_t stream);
 int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
                          uintptr_t stream);
+int select_indices_async_pay(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
+                             uintptr_t pay_src, uintptr_t pay_dst, uintptr_t stream);
 int divide_mask_dev(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, uintptr_t cell_map,
                     uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result, int rounds, uint64_t seed,
                     uint64_t call, uintptr_t wins, uintptr_t dcount, long long n0, int m, uintptr_t par,
@@ -161,24 +166,30 @@ __global__ void __launch_bounds__(256) threshold_masks_kernel(int n, int m, int 
 // over it with the children appended after the device survivor count (rows dn..). Both masks are
 // uint8 over the same n cells. Returns the status slots of the survivor count and of the winner
 // count; the population is their sum.
-std::pair<int, int> fast_kill_divide(const FastWorld& f, int n, uintptr_t kill, uintptr_t divide, uintptr_t map,
-                                     int mdt, uintptr_t corr, uint64_t seed, uint64_t call, uintptr_t stream) {
+static std::pair<int, int> kill_divide_impl(const FastWorld& f, int n, uintptr_t kill, uintptr_t divide, uintptr_t map,
+                                            int mdt, uintptr_t corr, uint64_t seed, uint64_t call, uintptr_t stream,
+                                            bool spilled) {
   if (!f.ready) throw std::invalid_argument("fast_kill_divide: descriptor not finalized");
   if (n <= 0 || 2ll * n > f.cap) throw std::invalid_argument("fast_kill_divide: 2 x cell count exceeds the capacity");
   if (!f.dmask) throw std::invalid_argument("fast_kill_divide: no mask scratch");
   hipStream_t s = S_(stream);
-  spill_free_mask(n, f.m, kill, f.pos, f.R, f.C, f.mols, map, f.cell_map, mdt, corr, stream);
-  const int slot_k = select_indices_async(n, 1 /* clear */, kill, f.sel, 0, f.dcount, stream);
+  if (!spilled) spill_free_mask(n, f.m, kill, f.pos, f.R, f.C, f.mols, map, f.cell_map, mdt, corr, stream);
+  // the survivors, and with them the division mask compacted (dmask[k] = divide[sel[k]], zeros past
+  // the survivor count) in the same single-pass selection
+  const int slot_k = select_indices_async_pay(n, 1 /* clear */, kill, f.sel, 0, f.dcount, divide, f.dmask, stream);
   const int* dn = P_<int>(f.dcount);
   launch_row_args(f.fwd, n, dn, P_<int64_t>(f.sel), nullptr, 0, s);
   launch_row_args(f.back, n, dn, nullptr, nullptr, 0, s);
-  compact_mask_kernel<<<cdiv(n, 256), 256, 0, s>>>(n, dn, P_<int64_t>(f.sel), P_<uint8_t>(divide), P_<uint8_t>(f.dmask));
-  MS_LAUNCH_CHECK();
   const int slot_d = divide_mask_dev_at(n, f.dmask, f.pos, f.R, f.C, f.r_lo, f.r_hi, f.wrap, f.cell_map, f.pending,
                                         f.cand, f.claim, f.result, f.rounds, seed, call, f.wins, f.dcount2, 0, f.dcount,
                                         f.m, f.par, f.mols, f.div, f.life, stream);
   launch_row_args(f.clone, n, P_<int>(f.dcount2), P_<int64_t>(f.par), nullptr, 0, s, dn);
   return {slot_k, slot_d};
+}
+
+std::pair<int, int> fast_kill_divide(const FastWorld& f, int n, uintptr_t kill, uintptr_t divide, uintptr_t map,
+                                     int mdt, uintptr_t corr, uint64_t seed, uint64_t call, uintptr_t stream) {
+  return kill_divide_impl(f, n, kill, divide, map, mdt, corr, seed, call, stream, false);
 }
 
 // The threshold masks alone (a decomposed world's strips: their division is a collective protocol)
@@ -208,11 +219,11 @@ std::pair<int, int> fast_kill_divide_where(const FastWorld& f, int n, int mol, f
                                            uint64_t call, uintptr_t stream) {
   if (!f.ready) throw std::invalid_argument("fast_kill_divide_where: descriptor not finalized");
   if (n <= 0 || mol < 0 || mol >= f.m) throw std::invalid_argument("fast_kill_divide_where: bad cell count or molecule");
-  threshold_masks_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, f.m, mol, kill_below, divide_above, cost, kill_p,
-                                                                  mseed, mcall, P_<float>(f.mols), P_<uint8_t>(kill),
-                                                                  P_<uint8_t>(divide));
-  MS_LAUNCH_CHECK();
-  return fast_kill_divide(f, n, kill, divide, map, mdt, corr, seed, call, stream);
+  if (n > f.cap / 2) throw std::invalid_argument("fast_kill_divide: 2 x cell count exceeds the capacity");
+  // the masks and the killed cells' spill in one launch (maps.hip threshold_spill_kernel)
+  threshold_spill(n, f.m, mol, kill_below, divide_above, cost, kill_p, mseed, mcall, f.mols, kill, divide, f.pos, f.R,
+                  f.C, map, f.cell_map, mdt, corr, stream);
+  return kill_divide_impl(f, n, kill, divide, map, mdt, corr, seed, call, stream, true);
 }
 
 // ---- the strip protocol of a decomposed world's divide_cells over a mask (parallel/dist_world.py),

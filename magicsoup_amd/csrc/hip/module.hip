@@ -24,6 +24,7 @@ void place_rounds_mask(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r
                        uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result,
                        int rounds, uint64_t seed, uint64_t call, uintptr_t stream);
 void set_coop_blocks(int n);
+void set_place_tail(int on);
 void set_stencil_vec(int v);
 void set_stencil_prefetch(int pf);
 void set_stencil_band(int b);
@@ -170,6 +171,7 @@ void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t d
 int count_to_host(uintptr_t dcount, uintptr_t stream);
 int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
                          uintptr_t stream);
+void set_select_single_pass(int on, int items);
 void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
 int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t cnt, uintptr_t stream);
 std::tuple<long long, long long, long long, long long> status_read(int slot);
@@ -280,6 +282,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("spill_free_mask", &msd::spill_free_mask);
   m.def("place_rounds", &msd::place_rounds);
   m.def("place_rounds_mask", &msd::place_rounds_mask, "cooperative placement over cells selected by a mask");
+  m.def("set_place_tail", &msd::set_place_tail, "1: single-launch placement with one grid barrier + a one-workgroup tail of the later rounds");
   m.def("set_coop_blocks", &msd::set_coop_blocks, "workgroups of the cooperative placement (A/B)");
   m.def("set_stencil_vec", &msd::set_stencil_vec, "diffusion stencil columns per lane: 8 (default), 4 or 1");
   m.def("set_stencil_prefetch", &msd::set_stencil_prefetch, "rows the vector stencils load ahead (-1 auto, 0-3)");
@@ -299,6 +302,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("translate_write", &msd::translate_write);
   m.def("translate_fused", &msd::translate_fused);
   m.def("set_spl2_waves", &msd::set_spl2_waves, "waves per SIMD of the wide chemistries' narrow launch (2-4)");
+  m.def("set_select_single_pass", &msd::set_select_single_pass, py::arg("on"), py::arg("items") = 0,
+        "1: selections of <= 4M items in one launch (tile counts tagged + summed); 0: count + write passes; items: per thread of its tiles (1, 4, 16; 0 keeps)");
   m.def("set_rec_thinning", &msd::set_rec_thinning, "1: recombination (thinned) and mutation draws appended + sorted (0: count + selection passes)");
   m.def("set_rescue_mode", &msd::set_rescue_mode, "1: one launch behind the speculative integrator (0: separate)");
   m.def("rescue_error_take", &msd::rescue_error_take, "1 if the integrator rescue launch's grid barrier timed out");

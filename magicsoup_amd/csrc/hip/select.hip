@@ -19,12 +19,10 @@
 #include <vector>
 
 #include "hip_common.h"
+#include "select_lb.h"
 
 namespace msd {
 
-constexpr int kSelThreads = 256;
-constexpr int kSelItems = 16;
-constexpr int kSelTile = kSelThreads * kSelItems;  // 4096
 
 enum SelKind { kMaskSet = 0, kMaskClear = 1, kI32Pos = 2, kI64NonNeg = 3 };
 
@@ -148,6 +146,28 @@ __global__ void __launch_bounds__(kSelThreads) select_write_kernel(long long n, 
   }
 }
 
+// Single-pass form of the two kernels above (select_lb.h): one launch per selection. Optional
+// payload: pay_dst[k] = pay_src[i] for the k-th selected item i, and 0 for the rejected items from
+// the end (pay_dst[n - 1 - r] for the r-th rejected), so pay_dst[dn..n) is all zeros (the division
+// mask compacted with the survivors of kill_divide, fast.hip).
+template <int K, int ITEMS>
+__global__ void __launch_bounds__(kSelThreads) select_lb_kernel(long long n, const void* src, unsigned long long* status,
+                                                                uint32_t gen, int64_t* sel, int64_t* rest,
+                                                                int32_t* out, long long* host64, const uint8_t* pay_src,
+                                                                uint8_t* pay_dst) {
+  select_lb_tile<ITEMS>(
+      n, [&](long long i) { return sel_pred<K>(src, i); }, status, gen,
+      [&](long long k, long long i) {
+        sel[k] = i;
+        if (pay_dst) pay_dst[k] = pay_src[i];
+      },
+      [&](long long r, long long i) {
+        if (rest) rest[r] = i;
+        if (pay_dst) pay_dst[n - 1 - r] = 0;
+      },
+      out, host64);
+}
+
 // Per-genome protein totals (fwd + rev) and the maxima a translate count pass needs on the host.
 // Block maxima are combined with atomicMax in a device accumulator; the last block to finish
 // (done counter) publishes {max proteins, max domains, long genomes} to pinned host memory and
@@ -207,6 +227,14 @@ std::pair<int32_t*, int32_t*> tiles_for(hipStream_t s, long long tiles) {
   }
   return {b.p, b.p + b.cap};
 }
+// per stream: the tile status words of select_lb_tile and the generation of its last call
+struct LbBuf {
+  unsigned long long* p = nullptr;
+  uint32_t gen = 0;
+};
+std::unordered_map<hipStream_t, LbBuf> g_lb;
+int g_sel_single = 1;  // select_indices_async takes the single-pass kernel when the grid allows
+int g_sel_items = 4;   // items per thread of its tiles (1, 4 or 16) while the status words suffice
 int32_t* g_tacc = nullptr;  // device {max proteins, max domains, done blocks}, zero between calls
 
 void ensure_host() {
@@ -322,6 +350,19 @@ int count_to_host(uintptr_t dcount, uintptr_t stream) {
   return slot;
 }
 
+int status_slot_new(long long** dev) {
+  if (!g_status) {
+    MS_HIP_CHECK(hipHostMalloc((void**)&g_status, kStatusSlots * 4 * sizeof(long long),
+                               hipHostMallocMapped | hipHostMallocCoherent));
+    MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_status_dev, g_status, 0));
+  }
+  const int slot = g_status_next;
+  g_status_next = (g_status_next + 1) % kStatusSlots;
+  for (int i = 0; i < 4; ++i) g_status[slot * 4 + i] = -1;
+  *dev = g_status_dev + slot * 4;
+  return slot;
+}
+
 std::tuple<long long, long long, long long, long long> status_read(int slot) {
   if (!g_status || slot < 0 || slot >= kStatusSlots) throw std::invalid_argument("status_read: bad slot");
   const long long* v = g_status + slot * 4;
@@ -338,8 +379,32 @@ std::tuple<long long, long long, long long, long long> stream_sync_read(int slot
 // select_indices_dev whose last tile also writes {count, max} into a fresh pinned status slot
 // (returned): the host launches the work that depends on the count with `out_dev` as device count
 // and reads the slot after one stream synchronisation (no separate copy launch).
-int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
-                         uintptr_t stream) {
+LbState lb_begin(hipStream_t s) {
+  LbBuf& lb = g_lb[s];
+  if (!lb.p) {
+    MS_HIP_CHECK(hipMalloc((void**)&lb.p, kLbMaxTiles * sizeof(unsigned long long)));
+    MS_HIP_CHECK(hipMemsetAsync(lb.p, 0, kLbMaxTiles * sizeof(unsigned long long), s));
+  }
+  if (++lb.gen == 0) {  // the tags wrapped: clear the words (no stale tag can match gen 1 then)
+    MS_HIP_CHECK(hipMemsetAsync(lb.p, 0, kLbMaxTiles * sizeof(unsigned long long), s));
+    lb.gen = 1;
+  }
+  return {lb.p, lb.gen};
+}
+
+bool select_single_pass(long long n) { return g_sel_single && (n + kSelTile - 1) / kSelTile <= kLbMaxTiles; }
+
+void set_select_single_pass(int on, int items) {
+  g_sel_single = on;
+  if (items == 1 || items == 4 || items == kSelItems) g_sel_items = items;
+}
+
+// select_indices_async with the payload of select_lb_kernel (pay_dst: n bytes); single-pass only
+int select_indices_async_pay(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
+                             uintptr_t pay_src, uintptr_t pay_dst, uintptr_t stream);
+
+static int select_async_impl(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
+                             uintptr_t pay_src, uintptr_t pay_dst, uintptr_t stream) {
   if (!g_status) {
     MS_HIP_CHECK(hipHostMalloc((void**)&g_status, kStatusSlots * 4 * sizeof(long long),
                                hipHostMallocMapped | hipHostMallocCoherent));
@@ -359,6 +424,37 @@ int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, ui
   if (n >= (1ll << 40)) throw std::invalid_argument("select_indices_async: n too large");
   const long long tiles = (n + kSelTile - 1) / kSelTile;
   const void* sp = reinterpret_cast<const void*>(src);
+  if ((g_sel_single && tiles <= kLbMaxTiles) || pay_dst) {
+    if (tiles > kLbMaxTiles) throw std::invalid_argument("select_indices_async: payload selection of too many items");
+    const LbState lb = lb_begin(s);
+    // smaller tiles while they fit the status words: more workgroups, shorter per-tile chains
+    const int items = g_sel_items < kSelItems && n <= (long long)kLbMaxTiles * kSelThreads * g_sel_items ? g_sel_items
+                                                                                                      : kSelItems;
+    const unsigned grid = (unsigned)((n + (long long)kSelThreads * items - 1) / ((long long)kSelThreads * items));
+#define MS_SEL1(K, I)                                                                                               \
+  select_lb_kernel<K, I><<<grid, kSelThreads, 0, s>>>(n, sp, lb.status, lb.gen, P_<int64_t>(sel),                   \
+                                                      rest ? P_<int64_t>(rest) : nullptr, P_<int32_t>(out_dev), h64, \
+                                                      P_<uint8_t>(pay_src), P_<uint8_t>(pay_dst));                  \
+  MS_LAUNCH_CHECK();
+#define MS_SELI(K)             \
+  if (items == 1) {            \
+    MS_SEL1(K, 1)              \
+  } else if (items == 4) {     \
+    MS_SEL1(K, 4)              \
+  } else {                     \
+    MS_SEL1(K, kSelItems)      \
+  }
+    switch (kind) {
+      case kMaskSet: MS_SELI(kMaskSet) break;
+      case kMaskClear: MS_SELI(kMaskClear) break;
+      case kI32Pos: MS_SELI(kI32Pos) break;
+      case kI64NonNeg: MS_SELI(kI64NonNeg) break;
+      default: throw std::invalid_argument("select_indices_async: unknown predicate");
+    }
+#undef MS_SELI
+#undef MS_SEL1
+    return slot;
+  }
   auto tb = tiles_for(s, tiles);
   int32_t* tc = tb.first;
   int32_t* tm = tb.second;
@@ -378,6 +474,17 @@ int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, ui
   }
 #undef MS_SEL
   return slot;
+}
+
+int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
+                         uintptr_t stream) {
+  return select_async_impl(n, kind, src, sel, rest, out_dev, 0, 0, stream);
+}
+
+int select_indices_async_pay(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
+                             uintptr_t pay_src, uintptr_t pay_dst, uintptr_t stream) {
+  if (!pay_src || !pay_dst) throw std::invalid_argument("select_indices_async_pay: no payload");
+  return select_async_impl(n, kind, src, sel, rest, out_dev, pay_src, pay_dst, stream);
 }
 
 void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t dst, uintptr_t stream) {

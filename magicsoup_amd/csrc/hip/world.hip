@@ -12,6 +12,7 @@
 #include <unordered_map>
 
 #include "hip_common.h"
+#include "select_lb.h"
 
 namespace msd {
 
@@ -64,6 +65,46 @@ __global__ void __launch_bounds__(256) divide_commit_kernel(const int* dn, const
     cell_mols[c * m + j] = h;
     if (j == 0) {
       par[i] = p;
+      const long long px = result[p];
+      pos[2 * c] = (int32_t)(px / C);
+      pos[2 * c + 1] = (int32_t)(px - (px / C) * C);
+      const int32_t d = divisions[p] + 1;
+      divisions[p] = d;
+      divisions[c] = d;
+      lifetimes[p] = 0;
+      lifetimes[c] = 0;
+    }
+  }
+}
+
+// The winner selection of divide_mask_dev_at and divide_commit_kernel in one launch (select_lb.h):
+// the k-th parent p (result[p] >= 0, ascending) becomes parent of row n0 (+ *n0_dev) + k. Each
+// tile (256 cells: one per thread, so the grid has as many workgroups as divide_commit_kernel
+// needs for its latency-bound row updates) commits its own winners afterwards, the workgroup's
+// threads over (winners x m).
+__global__ void __launch_bounds__(kSelThreads) select_commit_kernel(int n, const long long* result,
+                                                                    unsigned long long* status, uint32_t gen,
+                                                                    int64_t* wins, int32_t* dcount, long long* host64,
+                                                                    int C, long long n0, const int* n0_dev, int m,
+                                                                    int64_t* par, int32_t* pos, float* cell_mols,
+                                                                    int32_t* divisions, int32_t* lifetimes) {
+  int cnt = 0;
+  const long long toff = select_lb_tile<1>(
+      n, [&](long long i) { return result[i] >= 0; }, status, gen,
+      [&](long long k, long long p) {
+        wins[k] = p;
+        par[k] = p;
+      },
+      [](long long, long long) {}, dcount, host64, &cnt);
+  __syncthreads();  // the tile's wins[] entries (this workgroup's stores) are visible to all its waves
+  const long long c0 = n0 + (n0_dev ? (long long)*n0_dev : 0ll) + toff;
+  for (int t = threadIdx.x; t < cnt * m; t += blockDim.x) {
+    const int q = t / m, j = t - q * m;
+    const long long p = wins[toff + q], c = c0 + q;
+    const float h = cell_mols[p * m + j] * 0.5f;
+    cell_mols[p * m + j] = h;
+    cell_mols[c * m + j] = h;
+    if (j == 0) {
       const long long px = result[p];
       pos[2 * c] = (int32_t)(px / C);
       pos[2 * c + 1] = (int32_t)(px - (px / C) * C);
@@ -292,10 +333,13 @@ __global__ void __launch_bounds__(1024) place_rounds_wg_kernel(int k, const int6
 // barriers per round. The list is `cells` (list position = priority) or, with cells == nullptr,
 // cell i itself for i < k with `mask[i]` selecting the cells that take part (divide_cells(mask):
 // no index compaction and no host round trip before placement).
-// ctl: unsigned[2 + kMaxRounds], zeroed before the launch (barrier counter, pending per round,
+// ctl: unsigned[kCtlWords], zeroed before the launch (barrier counter, pending per round,
 // barrier-timeout error word). A barrier timeout is also reported in `err_host` (pinned, mapped),
 // which the host checks after the placement's one synchronisation (place_error_take).
 constexpr int kMaxRounds = 16;
+// control words per launch: barrier counter, pending per round, timeout error word, then the tail
+// kernel's done-workgroup counter and list length
+constexpr int kCtlDone = kMaxRounds + 2, kCtlList = kMaxRounds + 3, kCtlWords = kMaxRounds + 4;
 
 // Grid-wide barrier of a cooperative launch. Data shared between workgroups of different XCDs
 // (their L2s are not coherent for ordinary device memory) is only touched with device-scope atomics
@@ -344,7 +388,7 @@ __global__ void __launch_bounds__(256) place_rounds_coop_kernel(int k, const int
   // the other control buffer, used by the next launch on this stream (which starts after this one
   // ended), cleared here: no memset launch before every placement
   if (blockIdx.x == 0)
-    for (int j = threadIdx.x; j < kMaxRounds + 2; j += blockDim.x) ctl_next[j] = 0u;
+    for (int j = threadIdx.x; j < kCtlWords; j += blockDim.x) ctl_next[j] = 0u;
   const int stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
   unsigned phase = 0;
   __shared__ int s_left;
@@ -404,6 +448,147 @@ __global__ void __launch_bounds__(256) place_rounds_coop_kernel(int k, const int
     const long long px = result[i];
     if (px >= 0) claim[px] = kNoClaim;
   }
+}
+
+// place_rounds_coop_kernel with the later rounds over round 0's losers only. Round 0 runs over all
+// cells -- its bids read the map with plain loads (nothing in this launch has written it yet) --
+// then a grid barrier, the round's resolution with the losers appended to a list (device-scope
+// atomics), a second barrier, and the remaining rounds over that list: by workgroup 0 alone, rounds
+// separated by __syncthreads, when the list is short (a sparse map: round 0 places almost every
+// cell), else by the whole grid with two barriers per round. Same bids, priorities (claims:
+// atomicMin of the cell's list position) and RNG streams as the other paths, so the same placement;
+// the all-grid form paid two grid barriers per round over all cells, at least four in all.
+// Cross-XCD rule (as above): data one workgroup writes and another reads goes through device-scope
+// atomics (map, claims, list entries); a loser's result, pending state and later bids are written by
+// the tail workgroup only (ls: per list entry -2 done, -1 pending, >= 0 the current bid pixel).
+constexpr long long kLsDone = -2, kLsPending = -1;
+constexpr int kTailAlone = 512;  // list entries one workgroup takes on (2 per thread)
+__global__ void __launch_bounds__(256) place_tail_coop_kernel(int k, const int64_t* cells, const uint8_t* mask,
+                                                              const int32_t* pos, Geom g, bool vacate,
+                                                              uint8_t* cell_map, uint64_t seed, uint64_t call,
+                                                              long long* cand, int* claim, long long* result,
+                                                              int rounds, unsigned* ctl, unsigned* ctl_next,
+                                                              unsigned* err_host, int* list, long long* ls) {
+  const unsigned nb = gridDim.x;
+  if (blockIdx.x == 0)
+    for (int j = threadIdx.x; j < kCtlWords; j += blockDim.x) ctl_next[j] = 0u;
+  const int stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned phase = 0;
+  // round 0: bids (cand[i] >= 0 marks a bidder; the owner thread reads it back after the barrier)
+  for (int i = t0; i < k; i += stride) {
+    long long px = -1;
+    if (mask ? (mask[i] != 0) : true) {
+      const int c = cells ? (int)cells[i] : i;
+      long long nbh[8], fr[8];
+      const int cnt = moore(pos[2 * c], pos[2 * c + 1], g, nbh);
+      int nf = 0;
+      for (int q = 0; q < cnt; ++q)
+        if (!cell_map[nbh[q]]) fr[nf++] = nbh[q];
+      if (nf > 0) {
+        Philox rng(seed, call, (uint32_t)i);
+        px = fr[rng.below((uint32_t)nf)];
+        atomicMin(claim + px, i);
+      }
+    }
+    cand[i] = px;
+  }
+  grid_barrier(ctl, nb, phase, err_host);
+  for (int i = t0; i < k; i += stride) {
+    const long long px = cand[i];
+    if (px < 0) {
+      result[i] = -1;
+      continue;
+    }
+    if (__hip_atomic_load(claim + px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == i) {
+      result[i] = px;
+      map_set(cell_map, px);
+      const int x = (int)(px / g.C);
+      if (vacate && (g.wrap || (x >= g.r_lo && x < g.r_hi))) {
+        const int c = cells ? (int)cells[i] : i;
+        map_clear(cell_map, (long long)pos[2 * c] * g.C + pos[2 * c + 1]);
+      }
+    } else {
+      const unsigned j = __hip_atomic_fetch_add(ctl + kCtlList, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(list + j, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // the list is complete and round 0's claims / map bits are in once every workgroup is past this
+  grid_barrier(ctl, nb, phase, err_host);
+  // round-0 winners release their claims (a claimed pixel is occupied now: no later bid targets it)
+  for (int i = t0; i < k; i += stride) {
+    const long long px = cand[i];
+    if (px >= 0 && result[i] == px) claim[px] = kNoClaim;
+  }
+  const int L = (int)__hip_atomic_load(ctl + kCtlList, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (L == 0) return;
+  // a short list: workgroup 0 alone, rounds separated by __syncthreads; a long one (crowded maps,
+  // where most bids collide): the whole grid over the list, two grid barriers per round as before
+  const bool alone = L <= kTailAlone;
+  if (alone && blockIdx.x != 0) return;
+  const int j0 = alone ? (int)threadIdx.x : t0, js = alone ? (int)blockDim.x : stride;
+  __shared__ int s_left;
+  for (int j = j0; j < L; j += js) ls[j] = kLsPending;  // (entry j: always this thread's)
+  for (int r = 1; r < rounds; ++r) {
+    const uint64_t rc = call + ((uint64_t)r << 48);
+    for (int j = j0; j < L; j += js) {
+      if (ls[j] == kLsDone) continue;
+      const int i = __hip_atomic_load(list + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int c = cells ? (int)cells[i] : i;
+      long long nbh[8], fr[8];
+      const int cnt = moore(pos[2 * c], pos[2 * c + 1], g, nbh);
+      int nf = 0;
+      for (int q = 0; q < cnt; ++q)
+        if (!map_get(cell_map, nbh[q])) fr[nf++] = nbh[q];
+      if (nf == 0) {
+        ls[j] = kLsDone;
+        result[i] = -1;
+        continue;
+      }
+      Philox rng(seed, rc, (uint32_t)i);
+      const long long px = fr[rng.below((uint32_t)nf)];
+      ls[j] = px;
+      atomicMin(claim + px, i);
+    }
+    if (threadIdx.x == 0) s_left = 0;
+    if (alone)
+      __syncthreads();
+    else
+      grid_barrier(ctl, nb, phase, err_host);
+    int left = 0;
+    for (int j = j0; j < L; j += js) {
+      const long long px = ls[j];
+      if (px < 0) continue;
+      const int i = __hip_atomic_load(list + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_load(claim + px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == i) {
+        result[i] = px;
+        ls[j] = kLsDone;
+        map_set(cell_map, px);
+        const int x = (int)(px / g.C);
+        if (vacate && (g.wrap || (x >= g.r_lo && x < g.r_hi))) {
+          const int c = cells ? (int)cells[i] : i;
+          map_clear(cell_map, (long long)pos[2 * c] * g.C + pos[2 * c + 1]);
+        }
+        claim[px] = kNoClaim;  // a loser comparing after this sees no claim of its own either
+      } else {
+        ls[j] = kLsPending;
+        ++left;
+      }
+    }
+    if (left) atomicAdd(&s_left, left);
+    __syncthreads();
+    if (alone) {
+      const int tot = s_left;
+      __syncthreads();  // read by every thread before thread 0 clears it in the next round
+      if (tot == 0) break;
+    } else {
+      if (threadIdx.x == 0 && s_left) atomicAdd(ctl + 1 + r, (unsigned)s_left);
+      grid_barrier(ctl, nb, phase, err_host);
+      if (__hip_atomic_load(ctl + 1 + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) break;
+    }
+  }
+  // cells still pending after the last round stay where they are
+  for (int j = j0; j < L; j += js)
+    if (ls[j] != kLsDone) result[__hip_atomic_load(list + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)] = -1;
 }
 
 // ---------------------------------------------------------------- neighbours
@@ -699,6 +884,11 @@ static int g_place_par[kMaxDevices] = {};
 static unsigned* g_place_err = nullptr;           // pinned, mapped: a barrier timed out (any device)
 static unsigned* g_place_err_dev = nullptr;
 void set_place_mode(int mode) { g_place_mode = mode; }
+// 1: the single-launch placement with one grid barrier and a one-workgroup tail (place_tail_coop_kernel)
+static int g_place_tail = 1;
+static char* g_place_list[kMaxDevices] = {};
+static long long g_place_list_cap[kMaxDevices] = {};
+void set_place_tail(int on) { g_place_tail = on; }
 
 // 1 if a cooperative placement's grid barrier timed out since the last call (then its claims may
 // have raced: the caller treats the world state as corrupt); clears the word.
@@ -718,8 +908,8 @@ static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, co
   MS_HIP_CHECK(hipGetDevice(&dev));
   if (dev < 0 || dev >= kMaxDevices) throw std::runtime_error("place_coop: device index out of range");
   if (!g_place_ctl[dev]) {
-    MS_HIP_CHECK(hipMalloc((void**)&g_place_ctl[dev], 2 * (2 + kMaxRounds) * sizeof(unsigned)));
-    MS_HIP_CHECK(hipMemset(g_place_ctl[dev], 0, 2 * (2 + kMaxRounds) * sizeof(unsigned)));
+    MS_HIP_CHECK(hipMalloc((void**)&g_place_ctl[dev], 2 * kCtlWords * sizeof(unsigned)));
+    MS_HIP_CHECK(hipMemset(g_place_ctl[dev], 0, 2 * kCtlWords * sizeof(unsigned)));
     g_place_par[dev] = 0;
   }
   if (!g_place_err) {
@@ -737,13 +927,40 @@ static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, co
   int* cl = P_<int>(claim);
   long long* res = P_<long long>(result);
   int rr = std::min(rounds, kMaxRounds);
-  unsigned* ctl = g_place_ctl[dev] + g_place_par[dev] * (2 + kMaxRounds);
-  unsigned* ctl_next = g_place_ctl[dev] + (1 - g_place_par[dev]) * (2 + kMaxRounds);
+  unsigned* ctl = g_place_ctl[dev] + g_place_par[dev] * kCtlWords;
+  unsigned* ctl_next = g_place_ctl[dev] + (1 - g_place_par[dev]) * kCtlWords;
   unsigned* err = g_place_err_dev;
   Geom gg = g;
   bool vac = vacate;
   void* args[] = {&kk, &cp, &mp, &pp, &gg, &vac, &cm, &pend, &seed, &call, &cd, &cl, &res, &rr, &ctl, &ctl_next, &err};
   unsigned grid = std::min<unsigned>(cdiv(k, 256), (unsigned)g_coop_blocks);
+  if (g_place_tail && g_place_mode == 0) {
+    // the list of round-0 losers + the tail workgroup's per-entry state (grown when k grows: the
+    // stream is drained first, an earlier launch may still use the old buffer)
+    if ((long long)k > g_place_list_cap[dev]) {
+      if (g_place_list[dev]) {
+        MS_HIP_CHECK(hipStreamSynchronize(s));
+        MS_HIP_CHECK(hipFree(g_place_list[dev]));
+      }
+      g_place_list_cap[dev] = std::max<long long>(k, 1ll << 16);
+      MS_HIP_CHECK(hipMalloc((void**)&g_place_list[dev], g_place_list_cap[dev] * 12));
+    }
+    long long* ls = reinterpret_cast<long long*>(g_place_list[dev]);
+    int* list = reinterpret_cast<int*>(ls + g_place_list_cap[dev]);
+    static int resident_t[kMaxDevices] = {};
+    if (!resident_t[dev]) {
+      int per_cu = 0, cus = 0;
+      MS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)place_tail_coop_kernel, 256, 0));
+      MS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      resident_t[dev] = std::max(1, per_cu * cus);
+    }
+    grid = std::min<unsigned>(grid, (unsigned)resident_t[dev]);
+    place_tail_coop_kernel<<<grid, 256, 0, s>>>(kk, cp, mp, pp, gg, vac, cm, seed, call, cd, cl, res, rr, ctl, ctl_next,
+                                                err, list, ls);
+    MS_LAUNCH_CHECK();
+    g_place_par[dev] ^= 1;
+    return true;
+  }
   if (g_place_mode == 2) {
     const hipError_t e = hipLaunchCooperativeKernel((const void*)place_rounds_coop_kernel, dim3(grid), dim3(256), args,
                                                     0, s);
@@ -849,6 +1066,17 @@ int divide_mask_dev_at(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r
   if (g_place_mode == 1 ||
       !place_coop(n, 0, mask, pos, g, false, cell_map, pending, cand, claim, result, rounds, seed, call, s))
     place_rounds_launches(n, 0, mask, pos, g, false, cell_map, pending, cand, claim, result, rounds, seed, call, s);
+  if (select_single_pass(n) && cdiv(n, kSelThreads) <= (unsigned)kLbMaxTiles) {
+    long long* h64 = nullptr;
+    const int slot = status_slot_new(&h64);
+    const LbState lb = lb_begin(s);
+    select_commit_kernel<<<cdiv(n, kSelThreads), kSelThreads, 0, s>>>(
+        n, P_<long long>(result), lb.status, lb.gen, P_<int64_t>(wins), P_<int32_t>(dcount), h64, C, n0,
+        n0_dev ? P_<int>(n0_dev) : nullptr, m, P_<int64_t>(par), P_<int32_t>(pos), P_<float>(cell_mols),
+        P_<int32_t>(divisions), P_<int32_t>(lifetimes));
+    MS_LAUNCH_CHECK();
+    return slot;
+  }
   const int slot = select_indices_async(n, 3 /* int64 >= 0 */, result, wins, 0, dcount, stream);
   const unsigned grid = std::min<unsigned>(cdiv((long long)n * m, 256), 512u);
   divide_commit_kernel<<<grid, 256, 0, s>>>(P_<int>(dcount), P_<int64_t>(wins), P_<long long>(result), C, n0,

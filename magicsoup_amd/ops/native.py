@@ -84,6 +84,9 @@ def hip():
     if fresh and os.environ.get("MS_PLACE_MODE"):
         # 1: per-round placement launches, 2: the single launch as a cooperative launch (world.hip)
         mod.set_place_mode(int(os.environ["MS_PLACE_MODE"]))  # type: ignore[attr-defined]
+    if fresh and os.environ.get("MS_PLACE_TAIL"):
+        # 0: the all-grid placement rounds (two grid barriers per round) for A/B
+        mod.set_place_tail(int(os.environ["MS_PLACE_TAIL"]))  # type: ignore[attr-defined]
     if fresh and os.environ.get("MS_COOP_BLOCKS"):
         mod.set_coop_blocks(int(os.environ["MS_COOP_BLOCKS"]))  # type: ignore[attr-defined]
     if fresh and os.environ.get("MS_STENCIL_BLOCKS"):
@@ -95,6 +98,9 @@ def hip():
     if fresh and os.environ.get("MS_REC_THIN"):
         # 0: the per-slot recombination draws + selection pass (world.hip rec_slots) for A/B
         mod.set_rec_thinning(int(os.environ["MS_REC_THIN"]))  # type: ignore[attr-defined]
+    if fresh and os.environ.get("MS_SELECT_SINGLE"):
+        # 0: the two-launch count + write selection (select.hip) for A/B
+        mod.set_select_single_pass(int(os.environ["MS_SELECT_SINGLE"]), int(os.environ.get("MS_SELECT_ITEMS", "0")))  # type: ignore[attr-defined]
     if fresh and os.environ.get("MS_STENCIL_PF"):
         # rows in flight ahead of the stencil's current row (-1: auto, 0-3)
         mod.set_stencil_prefetch(int(os.environ["MS_STENCIL_PF"]))  # type: ignore[attr-defined]

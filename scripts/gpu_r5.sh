@@ -15,7 +15,7 @@ run() {  # run <name> <seconds> <cmd...>
   echo "   rc=$rc $(grep -h '^{"metric"' "$O/$name.log" | cut -c100-200)"
   if [ $rc -ne 0 ]; then tail -5 "$O/$name.log"; fi
   if fatal $rc; then echo "fatal rc=$rc in $name"; tail -30 "$O/$name.log"; exit $rc; fi
-  return 0
+  return $rc
 }
 trace() {  # trace <name> <steps-to-summarise> <bench args...>
   local name="$1" k="$2"; shift 2
@@ -32,8 +32,13 @@ for s in "$@"; do case "$s" in
   dt) run tests_diff 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_distributed.py -m gpu -q -x -k "diffus or stencil or mass or halo or strip" --timeout 300 --timeout-method thread ;;
   gt) run tests_gen 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_mutation_stats.py tests/test_gpu_distributed.py -m gpu -q -x -k "pipeline or recomb or evolve or merged or mutat or genetic" --timeout 300 --timeout-method thread ;;
   cbt) run tests_cb 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -x -k "chain_issued or pipeline or merged or recomb or kill_divide or lazy" --timeout 300 --timeout-method thread ;;
+  selt) run tests_sel 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -x -k "select or kill_divide or chain_issued or lazy or placement or divide" --timeout 300 --timeout-method thread || exit 1 ;;
+  selb) run select_bench 120 python scripts/select_bench.py ;;
+  ptab) for i in 1 2; do for t in 1 0; do MS_PLACE_TAIL=$t run ptab_${t}_$i 300 python bench.py; done; done ;;
+  kab) for kn in ${KAB:-set_place_tail=1,0 set_select_single_pass=1,0}; do run kab_${kn%%=*} 300 python scripts/knob_ab.py $kn --blocks 10 --k 20; done ;;
   spin) for i in 1 2; do for t in 1 0; do MS_EVENT_SPIN=$t run spin_${t}_$i 300 python bench.py; done; done ;;
   cbab) for i in 1 2; do for t in 1 0; do MS_CHAIN_BOUND=$t run cbab_${t}_$i 300 python bench.py; done; done ;;
+  ssab) for i in 1 2; do for t in 1 0; do MS_SELECT_SINGLE=$t run ssab_${t}_$i 300 python bench.py; done; done ;;
   rthin) for i in 1 2; do for t in 1 0; do MS_REC_THIN=$t run rthin_${t}_$i 300 python bench.py; done; done ;;
   tmem) run tests_mem 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -k "memory_model or past_2_31" --timeout 300 --timeout-method thread ;;
   tests) run tests 1000 python -u -m pytest tests -m gpu -q --maxfail 5 --timeout 120 --timeout-method thread ;;

@@ -437,6 +437,55 @@ def test_select_matches_nonzero(n):
     assert torch.equal(hip_ops.select(r, "i64nonneg")[0], torch.nonzero(r >= 0).flatten())
 
 
+@pytest.mark.parametrize("n", [1, 63, 4097, 50_000, 1_000_003, 4096 * 1024 + 5])
+def test_select_async_single_pass_matches_nonzero(n):
+    """select_indices_async: the single-pass form (tile counts tagged with a per-call generation,
+    select_lb.h; up to 1024 tiles) and the count + write pair (beyond, or switched off) give
+    torch.nonzero's lists and count, also for back-to-back calls on the same tile words."""
+    from magicsoup_amd.ops import hip_ops, native
+
+    g = torch.Generator(device="cuda").manual_seed(n)
+    try:
+        for single in (1, 0, 1):
+            native.hip().set_select_single_pass(single)
+            for p in (0.3, 0.97, 0.0):
+                mask = torch.rand(n, device="cuda", generator=g) < p
+                sel, rest, dcount, slot = hip_ops.select_async(mask, "set", rest=True)
+                cnt = hip_ops.wait_count(slot)
+                ref = torch.nonzero(mask).flatten()
+                assert cnt == ref.numel() == int(dcount[0])
+                assert torch.equal(sel[:cnt], ref)
+                assert torch.equal(rest[: n - cnt], torch.nonzero(~mask).flatten())
+    finally:
+        native.hip().set_select_single_pass(1)
+
+
+@pytest.mark.parametrize("map_size,n", [(64, 2500), (256, 6_000), (1024, 50_000)])
+def test_placement_tail_kernel_matches_all_grid_rounds(map_size, n):
+    """The one-barrier placement (round 0 over the grid, later rounds in one workgroup over round 0's
+    losers: world.hip place_tail_coop_kernel) places every cell where the all-grid rounds do -- on a
+    dense map (long tail) and a sparse one -- for divisions over a mask and for moves."""
+    from magicsoup_amd.ops import native
+
+    base = _world("cuda", map_size=map_size, n=n, s=200, seed=5)
+    base.synchronize()
+    out = []
+    try:
+        for tail in (1, 0):
+            native.hip().set_place_tail(tail)
+            w = copy.deepcopy(base)
+            ms.set_seed(9)
+            w.divide_cells(torch.arange(w.n_cells, device="cuda"))
+            w.move_cells(torch.arange(0, w.n_cells, 3, device="cuda"))
+            w.synchronize()
+            w.check_invariants()
+            out.append((w.n_cells, w.cell_positions.clone(), w.cell_map.clone()))
+    finally:
+        native.hip().set_place_tail(1)
+    assert out[0][0] == out[1][0] > n
+    assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][2], out[1][2])
+
+
 @pytest.mark.parametrize("n", [500, 6_000])
 def test_divide_placement_both_paths_keep_occupancy_consistent(n):
     """Single-workgroup placement rounds (k <= 2048) and the multi-launch path (larger k) both
@@ -1381,6 +1430,39 @@ def test_kill_divide_where_matches_masks_on_gpu():
     w1.kill_divide_where(atp, -1.0, 1e9, kill_fraction=0.3)
     assert 0.6 * n < w1.n_cells < 0.8 * n
     w1.check_invariants()
+
+
+@pytest.mark.gpu
+def test_kill_divide_single_pass_selections_match_two_pass():
+    """kill_divide_where with the single-pass selections (survivors + compacted division mask in one
+    launch, winners + division commit in one launch: select_lb.h) against the count + write passes
+    with the separate mask compaction and commit kernels: the same world, bit for bit."""
+    from magicsoup_amd.ops import native
+
+    base = _world("cuda", map_size=96, n=3000, s=400, seed=21)
+    base.enzymatic_activity()
+    base.synchronize()
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    out = []
+    try:
+        for single in (1, 0):
+            native.hip().set_select_single_pass(single)
+            w = copy.deepcopy(base)
+            ms.set_seed(6)
+            for _ in range(3):
+                w.kill_divide_where(atp, 1.0, 3.0, 2.0, kill_fraction=0.05)
+                w.enzymatic_activity()
+            w.synchronize()
+            w.check_invariants()
+            out.append({k: getattr(w, k).clone() for k in ("cell_molecules", "cell_positions", "cell_divisions",
+                                                          "cell_lifetimes", "molecule_map", "cell_map")})
+            out[-1]["genomes"] = list(w.cell_genomes)
+    finally:
+        native.hip().set_select_single_pass(1)
+    a, b = out
+    assert a["cell_positions"].shape[0] > 1000
+    for k in a:
+        assert (torch.equal(a[k], b[k]) if isinstance(a[k], torch.Tensor) else a[k] == b[k]), k
 
 
 @pytest.mark.gpu
