@@ -564,34 +564,44 @@ __global__ void __launch_bounds__(256) spill_free_kernel(int k, int m, const int
 
 // The kill / divide thresholds of kill_divide_where (fast.hip threshold_masks_kernel: kill below
 // `kill_below` or with probability `kill_p`, divide above `divide_above` paying `cost`) fused with
-// the killed cells' spill onto their pixels (spill_free_kernel): one thread per cell, the spill's
-// m map updates by the ~few percent of threads whose cell dies. One launch less in the step.
+// the killed cells' spill onto their pixels (spill_free_kernel). Thread (cell i, molecule j), as the
+// spill, whole cells per workgroup (blockDim = m * cells per block): every thread of a cell derives
+// its kill decision (same value, same Philox draw) before the barrier, after which j == 0 writes
+// the masks and the payment (a paying cell survives, so no spill reads the paid molecule).
+// One launch less in the step.
 template <class T>
 __global__ void __launch_bounds__(256) threshold_spill_kernel(int n, int m, int mol, float kill_below, float divide_above,
                                                               float cost, float kill_p, uint64_t seed, uint64_t call,
                                                               float* mols, uint8_t* kill, uint8_t* divide,
                                                               const int32_t* pos, int C, long long plane, T* map,
                                                               uint8_t* cell_map, const float* corr) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  // (more molecules than threads: one cell per workgroup, molecules strided over the threads)
+  const int cpb = max(1, (int)blockDim.x / m), jstep = cpb == 1 ? (int)blockDim.x : m;
+  const int i = blockIdx.x * cpb + (cpb == 1 ? 0 : (int)threadIdx.x / m);
+  const int j = cpb == 1 ? (int)threadIdx.x : (int)threadIdx.x % m;
+  const bool live = (cpb == 1 || (int)threadIdx.x < cpb * m) && i < n && j < m;
   float* x = mols + (size_t)i * m + mol;
-  const float v = *x;
+  const float v = live ? *x : 0.0f;
   bool k = v < kill_below;
   if (kill_p > 0.0f) {
     Philox rng(seed, call, (uint32_t)i);
     k |= rng.uniform() < kill_p;
   }
-  const bool d = !k && v > divide_above;
-  if (d) *x = v - cost;
-  kill[i] = k;
-  divide[i] = d;
+  __syncthreads();  // every thread of the cell has read the molecule before j == 0 pays from it
+  if (!live) return;
+  if (j == 0) {
+    const bool d = !k && v > divide_above;
+    if (d) *x = v - cost;
+    kill[i] = k;
+    divide[i] = d;
+  }
   if (k) {
     const long long pix = (long long)pos[2 * i] * C + pos[2 * i + 1];
-    for (int j = 0; j < m; ++j) {
-      T* p = map + j * plane + pix;
-      st(p, corr_out(corr_in(ld(p), corr, j) + mols[(size_t)i * m + j], corr, j));
+    for (int jj = j; jj < m; jj += jstep) {
+      T* p = map + jj * plane + pix;
+      st(p, corr_out(corr_in(ld(p), corr, jj) + mols[(size_t)i * m + jj], corr, jj));
     }
-    cell_map[pix] = 0;
+    if (j == 0) cell_map[pix] = 0;
   }
 }
 
@@ -906,7 +916,8 @@ void threshold_spill(int n, int m, int mol, float kill_below, float divide_above
                      uint64_t call, uintptr_t mols, uintptr_t kill, uintptr_t divide, uintptr_t pos, int R, int C,
                      uintptr_t map, uintptr_t cell_map, int dtype, uintptr_t corr, uintptr_t stream) {
   if (n <= 0 || m <= 0) return;
-  MS_MAP_DISPATCH(dtype, (threshold_spill_kernel<T><<<cdiv(n, 256), 256, 0, S_(stream)>>>(
+  const int cpb = std::max(1, 256 / m);
+  MS_MAP_DISPATCH(dtype, (threshold_spill_kernel<T><<<cdiv(n, cpb), cpb == 1 ? 256 : cpb * m, 0, S_(stream)>>>(
                              n, m, mol, kill_below, divide_above, cost, kill_p, seed, call, P_<float>(mols),
                              P_<uint8_t>(kill), P_<uint8_t>(divide), P_<int32_t>(pos), C, (long long)R * C, P_<T>(map),
                              P_<uint8_t>(cell_map), P_<float>(corr))));
