@@ -1310,6 +1310,9 @@ __global__ void __launch_bounds__(kBlock, 1) integrate_rescue_kernel(RescueArgs 
 
 static int g_rescue_mode = 1;  // 0: the separate launches (A/B)
 void set_rescue_mode(int m) { g_rescue_mode = m; }
+// workgroups of the strided 64-lane overflow-list launch (its length is only known on the device)
+static unsigned g_ovf_blocks = 64;
+void set_overflow_blocks(int n) { g_ovf_blocks = (unsigned)std::max(1, std::min(n, 4096)); }
 static unsigned g_rescue_blocks = 0;  // co-resident grid: one block per CU
 static unsigned* g_rescue_err = nullptr;
 static unsigned* g_rescue_err_dev = nullptr;
@@ -1825,7 +1828,7 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
           *g_rescue_err = 0;
           MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_rescue_err_dev, g_rescue_err, 0));
         }
-        integrate_fast_kernel<64, kNzWide, true, true><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
+        integrate_fast_kernel<64, kNzWide, true, true><<<g_ovf_blocks, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
         MS_LAUNCH_CHECK();
         RescueArgs r{};
         r.lb = a;
@@ -1873,7 +1876,7 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
         MS_LAUNCH_CHECK();
         return 1;
       }
-      integrate_fast_kernel<64, kNzWide, true, true><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
+      integrate_fast_kernel<64, kNzWide, true, true><<<g_ovf_blocks, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
       MS_LAUNCH_CHECK();
     } else {
       // 64-lane cells: no wider register level for more than 64 active proteins, so the narrow
@@ -1892,12 +1895,12 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
         else if (g_spl2_waves == 3) integrate_spl2_spec_kernel<3><<<g2, kBlock, lds_n, st>>>(an);
         else integrate_spl2_spec_kernel<4><<<g2, kBlock, lds_n, st>>>(an);
         MS_LAUNCH_CHECK();
-        integrate_fast_kernel<64, kNzWide, true, true, 2><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
+        integrate_fast_kernel<64, kNzWide, true, true, 2><<<g_ovf_blocks, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
       } else {
         integrate_fast_kernel<64, kNzReg, false, true><<<cdiv(c, kBlock / 64), kBlock, lds_n, st>>>(an, nullptr,
                                                                                                  nullptr);
         MS_LAUNCH_CHECK();
-        integrate_fast_kernel<64, kNzWide, true, true><<<64, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
+        integrate_fast_kernel<64, kNzWide, true, true><<<g_ovf_blocks, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
       }
       MS_LAUNCH_CHECK();
     }

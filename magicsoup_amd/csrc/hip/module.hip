@@ -24,6 +24,7 @@ void place_rounds_mask(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r
                        uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result,
                        int rounds, uint64_t seed, uint64_t call, uintptr_t stream);
 void set_coop_blocks(int n);
+void set_overflow_blocks(int n);
 void set_place_tail(int on);
 void set_stencil_vec(int v);
 void set_stencil_prefetch(int pf);
@@ -283,6 +284,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("place_rounds", &msd::place_rounds);
   m.def("place_rounds_mask", &msd::place_rounds_mask, "cooperative placement over cells selected by a mask");
   m.def("set_place_tail", &msd::set_place_tail, "1: single-launch placement with one grid barrier + a one-workgroup tail of the later rounds");
+  m.def("set_overflow_blocks", &msd::set_overflow_blocks, "workgroups of the integrator's strided overflow-list launch");
   m.def("set_coop_blocks", &msd::set_coop_blocks, "workgroups of the cooperative placement (A/B)");
   m.def("set_stencil_vec", &msd::set_stencil_vec, "diffusion stencil columns per lane: 8 (default), 4 or 1");
   m.def("set_stencil_prefetch", &msd::set_stencil_prefetch, "rows the vector stencils load ahead (-1 auto, 0-3)");

@@ -59,10 +59,25 @@ def main():
         trace(genome_pipeline, name)
     trace(streams.NEvent, "synchronize")
     trace(hip_ops, "guarded_sync")
+    trace(hip_ops, "_launch_integrate")
     ms.set_seed(0)
     torch.manual_seed(0)
     bench._prime_rare_paths(CHEMISTRY, "cuda:0", torch.float32, 500)
-    w = ms.World(chemistry=CHEMISTRY, map_size=S, device="cuda:0", seed=0)
+    if os.environ.get("MS_VIRTUAL_STRIPS") == "1":  # a one-rank strip world (host_split.py)
+        import torch.distributed as dist
+
+        from magicsoup_amd.parallel import DistributedWorld, dist_world
+
+        for name in ("enzymatic_activity", "_resolve_count", "_divide_phase_b", "_divide_mask_native",
+                     "kill_divide_where", "_evolve", "diffuse_molecules"):
+            if name in DistributedWorld.__dict__:
+                trace(DistributedWorld, name)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29548")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        w = DistributedWorld(chemistry=CHEMISTRY, map_size=S, device="cuda", seed=0, strips=True)
+    else:
+        w = ms.World(chemistry=CHEMISTRY, map_size=S, device="cuda:0", seed=0)
     w.spawn_cells(bench.random_genomes(N, 500, "cuda:0"))
     atp = CHEMISTRY.molname_2_idx["ATP"]
     for _ in range(warm):

@@ -40,6 +40,8 @@ for s in "$@"; do case "$s" in
      (cd /tmp && timeout -k 10 120 rocprofv3 --kernel-trace -d "$OLDPWD/$O/evlab" -o run --output-format csv -- /tmp/event_lab.bin) > $O/evlab.log 2>&1 && \
      python scripts/event_lab_report.py $O/evlab/run_kernel_trace.csv | tee -a $O/evlab.log ;;
   virtab) for i in 1 2; do for c in 1,1 0,1 1,0 0,0; do IFS=, read pt ss <<< "$c"; MS_PLACE_TAIL=$pt MS_SELECT_SINGLE=$ss MS_VIRTUAL_STRIPS=1 run virtab_${pt}_${ss}_$i 300 python bench.py --map-size 1448 --cells 6250; done; done ;;
+  cov) MS_VIRTUAL_STRIPS=1 run call_order_virtual 300 python scripts/call_order.py 4096 50000 20 2 ;;
+  kab256) for kn in ${KAB:-set_overflow_blocks=64,512}; do run kab256_${kn%%=*} 300 python scripts/knob_ab.py $kn --blocks 10 --k 20 --size 256 --cells 40000; done ;;
   spin) for i in 1 2; do for t in 1 0; do MS_EVENT_SPIN=$t run spin_${t}_$i 300 python bench.py; done; done ;;
   cbab) for i in 1 2; do for t in 1 0; do MS_CHAIN_BOUND=$t run cbab_${t}_$i 300 python bench.py; done; done ;;
   ssab) for i in 1 2; do for t in 1 0; do MS_SELECT_SINGLE=$t run ssab_${t}_$i 300 python bench.py; done; done ;;
