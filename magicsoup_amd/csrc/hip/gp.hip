@@ -391,7 +391,8 @@ __global__ void __launch_bounds__(256) gp_union_kernel(int ucap, int mcap, const
                                                        const int* mut_cnt, const int64_t* mut_sel, long long arr0,
                                                        int narr, int64_t* cells, int* cnt_u, const int* rec_pairs,
                                                        const int* rec_opflags, const int* mut_opflags,
-                                                       long long* parts_status) {
+                                                       long long* parts_status, const unsigned long long* top,
+                                                       long long* top_host) {
   const int cr = *rec_cnt, cm = min(*mut_cnt, mcap);
   const int nr = min(cr, ucap - narr), nm = min(cm, ucap - narr - nr);
   for (int j = threadIdx.x; j < nr; j += blockDim.x) cells[j] = rec_cells[j];
@@ -403,6 +404,11 @@ __global__ void __launch_bounds__(256) gp_union_kernel(int ucap, int mcap, const
     parts_status[1] = __hip_atomic_load(rec_opflags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     parts_status[2] = *mut_cnt;
     parts_status[3] = __hip_atomic_load(mut_opflags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the pool's bump counter after the chain's last allocation, mirrored into mapped host memory:
+    // the host tightens its upper bound of it at the next reconcile without a read-back
+    if (top_host)
+      __hip_atomic_store(top_host, (long long)__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -436,7 +442,8 @@ std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpAren
                               double p, double p_indel, double p_del, uint64_t seed_m, uint64_t call_m, int mcap,
                               int kcap, int dcap, uintptr_t mark, uint64_t gen, uintptr_t blob_r, uintptr_t blob_m,
                               uintptr_t blob_u, bool fresh, long long nrows, py::object extra, uintptr_t nres,
-                              long long arr0, int narr, uintptr_t nd_a, uintptr_t nd_b, uintptr_t stream) {
+                              long long arr0, int narr, uintptr_t nd_a, uintptr_t nd_b, uintptr_t top_host,
+                              uintptr_t stream) {
   hipStream_t s = S_(stream);
   if (narr < 0) throw std::invalid_argument("gp_evolve: negative arrival count");
   const int n = ar.n, L = ar.width;
@@ -483,7 +490,8 @@ std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpAren
   gp_union_kernel<<<1, 256, 0, s>>>(ucap, mcap, P_<int>(ar.cnt2), P_<int64_t>(cells), P_<int>(am.cnt),
                                     P_<int64_t>(msel), arr0, narr, P_<int64_t>(ucells), P_<int>(ucnt),
                                     P_<int>(xr ? nres : ar.cnt),
-                                    P_<int>(ar.opflags), P_<int>(am.opflags), ps.first);
+                                    P_<int>(ar.opflags), P_<int>(am.opflags), ps.first,
+                                    P_<unsigned long long>(ar.top), top_host ? P_<long long>(top_host) : nullptr);
   MS_LAUNCH_CHECK();
   const int slot_u = rebuild(ucap, ucells, ucnt, au, g, k, dcap, cu, ucnt, s);
   return {slot_u, ps.second};
@@ -492,6 +500,21 @@ std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpAren
 void bind_gp(py::module_& m) {
   m.def("gp_evolve", &gp_evolve, "device-pipeline recombinate_cells() + mutate_cells() with one rebuild (no sync)");
   m.def("gp_evolve_union_bytes", &gp_evolve_union_bytes);
+  // a pinned, device-mapped int64 (host pointer, device pointer) and its host-side read / write
+  m.def("mapped_i64", []() {
+    long long* h = nullptr;
+    long long* d = nullptr;
+    MS_HIP_CHECK(hipHostMalloc((void**)&h, sizeof(long long), hipHostMallocMapped | hipHostMallocCoherent));
+    MS_HIP_CHECK(hipHostGetDevicePointer((void**)&d, h, 0));
+    *h = -1;
+    return std::make_pair(reinterpret_cast<uintptr_t>(h), reinterpret_cast<uintptr_t>(d));
+  });
+  m.def("mapped_i64_read", [](uintptr_t h) {
+    return __atomic_load_n(reinterpret_cast<long long*>(h), __ATOMIC_ACQUIRE);
+  });
+  m.def("mapped_i64_write", [](uintptr_t h, long long v) {
+    __atomic_store_n(reinterpret_cast<long long*>(h), v, __ATOMIC_RELEASE);
+  });
   py::class_<GpArena>(m, "GpArena", py::module_local())
       .def(py::init<>())
       .def_readwrite("data", &GpArena::data).def_readwrite("lens", &GpArena::lens)

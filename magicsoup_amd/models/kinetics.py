@@ -562,15 +562,16 @@ class Kinetics:
         self._sync()
         return self._alloc_rows_now(k)
 
-    def _reserve_rows(self, k: int, sync: bool = True) -> None:
+    def _reserve_rows(self, k: int, sync: bool = True, headroom: int = 0) -> None:
         """Make room for k fresh rows without taking them (the device genome pipeline takes them
         with its own device-side row counter, magicsoup_amd.ops.genome_pipeline). ``sync=False``: the
         owner's pending state is not resolved first (a chain issued on a device count; the caller
-        checked :meth:`_rows_available`)."""
+        checked :meth:`_rows_available`). ``headroom``: room for that many more (a recycling or a
+        growth now, so that the next chains find their rows without one)."""
         if sync:
             self._sync()
-        self._alloc_rows_now(k, want=False)
-        self.__dict__["_nrows"] -= k
+        self._alloc_rows_now(k + headroom, want=False)
+        self.__dict__["_nrows"] -= k + headroom
 
     def _rows_available(self, k: int) -> bool:
         """Whether k fresh rows exist without a recycling or a growth (slot mode)."""

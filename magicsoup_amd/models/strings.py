@@ -240,9 +240,29 @@ class PoolArena:
         self.data = torch.empty(_POOL_MIN, dtype=torch.uint8, device=self.device)
         self.top = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.failed = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self.top_ub = 0
+        self._top_ub = 0
+        self.inc_total = 0  # every raise of top_ub so far (genome_pipeline's pool mirror bound)
+        self.collects = 0  # pool replacements (collect / clear): a mirrored device top is void after one
         self.n = 0
         self.version = 0
+
+    def __setstate__(self, state: dict) -> None:
+        # (states saved before the bound tracking carry a plain ``top_ub``)
+        if "top_ub" in state:
+            state["_top_ub"] = state.pop("top_ub")
+        state.setdefault("inc_total", 0)
+        state.setdefault("collects", 0)
+        self.__dict__.update(state)
+
+    @property
+    def top_ub(self) -> int:
+        return self._top_ub
+
+    @top_ub.setter
+    def top_ub(self, v: int) -> None:
+        if v > self._top_ub:
+            self.inc_total += v - self._top_ub
+        self._top_ub = v
 
     # ---------------------------------------------------------------- capacity
     @property
@@ -299,6 +319,7 @@ class PoolArena:
         from magicsoup_amd.ops.hip_ops import _stream
 
         n = self.n
+        self.collects += 1
         if n == 0:
             self.data = torch.empty(max(_POOL_MIN, 2 * _r16(extra)), dtype=torch.uint8, device=self.device)
             self.top.zero_()
@@ -408,6 +429,7 @@ class PoolArena:
     def clear(self) -> None:
         self.n = 0
         self.top.zero_()
+        self.collects += 1
         self.top_ub = 0
         self.version += 1
 

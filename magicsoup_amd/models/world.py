@@ -57,9 +57,11 @@ _COUNT_SAFE_OPS = frozenset({"mutate_cells", "recombinate_cells", "degrade_molec
 # harmless for stale ones)
 _CHECK_ENV = os.environ.get("MS_CHECK_INVARIANTS") == "1"
 _DEFER_ENV = os.environ.get("MS_DEFER_GENOME_OPS", "1")
-# issue a queued recombinate + mutate pair on a pending kill_divide's device count (World._chain_bound;
-# MS_CHAIN_BOUND=0: wait for the count on the host first)
-_CHAIN_BOUND = os.environ.get("MS_CHAIN_BOUND", "1") != "0"
+# issue a queued recombinate + mutate pair on a pending kill_divide's device count (World._chain_bound)
+# instead of waiting for the count on the host first. Off by default: in-process A/B over 400 steps
+# (scripts/knob_ab.py, profiles/r5/devcount/) the bound-sized chain was 3-4 % slower on the flagship
+# (later, grown-genome steps) and on 256^2 / 40k; over the driver's early steps it is a tie.
+_CHAIN_BOUND = os.environ.get("MS_CHAIN_BOUND", "0") == "1"
 # The genome chains flushed onto the side stream (World._flush_deferred) are joined into the compute
 # stream at the next op that needs their results (the activity, or a read of genomes / parameters),
 # not right after the flush: the molecule-only work in between (the lifetimes, the loop's masks)

@@ -370,6 +370,11 @@ class _PartHost:
         return {0: self.parts[2], 1: self.parts[3], 2: 0, 3: self.parts[2]}[i]
 
 
+# why issues on a pending kill_divide's device count were declined (World._chain_bound; the caller
+# then waits for the count): diagnostics for scripts/call_order.py
+BOUND_DECLINED = {"pending": 0, "caps": 0, "rows": 0, "pool": 0}
+
+
 def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=None, arrivals=None,
            bound=None) -> bool:
     """``recombinate_cells(p=p_rec)`` followed by ``mutate_cells(p, p_indel, p_del)`` over all cells
@@ -398,6 +403,7 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
     st = _state(world)
     if any(pd.kind in ("rec", "mut", "evo") for pd in st["pending"]):
         if bound is not None:
+            BOUND_DECLINED["pending"] += 1
             return False
         reconcile(world)
     dev = arena.data.device
@@ -414,13 +420,19 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
         # collection (it moves the live cells' genomes)
         sc_cap = int(_m().sel_sort_cap())
         if extra is not None or narr or max(pcap, mcap, 2 * pcap) > sc_cap:
+            BOUND_DECLINED["caps"] += 1
             return False
         if fresh and not kin._rows_available(2 * min(n, N_CAP)):
+            BOUND_DECLINED["rows"] += 1
             return False
         if arena.top_ub + room > arena.pool_cap:
+            BOUND_DECLINED["pool"] += 1
             return False
     if fresh:
-        kin._reserve_rows(2 * min(n, N_CAP) + narr, sync=bound is None)
+        # (on the synchronous path with room for the next call as well: chains issued on a device
+        # count cannot recycle rows, World._chain_bound)
+        kin._reserve_rows(2 * min(n, N_CAP) + narr, sync=bound is None,
+                          headroom=2 * N_CAP if bound is None else 0)
     _room(world, room)
     br, bm, bu = _bufs(world, "rec"), _bufs(world, "mut"), _bufs(world, "evo")
     ar, am, au = _arena_desc(world, br), _arena_desc(world, bm), _arena_desc(world, bu)
@@ -443,10 +455,14 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
         sc.bufs["arena_gen"] = 0
     gen = sc.bufs["arena_gen"] = sc.bufs.get("arena_gen", 0) + 1
     rng_r, rng_m = _rng(), _rng()
+    mirror = _top_mirror(world)
+    _m().mapped_i64_write(mirror[0], -1)
+    st["mirror_mark"] = (arena.collects, arena.inc_total, mirror[0])
     slot_u, slot_p = _m().gp_evolve(ar, am, au, _gen_desc(world, dev), k, _p(keys), nbr, float(p_rec), rng_r[0],
                                     rng_r[1], pcap, float(p), float(p_indel), float(p_del), rng_m[0], rng_m[1], mcap,
                                     K_CAP, D_CAP, _p(mark), int(gen), _p(blob_r), _p(blob_m), _p(blob_u), fresh,
-                                    int(kin.__dict__["_nrows"]), extra, _p(nres), arr0, narr, nd[0], nd[1], _stream())
+                                    int(kin.__dict__["_nrows"]), extra, _p(nres), arr0, narr, nd[0], nd[1], mirror[1],
+                                    _stream())
     lay_r = _m().gp_layout(1, n, pcap, L, K_CAP, xr)
     lay_m = _m().gp_layout(0, n, mcap, L, K_CAP, 0)
     parts = _StatusSlot(slot_p)
@@ -569,11 +585,36 @@ def reconcile(world) -> None:
     world_ops.enzymatic_activity(world)
 
 
+def _top_mirror(world) -> tuple[int, int]:
+    """(host, device) address of the mapped int64 into which a merged chain writes the pool's bump
+    counter after its last allocation (gp.hip gp_union_kernel)."""
+    c = _cache(world)
+    mm = c.get("top_mirror")
+    if mm is None:
+        mm = c["top_mirror"] = _m().mapped_i64()
+    return mm
+
+
+def _tighten_pool_bound(world) -> None:
+    """With every issued chain complete: the host bound of the pool counter becomes the last merged
+    chain's mirrored counter plus what was reserved since that chain's issue (instead of the sum of
+    every call's worst case since the last read-back). Keeps the device-count issue
+    (World._chain_bound) from being declined for pool room that was reserved but never used."""
+    mm = _state(world).get("mirror_mark")
+    arena = world._genomes
+    if mm is None or mm[0] != arena.collects or mm[2] != _top_mirror(world)[0]:
+        return
+    v = int(_m().mapped_i64_read(mm[2]))
+    if v >= 0:
+        arena.top_ub = min(arena.top_ub, v + arena.inc_total - mm[1])
+
+
 def _resolve(world, pend: list) -> bool:
     """True if any genome or parameter was changed on the host."""
     rebuilt = False
     kin = world.kinetics
     pend[-1].event.synchronize()
+    _tighten_pool_bound(world)
     kin.__dict__["_nrows"] = max(int(kin.__dict__["_nrows"]), int(pend[-1].host[2]))
     for pd in pend:
         if pd.kind == "evo":

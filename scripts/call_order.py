@@ -90,6 +90,7 @@ def main():
         bench.step(w, N, 500, atp)
         on[0] = False
     w.synchronize()
+    print("declined device-count chain issues:", genome_pipeline.BOUND_DECLINED, flush=True)
 
 
 if __name__ == "__main__":

@@ -35,15 +35,18 @@ for s in "$@"; do case "$s" in
   selt) run tests_sel 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -x -k "select or kill_divide or chain_issued or lazy or placement or divide" --timeout 300 --timeout-method thread || exit 1 ;;
   selb) run select_bench 120 python scripts/select_bench.py ;;
   ptab) for i in 1 2; do for t in 1 0; do MS_PLACE_TAIL=$t run ptab_${t}_$i 300 python bench.py; done; done ;;
-  kab) for kn in ${KAB:-set_place_tail=1,0 set_select_single_pass=1,0}; do run kab_${kn%%=*} 300 python scripts/knob_ab.py $kn --blocks 10 --k 20; done ;;
+  kab) for kn in ${KAB:-set_place_tail=1,0 set_select_single_pass=1,0}; do run kab_$(echo ${kn%%=*} | tr -c "a-zA-Z0-9_\n" _) 300 python scripts/knob_ab.py $kn --blocks 10 --k 20; done ;;
   evlab) hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/event_lab.hip -o /tmp/event_lab.bin && \
      (cd /tmp && timeout -k 10 120 rocprofv3 --kernel-trace -d "$OLDPWD/$O/evlab" -o run --output-format csv -- /tmp/event_lab.bin) > $O/evlab.log 2>&1 && \
      python scripts/event_lab_report.py $O/evlab/run_kernel_trace.csv | tee -a $O/evlab.log ;;
   virtab) for i in 1 2; do for c in 1,1 0,1 1,0 0,0; do IFS=, read pt ss <<< "$c"; MS_PLACE_TAIL=$pt MS_SELECT_SINGLE=$ss MS_VIRTUAL_STRIPS=1 run virtab_${pt}_${ss}_$i 300 python bench.py --map-size 1448 --cells 6250; done; done ;;
   cov) MS_VIRTUAL_STRIPS=1 run call_order_virtual 300 python scripts/call_order.py 4096 50000 20 2 ;;
-  kab256) for kn in ${KAB:-set_overflow_blocks=64,512}; do run kab256_${kn%%=*} 300 python scripts/knob_ab.py $kn --blocks 10 --k 20 --size 256 --cells 40000; done ;;
+  kab256) for kn in ${KAB:-set_overflow_blocks=64,512}; do run kab256_$(echo ${kn%%=*} | tr -c "a-zA-Z0-9_\n" _) 300 python scripts/knob_ab.py $kn --blocks 10 --k 20 --size 256 --cells 40000; done ;;
+  co256) run call_order_c256 300 python scripts/call_order.py 256 40000 20 3 ;;
+  dcab) for i in 1 2; do for t in 1 0; do MS_DEVCOUNT_OPS=$t run dcab256_${t}_$i 300 python bench.py --map-size 256 --cells 40000; MS_DEVCOUNT_OPS=$t run dcabf_${t}_$i 300 python bench.py; done; done ;;
+  lt) run tests_loop 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -x -k "deterministic or lazy or kill_divide or chain_issued or permeat or lifetime" --timeout 300 --timeout-method thread || exit 1 ;;
   spin) for i in 1 2; do for t in 1 0; do MS_EVENT_SPIN=$t run spin_${t}_$i 300 python bench.py; done; done ;;
-  cbab) for i in 1 2; do for t in 1 0; do MS_CHAIN_BOUND=$t run cbab_${t}_$i 300 python bench.py; done; done ;;
+  cbab) for i in 1 2 3; do for t in 1 0; do MS_CHAIN_BOUND=$t run cbab_${t}_$i 300 python bench.py; done; done ;;
   ssab) for i in 1 2; do for t in 1 0; do MS_SELECT_SINGLE=$t run ssab_${t}_$i 300 python bench.py; done; done ;;
   rthin) for i in 1 2; do for t in 1 0; do MS_REC_THIN=$t run rthin_${t}_$i 300 python bench.py; done; done ;;
   tmem) run tests_mem 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -k "memory_model or past_2_31" --timeout 300 --timeout-method thread ;;

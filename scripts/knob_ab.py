@@ -29,7 +29,16 @@ def main():
         opts[f] = int(v)
     name, vals = knob.split("=")
     vals = [int(v) for v in vals.split(",")]
-    setter = getattr(native.hip(), name)
+    if name.startswith("py:"):  # a module-level switch, e.g. py:magicsoup_amd.models.world._DEVCOUNT_OPS
+        import importlib
+
+        mod_name, attr = name[3:].rsplit(".", 1)
+        mod = importlib.import_module(mod_name)
+
+        def setter(v):
+            setattr(mod, attr, type(getattr(mod, attr))(v))
+    else:
+        setter = getattr(native.hip(), name)
     S, N = opts["--size"], opts["--cells"]
     ms.set_seed(0)
     torch.manual_seed(0)
