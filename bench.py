@@ -114,7 +114,7 @@ def random_genomes(k: int, size: int, device) -> tuple[torch.Tensor, torch.Tenso
 
 # running means of divisions / starvation deaths, and the previous step's dilution (its kill and
 # division counts are only read at the next step's start, when the population is known anyway)
-_CHEMOSTAT = {"divided": 0, "starved": 0, "steps": 0, "excess": None}
+_CHEMOSTAT = {"divided": 0, "starved": 0, "steps": 0, "excess": None, "last_d": 0, "last_s": 0}
 
 
 _NULL = contextlib.nullcontext()
@@ -140,6 +140,7 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
             first = not _CHEMOSTAT["steps"]
             _CHEMOSTAT["divided"] = d if first else (_CHEMOSTAT["divided"] + d) // 2
             _CHEMOSTAT["starved"] = starved if first else (_CHEMOSTAT["starved"] + starved) // 2
+            _CHEMOSTAT["last_d"], _CHEMOSTAT["last_s"] = d, starved
             _CHEMOSTAT["steps"] += 1
             _CHEMOSTAT["excess"] = None
             note("divided", d)
@@ -152,7 +153,11 @@ def step(world, n_target: int, genome_size: int, atp: int, timer=None, stats=Non
         # margin: 2 % plus three standard deviations of the step's random division / dilution counts;
         # the estimates are running means (spawned cells divide more in their first step, and a
         # last-step estimate makes the population oscillate around the target)
-        d_est, s_est = _CHEMOSTAT["divided"], _CHEMOSTAT["starved"]
+        # (the cautious side of the running mean and the last step: fewer divisions, more starvation
+        # -- a fresh population's starvation ramps up over its first steps, and a lagging estimate
+        # over-dilutes it into a top-up of thousands of random cells)
+        d_est = min(_CHEMOSTAT["divided"], _CHEMOSTAT["last_d"])
+        s_est = max(_CHEMOSTAT["starved"], _CHEMOSTAT["last_s"])
         margin = n_target // 50 + 3 * int(math.sqrt(d_est + 1))
         keep = n_target + margin - d_est + s_est
         excess = min(n0 - keep, n0)
@@ -216,7 +221,7 @@ def _prime_rare_paths(chem, device, mdt, genome_size: int) -> None:
     w._genomes.collect()
     torch.cuda.synchronize()
     del w
-    _CHEMOSTAT.update(divided=0, starved=0, steps=0, excess=None)
+    _CHEMOSTAT.update(divided=0, starved=0, steps=0, excess=None, last_d=0, last_s=0)
 
 
 def _self_launch(a) -> int | None:
@@ -351,18 +356,21 @@ def main():
     timer = PhaseTimer(device, sync=a.phase_sync) if a.profile_phases else None
     t0 = time.perf_counter()
     stats = {} if a.profile_phases else None
-    per_step = []
+    per_step, per_spawn = [], []
     for _ in range(a.steps):
         t1 = time.perf_counter()
-        step(world, n_target, a.genome_size, atp, timer, stats)
+        st1 = {} if a.step_times and stats is None else stats
+        step(world, n_target, a.genome_size, atp, timer, st1)
         if a.step_times:
             sync()
             per_step.append(round((time.perf_counter() - t1) * 1e3, 3))
+            per_spawn.append(int((st1 or {}).get("spawned", 0)) if stats is None else None)
     sync()
     gc.enable()
     if per_step and rank == 0:
         srt = sorted(per_step)
-        print(json.dumps({"step_ms": per_step, "median_ms": srt[len(srt) // 2], "max_ms": srt[-1]}), file=sys.stderr)
+        print(json.dumps({"step_ms": per_step, "median_ms": srt[len(srt) // 2], "max_ms": srt[-1],
+                          "spawned": per_spawn}), file=sys.stderr)
     if (a.memory_report or a.preset == "hbm") and torch.cuda.is_available() and rank == 0:
         from magicsoup_amd.utils import memory
 

@@ -17,41 +17,72 @@
 
 namespace msd {
 
-// One wavefront per genome j: bytes rows[j, :lens[j]] (row stride L_in) -> a new allocation; cell
-// dst[j] (or n0 + j) gets its offset and length. A full pool sets *failed (the host sized the pool
-// so that it never is; the flag makes a sizing bug loud instead of silent).
-__global__ void __launch_bounds__(64) pool_write_kernel(int k, int L_in, const uint8_t* rows, const int32_t* lens,
-                                                        const int64_t* dst, long long n0, uint8_t* pool, int64_t* off,
-                                                        unsigned long long* top, long long cap, int32_t* out_lens,
-                                                        int* failed) {
-  const int lane = threadIdx.x;
+// Genome j: bytes rows[j, :lens[j]] (row stride L_in) -> a new allocation; cell dst[j] (or n0 + j)
+// gets its offset and length. A workgroup takes kPwChunk genomes at a time: their (pool_alloc-sized)
+// allocations are one atomic on the bump counter -- one per genome serialised ~10k atomics on one
+// address (137 us for a 10.8k-cell top-up spawn) -- and its four waves copy them. A full pool sets
+// *failed (the host sized the pool so that it never is; the flag makes a sizing bug loud).
+constexpr int kPwChunk = 16;
+__global__ void __launch_bounds__(256) pool_write_kernel(int k, int L_in, const uint8_t* rows, const int32_t* lens,
+                                                         const int64_t* dst, long long n0, uint8_t* pool, int64_t* off,
+                                                         unsigned long long* top, long long cap, int32_t* out_lens,
+                                                         int* failed) {
+  __shared__ long long s_off[kPwChunk];
+  __shared__ int s_len[kPwChunk];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool vec = (L_in & 15) == 0 && (reinterpret_cast<uintptr_t>(rows) & 15) == 0;
-  for (int j = blockIdx.x; j < k; j += gridDim.x) {
-    const int L = min(max(lens[j], 0), L_in);
-    long long o = 0;
-    if (lane == 0) o = pool_alloc(top, cap, L);
-    o = (long long)(((unsigned long long)(unsigned)__shfl((int)(o >> 32), 0) << 32) |
-                    (unsigned long long)(unsigned)__shfl((int)(o & 0xFFFFFFFFll), 0));
-    const long long c = dst ? dst[j] : n0 + j;
-    if (o < 0) {
-      if (lane == 0) {
-        if (failed) atomicOr(failed, 1);
-        off[c] = 0;
-        out_lens[c] = 0;
+  for (long long j0 = (long long)blockIdx.x * kPwChunk; j0 < k; j0 += (long long)gridDim.x * kPwChunk) {
+    if (w == 0) {
+      const long long j = j0 + lane;
+      int L = 0, sz = 0;
+      if (lane < kPwChunk && j < k) {
+        L = min(max(lens[j], 0), L_in);
+        sz = ((L > 1 ? L : 1) + 15) & ~15;  // (as pool_alloc: every allocation has its own offset)
       }
-      continue;
+      int incl = sz;  // inclusive prefix over the chunk's lanes
+      for (int o = 1; o < kPwChunk; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+      }
+      const int total = __shfl(incl, kPwChunk - 1);
+      unsigned long long base = 0;
+      if (lane == 0) base = atomicAdd(top, (unsigned long long)total);
+      const unsigned lo = __shfl((unsigned)(base & 0xFFFFFFFFull), 0), hi = __shfl((unsigned)(base >> 32), 0);
+      base = ((unsigned long long)hi << 32) | lo;
+      if (lane < kPwChunk) {
+        s_off[lane] = (long long)(base + (unsigned long long)total) <= cap ? (long long)(base + incl - sz) : -1ll;
+        s_len[lane] = L;
+      }
     }
-    const uint8_t* s = rows + (size_t)j * L_in;
-    uint8_t* d = pool + o;
-    if (vec) {
-      for (int t = lane * 16; t < L; t += 64 * 16) *reinterpret_cast<uint4*>(d + t) = *reinterpret_cast<const uint4*>(s + t);
-    } else {
-      for (int t = lane; t < L; t += 64) d[t] = s[t];
+    __syncthreads();
+    for (int q = w; q < kPwChunk; q += 4) {
+      const long long j = j0 + q;
+      if (j >= k) break;
+      const long long o = s_off[q];
+      const int L = s_len[q];
+      const long long c = dst ? dst[j] : n0 + j;
+      if (o < 0) {
+        if (lane == 0) {
+          if (failed) atomicOr(failed, 1);
+          off[c] = 0;
+          out_lens[c] = 0;
+        }
+        continue;
+      }
+      const uint8_t* src = rows + (size_t)j * L_in;
+      uint8_t* d = pool + o;
+      if (vec) {
+        for (int t = lane * 16; t < L; t += 64 * 16)
+          *reinterpret_cast<uint4*>(d + t) = *reinterpret_cast<const uint4*>(src + t);
+      } else {
+        for (int t = lane; t < L; t += 64) d[t] = src[t];
+      }
+      if (lane == 0) {
+        off[c] = o;
+        out_lens[c] = L;
+      }
     }
-    if (lane == 0) {
-      off[c] = o;
-      out_lens[c] = L;
-    }
+    __syncthreads();  // (the chunk's offsets are read before the next chunk's wave 0 overwrites them)
   }
 }
 
@@ -215,7 +246,8 @@ void pool_write(int k, int L_in, uintptr_t rows, uintptr_t lens, uintptr_t dst, 
                 uintptr_t off, uintptr_t top, long long cap, uintptr_t out_lens, uintptr_t failed, uintptr_t stream) {
   if (k <= 0) return;
   if (L_in < 0) throw std::invalid_argument("pool_write: negative row width");
-  pool_write_kernel<<<grid_for(k), 64, 0, S_(stream)>>>(k, L_in, P_<uint8_t>(rows), P_<int32_t>(lens),
+  const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(((long long)k + kPwChunk - 1) / kPwChunk, 4096));
+  pool_write_kernel<<<grid, 256, 0, S_(stream)>>>(k, L_in, P_<uint8_t>(rows), P_<int32_t>(lens),
                                                         dst ? P_<int64_t>(dst) : nullptr, n0, P_<uint8_t>(pool),
                                                         P_<int64_t>(off), P_<unsigned long long>(top), cap,
                                                         P_<int32_t>(out_lens), failed ? P_<int>(failed) : nullptr);

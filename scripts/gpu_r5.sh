@@ -101,6 +101,12 @@ for s in "$@"; do case "$s" in
   wide) run wide 300 python bench.py --preset wide ;;
   c1024) run c1024 300 python bench.py --preset c1024 --steps 30 --warmup 5 ;;
   c256) run c256_40k 300 python bench.py --map-size 256 --cells 40000 ;;
+  tdrv) trace tdrv 19 --steps 20 --warmup 5 ;;
+  hsdrv) MS_NATIVE_TIMES=1 MS_PY_TIMES=1 run host_split_drv 300 python scripts/host_split.py 4096 50000 20 5 ;;
+  drvst) run drv_step_times 300 python bench.py --steps 20 --warmup 5 --step-times ;;
+  rsab) for i in 1 2 3; do for t in 1 0; do MS_BENCH_RESERVE=$t run rsab_${t}_$i 300 python bench.py --steps 20 --warmup 5 --step-times; done; done ;;
+  drvst3) for i in 1 2 3; do run drv_step_times_$i 300 python bench.py --steps 20 --warmup 5 --step-times; done; run flag_step_times 300 python bench.py --step-times ;;
+  poolt) run tests_pool 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -x -k "pool or spawn or arena or genome" --timeout 300 --timeout-method thread || exit 1 ;;
   tflag) trace tflag 19 --steps 20 --warmup 20 ;;
   tnodefer) MS_DEFER_GENOME_OPS=0 trace tnodefer 19 --steps 20 --warmup 20 ;;
   tc256) trace tc256 19 --map-size 256 --cells 40000 --steps 20 --warmup 20 ;;

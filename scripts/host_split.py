@@ -23,6 +23,7 @@ from magicsoup_amd.ops import hip_ops  # noqa: E402
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 1448
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 6250
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 60
+warm = int(sys.argv[4]) if len(sys.argv) > 4 else 20
 
 OPS = ["spawn_cells", "enzymatic_activity", "kill_divide_where", "kill_divide_t", "kill_cells", "divide_cells_t", "recombinate_cells", "mutate_cells",
        "degrade_molecules", "diffuse_molecules", "increment_cell_lifetimes"]
@@ -159,7 +160,7 @@ for name in OPS:
             setattr(c, name, op(c.__dict__[name], name))
 w.spawn_cells(bench.random_genomes(N, 500, "cuda"))
 atp = CHEMISTRY.molname_2_idx["ATP"]
-for _ in range(20):
+for _ in range(warm):
     bench.step(w, N, 500, atp)
 torch.cuda.synchronize()
 for d in (busy, blocked, calls, native_t, native_n, py_t, py_n):

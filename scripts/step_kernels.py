@@ -28,8 +28,12 @@ walls = []
 for j in range(len(marks) - nst, len(marks)):
     walls.append((int(rows[marks[j]]["End_Timestamp"]) - int(rows[marks[j - 1]]["End_Timestamp"]), j))
 med = sorted(walls)[len(walls) // 2]
+if os.environ.get("STEP") == "max":  # list the slowest step instead
+    med = max(walls)
+elif os.environ.get("STEP", "").lstrip("-").isdigit():  # or the k-th timed step (0: the first)
+    med = walls[int(os.environ["STEP"])]
 print(f"step walls (us): median {statistics.median(w for w, _ in walls) / 1e3:.1f}, "
-      f"min {min(walls)[0] / 1e3:.1f}, max {max(walls)[0] / 1e3:.1f}; listing the median step")
+      f"min {min(walls)[0] / 1e3:.1f}, max {max(walls)[0] / 1e3:.1f}; listing the {os.environ.get('STEP', 'median')} step")
 j = med[1]
 one = rows[marks[j - 1] + 1 : marks[j] + 1]
 base = int(rows[marks[j - 1]]["End_Timestamp"])
