@@ -58,10 +58,13 @@ _COUNT_SAFE_OPS = frozenset({"mutate_cells", "recombinate_cells", "degrade_molec
 _CHECK_ENV = os.environ.get("MS_CHECK_INVARIANTS") == "1"
 _DEFER_ENV = os.environ.get("MS_DEFER_GENOME_OPS", "1")
 # issue a queued recombinate + mutate pair on a pending kill_divide's device count (World._chain_bound)
-# instead of waiting for the count on the host first. Off by default: in-process A/B over 400 steps
-# (scripts/knob_ab.py, profiles/r5/devcount/) the bound-sized chain was 3-4 % slower on the flagship
-# (later, grown-genome steps) and on 256^2 / 40k; over the driver's early steps it is a tie.
-_CHAIN_BOUND = os.environ.get("MS_CHAIN_BOUND", "0") == "1"
+# instead of waiting for the count on the host first: always (MS_CHAIN_BOUND=1), never (0), or by
+# default for populations up to _CHAIN_BOUND_MAX cells. Small populations are host-bound and gain
+# (1024^2 / 10k: +17 %); at 40-50k cells the bound-sized chain was 3-4 % slower in in-process A/Bs
+# over 400 steps (scripts/knob_ab.py, profiles/r5/devcount/).
+_CHAIN_BOUND_ENV = os.environ.get("MS_CHAIN_BOUND", "auto")
+_CHAIN_BOUND = _CHAIN_BOUND_ENV != "0"
+_CHAIN_BOUND_MAX = 1 << 30 if _CHAIN_BOUND_ENV == "1" else 16384
 # The genome chains flushed onto the side stream (World._flush_deferred) are joined into the compute
 # stream at the next op that needs their results (the activity, or a read of genomes / parameters),
 # not right after the flush: the molecule-only work in between (the lifetimes, the loop's masks)
@@ -360,6 +363,8 @@ class World:
         d = self.__dict__
         pend = d["_count_pending"]
         if not _CHAIN_BOUND or len(pend) < 4 or not isinstance(pend[1], tuple) or len(q) != 2:
+            return None
+        if int(pend[0]) > _CHAIN_BOUND_MAX:
             return None
         if getattr(q[0], "kind", None) != "rec" or getattr(q[1], "kind", None) != "mut":
             return None

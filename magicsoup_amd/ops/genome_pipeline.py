@@ -429,10 +429,13 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
             BOUND_DECLINED["pool"] += 1
             return False
     if fresh:
-        # (on the synchronous path with room for the next call as well: chains issued on a device
-        # count cannot recycle rows, World._chain_bound)
+        # (with chains issued on a device count enabled, the synchronous path reserves room for the
+        # next call as well: those cannot recycle rows, World._chain_bound)
+        from magicsoup_amd.models import world as world_mod
+
+        room_next = bound is None and world_mod._CHAIN_BOUND and n <= world_mod._CHAIN_BOUND_MAX
         kin._reserve_rows(2 * min(n, N_CAP) + narr, sync=bound is None,
-                          headroom=2 * N_CAP if bound is None else 0)
+                          headroom=2 * min(2 * n, N_CAP) if room_next else 0)
     _room(world, room)
     br, bm, bu = _bufs(world, "rec"), _bufs(world, "mut"), _bufs(world, "evo")
     ar, am, au = _arena_desc(world, br), _arena_desc(world, bm), _arena_desc(world, bu)

@@ -107,6 +107,13 @@ for s in "$@"; do case "$s" in
   rsab) for i in 1 2 3; do for t in 1 0; do MS_BENCH_RESERVE=$t run rsab_${t}_$i 300 python bench.py --steps 20 --warmup 5 --step-times; done; done ;;
   drvst3) for i in 1 2 3; do run drv_step_times_$i 300 python bench.py --steps 20 --warmup 5 --step-times; done; run flag_step_times 300 python bench.py --step-times ;;
   poolt) run tests_pool 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -x -k "pool or spawn or arena or genome" --timeout 300 --timeout-method thread || exit 1 ;;
+  smallab) for i in 1 2; do run c1024_$i 300 python bench.py --preset c1024 --steps 30 --warmup 5; run c256_$i 300 python bench.py --map-size 256 --cells 40000; done ;;
+  c1024ab) run c1024_base 300 python bench.py --preset c1024 --steps 30 --warmup 5
+     MS_SELECT_SINGLE=0 run c1024_sel0 300 python bench.py --preset c1024 --steps 30 --warmup 5
+     MS_PLACE_TAIL=0 run c1024_tail0 300 python bench.py --preset c1024 --steps 30 --warmup 5
+     MS_CHAIN_BOUND=1 run c1024_cb1 300 python bench.py --preset c1024 --steps 30 --warmup 5
+     run c1024_base2 300 python bench.py --preset c1024 --steps 30 --warmup 5 ;;
+  smallab2) for i in 1 2; do run c1024_$i 300 python bench.py --preset c1024 --steps 30 --warmup 5; run c256_$i 300 python bench.py --map-size 256 --cells 40000; run proxy_$i 300 python bench.py --map-size 1448 --cells 6250; done ;;
   tflag) trace tflag 19 --steps 20 --warmup 20 ;;
   tnodefer) MS_DEFER_GENOME_OPS=0 trace tnodefer 19 --steps 20 --warmup 20 ;;
   tc256) trace tc256 19 --map-size 256 --cells 40000 --steps 20 --warmup 20 ;;
