@@ -284,6 +284,34 @@ void fast_dist_divide_a(const FastWorld& f, int n, uintptr_t mask, uintptr_t com
                                 20 * sizeof(int32_t), hipMemcpyDeviceToHost, S_(stream)));
 }
 
+// The strip's kill / replicate step up to the division's one synchronisation, with no wait for the
+// kill's survivor count: threshold masks + the killed cells' spill (one launch), the survivors
+// selected with the division mask compacted alongside (zeros past the survivor count), every
+// per-cell buffer compacted, then phase A over all n rows -- rows past the survivors carry a zero
+// mask, so they take no part in the marks (the occupancy marks come from the cell map), the
+// placement or the split. Indices, draws and order are those of the eager kill followed by phase A
+// over the survivors. Returns the pinned status slot of the survivor count; phase B then runs with
+// n0 = that count and kk = n (the par3 / npos3 offsets).
+int fast_dist_kill_divide_a(const FastWorld& f, int n, int mol, float kill_below, float divide_above, float cost,
+                            float kill_p, uint64_t mseed, uint64_t mcall, uintptr_t kill, uintptr_t divide,
+                            uintptr_t map, int mdt, uintptr_t corr, uintptr_t comm, int up, int down, uint64_t seed,
+                            uint64_t call, uintptr_t marks, uintptr_t par3, uintptr_t npos3, uintptr_t st, int lw,
+                            int gw, uintptr_t host_st, uintptr_t stream) {
+  if (!f.ready) throw std::invalid_argument("fast_dist_kill_divide_a: descriptor not finalized");
+  if (n <= 0 || n > f.cap) throw std::invalid_argument("fast_dist_kill_divide_a: cell count outside the capacity");
+  if (mol < 0 || mol >= f.m) throw std::invalid_argument("fast_dist_kill_divide_a: molecule index");
+  if (!f.dmask) throw std::invalid_argument("fast_dist_kill_divide_a: no mask scratch");
+  hipStream_t s = S_(stream);
+  threshold_spill(n, f.m, mol, kill_below, divide_above, cost, kill_p, mseed, mcall, f.mols, kill, divide, f.pos, f.R,
+                  f.C, map, f.cell_map, mdt, corr, stream);
+  const int slot = select_indices_async_pay(n, 1 /* clear */, kill, f.sel, 0, f.dcount, divide, f.dmask, stream);
+  const int* dn = P_<int>(f.dcount);
+  launch_row_args(f.fwd, n, dn, P_<int64_t>(f.sel), nullptr, 0, s);
+  launch_row_args(f.back, n, dn, nullptr, nullptr, 0, s);
+  fast_dist_divide_a(f, n, f.dmask, comm, up, down, seed, call, marks, par3, npos3, st, lw, gw, host_st, stream);
+  return slot;
+}
+
 // Phase B (after the synchronisation, counts known): child records of the exporting parents packed
 // and exchanged, local children committed as rows n0.. (positions, halved molecules, divisions,
 // lifetimes; exporters halved too) with their genome / label / parameter-row entries cloned, the
@@ -374,6 +402,8 @@ void bind_fast(pybind11::module_& m) {
         "kill_cells(kill) + divide_cells(divide & survivors) in one call (status slots of both counts)");
   m.def("fast_dist_divide_a", &fast_dist_divide_a, "strip divide protocol up to the synchronisation");
   m.def("fast_dist_divide_b", &fast_dist_divide_b, "strip divide protocol after the synchronisation");
+  m.def("fast_dist_kill_divide_a", &fast_dist_kill_divide_a,
+        "strip kill / replicate step up to the division's synchronisation (status slot of the survivor count)");
 }
 
 }  // namespace msd

@@ -1094,6 +1094,9 @@ class World:
         if kill_mask.numel() != n or divide_mask.numel() != n:
             raise ValueError(f"kill_divide_t: masks of {kill_mask.numel()} / {divide_mask.numel()} cells for {n}")
         if n == 0:
+            if getattr(self, "_exchange_map_halo", None) is not None:  # (collective: see below)
+                self.__dict__["last_kill"] = (0, 0)
+                self.divide_cells_t(torch.zeros(0, dtype=torch.long, device=self.device))
             return
         if not kill_mask.is_cuda or getattr(self, "_exchange_map_halo", None) is not None:
             # CPU worlds, and a decomposed world's strips (their division is a collective protocol):
@@ -1103,6 +1106,9 @@ class World:
             self.__dict__["last_kill"] = (n, self.n_cells)
             if self.n_cells > 0:
                 self.divide_cells_t(div, lazy=kill_mask.is_cuda)
+            elif getattr(self, "_exchange_map_halo", None) is not None:
+                # (the strip division is collective: an emptied strip still takes part)
+                self.divide_cells_t(torch.zeros(0, dtype=torch.long, device=self.device))
             return
         from magicsoup_amd.ops import hip_ops
         from magicsoup_amd.ops.streams import NEvent
@@ -1131,9 +1137,16 @@ class World:
         if not 0 <= mol < self.n_molecules:
             raise ValueError(f"kill_divide_where: molecule index {mol} out of range")
         n = self.n_cells
+        strip = getattr(self, "_exchange_map_halo", None) is not None
         if n == 0:
+            if strip:  # (the strip division is collective: an empty strip still takes part)
+                self.__dict__["last_kill"] = (0, 0)
+                self.divide_cells_t(torch.zeros(0, dtype=torch.long, device=self.device))
             return
-        if self._genomes.data.is_cuda and getattr(self, "_exchange_map_halo", None) is not None:
+        if self._genomes.data.is_cuda and strip:
+            native = getattr(self, "_kill_divide_native", None)
+            if native is not None and native(n, mol, kill_below, divide_above, divide_cost, kill_fraction):
+                return
             # a decomposed world's strip: native masks and kill (its one synchronisation), the
             # division mask compacted with the survivors on the device, then the strip's lazy
             # division protocol
@@ -1158,6 +1171,8 @@ class World:
                 fw = self._fast_world(n_after)  # (the kill's survivor indices are in this descriptor's sel)
                 m_.fast_compact_mask(fw, n, bufs["dvmask"].data_ptr(), bufs["dvmask2"].data_ptr(), hip_ops._stream())
                 self.divide_cells_t(bufs["dvmask2"][:n_after].view(torch.bool), lazy=True)
+            else:
+                self.divide_cells_t(torch.zeros(0, dtype=torch.long, device=self.device))
             return
         if not self._genomes.data.is_cuda:
             a = self.cell_molecules[:, mol]

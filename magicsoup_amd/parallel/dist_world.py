@@ -97,6 +97,9 @@ def _copy_maps(dst: World, src: World) -> None:
 _XB_EARLY = os.environ.get("MS_XB_EARLY", "1") != "0"
 # a lazy division's arrivals are built by the queued genome chain that follows (_divide_phase_b)
 _ARRIVALS_MERGE = True
+# the strip's kill / replicate step without a wait for the kill's survivor count (MS_STRIP_LAZY_KILL=0:
+# the eager kill, then the lazy division)
+_LAZY_KILL = os.environ.get("MS_STRIP_LAZY_KILL", "1") != "0"
 
 
 class DistributedWorld(World):
@@ -582,7 +585,53 @@ class DistributedWorld(World):
         hip_ops.guarded_sync()  # (peer failures raise instead of hanging the read-back)
         return self._divide_phase_b(n0, lw, gw)
 
-    def _divide_phase_b(self, n0: int, lw: int, gw: int, defer_arrivals: bool = False
+    def _kill_divide_native(self, n: int, mol: int, kill_below: float, divide_above: float, divide_cost: float,
+                            kill_fraction: float) -> bool:
+        """World.kill_divide_where on a strip whose exchanges go over RCCL, without waiting for the
+        kill's survivor count (csrc/hip/fast.hip fast_dist_kill_divide_a): masks, payment, spill,
+        the survivors' compaction and phase A of the division protocol over all ``n`` rows (rows past
+        the survivors have a zero division mask) are one native call. The survivor count reaches the
+        host with phase A's counts, at the one read-back of :meth:`_resolve_count`; ``last_kill`` is
+        set there. Same draws, placement and rows as the eager kill followed by the lazy division
+        (``MS_STRIP_LAZY_KILL=0``). Returns False when the eager path must run."""
+        if not (_LAZY_KILL and self._strips and self._rccl_native()):
+            return False
+        from magicsoup_amd.ops import hip_ops
+        from magicsoup_amd.ops.hip_ops import _m, _p, _scratch, _stream
+        from magicsoup_amd.ops.streams import NEvent
+
+        comm = self.__dict__["_comm"]
+        dev = self._tensor_device()
+        C = self.map_size
+        lw, gw = int(self._labels.width), int(self._genomes.width)
+        fw = self._fast_world(n)
+        bufs = self.__dict__["_fw_bufs"]
+        cap = int(bufs["sel"].numel())
+        if bufs.get("kmask") is None or bufs["kmask"].numel() < cap:
+            bufs["kmask"] = torch.empty(cap, dtype=torch.uint8, device=dev)
+            bufs["dvmask"] = torch.empty_like(bufs["kmask"])
+            bufs["dvmask2"] = torch.empty_like(bufs["kmask"])
+        mm, corr = hip_ops.map_for_pixels(self)
+        sc = _scratch(self)
+        mk = sc.get("dv_marks", 4 * C, _U8, dev)
+        par = sc.get("dv_par", 3 * n, torch.int64, dev)
+        npos = sc.get("dv_npos", 6 * n, torch.int32, dev)
+        st = sc.get("dv_status", 20, torch.int32, dev)
+        host_st = self.__dict__.get("_dv_host_st")
+        if host_st is None:
+            host_st = self.__dict__["_dv_host_st"] = torch.zeros(20, dtype=torch.int32, pin_memory=True)
+        # (the same draws in the same order as the eager path: the dilution's, then the placement's)
+        mseed, mcall = hip_ops._rng() if kill_fraction > 0.0 else (0, 0)
+        seed, call = hip_ops._rng()
+        slot = _m().fast_dist_kill_divide_a(
+            fw, n, mol, float(kill_below), float(divide_above), float(divide_cost), float(kill_fraction),
+            mseed ^ 0x6A09E667F3BCC909, mcall, bufs["kmask"].data_ptr(), bufs["dvmask"].data_ptr(), mm.data_ptr(),
+            hip_ops._mdt(mm), hip_ops._p(corr), comm.handle, comm.up, comm.down, seed, call, _p(mk), _p(par),
+            _p(npos), _p(st), lw, gw, host_st.data_ptr(), _stream())
+        self.__dict__["_count_pending"] = (n, None, NEvent().record(), "strip", lw, gw, int(slot))
+        return True
+
+    def _divide_phase_b(self, n0: int, lw: int, gw: int, defer_arrivals: bool = False, kk: int | None = None
                         ) -> tuple[torch.Tensor, torch.Tensor]:
         """Phase B of :meth:`_divide_mask_native` once phase A's counts are on the host (its pinned
         status copy is complete): records out, children in, arrivals appended and their parameter
@@ -596,8 +645,10 @@ class DistributedWorld(World):
         dev = self._tensor_device()
         m = self.n_molecules
         sc = _scratch(self)
-        par = sc.get("dv_par", 3 * n0, torch.int64, dev)
-        npos = sc.get("dv_npos", 6 * n0, torch.int32, dev)
+        # kk: the row count phase A ran over (the cells before a lazy kill; par / npos offsets)
+        kk = n0 if kk is None else int(kk)
+        par = sc.get("dv_par", 3 * kk, torch.int64, dev)
+        npos = sc.get("dv_npos", 6 * kk, torch.int32, dev)
         v = self.__dict__["_dv_host_st"].tolist()  # local winner counts + the neighbours' headers
         hip_ops.check_placement()
         n_loc, n_up, n_dn = v[0], v[1], v[2]
@@ -620,7 +671,7 @@ class DistributedWorld(World):
             self._genomes.top_ub += need
         fw = self._fast_world(n_new)
         zero_row = self.kinetics._zero_row()
-        _m().fast_dist_divide_b(fw, n0, comm.handle, comm.up, comm.down, _p(par), _p(npos), n0, n_loc, n_up, n_dn, lw,
+        _m().fast_dist_divide_b(fw, n0, comm.handle, comm.up, comm.down, _p(par), _p(npos), kk, n_loc, n_up, n_dn, lw,
                                 gw, _p(out), _p(inb), hdr_up[0], hdr_up[1], hdr_up[2], hdr_dn[0], hdr_dn[1],
                                 hdr_dn[2], _p(zero_row), _stream())
         self._adopt_count(n_new)
@@ -634,7 +685,7 @@ class DistributedWorld(World):
         mig = self.migrated
         mig["divided_out"] += n_up + n_dn
         mig["divided_in"] += k_in
-        self.__dict__["_xfer"] = (par[n0 : n0 + n_up], par[2 * n0 : 2 * n0 + n_dn], int(hdr_up[0]), int(hdr_dn[0]))
+        self.__dict__["_xfer"] = (par[kk : kk + n_up], par[2 * kk : 2 * kk + n_dn], int(hdr_up[0]), int(hdr_dn[0]))
         return par[:n_loc], torch.arange(n0, n0 + n_loc, device=self.device)
 
     def _resolve_count(self) -> None:
@@ -648,10 +699,17 @@ class DistributedWorld(World):
             return super()._resolve_count()
         from magicsoup_amd.ops import hip_ops
 
-        n0, _, ev, _, lw, gw = pend
+        n0, _, ev, _, lw, gw = pend[:6]
         hip_ops.guarded_sync(ev)
         # (the entry stays until the counts are read: a failure above leaves it for a retry)
         d["_count_pending"] = None
+        kk = n0
+        if len(pend) > 6:  # a lazy kill before phase A (_kill_divide_native): its survivors first
+            n_k = int(hip_ops._m().status_read(pend[6])[0])
+            d["last_kill"] = (n0, n_k)
+            if n_k != n0:
+                self._adopt_count(n_k)
+            n0 = n_k
         # the genome ops queued since the division stay queued during phase B: its parameter
         # rebuild of the arrivals reconciles the world (Kinetics._sync), which would otherwise issue
         # them against the state before phase B
@@ -660,7 +718,7 @@ class DistributedWorld(World):
         pair = (_ARRIVALS_MERGE and queued is not None and len(queued) >= 2 and getattr(queued[0], "kind", None) == "rec"
                 and getattr(queued[1], "kind", None) == "mut")
         try:
-            self._divide_phase_b(n0, lw, gw, defer_arrivals=pair)
+            self._divide_phase_b(n0, lw, gw, defer_arrivals=pair, kk=kk)
         finally:
             if queued:
                 from magicsoup_amd.ops.streams import NEvent

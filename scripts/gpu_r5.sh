@@ -50,6 +50,8 @@ for s in "$@"; do case "$s" in
   ssab) for i in 1 2; do for t in 1 0; do MS_SELECT_SINGLE=$t run ssab_${t}_$i 300 python bench.py; done; done ;;
   rthin) for i in 1 2; do for t in 1 0; do MS_REC_THIN=$t run rthin_${t}_$i 300 python bench.py; done; done ;;
   tmem) run tests_mem 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -k "memory_model or past_2_31" --timeout 300 --timeout-method thread ;;
+  hipt) echo "== hipt $(date +%T)"; MS_VIRTUAL_STRIPS=1 timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --stats -d $O/hipt_virt -o run --output-format csv -- python bench.py --map-size 1448 --cells 6250 > $O/hipt_virt.log 2>&1; rc=$?; echo "   rc=$rc"; if fatal $rc; then exit $rc; fi ;;
+  hiptp) echo "== hiptp $(date +%T)"; timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --stats -d $O/hipt_plain -o run --output-format csv -- python bench.py --map-size 1448 --cells 6250 > $O/hipt_plain.log 2>&1; rc=$?; echo "   rc=$rc"; if fatal $rc; then exit $rc; fi ;;
   tests) run tests 1000 python -u -m pytest tests -m gpu -q --maxfail 5 --timeout 120 --timeout-method thread ;;
   smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   flagship) run flagship 300 python bench.py ;;

@@ -489,16 +489,23 @@ def _body_strip_kill_divide_where(rank, ws):
     w = ms.World(chemistry=_chem(), map_size=64, seed=41, device="cpu")
     w.spawn_cells(gen_genomes(1200, 300))
     atp = _chem().molname_2_idx["ATP"]
-    out = {}
-    for fused in (False, True):
+    from magicsoup_amd.parallel import dist_world
+
+    out, kills = {}, {}
+    lazy0 = dist_world._LAZY_KILL
+    # masks: torch masks + kill_cells + lazy divide; eager: native masks, the kill's read-back, lazy
+    # divide; lazy: kill and phase A in one call, the survivor count read with phase A's counts
+    # (*_f: with a chemostat dilution, whose draws the torch masks cannot reproduce)
+    for fused in ("masks", "eager", "lazy", "eager_f", "lazy_f"):
+        dist_world._LAZY_KILL = fused.startswith("lazy")
         dw = DistributedWorld(chemistry=_chem(), map_size=64, seed=42, device="cuda", strips=True)
         dw.adopt_maps(w)
         dw.scatter_from(w, maps=False)
         ms.set_seed(43)
         for it in range(3):
             dw.enzymatic_activity()
-            if fused:
-                dw.kill_divide_where(atp, 0.5, 2.0, 1.0)
+            if fused != "masks":
+                dw.kill_divide_where(atp, 0.5, 2.0, 1.0, kill_fraction=0.2 if fused.endswith("_f") else 0.0)
             else:
                 a = dw.cell_molecules[:, atp]
                 kill = a < 0.5
@@ -509,12 +516,21 @@ def _body_strip_kill_divide_where(rank, ws):
             dw.degrade_molecules()
             dw.diffuse_molecules()
             dw.increment_cell_lifetimes()
+            if fused != "masks":  # (the diffusion completed the lazy division: the counts are in)
+                kills.setdefault(fused, []).append(tuple(dw.last_kill))
         dw.synchronize()
         dw.check_invariants("strip kill_divide_where")
         out[fused] = (dw.cell_positions.cpu(), dw.cell_molecules.cpu(), dw.cell_divisions.cpu(), list(dw.cell_genomes))
         dw.close()
-    a, b = out[False], out[True]
+    dist_world._LAZY_KILL = lazy0
+    a = out["masks"]
+    for k in ("eager", "lazy"):
+        b = out[k]
+        assert all(torch.equal(x, y) for x, y in zip(a[:3], b[:3])) and a[3] == b[3], k
+    assert kills["eager"] == kills["lazy"] and kills["eager_f"] == kills["lazy_f"]
+    a, b = out["eager_f"], out["lazy_f"]
     assert all(torch.equal(x, y) for x, y in zip(a[:3], b[:3])) and a[3] == b[3]
+    assert kills["lazy_f"][0][1] < kills["lazy"][0][1]  # (the dilution killed cells)
 
 
 def test_strip_kill_divide_where_matches_masks():
