@@ -419,6 +419,40 @@ def test_distributed_rank_without_cells_joins_integrator_collectives():
     run_ranks(_body_empty_rank, 2, timeout=120.0)
 
 
+def _body_empty_rank_kill_divide(rank, ws):
+    # the strip division is collective: a rank whose strip is (or becomes) empty still joins the
+    # kill / replicate step's division exchanges, or its neighbour would wait for it forever
+    g = _global_world(map_size=16, n=0)
+    from tests.conftest import gen_genomes
+
+    genomes = gen_genomes(20, 300)
+    pos = torch.tensor([[i // 8, 2 * (i % 8)] for i in range(20)], dtype=torch.int32)
+    g._grow(20)
+    g._genomes.append_strings(genomes)
+    g._labels.append_strings([f"c{i}" for i in range(20)])
+    g._place(torch.arange(20), pos)
+    g._update_params_rows(torch.arange(20))
+    dw = _dworld(16)
+    dw.scatter_from(g)
+    assert dw.n_cells == (20 if rank == 0 else 0)
+    atp = _chem().molname_2_idx["ATP"]
+    dw.cell_molecules[:, atp] = 10.0
+    dw.kill_divide_where(atp, 1.0, 5.0, 4.0)  # rank 0 divides, rank 1 is empty
+    assert dw.last_kill == ((20, 20) if rank == 0 else (0, 0))
+    n1 = dw.n_cells
+    assert n1 >= (21 if rank == 0 else 0)
+    # everything dies on rank 0 (its strip empties), rank 1 got nothing or the arrivals
+    kill = torch.ones(n1, dtype=torch.bool) if rank == 0 else torch.zeros(n1, dtype=torch.bool)
+    dw.kill_divide_t(kill, torch.zeros(n1, dtype=torch.bool))
+    assert dw.n_cells == (0 if rank == 0 else n1)
+    dw.kill_divide_where(atp, 1.0, 5.0, 4.0)
+    _check_local(dw)
+
+
+def test_distributed_empty_strip_joins_kill_divide():
+    run_ranks(_body_empty_rank_kill_divide, 2, timeout=120.0)
+
+
 def _body_virtual_strips(rank, ws):
     """One rank running the strip code path (its own up / down neighbour): the halo rows are copies
     of its own boundary rows, i.e. the torus wrap, so physics match a plain World and the lifecycle
