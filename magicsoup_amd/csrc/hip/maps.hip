@@ -221,8 +221,14 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) r.v[j] = col ? r.v[j] : 0u;
-    r.el = ld_bits(src + base + (need_l ? yl : yc));
-    r.er = ld_bits(src + base + (need_r ? yr : yc));
+    if constexpr (FULL) {
+      // every strip is whole: only lane 0 needs a left and only lane 63 a right edge value, so
+      // one edge load per row serves both (a third fewer load instructions per row)
+      r.el = ld_bits(src + base + (need_l ? yl : (need_r ? yr : yc)));
+    } else {
+      r.el = ld_bits(src + base + (need_l ? yl : yc));
+      r.er = ld_bits(src + base + (need_r ? yr : yc));
+    }
   };
   // scaled values of the row plus the left neighbour of column y0 and the right one of y0 + 3
   auto finish = [&](const Raw& r, float v[4], float& L, float& Rn) {
@@ -230,7 +236,8 @@ __global__ void __launch_bounds__(256) diffuse_stencil4_kernel(const T* __restri
     for (int j = 0; j < 4; ++j) v[j] = corr_in(from_bits<T>(r.v[j]), corr, mol) * sc;
     const float up = __shfl_up(v[3], 1), dn = __shfl_down(v[0], 1);
     // (both edge values computed by every lane and selected: no branch, see band_loop)
-    const float el = corr_in(from_bits<T>(r.el), corr, mol) * sc, er = corr_in(from_bits<T>(r.er), corr, mol) * sc;
+    const float el = corr_in(from_bits<T>(r.el), corr, mol) * sc;
+    const float er = FULL ? el : corr_in(from_bits<T>(r.er), corr, mol) * sc;
     L = need_l ? el : up;
     Rn = need_r ? er : dn;
   };
@@ -352,8 +359,12 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
         r.v.q[i].z = col ? r.v.q[i].z : 0u;
         r.v.q[i].w = col ? r.v.q[i].w : 0u;
       }
-      r.el = ld_bits(src + base + (need_l ? yl : yc));
-      r.er = ld_bits(src + base + (need_r ? yr : yc));
+      if constexpr (FULL) {  // (one edge load per row, see diffuse_stencil4_kernel)
+        r.el = ld_bits(src + base + (need_l ? yl : (need_r ? yr : yc)));
+      } else {
+        r.el = ld_bits(src + base + (need_l ? yl : yc));
+        r.er = ld_bits(src + base + (need_r ? yr : yc));
+      }
     };
     auto cin = [&](float raw) { return (has_c ? fmaxf(raw + cm, 0.0f) : raw) * sc; };
     auto finish = [&](const Raw& r, float v[8], float& L, float& Rn) {
@@ -361,7 +372,7 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = cin(v[j]);
       const float up = __shfl_up(v[7], 1), dn = __shfl_down(v[0], 1);
-      const float el = cin(from_bits<T>(r.el)), er = cin(from_bits<T>(r.er));  // (selected: no branch)
+      const float el = cin(from_bits<T>(r.el)), er = FULL ? el : cin(from_bits<T>(r.er));  // (selected: no branch)
       L = need_l ? el : up;
       Rn = need_r ? er : dn;
     };
