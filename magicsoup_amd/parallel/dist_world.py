@@ -100,6 +100,13 @@ _ARRIVALS_MERGE = True
 # the strip's kill / replicate step without a wait for the kill's survivor count (MS_STRIP_LAZY_KILL=0:
 # the eager kill, then the lazy division)
 _LAZY_KILL = os.environ.get("MS_STRIP_LAZY_KILL", "1") != "0"
+# a lazy strip division's phase B after the diffusion stencil, on the side stream (MS_EARLY_STENCIL=0:
+# phase B, then the stencil, on the compute stream), for strips of up to MS_EARLY_STENCIL_MAX_PX owned
+# pixels: a 1448^2 strip (an 8-GPU rank's share of the flagship) gains ~12 %; on a 4096^2 strip the
+# side stream's phase B + boundary recombination + chain outlast the stencil and the chain lands
+# before the next activity instead of next to the stencil (no gain, profiles/r5/early_stencil/)
+_EARLY_STENCIL = os.environ.get("MS_EARLY_STENCIL", "1") != "0"
+_EARLY_STENCIL_MAX_PX = int(os.environ.get("MS_EARLY_STENCIL_MAX_PX", str(4 << 20)))
 
 
 class DistributedWorld(World):
@@ -631,8 +638,9 @@ class DistributedWorld(World):
         self.__dict__["_count_pending"] = (n, None, NEvent().record(), "strip", lw, gw, int(slot))
         return True
 
-    def _divide_phase_b(self, n0: int, lw: int, gw: int, defer_arrivals: bool = False, kk: int | None = None
-                        ) -> tuple[torch.Tensor, torch.Tensor]:
+    def _divide_phase_b(self, n0: int, lw: int, gw: int, defer_arrivals: bool = False, kk: int | None = None,
+                        pairs: bool = True, stencil_first=None, _prepared: bool = False
+                        ) -> tuple[torch.Tensor, torch.Tensor] | None:
         """Phase B of :meth:`_divide_mask_native` once phase A's counts are on the host (its pinned
         status copy is complete): records out, children in, arrivals appended and their parameter
         rows rebuilt on the device -- or, with ``defer_arrivals`` (a queued recombinate_cells() +
@@ -660,7 +668,7 @@ class DistributedWorld(World):
             m, hdr_dn[1], hdr_dn[2])
         inb = sc.get("dv_in", max(1, b_in), _U8, dev)
         n_new = n0 + n_loc + k_in
-        if k_in:
+        if k_in and not _prepared:
             for arena, wi in ((self._genomes, 2), (self._labels, 1)):
                 w = max(int(hdr_up[wi]), int(hdr_dn[wi]), 1)
                 if w > arena.width:
@@ -671,6 +679,24 @@ class DistributedWorld(World):
             self._genomes.top_ub += need
         fw = self._fast_world(n_new)
         zero_row = self.kinetics._zero_row()
+        if stencil_first is not None:
+            # the diffusion stencil first (it reads and writes only the molecule map, which phase B
+            # does not touch: every capacity change above is done), then phase B on the side stream
+            # over the side communicator, next to the stencil (see _diffuse_early)
+            from magicsoup_amd.ops import world_ops
+            from magicsoup_amd.ops.streams import NEvent, on_stream
+
+            before = NEvent().record()
+            world_ops.diffuse(self)
+            side = stencil_first
+            before.wait(side.cuda_stream)
+            self.__dict__["_side_active"] = True
+            try:
+                with on_stream(side):
+                    return self._divide_phase_b(n0, lw, gw, defer_arrivals, kk, pairs, _prepared=True)
+            finally:
+                self.__dict__["_side_active"] = False
+        comm = self._active_comm()
         _m().fast_dist_divide_b(fw, n0, comm.handle, comm.up, comm.down, _p(par), _p(npos), kk, n_loc, n_up, n_dn, lw,
                                 gw, _p(out), _p(inb), hdr_up[0], hdr_up[1], hdr_up[2], hdr_dn[0], hdr_dn[1],
                                 hdr_dn[2], _p(zero_row), _stream())
@@ -686,13 +712,16 @@ class DistributedWorld(World):
         mig["divided_out"] += n_up + n_dn
         mig["divided_in"] += k_in
         self.__dict__["_xfer"] = (par[kk : kk + n_up], par[2 * kk : 2 * kk + n_dn], int(hdr_up[0]), int(hdr_dn[0]))
+        if not pairs:  # (a lazy division's pairs are discarded: no arange launch for them)
+            return None
         return par[:n_loc], torch.arange(n0, n0 + n_loc, device=self.device)
 
-    def _resolve_count(self) -> None:
+    def _resolve_count(self, stencil_first=None) -> None:
         """Adopt a pending division: World's (a winner count) or a strip division issued with
         ``lazy=True`` (wait for its phase A only, then issue phase B, see _divide_mask_native). Queued
         genome operations then depend on phase B: their chains wait for it, not for the state when
-        they were queued."""
+        they were queued. ``stencil_first`` (a side stream, :meth:`_diffuse_early`): the diffusion
+        stencil is issued before phase B, which goes to that stream."""
         d = self.__dict__
         pend = d.get("_count_pending")
         if pend is None or len(pend) < 4:
@@ -718,22 +747,66 @@ class DistributedWorld(World):
         pair = (_ARRIVALS_MERGE and queued is not None and len(queued) >= 2 and getattr(queued[0], "kind", None) == "rec"
                 and getattr(queued[1], "kind", None) == "mut")
         try:
-            self._divide_phase_b(n0, lw, gw, defer_arrivals=pair, kk=kk)
+            self._divide_phase_b(n0, lw, gw, defer_arrivals=pair, kk=kk, pairs=False, stencil_first=stencil_first)
         finally:
             if queued:
                 from magicsoup_amd.ops.streams import NEvent
 
                 d["_deferred"] = queued + d["_deferred"]
-                d["_defer_event"] = NEvent().record()
+                # (after phase B: on the side stream when it went there)
+                d["_defer_event"] = NEvent().record(stencil_first.cuda_stream if stencil_first is not None else None)
 
     @_op("diffuse_molecules")
     def diffuse_molecules(self):
         """World's diffusion; a strip division issued lazily is completed first, so that its record
-        exchange and commit are queued before the stencil and the genome chains that follow it."""
+        exchange and commit are queued before the genome chains that follow it -- and, over RCCL with
+        a side communicator of its own, after the stencil (:meth:`_diffuse_early`)."""
         if self._strips and self.__dict__.get("_count_pending") is not None:
+            if self._early_stencil_ok():
+                return self._diffuse_early()
             self._resolve_count()
             self._xb_pre_issue_queued()
         return super().diffuse_molecules()
+
+    def _early_stencil_ok(self) -> bool:
+        d = self.__dict__
+        pend = d.get("_count_pending")
+        return (_EARLY_STENCIL and pend is not None and len(pend) >= 6 and self._molmap.is_cuda
+                and self.H * self.map_size <= _EARLY_STENCIL_MAX_PX
+                and isinstance(d.get("_comm"), RcclComm) and isinstance(d.get("_comm_side"), RcclComm)
+                and d["_comm_side"] is not d["_comm"] and not d.get("_side_active"))
+
+    def _diffuse_early(self) -> None:
+        """diffuse_molecules while a lazy strip division is pending, with the stencil before phase B.
+
+        Phase B (record exchange, children and arrivals committed, halo rows cleared) touches the
+        per-cell rows and the cell map, never the molecule map, and phase A's spill is done; the
+        stencil reads and writes only the map. So after the one wait for phase A's counts the
+        stencil is issued first, and phase B, the boundary recombination's collective part and the
+        genome chains follow on the side stream over the side communicator, next to it: the device
+        no longer idles while the host issues phase B and the chains (~150 us per flagship step as
+        one virtual strip, profiles/r5/lazykill). Same kernels, draws and order per communicator on
+        every rank, so the same results. The permeation waits for the side stream (it reads the
+        committed children)."""
+        from magicsoup_amd.ops import world_ops
+        from magicsoup_amd.ops.hip_ops import _stream
+        from magicsoup_amd.ops.streams import join
+
+        d = self.__dict__
+        side = d.get("_side_stream")
+        if side is None:
+            side = d["_side_stream"] = torch.cuda.Stream(device=self._genomes.data.device, priority=-1)
+        main = _stream()
+        self._resolve_count(stencil_first=side)
+        from magicsoup_amd.ops.streams import on_stream
+
+        with on_stream(side):
+            self._xb_pre_issue_queued()
+        if d.get("_deferred"):
+            self._flush_deferred()
+        join(main, side.cuda_stream)  # (phase B's rows before the permeation and what follows)
+        if self.n_cells > 0:
+            world_ops.permeate(self)
 
     def _xb_pre_issue_queued(self) -> None:
         """After a lazy division completed: issue the boundary recombination's collective part of

@@ -52,6 +52,10 @@ for s in "$@"; do case "$s" in
   tmem) run tests_mem 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -k "memory_model or past_2_31" --timeout 300 --timeout-method thread ;;
   hipt) echo "== hipt $(date +%T)"; MS_VIRTUAL_STRIPS=1 timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --stats -d $O/hipt_virt -o run --output-format csv -- python bench.py --map-size 1448 --cells 6250 > $O/hipt_virt.log 2>&1; rc=$?; echo "   rc=$rc"; if fatal $rc; then exit $rc; fi ;;
   hiptp) echo "== hiptp $(date +%T)"; timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --stats -d $O/hipt_plain -o run --output-format csv -- python bench.py --map-size 1448 --cells 6250 > $O/hipt_plain.log 2>&1; rc=$?; echo "   rc=$rc"; if fatal $rc; then exit $rc; fi ;;
+  hsfv) MS_VIRTUAL_STRIPS=1 MS_NATIVE_TIMES=1 MS_PY_TIMES=1 run host_split_flagship_virtual_detail 300 python scripts/host_split.py 4096 50000 40 ;;
+  stt) run tests_strip 600 python -u -m pytest tests/test_gpu_distributed.py -m gpu -q -x --timeout 300 --timeout-method thread ;;
+  abearly) for i in 1 2; do for t in 1 0; do MS_EARLY_STENCIL=$t MS_VIRTUAL_STRIPS=1 run fvirt_e${t}_$i 300 python bench.py
+            MS_EARLY_STENCIL=$t MS_VIRTUAL_STRIPS=1 run virt_e${t}_$i 300 python bench.py --map-size 1448 --cells 6250; done; done ;;
   tests) run tests 1000 python -u -m pytest tests -m gpu -q --maxfail 5 --timeout 120 --timeout-method thread ;;
   smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   flagship) run flagship 300 python bench.py ;;

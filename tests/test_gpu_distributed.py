@@ -492,12 +492,15 @@ def _body_strip_kill_divide_where(rank, ws):
     from magicsoup_amd.parallel import dist_world
 
     out, kills = {}, {}
-    lazy0 = dist_world._LAZY_KILL
+    lazy0, early0 = dist_world._LAZY_KILL, dist_world._EARLY_STENCIL
     # masks: torch masks + kill_cells + lazy divide; eager: native masks, the kill's read-back, lazy
     # divide; lazy: kill and phase A in one call, the survivor count read with phase A's counts
     # (*_f: with a chemostat dilution, whose draws the torch masks cannot reproduce)
-    for fused in ("masks", "eager", "lazy", "eager_f", "lazy_f"):
-        dist_world._LAZY_KILL = fused.startswith("lazy")
+    # (late: the stencil after phase B on the compute stream; the others issue phase B after the
+    # stencil on the side stream, DistributedWorld._diffuse_early)
+    for fused in ("masks", "eager", "lazy", "late", "eager_f", "lazy_f"):
+        dist_world._LAZY_KILL = fused.startswith("lazy") or fused == "late"
+        dist_world._EARLY_STENCIL = fused != "late"
         dw = DistributedWorld(chemistry=_chem(), map_size=64, seed=42, device="cuda", strips=True)
         dw.adopt_maps(w)
         dw.scatter_from(w, maps=False)
@@ -522,12 +525,12 @@ def _body_strip_kill_divide_where(rank, ws):
         dw.check_invariants("strip kill_divide_where")
         out[fused] = (dw.cell_positions.cpu(), dw.cell_molecules.cpu(), dw.cell_divisions.cpu(), list(dw.cell_genomes))
         dw.close()
-    dist_world._LAZY_KILL = lazy0
+    dist_world._LAZY_KILL, dist_world._EARLY_STENCIL = lazy0, early0
     a = out["masks"]
-    for k in ("eager", "lazy"):
+    for k in ("eager", "lazy", "late"):
         b = out[k]
         assert all(torch.equal(x, y) for x, y in zip(a[:3], b[:3])) and a[3] == b[3], k
-    assert kills["eager"] == kills["lazy"] and kills["eager_f"] == kills["lazy_f"]
+    assert kills["eager"] == kills["lazy"] == kills["late"] and kills["eager_f"] == kills["lazy_f"]
     a, b = out["eager_f"], out["lazy_f"]
     assert all(torch.equal(x, y) for x, y in zip(a[:3], b[:3])) and a[3] == b[3]
     assert kills["lazy_f"][0][1] < kills["lazy"][0][1]  # (the dilution killed cells)
