@@ -2233,7 +2233,11 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
   const long long groups = (long long)n * Pt;
   // with a device count the grid is capped and strides (the host passes the capacity as n)
   auto grid = [&](int g) { const unsigned full = cdiv(groups * g, kBlock); return dn ? std::min(full, 4096u) : full; };
-  if (s <= 32) build_params_kernel<32><<<grid(32), kBlock, 0, S_(stream)>>>(b);
+  // (the group is the narrowest power of two covering the signals: 16 lanes for the 14-molecule
+  // chemistry, where 32-lane groups left 18 of every 32 lanes idle; the energy butterfly only loses
+  // exact zero terms, so the bits are the same)
+  if (s <= 16) build_params_kernel<16><<<grid(16), kBlock, 0, S_(stream)>>>(b);
+  else if (s <= 32) build_params_kernel<32><<<grid(32), kBlock, 0, S_(stream)>>>(b);
   else build_params_kernel<64><<<grid(64), kBlock, 0, S_(stream)>>>(b);
   MS_LAUNCH_CHECK();
 }
