@@ -20,6 +20,7 @@
 
 #include "hip_common.h"
 #include "rec_common.h"
+#include "select_lb.h"
 
 namespace msd {
 
@@ -159,6 +160,102 @@ __global__ void __launch_bounds__(kSplitThreads) place_split_write_kernel(int k,
     int t = s_off[threadIdx.x];
     for (int j = 0; j < kSplitItems; ++j)
       for (int q = 0; q < W; ++q) t += s_wc[j][threadIdx.x][q];
+    counts[threadIdx.x] = t;
+    int32_t* hdr = threadIdx.x == 1 ? hdr_up : (threadIdx.x == 2 ? hdr_dn : nullptr);
+    if (hdr) {
+      hdr[0] = t;
+      hdr[1] = lw;
+      hdr[2] = gw;
+      hdr[3] = m;
+    }
+  }
+}
+
+// place_split_count_kernel + place_split_write_kernel in one launch (select_lb.h's scheme with three
+// classes): each tile publishes its three counts (12 bits each, a tile holds 2048 items) tagged with
+// the call's generation, sums the earlier tiles' words and writes its winners. Same output.
+__global__ void __launch_bounds__(kSplitThreads) place_split_lb_kernel(int k, const long long* result,
+                                                                       const int64_t* cells, int C, int H,
+                                                                       unsigned long long* status, uint32_t gen,
+                                                                       int64_t* par, int32_t* npos, int32_t* counts,
+                                                                       int32_t* hdr_up, int32_t* hdr_dn, int lw,
+                                                                       int gw, int m) {
+  constexpr int W = kSplitThreads / 64;
+  static_assert(kSplitTile < 4096, "tile counts are packed in 12 bits");
+  __shared__ int s_wc[kSplitItems][3][W];
+  __shared__ int s_pre[kSplitItems][3][W];
+  __shared__ int s_tot[3];
+  __shared__ int s_red[3][W];
+  __shared__ int s_off[3];
+  const int w = threadIdx.x >> 6, lane = lane_id();
+  const int b = blockIdx.x;
+  const long long base = (long long)b * kSplitTile;
+  uint64_t bal[kSplitItems][3];
+#pragma unroll
+  for (int j = 0; j < kSplitItems; ++j) {
+    const long long i = base + j * kSplitThreads + threadIdx.x;
+    const int cls = i < k ? split_class(result[i], C, H) : -1;
+    for (int q = 0; q < 3; ++q) {
+      bal[j][q] = __ballot(cls == q);
+      if (lane == 0) s_wc[j][q][w] = __popcll(bal[j][q]);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    int acc = 0;
+    for (int j = 0; j < kSplitItems; ++j)
+      for (int q = 0; q < W; ++q) {
+        s_pre[j][threadIdx.x][q] = acc;
+        acc += s_wc[j][threadIdx.x][q];
+      }
+    s_tot[threadIdx.x] = acc;
+  }
+  __syncthreads();
+  const unsigned long long tag = gen & 0xFFFFFFFull;
+  if (threadIdx.x == 0)
+    __hip_atomic_store(status + b,
+                       (tag << 36) | (unsigned long long)s_tot[0] | ((unsigned long long)s_tot[1] << 12) |
+                           ((unsigned long long)s_tot[2] << 24),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the earlier tiles' counts (every tile publishes before it waits; bounded spin as in select_lb.h)
+  int o[3] = {0, 0, 0};
+  for (int q = threadIdx.x; q < b; q += kSplitThreads) {
+    unsigned long long v = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int spin = 0; (v >> 36) != tag && spin < (1 << 22); ++spin) {
+      __builtin_amdgcn_s_sleep(1);
+      v = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    o[0] += (int)(v & 0xFFFu);
+    o[1] += (int)((v >> 12) & 0xFFFu);
+    o[2] += (int)((v >> 24) & 0xFFFu);
+  }
+  for (int c = 0; c < 3; ++c) {
+    for (int sh = 32; sh > 0; sh >>= 1) o[c] += __shfl_xor(o[c], sh);
+    if (lane == 0) s_red[c][w] = o[c];
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    int t = 0;
+    for (int q = 0; q < W; ++q) t += s_red[threadIdx.x][q];
+    s_off[threadIdx.x] = t;
+  }
+  __syncthreads();
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+  for (int j = 0; j < kSplitItems; ++j) {
+    const long long i = base + j * kSplitThreads + threadIdx.x;
+    if (i >= k) break;
+    for (int q = 0; q < 3; ++q) {
+      if (!((bal[j][q] >> lane) & 1ull)) continue;
+      const long long oo = (long long)q * k + s_off[q] + s_pre[j][q][w] + __popcll(bal[j][q] & lt);
+      const long long px = result[i];
+      par[oo] = cells ? cells[i] : i;
+      npos[2 * oo] = (int32_t)(px / C);
+      npos[2 * oo + 1] = (int32_t)(px - (px / C) * C);
+    }
+  }
+  if (b == (int)gridDim.x - 1 && threadIdx.x < 3) {
+    const int t = s_off[threadIdx.x] + s_tot[threadIdx.x];
     counts[threadIdx.x] = t;
     int32_t* hdr = threadIdx.x == 1 ? hdr_up : (threadIdx.x == 2 ? hdr_dn : nullptr);
     if (hdr) {
@@ -479,6 +576,7 @@ RecCols rec_cols(uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, c
 }
 int32_t* g_split_tiles = nullptr;
 long long g_split_cap = 0;
+int g_split_single = 1;  // place_split as one single-pass launch (0: count + write, A/B)
 }  // namespace
 
 void strip_marks(int C, int H, uintptr_t cell_map, int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, uintptr_t up,
@@ -513,6 +611,14 @@ void place_split(int k, uintptr_t result, uintptr_t cells, int C, int H, uintptr
   hipStream_t s = S_(stream);
   if (k < 0) throw std::invalid_argument("place_split: negative count");
   const long long tiles = std::max(1ll, ((long long)k + kSplitTile - 1) / kSplitTile);
+  if (g_split_single && tiles <= kLbMaxTiles) {  // one launch (the status words of select_lb.h)
+    const LbState lb = lb_begin(s);
+    place_split_lb_kernel<<<(unsigned)tiles, kSplitThreads, 0, s>>>(
+        k, P_<long long>(result), cells ? P_<int64_t>(cells) : nullptr, C, H, lb.status, lb.gen, P_<int64_t>(par),
+        P_<int32_t>(npos), P_<int32_t>(counts), P_<int32_t>(hdr_up), P_<int32_t>(hdr_dn), lw, gw, m);
+    MS_LAUNCH_CHECK();
+    return;
+  }
   if (tiles > g_split_cap) {
     if (g_split_tiles) {
       MS_HIP_CHECK(hipStreamSynchronize(s));
@@ -531,6 +637,8 @@ void place_split(int k, uintptr_t result, uintptr_t cells, int C, int H, uintptr
 }
 
 long long rec_record_bytes(int m, int lw, int gw) { return rec_bytes(m, lw, gw); }
+
+void set_split_single(int on) { g_split_single = on; }
 
 void rec_pack(int k_up, int k_dn, uintptr_t par_up, uintptr_t pos_up, uintptr_t par_dn, uintptr_t pos_dn,
               uintptr_t mols, uintptr_t pos, uintptr_t life, uintptr_t div, const GenomePoolArgs& gp, uintptr_t glen,

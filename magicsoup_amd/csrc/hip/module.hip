@@ -200,6 +200,7 @@ void strip_marks(int C, int H, uintptr_t cell_map, int k, uintptr_t cells, uintp
                  uintptr_t dn, uintptr_t stream);
 void strip_reserve(int C, int H, uintptr_t from_up, uintptr_t from_dn, uintptr_t cell_map, uintptr_t stream);
 void strip_clear(int C, int H, uintptr_t cell_map, uintptr_t stream);
+void set_split_single(int on);
 void place_split(int k, uintptr_t result, uintptr_t cells, int C, int H, uintptr_t par, uintptr_t npos, uintptr_t counts,
                  uintptr_t hdr_up, uintptr_t hdr_dn, int lw, int gw, int m, uintptr_t stream);
 long long rec_record_bytes(int m, int lw, int gw);
@@ -350,6 +351,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("strip_reserve", &msd::strip_reserve, "halo occupancy + reservations from the neighbours' marks");
   m.def("strip_clear", &msd::strip_clear);
   m.def("place_split", &msd::place_split, "placement winners split into local / up / down (device counts + headers)");
+  m.def("set_split_single", &msd::set_split_single, "1: place_split as one single-pass launch (0: count + write)");
   m.def("rec_record_bytes", &msd::rec_record_bytes);
   m.def("rec_pack", &msd::rec_pack);
   m.def("rec_unpack", &msd::rec_unpack);

@@ -57,6 +57,7 @@ for s in "$@"; do case "$s" in
   abearly) for i in 1 2; do for t in 1 0; do MS_EARLY_STENCIL=$t MS_VIRTUAL_STRIPS=1 run fvirt_e${t}_$i 300 python bench.py
             MS_EARLY_STENCIL=$t MS_VIRTUAL_STRIPS=1 run virt_e${t}_$i 300 python bench.py --map-size 1448 --cells 6250; done; done ;;
   tdrv) trace tdrv 19 --steps 20 --warmup 5 --step-times ;;
+  splt) run tests_split 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_distributed.py -m gpu -q -x -k "place_split or strip or lazy" --timeout 300 --timeout-method thread ;;
   tests) run tests 1000 python -u -m pytest tests -m gpu -q --maxfail 5 --timeout 120 --timeout-method thread ;;
   smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
   flagship) run flagship 300 python bench.py ;;

@@ -1518,3 +1518,50 @@ def test_chain_issued_on_device_count_matches_resolved_count(monkeypatch):
     _assert_params_equal(_real(a[2]), _real(b[2]), a[2]["_nprot"])
     assert torch.equal(a[3], b[3])
     assert torch.equal(a[4], b[4])
+
+
+@pytest.mark.parametrize("k", [0, 1, 2047, 2048, 5000, 70_000])
+def test_place_split_single_pass_matches_two_pass(k):
+    """The strip division's winners split by destination (dist.hip place_split): the single-pass
+    launch (tile counts published with a generation tag) writes the same parents, pixels, counts and
+    headers as the count + write pair, and both match a torch reference of the split."""
+    from magicsoup_amd.ops import native
+
+    C, H = 512, 64
+    g = torch.Generator().manual_seed(k + 1)
+    # placement results: -1 (no pixel) or a pixel of rows 0 .. H + 1 (0 / H + 1: the halo rows)
+    px = torch.randint(0, (H + 2) * C, (k,), generator=g)
+    px[torch.rand(k, generator=g) < 0.3] = -1
+    result = px.cuda()
+    cells = torch.randperm(max(k, 1), generator=g)[:k].cuda()
+    kk = max(k, 1)
+    outs = []
+    try:
+        for single in (1, 0):
+            native.hip().set_split_single(single)
+            for use_cells in (True, False):
+                par = torch.full((3 * kk,), -7, dtype=torch.int64, device="cuda")
+                npos = torch.full((6 * kk,), -7, dtype=torch.int32, device="cuda")
+                st = torch.zeros(20, dtype=torch.int32, device="cuda")
+                native.hip().place_split(k, result.data_ptr(), cells.data_ptr() if use_cells else 0, C, H,
+                                         par.data_ptr(), npos.data_ptr(), st.data_ptr(), st[4:].data_ptr(),
+                                         st[8:].data_ptr(), 12, 16, 14, torch.cuda.current_stream().cuda_stream)
+                torch.cuda.synchronize()
+                outs.append((single, use_cells, par.cpu(), npos.cpu(), st.cpu()))
+    finally:
+        native.hip().set_split_single(1)
+    x = torch.where(px >= 0, px // C, torch.full_like(px, -1))
+    cls = torch.where(px < 0, -1, torch.where(x == 0, 1, torch.where(x == H + 1, 2, 0)))
+    for single, use_cells, par, npos, st in outs:
+        src = cells.cpu() if use_cells else torch.arange(k)
+        for q in range(3):
+            sel = torch.nonzero(cls == q).flatten()
+            n_q = int(sel.numel())
+            assert int(st[q]) == n_q, (single, q)
+            assert torch.equal(par[q * kk : q * kk + n_q], src[sel]), (single, use_cells, q)
+            pos = npos.view(-1, 2)[q * kk : q * kk + n_q]
+            assert torch.equal(pos[:, 0].long(), px[sel] // C) and torch.equal(pos[:, 1].long(), px[sel] % C)
+        assert st[4:8].tolist() == [int((cls == 1).sum()), 12, 16, 14]
+        assert st[8:12].tolist() == [int((cls == 2).sum()), 12, 16, 14]
+    for a, b in zip(outs[:2], outs[2:]):
+        assert all(torch.equal(u, v) for u, v in zip(a[2:], b[2:]))
