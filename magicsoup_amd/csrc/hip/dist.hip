@@ -177,7 +177,8 @@ __global__ void __launch_bounds__(kSplitThreads) place_split_write_kernel(int k,
 __global__ void __launch_bounds__(kSplitThreads) place_split_lb_kernel(int k, const long long* result,
                                                                        const int64_t* cells, int C, int H,
                                                                        unsigned long long* status, uint32_t gen,
-                                                                       int64_t* par, int32_t* npos, int32_t* counts,
+                                                                       unsigned* err, int64_t* par, int32_t* npos,
+                                                                       int32_t* counts,
                                                                        int32_t* hdr_up, int32_t* hdr_dn, int lw,
                                                                        int gw, int m) {
   constexpr int W = kSplitThreads / 64;
@@ -211,7 +212,7 @@ __global__ void __launch_bounds__(kSplitThreads) place_split_lb_kernel(int k, co
     s_tot[threadIdx.x] = acc;
   }
   __syncthreads();
-  const unsigned long long tag = gen & 0xFFFFFFFull;
+  const unsigned long long tag = gen & kLbGenMask;  // (lb_begin keeps gen within the 28 bits)
   if (threadIdx.x == 0)
     __hip_atomic_store(status + b,
                        (tag << 36) | (unsigned long long)s_tot[0] | ((unsigned long long)s_tot[1] << 12) |
@@ -221,7 +222,11 @@ __global__ void __launch_bounds__(kSplitThreads) place_split_lb_kernel(int k, co
   int o[3] = {0, 0, 0};
   for (int q = threadIdx.x; q < b; q += kSplitThreads) {
     unsigned long long v = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int spin = 0; (v >> 36) != tag && spin < (1 << 22); ++spin) {
+    for (int spin = 0; (v >> 36) != tag; ++spin) {
+      if (spin >= (1 << 22)) {  // (reported through hip_ops.check_placement instead of a hang)
+        if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
       __builtin_amdgcn_s_sleep(1);
       v = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -614,8 +619,8 @@ void place_split(int k, uintptr_t result, uintptr_t cells, int C, int H, uintptr
   if (g_split_single && tiles <= kLbMaxTiles) {  // one launch (the status words of select_lb.h)
     const LbState lb = lb_begin(s);
     place_split_lb_kernel<<<(unsigned)tiles, kSplitThreads, 0, s>>>(
-        k, P_<long long>(result), cells ? P_<int64_t>(cells) : nullptr, C, H, lb.status, lb.gen, P_<int64_t>(par),
-        P_<int32_t>(npos), P_<int32_t>(counts), P_<int32_t>(hdr_up), P_<int32_t>(hdr_dn), lw, gw, m);
+        k, P_<long long>(result), cells ? P_<int64_t>(cells) : nullptr, C, H, lb.status, lb.gen, lb.err,
+        P_<int64_t>(par), P_<int32_t>(npos), P_<int32_t>(counts), P_<int32_t>(hdr_up), P_<int32_t>(hdr_dn), lw, gw, m);
     MS_LAUNCH_CHECK();
     return;
   }

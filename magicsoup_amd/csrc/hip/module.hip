@@ -142,6 +142,7 @@ void set_rec_thinning(int on);
 void set_spl2_waves(int w);
 void set_rescue_mode(int m);
 int rescue_error_take();
+int lb_error_take();
 // mutations.hip
 void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
                uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
@@ -172,6 +173,8 @@ void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t d
 int count_to_host(uintptr_t dcount, uintptr_t stream);
 int select_indices_async(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
                          uintptr_t stream);
+int select_indices_async_pay(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
+                             uintptr_t pay_src, uintptr_t pay_dst, uintptr_t stream);
 void set_select_single_pass(int on, int items);
 void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
 int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t cnt, uintptr_t stream);
@@ -309,6 +312,7 @@ PYBIND11_MODULE(_hip, m) {
         "1: selections of <= 4M items in one launch (tile counts tagged + summed); 0: count + write passes; items: per thread of its tiles (1, 4, 16; 0 keeps)");
   m.def("set_rec_thinning", &msd::set_rec_thinning, "1: recombination (thinned) and mutation draws appended + sorted (0: count + selection passes)");
   m.def("set_rescue_mode", &msd::set_rescue_mode, "1: one launch behind the speculative integrator (0: separate)");
+  m.def("lb_error_take", &msd::lb_error_take, "1 if a single-pass selection's look-back spin timed out");
   m.def("rescue_error_take", &msd::rescue_error_take, "1 if the integrator rescue launch's grid barrier timed out");
   m.def("set_integrate_mode", &msd::set_integrate_mode, "binned integrator launches: 0 serial, 1 concurrent, 2 concurrent + strided wide bin");
   m.def("translate_slot_bytes", &msd::translate_slot_bytes);
@@ -330,6 +334,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("cap_skip", &msd::cap_skip, "pipeline capacity guard: count > cap -> no-op call replayed by the host");
   m.def("select_indices_async", &msd::select_indices_async,
         "compaction with the count on the device and in a pinned status slot (returned); no sync");
+  m.def("select_indices_async_pay", &msd::select_indices_async_pay,
+        "select_indices_async plus pay_dst[k] = pay_src[sel[k]] (zeros past the count)");
   m.def("count_to_host", &msd::count_to_host, "device {count, max} -> pinned ring slot (returns the slot)");
   m.def("status_write", &msd::status_write, "pipeline status -> pinned ring slot (returns the slot)");
   m.def("status_read", &msd::status_read);

@@ -152,11 +152,11 @@ __global__ void __launch_bounds__(kSelThreads) select_write_kernel(long long n, 
 // mask compacted with the survivors of kill_divide, fast.hip).
 template <int K, int ITEMS>
 __global__ void __launch_bounds__(kSelThreads) select_lb_kernel(long long n, const void* src, unsigned long long* status,
-                                                                uint32_t gen, int64_t* sel, int64_t* rest,
-                                                                int32_t* out, long long* host64, const uint8_t* pay_src,
-                                                                uint8_t* pay_dst) {
+                                                                uint32_t gen, unsigned* err, int64_t* sel,
+                                                                int64_t* rest, int32_t* out, long long* host64,
+                                                                const uint8_t* pay_src, uint8_t* pay_dst) {
   select_lb_tile<ITEMS>(
-      n, [&](long long i) { return sel_pred<K>(src, i); }, status, gen,
+      n, [&](long long i) { return sel_pred<K>(src, i); }, status, gen, err,
       [&](long long k, long long i) {
         sel[k] = i;
         if (pay_dst) pay_dst[k] = pay_src[i];
@@ -233,6 +233,8 @@ struct LbBuf {
   uint32_t gen = 0;
 };
 std::unordered_map<hipStream_t, LbBuf> g_lb;
+unsigned* g_lb_err = nullptr;  // pinned, mapped: a look-back spin timed out (LbState::err)
+unsigned* g_lb_err_dev = nullptr;
 int g_sel_single = 1;  // select_indices_async takes the single-pass kernel when the grid allows
 int g_sel_items = 4;   // items per thread of its tiles (1, 4 or 16) while the status words suffice
 int32_t* g_tacc = nullptr;  // device {max proteins, max domains, done blocks}, zero between calls
@@ -385,11 +387,23 @@ LbState lb_begin(hipStream_t s) {
     MS_HIP_CHECK(hipMalloc((void**)&lb.p, kLbMaxTiles * sizeof(unsigned long long)));
     MS_HIP_CHECK(hipMemsetAsync(lb.p, 0, kLbMaxTiles * sizeof(unsigned long long), s));
   }
-  if (++lb.gen == 0) {  // the tags wrapped: clear the words (no stale tag can match gen 1 then)
+  if (!g_lb_err) {
+    MS_HIP_CHECK(hipHostMalloc((void**)&g_lb_err, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
+    *g_lb_err = 0;
+    MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_lb_err_dev, g_lb_err, 0));
+  }
+  // the tags wrapped (at the narrowest tag width of the kernels that share the words): clear the
+  // words, so no stale tag can match gen 1 then
+  if (++lb.gen > kLbGenMask) {
     MS_HIP_CHECK(hipMemsetAsync(lb.p, 0, kLbMaxTiles * sizeof(unsigned long long), s));
     lb.gen = 1;
   }
-  return {lb.p, lb.gen};
+  return {lb.p, lb.gen, g_lb_err_dev};
+}
+
+int lb_error_take() {
+  if (!g_lb_err) return 0;
+  return __atomic_exchange_n(g_lb_err, 0u, __ATOMIC_ACQ_REL) ? 1 : 0;
 }
 
 bool select_single_pass(long long n) { return g_sel_single && (n + kSelTile - 1) / kSelTile <= kLbMaxTiles; }
@@ -399,7 +413,16 @@ void set_select_single_pass(int on, int items) {
   if (items == 1 || items == 4 || items == kSelItems) g_sel_items = items;
 }
 
-// select_indices_async with the payload of select_lb_kernel (pay_dst: n bytes); single-pass only
+// The payload of a two-pass selection (too many items for the single-pass status words): the same
+// bytes select_lb_kernel writes, pay_dst[k] = pay_src[sel[k]] below the device count, 0 above.
+__global__ void __launch_bounds__(256) select_payload_kernel(long long n, const int32_t* cnt, const int64_t* sel,
+                                                             const uint8_t* pay_src, uint8_t* pay_dst) {
+  const long long c = *cnt;
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x)
+    pay_dst[k] = k < c ? pay_src[sel[k]] : (uint8_t)0;
+}
+
+// select_indices_async with the payload of select_lb_kernel (pay_dst: n bytes)
 int select_indices_async_pay(long long n, int kind, uintptr_t src, uintptr_t sel, uintptr_t rest, uintptr_t out_dev,
                              uintptr_t pay_src, uintptr_t pay_dst, uintptr_t stream);
 
@@ -424,15 +447,14 @@ static int select_async_impl(long long n, int kind, uintptr_t src, uintptr_t sel
   if (n >= (1ll << 40)) throw std::invalid_argument("select_indices_async: n too large");
   const long long tiles = (n + kSelTile - 1) / kSelTile;
   const void* sp = reinterpret_cast<const void*>(src);
-  if ((g_sel_single && tiles <= kLbMaxTiles) || pay_dst) {
-    if (tiles > kLbMaxTiles) throw std::invalid_argument("select_indices_async: payload selection of too many items");
+  if (g_sel_single && tiles <= kLbMaxTiles) {
     const LbState lb = lb_begin(s);
     // smaller tiles while they fit the status words: more workgroups, shorter per-tile chains
     const int items = g_sel_items < kSelItems && n <= (long long)kLbMaxTiles * kSelThreads * g_sel_items ? g_sel_items
                                                                                                       : kSelItems;
     const unsigned grid = (unsigned)((n + (long long)kSelThreads * items - 1) / ((long long)kSelThreads * items));
 #define MS_SEL1(K, I)                                                                                               \
-  select_lb_kernel<K, I><<<grid, kSelThreads, 0, s>>>(n, sp, lb.status, lb.gen, P_<int64_t>(sel),                   \
+  select_lb_kernel<K, I><<<grid, kSelThreads, 0, s>>>(n, sp, lb.status, lb.gen, lb.err, P_<int64_t>(sel),           \
                                                       rest ? P_<int64_t>(rest) : nullptr, P_<int32_t>(out_dev), h64, \
                                                       P_<uint8_t>(pay_src), P_<uint8_t>(pay_dst));                  \
   MS_LAUNCH_CHECK();
@@ -473,6 +495,11 @@ static int select_async_impl(long long n, int kind, uintptr_t src, uintptr_t sel
     default: throw std::invalid_argument("select_indices_async: unknown predicate");
   }
 #undef MS_SEL
+  if (pay_dst) {
+    const unsigned g = (unsigned)std::min<long long>((n + 255) / 256, 4096);
+    select_payload_kernel<<<g, 256, 0, s>>>(n, out, P_<int64_t>(sel), P_<uint8_t>(pay_src), P_<uint8_t>(pay_dst));
+    MS_LAUNCH_CHECK();
+  }
   return slot;
 }
 

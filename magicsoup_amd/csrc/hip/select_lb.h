@@ -4,8 +4,9 @@
 // selected count tagged with the call's generation (one 64-bit word per tile, never reset: a stale
 // word carries an older tag), then sums the published counts of the tiles before it and hands every
 // item its output position. Every tile publishes before it waits on anything and workgroups are
-// dispatched in index order, so the spin on an earlier tile ends; it is bounded anyway (a tile that
-// never publishes yields a wrong count instead of a hung device). One launch per selection instead
+// dispatched in index order, so the spin on an earlier tile ends; it is bounded anyway: a tile that
+// never publishes sets the mapped error word `err` (LbState::err, read by lb_error_take through
+// hip_ops.check_placement) instead of hanging the device. One launch per selection instead
 // of the count + write pair, and the caller's per-item work (a payload, a commit) rides along.
 #pragma once
 #include "hip_common.h"
@@ -18,13 +19,19 @@ constexpr int kSelTile = kSelThreads * kSelItems;  // 4096
 constexpr int kLbMaxTiles = 1024;
 
 // the tile status words of a stream and the tag of the call being issued (select.hip lb_begin)
+// Tags are 28 bits wide (place_split_lb_kernel packs three 12-bit counts beside its tag): lb_begin
+// clears the words whenever the generation wraps at 2^28, so no stale word carries a matching tag.
+constexpr uint32_t kLbGenMask = 0x0FFFFFFFu;
 struct LbState {
   unsigned long long* status;
-  uint32_t gen;
+  uint32_t gen;   // 1 .. kLbGenMask
+  unsigned* err;  // mapped host word: a look-back spin timed out (the selection's offsets are wrong)
 };
 LbState lb_begin(hipStream_t s);
 // whether select_indices_async takes the single-pass form for n items
 bool select_single_pass(long long n);
+// 1 if a single-pass selection's look-back spin timed out since the last call; clears the word
+int lb_error_take();
 // a fresh pinned status slot (select.hip ring) and its device pointer
 int status_slot_new(long long** dev);
 
@@ -35,7 +42,7 @@ int status_slot_new(long long** dev);
 // caller's per-tile work (world.hip select_commit_kernel commits a tile's winners in its workgroup).
 template <int ITEMS = kSelItems, class Pred, class OnSel, class OnRest>
 __device__ __forceinline__ long long select_lb_tile(long long n, Pred pred, unsigned long long* status, uint32_t gen,
-                                                    OnSel on_sel, OnRest on_rest, int32_t* out, long long* host64,
+                                                    unsigned* err, OnSel on_sel, OnRest on_rest, int32_t* out, long long* host64,
                                                     int* tile_cnt = nullptr) {
   constexpr int W = kSelThreads / 64;
   constexpr int kTile = kSelThreads * ITEMS;
@@ -69,7 +76,11 @@ __device__ __forceinline__ long long select_lb_tile(long long n, Pred pred, unsi
   long long off = 0;
   for (int q = threadIdx.x; q < b; q += kSelThreads) {
     unsigned long long v = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int spin = 0; (uint32_t)(v >> 32) != gen && spin < (1 << 22); ++spin) {
+    for (int spin = 0; (uint32_t)(v >> 32) != gen; ++spin) {
+      if (spin >= (1 << 22)) {  // (never in a healthy grid: report, do not hang)
+        if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
       __builtin_amdgcn_s_sleep(1);
       v = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

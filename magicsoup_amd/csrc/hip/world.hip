@@ -84,13 +84,13 @@ __global__ void __launch_bounds__(256) divide_commit_kernel(const int* dn, const
 // threads over (winners x m).
 __global__ void __launch_bounds__(kSelThreads) select_commit_kernel(int n, const long long* result,
                                                                     unsigned long long* status, uint32_t gen,
-                                                                    int64_t* wins, int32_t* dcount, long long* host64,
+                                                                    unsigned* err, int64_t* wins, int32_t* dcount, long long* host64,
                                                                     int C, long long n0, const int* n0_dev, int m,
                                                                     int64_t* par, int32_t* pos, float* cell_mols,
                                                                     int32_t* divisions, int32_t* lifetimes) {
   int cnt = 0;
   const long long toff = select_lb_tile<1>(
-      n, [&](long long i) { return result[i] >= 0; }, status, gen,
+      n, [&](long long i) { return result[i] >= 0; }, status, gen, err,
       [&](long long k, long long p) {
         wins[k] = p;
         par[k] = p;
@@ -1071,7 +1071,7 @@ int divide_mask_dev_at(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r
     const int slot = status_slot_new(&h64);
     const LbState lb = lb_begin(s);
     select_commit_kernel<<<cdiv(n, kSelThreads), kSelThreads, 0, s>>>(
-        n, P_<long long>(result), lb.status, lb.gen, P_<int64_t>(wins), P_<int32_t>(dcount), h64, C, n0,
+        n, P_<long long>(result), lb.status, lb.gen, lb.err, P_<int64_t>(wins), P_<int32_t>(dcount), h64, C, n0,
         n0_dev ? P_<int>(n0_dev) : nullptr, m, P_<int64_t>(par), P_<int32_t>(pos), P_<float>(cell_mols),
         P_<int32_t>(divisions), P_<int32_t>(lifetimes));
     MS_LAUNCH_CHECK();

@@ -607,7 +607,10 @@ class World:
             d["_count_pending"] = None
             d["last_kill"] = (n0, n_k)
             hip_ops.check_placement()
-            if n_k + k != n0:
+            # (adopted whenever rows moved, not only when the count changed: a step that kills as
+            # many cells as it divides still compacted the arenas, whose string caches are keyed on
+            # their version)
+            if n_k != n0 or k:
                 self._adopt_count(n_k + k)
             return
         k = int(hip_ops._m().status_read(slot)[0])
@@ -1620,6 +1623,11 @@ class World:
         self._reconcile()
         if self._molmap.is_cuda:
             torch.cuda.synchronize(self._molmap.device)
+            from magicsoup_amd.ops import hip_ops
+
+            # (the device's error words -- grid barriers, look-back spins -- of everything issued
+            # up to here, including an activity no division has confirmed yet)
+            hip_ops.check_placement()
 
     def enable_timings(self, sync: bool = False) -> None:
         """Time every public operation with HIP events (wall clock on CPU); read with

@@ -169,6 +169,9 @@ def check_placement() -> None:
     if _m().rescue_error_take():
         raise RuntimeError("integrator: a grid barrier of the rescue launch timed out (grid not co-resident); "
                            "the activity's results may be wrong")
+    if _m().lb_error_take():
+        raise RuntimeError("selection: a single-pass look-back spin timed out; the compaction or placement "
+                           "offsets of the last kill / division may be wrong")
 
 
 # ---------------------------------------------------------------------------- geometry

@@ -1465,6 +1465,72 @@ def test_kill_divide_single_pass_selections_match_two_pass():
         assert (torch.equal(a[k], b[k]) if isinstance(a[k], torch.Tensor) else a[k] == b[k]), k
 
 
+def test_kill_divide_with_as_many_kills_as_divisions_refreshes_strings():
+    """A kill_divide_t that kills exactly as many cells as it divides leaves n_cells unchanged but
+    still compacts the genome / label arenas and appends children: cached string views
+    (cell_genomes, cell_labels, read before the call) must show the new rows, as the synchronous
+    kill_cells + divide_cells_t do (the count was adopted only when it changed)."""
+    base = _world("cuda", map_size=64, n=200, s=300, seed=31)
+    base.cell_labels = [f"c{i}" for i in range(base.n_cells)]
+    base.synchronize()
+    n = base.n_cells
+    kill = torch.zeros(n, dtype=torch.bool, device="cuda")
+    kill[:10] = True
+    div = torch.zeros(n, dtype=torch.bool, device="cuda")
+    div[20:30] = True
+    ref = copy.deepcopy(base)
+    ms.set_seed(2)
+    ref.kill_cells(kill)
+    ref.divide_cells_t(div[~kill].clone())
+    ref.synchronize()
+    assert ref.n_cells == n, "the sparse map must place every child (precondition)"
+    w = copy.deepcopy(base)
+    before_g, before_l = list(w.cell_genomes), list(w.cell_labels)  # (fills the string caches)
+    ms.set_seed(2)
+    w.kill_divide_t(kill, div)
+    w.synchronize()
+    assert w.n_cells == n and w.last_kill == (n, n - 10)
+    assert list(w.cell_labels) == list(ref.cell_labels) != before_l
+    assert list(w.cell_genomes) == list(ref.cell_genomes) != before_g
+    assert w.cell_labels[0] == "c10" and w.cell_labels[n - 1] == "c29"
+    assert torch.equal(w.cell_positions, ref.cell_positions)
+
+
+def test_payload_selection_two_pass_matches_single_pass():
+    """select_indices_async_pay (the division mask compacted with the survivors) takes the count +
+    write passes plus a payload kernel when the single-pass status words do not suffice (> 4M
+    cells, forced here with set_select_single_pass(0)): same indices, count and payload bytes."""
+    from magicsoup_amd.ops import hip_ops
+
+    m = native.hip()
+    g = torch.Generator().manual_seed(5)
+    n = 50_000
+    src = (torch.rand(n, generator=g) < 0.3).to(torch.uint8).cuda()
+    pay = (torch.rand(n, generator=g) < 0.5).to(torch.uint8).cuda()
+    out = []
+    try:
+        for single in (1, 0):
+            m.set_select_single_pass(single)
+            sel = torch.full((n,), -7, dtype=torch.int64, device="cuda")
+            dst = torch.full((n,), 9, dtype=torch.uint8, device="cuda")
+            cnt = torch.zeros(2, dtype=torch.int32, device="cuda")
+            slot = m.select_indices_async_pay(n, 1, src.data_ptr(), sel.data_ptr(), 0, cnt.data_ptr(), pay.data_ptr(),
+                                              dst.data_ptr(), hip_ops._stream())
+            torch.cuda.synchronize()
+            k = int(m.status_read(slot)[0])
+            out.append((k, sel[:k].cpu(), dst.cpu(), int(cnt[0])))
+    finally:
+        m.set_select_single_pass(1)
+    (k1, s1, d1, c1), (k2, s2, d2, c2) = out
+    keep = torch.nonzero(src.cpu() == 0).flatten()
+    assert k1 == k2 == c1 == c2 == keep.numel()
+    assert torch.equal(s1, keep) and torch.equal(s2, keep)
+    want = torch.zeros(n, dtype=torch.uint8)
+    want[:k1] = pay.cpu()[keep]
+    assert torch.equal(d1, want) and torch.equal(d2, want)
+    assert not m.lb_error_take()
+
+
 @pytest.mark.gpu
 def test_chain_issued_on_device_count_matches_resolved_count(monkeypatch):
     """A recombinate + mutate pair queued behind a kill_divide is issued before the division's count
