@@ -6,6 +6,7 @@ void bind_genetics(py::module_& m);
 void bind_mutations(py::module_& m);
 void bind_kinetics(py::module_& m);
 void bind_world(py::module_& m);
+void bind_io(py::module_& m);
 }  // namespace ms_host
 
 PYBIND11_MODULE(_host, m) {
@@ -14,4 +15,5 @@ PYBIND11_MODULE(_host, m) {
   ms_host::bind_mutations(m);
   ms_host::bind_kinetics(m);
   ms_host::bind_world(m);
+  ms_host::bind_io(m);
 }

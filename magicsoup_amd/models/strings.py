@@ -175,32 +175,43 @@ class StringArena:
         return torch.nn.functional.pad(rows, (0, w - rows.size(1)))
 
     # ---------------------------------------------------------------- materialisation
-    def to_strings(self, rows: Iterable[int] | None = None) -> list[str]:
-        """The strings of all rows (or of ``rows``): the rows (cut to the longest string) are copied
-        to the host in one transfer, the host core concatenates their used bytes, and that buffer is
-        decoded once; the strings are slices of it."""
+    def packed(self, rows: Iterable[int] | None = None) -> tuple[np.ndarray, np.ndarray]:
+        """The strings of all rows (or of ``rows``) back to back as host bytes (uint8) plus their
+        lengths (int64): the rows, cut to the longest string, are copied to the host in one transfer
+        and the host core concatenates their used bytes (checkpoint shards store this layout)."""
         if rows is None:
             data, lens = self.data[: self.n], self.lens[: self.n]
         else:
             idx = torch.as_tensor(list(rows), dtype=torch.long, device=self.device)
             data, lens = self.data[idx], self.lens[idx]
-        if data.numel() == 0:
-            return [""] * int(lens.numel())
-        ls = lens.cpu()
-        lmax = int(ls.max()) if ls.numel() else 0
-        if lmax == 0:
-            return [""] * int(ls.numel())
+        ls = lens.cpu().numpy().astype(np.int64)
+        lmax = int(ls.max()) if ls.size else 0
+        if data.numel() == 0 or lmax == 0:
+            return np.zeros(0, dtype=np.uint8), np.zeros(ls.size, dtype=np.int64)
         from magicsoup_amd.ops import native
 
-        # rows cut to the longest string, one transfer; the host core concatenates the used bytes
         sub = data[:, :lmax].contiguous().cpu().numpy()
-        raw = native.host().unpack_rows(sub, ls.numpy().astype(np.int32, copy=False)).decode("ascii")
-        ends = np.cumsum(ls.numpy(), dtype=np.int64).tolist()
-        starts = [0] + ends[:-1]
-        return [raw[a:b] for a, b in zip(starts, ends)]
+        raw = native.host().unpack_rows(sub, ls.astype(np.int32))
+        return np.frombuffer(raw, dtype=np.uint8), ls
+
+    def to_strings(self, rows: Iterable[int] | None = None) -> list[str]:
+        """The strings of all rows (or of ``rows``): :meth:`packed`, decoded once; the strings are
+        slices of that buffer."""
+        buf, ls = self.packed(rows)
+        return _split(buf, ls)
 
 
 _POOL_MIN = 16 << 20  # bytes
+
+
+def _split(buf: np.ndarray, lens: np.ndarray) -> list[str]:
+    """Strings of the given lengths, back to back in ``buf`` (ASCII): one decode, then slices."""
+    if buf.size == 0:
+        return [""] * int(lens.size)
+    raw = str(memoryview(buf), "ascii")
+    ends = np.cumsum(lens, dtype=np.int64).tolist()
+    starts = [0] + ends[:-1]
+    return [raw[a:b] for a, b in zip(starts, ends)]
 
 
 def _r16(n: int) -> int:
@@ -482,31 +493,32 @@ class PoolArena:
         return self.rows_of(None), self.lens[: self.n]
 
     # ---------------------------------------------------------------- materialisation
-    def to_strings(self, rows: Iterable[int] | None = None) -> list[str]:
+    def packed(self, rows: Iterable[int] | None = None) -> tuple[np.ndarray, np.ndarray]:
+        """The genomes of all cells (or of ``rows``) back to back as host bytes (uint8) plus their
+        lengths (int64): gathered on the device at an exclusive prefix sum of the lengths, then one
+        transfer of exactly their bytes (checkpoint shards store this layout)."""
         idx = None if rows is None else torch.as_tensor(list(rows), dtype=torch.long, device=self.device)
         lens = self.lens[: self.n] if idx is None else self.lens[idx]
-        ls = lens.cpu()
-        k = int(ls.numel())
-        lmax = int(ls.max()) if k else 0
-        if lmax == 0:
-            return [""] * k
+        ls = lens.cpu().numpy().astype(np.int64)
+        k = int(ls.size)
+        if k == 0 or int(ls.max()) == 0:
+            return np.zeros(0, dtype=np.uint8), ls
         from magicsoup_amd.ops import native
         from magicsoup_amd.ops.hip_ops import _stream
 
-        # the genomes back to back on the device (exclusive prefix sum of the lengths), one
-        # transfer of exactly their bytes, one decode; the strings are slices of it
-        ends_np = np.cumsum(ls.numpy(), dtype=np.int64)
+        ends_np = np.cumsum(ls, dtype=np.int64)
         total = int(ends_np[-1])
-        starts_np = ends_np - ls.numpy()
-        dst_off = torch.from_numpy(starts_np).to(self.device)
+        dst_off = torch.from_numpy(ends_np - ls).to(self.device)
         out = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
         native.hip().pool_read_packed(k, 0 if idx is None else idx.data_ptr(), self.data.data_ptr(),
                                       self.off.data_ptr(), self.lens.data_ptr(), dst_off.data_ptr(), out.data_ptr(),
                                       _stream())
-        raw = str(memoryview(out[:total].cpu().numpy()), "ascii")
-        ends = ends_np.tolist()
-        starts = starts_np.tolist()
-        return [raw[a:b] for a, b in zip(starts, ends)]
+        return out[:total].cpu().numpy(), ls
+
+    def to_strings(self, rows: Iterable[int] | None = None) -> list[str]:
+        """One :meth:`packed` transfer, one decode; the strings are slices of it."""
+        buf, ls = self.packed(rows)
+        return _split(buf, ls)
 
 
 class StringColumn:

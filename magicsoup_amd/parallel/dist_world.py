@@ -1217,27 +1217,48 @@ class DistributedWorld(World):
             raise ValueError("map sizes differ")
         if maps:
             self.adopt_maps(world)
-        self.kill_cells_local_all()
-        mm = self.__dict__["_molmap"]
-        mm.zero_()
-        mm[:, lo : lo + H] = world.molecule_map[:, self.row0 : self.row0 + H].to(mm.device)
-        self.__dict__["_pending_scale"] = None
-        self.__dict__["_pending_corr"] = None
         gpos = world.cell_positions.long().cpu()
         mine = torch.nonzero((gpos[:, 0] >= self.row0) & (gpos[:, 0] < self.row0 + H)).flatten()
         k = int(mine.numel())
+        genomes = labels = None
         if k:
+            from magicsoup_amd.models.strings import pack_strings
+
             sel = mine.tolist()
+            arr, lens = pack_strings(world._genomes.to_strings(sel))
+            genomes = (torch.from_numpy(arr), torch.from_numpy(lens))
+            arr, lens = pack_strings(world._labels.to_strings(sel))
+            labels = (torch.from_numpy(arr), torch.from_numpy(lens))
+        lpos = gpos[mine].clone()
+        lpos[:, 0] += lo - self.row0
+        cols = {name: getattr(world, name)[mine.to(getattr(world, name).device)]
+                for name in ("cell_molecules", "cell_lifetimes", "cell_divisions")}
+        self._adopt_strip(world.molecule_map[:, self.row0 : self.row0 + H], genomes, labels, lpos.to(torch.int32), cols,
+                          params=params)
+
+    def _adopt_strip(self, owned_map: torch.Tensor, genomes, labels, lpos: torch.Tensor, cols: dict,
+                     params: bool = True) -> None:
+        """Replace this rank's state: ``owned_map`` (m, H, map_size) becomes the owned rows of the
+        molecule map; the cells -- packed genome / label rows + lengths, local positions, and the
+        ``cell_molecules`` / ``cell_lifetimes`` / ``cell_divisions`` rows -- replace the local ones
+        (parameters rebuilt on the device unless ``params`` is False); halos are refreshed
+        (collective in strips)."""
+        H, lo = self.H, self._lo
+        self.kill_cells_local_all()
+        mm = self.__dict__["_molmap"]
+        mm.zero_()
+        mm[:, lo : lo + H] = owned_map.to(mm.device, mm.dtype)
+        self.__dict__["_pending_scale"] = None
+        self.__dict__["_pending_corr"] = None
+        k = int(lpos.size(0))
+        if k:
             self._grow(k)
-            self._genomes.append_strings(world._genomes.to_strings(sel))
-            self._labels.append_strings(world._labels.to_strings(sel))
-            lpos = gpos[mine].clone()
-            lpos[:, 0] += lo - self.row0
+            self._genomes.append_packed(*genomes)
+            self._labels.append_packed(*labels)
             new = torch.arange(k, device=self.device)
             self._place(new, lpos.to(torch.int32))
-            self.cell_molecules[:] = world.cell_molecules[mine.to(world.cell_molecules.device)].to(self.device)
-            self.cell_lifetimes[:] = world.cell_lifetimes[mine.to(world.cell_lifetimes.device)].to(self.device)
-            self.cell_divisions[:] = world.cell_divisions[mine.to(world.cell_divisions.device)].to(self.device)
+            for name, t in cols.items():
+                getattr(self, name)[:] = t.to(self.device)
             if params:
                 self._update_params_rows(new)
         if self._strips:
@@ -1290,27 +1311,50 @@ class DistributedWorld(World):
         if self.n_cells:
             self._remove(torch.arange(self.n_cells, device=self.device))
 
-    def save_state(self, statedir: Path):
-        """Collective: rank 0 writes the global state in the reference's format."""
+    def save_state(self, statedir: Path, assemble: bool = True):
+        """Collective. Every rank writes its shard under ``statedir/shards/`` at the same time, from
+        its own device memory (utils.checkpoint.save_shard: owned map rows, its cells with global
+        positions, genomes / labels as packed bytes, its random streams); with ``assemble`` rank 0
+        then writes the reference layout from the shards (``cells.fasta``, ``*.pt``, as a
+        single-process world's ``save_state``). ``assemble=False`` skips that step for worlds
+        whose global map one host should not hold (``checkpoint.assemble_state`` does it offline)."""
+        from magicsoup_amd.utils import checkpoint
+
+        statedir = Path(statedir)
+        if self.rank == 0:
+            # (a stale shard set of another rank count would make the directory ambiguous)
+            import shutil
+
+            root = statedir / checkpoint.SHARD_DIR
+            if root.is_dir():
+                for p in root.iterdir():
+                    if not p.name.endswith(f"_of{self.world_size:04d}"):
+                        shutil.rmtree(p)
+        dist.barrier(group=self.group)
+        checkpoint.save_shard(self, statedir)
+        dist.barrier(group=self.group)
+        if assemble and self.rank == 0:
+            checkpoint.assemble_state(statedir)
+        dist.barrier(group=self.group)
+
+    def save_state_gathered(self, statedir: Path):
+        """Collective: rank 0 assembles the global world on the CPU (:meth:`gather`: every genome
+        re-translated there) and writes it; kept as the oracle of the sharded :meth:`save_state`."""
         w = self.gather()
         if w is not None:
             w.save_state(Path(statedir))
         dist.barrier(group=self.group)
 
-    def load_state(self, statedir: Path, ignore_cell_params: bool = False, restore_rng: bool = False):
-        """Collective: every rank reads the global state and keeps its strip. (The random streams
-        are per rank; a gathered state's ``rng_state.pt`` is rank 0's and is not restored.)"""
-        w = World(
-            chemistry=self.chemistry,
-            map_size=self.map_size,
-            abs_temp=self.abs_temp,
-            mol_map_init="zeros",
-            start_codons=self.genetics.start_codons,
-            stop_codons=self.genetics.stop_codons,
-            device="cpu",
-        )
-        w.load_state(Path(statedir), ignore_cell_params=True, restore_rng=False)
-        self.scatter_from(w, maps=False, params=not ignore_cell_params)
+    def load_state(self, statedir: Path, ignore_cell_params: bool = False, restore_rng: bool = False) -> str:
+        """Collective. Each rank loads its own shard when the state has shards of this rank count
+        (``restore_rng`` then restores the rank's random streams: a run resumes exactly), otherwise
+        its strip of the reference files -- map rows memory-mapped, its cells picked from the FASTA
+        -- with no CPU world. Returns the source used (``"shard"`` / ``"reference"``)."""
+        from magicsoup_amd.utils import checkpoint
+
+        self._reconcile()
+        return checkpoint.load_strip(self, Path(statedir), ignore_cell_params=ignore_cell_params,
+                                     restore_rng=restore_rng)
 
     def close(self) -> None:
         """Release the communicator (collective). The world cannot exchange afterwards."""

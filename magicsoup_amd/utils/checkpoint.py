@@ -31,6 +31,7 @@ import pickle
 import random
 from pathlib import Path
 
+import numpy as np
 import torch
 
 _FILES = ("cell_molecules", "cell_map", "molecule_map", "cell_lifetimes", "cell_positions", "cell_divisions")
@@ -44,12 +45,46 @@ def save_state(world, statedir: Path) -> None:
         if name == "molecule_map":
             t = t.to(torch.float32)  # checkpoints always hold fp32 maps, whatever the storage dtype
         torch.save(t.clone(), statedir / f"{name}.pt")
-    genomes = world.cell_genomes.tolist()
-    labels = world.cell_labels.tolist()
-    text = "\n".join(f">{i} {lab}\n{g}" for i, (g, lab) in enumerate(zip(genomes, labels)))
-    with open(statedir / "cells.fasta", "w", encoding="utf-8") as fh:
-        fh.write(text)
+    # genomes and labels go from the arenas to the file as packed bytes (host core fasta_write: no
+    # Python string per cell); the text is the reference's, entries joined by "\n"
+    g, gl = world._genomes.packed()
+    lab, ll = world._labels.packed()
+    _host().fasta_write(str(statedir / "cells.fasta"), 0, g, gl, lab, ll)
     torch.save(rng_state(world.device), statedir / RNG_FILE)
+
+
+def _host():
+    from magicsoup_amd.ops import native
+
+    return native.host()
+
+
+def read_fasta_packed(path: Path) -> tuple:
+    """(genome bytes, genome lengths, label bytes, label lengths) of a ``cells.fasta`` -- the
+    reference's parsing rules (``world.py:853-866``), in the host core."""
+    return _host().fasta_parse(str(path))
+
+
+def packed_rows(buf, lens, idx=None) -> tuple[torch.Tensor, torch.Tensor]:
+    """Zero-padded uint8 rows (k, width) + int32 lengths of the strings ``idx`` (all when None) of
+    a packed buffer: what the arenas' ``append_packed`` takes."""
+    buf = np.asarray(buf, dtype=np.uint8)
+    lens = np.asarray(lens, dtype=np.int64)
+    if idx is not None:
+        idx = np.asarray(idx, dtype=np.int64)
+        starts = np.cumsum(lens) - lens
+        sl = lens[idx]
+        total = int(sl.sum())
+        if total:
+            # byte j of the selection: its string's start + its position within the string
+            rep = np.repeat(starts[idx] - (np.cumsum(sl) - sl), sl)
+            buf = buf[rep + np.arange(total, dtype=np.int64)]
+        else:
+            buf = np.zeros(0, dtype=np.uint8)
+        lens = sl
+    width = max(16, (int(lens.max()) + 15) // 16 * 16 if lens.size else 16)
+    rows = _host().pack_rows(buf.tobytes(), lens.astype(np.int32), width)
+    return torch.from_numpy(rows), torch.from_numpy(lens.astype(np.int32))
 
 
 def rng_state(device) -> dict:
@@ -112,9 +147,8 @@ def load_state(world, statedir: Path, ignore_cell_params: bool = False, restore_
     def ld(name):
         return torch.load(statedir / f"{name}.pt", map_location=dev, weights_only=True)
 
-    with open(statedir / "cells.fasta", "r", encoding="utf-8") as fh:
-        genomes, labels = _parse_fasta(fh.read())
-    n = len(genomes)
+    g, gl, lab, ll = read_fasta_packed(statedir / "cells.fasta")
+    n = int(gl.size)
     cell_map = ld("cell_map").bool()
     world.molecule_map = ld("molecule_map").to(torch.float32).contiguous()
     world.cell_map = cell_map
@@ -126,13 +160,171 @@ def load_state(world, statedir: Path, ignore_cell_params: bool = False, restore_
     world.cell_divisions[:] = ld("cell_divisions").int()
     world._genomes.clear()
     world._labels.clear()
-    world._genomes.append_strings(genomes)
-    world._labels.append_strings(labels)
+    if n:
+        world._genomes.append_packed(*packed_rows(g, gl))
+        world._labels.append_packed(*packed_rows(lab, ll))
     if not ignore_cell_params and n > 0:
         world._update_params_rows(torch.arange(n, device=dev))
     rng_file = statedir / RNG_FILE
     if restore_rng and rng_file.exists():
         set_rng_state(torch.load(rng_file, map_location="cpu", weights_only=True), world.device)
+
+
+# ---------------------------------------------------------------------------- decomposed worlds
+# A DistributedWorld checkpoints as one shard per rank, written by every rank at the same time from
+# its own device memory (no gather through one process, no CPU World, no re-translation): the
+# strip's owned map rows, its cells' columns with global positions, genomes and labels as packed
+# bytes straight from the arenas, and the rank's random streams. ``assemble_state`` turns the
+# shards into the reference layout (the files ``save_state`` writes) -- by rank 0 right after the
+# save, or offline later for worlds whose global map rank 0 should not hold. Loading takes the
+# shards directly when the rank count matches, and otherwise each rank reads only its strip of the
+# reference files (memory-mapped map rows, its cells from the FASTA).
+SHARD_DIR = "shards"
+SHARD_FILES = ("molecule_map", "cell_map", "cell_molecules", "cell_positions", "cell_lifetimes", "cell_divisions",
+               "genomes", "genome_lens", "labels", "label_lens")
+
+
+def shard_dir(statedir: Path, rank: int, world_size: int) -> Path:
+    return Path(statedir) / SHARD_DIR / f"rank{rank:04d}_of{world_size:04d}"
+
+
+def save_shard(world, statedir: Path) -> Path:
+    """Write this rank's shard of a DistributedWorld (not collective; the caller synchronises)."""
+    import json
+
+    d = shard_dir(statedir, world.rank, world.world_size)
+    d.mkdir(parents=True, exist_ok=True)
+    world._reconcile()
+    g, gl = world._genomes.packed()
+    lab, ll = world._labels.packed()
+    tensors = {
+        "molecule_map": world.owned_molecule_map(),  # (the storage dtype: fp16 / bf16 maps stay small)
+        "cell_map": world.owned_cell_map(),
+        "cell_molecules": world.cell_molecules,
+        "cell_positions": world.global_positions(),
+        "cell_lifetimes": world.cell_lifetimes,
+        "cell_divisions": world.cell_divisions,
+        "genomes": torch.from_numpy(np.array(g, dtype=np.uint8)),
+        "genome_lens": torch.from_numpy(gl),
+        "labels": torch.from_numpy(np.array(lab, dtype=np.uint8)),
+        "label_lens": torch.from_numpy(ll),
+    }
+    for name, t in tensors.items():
+        torch.save(t.detach().cpu().contiguous().clone(), d / f"{name}.pt")
+    torch.save(rng_state(world.device), d / RNG_FILE)
+    meta = {"format": 1, "rank": world.rank, "world_size": world.world_size, "map_size": world.map_size,
+            "H": world.H, "row0": world.row0, "n_cells": world.n_cells, "n_molecules": world.n_molecules,
+            "map_dtype": str(world.__dict__.get("map_dtype", torch.float32)).replace("torch.", ""), "xcall": int(world.__dict__.get("_xcall", 0)),
+            "xseed": int(world.__dict__.get("_xseed", 0)),
+            # (the arenas' length bounds: the strip-boundary recombination sizes its exchange by them)
+            "genome_width": int(world._genomes.width), "label_width": int(world._labels.width)}
+    (d / "meta.json").write_text(json.dumps(meta))
+    return d
+
+
+def shard_metas(statedir: Path) -> list[dict]:
+    """The metas of the shards under ``statedir`` (sorted by rank; empty without shards). Raises if
+    the shards of more than one rank count are mixed or a rank is missing."""
+    import json
+
+    root = Path(statedir) / SHARD_DIR
+    if not root.is_dir():
+        return []
+    metas = sorted((json.loads((p / "meta.json").read_text()) for p in root.iterdir() if (p / "meta.json").exists()),
+                   key=lambda m: m["rank"])
+    if not metas:
+        return []
+    n = metas[0]["world_size"]
+    if [m["rank"] for m in metas] != list(range(n)) or any(m["world_size"] != n for m in metas):
+        raise ValueError(f"{root}: incomplete or mixed shards ({[(m['rank'], m['world_size']) for m in metas]})")
+    return metas
+
+
+def _ld(path: Path, device="cpu", mmap: bool = False) -> torch.Tensor:
+    return torch.load(path, map_location=device, weights_only=True, mmap=mmap)
+
+
+def assemble_state(statedir: Path) -> None:
+    """Write the reference layout (``cell_*.pt``, ``molecule_map.pt``, ``cells.fasta``,
+    ``rng_state.pt`` of rank 0) into ``statedir`` from its shards: maps stacked by rows, cells
+    numbered rank by rank (the global index space of ``DistributedWorld``). The result is byte-equal
+    to what a gathered single-process save of the same world writes."""
+    statedir = Path(statedir)
+    metas = shard_metas(statedir)
+    if not metas:
+        raise FileNotFoundError(f"{statedir}: no shards")
+    dirs = [shard_dir(statedir, m["rank"], m["world_size"]) for m in metas]
+    mm = torch.cat([_ld(d / "molecule_map.pt", mmap=True).to(torch.float32) for d in dirs], dim=1)
+    torch.save(mm, statedir / "molecule_map.pt")
+    del mm
+    for name, dt in (("cell_map", torch.bool), ("cell_molecules", torch.float32), ("cell_positions", torch.int32),
+                     ("cell_lifetimes", torch.int32), ("cell_divisions", torch.int32)):
+        t = torch.cat([_ld(d / f"{name}.pt", mmap=True) for d in dirs], dim=0).to(dt)
+        torch.save(t, statedir / f"{name}.pt")
+    idx0 = 0
+    for r, d in enumerate(dirs):
+        gl = _ld(d / "genome_lens.pt").numpy()
+        _host().fasta_write(str(statedir / "cells.fasta"), idx0, _ld(d / "genomes.pt").numpy(), gl,
+                            _ld(d / "labels.pt").numpy(), _ld(d / "label_lens.pt").numpy(), r > 0, idx0 > 0)
+        idx0 += int(gl.size)
+    import shutil
+
+    shutil.copyfile(dirs[0] / RNG_FILE, statedir / RNG_FILE)
+
+
+def load_strip(world, statedir: Path, ignore_cell_params: bool = False, restore_rng: bool = False) -> str:
+    """Load this rank's part of a state into a DistributedWorld (collective only through the halo
+    refresh at the end): its own shard when the state holds shards of the same rank count and map
+    (then ``restore_rng`` restores the rank's random streams and the boundary-recombination counter,
+    and a run continues as an uninterrupted one), otherwise its strip of the reference files.
+    Returns ``"shard"`` or ``"reference"``."""
+    statedir = Path(statedir)
+    metas = shard_metas(statedir)
+    lo, H, row0 = world._lo, world.H, world.row0
+    if metas and metas[0]["world_size"] == world.world_size and metas[0]["map_size"] == world.map_size:
+        d = shard_dir(statedir, world.rank, world.world_size)
+        meta = metas[world.rank]
+        if meta["row0"] != row0 or meta["H"] != H:
+            raise ValueError(f"{d}: strip rows {meta['row0']}+{meta['H']} differ from this rank's {row0}+{H}")
+        mm = _ld(d / "molecule_map.pt")
+        gpos = _ld(d / "cell_positions.pt").long()
+        cols = {k: _ld(d / f"{k}.pt") for k in ("cell_molecules", "cell_lifetimes", "cell_divisions")}
+        g, gl = _ld(d / "genomes.pt").numpy(), _ld(d / "genome_lens.pt").numpy()
+        lab, ll = _ld(d / "labels.pt").numpy(), _ld(d / "label_lens.pt").numpy()
+        mine = None
+        kind = "shard"
+    else:
+        # the reference files: map rows memory-mapped (only this strip's pages are read), the cell
+        # table filtered by global row
+        mm = _ld(statedir / "molecule_map.pt", mmap=True)[:, row0 : row0 + H]
+        gpos_all = _ld(statedir / "cell_positions.pt").long()
+        sel = torch.nonzero((gpos_all[:, 0] >= row0) & (gpos_all[:, 0] < row0 + H)).flatten()
+        gpos = gpos_all[sel]
+        cols = {k: _ld(statedir / f"{k}.pt", mmap=True)[sel] for k in ("cell_molecules", "cell_lifetimes",
+                                                                       "cell_divisions")}
+        g, gl, lab, ll = read_fasta_packed(statedir / "cells.fasta")
+        if int(gl.size) != int(gpos_all.size(0)):
+            raise ValueError(f"{statedir}: {gl.size} FASTA entries for {gpos_all.size(0)} positions")
+        mine = sel.numpy()
+        kind = "reference"
+        meta = None
+    k = int(gpos.size(0))
+    genomes = packed_rows(g, gl, mine) if k else None
+    labels = packed_rows(lab, ll, mine) if k else None
+    lpos = gpos.clone()
+    lpos[:, 0] += lo - row0
+    world._adopt_strip(mm, genomes, labels, lpos.to(torch.int32), cols, params=not ignore_cell_params)
+    if kind == "shard" and restore_rng:
+        set_rng_state(_ld(shard_dir(statedir, world.rank, world.world_size) / RNG_FILE), world.device)
+        # (the strip-boundary recombination streams: a seed shared by all ranks and a call counter)
+        world.__dict__["_xcall"] = int(meta.get("xcall", 0))
+        if "xseed" in meta:
+            world.__dict__["_xseed"] = int(meta["xseed"])
+    if meta is not None:
+        for arena, key in ((world._genomes, "genome_width"), (world._labels, "label_width")):
+            if key in meta and int(meta[key]) > arena.width:
+                arena.reserve(arena.n, int(meta[key]))
+    return kind
 
 
 # ---------------------------------------------------------------------------- world pickles

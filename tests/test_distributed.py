@@ -31,10 +31,10 @@ def _global_world(map_size=16, n=60, seed=3):
     return w
 
 
-def _dworld(map_size, seed=5):
+def _dworld(map_size, seed=5, device="cpu", **kw):
     from magicsoup_amd.parallel import DistributedWorld
 
-    return DistributedWorld(chemistry=_chem(), map_size=map_size, seed=seed)
+    return DistributedWorld(chemistry=_chem(), map_size=map_size, seed=seed, device=device, **kw)
 
 
 def _check_global(w):
@@ -277,6 +277,99 @@ def _body_state_roundtrip(rank, ws, statedir):
 def test_distributed_save_load_state():
     with tempfile.TemporaryDirectory() as d:
         run_ranks(_body_state_roundtrip, 2, d)
+
+
+def _evolve(dw, steps, seed_mol="ATP"):
+    atp = dw.chemistry.molname_2_idx[seed_mol]
+    for _ in range(steps):
+        dw.enzymatic_activity()
+        dw.kill_divide_where(atp, 0.5, 4.0, 2.0, kill_fraction=0.05)
+        dw.recombinate_cells(p=1e-3)
+        dw.mutate_cells(p=1e-3)
+        dw.degrade_molecules()
+        dw.diffuse_molecules()
+        dw.increment_cell_lifetimes()
+
+
+def _state_of(dw):
+    dw.synchronize()
+    return {"pos": dw.global_positions().clone(), "mol": dw.cell_molecules.clone(),
+            "life": dw.cell_lifetimes.clone(), "div": dw.cell_divisions.clone(),
+            "mm": dw.owned_molecule_map().clone(), "cm": dw.owned_cell_map().clone(),
+            "genomes": list(dw.cell_genomes), "labels": list(dw.cell_labels)}
+
+
+def _same_files(a, b, skip=("rng_state.pt",)):
+    import os
+
+    names = sorted(f for f in os.listdir(a) if os.path.isfile(os.path.join(a, f)) and f not in skip)
+    assert names == sorted(f for f in os.listdir(b) if os.path.isfile(os.path.join(b, f)) and f not in skip)
+    for f in names:
+        with open(os.path.join(a, f), "rb") as fa, open(os.path.join(b, f), "rb") as fb:
+            assert fa.read() == fb.read(), f
+    return names
+
+
+def _body_sharded_state(rank, ws, root, device="cpu", kw=None):
+    """save_state writes one shard per rank from the rank's own memory and rank 0 assembles the
+    reference layout from them: byte-equal to the gathered single-process save. Loading takes the
+    shards (the same local state, bit for bit) or, without shards, each rank's strip of the
+    reference files; load -> save reproduces the files; restore_rng resumes exactly."""
+    import os
+    import shutil
+
+    import torch.distributed as dist
+
+    from tests.conftest import gen_genomes
+
+    dw = _dworld(24, seed=13, device=device, **(kw or {}))
+    dw.spawn_cells(gen_genomes(60, 250))
+    _evolve(dw, 3)
+    a, b, c = (os.path.join(root, x) for x in ("sharded", "gathered", "again"))
+    dw.save_state(a)
+    dw.save_state_gathered(b)
+    if rank == 0:
+        names = _same_files(a, b)
+        assert "cells.fasta" in names and "molecule_map.pt" in names
+        # the reference-only copy (no shards) for the strip reader below
+        shutil.copytree(b, os.path.join(root, "refonly"))
+    dist.barrier()
+    ref = _state_of(dw)
+    for src, kind in ((a, "shard"), (os.path.join(root, "refonly"), "reference")):
+        dw2 = _dworld(24, seed=99, device=device, **(kw or {}))
+        dw2.adopt_maps(dw)
+        assert dw2.load_state(src) == kind
+        got = _state_of(dw2)
+        for k in ref:
+            v, w = ref[k], got[k]
+            assert (torch.equal(v, w) if isinstance(v, torch.Tensor) else v == w), (kind, k)
+        p = min(dw.kinetics.N.size(1), dw2.kinetics.N.size(1))
+        assert torch.equal(dw.kinetics.N[: dw.n_cells, :p], dw2.kinetics.N[: dw2.n_cells, :p])
+    dw2.save_state(c)
+    if rank == 0:
+        _same_files(a, c)
+    # exact resume from the shards: save -> 3 steps == load(restore_rng) -> 3 steps
+    d = os.path.join(root, "resume")
+    dw.save_state(d, assemble=False)
+    if rank == 0:
+        assert not os.path.exists(os.path.join(d, "cells.fasta"))
+    _evolve(dw, 3)
+    want = _state_of(dw)
+    dw3 = _dworld(24, seed=5, device=device, **(kw or {}))
+    dw3.adopt_maps(dw)
+    dw3.load_state(d, restore_rng=True)
+    _evolve(dw3, 3)
+    got = _state_of(dw3)
+    for k in want:
+        v, w = want[k], got[k]
+        assert (torch.equal(v, w) if isinstance(v, torch.Tensor) else v == w), ("resume", k)
+    dist.barrier()
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_distributed_sharded_state_matches_gathered(ranks):
+    with tempfile.TemporaryDirectory() as d:
+        run_ranks(_body_sharded_state, ranks, d)
 
 
 def _body_four_ranks(rank, ws):

@@ -538,3 +538,19 @@ def _body_strip_kill_divide_where(rank, ws):
 
 def test_strip_kill_divide_where_matches_masks():
     run_ranks(_body_strip_kill_divide_where, 1, timeout=300, backend="nccl")
+
+
+def test_gpu_sharded_state_matches_gathered(tmp_path):
+    """The sharded checkpoint of GPU strips (2 gloo ranks sharing the device): shards written from
+    device memory, the assembled reference layout byte-equal to the gathered save, shard and
+    reference-file loads bit-exact, load -> save reproducing the files, exact resume."""
+    from tests.test_distributed import _body_sharded_state
+
+    run_ranks(_body_sharded_state, 2, str(tmp_path), "cuda", timeout=600)
+
+
+def test_gpu_sharded_state_virtual_strip_over_rccl(tmp_path):
+    """The same on one rank as a virtual strip over the native RCCL communicator."""
+    from tests.test_distributed import _body_sharded_state
+
+    run_ranks(_body_sharded_state, 1, str(tmp_path), "cuda", {"strips": True}, timeout=300, backend="nccl")
