@@ -38,7 +38,7 @@ constexpr int kChunk = 32;
 constexpr int kNarrowP = 12;  // LDS protein slots of the narrow integrator launch
 constexpr int kWideBlocksPerCU = 2;  // resident blocks per CU of the strided wide launch
 constexpr int kMaxParts = 4;  // speculative mode: 4 parts x 4 iterations in one 16-bit flag set
-// binned launch mode (set_integrate_mode, for A/B on one state: scripts/integrator_bench.py):
+// binned launch mode (set_integrate_mode, for A/B on one state: scripts/lab/integrator_bench.py):
 // bit 0: the wide launch on a side stream next to the narrow one (else serial, wide first); bit 1:
 // the wide bin on a small strided grid (else a full grid); bit 2: 16-lane groups for the narrow
 // launch. Measured at 4096^2 / 50k (3 parts, 4 iterations): serial 532 us, concurrent 558 us,
@@ -514,7 +514,7 @@ __global__ void __launch_bounds__(kBlock) integrate_spec_lds_kernel(IntegrateArg
 // by the protein lanes, all loads independent). Entries past a protein's non-zero count are zero
 // words, which leave every product unchanged, so the protein loops run branch-free to the wave's
 // largest count. Every sum and product runs in the same order as integrate_item (ascending protein
-// / ascending signal), so both paths give bit-identical results (scripts/integrator_bench.py). A
+// / ascending signal), so both paths give bit-identical results (scripts/lab/integrator_bench.py). A
 // cell with more than G active proteins is appended (part 0) to the wide list and integrated by
 // integrate_item with all P protein slots.
 constexpr int kNzReg = 16;  // non-zero signals per protein in the LDS lists (more: the cell goes wide)
@@ -1705,7 +1705,7 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
   // Speculative all-parts path (s <= 128, the whole part range with the write-back, mode bits 3-7
   // clear): the reference's global exit (kinetics.py:846) cuts a part short only when no cell of the
   // whole population still has an impactful correction, which never happened in 40-step runs of any
-  // BASELINE config (scripts/spec_rate.py: all 3 parts at 4 iterations in every step at 10k-50k
+  // BASELINE config (scripts/lab/spec_rate.py: all 3 parts at 4 iterations in every step at 10k-50k
   // cells; a 500-cell world ends early in about half the steps). So every cell runs all parts in one
   // launch, each part starting from the previous part's last candidate: the compaction and
   // stoichiometry staging happen once instead of once per part, no intermediate candidates are
@@ -2013,7 +2013,7 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
     int32_t* total = order + c;  // = c (device count for the list launch)
     uint8_t* na = reinterpret_cast<uint8_t*>(total + 1);
     // off by default: on the flagship state the sorted order was 31 % slower (682 vs 521 us per
-    // 3-part integration, scripts/integrator_bench.py) -- neighbouring cells' parameter rows are
+    // 3-part integration, scripts/lab/integrator_bench.py) -- neighbouring cells' parameter rows are
     // neighbours in memory, and losing that locality costs more than the wasted lanes
     const bool sorted = (g_integrate_mode & 16) != 0;
     // mode bit 5: skip the 64-lane level (the whole wide list takes the LDS path; for A/B)

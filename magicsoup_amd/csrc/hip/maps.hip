@@ -138,7 +138,7 @@ static int stencil_band(int, int, int, int, int) { return g_vband; }
 // clamped to o1 (the halo row below it, already the last row the PF = 0 loop loads). Whole turns of
 // the ring run without a branch (and the fetches themselves are branch-free): the compiler's vmcnt
 // waits only count exactly across straight-line code, so a guard per row made every step wait for
-// all but the newest loads and the ring collapsed to one row in flight (scripts/stencil_lab.hip:
+// all but the newest loads and the ring collapsed to one row in flight (scripts/lab/stencil_lab.hip:
 // 4096^2 x 14 fp32, 360 -> 328-333 us at 3 rows ahead, 64-row bands, 512-768 blocks).
 template <int PF, class Raw, class Fetch, class Step>
 __device__ __forceinline__ void band_loop(int o0, int o1, Raw& first, Raw& spare, Fetch&& fetch, Step&& row_step) {
@@ -887,6 +887,38 @@ void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uin
 void diffuse_corr(int m, uintptr_t totals, double n_pix, uintptr_t corr, uintptr_t stream) {
   if (m <= 0) return;
   diffuse_corr_kernel<<<cdiv(m, 64), 64, 0, S_(stream)>>>(P_<double>(totals), m, n_pix, P_<float>(corr));
+  MS_LAUNCH_CHECK();
+}
+
+// Per-species totals of the owned rows [r_lo, r_hi) of a map in float64, as a reader sees it (the
+// pending correction and degradation applied on the fly, nothing written): one block per (species,
+// chunk of rows) writes a partial, atomically added into out[mol] (zeroed by the caller). A read
+// of the map instead of the full read + write of apply_pending (World.molecule_totals).
+template <class T>
+__global__ void __launch_bounds__(256) map_totals_kernel(const T* __restrict__ map, int R, int C, int r_lo, int r_hi,
+                                                         const float* corr, const float* f, double* out) {
+  const int mol = blockIdx.y;
+  const long long plane = (long long)R * C;
+  const long long lo = (long long)r_lo * C, hi = (long long)r_hi * C;
+  double acc = 0.0;
+  const float sc = f ? f[mol] : 1.0f;
+  for (long long i = lo + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += (long long)gridDim.x * blockDim.x)
+    acc += (double)(corr_in(ld(map + mol * plane + i), corr, mol) * sc);
+  acc = wave_sum_d(acc);
+  __shared__ double sh[4];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out + mol, (sh[0] + sh[1]) + (sh[2] + sh[3]));
+}
+
+void map_totals(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t corr, uintptr_t f, int dtype,
+                uintptr_t out, uintptr_t stream) {
+  if (m <= 0 || r_hi <= r_lo) return;
+  const long long px = (long long)(r_hi - r_lo) * C;
+  const dim3 g((unsigned)std::max<long long>(1, std::min<long long>(cdiv(px, 256 * 8), 512)), (unsigned)m);
+  MS_MAP_DISPATCH(dtype, (map_totals_kernel<T><<<g, 256, 0, S_(stream)>>>(
+                             P_<T>(map), R, C, r_lo, r_hi, corr ? P_<float>(corr) : nullptr,
+                             f ? P_<float>(f) : nullptr, P_<double>(out))));
   MS_LAUNCH_CHECK();
 }
 

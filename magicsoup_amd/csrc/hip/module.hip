@@ -52,6 +52,8 @@ void diffuse_strip(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintp
                    uintptr_t new_corr, double n_pix, int dtype, uintptr_t comm, int up, int down, uintptr_t halo_bufs,
                    uintptr_t halo_stream, uintptr_t stream);
 void apply_pending(int m, long long plane, uintptr_t map, uintptr_t corr, uintptr_t f, int dtype, uintptr_t stream);
+void map_totals(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t corr, uintptr_t f, int dtype,
+                uintptr_t out, uintptr_t stream);
 void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t totals,
                      double n_pix, int dtype, uintptr_t stream);
 void scale_planes(int m, long long plane, uintptr_t map, uintptr_t f, int dtype, uintptr_t stream);
@@ -275,6 +277,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("diffuse_boundary", &msd::diffuse_boundary);
   m.def("diffuse_boundary_partials_len", &msd::diffuse_boundary_partials_len);
   m.def("diffuse_strip", &msd::diffuse_strip);
+  m.def("map_totals", &msd::map_totals, "per-species float64 totals of owned map rows (pending corr / scale applied)");
   m.def("apply_pending", &msd::apply_pending);
   m.def("diffuse_partials_len", &msd::diffuse_partials_len);
   m.def("scale_planes", &msd::scale_planes);

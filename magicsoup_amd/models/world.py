@@ -61,7 +61,7 @@ _DEFER_ENV = os.environ.get("MS_DEFER_GENOME_OPS", "1")
 # instead of waiting for the count on the host first: always (MS_CHAIN_BOUND=1), never (0), or by
 # default for populations up to _CHAIN_BOUND_MAX cells. Small populations are host-bound and gain
 # (1024^2 / 10k: +17 %); at 40-50k cells the bound-sized chain was 3-4 % slower in in-process A/Bs
-# over 400 steps (scripts/knob_ab.py, profiles/r5/devcount/).
+# over 400 steps (scripts/lab/knob_ab.py, profiles/r5/devcount/).
 _CHAIN_BOUND_ENV = os.environ.get("MS_CHAIN_BOUND", "auto")
 _CHAIN_BOUND = _CHAIN_BOUND_ENV != "0"
 _CHAIN_BOUND_MAX = 1 << 30 if _CHAIN_BOUND_ENV == "1" else 16384
@@ -1628,6 +1628,52 @@ class World:
             # (the device's error words -- grid barriers, look-back spins -- of everything issued
             # up to here, including an activity no division has confirmed yet)
             hip_ops.check_placement()
+
+    def molecule_totals(self) -> torch.Tensor:
+        """Per-species amounts, float64 ``(n_molecules, 2)`` on the world's device: column 0 the
+        molecule map (a decomposed world: the whole global map, all-reduced -- collective), column 1
+        all cells' intracellular molecules. Nothing waits on the device: on the GPU the map is read
+        once by a native reduction with the pending diffusion correction / degradation applied on the
+        fly (no full read + write pass to materialise it, as ``world.molecule_map`` would need), and
+        one ``.tolist()`` gives all of it to the host. The reference's per-step molecule log
+        (performance/run_simulation.py:102-113) is :meth:`molecule_means`."""
+        self._reconcile()
+        d = self.__dict__
+        mm = d["_molmap"]
+        m = self.n_molecules
+        out = torch.zeros(m, 2, dtype=torch.float64, device=mm.device)
+        R, C = int(mm.size(1)), int(mm.size(2))
+        lo = 1 if getattr(self, "_exchange_map_halo", None) is not None else 0
+        hi = R - lo
+        if mm.is_cuda:
+            from magicsoup_amd.ops import hip_ops
+
+            tot = torch.zeros(m, dtype=torch.float64, device=mm.device)
+            hip_ops._m().map_totals(m, R, C, lo, hi, mm.data_ptr(), hip_ops._p(d.get("_pending_corr")),
+                                    hip_ops._p(d.get("_pending_scale")), hip_ops._mdt(mm), tot.data_ptr(),
+                                    hip_ops._stream())
+            out[:, 0] = tot
+        else:
+            out[:, 0] = self.molecule_map[:, lo:hi].double().sum(dim=(1, 2))
+        if self.n_cells:
+            out[:, 1] = self.cell_molecules.double().sum(dim=0)
+        reduce = d.get("_allreduce_totals")
+        if reduce is not None:
+            reduce(out)
+        return out
+
+    def molecule_means(self) -> list[float]:
+        """Per-species mean over all pixels and cells, (map total + cell total) / (pixels + cells) --
+        what the reference's macro benchmark logs every step (performance/run_simulation.py:102-113,
+        2m ``.item()`` synchronisations there; one here). Collective for a decomposed world."""
+        t = self.molecule_totals()
+        n = torch.tensor([float(self.n_cells)], dtype=torch.float64, device=t.device)
+        reduce = self.__dict__.get("_allreduce_totals")
+        if reduce is not None:
+            reduce(n)
+        v = torch.cat([t.sum(dim=1), n]).tolist()
+        denom = float(self.map_size) ** 2 + v[-1]
+        return [x / denom for x in v[:-1]]
 
     def enable_timings(self, sync: bool = False) -> None:
         """Time every public operation with HIP events (wall clock on CPU); read with

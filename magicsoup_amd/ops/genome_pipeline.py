@@ -371,7 +371,7 @@ class _PartHost:
 
 
 # why issues on a pending kill_divide's device count were declined (World._chain_bound; the caller
-# then waits for the count): diagnostics for scripts/call_order.py
+# then waits for the count): diagnostics for scripts/lab/call_order.py
 BOUND_DECLINED = {"pending": 0, "caps": 0, "rows": 0, "pool": 0}
 
 

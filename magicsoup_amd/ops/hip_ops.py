@@ -507,7 +507,7 @@ def diffuse(world) -> None:
 
 # The stencil's output buffer sits at an address offset of _MAP_SKEW (mod 2 MiB) against the map's: a
 # read stream and a write stream whose addresses differ by a multiple of 1 MiB hit the same HBM
-# channels at the same time (scripts/stencil_lab.hip, 4096^2 x 14 fp32 on MI355X: a float4 copy
+# channels at the same time (scripts/lab/stencil_lab.hip, 4096^2 x 14 fp32 on MI355X: a float4 copy
 # 5.50 TB/s at offset 0 or 1 MiB, 5.90-5.96 at 4 KiB, 1 MiB + 4 KiB or 2 MiB + 8 KiB; the pipelined
 # stencil 350-355 -> 328-333 us). The two buffers swap every step, so the offset holds both ways.
 _MAP_SKEW = int(os.environ.get("MS_MAP_SKEW", 8192))

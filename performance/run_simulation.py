@@ -84,7 +84,8 @@ def main() -> None:
             totals[k] = totals.get(k, 0.0) + v
         if log:
             rec = {"step": step, "n_cells": world.n_cells, **{f"Time[s]/{k}": round(v, 6) for k, v in times.items()}}
-            rec["mean_molecules"] = world.cell_molecules.mean(0).tolist() if world.n_cells else []
+            # the reference's per-molecule means over map pixels and cells (one synchronisation)
+            rec["Molecules"] = dict(zip([mol.name for mol in CHEMISTRY.molecules], world.molecule_means()))
             log.write(json.dumps(rec) + "\n")
     wall = time.perf_counter() - t_start
     summary = {

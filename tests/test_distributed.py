@@ -646,3 +646,25 @@ def _body_exchange_contract(rank, ws):
 @pytest.mark.parametrize("ws", [2, 3, 4])
 def test_exchange_skips_empty_ops_on_both_sides(ws):
     run_ranks(_body_exchange_contract, ws)
+
+
+def _body_molecule_totals(rank, ws):
+    """molecule_totals / molecule_means of a decomposed world equal the gathered world's."""
+    from tests.conftest import gen_genomes
+
+    dw = _dworld(16, seed=3)
+    dw.spawn_cells(gen_genomes(30, 200))
+    dw.enzymatic_activity()
+    dw.diffuse_molecules()
+    t = dw.molecule_totals()
+    means = dw.molecule_means()
+    full = dw.gather()
+    if rank == 0:
+        want = torch.stack([full.molecule_map.double().sum(dim=(1, 2)), full.cell_molecules.double().sum(0)], dim=1)
+        assert torch.allclose(t, want, rtol=1e-9, atol=1e-6)
+        assert means == pytest.approx(full.molecule_means(), rel=1e-9)
+
+
+@pytest.mark.one_comm_mode
+def test_distributed_molecule_totals():
+    run_ranks(_body_molecule_totals, 2)

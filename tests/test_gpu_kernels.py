@@ -236,6 +236,57 @@ def test_permeation_matches_host():
     assert torch.allclose(wg.molecule_map.cpu(), wc.molecule_map, rtol=1e-6, atol=1e-6)
 
 
+def _torch_diffuse_permeate(w, mm: torch.Tensor, cm: torch.Tensor, pos: torch.Tensor):
+    """The reference's diffuse_molecules (world.py:627-665) in plain fp32 torch on the GPU: one
+    circular Conv2d per molecule with the mass correction and clamp, then permeation between each
+    cell and its pixel. Independent of the host core."""
+    import torch.nn.functional as F
+
+    S = mm.size(1)
+    mm = mm.clone()
+    for i, (a, b) in enumerate(w._diffusion):
+        k = torch.tensor([[a, a, a], [a, b, a], [a, a, a]], dtype=torch.float32, device=mm.device).view(1, 1, 3, 3)
+        x = mm[i].view(1, 1, S, S)
+        before = x.sum()
+        y = F.conv2d(F.pad(x, (1, 1, 1, 1), mode="circular"), k).view(S, S)
+        y = y + (before - y.sum()) / (S * S)
+        mm[i] = y.clamp(min=0.0)
+    m = w.n_molecules
+    X = torch.cat([cm, mm[:, pos[:, 0], pos[:, 1]].T], dim=1)
+    for i, p in enumerate(w._permeation):
+        d_int = X[:, i] * p
+        d_ext = X[:, i + m] * p
+        X[:, i] += d_ext - d_int
+        X[:, i + m] += d_int - d_ext
+    mm[:, pos[:, 0], pos[:, 1]] = X[:, m:].T
+    return mm, X[:, :m]
+
+
+@pytest.mark.parametrize("size", [64, 255, 1000])
+def test_diffusion_and_permeation_match_torch_conv_oracle(size):
+    """World.diffuse_molecules (register-sliding stencil, deferred mass correction, permeation
+    kernel) against the reference's torch ops directly on the GPU -- the oracle the host core is
+    checked against on the CPU (tests/test_world.py), so the GPU path is pinned independently."""
+    w = _world("cuda", map_size=size, n=min(400, size * size // 8))
+    w.synchronize()
+    pos = w.cell_positions.long()
+    mm, cm = _torch_diffuse_permeate(w, w.molecule_map.float(), w.cell_molecules.clone(), pos)
+    w.diffuse_molecules()
+    got_mm, got_cm = w.molecule_map.float(), w.cell_molecules
+    # (summation orders differ: the conv's reduction tree vs the stencil's and the correction's)
+    assert torch.allclose(got_mm, mm, rtol=2e-5, atol=2e-5), (got_mm - mm).abs().max()
+    assert torch.allclose(got_cm, cm, rtol=2e-5, atol=2e-5), (got_cm - cm).abs().max()
+    # and three steps with degradation folded into the stencil (the pending scale)
+    for _ in range(3):
+        mm = mm * torch.tensor(w._mol_degrads, device="cuda").view(-1, 1, 1)
+        cm = cm * torch.tensor(w._mol_degrads, device="cuda").view(1, -1)
+        mm, cm = _torch_diffuse_permeate(w, mm, cm, pos)
+        w.degrade_molecules()
+        w.diffuse_molecules()
+    assert torch.allclose(w.molecule_map.float(), mm, rtol=1e-4, atol=1e-4), (w.molecule_map.float() - mm).abs().max()
+    assert torch.allclose(w.cell_molecules, cm, rtol=1e-4, atol=1e-4)
+
+
 def test_neighbors_match_host():
     wc = _world("cpu", map_size=32, n=600)
     wg = _copy_world_cpu_to_gpu(wc)
@@ -1631,3 +1682,30 @@ def test_place_split_single_pass_matches_two_pass(k):
         assert st[8:12].tolist() == [int((cls == 2).sum()), 12, 16, 14]
     for a, b in zip(outs[:2], outs[2:]):
         assert all(torch.equal(u, v) for u, v in zip(a[2:], b[2:]))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_molecule_totals_match_torch_sums(dtype):
+    """World.molecule_totals reads the map once with the pending diffusion correction and
+    degradation applied on the fly: equal (to float64 summation order) to torch sums over the
+    materialised map and the cell molecules; molecule_means is the reference's logged quantity."""
+    w = _world("cuda", map_size=300, n=500)
+    if dtype != torch.float32:
+        w.__dict__["map_dtype"] = dtype
+        w.molecule_map = w.molecule_map.to(dtype)
+    w.enzymatic_activity()
+    w.degrade_molecules()
+    w.diffuse_molecules()
+    w.degrade_molecules()  # (a pending scale on top of the pending correction)
+    assert w.__dict__.get("_pending_corr") is not None and w.__dict__.get("_pending_scale") is not None
+    t = w.molecule_totals().cpu()
+    mm = w.molecule_map.double()  # (materialises the pending state)
+    want = torch.stack([mm.sum(dim=(1, 2)).cpu(), w.cell_molecules.double().sum(0).cpu()], dim=1)
+    # (fp16: the materialisation rounds every corrected value to the storage dtype; the totals are
+    # of the fp32 values the readers -- integrator, permeation -- compute with)
+    rel = 1e-9 if dtype == torch.float32 else 2e-4
+    assert torch.allclose(t, want, rtol=rel, atol=1e-6), (t - want).abs().max()
+    means = w.molecule_means()
+    ref = [(float(mm[i].sum()) + float(w.cell_molecules[:, i].double().sum())) / (300 * 300 + w.n_cells)
+           for i in range(w.n_molecules)]
+    assert means == pytest.approx(ref, rel=rel)
