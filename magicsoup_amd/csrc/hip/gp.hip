@@ -13,6 +13,7 @@
 #include <tuple>
 
 #include "hip_common.h"
+#include "params.h"
 
 namespace py = pybind11;
 
@@ -43,7 +44,7 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
                   uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
                   uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
                   uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t W, uintptr_t Q, uintptr_t overflow,
-                  uintptr_t dn, uintptr_t stream);
+                  uintptr_t dn, uintptr_t roff, uintptr_t stream);
 int translate_lds_max();  // genetics.hip: the longest genome of the LDS translation pass
 void mut_count_select(int n, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
                       uintptr_t gflags, uintptr_t opflags, uintptr_t sel, uintptr_t out_dev, int cap, uintptr_t cand,
@@ -88,44 +89,35 @@ __global__ void __launch_bounds__(256) gp_zero_kernel(int cap, const int* dn, lo
     buf[i] = 0;
 }
 
-// One workgroup: proteome-shape checks, fresh parameter rows and the call's status {rebuilt, op
-// flags, row counter, count} into its pinned slot. Fresh row j is base + j (dense storage tail) or
-// free[base + j] (recycled rows of removed cells, Kinetics._recycle_rows); row_cap bounds the counter.
+// One workgroup: proteome-shape checks, fresh parameter records (params.h: each cell's proteins
+// as consecutive records from the bump counter *rtop, which the kinetics storage owns) and the
+// call's status {rebuilt, op flags, record counter, count} into its pinned slot. A cell whose
+// records do not fit below rec_cap keeps its old ones and is flagged for a host rebuild; a proteome
+// longer than the token slots is built from its first Pcap proteins and flagged as well.
 constexpr int kFlagTranslateBit = 1, kFlagRowsBit = 4;  // select.hip DevFlag
 __global__ void __launch_bounds__(1024) gp_check_assign_kernel(int cap, int lcap, const int* dn, const int32_t* counts,
                                                                const int32_t* ndom, const int32_t* long_count,
                                                                int32_t* per, int Pcap, int Dcap, const int64_t* cells,
-                                                               int64_t* slot, long long* d_rows, long long row_cap,
-                                                               const int64_t* free,
-                                                               int32_t* rows_out, int* opflags, const int* stat_cnt,
+                                                               int64_t* slot, long long* rtop, long long rec_cap,
+                                                               int64_t* roff, int* opflags, const int* stat_cnt,
                                                                long long* status) {
   const int n = min(*dn, cap);
-  const long long base = *d_rows;
   if (threadIdx.x == 0) {
     if (*dn > cap) atomicOr(opflags, 2);  // kFlagCapacity
     if (*long_count > lcap) atomicOr(opflags, kFlagTranslateBit);  // more long genomes than global slots
   }
   for (int j = threadIdx.x; j < n; j += blockDim.x) {
     const int p = counts[2 * j] + counts[2 * j + 1];
-    per[j] = p;
     if (p > Pcap || ndom[2 * j] > Dcap || ndom[2 * j + 1] > Dcap) atomicOr(opflags, kFlagTranslateBit);
-    const long long r = base + j;
-    if (r >= row_cap) {
-      atomicOr(opflags, kFlagRowsBit);
-      rows_out[j] = -1;  // the build skips it; the host rebuilds the cell
-      continue;
-    }
-    const long long row = free ? free[r] : r;
-    rows_out[j] = (int32_t)row;
-    slot[cells[j]] = row;
+    per[j] = p < Pcap ? p : Pcap;
   }
   __syncthreads();
+  assign_records_block(n, per, cells, slot, rtop, rec_cap, Pcap, roff, opflags, kFlagRowsBit);
+  __syncthreads();
   if (threadIdx.x == 0) {
-    const long long nr = base + n < row_cap ? base + n : row_cap;
-    *d_rows = nr;
     status[0] = *dn;
     status[1] = __hip_atomic_load(opflags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    status[2] = nr;
+    status[2] = *rtop;
     status[3] = *stat_cnt;
   }
 }
@@ -141,11 +133,10 @@ struct GpGen {  // translation LUTs (Genetics.device_luts)
   uintptr_t small = 0, dom_type = 0, two_codon = 0;
   int dt_entries = 0, dom_size = 0, dom_type_size = 0;
 };
-struct GpKin {  // parameter storage (capacity rows) + token LUTs + cell -> row map
-  uintptr_t N = 0, Nf = 0, Nb = 0, A = 0, Kmr = 0, Kmf = 0, Kmb = 0, Vmax = 0, Ke = 0;
-  uintptr_t W = 0, Q = 0, overflow = 0, slot = 0, free = 0;
+struct GpKin {  // ragged parameter records (params.h) + token LUTs + the cell -> records map
+  uintptr_t Kmr = 0, W = 0, Q = 0, overflow = 0, slot = 0, rtop = 0;
   int P = 0, s = 0;
-  long long row_cap = 0;
+  long long rec_cap = 0;
   uintptr_t vmax = 0, km = 0, signs = 0, hills = 0, react = 0, trnsp = 0, eff = 0, energies = 0;
   int nw = 0, nk = 0, nsg = 0, nh = 0, nv = 0;
   float abs_temp = 0.f, gas = 0.f;
@@ -179,7 +170,7 @@ size_t rebuild_bytes(int cap, int P, int dcap, int width) {
   c.take(4 * (size_t)cap);                        // long list
   c.take(16);                                     // long count
   c.take(4 * (size_t)cap);                        // proteins per cell
-  c.take(4 * (size_t)cap);                        // rows out
+  c.take(8 * (size_t)cap);                        // record offsets
   c.take(4 * (size_t)cap * P * dcap * 5);         // tokens
   return c.off + 256;
 }
@@ -192,7 +183,7 @@ int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const Gp
   const uintptr_t gslot = c.take((size_t)lcap * translate_slot_bytes(a.width));
   const uintptr_t counts = c.take(8 * (size_t)cap), ndom = c.take(8 * (size_t)cap);
   const uintptr_t long_list = c.take(4 * (size_t)cap), long_count = c.take(16);
-  const uintptr_t per = c.take(4 * (size_t)cap), rows_out = c.take(4 * (size_t)cap);
+  const uintptr_t per = c.take(4 * (size_t)cap), roff = c.take(8 * (size_t)cap);
   const uintptr_t tokens = c.take(4 * (size_t)cap * k.P * dcap * 5);
   const long long row = (long long)k.P * dcap * 5;
   const unsigned gz = (unsigned)std::max<long long>(1, std::min<long long>(cdiv((long long)cap * row, 256), 1024));
@@ -207,13 +198,12 @@ int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const Gp
   auto sl = status_slot();
   gp_check_assign_kernel<<<1, 1024, 0, s>>>(cap, lcap, P_<int>(dcnt), P_<int32_t>(counts), P_<int32_t>(ndom),
                                             P_<int32_t>(long_count), P_<int32_t>(per), k.P, dcap, P_<int64_t>(cells),
-                                            P_<int64_t>(k.slot), P_<long long>(a.d_rows), k.row_cap,
-                                            k.free ? P_<int64_t>(k.free) : nullptr, P_<int32_t>(rows_out),
+                                            P_<int64_t>(k.slot), P_<long long>(k.rtop), k.rec_cap, P_<int64_t>(roff),
                                             P_<int>(a.opflags), P_<int>(stat_cnt), sl.first);
   MS_LAUNCH_CHECK();
-  build_params(cap, k.P, dcap, k.P, k.s, tokens, rows_out, k.vmax, k.nw, k.km, k.nk, k.signs, k.nsg, k.hills, k.nh,
-               k.react, k.trnsp, k.eff, k.nv, k.energies, k.abs_temp, k.gas, k.N, k.Nf, k.Nb, k.A, k.Kmr, k.Kmf, k.Kmb,
-               k.Vmax, k.Ke, per, k.W, k.Q, k.overflow, dcnt, st);
+  build_params(cap, k.P, dcap, k.P, k.s, tokens, 0, k.vmax, k.nw, k.km, k.nk, k.signs, k.nsg, k.hills, k.nh,
+               k.react, k.trnsp, k.eff, k.nv, k.energies, k.abs_temp, k.gas, 0, 0, 0, 0, k.Kmr, 0, 0, 0, 0, per, k.W, k.Q,
+               k.overflow, dcnt, roff, st);
   return sl.second;
 }
 }  // namespace
@@ -302,7 +292,7 @@ __global__ void gp_begin_kernel(int* opflags, int* gflags, long long* d_rows, lo
   *opflags = 0;
   if (fresh) {
     *gflags = 0;
-    *d_rows = nrows;
+    if (nrows >= 0) *d_rows = nrows;  // (-1: the counter is the kinetics' record counter, kept)
   }
 }
 
@@ -418,7 +408,7 @@ __global__ void gp_begin3_kernel(int* f0, int* f1, int* f2, int* gflags, long lo
   *f2 = 0;
   if (fresh) {
     *gflags = 0;
-    *d_rows = nrows;
+    if (nrows >= 0) *d_rows = nrows;  // (-1: the counter is the kinetics' record counter, kept)
   }
 }
 
@@ -531,13 +521,11 @@ void bind_gp(py::module_& m) {
       .def_readwrite("dom_size", &GpGen::dom_size).def_readwrite("dom_type_size", &GpGen::dom_type_size);
   py::class_<GpKin>(m, "GpKin", py::module_local())
       .def(py::init<>())
-      .def_readwrite("N", &GpKin::N).def_readwrite("Nf", &GpKin::Nf).def_readwrite("Nb", &GpKin::Nb)
-      .def_readwrite("A", &GpKin::A).def_readwrite("Kmr", &GpKin::Kmr).def_readwrite("Kmf", &GpKin::Kmf)
-      .def_readwrite("Kmb", &GpKin::Kmb).def_readwrite("Vmax", &GpKin::Vmax).def_readwrite("Ke", &GpKin::Ke)
+      .def_readwrite("Kmr", &GpKin::Kmr)
       .def_readwrite("W", &GpKin::W).def_readwrite("Q", &GpKin::Q).def_readwrite("overflow", &GpKin::overflow)
-      .def_readwrite("slot", &GpKin::slot).def_readwrite("free", &GpKin::free).def_readwrite("P", &GpKin::P)
+      .def_readwrite("slot", &GpKin::slot).def_readwrite("rtop", &GpKin::rtop).def_readwrite("P", &GpKin::P)
       .def_readwrite("s", &GpKin::s)
-      .def_readwrite("row_cap", &GpKin::row_cap).def_readwrite("vmax", &GpKin::vmax).def_readwrite("km", &GpKin::km)
+      .def_readwrite("rec_cap", &GpKin::rec_cap).def_readwrite("vmax", &GpKin::vmax).def_readwrite("km", &GpKin::km)
       .def_readwrite("signs", &GpKin::signs).def_readwrite("hills", &GpKin::hills)
       .def_readwrite("react", &GpKin::react).def_readwrite("trnsp", &GpKin::trnsp).def_readwrite("eff", &GpKin::eff)
       .def_readwrite("energies", &GpKin::energies).def_readwrite("nw", &GpKin::nw).def_readwrite("nk", &GpKin::nk)

@@ -18,6 +18,7 @@
 #include <algorithm>
 
 #include "hip_common.h"
+#include "params.h"
 #include "map_types.h"
 #include "ms_kinetics.h"
 
@@ -168,7 +169,9 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
   const bool valid = valid0 && (unsigned)cell0 < (unsigned)a.c;  // (a list entry is a cell index)
   const int cell = valid ? cell0 : 0;
   const int P = a.P, s = a.s, SP = a.sp, Ps = a.Ps;
-  const size_t prow = valid ? (a.prow ? (size_t)a.prow[cell] : (size_t)cell) : 0;  // parameter row
+  size_t pbase;  // the cell's first parameter record (params.h) ...
+  int pc;        // ... and its proteins (records past them: absent, i.e. inactive)
+  prot_range(a.prow, cell, P, valid, pbase, pc);
 
   int* words = smem + slot * a.slot_words;
   int* act = words + Ps * SP;
@@ -200,9 +203,9 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
     for (int p0 = 0; p0 < P; p0 += G) {
       const int p = p0 + lane;
       float4 q = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      if (valid && p < P) q = a.Q[prow * P + p];
+      if (p < pc) q = a.Q[pbase + p];
       const float vm = q.x * a.trim;
-      const bool on = valid && p < P && !(vm <= 0.0f);  // NaN stays active (propagates like the reference)
+      const bool on = p < pc && !(vm <= 0.0f);  // NaN stays active (propagates like the reference)
       const unsigned long long bal = __ballot(on);
       unsigned long long gm;
       if constexpr (G == 64) gm = bal;
@@ -233,7 +236,7 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int k = k0 + u;
-        w[u] = (k < na && j < s) ? a.W[(prow * P + act[k]) * s + j] : 0;
+        w[u] = (k < na && j < s) ? a.W[(pbase + act[k]) * s + j] : 0;
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -265,7 +268,7 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
   // ---- 4. velocities (protein phase)
   for (int k = lane; k < na; k += G) {
     const int* wr = words + k * SP;
-    const float* kmr = a.Kmr + (prow * P + act[k]) * s;
+    const float* kmr = a.Kmr + (pbase + act[k]) * s;
     const uint8_t* nz = nzj + k * s;
     const int cnt = nnz[k];
     float xf = 1.0f, xb = 1.0f, ar = 1.0f;
@@ -607,7 +610,11 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   const bool listed = listed0 && (unsigned)cell0 < (unsigned)a.c;  // (a list entry is a cell index)
   const int cell = listed ? cell0 : 0;
   const int P = a.P, s = a.s;
-  const size_t prow = listed ? (a.prow ? (size_t)a.prow[cell] : (size_t)cell) : 0;
+  size_t pbase;  // the cell's parameter records (params.h)
+  int pc;
+  prot_range(a.prow, cell, P, listed, pbase, pc);
+  // wave-uniform bound of the protein scan (its ballots need every lane of the wave)
+  const int pc_w = __builtin_amdgcn_readfirstlane(wave_max(pc));
 
   constexpr int ES = ent_stride<NZ>(), JS = jl_stride<NZ>();
   constexpr int SW = fast_slot_words<G, NZ, SPL>();
@@ -636,13 +643,13 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   const int nparts = spec ? a.spec_parts : 1;
   int na = 0;
   bool trim_diff = false;  // speculative mode: every part must see the same active set
-  for (int p0 = 0; p0 < P; p0 += G) {
+  for (int p0 = 0; p0 < pc_w; p0 += G) {
     const int p = p0 + lane;
     float vmax = 0.0f;
-    if (listed && p < P) vmax = a.Q[prow * P + p].x;
+    if (p < pc) vmax = a.Q[pbase + p].x;
     const float vm = vmax * (spec ? a.trims[0] : a.trim);
-    const bool on = listed && p < P && !(vm <= 0.0f);
-    for (int q = 1; q < nparts; ++q) trim_diff |= on != (listed && p < P && !(vmax * trim_of(a, q) <= 0.0f));
+    const bool on = p < pc && !(vm <= 0.0f);
+    for (int q = 1; q < nparts; ++q) trim_diff |= on != (p < pc && !(vmax * trim_of(a, q) <= 0.0f));
     const unsigned long long gm = group_ballot<G>(on);
     const int k = na + __popcll(gm & ((1ull << lane) - 1ull)) - grp * G;
     if (on && k >= 0 && k < G) act[k] = p;
@@ -671,7 +678,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int k = k0 + u, j = lane + h * G;
-        w[h][u] = (k < nac && listed && j < s) ? a.W[(prow * P + act[k]) * s + j] : 0;
+        w[h][u] = (k < nac && listed && j < s) ? a.W[(pbase + act[k]) * s + j] : 0;
       }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -748,7 +755,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   int nfs_p = 0, nbs_p = 0;  // any forward / backward exponent of this protein
   if (prot) {
     pk = act[lane];
-    const float4 q4 = a.Q[prow * P + pk];
+    const float4 q4 = a.Q[pbase + pk];
     vraw = q4.x;
     kmf = q4.y;
     kmb = q4.z;
@@ -859,7 +866,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   // ---- 4. velocity (protein lane; entries past the count are zero words: no effect)
   float v = 0.0f;
   {
-    const float* kmr = a.Kmr + (prow * P + pk) * s;
+    const float* kmr = a.Kmr + (pbase + pk) * s;
     float xf = 1.0f, xb = 1.0f, ar = 1.0f;
 #pragma unroll
     for (int q = 0; q < NZ; ++q) asm volatile("" : "+v"(e16[q >> 1]));  // (no hoisting, see signal_pass)
@@ -1329,9 +1336,11 @@ __global__ void __launch_bounds__(256) bin_cells_kernel(int c, int P, int pn, co
                                                         int32_t* lists, int32_t* counts) {
   const int cell = blockIdx.x * blockDim.x + threadIdx.x;
   if (cell >= c) return;
-  const size_t r = prow ? (size_t)prow[cell] : (size_t)cell;
+  size_t r;
+  int pc;
+  prot_range(prow, cell, P, true, r, pc);
   int na = 0;
-  for (int p = 0; p < P; ++p) na += !(Q[r * P + p].x <= 0.0f);
+  for (int p = 0; p < pc; ++p) na += !(Q[r + p].x <= 0.0f);
   if (na <= pn) lists[atomicAdd(counts, 1)] = cell;
   else lists[c + atomicAdd(counts + 1, 1)] = cell;
 }
@@ -1400,9 +1409,11 @@ __global__ void __launch_bounds__(256) na_hist_kernel(int c, int P, const float4
   __syncthreads();
   const int cell = blockIdx.x * blockDim.x + threadIdx.x;
   if (cell < c) {
-    const size_t r = prow ? (size_t)prow[cell] : (size_t)cell;
+    size_t r;
+    int pc;
+    prot_range(prow, cell, P, true, r, pc);
     int na = 0;
-    for (int p = 0; p < P; ++p) na += !(Q[r * P + p].x <= 0.0f);
+    for (int p = 0; p < pc; ++p) na += !(Q[r + p].x <= 0.0f);
     const int b = na > 32 ? 33 : na;
     na_out[cell] = (uint8_t)b;
     atomicAdd(&h[b], 1);
@@ -1497,11 +1508,14 @@ __global__ void __launch_bounds__(kBlock) gather_bin_kernel(int c, int s, int m,
     snap[(size_t)cell * ms::kSnap * s + j] = x;
   }
   if constexpr (G == 64) return;
-  const size_t r = ok ? (prow ? (size_t)prow[cell] : (size_t)cell) : 0;
+  size_t r;
+  int pc;
+  prot_range(prow, cell, P, ok, r, pc);
+  const int pc_w = __builtin_amdgcn_readfirstlane(wave_max(pc));  // (uniform bound: the ballots)
   int na = 0;
-  for (int p0 = 0; p0 < P; p0 += 32) {
+  for (int p0 = 0; p0 < pc_w; p0 += 32) {
     const int p = p0 + lane;
-    const bool on = ok && p < P && !(Q[r * P + p].x * trim0 <= 0.0f);
+    const bool on = p < pc && !(Q[r + p].x * trim0 <= 0.0f);
     na += __popcll(group_ballot<32>(on));
   }
   if (ok && lane == 0 && na > 32) wide_list[atomicAdd(reinterpret_cast<int*>(wide), 1)] = cell;
@@ -1548,6 +1562,9 @@ struct BuildArgs {
   float4* Q;
   int* overflow;
   const int* dn;  // optional device row count (<= n; n is then the capacity)
+  // ragged storage (params.h): the first record of item ci (-1: nothing to write), its proteins
+  // nprot[ci] are records roff[ci] + p; the padding proteins get no records (rows / Pt unused)
+  const int64_t* roff;
 };
 
 __device__ __forceinline__ int lut(int t, int lim) { return (t >= 0 && t < lim) ? t : 0; }
@@ -1560,9 +1577,16 @@ __device__ __forceinline__ int lut(int t, int lim) { return (t >= 0 && t < lim) 
 template <int G>
 __device__ __forceinline__ void build_group(const BuildArgs& b, long long grp, int lane) {
   const int ci = (int)(grp / b.Pt), p = (int)(grp - (long long)ci * b.Pt);
-  if (b.rows[ci] < 0) return;  // no row assigned (device pipeline ran out of rows)
-  const size_t row = (size_t)b.rows[ci];
-  const size_t o2 = row * b.Pt + p, o3 = o2 * b.s;
+  size_t o2;
+  if (b.roff) {
+    const long long ro = b.roff[ci];
+    if (ro < 0 || p >= (b.nprot ? b.nprot[ci] : b.P)) return;  // no records / a padding protein
+    o2 = (size_t)ro + p;
+  } else {
+    if (b.rows[ci] < 0) return;  // no row assigned
+    o2 = (size_t)b.rows[ci] * b.Pt + p;
+  }
+  const size_t o3 = o2 * b.s;
   const int32_t* pt = b.tokens + ((size_t)ci * b.P + (p < b.P ? p : 0)) * b.D * 5;
   // (b.full: the eight unpacked parameter tensors are held too; compact storage has W / Q / Kmr only)
   if (b.nprot && b.nprot[ci] == 0) {  // empty proteome: unset_cell_params semantics (all zero)
@@ -2212,7 +2236,7 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
                   uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
                   uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
                   uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t W, uintptr_t Q, uintptr_t overflow,
-                  uintptr_t dn, uintptr_t stream) {
+                  uintptr_t dn, uintptr_t roff, uintptr_t stream) {
   if (n <= 0 || Pt <= 0) return;
   if ((W == 0) != (Q == 0) || (W != 0 && overflow == 0)) throw std::invalid_argument("build_params: W, Q, overflow");
   if ((N == 0 || Ke == 0) && W == 0) throw std::invalid_argument("build_params: no parameter layout to write");
@@ -2230,6 +2254,8 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
   b.Kmr = P_<float>(Kmr); b.Kmf = P_<float>(Kmf); b.Kmb = P_<float>(Kmb); b.Vmax = P_<float>(Vmax); b.Ke = P_<float>(Ke);
   b.W = W ? P_<int32_t>(W) : nullptr; b.Q = Q ? P_<float4>(Q) : nullptr; b.overflow = P_<int>(overflow);
   b.dn = dn ? P_<int>(dn) : nullptr;
+  b.roff = roff ? P_<int64_t>(roff) : nullptr;
+  if (b.roff && (b.N || b.Ke)) throw std::invalid_argument("build_params: ragged records hold the packed layout only");
   const long long groups = (long long)n * Pt;
   // with a device count the grid is capped and strides (the host passes the capacity as n)
   auto grid = [&](int g) { const unsigned full = cdiv(groups * g, kBlock); return dn ? std::min(full, 4096u) : full; };
@@ -2239,6 +2265,95 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
   if (s <= 16) build_params_kernel<16><<<grid(16), kBlock, 0, S_(stream)>>>(b);
   else if (s <= 32) build_params_kernel<32><<<grid(32), kBlock, 0, S_(stream)>>>(b);
   else build_params_kernel<64><<<grid(64), kBlock, 0, S_(stream)>>>(b);
+  MS_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Ragged parameter records (params.h): assignment, dense views, collection
+
+__global__ void __launch_bounds__(1024) assign_records_kernel(int n, const int* dn, const int32_t* nprot,
+                                                              const int64_t* cells, int64_t* slot, long long* rtop,
+                                                              long long rcap, int width, int64_t* roff, int* flags) {
+  const int ne = dn ? min(*dn, n) : n;
+  assign_records_block(ne, nprot, cells, slot, rtop, rcap, width, roff, flags, 1);
+}
+
+// The dense (n, P, s) / (n, P) view of the records (Kinetics._materialize): protein p < count is its
+// record, count <= p < width the build's padding (Vmax 0, Kmf = Kmb = EPS, Ke 1, Kmr 1, words 0 --
+// what build_group computes for a protein without domains), beyond that zeros (a widening).
+__global__ void __launch_bounds__(256) records_to_dense_kernel(int n, int P, int s, const int64_t* slot,
+                                                               const int32_t* W, const float4* Q, const float* Kmr,
+                                                               int32_t* Wd, float4* Qd, float* Kmrd) {
+  const long long total = (long long)n * P * s;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const long long ip = t / s;
+    const int j = (int)(t - ip * s);
+    const int i = (int)(ip / P), p = (int)(ip - (long long)i * P);
+    const long long v = slot ? slot[i] : rec_encode((long long)i * P, P, P);
+    const int cnt = rec_cnt(v), wid = rec_width(v);
+    const long long r = rec_off(v) + p;
+    if (p < cnt) {
+      Wd[t] = W[r * s + j];
+      Kmrd[t] = Kmr[r * s + j];
+    } else {
+      Wd[t] = 0;
+      Kmrd[t] = p < wid ? 1.0f : 0.0f;
+    }
+    if (j == 0)
+      Qd[ip] = p < cnt ? Q[r] : (p < wid ? make_float4(0.0f, ms::kEps, ms::kEps, 1.0f) : make_float4(0.f, 0.f, 0.f, 0.f));
+  }
+}
+
+// Collection: cell i's records move to new_off[i] (an exclusive scan of the counts) in fresh
+// buffers, one 64-lane group per cell; the cell's new slot goes to slot_out (sharers of a record run
+// get a copy each).
+__global__ void __launch_bounds__(256) records_move_kernel(int n, int s, const int64_t* slot, const int64_t* new_off,
+                                                           const int32_t* W, const float4* Q, const float* Kmr,
+                                                           int32_t* W2, float4* Q2, float* Kmr2, int64_t* slot_out) {
+  const int lane = threadIdx.x & 63;
+  const int g0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, ng = (gridDim.x * blockDim.x) >> 6;
+  for (int i = g0; i < n; i += ng) {
+    const long long v = slot[i];
+    const int cnt = rec_cnt(v);
+    const long long src = rec_off(v), dst = new_off[i];
+    const long long words = (long long)cnt * s;
+    for (long long t = lane; t < words; t += 64) {
+      W2[dst * s + t] = W[src * s + t];
+      Kmr2[dst * s + t] = Kmr[src * s + t];
+    }
+    for (int p = lane; p < cnt; p += 64) Q2[dst + p] = Q[src + p];
+    if (lane == 0) slot_out[i] = cnt ? rec_encode(dst, cnt, rec_width(v)) : 0;
+  }
+}
+
+void assign_records(int n, uintptr_t dn, uintptr_t nprot, uintptr_t cells, uintptr_t slot, uintptr_t rtop,
+                    long long rcap, int width, uintptr_t roff, uintptr_t flags, uintptr_t stream) {
+  if (n <= 0) return;
+  if (width < 0 || width > kRecMaxProteins) throw std::invalid_argument("assign_records: protein width too large");
+  if (rcap > (long long)kRecOffMask) throw std::invalid_argument("assign_records: record capacity too large");
+  assign_records_kernel<<<1, 1024, 0, S_(stream)>>>(n, dn ? P_<int>(dn) : nullptr, P_<int32_t>(nprot),
+                                                    cells ? P_<int64_t>(cells) : nullptr, P_<int64_t>(slot),
+                                                    P_<long long>(rtop), rcap, width, P_<int64_t>(roff), P_<int>(flags));
+  MS_LAUNCH_CHECK();
+}
+
+void records_to_dense(int n, int P, int s, uintptr_t slot, uintptr_t W, uintptr_t Q, uintptr_t Kmr, uintptr_t Wd,
+                      uintptr_t Qd, uintptr_t Kmrd, uintptr_t stream) {
+  if (n <= 0 || P <= 0) return;
+  const unsigned g = (unsigned)std::min<long long>(cdiv((long long)n * P * s, 256), 8192);
+  records_to_dense_kernel<<<g, 256, 0, S_(stream)>>>(n, P, s, slot ? P_<int64_t>(slot) : nullptr, P_<int32_t>(W),
+                                                     P_<float4>(Q), P_<float>(Kmr), P_<int32_t>(Wd), P_<float4>(Qd),
+                                                     P_<float>(Kmrd));
+  MS_LAUNCH_CHECK();
+}
+
+void records_move(int n, int s, uintptr_t slot, uintptr_t new_off, uintptr_t W, uintptr_t Q, uintptr_t Kmr,
+                  uintptr_t W2, uintptr_t Q2, uintptr_t Kmr2, uintptr_t slot_out, uintptr_t stream) {
+  if (n <= 0) return;
+  const unsigned g = (unsigned)std::min<long long>(cdiv((long long)n * 64, 256), 8192);
+  records_move_kernel<<<g, 256, 0, S_(stream)>>>(n, s, P_<int64_t>(slot), P_<int64_t>(new_off), P_<int32_t>(W),
+                                                 P_<float4>(Q), P_<float>(Kmr), P_<int32_t>(W2), P_<float4>(Q2),
+                                                 P_<float>(Kmr2), P_<int64_t>(slot_out));
   MS_LAUNCH_CHECK();
 }
 

@@ -111,7 +111,13 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
                   uintptr_t TM, uintptr_t EM, int nv, uintptr_t energies, float abs_temp, float gas, uintptr_t N,
                   uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Kmr, uintptr_t Kmf, uintptr_t Kmb,
                   uintptr_t Vmax, uintptr_t Ke, uintptr_t nprot, uintptr_t W, uintptr_t Q, uintptr_t overflow,
-                  uintptr_t dn, uintptr_t stream);
+                  uintptr_t dn, uintptr_t roff, uintptr_t stream);
+void assign_records(int n, uintptr_t dn, uintptr_t nprot, uintptr_t cells, uintptr_t slot, uintptr_t rtop,
+                    long long rcap, int width, uintptr_t roff, uintptr_t flags, uintptr_t stream);
+void records_to_dense(int n, int P, int s, uintptr_t slot, uintptr_t W, uintptr_t Q, uintptr_t Kmr, uintptr_t Wd,
+                      uintptr_t Qd, uintptr_t Kmrd, uintptr_t stream);
+void records_move(int n, int s, uintptr_t slot, uintptr_t new_off, uintptr_t W, uintptr_t Q, uintptr_t Kmr,
+                  uintptr_t W2, uintptr_t Q2, uintptr_t Kmr2, uintptr_t slot_out, uintptr_t stream);
 void pack_params(long long items, int s, uintptr_t N, uintptr_t Nf, uintptr_t Nb, uintptr_t A, uintptr_t Vmax,
                  uintptr_t Kmf, uintptr_t Kmb, uintptr_t Ke, uintptr_t W, uintptr_t Q, uintptr_t overflow,
                  uintptr_t stream);
@@ -270,6 +276,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("release_static", &msd::release_static);
   msd::bind_events(m);
   m.def("build_params", &msd::build_params);
+  m.def("assign_records", &msd::assign_records, "ragged parameter records for built cells (one workgroup scan)");
+  m.def("records_to_dense", &msd::records_to_dense, "dense (n, P, s) view of the ragged parameter records");
+  m.def("records_move", &msd::records_move, "collection: every cell's records to an exclusive-scan offset");
   m.def("pack_params", &msd::pack_params);
   m.def("diffuse_stencil", &msd::diffuse_stencil);
   m.def("diffuse_correct", &msd::diffuse_correct);

@@ -222,6 +222,35 @@ def _spare_rows(n: int, row_bytes: int) -> int:
     return max(n // 8, min(3 * n, (8 << 30) // max(row_bytes, 1)), 1024)
 
 
+# ragged parameter records (csrc/hip/params.h): slot = offset | count << 36 | build width << 50
+_REC_OFF_BITS = 36
+_REC_CNT_MASK = (1 << 14) - 1
+_MAX_PROTEINS = 8191  # (the widths the host encodes stay below the int64 sign bit)
+
+
+def _rec_code(off: int, cnt: int, width: int) -> int:
+    return int(off) + (int(cnt) << _REC_OFF_BITS) + (int(width) << (_REC_OFF_BITS + 14))
+
+
+def _retire_t(t: torch.Tensor | None) -> None:
+    """A storage tensor about to be dropped while queued work may still read it (see
+    models/strings.py _retire)."""
+    if t is not None and t.is_cuda:
+        t.record_stream(torch.cuda.current_stream(t.device))
+
+
+def _record_flag(kin):
+    """Mapped host word the record assignment sets when records run out (a host build sized its
+    reservation wrong: raised at the next integration, as the int8 overflow flag)."""
+    from magicsoup_amd.ops import hip_ops
+
+    sc = hip_ops._scratch(kin)
+    f = getattr(sc, "rec_flag", None)
+    if f is None:
+        f = sc.rec_flag = hip_ops._HostFlag()
+    return f
+
+
 class Kinetics:
     """Protein work of all cells.
 
@@ -351,20 +380,22 @@ class Kinetics:
         self.set_cell_params_tokens(cell_idxs, tokens)
 
     def set_cell_params_tokens(self, cell_idxs, tokens: torch.Tensor, nprot: torch.Tensor | None = None):
-        """Fused parameter build from dense tokens (n, P, D, 5) int32 for rows ``cell_idxs``;
-        rows with ``nprot == 0`` (if given) are unset."""
+        """Fused parameter build from dense tokens (n, P, D, 5) int32 for cells ``cell_idxs``;
+        cells with ``nprot == 0`` (if given) are unset. On the GPU the cells take fresh records of
+        their proteomes' size (cells may share records: a division's child its parent's)."""
         if tokens.size(1) > self._P():
             self.increase_max_proteins(int(tokens.size(1)))
-        slot = self._slot_tensor()
-        if slot is None:
-            rows = torch.as_tensor(cell_idxs, dtype=torch.int32)
-        else:
-            # rows may be shared (children of a division point at their parent's row): the new
-            # parameters go to fresh rows
-            cells = torch.as_tensor(cell_idxs, device=slot.device).long()
-            fresh = self._alloc_rows(int(cells.numel()))
-            self.__dict__["_slot"][cells] = fresh
-            rows = fresh.to(torch.int32)
+        dev = self._store["Kmr"].device
+        if dev.type == "cuda":
+            self._sync()
+            cells = torch.as_tensor(cell_idxs, device=dev).long().contiguous()
+            if cells.numel() == 0:
+                return
+            tokens = tokens.to(device=dev, dtype=torch.int32).contiguous()
+            roff, nprot = self._alloc_cells(cells, tokens, nprot)
+            kinetics_ops.build_params(self, None, tokens, nprot=nprot, roff=roff)
+            return
+        rows = torch.as_tensor(cell_idxs, dtype=torch.int32)
         kinetics_ops.build_params(self, rows, tokens, nprot=nprot)
 
     def unset_cell_params(self, cell_idxs):
@@ -426,19 +457,33 @@ class Kinetics:
         d["_ncells"] += k
 
     # ---- parameter storage ----
-    # The parameters live in row-storage tensors with spare capacity; cell i's row is _slot[i]
-    # (None: row i). On the GPU, removing cells only compacts the small slot vector and new cells
-    # take fresh rows at the end, so the (c, p, s) rows are not moved on every kill_cells (the
-    # reference copies all parameter tensors there, kinetics.py:667-686). The storage is gathered
-    # back into cell order when it runs out of rows, when p grows, or when a parameter tensor is
-    # read through the public attributes -- users always see dense, cell-ordered tensors they
-    # can modify in place.
+    # CPU (and a GPU world right after its dense tensors were read from Python): dense, cell-ordered
+    # (c, p, s) / (c, p) tensors, as the reference keeps them (kinetics.py:399-409).
+    #
+    # GPU: ragged records (csrc/hip/params.h). Every protein of a cell is one record of a record pool
+    # -- its packed stoichiometry words "_W" (s int32), "Kmr" (s fp32) and "_Q" (Vmax, Kmf, Kmb, Ke) --
+    # and a cell owns a contiguous run of as many records as its proteome has proteins, named by one
+    # int64 per cell (_slot: offset, count, build width). No cell is padded to the population's longest
+    # proteome: a population of 500 nt genomes holds ~10 records per cell instead of the 45-160 protein
+    # slots of a dense row, and widening the protein dimension moves nothing (_pmax is only a bound).
+    # Records are written once: a rebuild takes fresh records from the device bump counter _rtop
+    # (the genome pipeline's chains take theirs on the device, gp.hip), a division's child shares its
+    # parent's, and removing cells only compacts the slot map. When the pool runs out the live records
+    # are compacted into a fresh pool (_collect_records). The host keeps an upper bound _rtop_ub of the
+    # device counter (worst cases added at issue, tightened from the chains' status words), so issuing
+    # a build never waits for the device. Reading a parameter tensor from Python materialises the dense
+    # tensors (records_to_dense: the reference's padding for a cell's missing proteins), which users
+    # may modify in place; the next kernel use packs them back into records.
     @property
     def _store(self) -> dict[str, torch.Tensor]:
         return self.__dict__["_store_d"]
 
     def _P(self) -> int:
-        return int(self._store["Kmr"].size(1))
+        d = self.__dict__
+        if d.get("_slot") is not None:
+            return int(d.get("_pmax", 0))
+        store = self._store
+        return int(store["Kmr"].size(1)) if "Kmr" in store and store["Kmr"].dim() == 3 else 0
 
     def _get_param(self, name: str) -> torch.Tensor:
         self._sync()
@@ -454,7 +499,6 @@ class Kinetics:
         self._sync()
         self._materialize()
         self._drop_packed()
-        d.pop("_zero_row_t", None)
         t = torch.as_tensor(value)
         if not t.is_contiguous():
             t = t.contiguous()
@@ -463,31 +507,58 @@ class Kinetics:
         d.get("_spare", {}).pop(name, None)
 
     def _rows(self, cells):
-        """Storage rows of cells (identity unless cells were removed on the GPU)."""
-        slot = self.__dict__["_slot"]
-        if slot is None:
-            return cells
-        return slot[torch.as_tensor(cells, device=slot.device)]
+        """Dense storage rows of cells (the dense layout is cell ordered)."""
+        return cells
 
     def _slot_tensor(self) -> torch.Tensor | None:
         return self.__dict__["_slot"]
 
     def _enter_slot_mode(self) -> None:
-        """GPU: switch from dense cell-ordered rows to the cell -> row map (identity to start). The
-        map lives in a capacity buffer (plus a spare of the same size for compactions), so the world
-        can move it together with its per-cell columns in one row gather."""
+        """GPU: switch from the dense layout to ragged records. The dense rows become records as they
+        are (cell i's P proteins at records i * P .., a view: nothing is copied), so the parameters a
+        user may have written are kept exactly; rebuilt cells then take records of their own size.
+        The slot map lives in a capacity buffer (plus a spare of the same size for compactions), so
+        the world moves it together with its per-cell columns in one row gather."""
         d = self.__dict__
-        if d["_slot"] is None:
-            n = d["_ncells"]
-            dev = self._store["Kmr"].device
-            self._slot_reserve(n, dev)
-            buf = d["_slot_buf"]
+        if d["_slot"] is not None:
+            return
+        store = self._store
+        dev = store["Kmr"].device
+        if dev.type != "cuda":
+            return
+        n = d["_ncells"]
+        s = int(self.n_signals)
+        if store["Kmr"].dim() == 3 and store["Kmr"].size(1) > 0:
+            packed = self._packed_params()
+            P, rows = int(packed["Kmr"].size(1)), int(packed["Kmr"].size(0))
+            W = packed["_W"].reshape(rows * P, s)
+            Q = packed["_Q"].reshape(rows * P, 4)
+            K = packed["Kmr"].reshape(rows * P, s)
+        else:
+            P, rows = 0, 0
+            W = torch.zeros(0, s, dtype=torch.int32, device=dev)
+            Q = torch.zeros(0, 4, dtype=torch.float32, device=dev)
+            K = torch.zeros(0, s, dtype=torch.float32, device=dev)
+        if P > _MAX_PROTEINS:
+            raise ValueError(f"a proteome of {P} proteins exceeds the record layout's {_MAX_PROTEINS}")
+        store.clear()
+        store.update({"_W": W, "_Q": Q, "Kmr": K})
+        d.pop("_spare", None)
+        self._slot_reserve(n, dev)
+        buf = d["_slot_buf"]
+        if P:
             torch.arange(n, device=dev, out=buf[:n])
-            d["_slot"] = buf[:n]
-            d["_nrows"] = n
-            d["_free"] = None
-        if not d.get("_compact") and _COMPACT and d["_slot"].is_cuda and self._pack_ok():
-            self._compact_store()
+            buf[:n].mul_(P).add_(_rec_code(0, P, P))
+        else:
+            buf[:n].zero_()
+        d["_slot"] = buf[:n]
+        d["_pmax"] = P
+        d["_rtop"] = torch.full((1,), n * P, dtype=torch.int64, device=dev)
+        d["_rtop_ub"] = n * P
+        d.setdefault("_res_total", 0)
+        d["_compact"] = True
+        d["_free"] = None
+        d.pop("_packed_stamp", None)
 
     def _slot_reserve(self, n: int, dev=None) -> None:
         """Capacity of the slot buffers >= n (keeps the live entries)."""
@@ -543,108 +614,154 @@ class Kinetics:
             w._reconcile()
 
     def _zero_row(self) -> torch.Tensor:
-        """Index (int64 (1,), device) of a storage row holding all-zero parameters, shared by cells
-        without a proteome. Created once per storage layout; never written afterwards (builds
-        always take fresh rows)."""
+        """The slot (int64 (1,), device) of a cell without parameters: 0 (no records; the dense view
+        is all zero, as after unset_cell_params). Cells are pointed at it by filling their slots."""
         d = self.__dict__
         z = d.get("_zero_row_t")
-        if z is not None:
-            return z
-        z = self._alloc_rows(1)
-        ok = self._pack_ok()
-        for t in self._store.values():
-            t.index_fill_(0, z, 0)  # packed words 0 and Q = 0 match all-zero parameters
-        self._restamp(ok)
-        d["_zero_row_t"] = z
+        if z is None or z.device != self._store["Kmr"].device:
+            z = d["_zero_row_t"] = torch.zeros(1, dtype=torch.int64, device=self._store["Kmr"].device)
         return z
 
-    def _alloc_rows(self, k: int) -> torch.Tensor:
-        self._sync()
-        return self._alloc_rows_now(k)
+    # -- record pool
+    def _rec_cap(self) -> int:
+        return int(self._store["Kmr"].size(0))
 
-    def _reserve_rows(self, k: int, sync: bool = True, headroom: int = 0) -> None:
-        """Make room for k fresh rows without taking them (the device genome pipeline takes them
-        with its own device-side row counter, magicsoup_amd.ops.genome_pipeline). ``sync=False``: the
-        owner's pending state is not resolved first (a chain issued on a device count; the caller
-        checked :meth:`_rows_available`). ``headroom``: room for that many more (a recycling or a
-        growth now, so that the next chains find their rows without one)."""
-        if sync:
-            self._sync()
-        self._alloc_rows_now(k + headroom, want=False)
-        self.__dict__["_nrows"] -= k + headroom
+    def _row_limit(self) -> tuple[int, None]:
+        """(record capacity of the pool, None): the device genome pipeline takes records below it."""
+        return self._rec_cap(), None
+
+    def _est_records(self) -> int:
+        """Records a device chain reserves per rebuilt cell: twice the live mean proteome plus 8,
+        at most the protein bound. A chain that needs more than the pool holds flags the cells it
+        could not place (genome_pipeline: rebuilt on the host, which reserves exactly), and its
+        status resets the host bound, so an estimate costs a rare host rebuild, never corruption;
+        the worst case (the bound, 45-160 proteins) would size the pool for nothing."""
+        d = self.__dict__
+        P = max(self._P(), 1)
+        mean = d.get("_mean_np")
+        return P if mean is None else max(1, min(P, int(2 * mean) + 8))
 
     def _rows_available(self, k: int) -> bool:
-        """Whether k fresh rows exist without a recycling or a growth (slot mode)."""
+        """Whether the records of k rebuilt cells (estimated, :meth:`_est_records`) fit below the
+        capacity without a collection (slot mode)."""
         d = self.__dict__
         if d.get("_slot") is None:
             return False
-        limit, _ = self._row_limit()
-        return d["_nrows"] + k <= limit
+        return d["_rtop_ub"] + k * self._est_records() <= self._rec_cap()
 
-    def _row_limit(self) -> tuple[int, torch.Tensor | None]:
-        """(bound of the fresh-row counter ``_nrows``, free-row list or None). Fresh row j is
-        ``_nrows + j`` of the dense storage tail, or ``free[_nrows + j]`` once rows are recycled."""
-        d = self.__dict__
-        free = d.get("_free") if d["_slot"] is not None else None
-        if free is not None:
-            return int(free.numel()), free
-        return min(int(t.size(0)) for t in self._store.values()), None
-
-    def _alloc_rows_now(self, k: int, want: bool = True) -> torch.Tensor | None:
-        """k unused storage rows (int64, device) for cells whose parameters are about to be written.
-        Rows of removed cells are not tracked as they die (a row may be shared); when the fresh rows
-        run out, the rows no live cell maps to are collected into a free list (no parameter data
-        moves), and only when too few are free does the storage grow."""
-        d = self.__dict__
+    def _reserve_rows(self, k: int, sync: bool = True, headroom: int = 0) -> int:
+        """Room for the records of k rebuilt cells that a device chain takes with its own counter
+        (magicsoup_amd.ops.genome_pipeline): the capacity is made for k + ``headroom`` cells (a
+        collection or growth now, so that the next chains find their records without one), k cells'
+        records are added to the host bound (per cell :meth:`_est_records`). ``sync=False``: the
+        owner's pending state is not resolved first (a chain issued on a device count; the caller
+        checked :meth:`_rows_available`). Returns the reservation mark the chain's status is adopted
+        with (:meth:`_adopt_rtop`)."""
         self._enter_slot_mode()
-        limit, free = self._row_limit()
-        if d["_nrows"] + k > limit:
-            free = self._recycle_rows(k)
-        r0 = d["_nrows"]
-        d["_nrows"] = r0 + k
-        if not want:
-            return None
-        if free is not None:
-            return free[r0 : r0 + k]
-        return torch.arange(r0, r0 + k, device=self._store["Kmr"].device)
+        e = self._est_records()
+        self._ensure_records((k + headroom) * e, sync=sync)
+        return self._note_records(k * e)
 
-    def _recycle_rows(self, k: int) -> torch.Tensor | None:
-        """Make >= k fresh rows available: the free list of storage rows that no live cell (and not
-        the shared all-zero row) maps to, or -- with fewer than k plus a quarter of the spare target
-        (_spare_rows) free -- a dense re-gather into a larger storage."""
+    def _note_records(self, need: int) -> int:
+        d = self.__dict__
+        d["_rtop_ub"] += int(need)
+        d["_res_total"] = d.get("_res_total", 0) + int(need)
+        return d["_res_total"]
+
+    def _adopt_rtop(self, value: int, mark: int | None) -> None:
+        """A chain's status holds the device counter right after its records were taken: the host
+        bound becomes that plus what was reserved since the chain was issued."""
+        d = self.__dict__
+        if d.get("_slot") is None or mark is None:
+            return
+        ub = int(value) + (d.get("_res_total", 0) - int(mark))
+        if ub < d["_rtop_ub"]:
+            d["_rtop_ub"] = ub
+
+    def _ensure_records(self, need: int, sync: bool = True) -> None:
+        """Room for ``need`` more records above the host bound of the counter: a read of the device
+        counter (after resolving the owner's pending chains), then a collection / growth."""
+        d = self.__dict__
+        if d["_rtop_ub"] + need <= self._rec_cap():
+            return
+        if not sync:
+            raise RuntimeError("parameter records: no room for a chain issued without synchronisation")
+        self._sync()
+        if d["_rtop_ub"] + need <= self._rec_cap():
+            return
+        d["_rtop_ub"] = int(d["_rtop"].item())
+        if d["_rtop_ub"] + need <= self._rec_cap():
+            return
+        self._collect_records(need)
+
+    def _collect_records(self, need: int) -> None:
+        """Compact the live cells' records into a fresh pool (in cell order, a run per cell) with room
+        for ``need`` more, growing it when less than about the live size would be left free. Cells
+        that shared a run (a division's parent and child) get a copy each. Two synchronisations (the
+        live count, the counter)."""
+        from magicsoup_amd.ops import hip_ops
+
         d = self.__dict__
         store = self._store
         n = d["_ncells"]
-        cap = min(int(t.size(0)) for t in store.values())
-        row_bytes = sum(t[:1].numel() * t.element_size() for t in store.values())
-        spare = _spare_rows(n, row_bytes)
         slot = d["_slot"]
-        if slot.is_cuda and cap - n >= k + spare // 4:
-            from magicsoup_amd.ops import hip_ops
+        dev = slot.device
+        s = int(self.n_signals)
+        cnt = (slot >> _REC_OFF_BITS) & _REC_CNT_MASK
+        ends = torch.cumsum(cnt, 0)
+        live = int(ends[-1].item()) if n else 0
+        cap = self._rec_cap()
+        free_target = max(live, int(need), 1 << 16)
+        new_cap = cap if live + need + free_target // 2 <= cap else int((live + need + free_target) * 1.25)
+        W2 = torch.empty(new_cap, s, dtype=torch.int32, device=dev)
+        Q2 = torch.empty(new_cap, 4, dtype=torch.float32, device=dev)
+        K2 = torch.empty(new_cap, s, dtype=torch.float32, device=dev)
+        out = d["_slot_spare"][:n]
+        if n:
+            new_off = (ends - cnt).contiguous()
+            hip_ops._m().records_move(n, s, slot.data_ptr(), new_off.data_ptr(), store["_W"].data_ptr(),
+                                      store["_Q"].data_ptr(), store["Kmr"].data_ptr(), W2.data_ptr(), Q2.data_ptr(),
+                                      K2.data_ptr(), out.data_ptr(), hip_ops._stream())
+        from magicsoup_amd.models.strings import _retire
 
-            used = torch.zeros(cap, dtype=torch.uint8, device=slot.device)
-            if n:
-                used.index_fill_(0, slot, 1)
-            z = d.get("_zero_row_t")
-            if z is not None:
-                used.index_fill_(0, z, 1)
-            free = hip_ops.select(used, "clear")[0]
-            if int(free.numel()) >= k + spare // 4:  # else: grow (recycling would come back soon)
-                d["_free"] = free
-                d["_nrows"] = 0
-                return free
-        self._materialize(expand=False)  # dense again: rows 0..n-1 live
+        for t in (store["_W"], store["_Q"], store["Kmr"], slot):
+            _retire(t)
+        store.update({"_W": W2, "_Q": Q2, "Kmr": K2})
+        d["_slot_buf"], d["_slot_spare"] = d["_slot_spare"], d["_slot_buf"]
+        d["_slot"] = d["_slot_buf"][:n]
+        d["_rtop"].fill_(live)
+        d["_rtop_ub"] = live
+        if n:
+            d["_mean_np"] = live / n
+        d["_collections"] = d.get("_collections", 0) + 1
+
+    def _alloc_cells(self, cells: torch.Tensor, tokens: torch.Tensor, nprot: torch.Tensor | None) -> torch.Tensor:
+        """Records for the rebuilt ``cells`` (their proteomes: ``nprot`` proteins each, or counted from
+        the tokens): taken on the device in cell order by one scan launch, the cells' slots written.
+        Returns the first record of each (int64, -1: no proteins) and the protein counts (int32)."""
+        from magicsoup_amd.ops import hip_ops
+
         self._enter_slot_mode()
-        if n + k + spare > cap:
-            new_cap = max(n + k + spare, int(cap * 1.5) + 64)
-            ok = self._pack_ok()
-            for name, t in list(store.items()):
-                nb = torch.empty(new_cap, *t.shape[1:], dtype=t.dtype, device=t.device)
-                nb[:n] = t[:n]
-                store[name] = nb
-            d.pop("_spare", None)
-            self._restamp(ok)
-        return None
+        d = self.__dict__
+        dev = d["_slot"].device
+        k = int(cells.numel())
+        if nprot is None:
+            nprot = (tokens[..., 0] != 0).any(dim=-1).sum(dim=-1)
+        nprot = nprot.to(device=dev, dtype=torch.int32).contiguous()
+        # the exact count (the translation that made the tokens synchronised already): the host
+        # bound stays tight, and the pool is not sized for the batch's longest proteome per cell
+        need = int(nprot.sum().item())
+        if k:
+            mean = d.get("_mean_np")
+            d["_mean_np"] = need / k if mean is None else 0.5 * (mean + need / k)
+        self._ensure_records(need)
+        self._note_records(need)
+        roff = torch.empty(k, dtype=torch.int64, device=dev)
+        flag = _record_flag(self)
+        hip_ops._m().assign_records(k, 0, nprot.data_ptr(), cells.data_ptr(), d["_slot"].data_ptr(),
+                                    d["_rtop"].data_ptr(), self._rec_cap(), self._P(), roff.data_ptr(),
+                                    flag.data_ptr(), hip_ops._stream())
+        return roff, nprot
 
     def _kernel_params(self) -> dict[str, torch.Tensor]:
         """Storage tensors in kernel layout (contiguous int32 / float32), rows = capacity."""
@@ -659,7 +776,7 @@ class Kinetics:
     # ---- integrator layout (GPU) ----
     # "_W" / "_Q" are rebuilt from the API tensors whenever those were replaced or modified from
     # Python (detected through tensor identity + version counter); the GPU parameter build writes
-    # both layouts, and every row operation below moves them together with the API tensors.
+    # the packed layout directly.
     def _pack_stamp(self):
         store = self.__dict__.get("_store_d", {})
         return tuple((weakref.ref(store[k]), store[k]._version) for k in _PACK_SRC if k in store)
@@ -695,7 +812,7 @@ class Kinetics:
             return store
         from magicsoup_amd.ops import hip_ops
 
-        # pack the live rows only, in cell order (free storage rows may hold stale data)
+        # pack the live rows only, in cell order
         self._materialize()
         store = self._store
         self._drop_packed()
@@ -707,11 +824,6 @@ class Kinetics:
         self._restamp(True)
         return store
 
-    # ---- compact GPU storage: in row-storage mode the integrator layout (_W: packed int8 N / Nf /
-    # Nb / A per (protein, signal), _Q: Vmax / Kmf / Kmb / Ke per protein) plus Kmr is all a row holds;
-    # the eight parameter tensors it packs are unpacked only when the dense API tensors are read
-    # (_materialize). A row takes 8 bytes per (protein, signal) instead of 24, which is what the
-    # parameter builds, row clones, storage growth and protein-slot growth move.
     def _compact_store(self) -> None:
         d = self.__dict__
         store = self._store
@@ -724,7 +836,8 @@ class Kinetics:
         d.pop("_packed_stamp", None)
 
     def _expand_store(self) -> None:
-        """Unpack the eight parameter tensors from _W / _Q (same rows) and leave compact mode."""
+        """Unpack the eight parameter tensors from a dense _W / _Q (same rows) and leave compact
+        mode."""
         d = self.__dict__
         if not d.get("_compact"):
             return
@@ -740,46 +853,38 @@ class Kinetics:
         self._restamp(True)
 
     def _materialize(self, expand: bool = True) -> None:
-        """Dense, cell-ordered rows (leaves row-storage mode). ``expand``: also unpack the API
-        tensors of compact storage (internal re-layouts keep it compact)."""
+        """Dense, cell-ordered tensors (leaves record mode): every cell's records, the build's padding
+        for its missing proteins (records_to_dense). ``expand``: also unpack the eight API tensors
+        from the packed words."""
         d = self.__dict__
         slot = d.get("_slot")
         if slot is None:
             if expand:
                 self._expand_store()
             return
-        ok = self._pack_ok()
-        n = d["_ncells"]
-        store = self._store
-        spare = d.setdefault("_spare", {})
-        target = {}
-        for name, t in store.items():
-            sp = spare.get(name)
-            if sp is None or sp.size(0) < max(n, 1) or sp.shape[1:] != t.shape[1:] or sp.dtype != t.dtype or sp.device != t.device:
-                sp = torch.empty(max(n, t.size(0)), *t.shape[1:], dtype=t.dtype, device=t.device)
-            target[name] = sp
-        if slot.is_cuda:
-            from magicsoup_amd.ops import hip_ops
+        from magicsoup_amd.ops import hip_ops
 
-            hip_ops.gather_rows([(store[k], target[k][:n]) for k in store], n, src_rows=slot)
-        else:
-            for k in store:
-                torch.index_select(store[k], 0, slot, out=target[k][:n])
-        for k in list(store):
-            spare[k], store[k] = store[k], target[k]
-        if slot.is_cuda:
-            # the old storage is not kept as the next re-gather's target: a dense re-gather is rare
-            # (rows are recycled in place first), and keeping it would hold the parameter storage
-            # twice in HBM (utils/memory.py plans without it); freed once the gather above ran
-            cur = torch.cuda.current_stream(slot.device)
-            for t in spare.values():
-                t.record_stream(cur)
-            spare.clear()
+        n = d["_ncells"]
+        P = self._P()
+        store = self._store
+        s = int(self.n_signals)
+        dev = slot.device
+        Wd = torch.empty(n, P, s, dtype=torch.int32, device=dev)
+        Qd = torch.empty(n, P, 4, dtype=torch.float32, device=dev)
+        Kd = torch.empty(n, P, s, dtype=torch.float32, device=dev)
+        hip_ops._m().records_to_dense(n, P, s, slot.data_ptr(), store["_W"].data_ptr(), store["_Q"].data_ptr(),
+                                      store["Kmr"].data_ptr(), Wd.data_ptr(), Qd.data_ptr(), Kd.data_ptr(),
+                                      hip_ops._stream())
+        for t in list(store.values()):
+            _retire_t(t)
+        store.clear()
+        store.update({"_W": Wd, "_Q": Qd, "Kmr": Kd})
+        for k in ("_spare", "_rtop", "_rtop_ub", "_pmax", "_free"):
+            d.pop(k, None)
         d["_slot"] = None
-        d["_free"] = None
         d["_nrows"] = n
-        d.pop("_zero_row_t", None)
-        self._restamp(ok)
+        d["_compact"] = True
+        d.pop("_packed_stamp", None)
         if expand:
             self._expand_store()
 
@@ -793,8 +898,8 @@ class Kinetics:
         d = self.__dict__
         k = int(idx.numel())
         if idx.is_cuda:
-            # only the cell -> row map is compacted; rows of removed cells (possibly shared with
-            # survivors) stay until the next re-gather (_alloc_rows)
+            # only the slot map is compacted; the records of removed cells (possibly shared with
+            # survivors) stay until the next collection
             if gathered and d["_slot"] is not None:
                 d["_slot_buf"], d["_slot_spare"] = d["_slot_spare"], d["_slot_buf"]
             else:
@@ -819,13 +924,23 @@ class Kinetics:
         self._restamp(ok)
 
     def reserve_cells(self, n: int) -> None:
-        """Row capacity of the parameter storage for ``n`` cells plus the usual spare rows, allocated
-        at once (no-op if it holds them already, or before the first proteome fixed the protein
-        dimension). Growing a large population in batches otherwise re-allocates the storage by
-        1.5x each time, with the old and the new storage alive together (an HBM-sized world would
-        need 2.5x its parameter bytes for a moment)."""
+        """Room for ``n`` cells allocated at once (no-op before the first proteome fixed the protein
+        dimension). Record pool: three times the live cells' mean proteome per cell (a collection
+        runs when garbage -- replaced and dead cells' records -- fills the rest); dense layout: rows
+        plus the usual spare. Growing a large population in batches otherwise re-allocates the storage
+        repeatedly with the old and the new copy alive together."""
         store = self._store
         if not store or self._P() == 0:
+            return
+        d = self.__dict__
+        if d.get("_slot") is not None:
+            self._sync()
+            slot = d["_slot"]
+            live = int(((slot >> _REC_OFF_BITS) & _REC_CNT_MASK).sum().item()) if slot.numel() else 0
+            per = max(live / max(slot.numel(), 1), 4.0)
+            want = int(3 * n * per) + (1 << 16)
+            if want > self._rec_cap():
+                self._grow_records(want)
             return
         cap = min(int(t.size(0)) for t in store.values())
         row_bytes = sum(t[:1].numel() * t.element_size() for t in store.values())
@@ -836,10 +951,24 @@ class Kinetics:
         ok = self._pack_ok()
         for name, t in list(store.items()):
             nb = torch.empty(want, *t.shape[1:], dtype=t.dtype, device=t.device)
-            nb[:cap] = t[:cap]  # (every row: the cell -> row map may point anywhere below cap)
+            nb[:cap] = t[:cap]
             store[name] = nb
         self.__dict__.pop("_spare", None)
         self._restamp(ok)
+
+    def _grow_records(self, cap: int) -> None:
+        """A larger record pool: the records below the device counter are copied as they are."""
+        d = self.__dict__
+        store = self._store
+        top = int(d["_rtop"].item())
+        for name in ("_W", "_Q", "Kmr"):
+            t = store[name]
+            nb = torch.empty(cap, *t.shape[1:], dtype=t.dtype, device=t.device)
+            if top:
+                nb[:top] = t[:top]
+            _retire_t(t)
+            store[name] = nb
+        d["_rtop_ub"] = top
 
     def increase_max_cells(self, by_n: int, zero: bool = True):
         """Append ``by_n`` cells (parameters zero-filled unless the caller writes them all)."""
@@ -848,12 +977,14 @@ class Kinetics:
         d = self.__dict__
         store = self._store
         if d["_slot"] is not None:
-            # GPU row storage: the new cells share the all-zero row (a later build gives them
-            # rows of their own)
-            row = self._zero_row()
-            self._slot_append(by_n).copy_(row.expand(by_n))
+            # record storage: the new cells have no records (slot 0) until a build gives them some
+            self._slot_append(by_n).zero_()
             d["_ncells"] += by_n
             return
+        if store["Kmr"].device.type == "cuda" and d["_ncells"] == 0 and self._P() == 0:
+            # a fresh GPU world: record storage from the start (no dense rows for the population)
+            self._enter_slot_mode()
+            return self.increase_max_cells(by_n, zero)
         cap = min(int(t.size(0)) for t in store.values())
         ok = self._pack_ok()
         n = d["_ncells"]
@@ -869,48 +1000,21 @@ class Kinetics:
         if zero:
             for t in store.values():
                 t[n : n + by_n].zero_()
-        # zero=False: the caller fills the new rows with a GPU build or row copy, both of which
-        # write the packed layout too
         self._restamp(ok)
 
     def increase_max_proteins(self, max_n: int):
-        """Grow the protein dimension of every parameter tensor to ``max_n`` (zero-filled)."""
+        """Grow the protein dimension of every parameter tensor to ``max_n`` (zero-filled). On the
+        GPU only the bound grows: records are per protein, nothing moves (the dense view shows the
+        new proteins as zeros, as the reference's widened tensors, kinetics.py:705-723)."""
         if max_n <= self._P():
             return
         self._sync()
         store = self._store
-        dev = store["Kmr"].device
-        if dev.type == "cuda":
-            # widen into new storage of the same row capacity, moving only the live cells' rows
-            # (gathered to cell order, one launch) -- not every storage row -- and zeroing only
-            # their new protein slots; the storage is dense (cell i -> row i) afterwards
-            from magicsoup_amd.ops import hip_ops
-
-            d = self.__dict__
-            n = d["_ncells"]
-            slot = d["_slot"]
-            p_old = self._P()
-            ok = self._pack_ok()
-            # row capacity of the new layout: the live rows plus the usual spare (not the old
-            # capacity, which earlier growth may have inflated)
-            row_bytes = sum(t[:1].numel() * t.element_size() for t in store.values()) * max_n // max(p_old, 1)
-            rows_new = n + _spare_rows(n, row_bytes)
-            moves = []
-            for name, t in list(store.items()):
-                # dense rows for all n cells (in row-storage mode cells share rows, so n may exceed
-                # the storage's row count)
-                nb = torch.empty(rows_new, max_n, *t.shape[2:], dtype=t.dtype, device=dev)
-                moves.append((t, nb))
-                store[name] = nb
-            hip_ops.copy_row_prefixes(moves, n, src_rows=slot)
-            for _, nb in moves:
-                nb[:n, p_old:].zero_()
-            d["_slot"] = None
-            d["_free"] = None
-            d["_nrows"] = n
-            d.pop("_zero_row_t", None)
-            d.pop("_spare", None)
-            self._restamp(ok)
+        if store["Kmr"].device.type == "cuda":
+            if max_n > _MAX_PROTEINS:
+                raise ValueError(f"a proteome of {max_n} proteins exceeds the record layout's {_MAX_PROTEINS}")
+            self._enter_slot_mode()
+            self.__dict__["_pmax"] = int(max_n)
             return
         self._materialize()
         ok = self._pack_ok()
@@ -931,9 +1035,8 @@ class Kinetics:
         for name, t in list(self._store.items()):
             self._store[name] = t[:n].to(dev)
         self.__dict__["_nrows"] = n
-        self.__dict__.pop("_spare", None)
-        self.__dict__.pop("_slot_buf", None)
-        self.__dict__.pop("_slot_spare", None)
+        for k in ("_spare", "_slot_buf", "_slot_spare", "_zero_row_t"):
+            self.__dict__.pop(k, None)
 
     # ------------------------------------------------------------------ integration
     def integrate_signals(self, X: torch.Tensor, _reduce_mask=None) -> torch.Tensor:
@@ -1054,7 +1157,8 @@ class Kinetics:
         self._materialize()
         state = self.__dict__.copy()
         state["last_masks"] = []
-        for k in ("_spare", "_hip_scratch", "_owner", "_lut_cache", "_slot_buf", "_slot_spare", "_free"):
+        for k in ("_spare", "_hip_scratch", "_owner", "_lut_cache", "_slot_buf", "_slot_spare", "_free", "_zero_row_t",
+                  "_rtop", "_rtop_ub", "_pmax"):
             state.pop(k, None)
         n = state["_ncells"]
         state["_store_d"] = {k: v[:n].clone() for k, v in self._store.items() if k not in _PACKED}

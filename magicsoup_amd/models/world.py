@@ -408,7 +408,7 @@ class World:
         kd = self.kinetics.__dict__
         refs.extend(kd.get("_store_d", {}).values())
         refs.extend(kd.get("_spare", {}).values())
-        for k in ("_slot_buf", "_slot_spare", "_free", "_zero_row_t"):
+        for k in ("_slot_buf", "_slot_spare", "_free", "_zero_row_t", "_rtop"):
             refs.append(kd.get(k))
         return refs
 

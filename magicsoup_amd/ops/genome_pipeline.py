@@ -137,19 +137,27 @@ def _usable(world, expected: float, limit: float = N_CAP / 4) -> bool:
     return enabled(world) and expected <= limit
 
 
+def _prepare_records(world, cells: int, sync: bool = True, headroom: int = 0) -> None:
+    """Room in the kinetics' record pool for the parameters of a call's (at most) ``cells`` rebuilt
+    cells, made BEFORE the call reads any world state: when the pool is short this resolves the
+    pending chains and collects the records (a reconcile can change the population, the arena's
+    length bound, ...), so the call must size itself afterwards."""
+    _state(world)["res_mark"] = world.kinetics._reserve_rows(int(cells), sync=sync, headroom=headroom)
+
+
 def _begin(world, kind: str) -> dict:
     """Per-call device state. A pending call of the same kind is resolved first (its scratch is
-    reused); with nothing pending the shared flags and the device row counter are (re)set from
-    the host, after making room for two calls' worth of fresh rows."""
+    reused); with nothing pending the shared flags are reset. (The call made room for its records
+    first: _prepare_records.)"""
     st = _state(world)
     if st["pending"] and any(pd.kind == kind for pd in st["pending"]):
         reconcile(world)
     kin = world.kinetics
     b = _bufs(world, kind)
+    kin._enter_slot_mode()
     fresh = not st["pending"]
-    if fresh:
-        kin._reserve_rows(2 * min(world.n_cells, N_CAP))
-    _m().gp_begin(_arena_desc(world, b), fresh, int(kin.__dict__["_nrows"]), _stream())
+    # (-1: the chain takes parameter records from the kinetics' own device counter, gp.hip)
+    _m().gp_begin(_arena_desc(world, b), fresh, -1, _stream())
     return b
 
 
@@ -158,8 +166,10 @@ def _arena_desc(world, b: dict):
     a = b.get("desc")
     if a is None:
         a = b["desc"] = _m().GpArena()
-        a.cnt, a.cnt2, a.opflags, a.gflags, a.d_rows = (_p(b["cnt"]), _p(b["cnt2"]), _p(b["opflags"]),
-                                                        _p(b["gflags"]), _p(b["d_rows"]))
+        a.cnt, a.cnt2, a.opflags, a.gflags = _p(b["cnt"]), _p(b["cnt2"]), _p(b["opflags"]), _p(b["gflags"])
+    # the record counter of the kinetics' ragged parameter storage (reported in the status slots)
+    rtop = world.kinetics.__dict__.get("_rtop")
+    a.d_rows = rtop.data_ptr() if rtop is not None else _p(b["d_rows"])
     arena = world._genomes
     a.data, a.lens, a.width, a.n = arena.data.data_ptr(), arena.lens.data_ptr(), arena.width, arena.n
     a.off, a.top, a.pool_cap = arena.off.data_ptr(), arena.top.data_ptr(), arena.pool_cap
@@ -193,18 +203,15 @@ def _gen_desc(world, dev):
 
 
 def _kin_desc(world, dev):
-    """Parameter storage (kernel layout, capacity rows), token LUTs, the cell -> row map and the
-    free-row list. Rebuilt only when the storage layout changed; the row map pointer (swapped by
-    every compaction) is refreshed on each call."""
+    """Ragged parameter records (kernel layout, csrc/hip/params.h), token LUTs and the cell ->
+    records map. Rebuilt only when the storage changed; the slot map pointer (swapped by every
+    compaction) and the protein bound are refreshed on each call."""
     kin = world.kinetics
-    store = kin._kernel_params()
     kin._enter_slot_mode()
-    packed = kin._pack_ok()
-    row_cap, free = kin._row_limit()
-    N = store["Kmr"]  # (compact storage holds no N: Kmr has the same (rows, P, s) shape)
-    key = (_p(store.get("N")), N.size(1), N.size(2), store["Kmr"].data_ptr(), _p(store.get("Vmax")),
-           store["_W"].data_ptr() if packed else 0, store["_Q"].data_ptr() if packed else 0, row_cap,
-           _p(free), float(kin.abs_temp), id(store))
+    store = kin._kernel_params()
+    rec_cap = kin._rec_cap()
+    key = (store["Kmr"].data_ptr(), store["_W"].data_ptr(), store["_Q"].data_ptr(), rec_cap,
+           kin.__dict__["_rtop"].data_ptr(), float(kin.abs_temp), id(store), int(kin.n_signals))
     c = _cache(world)
     hit = c.get("kin")
     if hit is not None and hit[0] == key:
@@ -215,12 +222,9 @@ def _kin_desc(world, dev):
 
         lu = build_luts(kin, dev)
         k = _m().GpKin()
-        k.N, k.Nf, k.Nb, k.A, k.Kmr = (_p(store.get(n)) for n in ("N", "Nf", "Nb", "A", "Kmr"))
-        k.Kmf, k.Kmb, k.Vmax, k.Ke = (_p(store.get(n)) for n in ("Kmf", "Kmb", "Vmax", "Ke"))
-        if packed:
-            k.W, k.Q, k.overflow = _p(store["_W"]), _p(store["_Q"]), _p(hip_ops._overflow_flag(kin))
-        k.P, k.s = int(N.size(1)), int(N.size(2))
-        k.row_cap, k.free = row_cap, _p(free)
+        k.Kmr, k.W, k.Q, k.overflow = _p(store["Kmr"]), _p(store["_W"]), _p(store["_Q"]), _p(hip_ops._overflow_flag(kin))
+        k.rtop, k.rec_cap = kin.__dict__["_rtop"].data_ptr(), rec_cap
+        k.s = int(kin.n_signals)
         k.vmax, k.km, k.signs, k.hills = _p(lu["vmax"]), _p(lu["km"]), _p(lu["signs"]), _p(lu["hills"])
         k.react, k.trnsp, k.eff, k.energies = _p(lu["react"]), _p(lu["trnsp"]), _p(lu["eff"]), _p(lu["energies"])
         k.nw, k.nk, k.nsg, k.nh = lu["vmax"].numel(), lu["km"].numel(), lu["signs"].numel(), lu["hills"].numel()
@@ -228,6 +232,7 @@ def _kin_desc(world, dev):
         k.abs_temp, k.gas = float(kin.abs_temp), float(GAS_CONSTANT)
         # the LUT tensors stay referenced by the cache entry while their pointers are in use
         c["kin"] = (key, k, lu)
+    k.P = kin._P()
     k.slot = kin._slot_tensor().data_ptr()
     return k
 
@@ -277,9 +282,14 @@ def point_mutations(world, p: float, p_indel: float, p_del: float) -> bool:
     """Device-pipeline ``mutate_cells()`` over all cells (one C++ call issuing the chain, gp.hip);
     False if this call should take the synchronous path instead."""
     arena = world._genomes
-    n = arena.n
-    if n == 0:
+    if arena.n == 0:
         return True
+    if not enabled(world):
+        return False
+    # (the call's capacity at the current state: the record reservation's size; everything is
+    # re-read after it)
+    _prepare_records(world, _cap(arena.n * p * int(arena.width), min(arena.n, N_CAP)))
+    n = arena.n
     L = int(arena.width)  # every genome fits its row
     if p * L > LAM_MAX or not _usable(world, n * p * L):
         return False
@@ -308,6 +318,13 @@ def recombinate_all(world, p: float, extra=None) -> bool:
     out_len, out_rows, nres)`` (device pointers) writes them and the number of result rows to
     commit; they are committed after (so they override) the local results, in the same passes."""
     arena = world._genomes
+    if world.n_cells < 2:
+        return True
+    if not enabled(world):
+        return False
+    n0, L0 = world.n_cells, int(arena.width)
+    pc0 = _pair_cap(n0, 4 * n0 * p * 2 * L0, extra) or min(n0, N_CAP) // 2
+    _prepare_records(world, 2 * pc0 + (0 if extra is None else int(extra.rows)))
     n = world.n_cells
     if n < 2:
         return True
@@ -390,8 +407,39 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
     issue touches would depend on the count."""
     arena = world._genomes
     n = int(bound[0]) if bound is not None else world.n_cells
-    if n < 2:
+    if n < 2 or not enabled(world):
         return False
+    st = _state(world)
+    if any(pd.kind in ("rec", "mut", "evo") for pd in st["pending"]):
+        if bound is not None:
+            BOUND_DECLINED["pending"] += 1
+            return False
+        reconcile(world)  # (before anything below reads the world state it may change)
+        n = world.n_cells
+        if n < 2:
+            return False
+    # records for the union's rebuilt cells (at most): made before anything below reads world state
+    # (see _prepare_records); with chains issued on a device count enabled, the synchronous path
+    # makes room for the next call as well: those cannot collect (World._chain_bound)
+    from magicsoup_amd.models import world as world_mod
+
+    # (the union's capacity at the current state sizes the reservation; re-read after it)
+    L0 = int(arena.width)
+    pc0 = _pair_cap(n, 4 * n * p_rec * 2 * L0, extra) or min(n, N_CAP) // 2
+    ucap_max = 2 * pc0 + _cap(n * p * L0, min(n, N_CAP)) + (0 if extra is None else int(extra.rows)) + (
+        0 if arrivals is None else int(arrivals[1]))
+    kin = world.kinetics
+    if bound is not None:
+        if not kin._rows_available(ucap_max):
+            BOUND_DECLINED["rows"] += 1
+            return False
+        _prepare_records(world, ucap_max, sync=False)
+    else:
+        room_next = world_mod._CHAIN_BOUND and n <= world_mod._CHAIN_BOUND_MAX
+        _prepare_records(world, ucap_max, headroom=ucap_max if room_next else 0)
+        n = world.n_cells
+        if n < 2:
+            return False
     L = int(arena.width)
     exp_rec = 4 * n * p_rec * 2 * L
     if (p_rec * 2 * L > LAM_MAX or p * L > LAM_MAX or not _usable(world, exp_rec, N_CAP)
@@ -422,20 +470,9 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
         if extra is not None or narr or max(pcap, mcap, 2 * pcap) > sc_cap:
             BOUND_DECLINED["caps"] += 1
             return False
-        if fresh and not kin._rows_available(2 * min(n, N_CAP)):
-            BOUND_DECLINED["rows"] += 1
-            return False
         if arena.top_ub + room > arena.pool_cap:
             BOUND_DECLINED["pool"] += 1
             return False
-    if fresh:
-        # (with chains issued on a device count enabled, the synchronous path reserves room for the
-        # next call as well: those cannot recycle rows, World._chain_bound)
-        from magicsoup_amd.models import world as world_mod
-
-        room_next = bound is None and world_mod._CHAIN_BOUND and n <= world_mod._CHAIN_BOUND_MAX
-        kin._reserve_rows(2 * min(n, N_CAP) + narr, sync=bound is None,
-                          headroom=2 * min(2 * n, N_CAP) if room_next else 0)
     _room(world, room)
     br, bm, bu = _bufs(world, "rec"), _bufs(world, "mut"), _bufs(world, "evo")
     ar, am, au = _arena_desc(world, br), _arena_desc(world, bm), _arena_desc(world, bu)
@@ -464,7 +501,7 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
     slot_u, slot_p = _m().gp_evolve(ar, am, au, _gen_desc(world, dev), k, _p(keys), nbr, float(p_rec), rng_r[0],
                                     rng_r[1], pcap, float(p), float(p_indel), float(p_del), rng_m[0], rng_m[1], mcap,
                                     K_CAP, D_CAP, _p(mark), int(gen), _p(blob_r), _p(blob_m), _p(blob_u), fresh,
-                                    int(kin.__dict__["_nrows"]), extra, _p(nres), arr0, narr, nd[0], nd[1], mirror[1],
+                                    -1, extra, _p(nres), arr0, narr, nd[0], nd[1], mirror[1],
                                     _stream())
     lay_r = _m().gp_layout(1, n, pcap, L, K_CAP, xr)
     lay_m = _m().gp_layout(0, n, mcap, L, K_CAP, 0)
@@ -526,9 +563,8 @@ def rebuild_rows(world, rows: torch.Tensor) -> bool:
     if not enabled(world) or k > 8 * N_CAP or world.kinetics._P() == 0:
         return False  # (no protein slots yet: the synchronous path sizes the storage)
     if k > N_CAP:
-        # a large batch (e.g. a big top-up): start from a fresh chain with room for all its rows
-        reconcile(world)
-        world.kinetics._reserve_rows(k + 2 * N_CAP)
+        reconcile(world)  # (a large batch, e.g. a big top-up: a fresh chain)
+    _prepare_records(world, k)
     b = _begin(world, "imm")
     dcnt = b["cnt"]
     dcnt[:1].fill_(k)
@@ -618,7 +654,9 @@ def _resolve(world, pend: list) -> bool:
     kin = world.kinetics
     pend[-1].event.synchronize()
     _tighten_pool_bound(world)
-    kin.__dict__["_nrows"] = max(int(kin.__dict__["_nrows"]), int(pend[-1].host[2]))
+    # (the device record counter after the chain's last build: the host bound tightens to it plus
+    # what was reserved since the chain started)
+    kin._adopt_rtop(int(pend[-1].host[2]), _state(world).get("res_mark"))
     for pd in pend:
         if pd.kind == "evo":
             rebuilt |= _resolve_evo(world, pd)

@@ -206,12 +206,17 @@ def _overflow_flag(kin) -> _HostFlag:
 
 
 def _check_overflow(kin) -> None:
-    """Raise if a pack / build reported an int8 overflow (a read of mapped host memory: it never
-    waits on the device; a build still running is seen at the next integration)."""
-    f = getattr(_scratch(kin), "overflow", None)
+    """Raise if a pack / build reported an int8 overflow, or a host build found the parameter
+    records exhausted (reads of mapped host memory: they never wait on the device; a build still
+    running is seen at the next integration)."""
+    sc = _scratch(kin)
+    f = getattr(sc, "overflow", None)
     if f is not None and f.read() != 0:
         raise OverflowError("a protein's stoichiometry or allosteric exponent exceeds the int8 range of the "
                             "integrator's packed parameter layout (|N|, |A| <= 127, Nf, Nb <= 255)")
+    f = getattr(sc, "rec_flag", None)
+    if f is not None and f.read() != 0:
+        raise RuntimeError("parameter records: a host build found the record pool exhausted (reservation bug)")
 
 
 def pack_params(kin, store: dict, rows: int | None = None) -> None:
@@ -229,7 +234,7 @@ def _launch_integrate(kin, p, c, X_io=None, world=None, trims=(0.7, 0.2, 0.1), n
                       slot=None, save=None):
     _check_overflow(kin)
     W = p["_W"]
-    P, s = int(W.size(1)), int(W.size(2))
+    P, s = kin._P(), int(W.size(-1))  # (record storage: P is the protein bound, W is (records, s))
     dev = W.device
     sc = _scratch(kin)
     snap_a = sc.get("snap_a", c * _SNAP * s, torch.float32, dev)
@@ -386,11 +391,14 @@ def restore_cell_state(world, buf: torch.Tensor) -> None:
                        _p(d["_cols"]["cell_molecules"].view(n)), _p(buf), True, _stream())
 
 
-def build_params(kin, tokens, rows, luts, p, abs_temp: float, gas: float, nprot=None, dn=None) -> None:
-    """Fused parameter build; also writes the integrator layout when it is current."""
+def build_params(kin, tokens, rows, luts, p, abs_temp: float, gas: float, nprot=None, dn=None, roff=None) -> None:
+    """Fused parameter build; also writes the integrator layout when it is current. ``roff``: the
+    records of ragged storage (the packed layout only), else dense rows ``rows``."""
     packed = kin._pack_ok()
     n, P, D = int(tokens.size(0)), int(tokens.size(1)), int(tokens.size(2))
-    Pt, s = int(p["Kmr"].size(1)), int(p["Kmr"].size(2))
+    Pt, s = kin._P(), int(p["Kmr"].size(-1))
+    if roff is not None and not packed:
+        raise RuntimeError("build_params: record storage without the packed layout")
     _m().build_params(
         n, P, D, Pt, s, _p(tokens), _p(rows),
         _p(luts["vmax"]), luts["vmax"].numel(), _p(luts["km"]), luts["km"].numel(),
@@ -401,7 +409,7 @@ def build_params(kin, tokens, rows, luts, p, abs_temp: float, gas: float, nprot=
         _p(nprot),
         _p(p["_W"] if packed else None), _p(p["_Q"] if packed else None),
         _p(_overflow_flag(kin) if packed else None),
-        _p(dn),
+        _p(dn), _p(roff),
         _stream(),
     )
 

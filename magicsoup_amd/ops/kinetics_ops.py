@@ -90,25 +90,30 @@ def _luts(kin, device) -> dict[str, torch.Tensor]:
     }
 
 
-def build_params(kin, rows: torch.Tensor, tokens: torch.Tensor, nprot: torch.Tensor | None = None) -> None:
+def build_params(kin, rows: torch.Tensor | None, tokens: torch.Tensor, nprot: torch.Tensor | None = None,
+                 roff: torch.Tensor | None = None) -> None:
     """Write parameter rows ``rows`` from dense tokens (n, P, D, 5). With ``nprot`` (GPU), rows
-    whose proteome is empty are unset (all zero) in the same launch."""
+    whose proteome is empty are unset (all zero) in the same launch. ``roff`` (GPU record storage,
+    Kinetics._alloc_cells): the first record of each item instead of rows; only its ``nprot``
+    proteins are written."""
     p = _canonical_params(kin)
     dev = p["Kmr"].device
     if dev.type != "cuda":
         kin._materialize()  # (host builds write the full parameter set)
         p = _canonical_params(kin)
-    if rows.numel() == 0:
+    n = int(tokens.size(0)) if roff is not None else int(rows.numel())
+    if n == 0:
         return
     tokens = tokens.to(device=dev, dtype=torch.int32).contiguous()
-    rows = rows.to(device=dev, dtype=torch.int32).contiguous()
     luts = build_luts(kin, dev)
     if dev.type == "cuda":
         from magicsoup_amd.ops import hip_ops
 
         np_ = None if nprot is None else nprot.to(device=dev, dtype=torch.int32).contiguous()
-        hip_ops.build_params(kin, tokens, rows, luts, p, float(kin.abs_temp), GAS_CONSTANT, nprot=np_)
+        rows = None if rows is None else rows.to(device=dev, dtype=torch.int32).contiguous()
+        hip_ops.build_params(kin, tokens, rows, luts, p, float(kin.abs_temp), GAS_CONSTANT, nprot=np_, roff=roff)
         return
+    rows = rows.to(device=dev, dtype=torch.int32).contiguous()
     if nprot is not None:
         nprot = nprot.cpu()
         empty = nprot == 0

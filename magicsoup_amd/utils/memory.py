@@ -22,10 +22,12 @@ for order-preserving compactions):
 * intracellular molecules (``m`` fp32), position (2 int32), lifetime and divisions (int32);
 * the genome pool (one byte per nt, ragged: offsets + lengths per cell, no padding to the longest
   genome; twice the live bytes between collections) and a label row (16 B);
-* the cell -> parameter-row map (int64) and the division / kill scratch of the native fast path;
-* parameter rows in compact storage: per (protein, signal) the packed N/Nf/Nb/A word (int32) and
-  Kmr (fp32), per protein Vmax/Kmf/Kmb/Ke (4 fp32), for the live cells plus the spare rows fresh
-  builds take (``models/kinetics.py`` ``_spare_rows``: up to 3n within 8 GiB);
+* the cell -> parameter-records map (int64) and the division / kill scratch of the native fast path;
+* ragged parameter records (``csrc/hip/params.h``): one per protein of a cell's own proteome --
+  per signal the packed N/Nf/Nb/A word (int32) and Kmr (fp32), plus Vmax/Kmf/Kmb/Ke (4 fp32) --
+  not padded to the population's longest proteome; the pool holds about three times the live
+  records (``Kinetics.reserve_cells``; replaced and dead cells' records are garbage until the next
+  collection compacts them);
 * the ops' per-cell scratch (integrator snapshots, neighbour keys, placement lists).
 """
 from __future__ import annotations
@@ -49,6 +51,13 @@ def proteins_per_genome(genome_len: int) -> int:
     profiles/r5/hbm_probe.log; SURVEY.md §2.3 measured 24 at 500 nt and 40 at 1 kbp for ~10k
     cells -- the tail grows with the population)."""
     return max(8, int(math.ceil(genome_len / 16.0)))
+
+
+def proteins_mean(genome_len: int) -> float:
+    """Mean proteome size of random genomes of ``genome_len`` nt: 6.9 / 16.8 / 54.7 proteins at
+    500 / 1000 / 3000 nt (3000 random genomes each, this package's translation); about one protein
+    per 55 nt, rounded up for the growth an evolving population shows."""
+    return max(1.0, genome_len / 55.0)
 
 
 def protein_slots(genome_len: int) -> int:
@@ -76,8 +85,8 @@ def footprint(map_size: int, n_molecules: int, cells: int, map_dtype=torch.float
     cap = int(n * _CAP)
     P = p_max if p_max is not None else protein_slots(genome_len)
     s = 2 * m
-    row_bytes = P * s * 8 + P * 16  # packed word + Kmr per (protein, signal); Vmax/Kmf/Kmb/Ke per protein
-    spare_rows = max(n // 8, min(3 * n, _KIN_SPARE_BUDGET // max(row_bytes, 1)), 1024)
+    rec_bytes = s * 8 + 16  # packed word + Kmr per signal, Vmax/Kmf/Kmb/Ke: one record per protein
+    records = int(3 * n * max(proteins_mean(genome_len), 4.0)) + (1 << 16)  # (Kinetics.reserve_cells)
     parts = {
         "molecule_map": pix * m * es * 2,
         "pixel_maps": pix * (1 + 4 + 4),
@@ -87,7 +96,7 @@ def footprint(map_size: int, n_molecules: int, cells: int, map_dtype=torch.float
         "genome_pool": cap * (8 + 4) * 2 + max(16 << 20, 2 * n * ((int(genome_len * 1.1) + 15) // 16 * 16)),
         "label_arena": cap * (16 + 4) * 2,
         "row_maps": cap * (8 * 2 + 6 * 8 + 1),
-        "kinetics_rows": int((n + spare_rows) * row_bytes * 1.0),
+        "kinetics_rows": records * rec_bytes,
         # per-cell scratch of the ops (ops/hip_ops.py): the integrator's two candidate snapshots
         # (5 states of s signals each) and cell lists, the speculative activity's saved state, the
         # neighbour-slot keys / event counts, the placement and division lists

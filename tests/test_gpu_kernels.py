@@ -871,8 +871,8 @@ def test_deferred_genome_ops_match_immediate_issue(monkeypatch):
 
 
 def test_widening_proteins_keeps_parameters_in_slot_mode():
-    """Growing the protein dimension while cells map to scattered (recycled) storage rows moves the
-    live rows only: every cell keeps its parameters, the new protein slots are zero."""
+    """Growing the protein dimension while cells map to scattered (collected, shared) ragged records
+    moves nothing: every cell keeps its parameters, the new protein slots read as zeros."""
     import bench
 
     atp = CHEMISTRY.molname_2_idx["ATP"]
@@ -882,7 +882,7 @@ def test_widening_proteins_keeps_parameters_in_slot_mode():
         w.mutate_cells(p=1e-4)
     w._reconcile()
     kin = w.kinetics
-    kin.__dict__["_nrows"] = kin._row_limit()[0]  # force recycled rows for the next builds
+    kin._collect_records(0)  # (records compacted; later builds take fresh ones past them)
     bench.step(w, 1500, 500, atp)
     w.mutate_cells(p=1e-4)
     w._reconcile()
@@ -1065,21 +1065,21 @@ def test_integrator_flags_match_host_core_on_small_populations():
 
 @pytest.mark.parametrize("recycle", [False, True])
 def test_parameter_rows_follow_genomes_through_bench_steps(monkeypatch, recycle):
-    """After kills (the cell -> row map gathered with the columns), divisions (cloned in the same
+    """After kills (the cell -> records map gathered with the columns), divisions (cloned in the same
     gather), mutations / recombinations (device pipeline) and spawns, every cell's parameters equal
-    a fresh translation + build of its current genome. ``recycle``: the fresh storage rows are
-    declared used up midway, so later builds take recycled rows of dead cells (free list)."""
+    a fresh translation + build of its current genome. ``recycle``: the record pool is declared
+    used up midway (device counter at the capacity), so the device chains run out of records (their
+    cells are rebuilt on the host) and the next reservation collects the live records."""
     import bench
 
     recycled = []
-    orig = Kinetics._recycle_rows
+    orig = Kinetics._collect_records
 
-    def spy(self, k):
-        out = orig(self, k)
-        recycled.append(out is not None)
-        return out
+    def spy(self, need):
+        orig(self, need)
+        recycled.append(True)
 
-    monkeypatch.setattr(Kinetics, "_recycle_rows", spy)
+    monkeypatch.setattr(Kinetics, "_collect_records", spy)
     atp = CHEMISTRY.molname_2_idx["ATP"]
     w = _world("cuda", map_size=128, n=3000, s=500)
     for i in range(8):
@@ -1088,7 +1088,8 @@ def test_parameter_rows_follow_genomes_through_bench_steps(monkeypatch, recycle)
             # between re-packs the storage densely with fresh spare rows)
             w._reconcile()
             kin = w.kinetics
-            kin.__dict__["_nrows"] = kin._row_limit()[0]
+            kin.__dict__["_rtop"].fill_(kin._rec_cap() - 8)
+            kin.__dict__["_rtop_ub"] = kin._rec_cap() - 8
         bench.step(w, 3000, 500, atp)
         # the step's genome chains were flushed onto the side stream and are joined lazily (at the
         # next activity): compute-stream allocations of storage-sized blocks now must not receive
@@ -1709,3 +1710,40 @@ def test_molecule_totals_match_torch_sums(dtype):
     ref = [(float(mm[i].sum()) + float(w.cell_molecules[:, i].double().sum())) / (300 * 300 + w.n_cells)
            for i in range(w.n_molecules)]
     assert means == pytest.approx(ref, rel=rel)
+
+
+def test_ragged_records_match_host_build():
+    """Cells built on the GPU take ragged records (csrc/hip/params.h): exactly one per protein of
+    their own proteome, none for the padding; their dense view -- records, then the build's padding
+    values up to the build width -- equals the host core's dense build of the same genomes."""
+    from magicsoup_amd.ops import world_ops
+
+    wc = _world("cpu", map_size=64, n=300, s=500, seed=9)
+    wg = _copy_world_cpu_to_gpu(wc)
+    rows = torch.arange(wg.n_cells, device="cuda")
+    wg._update_params_rows(rows)
+    kin = wg.kinetics
+    slot = kin.__dict__["_slot"]
+    assert slot is not None
+    cnt = ((slot >> 36) & 0x3FFF).cpu()
+    _, nprot = world_ops.translate(wc, torch.arange(wc.n_cells))
+    assert torch.equal(cnt, nprot.to(torch.int64).cpu())
+    # (the copied world's dense rows became records first; a collection keeps only the live runs)
+    kin._collect_records(0)
+    assert int(kin.__dict__["_rtop"].item()) == int(nprot.sum())
+    assert torch.equal(((kin.__dict__["_slot"] >> 36) & 0x3FFF).cpu(), cnt)
+    P = wc.kinetics.N.size(1)
+    for name in ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke"):
+        a, b = getattr(kin, name)[:, :P].cpu(), getattr(wc.kinetics, name)
+        if a.dtype == torch.int32:
+            assert torch.equal(a, b), name
+        else:
+            assert torch.allclose(a, b, rtol=1e-5, atol=1e-30, equal_nan=True), name
+    # the same activity from the records and from the dense layout they materialise to
+    wd = copy.deepcopy(wg)  # (the copy holds the dense tensors read above)
+    assert wd.kinetics.__dict__["_slot"] is None
+    wg2 = copy.deepcopy(wg)
+    wg2._update_params_rows(rows)  # records again
+    for w in (wd, wg2):
+        w.enzymatic_activity()
+    assert torch.equal(wd.cell_molecules, wg2.cell_molecules)
