@@ -374,11 +374,14 @@ def main():
     if (a.memory_report or a.preset == "hbm") and torch.cuda.is_available() and rank == 0:
         from magicsoup_amd.utils import memory
 
-        held = memory.measured(world)["bytes"]
+        meas = memory.measured(world)
+        held = meas["bytes"]
         fp = memory.footprint(a.map_size, len(chem.molecules), a.cells, a.map_dtype, a.genome_size,
                               ranks=world_size if distributed else 1)
         print(json.dumps({"memory": {"measured_gib": round(held / 2**30, 2), "model_gib": round(fp["total"] / 2**30, 2),
                                      "model_over_measured": round(fp["total"] / held, 3),
+                                     "measured_kinetics_gib": round(meas["kinetics_bytes"] / 2**30, 2),
+                                     "measured_molecule_map_gib": round(meas["molecule_map_bytes"] / 2**30, 2),
                                      "allocated_gib": round(torch.cuda.memory_allocated() / 2**30, 2),
                                      "reserved_gib": round(torch.cuda.memory_reserved() / 2**30, 2),
                                      "parts_gib": {k: round(v / 2**30, 2) for k, v in fp.items()

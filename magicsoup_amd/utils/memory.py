@@ -185,7 +185,15 @@ def measured(world) -> dict:
     sc = d.get("_hip_scratch")
     if sc is not None:
         add(getattr(sc, "bufs", {}))
+    before = total["bytes"]
+    mm = d.get("_molmap")
+    maps = 0
+    if isinstance(mm, torch.Tensor):
+        maps = mm.untyped_storage().nbytes()
+        tmp = getattr(sc, "bufs", {}).get("diff_tmp") if sc is not None else None
+        maps += tmp.untyped_storage().nbytes() if isinstance(tmp, torch.Tensor) else 0
     kd = world.kinetics.__dict__
     for k, v in kd.items():
         add(v)
-    return {"bytes": total["bytes"]}
+    # (kinetics: the parameter storage -- ragged records on the GPU -- with its slot map)
+    return {"bytes": total["bytes"], "kinetics_bytes": total["bytes"] - before, "molecule_map_bytes": maps}
