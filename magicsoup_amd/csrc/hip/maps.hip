@@ -976,46 +976,25 @@ void spill_free_mask(int n, int m, uintptr_t dead, uintptr_t pos, int R, int C, 
   MS_LAUNCH_CHECK();
 }
 
-// spawn_cells without a host round trip. One thread per new cell j (row n0 + j): claim a free pixel
-// of the owned rows -- random probes (as claim_free), then a linear scan from a random start, which
-// always succeeds when the caller spawns at most as many cells as there are free owned pixels (the
-// host knows that count: one cell per pixel) -- then position, lifetime 0, divisions 0, half of the
-// pixel's molecules (the pixel keeps the other half, as pickup) and a random 12-character label.
+// spawn_cells without a host round trip: the new cells' pixels from spawn_claims (world.hip:
+// deterministic priority rounds), then one thread per new cell j (row n0 + j): position, lifetime 0,
+// divisions 0, half of the pixel's molecules (the pixel keeps the other half, as pickup) and a random
+// 12-character label.
 constexpr int kLabelLen = 12;
-__global__ void __launch_bounds__(256) spawn_place_kernel(int k, int R, int C, int r_lo, int r_hi, uint8_t* cell_map,
-                                                          uint64_t seed, uint64_t call, int attempts, long long n0,
-                                                          int m, int32_t* pos, int32_t* lifetimes, int32_t* divisions,
-                                                          float* cell_mols, void* map, int dtype, const float* corr,
-                                                          uint8_t* labels, int label_w, int32_t* label_lens,
-                                                          int* failed) {
+__global__ void __launch_bounds__(256) spawn_init_kernel(int k, int R, int C, const long long* result, uint64_t seed,
+                                                         uint64_t call, long long n0, int m, int32_t* pos,
+                                                         int32_t* lifetimes, int32_t* divisions, float* cell_mols,
+                                                         void* map, int dtype, const float* corr, uint8_t* labels,
+                                                         int label_w, int32_t* label_lens, int* failed) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= k) return;
-  Philox rng(seed, call, (uint32_t)j);
-  const long long base = (long long)r_lo * C, n_pix = (long long)(r_hi - r_lo) * C;
-  auto claim = [&](long long pix) -> bool {
-    if (cell_map[pix]) return false;
-    unsigned* word = reinterpret_cast<unsigned*>(cell_map + (pix & ~3ll));
-    const unsigned bit = 1u << (8 * (pix & 3));
-    const unsigned old = atomicOr(word, bit);
-    return !(old & (0xFFu << (8 * (pix & 3))));
-  };
-  long long got = -1;
-  for (int t = 0; t < attempts && got < 0; ++t) {
-    const long long pix = base + (long long)rng.below64((uint64_t)n_pix);
-    if (claim(pix)) got = pix;
-  }
-  if (got < 0) {
-    const long long start = (long long)rng.below64((uint64_t)n_pix);
-    for (long long s = 0; s < n_pix && got < 0; ++s) {
-      const long long pix = base + (start + s) % n_pix;
-      if (claim(pix)) got = pix;
-    }
-  }
+  const long long got = result[j];
   const long long c = n0 + j;
   if (got < 0) {  // more new cells than free pixels: the caller's count was wrong
     atomicOr(failed, 1);
     return;
   }
+  Philox rng(seed, call ^ 0x9E3779B97F4A7C15ull, (uint32_t)j);  // (the labels' stream)
   const int x = (int)(got / C), y = (int)(got - (long long)(got / C) * C);
   pos[2 * c] = x;
   pos[2 * c + 1] = y;
@@ -1035,6 +1014,9 @@ __global__ void __launch_bounds__(256) spawn_place_kernel(int k, int R, int C, i
   label_lens[c] = kLabelLen;
 }
 
+void spawn_claims(int k, int C, int r_lo, int r_hi, uintptr_t cell_map, uintptr_t claim, uintptr_t cand,
+                  uintptr_t result, uint64_t seed, uint64_t call, uintptr_t failed, hipStream_t s);  // world.hip
+
 void pool_write(int k, int L_in, uintptr_t rows, uintptr_t lens, uintptr_t dst, long long n0, uintptr_t pool,
                 uintptr_t off, uintptr_t top, long long cap, uintptr_t out_lens, uintptr_t failed, uintptr_t stream);
 
@@ -1042,16 +1024,18 @@ void spawn_dev(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uint
                long long n0, int m, uintptr_t pos, uintptr_t lifetimes, uintptr_t divisions, uintptr_t cell_mols,
                uintptr_t map, int dtype, uintptr_t corr, uintptr_t labels, int label_w, uintptr_t label_lens,
                int L_in, uintptr_t rows, uintptr_t lens, uintptr_t pool, uintptr_t off, uintptr_t top,
-               long long pool_cap, uintptr_t arena_lens, uintptr_t failed, uintptr_t pool_failed, uintptr_t stream) {
+               long long pool_cap, uintptr_t arena_lens, uintptr_t failed, uintptr_t pool_failed, uintptr_t claim,
+               uintptr_t cand, uintptr_t result, uintptr_t stream) {
   if (k <= 0) return;
   if (R <= 0 || C <= 0 || r_lo < 0 || r_hi > R || r_lo >= r_hi) throw std::invalid_argument("spawn_dev: bad geometry");
   if (label_w < kLabelLen) throw std::invalid_argument("spawn_dev: label rows too narrow");
+  if (!claim || !cand || !result) throw std::invalid_argument("spawn_dev: claim map and scratch required");
   hipStream_t s = S_(stream);
-  spawn_place_kernel<<<cdiv(k, 256), 256, 0, s>>>(k, R, C, r_lo, r_hi, P_<uint8_t>(cell_map), seed, call, 64, n0, m,
-                                                  P_<int32_t>(pos), P_<int32_t>(lifetimes), P_<int32_t>(divisions),
-                                                  P_<float>(cell_mols), P_<void>(map), dtype,
-                                                  corr ? P_<float>(corr) : nullptr, P_<uint8_t>(labels), label_w,
-                                                  P_<int32_t>(label_lens), P_<int>(failed));
+  spawn_claims(k, C, r_lo, r_hi, cell_map, claim, cand, result, seed, call, failed, s);
+  spawn_init_kernel<<<cdiv(k, 256), 256, 0, s>>>(k, R, C, P_<long long>(result), seed, call, n0, m, P_<int32_t>(pos),
+                                                 P_<int32_t>(lifetimes), P_<int32_t>(divisions), P_<float>(cell_mols),
+                                                 P_<void>(map), dtype, corr ? P_<float>(corr) : nullptr,
+                                                 P_<uint8_t>(labels), label_w, P_<int32_t>(label_lens), P_<int>(failed));
   MS_LAUNCH_CHECK();
   // the genomes into fresh pool space (pool.hip)
   pool_write(k, L_in, rows, lens, 0, n0, pool, off, top, pool_cap, arena_lens, pool_failed, stream);

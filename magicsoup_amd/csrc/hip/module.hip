@@ -71,7 +71,8 @@ void spawn_dev(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uint
                long long n0, int m, uintptr_t pos, uintptr_t lifetimes, uintptr_t divisions, uintptr_t cell_mols,
                uintptr_t map, int dtype, uintptr_t corr, uintptr_t labels, int label_w, uintptr_t label_lens,
                int L_in, uintptr_t rows, uintptr_t lens, uintptr_t pool, uintptr_t off, uintptr_t top,
-               long long pool_cap, uintptr_t arena_lens, uintptr_t failed, uintptr_t pool_failed, uintptr_t stream);
+               long long pool_cap, uintptr_t arena_lens, uintptr_t failed, uintptr_t pool_failed, uintptr_t claim,
+               uintptr_t cand, uintptr_t result, uintptr_t stream);
 void permeate(int c, int m, int R, int C, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map, int dtype,
               uintptr_t corr, uintptr_t stream);
 void gather_rows(int n, uintptr_t dn, uintptr_t src_rows, uintptr_t dst_rows,

@@ -991,6 +991,127 @@ static void place_rounds_launches(int k, uintptr_t cells, uintptr_t mask, uintpt
                                   uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim,
                                   uintptr_t result, int rounds, uint64_t seed, uint64_t call, hipStream_t s);
 
+// Deterministic spawn placement (spawn_cells on the GPU; the reference samples the free pixels with
+// its RNG, world.py:910-920). New cell j draws up to kSpawnProbes uniform pixels of the owned rows
+// per round from its own Philox stream and bids for the first free one (atomicMin of j on the claim
+// map); the lowest bidder takes the pixel. Rounds are separated by grid barriers (a co-resident
+// grid, as place_rounds_coop_kernel), so every bid reads the occupancy of the round's start: the
+// winners, and so every position, are a function of the seed alone -- not of which wave's atomic
+// landed first, as with the racing claims before. Cells still unplaced after kMaxRounds rounds (a
+// nearly full map) are placed by one thread in index order, scanning from a drawn start. Winners
+// release their claims at the end. result[j]: the pixel (-1 and `failed` set: no free pixel left).
+constexpr int kSpawnProbes = 8;
+__global__ void __launch_bounds__(256) spawn_claim_coop_kernel(int k, long long base, long long n_pix, uint8_t* cell_map,
+                                                               uint64_t seed, uint64_t call, long long* cand, int* claim,
+                                                               long long* result, unsigned* ctl, unsigned* ctl_next,
+                                                               unsigned* err_host, int* failed) {
+  const unsigned nb = gridDim.x;
+  if (blockIdx.x == 0)
+    for (int j = threadIdx.x; j < kCtlWords; j += blockDim.x) ctl_next[j] = 0u;
+  const int stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned phase = 0;
+  __shared__ int s_left;
+  int r = 0;
+  for (; r < kMaxRounds; ++r) {
+    const uint64_t rc = call + ((uint64_t)r << 48);
+    for (int i = t0; i < k; i += stride) {
+      if (r == 0) __hip_atomic_store(result + i, -1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else if (__hip_atomic_load(result + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 0) continue;
+      Philox rng(seed, rc, (uint32_t)i);
+      long long px = -1;
+      for (int t = 0; t < kSpawnProbes; ++t) {
+        const long long q = base + (long long)rng.below64((uint64_t)n_pix);
+        if (!map_get(cell_map, q)) {
+          px = q;
+          break;
+        }
+      }
+      cand[i] = px;
+      if (px >= 0) atomicMin(claim + px, i);
+    }
+    grid_barrier(ctl, nb, phase, err_host);
+    if (threadIdx.x == 0) s_left = 0;
+    __syncthreads();
+    int left = 0;
+    for (int i = t0; i < k; i += stride) {
+      if (__hip_atomic_load(result + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 0) continue;
+      const long long px = cand[i];
+      if (px >= 0 && __hip_atomic_load(claim + px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == i) {
+        __hip_atomic_store(result + i, px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        map_set(cell_map, px);
+      } else {
+        ++left;
+      }
+    }
+    if (left) atomicAdd(&s_left, left);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_left) atomicAdd(ctl + 1 + r, (unsigned)s_left);
+    grid_barrier(ctl, nb, phase, err_host);
+    if (__hip_atomic_load(ctl + 1 + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) break;
+  }
+  // winners release their claims (a claimed pixel's claim is its winner's)
+  for (int i = t0; i < k; i += stride) {
+    const long long px = __hip_atomic_load(result + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (px >= 0) claim[px] = kNoClaim;
+  }
+  // a nearly full map: what the rounds left, in index order by one thread (deterministic)
+  if (r == kMaxRounds && blockIdx.x == 0 && threadIdx.x == 0) {
+    for (int i = 0; i < k; ++i) {
+      if (__hip_atomic_load(result + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 0) continue;
+      Philox rng(seed, call ^ 0x5DEECE66Dull, (uint32_t)i);
+      const long long start = (long long)rng.below64((uint64_t)n_pix);
+      long long got = -1;
+      for (long long q = 0; q < n_pix && got < 0; ++q) {
+        const long long px = base + (start + q) % n_pix;
+        if (!map_get(cell_map, px)) got = px;
+      }
+      if (got < 0) {
+        atomicOr(failed, 1);
+        break;
+      }
+      map_set(cell_map, got);
+      __hip_atomic_store(result + i, got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Launcher of spawn_claim_coop_kernel (maps.hip spawn_dev): rows [r_lo, r_hi) of a C-wide map, the
+// world's claim map (all kNoClaim between calls), per-cell scratch cand / result (k each).
+void spawn_claims(int k, int C, int r_lo, int r_hi, uintptr_t cell_map, uintptr_t claim, uintptr_t cand,
+                  uintptr_t result, uint64_t seed, uint64_t call, uintptr_t failed, hipStream_t s) {
+  if (k <= 0) return;
+  int dev = 0;
+  MS_HIP_CHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= kMaxDevices) throw std::runtime_error("spawn_claims: device index out of range");
+  if (!g_place_ctl[dev]) {
+    MS_HIP_CHECK(hipMalloc((void**)&g_place_ctl[dev], 2 * kCtlWords * sizeof(unsigned)));
+    MS_HIP_CHECK(hipMemset(g_place_ctl[dev], 0, 2 * kCtlWords * sizeof(unsigned)));
+    g_place_par[dev] = 0;
+  }
+  if (!g_place_err) {
+    MS_HIP_CHECK(hipHostMalloc((void**)&g_place_err, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
+    *g_place_err = 0;
+    MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_place_err_dev, g_place_err, 0));
+  }
+  static int resident[kMaxDevices] = {};
+  if (!resident[dev]) {
+    int per_cu = 0, cus = 0;
+    MS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)spawn_claim_coop_kernel, 256, 0));
+    MS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    resident[dev] = std::max(1, per_cu * cus);
+  }
+  // (a co-resident grid: every workgroup reaches the barriers; grid-stride over the cells)
+  const unsigned grid = std::min<unsigned>(std::min<unsigned>(cdiv(k, 256), (unsigned)g_coop_blocks),
+                                           (unsigned)resident[dev]);
+  unsigned* ctl = g_place_ctl[dev] + g_place_par[dev] * kCtlWords;
+  unsigned* ctl_next = g_place_ctl[dev] + (1 - g_place_par[dev]) * kCtlWords;
+  spawn_claim_coop_kernel<<<grid, 256, 0, s>>>(k, (long long)r_lo * C, (long long)(r_hi - r_lo) * C,
+                                               P_<uint8_t>(cell_map), seed, call, P_<long long>(cand), P_<int>(claim),
+                                               P_<long long>(result), ctl, ctl_next, g_place_err_dev, P_<int>(failed));
+  MS_LAUNCH_CHECK();
+  g_place_par[dev] ^= 1;
+}
+
 // Placement with a participation mask instead of a cell list (cells 0..n-1, priority = index).
 void place_rounds_mask(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap, bool vacate,
                        uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim, uintptr_t result,

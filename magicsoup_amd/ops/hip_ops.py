@@ -350,7 +350,10 @@ def spawn_issue(world, rows: torch.Tensor, lens: torch.Tensor, n0: int) -> None:
     lens = lens.to(torch.int32).contiguous()
     mm, corr = map_for_pixels(world)
     g, lab = world._genomes, world._labels
-    failed = _scratch(world).get("spawn_failed", 1, torch.int32, mm.device)
+    sc = _scratch(world)
+    failed = sc.get("spawn_failed", 1, torch.int32, mm.device)
+    cand = sc.get("sp_cand", k, torch.int64, mm.device)
+    result = sc.get("sp_result", k, torch.int64, mm.device)
     need = k * ((L_in + 15) // 16 * 16)
     g.ensure(need)  # (the genomes go to fresh pool space)
     seed, call = _rng()
@@ -358,7 +361,7 @@ def spawn_issue(world, rows: torch.Tensor, lens: torch.Tensor, n0: int) -> None:
                    _p(cols["cell_positions"].buf), _p(cols["cell_lifetimes"].buf), _p(cols["cell_divisions"].buf),
                    _p(cols["cell_molecules"].buf), _p(mm), _mdt(mm), _p(corr), _p(lab.data), int(lab.width),
                    _p(lab.lens), L_in, _p(rows), _p(lens), _p(g.data), _p(g.off), _p(g.top), g.pool_cap, _p(g.lens),
-                   _p(failed), _p(g.failed), _stream())
+                   _p(failed), _p(g.failed), _p(_claim_map(world)), _p(cand), _p(result), _stream())
     g.top_ub += need
 
 
@@ -622,6 +625,17 @@ apply_pending_scale = apply_pending
 
 
 # ---------------------------------------------------------------------------- placement
+def _claim_map(world) -> torch.Tensor:
+    """The world's placement claim map (int32 per pixel, 0x7FFFFFFF = unclaimed between calls)."""
+    R, C = geom(world)[:2]
+    dev = world.__dict__["_molmap"].device
+    claim = world.__dict__.get("_claim_map")
+    if claim is None or claim.numel() != R * C or claim.device != dev:
+        claim = torch.full((R * C,), 0x7FFFFFFF, dtype=torch.int32, device=dev)
+        world.__dict__["_claim_map"] = claim
+    return claim
+
+
 def _cell_map_bytes(world) -> torch.Tensor:
     cmap = world.cell_map
     return cmap.view(torch.uint8).reshape(-1)

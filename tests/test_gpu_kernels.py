@@ -1366,13 +1366,53 @@ def test_genome_pool_collect_layout_matches_sorted_reference():
 
 
 @pytest.mark.gpu
+def test_bench_steps_with_spawns_replay_bit_identically():
+    """30 bench steps (chemostat kill / divide, top-up spawns, the genome chains) from the same seed
+    in two FRESH worlds -- their initial populations spawned as well -- end bit-identical: the spawn's
+    pixel claims are priority rounds (world.hip spawn_claim_coop_kernel: lowest bidder wins, rounds
+    behind grid barriers), so a seed fixes which cell gets which pixel (the reference samples free
+    pixels from its RNG, world.py:910-920)."""
+    import random
+
+    import bench
+
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    runs = []
+    for _ in range(2):
+        random.seed(21)
+        ms.set_seed(21)
+        torch.manual_seed(21)
+        bench._CHEMOSTAT.update(divided=0, starved=0, steps=0, excess=None, last_d=0, last_s=0)
+        w = ms.World(chemistry=CHEMISTRY, map_size=96, device="cuda", seed=21)
+        w.spawn_cells(bench.random_genomes(3000, 500, "cuda"))
+        spawned = 0
+        for _ in range(30):
+            st = {}
+            bench.step(w, 3000, 500, atp, stats=st)
+            spawned += st.get("spawned", 0)
+        w.synchronize()
+        k = w.kinetics
+        runs.append({
+            "n": w.n_cells, "spawned": spawned, "positions": w.cell_positions.clone(),
+            "molecules": w.cell_molecules.clone(), "lifetimes": w.cell_lifetimes.clone(),
+            "divisions": w.cell_divisions.clone(), "cell_map": w.cell_map.clone(), "map": w.molecule_map.clone(),
+            "genomes": list(w.cell_genomes), "labels": list(w.cell_labels),
+            **{p: getattr(k, p).clone() for p in ("N", "A", "Kmr", "Vmax", "Ke")},
+        })
+    a, b = runs
+    assert a["spawned"] > 0  # (top-ups happened inside the replayed window)
+    bad = [key for key in a if not (torch.equal(a[key], b[key]) if isinstance(a[key], torch.Tensor) else a[key] == b[key])]
+    assert not bad, bad
+    bench._CHEMOSTAT.update(divided=0, starved=0, steps=0, excess=None, last_d=0, last_s=0)
+
+
 def test_gpu_step_loop_is_deterministic():
     """The reference loop as bench.py issues it (activity, kill, lazy division, queued
     recombination + mutation chain, degradation, diffusion next to the chain, lifetimes; no host
     synchronisation besides the API's own) replayed twice from one state with the same seeds ends in
     bit-identical worlds: the device placement, selections, genome chains, speculative activity and
-    stencil reductions do not depend on thread timing. (Only the spawn's pixel claims race -- both
-    runs start from one deep-copied world and spawn nothing.)"""
+    stencil reductions do not depend on thread timing. (Spawns are covered by
+    test_bench_steps_with_spawns_replay_bit_identically.)"""
     import random
 
     import bench
