@@ -16,6 +16,7 @@
 //     (or the final scatter) picks the state where the reference's global `torch.any` loop stops.
 //   3 part launches + 1 scatter launch per enzymatic_activity; no grid barriers, no host syncs.
 #include <algorithm>
+#include <unordered_map>
 
 #include "hip_common.h"
 #include "params.h"
@@ -1106,8 +1107,9 @@ __global__ void __launch_bounds__(kBlock, W) integrate_narrow_spec_kernel(Integr
 // compiled for W waves per SIMD: the path needs ~256 VGPRs to run without spills (316 B/lane of
 // scratch at 4 waves, 208 at 3, 44 at 2), so occupancy and spills trade (set_spl2_waves).
 template <int W>
-__global__ void __launch_bounds__(kBlock, W) integrate_spl2_spec_kernel(IntegrateArgs a) {
+__global__ void __launch_bounds__(kBlock, W) integrate_spl2_spec_kernel(const IntegrateArgs* __restrict__ args) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
+  const IntegrateArgs& a = args[0];  // (device memory, as integrate_spec_fused_kernel)
   unsigned bits = 0u;
   integrate_item_fast<64, kNzReg, true, 2>(a, smem, (int)blockIdx.x * (kBlock / 64) + (int)threadIdx.x / 64, bits,
                                            nullptr, nullptr);
@@ -1150,7 +1152,10 @@ __global__ void __launch_bounds__(kBlock, W) integrate_fused_kernel(IntegrateArg
 // at the front of the grid with as many blocks as there are such cells, each as 32-protein chains,
 // under the narrow cells' throughput work instead of after it. Cells that fit neither role (too
 // many proteins or non-zeros, large exponents) go to the overflow lists for the launches behind.
-__device__ __forceinline__ void integrate_wide_cells(const IntegrateArgs& aw, int* smem, unsigned& bits) {
+// (not inlined: the wide role's second copy of integrate_item_fast has a register allocation of its
+// own instead of adding its uniform values to the narrow path's -- 498 -> 76 SGPR spills with the
+// argument blocks in memory, below)
+__device__ __attribute__((noinline)) void integrate_wide_cells(const IntegrateArgs& aw, int* smem, unsigned& bits) {
   const int nw = *aw.count;  // (block-uniform: the multi-group cell's barriers need every wave)
   for (int item = (int)blockIdx.x; item < nw; item += (int)gridDim.x) {
     integrate_item_fast<32, kNzReg, true, 1, kBlock / 32>(aw, smem, item, bits, nullptr, nullptr);
@@ -1158,9 +1163,15 @@ __device__ __forceinline__ void integrate_wide_cells(const IntegrateArgs& aw, in
   }
 }
 
+// The two argument blocks (narrow, wide) are read from device memory (args[0], args[1]: written by
+// the input kernel before it, gather_bin_kernel) instead of being passed by value: by-value blocks
+// were loaded into SGPRs at the kernel start and spilled (498 SGPR spills, 84 B/lane of scratch at
+// the 80-VGPR cap); through a pointer the fields are loaded where they are used.
 template <int W>
-__global__ void __launch_bounds__(kBlock, W) integrate_spec_fused_kernel(IntegrateArgs a, IntegrateArgs aw) {
+__global__ void __launch_bounds__(kBlock, W) integrate_spec_fused_kernel(const IntegrateArgs* __restrict__ args) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
+  const IntegrateArgs& a = args[0];
+  const IntegrateArgs& aw = args[1];
   constexpr int kGroups = kBlock / 32;
   unsigned bits = 0u;
   if ((int)blockIdx.x < *aw.count) integrate_wide_cells(aw, smem, bits);
@@ -1483,8 +1494,14 @@ __global__ void __launch_bounds__(kBlock) gather_bin_kernel(int c, int s, int m,
                                                             const int64_t* prow, float trim0, float* snap,
                                                             int32_t* wide_list, unsigned* wide, unsigned* zero,
                                                             int nz, int32_t* zero_wc, float* save, int nparts,
-                                                            bool void_spec) {
+                                                            bool void_spec, IntegrateArgs pa, IntegrateArgs pw,
+                                                            IntegrateArgs* args_out) {
   clear_words(zero, nz, zero_wc);
+  // (the register launch's argument blocks into device memory: see integrate_spec_fused_kernel)
+  if (args_out && blockIdx.x == 0 && threadIdx.x == 0) {
+    args_out[0] = pa;
+    args_out[1] = pw;
+  }
   // (void_spec, mode bit 9, for tests: the unfit word starts set, so the exact launches run)
   if (blockIdx.x == 0 && threadIdx.x < ms::kEqIters * kMaxParts + 1)
     wide[4 + threadIdx.x] = (void_spec && threadIdx.x == ms::kEqIters * nparts) ? 1u : 0u;
@@ -1706,6 +1723,15 @@ static int slot_words_for(int P, int s, int sp) {
 // Would an integration of `s` signals in `nparts` parts take the speculative path (given the cell
 // lists and the speculation buffer)? Every rank of a decomposed world sees the same answer, also a
 // rank without cells (it still joins the all-reduces of the protocol it implies).
+// Per stream: device memory for the register launch's argument blocks (two IntegrateArgs), written
+// by the input kernel and read by integrate_spec_fused_kernel on the same stream.
+static std::unordered_map<hipStream_t, IntegrateArgs*> g_args_dev;
+static IntegrateArgs* args_block(hipStream_t st) {
+  IntegrateArgs*& p = g_args_dev[st];
+  if (!p) MS_HIP_CHECK(hipMalloc((void**)&p, 2 * sizeof(IntegrateArgs)));
+  return p;
+}
+
 bool integrate_spec_ok(int s, int nparts) {
   return s <= 128 && (g_integrate_mode & 8) == 0 && nparts >= 1 && nparts <= kMaxParts && (nparts & 1) == 1 &&
          (g_integrate_mode & 0xF8) == 0;
@@ -1784,17 +1810,6 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
     int32_t* wc3 = L + 2 * (size_t)c + 2;                      // sort order / histogram slots, unused here)
     unsigned* sflags = spec_w + 4;          // speculative flags (4 per part) + the unfit word
     if (spec_path) {
-    if (Gs == 32)
-      gather_bin_kernel<32><<<cdiv(c, kBlock / 32), kBlock, 0, st>>>(
-          c, s, m, R, C, P, X_io ? P_<float>(X_io) : nullptr, P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr,
-          P_<int32_t>(positions), P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr, trims[0], snaps[1], wl, spec_w, mk,
-          nz, zwc, X_io ? nullptr : P_<float>(save_buf), nparts, (g_integrate_mode & 512) != 0);
-    else
-      gather_bin_kernel<64><<<cdiv(c, kBlock / 64), kBlock, 0, st>>>(
-          c, s, m, R, C, P, X_io ? P_<float>(X_io) : nullptr, P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr,
-          P_<int32_t>(positions), P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr, trims[0], snaps[1], wl, spec_w, mk,
-          nz, zwc, X_io ? nullptr : P_<float>(save_buf), nparts, (g_integrate_mode & 512) != 0);
-    MS_LAUNCH_CHECK();
     IntegrateArgs a{};
     a.c = c; a.P = P; a.s = s;
     a.W = P_<int32_t>(W); a.Q = P_<float4>(Q); a.Kmr = P_<float>(Kmr);
@@ -1833,12 +1848,31 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
     IntegrateArgs ao = aw;  // the overflow list (rare) on 64-lane slots with 2 * kNzReg non-zeros
     ao.list = wl2;
     ao.count = wc2;
+    // the input kernel also stores the register launch's argument blocks in device memory (32-lane
+    // cells: narrow + wide for integrate_spec_fused_kernel; two signals per lane: the narrow block of
+    // integrate_spl2_spec_kernel)
+    IntegrateArgs an = a;
+    an.Ps = 64;
+    an.prelisted = 0;
+    const bool spl2 = Gs == 64 && s > 64;
+    IntegrateArgs* dargs = (Gs == 32 || spl2) ? args_block(st) : nullptr;
+    if (Gs == 32)
+      gather_bin_kernel<32><<<cdiv(c, kBlock / 32), kBlock, 0, st>>>(
+          c, s, m, R, C, P, X_io ? P_<float>(X_io) : nullptr, P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr,
+          P_<int32_t>(positions), P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr, trims[0], snaps[1], wl, spec_w, mk,
+          nz, zwc, X_io ? nullptr : P_<float>(save_buf), nparts, (g_integrate_mode & 512) != 0, a, aw, dargs);
+    else
+      gather_bin_kernel<64><<<cdiv(c, kBlock / 64), kBlock, 0, st>>>(
+          c, s, m, R, C, P, X_io ? P_<float>(X_io) : nullptr, P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr,
+          P_<int32_t>(positions), P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr, trims[0], snaps[1], wl, spec_w, mk,
+          nz, zwc, X_io ? nullptr : P_<float>(save_buf), nparts, (g_integrate_mode & 512) != 0, an, an, dargs);
+    MS_LAUNCH_CHECK();
     if (Gs == 32) {
       const size_t lds_fast = (size_t)(kBlock / 32) * fast_slot_words<32, kNzReg>() * 4;
       const size_t lds_fw = (size_t)(kBlock / 64) * fast_slot_words<64, kNzWide>() * 4;
       // (6 waves per SIMD: measured faster than 5 -- 96 VGPRs, fewer spills -- by 3-5 % on the
       // flagship state, profiles/r5/ab_integrator_*.log)
-      integrate_spec_fused_kernel<6><<<cdiv(c, kBlock / 32), kBlock, lds_fast, st>>>(a, aw);
+      integrate_spec_fused_kernel<6><<<cdiv(c, kBlock / 32), kBlock, lds_fast, st>>>(dargs);
       MS_LAUNCH_CHECK();
       if (dist_stage == 0 && g_rescue_mode && scatter) {
         // one launch for the overflow lists, the exact fallback and the write-back (see
@@ -1906,18 +1940,15 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
       // 64-lane cells: no wider register level for more than 64 active proteins, so the narrow
       // launch passes every cell it cannot take (too many proteins, non-zeros or large exponents) to
       // the overflow list; the 64-lane kNzWide launch passes what it cannot take on to the LDS list
-      IntegrateArgs an = a;
-      an.Ps = 64;
-      an.prelisted = 0;
       const size_t lds_n = (size_t)(kBlock / 64) *
                            (two ? fast_slot_words<64, kNzReg, 2>() : fast_slot_words<64, kNzReg>()) * 4;
       const size_t lds_fw =
           (size_t)(kBlock / 64) * (two ? fast_slot_words<64, kNzWide, 2>() : fast_slot_words<64, kNzWide>()) * 4;
       if (two) {
         const unsigned g2 = cdiv(c, kBlock / 64);
-        if (g_spl2_waves == 2) integrate_spl2_spec_kernel<2><<<g2, kBlock, lds_n, st>>>(an);
-        else if (g_spl2_waves == 3) integrate_spl2_spec_kernel<3><<<g2, kBlock, lds_n, st>>>(an);
-        else integrate_spl2_spec_kernel<4><<<g2, kBlock, lds_n, st>>>(an);
+        if (g_spl2_waves == 2) integrate_spl2_spec_kernel<2><<<g2, kBlock, lds_n, st>>>(dargs);
+        else if (g_spl2_waves == 3) integrate_spl2_spec_kernel<3><<<g2, kBlock, lds_n, st>>>(dargs);
+        else integrate_spl2_spec_kernel<4><<<g2, kBlock, lds_n, st>>>(dargs);
         MS_LAUNCH_CHECK();
         integrate_fast_kernel<64, kNzWide, true, true, 2><<<g_ovf_blocks, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
       } else {
