@@ -142,7 +142,7 @@ std::string rccl_guarded_wait(const std::vector<uintptr_t>& comms, uintptr_t str
   const auto t0 = std::chrono::steady_clock::now();
   std::string why;
   for (long long it = 0;; ++it) {
-    const hipError_t q = ev ? hipEventQuery(ev) : hipStreamQuery(s);
+    const hipError_t q = ev ? msd::event_query(ev) : msd::stream_query(s);
     if (q == hipSuccess) return std::string();
     if (q != hipErrorNotReady) MS_HIP_CHECK(q);
     // errors are polled every 256 queries (~tens of microseconds): the common case (a healthy job
@@ -177,6 +177,7 @@ void rccl_allreduce(uintptr_t comm, uintptr_t buf, long long count, int dtype, i
   static const ncclRedOp_t kO[] = {ncclSum, ncclMax, ncclMin};
   if (dtype < 0 || dtype > 3 || op < 0 || op > 2) throw std::invalid_argument("rccl_allreduce: bad dtype / op");
   if (count <= 0) return;
+  batch_flush();  // (the kernels recorded before it run first)
   void* p = reinterpret_cast<void*>(buf);
   check(api().AllReduce(p, p, (size_t)count, kT[dtype], kO[op], C_(comm), S_(stream)), "ncclAllReduce");
 }
@@ -192,6 +193,7 @@ void rccl_exchange(uintptr_t comm, int up, int down, uintptr_t send_up, long lon
   ncclComm_t c = C_(comm);
   hipStream_t s = S_(stream);
   if (n_send_up + n_send_down + n_recv_down + n_recv_up == 0) return;
+  batch_flush();  // (the kernels recorded before it run first)
   check(r.GroupStart(), "ncclGroupStart");
   try {
     if (n_send_up > 0) check(r.Send(reinterpret_cast<void*>(send_up), (size_t)n_send_up, ncclUint8, up, c, s), "ncclSend");

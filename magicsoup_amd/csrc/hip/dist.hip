@@ -588,10 +588,10 @@ void strip_marks(int C, int H, uintptr_t cell_map, int k, uintptr_t cells, uintp
                  uintptr_t dn, uintptr_t stream) {
   if (H < 2 || C < 1) throw std::invalid_argument("strip_marks: bad strip");
   if (!cells && !mask && k > 0) throw std::invalid_argument("strip_marks: give cells or a mask");
-  strip_occ_kernel<<<cdiv(C, 256), 256, 0, S_(stream)>>>(C, H, P_<uint8_t>(cell_map), P_<uint8_t>(up), P_<uint8_t>(dn));
+  msd::kl(strip_occ_kernel, cdiv(C, 256), 256, 0, S_(stream))(C, H, P_<uint8_t>(cell_map), P_<uint8_t>(up), P_<uint8_t>(dn));
   MS_LAUNCH_CHECK();
   if (k > 0) {
-    strip_div_kernel<<<cdiv(k, 256), 256, 0, S_(stream)>>>(k, cells ? P_<int64_t>(cells) : nullptr,
+    msd::kl(strip_div_kernel, cdiv(k, 256), 256, 0, S_(stream))(k, cells ? P_<int64_t>(cells) : nullptr,
                                                             mask ? P_<uint8_t>(mask) : nullptr, P_<int32_t>(pos), C,
                                                             H, P_<uint8_t>(up), P_<uint8_t>(dn));
     MS_LAUNCH_CHECK();
@@ -599,13 +599,13 @@ void strip_marks(int C, int H, uintptr_t cell_map, int k, uintptr_t cells, uintp
 }
 
 void strip_reserve(int C, int H, uintptr_t from_up, uintptr_t from_dn, uintptr_t cell_map, uintptr_t stream) {
-  strip_reserve_kernel<<<cdiv(C, 256), 256, 0, S_(stream)>>>(C, H, P_<uint8_t>(from_up), P_<uint8_t>(from_dn),
+  msd::kl(strip_reserve_kernel, cdiv(C, 256), 256, 0, S_(stream))(C, H, P_<uint8_t>(from_up), P_<uint8_t>(from_dn),
                                                               P_<uint8_t>(cell_map));
   MS_LAUNCH_CHECK();
 }
 
 void strip_clear(int C, int H, uintptr_t cell_map, uintptr_t stream) {
-  strip_clear_kernel<<<cdiv(C, 256), 256, 0, S_(stream)>>>(C, H, P_<uint8_t>(cell_map));
+  msd::kl(strip_clear_kernel, cdiv(C, 256), 256, 0, S_(stream))(C, H, P_<uint8_t>(cell_map));
   MS_LAUNCH_CHECK();
 }
 
@@ -618,7 +618,7 @@ void place_split(int k, uintptr_t result, uintptr_t cells, int C, int H, uintptr
   const long long tiles = std::max(1ll, ((long long)k + kSplitTile - 1) / kSplitTile);
   if (g_split_single && tiles <= kLbMaxTiles) {  // one launch (the status words of select_lb.h)
     const LbState lb = lb_begin(s);
-    place_split_lb_kernel<<<(unsigned)tiles, kSplitThreads, 0, s>>>(
+    msd::kl(place_split_lb_kernel, (unsigned)tiles, kSplitThreads, 0, s)(
         k, P_<long long>(result), cells ? P_<int64_t>(cells) : nullptr, C, H, lb.status, lb.gen, lb.err,
         P_<int64_t>(par), P_<int32_t>(npos), P_<int32_t>(counts), P_<int32_t>(hdr_up), P_<int32_t>(hdr_dn), lw, gw, m);
     MS_LAUNCH_CHECK();
@@ -626,15 +626,15 @@ void place_split(int k, uintptr_t result, uintptr_t cells, int C, int H, uintptr
   }
   if (tiles > g_split_cap) {
     if (g_split_tiles) {
-      MS_HIP_CHECK(hipStreamSynchronize(s));
-      MS_HIP_CHECK(hipFree(g_split_tiles));
+      MS_HIP_CHECK(msd::stream_synchronize(s));
+      MS_HIP_CHECK(msd::dev_free(g_split_tiles));
     }
     g_split_cap = std::max(tiles, 64ll);
-    MS_HIP_CHECK(hipMalloc((void**)&g_split_tiles, 3 * g_split_cap * sizeof(int32_t)));
+    MS_HIP_CHECK(msd::dev_malloc((void**)&g_split_tiles, 3 * g_split_cap * sizeof(int32_t)));
   }
-  place_split_count_kernel<<<(unsigned)tiles, kSplitThreads, 0, s>>>(k, P_<long long>(result), C, H, g_split_tiles);
+  msd::kl(place_split_count_kernel, (unsigned)tiles, kSplitThreads, 0, s)(k, P_<long long>(result), C, H, g_split_tiles);
   MS_LAUNCH_CHECK();
-  place_split_write_kernel<<<(unsigned)tiles, kSplitThreads, 0, s>>>(
+  msd::kl(place_split_write_kernel, (unsigned)tiles, kSplitThreads, 0, s)(
       k, P_<long long>(result), cells ? P_<int64_t>(cells) : nullptr, C, H, g_split_tiles, P_<int64_t>(par),
       P_<int32_t>(npos),
       P_<int32_t>(counts), P_<int32_t>(hdr_up), P_<int32_t>(hdr_dn), lw, gw, m);
@@ -651,7 +651,7 @@ void rec_pack(int k_up, int k_dn, uintptr_t par_up, uintptr_t pos_up, uintptr_t 
               uintptr_t stream) {
   if (k_up + k_dn <= 0) return;
   const RecCols w = rec_cols(mols, pos, life, div, gp, glen, gw, ldata, llen, lw, m);
-  rec_pack_kernel<<<k_up + k_dn, 64, 0, S_(stream)>>>(k_up, k_dn, P_<int64_t>(par_up), P_<int32_t>(pos_up),
+  msd::kl(rec_pack_kernel, k_up + k_dn, 64, 0, S_(stream))(k_up, k_dn, P_<int64_t>(par_up), P_<int32_t>(pos_up),
                                                       P_<int64_t>(par_dn), P_<int32_t>(pos_dn), w, child,
                                                       P_<uint8_t>(out_up), P_<uint8_t>(out_dn));
   MS_LAUNCH_CHECK();
@@ -664,7 +664,7 @@ void rec_unpack(int n0, int k_up, uintptr_t in_up, int up_lw, int up_gw, int k_d
   if (k_up + k_dn <= 0) return;
   if (up_lw % 4 || up_gw % 4 || dn_lw % 4 || dn_gw % 4) throw std::invalid_argument("rec_unpack: bad sender widths");
   const RecCols w = rec_cols(mols, pos, life, div, gp, glen, gw, ldata, llen, lw, m);
-  rec_unpack_kernel<<<k_up + k_dn, 64, 0, S_(stream)>>>(n0, k_up, P_<uint8_t>(in_up), up_lw, up_gw, k_dn,
+  msd::kl(rec_unpack_kernel, k_up + k_dn, 64, 0, S_(stream))(n0, k_up, P_<uint8_t>(in_up), up_lw, up_gw, k_dn,
                                                         P_<uint8_t>(in_dn), dn_lw, dn_gw, C, H, w,
                                                         P_<uint8_t>(cell_map));
   MS_LAUNCH_CHECK();
@@ -673,10 +673,10 @@ void rec_unpack(int n0, int k_up, uintptr_t in_up, int up_lw, int up_gw, int k_d
 void halo_pack(int m, int C, int H, int elem, uintptr_t map, uintptr_t send_up, uintptr_t send_dn, uintptr_t stream) {
   const unsigned g = cdiv((long long)m * C, 256);
   if (elem == 4)
-    halo_pack_kernel<uint32_t><<<g, 256, 0, S_(stream)>>>(m, C, H, P_<uint32_t>(map), P_<uint32_t>(send_up),
+    msd::kl(halo_pack_kernel<uint32_t>, g, 256, 0, S_(stream))(m, C, H, P_<uint32_t>(map), P_<uint32_t>(send_up),
                                                           P_<uint32_t>(send_dn));
   else if (elem == 2)
-    halo_pack_kernel<uint16_t><<<g, 256, 0, S_(stream)>>>(m, C, H, P_<uint16_t>(map), P_<uint16_t>(send_up),
+    msd::kl(halo_pack_kernel<uint16_t>, g, 256, 0, S_(stream))(m, C, H, P_<uint16_t>(map), P_<uint16_t>(send_up),
                                                           P_<uint16_t>(send_dn));
   else
     throw std::invalid_argument("halo_pack: element size must be 2 or 4");
@@ -686,10 +686,10 @@ void halo_pack(int m, int C, int H, int elem, uintptr_t map, uintptr_t send_up, 
 void halo_unpack(int m, int C, int H, int elem, uintptr_t map, uintptr_t from_up, uintptr_t from_dn, uintptr_t stream) {
   const unsigned g = cdiv((long long)m * C, 256);
   if (elem == 4)
-    halo_unpack_kernel<uint32_t><<<g, 256, 0, S_(stream)>>>(m, C, H, P_<uint32_t>(map), P_<uint32_t>(from_up),
+    msd::kl(halo_unpack_kernel<uint32_t>, g, 256, 0, S_(stream))(m, C, H, P_<uint32_t>(map), P_<uint32_t>(from_up),
                                                             P_<uint32_t>(from_dn));
   else if (elem == 2)
-    halo_unpack_kernel<uint16_t><<<g, 256, 0, S_(stream)>>>(m, C, H, P_<uint16_t>(map), P_<uint16_t>(from_up),
+    msd::kl(halo_unpack_kernel<uint16_t>, g, 256, 0, S_(stream))(m, C, H, P_<uint16_t>(map), P_<uint16_t>(from_up),
                                                             P_<uint16_t>(from_dn));
   else
     throw std::invalid_argument("halo_unpack: element size must be 2 or 4");
@@ -705,7 +705,7 @@ XbEvents xb_ev(uintptr_t evbuf, int E2) {
 // evbuf: int32[5 * 2E + 4] (event fields, then counts; counts[3] accumulates dropped events)
 void xb_prep(int C, int H, int n, uintptr_t pos, uintptr_t idx_map, uintptr_t lens, int width, uintptr_t len_up,
              uintptr_t len_dn, uintptr_t own1, uintptr_t ownH, uintptr_t stream) {
-  xb_prep_kernel<<<cdiv(C, 256), 256, 0, S_(stream)>>>(C, H, n, P_<int32_t>(pos), P_<int32_t>(idx_map),
+  msd::kl(xb_prep_kernel, cdiv(C, 256), 256, 0, S_(stream))(C, H, n, P_<int32_t>(pos), P_<int32_t>(idx_map),
                                                         P_<int32_t>(lens), width, P_<int32_t>(len_up),
                                                         P_<int32_t>(len_dn), P_<int32_t>(own1), P_<int32_t>(ownH));
   MS_LAUNCH_CHECK();
@@ -716,7 +716,7 @@ void xb_events(int C, int E, int slot_w, double p, int kcap, uint64_t seed_dn, u
                uintptr_t ownH, uintptr_t arena, uintptr_t off, uintptr_t evbuf, uintptr_t slots_dn, uintptr_t slots_up,
                uintptr_t stream) {
   if (E < 1 || slot_w < 4 || slot_w % 4) throw std::invalid_argument("xb_events: bad capacity / slot width");
-  xb_events_kernel<<<1, kXbThreads, 0, S_(stream)>>>(C, E, slot_w, p, kcap, seed_dn, seed_up, call,
+  msd::kl(xb_events_kernel, 1, kXbThreads, 0, S_(stream))(C, E, slot_w, p, kcap, seed_dn, seed_up, call,
                                                      P_<int32_t>(mine_dn), P_<int32_t>(from_dn), P_<int32_t>(mine_up),
                                                      P_<int32_t>(from_up), P_<int32_t>(own1), P_<int32_t>(ownH),
                                                      P_<uint8_t>(arena), P_<int64_t>(off), xb_ev(evbuf, 2 * E),
@@ -728,7 +728,7 @@ void xb_apply(int C, int E, int slot_w, uint64_t seed_dn, uint64_t seed_up, uint
               uintptr_t slots_dn, uintptr_t slots_up, uintptr_t recv_dn, uintptr_t recv_up, uintptr_t parts,
               int parts_cap, uintptr_t pair_count, uintptr_t out, int out_width, uintptr_t out_len,
               uintptr_t out_rows, uintptr_t other, uintptr_t nres, uintptr_t stream) {
-  xb_apply_kernel<<<2 * E, 64, 0, S_(stream)>>>(C, slot_w, seed_dn, seed_up, call, xb_ev(evbuf, 2 * E),
+  msd::kl(xb_apply_kernel, 2 * E, 64, 0, S_(stream))(C, slot_w, seed_dn, seed_up, call, xb_ev(evbuf, 2 * E),
                                                 P_<uint8_t>(slots_dn), P_<uint8_t>(slots_up), P_<uint8_t>(recv_dn),
                                                 P_<uint8_t>(recv_up), P_<int32_t>(parts), parts_cap,
                                                 pair_count ? P_<int>(pair_count) : nullptr, P_<uint8_t>(out),
@@ -738,7 +738,7 @@ void xb_apply(int C, int E, int slot_w, uint64_t seed_dn, uint64_t seed_up, uint
 }
 
 void release_dist_buffers() {
-  if (g_split_tiles) MS_HIP_CHECK(hipFree(g_split_tiles));
+  if (g_split_tiles) MS_HIP_CHECK(msd::dev_free(g_split_tiles));
   g_split_tiles = nullptr;
   g_split_cap = 0;
 }

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "hip_common.h"
+#include "bind_util.h"
 
 namespace py = pybind11;
 
@@ -40,16 +41,16 @@ void ev_release(uintptr_t e) {
 }
 
 void ev_record(uintptr_t e, uintptr_t stream) {
-  MS_HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(e), reinterpret_cast<hipStream_t>(stream)));
+  MS_HIP_CHECK(msd::event_record(reinterpret_cast<hipEvent_t>(e), reinterpret_cast<hipStream_t>(stream)));
 }
 
 // `stream` waits (device-side) for the work recorded in `e`
 void ev_wait(uintptr_t stream, uintptr_t e) {
-  MS_HIP_CHECK(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), reinterpret_cast<hipEvent_t>(e), 0));
+  MS_HIP_CHECK(msd::stream_wait_event(reinterpret_cast<hipStream_t>(stream), reinterpret_cast<hipEvent_t>(e), 0));
 }
 
 bool ev_query(uintptr_t e) {
-  const hipError_t r = hipEventQuery(reinterpret_cast<hipEvent_t>(e));
+  const hipError_t r = msd::event_query(reinterpret_cast<hipEvent_t>(e));
   if (r == hipErrorNotReady) return false;
   MS_HIP_CHECK(r);
   return true;
@@ -69,7 +70,7 @@ void ev_sync(uintptr_t e) {
     constexpr int64_t kSpinNs = 20'000'000;  // 20 ms
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned it = 0;; ++it) {
-      const hipError_t r = hipEventQuery(ev);
+      const hipError_t r = msd::event_query(ev);
       if (r == hipSuccess) return;
       if (r != hipErrorNotReady) MS_HIP_CHECK(r);
       __builtin_ia32_pause();
@@ -78,7 +79,7 @@ void ev_sync(uintptr_t e) {
         break;
     }
   }
-  MS_HIP_CHECK(hipEventSynchronize(ev));
+  MS_HIP_CHECK(msd::event_synchronize(ev));
 }
 
 // `dst` waits for everything issued to `src` so far (a fresh pooled event in between)
@@ -98,14 +99,14 @@ void release_events() {
 }
 
 void bind_events(py::module_& m) {
-  m.def("ev_acquire", &ev_acquire);
-  m.def("ev_release", &ev_release);
-  m.def("ev_record", &ev_record);
-  m.def("ev_wait", &ev_wait);
-  m.def("ev_query", &ev_query);
-  m.def("ev_sync", &ev_sync, py::call_guard<py::gil_scoped_release>());
-  m.def("set_event_spin", &set_event_spin, "1: host event waits spin before blocking (0: block at once)");
-  m.def("stream_join", &stream_join);
+  msd::gdef(m, "ev_acquire", &ev_acquire);
+  msd::gdef(m, "ev_release", &ev_release);
+  msd::gdef(m, "ev_record", &ev_record);
+  msd::gdef(m, "ev_wait", &ev_wait);
+  msd::gdef(m, "ev_query", &ev_query);
+  msd::gdef(m, "ev_sync", &ev_sync, py::call_guard<py::gil_scoped_release>());
+  msd::gdef(m, "set_event_spin", &set_event_spin, "1: host event waits spin before blocking (0: block at once)");
+  msd::gdef(m, "stream_join", &stream_join);
 }
 
 }  // namespace msd

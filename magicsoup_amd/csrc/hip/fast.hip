@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "rows.h"
+#include "bind_util.h"
 
 namespace msd {
 
@@ -198,7 +199,7 @@ void fast_threshold_masks(const FastWorld& f, int n, int mol, float kill_below, 
                           uintptr_t stream) {
   if (!f.ready) throw std::invalid_argument("fast_threshold_masks: descriptor not finalized");
   if (n <= 0 || mol < 0 || mol >= f.m) throw std::invalid_argument("fast_threshold_masks: bad cell count or molecule");
-  threshold_masks_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, f.m, mol, kill_below, divide_above, cost, kill_p, seed,
+  msd::kl(threshold_masks_kernel, cdiv(n, 256), 256, 0, S_(stream))(n, f.m, mol, kill_below, divide_above, cost, kill_p, seed,
                                                                   call, P_<float>(f.mols), P_<uint8_t>(kill),
                                                                   P_<uint8_t>(divide));
   MS_LAUNCH_CHECK();
@@ -207,7 +208,7 @@ void fast_threshold_masks(const FastWorld& f, int n, int mol, float kill_below, 
 // A mask over the n cells before the last fast_kill compacted with its survivors (f.sel, f.dcount)
 void fast_compact_mask(const FastWorld& f, int n, uintptr_t mask, uintptr_t out, uintptr_t stream) {
   if (!f.ready || n <= 0) throw std::invalid_argument("fast_compact_mask: descriptor / count");
-  compact_mask_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, P_<int>(f.dcount), P_<int64_t>(f.sel), P_<uint8_t>(mask),
+  msd::kl(compact_mask_kernel, cdiv(n, 256), 256, 0, S_(stream))(n, P_<int>(f.dcount), P_<int64_t>(f.sel), P_<uint8_t>(mask),
                                                                P_<uint8_t>(out));
   MS_LAUNCH_CHECK();
 }
@@ -280,7 +281,7 @@ void fast_dist_divide_a(const FastWorld& f, int n, uintptr_t mask, uintptr_t com
   place_split(n, f.result, 0, C, H, par3, npos3, st, st + 16, st + 32, lw, gw, f.m, stream);
   rccl_exchange(comm, up, down, st + 16, 16, st + 32, 16, st + 64, 16, st + 48, 16, stream);
   if (host_st)
-    MS_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(host_st), reinterpret_cast<const void*>(st),
+    MS_HIP_CHECK(msd::memcpy_async(reinterpret_cast<void*>(host_st), reinterpret_cast<const void*>(st),
                                 20 * sizeof(int32_t), hipMemcpyDeviceToHost, S_(stream)));
 }
 
@@ -342,7 +343,7 @@ void fast_dist_divide_b(const FastWorld& f, long long n0, uintptr_t comm, int up
     rec_unpack((int)(n0 + n_loc), in_up, rin_up, up_lw, up_gw, in_dn, rin_dn, dn_lw, dn_gw, C, H, f.mols, f.pos, f.life,
                f.div, f.gpool, f.g_lens, std::max(up_gw, dn_gw), f.l_data, f.l_lens, f.l_width, m, f.cell_map,
                stream);
-    fill_i64_kernel<<<cdiv(k_in, 256), 256, 0, s>>>(P_<int64_t>(f.slot) + n0 + n_loc, P_<int64_t>(zero_row), k_in);
+    msd::kl(fill_i64_kernel, cdiv(k_in, 256), 256, 0, s)(P_<int64_t>(f.slot) + n0 + n_loc, P_<int64_t>(zero_row), k_in);
     MS_LAUNCH_CHECK();
   }
   strip_clear(C, H, f.cell_map, stream);
@@ -392,17 +393,17 @@ void bind_fast(pybind11::module_& m) {
       .def_readwrite("dmask", &FastWorld::dmask)
       .def_readwrite("rounds", &FastWorld::rounds)
       .def("finalize", &FastWorld::finalize);
-  m.def("fast_kill", &fast_kill, "kill_cells(mask) in one call (status slot of the survivor count)");
-  m.def("fast_divide", &fast_divide, "divide_cells(mask) in one call (status slot of the winner count)");
-  m.def("fast_threshold_masks", &fast_threshold_masks, "threshold kill / replicate masks (and the payment)");
-  m.def("fast_compact_mask", &fast_compact_mask, "a mask compacted with the last fast_kill's survivors");
-  m.def("fast_kill_divide_where", &fast_kill_divide_where,
+  msd::gdef(m, "fast_kill", &fast_kill, "kill_cells(mask) in one call (status slot of the survivor count)");
+  msd::gdef(m, "fast_divide", &fast_divide, "divide_cells(mask) in one call (status slot of the winner count)");
+  msd::gdef(m, "fast_threshold_masks", &fast_threshold_masks, "threshold kill / replicate masks (and the payment)");
+  msd::gdef(m, "fast_compact_mask", &fast_compact_mask, "a mask compacted with the last fast_kill's survivors");
+  msd::gdef(m, "fast_kill_divide_where", &fast_kill_divide_where,
         "threshold kill / replicate masks + fast_kill_divide in one call (status slots of both counts)");
-  m.def("fast_kill_divide", &fast_kill_divide,
+  msd::gdef(m, "fast_kill_divide", &fast_kill_divide,
         "kill_cells(kill) + divide_cells(divide & survivors) in one call (status slots of both counts)");
-  m.def("fast_dist_divide_a", &fast_dist_divide_a, "strip divide protocol up to the synchronisation");
-  m.def("fast_dist_divide_b", &fast_dist_divide_b, "strip divide protocol after the synchronisation");
-  m.def("fast_dist_kill_divide_a", &fast_dist_kill_divide_a,
+  msd::gdef(m, "fast_dist_divide_a", &fast_dist_divide_a, "strip divide protocol up to the synchronisation");
+  msd::gdef(m, "fast_dist_divide_b", &fast_dist_divide_b, "strip divide protocol after the synchronisation");
+  msd::gdef(m, "fast_dist_kill_divide_a", &fast_dist_kill_divide_a,
         "strip kill / replicate step up to the division's synchronisation (status slot of the survivor count)");
 }
 

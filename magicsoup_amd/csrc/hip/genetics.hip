@@ -346,9 +346,9 @@ static void launch(int mode, int n, uintptr_t rows, uintptr_t arena, uintptr_t o
   a.gpb = gpb;
   const size_t lds = fixed + (a.gslot ? 0 : gpb * slot);
   const unsigned grid = cdiv(n, gpb);
-  if (mode == 0) translate_kernel<true, false><<<grid, gpb * 64, lds, S_(stream)>>>(a);
-  else if (mode == 1) translate_kernel<false, true><<<grid, gpb * 64, lds, S_(stream)>>>(a);
-  else translate_kernel<true, true><<<grid, gpb * 64, lds, S_(stream)>>>(a);
+  if (mode == 0) msd::kl(translate_kernel<true, false>, grid, gpb * 64, lds, S_(stream))(a);
+  else if (mode == 1) msd::kl(translate_kernel<false, true>, grid, gpb * 64, lds, S_(stream))(a);
+  else msd::kl(translate_kernel<true, true>, grid, gpb * 64, lds, S_(stream))(a);
   MS_LAUNCH_CHECK();
 }
 

@@ -14,6 +14,7 @@
 
 #include "hip_common.h"
 #include "params.h"
+#include "bind_util.h"
 
 namespace py = pybind11;
 
@@ -187,7 +188,7 @@ int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const Gp
   const uintptr_t tokens = c.take(4 * (size_t)cap * k.P * dcap * 5);
   const long long row = (long long)k.P * dcap * 5;
   const unsigned gz = (unsigned)std::max<long long>(1, std::min<long long>(cdiv((long long)cap * row, 256), 1024));
-  gp_zero_kernel<<<gz, 256, 0, s>>>(cap, P_<int>(dcnt), row, P_<int32_t>(tokens), P_<int32_t>(long_count));
+  msd::kl(gp_zero_kernel, gz, 256, 0, s)(cap, P_<int>(dcnt), row, P_<int32_t>(tokens), P_<int32_t>(long_count));
   MS_LAUNCH_CHECK();
   translate_fused(cap, cells, a.data, a.off, a.width, a.lens, g.small, g.dom_type, g.dt_entries, g.two_codon, g.dom_size,
                   g.dom_type_size, counts, ndom, k.P, dcap, tokens, long_list, long_count, dcnt, st);
@@ -196,7 +197,7 @@ int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const Gp
                          g.dom_size, g.dom_type_size, counts, ndom, k.P, dcap, tokens, long_list, gslot, long_count,
                          st);
   auto sl = status_slot();
-  gp_check_assign_kernel<<<1, 1024, 0, s>>>(cap, lcap, P_<int>(dcnt), P_<int32_t>(counts), P_<int32_t>(ndom),
+  msd::kl(gp_check_assign_kernel, 1, 1024, 0, s)(cap, lcap, P_<int>(dcnt), P_<int32_t>(counts), P_<int32_t>(ndom),
                                             P_<int32_t>(long_count), P_<int32_t>(per), k.P, dcap, P_<int64_t>(cells),
                                             P_<int64_t>(k.slot), P_<long long>(k.rtop), k.rec_cap, P_<int64_t>(roff),
                                             P_<int>(a.opflags), P_<int>(stat_cnt), sl.first);
@@ -297,7 +298,7 @@ __global__ void gp_begin_kernel(int* opflags, int* gflags, long long* d_rows, lo
 }
 
 void gp_begin(const GpArena& a, bool fresh, long long nrows, uintptr_t stream) {
-  gp_begin_kernel<<<1, 1, 0, S_(stream)>>>(P_<int>(a.opflags), P_<int>(a.gflags), P_<long long>(a.d_rows), nrows,
+  msd::kl(gp_begin_kernel, 1, 1, 0, S_(stream))(P_<int>(a.opflags), P_<int>(a.gflags), P_<long long>(a.d_rows), nrows,
                                            fresh ? 1 : 0);
   MS_LAUNCH_CHECK();
 }
@@ -439,7 +440,7 @@ std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpAren
   const int n = ar.n, L = ar.width;
   const int xr = extra.is_none() ? 0 : extra.attr("rows").cast<int>();
   if (xr && !nres) throw std::invalid_argument("gp_evolve: boundary rows need the result-row counter");
-  gp_begin3_kernel<<<1, 1, 0, s>>>(P_<int>(ar.opflags), P_<int>(am.opflags), P_<int>(au.opflags), P_<int>(ar.gflags),
+  msd::kl(gp_begin3_kernel, 1, 1, 0, s)(P_<int>(ar.opflags), P_<int>(am.opflags), P_<int>(au.opflags), P_<int>(ar.gflags),
                                    P_<long long>(ar.d_rows), nrows, fresh ? 1 : 0);
   MS_LAUNCH_CHECK();
   // recombination (gp_recombine's layout of blob_r, without its rebuild)
@@ -477,7 +478,7 @@ std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpAren
   Carve cu(blob_u);
   const uintptr_t ucells = cu.take(8 * (size_t)ucap), ucnt = cu.take(16);
   auto ps = status_slot();
-  gp_union_kernel<<<1, 256, 0, s>>>(ucap, mcap, P_<int>(ar.cnt2), P_<int64_t>(cells), P_<int>(am.cnt),
+  msd::kl(gp_union_kernel, 1, 256, 0, s)(ucap, mcap, P_<int>(ar.cnt2), P_<int64_t>(cells), P_<int>(am.cnt),
                                     P_<int64_t>(msel), arr0, narr, P_<int64_t>(ucells), P_<int>(ucnt),
                                     P_<int>(xr ? nres : ar.cnt),
                                     P_<int>(ar.opflags), P_<int>(am.opflags), ps.first,
@@ -488,10 +489,10 @@ std::pair<int, int> gp_evolve(const GpArena& ar, const GpArena& am, const GpAren
 }
 
 void bind_gp(py::module_& m) {
-  m.def("gp_evolve", &gp_evolve, "device-pipeline recombinate_cells() + mutate_cells() with one rebuild (no sync)");
-  m.def("gp_evolve_union_bytes", &gp_evolve_union_bytes);
+  msd::gdef(m, "gp_evolve", &gp_evolve, "device-pipeline recombinate_cells() + mutate_cells() with one rebuild (no sync)");
+  msd::gdef(m, "gp_evolve_union_bytes", &gp_evolve_union_bytes);
   // a pinned, device-mapped int64 (host pointer, device pointer) and its host-side read / write
-  m.def("mapped_i64", []() {
+  msd::gdef(m, "mapped_i64", []() {
     long long* h = nullptr;
     long long* d = nullptr;
     MS_HIP_CHECK(hipHostMalloc((void**)&h, sizeof(long long), hipHostMallocMapped | hipHostMallocCoherent));
@@ -499,10 +500,10 @@ void bind_gp(py::module_& m) {
     *h = -1;
     return std::make_pair(reinterpret_cast<uintptr_t>(h), reinterpret_cast<uintptr_t>(d));
   });
-  m.def("mapped_i64_read", [](uintptr_t h) {
+  msd::gdef(m, "mapped_i64_read", [](uintptr_t h) {
     return __atomic_load_n(reinterpret_cast<long long*>(h), __ATOMIC_ACQUIRE);
   });
-  m.def("mapped_i64_write", [](uintptr_t h, long long v) {
+  msd::gdef(m, "mapped_i64_write", [](uintptr_t h, long long v) {
     __atomic_store_n(reinterpret_cast<long long*>(h), v, __ATOMIC_RELEASE);
   });
   py::class_<GpArena>(m, "GpArena", py::module_local())
@@ -531,12 +532,12 @@ void bind_gp(py::module_& m) {
       .def_readwrite("energies", &GpKin::energies).def_readwrite("nw", &GpKin::nw).def_readwrite("nk", &GpKin::nk)
       .def_readwrite("nsg", &GpKin::nsg).def_readwrite("nh", &GpKin::nh).def_readwrite("nv", &GpKin::nv)
       .def_readwrite("abs_temp", &GpKin::abs_temp).def_readwrite("gas", &GpKin::gas);
-  m.def("gp_begin", &gp_begin);
-  m.def("gp_blob_bytes", &gp_blob_bytes);
-  m.def("gp_layout", &gp_layout);
-  m.def("gp_mutate", &gp_mutate, "device-pipeline point mutations over all genomes (one call, no sync)");
-  m.def("gp_recombine", &gp_recombine, "device-pipeline recombinations over neighbour slot keys (one call, no sync)");
-  m.def("gp_rebuild", &gp_rebuild, "device-pipeline translation + parameter build of listed cells (no sync)");
+  msd::gdef(m, "gp_begin", &gp_begin);
+  msd::gdef(m, "gp_blob_bytes", &gp_blob_bytes);
+  msd::gdef(m, "gp_layout", &gp_layout);
+  msd::gdef(m, "gp_mutate", &gp_mutate, "device-pipeline point mutations over all genomes (one call, no sync)");
+  msd::gdef(m, "gp_recombine", &gp_recombine, "device-pipeline recombinations over neighbour slot keys (one call, no sync)");
+  msd::gdef(m, "gp_rebuild", &gp_rebuild, "device-pipeline translation + parameter build of listed cells (no sync)");
 }
 
 }  // namespace msd

@@ -6,6 +6,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "launch.h"
 #include "ms_common.h"
 
 #define MS_HIP_CHECK(expr)                                                                  \

@@ -1728,7 +1728,7 @@ static int slot_words_for(int P, int s, int sp) {
 static std::unordered_map<hipStream_t, IntegrateArgs*> g_args_dev;
 static IntegrateArgs* args_block(hipStream_t st) {
   IntegrateArgs*& p = g_args_dev[st];
-  if (!p) MS_HIP_CHECK(hipMalloc((void**)&p, 2 * sizeof(IntegrateArgs)));
+  if (!p) MS_HIP_CHECK(msd::dev_malloc((void**)&p, 2 * sizeof(IntegrateArgs)));
   return p;
 }
 
@@ -1857,12 +1857,12 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
     const bool spl2 = Gs == 64 && s > 64;
     IntegrateArgs* dargs = (Gs == 32 || spl2) ? args_block(st) : nullptr;
     if (Gs == 32)
-      gather_bin_kernel<32><<<cdiv(c, kBlock / 32), kBlock, 0, st>>>(
+      msd::kl(gather_bin_kernel<32>, cdiv(c, kBlock / 32), kBlock, 0, st)(
           c, s, m, R, C, P, X_io ? P_<float>(X_io) : nullptr, P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr,
           P_<int32_t>(positions), P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr, trims[0], snaps[1], wl, spec_w, mk,
           nz, zwc, X_io ? nullptr : P_<float>(save_buf), nparts, (g_integrate_mode & 512) != 0, a, aw, dargs);
     else
-      gather_bin_kernel<64><<<cdiv(c, kBlock / 64), kBlock, 0, st>>>(
+      msd::kl(gather_bin_kernel<64>, cdiv(c, kBlock / 64), kBlock, 0, st)(
           c, s, m, R, C, P, X_io ? P_<float>(X_io) : nullptr, P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr,
           P_<int32_t>(positions), P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr, trims[0], snaps[1], wl, spec_w, mk,
           nz, zwc, X_io ? nullptr : P_<float>(save_buf), nparts, (g_integrate_mode & 512) != 0, an, an, dargs);
@@ -1872,7 +1872,7 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
       const size_t lds_fw = (size_t)(kBlock / 64) * fast_slot_words<64, kNzWide>() * 4;
       // (6 waves per SIMD: measured faster than 5 -- 96 VGPRs, fewer spills -- by 3-5 % on the
       // flagship state, profiles/r5/ab_integrator_*.log)
-      integrate_spec_fused_kernel<6><<<cdiv(c, kBlock / 32), kBlock, lds_fast, st>>>(dargs);
+      msd::kl(integrate_spec_fused_kernel<6>, cdiv(c, kBlock / 32), kBlock, lds_fast, st)(dargs);
       MS_LAUNCH_CHECK();
       if (dist_stage == 0 && g_rescue_mode && scatter) {
         // one launch for the overflow lists, the exact fallback and the write-back (see
@@ -1886,7 +1886,7 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
           *g_rescue_err = 0;
           MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_rescue_err_dev, g_rescue_err, 0));
         }
-        integrate_fast_kernel<64, kNzWide, true, true><<<g_ovf_blocks, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
+        msd::kl(integrate_fast_kernel<64, kNzWide, true, true>, g_ovf_blocks, kBlock, lds_fw, st)(ao, nullptr, nullptr);
         MS_LAUNCH_CHECK();
         RescueArgs r{};
         r.lb = a;
@@ -1930,11 +1930,11 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
         r.X_out = X_io ? P_<float>(X_io) : nullptr;
         r.all_from_snap = spec_wb ? 0 : 1;
         const size_t lds_r = (size_t)r.cps * slot_bytes;
-        integrate_rescue_kernel<<<g_rescue_blocks, kBlock, lds_r, st>>>(r);
+        msd::kl(integrate_rescue_kernel, g_rescue_blocks, kBlock, lds_r, st)(r);
         MS_LAUNCH_CHECK();
         return 1;
       }
-      integrate_fast_kernel<64, kNzWide, true, true><<<g_ovf_blocks, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
+      msd::kl(integrate_fast_kernel<64, kNzWide, true, true>, g_ovf_blocks, kBlock, lds_fw, st)(ao, nullptr, nullptr);
       MS_LAUNCH_CHECK();
     } else {
       // 64-lane cells: no wider register level for more than 64 active proteins, so the narrow
@@ -1946,16 +1946,16 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
           (size_t)(kBlock / 64) * (two ? fast_slot_words<64, kNzWide, 2>() : fast_slot_words<64, kNzWide>()) * 4;
       if (two) {
         const unsigned g2 = cdiv(c, kBlock / 64);
-        if (g_spl2_waves == 2) integrate_spl2_spec_kernel<2><<<g2, kBlock, lds_n, st>>>(dargs);
-        else if (g_spl2_waves == 3) integrate_spl2_spec_kernel<3><<<g2, kBlock, lds_n, st>>>(dargs);
-        else integrate_spl2_spec_kernel<4><<<g2, kBlock, lds_n, st>>>(dargs);
+        if (g_spl2_waves == 2) msd::kl(integrate_spl2_spec_kernel<2>, g2, kBlock, lds_n, st)(dargs);
+        else if (g_spl2_waves == 3) msd::kl(integrate_spl2_spec_kernel<3>, g2, kBlock, lds_n, st)(dargs);
+        else msd::kl(integrate_spl2_spec_kernel<4>, g2, kBlock, lds_n, st)(dargs);
         MS_LAUNCH_CHECK();
-        integrate_fast_kernel<64, kNzWide, true, true, 2><<<g_ovf_blocks, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
+        msd::kl(integrate_fast_kernel<64, kNzWide, true, true, 2>, g_ovf_blocks, kBlock, lds_fw, st)(ao, nullptr, nullptr);
       } else {
-        integrate_fast_kernel<64, kNzReg, false, true><<<cdiv(c, kBlock / 64), kBlock, lds_n, st>>>(an, nullptr,
+        msd::kl(integrate_fast_kernel<64, kNzReg, false, true>, cdiv(c, kBlock / 64), kBlock, lds_n, st)(an, nullptr,
                                                                                                  nullptr);
         MS_LAUNCH_CHECK();
-        integrate_fast_kernel<64, kNzWide, true, true><<<g_ovf_blocks, kBlock, lds_fw, st>>>(ao, nullptr, nullptr);
+        msd::kl(integrate_fast_kernel<64, kNzWide, true, true>, g_ovf_blocks, kBlock, lds_fw, st)(ao, nullptr, nullptr);
       }
       MS_LAUNCH_CHECK();
     }
@@ -1966,8 +1966,8 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
       l.count = wc3;
       l.Ps = P;
       l.slot_words = slot_words;
-      if (Gs == 32) integrate_spec_lds_kernel<32><<<std::min<unsigned>(grid, 256), cps * 32, lds, st>>>(l);
-      else integrate_spec_lds_kernel<64><<<std::min<unsigned>(grid, 256), cps * 64, lds, st>>>(l);
+      if (Gs == 32) msd::kl(integrate_spec_lds_kernel<32>, std::min<unsigned>(grid, 256), cps * 32, lds, st)(l);
+      else msd::kl(integrate_spec_lds_kernel<64>, std::min<unsigned>(grid, 256), cps * 64, lds, st)(l);
       MS_LAUNCH_CHECK();
     }
     }  // spec_path
@@ -1991,8 +1991,8 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
       f.spec_check = sflags;
       f.spec_n = nparts;
       f.copy_to = part == nparts - 1 ? mk : nullptr;
-      if (Gs == 32) integrate_part_kernel<32, true><<<grid, cps * 32, lds, st>>>(f);
-      else integrate_part_kernel<64, true><<<grid, cps * 64, lds, st>>>(f);
+      if (Gs == 32) msd::kl(integrate_part_kernel<32, true>, grid, cps * 32, lds, st)(f);
+      else msd::kl(integrate_part_kernel<64, true>, grid, cps * 64, lds, st)(f);
       MS_LAUNCH_CHECK();
     }
   } else if (part_begin == 0) {
@@ -2002,9 +2002,9 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
     if (nz > kBlock) throw std::invalid_argument("integrate: too many parts");
     int32_t* zwc = fast_path ? P_<int32_t>(lists) + 2 * (size_t)c + 1 : nullptr;
     if (X_io) {
-      load_x_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(c, s, P_<float>(X_io), snaps[1], mk, nz, zwc);
+      msd::kl(load_x_kernel, cdiv((long long)c * s, kBlock), kBlock, 0, st)(c, s, P_<float>(X_io), snaps[1], mk, nz, zwc);
     } else {
-      gather_x_kernel<<<cdiv((long long)c * s, kBlock), kBlock, 0, st>>>(c, s, m, R, C, P_<float>(cell_mols),
+      msd::kl(gather_x_kernel, cdiv((long long)c * s, kBlock), kBlock, 0, st)(c, s, m, R, C, P_<float>(cell_mols),
                                                                           P_<void>(molmap), map_dtype, corr,
                                                                           P_<int32_t>(positions), snaps[1], mk, nz,
                                                                           zwc);
@@ -2074,10 +2074,10 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
     // mode bit 5: skip the 64-lane level (the whole wide list takes the LDS path; for A/B)
     const bool fw = (g_integrate_mode & 32) == 0;
     if (sorted && part_begin == 0) {
-      na_hist_kernel<<<cdiv(c, 256), 256, 0, st>>>(c, P, P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr, na, hist,
+      msd::kl(na_hist_kernel, cdiv(c, 256), 256, 0, st)(c, P, P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr, na, hist,
                                                     total);
       MS_LAUNCH_CHECK();
-      na_scatter_kernel<<<cdiv(c, 256), 256, 0, st>>>(c, na, hist, cursor, order);
+      msd::kl(na_scatter_kernel, cdiv(c, 256), 256, 0, st)(c, na, hist, cursor, order);
       MS_LAUNCH_CHECK();
     }
     for (int part = part_begin; part < part_end; ++part) {
@@ -2096,23 +2096,23 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
       // occupancy target leaves)
       const bool fused = G == 32 && fw && part > 0 && (g_integrate_mode & 64) == 0;
       if (fused) {
-        integrate_fused_kernel<32><<<cdiv(c, cps) + kFusedWideBlocks, kBlock, lds_fast, st>>>(a, aw, kFusedWideBlocks);
+        msd::kl(integrate_fused_kernel<32>, cdiv(c, cps) + kFusedWideBlocks, kBlock, lds_fast, st)(a, aw, kFusedWideBlocks);
         MS_LAUNCH_CHECK();
       } else {
         if (G == 32)
-          integrate_fast_kernel<32, kNzReg, false><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
+          msd::kl(integrate_fast_kernel<32, kNzReg, false>, cdiv(c, cps), kBlock, lds_fast, st)(a, part == 0 ? wl : nullptr, wc);
         else if (two)
-          integrate_fast_kernel<64, kNzReg, false, false, 2><<<cdiv(c, cps), kBlock, lds_fast, st>>>(
+          msd::kl(integrate_fast_kernel<64, kNzReg, false, false, 2>, cdiv(c, cps), kBlock, lds_fast, st)(
               a, part == 0 ? wl : nullptr, wc);
         else
-          integrate_fast_kernel<64, kNzReg, false><<<cdiv(c, cps), kBlock, lds_fast, st>>>(a, part == 0 ? wl : nullptr, wc);
+          msd::kl(integrate_fast_kernel<64, kNzReg, false>, cdiv(c, cps), kBlock, lds_fast, st)(a, part == 0 ? wl : nullptr, wc);
         MS_LAUNCH_CHECK();
         if (fw) {
           if (two)
-            integrate_fast_kernel<64, kNzWide, true, false, 2><<<grid_fw, kBlock, lds_fw, st>>>(
+            msd::kl(integrate_fast_kernel<64, kNzWide, true, false, 2>, grid_fw, kBlock, lds_fw, st)(
                 aw, part == 0 ? wl2 : nullptr, wc2);
           else
-            integrate_fast_kernel<64, kNzWide, true><<<grid_fw, kBlock, lds_fw, st>>>(aw, part == 0 ? wl2 : nullptr, wc2);
+            msd::kl(integrate_fast_kernel<64, kNzWide, true>, grid_fw, kBlock, lds_fw, st)(aw, part == 0 ? wl2 : nullptr, wc2);
           MS_LAUNCH_CHECK();
         }
       }
@@ -2120,8 +2120,8 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
       a.count = fw ? wc2 : wc;
       a.Ps = P;
       a.slot_words = slot_words;
-      if (G == 32) integrate_part_kernel<32, true><<<gridw, cpsw * G, ldsw, st>>>(a);
-      else integrate_part_kernel<64, true><<<gridw, cpsw * G, ldsw, st>>>(a);
+      if (G == 32) msd::kl(integrate_part_kernel<32, true>, gridw, cpsw * G, ldsw, st)(a);
+      else msd::kl(integrate_part_kernel<64, true>, gridw, cpsw * G, ldsw, st)(a);
       MS_LAUNCH_CHECK();
     }
   } else {
@@ -2135,8 +2135,8 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
     int32_t* lst = P_<int32_t>(lists);
     int32_t* cnt = lst ? lst + 2 * (size_t)c : nullptr;
     if (binned && part_begin == 0) {
-      MS_HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), st));
-      bin_cells_kernel<<<cdiv(c, 256), 256, 0, st>>>(c, P, kNarrowP, P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr,
+      MS_HIP_CHECK(msd::memset_async(cnt, 0, 2 * sizeof(int32_t), st));
+      msd::kl(bin_cells_kernel, cdiv(c, 256), 256, 0, st)(c, P, kNarrowP, P_<float4>(Q), prow ? P_<int64_t>(prow) : nullptr,
                                                      lst, cnt);
       MS_LAUNCH_CHECK();
     }
@@ -2167,8 +2167,8 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
     }
     for (int part = part_begin; part < part_end; ++part) {
       if (conc) {
-        MS_HIP_CHECK(hipEventRecord(ev_fork, st));
-        MS_HIP_CHECK(hipStreamWaitEvent(side, ev_fork, 0));
+        MS_HIP_CHECK(msd::event_record(ev_fork, st));
+        MS_HIP_CHECK(msd::stream_wait_event(side, ev_fork, 0));
       }
       for (int li = nl - 1; li >= 0; --li) {  // wide first: its long chains start early
         const Launch& L = launches[li];
@@ -2193,19 +2193,19 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
         a.count = L.count;
         a.Ps = L.Ps;
         if (G == 16) {
-          integrate_part_kernel<16, false><<<grid, threads, lds, ls>>>(a);
+          msd::kl(integrate_part_kernel<16, false>, grid, threads, lds, ls)(a);
         } else if (G == 32) {
-          if (stride) integrate_part_kernel<32, true><<<grid, threads, lds, ls>>>(a);
-          else integrate_part_kernel<32, false><<<grid, threads, lds, ls>>>(a);
+          if (stride) msd::kl(integrate_part_kernel<32, true>, grid, threads, lds, ls)(a);
+          else msd::kl(integrate_part_kernel<32, false>, grid, threads, lds, ls)(a);
         } else {
-          if (stride) integrate_part_kernel<64, true><<<grid, threads, lds, ls>>>(a);
-          else integrate_part_kernel<64, false><<<grid, threads, lds, ls>>>(a);
+          if (stride) msd::kl(integrate_part_kernel<64, true>, grid, threads, lds, ls)(a);
+          else msd::kl(integrate_part_kernel<64, false>, grid, threads, lds, ls)(a);
         }
         MS_LAUNCH_CHECK();
       }
       if (conc) {
-        MS_HIP_CHECK(hipEventRecord(ev_join, side));
-        MS_HIP_CHECK(hipStreamWaitEvent(st, ev_join, 0));
+        MS_HIP_CHECK(msd::event_record(ev_join, side));
+        MS_HIP_CHECK(msd::stream_wait_event(st, ev_join, 0));
       }
     }
   }
@@ -2213,7 +2213,7 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
   // domain-decomposed caller runs it as a separate call once those flags are global
   if (scatter && part_end == nparts && nparts > 0) {
     const int last = nparts - 1;
-    integrate_scatter_kernel<<<(unsigned)std::min<long long>(cdiv((long long)c * s, kBlock), 2048), kBlock, 0, st>>>(
+    msd::kl(integrate_scatter_kernel, (unsigned)std::min<long long>(cdiv((long long)c * s, kBlock), 2048), kBlock, 0, st)(
         c, s, m, R, C, snaps[last & 1], mk + ms::kEqIters * last, n_iters, P_<int32_t>(positions),
         P_<float>(cell_mols), P_<void>(molmap), map_dtype, corr, X_io ? P_<float>(X_io) : nullptr,
         spec_any ? spec_w : nullptr, spec_any && spec_wb ? spec_w + 4 : nullptr, nparts,
@@ -2256,7 +2256,7 @@ void pack_params(long long items, int s, uintptr_t N, uintptr_t Nf, uintptr_t Nb
                  uintptr_t Kmf, uintptr_t Kmb, uintptr_t Ke, uintptr_t W, uintptr_t Q, uintptr_t overflow,
                  uintptr_t stream) {
   if (items <= 0 || s <= 0) return;
-  pack_params_kernel<<<cdiv(items * s, kBlock), kBlock, 0, S_(stream)>>>(
+  msd::kl(pack_params_kernel, cdiv(items * s, kBlock), kBlock, 0, S_(stream))(
       items, s, P_<int32_t>(N), P_<int32_t>(Nf), P_<int32_t>(Nb), P_<int32_t>(A), P_<float>(Vmax), P_<float>(Kmf),
       P_<float>(Kmb), P_<float>(Ke), P_<int32_t>(W), P_<float4>(Q), P_<int>(overflow));
   MS_LAUNCH_CHECK();
@@ -2293,9 +2293,9 @@ void build_params(int n, int P, int D, int Pt, int s, uintptr_t tokens, uintptr_
   // (the group is the narrowest power of two covering the signals: 16 lanes for the 14-molecule
   // chemistry, where 32-lane groups left 18 of every 32 lanes idle; the energy butterfly only loses
   // exact zero terms, so the bits are the same)
-  if (s <= 16) build_params_kernel<16><<<grid(16), kBlock, 0, S_(stream)>>>(b);
-  else if (s <= 32) build_params_kernel<32><<<grid(32), kBlock, 0, S_(stream)>>>(b);
-  else build_params_kernel<64><<<grid(64), kBlock, 0, S_(stream)>>>(b);
+  if (s <= 16) msd::kl(build_params_kernel<16>, grid(16), kBlock, 0, S_(stream))(b);
+  else if (s <= 32) msd::kl(build_params_kernel<32>, grid(32), kBlock, 0, S_(stream))(b);
+  else msd::kl(build_params_kernel<64>, grid(64), kBlock, 0, S_(stream))(b);
   MS_LAUNCH_CHECK();
 }
 
@@ -2362,7 +2362,7 @@ void assign_records(int n, uintptr_t dn, uintptr_t nprot, uintptr_t cells, uintp
   if (n <= 0) return;
   if (width < 0 || width > kRecMaxProteins) throw std::invalid_argument("assign_records: protein width too large");
   if (rcap > (long long)kRecOffMask) throw std::invalid_argument("assign_records: record capacity too large");
-  assign_records_kernel<<<1, 1024, 0, S_(stream)>>>(n, dn ? P_<int>(dn) : nullptr, P_<int32_t>(nprot),
+  msd::kl(assign_records_kernel, 1, 1024, 0, S_(stream))(n, dn ? P_<int>(dn) : nullptr, P_<int32_t>(nprot),
                                                     cells ? P_<int64_t>(cells) : nullptr, P_<int64_t>(slot),
                                                     P_<long long>(rtop), rcap, width, P_<int64_t>(roff), P_<int>(flags));
   MS_LAUNCH_CHECK();
@@ -2372,7 +2372,7 @@ void records_to_dense(int n, int P, int s, uintptr_t slot, uintptr_t W, uintptr_
                       uintptr_t Qd, uintptr_t Kmrd, uintptr_t stream) {
   if (n <= 0 || P <= 0) return;
   const unsigned g = (unsigned)std::min<long long>(cdiv((long long)n * P * s, 256), 8192);
-  records_to_dense_kernel<<<g, 256, 0, S_(stream)>>>(n, P, s, slot ? P_<int64_t>(slot) : nullptr, P_<int32_t>(W),
+  msd::kl(records_to_dense_kernel, g, 256, 0, S_(stream))(n, P, s, slot ? P_<int64_t>(slot) : nullptr, P_<int32_t>(W),
                                                      P_<float4>(Q), P_<float>(Kmr), P_<int32_t>(Wd), P_<float4>(Qd),
                                                      P_<float>(Kmrd));
   MS_LAUNCH_CHECK();
@@ -2382,7 +2382,7 @@ void records_move(int n, int s, uintptr_t slot, uintptr_t new_off, uintptr_t W, 
                   uintptr_t W2, uintptr_t Q2, uintptr_t Kmr2, uintptr_t slot_out, uintptr_t stream) {
   if (n <= 0) return;
   const unsigned g = (unsigned)std::min<long long>(cdiv((long long)n * 64, 256), 8192);
-  records_move_kernel<<<g, 256, 0, S_(stream)>>>(n, s, P_<int64_t>(slot), P_<int64_t>(new_off), P_<int32_t>(W),
+  msd::kl(records_move_kernel, g, 256, 0, S_(stream))(n, s, P_<int64_t>(slot), P_<int64_t>(new_off), P_<int32_t>(W),
                                                  P_<float4>(Q), P_<float>(Kmr), P_<int32_t>(W2), P_<float4>(Q2),
                                                  P_<float>(Kmr2), P_<int64_t>(slot_out));
   MS_LAUNCH_CHECK();

@@ -442,8 +442,7 @@ __global__ void __launch_bounds__(256) diffuse_stencil8_kernel(const T* __restri
 // (corr_out: also the new per-species correction of a single-process map, (before - after) / n_pix,
 // which otherwise takes a diffuse_corr launch after the totals were all-reduced)
 __global__ void __launch_bounds__(256) diffuse_reduce_kernel(const double* partials, int tiles, double* totals,
-                                                             bool accumulate, float* corr_out = nullptr,
-                                                             double n_pix = 1.0) {
+                                                             bool accumulate, float* corr_out, double n_pix) {
   __shared__ double sb[4], sa[4];
   const int mol = blockIdx.x;
   double b = 0.0, a = 0.0;
@@ -551,6 +550,19 @@ __global__ void __launch_bounds__(256) scale_planes_kernel(T* map, const float* 
   const long long total = plane * m;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
     st(map + i, ld(map + i) * f[i / plane]);
+}
+
+// cell_molecules (rows, m) *= f[mol] (the cells' share of degrade_molecules: torch's mul_ with the
+// factor row broadcast, one fp32 product per entry)
+__global__ void __launch_bounds__(256) scale_rows_kernel(float* x, const float* f, long long total, int m) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
+    x[i] = x[i] * f[i % m];
+}
+
+// x[i] += v (increment_cell_lifetimes)
+__global__ void __launch_bounds__(256) add_i32_kernel(int32_t* x, long long n, int v) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    x[i] += v;
 }
 
 // ---------------------------------------------------------------- cell <-> pixel exchanges
@@ -754,19 +766,19 @@ static int stencil_launch(int m, int R, int C, int r_lo, int r_hi, int wrap, uin
   if (v8) {
     const int ntiles = (int)(grid.x * grid.y * grid.z);
     const int blocks = g_stencil_blocks > 0 ? std::min(ntiles, g_stencil_blocks) : ntiles;
-    MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), C % 512 == 0, (diffuse_stencil8_kernel<T, PF, FULL><<<blocks, 256, 0, st_>>>(
+    MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), C % 512 == 0, (msd::kl(diffuse_stencil8_kernel<T, PF, FULL>, blocks, 256, 0, st_)(
                                P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
                                corr ? P_<float>(corr) : nullptr, g, P_<double>(partials), (int)grid.x, (int)grid.y,
                                ntiles, vband))));
   } else if (v4) {
     const int ntiles = (int)(grid.x * grid.y * grid.z);
     const int blocks = g_stencil_blocks > 0 ? std::min(ntiles, g_stencil_blocks) : ntiles;
-    MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), C % 256 == 0, (diffuse_stencil4_kernel<T, PF, FULL><<<blocks, 256, 0, st_>>>(
+    MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), C % 256 == 0, (msd::kl(diffuse_stencil4_kernel<T, PF, FULL>, blocks, 256, 0, st_)(
                                P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
                                corr ? P_<float>(corr) : nullptr, g, P_<double>(partials), (int)grid.x, (int)grid.y,
                                ntiles, vband))));
   } else {
-    MS_MAP_DISPATCH(dtype, (diffuse_stencil_kernel<T><<<grid, 64 * kWaves, 0, st_>>>(
+    MS_MAP_DISPATCH(dtype, (msd::kl(diffuse_stencil_kernel<T>, grid, 64 * kWaves, 0, st_)(
                                P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
                                corr ? P_<float>(corr) : nullptr, g, P_<double>(partials))));
   }
@@ -781,7 +793,7 @@ void diffuse_stencil(int m, int R, int C, int r_lo, int r_hi, int wrap, uintptr_
   // stencil split into interior rows, issued while the halo rows are exchanged, and boundary rows)
   if (m <= 0 || r_hi <= r_lo) return;
   const int tiles = stencil_launch(m, R, C, r_lo, r_hi, wrap, map, tmp, wa, wb, scale, corr, partials, dtype, stream);
-  diffuse_reduce_kernel<<<m, 256, 0, S_(stream)>>>(P_<double>(partials), tiles, P_<double>(totals), accumulate != 0,
+  msd::kl(diffuse_reduce_kernel, m, 256, 0, S_(stream))(P_<double>(partials), tiles, P_<double>(totals), accumulate != 0,
                                                    corr_out ? P_<float>(corr_out) : nullptr, n_pix);
   MS_LAUNCH_CHECK();
 }
@@ -802,15 +814,15 @@ static int boundary_launch(int m, int R, int C, int r_lo, int r_hi, uintptr_t ma
     const MGeom g = mgeom(R, C, row, row + 1, 0);
     double* part = P_<double>(partials) + (size_t)b * tiles * 2;
     if (v8) {
-      MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), C % 512 == 0, (diffuse_stencil8_kernel<T, PF, FULL><<<tiles, 256, 0, st_>>>(
+      MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), C % 512 == 0, (msd::kl(diffuse_stencil8_kernel<T, PF, FULL>, tiles, 256, 0, st_)(
                                  P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
                                  corr ? P_<float>(corr) : nullptr, g, part, gx, 1, tiles, kVBand))));
     } else if (v4) {
-      MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), C % 256 == 0, (diffuse_stencil4_kernel<T, PF, FULL><<<tiles, 256, 0, st_>>>(
+      MS_MAP_DISPATCH(dtype, MS_PF_DISPATCH(stencil_pf(dtype), C % 256 == 0, (msd::kl(diffuse_stencil4_kernel<T, PF, FULL>, tiles, 256, 0, st_)(
                                  P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
                                  corr ? P_<float>(corr) : nullptr, g, part, gx, 1, tiles, kVBand))));
     } else {
-      MS_MAP_DISPATCH(dtype, (diffuse_stencil_kernel<T><<<dim3(gx, 1, m), 64 * kWaves, 0, st_>>>(
+      MS_MAP_DISPATCH(dtype, (msd::kl(diffuse_stencil_kernel<T>, dim3(gx, 1, m), 64 * kWaves, 0, st_)(
                                  P_<T>(map), P_<T>(tmp), P_<float>(wa), P_<float>(wb), scale ? P_<float>(scale) : nullptr,
                                  corr ? P_<float>(corr) : nullptr, g, part)));
     }
@@ -828,9 +840,9 @@ void diffuse_boundary(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, ui
   const int tiles = gx * m;
   // partials of both launches: (mol, tile) pairs, launch b at offset b * tiles; reduce them as one
   // (2 * gx)-tile layout per molecule requires mol-major order, so reduce each launch and accumulate
-  diffuse_reduce_kernel<<<m, 256, 0, st_>>>(P_<double>(partials), gx, P_<double>(totals), true);
+  msd::kl(diffuse_reduce_kernel, m, 256, 0, st_)(P_<double>(partials), gx, P_<double>(totals), true, nullptr, 1.0);
   MS_LAUNCH_CHECK();
-  diffuse_reduce_kernel<<<m, 256, 0, st_>>>(P_<double>(partials) + (size_t)tiles * 2, gx, P_<double>(totals), true);
+  msd::kl(diffuse_reduce_kernel, m, 256, 0, st_)(P_<double>(partials) + (size_t)tiles * 2, gx, P_<double>(totals), true, nullptr, 1.0);
   MS_LAUNCH_CHECK();
 }
 
@@ -866,7 +878,7 @@ void diffuse_strip(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintp
   const int ti = stencil_launch(m, R, C, r_lo + 1, r_hi - 1, 0, map, tmp, wa, wb, scale, corr, partials, dtype, stream);
   stream_join(stream, halo_stream);
   const int gx = boundary_launch(m, R, C, r_lo, r_hi, map, tmp, wa, wb, scale, corr, partials_b, dtype, stream);
-  diffuse_reduce_strip_kernel<<<m, 256, 0, S_(stream)>>>(P_<double>(partials), ti, P_<double>(partials_b), gx, m,
+  msd::kl(diffuse_reduce_strip_kernel, m, 256, 0, S_(stream))(P_<double>(partials), ti, P_<double>(partials_b), gx, m,
                                                          P_<double>(totals));
   MS_LAUNCH_CHECK();
   rccl_allreduce(comm, totals, 2ll * m, 2 /* float64 */, 0 /* sum */, stream);
@@ -878,7 +890,7 @@ void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uin
   if (m <= 0) return;
   const long long plane = (long long)R * C, start = (long long)r_lo * C, span = (long long)(r_hi - r_lo) * C;
   const unsigned g = std::min<long long>(cdiv((span + 3) / 4 * m, 256), 8192);
-  MS_MAP_DISPATCH(dtype, (diffuse_correct_kernel<T><<<g, 256, 0, S_(stream)>>>(P_<T>(tmp), P_<T>(map),
+  MS_MAP_DISPATCH(dtype, (msd::kl(diffuse_correct_kernel<T>, g, 256, 0, S_(stream))(P_<T>(tmp), P_<T>(map),
                                                                                P_<double>(totals), n_pix, plane,
                                                                                start, span, m)));
   MS_LAUNCH_CHECK();
@@ -886,7 +898,7 @@ void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uin
 
 void diffuse_corr(int m, uintptr_t totals, double n_pix, uintptr_t corr, uintptr_t stream) {
   if (m <= 0) return;
-  diffuse_corr_kernel<<<cdiv(m, 64), 64, 0, S_(stream)>>>(P_<double>(totals), m, n_pix, P_<float>(corr));
+  msd::kl(diffuse_corr_kernel, cdiv(m, 64), 64, 0, S_(stream))(P_<double>(totals), m, n_pix, P_<float>(corr));
   MS_LAUNCH_CHECK();
 }
 
@@ -916,7 +928,7 @@ void map_totals(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_
   if (m <= 0 || r_hi <= r_lo) return;
   const long long px = (long long)(r_hi - r_lo) * C;
   const dim3 g((unsigned)std::max<long long>(1, std::min<long long>(cdiv(px, 256 * 8), 512)), (unsigned)m);
-  MS_MAP_DISPATCH(dtype, (map_totals_kernel<T><<<g, 256, 0, S_(stream)>>>(
+  MS_MAP_DISPATCH(dtype, (msd::kl(map_totals_kernel<T>, g, 256, 0, S_(stream))(
                              P_<T>(map), R, C, r_lo, r_hi, corr ? P_<float>(corr) : nullptr,
                              f ? P_<float>(f) : nullptr, P_<double>(out))));
   MS_LAUNCH_CHECK();
@@ -925,7 +937,7 @@ void map_totals(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_
 void apply_pending(int m, long long plane, uintptr_t map, uintptr_t corr, uintptr_t f, int dtype, uintptr_t stream) {
   if (m <= 0 || plane <= 0 || (!corr && !f)) return;
   const unsigned g = std::min<long long>(cdiv(plane * m, 256), 8192);
-  MS_MAP_DISPATCH(dtype, (apply_pending_kernel<T><<<g, 256, 0, S_(stream)>>>(
+  MS_MAP_DISPATCH(dtype, (msd::kl(apply_pending_kernel<T>, g, 256, 0, S_(stream))(
                              P_<T>(map), corr ? P_<float>(corr) : nullptr, f ? P_<float>(f) : nullptr, plane, m)));
   MS_LAUNCH_CHECK();
 }
@@ -934,7 +946,7 @@ void health_scan(int planes, long long span, long long stride, uintptr_t x, int 
                  uintptr_t stream) {
   if (planes <= 0 || span <= 0) return;
   const unsigned g = std::min<long long>(cdiv((long long)planes * span, 256), 4096);
-  MS_MAP_DISPATCH(dtype, (health_kernel<T><<<g, 256, 0, S_(stream)>>>(P_<T>(x), planes, span, stride, shift,
+  MS_MAP_DISPATCH(dtype, (msd::kl(health_kernel<T>, g, 256, 0, S_(stream))(P_<T>(x), planes, span, stride, shift,
                                                                         P_<int>(flags))));
   MS_LAUNCH_CHECK();
 }
@@ -942,14 +954,28 @@ void health_scan(int planes, long long span, long long stride, uintptr_t x, int 
 void scale_planes(int m, long long plane, uintptr_t map, uintptr_t f, int dtype, uintptr_t stream) {
   if (m <= 0 || plane <= 0) return;
   const unsigned g = std::min<long long>(cdiv(plane * m, 256), 8192);
-  MS_MAP_DISPATCH(dtype, (scale_planes_kernel<T><<<g, 256, 0, S_(stream)>>>(P_<T>(map), P_<float>(f), plane, m)));
+  MS_MAP_DISPATCH(dtype, (msd::kl(scale_planes_kernel<T>, g, 256, 0, S_(stream))(P_<T>(map), P_<float>(f), plane, m)));
+  MS_LAUNCH_CHECK();
+}
+
+void scale_rows(long long rows, int m, uintptr_t x, uintptr_t f, uintptr_t stream) {
+  if (rows <= 0 || m <= 0) return;
+  const unsigned g = std::min<long long>(cdiv(rows * m, 256), 4096);
+  msd::kl(scale_rows_kernel, g, 256, 0, S_(stream))(P_<float>(x), P_<float>(f), rows * m, m);
+  MS_LAUNCH_CHECK();
+}
+
+void add_i32(long long n, uintptr_t x, int v, uintptr_t stream) {
+  if (n <= 0) return;
+  const unsigned g = std::min<long long>(cdiv(n, 256), 4096);
+  msd::kl(add_i32_kernel, g, 256, 0, S_(stream))(P_<int32_t>(x), n, v);
   MS_LAUNCH_CHECK();
 }
 
 void spill_free(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
                 uintptr_t cell_map, int dtype, uintptr_t corr, uintptr_t stream) {
   if (k <= 0 || m <= 0) return;
-  MS_MAP_DISPATCH(dtype, (spill_free_kernel<T><<<cdiv((long long)k * m, 256), 256, 0, S_(stream)>>>(
+  MS_MAP_DISPATCH(dtype, (msd::kl(spill_free_kernel<T>, cdiv((long long)k * m, 256), 256, 0, S_(stream))(
                              k, m, P_<int64_t>(idxs), nullptr, P_<int32_t>(pos), C, (long long)R * C,
                              P_<float>(cell_mols), P_<T>(map), P_<uint8_t>(cell_map), P_<float>(corr))));
   MS_LAUNCH_CHECK();
@@ -960,7 +986,7 @@ void threshold_spill(int n, int m, int mol, float kill_below, float divide_above
                      uintptr_t map, uintptr_t cell_map, int dtype, uintptr_t corr, uintptr_t stream) {
   if (n <= 0 || m <= 0) return;
   const int cpb = std::max(1, 256 / m);
-  MS_MAP_DISPATCH(dtype, (threshold_spill_kernel<T><<<cdiv(n, cpb), cpb == 1 ? 256 : cpb * m, 0, S_(stream)>>>(
+  MS_MAP_DISPATCH(dtype, (msd::kl(threshold_spill_kernel<T>, cdiv(n, cpb), cpb == 1 ? 256 : cpb * m, 0, S_(stream))(
                              n, m, mol, kill_below, divide_above, cost, kill_p, seed, call, P_<float>(mols),
                              P_<uint8_t>(kill), P_<uint8_t>(divide), P_<int32_t>(pos), C, (long long)R * C, P_<T>(map),
                              P_<uint8_t>(cell_map), P_<float>(corr))));
@@ -970,7 +996,7 @@ void threshold_spill(int n, int m, int mol, float kill_below, float divide_above
 void spill_free_mask(int n, int m, uintptr_t dead, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
                      uintptr_t cell_map, int dtype, uintptr_t corr, uintptr_t stream) {
   if (n <= 0 || m <= 0) return;
-  MS_MAP_DISPATCH(dtype, (spill_free_kernel<T><<<cdiv((long long)n * m, 256), 256, 0, S_(stream)>>>(
+  MS_MAP_DISPATCH(dtype, (msd::kl(spill_free_kernel<T>, cdiv((long long)n * m, 256), 256, 0, S_(stream))(
                              n, m, nullptr, P_<uint8_t>(dead), P_<int32_t>(pos), C, (long long)R * C,
                              P_<float>(cell_mols), P_<T>(map), P_<uint8_t>(cell_map), P_<float>(corr))));
   MS_LAUNCH_CHECK();
@@ -1032,7 +1058,7 @@ void spawn_dev(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uint
   if (!claim || !cand || !result) throw std::invalid_argument("spawn_dev: claim map and scratch required");
   hipStream_t s = S_(stream);
   spawn_claims(k, C, r_lo, r_hi, cell_map, claim, cand, result, seed, call, failed, s);
-  spawn_init_kernel<<<cdiv(k, 256), 256, 0, s>>>(k, R, C, P_<long long>(result), seed, call, n0, m, P_<int32_t>(pos),
+  msd::kl(spawn_init_kernel, cdiv(k, 256), 256, 0, s)(k, R, C, P_<long long>(result), seed, call, n0, m, P_<int32_t>(pos),
                                                  P_<int32_t>(lifetimes), P_<int32_t>(divisions), P_<float>(cell_mols),
                                                  P_<void>(map), dtype, corr ? P_<float>(corr) : nullptr,
                                                  P_<uint8_t>(labels), label_w, P_<int32_t>(label_lens), P_<int>(failed));
@@ -1065,7 +1091,7 @@ __global__ void __launch_bounds__(256) cell_state_io_kernel(int n, int m, const 
 void cell_state_io(int n, int m, uintptr_t pos, int R, int C, uintptr_t map, int dtype, uintptr_t cell_mols,
                    uintptr_t buf, bool restore, uintptr_t stream) {
   if (n <= 0 || m <= 0) return;
-  cell_state_io_kernel<<<cdiv((long long)n * m, 256), 256, 0, S_(stream)>>>(
+  msd::kl(cell_state_io_kernel, cdiv((long long)n * m, 256), 256, 0, S_(stream))(
       n, m, P_<int32_t>(pos), C, (long long)R * C, P_<void>(map), dtype, P_<float>(cell_mols), P_<float>(buf),
       restore ? 1 : 0);
   MS_LAUNCH_CHECK();
@@ -1074,7 +1100,7 @@ void cell_state_io(int n, int m, uintptr_t pos, int R, int C, uintptr_t map, int
 void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map, int dtype,
             uintptr_t corr, uintptr_t stream) {
   if (k <= 0 || m <= 0) return;
-  MS_MAP_DISPATCH(dtype, (pickup_kernel<T><<<cdiv((long long)k * m, 256), 256, 0, S_(stream)>>>(
+  MS_MAP_DISPATCH(dtype, (msd::kl(pickup_kernel<T>, cdiv((long long)k * m, 256), 256, 0, S_(stream))(
                              k, m, P_<int64_t>(idxs), P_<int32_t>(pos), C, (long long)R * C, P_<float>(cell_mols),
                              P_<T>(map), P_<float>(corr))));
   MS_LAUNCH_CHECK();
@@ -1083,7 +1109,7 @@ void pickup(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t
 void permeate(int c, int m, int R, int C, uintptr_t pos, uintptr_t perm, uintptr_t cell_mols, uintptr_t map, int dtype,
               uintptr_t corr, uintptr_t stream) {
   if (c <= 0 || m <= 0) return;
-  MS_MAP_DISPATCH(dtype, (permeate_kernel<T><<<cdiv((long long)c * m, 256), 256, 0, S_(stream)>>>(
+  MS_MAP_DISPATCH(dtype, (msd::kl(permeate_kernel<T>, cdiv((long long)c * m, 256), 256, 0, S_(stream))(
                              c, m, (long long)R * C, C, P_<int32_t>(pos), P_<float>(perm), P_<float>(cell_mols),
                              P_<T>(map), P_<float>(corr))));
   MS_LAUNCH_CHECK();

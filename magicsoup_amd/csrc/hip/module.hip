@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "hip_common.h"
+#include "bind_util.h"
 
 namespace py = pybind11;
 
@@ -57,6 +58,8 @@ void map_totals(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_
 void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uintptr_t tmp, uintptr_t totals,
                      double n_pix, int dtype, uintptr_t stream);
 void scale_planes(int m, long long plane, uintptr_t map, uintptr_t f, int dtype, uintptr_t stream);
+void scale_rows(long long rows, int m, uintptr_t x, uintptr_t f, uintptr_t stream);
+void add_i32(long long n, uintptr_t x, int v, uintptr_t stream);
 void health_scan(int planes, long long span, long long stride, uintptr_t x, int dtype, int shift, uintptr_t flags,
                  uintptr_t stream);
 void spill_free(int k, int m, uintptr_t idxs, uintptr_t pos, int R, int C, uintptr_t cell_mols, uintptr_t map,
@@ -95,7 +98,7 @@ void bind_events(py::module_& m);
 // process-wide pinned / device buffers and streams of the extension while the HIP runtime (and a
 // profiler's interception layer, which finalises in the C exit handlers after Python's) is intact.
 void release_static() {
-  MS_HIP_CHECK(hipDeviceSynchronize());
+  MS_HIP_CHECK(msd::device_synchronize());
   release_select_buffers();
   release_dist_buffers();
   release_world_buffers();
@@ -243,6 +246,7 @@ void xb_apply(int C, int E, int slot_w, uint64_t seed_dn, uint64_t seed_up, uint
 void bind_gp(py::module_& m);
 void bind_pool(py::module_& m);
 void bind_fast(py::module_& m);
+void bind_launch(py::module_& m);
 }  // namespace msd
 
 namespace {
@@ -252,137 +256,140 @@ std::atomic<uint64_t> g_call{0};
 
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "magicsoup_amd gfx950 (MI355X) device kernels";
-  m.def("set_seed", [](uint64_t s) {
+  msd::gdef(m, "set_seed", [](uint64_t s) {
     g_seed.store(s);
     g_call.store(0);
   });
-  m.def("next_call", []() { return py::make_tuple(g_seed.load(), g_call.fetch_add(1) + 1); },
+  msd::gdef(m, "next_call", []() { return py::make_tuple(g_seed.load(), g_call.fetch_add(1) + 1); },
         "(seed, call) for a fresh Philox stream family");
-  m.def("get_rng_state", []() { return py::make_tuple(g_seed.load(), g_call.load()); },
+  msd::gdef(m, "get_rng_state", []() { return py::make_tuple(g_seed.load(), g_call.load()); },
         "(seed, calls drawn) of the device Philox streams");
-  m.def("set_rng_state", [](uint64_t s, uint64_t c) {
+  msd::gdef(m, "set_rng_state", [](uint64_t s, uint64_t c) {
     g_seed.store(s);
     g_call.store(c);
   }, "restore a get_rng_state() value");
-  m.def("device_arch", []() {
+  msd::gdef(m, "device_arch", []() {
     hipDeviceProp_t p;
     int dev = 0;
     MS_HIP_CHECK(hipGetDevice(&dev));
     MS_HIP_CHECK(hipGetDeviceProperties(&p, dev));
     return std::string(p.gcnArchName);
   });
-  m.def("integrate", &msd::integrate);
-  m.def("integrate_spec_ok", &msd::integrate_spec_ok);
-  m.def("integrate_dist", &msd::integrate_dist);
-  m.def("release_static", &msd::release_static);
+  msd::gdef(m, "integrate", &msd::integrate);
+  msd::gdef(m, "integrate_spec_ok", &msd::integrate_spec_ok);
+  msd::gdef(m, "integrate_dist", &msd::integrate_dist);
+  msd::gdef(m, "release_static", &msd::release_static);
   msd::bind_events(m);
-  m.def("build_params", &msd::build_params);
-  m.def("assign_records", &msd::assign_records, "ragged parameter records for built cells (one workgroup scan)");
-  m.def("records_to_dense", &msd::records_to_dense, "dense (n, P, s) view of the ragged parameter records");
-  m.def("records_move", &msd::records_move, "collection: every cell's records to an exclusive-scan offset");
-  m.def("pack_params", &msd::pack_params);
-  m.def("diffuse_stencil", &msd::diffuse_stencil);
-  m.def("diffuse_correct", &msd::diffuse_correct);
-  m.def("diffuse_corr", &msd::diffuse_corr);
-  m.def("diffuse_boundary", &msd::diffuse_boundary);
-  m.def("diffuse_boundary_partials_len", &msd::diffuse_boundary_partials_len);
-  m.def("diffuse_strip", &msd::diffuse_strip);
-  m.def("map_totals", &msd::map_totals, "per-species float64 totals of owned map rows (pending corr / scale applied)");
-  m.def("apply_pending", &msd::apply_pending);
-  m.def("diffuse_partials_len", &msd::diffuse_partials_len);
-  m.def("scale_planes", &msd::scale_planes);
-  m.def("health_scan", &msd::health_scan);
-  m.def("gather_rows", &msd::gather_rows);
-  m.def("neighbor_slots", &msd::neighbor_slots);
-  m.def("rec_count_keys", &msd::rec_count_keys);
-  m.def("spill_free", &msd::spill_free);
-  m.def("pickup", &msd::pickup);
-  m.def("spill_free_mask", &msd::spill_free_mask);
-  m.def("place_rounds", &msd::place_rounds);
-  m.def("place_rounds_mask", &msd::place_rounds_mask, "cooperative placement over cells selected by a mask");
-  m.def("set_place_tail", &msd::set_place_tail, "1: single-launch placement with one grid barrier + a one-workgroup tail of the later rounds");
-  m.def("set_overflow_blocks", &msd::set_overflow_blocks, "workgroups of the integrator's strided overflow-list launch");
-  m.def("set_coop_blocks", &msd::set_coop_blocks, "workgroups of the cooperative placement (A/B)");
-  m.def("set_stencil_vec", &msd::set_stencil_vec, "diffusion stencil columns per lane: 8 (default), 4 or 1");
-  m.def("set_stencil_prefetch", &msd::set_stencil_prefetch, "rows the vector stencils load ahead (-1 auto, 0-3)");
-  m.def("set_stencil_band", &msd::set_stencil_band, "rows per wave band of the vector stencils (16-256; 0 = the default 64)");
-  m.def("set_stencil_blocks", &msd::set_stencil_blocks, "blocks of the vector diffusion stencil (0: one per tile)");
-  m.def("set_place_mode", &msd::set_place_mode, "0 single-launch placement, ordinary launch (default), 1 multi-launch rounds, 2 single launch as a cooperative launch");
-  m.def("place_error_take", &msd::place_error_take,
+  msd::bind_launch(m);
+  msd::gdef(m, "build_params", &msd::build_params);
+  msd::gdef(m, "assign_records", &msd::assign_records, "ragged parameter records for built cells (one workgroup scan)");
+  msd::gdef(m, "records_to_dense", &msd::records_to_dense, "dense (n, P, s) view of the ragged parameter records");
+  msd::gdef(m, "records_move", &msd::records_move, "collection: every cell's records to an exclusive-scan offset");
+  msd::gdef(m, "pack_params", &msd::pack_params);
+  msd::gdef(m, "diffuse_stencil", &msd::diffuse_stencil);
+  msd::gdef(m, "diffuse_correct", &msd::diffuse_correct);
+  msd::gdef(m, "diffuse_corr", &msd::diffuse_corr);
+  msd::gdef(m, "diffuse_boundary", &msd::diffuse_boundary);
+  msd::gdef(m, "diffuse_boundary_partials_len", &msd::diffuse_boundary_partials_len);
+  msd::gdef(m, "diffuse_strip", &msd::diffuse_strip);
+  msd::gdef(m, "map_totals", &msd::map_totals, "per-species float64 totals of owned map rows (pending corr / scale applied)");
+  msd::gdef(m, "apply_pending", &msd::apply_pending);
+  msd::gdef(m, "diffuse_partials_len", &msd::diffuse_partials_len);
+  msd::gdef(m, "scale_planes", &msd::scale_planes);
+  msd::gdef(m, "scale_rows", &msd::scale_rows, "x (rows, m) *= f[col] in place (fp32)");
+  msd::gdef(m, "add_i32", &msd::add_i32, "x[:n] += v in place (int32)");
+  msd::gdef(m, "health_scan", &msd::health_scan);
+  msd::gdef(m, "gather_rows", &msd::gather_rows);
+  msd::gdef(m, "neighbor_slots", &msd::neighbor_slots);
+  msd::gdef(m, "rec_count_keys", &msd::rec_count_keys);
+  msd::gdef(m, "spill_free", &msd::spill_free);
+  msd::gdef(m, "pickup", &msd::pickup);
+  msd::gdef(m, "spill_free_mask", &msd::spill_free_mask);
+  msd::gdef(m, "place_rounds", &msd::place_rounds);
+  msd::gdef(m, "place_rounds_mask", &msd::place_rounds_mask, "cooperative placement over cells selected by a mask");
+  msd::gdef(m, "set_place_tail", &msd::set_place_tail, "1: single-launch placement with one grid barrier + a one-workgroup tail of the later rounds");
+  msd::gdef(m, "set_overflow_blocks", &msd::set_overflow_blocks, "workgroups of the integrator's strided overflow-list launch");
+  msd::gdef(m, "set_coop_blocks", &msd::set_coop_blocks, "workgroups of the cooperative placement (A/B)");
+  msd::gdef(m, "set_stencil_vec", &msd::set_stencil_vec, "diffusion stencil columns per lane: 8 (default), 4 or 1");
+  msd::gdef(m, "set_stencil_prefetch", &msd::set_stencil_prefetch, "rows the vector stencils load ahead (-1 auto, 0-3)");
+  msd::gdef(m, "set_stencil_band", &msd::set_stencil_band, "rows per wave band of the vector stencils (16-256; 0 = the default 64)");
+  msd::gdef(m, "set_stencil_blocks", &msd::set_stencil_blocks, "blocks of the vector diffusion stencil (0: one per tile)");
+  msd::gdef(m, "set_place_mode", &msd::set_place_mode, "0 single-launch placement, ordinary launch (default), 1 multi-launch rounds, 2 single launch as a cooperative launch");
+  msd::gdef(m, "place_error_take", &msd::place_error_take,
         "1 if a cooperative placement's grid barrier timed out since the last call (clears the flag)");
-  m.def("split_cells", &msd::split_cells);
-  m.def("permeate", &msd::permeate);
-  m.def("claim_free", &msd::claim_free);
-  m.def("index_map", &msd::index_map);
-  m.def("index_map_lmax", &msd::index_map_lmax, "index map + the longest genome into a (gen << 32 | length) word");
-  m.def("sel_sort_cap", &msd::sel_sort_cap, "capacity of the append + sort selections of the genome pipeline");
-  m.def("neighbor_pairs_sorted", &msd::neighbor_pairs_sorted, "unique neighbour pairs in (a, b)-sorted slots");
-  m.def("translate_count", &msd::translate_count);
-  m.def("translate_write", &msd::translate_write);
-  m.def("translate_fused", &msd::translate_fused);
-  m.def("set_spl2_waves", &msd::set_spl2_waves, "waves per SIMD of the wide chemistries' narrow launch (2-4)");
-  m.def("set_select_single_pass", &msd::set_select_single_pass, py::arg("on"), py::arg("items") = 0,
+  msd::gdef(m, "split_cells", &msd::split_cells);
+  msd::gdef(m, "permeate", &msd::permeate);
+  msd::gdef(m, "claim_free", &msd::claim_free);
+  msd::gdef(m, "index_map", &msd::index_map);
+  msd::gdef(m, "index_map_lmax", &msd::index_map_lmax, "index map + the longest genome into a (gen << 32 | length) word");
+  msd::gdef(m, "sel_sort_cap", &msd::sel_sort_cap, "capacity of the append + sort selections of the genome pipeline");
+  msd::gdef(m, "neighbor_pairs_sorted", &msd::neighbor_pairs_sorted, "unique neighbour pairs in (a, b)-sorted slots");
+  msd::gdef(m, "translate_count", &msd::translate_count);
+  msd::gdef(m, "translate_write", &msd::translate_write);
+  msd::gdef(m, "translate_fused", &msd::translate_fused);
+  msd::gdef(m, "set_spl2_waves", &msd::set_spl2_waves, "waves per SIMD of the wide chemistries' narrow launch (2-4)");
+  msd::gdef(m, "set_select_single_pass", &msd::set_select_single_pass, py::arg("on"), py::arg("items") = 0,
         "1: selections of <= 4M items in one launch (tile counts tagged + summed); 0: count + write passes; items: per thread of its tiles (1, 4, 16; 0 keeps)");
-  m.def("set_rec_thinning", &msd::set_rec_thinning, "1: recombination (thinned) and mutation draws appended + sorted (0: count + selection passes)");
-  m.def("set_rescue_mode", &msd::set_rescue_mode, "1: one launch behind the speculative integrator (0: separate)");
-  m.def("lb_error_take", &msd::lb_error_take, "1 if a single-pass selection's look-back spin timed out");
-  m.def("rescue_error_take", &msd::rescue_error_take, "1 if the integrator rescue launch's grid barrier timed out");
-  m.def("set_integrate_mode", &msd::set_integrate_mode, "binned integrator launches: 0 serial, 1 concurrent, 2 concurrent + strided wide bin");
-  m.def("translate_slot_bytes", &msd::translate_slot_bytes);
-  m.def("mut_count", &msd::mut_count);
-  m.def("mut_apply", &msd::mut_apply);
-  m.def("rec_count", &msd::rec_count);
-  m.def("rec_apply", &msd::rec_apply);
-  m.def("arena_scatter", &msd::arena_scatter);
-  m.def("place_collect", &msd::place_collect);
-  m.def("divide_commit_list", &msd::divide_commit_list, "division commit with a host count (+ exporting parents)");
-  m.def("cell_state_io", &msd::cell_state_io, "save / restore cell molecules + raw pixel values under the cells");
-  m.def("spawn_dev", &msd::spawn_dev, "spawn_cells without a sync: claim pixels, init rows, pick up molecules, labels, genomes");
-  m.def("divide_mask_dev", &msd::divide_mask_dev,
+  msd::gdef(m, "set_rec_thinning", &msd::set_rec_thinning, "1: recombination (thinned) and mutation draws appended + sorted (0: count + selection passes)");
+  msd::gdef(m, "set_rescue_mode", &msd::set_rescue_mode, "1: one launch behind the speculative integrator (0: separate)");
+  msd::gdef(m, "lb_error_take", &msd::lb_error_take, "1 if a single-pass selection's look-back spin timed out");
+  msd::gdef(m, "rescue_error_take", &msd::rescue_error_take, "1 if the integrator rescue launch's grid barrier timed out");
+  msd::gdef(m, "set_integrate_mode", &msd::set_integrate_mode, "binned integrator launches: 0 serial, 1 concurrent, 2 concurrent + strided wide bin");
+  msd::gdef(m, "translate_slot_bytes", &msd::translate_slot_bytes);
+  msd::gdef(m, "mut_count", &msd::mut_count);
+  msd::gdef(m, "mut_apply", &msd::mut_apply);
+  msd::gdef(m, "rec_count", &msd::rec_count);
+  msd::gdef(m, "rec_apply", &msd::rec_apply);
+  msd::gdef(m, "arena_scatter", &msd::arena_scatter);
+  msd::gdef(m, "place_collect", &msd::place_collect);
+  msd::gdef(m, "divide_commit_list", &msd::divide_commit_list, "division commit with a host count (+ exporting parents)");
+  msd::gdef(m, "cell_state_io", &msd::cell_state_io, "save / restore cell molecules + raw pixel values under the cells");
+  msd::gdef(m, "spawn_dev", &msd::spawn_dev, "spawn_cells without a sync: claim pixels, init rows, pick up molecules, labels, genomes");
+  msd::gdef(m, "divide_mask_dev", &msd::divide_mask_dev,
         "divide_cells over a mask: placement, winner compaction and commit issued without a sync; returns the status slot");
-  m.def("translate_stats", &msd::translate_stats,
+  msd::gdef(m, "translate_stats", &msd::translate_stats,
         "(max proteins, max domains, long genomes) of a translate count pass; synchronises the stream");
-  m.def("select_indices_dev", &msd::select_indices_dev);
-  m.def("gather_dev", &msd::gather_dev);
-  m.def("cap_skip", &msd::cap_skip, "pipeline capacity guard: count > cap -> no-op call replayed by the host");
-  m.def("select_indices_async", &msd::select_indices_async,
+  msd::gdef(m, "select_indices_dev", &msd::select_indices_dev);
+  msd::gdef(m, "gather_dev", &msd::gather_dev);
+  msd::gdef(m, "cap_skip", &msd::cap_skip, "pipeline capacity guard: count > cap -> no-op call replayed by the host");
+  msd::gdef(m, "select_indices_async", &msd::select_indices_async,
         "compaction with the count on the device and in a pinned status slot (returned); no sync");
-  m.def("select_indices_async_pay", &msd::select_indices_async_pay,
+  msd::gdef(m, "select_indices_async_pay", &msd::select_indices_async_pay,
         "select_indices_async plus pay_dst[k] = pay_src[sel[k]] (zeros past the count)");
-  m.def("count_to_host", &msd::count_to_host, "device {count, max} -> pinned ring slot (returns the slot)");
-  m.def("status_write", &msd::status_write, "pipeline status -> pinned ring slot (returns the slot)");
-  m.def("status_read", &msd::status_read);
-  m.def("mapped_flag", &msd::mapped_flag, "a zeroed int in mapped pinned memory: (host pointer, device pointer)");
-  m.def("mapped_flag_read", &msd::mapped_flag_read);
-  m.def("stream_sync_read", &msd::stream_sync_read, "synchronise a stream, then read a pinned status slot");
-  m.def("rccl_load", &msd::rccl_load, "resolve RCCL from a loaded librccl.so path; returns its version");
-  m.def("rccl_unique_id", [](){ return py::bytes(msd::rccl_unique_id()); });
-  m.def("rccl_init", [](py::bytes uid, int nranks, int rank) { return msd::rccl_init(std::string(uid), nranks, rank); });
-  m.def("rccl_destroy", &msd::rccl_destroy);
-  m.def("rccl_async_error", &msd::rccl_async_error);
-  m.def("rccl_guarded_wait", &msd::rccl_guarded_wait, py::call_guard<py::gil_scoped_release>(), py::arg("comms"),
+  msd::gdef(m, "count_to_host", &msd::count_to_host, "device {count, max} -> pinned ring slot (returns the slot)");
+  msd::gdef(m, "status_write", &msd::status_write, "pipeline status -> pinned ring slot (returns the slot)");
+  msd::gdef(m, "status_read", &msd::status_read);
+  msd::gdef(m, "mapped_flag", &msd::mapped_flag, "a zeroed int in mapped pinned memory: (host pointer, device pointer)");
+  msd::gdef(m, "mapped_flag_read", &msd::mapped_flag_read);
+  msd::gdef(m, "stream_sync_read", &msd::stream_sync_read, "synchronise a stream, then read a pinned status slot");
+  msd::gdef(m, "rccl_load", &msd::rccl_load, "resolve RCCL from a loaded librccl.so path; returns its version");
+  msd::gdef(m, "rccl_unique_id", [](){ return py::bytes(msd::rccl_unique_id()); });
+  msd::gdef(m, "rccl_init", [](py::bytes uid, int nranks, int rank) { return msd::rccl_init(std::string(uid), nranks, rank); });
+  msd::gdef(m, "rccl_destroy", &msd::rccl_destroy);
+  msd::gdef(m, "rccl_async_error", &msd::rccl_async_error);
+  msd::gdef(m, "rccl_guarded_wait", &msd::rccl_guarded_wait, py::call_guard<py::gil_scoped_release>(), py::arg("comms"),
         py::arg("stream"), py::arg("timeout_s"), py::arg("event") = 0,
         "wait for a stream (or one event on it) while polling RCCL errors; aborts the communicators on error / "
         "timeout");
-  m.def("rccl_allreduce", &msd::rccl_allreduce, "in-place all-reduce on a stream (dtype 0 i32 1 f32 2 f64 3 i64; op 0 sum 1 max 2 min)");
-  m.def("rccl_exchange", &msd::rccl_exchange, "grouped byte send/recv with the up / down neighbours on a stream");
-  m.def("strip_marks", &msd::strip_marks, "boundary-row bytes (1 occupied, 3 dividing) for the strip neighbours");
-  m.def("strip_reserve", &msd::strip_reserve, "halo occupancy + reservations from the neighbours' marks");
-  m.def("strip_clear", &msd::strip_clear);
-  m.def("place_split", &msd::place_split, "placement winners split into local / up / down (device counts + headers)");
-  m.def("set_split_single", &msd::set_split_single, "1: place_split as one single-pass launch (0: count + write)");
-  m.def("rec_record_bytes", &msd::rec_record_bytes);
-  m.def("rec_pack", &msd::rec_pack);
-  m.def("rec_unpack", &msd::rec_unpack);
-  m.def("halo_pack", &msd::halo_pack);
-  m.def("halo_unpack", &msd::halo_unpack);
-  m.def("xb_prep", &msd::xb_prep);
-  m.def("xb_events", &msd::xb_events, "strip-boundary recombination events (one workgroup, both boundaries)");
-  m.def("xb_begin", &msd::xb_begin);
-  m.def("xb_apply", &msd::xb_apply);
+  msd::gdef(m, "rccl_allreduce", &msd::rccl_allreduce, "in-place all-reduce on a stream (dtype 0 i32 1 f32 2 f64 3 i64; op 0 sum 1 max 2 min)");
+  msd::gdef(m, "rccl_exchange", &msd::rccl_exchange, "grouped byte send/recv with the up / down neighbours on a stream");
+  msd::gdef(m, "strip_marks", &msd::strip_marks, "boundary-row bytes (1 occupied, 3 dividing) for the strip neighbours");
+  msd::gdef(m, "strip_reserve", &msd::strip_reserve, "halo occupancy + reservations from the neighbours' marks");
+  msd::gdef(m, "strip_clear", &msd::strip_clear);
+  msd::gdef(m, "place_split", &msd::place_split, "placement winners split into local / up / down (device counts + headers)");
+  msd::gdef(m, "set_split_single", &msd::set_split_single, "1: place_split as one single-pass launch (0: count + write)");
+  msd::gdef(m, "rec_record_bytes", &msd::rec_record_bytes);
+  msd::gdef(m, "rec_pack", &msd::rec_pack);
+  msd::gdef(m, "rec_unpack", &msd::rec_unpack);
+  msd::gdef(m, "halo_pack", &msd::halo_pack);
+  msd::gdef(m, "halo_unpack", &msd::halo_unpack);
+  msd::gdef(m, "xb_prep", &msd::xb_prep);
+  msd::gdef(m, "xb_events", &msd::xb_events, "strip-boundary recombination events (one workgroup, both boundaries)");
+  msd::gdef(m, "xb_begin", &msd::xb_begin);
+  msd::gdef(m, "xb_apply", &msd::xb_apply);
   msd::bind_fast(m);
   msd::bind_gp(m);
   msd::bind_pool(m);
-  m.def("select_indices", &msd::select_indices,
+  msd::gdef(m, "select_indices", &msd::select_indices,
         "(count, max) of an order-preserving compaction; synchronises the stream");
 }

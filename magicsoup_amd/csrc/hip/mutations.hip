@@ -366,7 +366,7 @@ static unsigned item_grid(long long n, uintptr_t dn) {
 void mut_count(int n, uintptr_t rows, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k, int kcap,
                uintptr_t gflags, uintptr_t opflags, uintptr_t stream) {
   if (n <= 0) return;
-  mut_count_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, rows ? P_<int64_t>(rows) : nullptr, P_<int32_t>(lens), p,
+  msd::kl(mut_count_kernel, cdiv(n, 256), 256, 0, S_(stream))(n, rows ? P_<int64_t>(rows) : nullptr, P_<int32_t>(lens), p,
                                                          seed, call, P_<int32_t>(k), kcap,
                                                          gflags ? P_<int>(gflags) : nullptr, P_<int>(opflags));
   MS_LAUNCH_CHECK();
@@ -394,7 +394,7 @@ void mut_count_select(int n, uintptr_t lens, double p, uint64_t seed, uint64_t c
   hipStream_t s = S_(stream);
   if (g_mut_append && cand && cap <= sel_sort_cap()) {
     int* cnt = append_counter(s);
-    mut_draw_kernel<<<cdiv(n, 256), 256, 0, s>>>(n, P_<int32_t>(lens), p, seed, call, P_<int32_t>(k), kcap,
+    msd::kl(mut_draw_kernel, cdiv(n, 256), 256, 0, s)(n, P_<int32_t>(lens), p, seed, call, P_<int32_t>(k), kcap,
                                                  gflags ? P_<int>(gflags) : nullptr, P_<int>(opflags),
                                                  P_<int64_t>(cand), cnt, cap, na ? P_<int>(na) : nullptr,
                                                  nb ? P_<int>(nb) : nullptr);
@@ -406,7 +406,7 @@ void mut_count_select(int n, uintptr_t lens, double p, uint64_t seed, uint64_t c
   constexpr int kSelTile = 4096, kBlock = 256;  // select.hip tile; 16 count blocks per tile
   const long long blocks = ((long long)n + kSelTile - 1) / kSelTile * (kSelTile / kBlock);
   auto tiles = select_tiles(blocks, s);
-  mut_count_tiles_kernel<<<(unsigned)blocks, kBlock, 0, s>>>(n, P_<int32_t>(lens), p, seed, call, P_<int32_t>(k), kcap,
+  msd::kl(mut_count_tiles_kernel, (unsigned)blocks, kBlock, 0, s)(n, P_<int32_t>(lens), p, seed, call, P_<int32_t>(k), kcap,
                                                             gflags ? P_<int>(gflags) : nullptr, P_<int>(opflags),
                                                             tiles.first, tiles.second);
   MS_LAUNCH_CHECK();
@@ -417,7 +417,7 @@ void mut_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t rows, uintptr_t 
                uintptr_t k, double p_indel, double p_del, uint64_t seed, uint64_t call, uintptr_t out, int out_width,
                uintptr_t out_len, uintptr_t stream) {
   if (nsel <= 0) return;
-  mut_apply_kernel<<<item_grid(nsel, dn), 64, 0, S_(stream)>>>(
+  msd::kl(mut_apply_kernel, item_grid(nsel, dn), 64, 0, S_(stream))(
       nsel, dn ? P_<int>(dn) : nullptr, P_<int64_t>(sel), rows ? P_<int64_t>(rows) : nullptr, P_<uint8_t>(arena),
       P_<int64_t>(off), P_<int32_t>(lens), P_<int32_t>(k), p_indel, p_del, seed, call, P_<uint8_t>(out), out_width,
       P_<int32_t>(out_len));
@@ -427,7 +427,7 @@ void mut_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t rows, uintptr_t 
 void rec_count(int n, uintptr_t pairs, uintptr_t lens, double p, uint64_t seed, uint64_t call, uintptr_t k,
                uintptr_t stream) {
   if (n <= 0) return;
-  rec_count_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, P_<int32_t>(pairs), P_<int32_t>(lens), p, seed, call,
+  msd::kl(rec_count_kernel, cdiv(n, 256), 256, 0, S_(stream))(n, P_<int32_t>(pairs), P_<int32_t>(lens), p, seed, call,
                                                          P_<int32_t>(k));
   MS_LAUNCH_CHECK();
 }
@@ -436,7 +436,7 @@ void rec_count_keys(int n, uintptr_t keys, uintptr_t lens, double p, uint64_t se
                     uintptr_t tot, int kcap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream,
                     uintptr_t lw_word) {
   if (n <= 0) return;
-  rec_count_keys_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, P_<int64_t>(keys), P_<int32_t>(lens), p, seed, call,
+  msd::kl(rec_count_keys_kernel, cdiv(n, 256), 256, 0, S_(stream))(n, P_<int64_t>(keys), P_<int32_t>(lens), p, seed, call,
                                                               P_<int32_t>(k), tot ? P_<int32_t>(tot) : nullptr, kcap,
                                                               gflags ? P_<int>(gflags) : nullptr, P_<int>(opflags),
                                                               lw_word ? P_<unsigned long long>(lw_word) : nullptr);
@@ -448,7 +448,7 @@ void rec_apply(int nsel, uintptr_t dn, uintptr_t sel, uintptr_t pairs, uintptr_t
                int out_width, uintptr_t out_len, uintptr_t out_rows, uintptr_t stream) {
   if (nsel <= 0) return;
   if ((pairs == 0) == (keys == 0)) throw std::invalid_argument("rec_apply: give exactly one of pairs / keys");
-  rec_apply_kernel<<<item_grid(nsel, dn), 64, 0, S_(stream)>>>(
+  msd::kl(rec_apply_kernel, item_grid(nsel, dn), 64, 0, S_(stream))(
       nsel, dn ? P_<int>(dn) : nullptr, P_<int64_t>(sel), pairs ? P_<int32_t>(pairs) : nullptr,
       keys ? P_<int64_t>(keys) : nullptr, P_<uint8_t>(arena), P_<int64_t>(off), P_<int32_t>(lens), P_<int32_t>(k), seed,
       call,
@@ -468,10 +468,10 @@ static void arena_scatter_impl(int k, uintptr_t dn, int dn_mul, uintptr_t rows, 
   const int* d = dn ? P_<int>(dn) : nullptr;
   if (mark) {
     const unsigned g = dn ? std::min<unsigned>(cdiv(k, 256), 256u) : cdiv(k, 256);
-    arena_mark_kernel<<<g, 256, 0, S_(stream)>>>(k, d, dn_mul, P_<int64_t>(rows), P_<unsigned long long>(mark), gen);
+    msd::kl(arena_mark_kernel, g, 256, 0, S_(stream))(k, d, dn_mul, P_<int64_t>(rows), P_<unsigned long long>(mark), gen);
     MS_LAUNCH_CHECK();
   }
-  arena_scatter_kernel<<<item_grid(k, dn), 64, 0, S_(stream)>>>(
+  msd::kl(arena_scatter_kernel, item_grid(k, dn), 64, 0, S_(stream))(
       k, d, dn_mul, P_<int64_t>(rows), P_<uint8_t>(src), src_width, P_<int32_t>(src_len), P_<uint8_t>(pool),
       P_<int64_t>(off), P_<unsigned long long>(top), pool_cap, width, P_<int32_t>(lens), mark ? P_<unsigned long long>(mark) : nullptr, gen, flags ? P_<uint8_t>(flags) : nullptr,
       gflags ? P_<int>(gflags) : nullptr, opflags ? P_<int>(opflags) : nullptr, app_cand, app_cnt);

@@ -14,6 +14,7 @@
 #include <stdexcept>
 
 #include "hip_common.h"
+#include "bind_util.h"
 
 namespace msd {
 
@@ -247,7 +248,7 @@ void pool_write(int k, int L_in, uintptr_t rows, uintptr_t lens, uintptr_t dst, 
   if (k <= 0) return;
   if (L_in < 0) throw std::invalid_argument("pool_write: negative row width");
   const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(((long long)k + kPwChunk - 1) / kPwChunk, 4096));
-  pool_write_kernel<<<grid, 256, 0, S_(stream)>>>(k, L_in, P_<uint8_t>(rows), P_<int32_t>(lens),
+  msd::kl(pool_write_kernel, grid, 256, 0, S_(stream))(k, L_in, P_<uint8_t>(rows), P_<int32_t>(lens),
                                                         dst ? P_<int64_t>(dst) : nullptr, n0, P_<uint8_t>(pool),
                                                         P_<int64_t>(off), P_<unsigned long long>(top), cap,
                                                         P_<int32_t>(out_lens), failed ? P_<int>(failed) : nullptr);
@@ -257,7 +258,7 @@ void pool_write(int k, int L_in, uintptr_t rows, uintptr_t lens, uintptr_t dst, 
 void pool_read(int k, uintptr_t src, uintptr_t pool, uintptr_t off, uintptr_t lens, uintptr_t out, int W,
                uintptr_t stream) {
   if (k <= 0 || W <= 0) return;
-  pool_read_kernel<<<grid_for(k), 64, 0, S_(stream)>>>(k, src ? P_<int64_t>(src) : nullptr, P_<uint8_t>(pool),
+  msd::kl(pool_read_kernel, grid_for(k), 64, 0, S_(stream))(k, src ? P_<int64_t>(src) : nullptr, P_<uint8_t>(pool),
                                                        P_<int64_t>(off), P_<int32_t>(lens), P_<uint8_t>(out), W);
   MS_LAUNCH_CHECK();
 }
@@ -265,7 +266,7 @@ void pool_read(int k, uintptr_t src, uintptr_t pool, uintptr_t off, uintptr_t le
 void pool_read_packed(int k, uintptr_t src, uintptr_t pool, uintptr_t off, uintptr_t lens, uintptr_t dst_off,
                       uintptr_t out, uintptr_t stream) {
   if (k <= 0) return;
-  pool_read_packed_kernel<<<grid_for(k), 64, 0, S_(stream)>>>(k, src ? P_<int64_t>(src) : nullptr, P_<uint8_t>(pool),
+  msd::kl(pool_read_packed_kernel, grid_for(k), 64, 0, S_(stream))(k, src ? P_<int64_t>(src) : nullptr, P_<uint8_t>(pool),
                                                               P_<int64_t>(off), P_<int32_t>(lens), P_<int64_t>(dst_off),
                                                               P_<uint8_t>(out));
   MS_LAUNCH_CHECK();
@@ -275,7 +276,7 @@ void pool_compact(int nu, uintptr_t old_pool, uintptr_t old_off, uintptr_t sizes
                   uintptr_t new_off, uintptr_t stream) {
   if (nu <= 0) return;
   if ((old_pool | new_pool) & 15) throw std::invalid_argument("pool_compact: pools must be 16-byte aligned");
-  pool_compact_kernel<<<grid_for(nu), 64, 0, S_(stream)>>>(nu, P_<uint8_t>(old_pool), P_<int64_t>(old_off),
+  msd::kl(pool_compact_kernel, grid_for(nu), 64, 0, S_(stream))(nu, P_<uint8_t>(old_pool), P_<int64_t>(old_off),
                                                            P_<int64_t>(sizes), P_<uint8_t>(new_pool),
                                                            P_<int64_t>(new_off));
   MS_LAUNCH_CHECK();
@@ -289,18 +290,18 @@ void pool_collect_plan(int n, uintptr_t off, uintptr_t lens, long long G, uintpt
   if (n <= 0 || G <= 0) throw std::invalid_argument("pool_collect_plan: empty pool");
   if (G >= (1ll << 31)) throw std::invalid_argument("pool_collect_plan: pool too large for int32 granule offsets");
   hipStream_t s = S_(stream);
-  MS_HIP_CHECK(hipMemsetAsync(P_<int32_t>(size_g), 0, (size_t)G * 4, s));
-  MS_HIP_CHECK(hipMemsetAsync(P_<int32_t>(owner_g), 0x7F, (size_t)G * 4, s));
-  pool_mark_kernel<<<cdiv(n, 256), 256, 0, s>>>(n, P_<int64_t>(off), P_<int32_t>(lens), P_<int32_t>(size_g),
+  MS_HIP_CHECK(msd::memset_async(P_<int32_t>(size_g), 0, (size_t)G * 4, s));
+  MS_HIP_CHECK(msd::memset_async(P_<int32_t>(owner_g), 0x7F, (size_t)G * 4, s));
+  msd::kl(pool_mark_kernel, cdiv(n, 256), 256, 0, s)(n, P_<int64_t>(off), P_<int32_t>(lens), P_<int32_t>(size_g),
                                                 P_<int32_t>(owner_g));
   MS_LAUNCH_CHECK();
   const long long tiles = (G + kScanTile - 1) / kScanTile;
-  pool_scan_tiles_kernel<<<(unsigned)tiles, kScanThreads, 0, s>>>(G, P_<int32_t>(size_g), P_<int32_t>(new_g),
+  msd::kl(pool_scan_tiles_kernel, (unsigned)tiles, kScanThreads, 0, s)(G, P_<int32_t>(size_g), P_<int32_t>(new_g),
                                                                   P_<long long>(tile_sum));
   MS_LAUNCH_CHECK();
-  pool_scan_sums_kernel<<<1, kScanThreads, 0, s>>>(tiles, P_<long long>(tile_sum), P_<long long>(total_out));
+  msd::kl(pool_scan_sums_kernel, 1, kScanThreads, 0, s)(tiles, P_<long long>(tile_sum), P_<long long>(total_out));
   MS_LAUNCH_CHECK();
-  pool_scan_add_kernel<<<(unsigned)cdiv(G, kScanThreads), kScanThreads, 0, s>>>(G, P_<int32_t>(new_g),
+  msd::kl(pool_scan_add_kernel, (unsigned)cdiv(G, kScanThreads), kScanThreads, 0, s)(G, P_<int32_t>(new_g),
                                                                                 P_<long long>(tile_sum));
   MS_LAUNCH_CHECK();
 }
@@ -310,7 +311,7 @@ void pool_collect_move(int n, uintptr_t off, uintptr_t old_pool, uintptr_t new_p
                        uintptr_t owner_g, uintptr_t new_g, uintptr_t stream) {
   if (n <= 0) return;
   if ((old_pool | new_pool) & 15) throw std::invalid_argument("pool_collect_move: pools must be 16-byte aligned");
-  pool_move_kernel<<<grid_for(n), 64, 0, S_(stream)>>>(n, P_<int64_t>(off), P_<uint8_t>(old_pool),
+  msd::kl(pool_move_kernel, grid_for(n), 64, 0, S_(stream))(n, P_<int64_t>(off), P_<uint8_t>(old_pool),
                                                        P_<uint8_t>(new_pool), P_<int32_t>(size_g),
                                                        P_<int32_t>(owner_g), P_<int32_t>(new_g));
   MS_LAUNCH_CHECK();
@@ -325,12 +326,12 @@ void bind_pool(pybind11::module_& m) {
       .def_readwrite("top", &GenomePoolArgs::top)
       .def_readwrite("failed", &GenomePoolArgs::failed)
       .def_readwrite("cap", &GenomePoolArgs::cap);
-  m.def("pool_write", &pool_write, "genome rows (k, L) -> new pool allocations of cells dst[j] (or n0 + j)");
-  m.def("pool_read", &pool_read, "genomes of cells -> zero-padded rows (k, W)");
-  m.def("pool_read_packed", &pool_read_packed, "genomes of cells back to back (no padding)");
-  m.def("pool_compact", &pool_compact, "copy unique genomes into a new pool");
-  m.def("pool_collect_plan", &pool_collect_plan, "collection phase 1: per-granule sizes / owners and their scan");
-  m.def("pool_collect_move", &pool_collect_move, "collection phase 2: copy the allocations, remap the offsets");
+  msd::gdef(m, "pool_write", &pool_write, "genome rows (k, L) -> new pool allocations of cells dst[j] (or n0 + j)");
+  msd::gdef(m, "pool_read", &pool_read, "genomes of cells -> zero-padded rows (k, W)");
+  msd::gdef(m, "pool_read_packed", &pool_read_packed, "genomes of cells back to back (no padding)");
+  msd::gdef(m, "pool_compact", &pool_compact, "copy unique genomes into a new pool");
+  msd::gdef(m, "pool_collect_plan", &pool_collect_plan, "collection phase 1: per-granule sizes / owners and their scan");
+  msd::gdef(m, "pool_collect_move", &pool_collect_move, "collection phase 2: copy the allocations, remap the offsets");
 }
 
 }  // namespace msd

@@ -83,7 +83,7 @@ void launch_row_args(const RowArgs& plan, int n, const int* dn, const int64_t* s
   // enough blocks for the widest descriptor, capped (grid-stride beyond); ~2k blocks fill the chip
   const long long blocks = (widest + 255) / 256;
   const unsigned gx = (unsigned)(blocks < 2048 ? blocks : 2048);
-  gather_rows_kernel<<<dim3(gx, a.nd), 256, 0, s>>>(a);
+  msd::kl(gather_rows_kernel, dim3(gx, a.nd), 256, 0, s)(a);
   MS_LAUNCH_CHECK();
 }
 

@@ -73,9 +73,8 @@ template <int K>
 __global__ void __launch_bounds__(kSelThreads) select_write_kernel(long long n, const void* src, const int32_t* tile_count,
                                                                    const int32_t* tile_max, int64_t* sel,
                                                                    int64_t* rest, int32_t* host_out,
-                                                                   long long* host64 = nullptr, int cap = -1,
-                                                                   int* cap_gflags = nullptr,
-                                                                   int* cap_opflags = nullptr, int sub = 1) {
+                                                                   long long* host64, int cap, int* cap_gflags,
+                                                                   int* cap_opflags, int sub) {
   constexpr int W = kSelThreads / 64;
   __shared__ long long s_red[W];
   __shared__ int s_wc[kSelItems][W];
@@ -219,11 +218,11 @@ std::pair<int32_t*, int32_t*> tiles_for(hipStream_t s, long long tiles) {
   TileBuf& b = g_tiles[s];
   if (tiles > b.cap) {
     if (b.p) {
-      MS_HIP_CHECK(hipStreamSynchronize(s));  // the old buffer may still be read by this stream
-      MS_HIP_CHECK(hipFree(b.p));
+      MS_HIP_CHECK(msd::stream_synchronize(s));  // the old buffer may still be read by this stream
+      MS_HIP_CHECK(msd::dev_free(b.p));
     }
     b.cap = std::max(tiles, 256ll);
-    MS_HIP_CHECK(hipMalloc((void**)&b.p, 2 * b.cap * sizeof(int32_t)));
+    MS_HIP_CHECK(msd::dev_malloc((void**)&b.p, 2 * b.cap * sizeof(int32_t)));
   }
   return {b.p, b.p + b.cap};
 }
@@ -252,15 +251,15 @@ std::tuple<int, int, int> translate_stats(int n, uintptr_t counts, uintptr_t ndo
   if (n <= 0) return {0, 0, 0};
   ensure_host();
   if (!g_tacc) {
-    MS_HIP_CHECK(hipMalloc((void**)&g_tacc, 4 * sizeof(int32_t)));
-    MS_HIP_CHECK(hipMemset(g_tacc, 0, 4 * sizeof(int32_t)));
+    MS_HIP_CHECK(msd::dev_malloc((void**)&g_tacc, 4 * sizeof(int32_t)));
+    MS_HIP_CHECK(msd::dev_memset(g_tacc, 0, 4 * sizeof(int32_t)));
   }
   g_host[0] = -1;
   const unsigned grid = std::min(cdiv(n, 256), 1024u);
-  translate_stats_kernel<<<grid, 256, 0, S_(stream)>>>(n, P_<int32_t>(counts), P_<int32_t>(ndom),
+  msd::kl(translate_stats_kernel, grid, 256, 0, S_(stream))(n, P_<int32_t>(counts), P_<int32_t>(ndom),
                                                       P_<int32_t>(long_count), P_<int32_t>(per), g_tacc, g_host_dev);
   MS_LAUNCH_CHECK();
-  MS_HIP_CHECK(hipStreamSynchronize(S_(stream)));
+  MS_HIP_CHECK(msd::stream_synchronize(S_(stream)));
   if (g_host[0] < 0) throw std::runtime_error("translate_stats: bad read-back");
   return {g_host[0], g_host[1], g_host[2]};
 }
@@ -294,7 +293,7 @@ __global__ void cap_skip_kernel(int* dn, int cap, int* gflags, int* opflags) {
 }
 
 void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream) {
-  cap_skip_kernel<<<1, 1, 0, S_(stream)>>>(P_<int>(dn), cap, P_<int>(gflags), P_<int>(opflags));
+  msd::kl(cap_skip_kernel, 1, 1, 0, S_(stream))(P_<int>(dn), cap, P_<int>(gflags), P_<int>(opflags));
   MS_LAUNCH_CHECK();
 }
 
@@ -323,7 +322,7 @@ int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t 
   const int slot = g_status_next;
   g_status_next = (g_status_next + 1) % kStatusSlots;
   for (int i = 0; i < 4; ++i) g_status[slot * 4 + i] = -1;
-  status_write_kernel<<<1, 1, 0, S_(stream)>>>(P_<int>(dcnt), P_<int>(opflags), P_<long long>(d_rows), P_<int>(cnt),
+  msd::kl(status_write_kernel, 1, 1, 0, S_(stream))(P_<int>(dcnt), P_<int>(opflags), P_<long long>(d_rows), P_<int>(cnt),
                                                g_status_dev + slot * 4);
   MS_LAUNCH_CHECK();
   return slot;
@@ -347,7 +346,7 @@ int count_to_host(uintptr_t dcount, uintptr_t stream) {
   const int slot = g_status_next;
   g_status_next = (g_status_next + 1) % kStatusSlots;
   for (int i = 0; i < 4; ++i) g_status[slot * 4 + i] = -1;
-  count_to_host_kernel<<<1, 1, 0, S_(stream)>>>(P_<int>(dcount), g_status_dev + slot * 4);
+  msd::kl(count_to_host_kernel, 1, 1, 0, S_(stream))(P_<int>(dcount), g_status_dev + slot * 4);
   MS_LAUNCH_CHECK();
   return slot;
 }
@@ -374,7 +373,7 @@ std::tuple<long long, long long, long long, long long> status_read(int slot) {
 
 // One stream synchronisation, then the slot (what wait_count needs, without a Python stream object).
 std::tuple<long long, long long, long long, long long> stream_sync_read(int slot, uintptr_t stream) {
-  MS_HIP_CHECK(hipStreamSynchronize(S_(stream)));
+  MS_HIP_CHECK(msd::stream_synchronize(S_(stream)));
   return status_read(slot);
 }
 
@@ -384,8 +383,8 @@ std::tuple<long long, long long, long long, long long> stream_sync_read(int slot
 LbState lb_begin(hipStream_t s) {
   LbBuf& lb = g_lb[s];
   if (!lb.p) {
-    MS_HIP_CHECK(hipMalloc((void**)&lb.p, kLbMaxTiles * sizeof(unsigned long long)));
-    MS_HIP_CHECK(hipMemsetAsync(lb.p, 0, kLbMaxTiles * sizeof(unsigned long long), s));
+    MS_HIP_CHECK(msd::dev_malloc((void**)&lb.p, kLbMaxTiles * sizeof(unsigned long long)));
+    MS_HIP_CHECK(msd::memset_async(lb.p, 0, kLbMaxTiles * sizeof(unsigned long long), s));
   }
   if (!g_lb_err) {
     MS_HIP_CHECK(hipHostMalloc((void**)&g_lb_err, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
@@ -395,7 +394,7 @@ LbState lb_begin(hipStream_t s) {
   // the tags wrapped (at the narrowest tag width of the kernels that share the words): clear the
   // words, so no stale tag can match gen 1 then
   if (++lb.gen > kLbGenMask) {
-    MS_HIP_CHECK(hipMemsetAsync(lb.p, 0, kLbMaxTiles * sizeof(unsigned long long), s));
+    MS_HIP_CHECK(msd::memset_async(lb.p, 0, kLbMaxTiles * sizeof(unsigned long long), s));
     lb.gen = 1;
   }
   return {lb.p, lb.gen, g_lb_err_dev};
@@ -439,8 +438,8 @@ static int select_async_impl(long long n, int kind, uintptr_t src, uintptr_t sel
   long long* h64 = g_status_dev + slot * 4;
   hipStream_t s = S_(stream);
   if (n <= 0) {
-    MS_HIP_CHECK(hipMemsetAsync(P_<int32_t>(out_dev), 0, 2 * sizeof(int32_t), s));
-    count_to_host_kernel<<<1, 1, 0, s>>>(P_<int>(out_dev), h64);
+    MS_HIP_CHECK(msd::memset_async(P_<int32_t>(out_dev), 0, 2 * sizeof(int32_t), s));
+    msd::kl(count_to_host_kernel, 1, 1, 0, s)(P_<int>(out_dev), h64);
     MS_LAUNCH_CHECK();
     return slot;
   }
@@ -454,7 +453,7 @@ static int select_async_impl(long long n, int kind, uintptr_t src, uintptr_t sel
                                                                                                       : kSelItems;
     const unsigned grid = (unsigned)((n + (long long)kSelThreads * items - 1) / ((long long)kSelThreads * items));
 #define MS_SEL1(K, I)                                                                                               \
-  select_lb_kernel<K, I><<<grid, kSelThreads, 0, s>>>(n, sp, lb.status, lb.gen, lb.err, P_<int64_t>(sel),           \
+  msd::kl(select_lb_kernel<K, I>, grid, kSelThreads, 0, s)(n, sp, lb.status, lb.gen, lb.err, P_<int64_t>(sel),           \
                                                       rest ? P_<int64_t>(rest) : nullptr, P_<int32_t>(out_dev), h64, \
                                                       P_<uint8_t>(pay_src), P_<uint8_t>(pay_dst));                  \
   MS_LAUNCH_CHECK();
@@ -482,10 +481,10 @@ static int select_async_impl(long long n, int kind, uintptr_t src, uintptr_t sel
   int32_t* tm = tb.second;
   int32_t* out = P_<int32_t>(out_dev);
 #define MS_SEL(K)                                                                                                \
-  select_count_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, nullptr, tc, tm);                      \
+  msd::kl(select_count_kernel<K>, (unsigned)tiles, kSelThreads, 0, s)(n, sp, nullptr, tc, tm);                      \
   MS_LAUNCH_CHECK();                                                                                             \
-  select_write_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, tc, tm, P_<int64_t>(sel),              \
-                                                                 rest ? P_<int64_t>(rest) : nullptr, out, h64);  \
+  msd::kl(select_write_kernel<K>, (unsigned)tiles, kSelThreads, 0, s)(n, sp, tc, tm, P_<int64_t>(sel),              \
+                                                                 rest ? P_<int64_t>(rest) : nullptr, out, h64, -1, nullptr, nullptr, 1);  \
   MS_LAUNCH_CHECK();
   switch (kind) {
     case kMaskSet: MS_SEL(kMaskSet) break;
@@ -497,7 +496,7 @@ static int select_async_impl(long long n, int kind, uintptr_t src, uintptr_t sel
 #undef MS_SEL
   if (pay_dst) {
     const unsigned g = (unsigned)std::min<long long>((n + 255) / 256, 4096);
-    select_payload_kernel<<<g, 256, 0, s>>>(n, out, P_<int64_t>(sel), P_<uint8_t>(pay_src), P_<uint8_t>(pay_dst));
+    msd::kl(select_payload_kernel, g, 256, 0, s)(n, out, P_<int64_t>(sel), P_<uint8_t>(pay_src), P_<uint8_t>(pay_dst));
     MS_LAUNCH_CHECK();
   }
   return slot;
@@ -516,7 +515,7 @@ int select_indices_async_pay(long long n, int kind, uintptr_t src, uintptr_t sel
 
 void gather_dev(int cap, uintptr_t dn, uintptr_t idx, uintptr_t src, uintptr_t dst, uintptr_t stream) {
   const unsigned g = std::min(cdiv(cap, 256), 64u);
-  gather_dev_kernel<<<g, 256, 0, S_(stream)>>>(cap, P_<int>(dn), P_<int64_t>(idx), P_<int64_t>(src), P_<int64_t>(dst));
+  msd::kl(gather_dev_kernel, g, 256, 0, S_(stream))(cap, P_<int>(dn), P_<int64_t>(idx), P_<int64_t>(src), P_<int64_t>(dst));
   MS_LAUNCH_CHECK();
 }
 
@@ -536,10 +535,10 @@ std::pair<long long, int> select_indices(long long n, int kind, uintptr_t src, u
   int32_t* tc = tb.first;
   int32_t* tm = tb.second;
 #define MS_SEL(K)                                                                                               \
-  select_count_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, vp, tc, tm);                          \
+  msd::kl(select_count_kernel<K>, (unsigned)tiles, kSelThreads, 0, s)(n, sp, vp, tc, tm);                          \
   MS_LAUNCH_CHECK();                                                                                            \
-  select_write_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, tc, tm, P_<int64_t>(sel),             \
-                                                                 rest ? P_<int64_t>(rest) : nullptr, g_host_dev); \
+  msd::kl(select_write_kernel<K>, (unsigned)tiles, kSelThreads, 0, s)(n, sp, tc, tm, P_<int64_t>(sel),             \
+                                                                 rest ? P_<int64_t>(rest) : nullptr, g_host_dev, nullptr, -1, nullptr, nullptr, 1); \
   MS_LAUNCH_CHECK();
   switch (kind) {
     case kMaskSet: MS_SEL(kMaskSet) break;
@@ -549,7 +548,7 @@ std::pair<long long, int> select_indices(long long n, int kind, uintptr_t src, u
     default: throw std::invalid_argument("select_indices: unknown predicate");
   }
 #undef MS_SEL
-  MS_HIP_CHECK(hipStreamSynchronize(s));
+  MS_HIP_CHECK(msd::stream_synchronize(s));
   const long long cnt = g_host[0];
   if (cnt < 0 || cnt > n) throw std::runtime_error("select_indices: bad count read-back");
   return {cnt, g_host[1]};
@@ -560,7 +559,7 @@ void select_indices_capped(long long n, int kind, uintptr_t src, uintptr_t sel, 
                            uintptr_t gflags, uintptr_t opflags, uintptr_t stream) {
   hipStream_t s = S_(stream);
   if (n <= 0) {
-    MS_HIP_CHECK(hipMemsetAsync(P_<int32_t>(out_dev), 0, 2 * sizeof(int32_t), s));
+    MS_HIP_CHECK(msd::memset_async(P_<int32_t>(out_dev), 0, 2 * sizeof(int32_t), s));
     return;
   }
   if (n >= (1ll << 40)) throw std::invalid_argument("select_indices_capped: n too large");
@@ -570,11 +569,11 @@ void select_indices_capped(long long n, int kind, uintptr_t src, uintptr_t sel, 
   int32_t* tc = tb.first;
   int32_t* tm = tb.second;
 #define MS_SEL(K)                                                                                                \
-  select_count_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, nullptr, tc, tm);                      \
+  msd::kl(select_count_kernel<K>, (unsigned)tiles, kSelThreads, 0, s)(n, sp, nullptr, tc, tm);                      \
   MS_LAUNCH_CHECK();                                                                                             \
-  select_write_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, tc, tm, P_<int64_t>(sel), nullptr,     \
+  msd::kl(select_write_kernel<K>, (unsigned)tiles, kSelThreads, 0, s)(n, sp, tc, tm, P_<int64_t>(sel), nullptr,     \
                                                                  P_<int32_t>(out_dev), nullptr, cap,             \
-                                                                 P_<int>(gflags), P_<int>(opflags));             \
+                                                                 P_<int>(gflags), P_<int>(opflags), 1);             \
   MS_LAUNCH_CHECK();
   switch (kind) {
     case kMaskSet: MS_SEL(kMaskSet) break;
@@ -593,7 +592,7 @@ void select_write_i32pos_capped(long long n, uintptr_t src, int32_t* tc, int32_t
                                 uintptr_t out_dev, int cap, uintptr_t gflags, uintptr_t opflags, hipStream_t s) {
   if (kSelTile % sub) throw std::invalid_argument("select_write_i32pos_capped: bad sub-tile count");
   const long long tiles = (n + kSelTile - 1) / kSelTile;
-  select_write_kernel<kI32Pos><<<(unsigned)tiles, kSelThreads, 0, s>>>(
+  msd::kl(select_write_kernel<kI32Pos>, (unsigned)tiles, kSelThreads, 0, s)(
       n, reinterpret_cast<const void*>(src), tc, tm, P_<int64_t>(sel), nullptr, P_<int32_t>(out_dev), nullptr, cap,
       P_<int>(gflags), P_<int>(opflags), sub);
   MS_LAUNCH_CHECK();
@@ -616,7 +615,7 @@ void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, ui
                         uintptr_t out_dev, uintptr_t stream) {
   hipStream_t s = S_(stream);
   if (n <= 0) {
-    MS_HIP_CHECK(hipMemsetAsync(P_<int32_t>(out_dev), 0, 2 * sizeof(int32_t), s));
+    MS_HIP_CHECK(msd::memset_async(P_<int32_t>(out_dev), 0, 2 * sizeof(int32_t), s));
     return;
   }
   if (n >= (1ll << 40)) throw std::invalid_argument("select_indices_dev: n too large");
@@ -628,10 +627,10 @@ void select_indices_dev(long long n, int kind, uintptr_t src, uintptr_t vals, ui
   int32_t* tm = tb.second;
   int32_t* out = P_<int32_t>(out_dev);
 #define MS_SEL(K)                                                                                                \
-  select_count_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, vp, tc, tm);                           \
+  msd::kl(select_count_kernel<K>, (unsigned)tiles, kSelThreads, 0, s)(n, sp, vp, tc, tm);                           \
   MS_LAUNCH_CHECK();                                                                                             \
-  select_write_kernel<K><<<(unsigned)tiles, kSelThreads, 0, s>>>(n, sp, tc, tm, P_<int64_t>(sel),              \
-                                                                 rest ? P_<int64_t>(rest) : nullptr, out);       \
+  msd::kl(select_write_kernel<K>, (unsigned)tiles, kSelThreads, 0, s)(n, sp, tc, tm, P_<int64_t>(sel),              \
+                                                                 rest ? P_<int64_t>(rest) : nullptr, out, nullptr, -1, nullptr, nullptr, 1);       \
   MS_LAUNCH_CHECK();
   switch (kind) {
     case kMaskSet: MS_SEL(kMaskSet) break;
@@ -670,12 +669,12 @@ void release_select_buffers() {
   g_flag_next = kFlagBlock;
   if (g_host) MS_HIP_CHECK(hipHostFree(g_host));
   g_host = g_host_dev = nullptr;
-  if (g_tacc) MS_HIP_CHECK(hipFree(g_tacc));
+  if (g_tacc) MS_HIP_CHECK(msd::dev_free(g_tacc));
   g_tacc = nullptr;
   if (g_status) MS_HIP_CHECK(hipHostFree(g_status));
   g_status = g_status_dev = nullptr;
   for (auto& kv : g_tiles)
-    if (kv.second.p) MS_HIP_CHECK(hipFree(kv.second.p));
+    if (kv.second.p) MS_HIP_CHECK(msd::dev_free(kv.second.p));
   g_tiles.clear();
 }
 

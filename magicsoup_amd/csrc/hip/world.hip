@@ -153,7 +153,7 @@ void divide_commit_list(int k, uintptr_t par, uintptr_t npos, long long n0, int 
                         uintptr_t pos, uintptr_t cell_mols, uintptr_t divisions, uintptr_t lifetimes, uintptr_t stream) {
   if (k + n_exp <= 0 || m <= 0) return;
   const unsigned grid = std::min<unsigned>(cdiv((long long)(k + n_exp) * m, 256), 512u);
-  divide_commit_list_kernel<<<grid, 256, 0, S_(stream)>>>(k, P_<int64_t>(par), P_<int32_t>(npos), n0, n_exp,
+  msd::kl(divide_commit_list_kernel, grid, 256, 0, S_(stream))(k, P_<int64_t>(par), P_<int32_t>(npos), n0, n_exp,
                                                           P_<int64_t>(exp), m, P_<int32_t>(pos), P_<float>(cell_mols),
                                                           P_<int32_t>(divisions), P_<int32_t>(lifetimes));
   MS_LAUNCH_CHECK();
@@ -849,7 +849,7 @@ static Geom geom(int R, int C, int r_lo, int r_hi, int wrap) {
 void split_cells(int k, int m, uintptr_t parents, uintptr_t children, uintptr_t cell_mols, uintptr_t divisions,
                  uintptr_t lifetimes, uintptr_t stream) {
   if (k <= 0 || m <= 0) return;
-  split_cells_kernel<<<cdiv((long long)k * m, 256), 256, 0, S_(stream)>>>(
+  msd::kl(split_cells_kernel, cdiv((long long)k * m, 256), 256, 0, S_(stream))(
       k, m, P_<int64_t>(parents), P_<int64_t>(children), P_<float>(cell_mols), P_<int32_t>(divisions),
       P_<int32_t>(lifetimes));
   MS_LAUNCH_CHECK();
@@ -859,7 +859,7 @@ void claim_free(int k, int R, int C, int r_lo, int r_hi, uintptr_t cell_map, uin
                 int attempts, uintptr_t out, uintptr_t stream) {
   if (k <= 0) return;
   const Geom g = geom(R, C, r_lo, r_hi, 1);
-  claim_free_kernel<<<cdiv(k, 256), 256, 0, S_(stream)>>>(k, g, P_<uint8_t>(cell_map), seed, call, attempts,
+  msd::kl(claim_free_kernel, cdiv(k, 256), 256, 0, S_(stream))(k, g, P_<uint8_t>(cell_map), seed, call, attempts,
                                                            P_<long long>(out));
   MS_LAUNCH_CHECK();
 }
@@ -908,8 +908,8 @@ static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, co
   MS_HIP_CHECK(hipGetDevice(&dev));
   if (dev < 0 || dev >= kMaxDevices) throw std::runtime_error("place_coop: device index out of range");
   if (!g_place_ctl[dev]) {
-    MS_HIP_CHECK(hipMalloc((void**)&g_place_ctl[dev], 2 * kCtlWords * sizeof(unsigned)));
-    MS_HIP_CHECK(hipMemset(g_place_ctl[dev], 0, 2 * kCtlWords * sizeof(unsigned)));
+    MS_HIP_CHECK(msd::dev_malloc((void**)&g_place_ctl[dev], 2 * kCtlWords * sizeof(unsigned)));
+    MS_HIP_CHECK(msd::dev_memset(g_place_ctl[dev], 0, 2 * kCtlWords * sizeof(unsigned)));
     g_place_par[dev] = 0;
   }
   if (!g_place_err) {
@@ -939,11 +939,11 @@ static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, co
     // stream is drained first, an earlier launch may still use the old buffer)
     if ((long long)k > g_place_list_cap[dev]) {
       if (g_place_list[dev]) {
-        MS_HIP_CHECK(hipStreamSynchronize(s));
-        MS_HIP_CHECK(hipFree(g_place_list[dev]));
+        MS_HIP_CHECK(msd::stream_synchronize(s));
+        MS_HIP_CHECK(msd::dev_free(g_place_list[dev]));
       }
       g_place_list_cap[dev] = std::max<long long>(k, 1ll << 16);
-      MS_HIP_CHECK(hipMalloc((void**)&g_place_list[dev], g_place_list_cap[dev] * 12));
+      MS_HIP_CHECK(msd::dev_malloc((void**)&g_place_list[dev], g_place_list_cap[dev] * 12));
     }
     long long* ls = reinterpret_cast<long long*>(g_place_list[dev]);
     int* list = reinterpret_cast<int*>(ls + g_place_list_cap[dev]);
@@ -955,14 +955,14 @@ static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, co
       resident_t[dev] = std::max(1, per_cu * cus);
     }
     grid = std::min<unsigned>(grid, (unsigned)resident_t[dev]);
-    place_tail_coop_kernel<<<grid, 256, 0, s>>>(kk, cp, mp, pp, gg, vac, cm, seed, call, cd, cl, res, rr, ctl, ctl_next,
+    msd::kl(place_tail_coop_kernel, grid, 256, 0, s)(kk, cp, mp, pp, gg, vac, cm, seed, call, cd, cl, res, rr, ctl, ctl_next,
                                                 err, list, ls);
     MS_LAUNCH_CHECK();
     g_place_par[dev] ^= 1;
     return true;
   }
   if (g_place_mode == 2) {
-    const hipError_t e = hipLaunchCooperativeKernel((const void*)place_rounds_coop_kernel, dim3(grid), dim3(256), args,
+    const hipError_t e = msd::flushed_coop_launch((const void*)place_rounds_coop_kernel, dim3(grid), dim3(256), args,
                                                     0, s);
     if (e != hipSuccess) {
       (void)hipGetLastError();  // clear the sticky launch error; fall back
@@ -980,7 +980,7 @@ static bool place_coop(int k, uintptr_t cells, uintptr_t mask, uintptr_t pos, co
     resident[dev] = std::max(1, per_cu * cus);
   }
   grid = std::min<unsigned>(grid, (unsigned)resident[dev]);
-  place_rounds_coop_kernel<<<grid, 256, 0, s>>>(kk, cp, mp, pp, gg, vac, cm, pend, seed, call, cd, cl, res, rr, ctl,
+  msd::kl(place_rounds_coop_kernel, grid, 256, 0, s)(kk, cp, mp, pp, gg, vac, cm, pend, seed, call, cd, cl, res, rr, ctl,
                                                  ctl_next, err);
   MS_LAUNCH_CHECK();
   g_place_par[dev] ^= 1;
@@ -1084,8 +1084,8 @@ void spawn_claims(int k, int C, int r_lo, int r_hi, uintptr_t cell_map, uintptr_
   MS_HIP_CHECK(hipGetDevice(&dev));
   if (dev < 0 || dev >= kMaxDevices) throw std::runtime_error("spawn_claims: device index out of range");
   if (!g_place_ctl[dev]) {
-    MS_HIP_CHECK(hipMalloc((void**)&g_place_ctl[dev], 2 * kCtlWords * sizeof(unsigned)));
-    MS_HIP_CHECK(hipMemset(g_place_ctl[dev], 0, 2 * kCtlWords * sizeof(unsigned)));
+    MS_HIP_CHECK(msd::dev_malloc((void**)&g_place_ctl[dev], 2 * kCtlWords * sizeof(unsigned)));
+    MS_HIP_CHECK(msd::dev_memset(g_place_ctl[dev], 0, 2 * kCtlWords * sizeof(unsigned)));
     g_place_par[dev] = 0;
   }
   if (!g_place_err) {
@@ -1105,7 +1105,7 @@ void spawn_claims(int k, int C, int r_lo, int r_hi, uintptr_t cell_map, uintptr_
                                            (unsigned)resident[dev]);
   unsigned* ctl = g_place_ctl[dev] + g_place_par[dev] * kCtlWords;
   unsigned* ctl_next = g_place_ctl[dev] + (1 - g_place_par[dev]) * kCtlWords;
-  spawn_claim_coop_kernel<<<grid, 256, 0, s>>>(k, (long long)r_lo * C, (long long)(r_hi - r_lo) * C,
+  msd::kl(spawn_claim_coop_kernel, grid, 256, 0, s)(k, (long long)r_lo * C, (long long)(r_hi - r_lo) * C,
                                                P_<uint8_t>(cell_map), seed, call, P_<long long>(cand), P_<int>(claim),
                                                P_<long long>(result), ctl, ctl_next, g_place_err_dev, P_<int>(failed));
   MS_LAUNCH_CHECK();
@@ -1131,15 +1131,15 @@ static void place_rounds_launches(int k, uintptr_t cells, uintptr_t mask, uintpt
                                   uintptr_t cell_map, uintptr_t pending, uintptr_t cand, uintptr_t claim,
                                   uintptr_t result, int rounds, uint64_t seed, uint64_t call, hipStream_t s) {
   if (mask) {
-    place_init_mask_kernel<<<cdiv(k, 256), 256, 0, s>>>(k, P_<uint8_t>(mask), P_<uint8_t>(pending), P_<long long>(result));
+    msd::kl(place_init_mask_kernel, cdiv(k, 256), 256, 0, s)(k, P_<uint8_t>(mask), P_<uint8_t>(pending), P_<long long>(result));
     MS_LAUNCH_CHECK();
   } else {
-    MS_HIP_CHECK(hipMemsetAsync(P_<uint8_t>(pending), 1, (size_t)k, s));
-    MS_HIP_CHECK(hipMemsetAsync(P_<long long>(result), 0xFF, (size_t)k * sizeof(long long), s));
+    MS_HIP_CHECK(msd::memset_async(P_<uint8_t>(pending), 1, (size_t)k, s));
+    MS_HIP_CHECK(msd::memset_async(P_<long long>(result), 0xFF, (size_t)k * sizeof(long long), s));
   }
   const int64_t* cp = cells ? P_<int64_t>(cells) : nullptr;
   if (k <= kPlaceWgMax && cells) {
-    place_rounds_wg_kernel<<<1, 1024, 0, s>>>(k, cp, P_<int32_t>(pos), g, vacate, P_<uint8_t>(cell_map),
+    msd::kl(place_rounds_wg_kernel, 1, 1024, 0, s)(k, cp, P_<int32_t>(pos), g, vacate, P_<uint8_t>(cell_map),
                                               P_<uint8_t>(pending), seed, call, P_<long long>(cand), P_<int>(claim),
                                               P_<long long>(result), rounds);
     MS_LAUNCH_CHECK();
@@ -1147,10 +1147,10 @@ static void place_rounds_launches(int k, uintptr_t cells, uintptr_t mask, uintpt
   }
   const unsigned grid = cdiv(k, 256);
   for (int r = 0; r < rounds; ++r) {
-    place_bid_kernel<<<grid, 256, 0, s>>>(k, cp, P_<int32_t>(pos), g, P_<uint8_t>(cell_map), P_<uint8_t>(pending),
+    msd::kl(place_bid_kernel, grid, 256, 0, s)(k, cp, P_<int32_t>(pos), g, P_<uint8_t>(cell_map), P_<uint8_t>(pending),
                                           seed, call + ((uint64_t)r << 48), P_<long long>(cand), P_<int>(claim));
     MS_LAUNCH_CHECK();
-    place_resolve_kernel<<<grid, 256, 0, s>>>(k, cp, P_<int32_t>(pos), g, vacate, P_<uint8_t>(cell_map),
+    msd::kl(place_resolve_kernel, grid, 256, 0, s)(k, cp, P_<int32_t>(pos), g, vacate, P_<uint8_t>(cell_map),
                                               P_<uint8_t>(pending), P_<long long>(cand), P_<int>(claim),
                                               P_<long long>(result));
     MS_LAUNCH_CHECK();
@@ -1191,7 +1191,7 @@ int divide_mask_dev_at(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r
     long long* h64 = nullptr;
     const int slot = status_slot_new(&h64);
     const LbState lb = lb_begin(s);
-    select_commit_kernel<<<cdiv(n, kSelThreads), kSelThreads, 0, s>>>(
+    msd::kl(select_commit_kernel, cdiv(n, kSelThreads), kSelThreads, 0, s)(
         n, P_<long long>(result), lb.status, lb.gen, lb.err, P_<int64_t>(wins), P_<int32_t>(dcount), h64, C, n0,
         n0_dev ? P_<int>(n0_dev) : nullptr, m, P_<int64_t>(par), P_<int32_t>(pos), P_<float>(cell_mols),
         P_<int32_t>(divisions), P_<int32_t>(lifetimes));
@@ -1200,7 +1200,7 @@ int divide_mask_dev_at(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r
   }
   const int slot = select_indices_async(n, 3 /* int64 >= 0 */, result, wins, 0, dcount, stream);
   const unsigned grid = std::min<unsigned>(cdiv((long long)n * m, 256), 512u);
-  divide_commit_kernel<<<grid, 256, 0, s>>>(P_<int>(dcount), P_<int64_t>(wins), P_<long long>(result), C, n0,
+  msd::kl(divide_commit_kernel, grid, 256, 0, s)(P_<int>(dcount), P_<int64_t>(wins), P_<long long>(result), C, n0,
                                             n0_dev ? P_<int>(n0_dev) : nullptr, m,
                                             P_<int64_t>(par), P_<int32_t>(pos), P_<float>(cell_mols),
                                             P_<int32_t>(divisions), P_<int32_t>(lifetimes));
@@ -1219,7 +1219,7 @@ int divide_mask_dev(int n, uintptr_t mask, uintptr_t pos, int R, int C, int r_lo
 void place_collect(int k, uintptr_t wins, uintptr_t cells, uintptr_t result, int C, uintptr_t par, uintptr_t npos,
                    uintptr_t stream) {
   if (k <= 0) return;
-  place_collect_kernel<<<cdiv(k, 256), 256, 0, S_(stream)>>>(k, P_<int64_t>(wins), cells ? P_<int64_t>(cells) : nullptr,
+  msd::kl(place_collect_kernel, cdiv(k, 256), 256, 0, S_(stream))(k, P_<int64_t>(wins), cells ? P_<int64_t>(cells) : nullptr,
                                                               P_<long long>(result), C, P_<int64_t>(par),
                                                               P_<int32_t>(npos));
   MS_LAUNCH_CHECK();
@@ -1227,7 +1227,7 @@ void place_collect(int k, uintptr_t wins, uintptr_t cells, uintptr_t result, int
 
 void index_map(int c, uintptr_t pos, int C, uintptr_t idx_map, bool clear, uintptr_t stream) {
   if (c <= 0) return;
-  index_map_kernel<<<cdiv(c, 256), 256, 0, S_(stream)>>>(c, P_<int32_t>(pos), C, P_<int32_t>(idx_map), clear);
+  msd::kl(index_map_kernel, cdiv(c, 256), 256, 0, S_(stream))(c, P_<int32_t>(pos), C, P_<int32_t>(idx_map), clear);
   MS_LAUNCH_CHECK();
 }
 
@@ -1236,7 +1236,7 @@ void index_map_lmax(int c, uintptr_t pos, int C, uintptr_t idx_map, uintptr_t le
   if (c <= 0) return;
   if (gen == 0 || gen >= (1ull << 31)) throw std::invalid_argument("index_map_lmax: generation out of range");
   if ((na == 0) != (nb == 0)) throw std::invalid_argument("index_map_lmax: give both device count words or neither");
-  index_map_lmax_kernel<<<cdiv(c, 256), 256, 0, S_(stream)>>>(c, P_<int32_t>(pos), C, P_<int32_t>(idx_map),
+  msd::kl(index_map_lmax_kernel, cdiv(c, 256), 256, 0, S_(stream))(c, P_<int32_t>(pos), C, P_<int32_t>(idx_map),
                                                                P_<int32_t>(lens), P_<unsigned long long>(word), gen,
                                                                na ? P_<int>(na) : nullptr, nb ? P_<int>(nb) : nullptr);
   MS_LAUNCH_CHECK();
@@ -1246,7 +1246,7 @@ void neighbor_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int 
                     uintptr_t stream) {
   if (n <= 0) return;
   const Geom g = geom(R, C, r_lo, r_hi, wrap);
-  neighbor_slots_kernel<<<cdiv(8LL * n, 256), 256, 0, S_(stream)>>>(n, P_<int32_t>(pos), g, P_<int32_t>(idx_map),
+  msd::kl(neighbor_slots_kernel, cdiv(8LL * n, 256), 256, 0, S_(stream))(n, P_<int32_t>(pos), g, P_<int32_t>(idx_map),
                                                                P_<int64_t>(keys));
   MS_LAUNCH_CHECK();
 }
@@ -1261,14 +1261,14 @@ static std::unordered_map<hipStream_t, int*> g_sel_cnt;
 int* append_counter(hipStream_t s) {
   int*& cnt = g_sel_cnt[s];
   if (!cnt) {
-    MS_HIP_CHECK(hipMalloc((void**)&cnt, sizeof(int)));
-    MS_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int), s));
+    MS_HIP_CHECK(msd::dev_malloc((void**)&cnt, sizeof(int)));
+    MS_HIP_CHECK(msd::memset_async(cnt, 0, sizeof(int), s));
   }
   return cnt;
 }
 void sel_sort(uintptr_t cand, int* cnt, int cap, uintptr_t sel, uintptr_t out_dev, uintptr_t gflags, uintptr_t opflags,
               hipStream_t s, uintptr_t gather) {
-  rec_sort_kernel<<<1, 1024, 0, s>>>(P_<int64_t>(cand), cnt, cap, P_<int64_t>(sel), P_<int32_t>(out_dev),
+  msd::kl(rec_sort_kernel, 1, 1024, 0, s)(P_<int64_t>(cand), cnt, cap, P_<int64_t>(sel), P_<int32_t>(out_dev),
                                      P_<int>(gflags), P_<int>(opflags), gather ? P_<int64_t>(gather) : nullptr);
   MS_LAUNCH_CHECK();
 }
@@ -1293,7 +1293,7 @@ void rec_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap,
   const auto* lw = P_<unsigned long long>(lw_word);
   if (g_rec_thin && cand && cap <= kRecSortCap) {
     int* cnt = append_counter(s);
-    rec_draw_kernel<<<(unsigned)cdiv(total, 256), 256, 0, s>>>(
+    msd::kl(rec_draw_kernel, (unsigned)cdiv(total, 256), 256, 0, s)(
         n, P_<int32_t>(pos), g, P_<int32_t>(idx_map), P_<int32_t>(lens), lw, p, seed, call, kcap, P_<int>(gflags),
         P_<int>(opflags), P_<int64_t>(keys), P_<int32_t>(k), P_<int64_t>(cand), cnt, cap, na ? P_<int>(na) : nullptr,
         nb ? P_<int>(nb) : nullptr);
@@ -1306,7 +1306,7 @@ void rec_slots(int n, uintptr_t pos, int R, int C, int r_lo, int r_hi, int wrap,
   const long long blocks = (total + kSelTile - 1) / kSelTile * (kSelTile / kSlotBlock);
   auto tiles = select_tiles(blocks, s);
   // (the blocks past the last slot write zero counts: the write pass reads whole tiles' counts)
-  rec_slots_kernel<<<(unsigned)blocks, 256, 0, s>>>(n, P_<int32_t>(pos), g, P_<int32_t>(idx_map), P_<int32_t>(lens), lw,
+  msd::kl(rec_slots_kernel, (unsigned)blocks, 256, 0, s)(n, P_<int32_t>(pos), g, P_<int32_t>(idx_map), P_<int32_t>(lens), lw,
                                                     p, seed, call, kcap, P_<int>(gflags), P_<int>(opflags),
                                                     P_<int64_t>(keys), P_<int32_t>(k), tiles.first, tiles.second);
   MS_LAUNCH_CHECK();
@@ -1318,7 +1318,7 @@ void neighbor_pairs_sorted(int n, uintptr_t pos, int R, int C, int r_lo, int r_h
                            uintptr_t in_from, uintptr_t in_to, uintptr_t keys, uintptr_t stream) {
   if (n <= 0) return;
   const Geom g = geom(R, C, r_lo, r_hi, wrap);
-  neighbor_pairs_sorted_kernel<<<cdiv(n, 256), 256, 0, S_(stream)>>>(n, P_<int32_t>(pos), g, P_<int32_t>(idx_map),
+  msd::kl(neighbor_pairs_sorted_kernel, cdiv(n, 256), 256, 0, S_(stream))(n, P_<int32_t>(pos), g, P_<int32_t>(idx_map),
                                                                      P_<uint8_t>(in_from), P_<uint8_t>(in_to),
                                                                      P_<int64_t>(keys));
   MS_LAUNCH_CHECK();
@@ -1331,7 +1331,7 @@ void release_world_buffers() {
   for (int d = 0; d < kMaxDevices; ++d) {
     if (!g_place_ctl[d]) continue;
     MS_HIP_CHECK(hipSetDevice(d));
-    MS_HIP_CHECK(hipFree(g_place_ctl[d]));
+    MS_HIP_CHECK(msd::dev_free(g_place_ctl[d]));
     g_place_ctl[d] = nullptr;
   }
   MS_HIP_CHECK(hipSetDevice(cur));

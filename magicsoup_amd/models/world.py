@@ -1362,7 +1362,13 @@ class World:
     @_op("increment_cell_lifetimes")
     def increment_cell_lifetimes(self):
         """Add 1 to every cell's lifetime."""
-        self.cell_lifetimes += 1
+        lt = self.cell_lifetimes
+        if lt.is_cuda and lt.numel() and lt.is_contiguous():
+            from magicsoup_amd.ops import hip_ops
+
+            hip_ops._m().add_i32(lt.numel(), lt.data_ptr(), 1, hip_ops._stream())  # (one native launch)
+        else:
+            self.cell_lifetimes += 1
 
     # ------------------------------------------------------------------ evolution
     @_op("mutate_cells")

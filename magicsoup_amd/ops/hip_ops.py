@@ -598,10 +598,14 @@ def degrade(world) -> None:
     if world.__dict__.get("_count_pending") is not None:
         # a division's count is still on its way to the host: every capacity row (the children
         # are among them; rows past the population are dead and get overwritten before use)
-        world._cols["cell_molecules"].buf.mul_(f)
-    elif world.n_cells > 0:
-        cm = world.cell_molecules
-        cm.mul_(f)
+        cm = world._cols["cell_molecules"].buf
+    else:
+        cm = world.cell_molecules if world.n_cells > 0 else None
+    if cm is not None and cm.numel():
+        # (one native launch: torch's broadcast mul_, bit for bit, without its dispatch)
+        m = int(cm.size(-1))
+        assert cm.is_contiguous() and cm.dtype == torch.float32
+        _m().scale_rows(cm.numel() // m, m, cm.data_ptr(), f.data_ptr(), _stream())
     pend = world.__dict__.get("_pending_scale")
     # the cached factor tensor itself (pending factors are only ever read or replaced, never
     # written in place)

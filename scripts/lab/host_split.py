@@ -166,6 +166,8 @@ torch.cuda.synchronize()
 for d in (busy, blocked, calls, native_t, native_n, py_t, py_n):
     d.clear()
 blk[0] = 0.0
+_hipm = hip_ops._m()
+gb0 = _hipm.graph_batch_stats() if hasattr(_hipm, "graph_batch_stats") else None
 prof = None
 if os.environ.get("MS_CPROFILE") == "1":  # per-function host time (tottime) of the timed steps
     import cProfile
@@ -177,6 +179,12 @@ for _ in range(steps):
     bench.step(w, N, 500, atp)
 torch.cuda.synchronize()
 wall = (time.perf_counter() - t0) / steps * 1e6
+if gb0 is not None:  # graph batching of the native launches (csrc/hip/launch.h), per step
+    gb1 = _hipm.graph_batch_stats()
+    per = {k: round((gb1[k] - gb0[k]) / steps, 2) for k in ("graph_launches", "graph_nodes", "direct", "updated_nodes",
+                                                             "instantiated", "flushes")}
+    hist = {int(k): round((v - gb0["batch_sizes"].get(k, 0)) / steps, 2) for k, v in gb1["batch_sizes"].items()}
+    print("graph batching per step:", per, "batch lengths:", {k: v for k, v in sorted(hist.items()) if v})
 if prof is not None:
     import io
     import pstats

@@ -23,6 +23,14 @@ struct Big {
 __global__ void k_small(int* p, int v) {
   if (threadIdx.x == 0 && blockIdx.x == 0 && v == -12345) *p = v;
 }
+// writes its own (slot, value) after a short spin: a graph updated while earlier launches of it are
+// still queued must not show them the later arguments
+__global__ void k_rec(int* out, int slot, int val, int spin) {
+  long long t0 = clock64();
+  while (clock64() - t0 < spin) {
+  }
+  if (threadIdx.x == 0) atomicAdd(out + slot, val);
+}
 __global__ void k_big(Big b) {
   if (threadIdx.x == 0 && blockIdx.x == 0 && b.w[3] == 12345ull) *reinterpret_cast<int*>(b.w[0]) = 1;
 }
@@ -75,5 +83,149 @@ int main() {
   double t4 = now_us();
   std::printf("{\"graph17_launch_us\": %.2f, \"direct17_us\": %.2f, \"graph17_device_us\": %.2f, \"direct17_device_us\": %.2f}\n",
               (t1 - t0) / M, (t3 - t2) / M, (t2 - t0) / M, (t4 - t2) / M);
+  // every node's arguments and grid changed before each launch (hipGraphExecKernelNodeSetParams)
+  {
+    size_t nn = 0;
+    CK(hipGraphGetNodes(g, nullptr, &nn));
+    hipGraphNode_t nodes[64];
+    CK(hipGraphGetNodes(g, nodes, &nn));
+    hipKernelNodeParams kp[64];
+    for (size_t j = 0; j < nn; ++j) CK(hipGraphKernelNodeGetParams(nodes[j], &kp[j]));
+    Big bb[64];
+    void* argp[64][1];
+    double u0 = now_us();
+    for (int i = 0; i < M; ++i) {
+      for (size_t j = 0; j < nn; ++j) {
+        bb[j] = b;
+        bb[j].w[5] = (unsigned long long)(i * 64 + j);
+        argp[j][0] = &bb[j];
+        kp[j].kernelParams = argp[j];
+        kp[j].gridDim = dim3(64 + (i & 1), 1, 1);
+        CK(hipGraphExecKernelNodeSetParams(ge, nodes[j], &kp[j]));
+      }
+      CK(hipGraphLaunch(ge, s));
+    }
+    double u1 = now_us();
+    CK(hipStreamSynchronize(s));
+    double u2 = now_us();
+    std::printf("{\"graph17_setparams_launch_us\": %.2f, \"graph17_setparams_device_us\": %.2f}\n", (u1 - u0) / M,
+                (u2 - u0) / M);
+  }
+  // a graph whose kernels read their arguments from a device block refreshed by a captured
+  // host-to-device copy from pinned memory (one memcpy node + 17 kernels)
+  {
+    Big* hb;
+    Big* db;
+    CK(hipHostMalloc(&hb, sizeof(Big), 0));
+    CK(hipMalloc(&db, sizeof(Big)));
+    *hb = b;
+    hipGraph_t g2;
+    hipGraphExec_t ge2;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+    CK(hipMemcpyAsync(db, hb, sizeof(Big), hipMemcpyHostToDevice, s));
+    for (int i = 0; i < 17; ++i) k_small<<<64, 256, 0, s>>>(reinterpret_cast<int*>(db), i);
+    CK(hipStreamEndCapture(s, &g2));
+    CK(hipGraphInstantiate(&ge2, g2, nullptr, nullptr, 0));
+    for (int i = 0; i < 20; ++i) CK(hipGraphLaunch(ge2, s));
+    CK(hipStreamSynchronize(s));
+    double v0 = now_us();
+    for (int i = 0; i < M; ++i) {
+      CK(hipGraphLaunch(ge2, s));
+      CK(hipStreamSynchronize(s));  // (the pinned block is rewritten for the next launch)
+      hb->w[5] = i;
+    }
+    double v1 = now_us();
+    std::printf("{\"graph_memcpy17_launch_sync_us\": %.2f}\n", (v1 - v0) / M);
+    double w0 = now_us();
+    for (int i = 0; i < M; ++i) {
+      for (int j = 0; j < 17; ++j) k_big<<<64, 256, 0, s>>>(b);
+      CK(hipStreamSynchronize(s));
+    }
+    double w1 = now_us();
+    std::printf("{\"direct17_sync_us\": %.2f}\n", (w1 - w0) / M);
+  }
+  // correctness of in-flight updates: 200 launches of a 17-node graph, every node's arguments
+  // changed before each launch, the device ~20 us behind per node
+  {
+    const int L = 200, K = 17;
+    int* out;
+    CK(hipMalloc(&out, L * K * sizeof(int)));
+    CK(hipMemset(out, 0, L * K * sizeof(int)));
+    hipGraph_t g3;
+    hipGraphExec_t ge3;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+    for (int j = 0; j < K; ++j) k_rec<<<4, 64, 0, s>>>(out, 0, 0, 1);
+    CK(hipStreamEndCapture(s, &g3));
+    CK(hipGraphInstantiate(&ge3, g3, nullptr, nullptr, 0));
+    size_t nn = 0;
+    CK(hipGraphGetNodes(g3, nullptr, &nn));
+    hipGraphNode_t nodes[64];
+    CK(hipGraphGetNodes(g3, nodes, &nn));
+    hipKernelNodeParams kp;
+    CK(hipGraphKernelNodeGetParams(nodes[0], &kp));
+    int spin = 20000;
+    double t0 = now_us();
+    for (int i = 0; i < L; ++i) {
+      for (size_t j = 0; j < nn; ++j) {
+        int slot = i * K + (int)j, val = slot + 1;
+        void* a[4] = {&out, &slot, &val, &spin};
+        kp.kernelParams = a;
+        kp.gridDim = dim3(1 + (i % 4), 1, 1);
+        CK(hipGraphExecKernelNodeSetParams(ge3, nodes[j], &kp));
+      }
+      CK(hipGraphLaunch(ge3, s));
+    }
+    double t1 = now_us();
+    CK(hipStreamSynchronize(s));
+    double t2 = now_us();
+    int* h = (int*)std::malloc(L * K * sizeof(int));
+    CK(hipMemcpy(h, out, L * K * sizeof(int), hipMemcpyDeviceToHost));
+    int bad = 0;
+    for (int i = 0; i < L; ++i)
+      for (int j = 0; j < K; ++j) {
+        const int x = i * K + j;
+        if (h[x] != (x + 1) * (1 + (i % 4))) ++bad;
+      }
+    std::printf("{\"inflight_update_bad_slots\": %d, \"of\": %d, \"host_us_per_launch\": %.2f, \"device_us_per_launch\": %.2f}\n",
+                bad, L * K, (t1 - t0) / L, (t2 - t0) / L);
+  }
+  // concurrency across streams: a 300 us kernel on stream A, then 3 short kernels on stream B --
+  // directly and as a graph -- and the host time until B's event completes
+  {
+    hipStream_t sa, sb;
+    CK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+    int* o;
+    CK(hipMalloc(&o, 64 * sizeof(int)));
+    hipEvent_t eb;
+    CK(hipEventCreateWithFlags(&eb, hipEventDisableTiming));
+    hipGraph_t g4;
+    hipGraphExec_t ge4;
+    CK(hipStreamBeginCapture(sb, hipStreamCaptureModeGlobal));
+    for (int j = 0; j < 3; ++j) k_rec<<<1, 64, 0, sb>>>(o, j, 1, 1000);
+    CK(hipStreamEndCapture(sb, &g4));
+    CK(hipGraphInstantiate(&ge4, g4, nullptr, nullptr, 0));
+    CK(hipGraphLaunch(ge4, sb));
+    CK(hipDeviceSynchronize());
+    const int spin_a = 300 * 2100;  // ~300 us at ~2.1 GHz
+    for (int mode = 0; mode < 2; ++mode) {
+      double tot = 0.0;
+      for (int rep = 0; rep < 20; ++rep) {
+        k_rec<<<1, 64, 0, sa>>>(o, 10, 1, spin_a);
+        double t0 = now_us();
+        if (mode == 0) {
+          for (int j = 0; j < 3; ++j) k_rec<<<1, 64, 0, sb>>>(o, j, 1, 1000);
+        } else {
+          CK(hipGraphLaunch(ge4, sb));
+        }
+        CK(hipEventRecord(eb, sb));
+        while (hipEventQuery(eb) == hipErrorNotReady) {
+        }
+        tot += now_us() - t0;
+        CK(hipDeviceSynchronize());
+      }
+      std::printf("{\"cross_stream_%s_us\": %.1f}\n", mode == 0 ? "direct" : "graph", tot / 20);
+    }
+  }
   return 0;
 }

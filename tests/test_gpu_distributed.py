@@ -53,6 +53,61 @@ def test_gpu_distributed_physics_match_single_process():
     run_ranks(_body_physics, 2, timeout=600)
 
 
+def _by_position(w, C):
+    key = w.cell_positions.long().cpu() @ torch.tensor([C, 1])
+    return torch.argsort(key)
+
+
+def _body_physics_stepwise(rank, ws):
+    """Per-op exactness against a single-process world that restarts from the gathered distributed
+    state before every op (no drift between the two): the activity -- whose early exits are global
+    decisions, the all-reduced flags here and the population-wide `any` there -- gives every cell the
+    same bits; degradation too; diffusion + permeation agree to float rounding (the mass correction
+    sums its global totals in another order)."""
+    import magicsoup_amd as ms
+    from magicsoup_amd.parallel import DistributedWorld
+    from tests.conftest import gen_genomes
+
+    C = 64
+    ms.set_seed(4)
+    torch.manual_seed(4)
+    g = ms.World(chemistry=_chem(), map_size=C, seed=4, device="cpu")
+    g.spawn_cells(gen_genomes(700, 300))
+    dw = DistributedWorld(chemistry=_chem(), map_size=C, seed=6, device="cuda")
+    dw.scatter_from(g)
+    checked = {"activity": 0, "degrade": 0, "diffuse": 0}
+    for it in range(3):
+        for op in ("enzymatic_activity", "degrade_molecules", "diffuse_molecules"):
+            ref = dw.gather()
+            if rank == 0:
+                ref = ref.to("cuda")
+                getattr(ref, op)()
+            getattr(dw, op)()
+            full = dw.gather()
+            if rank != 0:
+                continue
+            ref = ref.to("cpu")
+            oa, ob = _by_position(full, C), _by_position(ref, C)
+            assert torch.equal(full.cell_positions[oa], ref.cell_positions[ob])
+            if op == "diffuse_molecules":
+                assert torch.allclose(full.molecule_map, ref.molecule_map, rtol=2e-6, atol=1e-6)
+                assert torch.allclose(full.cell_molecules[oa], ref.cell_molecules[ob], rtol=2e-6, atol=1e-6)
+                checked["diffuse"] += 1
+            else:
+                a, b = full.cell_molecules[oa], ref.cell_molecules[ob]
+                bad = (a != b).any(dim=1)
+                assert not bad.any(), (op, it, int(bad.sum()), float((a - b).abs().max()),
+                                       float(((a - b).abs() / b.abs().clamp(min=1e-30)).max()))
+                assert torch.equal(full.molecule_map, ref.molecule_map), (op, it)
+                checked["activity" if op == "enzymatic_activity" else "degrade"] += 1
+    if rank == 0:
+        assert checked == {"activity": 3, "degrade": 3, "diffuse": 3}
+
+
+def test_gpu_distributed_physics_exact_per_op():
+    run_ranks(_body_physics_stepwise, 2, timeout=600)
+
+
 def _body_steps(rank, ws):
     import torch.distributed as dist
 

@@ -1406,6 +1406,52 @@ def test_bench_steps_with_spawns_replay_bit_identically():
     bench._CHEMOSTAT.update(divided=0, starved=0, steps=0, excess=None, last_d=0, last_s=0)
 
 
+@pytest.mark.gpu
+def test_graph_batched_launches_match_direct_launches():
+    """With graph batching on, the kernels each native call records go out as one hipGraph launch,
+    replayed with updated arguments (csrc/hip/launch.h, opt-in): 20 bench steps (top-ups, chemostat kill / divide, the genome
+    chains) from one seed end bit-identical with batching on and with every kernel launched
+    directly, and the batched run did launch graphs (and re-used them)."""
+    import random
+
+    import bench
+    from magicsoup_amd.ops import native
+
+    m = native.hip()
+    atp = CHEMISTRY.molname_2_idx["ATP"]
+    runs, stats = [], []
+    try:
+        for on in (False, True):
+            m.set_graph_batch(on)
+            m.graph_batch_reset()
+            random.seed(5)
+            ms.set_seed(5)
+            torch.manual_seed(5)
+            bench._CHEMOSTAT.update(divided=0, starved=0, steps=0, excess=None, last_d=0, last_s=0)
+            w = ms.World(chemistry=CHEMISTRY, map_size=96, device="cuda", seed=5)
+            w.spawn_cells(bench.random_genomes(3000, 500, "cuda"))
+            for _ in range(20):
+                bench.step(w, 3000, 500, atp)
+            w.synchronize()
+            stats.append(m.graph_batch_stats())
+            k = w.kinetics
+            runs.append({
+                "n": w.n_cells, "positions": w.cell_positions.clone(), "molecules": w.cell_molecules.clone(),
+                "lifetimes": w.cell_lifetimes.clone(), "divisions": w.cell_divisions.clone(),
+                "cell_map": w.cell_map.clone(), "map": w.molecule_map.clone(), "genomes": list(w.cell_genomes),
+                **{p: getattr(k, p).clone() for p in ("N", "A", "Kmr", "Vmax", "Ke")},
+            })
+    finally:
+        m.set_graph_batch(False)
+        bench._CHEMOSTAT.update(divided=0, starved=0, steps=0, excess=None, last_d=0, last_s=0)
+    a, b = runs
+    bad = [key for key in a if not (torch.equal(a[key], b[key]) if isinstance(a[key], torch.Tensor) else a[key] == b[key])]
+    assert not bad, bad
+    assert stats[0]["graph_launches"] == 0
+    assert stats[1]["graph_launches"] >= 40 and stats[1]["graph_nodes"] > 2 * stats[1]["graph_launches"], stats[1]
+    assert stats[1]["instantiated"] < stats[1]["graph_launches"] // 2, stats[1]  # (replayed, not rebuilt)
+
+
 def test_gpu_step_loop_is_deterministic():
     """The reference loop as bench.py issues it (activity, kill, lazy division, queued
     recombination + mutation chain, degradation, diffusion next to the chain, lifetimes; no host
