@@ -1665,7 +1665,8 @@ __device__ __forceinline__ void build_group(const BuildArgs& b, long long grp, i
       b.A[o3 + j] = av;
     }
     if (b.W) b.W[o3 + j] = pack_word(n, nf, nb, av, b.overflow);
-    b.Kmr[o3 + j] = powf(kc > 0 ? ks / (float)kc : 0.0f, (float)av);
+    // (x^a by multiplications, as the host build: device and host powf differ in the last bit)
+    b.Kmr[o3 + j] = ms::ipow(kc > 0 ? ks / (float)kc : 0.0f, av);
     E += (double)n * (double)b.energies[j];
   }
   for (int o = G / 2; o > 0; o >>= 1) E += __shfl_xor(E, o, G);

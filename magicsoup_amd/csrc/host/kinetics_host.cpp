@@ -341,7 +341,7 @@ void build_params(iarr tokens, iarr rows, farr vmax_w, farr km_w, iarr signs, ia
       double E = 0.0;
       for (int j = 0; j < s; ++j) {
         const float km_mean = kmr_cnt[j] > 0 ? kmr_sum[j] / (float)kmr_cnt[j] : 0.0f;
-        kmr_[j] = powf(km_mean, (float)a_[j]);
+        kmr_[j] = ms::ipow(km_mean, a_[j]);  // (the device build computes the same products)
         E += (double)n_[j] * (double)en[j];
       }
       float ke = expf(-(float)E / abs_temp / gas_const);

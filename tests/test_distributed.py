@@ -82,6 +82,38 @@ def test_distributed_physics_match_single_process():
     run_ranks(_body_physics, 2)
 
 
+def _body_physics_per_op(rank, ws):
+    """Each op from the same (gathered) state in both worlds: the activity -- with the early exits as
+    global decisions -- and the degradation give every cell the same bits; the diffusion agrees to
+    float rounding."""
+    g = _global_world(map_size=24, n=150)
+    dw = _dworld(24)
+    dw.scatter_from(g)
+    for it in range(3):
+        for op in ("enzymatic_activity", "degrade_molecules", "diffuse_molecules"):
+            ref = dw.gather()
+            if rank == 0:
+                getattr(ref, op)()
+            getattr(dw, op)()
+            full = dw.gather()
+            if rank != 0:
+                continue
+            oa = torch.argsort(full.cell_positions.long() @ torch.tensor([24, 1]))
+            ob = torch.argsort(ref.cell_positions.long() @ torch.tensor([24, 1]))
+            a, b = full.cell_molecules[oa], ref.cell_molecules[ob]
+            if op == "diffuse_molecules":
+                assert torch.allclose(full.molecule_map, ref.molecule_map, rtol=2e-6, atol=1e-6)
+                assert torch.allclose(a, b, rtol=2e-6, atol=1e-6)
+            else:
+                bad = (a != b).any(dim=1)
+                assert not bad.any(), (op, it, int(bad.sum()), float((a - b).abs().max()))
+                assert torch.equal(full.molecule_map, ref.molecule_map), (op, it)
+
+
+def test_distributed_physics_exact_per_op():
+    run_ranks(_body_physics_per_op, 2)
+
+
 def _body_diffusion_mass(rank, ws):
     dw = _dworld(32)
     before = dw.owned_molecule_map().double().sum(dim=[1, 2]).clone()

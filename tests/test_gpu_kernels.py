@@ -68,7 +68,10 @@ def test_param_build_matches_host():
         assert torch.equal(getattr(kg, name).cpu()[full], getattr(kc, name)[full]), name
     for name in ("Kmr", "Kmf", "Kmb", "Vmax", "Ke"):
         a, b = getattr(kg, name).cpu()[full], getattr(kc, name)[full]
-        assert torch.allclose(a, b, rtol=1e-5, atol=1e-30, equal_nan=True), name
+        # bit for bit: the Kmr powers are integer products in both builds (device powf differs from
+        # the host's in the last bit, and a decomposed world's ranks build on the device what a
+        # gathered world rebuilds on the host)
+        assert torch.equal(a.nan_to_num(-7.0), b.nan_to_num(-7.0)), name
 
 
 @pytest.mark.parametrize("n_iters", [0, 4])
