@@ -1678,7 +1678,9 @@ __device__ __forceinline__ void build_group(const BuildArgs& b, long long grp, i
     vm.add(b.vmax_w[lut(dm[1], b.nw)]);
     km.add(b.km_w[lut(dm[2], b.nk)]);
   }
-  float kev = expf(-(float)E / b.abs_temp / b.gas);
+  // (the float exponent as before, evaluated in double and rounded once: device and host expf differ
+  // in the last bit for ~1 in 10^4 proteins, the double results round to the same float)
+  float kev = (float)exp((double)(-(float)E / b.abs_temp / b.gas));
   kev = kev < ms::kEps ? ms::kEps : (kev > ms::kMax ? ms::kMax : kev);
   const float kmn = km.value0();
   float kmfv = kev >= 1.0f ? kmn : kmn / kev;

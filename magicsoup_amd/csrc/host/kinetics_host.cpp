@@ -344,7 +344,7 @@ void build_params(iarr tokens, iarr rows, farr vmax_w, farr km_w, iarr signs, ia
         kmr_[j] = ms::ipow(km_mean, a_[j]);  // (the device build computes the same products)
         E += (double)n_[j] * (double)en[j];
       }
-      float ke = expf(-(float)E / abs_temp / gas_const);
+      float ke = (float)std::exp((double)(-(float)E / abs_temp / gas_const));  // (as the device build)
       ke = ke < ms::kEps ? ms::kEps : (ke > ms::kMax ? ms::kMax : ke);
       const float kmn = km.value0();
       float kmf = ke >= 1.0f ? kmn : kmn / ke;

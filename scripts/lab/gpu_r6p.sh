@@ -4,7 +4,8 @@
 set -o pipefail
 O=gpurun_out/r6p
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit $?
+true
+timeout -k 10 200 python -u scripts/lab/param_paths.py 30000 > $O/param_paths_30k.log 2>&1 || exit $?
 timeout -k 10 200 python -u bench.py > $O/flag.log 2>&1 &&
 timeout -k 10 200 python -u bench.py --map-size 1448 --cells 6250 > $O/plain8.log 2>&1 &&
 MS_VIRTUAL_STRIPS=1 timeout -k 10 200 python -u bench.py --map-size 1448 --cells 6250 > $O/virt8.log 2>&1

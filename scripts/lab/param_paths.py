@@ -17,7 +17,7 @@ from tests.conftest import gen_genomes  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 700
 ms.set_seed(4)
 torch.manual_seed(4)
-g = ms.World(chemistry=CHEMISTRY, map_size=64, seed=4, device="cpu")
+g = ms.World(chemistry=CHEMISTRY, map_size=256 if n > 3000 else 64, seed=4, device="cpu")
 g.spawn_cells(gen_genomes(n, 300))
 a = copy.deepcopy(g).to("cuda")  # host-derived parameters, moved
 b = copy.deepcopy(g).to("cuda")
@@ -32,7 +32,7 @@ for name in ("N", "Nf", "Nb", "A", "Kmf", "Kmb", "Kmr", "Vmax", "Ke"):
     P = min(x.size(1), y.size(1))
     x, y = x[:, :P], y[:, :P]
     d = x != y
-    cells = int(d.reshape(n, -1).any(dim=1).sum())
+    cells = int(d.reshape(d.size(0), -1).any(dim=1).sum())
     rel = 0.0
     if x.is_floating_point() and d.any():
         rel = float(((x - y).abs() / x.abs().clamp(min=1e-30))[d].max())

@@ -51,8 +51,9 @@ def _copy_world_cpu_to_gpu(wc):
     return wg.to("cuda")
 
 
-def test_param_build_matches_host():
-    wc = _world("cpu", n=200)
+@pytest.mark.parametrize("n", [200, 30000])
+def test_param_build_matches_host(n):
+    wc = _world("cpu", n=n, map_size=64 if n < 3000 else 256)
     rows = torch.arange(wc.n_cells)
     from magicsoup_amd.ops import world_ops, hip_ops, kinetics_ops
 
