@@ -107,6 +107,8 @@ _LAZY_KILL = os.environ.get("MS_STRIP_LAZY_KILL", "1") != "0"
 # before the next activity instead of next to the stencil (no gain, profiles/r5/early_stencil/)
 _EARLY_STENCIL = os.environ.get("MS_EARLY_STENCIL", "1") != "0"
 _EARLY_STENCIL_MAX_PX = int(os.environ.get("MS_EARLY_STENCIL_MAX_PX", str(4 << 20)))
+# ... and that stencil issued before the host waits for phase A's counts (0: after the wait)
+_STENCIL_BEFORE_WAIT = os.environ.get("MS_STENCIL_BEFORE_WAIT", "1") != "0"
 
 
 class DistributedWorld(World):
@@ -639,7 +641,7 @@ class DistributedWorld(World):
         return True
 
     def _divide_phase_b(self, n0: int, lw: int, gw: int, defer_arrivals: bool = False, kk: int | None = None,
-                        pairs: bool = True, stencil_first=None, _prepared: bool = False
+                        pairs: bool = True, stencil_first=None, _prepared: bool = False, stencil_before=None
                         ) -> tuple[torch.Tensor, torch.Tensor] | None:
         """Phase B of :meth:`_divide_mask_native` once phase A's counts are on the host (its pinned
         status copy is complete): records out, children in, arrivals appended and their parameter
@@ -653,6 +655,8 @@ class DistributedWorld(World):
         dev = self._tensor_device()
         m = self.n_molecules
         sc = _scratch(self)
+        # (the stencil went out before the counts were read: the buffers as they were then)
+        bufs0 = self._buffer_objs() if stencil_before is not None else None
         # kk: the row count phase A ran over (the cells before a lazy kill; par / npos offsets)
         kk = n0 if kk is None else int(kk)
         par = sc.get("dv_par", 3 * kk, torch.int64, dev)
@@ -686,8 +690,14 @@ class DistributedWorld(World):
             from magicsoup_amd.ops import world_ops
             from magicsoup_amd.ops.streams import NEvent, on_stream
 
-            before = NEvent().record()
-            world_ops.diffuse(self)
+            if stencil_before is None:
+                before = NEvent().record()
+                world_ops.diffuse(self)
+            elif all(a is b for a, b in zip(self._buffer_objs(), bufs0)):
+                before = stencil_before  # (the capacity steps above issued no device work)
+            else:
+                # a buffer was reallocated behind the stencil (rare): phase B waits for the copy
+                before = NEvent().record()
             side = stencil_first
             before.wait(side.cuda_stream)
             self.__dict__["_side_active"] = True
@@ -716,7 +726,14 @@ class DistributedWorld(World):
             return None
         return par[:n_loc], torch.arange(n0, n0 + n_loc, device=self.device)
 
-    def _resolve_count(self, stencil_first=None) -> None:
+    def _buffer_objs(self) -> tuple:
+        """The per-cell buffer objects a capacity step replaces when it reallocates (a new tensor
+        object each time, see World._fast_world)."""
+        g, lab, kd = self._genomes, self._labels, self.kinetics.__dict__
+        return (g.data, g.off, g.lens, lab.data, lab.lens, kd.get("_slot_buf"), kd.get("_slot_spare"),
+                self.__dict__.get("_cell_map"), *(c.buf for c in self._cols.values()))
+
+    def _resolve_count(self, stencil_first=None, stencil_before=None) -> None:
         """Adopt a pending division: World's (a winner count) or a strip division issued with
         ``lazy=True`` (wait for its phase A only, then issue phase B, see _divide_mask_native). Queued
         genome operations then depend on phase B: their chains wait for it, not for the state when
@@ -747,7 +764,8 @@ class DistributedWorld(World):
         pair = (_ARRIVALS_MERGE and queued is not None and len(queued) >= 2 and getattr(queued[0], "kind", None) == "rec"
                 and getattr(queued[1], "kind", None) == "mut")
         try:
-            self._divide_phase_b(n0, lw, gw, defer_arrivals=pair, kk=kk, pairs=False, stencil_first=stencil_first)
+            self._divide_phase_b(n0, lw, gw, defer_arrivals=pair, kk=kk, pairs=False, stencil_first=stencil_first,
+                                 stencil_before=stencil_before)
         finally:
             if queued:
                 from magicsoup_amd.ops.streams import NEvent
@@ -780,9 +798,10 @@ class DistributedWorld(World):
         """diffuse_molecules while a lazy strip division is pending, with the stencil before phase B.
 
         Phase B (record exchange, children and arrivals committed, halo rows cleared) touches the
-        per-cell rows and the cell map, never the molecule map, and phase A's spill is done; the
-        stencil reads and writes only the map. So after the one wait for phase A's counts the
-        stencil is issued first, and phase B, the boundary recombination's collective part and the
+        per-cell rows and the cell map, never the molecule map, and phase A's spill is queued before
+        it; the stencil reads and writes only the map. So the stencil is issued first -- before the
+        one wait for phase A's counts (``MS_STENCIL_BEFORE_WAIT``, default on: the host issues it
+        while the counts travel) -- and phase B, the boundary recombination's collective part and the
         genome chains follow on the side stream over the side communicator, next to it: the device
         no longer idles while the host issues phase B and the chains (~150 us per flagship step as
         one virtual strip, profiles/r5/lazykill). Same kernels, draws and order per communicator on
@@ -797,7 +816,17 @@ class DistributedWorld(World):
         if side is None:
             side = d["_side_stream"] = torch.cuda.Stream(device=self._genomes.data.device, priority=-1)
         main = _stream()
-        self._resolve_count(stencil_first=side)
+        from magicsoup_amd.ops.streams import NEvent
+
+        if _STENCIL_BEFORE_WAIT:
+            # the stencil before the wait for phase A's counts: it reads and writes only the map (phase
+            # A's spill is queued before it), so the host issues it while the counts are on their way
+            # instead of after them
+            before = NEvent().record()
+            world_ops.diffuse(self)
+            self._resolve_count(stencil_first=side, stencil_before=before)
+        else:
+            self._resolve_count(stencil_first=side)
         from magicsoup_amd.ops.streams import on_stream
 
         with on_stream(side):
