@@ -597,6 +597,24 @@ template <int NZ>
 constexpr int vote_word(int v) { return (v * jl_stride<NZ>() + NZ) / 4; }  // row v's pad
 constexpr int kMgSumWord = 16;  // first jl word of the chunk-sum buffers (past the vote rows 0..2)
 
+// Phase timing of the register integrator (lab builds only: -DMS_INT_PROF, scripts/lab/int_prof.py):
+// cycles per phase of the first cell of a launch, summed over launches, read by int_prof_read().
+#ifdef MS_INT_PROF
+__device__ unsigned long long g_int_prof[64];
+#define MS_PROBE(id)                                                   \
+  do {                                                                 \
+    if (item == 0 && lane == 0 && grp == 0) {                          \
+      const unsigned long long t_ = clock64();                         \
+      g_int_prof[id] += t_ - prof_t;                                   \
+      prof_t = t_;                                                     \
+    }                                                                  \
+  } while (0)
+#else
+#define MS_PROBE(id) \
+  do {               \
+  } while (0)
+#endif
+
 template <int G, int NZ, bool kSpec = false, int SPL = 1, int NG = 1>
 __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int* smem, int item, unsigned& bits,
                                                     int32_t* wide_list, int32_t* wide_count) {
@@ -606,6 +624,9 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   static_assert(G == kChunk || G == 2 * kChunk, "a group covers one or two canonical chunks");
   const int slot = threadIdx.x / G, lane = threadIdx.x % G;
   const int grp = NG > 1 ? slot : 0;  // this group's chunk of the cell's active proteins
+#ifdef MS_INT_PROF
+  unsigned long long prof_t = clock64();
+#endif
   const bool listed0 = a.list ? item < *a.count : item < a.c;
   const int cell0 = listed0 ? (a.list ? a.list[item] : item) : 0;
   const bool listed = listed0 && (unsigned)cell0 < (unsigned)a.c;  // (a list entry is a cell index)
@@ -638,6 +659,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
     }
   }
 
+  MS_PROBE(0);
   // ---- 2. active proteins (Vmax' != 0, NaN included) in ascending order; group grp keeps entries
   //         [grp * G, grp * G + G) of the compacted list
   constexpr bool spec = kSpec;
@@ -662,6 +684,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   // wave-uniform bound of the protein loops (both groups of a wave), in an SGPR: scalar loop exits
   const int na_w = __builtin_amdgcn_readfirstlane(wave_max(nac));
 
+  MS_PROBE(1);
   // ---- 3. this lane's signals' stoichiometry columns (int8 n per protein, packed in registers) and
   //         the per-protein non-zero lists (one ballot per protein and half), 8 rows of loads in flight
   int npk[SPL][G / 4];
@@ -702,6 +725,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
       wide_ok &= base <= NZ;
     }
   }
+  MS_PROBE(2);
   bool nz_ok = group_ballot<G>(!wide_ok) == 0ull;
   // multi-group: word v of group g's votes (a pad word of its slot's entry-index rows)
   auto vote = [&](int g, int v) -> int& { return smem[g * SW + G * ES + vote_word<NZ>(v)]; };
@@ -860,6 +884,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   float xc[SPL];
 #pragma unroll
   for (int h = 0; h < SPL; ++h) xc[h] = x0[h];
+  MS_PROBE(3);
   for (int part = 0; part < nparts; ++part) {
   const float vm = vraw * (spec ? trim_of(a, part) : a.trim);
   const float vmx = prot && (vm > 0.0f || vm != vm) ? vm : 0.0f;
@@ -912,6 +937,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   pub[lane] = v;
   wave_lds_sync();
 
+  MS_PROBE(4);
   // ---- 5. consumption per signal -> negative-concentration factor (signal lane)
   {
     float cons[SPL];
@@ -930,6 +956,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   }
   wave_lds_sync();
 
+  MS_PROBE(5);
   // ---- 6. per-protein limiting factor (protein lane)
   float va = 0.0f, F = 1.0f;
   int flg = 0;
@@ -955,6 +982,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   pub[lane] = va;
   wave_lds_sync();
 
+  MS_PROBE(6);
   // ---- 7. candidate 0 (signal lane)
   auto advance = [&]() {  // X0 + sum_k n_k * pub_k (canonical order), clamped at 0
     float x[SPL];
@@ -975,6 +1003,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   }
   wave_lds_sync();
 
+  MS_PROBE(7);
   // ---- 8. equilibrium damping trajectory
   float inc = 0.5f;
   for (int it = 0; it < a.n_iters; ++it, inc *= 0.5f) {
@@ -1045,6 +1074,7 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
   }
 #pragma unroll
   for (int h = 0; h < SPL; ++h) x0[h] = xc[h];  // the next part starts from this part's last candidate
+  MS_PROBE(8);
   }
   if (spec) {
 #pragma unroll
@@ -1064,6 +1094,10 @@ __device__ __forceinline__ void integrate_item_fast(const IntegrateArgs& a, int*
       }
     }
   }
+  MS_PROBE(9);
+#ifdef MS_INT_PROF
+  if (item == 0 && lane == 0 && grp == 0) g_int_prof[63] += 1;
+#endif
 #undef MS_E
 }
 
@@ -1728,6 +1762,22 @@ static int slot_words_for(int P, int s, int sp) {
 // rank without cells (it still joins the all-reduces of the protocol it implies).
 // Per stream: device memory for the register launch's argument blocks (two IntegrateArgs), written
 // by the input kernel and read by integrate_spec_fused_kernel on the same stream.
+std::vector<unsigned long long> int_prof_read(bool reset) {
+#ifdef MS_INT_PROF
+  std::vector<unsigned long long> v(64);
+  MS_HIP_CHECK(msd::device_synchronize());
+  MS_HIP_CHECK(hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_int_prof), 64 * sizeof(unsigned long long)));
+  if (reset) {
+    std::vector<unsigned long long> z(64, 0ull);
+    MS_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_int_prof), z.data(), 64 * sizeof(unsigned long long)));
+  }
+  return v;
+#else
+  (void)reset;
+  return {};
+#endif
+}
+
 static std::unordered_map<hipStream_t, IntegrateArgs*> g_args_dev;
 static IntegrateArgs* args_block(hipStream_t st) {
   IntegrateArgs*& p = g_args_dev[st];

@@ -59,6 +59,7 @@ void diffuse_correct(int m, int R, int C, int r_lo, int r_hi, uintptr_t map, uin
                      double n_pix, int dtype, uintptr_t stream);
 void scale_planes(int m, long long plane, uintptr_t map, uintptr_t f, int dtype, uintptr_t stream);
 void scale_rows(long long rows, int m, uintptr_t x, uintptr_t f, uintptr_t stream);
+std::vector<unsigned long long> int_prof_read(bool reset);
 void add_i32(long long n, uintptr_t x, int v, uintptr_t stream);
 void health_scan(int planes, long long span, long long stride, uintptr_t x, int dtype, int shift, uintptr_t flags,
                  uintptr_t stream);
@@ -296,6 +297,7 @@ PYBIND11_MODULE(_hip, m) {
   msd::gdef(m, "apply_pending", &msd::apply_pending);
   msd::gdef(m, "diffuse_partials_len", &msd::diffuse_partials_len);
   msd::gdef(m, "scale_planes", &msd::scale_planes);
+  msd::gdef(m, "int_prof_read", &msd::int_prof_read, "register integrator phase cycles (lab builds with -DMS_INT_PROF; empty otherwise)");
   msd::gdef(m, "scale_rows", &msd::scale_rows, "x (rows, m) *= f[col] in place (fp32)");
   msd::gdef(m, "add_i32", &msd::add_i32, "x[:n] += v in place (int32)");
   msd::gdef(m, "health_scan", &msd::health_scan);

@@ -2,7 +2,9 @@
 objects of every source except those given, which are compiled from the given files.
 
     python scripts/lab/build_variant.py <out.so> <variant.hip> [...]   (each replaces its namesake)
-"""
+
+MS_VARIANT_FLAGS: extra compiler flags for the variant sources (e.g. -DMS_INT_PROF)."""
+import os
 import subprocess
 import sys
 from pathlib import Path
@@ -26,7 +28,8 @@ def main():
     for src in sorted((build.CSRC / "hip").glob("*.hip")):
         if src.stem in variants:
             o = tmp / (src.stem + ".o")
-            subprocess.run([hipcc, *cflags, "-c", str(variants[src.stem]), "-o", str(o)], check=True)
+            extra = os.environ.get("MS_VARIANT_FLAGS", "").split()
+            subprocess.run([hipcc, *cflags, *extra, "-c", str(variants[src.stem]), "-o", str(o)], check=True)
             objs.append(o)
         else:
             objs.append(objdir / (src.stem + ".o"))

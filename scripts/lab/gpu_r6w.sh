@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 6, batch W: the allosteric Kmr prefetch in the register integrator -- in-process A/B against
+# the previous kinetics.hip (ab/int_base.so) at 200 / 6250 / 50000 cells and the wide chemistry, and
+# the phase profile of the new build.
+set -o pipefail
+O=gpurun_out/r6w
+mkdir -p $O
+timeout -k 10 120 python -u scripts/lab/ab_so.py --size 64 --cells 200 ab/int_base.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so > $O/ab_200.log 2>&1 &&
+timeout -k 10 120 python -u scripts/lab/ab_so.py --size 1448 --cells 6250 ab/int_base.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so > $O/ab_6250.log 2>&1 &&
+timeout -k 10 300 python -u scripts/lab/ab_so.py ab/int_base.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so > $O/ab_flagship.log 2>&1 &&
+timeout -k 10 300 python -u scripts/lab/ab_so.py --chem synthetic:64:256 ab/int_base.so magicsoup_amd/_hip.cpython-310-x86_64-linux-gnu.so > $O/ab_wide.log 2>&1 &&
+timeout -k 10 120 python -u scripts/lab/int_prof.py ab/int_prof2.so 64 200 > $O/p200.log 2>&1 &&
+timeout -k 10 120 python -u scripts/lab/int_prof.py ab/int_prof2.so 1448 6250 > $O/p6250.log 2>&1

@@ -1,0 +1,52 @@
+"""Proteome shape of the bench population after some steps (plain world or, with
+MS_VIRTUAL_STRIPS=1, one virtual strip): protein counts per cell (from the record slots) and active
+proteins (Vmax != 0), and the activity's device time (events around enzymatic_activity).
+
+usage: python scripts/lab/pop_shape.py [map_size] [cells] [steps]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import magicsoup_amd as ms  # noqa: E402
+from magicsoup_amd.examples.wood_ljungdahl import CHEMISTRY  # noqa: E402
+
+S = int(sys.argv[1]) if len(sys.argv) > 1 else 1448
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 6250
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 60
+virtual = os.environ.get("MS_VIRTUAL_STRIPS") == "1"
+if virtual:
+    import torch.distributed as dist
+
+    from magicsoup_amd.parallel import DistributedWorld
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29549")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    w = DistributedWorld(chemistry=CHEMISTRY, map_size=S, device="cuda", seed=0, strips=True)
+else:
+    w = ms.World(chemistry=CHEMISTRY, map_size=S, device="cuda", seed=0)
+w.spawn_cells(bench.random_genomes(N, 500, "cuda"))
+atp = CHEMISTRY.molname_2_idx["ATP"]
+for _ in range(steps):
+    bench.step(w, N, 500, atp)
+w.synchronize()
+slot = w.kinetics._slot_tensor().cpu()
+cnt = ((slot >> 36) & ((1 << 14) - 1)).float()
+act = (w.kinetics.Vmax != 0).sum(dim=1).float().cpu()
+q = torch.tensor([0.5, 0.9, 0.99, 1.0])
+print({"virtual": virtual, "cells": w.n_cells, "proteins_mean": round(float(cnt.mean()), 2),
+       "proteins_q": [float(x) for x in torch.quantile(cnt, q)], "active_mean": round(float(act.mean()), 2),
+       "active_q": [float(x) for x in torch.quantile(act, q)], "active_gt32": int((act > 32).sum()),
+       "active_gt64": int((act > 64).sum())})
+ts = []
+for _ in range(10):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    w.enzymatic_activity()
+    b.record()
+    torch.cuda.synchronize()
+    ts.append(round(a.elapsed_time(b) * 1e3, 1))
+print({"activity_us": ts})
