@@ -938,9 +938,71 @@ class DistributedWorld(World):
         else:
             self._compact(torch.nonzero(keep).flatten(), keep)
 
-    def reposition_cells(self, cell_idxs=None):
-        """Move cells to random free pixels of this rank's strip (cells do not change rank)."""
-        return super().reposition_cells(cell_idxs)
+    def reposition_cells(self, cell_idxs=None, uniform: bool = False):
+        """Move cells to random free pixels. Default: pixels of this rank's strip (cells do not change
+        rank; every rank may call it alone). ``uniform=True`` (collective, every rank calls it with
+        its own local ``cell_idxs``): the reference semantics (world.py:575-608) -- the listed cells of
+        all ranks leave their pixels and take uniformly random free pixels of the whole map, so a cell
+        may move to another rank. One shared draw decides how many land on each rank (multivariate
+        hypergeometric over the ranks' free pixels, the vacated ones included, as
+        GlobalWorld.reposition_cells); which cells go where follows a shared permutation of the
+        selected cells in rank order. Movers' records travel through one object all-gather (host);
+        the stayers are repositioned inside the strip, the arrivals placed at random free pixels."""
+        if not uniform or self.world_size == 1:
+            return super().reposition_cells(cell_idxs)
+        import numpy as np
+
+        from magicsoup_amd.parallel.global_world import _CellRecord
+
+        self._reconcile()
+        n = self.n_cells
+        if cell_idxs is None:
+            idx = np.arange(n, dtype=np.int64)
+        else:
+            idx = np.unique(np.asarray(self._idx_tensor(cell_idxs).cpu(), dtype=np.int64))
+        ws, me, g = self.world_size, self.rank, self.group
+        info = [None] * ws
+        dist.all_gather_object(info, (int(idx.size), int(self.H * self.map_size - n)), group=g)
+        sel = [int(a) for a, _ in info]
+        free = [int(b) + int(a) for a, b in info]  # (the selected cells' own pixels are vacated first)
+        k = sum(sel)
+        if k == 0:
+            return
+        calls = self.__dict__["_repos_calls"] = self.__dict__.get("_repos_calls", 0) + 1
+        rng = np.random.default_rng([int(self._xseed) & ((1 << 63) - 1), calls, 0x5EED])  # (shared by the ranks)
+        order = rng.permutation(k)
+        counts = rng.multivariate_hypergeometric(np.asarray(free, dtype=np.int64), k)
+        dest = np.empty(k, dtype=np.int64)
+        lo = 0
+        for r, c in enumerate(counts):
+            dest[order[lo : lo + int(c)]] = r
+            lo += int(c)
+        first = int(sum(sel[:me]))
+        mine = dest[first : first + idx.size]
+        stay, leave = idx[mine == me], idx[mine != me]
+        leave_g = np.arange(first, first + idx.size)[mine != me]  # (global order of the movers)
+        records = []
+        if leave.size:
+            rows = torch.as_tensor(leave, device=self.device)
+            genomes, labels = self.cell_genomes, self.cell_labels
+            mol = self.cell_molecules[rows].detach().cpu()
+            life = self.cell_lifetimes[rows].tolist()
+            div = self.cell_divisions[rows].tolist()
+            records = [(int(gi), int(dest[gi]), _CellRecord(genomes[int(r)], labels[int(r)], mol[i], life[i], div[i]))
+                       for i, (gi, r) in enumerate(zip(leave_g.tolist(), leave.tolist()))]
+            self._remove(torch.as_tensor(np.sort(leave), device=self.device))
+        allrec = [None] * ws
+        dist.all_gather_object(allrec, records, group=g)
+        if stay.size:
+            # (the rows of the stayers after the movers' removal: the rank of each among the kept)
+            kept = np.setdiff1d(np.arange(n, dtype=np.int64), leave, assume_unique=True)
+            super().reposition_cells(torch.as_tensor(np.searchsorted(kept, stay), device=self.device))
+        arrivals = sorted((gi, rec) for rr in allrec for gi, d, rec in rr if d == me)
+        if arrivals:
+            placed = self.add_cells([rec.cell(self) for _, rec in arrivals])
+            assert len(placed) == len(arrivals), "no free pixel left for an arriving cell"
+        self.migrated["moved_out"] += int(leave.size)
+        self.migrated["moved_in"] += len(arrivals)
 
     # ------------------------------------------------------------------ recombination
     @_op("recombinate_cells")

@@ -114,6 +114,40 @@ def test_distributed_physics_exact_per_op():
     run_ranks(_body_physics_per_op, 2)
 
 
+def _body_uniform_reposition(rank, ws):
+    """reposition_cells(uniform=True): cells of all ranks take uniformly random free pixels of the
+    whole map (reference world.py:575-608), so some change rank; nothing is lost or duplicated and the
+    occupancy stays consistent."""
+    import torch.distributed as dist
+
+    g = _global_world(map_size=24, n=200)
+    dw = _dworld(24)
+    dw.scatter_from(g)
+    before = dw.gather()
+    moved_rank = 0
+    for it in range(3):
+        n_loc = dw.n_cells
+        pick = list(range(0, n_loc, 2)) if it == 1 else None  # (a subset once)
+        out0 = dw.migrated["moved_out"]
+        dw.reposition_cells(pick, uniform=True)
+        _check_local(dw)
+        moved_rank += dw.migrated["moved_out"] - out0
+    t = torch.tensor([moved_rank])
+    dist.all_reduce(t)
+    full = dw.gather()
+    if rank == 0:
+        _check_global(full)
+        assert full.n_cells == before.n_cells
+        assert sorted(full.cell_genomes) == sorted(before.cell_genomes)
+        key = lambda w: sorted(zip(w.cell_genomes, [tuple(r) for r in w.cell_molecules.tolist()]))
+        assert key(full) == key(before)  # (each cell keeps its molecules)
+        assert int(t) > 0  # (cells crossed ranks)
+
+
+def test_distributed_uniform_reposition():
+    run_ranks(_body_uniform_reposition, 2)
+
+
 def _body_diffusion_mass(rank, ws):
     dw = _dworld(32)
     before = dw.owned_molecule_map().double().sum(dim=[1, 2]).clone()

@@ -108,6 +108,41 @@ def test_gpu_distributed_physics_exact_per_op():
     run_ranks(_body_physics_stepwise, 2, timeout=600)
 
 
+def _body_uniform_reposition_gpu(rank, ws):
+    """reposition_cells(uniform=True) on GPU strips: some cells change rank, none is lost or
+    duplicated, each keeps its molecules, occupancy stays consistent."""
+    import torch.distributed as dist
+
+    import magicsoup_amd as ms
+    from magicsoup_amd.parallel import DistributedWorld
+    from tests.conftest import gen_genomes
+
+    ms.set_seed(8)
+    torch.manual_seed(8)
+    g = ms.World(chemistry=_chem(), map_size=64, seed=8, device="cpu")
+    g.spawn_cells(gen_genomes(900, 300))
+    dw = DistributedWorld(chemistry=_chem(), map_size=64, seed=9, device="cuda")
+    dw.scatter_from(g)
+    before = dw.gather()
+    for _ in range(2):
+        dw.reposition_cells(None, uniform=True)
+        pos = dw.cell_positions.long()
+        assert bool(((pos[:, 0] >= 1) & (pos[:, 0] <= dw.H)).all())
+        assert int(dw.owned_cell_map().sum()) == dw.n_cells
+    t = torch.tensor([dw.migrated["moved_out"]])
+    dist.all_reduce(t)
+    full = dw.gather()
+    if rank == 0:
+        assert full.n_cells == before.n_cells and int(full.cell_map.sum()) == full.n_cells
+        key = lambda w: sorted(zip(w.cell_genomes, [tuple(r) for r in w.cell_molecules.tolist()]))
+        assert key(full) == key(before)
+        assert int(t) > 0
+
+
+def test_gpu_distributed_uniform_reposition():
+    run_ranks(_body_uniform_reposition_gpu, 2, timeout=600)
+
+
 def _body_steps(rank, ws):
     import torch.distributed as dist
 
