@@ -15,7 +15,10 @@
 // still runs next to another stream's kernel), and a bench step's genome chain issues 15 us faster --
 // but whole steps run 2-7 % SLOWER batched (in-process A/B, alternating blocks of steps in one world:
 // flagship 0.829 vs 0.813 ms, the flagship as one strip 1.09 vs 1.02, the N = 8 proxy 0.385 vs
-// 0.366), so direct launches stay the default. Results are bit-identical either way
+// 0.366), so direct launches stay the default: on the device a graph's kernel nodes run slower
+// than the same kernels launched directly with the host ahead (8 write / read-back pairs of a 2 MiB
+// buffer: 4.85 vs 4.20 us per pair, launch_lab_l2.log), which outweighs the host saving wherever the
+// step is device-bound. Results are bit-identical either way
 // (test_graph_batched_launches_match_direct_launches).
 #pragma once
 #include <hip/hip_runtime.h>

@@ -31,6 +31,15 @@ __global__ void k_rec(int* out, int slot, int val, int spin) {
   }
   if (threadIdx.x == 0) atomicAdd(out + slot, val);
 }
+// producer / consumer pair over a buffer that fits the L2: is a graph's data still in the cache
+__global__ void k_write(float* x, int n, float v) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) x[i] = v + (float)i;
+}
+__global__ void k_read(const float* x, int n, float* out) {
+  float a = 0.0f;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) a += x[i];
+  if (a == -1.0f) *out = a;
+}
 __global__ void k_big(Big b) {
   if (threadIdx.x == 0 && blockIdx.x == 0 && b.w[3] == 12345ull) *reinterpret_cast<int*>(b.w[0]) = 1;
 }
@@ -188,6 +197,53 @@ int main() {
       }
     std::printf("{\"inflight_update_bad_slots\": %d, \"of\": %d, \"host_us_per_launch\": %.2f, \"device_us_per_launch\": %.2f}\n",
                 bad, L * K, (t1 - t0) / L, (t2 - t0) / L);
+  }
+  // L2 reuse inside a graph: 8 x (write 2 MiB, read it back) as direct launches and as one graph,
+  // device time from events with the host far ahead (a 2 ms spin first)
+  {
+    const int n = 512 * 1024;
+    float *x, *o;
+    CK(hipMalloc(&x, n * sizeof(float)));
+    CK(hipMalloc(&o, sizeof(float)));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    hipGraph_t g5;
+    hipGraphExec_t ge5;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+    for (int j = 0; j < 8; ++j) {
+      k_write<<<256, 256, 0, s>>>(x, n, (float)j);
+      k_read<<<256, 256, 0, s>>>(x, n, o);
+    }
+    CK(hipStreamEndCapture(s, &g5));
+    CK(hipGraphInstantiate(&ge5, g5, nullptr, nullptr, 0));
+    CK(hipGraphLaunch(ge5, s));
+    CK(hipStreamSynchronize(s));
+    for (int mode = 0; mode < 2; ++mode) {
+      float best = 1e9f, tot = 0.0f;
+      for (int rep = 0; rep < 20; ++rep) {
+        k_rec<<<1, 64, 0, s>>>(o ? reinterpret_cast<int*>(o) : nullptr, 0, 0, 2100 * 2000);
+        CK(hipEventRecord(e0, s));
+        for (int r2 = 0; r2 < 4; ++r2) {
+          if (mode == 0) {
+            for (int j = 0; j < 8; ++j) {
+              k_write<<<256, 256, 0, s>>>(x, n, (float)j);
+              k_read<<<256, 256, 0, s>>>(x, n, o);
+            }
+          } else {
+            CK(hipGraphLaunch(ge5, s));
+          }
+        }
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms = 0.0f;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        best = ms < best ? ms : best;
+        tot += ms;
+      }
+      std::printf("{\"l2_pairs_%s_us_per_pair\": %.2f, \"mean\": %.2f}\n", mode == 0 ? "direct" : "graph",
+                  best * 1e3f / 32.0f, tot / 20.0f * 1e3f / 32.0f);
+    }
   }
   // concurrency across streams: a 300 us kernel on stream A, then 3 short kernels on stream B --
   // directly and as a graph -- and the host time until B's event completes
