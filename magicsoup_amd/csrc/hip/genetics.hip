@@ -43,13 +43,31 @@ struct TransArgs {
   const int* dn;    // optional device item count (<= n; n is then the capacity)
 };
 
-// cds [2][cap] u32 | nstop [2][w] u16 | order [2][cap] u16 | codons [2][w] u8 | domain type [2][w] u8
-// | next domain [2][w] u16 | counters
-__host__ __device__ inline size_t slot_bytes_for(int width, int cap) {
-  return ((size_t)2 * cap * 4 + (size_t)2 * width * 2 + (size_t)2 * cap * 2 + (size_t)2 * width * 2 +
-          (size_t)2 * width * 2 + 16 + 15) &
+// Positions in a slot are 16-bit for genomes below 64 Ki nt and 32-bit above (Wide: the long-genome
+// pass of such a width; recombination lets genomes grow past it in long evolving runs):
+// cds [2][cap] (q, p) packed in 2 positions | nstop [2][w] pos | order [2][cap] pos | codons [2][w] u8
+// | domain type [2][w] u8 | next domain [2][w] pos | counters
+constexpr int kWidePositions = 65535;  // a length bound above this takes the 32-bit layout
+__host__ __device__ inline size_t slot_bytes_for(int width, int cap, bool wide = false) {
+  const size_t ps = wide ? 4 : 2;
+  return ((size_t)2 * cap * 2 * ps + (size_t)2 * width * ps + (size_t)2 * cap * ps + (size_t)2 * width * 2 +
+          (size_t)2 * width * ps + 16 + 15) &
          ~(size_t)15;
 }
+template <bool Wide>
+struct PosT {
+  using pos = uint16_t;
+  using pair = uint32_t;
+  static constexpr int kShift = 16;
+  static constexpr int kNone = 0xFFFF;  // no stop / no domain (positions stay below it)
+};
+template <>
+struct PosT<true> {
+  using pos = uint32_t;
+  using pair = uint64_t;
+  static constexpr int kShift = 32;
+  static constexpr int kNone = 0x7FFFFFFF;
+};
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -57,8 +75,13 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-template <bool kCount, bool kWrite>
+template <bool kCount, bool kWrite, bool Wide = false>
 __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
+  using pos_t = typename PosT<Wide>::pos;
+  using pair_t = typename PosT<Wide>::pair;
+  constexpr int kNone = PosT<Wide>::kNone;
+  constexpr int kSh = PosT<Wide>::kShift;
+  constexpr pair_t kLo = ((pair_t)1 << kSh) - 1;
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint8_t* l_start = sm;
@@ -69,19 +92,19 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   const int dt_bytes = a.stage_dt ? ((a.dt_entries + 15) & ~15) : 0;
   // per-wave slot: CDS lists [2][cap] u32, next stop [2][lmax] u16, emission order [2][cap] u16,
   // codons [2][lmax] u8, domain type at position [2][lmax] u8, counters
-  const size_t slot_bytes = slot_bytes_for(a.lmax, a.cap);
+  const size_t slot_bytes = slot_bytes_for(a.lmax, a.cap, Wide);
   const int item = blockIdx.x * a.gpb + wid;
   const int n_eff = a.dn ? min(*a.dn, a.n) : a.n;
   if ((int)blockIdx.x * a.gpb >= n_eff) return;  // whole block past the device count
   uint8_t* slot = a.gslot ? a.gslot + (size_t)item * slot_bytes
                           : sm + kLutBytes + dt_bytes + (size_t)wid * slot_bytes;
   const int LW = a.lmax;
-  uint32_t* cds = reinterpret_cast<uint32_t*>(slot);  // (q << 16) | p
-  uint16_t* nstop = reinterpret_cast<uint16_t*>(cds + 2 * a.cap);
-  uint16_t* order = nstop + 2 * LW;
+  pair_t* cds = reinterpret_cast<pair_t*>(slot);  // (q << kSh) | p
+  pos_t* nstop = reinterpret_cast<pos_t*>(cds + 2 * a.cap);
+  pos_t* order = nstop + 2 * LW;
   uint8_t* cod = reinterpret_cast<uint8_t*>(order + 2 * a.cap);
   uint8_t* dtp = cod + 2 * LW;
-  uint16_t* nxd = reinterpret_cast<uint16_t*>(dtp + 2 * LW);
+  pos_t* nxd = reinterpret_cast<pos_t*>(dtp + 2 * LW);
   int* counters = reinterpret_cast<int*>(nxd + 2 * LW);
 
   for (int i = threadIdx.x; i < 64; i += blockDim.x) {
@@ -158,16 +181,16 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   for (int st = 0; st < 2; ++st) {
     const uint8_t* c = cod + st * LW;
     const uint8_t* dt = dtp + st * LW;
-    uint16_t* ns = nstop + st * LW;
-    uint16_t* nd = nxd + st * LW;
+    pos_t* ns = nstop + st * LW;
+    pos_t* nd = nxd + st * LW;
     for (int f = 0; f < 3; ++f) {
       const int nf = ncod > f ? (ncod - f + 2) / 3 : 0;  // positions f, f+3, ... < ncod
-      int carry = 0xFFFF, carry_d = 0xFFFF;
+      int carry = kNone, carry_d = kNone;
       for (int hi = nf; hi > 0; hi -= 64) {
         const int e = hi - 64 + lane;
         const int pe = f + 3 * e;
-        int v = (e >= 0 && l_stop[c[pe]]) ? pe : 0xFFFF;
-        int w = (e >= 0 && dt[pe]) ? pe : 0xFFFF;
+        int v = (e >= 0 && l_stop[c[pe]]) ? pe : kNone;
+        int w = (e >= 0 && dt[pe]) ? pe : kNone;
         for (int off = 1; off < 64; off <<= 1) {
           const int u = __shfl_down(v, off), x = __shfl_down(w, off);
           if (lane + off < 64) {
@@ -178,8 +201,8 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
         v = min(v, carry);
         w = min(w, carry_d);
         if (e >= 0) {
-          ns[pe] = (uint16_t)v;
-          nd[pe] = (uint16_t)w;
+          ns[pe] = (pos_t)v;
+          nd[pe] = (pos_t)w;
         }
         carry = __shfl(v, 0);
         carry_d = __shfl(w, 0);
@@ -192,13 +215,13 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   if (L >= a.dom_size && L >= 3) {
     for (int st = 0; st < 2; ++st) {
       const uint8_t* c = cod + st * LW;
-      const uint16_t* ns = nstop + st * LW;
+      const pos_t* ns = nstop + st * LW;
       for (int p = lane; p < ncod; p += 64) {
         if (!l_start[c[p]]) continue;
-        const int q = p + 3 < ncod ? (int)ns[p + 3] : 0xFFFF;
-        if (q == 0xFFFF || q + 3 - p < a.dom_size) continue;
+        const int q = p + 3 < ncod ? (int)ns[p + 3] : kNone;
+        if (q == kNone || q + 3 - p < a.dom_size) continue;
         const int k = atomicAdd(&counters[st], 1);
-        cds[st * a.cap + k] = ((uint32_t)q << 16) | (uint32_t)p;  // k < ncod <= cap
+        cds[st * a.cap + k] = ((pair_t)q << kSh) | (pair_t)p;  // k < ncod <= cap
       }
     }
   }
@@ -208,16 +231,16 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   int ncds[2];
   for (int st = 0; st < 2; ++st) {
     ncds[st] = counters[st];
-    const uint32_t* lst = cds + st * a.cap;
+    const pair_t* lst = cds + st * a.cap;
     for (int e = lane; e < ncds[st]; e += 64) {
-      const uint32_t ve = lst[e];
-      const uint32_t ke = (ve & 0xFFFF0000u) | (0xFFFFu - (ve & 0xFFFFu));
+      const pair_t ve = lst[e];
+      const pair_t ke = (ve & ~kLo) | (kLo - (ve & kLo));  // stop ascending, start descending
       int rank = 0;
       for (int f = 0; f < ncds[st]; ++f) {
-        const uint32_t vf = lst[f];
-        rank += ((vf & 0xFFFF0000u) | (0xFFFFu - (vf & 0xFFFFu))) < ke;
+        const pair_t vf = lst[f];
+        rank += ((vf & ~kLo) | (kLo - (vf & kLo))) < ke;
       }
-      order[st * a.cap + rank] = (uint16_t)e;
+      order[st * a.cap + rank] = (pos_t)e;
     }
   }
   wave_sync();
@@ -227,16 +250,16 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   for (int st = 0; st < 2; ++st) {
     const uint8_t* c = cod + st * LW;
     const uint8_t* dt = dtp + st * LW;
-    const uint16_t* nd_s = nxd + st * LW;
+    const pos_t* nd_s = nxd + st * LW;
     int n_prot = 0, max_dom = 0;
     for (int e0 = 0; e0 < ncds[st]; e0 += 64) {
       const int e = e0 + lane;
       const bool have = e < ncds[st];
       int p = 0, n = 0;
       if (have) {
-        const uint32_t v = cds[st * a.cap + order[st * a.cap + e]];
-        p = (int)(v & 0xFFFFu);
-        n = (int)(v >> 16) + 3 - p;
+        const pair_t v = cds[st * a.cap + order[st * a.cap + e]];
+        p = (int)(v & kLo);
+        n = (int)(v >> kSh) + 3 - p;
       }
       // domains of the CDS [p, p + n): from position x, the next one starts at nd_s[x] (same frame;
       // every skipped position has no domain type); it counts if it ends inside the CDS
@@ -245,7 +268,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
       bool useful = false;
       for (int x = p; x < ncod;) {
         x = nd_s[x];
-        if (x == 0xFFFF || x + ds > end) break;
+        if (x == kNone || x + ds > end) break;
         useful |= dt[x] != 3;
         ++nd;
         x += ds;
@@ -259,7 +282,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
           int d = 0;
           for (int x = p; x < ncod && d < a.D;) {
             x = nd_s[x];
-            if (x == 0xFFFF || x + ds > end) break;
+            if (x == kNone || x + ds > end) break;
             const int o = x + dts;
             int32_t* dm = tk + d * 5;
             dm[0] = dt[x];
@@ -305,7 +328,7 @@ static void launch(int mode, int n, uintptr_t rows, uintptr_t arena, uintptr_t o
   if (n <= 0) return;
   if (width % 16 != 0) throw std::invalid_argument("genome length bound must be a multiple of 16");
   if (!off) throw std::invalid_argument("translate: genome offsets required");
-  if (width > 65535) throw std::invalid_argument("genomes longer than 65535 nt are not supported on the GPU");
+  if (width > (1 << 30)) throw std::invalid_argument("genomes longer than 2^30 nt are not supported on the GPU");
   TransArgs a{};
   a.n = n;
   a.width = width;
@@ -336,8 +359,9 @@ static void launch(int mode, int n, uintptr_t rows, uintptr_t arena, uintptr_t o
   // LDS pass: slots for genomes up to kLdsMaxLen (longer ones are queued); global pass: whole width
   a.lmax = a.gslot ? width : (width < kLdsMaxLen ? width : kLdsMaxLen);
   a.cap = a.lmax;  // a strand has at most one CDS per codon position
+  const bool wide = a.lmax > kWidePositions;  // (only the global-slot pass of a length bound past 64 Ki)
   const size_t fixed = kLutBytes + (a.stage_dt ? ((dt_entries + 15) & ~15) : 0);
-  const size_t slot = slot_bytes_for(a.lmax, a.cap);
+  const size_t slot = slot_bytes_for(a.lmax, a.cap, wide);
   int gpb = kGBlock / 64;
   if (!a.gslot) {
     while (gpb > 1 && fixed + gpb * slot > 64 * 1024) --gpb;
@@ -346,13 +370,21 @@ static void launch(int mode, int n, uintptr_t rows, uintptr_t arena, uintptr_t o
   a.gpb = gpb;
   const size_t lds = fixed + (a.gslot ? 0 : gpb * slot);
   const unsigned grid = cdiv(n, gpb);
-  if (mode == 0) msd::kl(translate_kernel<true, false>, grid, gpb * 64, lds, S_(stream))(a);
-  else if (mode == 1) msd::kl(translate_kernel<false, true>, grid, gpb * 64, lds, S_(stream))(a);
-  else msd::kl(translate_kernel<true, true>, grid, gpb * 64, lds, S_(stream))(a);
+  if (wide) {
+    if (mode == 0) msd::kl(translate_kernel<true, false, true>, grid, gpb * 64, lds, S_(stream))(a);
+    else if (mode == 1) msd::kl(translate_kernel<false, true, true>, grid, gpb * 64, lds, S_(stream))(a);
+    else msd::kl(translate_kernel<true, true, true>, grid, gpb * 64, lds, S_(stream))(a);
+  } else if (mode == 0) {
+    msd::kl(translate_kernel<true, false>, grid, gpb * 64, lds, S_(stream))(a);
+  } else if (mode == 1) {
+    msd::kl(translate_kernel<false, true>, grid, gpb * 64, lds, S_(stream))(a);
+  } else {
+    msd::kl(translate_kernel<true, true>, grid, gpb * 64, lds, S_(stream))(a);
+  }
   MS_LAUNCH_CHECK();
 }
 
-size_t translate_slot_bytes(int width) { return slot_bytes_for(width, width); }
+size_t translate_slot_bytes(int width) { return slot_bytes_for(width, width, width > kWidePositions); }
 
 // n items; list: item -> genome index into rows (0 = identity); gslot: global slots for the
 // long-genome pass (n * translate_slot_bytes(width) bytes) or 0 for the LDS pass, which queues

@@ -108,6 +108,10 @@ struct IntegrateArgs {
   const int32_t* wb_pos;
   float* wb_x;
   int wb_m, wb_R, wb_C, wb_dtype;
+  // LDS-path slots in global memory instead (a proteome whose slot exceeds the 160 KiB of LDS; see
+  // lds_slots): block b's slots start at gslots + b * gslot_stride * slot_words
+  int* gslots = nullptr;
+  int gslot_stride = 0;
 };
 
 // a.trims[q] without dynamic indexing (a dynamically indexed kernel-argument array is copied to
@@ -174,7 +178,8 @@ __device__ __forceinline__ void integrate_item(const IntegrateArgs& a, int* smem
   int pc;        // ... and its proteins (records past them: absent, i.e. inactive)
   prot_range(a.prow, cell, P, valid, pbase, pc);
 
-  int* words = smem + slot * a.slot_words;
+  int* words = (a.gslots ? a.gslots + (size_t)blockIdx.x * a.gslot_stride * a.slot_words : smem) +
+               (size_t)slot * a.slot_words;
   int* act = words + Ps * SP;
   float* V = reinterpret_cast<float*>(act + Ps);
   float* Va = V + Ps;
@@ -1747,6 +1752,33 @@ __global__ void __launch_bounds__(kBlock) build_params_kernel(BuildArgs b) {
 void cell_state_io(int n, int m, uintptr_t pos, int R, int C, uintptr_t map, int dtype, uintptr_t cell_mols,
                    uintptr_t buf, bool restore, uintptr_t stream);  // maps.hip
 
+// LDS-path slots of `cps` cells per block for `blocks` blocks: in LDS when they fit (returns the
+// dynamic LDS bytes), else in a device buffer (a cell with a proteome of ~900+ proteins: its slot alone
+// exceeds the 160 KiB of LDS; long evolving runs grow such genomes by recombination) -- the same
+// kernels, slower, and only for those launches. Sets `a`'s global-slot fields either way.
+static std::unordered_map<int, std::pair<int*, size_t>> g_gslots;
+static size_t lds_slots(IntegrateArgs& a, size_t slot_bytes, int cps, unsigned blocks) {
+  const size_t lds = (size_t)cps * slot_bytes;
+  if (lds <= 160 * 1024) {
+    a.gslots = nullptr;
+    a.gslot_stride = 0;
+    return lds;
+  }
+  int dev = 0;
+  MS_HIP_CHECK(hipGetDevice(&dev));
+  auto& b = g_gslots[dev];
+  const size_t need = (size_t)blocks * lds;
+  if (b.second < need) {
+    if (b.first) MS_HIP_CHECK(msd::dev_free(b.first));  // (synchronises: a queued launch may use it)
+    b.first = nullptr;
+    MS_HIP_CHECK(msd::dev_malloc((void**)&b.first, need));
+    b.second = need;
+  }
+  a.gslots = b.first;
+  a.gslot_stride = cps;
+  return 0;
+}
+
 static int slot_words_for(int P, int s, int sp) {
   int w = P * sp + P * 8 + 3 * s + 1 + P + (P * s + 3) / 4;
   return (w + 3) & ~3;  // keep every slot 16-byte aligned
@@ -1849,9 +1881,10 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
     const bool two = s > 64;
     int cps = kBlock / Gs;
     while (cps > 1 && cps * slot_bytes > 64 * 1024) --cps;
-    const size_t lds = cps * slot_bytes;
-    if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
-    const long long per_cu = std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)lds));
+    const size_t lds_full = cps * slot_bytes;  // (beyond 160 KiB the slots go to device memory, lds_slots)
+    const long long per_cu =
+        lds_full > 160 * 1024 ? kWideBlocksPerCU
+                              : std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)lds_full));
     const unsigned grid = (unsigned)std::min<long long>(cdiv(c, cps), 256 * per_cu);
     const int nz = ms::kEqIters * (nparts + 1);
     int32_t* L = P_<int32_t>(lists);
@@ -1982,7 +2015,9 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
         r.corr = corr;
         r.X_out = X_io ? P_<float>(X_io) : nullptr;
         r.all_from_snap = spec_wb ? 0 : 1;
-        const size_t lds_r = (size_t)r.cps * slot_bytes;
+        const size_t lds_r = lds_slots(r.lb, slot_bytes, r.cps, g_rescue_blocks);
+        r.fb.gslots = r.lb.gslots;
+        r.fb.gslot_stride = r.lb.gslot_stride;
         msd::kl(integrate_rescue_kernel, g_rescue_blocks, kBlock, lds_r, st)(r);
         MS_LAUNCH_CHECK();
         return 1;
@@ -2019,8 +2054,10 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
       l.count = wc3;
       l.Ps = P;
       l.slot_words = slot_words;
-      if (Gs == 32) msd::kl(integrate_spec_lds_kernel<32>, std::min<unsigned>(grid, 256), cps * 32, lds, st)(l);
-      else msd::kl(integrate_spec_lds_kernel<64>, std::min<unsigned>(grid, 256), cps * 64, lds, st)(l);
+      const unsigned gl = std::min<unsigned>(grid, 256);
+      const size_t lds = lds_slots(l, slot_bytes, cps, gl);
+      if (Gs == 32) msd::kl(integrate_spec_lds_kernel<32>, gl, cps * 32, lds, st)(l);
+      else msd::kl(integrate_spec_lds_kernel<64>, gl, cps * 64, lds, st)(l);
       MS_LAUNCH_CHECK();
     }
     }  // spec_path
@@ -2044,6 +2081,7 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
       f.spec_check = sflags;
       f.spec_n = nparts;
       f.copy_to = part == nparts - 1 ? mk : nullptr;
+      const size_t lds = lds_slots(f, slot_bytes, cps, grid);
       if (Gs == 32) msd::kl(integrate_part_kernel<32, true>, grid, cps * 32, lds, st)(f);
       else msd::kl(integrate_part_kernel<64, true>, grid, cps * 64, lds, st)(f);
       MS_LAUNCH_CHECK();
@@ -2108,9 +2146,10 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
     const size_t slot_bytes = (size_t)slot_words * 4;
     int cpsw = kBlock / G;
     while (cpsw > 1 && cpsw * slot_bytes > 64 * 1024) --cpsw;
-    const size_t ldsw = cpsw * slot_bytes;
-    if (ldsw > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
-    const long long per_cu = std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)ldsw));
+    const size_t ldsw_full = cpsw * slot_bytes;
+    const long long per_cu =
+        ldsw_full > 160 * 1024 ? kWideBlocksPerCU
+                               : std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)ldsw_full));
     const unsigned gridw = (unsigned)std::min<long long>(cdiv(c, cpsw), 256 * per_cu);
     // lists layout: [0, c) second-level wide list, [c, 2c) wide list, 2c / 2c + 1 their counts,
     // 2c + 2 .. histogram + cursors (cleared by the input kernel of part 0), then the sort order (c)
@@ -2173,6 +2212,7 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
       a.count = fw ? wc2 : wc;
       a.Ps = P;
       a.slot_words = slot_words;
+      const size_t ldsw = lds_slots(a, slot_bytes, cpsw, gridw);
       if (G == 32) msd::kl(integrate_part_kernel<32, true>, gridw, cpsw * G, ldsw, st)(a);
       else msd::kl(integrate_part_kernel<64, true>, gridw, cpsw * G, ldsw, st)(a);
       MS_LAUNCH_CHECK();
@@ -2231,17 +2271,19 @@ int integrate(int c, int P, int s, int m, int R, int C, uintptr_t W, uintptr_t Q
         const size_t slot_bytes = (size_t)slot_words * 4;
         int cps = kBlock / G;
         while (cps > 1 && cps * slot_bytes > 64 * 1024) --cps;
-        const size_t lds = cps * slot_bytes;
-        if (lds > 160 * 1024) throw std::runtime_error("integrate: a single cell's proteome does not fit in LDS");
+        const size_t lds_full = cps * slot_bytes;
         const int threads = cps * G;
         const bool stride = nl == 2 && li == 1 && (g_integrate_mode & 2) != 0;
         unsigned grid = cdiv(c, cps);
         if (stride) {  // the wide bin: at most kWideBlocksPerCU resident blocks per CU, striding
-          const long long per_cu = std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)lds));
+          const long long per_cu =
+              lds_full > 160 * 1024 ? kWideBlocksPerCU
+                                    : std::max<long long>(1, std::min<long long>(kWideBlocksPerCU, (160 * 1024) / (long long)lds_full));
           grid = (unsigned)std::min<long long>(grid, 256 * per_cu);
         }
         IntegrateArgs a = part_args(part);
         a.slot_words = slot_words;
+        const size_t lds = lds_slots(a, slot_bytes, cps, grid);
         a.list = L.list;
         a.count = L.count;
         a.Ps = L.Ps;

@@ -46,6 +46,26 @@ def test_translation_matches_host():
     assert torch.equal(tok_d.cpu(), torch.as_tensor(tok_h))
 
 
+def test_translation_past_64k_nt_matches_host():
+    """Genomes past 65535 nt (long evolving runs grow them by recombination) translate through the
+    32-bit position layout of the global-slot pass (genetics.hip PosT<true>) with the host's tokens."""
+    genetics = ms.Genetics()
+    ms.set_seed(6)
+    genomes = [ms.random_genome(70000), ms.random_genome(131072 + 5)] + gen_genomes(40, 600) + [ms.random_genome(5000)]
+    from magicsoup_amd.models.strings import PoolArena, pack_strings
+    from magicsoup_amd.ops import hip_ops
+
+    arr, lens = pack_strings(genomes)
+    tok_h, np_h = genetics.tables.translate_tokens(arr, lens)
+    pool = PoolArena("cuda")
+    pool.append_packed(torch.from_numpy(arr), torch.from_numpy(lens))
+    rows = torch.arange(len(genomes), device="cuda")
+    tok_d, np_d = hip_ops.translate(genetics, pool, rows)
+    assert int(np_d[1]) > 1000  # (the 131k-nt genome's proteome)
+    assert torch.equal(np_d.cpu(), torch.as_tensor(np_h))
+    assert torch.equal(tok_d.cpu(), torch.as_tensor(tok_h))
+
+
 def _copy_world_cpu_to_gpu(wc):
     wg = copy.deepcopy(wc)
     return wg.to("cuda")
@@ -142,6 +162,23 @@ def test_integrator_matches_host_core():
     border = np.array(border)
     assert close[~border].all(), np.nonzero(~close & ~border)
     assert wg.kinetics.last_masks == wc.kinetics.last_masks
+
+
+def test_huge_proteome_integrates_through_device_memory_slots():
+    """A cell whose proteome overflows an LDS slot (1169 proteins here: 206 KiB of slot; long evolving
+    runs grow such genomes by recombination) integrates through slots in device memory
+    (kinetics.hip lds_slots) instead of failing, with the host core's results."""
+    ms.set_seed(2)
+    torch.manual_seed(2)
+    wc = ms.World(chemistry=CHEMISTRY, map_size=32, device="cpu", seed=2)
+    wc.spawn_cells([ms.random_genome(60000) for _ in range(3)] + gen_genomes(60, 500))
+    assert wc.kinetics.N.size(1) > 1000
+    wg = _copy_world_cpu_to_gpu(wc)
+    for _ in range(2):
+        wc.enzymatic_activity()
+        wg.enzymatic_activity()
+    assert torch.allclose(wg.cell_molecules.cpu(), wc.cell_molecules, rtol=1e-4, atol=1e-4)
+    assert torch.allclose(wg.molecule_map.cpu(), wc.molecule_map, rtol=1e-4, atol=1e-4)
 
 
 def test_enzymatic_activity_matches_host():
