@@ -20,6 +20,7 @@
 namespace msd {
 
 constexpr int kGBlock = 256;  // 4 waves -> up to 4 genomes per workgroup
+constexpr int kRankMax = 64;  // CDS lists up to this long are ranked by counting, longer ones sorted
 constexpr int kLutBytes = 64 * 3 + 16 + 4096 * 2;
 
 struct TransArgs {
@@ -227,20 +228,66 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   }
   wave_sync();
 
-  // ---- 4. emission order: stop ascending, start descending
+  // ---- 4. emission order: stop ascending, start descending, i.e. ascending keys
+  //         (stop << kSh) | (kLo - start) -- unique, since every CDS has its own start. Short lists
+  //         are ranked by counting (one pass, O(n^2)); long ones (long genomes: hundreds of CDSs,
+  //         the quadratic ranking took most of an evolved population's translation time) are sorted
+  //         in place by an all-ascending bitonic network (mirrored first comparison per stage, so
+  //         positions past n act as +inf and need no padding), and phase 5 decodes the keys.
   int ncds[2];
+  bool keyed[2];
   for (int st = 0; st < 2; ++st) {
     ncds[st] = counters[st];
-    const pair_t* lst = cds + st * a.cap;
-    for (int e = lane; e < ncds[st]; e += 64) {
-      const pair_t ve = lst[e];
-      const pair_t ke = (ve & ~kLo) | (kLo - (ve & kLo));  // stop ascending, start descending
-      int rank = 0;
-      for (int f = 0; f < ncds[st]; ++f) {
-        const pair_t vf = lst[f];
-        rank += ((vf & ~kLo) | (kLo - (vf & kLo))) < ke;
+    const int n = ncds[st];
+    pair_t* lst = cds + st * a.cap;
+    keyed[st] = n > kRankMax;
+    if (!keyed[st]) {
+      for (int e = lane; e < n; e += 64) {
+        const pair_t ve = lst[e];
+        const pair_t ke = (ve & ~kLo) | (kLo - (ve & kLo));
+        int rank = 0;
+        for (int f = 0; f < n; ++f) {
+          const pair_t vf = lst[f];
+          rank += ((vf & ~kLo) | (kLo - (vf & kLo))) < ke;
+        }
+        order[st * a.cap + rank] = (pos_t)e;
       }
-      order[st * a.cap + rank] = (pos_t)e;
+      continue;
+    }
+    for (int e = lane; e < n; e += 64) {
+      const pair_t ve = lst[e];
+      lst[e] = (ve & ~kLo) | (kLo - (ve & kLo));
+    }
+    wave_sync();
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    for (int k = 2; k <= n2; k <<= 1) {
+      for (int i = lane; i < n2 / 2; i += 64) {  // mirrored pairs of each k-block
+        const int blk = i / (k / 2), off = i - blk * (k / 2);
+        const int lo = blk * k + off, hi = blk * k + k - 1 - off;
+        if (hi < n) {
+          const pair_t x = lst[lo], y = lst[hi];
+          if (y < x) {
+            lst[lo] = y;
+            lst[hi] = x;
+          }
+        }
+      }
+      wave_sync();
+      for (int j = k / 4; j >= 1; j >>= 1) {  // half-cleaners
+        for (int i = lane; i < n2 / 2; i += 64) {
+          const int blk = i / j, off = i - blk * j;
+          const int lo = blk * 2 * j + off, hi = lo + j;
+          if (hi < n) {
+            const pair_t x = lst[lo], y = lst[hi];
+            if (y < x) {
+              lst[lo] = y;
+              lst[hi] = x;
+            }
+          }
+        }
+        wave_sync();
+      }
     }
   }
   wave_sync();
@@ -257,9 +304,15 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
       const bool have = e < ncds[st];
       int p = 0, n = 0;
       if (have) {
-        const pair_t v = cds[st * a.cap + order[st * a.cap + e]];
-        p = (int)(v & kLo);
-        n = (int)(v >> kSh) + 3 - p;
+        if (keyed[st]) {  // (a sorted key: stop, and the start inverted)
+          const pair_t k = cds[st * a.cap + e];
+          p = (int)(kLo - (k & kLo));
+          n = (int)(k >> kSh) + 3 - p;
+        } else {
+          const pair_t v = cds[st * a.cap + order[st * a.cap + e]];
+          p = (int)(v & kLo);
+          n = (int)(v >> kSh) + 3 - p;
+        }
       }
       // domains of the CDS [p, p + n): from position x, the next one starts at nd_s[x] (same frame;
       // every skipped position has no domain type); it counts if it ends inside the CDS

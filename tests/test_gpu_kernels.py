@@ -52,6 +52,8 @@ def test_translation_past_64k_nt_matches_host():
     genetics = ms.Genetics()
     ms.set_seed(6)
     genomes = [ms.random_genome(70000), ms.random_genome(131072 + 5)] + gen_genomes(40, 600) + [ms.random_genome(5000)]
+    # (long CDS lists -- more than kRankMax per strand -- take the sorted emission order)
+    genomes += [ms.random_genome(n) for n in (4000, 8000, 16000, 30000, 12345)]
     from magicsoup_amd.models.strings import PoolArena, pack_strings
     from magicsoup_amd.ops import hip_ops
 
