@@ -76,15 +76,27 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-template <bool kCount, bool kWrite, bool Wide = false>
-__global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
+// kT: threads per genome -- one wave (LDS pass: up to four genomes per workgroup) or a whole
+// workgroup of kLongT (global-slot pass: one long genome per workgroup; one wave per genome left a
+// long evolving run's few genomes of 10^4..10^5 nt latency-bound on serial global-memory loops)
+template <bool kCount, bool kWrite, bool Wide = false, int kT = 64>
+__global__ void __launch_bounds__(kT > 64 ? kT : kGBlock) translate_kernel(TransArgs a) {
+  constexpr bool kBlk = kT > 64;
+  constexpr int kNw = kT / 64;  // waves per genome
   using pos_t = typename PosT<Wide>::pos;
   using pair_t = typename PosT<Wide>::pair;
   constexpr int kNone = PosT<Wide>::kNone;
   constexpr int kSh = PosT<Wide>::kShift;
   constexpr pair_t kLo = ((pair_t)1 << kSh) - 1;
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wid = kBlk ? 0 : wv;                  // genome of the workgroup
+  const int t = kBlk ? (int)threadIdx.x : lane;  // thread within the genome's group
+  auto gsync = [] {
+    if constexpr (kBlk) __syncthreads();
+    else wave_sync();
+  };
+  __shared__ int s_aux[kBlk ? 2 + 2 * 6 * kNw + 3 * kNw : 1];  // counters | chunk minima | counts, maxima
   uint8_t* l_start = sm;
   uint8_t* l_stop = sm + 64;
   uint8_t* l_one = sm + 128;
@@ -106,7 +118,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   uint8_t* cod = reinterpret_cast<uint8_t*>(order + 2 * a.cap);
   uint8_t* dtp = cod + 2 * LW;
   pos_t* nxd = reinterpret_cast<pos_t*>(dtp + 2 * LW);
-  int* counters = reinterpret_cast<int*>(nxd + 2 * LW);
+  int* counters = kBlk ? s_aux : reinterpret_cast<int*>(nxd + 2 * LW);
 
   for (int i = threadIdx.x; i < 64; i += blockDim.x) {
     l_start[i] = a.is_start[i];
@@ -128,27 +140,27 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
     const int64_t r = a.rows[g];
     L = a.lens[r];
     s = a.arena + a.off[r];
-    if (lane < 2) counters[lane] = 0;
+    if (t < 2) counters[t] = 0;
   }
   __syncthreads();
   if (!active) return;  // whole waves only; no block-wide barrier below
   if (L > LW) {         // LDS pass: too long for a slot -> queued for the global-slot pass
-    if (kCount && lane == 0) a.long_list[atomicAdd(a.long_count, 1)] = g;
+    if (kCount && t == 0) a.long_list[atomicAdd(a.long_count, 1)] = g;
     return;
   }
-  wave_sync();
+  gsync();
 
   // ---- 0. stage the genome in LDS (16-byte loads: pool allocations are 16-byte aligned and
   //         rounded up; the staging area -- the domain-type table, filled in step 2 -- holds
   //         2 * LW >= L rounded up)
   uint8_t* raw = dtp;
-  for (int i = lane * 16; i < L; i += 64 * 16)
+  for (int i = t * 16; i < L; i += kT * 16)
     *reinterpret_cast<uint4*>(raw + i) = *reinterpret_cast<const uint4*>(s + i);
-  wave_sync();
+  gsync();
 
   // ---- 1. codon index per position, both strands (0xFF past the end)
   const int ncod = L - 2;
-  for (int i = lane; i < L; i += 64) {
+  for (int i = t; i < L; i += kT) {
     uint8_t cf = 0xFF, cr = 0xFF;
     if (i < ncod) {
       cf = (uint8_t)((ms::nt_code(raw[i]) << 4) | (ms::nt_code(raw[i + 1]) << 2) | ms::nt_code(raw[i + 2]));
@@ -159,7 +171,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
     cod[i] = cf;
     cod[LW + i] = cr;
   }
-  wave_sync();
+  gsync();
 
   // ---- 2. domain type starting at every position; then, per strand and frame, the next in-frame
   //         stop and the next in-frame domain start at or after every position (suffix-min scans;
@@ -168,7 +180,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
   for (int st = 0; st < 2; ++st) {
     const uint8_t* c = cod + st * LW;
     uint8_t* dt = dtp + st * LW;
-    for (int p = lane; p < L; p += 64) {
+    for (int p = t; p < L; p += kT) {
       uint8_t ty = 0;
       if (p + dts <= L) {
         int idx = 0;
@@ -178,46 +190,78 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
       dt[p] = ty;
     }
   }
-  wave_sync();
-  for (int st = 0; st < 2; ++st) {
+  gsync();
+  // (a workgroup per genome: each wave scans its own contiguous chunk of every strand / frame
+  // sequence, then takes the minima of the chunks after it in a second pass)
+  int* cmin = s_aux + 2;
+  for (int sf = 0; sf < 6; ++sf) {
+    const int st = sf / 3, f = sf - 3 * st;
     const uint8_t* c = cod + st * LW;
     const uint8_t* dt = dtp + st * LW;
     pos_t* ns = nstop + st * LW;
     pos_t* nd = nxd + st * LW;
-    for (int f = 0; f < 3; ++f) {
-      const int nf = ncod > f ? (ncod - f + 2) / 3 : 0;  // positions f, f+3, ... < ncod
-      int carry = kNone, carry_d = kNone;
-      for (int hi = nf; hi > 0; hi -= 64) {
-        const int e = hi - 64 + lane;
-        const int pe = f + 3 * e;
-        int v = (e >= 0 && l_stop[c[pe]]) ? pe : kNone;
-        int w = (e >= 0 && dt[pe]) ? pe : kNone;
-        for (int off = 1; off < 64; off <<= 1) {
-          const int u = __shfl_down(v, off), x = __shfl_down(w, off);
-          if (lane + off < 64) {
-            v = min(v, u);
-            w = min(w, x);
-          }
+    const int nf = ncod > f ? (ncod - f + 2) / 3 : 0;  // positions f, f+3, ... < ncod
+    const int cs = kBlk ? (nf + kNw - 1) / kNw : nf;
+    const int lo = kBlk ? min(wv * cs, nf) : 0, top = kBlk ? min(lo + cs, nf) : nf;
+    int carry = kNone, carry_d = kNone;
+    for (int hi = top; hi > lo; hi -= 64) {
+      const int e = hi - 64 + lane;
+      const int pe = f + 3 * e;
+      int v = (e >= lo && l_stop[c[pe]]) ? pe : kNone;
+      int w = (e >= lo && dt[pe]) ? pe : kNone;
+      for (int off = 1; off < 64; off <<= 1) {
+        const int u = __shfl_down(v, off), x = __shfl_down(w, off);
+        if (lane + off < 64) {
+          v = min(v, u);
+          w = min(w, x);
         }
-        v = min(v, carry);
-        w = min(w, carry_d);
-        if (e >= 0) {
-          ns[pe] = (pos_t)v;
-          nd[pe] = (pos_t)w;
-        }
-        carry = __shfl(v, 0);
-        carry_d = __shfl(w, 0);
+      }
+      v = min(v, carry);
+      w = min(w, carry_d);
+      if (e >= lo) {
+        ns[pe] = (pos_t)v;
+        nd[pe] = (pos_t)w;
+      }
+      carry = __shfl(v, 0);
+      carry_d = __shfl(w, 0);
+    }
+    if constexpr (kBlk) {
+      if (lane == 0) {
+        cmin[(2 * sf) * kNw + wv] = carry;
+        cmin[(2 * sf + 1) * kNw + wv] = carry_d;
       }
     }
   }
-  wave_sync();
+  if constexpr (kBlk) {
+    __syncthreads();
+    for (int sf = 0; sf < 6; ++sf) {
+      const int st = sf / 3, f = sf - 3 * st;
+      pos_t* ns = nstop + st * LW;
+      pos_t* nd = nxd + st * LW;
+      const int nf = ncod > f ? (ncod - f + 2) / 3 : 0;
+      const int cs = (nf + kNw - 1) / kNw;
+      const int lo = min(wv * cs, nf), top = min(lo + cs, nf);
+      int cv = kNone, cd = kNone;
+      for (int w = wv + 1; w < kNw; ++w) {
+        cv = min(cv, cmin[(2 * sf) * kNw + w]);
+        cd = min(cd, cmin[(2 * sf + 1) * kNw + w]);
+      }
+      if (cv == kNone && cd == kNone) continue;
+      for (int e = lo + lane; e < top; e += 64) {
+        const int pe = f + 3 * e;
+        ns[pe] = (pos_t)min((int)ns[pe], cv);
+        nd[pe] = (pos_t)min((int)nd[pe], cd);
+      }
+    }
+  }
+  gsync();
 
   // ---- 3. CDS candidates: start codon -> first in-frame stop (too short / unstopped: dropped)
   if (L >= a.dom_size && L >= 3) {
     for (int st = 0; st < 2; ++st) {
       const uint8_t* c = cod + st * LW;
       const pos_t* ns = nstop + st * LW;
-      for (int p = lane; p < ncod; p += 64) {
+      for (int p = t; p < ncod; p += kT) {
         if (!l_start[c[p]]) continue;
         const int q = p + 3 < ncod ? (int)ns[p + 3] : kNone;
         if (q == kNone || q + 3 - p < a.dom_size) continue;
@@ -226,7 +270,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
       }
     }
   }
-  wave_sync();
+  gsync();
 
   // ---- 4. emission order: stop ascending, start descending, i.e. ascending keys
   //         (stop << kSh) | (kLo - start) -- unique, since every CDS has its own start. Short lists
@@ -242,7 +286,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
     pair_t* lst = cds + st * a.cap;
     keyed[st] = n > kRankMax;
     if (!keyed[st]) {
-      for (int e = lane; e < n; e += 64) {
+      for (int e = t; e < n; e += kT) {
         const pair_t ve = lst[e];
         const pair_t ke = (ve & ~kLo) | (kLo - (ve & kLo));
         int rank = 0;
@@ -254,15 +298,15 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
       }
       continue;
     }
-    for (int e = lane; e < n; e += 64) {
+    for (int e = t; e < n; e += kT) {
       const pair_t ve = lst[e];
       lst[e] = (ve & ~kLo) | (kLo - (ve & kLo));
     }
-    wave_sync();
+    gsync();
     int n2 = 1;
     while (n2 < n) n2 <<= 1;
     for (int k = 2; k <= n2; k <<= 1) {
-      for (int i = lane; i < n2 / 2; i += 64) {  // mirrored pairs of each k-block
+      for (int i = t; i < n2 / 2; i += kT) {  // mirrored pairs of each k-block
         const int blk = i / (k / 2), off = i - blk * (k / 2);
         const int lo = blk * k + off, hi = blk * k + k - 1 - off;
         if (hi < n) {
@@ -273,9 +317,9 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
           }
         }
       }
-      wave_sync();
+      gsync();
       for (int j = k / 4; j >= 1; j >>= 1) {  // half-cleaners
-        for (int i = lane; i < n2 / 2; i += 64) {
+        for (int i = t; i < n2 / 2; i += kT) {
           const int blk = i / j, off = i - blk * j;
           const int lo = blk * 2 * j + off, hi = lo + j;
           if (hi < n) {
@@ -286,11 +330,11 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
             }
           }
         }
-        wave_sync();
+        gsync();
       }
     }
   }
-  wave_sync();
+  gsync();
 
   // ---- 5. domain extraction in emission order
   int prot_base = 0;  // forward-strand proteins come first
@@ -299,8 +343,8 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
     const uint8_t* dt = dtp + st * LW;
     const pos_t* nd_s = nxd + st * LW;
     int n_prot = 0, max_dom = 0;
-    for (int e0 = 0; e0 < ncds[st]; e0 += 64) {
-      const int e = e0 + lane;
+    for (int e0 = 0; e0 < ncds[st]; e0 += kT) {
+      const int e = e0 + t;
       const bool have = e < ncds[st];
       int p = 0, n = 0;
       if (have) {
@@ -327,7 +371,19 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
         x += ds;
       }
       const unsigned long long bal = __ballot(useful);
-      const int rank = __popcll(bal & ((1ull << lane) - 1ull));
+      int rank = __popcll(bal & ((1ull << lane) - 1ull)), emitted = __popcll(bal);
+      if constexpr (kBlk) {  // (the waves' proteins in wave order)
+        int* wcnt = s_aux + 2 + 12 * kNw;
+        if (lane == 0) wcnt[wv] = emitted;
+        __syncthreads();
+        emitted = 0;
+        for (int w = 0; w < kNw; ++w) {
+          const int x = wcnt[w];
+          rank += w < wv ? x : 0;
+          emitted += x;
+        }
+        __syncthreads();
+      }
       if constexpr (kWrite) {
         const int slot_p = prot_base + n_prot + rank;
         if (useful && slot_p < a.P) {
@@ -351,11 +407,17 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
       if constexpr (kCount) {
         if (useful && nd > max_dom) max_dom = nd;
       }
-      n_prot += __popcll(bal);
+      n_prot += emitted;
     }
     if constexpr (kCount) {
       for (int o = 32; o > 0; o >>= 1) max_dom = max(max_dom, __shfl_xor(max_dom, o));
-      if (lane == 0) {
+      if constexpr (kBlk) {
+        int* wmax = s_aux + 2 + 12 * kNw + (1 + st) * kNw;
+        if (lane == 0) wmax[wv] = max_dom;
+        __syncthreads();
+        for (int w = 0; w < kNw; ++w) max_dom = max(max_dom, wmax[w]);
+      }
+      if (t == 0) {
         a.nprot[2 * g + st] = n_prot;
         a.ndom[2 * g + st] = max_dom;
       }
@@ -370,6 +432,7 @@ __global__ void __launch_bounds__(kGBlock) translate_kernel(TransArgs a) {
 // 100 us per chain under the diffusion stencil (profiles/r4/s17/tlong_steps.txt)
 constexpr int kLdsMaxLen = 2048;
 int translate_lds_max() { return kLdsMaxLen; }
+constexpr int kLongT = 1024;  // threads per genome of the global-slot pass
 
 // mode: 0 count pass, 1 write pass, 2 fused (counts and tokens; the caller checks the counts
 // against P / D afterwards)
@@ -419,20 +482,32 @@ static void launch(int mode, int n, uintptr_t rows, uintptr_t arena, uintptr_t o
   if (!a.gslot) {
     while (gpb > 1 && fixed + gpb * slot > 64 * 1024) --gpb;
     if (fixed + gpb * slot > 160 * 1024) throw std::invalid_argument("translation slot does not fit in LDS");
+  } else {
+    gpb = 1;  // one genome per workgroup of kLongT threads
   }
   a.gpb = gpb;
   const size_t lds = fixed + (a.gslot ? 0 : gpb * slot);
   const unsigned grid = cdiv(n, gpb);
-  if (wide) {
-    if (mode == 0) msd::kl(translate_kernel<true, false, true>, grid, gpb * 64, lds, S_(stream))(a);
-    else if (mode == 1) msd::kl(translate_kernel<false, true, true>, grid, gpb * 64, lds, S_(stream))(a);
-    else msd::kl(translate_kernel<true, true, true>, grid, gpb * 64, lds, S_(stream))(a);
+  hipStream_t st = S_(stream);
+  if (a.gslot) {
+    constexpr int T = kLongT;
+    if (wide) {
+      if (mode == 0) msd::kl(translate_kernel<true, false, true, T>, grid, T, lds, st)(a);
+      else if (mode == 1) msd::kl(translate_kernel<false, true, true, T>, grid, T, lds, st)(a);
+      else msd::kl(translate_kernel<true, true, true, T>, grid, T, lds, st)(a);
+    } else if (mode == 0) {
+      msd::kl(translate_kernel<true, false, false, T>, grid, T, lds, st)(a);
+    } else if (mode == 1) {
+      msd::kl(translate_kernel<false, true, false, T>, grid, T, lds, st)(a);
+    } else {
+      msd::kl(translate_kernel<true, true, false, T>, grid, T, lds, st)(a);
+    }
   } else if (mode == 0) {
-    msd::kl(translate_kernel<true, false>, grid, gpb * 64, lds, S_(stream))(a);
+    msd::kl(translate_kernel<true, false>, grid, gpb * 64, lds, st)(a);
   } else if (mode == 1) {
-    msd::kl(translate_kernel<false, true>, grid, gpb * 64, lds, S_(stream))(a);
+    msd::kl(translate_kernel<false, true>, grid, gpb * 64, lds, st)(a);
   } else {
-    msd::kl(translate_kernel<true, true>, grid, gpb * 64, lds, S_(stream))(a);
+    msd::kl(translate_kernel<true, true>, grid, gpb * 64, lds, st)(a);
   }
   MS_LAUNCH_CHECK();
 }

@@ -79,6 +79,8 @@ int sel_sort_cap();
 extern int g_mut_append;
 
 std::pair<long long*, int> status_slot();
+long long* status_bad_dev(int slot);
+int status_bad_cap();
 
 // ---- fused small steps of the rebuild chain
 // token rows of the live items cleared and the long-genome counter reset, one launch
@@ -93,29 +95,45 @@ __global__ void __launch_bounds__(256) gp_zero_kernel(int cap, const int* dn, lo
 // One workgroup: proteome-shape checks, fresh parameter records (params.h: each cell's proteins
 // as consecutive records from the bump counter *rtop, which the kinetics storage owns) and the
 // call's status {rebuilt, op flags, record counter, count} into its pinned slot. A cell whose
-// records do not fit below rec_cap keeps its old ones and is flagged for a host rebuild; a proteome
-// longer than the token slots is built from its first Pcap proteins and flagged as well.
-constexpr int kFlagTranslateBit = 1, kFlagRowsBit = 4;  // select.hip DevFlag
+// records do not fit below rec_cap keeps its old ones and is flagged for a host rebuild. A cell
+// whose proteome outgrew the token slots (more than Pcap proteins or Dcap domains in one), or whose
+// long genome found no global translation slot, is built from what fit and listed in the call's
+// pinned overflow list {count, cell...} for a host rebuild of just those cells (kFlagPartialBit);
+// a list that overflows falls back to the whole call (kFlagTranslateBit).
+constexpr int kFlagTranslateBit = 1, kFlagRowsBit = 4, kFlagPartialBit = 32;  // select.hip DevFlag
 __global__ void __launch_bounds__(1024) gp_check_assign_kernel(int cap, int lcap, const int* dn, const int32_t* counts,
-                                                               const int32_t* ndom, const int32_t* long_count,
-                                                               int32_t* per, int Pcap, int Dcap, const int64_t* cells,
-                                                               int64_t* slot, long long* rtop, long long rec_cap,
-                                                               int64_t* roff, int* opflags, const int* stat_cnt,
-                                                               long long* status) {
+                                                               const int32_t* ndom, const int32_t* long_list,
+                                                               const int32_t* long_count, int32_t* per, int Pcap,
+                                                               int Dcap, const int64_t* cells, int64_t* slot,
+                                                               long long* rtop, long long rec_cap, int64_t* roff,
+                                                               int* opflags, const int* stat_cnt, long long* status,
+                                                               long long* bad, int bad_cap) {
+  __shared__ int nbad;
   const int n = min(*dn, cap);
   if (threadIdx.x == 0) {
+    nbad = 0;
     if (*dn > cap) atomicOr(opflags, 2);  // kFlagCapacity
-    if (*long_count > lcap) atomicOr(opflags, kFlagTranslateBit);  // more long genomes than global slots
-  }
-  for (int j = threadIdx.x; j < n; j += blockDim.x) {
-    const int p = counts[2 * j] + counts[2 * j + 1];
-    if (p > Pcap || ndom[2 * j] > Dcap || ndom[2 * j + 1] > Dcap) atomicOr(opflags, kFlagTranslateBit);
-    per[j] = p < Pcap ? p : Pcap;
   }
   __syncthreads();
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    const int p = counts[2 * j] + counts[2 * j + 1];
+    if (p > Pcap || ndom[2 * j] > Dcap || ndom[2 * j + 1] > Dcap) {
+      const int b = atomicAdd(&nbad, 1);
+      if (b < bad_cap) bad[1 + b] = cells[j];
+    }
+    per[j] = p < Pcap ? p : Pcap;
+  }
+  // (long genomes past the global slots: not translated, their counts are stale)
+  for (int i = lcap + threadIdx.x; i < min(*long_count, n); i += blockDim.x) {
+    const int b = atomicAdd(&nbad, 1);
+    if (b < bad_cap) bad[1 + b] = cells[long_list[i]];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && nbad > 0) atomicOr(opflags, nbad > bad_cap ? kFlagTranslateBit : kFlagPartialBit);
   assign_records_block(n, per, cells, slot, rtop, rec_cap, Pcap, roff, opflags, kFlagRowsBit);
   __syncthreads();
   if (threadIdx.x == 0) {
+    bad[0] = min(nbad, bad_cap);
     status[0] = *dn;
     status[1] = __hip_atomic_load(opflags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     status[2] = *rtop;
@@ -198,9 +216,10 @@ int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const Gp
                          st);
   auto sl = status_slot();
   msd::kl(gp_check_assign_kernel, 1, 1024, 0, s)(cap, lcap, P_<int>(dcnt), P_<int32_t>(counts), P_<int32_t>(ndom),
-                                            P_<int32_t>(long_count), P_<int32_t>(per), k.P, dcap, P_<int64_t>(cells),
-                                            P_<int64_t>(k.slot), P_<long long>(k.rtop), k.rec_cap, P_<int64_t>(roff),
-                                            P_<int>(a.opflags), P_<int>(stat_cnt), sl.first);
+                                            P_<int32_t>(long_list), P_<int32_t>(long_count), P_<int32_t>(per), k.P,
+                                            dcap, P_<int64_t>(cells), P_<int64_t>(k.slot), P_<long long>(k.rtop),
+                                            k.rec_cap, P_<int64_t>(roff), P_<int>(a.opflags), P_<int>(stat_cnt),
+                                            sl.first, status_bad_dev(sl.second), status_bad_cap());
   MS_LAUNCH_CHECK();
   build_params(cap, k.P, dcap, k.P, k.s, tokens, 0, k.vmax, k.nw, k.km, k.nk, k.signs, k.nsg, k.hills, k.nh,
                k.react, k.trnsp, k.eff, k.nv, k.energies, k.abs_temp, k.gas, 0, 0, 0, 0, k.Kmr, 0, 0, 0, 0, per, k.W, k.Q,

@@ -192,6 +192,7 @@ void set_select_single_pass(int on, int items);
 void cap_skip(uintptr_t dn, int cap, uintptr_t gflags, uintptr_t opflags, uintptr_t stream);
 int status_write(uintptr_t dcnt, uintptr_t opflags, uintptr_t d_rows, uintptr_t cnt, uintptr_t stream);
 std::tuple<long long, long long, long long, long long> status_read(int slot);
+std::vector<long long> status_bad_read(int slot);
 std::pair<uintptr_t, uintptr_t> mapped_flag();
 int mapped_flag_read(uintptr_t host);
 std::tuple<long long, long long, long long, long long> stream_sync_read(int slot, uintptr_t stream);
@@ -361,6 +362,7 @@ PYBIND11_MODULE(_hip, m) {
   msd::gdef(m, "count_to_host", &msd::count_to_host, "device {count, max} -> pinned ring slot (returns the slot)");
   msd::gdef(m, "status_write", &msd::status_write, "pipeline status -> pinned ring slot (returns the slot)");
   msd::gdef(m, "status_read", &msd::status_read);
+  msd::gdef(m, "status_bad_read", &msd::status_bad_read);
   msd::gdef(m, "mapped_flag", &msd::mapped_flag, "a zeroed int in mapped pinned memory: (host pointer, device pointer)");
   msd::gdef(m, "mapped_flag_read", &msd::mapped_flag_read);
   msd::gdef(m, "stream_sync_read", &msd::stream_sync_read, "synchronise a stream, then read a pinned status slot");

@@ -598,6 +598,32 @@ void select_write_i32pos_capped(long long n, uintptr_t src, int32_t* tc, int32_t
   MS_LAUNCH_CHECK();
 }
 
+// Overflow lists beside the status ring (gp.hip gp_check_assign_kernel): a rebuild call's cells
+// whose proteome outgrew the speculative token layout, {count, cell...}, written by the device into
+// coherent host memory so the host rebuilds just those cells once the call's event completed.
+constexpr int kBadWords = 256;
+long long* g_bad = nullptr;
+long long* g_bad_dev = nullptr;
+
+long long* status_bad_dev(int slot) {
+  if (!g_bad) {
+    MS_HIP_CHECK(hipHostMalloc((void**)&g_bad, kStatusSlots * kBadWords * sizeof(long long),
+                               hipHostMallocMapped | hipHostMallocCoherent));
+    MS_HIP_CHECK(hipHostGetDevicePointer((void**)&g_bad_dev, g_bad, 0));
+  }
+  g_bad[slot * kBadWords] = -1;
+  return g_bad_dev + slot * kBadWords;
+}
+
+int status_bad_cap() { return kBadWords - 1; }
+
+std::vector<long long> status_bad_read(int slot) {
+  if (!g_bad || slot < 0 || slot >= kStatusSlots) throw std::invalid_argument("status_bad_read: bad slot");
+  const long long* v = g_bad + slot * kBadWords;
+  if (v[0] < 0 || v[0] > kBadWords - 1) throw std::runtime_error("status_bad_read: list not written");
+  return std::vector<long long>(v + 1, v + 1 + v[0]);
+}
+
 // A fresh pinned status slot: {device pointer of its 4 int64 words, slot index}.
 std::pair<long long*, int> status_slot() {
   if (!g_status) {

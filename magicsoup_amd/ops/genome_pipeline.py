@@ -64,7 +64,7 @@ def _pair_cap(n: int, expected: float, extra) -> int | None:
         return None
     return _cap(expected, limit)
 # flag bits (select.hip DevFlag, mutations.hip kGp*)
-_F_TRANSLATE, _F_CAPACITY, _F_ROWS, _F_WIDTH, _F_SKIPPED = 1, 2, 4, 8, 16
+_F_TRANSLATE, _F_CAPACITY, _F_ROWS, _F_WIDTH, _F_SKIPPED, _F_PARTIAL = 1, 2, 4, 8, 16, 32
 _SEL_I32POS, _SEL_SET = 2, 0
 
 
@@ -516,6 +516,20 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
     return True
 
 
+def _rebuild_set(pd):
+    """Cells of a resolved call whose device-built parameters need the synchronous rebuild: all of
+    the call's cells when the records outgrew the storage or the overflow list, the listed ones when
+    only some proteomes outgrew the speculative token layout (gp.hip gp_check_assign_kernel), else
+    None."""
+    flags = int(pd.host[1])
+    if flags & (_F_TRANSLATE | _F_ROWS):
+        return pd.cells[: int(pd.host[0])]
+    if flags & _F_PARTIAL:
+        bad = _m().status_bad_read(pd.host._slot)
+        return torch.tensor(bad, dtype=torch.long, device=pd.cells.device)
+    return None
+
+
 def _resolve_evo(world, pd) -> bool:
     """Reconcile a merged ``evolve`` call: each half like a call of its own (replay when skipped,
     re-commit when a result outgrew the arena), then the union's translation flags."""
@@ -543,9 +557,10 @@ def _resolve_evo(world, pd) -> bool:
     elif fm & _F_WIDTH:
         rebuilt = True
         changed.append(_recommit(world, mut))
-    if int(pd.host[1]) & (_F_TRANSLATE | _F_ROWS):
+    part = _rebuild_set(pd)
+    if part is not None:
         rebuilt = True
-        changed.append(pd.cells[: int(pd.host[0])])
+        changed.append(part)
     changed = [c for c in changed if c.numel()]
     if changed:
         world._update_params_rows(torch.unique(torch.cat([c.to(torch.long) for c in changed])))
@@ -680,10 +695,10 @@ def _resolve(world, pend: list) -> bool:
             if cells.numel():
                 world._update_params_rows(cells)
             continue
-        if flags & (_F_TRANSLATE | _F_ROWS):
+        cells = _rebuild_set(pd)
+        if cells is not None:
             # parameters are a pure function of the current genome: rebuild on the synchronous path
             rebuilt = True
-            cells = pd.cells[: int(pd.host[0])]
             if cells.numel():
                 world._update_params_rows(torch.unique(cells))
     return rebuilt

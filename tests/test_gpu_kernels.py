@@ -791,14 +791,33 @@ def test_device_genome_pipeline_capacity_skip_replays(monkeypatch):
     assert torch.equal(x0, x1)
 
 
-@pytest.mark.parametrize("d_cap", [None, 1])
+@pytest.mark.parametrize("d_cap", [None, 1, 4])
 def test_device_genome_pipeline_matches_sync_path(monkeypatch, d_cap):
     """Sync-free mutate / recombinate (device counts, speculative token layout, fresh rows) give
     the same genomes, parameters and trajectory as the synchronous path; with one domain slot
-    per protein the overflow flags force the reconcile rebuild, with the same result."""
+    or four per protein the cells past the layout are listed and rebuilt alone at reconcile (gp.hip
+    overflow list; every changed cell once the list overflows) -- same result."""
+    from magicsoup_amd.ops import genome_pipeline
+
     base = _world("cuda", map_size=64, n=800, s=400, seed=7)
-    g0, p0, x0 = _genetics_run(monkeypatch, base, sync=True)
-    g1, p1, x1 = _genetics_run(monkeypatch, base, sync=False, d_cap=d_cap)
+    kw = {}
+    if d_cap == 4:  # (genomes past the LDS slots: the chain's global-slot pass, a workgroup each;
+        # the rate keeps rate * length bound within genome_pipeline.LAM_MAX)
+        ms.set_seed(4)
+        base.spawn_cells([ms.random_genome(n) for n in (2100, 2500, 3000, 3500, 4000)])
+        kw = dict(mut_kw={"p": 2e-4})
+    g0, p0, x0 = _genetics_run(monkeypatch, base, sync=True, **kw)
+    seen = []
+    orig = genome_pipeline._rebuild_set
+
+    def spy(pd):
+        seen.append(int(pd.host[1]))
+        return orig(pd)
+
+    monkeypatch.setattr(genome_pipeline, "_rebuild_set", spy)
+    g1, p1, x1 = _genetics_run(monkeypatch, base, sync=False, d_cap=d_cap, **kw)
+    if d_cap is not None:  # (listed cells, or every changed cell once the list overflowed)
+        assert any(f & (genome_pipeline._F_PARTIAL | genome_pipeline._F_TRANSLATE) for f in seen), seen
     assert g0 == g1
     _assert_params_equal(_real(p0), _real(p1), p0["_nprot"])
     assert torch.equal(x0, x1)
