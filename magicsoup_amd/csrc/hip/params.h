@@ -6,9 +6,9 @@
 // proteome -- named by one int64 per cell (the kinetics "slot", moved with the per-cell columns by
 // every compaction / clone gather):
 //
-//   bits  0..35  offset of the first record
-//   bits 36..49  record count (proteins)
-//   bits 50..63  protein width of the build that wrote them (the dense API pads the proteins
+//   bits  0..31  offset of the first record (4 Gi records: past any record pool of 288 GB)
+//   bits 32..47  record count (proteins, at most kRecMaxProteins)
+//   bits 48..63  protein width of the build that wrote them (the dense API pads the proteins
 //                [count, width) with the reference's build padding -- Vmax 0, Kmf = Kmb = EPS, Ke 1,
 //                Kmr 1 -- and shows zeros beyond, as a later widening of the reference's tensors)
 //
@@ -22,9 +22,9 @@
 
 namespace msd {
 
-constexpr int kRecOffBits = 36;
-constexpr int kRecCntBits = 14;
-constexpr int kRecMaxProteins = (1 << kRecCntBits) - 1;
+constexpr int kRecOffBits = 32;
+constexpr int kRecCntBits = 16;
+constexpr int kRecMaxProteins = (1 << 15) - 1;  // (count and width; the width keeps the sign bit clear)
 constexpr unsigned long long kRecOffMask = (1ull << kRecOffBits) - 1ull;
 
 __host__ __device__ __forceinline__ long long rec_encode(long long off, int cnt, int width) {
@@ -35,7 +35,7 @@ __host__ __device__ __forceinline__ long long rec_off(long long v) {
   return (long long)((unsigned long long)v & kRecOffMask);
 }
 __host__ __device__ __forceinline__ int rec_cnt(long long v) {
-  return (int)(((unsigned long long)v >> kRecOffBits) & (unsigned long long)kRecMaxProteins);
+  return (int)(((unsigned long long)v >> kRecOffBits) & ((1ull << kRecCntBits) - 1ull));
 }
 __host__ __device__ __forceinline__ int rec_width(long long v) {
   return (int)((unsigned long long)v >> (kRecOffBits + kRecCntBits));

@@ -222,14 +222,15 @@ def _spare_rows(n: int, row_bytes: int) -> int:
     return max(n // 8, min(3 * n, (8 << 30) // max(row_bytes, 1)), 1024)
 
 
-# ragged parameter records (csrc/hip/params.h): slot = offset | count << 36 | build width << 50
-_REC_OFF_BITS = 36
-_REC_CNT_MASK = (1 << 14) - 1
-_MAX_PROTEINS = 8191  # (the widths the host encodes stay below the int64 sign bit)
+# ragged parameter records (csrc/hip/params.h): slot = offset | count << 32 | build width << 48
+_REC_OFF_BITS = 32
+_REC_CNT_BITS = 16
+_REC_CNT_MASK = (1 << _REC_CNT_BITS) - 1
+_MAX_PROTEINS = (1 << 15) - 1  # (the widths the host encodes stay below the int64 sign bit)
 
 
 def _rec_code(off: int, cnt: int, width: int) -> int:
-    return int(off) + (int(cnt) << _REC_OFF_BITS) + (int(width) << (_REC_OFF_BITS + 14))
+    return int(off) + (int(cnt) << _REC_OFF_BITS) + (int(width) << (_REC_OFF_BITS + _REC_CNT_BITS))
 
 
 def _retire_t(t: torch.Tensor | None) -> None:
@@ -713,6 +714,9 @@ class Kinetics:
         cap = self._rec_cap()
         free_target = max(live, int(need), 1 << 16)
         new_cap = cap if live + need + free_target // 2 <= cap else int((live + need + free_target) * 1.25)
+        new_cap = min(new_cap, (1 << _REC_OFF_BITS) - 1)  # (offsets the slot layout can name)
+        if live + need > new_cap:
+            raise RuntimeError(f"parameter records: {live + need} records exceed the slot layout's {new_cap}")
         W2 = torch.empty(new_cap, s, dtype=torch.int32, device=dev)
         Q2 = torch.empty(new_cap, 4, dtype=torch.float32, device=dev)
         K2 = torch.empty(new_cap, s, dtype=torch.float32, device=dev)

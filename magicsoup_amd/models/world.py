@@ -1467,7 +1467,10 @@ class World:
             # a new longest proteome: grow with headroom on the GPU (1.5x) so that genomes growing
             # through recombination do not re-layout the parameter storage every few dozen steps
             # (padding proteins are inert: Vmax 0)
-            self.kinetics.increase_max_proteins(P + max(8, P // 2) if rows.is_cuda else P)
+            from magicsoup_amd.models.kinetics import _MAX_PROTEINS
+
+            grown = min(P + max(8, P // 2), max(P, _MAX_PROTEINS))  # (the headroom stops at the layout)
+            self.kinetics.increase_max_proteins(grown if rows.is_cuda else P)
         # one build launch: rows without proteins are unset in the same pass
         self.kinetics.set_cell_params_tokens(rows, tokens, nprot=nprots)
 

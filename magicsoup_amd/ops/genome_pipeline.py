@@ -39,6 +39,10 @@ from magicsoup_amd.ops.streams import NEvent
 
 K_CAP = 32  # event-count cap per genome (P(Poisson(lam <= 1) > 32) < 1e-35)
 D_CAP = 12  # domain slots per protein in the speculative token layout
+# protein slots per cell in that layout: the kinetics' protein bound up to this (a long evolving run's
+# few giant proteomes -- thousands of proteins -- would otherwise size every chain cell's token rows;
+# the cells past it are listed and rebuilt on the host, gp.hip gp_check_assign_kernel)
+P_CAP = 1024
 N_CAP = 8192  # genomes per pipeline call (the expected count is kept <= N_CAP / 4)
 # largest Poisson mean of events per genome (rate x the genome length bound) a pipeline call takes:
 # the per-genome event count is capped at K_CAP, and P(Poisson(4) > 32) < 1e-18
@@ -232,7 +236,7 @@ def _kin_desc(world, dev):
         k.abs_temp, k.gas = float(kin.abs_temp), float(GAS_CONSTANT)
         # the LUT tensors stay referenced by the cache entry while their pointers are in use
         c["kin"] = (key, k, lu)
-    k.P = kin._P()
+    k.P = min(kin._P(), P_CAP)
     k.slot = kin._slot_tensor().data_ptr()
     return k
 

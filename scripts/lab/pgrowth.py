@@ -28,7 +28,7 @@ for i in range(steps):
         w.synchronize()
         kin = w.kinetics
         slot = kin._slot_tensor()
-        cnt = (slot >> 36) & ((1 << 14) - 1)
+        cnt = (slot >> 32) & ((1 << 16) - 1)
         lens = w._genomes.lens[: w.n_cells]
         print({"step": i, "cells": w.n_cells, "P": kin._P(), "max_proteome": int(cnt.max()),
                "mean_proteome": round(float(cnt.float().mean()), 1), "max_genome": int(lens.max()),

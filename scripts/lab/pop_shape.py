@@ -34,7 +34,7 @@ for _ in range(steps):
     bench.step(w, N, 500, atp)
 w.synchronize()
 slot = w.kinetics._slot_tensor().cpu()
-cnt = ((slot >> 36) & ((1 << 14) - 1)).float()
+cnt = ((slot >> 32) & ((1 << 16) - 1)).float()
 act = (w.kinetics.Vmax != 0).sum(dim=1).float().cpu()
 q = torch.tensor([0.5, 0.9, 0.99, 1.0])
 print({"virtual": virtual, "cells": w.n_cells, "proteins_mean": round(float(cnt.mean()), 2),

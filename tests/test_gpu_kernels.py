@@ -791,7 +791,7 @@ def test_device_genome_pipeline_capacity_skip_replays(monkeypatch):
     assert torch.equal(x0, x1)
 
 
-@pytest.mark.parametrize("d_cap", [None, 1, 4])
+@pytest.mark.parametrize("d_cap", [None, 1, 4, "p6"])
 def test_device_genome_pipeline_matches_sync_path(monkeypatch, d_cap):
     """Sync-free mutate / recombinate (device counts, speculative token layout, fresh rows) give
     the same genomes, parameters and trajectory as the synchronous path; with one domain slot
@@ -801,6 +801,9 @@ def test_device_genome_pipeline_matches_sync_path(monkeypatch, d_cap):
 
     base = _world("cuda", map_size=64, n=800, s=400, seed=7)
     kw = {}
+    if d_cap == "p6":  # (six protein slots per cell in the chain's layout: larger proteomes listed)
+        monkeypatch.setattr(genome_pipeline, "P_CAP", 6)
+        d_cap = 12
     if d_cap == 4:  # (genomes past the LDS slots: the chain's global-slot pass, a workgroup each;
         # the rate keeps rate * length bound within genome_pipeline.LAM_MAX)
         ms.set_seed(4)
@@ -1873,13 +1876,15 @@ def test_ragged_records_match_host_build():
     kin = wg.kinetics
     slot = kin.__dict__["_slot"]
     assert slot is not None
-    cnt = ((slot >> 36) & 0x3FFF).cpu()
+    from magicsoup_amd.models.kinetics import _REC_CNT_MASK, _REC_OFF_BITS
+
+    cnt = ((slot >> _REC_OFF_BITS) & _REC_CNT_MASK).cpu()
     _, nprot = world_ops.translate(wc, torch.arange(wc.n_cells))
     assert torch.equal(cnt, nprot.to(torch.int64).cpu())
     # (the copied world's dense rows became records first; a collection keeps only the live runs)
     kin._collect_records(0)
     assert int(kin.__dict__["_rtop"].item()) == int(nprot.sum())
-    assert torch.equal(((kin.__dict__["_slot"] >> 36) & 0x3FFF).cpu(), cnt)
+    assert torch.equal(((kin.__dict__["_slot"] >> _REC_OFF_BITS) & _REC_CNT_MASK).cpu(), cnt)
     P = wc.kinetics.N.size(1)
     for name in ("N", "Nf", "Nb", "A", "Kmr", "Kmf", "Kmb", "Vmax", "Ke"):
         a, b = getattr(kin, name)[:, :P].cpu(), getattr(wc.kinetics, name)
