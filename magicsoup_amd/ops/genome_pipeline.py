@@ -137,6 +137,14 @@ def _bufs(world, kind: str) -> dict:
     return b
 
 
+def _nt(world, n: int, L: int) -> int:
+    """Upper bound of the live genomes' total length for a call's expected counts: n genomes at the
+    length bound, or the pool's used bytes (every live genome lies below its top). A long evolving
+    run's few giant genomes raise the bound L a hundredfold over the typical genome, which priced
+    every call of such a population off the pipeline."""
+    return min(n * L, max(int(world._genomes.top_ub), 0))
+
+
 def _usable(world, expected: float, limit: float = N_CAP / 4) -> bool:
     return enabled(world) and expected <= limit
 
@@ -292,13 +300,14 @@ def point_mutations(world, p: float, p_indel: float, p_del: float) -> bool:
         return False
     # (the call's capacity at the current state: the record reservation's size; everything is
     # re-read after it)
-    _prepare_records(world, _cap(arena.n * p * int(arena.width), min(arena.n, N_CAP)))
+    _prepare_records(world, _cap(p * _nt(world, arena.n, int(arena.width)), min(arena.n, N_CAP)))
     n = arena.n
     L = int(arena.width)  # every genome fits its row
-    if p * L > LAM_MAX or not _usable(world, n * p * L):
+    exp_mut = p * _nt(world, n, L)
+    if p * L > LAM_MAX or not _usable(world, exp_mut):
         return False
     dev = arena.data.device
-    cap = _cap(n * p * L, min(n, N_CAP))
+    cap = _cap(exp_mut, min(n, N_CAP))
     b = _begin(world, "mut")
     _room(world, cap * _r16(L + K_CAP))
     k = _kin_desc(world, dev)
@@ -327,16 +336,17 @@ def recombinate_all(world, p: float, extra=None) -> bool:
     if not enabled(world):
         return False
     n0, L0 = world.n_cells, int(arena.width)
-    pc0 = _pair_cap(n0, 4 * n0 * p * 2 * L0, extra) or min(n0, N_CAP) // 2
+    pc0 = _pair_cap(n0, 8 * p * _nt(world, n0, L0), extra) or min(n0, N_CAP) // 2
     _prepare_records(world, 2 * pc0 + (0 if extra is None else int(extra.rows)))
     n = world.n_cells
     if n < 2:
         return True
     L = int(arena.width)
-    # upper bound: at most 4n neighbour pairs (each in one slot), both genomes at the length bound;
-    # real counts are several times lower (occupancy, mean lengths), so the bound may reach N_CAP:
+    # upper bound: at most 4n neighbour pairs (each in one slot), each genome in at most 8 of them,
+    # so at most 8 p times the total length (_nt); real counts are several times lower (occupancy),
+    # so the bound may reach N_CAP:
     # a count above the pair capacity makes the call a no-op that reconcile replays (cap_skip)
-    expected = 4 * n * p * 2 * L
+    expected = 8 * p * _nt(world, n, L)
     if p * 2 * L > LAM_MAX or not _usable(world, expected, N_CAP):
         return False
     pcap = _pair_cap(n, expected, extra)  # pairs per call (two results each)
@@ -429,8 +439,9 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
 
     # (the union's capacity at the current state sizes the reservation; re-read after it)
     L0 = int(arena.width)
-    pc0 = _pair_cap(n, 4 * n * p_rec * 2 * L0, extra) or min(n, N_CAP) // 2
-    ucap_max = 2 * pc0 + _cap(n * p * L0, min(n, N_CAP)) + (0 if extra is None else int(extra.rows)) + (
+    nt0 = _nt(world, n, L0)
+    pc0 = _pair_cap(n, 8 * p_rec * nt0, extra) or min(n, N_CAP) // 2
+    ucap_max = 2 * pc0 + _cap(p * nt0, min(n, N_CAP)) + (0 if extra is None else int(extra.rows)) + (
         0 if arrivals is None else int(arrivals[1]))
     kin = world.kinetics
     if bound is not None:
@@ -445,9 +456,10 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
         if n < 2:
             return False
     L = int(arena.width)
-    exp_rec = 4 * n * p_rec * 2 * L
+    nt = _nt(world, n, L)
+    exp_rec = 8 * p_rec * nt
     if (p_rec * 2 * L > LAM_MAX or p * L > LAM_MAX or not _usable(world, exp_rec, N_CAP)
-            or not _usable(world, n * p * L)):
+            or not _usable(world, p * nt)):
         return False
     pcap = _pair_cap(n, exp_rec, extra)
     if pcap is None:
@@ -459,7 +471,7 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
             return False
         reconcile(world)
     dev = arena.data.device
-    mcap = _cap(n * p * L, min(n, N_CAP))
+    mcap = _cap(p * nt, min(n, N_CAP))
     kin = world.kinetics
     arr0, narr = (0, 0) if arrivals is None else (int(arrivals[0]), int(arrivals[1]))
     fresh = not st["pending"]
