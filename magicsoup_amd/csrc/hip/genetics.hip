@@ -21,6 +21,7 @@ namespace msd {
 
 constexpr int kGBlock = 256;  // 4 waves -> up to 4 genomes per workgroup
 constexpr int kRankMax = 64;  // CDS lists up to this long are ranked by counting, longer ones sorted
+constexpr int kSortCap = 8192;  // global-slot pass: CDS lists up to this long are sorted in LDS
 constexpr int kLutBytes = 64 * 3 + 16 + 4096 * 2;
 
 struct TransArgs {
@@ -298,8 +299,14 @@ __global__ void __launch_bounds__(kT > 64 ? kT : kGBlock) translate_kernel(Trans
       }
       continue;
     }
+    // (a workgroup per genome sorts lists up to kSortCap in LDS: in its global-memory slot every
+    // compare-exchange pass of the network was a load round trip)
+    pair_t* const lst_g = lst;
+    if constexpr (kBlk) {
+      if (n <= kSortCap) lst = reinterpret_cast<pair_t*>(sm + kLutBytes + dt_bytes);
+    }
     for (int e = t; e < n; e += kT) {
-      const pair_t ve = lst[e];
+      const pair_t ve = lst_g[e];
       lst[e] = (ve & ~kLo) | (kLo - (ve & kLo));
     }
     gsync();
@@ -332,6 +339,10 @@ __global__ void __launch_bounds__(kT > 64 ? kT : kGBlock) translate_kernel(Trans
         }
         gsync();
       }
+    }
+    if (lst != lst_g) {  // (back to the slot: phase 5 reads it there; the buffer serves the next strand)
+      for (int e = t; e < n; e += kT) lst_g[e] = lst[e];
+      gsync();
     }
   }
   gsync();
@@ -486,7 +497,7 @@ static void launch(int mode, int n, uintptr_t rows, uintptr_t arena, uintptr_t o
     gpb = 1;  // one genome per workgroup of kLongT threads
   }
   a.gpb = gpb;
-  const size_t lds = fixed + (a.gslot ? 0 : gpb * slot);
+  const size_t lds = fixed + (a.gslot ? (size_t)kSortCap * (wide ? 8 : 4) : gpb * slot);
   const unsigned grid = cdiv(n, gpb);
   hipStream_t st = S_(stream);
   if (a.gslot) {
