@@ -183,6 +183,40 @@ def test_huge_proteome_integrates_through_device_memory_slots():
     assert torch.allclose(wg.molecule_map.cpu(), wc.molecule_map, rtol=1e-4, atol=1e-4)
 
 
+def test_proteome_past_8191_proteins_matches_host():
+    """A proteome past the old 14-bit record count (a seeded 3000-step flagship run grew one of ~9600
+    proteins): the record slot's 16-bit count names it (params.h), and its activity through
+    device-memory integrator slots matches the host core."""
+    from magicsoup_amd.models.kinetics import _REC_CNT_MASK, _REC_OFF_BITS
+
+    ms.set_seed(5)
+    torch.manual_seed(5)
+    wc = ms.World(chemistry=CHEMISTRY, map_size=32, device="cpu", seed=5)
+    wc.spawn_cells([ms.random_genome(460000)] + gen_genomes(30, 500))
+    assert wc.kinetics.N.size(1) > 8191
+    wg = _copy_world_cpu_to_gpu(wc)
+    wg.kinetics._enter_slot_mode()  # (the copied dense rows become records)
+    slot = wg.kinetics.__dict__["_slot"]
+    cnt = (slot >> _REC_OFF_BITS) & _REC_CNT_MASK
+    assert int(cnt.max()) > 8191
+    wc.enzymatic_activity()
+    wg.enzymatic_activity()
+    assert torch.allclose(wg.cell_molecules.cpu(), wc.cell_molecules, rtol=1e-4, atol=1e-4)
+    assert torch.allclose(wg.molecule_map.cpu(), wc.molecule_map, rtol=1e-4, atol=1e-4)
+    # (a rebuild on the device path: every cell takes records of its own proteome's size, the giant
+    # one past 8191; the copied dense rows were P records each)
+    from magicsoup_amd.ops import world_ops
+
+    wg._update_params_rows(torch.arange(wg.n_cells, device="cuda"))
+    cnt2 = (wg.kinetics.__dict__["_slot"] >> _REC_OFF_BITS) & _REC_CNT_MASK
+    _, nprot = world_ops.translate(wc, torch.arange(wc.n_cells))
+    assert int(nprot[0]) > 8191
+    assert torch.equal(cnt2.cpu(), nprot.to(torch.int64).cpu())
+    wg.enzymatic_activity()
+    wc.enzymatic_activity()
+    assert torch.allclose(wg.cell_molecules.cpu(), wc.cell_molecules, rtol=1e-4, atol=1e-4)
+
+
 def test_enzymatic_activity_matches_host():
     wc = _world("cpu", n=300)
     wg = _copy_world_cpu_to_gpu(wc)
