@@ -177,13 +177,18 @@ struct Carve {
   }
 };
 
-// genomes longer than the LDS translation slots handled per call (global-memory slots)
-int long_cap(int cap) { return std::min(cap, 1024); }
+// genomes longer than the LDS translation slots handled per call (global-memory slots, each sized
+// for the call's length bound: at most 1 GiB of them -- a long evolving run's bound of 10^6 nt makes
+// a slot 40 MB); the long genomes past them are listed for the host rebuild (gp_check_assign_kernel)
+int long_cap(int cap, int width) {
+  const size_t sb = std::max<size_t>(1, translate_slot_bytes(width));
+  return (int)std::max<size_t>(1, std::min<size_t>(std::min(cap, 1024), (size_t(1) << 30) / sb));
+}
 
 // translation + fresh rows + parameter build for cells[:*dcnt]
 size_t rebuild_bytes(int cap, int P, int dcap, int width) {
   Carve c(0);
-  c.take((size_t)long_cap(cap) * translate_slot_bytes(width));  // long-genome slots
+  c.take((size_t)long_cap(cap, width) * translate_slot_bytes(width));  // long-genome slots
   c.take(8 * (size_t)cap);                        // counts (2 per cell)
   c.take(8 * (size_t)cap);                        // ndom
   c.take(4 * (size_t)cap);                        // long list
@@ -198,7 +203,7 @@ size_t rebuild_bytes(int cap, int P, int dcap, int width) {
 int rebuild(int cap, uintptr_t cells, uintptr_t dcnt, const GpArena& a, const GpGen& g, const GpKin& k, int dcap,
             Carve& c, uintptr_t stat_cnt, hipStream_t s) {
   const uintptr_t st = reinterpret_cast<uintptr_t>(s);
-  const int lcap = long_cap(cap);
+  const int lcap = long_cap(cap, a.width);
   const uintptr_t gslot = c.take((size_t)lcap * translate_slot_bytes(a.width));
   const uintptr_t counts = c.take(8 * (size_t)cap), ndom = c.take(8 * (size_t)cap);
   const uintptr_t long_list = c.take(4 * (size_t)cap), long_count = c.take(16);

@@ -43,6 +43,10 @@ D_CAP = 12  # domain slots per protein in the speculative token layout
 # few giant proteomes -- thousands of proteins -- would otherwise size every chain cell's token rows;
 # the cells past it are listed and rebuilt on the host, gp.hip gp_check_assign_kernel)
 P_CAP = 1024
+# scratch bytes one call may take (its blob: result rows of the length bound, token rows, long-genome
+# translation slots); a call past it takes the synchronous path, which works in chunks -- a long
+# evolving run's length bound of 10^6 nt priced a merged chain at 70 GB
+_BLOB_MAX = int(os.environ.get("MS_GP_BLOB_MAX", 8 << 30))
 N_CAP = 8192  # genomes per pipeline call (the expected count is kept <= N_CAP / 4)
 # largest Poisson mean of events per genome (rate x the genome length bound) a pipeline call takes:
 # the per-genome event count is capped at K_CAP, and P(Poisson(4) > 32) < 1e-18
@@ -143,6 +147,16 @@ def _nt(world, n: int, L: int) -> int:
     run's few giant genomes raise the bound L a hundredfold over the typical genome, which priced
     every call of such a population off the pipeline."""
     return min(n * L, max(int(world._genomes.top_ub), 0))
+
+
+def _blob_ok(world, *sizes) -> bool:
+    """The call's scratch (gp_blob_bytes / gp_evolve_union_bytes of its parts) within _BLOB_MAX."""
+    return sum(int(b) for b in sizes) <= _BLOB_MAX
+
+
+def _token_p(world) -> int:
+    """Protein slots per cell of the chain's token layout (the _kin_desc bound)."""
+    return min(world.kinetics._P(), P_CAP)
 
 
 def _usable(world, expected: float, limit: float = N_CAP / 4) -> bool:
@@ -308,6 +322,8 @@ def point_mutations(world, p: float, p_indel: float, p_del: float) -> bool:
         return False
     dev = arena.data.device
     cap = _cap(exp_mut, min(n, N_CAP))
+    if not _blob_ok(world, _m().gp_blob_bytes(0, n, cap, _token_p(world), L, D_CAP, K_CAP, 0)):
+        return False
     b = _begin(world, "mut")
     _room(world, cap * _r16(L + K_CAP))
     k = _kin_desc(world, dev)
@@ -352,6 +368,9 @@ def recombinate_all(world, p: float, extra=None) -> bool:
     pcap = _pair_cap(n, expected, extra)  # pairs per call (two results each)
     if pcap is None:
         return False  # (the synchronous path commits the boundary results itself)
+    xr0 = 0 if extra is None else int(extra.rows)
+    if not _blob_ok(world, _m().gp_blob_bytes(1, n, pcap, _token_p(world), L, D_CAP, K_CAP, xr0)):
+        return False
     dev = arena.data.device
     b = _begin(world, "rec")
     _room(world, (2 * pcap + (0 if extra is None else int(extra.rows))) * _r16(2 * L))
@@ -403,7 +422,7 @@ class _PartHost:
 
 # why issues on a pending kill_divide's device count were declined (World._chain_bound; the caller
 # then waits for the count): diagnostics for scripts/lab/call_order.py
-BOUND_DECLINED = {"pending": 0, "caps": 0, "rows": 0, "pool": 0}
+BOUND_DECLINED = {"pending": 0, "caps": 0, "rows": 0, "pool": 0, "mem": 0}
 
 
 def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=None, arrivals=None,
@@ -477,6 +496,13 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
     fresh = not st["pending"]
     xr = 0 if extra is None else int(extra.rows)
     room = (2 * pcap + xr) * _r16(2 * L) + mcap * _r16(L + K_CAP)
+    tp = _token_p(world)
+    if not _blob_ok(world, _m().gp_blob_bytes(1, n, pcap, tp, L, D_CAP, K_CAP, xr),
+                    _m().gp_blob_bytes(0, n, mcap, tp, L, D_CAP, K_CAP, 0),
+                    _m().gp_evolve_union_bytes(2 * pcap + xr + mcap + narr, tp, D_CAP, L)):
+        if bound is not None:
+            BOUND_DECLINED["mem"] += 1
+        return False
     if bound is not None:
         # nothing here may wait for the count: the selections must fit the append + sort paths (the
         # count + selection passes size their grids by the count), the fresh rows must exist without
@@ -593,6 +619,8 @@ def rebuild_rows(world, rows: torch.Tensor) -> bool:
         return True
     if not enabled(world) or k > 8 * N_CAP or world.kinetics._P() == 0:
         return False  # (no protein slots yet: the synchronous path sizes the storage)
+    if not _blob_ok(world, _m().gp_blob_bytes(2, k, k, _token_p(world), int(world._genomes.width), D_CAP, 0, 0)):
+        return False
     if k > N_CAP:
         reconcile(world)  # (a large batch, e.g. a big top-up: a fresh chain)
     _prepare_records(world, k)
