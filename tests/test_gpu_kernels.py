@@ -825,7 +825,7 @@ def test_device_genome_pipeline_capacity_skip_replays(monkeypatch):
     assert torch.equal(x0, x1)
 
 
-@pytest.mark.parametrize("d_cap", [None, 1, 4, "p6"])
+@pytest.mark.parametrize("d_cap", [None, 1, 4, "p6", "blob"])
 def test_device_genome_pipeline_matches_sync_path(monkeypatch, d_cap):
     """Sync-free mutate / recombinate (device counts, speculative token layout, fresh rows) give
     the same genomes, parameters and trajectory as the synchronous path; with one domain slot
@@ -838,6 +838,10 @@ def test_device_genome_pipeline_matches_sync_path(monkeypatch, d_cap):
     if d_cap == "p6":  # (six protein slots per cell in the chain's layout: larger proteomes listed)
         monkeypatch.setattr(genome_pipeline, "P_CAP", 6)
         d_cap = 12
+    blob = d_cap == "blob"
+    if blob:  # (no call fits the scratch bound: every one declines to the synchronous path)
+        monkeypatch.setattr(genome_pipeline, "_BLOB_MAX", 1)
+        d_cap = None
     if d_cap == 4:  # (genomes past the LDS slots: the chain's global-slot pass, a workgroup each;
         # the rate keeps rate * length bound within genome_pipeline.LAM_MAX)
         ms.set_seed(4)
@@ -853,6 +857,8 @@ def test_device_genome_pipeline_matches_sync_path(monkeypatch, d_cap):
 
     monkeypatch.setattr(genome_pipeline, "_rebuild_set", spy)
     g1, p1, x1 = _genetics_run(monkeypatch, base, sync=False, d_cap=d_cap, **kw)
+    if blob:
+        assert not seen, seen
     if d_cap is not None:  # (listed cells, or every changed cell once the list overflowed)
         assert any(f & (genome_pipeline._F_PARTIAL | genome_pipeline._F_TRANSLATE) for f in seen), seen
     assert g0 == g1
