@@ -144,7 +144,7 @@ __global__ void __launch_bounds__(kT > 64 ? kT : kGBlock) translate_kernel(Trans
     if (t < 2) counters[t] = 0;
   }
   __syncthreads();
-  if (!active) return;  // whole waves only; no block-wide barrier below
+  if (!active) return;  // whole waves only (one genome per workgroup with kBlk: uniform there)
   if (L > LW) {         // LDS pass: too long for a slot -> queued for the global-slot pass
     if (kCount && t == 0) a.long_list[atomicAdd(a.long_count, 1)] = g;
     return;
