@@ -149,9 +149,14 @@ def _nt(world, n: int, L: int) -> int:
     return min(n * L, max(int(world._genomes.top_ub), 0))
 
 
-def _blob_ok(world, *sizes) -> bool:
-    """The call's scratch (gp_blob_bytes / gp_evolve_union_bytes of its parts) within _BLOB_MAX."""
-    return sum(int(b) for b in sizes) <= _BLOB_MAX
+def _blob_ok(world, L: int, sizes) -> bool:
+    """The call's scratch (``sizes()``: gp_blob_bytes / gp_evolve_union_bytes of its parts) within
+    _BLOB_MAX. Length bounds up to 16 Ki nt with token rows of up to 256 proteins stay below ~5 GB
+    whatever the capacities (N_CAP), so the common case skips the native size calls (host time of
+    small, host-bound configs)."""
+    if _BLOB_MAX >= (8 << 30) and L <= 16384 and _token_p(world) <= 256:
+        return True
+    return sum(int(b) for b in sizes()) <= _BLOB_MAX
 
 
 def _token_p(world) -> int:
@@ -322,7 +327,7 @@ def point_mutations(world, p: float, p_indel: float, p_del: float) -> bool:
         return False
     dev = arena.data.device
     cap = _cap(exp_mut, min(n, N_CAP))
-    if not _blob_ok(world, _m().gp_blob_bytes(0, n, cap, _token_p(world), L, D_CAP, K_CAP, 0)):
+    if not _blob_ok(world, L, lambda: [_m().gp_blob_bytes(0, n, cap, _token_p(world), L, D_CAP, K_CAP, 0)]):
         return False
     b = _begin(world, "mut")
     _room(world, cap * _r16(L + K_CAP))
@@ -369,7 +374,7 @@ def recombinate_all(world, p: float, extra=None) -> bool:
     if pcap is None:
         return False  # (the synchronous path commits the boundary results itself)
     xr0 = 0 if extra is None else int(extra.rows)
-    if not _blob_ok(world, _m().gp_blob_bytes(1, n, pcap, _token_p(world), L, D_CAP, K_CAP, xr0)):
+    if not _blob_ok(world, L, lambda: [_m().gp_blob_bytes(1, n, pcap, _token_p(world), L, D_CAP, K_CAP, xr0)]):
         return False
     dev = arena.data.device
     b = _begin(world, "rec")
@@ -497,9 +502,9 @@ def evolve(world, p_rec: float, p: float, p_indel: float, p_del: float, extra=No
     xr = 0 if extra is None else int(extra.rows)
     room = (2 * pcap + xr) * _r16(2 * L) + mcap * _r16(L + K_CAP)
     tp = _token_p(world)
-    if not _blob_ok(world, _m().gp_blob_bytes(1, n, pcap, tp, L, D_CAP, K_CAP, xr),
-                    _m().gp_blob_bytes(0, n, mcap, tp, L, D_CAP, K_CAP, 0),
-                    _m().gp_evolve_union_bytes(2 * pcap + xr + mcap + narr, tp, D_CAP, L)):
+    if not _blob_ok(world, L, lambda: [_m().gp_blob_bytes(1, n, pcap, tp, L, D_CAP, K_CAP, xr),
+                                       _m().gp_blob_bytes(0, n, mcap, tp, L, D_CAP, K_CAP, 0),
+                                       _m().gp_evolve_union_bytes(2 * pcap + xr + mcap + narr, tp, D_CAP, L)]):
         if bound is not None:
             BOUND_DECLINED["mem"] += 1
         return False
@@ -619,7 +624,8 @@ def rebuild_rows(world, rows: torch.Tensor) -> bool:
         return True
     if not enabled(world) or k > 8 * N_CAP or world.kinetics._P() == 0:
         return False  # (no protein slots yet: the synchronous path sizes the storage)
-    if not _blob_ok(world, _m().gp_blob_bytes(2, k, k, _token_p(world), int(world._genomes.width), D_CAP, 0, 0)):
+    Lw = int(world._genomes.width)
+    if not _blob_ok(world, Lw, lambda: [_m().gp_blob_bytes(2, k, k, _token_p(world), Lw, D_CAP, 0, 0)]):
         return False
     if k > N_CAP:
         reconcile(world)  # (a large batch, e.g. a big top-up: a fresh chain)

@@ -21,8 +21,11 @@ def test_total_length_bound_takes_the_smaller_of_rows_and_pool():
 
 
 def test_scratch_bound(monkeypatch):
-    monkeypatch.setattr(gp, "_BLOB_MAX", 1000)
+    monkeypatch.setattr(gp, "_token_p", lambda world: 64)
     w = _world(0)
-    assert gp._blob_ok(w, 400, 600)
-    assert not gp._blob_ok(w, 400, 601)
-    assert gp._blob_ok(w)
+    # the default bound: short length bounds skip the size calls
+    assert gp._blob_ok(w, 4096, lambda: 1 / 0)
+    monkeypatch.setattr(gp, "_BLOB_MAX", 1000)
+    assert gp._blob_ok(w, 4096, lambda: [400, 600])
+    assert not gp._blob_ok(w, 4096, lambda: [400, 601])
+    assert gp._blob_ok(w, 4096, lambda: [])
